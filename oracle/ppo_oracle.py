@@ -1,0 +1,372 @@
+"""Numpy restatement of the reference hot-path math (TEST INFRASTRUCTURE — see oracle/__init__.py).
+
+Each function cites the reference file:line (under /root/reference) it restates. Values are computed in
+float64 from float32 inputs unless the reference's result depends on float32 rounding, so the oracle is
+at least as accurate as the reference; forward values and analytic gradients are both given so the
+HIP kernels' forward AND backward can be checked without autograd.
+"""
+
+from __future__ import annotations
+
+import numpy as np
+
+AGG_MODES = ("token-mean", "seq-mean-token-sum", "seq-mean-token-mean", "seq-mean-token-sum-norm")
+KL_TYPES = {"kl": "k1", "k1": "k1", "abs": "abs", "mse": "k2", "k2": "k2", "low_var_kl": "k3", "k3": "k3"}
+
+f64 = np.float64
+
+
+# ---------------------------------------------------------------------------------------------
+# masked reductions — verl/utils/torch_functional.py:163-223
+# ---------------------------------------------------------------------------------------------
+def masked_sum(values, mask, axis=None):
+    """torch_functional.py:163-168: where(mask, v, 0) * mask, then sum."""
+    v = np.where(np.asarray(mask).astype(bool), np.asarray(values, f64), 0.0)
+    return (v * np.asarray(mask, f64)).sum(axis=axis)
+
+
+def masked_mean(values, mask, axis=None):
+    """torch_functional.py:171-185: masked_sum / (mask.sum() + 1e-8)."""
+    return masked_sum(values, mask, axis) / (np.asarray(mask, f64).sum(axis=axis) + 1e-8)
+
+
+def masked_var(values, mask, unbiased=True):
+    """torch_functional.py:188-203 (raises on mask_sum in {0, 1} like the reference)."""
+    mean = masked_mean(values, mask)
+    var = masked_mean((np.asarray(values, f64) - mean) ** 2, mask)
+    if unbiased:
+        n = np.asarray(mask, f64).sum()
+        if n == 0:
+            raise ValueError("At least one element in the mask has to be 1.")
+        if n == 1:
+            raise ValueError("The sum of the mask is one, which can cause a division by zero.")
+        var = var * (n / (n - 1))
+    return var
+
+
+def masked_whiten(values, mask, shift_mean=True):
+    """torch_functional.py:206-223."""
+    mean, var = masked_mean(values, mask), masked_var(values, mask)
+    w = (np.asarray(values, f64) - mean) / np.sqrt(var + 1e-8)
+    return w + mean if not shift_mean else w
+
+
+# ---------------------------------------------------------------------------------------------
+# agg_loss — verl/trainer/ppo/core_algos.py:703-736 (forward value and d loss / d loss_mat)
+# ---------------------------------------------------------------------------------------------
+def agg_loss(loss_mat, loss_mask, loss_agg_mode):
+    x = np.asarray(loss_mat, f64)
+    m = np.asarray(loss_mask, f64)
+    B, R = x.shape
+    with np.errstate(divide="ignore", invalid="ignore"):
+        if loss_agg_mode == "token-mean":
+            return masked_mean(x, loss_mask)
+        if loss_agg_mode == "seq-mean-token-sum":
+            return (x * m).sum(-1).mean()
+        if loss_agg_mode == "seq-mean-token-mean":
+            return ((x * m).sum(-1) / m.sum(-1)).mean()
+        if loss_agg_mode == "seq-mean-token-sum-norm":
+            return (x * m).sum(-1).sum() / R
+    raise ValueError(f"Invalid loss_agg_mode: {loss_agg_mode}")
+
+
+def agg_loss_grad(loss_mask, loss_agg_mode):
+    """d agg_loss / d loss_mat (the same weights every reduction in agg_loss applies)."""
+    m = np.asarray(loss_mask, f64)
+    B, R = m.shape
+    with np.errstate(divide="ignore", invalid="ignore"):
+        if loss_agg_mode == "token-mean":
+            return m / (m.sum() + 1e-8)
+        if loss_agg_mode == "seq-mean-token-sum":
+            return m / B
+        if loss_agg_mode == "seq-mean-token-mean":
+            return m / (B * m.sum(-1, keepdims=True))
+        if loss_agg_mode == "seq-mean-token-sum-norm":
+            return m / R
+    raise ValueError(f"Invalid loss_agg_mode: {loss_agg_mode}")
+
+
+# ---------------------------------------------------------------------------------------------
+# kl_penalty — core_algos.py:1272-1307 (value and d/d logprob)
+# ---------------------------------------------------------------------------------------------
+def kl_penalty(logprob, ref_logprob, kl_penalty):
+    kind = KL_TYPES.get(kl_penalty)
+    lp = np.asarray(logprob, np.float32)
+    rf = np.asarray(ref_logprob, np.float32)
+    if kind == "k1":
+        return (lp - rf).astype(f64), np.ones_like(lp, f64)
+    if kind == "abs":
+        d = lp - rf
+        return np.abs(d).astype(f64), np.sign(d).astype(f64)
+    if kind == "k2":
+        d = (lp - rf).astype(f64)
+        return 0.5 * d * d, d
+    if kind == "k3":
+        raw = (rf - lp).astype(f64)
+        kl = np.clip(raw, -20.0, 20.0)
+        g1 = ((raw >= -20.0) & (raw <= 20.0)).astype(f64)
+        ratio = np.exp(kl)
+        kld = ratio - kl - 1.0
+        out = np.clip(kld, -10.0, 10.0)
+        g2 = ((kld >= -10.0) & (kld <= 10.0)).astype(f64)
+        return out, -(ratio - 1.0) * g1 * g2
+    raise NotImplementedError(kl_penalty)
+
+
+# ---------------------------------------------------------------------------------------------
+# compute_policy_loss_vanilla — core_algos.py:815-889 (forward + analytic backward)
+# ---------------------------------------------------------------------------------------------
+def _max_grad(a, b):
+    """torch.maximum backward (tools/autograd/derivatives.yaml): ties split the gradient in half."""
+    ga = np.where(a > b, 1.0, np.where(a == b, 0.5, 0.0))
+    return ga, 1.0 - ga
+
+
+def policy_loss_vanilla(old_log_prob, log_prob, advantages, response_mask, loss_agg_mode="token-mean",
+                        clip_ratio_low=0.2, clip_ratio_high=0.2, clip_ratio_c=3.0):
+    """Returns (pg_loss, pg_clipfrac, ppo_kl, pg_clipfrac_lower, pg_losses, d pg_losses / d log_prob)."""
+    assert clip_ratio_c > 1.0
+    f32 = np.float32
+    # per-token values in float32 with the reference's op order: the branch decisions (clip, ties,
+    # clipfrac counts) depend on float32 rounding exactly at the clip bounds
+    raw = np.asarray(log_prob, f32) - np.asarray(old_log_prob, f32)
+    nkl = np.clip(raw, f32(-20.0), f32(20.0))
+    gate = ((raw >= -20.0) & (raw <= 20.0)).astype(f64)
+    ratio = np.exp(nkl.astype(f64)).astype(f32)  # correctly rounded float32 exp
+    A = np.asarray(advantages, f32)
+    negA = -A
+    L1 = negA * ratio
+    lo, hi = f32(1.0 - clip_ratio_low), f32(1.0 + clip_ratio_high)
+    rc = np.clip(ratio, lo, hi)
+    gc = ((ratio >= lo) & (ratio <= hi)).astype(f64)
+    L2 = negA * rc
+    C1 = np.maximum(L1, L2)
+    w1, w2 = _max_grad(L1, L2)
+    dC1 = w1 * (-A.astype(f64)) + w2 * (-A.astype(f64)) * gc
+    L3 = negA * f32(clip_ratio_c)
+    C2 = np.minimum(L3, C1)
+    _, wc1 = _max_grad(-L3, -C1)  # min(a, b) backward == max(-a, -b) backward
+    neg = A < 0
+    pg_losses = np.where(neg, C2, C1).astype(f64)
+    dpg_dratio = np.where(neg, wc1 * dC1, dC1)
+    dpg = dpg_dratio * ratio.astype(f64) * gate
+    nkl = nkl.astype(f64)
+    m = response_mask
+    pg_loss = agg_loss(pg_losses, m, loss_agg_mode)
+    ppo_kl = masked_mean(-nkl, m)
+    pg_clipfrac = masked_mean((L2 > L1).astype(f64), m)
+    pg_clipfrac_lower = masked_mean((C1 > L3).astype(f64) * neg.astype(f64), m)
+    return pg_loss, pg_clipfrac, ppo_kl, pg_clipfrac_lower, pg_losses, dpg
+
+
+def clip_boundary_tokens(old_log_prob, log_prob, advantages, response_mask, clip_ratio_low=0.2, clip_ratio_high=0.2,
+                         clip_ratio_c=3.0, ulps=2):
+    """Masked tokens whose clip decisions hinge on the last ulp of exp (|ratio - bound| <= ulps ulp).
+
+    float32 exp is not correctly rounded in torch (SLEEF), numpy or ocml, so pg_clipfrac and
+    pg_clipfrac_lower may differ by one count per such token between any two implementations; the
+    loss value and its gradient are continuous there and do not."""
+    f32 = np.float32
+    nkl = np.clip(np.asarray(log_prob, f32) - np.asarray(old_log_prob, f32), f32(-20), f32(20))
+    ratio = np.exp(nkl.astype(f64))
+    m = np.asarray(response_mask).astype(bool)
+    amb = np.zeros_like(m)
+    for bound in (f32(1.0 - clip_ratio_low), f32(1.0 + clip_ratio_high)):
+        amb |= np.abs(ratio - f64(bound)) <= ulps * np.spacing(bound)
+    A = np.asarray(advantages, f32)
+    # C1 vs L3 = -A*c ties: ratio near c on the dual-clip side
+    amb |= np.abs(ratio - f64(f32(clip_ratio_c))) <= ulps * np.spacing(f32(clip_ratio_c))
+    amb |= A == 0
+    return int((amb & m).sum())
+
+
+def actor_loss(old_log_prob, log_prob, advantages, response_mask, entropy, ref_log_prob, *, loss_agg_mode,
+               clip_ratio_low, clip_ratio_high, clip_ratio_c, entropy_coeff, use_kl_loss, kl_loss_type,
+               kl_loss_coef, loss_scale_factor):
+    """The per-micro-batch loss of DataParallelPPOActor.update_policy (dp_actor.py:419-466)."""
+    pg_loss, clipfrac, ppo_kl, clipfrac_lower, _, dpg = policy_loss_vanilla(
+        old_log_prob, log_prob, advantages, response_mask, loss_agg_mode, clip_ratio_low, clip_ratio_high, clip_ratio_c)
+    w = agg_loss_grad(response_mask, loss_agg_mode)
+    entropy_loss = agg_loss(entropy, response_mask, loss_agg_mode)
+    total = pg_loss - entropy_loss * entropy_coeff if entropy_coeff != 0 else pg_loss
+    kld, dkld = kl_penalty(log_prob, ref_log_prob, kl_loss_type)
+    kl_loss = agg_loss(kld, response_mask, loss_agg_mode)
+    dlogp = w * dpg
+    if use_kl_loss:
+        total = total + kl_loss * kl_loss_coef
+        dlogp = dlogp + kl_loss_coef * w * dkld
+    dent = -entropy_coeff * w if entropy_coeff != 0 else np.zeros_like(w)
+    return dict(pg_loss=pg_loss, pg_clipfrac=clipfrac, ppo_kl=ppo_kl, pg_clipfrac_lower=clipfrac_lower,
+                entropy_loss=entropy_loss, kl_loss=kl_loss, loss=total * loss_scale_factor,
+                dlogp=dlogp * loss_scale_factor, dentropy=dent * loss_scale_factor, kld=kld)
+
+
+# ---------------------------------------------------------------------------------------------
+# compute_grpo_outcome_advantage — core_algos.py:260-324
+# ---------------------------------------------------------------------------------------------
+def grpo_outcome_advantage(token_level_rewards, response_mask, index, epsilon=1e-6, norm_adv_by_std_in_grpo=True):
+    r = np.asarray(token_level_rewards, np.float32)
+    scores = r.astype(f64).sum(-1)
+    groups: dict = {}
+    for i, u in enumerate(index):
+        groups.setdefault(u, []).append(i)
+    out = np.empty_like(scores)
+    for members in groups.values():
+        s = scores[members]
+        if len(members) == 1:
+            mean, std = 0.0, 1.0
+        else:
+            mean = s.mean()
+            std = np.sqrt(((s - mean) ** 2).sum() / (len(s) - 1))
+        out[members] = (s - mean) / (std + epsilon) if norm_adv_by_std_in_grpo else s - mean
+    adv = out[:, None] * np.asarray(response_mask, f64)
+    return adv, adv
+
+
+def group_ids(index):
+    """uid strings -> dense int32 group ids in order of first appearance (the CSR the HIP kernel takes)."""
+    ids, order = {}, []
+    for u in index:
+        if u not in ids:
+            ids[u] = len(ids)
+        order.append(ids[u])
+    return np.asarray(order, np.int32), len(ids)
+
+
+# ---------------------------------------------------------------------------------------------
+# compute_gae_advantage_return — core_algos.py:208-256
+# ---------------------------------------------------------------------------------------------
+def gae_advantage_return(token_level_rewards, values, response_mask, gamma, lam):
+    r = np.asarray(token_level_rewards, f64)
+    v = np.asarray(values, f64)
+    m = np.asarray(response_mask, f64)
+    B, T = r.shape
+    nextvalues = np.zeros(B)
+    lastgaelam = np.zeros(B)
+    adv = np.zeros((B, T))
+    for t in reversed(range(T)):
+        delta = r[:, t] + gamma * nextvalues - v[:, t]
+        lg = delta + gamma * lam * lastgaelam
+        nextvalues = v[:, t] * m[:, t] + (1 - m[:, t]) * nextvalues
+        lastgaelam = lg * m[:, t] + (1 - m[:, t]) * lastgaelam
+        adv[:, t] = lastgaelam
+    returns = adv + v
+    return masked_whiten(adv, response_mask), returns
+
+
+# ---------------------------------------------------------------------------------------------
+# log-prob / entropy over the vocabulary — torch_functional.py:116-160 (+ backward)
+# ---------------------------------------------------------------------------------------------
+def logprob_entropy(logits, labels, temperature=1.0):
+    """Returns (logp[N], entropy[N], softmax[N,V]) computed in float64 from the given logits."""
+    z = np.asarray(logits, np.float32).astype(f64) / temperature
+    zmax = z.max(-1, keepdims=True)
+    e = np.exp(z - zmax)
+    s = e.sum(-1, keepdims=True)
+    lse = (np.log(s) + zmax)[:, 0]
+    p = e / s
+    logp = z[np.arange(z.shape[0]), labels] - lse
+    ent = lse - (p * z).sum(-1)
+    return logp, ent, p
+
+
+def logprob_entropy_backward(logits, labels, dlogp, dentropy, temperature=1.0):
+    """d/d logits of sum(dlogp*logp + dentropy*entropy)  (experimental/torch_functional.py:40-72)."""
+    logp, ent, p = logprob_entropy(logits, labels, temperature)
+    z = np.asarray(logits, np.float32).astype(f64) / temperature
+    lse = logp - z[np.arange(z.shape[0]), labels]  # = -lse
+    logsm = z + lse[:, None]
+    onehot = np.zeros_like(p)
+    onehot[np.arange(p.shape[0]), labels] = 1.0
+    g = np.asarray(dlogp, f64)[:, None] * (onehot - p)
+    g = g - np.asarray(dentropy, f64)[:, None] * p * (logsm + ent[:, None])
+    return g / temperature
+
+
+def fused_linear_logprob_entropy(hidden, weight, labels, temperature=1.0):
+    """FusedLinearForPPO forward (experimental/torch_functional.py:20-37)."""
+    logits = np.asarray(hidden, f64) @ np.asarray(weight, f64).T
+    logp, ent, _ = logprob_entropy(logits, labels, temperature)
+    return logp, ent
+
+
+def fused_linear_backward(hidden, weight, labels, dlogp, dentropy, temperature=1.0):
+    """FusedLinearForPPO backward (experimental/torch_functional.py:40-72): (d_hidden, d_weight)."""
+    h = np.asarray(hidden, f64)
+    w = np.asarray(weight, f64)
+    logits = h @ w.T
+    dlogits = logprob_entropy_backward(logits, labels, dlogp, dentropy, temperature)
+    return dlogits @ w, dlogits.T @ h
+
+
+# ---------------------------------------------------------------------------------------------
+# rollout bookkeeping — torch_functional.py:226-246, utils/model.py:219, hf_rollout.py:151-160
+# ---------------------------------------------------------------------------------------------
+def get_response_mask(response_id, eos_token):
+    eos = np.atleast_1d(np.asarray(eos_token))
+    is_eos = np.isin(np.asarray(response_id), eos).astype(np.int64)
+    return ((np.cumsum(is_eos, axis=1) - is_eos) == 0).astype(np.int64)
+
+
+def compute_position_id_with_mask(mask):
+    return np.clip(np.cumsum(np.asarray(mask, np.int64), axis=-1) - 1, 0, None)
+
+
+def response_position_ids(prompt_position_ids, response_length):
+    pos = np.asarray(prompt_position_ids, np.int64)
+    delta = np.arange(1, response_length + 1, dtype=np.int64)[None, :]
+    return np.concatenate([pos, pos[:, -1:] + delta], axis=-1)
+
+
+# ---------------------------------------------------------------------------------------------
+# decode-step token selection (HF generate semantics used by HFRollout, hf_rollout.py:112-124)
+# ---------------------------------------------------------------------------------------------
+def greedy(logits):
+    """argmax with first-index tie-break (torch.argmax semantics)."""
+    return np.asarray(logits).argmax(-1).astype(np.int64)
+
+
+def philox_uniform(seed, offset, counter):
+    """Counter-based uniform in (0,1) matching the HIP sampler (Philox4x32-10, first word, 24-bit mantissa)."""
+    M0, M1, W0, W1 = 0xD2511F53, 0xCD9E8D57, 0x9E3779B9, 0xBB67AE85
+    k0, k1 = np.uint64(seed & 0xFFFFFFFF), np.uint64((seed >> 32) & 0xFFFFFFFF)
+    c = [np.uint64(counter & 0xFFFFFFFF), np.uint64((counter >> 32) & 0xFFFFFFFF),
+         np.uint64(offset & 0xFFFFFFFF), np.uint64((offset >> 32) & 0xFFFFFFFF)]
+    mask = np.uint64(0xFFFFFFFF)
+    for _ in range(10):
+        p0 = np.uint64(M0) * c[0]
+        p1 = np.uint64(M1) * c[2]
+        c = [((p1 >> np.uint64(32)) ^ c[1] ^ k0) & mask, p1 & mask, ((p0 >> np.uint64(32)) ^ c[3] ^ k1) & mask, p0 & mask]
+        k0 = (k0 + np.uint64(W0)) & mask
+        k1 = (k1 + np.uint64(W1)) & mask
+    return (float(int(c[0]) >> 8) + 0.5) * (1.0 / 16777216.0)
+
+
+def sample_row(logits, temperature, top_k, top_p, seed, offset, row):
+    """Reference semantics of one sampling step: temperature -> top-k -> top-p -> categorical draw.
+
+    The draw uses the inverse CDF of the filtered distribution at a Philox uniform (the HIP sampler's
+    RNG), so HIP and oracle pick the same token; HF uses torch.multinomial (same distribution)."""
+    z = np.asarray(logits, np.float32).astype(f64) / temperature
+    V = z.shape[0]
+    keep = np.ones(V, bool)
+    if top_k and 0 < top_k < V:
+        kth = np.sort(z)[-top_k]
+        keep &= z >= kth
+    zs = np.where(keep, z, -np.inf)
+    p = np.exp(zs - zs.max())
+    p /= p.sum()
+    if top_p < 1.0:
+        order = np.argsort(-p, kind="stable")
+        cum = np.cumsum(p[order])
+        # HF TopPLogitsWarper: drop tokens whose ascending cumulative mass <= 1 - top_p, i.e. whose
+        # strictly-higher-ranked mass already reaches top_p (the top token is always kept)
+        drop = cum - p[order] >= top_p
+        drop[0] = False
+        keep2 = np.ones(V, bool)
+        keep2[order[drop]] = False
+        p = np.where(keep2, p, 0.0)
+        p /= p.sum()
+    u = philox_uniform(seed, offset, row)
+    cdf = np.cumsum(p)
+    return int(min(np.searchsorted(cdf, u * cdf[-1], side="right"), V - 1))

@@ -1,0 +1,28 @@
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU and the built HIP library")
+    config.addinivalue_line("markers", "slow: long-running")
+
+
+def load_golden(name):
+    """Load a committed golden fixture (plain arrays, no pickles) and its JSON metadata."""
+    z = np.load(os.path.join(GOLDEN, name), allow_pickle=False)
+    meta = json.loads(str(z["__meta__"]))
+    return z, meta
+
+
+@pytest.fixture(scope="session")
+def golden():
+    return load_golden

@@ -1,0 +1,355 @@
+"""Generate golden vectors by running the REFERENCE implementation (dots.rl / verl) on seeded inputs.
+
+Run in the survey/build container only (it needs ``/root/reference``; the GPU box never runs it):
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+
+Every fixture stores its inputs and the reference's outputs as plain arrays (``.npz``, no pickles).
+Reference call sites (file:line under /root/reference):
+
+* policy loss / agg / KL / total actor loss + backward : verl/trainer/ppo/core_algos.py:703-736, 815-889, 1272-1307
+  composed exactly as verl/workers/actor/dp_actor.py:419-466 does.
+* GRPO advantage : verl/trainer/ppo/core_algos.py:260-324
+* GAE + masked_whiten : verl/trainer/ppo/core_algos.py:208-256, verl/utils/torch_functional.py:171-223
+* log-prob / entropy over vocab (+ backward) : verl/utils/torch_functional.py:116-160
+* fused lm_head -> logp/entropy (+ backward) : verl/utils/experimental/torch_functional.py:20-216
+* response mask / position ids : verl/utils/torch_functional.py:226-246, verl/utils/model.py:219,
+  verl/workers/rollout/hf_rollout.py:151-160
+* masked_mean known answers : tests/utils/test_torch_functional.py:55-66 (reference test, reproduced as data)
+"""
+
+import hashlib
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+import _ref_stubs  # noqa: E402
+
+DictConfig = _ref_stubs.install()
+
+import verl.trainer.ppo.core_algos as ca  # noqa: E402
+import verl.utils.experimental.torch_functional as vxf  # noqa: E402
+import verl.utils.torch_functional as vF  # noqa: E402
+from verl.utils.model import compute_position_id_with_mask  # noqa: E402
+
+torch.set_num_threads(8)
+
+
+def _save(name, arrays, meta):
+    arrays = {k: (v.detach().cpu().numpy() if torch.is_tensor(v) else np.asarray(v)) for k, v in arrays.items()}
+    arrays["__meta__"] = np.array(json.dumps(meta))
+    path = os.path.join(HERE, name)
+    np.savez_compressed(path, **arrays)
+    print(f"wrote {path} ({os.path.getsize(path)} bytes)")
+
+
+# --------------------------------------------------------------------------------------------
+# A10-A13: vanilla PPO loss + entropy + KL, forward and backward (dp_actor.py:419-466)
+# --------------------------------------------------------------------------------------------
+def ppo_loss_inputs(g, B, R, kind):
+    old = -torch.rand(B, R, generator=g) * 6.0
+    delta = torch.randn(B, R, generator=g) * 0.3
+    if kind == "edges":
+        # hit the +-20 clamp, exact clip bounds and exact ties
+        delta[0, :4] = torch.tensor([25.0, -25.0, 20.0, -20.0])
+        delta[1, :3] = torch.tensor([float(np.log(np.float32(1.2))), float(np.log(np.float32(0.8))), 0.0])
+    logp = old + delta
+    adv = torch.randn(B, R, generator=g)
+    if kind == "edges":
+        adv[:, 5] = 0.0
+        adv[2, :] = -adv[2, :].abs()  # a row of negative advantages (dual-clip path)
+    mask = torch.ones(B, R, dtype=torch.int64)
+    lengths = torch.randint(1, R + 1, (B,), generator=g)
+    for i in range(B):
+        mask[i, lengths[i]:] = 0
+    if kind == "edges" and B > 3:
+        mask[3, :] = 0  # fully masked row
+        mask[3, 0] = 1
+    ent = torch.rand(B, R, generator=g) * 3.0
+    ref = logp + torch.randn(B, R, generator=g) * 0.2
+    if kind == "edges":
+        ref[0, 6:8] = logp[0, 6:8] + torch.tensor([30.0, -30.0])  # k3 clamps
+    return old.float(), logp.float(), adv.float(), mask, ent.float(), ref.float()
+
+
+def ref_actor_loss(old, logp, adv, mask, ent, ref, cfg):
+    logp = logp.clone().requires_grad_(True)
+    ent = ent.clone().requires_grad_(True)
+    pcfg = DictConfig(
+        clip_ratio=cfg["clip_ratio"],
+        clip_ratio_low=cfg["clip_ratio_low"],
+        clip_ratio_high=cfg["clip_ratio_high"],
+        clip_ratio_c=cfg["clip_ratio_c"],
+    )
+    mode = cfg["loss_agg_mode"]
+    pg_loss, pg_clipfrac, ppo_kl, pg_clipfrac_lower = ca.compute_policy_loss_vanilla(
+        old_log_prob=old, log_prob=logp, advantages=adv, response_mask=mask, loss_agg_mode=mode, config=pcfg
+    )
+    entropy_loss = ca.agg_loss(loss_mat=ent, loss_mask=mask, loss_agg_mode=mode)
+    policy_loss = pg_loss - entropy_loss * cfg["entropy_coeff"] if cfg["entropy_coeff"] != 0 else pg_loss
+    kld = ca.kl_penalty(logprob=logp, ref_logprob=ref, kl_penalty=cfg["kl_loss_type"])
+    kl_loss = ca.agg_loss(loss_mat=kld, loss_mask=mask, loss_agg_mode=mode)
+    if cfg["use_kl_loss"]:
+        policy_loss = policy_loss + kl_loss * cfg["kl_loss_coef"]
+    loss = policy_loss * cfg["loss_scale_factor"]
+    loss.backward()
+    return dict(
+        pg_loss=pg_loss.detach(),
+        pg_clipfrac=pg_clipfrac.detach(),
+        ppo_kl=ppo_kl.detach(),
+        pg_clipfrac_lower=pg_clipfrac_lower.detach(),
+        entropy_loss=entropy_loss.detach(),
+        kl_loss=kl_loss.detach(),
+        loss=loss.detach(),
+        dlogp=logp.grad.detach() if logp.grad is not None else torch.zeros_like(logp),
+        dentropy=ent.grad.detach() if ent.grad is not None else torch.zeros_like(ent),
+        kld=kld.detach(),
+    )
+
+
+def gen_ppo_loss():
+    g = torch.Generator().manual_seed(1234)
+    arrays, cases = {}, []
+    modes = ["token-mean", "seq-mean-token-sum", "seq-mean-token-mean", "seq-mean-token-sum-norm"]
+    kls = ["low_var_kl", "kl", "abs", "mse", "k3", "k1", "k2"]
+    ci = 0
+    for shape, kind in [((6, 16), "edges"), ((8, 64), "random"), ((16, 256), "random"), ((5, 33), "edges")]:
+        for mode in modes:
+            for kl in ([kls[ci % len(kls)], "low_var_kl"] if shape != (6, 16) else kls):
+                cfg = dict(
+                    clip_ratio=0.2,
+                    clip_ratio_low=0.2,
+                    clip_ratio_high=0.28 if ci % 3 == 1 else 0.2,
+                    clip_ratio_c=10.0 if ci % 3 == 1 else 3.0,
+                    loss_agg_mode=mode,
+                    entropy_coeff=[0.0, 0.001, 0.01][ci % 3],
+                    use_kl_loss=ci % 4 != 3,
+                    kl_loss_type=kl,
+                    kl_loss_coef=0.001 if ci % 2 == 0 else 0.05,
+                    loss_scale_factor=[1.0, 0.5, 0.125][ci % 3],
+                )
+                ins = ppo_loss_inputs(g, *shape, kind)
+                outs = ref_actor_loss(*ins, cfg)
+                for k, v in zip(["old_log_prob", "log_prob", "advantages", "response_mask", "entropy", "ref_log_prob"], ins):
+                    arrays[f"c{ci}_{k}"] = v
+                for k, v in outs.items():
+                    arrays[f"c{ci}_out_{k}"] = v
+                cases.append(cfg)
+                ci += 1
+    _save("ppo_loss.npz", arrays, {"cases": cases, "ref": "core_algos.py:703-889,1272-1307; dp_actor.py:419-466"})
+
+
+# --------------------------------------------------------------------------------------------
+# A11: masked_mean known answers from the reference's own test (tests/utils/test_torch_functional.py:55-66)
+# --------------------------------------------------------------------------------------------
+def gen_masked_mean():
+    arrays = {}
+    vals = torch.tensor([1.0, 2.0, float("nan"), 4.0])
+    mask = torch.tensor([1.0, 1.0, 0.0, 1.0])
+    arrays["kat_values"] = vals
+    arrays["kat_mask"] = mask
+    arrays["kat_out"] = vF.masked_mean(vals, mask)
+    g = torch.Generator().manual_seed(7)
+    v = torch.randn(9, 37, generator=g)
+    m = (torch.rand(9, 37, generator=g) > 0.3).to(torch.int64)
+    arrays["rand_values"] = v
+    arrays["rand_mask"] = m
+    arrays["rand_out_all"] = vF.masked_mean(v, m)
+    arrays["rand_out_axis1"] = vF.masked_mean(v, m, axis=1)
+    arrays["rand_whiten"] = vF.masked_whiten(v, m)
+    arrays["rand_var"] = vF.masked_var(v, m)
+    _save("masked_mean.npz", arrays, {"ref": "torch_functional.py:163-223; tests/utils/test_torch_functional.py:55-66"})
+
+
+# --------------------------------------------------------------------------------------------
+# A17: GRPO outcome advantage (core_algos.py:260-324)
+# --------------------------------------------------------------------------------------------
+def gen_grpo():
+    g = torch.Generator().manual_seed(99)
+    arrays, cases = {}, []
+    layouts = [
+        ("n8_interleaved", [8] * 8, False),
+        ("ragged_with_singletons", [3, 1, 5, 1, 2, 4], True),
+        ("n8_shuffled", [8] * 6, True),
+        ("ties_zero_std", [4, 4], False),
+    ]
+    ci = 0
+    for name, sizes, shuffle in layouts:
+        B = sum(sizes)
+        R = 24
+        uid = np.concatenate([np.full(s, f"uid-{gi}", dtype=object) for gi, s in enumerate(sizes)])
+        if shuffle:
+            perm = torch.randperm(B, generator=g).numpy()
+            uid = uid[perm]
+        mask = torch.ones(B, R, dtype=torch.int64)
+        lengths = torch.randint(1, R + 1, (B,), generator=g)
+        for i in range(B):
+            mask[i, lengths[i]:] = 0
+        rewards = torch.zeros(B, R)
+        if name == "ties_zero_std":
+            score = torch.ones(B)
+        else:
+            score = torch.bernoulli(torch.full((B,), 0.5), generator=g) + torch.randn(B, generator=g) * 0.1
+        for i in range(B):
+            rewards[i, lengths[i] - 1] = score[i]
+        if ci == 1:
+            rewards += torch.randn(B, R, generator=g) * 0.01 * mask  # dense token rewards too
+        for norm in (True, False):
+            adv, ret = ca.compute_grpo_outcome_advantage(
+                token_level_rewards=rewards, response_mask=mask, index=uid, norm_adv_by_std_in_grpo=norm
+            )
+            arrays[f"c{ci}_rewards"] = rewards
+            arrays[f"c{ci}_mask"] = mask
+            arrays[f"c{ci}_uid"] = np.array([str(u) for u in uid])
+            arrays[f"c{ci}_adv"] = adv
+            arrays[f"c{ci}_ret"] = ret
+            cases.append({"name": name, "norm_adv_by_std_in_grpo": norm, "epsilon": 1e-6})
+            ci += 1
+    _save("grpo.npz", arrays, {"cases": cases, "ref": "core_algos.py:260-324"})
+
+
+# --------------------------------------------------------------------------------------------
+# A18: GAE + masked_whiten (core_algos.py:208-256)
+# --------------------------------------------------------------------------------------------
+def gen_gae():
+    g = torch.Generator().manual_seed(5)
+    arrays, cases = {}, []
+    for ci, (B, R, gamma, lam, obs) in enumerate([(4, 12, 1.0, 1.0, False), (8, 64, 0.99, 0.95, True), (3, 7, 0.9, 0.5, True)]):
+        rewards = torch.randn(B, R, generator=g)
+        values = torch.randn(B, R, generator=g)
+        mask = torch.ones(B, R, dtype=torch.int64)
+        lengths = torch.randint(2, R + 1, (B,), generator=g)
+        for i in range(B):
+            mask[i, lengths[i]:] = 0
+        if obs:  # observation tokens inside the response (multi-turn), test_core_algos_on_cpu.py:134-188
+            mask[:, 1] = 0
+        adv, ret = ca.compute_gae_advantage_return(rewards, values, mask, gamma=gamma, lam=lam)
+        arrays[f"c{ci}_rewards"] = rewards
+        arrays[f"c{ci}_values"] = values
+        arrays[f"c{ci}_mask"] = mask
+        arrays[f"c{ci}_adv"] = adv
+        arrays[f"c{ci}_ret"] = ret
+        cases.append({"gamma": gamma, "lam": lam})
+    _save("gae.npz", arrays, {"cases": cases, "ref": "core_algos.py:208-256; torch_functional.py:206-223"})
+
+
+# --------------------------------------------------------------------------------------------
+# A8/A9: log-prob + entropy over the vocabulary, forward and backward (torch_functional.py:116-160)
+# --------------------------------------------------------------------------------------------
+def seeded_logits(seed, N, V, scale=3.0):
+    rng = np.random.default_rng(seed)
+    x = (rng.standard_normal((N, V), dtype=np.float32) * np.float32(scale)).astype(np.float32)
+    labels = rng.integers(0, V, size=(N,), dtype=np.int64)
+    dlogp = rng.standard_normal((N,), dtype=np.float32)
+    dent = rng.standard_normal((N,), dtype=np.float32)
+    return x, labels, dlogp, dent
+
+
+def gen_logprob():
+    arrays, cases = {}, []
+    specs = [(11, 64, 1000, False), (12, 33, 4099, False), (13, 8, 151936, True), (14, 17, 151936, True)]
+    for ci, (seed, N, V, from_seed) in enumerate(specs):
+        x, labels, dlogp, dent = seeded_logits(seed, N, V)
+        for dt in ("fp32", "bf16"):
+            logits = torch.from_numpy(x)
+            if dt == "bf16":
+                logits = logits.to(torch.bfloat16)
+            # fp32 path of the reference (flash-attn CE semantics = fp32 math on the given logits)
+            lf = logits.float().clone().requires_grad_(True)
+            lp = vF.logprobs_from_logits_v2(lf, torch.from_numpy(labels))
+            ent = vF.entropy_from_logits(lf)
+            (lp * torch.from_numpy(dlogp)).sum().backward(retain_graph=True)
+            g_lp = lf.grad.clone()
+            lf.grad = None
+            (ent * torch.from_numpy(dent)).sum().backward()
+            g_ent = lf.grad.clone()
+            key = f"c{ci}_{dt}"
+            arrays[f"{key}_logp"] = lp.detach()
+            arrays[f"{key}_entropy"] = ent.detach()
+            # backward outputs are large at V=151936; keep checksums + a strided sample there
+            if from_seed:
+                idx = np.arange(0, N * V, 997)
+                arrays[f"{key}_dlogits_lp_sample"] = g_lp.reshape(-1)[idx]
+                arrays[f"{key}_dlogits_ent_sample"] = g_ent.reshape(-1)[idx]
+                arrays[f"{key}_dlogits_lp_rowsum_abs"] = g_lp.abs().sum(-1)
+                arrays[f"{key}_dlogits_ent_rowsum_abs"] = g_ent.abs().sum(-1)
+            else:
+                arrays[f"{key}_dlogits_lp"] = g_lp
+                arrays[f"{key}_dlogits_ent"] = g_ent
+            if dt == "bf16":
+                # the reference's own bf16 path (keeps bf16 output, torch_functional.py:125-133)
+                arrays[f"{key}_logp_refbf16"] = vF.logprobs_from_logits_v2(logits, torch.from_numpy(labels)).float()
+        if not from_seed:
+            arrays[f"c{ci}_logits"] = x
+            arrays[f"c{ci}_labels"] = labels
+            arrays[f"c{ci}_dlogp"] = dlogp
+            arrays[f"c{ci}_dentropy"] = dent
+        arrays[f"c{ci}_sha256"] = np.array(hashlib.sha256(x.tobytes()).hexdigest())
+        cases.append({"seed": seed, "N": N, "V": V, "inputs_from_seed": from_seed, "scale": 3.0})
+    _save("logprob.npz", arrays, {"cases": cases, "generator": "numpy default_rng(seed): standard_normal(N,V,f32)*scale, integers(0,V,N), standard_normal(N) x2",
+                                  "ref": "torch_functional.py:116-160"})
+
+
+# --------------------------------------------------------------------------------------------
+# A21: FusedLinearForPPO (utils/experimental/torch_functional.py:20-216)
+# --------------------------------------------------------------------------------------------
+def gen_fused_linear():
+    arrays, cases = {}, []
+    for ci, (seed, N, H, V, temp) in enumerate([(21, 40, 64, 512, 1.0), (22, 130, 96, 1000, 1.5)]):
+        rng = np.random.default_rng(seed)
+        h = (rng.random((N, H), dtype=np.float32) - 0.5).astype(np.float32)
+        w = (rng.random((V, H), dtype=np.float32) - 0.5).astype(np.float32)
+        ids = rng.integers(0, V, size=(N,), dtype=np.int64)
+        dlp = rng.standard_normal((N,), dtype=np.float32)
+        den = rng.standard_normal((N,), dtype=np.float32)
+        ht = torch.from_numpy(h).requires_grad_(True)
+        wt = torch.from_numpy(w).requires_grad_(True)
+        lp, ent = vxf.FusedLinearForPPO(chunk_size=32)(ht, wt, torch.from_numpy(ids), temperature=temp)
+        ((lp * torch.from_numpy(dlp)).sum() + (ent * torch.from_numpy(den)).sum()).backward()
+        for k, v in dict(hidden=h, weight=w, input_ids=ids, dlogp=dlp, dentropy=den, out_logp=lp.detach(),
+                         out_entropy=ent.detach(), out_dhidden=ht.grad, out_dweight=wt.grad).items():
+            arrays[f"c{ci}_{k}"] = v
+        cases.append({"N": N, "H": H, "V": V, "temperature": temp})
+    _save("fused_linear.npz", arrays, {"cases": cases, "ref": "utils/experimental/torch_functional.py:20-216"})
+
+
+# --------------------------------------------------------------------------------------------
+# A4/A5: response mask, prompt positions and response-position continuation
+# --------------------------------------------------------------------------------------------
+def gen_masks():
+    arrays = {}
+    # the docstring example of get_response_mask (torch_functional.py:226-246)
+    resp = torch.tensor([[20, 10, 34, 1, 0, 0, 0], [78, 0, 76, 2, 1, 0, 0], [23, 98, 1, 0, 0, 0, 0], [33, 3, 98, 45, 1, 0, 0]])
+    arrays["doc_responses"] = resp
+    arrays["doc_mask_eos1"] = vF.get_response_mask(resp, eos_token=1)
+    arrays["doc_mask_eos12"] = vF.get_response_mask(resp, eos_token=[1, 2])
+    g = torch.Generator().manual_seed(3)
+    r = torch.randint(0, 40, (32, 50), generator=g)
+    r[5, :] = 7  # row that is all EOS
+    arrays["rand_responses"] = r
+    arrays["rand_mask_eos7"] = vF.get_response_mask(r, eos_token=7)
+    arrays["rand_mask_eos7_9_11"] = vF.get_response_mask(r, eos_token=[7, 9, 11])
+    # left-padded prompt attention masks -> position ids (utils/model.py:219)
+    am = torch.ones(16, 20, dtype=torch.int64)
+    pads = torch.randint(0, 20, (16,), generator=g)
+    for i in range(16):
+        am[i, : pads[i]] = 0
+    arrays["prompt_attention_mask"] = am
+    pos = compute_position_id_with_mask(am)
+    arrays["prompt_position_ids"] = pos
+    # response position continuation (hf_rollout.py:151-155)
+    R = 9
+    delta = torch.arange(1, R + 1).unsqueeze(0).repeat(16, 1)
+    arrays["full_position_ids"] = torch.cat([pos, pos[:, -1:] + delta], dim=-1)
+    _save("masks.npz", arrays, {"ref": "torch_functional.py:226-246; model.py:219; hf_rollout.py:151-160"})
+
+
+if __name__ == "__main__":
+    which = sys.argv[1:] or ["ppo_loss", "masked_mean", "grpo", "gae", "logprob", "fused_linear", "masks"]
+    for w in which:
+        globals()[f"gen_{w}"]()
