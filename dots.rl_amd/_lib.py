@@ -1,0 +1,137 @@
+"""ctypes binding of ``libdotsrl_amd.so`` (the C-ABI declared in ``include/dotsrl_amd.h``).
+
+torch is imported first on purpose: torch ships its own ``libamdhip64.so.7`` and the HIP library is
+linked against the same SONAME, so the dynamic loader reuses torch's HIP runtime and both sides share
+one device context, one allocator view and the same streams.
+
+There is no fallback: if the library is missing or fails to load, every entry point raises.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  (must precede the HIP library load, see module docstring)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("DOTSRL_AMD_LIB", os.path.join(_HERE, "libdotsrl_amd.so"))
+
+DRL_I64, DRL_I32, DRL_U8, DRL_F32, DRL_BF16 = 0, 1, 2, 3, 4
+DRL_OK = 0
+PPO_OUT_N = 8
+
+AGG_MODES = {"token-mean": 0, "seq-mean-token-sum": 1, "seq-mean-token-mean": 2, "seq-mean-token-sum-norm": 3}
+KL_TYPES = {"kl": 0, "k1": 0, "abs": 1, "mse": 2, "k2": 2, "low_var_kl": 3, "k3": 3}
+KL_NONE = -1
+
+
+class PPOLossParams(ctypes.Structure):
+    _fields_ = [
+        ("clip_ratio_low", ctypes.c_float),
+        ("clip_ratio_high", ctypes.c_float),
+        ("clip_ratio_c", ctypes.c_float),
+        ("entropy_coeff", ctypes.c_float),
+        ("kl_loss_coef", ctypes.c_float),
+        ("loss_scale_factor", ctypes.c_float),
+        ("loss_agg_mode", ctypes.c_int32),
+        ("kl_type", ctypes.c_int32),
+    ]
+
+
+class SamplingParams(ctypes.Structure):
+    _fields_ = [
+        ("do_sample", ctypes.c_int32),
+        ("temperature", ctypes.c_float),
+        ("top_k", ctypes.c_int32),
+        ("top_p", ctypes.c_float),
+        ("seed", ctypes.c_uint64),
+        ("offset", ctypes.c_uint64),
+        ("row_base", ctypes.c_int64),
+        ("pad_token_id", ctypes.c_int64),
+        ("eos_ids", ctypes.c_void_p),
+        ("n_eos", ctypes.c_int32),
+    ]
+
+
+class AdamWParams(ctypes.Structure):
+    _fields_ = [
+        ("lr", ctypes.c_float),
+        ("beta1", ctypes.c_float),
+        ("beta2", ctypes.c_float),
+        ("eps", ctypes.c_float),
+        ("weight_decay", ctypes.c_float),
+        ("step", ctypes.c_int32),
+        ("max_grad_norm", ctypes.c_float),
+    ]
+
+
+P = ctypes.c_void_p
+I64 = ctypes.c_int64
+I32 = ctypes.c_int32
+F32 = ctypes.c_float
+SZ = ctypes.c_size_t
+
+# name -> (restype, argtypes); must match include/dotsrl_amd.h exactly
+SIGNATURES = {
+    "drl_last_error": (ctypes.c_char_p, []),
+    "drl_abi_version": (ctypes.c_int, []),
+    "drl_device_cu_count": (ctypes.c_int, []),
+    "drl_ppo_loss_workspace_bytes": (SZ, [I64, I64]),
+    "drl_ppo_loss_fwd_bwd": (ctypes.c_int, [P, P, P, P, I32, P, P, I64, I64, ctypes.POINTER(PPOLossParams), P, P, P, P,
+                                            SZ, P]),
+    "drl_kl_penalty": (ctypes.c_int, [P, P, I64, I32, P, P]),
+    "drl_agg_loss_workspace_bytes": (SZ, [I64, I64]),
+    "drl_agg_loss": (ctypes.c_int, [P, P, I32, I64, I64, I32, P, P, SZ, P]),
+    "drl_logprob_entropy_fwd": (ctypes.c_int, [P, I32, I64, I64, I64, P, F32, P, P, P, P]),
+    "drl_logprob_entropy_bwd": (ctypes.c_int, [P, I32, I64, I64, I64, P, F32, P, P, P, P, P, I32, I64, P]),
+    "drl_grpo_workspace_bytes": (SZ, [I64]),
+    "drl_grpo_outcome_advantage": (ctypes.c_int, [P, P, I32, P, P, P, I64, I64, I64, F32, I32, P, P, P, SZ, P]),
+    "drl_gae_workspace_bytes": (SZ, [I64, I64]),
+    "drl_gae_advantage_return": (ctypes.c_int, [P, P, P, I32, I64, I64, F32, F32, P, P, P, SZ, P]),
+    "drl_select_tokens": (ctypes.c_int, [P, I32, I64, I64, I64, ctypes.POINTER(SamplingParams), P, P, I64, P]),
+    "drl_response_mask": (ctypes.c_int, [P, I64, I64, I64, P, I32, P, I32, I64, P]),
+    "drl_position_ids": (ctypes.c_int, [P, I32, I64, I64, P, P]),
+    "drl_response_position_ids": (ctypes.c_int, [P, I64, I64, I64, P]),
+    "drl_grad_norm_workspace_bytes": (SZ, [I64]),
+    "drl_grad_norm": (ctypes.c_int, [P, I64, P, P, SZ, P]),
+    "drl_adamw_step": (ctypes.c_int, [P, P, P, P, P, I64, ctypes.POINTER(AdamWParams), P, P]),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+class NativeLibraryError(RuntimeError):
+    pass
+
+
+def load(path: str | None = None):
+    """Load (once) and return the ctypes handle; raises NativeLibraryError if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise NativeLibraryError(
+                f"HIP library not found at {p}: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+                "or `make -C dots.rl_amd/csrc` (there is no CPU/eager fallback)")
+        lib = ctypes.CDLL(p, mode=ctypes.RTLD_GLOBAL)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        if lib.drl_abi_version() != 1:
+            raise NativeLibraryError(f"ABI mismatch: library reports {lib.drl_abi_version()}")
+        _lib = lib
+    return _lib
+
+
+def check(rc: int, what: str = ""):
+    if rc != DRL_OK:
+        msg = load().drl_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what} failed (code {rc}): {msg}")

@@ -1,0 +1,184 @@
+// K3 — GRPO outcome advantage and K5 — GAE + masked_whiten, on device.
+// References: verl/trainer/ppo/core_algos.py:208-256 (GAE), 260-324 (GRPO);
+// verl/utils/torch_functional.py:171-223 (masked_mean / masked_var / masked_whiten).
+// The reference runs both as Python loops on the driver CPU (core_algos.py:297-324); here the scores
+// are row sums of the (B, R) rewards in HBM, the group statistics come from a host-built CSR of the uid
+// groups (order of first appearance, the order torch.stack sees them), and the (B, R) outputs are
+// written in one coalesced pass.
+#include "common.h"
+
+namespace drl {
+namespace {
+
+// scores[b] = token_level_rewards[b, :].sum(-1), one wave per row
+__global__ __launch_bounds__(256) void row_sum_kernel(const float* x, int64_t B, int64_t R, float* out) {
+  const int64_t row = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= B) return;
+  float s = 0.f;
+  for (int64_t t = lane; t < R; t += 64) s += x[row * R + t];
+  s = wave_sum(s);
+  if (lane == 0) out[row] = s;
+}
+
+// per row: group mean/std over the CSR members (float32, torch.mean / unbiased torch.std), then
+// advantages[b, t] = returns[b, t] = norm_score[b] * mask[b, t]
+template <int MDT>
+__global__ __launch_bounds__(256) void grpo_write_kernel(const float* scores, const void* mask, const int32_t* row_group,
+                                                         const int32_t* off, const int32_t* mem, int64_t B, int64_t R,
+                                                         float eps, int norm_by_std, float* adv, float* ret) {
+  const int64_t row = blockIdx.x;
+  __shared__ float s_val;
+  if (threadIdx.x == 0) {
+    const int g = row_group[row];
+    const int b = off[g], e = off[g + 1], n = e - b;
+    float mean = 0.f, stdv = 1.f;
+    if (n > 1) {
+      float sum = 0.f;
+      for (int k = b; k < e; ++k) sum += scores[mem[k]];
+      mean = sum / static_cast<float>(n);
+      float ss = 0.f;
+      for (int k = b; k < e; ++k) {
+        const float d = scores[mem[k]] - mean;
+        ss += d * d;
+      }
+      stdv = sqrtf(ss / static_cast<float>(n - 1));
+    }
+    const float sc = scores[row];
+    s_val = norm_by_std ? (sc - mean) / (stdv + eps) : sc - mean;
+  }
+  __syncthreads();
+  const float v = s_val;
+  for (int64_t t = threadIdx.x; t < R; t += blockDim.x) {
+    const float o = v * mask_at<MDT>(mask, row * R + t);
+    adv[row * R + t] = o;
+    if (ret) ret[row * R + t] = o;
+  }
+}
+
+// GAE reverse scan, one thread per row (core_algos.py:237-256); also emits returns = adv + values.
+template <int MDT>
+__global__ __launch_bounds__(256) void gae_scan_kernel(const float* r, const float* v, const void* mask, int64_t B,
+                                                       int64_t R, float gamma, float lam, float* adv, float* ret) {
+  const int64_t row = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (row >= B) return;
+  float nextvalues = 0.f, lastgaelam = 0.f;
+  for (int64_t t = R - 1; t >= 0; --t) {
+    const int64_t i = row * R + t;
+    const float m = mask_at<MDT>(mask, i);
+    const float delta = r[i] + gamma * nextvalues - v[i];
+    const float lg = delta + gamma * lam * lastgaelam;
+    nextvalues = v[i] * m + (1.f - m) * nextvalues;
+    lastgaelam = lg * m + (1.f - m) * lastgaelam;
+    adv[i] = lastgaelam;
+    ret[i] = lastgaelam + v[i];
+  }
+}
+
+// masked_whiten over the whole (B, R) tensor in place: mean, unbiased var, (x - mean) * rsqrt(var + 1e-8).
+// One workgroup (the tensor is one PPO batch of advantages, a few MB); three ordered passes.
+template <int MDT>
+__global__ __launch_bounds__(1024) void masked_whiten_kernel(float* x, const void* mask, int64_t n, int* err) {
+  __shared__ double red[16][2];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  double s = 0.0, c = 0.0;
+  for (int64_t i = tid; i < n; i += 1024) {
+    const float m = mask_at<MDT>(mask, i);
+    s += (m != 0.f) ? static_cast<double>(x[i]) * m : 0.0;
+    c += m;
+  }
+  s = wave_sum(s);
+  c = wave_sum(c);
+  if (lane == 0) { red[wave][0] = s; red[wave][1] = c; }
+  __syncthreads();
+  double S = 0, C = 0;
+  for (int w = 0; w < 16; ++w) { S += red[w][0]; C += red[w][1]; }
+  __syncthreads();
+  const float mean = static_cast<float>(S / (C + 1e-8));
+  double q = 0.0;
+  for (int64_t i = tid; i < n; i += 1024) {
+    const float m = mask_at<MDT>(mask, i);
+    const double d = static_cast<double>(x[i] - mean);
+    q += (m != 0.f) ? d * d * m : 0.0;
+  }
+  q = wave_sum(q);
+  if (lane == 0) red[wave][0] = q;
+  __syncthreads();
+  double Q = 0;
+  for (int w = 0; w < 16; ++w) Q += red[w][0];
+  if (tid == 0 && (C == 0.0 || C == 1.0)) *err = 1;  // the reference raises ValueError
+  const double var = Q / (C + 1e-8) * (C / (C - 1.0));
+  const float rs = static_cast<float>(1.0 / sqrt(var + 1e-8));
+  for (int64_t i = tid; i < n; i += 1024) x[i] = (x[i] - mean) * rs;
+}
+
+}  // namespace
+}  // namespace drl
+
+extern "C" {
+
+size_t drl_grpo_workspace_bytes(int64_t B) { return drl::round_up(static_cast<size_t>(B) * sizeof(float), 256); }
+
+int drl_grpo_outcome_advantage(const float* rewards, const void* mask, int32_t mdt, const int32_t* row_group,
+                               const int32_t* group_offsets, const int32_t* group_members, int64_t B, int64_t R,
+                               int64_t G, float epsilon, int32_t norm_adv_by_std, float* advantages, float* returns,
+                               void* workspace, size_t workspace_bytes, void* stream) {
+  using namespace drl;
+  DRL_CHECK_ARG(rewards && mask && row_group && group_offsets && group_members && advantages, "NULL input");
+  DRL_CHECK_ARG(B >= 1 && R >= 1 && G >= 1 && G <= B, "bad shape B=%lld R=%lld G=%lld", (long long)B, (long long)R,
+                (long long)G);
+  DRL_CHECK_ARG(mdt == DRL_I64 || mdt == DRL_I32 || mdt == DRL_U8 || mdt == DRL_F32, "bad mask dtype");
+  if (workspace == nullptr || workspace_bytes < drl_grpo_workspace_bytes(B))
+    return fail(DRL_ERR_WORKSPACE, "workspace too small");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  float* scores = static_cast<float*>(workspace);
+  hipLaunchKernelGGL(row_sum_kernel, dim3((B + 3) / 4), dim3(256), 0, s, rewards, B, R, scores);
+  DRL_LAUNCH_CHECK();
+#define DRL_GRPO(MDT)                                                                                              \
+  hipLaunchKernelGGL(grpo_write_kernel<MDT>, dim3(B), dim3(256), 0, s, scores, mask, row_group, group_offsets,       \
+                     group_members, B, R, epsilon, norm_adv_by_std, advantages, returns)
+  switch (mdt) {
+    case DRL_I64: DRL_GRPO(DRL_I64); break;
+    case DRL_I32: DRL_GRPO(DRL_I32); break;
+    case DRL_U8: DRL_GRPO(DRL_U8); break;
+    default: DRL_GRPO(DRL_F32); break;
+  }
+#undef DRL_GRPO
+  DRL_LAUNCH_CHECK();
+  return DRL_OK;
+}
+
+size_t drl_gae_workspace_bytes(int64_t B, int64_t R) {
+  (void)B;
+  (void)R;
+  return 256;
+}
+
+int drl_gae_advantage_return(const float* rewards, const float* values, const void* mask, int32_t mdt, int64_t B,
+                             int64_t R, float gamma, float lam, float* advantages, float* returns, void* workspace,
+                             size_t workspace_bytes, void* stream) {
+  using namespace drl;
+  DRL_CHECK_ARG(rewards && values && mask && advantages && returns, "NULL input");
+  DRL_CHECK_ARG(B >= 1 && R >= 1, "bad shape");
+  DRL_CHECK_ARG(mdt == DRL_I64 || mdt == DRL_I32 || mdt == DRL_U8 || mdt == DRL_F32, "bad mask dtype");
+  if (workspace == nullptr || workspace_bytes < drl_gae_workspace_bytes(B, R))
+    return fail(DRL_ERR_WORKSPACE, "workspace too small");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  int* err = static_cast<int*>(workspace);
+  DRL_HIP(hipMemsetAsync(err, 0, sizeof(int), s));
+#define DRL_GAE(MDT)                                                                                               \
+  hipLaunchKernelGGL(gae_scan_kernel<MDT>, dim3((B + 255) / 256), dim3(256), 0, s, rewards, values, mask, B, R,      \
+                     gamma, lam, advantages, returns);                                                              \
+  hipLaunchKernelGGL(masked_whiten_kernel<MDT>, dim3(1), dim3(1024), 0, s, advantages, mask, B * R, err)
+  switch (mdt) {
+    case DRL_I64: DRL_GAE(DRL_I64); break;
+    case DRL_I32: DRL_GAE(DRL_I32); break;
+    case DRL_U8: DRL_GAE(DRL_U8); break;
+    default: DRL_GAE(DRL_F32); break;
+  }
+#undef DRL_GAE
+  DRL_LAUNCH_CHECK();
+  return DRL_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,126 @@
+// Shared device/host helpers for the gfx950 kernels behind include/dotsrl_amd.h.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <string>
+
+#include "dotsrl_amd.h"
+
+namespace drl {
+
+// ---------------------------------------------------------------- host: errors
+void set_error(const char* fmt, ...);
+int fail(int code, const char* fmt, ...);
+
+#define DRL_CHECK_ARG(cond, ...)                     \
+  do {                                               \
+    if (!(cond)) return ::drl::fail(DRL_ERR_INVALID, __VA_ARGS__); \
+  } while (0)
+
+#define DRL_HIP(call)                                                                               \
+  do {                                                                                              \
+    hipError_t e_ = (call);                                                                         \
+    if (e_ != hipSuccess)                                                                           \
+      return ::drl::fail(DRL_ERR_HIP, "%s failed: %s (%s:%d)", #call, hipGetErrorString(e_), __FILE__, \
+                         __LINE__);                                                                 \
+  } while (0)
+
+#define DRL_LAUNCH_CHECK() DRL_HIP(hipGetLastError())
+
+int cu_count();  // cached per device
+
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+inline size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// ---------------------------------------------------------------- device: wave/block reductions
+constexpr int kWave = 64;
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));
+  return v;
+}
+__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
+
+// bf16 <-> f32 (bit-level; bf16 stored as uint16_t)
+__device__ __forceinline__ float bf16_to_f32(uint16_t h) { return __uint_as_float(static_cast<uint32_t>(h) << 16); }
+__device__ __forceinline__ uint16_t f32_to_bf16(float f) {
+  // round-to-nearest-even; NaN stays NaN (quiet bit forced)
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x7fffffu)) return static_cast<uint16_t>((u >> 16) | 0x40u);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return static_cast<uint16_t>(u >> 16);
+}
+
+// Mask element -> 0/1 float, for the mask dtypes the boundary accepts.
+template <int DT>
+__device__ __forceinline__ float mask_at(const void* m, int64_t i) {
+  if constexpr (DT == DRL_I64) return static_cast<float>(static_cast<const int64_t*>(m)[i]);
+  else if constexpr (DT == DRL_I32) return static_cast<float>(static_cast<const int32_t*>(m)[i]);
+  else if constexpr (DT == DRL_U8) return static_cast<float>(static_cast<const uint8_t*>(m)[i]);
+  else return static_cast<const float*>(m)[i];
+}
+
+// Grid barrier for persistent launches whose every workgroup is co-resident (grid <= CUs x occupancy).
+// Counter form with agent-scope release before arrive and acquire after (MI355X_MICROARCH.md,
+// "barrier-counter"); `counter` is zeroed on the stream before the launch. A bounded spin sets
+// *timeout instead of hanging the GPU if residency was ever violated.
+__device__ __forceinline__ void grid_barrier(unsigned* counter, unsigned expected, unsigned* timeout) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned spins = 0;
+    while (__hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < expected) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > (1u << 26)) {
+        __hip_atomic_store(timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+}
+
+// "Last workgroup to arrive" ticket: every workgroup publishes its partials, then takes a ticket; the
+// one that draws gridDim-1 reduces all partials in a fixed order (bitwise-reproducible result).
+// Returns true in every thread of the last workgroup.
+__device__ __forceinline__ bool last_block_ticket(unsigned* ticket) {
+  __shared__ int is_last;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    is_last = (t == gridDim.x - 1);
+    if (is_last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  return is_last != 0;
+}
+
+}  // namespace drl

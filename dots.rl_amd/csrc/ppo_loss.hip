@@ -1,0 +1,516 @@
+// K1 — fused actor loss (vanilla PPO clip + dual clip, entropy bonus, KL-to-ref), forward AND backward,
+// one pass over HBM. Replaces dp_actor.py:419-466 (+ core_algos.py:703-736, 815-889, 1272-1307).
+//
+// Layout: the (B, R) float32 inputs are flattened to N = B*R tokens; each workgroup of a persistent grid
+// (<= 2 per CU, all co-resident) owns one contiguous token range and walks it 4 tokens per lane
+// (16-B loads, 1 KiB per wave-instruction per input).
+// token-mean needs the global mask count before any gradient can be written, so that mode runs two
+// phases around a grid barrier: phase 1 reads ONLY the mask, counts it and keeps it on chip as a bit
+// image in LDS (one 64-bit ballot per wave and element slot); phase 2 reads the other inputs, takes the
+// mask bits from LDS and writes the gradients. Every input byte crosses HBM once. The other modes know
+// their gradient weights up front (seq-mean-token-mean gets per-row counts from a small pre-pass) and
+// run phase 2 only. Forward scalars: per-workgroup partials (double) reduced by the last workgroup in a
+// fixed order, so results are bitwise reproducible run to run.
+#include "common.h"
+
+namespace drl {
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kTokPerIter = kThreads * 4;      // 1024 tokens per workgroup iteration
+constexpr int kBitWords = 4096;                // LDS bit image: 4096 x 64 bit = 32 KiB = 256 Ki tokens
+constexpr int kNumPartials = 8;
+
+struct Header {          // zeroed on the stream before every launch
+  unsigned barrier;
+  unsigned ticket;
+  unsigned timeout;
+  unsigned pad;
+  double mask_count;     // global sum(mask), published before the barrier
+  double pad2[6];
+};
+
+struct Args {
+  const float* old_lp;
+  const float* lp;
+  const float* adv;
+  const void* mask;
+  const float* ent;
+  const float* ref;
+  const float* rowcnt;  // seq-mean-token-mean: sum(mask) per row
+  float* dlp;
+  float* dent;
+  float* out;
+  Header* hdr;
+  double* partials;     // gridDim.x * kNumPartials
+  int64_t N, B, R;
+  float lo, hi, clip_c, ent_coef, kl_coef, lsf;
+  int mode, kl;
+};
+
+template <int MDT>
+__device__ __forceinline__ void load_mask4(const void* m, int64_t t, int64_t N, bool vec, float v[4]) {
+  if (vec && t + 3 < N) {
+    if constexpr (MDT == DRL_I64) {
+      const int4* p = reinterpret_cast<const int4*>(static_cast<const int64_t*>(m) + t);
+      int4 a = p[0], b = p[1];
+      v[0] = static_cast<float>(static_cast<int64_t>((static_cast<uint64_t>(static_cast<uint32_t>(a.y)) << 32) | static_cast<uint32_t>(a.x)));
+      v[1] = static_cast<float>(static_cast<int64_t>((static_cast<uint64_t>(static_cast<uint32_t>(a.w)) << 32) | static_cast<uint32_t>(a.z)));
+      v[2] = static_cast<float>(static_cast<int64_t>((static_cast<uint64_t>(static_cast<uint32_t>(b.y)) << 32) | static_cast<uint32_t>(b.x)));
+      v[3] = static_cast<float>(static_cast<int64_t>((static_cast<uint64_t>(static_cast<uint32_t>(b.w)) << 32) | static_cast<uint32_t>(b.z)));
+    } else if constexpr (MDT == DRL_I32) {
+      int4 a = *reinterpret_cast<const int4*>(static_cast<const int32_t*>(m) + t);
+      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+    } else if constexpr (MDT == DRL_U8) {
+      uint32_t a = *reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(m) + t);
+      v[0] = a & 0xff; v[1] = (a >> 8) & 0xff; v[2] = (a >> 16) & 0xff; v[3] = a >> 24;
+    } else {
+      float4 a = *reinterpret_cast<const float4*>(static_cast<const float*>(m) + t);
+      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = (t + j < N) ? mask_at<MDT>(m, t + j) : 0.f;
+  }
+}
+
+__device__ __forceinline__ void load4(const float* p, int64_t t, int64_t N, bool vec, float v[4]) {
+  if (vec && t + 3 < N) {
+    float4 a = *reinterpret_cast<const float4*>(p + t);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = (t + j < N) ? p[t + j] : 0.f;
+  }
+}
+
+__device__ __forceinline__ void store4(float* p, int64_t t, int64_t N, bool vec, const float v[4]) {
+  if (vec && t + 3 < N) {
+    *reinterpret_cast<float4*>(p + t) = make_float4(v[0], v[1], v[2], v[3]);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (t + j < N) p[t + j] = v[j];
+  }
+}
+
+// kl_penalty value and d/d logprob (core_algos.py:1272-1307)
+__device__ __forceinline__ void kl_term(int kl, float lp, float ref, float& val, float& dval) {
+  switch (kl) {
+    case DRL_KL_K1: val = lp - ref; dval = 1.f; break;
+    case DRL_KL_ABS: {
+      float d = lp - ref;
+      val = fabsf(d);
+      dval = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
+      break;
+    }
+    case DRL_KL_K2: {
+      float d = lp - ref;
+      val = 0.5f * (d * d);
+      dval = d;
+      break;
+    }
+    case DRL_KL_K3: {
+      float raw = ref - lp;
+      float k = fminf(fmaxf(raw, -20.f), 20.f);
+      float g1 = (raw >= -20.f && raw <= 20.f) ? 1.f : 0.f;
+      float r = expf(k);
+      float kld = (r - k) - 1.f;
+      val = fminf(fmaxf(kld, -10.f), 10.f);
+      float g2 = (kld >= -10.f && kld <= 10.f) ? 1.f : 0.f;
+      dval = -(r - 1.f) * g1 * g2;
+      break;
+    }
+    default: val = 0.f; dval = 0.f;
+  }
+}
+
+template <int MDT, bool TWO_PHASE>
+__global__ __launch_bounds__(kThreads) void ppo_loss_kernel(Args a) {
+  __shared__ unsigned long long bits[TWO_PHASE ? kBitWords : 1];
+  __shared__ double red[kThreads / kWave][kNumPartials];
+  __shared__ int wg_flags;  // bit0: keep mask on chip
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t N = a.N;
+  // contiguous range per workgroup, multiple of 4 tokens
+  const int64_t per = ((N + gridDim.x - 1) / gridDim.x + 3) & ~int64_t(3);
+  const int64_t t_begin = min(N, per * blockIdx.x);
+  const int64_t t_end = min(N, t_begin + per);
+  const bool vec = true;  // host guarantees 16-B aligned bases; tails fall back to scalar
+
+  float inv_cnt_global = 0.f;
+  const int64_t n_iter = (t_end - t_begin + kTokPerIter - 1) / kTokPerIter;
+
+  if constexpr (TWO_PHASE) {
+    // ---- phase 1: mask -> count + on-chip bit image
+    if (tid == 0) wg_flags = (n_iter * 16 <= kBitWords) ? 1 : 0;
+    __syncthreads();
+    const bool keep = wg_flags & 1;
+    float cnt = 0.f;
+    bool nonbin = false;
+    for (int64_t it = 0; it < n_iter; ++it) {
+      const int64_t t = t_begin + it * kTokPerIter + tid * 4;
+      float m[4];
+      if (t < t_end) load_mask4<MDT>(a.mask, t, t_end, vec, m);
+      else m[0] = m[1] = m[2] = m[3] = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        cnt += m[j];
+        nonbin |= (m[j] != 0.f && m[j] != 1.f);
+        unsigned long long b = __ballot(m[j] != 0.f);
+        if (keep && lane == 0) bits[(it * 4 + wave) * 4 + j] = b;
+      }
+    }
+    if (__any(nonbin) && lane == 0) atomicAnd(&wg_flags, ~1);
+    double c = wave_sum(static_cast<double>(cnt));
+    if (lane == 0) red[wave][0] = c;
+    __syncthreads();
+    if (tid == 0) {
+      double s = red[0][0] + red[1][0] + red[2][0] + red[3][0];
+      atomicAdd(&a.hdr->mask_count, s);
+    }
+    grid_barrier(&a.hdr->barrier, gridDim.x, &a.hdr->timeout);
+    const double total = __hip_atomic_load(&a.hdr->mask_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    inv_cnt_global = static_cast<float>(total);  // reuse as the token-mean denominator base
+  }
+  const bool keep_bits = TWO_PHASE && (wg_flags & 1);
+
+  // ---- phase 2: per-token loss terms, gradients, weighted partial sums
+  const float denom_tm = inv_cnt_global + 1e-8f;  // masked_mean: sum / (mask.sum() + 1e-8)
+  float s_pg = 0.f, s_clip = 0.f, s_kl = 0.f, s_cliplow = 0.f, s_ent = 0.f, s_kld = 0.f, s_cnt = 0.f;
+  const bool has_ent = a.ent != nullptr, has_kl = a.kl != DRL_KL_NONE;
+  const bool want_dlp = a.dlp != nullptr, want_dent = a.dent != nullptr;
+
+  for (int64_t it = 0; it < n_iter; ++it) {
+    const int64_t t = t_begin + it * kTokPerIter + tid * 4;
+    if (t >= t_end) continue;
+    float m[4], old[4], lp[4], A[4], en[4], rf[4];
+    if (keep_bits) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) m[j] = (bits[(it * 4 + wave) * 4 + j] >> lane) & 1ull ? 1.f : 0.f;
+    } else {
+      load_mask4<MDT>(a.mask, t, t_end, vec, m);
+    }
+    load4(a.old_lp, t, t_end, vec, old);
+    load4(a.lp, t, t_end, vec, lp);
+    load4(a.adv, t, t_end, vec, A);
+    if (has_ent) load4(a.ent, t, t_end, vec, en);
+    if (has_kl) load4(a.ref, t, t_end, vec, rf);
+    float g_lp[4], g_en[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const bool valid = t + j < t_end;
+      // compute_policy_loss_vanilla, float32 with the reference's op order
+      const float raw = lp[j] - old[j];
+      const float nkl = fminf(fmaxf(raw, -20.f), 20.f);
+      const float gate = (raw >= -20.f && raw <= 20.f) ? 1.f : 0.f;
+      const float ratio = expf(nkl);
+      const float negA = -A[j];
+      const float L1 = negA * ratio;
+      const float rc = fminf(fmaxf(ratio, a.lo), a.hi);
+      const float gc = (ratio >= a.lo && ratio <= a.hi) ? 1.f : 0.f;
+      const float L2 = negA * rc;
+      const float C1 = fmaxf(L1, L2);
+      const float w1 = L1 > L2 ? 1.f : (L1 == L2 ? 0.5f : 0.f);  // torch.maximum splits ties
+      const float dC1 = (w1 + (1.f - w1) * gc) * negA;
+      const float L3 = negA * a.clip_c;
+      const float C2 = fminf(L3, C1);
+      const float wc = C1 < L3 ? 1.f : (C1 == L3 ? 0.5f : 0.f);
+      const bool neg = A[j] < 0.f;
+      const float pg = neg ? C2 : C1;
+      const float dpg = (neg ? wc * dC1 : dC1) * ratio * gate;
+
+      const float mj = valid ? m[j] : 0.f;
+      const bool mb = mj != 0.f;
+      // agg weight of this token (d agg / d loss_mat) and its forward contribution
+      float w;
+      switch (a.mode) {
+        case DRL_AGG_TOKEN_MEAN: w = mb ? mj / denom_tm : 0.f; break;
+        case DRL_AGG_SEQ_MEAN_TOKEN_SUM: w = mj / static_cast<float>(a.B); break;
+        case DRL_AGG_SEQ_MEAN_TOKEN_MEAN: {
+          const int64_t row = (t + j) / a.R;
+          w = mj / (static_cast<float>(a.B) * a.rowcnt[valid ? row : 0]);
+          break;
+        }
+        default: w = mj / static_cast<float>(a.R); break;
+      }
+      // forward sums: token-mean uses where(mask, x, 0) * mask; the seq modes use x * mask
+      const bool tm = a.mode == DRL_AGG_TOKEN_MEAN;
+      auto agg_val = [&](float x) -> float {
+        if (tm) return mb ? x * mj : 0.f;
+        if (a.mode == DRL_AGG_SEQ_MEAN_TOKEN_MEAN) {
+          const int64_t row = (t + j) / a.R;
+          return (x * mj) / a.rowcnt[valid ? row : 0];
+        }
+        return x * mj;
+      };
+      if (valid) {
+        s_pg += agg_val(pg);
+        s_cnt += mj;
+        s_clip += mb ? (L2 > L1 ? mj : 0.f) : 0.f;
+        s_kl += mb ? -nkl * mj : 0.f;
+        s_cliplow += mb ? ((C1 > L3 && neg) ? mj : 0.f) : 0.f;
+      }
+      float gl = w * dpg;
+      if (has_kl) {
+        float kv, dk;
+        kl_term(a.kl, lp[j], rf[j], kv, dk);
+        if (valid) s_kld += agg_val(kv);
+        gl += a.kl_coef * (w * dk);
+      }
+      if (has_ent && valid) s_ent += agg_val(en[j]);
+      g_lp[j] = a.lsf * gl;
+      g_en[j] = a.ent_coef != 0.f ? a.lsf * (-a.ent_coef * w) : 0.f;
+    }
+    if (want_dlp) store4(a.dlp, t, t_end, vec, g_lp);
+    if (want_dent) store4(a.dent, t, t_end, vec, g_en);
+  }
+
+  // ---- workgroup partials -> last workgroup reduces in a fixed order
+  const float vals[kNumPartials] = {s_pg, s_clip, s_kl, s_cliplow, s_ent, s_kld, s_cnt, 0.f};
+#pragma unroll
+  for (int k = 0; k < kNumPartials; ++k) {
+    double v = wave_sum(static_cast<double>(vals[k]));
+    if (lane == 0) red[wave][k] = v;
+  }
+  __syncthreads();
+  if (tid < kNumPartials) {
+    double s = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
+    a.partials[blockIdx.x * kNumPartials + tid] = s;
+  }
+  if (last_block_ticket(&a.hdr->ticket)) {
+    if (tid < kNumPartials) {
+      double s = 0.0;
+      for (unsigned g = 0; g < gridDim.x; ++g) s += a.partials[g * kNumPartials + tid];
+      red[0][tid] = s;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      const double cnt = red[0][6];
+      const double dm = static_cast<double>(static_cast<float>(cnt) + 1e-8f);
+      auto agg = [&](double s) -> double {
+        switch (a.mode) {
+          case DRL_AGG_TOKEN_MEAN: return s / dm;
+          case DRL_AGG_SEQ_MEAN_TOKEN_SUM: return s / static_cast<double>(a.B);
+          case DRL_AGG_SEQ_MEAN_TOKEN_MEAN: return s / static_cast<double>(a.B);
+          default: return s / static_cast<double>(a.R);
+        }
+      };
+      const double pg_loss = agg(red[0][0]);
+      const double ent_loss = has_ent ? agg(red[0][4]) : 0.0;
+      const double kl_loss = has_kl ? agg(red[0][5]) : 0.0;
+      double total = pg_loss;
+      if (a.ent_coef != 0.f) total -= ent_loss * a.ent_coef;
+      if (has_kl) total += kl_loss * a.kl_coef;
+      a.out[DRL_PPO_OUT_PG_LOSS] = static_cast<float>(pg_loss);
+      a.out[DRL_PPO_OUT_PG_CLIPFRAC] = static_cast<float>(red[0][1] / dm);
+      a.out[DRL_PPO_OUT_PPO_KL] = static_cast<float>(red[0][2] / dm);
+      a.out[DRL_PPO_OUT_PG_CLIPFRAC_LOWER] = static_cast<float>(red[0][3] / dm);
+      a.out[DRL_PPO_OUT_ENTROPY_LOSS] = static_cast<float>(ent_loss);
+      a.out[DRL_PPO_OUT_KL_LOSS] = static_cast<float>(kl_loss);
+      a.out[DRL_PPO_OUT_LOSS] = static_cast<float>(total * a.lsf);
+      a.out[DRL_PPO_OUT_MASK_COUNT] = static_cast<float>(cnt);
+    }
+  }
+}
+
+// sum(mask) per row, one wave per row (seq-mean-token-mean pre-pass)
+template <int MDT>
+__global__ __launch_bounds__(256) void row_count_kernel(const void* mask, int64_t B, int64_t R, float* rowcnt) {
+  const int64_t row = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= B) return;
+  float c = 0.f;
+  for (int64_t t = lane; t < R; t += 64) c += mask_at<MDT>(mask, row * R + t);
+  c = wave_sum(c);
+  if (lane == 0) rowcnt[row] = c;
+}
+
+template <int MDT>
+int launch(const Args& base, bool two_phase, int grid, hipStream_t s) {
+  if (base.mode == DRL_AGG_SEQ_MEAN_TOKEN_MEAN) {
+    hipLaunchKernelGGL(row_count_kernel<MDT>, dim3((base.B + 3) / 4), dim3(256), 0, s, base.mask, base.B, base.R,
+                       const_cast<float*>(base.rowcnt));
+    DRL_LAUNCH_CHECK();
+  }
+  if (two_phase)
+    hipLaunchKernelGGL((ppo_loss_kernel<MDT, true>), dim3(grid), dim3(kThreads), 0, s, base);
+  else
+    hipLaunchKernelGGL((ppo_loss_kernel<MDT, false>), dim3(grid), dim3(kThreads), 0, s, base);
+  DRL_LAUNCH_CHECK();
+  return DRL_OK;
+}
+
+int max_grid() { return cu_count() * 2; }
+
+size_t ws_layout(int64_t B, size_t* off_partials, size_t* off_rowcnt) {
+  const size_t grid = static_cast<size_t>(max_grid());
+  *off_partials = round_up(sizeof(Header), 256);
+  *off_rowcnt = round_up(*off_partials + grid * kNumPartials * sizeof(double), 256);
+  return round_up(*off_rowcnt + static_cast<size_t>(B) * sizeof(float), 256);
+}
+
+
+__global__ __launch_bounds__(256) void kl_penalty_kernel(const float* lp, const float* ref, int64_t n, int kl, float* out) {
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    float v, d;
+    kl_term(kl, lp[i], ref[i], v, d);
+    out[i] = v;
+  }
+}
+
+// agg_loss forward: weighted partial sums per workgroup, last workgroup finishes (fixed order).
+template <int MDT>
+__global__ __launch_bounds__(256) void agg_loss_kernel(const float* x, const void* mask, int64_t B, int64_t R,
+                                                       int mode, const float* rowcnt, double* partials, Header* hdr,
+                                                       float* out) {
+  const int64_t N = B * R;
+  double s = 0.0, c = 0.0;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < N;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const float m = mask_at<MDT>(mask, i);
+    float v;
+    if (mode == DRL_AGG_TOKEN_MEAN) v = m != 0.f ? x[i] * m : 0.f;
+    else if (mode == DRL_AGG_SEQ_MEAN_TOKEN_MEAN) v = (x[i] * m) / rowcnt[i / R];
+    else v = x[i] * m;
+    s += v;
+    c += m;
+  }
+  s = wave_sum(s);
+  c = wave_sum(c);
+  __shared__ double red[4][2];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) { red[wave][0] = s; red[wave][1] = c; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    partials[2 * blockIdx.x] = red[0][0] + red[1][0] + red[2][0] + red[3][0];
+    partials[2 * blockIdx.x + 1] = red[0][1] + red[1][1] + red[2][1] + red[3][1];
+  }
+  if (last_block_ticket(&hdr->ticket) && threadIdx.x == 0) {
+    double S = 0.0, C = 0.0;
+    for (unsigned b = 0; b < gridDim.x; ++b) { S += partials[2 * b]; C += partials[2 * b + 1]; }
+    double r;
+    if (mode == DRL_AGG_TOKEN_MEAN) r = S / static_cast<double>(static_cast<float>(C) + 1e-8f);
+    else if (mode == DRL_AGG_SEQ_MEAN_TOKEN_SUM || mode == DRL_AGG_SEQ_MEAN_TOKEN_MEAN) r = S / static_cast<double>(B);
+    else r = S / static_cast<double>(R);
+    *out = static_cast<float>(r);
+  }
+}
+
+template <int MDT>
+int launch_agg(const float* x, const void* mask, int64_t B, int64_t R, int mode, char* ws, size_t off_part,
+               size_t off_row, float* out, hipStream_t s) {
+  float* rowcnt = reinterpret_cast<float*>(ws + off_row);
+  if (mode == DRL_AGG_SEQ_MEAN_TOKEN_MEAN) {
+    hipLaunchKernelGGL(row_count_kernel<MDT>, dim3((B + 3) / 4), dim3(256), 0, s, mask, B, R, rowcnt);
+    DRL_LAUNCH_CHECK();
+  }
+  const int grid = static_cast<int>(std::min<int64_t>(max_grid(), (B * R + 255) / 256));
+  hipLaunchKernelGGL(agg_loss_kernel<MDT>, dim3(grid), dim3(256), 0, s, x, mask, B, R, mode, rowcnt,
+                     reinterpret_cast<double*>(ws + off_part), reinterpret_cast<Header*>(ws), out);
+  DRL_LAUNCH_CHECK();
+  return DRL_OK;
+}
+
+}  // namespace
+}  // namespace drl
+
+extern "C" {
+
+size_t drl_ppo_loss_workspace_bytes(int64_t B, int64_t R) {
+  (void)R;
+  size_t a, b;
+  return drl::ws_layout(B, &a, &b);
+}
+
+int drl_ppo_loss_fwd_bwd(const float* old_log_prob, const float* log_prob, const float* advantages,
+                         const void* response_mask, int32_t mask_dtype, const float* entropy,
+                         const float* ref_log_prob, int64_t B, int64_t R, const drl_ppo_loss_params* p,
+                         float* out_scalars, float* dlog_prob, float* dentropy, void* workspace,
+                         size_t workspace_bytes, void* stream) {
+  using namespace drl;
+  DRL_CHECK_ARG(p != nullptr, "params is NULL");
+  DRL_CHECK_ARG(B >= 1 && R >= 1, "bad shape B=%lld R=%lld", (long long)B, (long long)R);
+  DRL_CHECK_ARG(old_log_prob && log_prob && advantages && response_mask && out_scalars, "NULL input");
+  DRL_CHECK_ARG(p->loss_agg_mode >= 0 && p->loss_agg_mode <= 3, "bad loss_agg_mode %d", p->loss_agg_mode);
+  DRL_CHECK_ARG(p->kl_type >= DRL_KL_NONE && p->kl_type <= DRL_KL_K3, "bad kl_type %d", p->kl_type);
+  DRL_CHECK_ARG(p->kl_type == DRL_KL_NONE || ref_log_prob != nullptr, "kl_type set but ref_log_prob is NULL");
+  DRL_CHECK_ARG(p->entropy_coeff == 0.f || entropy != nullptr, "entropy_coeff != 0 but entropy is NULL");
+  DRL_CHECK_ARG(p->clip_ratio_c > 1.f, "clip_ratio_c must be > 1.0 (dual-clip PPO), got %f", p->clip_ratio_c);
+  DRL_CHECK_ARG(mask_dtype == DRL_I64 || mask_dtype == DRL_I32 || mask_dtype == DRL_U8 || mask_dtype == DRL_F32,
+                "unsupported mask dtype %d", mask_dtype);
+  const void* ptrs[] = {old_log_prob, log_prob, advantages, response_mask, entropy, ref_log_prob, dlog_prob, dentropy};
+  for (const void* q : ptrs) DRL_CHECK_ARG(q == nullptr || aligned16(q), "tensor base not 16-byte aligned");
+  size_t off_part, off_row;
+  const size_t need = ws_layout(B, &off_part, &off_row);
+  if (workspace == nullptr || workspace_bytes < need)
+    return fail(DRL_ERR_WORKSPACE, "workspace %zu < %zu bytes", workspace_bytes, need);
+
+  const int64_t N = B * R;
+  const int grid = static_cast<int>(std::min<int64_t>(max_grid(), (N + kTokPerIter - 1) / kTokPerIter));
+  auto* ws = static_cast<char*>(workspace);
+  Args a{};
+  a.old_lp = old_log_prob; a.lp = log_prob; a.adv = advantages; a.mask = response_mask;
+  a.ent = entropy; a.ref = p->kl_type == DRL_KL_NONE ? nullptr : ref_log_prob;
+  a.rowcnt = reinterpret_cast<const float*>(ws + off_row);
+  a.dlp = dlog_prob; a.dent = dentropy; a.out = out_scalars;
+  a.hdr = reinterpret_cast<Header*>(ws);
+  a.partials = reinterpret_cast<double*>(ws + off_part);
+  a.N = N; a.B = B; a.R = R;
+  // python computes 1 - cliprange_low in double; torch.clamp then casts the bound to float32
+  a.lo = static_cast<float>(1.0 - static_cast<double>(p->clip_ratio_low));
+  a.hi = static_cast<float>(1.0 + static_cast<double>(p->clip_ratio_high));
+  a.clip_c = p->clip_ratio_c; a.ent_coef = p->entropy_coeff; a.kl_coef = p->kl_loss_coef;
+  a.lsf = p->loss_scale_factor; a.mode = p->loss_agg_mode; a.kl = p->kl_type;
+  const bool two_phase = (p->loss_agg_mode == DRL_AGG_TOKEN_MEAN) && (dlog_prob != nullptr || dentropy != nullptr);
+
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  DRL_HIP(hipMemsetAsync(ws, 0, sizeof(Header), s));
+  switch (mask_dtype) {
+    case DRL_I64: return launch<DRL_I64>(a, two_phase, grid, s);
+    case DRL_I32: return launch<DRL_I32>(a, two_phase, grid, s);
+    case DRL_U8: return launch<DRL_U8>(a, two_phase, grid, s);
+    default: return launch<DRL_F32>(a, two_phase, grid, s);
+  }
+}
+
+
+int drl_kl_penalty(const float* log_prob, const float* ref_log_prob, int64_t n, int32_t kl_type, float* out,
+                   void* stream) {
+  using namespace drl;
+  DRL_CHECK_ARG(log_prob && ref_log_prob && out, "NULL input");
+  DRL_CHECK_ARG(kl_type >= DRL_KL_K1 && kl_type <= DRL_KL_K3, "bad kl_type %d", kl_type);
+  if (n <= 0) return DRL_OK;
+  const int grid = static_cast<int>(std::min<int64_t>(static_cast<int64_t>(cu_count()) * 8, (n + 255) / 256));
+  hipLaunchKernelGGL(kl_penalty_kernel, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream), log_prob,
+                     ref_log_prob, n, kl_type, out);
+  DRL_LAUNCH_CHECK();
+  return DRL_OK;
+}
+
+size_t drl_agg_loss_workspace_bytes(int64_t B, int64_t R) { return drl_ppo_loss_workspace_bytes(B, R); }
+
+int drl_agg_loss(const float* loss_mat, const void* loss_mask, int32_t mdt, int64_t B, int64_t R, int32_t mode,
+                 float* out, void* workspace, size_t workspace_bytes, void* stream) {
+  using namespace drl;
+  DRL_CHECK_ARG(loss_mat && loss_mask && out, "NULL input");
+  DRL_CHECK_ARG(B >= 1 && R >= 1, "bad shape");
+  DRL_CHECK_ARG(mode >= 0 && mode <= 3, "bad loss_agg_mode %d", mode);
+  size_t off_part, off_row;
+  const size_t need = ws_layout(B, &off_part, &off_row);
+  if (workspace == nullptr || workspace_bytes < need) return fail(DRL_ERR_WORKSPACE, "workspace too small");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  char* ws = static_cast<char*>(workspace);
+  DRL_HIP(hipMemsetAsync(ws, 0, sizeof(Header), s));
+  switch (mdt) {
+    case DRL_I64: return launch_agg<DRL_I64>(loss_mat, loss_mask, B, R, mode, ws, off_part, off_row, out, s);
+    case DRL_I32: return launch_agg<DRL_I32>(loss_mat, loss_mask, B, R, mode, ws, off_part, off_row, out, s);
+    case DRL_U8: return launch_agg<DRL_U8>(loss_mat, loss_mask, B, R, mode, ws, off_part, off_row, out, s);
+    case DRL_F32: return launch_agg<DRL_F32>(loss_mat, loss_mask, B, R, mode, ws, off_part, off_row, out, s);
+    default: return fail(DRL_ERR_INVALID, "bad mask dtype %d", mdt);
+  }
+}
+
+}  // extern "C"

@@ -1,0 +1,459 @@
+// K2 — log-prob of the label + entropy over the vocabulary (forward and backward), and
+// K4 — decode-step token selection (greedy / temperature sampling) over the vocabulary.
+//
+// Both stream one (N, V) logits row per workgroup (V = 151,936 for Qwen2.5: 297 KiB bf16 per row),
+// 8 bf16 / 4 f32 per lane per 16-B load, and keep all softmax state in registers with an online
+// (running max) formulation, so the logits are read exactly once in the forward and once in the
+// backward (which writes d logits in the same pass). HBM-bound: ~2V bytes per row forward.
+// References: verl/utils/torch_functional.py:64-160 (logprobs / entropy), experimental/torch_functional.py
+// :40-72 (backward formula), workers/rollout/hf_rollout.py:112-124 (HF generate greedy / sampling).
+#include "common.h"
+
+namespace drl {
+namespace {
+
+constexpr int kThreads = 256;
+
+template <int DT>
+struct Elem;
+template <>
+struct Elem<DRL_BF16> {
+  static constexpr int kVec = 8;
+  using T = uint16_t;
+  __device__ static float get(const void* p, int64_t i) { return bf16_to_f32(static_cast<const uint16_t*>(p)[i]); }
+  __device__ static void load_vec(const void* p, int64_t i, float v[8]) {
+    const uint4 q = *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(p) + i);
+    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      v[2 * k] = __uint_as_float(w[k] << 16);
+      v[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
+    }
+  }
+};
+template <>
+struct Elem<DRL_F32> {
+  static constexpr int kVec = 4;
+  using T = float;
+  __device__ static float get(const void* p, int64_t i) { return static_cast<const float*>(p)[i]; }
+  __device__ static void load_vec(const void* p, int64_t i, float v[4]) {
+    const float4 q = *reinterpret_cast<const float4*>(static_cast<const float*>(p) + i);
+    v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+  }
+};
+
+// logits / temperature. The logprob path mirrors `logits.div_(temperature)` (dp_actor.py:195,263), which
+// runs in the logits' dtype, so a bf16 row is rounded back to bf16 after the division; the sampler
+// mirrors HF's TemperatureLogitsWarper on fp32 scores (no rounding). Division, not a reciprocal
+// multiply, to keep the reference's rounding.
+template <int DT>
+__device__ __forceinline__ float scale_logit(float x, float temp, bool apply, bool round_bf16 = true) {
+  if (!apply) return x;
+  const float z = x / temp;
+  if constexpr (DT == DRL_BF16) return round_bf16 ? bf16_to_f32(f32_to_bf16(z)) : z;
+  else return z;
+}
+
+// merge two online-softmax states (max m, sum_e s = sum exp(z-m), sum_ez t = sum exp(z-m)*z)
+__device__ __forceinline__ void merge_state(float& m, float& s, float& t, float m2, float s2, float t2) {
+  const float mn = fmaxf(m, m2);
+  const float a = (m == -INFINITY) ? 0.f : expf(m - mn);
+  const float b = (m2 == -INFINITY) ? 0.f : expf(m2 - mn);
+  s = s * a + s2 * b;
+  t = t * a + t2 * b;
+  m = mn;
+}
+
+template <int DT, bool WANT_T, bool ROUND = true>
+__device__ __forceinline__ void row_softmax_state(const void* row, int64_t V, bool vec, float inv_t, bool apply_t,
+                                                  float& m, float& s, float& t) {
+  constexpr int kV = Elem<DT>::kVec;
+  m = -INFINITY; s = 0.f; t = 0.f;
+  const int tid = threadIdx.x;
+  if (vec) {
+    const int64_t nfull = V / kV;
+    for (int64_t c = tid; c < nfull; c += kThreads) {
+      float v[kV];
+      Elem<DT>::load_vec(row, c * kV, v);
+      float mx = -INFINITY;
+#pragma unroll
+      for (int k = 0; k < kV; ++k) {
+        v[k] = scale_logit<DT>(v[k], inv_t, apply_t, ROUND);
+        mx = fmaxf(mx, v[k]);
+      }
+      if (mx > m) {
+        const float sc = (m == -INFINITY) ? 0.f : expf(m - mx);
+        s *= sc;
+        if (WANT_T) t *= sc;
+        m = mx;
+      }
+#pragma unroll
+      for (int k = 0; k < kV; ++k) {
+        const float e = expf(v[k] - m);
+        s += e;
+        if (WANT_T) t = fmaf(e, v[k], t);
+      }
+    }
+    for (int64_t i = nfull * kV + tid; i < V; i += kThreads) {
+      const float z = scale_logit<DT>(Elem<DT>::get(row, i), inv_t, apply_t, ROUND);
+      if (z > m) {
+        const float sc = (m == -INFINITY) ? 0.f : expf(m - z);
+        s *= sc;
+        if (WANT_T) t *= sc;
+        m = z;
+      }
+      const float e = expf(z - m);
+      s += e;
+      if (WANT_T) t = fmaf(e, z, t);
+    }
+  } else {
+    for (int64_t i = tid; i < V; i += kThreads) {
+      const float z = scale_logit<DT>(Elem<DT>::get(row, i), inv_t, apply_t, ROUND);
+      if (z > m) {
+        const float sc = (m == -INFINITY) ? 0.f : expf(m - z);
+        s *= sc;
+        if (WANT_T) t *= sc;
+        m = z;
+      }
+      const float e = expf(z - m);
+      s += e;
+      if (WANT_T) t = fmaf(e, z, t);
+    }
+  }
+  // wave then block merge
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float m2 = __shfl_xor(m, o, kWave), s2 = __shfl_xor(s, o, kWave), t2 = WANT_T ? __shfl_xor(t, o, kWave) : 0.f;
+    merge_state(m, s, t, m2, s2, t2);
+  }
+  __shared__ float sm[kThreads / kWave][3];
+  const int lane = tid & 63, wave = tid >> 6;
+  if (lane == 0) { sm[wave][0] = m; sm[wave][1] = s; sm[wave][2] = t; }
+  __syncthreads();
+  m = sm[0][0]; s = sm[0][1]; t = sm[0][2];
+#pragma unroll
+  for (int w = 1; w < kThreads / kWave; ++w) merge_state(m, s, t, sm[w][0], sm[w][1], sm[w][2]);
+  __syncthreads();
+}
+
+template <int DT>
+__global__ __launch_bounds__(kThreads) void logprob_fwd_kernel(const void* logits, int64_t V, int64_t ld,
+                                                               const int64_t* labels, float inv_t, int apply_t,
+                                                               bool vec, float* logp, float* ent, float* lse_out) {
+  const int64_t r = blockIdx.x;
+  const void* row = static_cast<const typename Elem<DT>::T*>(logits) + r * ld;
+  float m, s, t;
+  if (ent) row_softmax_state<DT, true>(row, V, vec, inv_t, apply_t, m, s, t);
+  else row_softmax_state<DT, false>(row, V, vec, inv_t, apply_t, m, s, t);
+  if (threadIdx.x == 0) {
+    const float lse = m + logf(s);
+    const int64_t y = labels[r];
+    const float zy = scale_logit<DT>(Elem<DT>::get(row, y), inv_t, apply_t);
+    logp[r] = zy - lse;
+    if (ent) ent[r] = lse - t / s;
+    if (lse_out) lse_out[r] = lse;
+  }
+}
+
+template <int DT, int ODT>
+__global__ __launch_bounds__(kThreads) void logprob_bwd_kernel(const void* logits, int64_t V, int64_t ld,
+                                                               const int64_t* labels, float inv_t, int apply_t,
+                                                               bool vec, const float* dlogp, const float* dent,
+                                                               const float* lse, const float* ent, void* dlogits,
+                                                               int64_t ld_out) {
+  constexpr int kV = Elem<DT>::kVec;
+  const int64_t r = blockIdx.x;
+  const void* row = static_cast<const typename Elem<DT>::T*>(logits) + r * ld;
+  const float gl = dlogp ? dlogp[r] : 0.f;
+  const float ge = dent ? dent[r] : 0.f;
+  const float L = lse[r];
+  const float H = ent ? ent[r] : 0.f;
+  const int64_t y = labels[r];
+  // d/dz of (gl*logp + ge*H) = gl*(onehot - p) - ge*p*(log p + H); d/dx = that / T
+  auto grad = [&](float x, int64_t i) -> float {
+    const float z = scale_logit<DT>(x, inv_t, apply_t);
+    const float lp = z - L;
+    const float p = expf(lp);
+    float g = -gl * p - ge * p * (lp + H);
+    if (i == y) g += gl;
+    return apply_t ? g / inv_t : g;
+  };
+  auto store = [&](int64_t i, float g) {
+    if constexpr (ODT == DRL_BF16) static_cast<uint16_t*>(dlogits)[r * ld_out + i] = f32_to_bf16(g);
+    else static_cast<float*>(dlogits)[r * ld_out + i] = g;
+  };
+  const int tid = threadIdx.x;
+  if (vec) {
+    const int64_t nfull = V / kV;
+    for (int64_t c = tid; c < nfull; c += kThreads) {
+      float v[kV];
+      Elem<DT>::load_vec(row, c * kV, v);
+      float g[kV];
+#pragma unroll
+      for (int k = 0; k < kV; ++k) g[k] = grad(v[k], c * kV + k);
+      if constexpr (ODT == DRL_BF16) {
+        uint32_t w[kV / 2];
+#pragma unroll
+        for (int k = 0; k < kV / 2; ++k)
+          w[k] = static_cast<uint32_t>(f32_to_bf16(g[2 * k])) | (static_cast<uint32_t>(f32_to_bf16(g[2 * k + 1])) << 16);
+        if constexpr (kV == 8)
+          *reinterpret_cast<uint4*>(static_cast<uint16_t*>(dlogits) + r * ld_out + c * kV) = make_uint4(w[0], w[1], w[2], w[3]);
+        else
+          *reinterpret_cast<uint2*>(static_cast<uint16_t*>(dlogits) + r * ld_out + c * kV) = make_uint2(w[0], w[1]);
+      } else {
+#pragma unroll
+        for (int k = 0; k < kV; k += 4)
+          *reinterpret_cast<float4*>(static_cast<float*>(dlogits) + r * ld_out + c * kV + k) =
+              make_float4(g[k], g[k + 1], g[k + 2], g[k + 3]);
+      }
+    }
+    for (int64_t i = nfull * kV + tid; i < V; i += kThreads) store(i, grad(Elem<DT>::get(row, i), i));
+  } else {
+    for (int64_t i = tid; i < V; i += kThreads) store(i, grad(Elem<DT>::get(row, i), i));
+  }
+}
+
+// ------------------------------------------------------------------------------------------------ K4
+__device__ __forceinline__ bool argmax_better(float v, int64_t i, float bv, int64_t bi) {
+  // torch.argmax: NaN is the maximum; ties -> first index
+  const bool vn = isnan(v), bn = isnan(bv);
+  if (vn != bn) return vn;
+  if (vn) return i < bi;
+  return v > bv || (v == bv && i < bi);
+}
+
+__device__ __forceinline__ uint32_t philox_u32(uint64_t seed, uint64_t offset, uint64_t counter) {
+  uint32_t c0 = static_cast<uint32_t>(counter), c1 = static_cast<uint32_t>(counter >> 32);
+  uint32_t c2 = static_cast<uint32_t>(offset), c3 = static_cast<uint32_t>(offset >> 32);
+  uint32_t k0 = static_cast<uint32_t>(seed), k1 = static_cast<uint32_t>(seed >> 32);
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const uint64_t p0 = static_cast<uint64_t>(0xD2511F53u) * c0;
+    const uint64_t p1 = static_cast<uint64_t>(0xCD9E8D57u) * c2;
+    const uint32_t n0 = static_cast<uint32_t>(p1 >> 32) ^ c1 ^ k0;
+    const uint32_t n1 = static_cast<uint32_t>(p1);
+    const uint32_t n2 = static_cast<uint32_t>(p0 >> 32) ^ c3 ^ k1;
+    const uint32_t n3 = static_cast<uint32_t>(p0);
+    c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c0;
+}
+
+struct SelectArgs {
+  const void* logits;
+  int64_t V, ld, ld_out;
+  bool vec;
+  int do_sample;
+  float temp;
+  uint64_t seed, offset;
+  int64_t row_base, pad;
+  const int64_t* eos;
+  int n_eos;
+  int32_t* unfinished;
+  int64_t* out;
+};
+
+template <int DT>
+__global__ __launch_bounds__(kThreads) void select_kernel(SelectArgs a) {
+  const int64_t r = blockIdx.x;
+  const void* row = static_cast<const typename Elem<DT>::T*>(a.logits) + r * a.ld;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  __shared__ float s_val[kThreads / kWave];
+  __shared__ int64_t s_idx[kThreads / kWave];
+  __shared__ double s_scan[kThreads / kWave];
+  __shared__ int64_t s_choice;
+  int64_t choice = 0;
+  if (!a.do_sample) {
+    float bv = -INFINITY;
+    int64_t bi = INT64_MAX;
+    for (int64_t i = tid; i < a.V; i += kThreads) {
+      const float v = Elem<DT>::get(row, i);
+      if (argmax_better(v, i, bv, bi)) { bv = v; bi = i; }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float v2 = __shfl_xor(bv, o, kWave);
+      const int64_t i2 = __shfl_xor(bi, o, kWave);
+      if (argmax_better(v2, i2, bv, bi)) { bv = v2; bi = i2; }
+    }
+    if (lane == 0) { s_val[wave] = bv; s_idx[wave] = bi; }
+    __syncthreads();
+    if (tid == 0) {
+      for (int w = 1; w < kThreads / kWave; ++w)
+        if (argmax_better(s_val[w], s_idx[w], bv, bi)) { bv = s_val[w]; bi = s_idx[w]; }
+      s_choice = bi;
+    }
+    __syncthreads();
+    choice = s_choice;
+  } else {
+    // pass 1: max of z = logit / T (HF TemperatureLogitsWarper on fp32 scores)
+    float m, sdummy, tdummy;
+    row_softmax_state<DT, false, false>(row, a.V, a.vec, a.temp, true, m, sdummy, tdummy);
+    const uint32_t bits = philox_u32(a.seed, a.offset, static_cast<uint64_t>(a.row_base + r));
+    const double u = (static_cast<double>(bits >> 8) + 0.5) * (1.0 / 16777216.0);
+    // pass 2/3: inverse CDF. Chunks of kThreads*8 elements, 8 contiguous per lane; every sum is taken
+    // in the same fixed order in both passes, so the scan ends exactly at the total.
+    constexpr int kE = 8;
+    const int64_t chunk = static_cast<int64_t>(kThreads) * kE;
+    auto lane_sum = [&](int64_t base, double e[kE]) -> double {
+      double acc = 0.0;
+#pragma unroll
+      for (int k = 0; k < kE; ++k) {
+        const int64_t i = base + tid * kE + k;
+        e[k] = i < a.V ? static_cast<double>(expf(scale_logit<DT>(Elem<DT>::get(row, i), a.temp, true, false) - m)) : 0.0;
+        acc += e[k];
+      }
+      return acc;
+    };
+    auto block_sum = [&](double v) -> double {
+      v = wave_sum(v);
+      if (lane == 0) s_scan[wave] = v;
+      __syncthreads();
+      const double tot = s_scan[0] + s_scan[1] + s_scan[2] + s_scan[3];
+      __syncthreads();
+      return tot;
+    };
+    double total = 0.0;
+    for (int64_t base = 0; base < a.V; base += chunk) {
+      double e[kE];
+      total += block_sum(lane_sum(base, e));
+    }
+    const double target = u * total;
+    if (tid == 0) s_choice = -1;
+    __syncthreads();
+    double running = 0.0;
+    for (int64_t base = 0; base < a.V; base += chunk) {
+      double e[kE];
+      const double mine = lane_sum(base, e);
+      const double ct = block_sum(mine);
+      if (running + ct > target || base + chunk >= a.V) {
+        // exclusive scan of the lane sums (wave inclusive scan + wave offsets)
+        double inc = mine;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const double x = __shfl_up(inc, o, kWave);
+          if (lane >= o) inc += x;
+        }
+        if (lane == 63) s_scan[wave] = inc;
+        __syncthreads();
+        double woff = 0.0;
+        for (int w = 0; w < wave; ++w) woff += s_scan[w];
+        double c = running + woff + inc - mine;
+#pragma unroll
+        for (int k = 0; k < kE; ++k) {
+          const int64_t i = base + tid * kE + k;
+          const double nc = c + e[k];
+          if (i < a.V && e[k] > 0.0 && c <= target && nc > target) s_choice = i;  // unique crossing
+          c = nc;
+        }
+        __syncthreads();
+        break;
+      }
+      running += ct;
+    }
+    __syncthreads();
+    choice = s_choice;
+    if (choice < 0) {  // target beyond the last crossing through rounding: last non-zero-mass token
+      choice = a.V - 1;
+    }
+  }
+  if (tid == 0) {
+    const bool alive = a.unfinished ? a.unfinished[r] != 0 : true;
+    const int64_t tok = alive ? choice : a.pad;
+    a.out[r * a.ld_out] = tok;
+    if (a.unfinished && alive) {
+      for (int k = 0; k < a.n_eos; ++k)
+        if (tok == a.eos[k]) { a.unfinished[r] = 0; break; }
+    }
+  }
+}
+
+bool rows_aligned(const void* p, int64_t ld, int dt) {
+  const int64_t esz = dt == DRL_BF16 ? 2 : 4;
+  return aligned16(p) && ((ld * esz) % 16 == 0);
+}
+
+}  // namespace
+}  // namespace drl
+
+extern "C" {
+
+int drl_logprob_entropy_fwd(const void* logits, int32_t dt, int64_t N, int64_t V, int64_t ld, const int64_t* labels,
+                            float temperature, float* log_prob, float* entropy, float* lse_out, void* stream) {
+  using namespace drl;
+  DRL_CHECK_ARG(logits && labels && log_prob, "NULL input");
+  DRL_CHECK_ARG(N >= 0 && V >= 1 && ld >= V, "bad shape N=%lld V=%lld ld=%lld", (long long)N, (long long)V, (long long)ld);
+  DRL_CHECK_ARG(dt == DRL_BF16 || dt == DRL_F32, "logits dtype must be F32 or BF16");
+  DRL_CHECK_ARG(temperature > 0.f, "temperature must be > 0");
+  DRL_CHECK_ARG(N <= 0x7fffffff, "too many rows");
+  if (N == 0) return DRL_OK;
+  const bool vec = rows_aligned(logits, ld, dt);
+  const float inv_t = temperature;  // kernels divide by it
+  const int apply_t = temperature != 1.0f;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (dt == DRL_BF16)
+    hipLaunchKernelGGL(logprob_fwd_kernel<DRL_BF16>, dim3(N), dim3(kThreads), 0, s, logits, V, ld, labels, inv_t,
+                       apply_t, vec, log_prob, entropy, lse_out);
+  else
+    hipLaunchKernelGGL(logprob_fwd_kernel<DRL_F32>, dim3(N), dim3(kThreads), 0, s, logits, V, ld, labels, inv_t,
+                       apply_t, vec, log_prob, entropy, lse_out);
+  DRL_LAUNCH_CHECK();
+  return DRL_OK;
+}
+
+int drl_logprob_entropy_bwd(const void* logits, int32_t dt, int64_t N, int64_t V, int64_t ld, const int64_t* labels,
+                            float temperature, const float* dlog_prob, const float* dentropy, const float* lse,
+                            const float* entropy, void* dlogits, int32_t odt, int64_t ld_out, void* stream) {
+  using namespace drl;
+  DRL_CHECK_ARG(logits && labels && lse && dlogits, "NULL input");
+  DRL_CHECK_ARG(dentropy == nullptr || entropy != nullptr, "dentropy needs the forward entropy");
+  DRL_CHECK_ARG(N >= 0 && V >= 1 && ld >= V && ld_out >= V, "bad shape");
+  DRL_CHECK_ARG(dt == DRL_BF16 || dt == DRL_F32, "logits dtype must be F32 or BF16");
+  DRL_CHECK_ARG(odt == DRL_BF16 || odt == DRL_F32, "dlogits dtype must be F32 or BF16");
+  DRL_CHECK_ARG(temperature > 0.f, "temperature must be > 0");
+  DRL_CHECK_ARG(dlogits != logits || (dt == odt && ld == ld_out), "in-place backward needs identical layout");
+  if (N == 0) return DRL_OK;
+  const bool vec = rows_aligned(logits, ld, dt) && rows_aligned(dlogits, ld_out, odt) &&
+                   (dt == DRL_BF16 ? 8 : 4) % (odt == DRL_BF16 ? 4 : 4) == 0;
+  const float inv_t = temperature;  // kernels divide by it
+  const int apply_t = temperature != 1.0f;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+#define DRL_BWD(DT, ODT)                                                                                      \
+  hipLaunchKernelGGL((logprob_bwd_kernel<DT, ODT>), dim3(N), dim3(kThreads), 0, s, logits, V, ld, labels, inv_t, \
+                     apply_t, vec, dlog_prob, dentropy, lse, entropy, dlogits, ld_out)
+  if (dt == DRL_BF16 && odt == DRL_BF16) DRL_BWD(DRL_BF16, DRL_BF16);
+  else if (dt == DRL_BF16) DRL_BWD(DRL_BF16, DRL_F32);
+  else if (odt == DRL_BF16) DRL_BWD(DRL_F32, DRL_BF16);
+  else DRL_BWD(DRL_F32, DRL_F32);
+#undef DRL_BWD
+  DRL_LAUNCH_CHECK();
+  return DRL_OK;
+}
+
+int drl_select_tokens(const void* logits, int32_t dt, int64_t N, int64_t V, int64_t ld,
+                      const drl_sampling_params* p, int32_t* unfinished, int64_t* out_tokens, int64_t ld_out,
+                      void* stream) {
+  using namespace drl;
+  DRL_CHECK_ARG(logits && p && out_tokens, "NULL input");
+  DRL_CHECK_ARG(N >= 0 && V >= 1 && ld >= V, "bad shape");
+  DRL_CHECK_ARG(dt == DRL_BF16 || dt == DRL_F32, "logits dtype must be F32 or BF16");
+  DRL_CHECK_ARG(p->n_eos == 0 || p->eos_ids != nullptr, "n_eos > 0 but eos_ids is NULL");
+  const bool sample = p->do_sample && p->temperature > 0.f;
+  if (sample && ((p->top_k > 0 && p->top_k < V) || p->top_p < 1.0f))
+    return fail(DRL_ERR_UNSUPPORTED, "top-k / top-p filtering is not implemented in this build");
+  if (N == 0) return DRL_OK;
+  SelectArgs a{};
+  a.logits = logits; a.V = V; a.ld = ld; a.ld_out = ld_out; a.vec = rows_aligned(logits, ld, dt);
+  a.do_sample = sample; a.temp = sample ? p->temperature : 1.0f;
+  a.seed = p->seed; a.offset = p->offset; a.row_base = p->row_base; a.pad = p->pad_token_id;
+  a.eos = p->eos_ids; a.n_eos = p->n_eos; a.unfinished = unfinished; a.out = out_tokens;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (dt == DRL_BF16) hipLaunchKernelGGL(select_kernel<DRL_BF16>, dim3(N), dim3(kThreads), 0, s, a);
+  else hipLaunchKernelGGL(select_kernel<DRL_F32>, dim3(N), dim3(kThreads), 0, s, a);
+  DRL_LAUNCH_CHECK();
+  return DRL_OK;
+}
+
+}  // extern "C"

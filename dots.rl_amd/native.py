@@ -1,0 +1,258 @@
+"""Torch-facing wrappers over the C-ABI (device pointers + the current HIP stream, nothing else).
+
+PyTorch-ROCm provides storage, streams and the allocator; every arithmetic step of the hot path runs
+in the gfx950 kernels of ``libdotsrl_amd.so``. Tensors must live on the GPU; anything else raises.
+"""
+
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import check
+
+_MASK_DTYPES = {torch.int64: _lib.DRL_I64, torch.int32: _lib.DRL_I32, torch.uint8: _lib.DRL_U8,
+                torch.bool: _lib.DRL_U8, torch.float32: _lib.DRL_F32}
+_LOGIT_DTYPES = {torch.float32: _lib.DRL_F32, torch.bfloat16: _lib.DRL_BF16}
+
+
+def lib():
+    return _lib.load()
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _p(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _dev(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise ValueError("dots.rl_amd kernels take GPU tensors (there is no CPU path)")
+
+
+def _c(t):
+    return None if t is None else t.contiguous()
+
+
+class _Workspace:
+    """Per-device scratch buffer, grown on demand; stream-ordered reuse on the current stream."""
+
+    def __init__(self):
+        self.buf = {}
+
+    def get(self, nbytes: int, device) -> torch.Tensor:
+        key = (device.index if device.index is not None else torch.cuda.current_device())
+        b = self.buf.get(key)
+        if b is None or b.numel() < nbytes:
+            b = torch.empty(max(nbytes, 1 << 16), dtype=torch.uint8, device=device)
+            self.buf[key] = b
+        return b
+
+
+_ws = _Workspace()
+
+
+def mask_dtype_code(mask: torch.Tensor) -> int:
+    try:
+        return _MASK_DTYPES[mask.dtype]
+    except KeyError as e:
+        raise ValueError(f"unsupported mask dtype {mask.dtype}") from e
+
+
+# ----------------------------------------------------------------------------------------------- K1
+def ppo_loss_fwd_bwd(old_log_prob, log_prob, advantages, response_mask, entropy=None, ref_log_prob=None, *,
+                     clip_ratio_low=0.2, clip_ratio_high=0.2, clip_ratio_c=3.0, entropy_coeff=0.0,
+                     kl_loss_coef=0.0, kl_loss_type=None, loss_agg_mode="token-mean", loss_scale_factor=1.0,
+                     want_dlogp=True, want_dentropy=False, out=None, dlogp=None, dentropy=None):
+    """One launch: the 8 loss scalars (see DRL_PPO_OUT_*) and d loss / d log_prob, d loss / d entropy."""
+    _dev(old_log_prob, log_prob, advantages, response_mask, entropy, ref_log_prob)
+    old_log_prob, log_prob, advantages = _c(old_log_prob.float()), _c(log_prob.float()), _c(advantages.float())
+    response_mask = _c(response_mask)
+    entropy = _c(entropy.float()) if entropy is not None else None
+    ref_log_prob = _c(ref_log_prob.float()) if ref_log_prob is not None else None
+    B, R = log_prob.shape
+    prm = _lib.PPOLossParams(clip_ratio_low, clip_ratio_high, clip_ratio_c, entropy_coeff, kl_loss_coef,
+                             loss_scale_factor, _lib.AGG_MODES[loss_agg_mode],
+                             _lib.KL_NONE if kl_loss_type is None else _lib.KL_TYPES[kl_loss_type])
+    dev = log_prob.device
+    if out is None:
+        out = torch.empty(_lib.PPO_OUT_N, dtype=torch.float32, device=dev)
+    if want_dlogp and dlogp is None:
+        dlogp = torch.empty_like(log_prob)
+    if want_dentropy and dentropy is None:
+        dentropy = torch.empty_like(log_prob)
+    L = lib()
+    nb = L.drl_ppo_loss_workspace_bytes(B, R)
+    ws = _ws.get(nb, dev)
+    check(L.drl_ppo_loss_fwd_bwd(_p(old_log_prob), _p(log_prob), _p(advantages), _p(response_mask),
+                                 mask_dtype_code(response_mask), _p(entropy), _p(ref_log_prob), B, R,
+                                 ctypes.byref(prm), _p(out), _p(dlogp if want_dlogp else None),
+                                 _p(dentropy if want_dentropy else None), _p(ws), ws.numel(), _stream()),
+          "drl_ppo_loss_fwd_bwd")
+    return out, (dlogp if want_dlogp else None), (dentropy if want_dentropy else None)
+
+
+def kl_penalty(log_prob, ref_log_prob, kl_type: str):
+    _dev(log_prob, ref_log_prob)
+    a, b = _c(log_prob.float()), _c(ref_log_prob.float())
+    out = torch.empty_like(a)
+    check(lib().drl_kl_penalty(_p(a), _p(b), a.numel(), _lib.KL_TYPES[kl_type], _p(out), _stream()), "drl_kl_penalty")
+    return out
+
+
+def agg_loss(loss_mat, loss_mask, loss_agg_mode):
+    _dev(loss_mat, loss_mask)
+    x, m = _c(loss_mat.float()), _c(loss_mask)
+    B, R = x.shape
+    out = torch.empty((), dtype=torch.float32, device=x.device)
+    L = lib()
+    ws = _ws.get(L.drl_agg_loss_workspace_bytes(B, R), x.device)
+    check(L.drl_agg_loss(_p(x), _p(m), mask_dtype_code(m), B, R, _lib.AGG_MODES[loss_agg_mode], _p(out), _p(ws),
+                         ws.numel(), _stream()), "drl_agg_loss")
+    return out
+
+
+# ----------------------------------------------------------------------------------------------- K2
+def _logits_2d(logits):
+    if logits.dtype not in _LOGIT_DTYPES:
+        raise ValueError(f"logits dtype {logits.dtype} not supported (float32 / bfloat16)")
+    if logits.dim() != 2:
+        logits = logits.reshape(-1, logits.shape[-1])
+    if logits.stride(-1) != 1:
+        logits = logits.contiguous()
+    return logits
+
+
+def logprob_entropy_fwd(logits, labels, temperature=1.0, want_entropy=True, want_lse=True):
+    _dev(logits, labels)
+    lg = _logits_2d(logits)
+    lab = _c(labels.reshape(-1).to(torch.int64))
+    N, V = lg.shape
+    dev = lg.device
+    logp = torch.empty(N, dtype=torch.float32, device=dev)
+    ent = torch.empty(N, dtype=torch.float32, device=dev) if want_entropy else None
+    lse = torch.empty(N, dtype=torch.float32, device=dev) if want_lse else None
+    check(lib().drl_logprob_entropy_fwd(_p(lg), _LOGIT_DTYPES[lg.dtype], N, V, lg.stride(0), _p(lab),
+                                        float(temperature), _p(logp), _p(ent), _p(lse), _stream()),
+          "drl_logprob_entropy_fwd")
+    return logp, ent, lse
+
+
+def logprob_entropy_bwd(logits, labels, temperature, dlogp, dentropy, lse, entropy, out=None, out_dtype=None):
+    _dev(logits, labels)
+    lg = _logits_2d(logits)
+    lab = _c(labels.reshape(-1).to(torch.int64))
+    N, V = lg.shape
+    if out is None:
+        out = torch.empty((N, V), dtype=out_dtype or lg.dtype, device=lg.device)
+    dlogp = _c(dlogp.reshape(-1).float()) if dlogp is not None else None
+    dentropy = _c(dentropy.reshape(-1).float()) if dentropy is not None else None
+    check(lib().drl_logprob_entropy_bwd(_p(lg), _LOGIT_DTYPES[lg.dtype], N, V, lg.stride(0), _p(lab),
+                                        float(temperature), _p(dlogp), _p(dentropy), _p(_c(lse)), _p(_c(entropy)),
+                                        _p(out), _LOGIT_DTYPES[out.dtype], out.stride(0), _stream()),
+          "drl_logprob_entropy_bwd")
+    return out
+
+
+# ----------------------------------------------------------------------------------------------- K3/K5
+def grpo_outcome_advantage(token_level_rewards, response_mask, row_group, group_offsets, group_members, G,
+                           epsilon=1e-6, norm_adv_by_std_in_grpo=True):
+    _dev(token_level_rewards, response_mask, row_group, group_offsets, group_members)
+    r, m = _c(token_level_rewards.float()), _c(response_mask)
+    B, R = r.shape
+    adv = torch.empty_like(r)
+    ret = torch.empty_like(r)
+    L = lib()
+    ws = _ws.get(L.drl_grpo_workspace_bytes(B), r.device)
+    check(L.drl_grpo_outcome_advantage(_p(r), _p(m), mask_dtype_code(m), _p(_c(row_group)), _p(_c(group_offsets)),
+                                       _p(_c(group_members)), B, R, G, float(epsilon), int(bool(norm_adv_by_std_in_grpo)),
+                                       _p(adv), _p(ret), _p(ws), ws.numel(), _stream()), "drl_grpo_outcome_advantage")
+    return adv, ret
+
+
+def gae_advantage_return(token_level_rewards, values, response_mask, gamma, lam):
+    _dev(token_level_rewards, values, response_mask)
+    r, v, m = _c(token_level_rewards.float()), _c(values.float()), _c(response_mask)
+    B, R = r.shape
+    adv, ret = torch.empty_like(r), torch.empty_like(r)
+    L = lib()
+    ws = _ws.get(L.drl_gae_workspace_bytes(B, R), r.device)
+    check(L.drl_gae_advantage_return(_p(r), _p(v), _p(m), mask_dtype_code(m), B, R, float(gamma), float(lam), _p(adv),
+                                     _p(ret), _p(ws), ws.numel(), _stream()), "drl_gae_advantage_return")
+    return adv, ret
+
+
+# ----------------------------------------------------------------------------------------------- K4
+def select_tokens(logits, out_tokens, *, do_sample=False, temperature=1.0, top_k=0, top_p=1.0, seed=0, step=0,
+                  row_base=0, pad_token_id=0, eos_ids=None, unfinished=None):
+    """Pick one token per row into ``out_tokens`` (int64 view with any row stride, e.g. responses[:, t])."""
+    _dev(logits, out_tokens, eos_ids, unfinished)
+    lg = _logits_2d(logits)
+    N, V = lg.shape
+    assert out_tokens.dtype == torch.int64 and out_tokens.numel() == N
+    ld_out = out_tokens.stride(0) if out_tokens.dim() == 1 else 1
+    prm = _lib.SamplingParams(int(bool(do_sample)), float(temperature), int(top_k), float(top_p),
+                              int(seed) & 0xFFFFFFFFFFFFFFFF, int(step), int(row_base), int(pad_token_id),
+                              None if eos_ids is None else eos_ids.data_ptr(),
+                              0 if eos_ids is None else eos_ids.numel())
+    check(lib().drl_select_tokens(_p(lg), _LOGIT_DTYPES[lg.dtype], N, V, lg.stride(0), ctypes.byref(prm),
+                                  _p(unfinished), _p(out_tokens), ld_out, _stream()), "drl_select_tokens")
+    return out_tokens
+
+
+def response_mask(responses, eos_ids, dtype=torch.int64, out=None):
+    _dev(responses, eos_ids)
+    B, R = responses.shape
+    if out is None:
+        out = torch.empty((B, R), dtype=dtype, device=responses.device)
+    code = {torch.int64: _lib.DRL_I64, torch.int32: _lib.DRL_I32, torch.uint8: _lib.DRL_U8, torch.bool: _lib.DRL_U8,
+            torch.float32: _lib.DRL_F32}[out.dtype]
+    check(lib().drl_response_mask(_p(responses), B, R, responses.stride(0), _p(eos_ids), eos_ids.numel(), _p(out),
+                                  code, out.stride(0), _stream()), "drl_response_mask")
+    return out
+
+
+def position_ids(attention_mask):
+    _dev(attention_mask)
+    m = _c(attention_mask)
+    B, T = m.shape
+    out = torch.empty((B, T), dtype=torch.int64, device=m.device)
+    check(lib().drl_position_ids(_p(m), mask_dtype_code(m), B, T, _p(out), _stream()), "drl_position_ids")
+    return out
+
+
+def response_position_ids_(position_ids_full, prompt_len):
+    """In place: fill columns [prompt_len:] of a (B, P+R) int64 buffer from column prompt_len-1."""
+    _dev(position_ids_full)
+    assert position_ids_full.is_contiguous() and position_ids_full.dtype == torch.int64
+    B, T = position_ids_full.shape
+    check(lib().drl_response_position_ids(_p(position_ids_full), B, prompt_len, T - prompt_len, _stream()),
+          "drl_response_position_ids")
+    return position_ids_full
+
+
+# ----------------------------------------------------------------------------------------------- A15
+def grad_norm(flat_grads, out=None):
+    _dev(flat_grads)
+    assert flat_grads.is_contiguous() and flat_grads.dtype == torch.float32
+    if out is None:
+        out = torch.empty(1, dtype=torch.float32, device=flat_grads.device)
+    L = lib()
+    ws = _ws.get(L.drl_grad_norm_workspace_bytes(flat_grads.numel()), flat_grads.device)
+    check(L.drl_grad_norm(_p(flat_grads), flat_grads.numel(), _p(out), _p(ws), ws.numel(), _stream()), "drl_grad_norm")
+    return out
+
+
+def adamw_step(params, grads, exp_avg, exp_avg_sq, *, lr, beta1, beta2, eps, weight_decay, step, max_grad_norm,
+               grad_norm_t=None, params_bf16=None):
+    _dev(params, grads, exp_avg, exp_avg_sq, grad_norm_t, params_bf16)
+    hp = _lib.AdamWParams(float(lr), float(beta1), float(beta2), float(eps), float(weight_decay), int(step),
+                          float(max_grad_norm))
+    check(lib().drl_adamw_step(_p(params), _p(grads), _p(exp_avg), _p(exp_avg_sq), _p(params_bf16), params.numel(),
+                               ctypes.byref(hp), _p(grad_norm_t), _stream()), "drl_adamw_step")

@@ -1,0 +1,214 @@
+/*
+ * dotsrl_amd.h — C-ABI of the MI355X (gfx950) PPO/GRPO actor-learner hot path.
+ *
+ * Drop-in boundary for the numeric core behind verl's DataParallelPPOActor / RayPPOTrainer
+ * (rednote-hilab/dots.rl @ 2025-09-19, paths relative to that tree). Every entry point replaces one
+ * reference interface (cited per function). Rules of the boundary:
+ *   - plain pointers + sizes; all buffers are device memory allocated by the caller (PyTorch-ROCm
+ *     storage in the Python host); the library never allocates, frees or synchronises;
+ *   - `stream` is a hipStream_t (passed as void*); every call only enqueues work on it, so the
+ *     calls are hipGraph-capturable;
+ *   - return 0 on success, a negative DRL_ERR_* code otherwise; drl_last_error() describes the last
+ *     failure on the calling thread. No C++ exception crosses the boundary.
+ *   - tensors are row-major and contiguous unless a leading dimension (`ld*`) is given.
+ */
+#ifndef DOTSRL_AMD_H_
+#define DOTSRL_AMD_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DRL_ABI_VERSION 1
+
+#define DRL_OK 0
+#define DRL_ERR_INVALID (-1)     /* bad argument (shape, dtype, null pointer, alignment) */
+#define DRL_ERR_HIP (-2)         /* a HIP runtime call failed */
+#define DRL_ERR_UNSUPPORTED (-3) /* valid request this build does not implement */
+#define DRL_ERR_WORKSPACE (-4)   /* workspace too small */
+
+typedef enum drl_dtype {
+  DRL_I64 = 0,
+  DRL_I32 = 1,
+  DRL_U8 = 2, /* also torch.bool */
+  DRL_F32 = 3,
+  DRL_BF16 = 4,
+} drl_dtype;
+
+/* loss_agg_mode of core_algos.agg_loss (verl/trainer/ppo/core_algos.py:703-736) */
+typedef enum drl_agg_mode {
+  DRL_AGG_TOKEN_MEAN = 0,
+  DRL_AGG_SEQ_MEAN_TOKEN_SUM = 1,
+  DRL_AGG_SEQ_MEAN_TOKEN_MEAN = 2,
+  DRL_AGG_SEQ_MEAN_TOKEN_SUM_NORM = 3,
+} drl_agg_mode;
+
+/* kl_penalty types (verl/trainer/ppo/core_algos.py:1272-1307) */
+typedef enum drl_kl_type {
+  DRL_KL_NONE = -1, /* use_kl_loss = False */
+  DRL_KL_K1 = 0,    /* "kl" / "k1" */
+  DRL_KL_ABS = 1,   /* "abs" */
+  DRL_KL_K2 = 2,    /* "mse" / "k2" */
+  DRL_KL_K3 = 3,    /* "low_var_kl" / "k3" */
+} drl_kl_type;
+
+const char* drl_last_error(void);
+int drl_abi_version(void);
+/* Number of compute units of the current device (grid sizing); <0 on error. */
+int drl_device_cu_count(void);
+
+/* ------------------------------------------------------------------------------------------------
+ * K1 — fused per-micro-batch actor loss, forward + backward in ONE launch.
+ * Replaces the eager chain of DataParallelPPOActor.update_policy (verl/workers/actor/dp_actor.py:419-466):
+ *   compute_policy_loss_vanilla (core_algos.py:815-889) + agg_loss(entropy) + kl_penalty + agg_loss(kld)
+ *   + `loss * loss_scale_factor` + loss.backward() down to d loss / d log_prob and d loss / d entropy.
+ * Inputs (B, R) float32, response_mask (B, R) of `mask_dtype` (I64/I32/U8/F32).
+ * entropy may be NULL (entropy_coeff must then be 0); ref_log_prob may be NULL (kl_type must be NONE).
+ * out_scalars: device float[DRL_PPO_OUT_N], see the enum. dlog_prob / dentropy may be NULL.
+ * ---------------------------------------------------------------------------------------------- */
+typedef struct drl_ppo_loss_params {
+  float clip_ratio_low;    /* actor.clip_ratio_low (defaults to clip_ratio) */
+  float clip_ratio_high;   /* actor.clip_ratio_high */
+  float clip_ratio_c;      /* actor.clip_ratio_c (dual clip, > 1) */
+  float entropy_coeff;     /* actor.entropy_coeff; 0 = term absent (dp_actor.py:441-447) */
+  float kl_loss_coef;      /* actor.kl_loss_coef */
+  float loss_scale_factor; /* 1 / gradient_accumulation (dp_actor.py:415-417) */
+  int32_t loss_agg_mode;   /* drl_agg_mode */
+  int32_t kl_type;         /* drl_kl_type; NONE = use_kl_loss False */
+} drl_ppo_loss_params;
+
+enum {
+  DRL_PPO_OUT_PG_LOSS = 0,
+  DRL_PPO_OUT_PG_CLIPFRAC = 1,
+  DRL_PPO_OUT_PPO_KL = 2,
+  DRL_PPO_OUT_PG_CLIPFRAC_LOWER = 3,
+  DRL_PPO_OUT_ENTROPY_LOSS = 4, /* agg_loss(entropy) when entropy != NULL, else 0 */
+  DRL_PPO_OUT_KL_LOSS = 5,      /* agg_loss(kld) when kl_type != NONE, else 0 */
+  DRL_PPO_OUT_LOSS = 6,         /* (pg - c_ent*ent + c_kl*kl) * loss_scale_factor — the value backpropagated */
+  DRL_PPO_OUT_MASK_COUNT = 7,   /* sum(response_mask) */
+  DRL_PPO_OUT_N = 8
+};
+
+size_t drl_ppo_loss_workspace_bytes(int64_t B, int64_t R);
+int drl_ppo_loss_fwd_bwd(const float* old_log_prob, const float* log_prob, const float* advantages,
+                         const void* response_mask, int32_t mask_dtype, const float* entropy,
+                         const float* ref_log_prob, int64_t B, int64_t R, const drl_ppo_loss_params* params,
+                         float* out_scalars, float* dlog_prob, float* dentropy, void* workspace,
+                         size_t workspace_bytes, void* stream);
+
+/* kl_penalty elementwise (core_algos.py:1272-1307): out[n] = kl(logprob[n], ref_logprob[n]). */
+int drl_kl_penalty(const float* log_prob, const float* ref_log_prob, int64_t n, int32_t kl_type, float* out,
+                   void* stream);
+
+/* agg_loss forward (core_algos.py:703-736), used for the driver-side entropy metric
+ * (ray_trainer.py:1215). out: device float[1]. */
+size_t drl_agg_loss_workspace_bytes(int64_t B, int64_t R);
+int drl_agg_loss(const float* loss_mat, const void* loss_mask, int32_t mask_dtype, int64_t B, int64_t R,
+                 int32_t loss_agg_mode, float* out, void* workspace, size_t workspace_bytes, void* stream);
+
+/* ------------------------------------------------------------------------------------------------
+ * K2 — log-prob of labels and entropy over the vocabulary, from logits (one pass, online softmax).
+ * Replaces logprobs_from_logits / entropy_from_logits (verl/utils/torch_functional.py:64-160) as called
+ * from _forward_micro_batch (dp_actor.py:198-211, 263-272) after `logits.div_(temperature)`.
+ * logits: (N, V) F32 or BF16 with row stride ld (elements). Math in float32; outputs float32
+ * (the flash-attn cross-entropy semantics of torch_functional.py:81-100).
+ * entropy / lse_out may be NULL. lse_out keeps logsumexp(logits/T) for the backward.
+ * ---------------------------------------------------------------------------------------------- */
+int drl_logprob_entropy_fwd(const void* logits, int32_t logits_dtype, int64_t N, int64_t V, int64_t ld,
+                            const int64_t* labels, float temperature, float* log_prob, float* entropy,
+                            float* lse_out, void* stream);
+/* d logits = (dlogp*(onehot - p) - dent*p*(log p + H)) / T   (experimental/torch_functional.py:40-72)
+ * dlog_prob / dentropy may be NULL (treated as 0). dlogits (N, V) of dlogits_dtype (F32/BF16), row stride
+ * ld_out; dlogits may alias logits (in-place backward, torch_functional.py:81 inplace_backward). */
+int drl_logprob_entropy_bwd(const void* logits, int32_t logits_dtype, int64_t N, int64_t V, int64_t ld,
+                            const int64_t* labels, float temperature, const float* dlog_prob,
+                            const float* dentropy, const float* lse, const float* entropy, void* dlogits,
+                            int32_t dlogits_dtype, int64_t ld_out, void* stream);
+
+/* ------------------------------------------------------------------------------------------------
+ * K3 — GRPO outcome advantage (core_algos.py:260-324), computed on device.
+ * group_offsets[G+1] / group_members[B] is the CSR of uid -> rows in order of first appearance
+ * (built on the host from DataProto.non_tensor_batch["uid"]). advantages/returns (B, R) float32.
+ * ---------------------------------------------------------------------------------------------- */
+size_t drl_grpo_workspace_bytes(int64_t B);
+int drl_grpo_outcome_advantage(const float* token_level_rewards, const void* response_mask, int32_t mask_dtype,
+                               const int32_t* row_group, const int32_t* group_offsets,
+                               const int32_t* group_members, int64_t B, int64_t R, int64_t G, float epsilon,
+                               int32_t norm_adv_by_std, float* advantages, float* returns, void* workspace,
+                               size_t workspace_bytes, void* stream);
+
+/* K5 — GAE + masked_whiten (core_algos.py:208-256, torch_functional.py:206-223). */
+size_t drl_gae_workspace_bytes(int64_t B, int64_t R);
+int drl_gae_advantage_return(const float* token_level_rewards, const float* values, const void* response_mask,
+                             int32_t mask_dtype, int64_t B, int64_t R, float gamma, float lam, float* advantages,
+                             float* returns, void* workspace, size_t workspace_bytes, void* stream);
+
+/* ------------------------------------------------------------------------------------------------
+ * K4 — decode-step token selection over the vocabulary (HF generate semantics that HFRollout
+ * delegates to, verl/workers/rollout/hf_rollout.py:112-124). One launch per decode step.
+ * logits (N, V) F32/BF16 (row stride ld). unfinished (N) int32 in/out: rows already finished emit
+ * pad_token_id (HF: next = next*unfinished + pad*(1-unfinished)) and a row hitting any eos id
+ * becomes finished. The chosen token is written to out_tokens[n*ld_out] (int64) — pass a column
+ * of the `responses` tensor to fill it in place. temperature <= 0 or do_sample == 0 -> greedy
+ * (argmax, first index on ties = torch.argmax). Sampling: temperature, then top-k (top_k <= 0 ->
+ * off), then top-p (>= 1 -> off), then the inverse CDF at a Philox4x32-10 uniform
+ * (seed, offset = decode step, counter = row_base + n).
+ * ---------------------------------------------------------------------------------------------- */
+typedef struct drl_sampling_params {
+  int32_t do_sample;
+  float temperature;
+  int32_t top_k;
+  float top_p;
+  uint64_t seed;
+  uint64_t offset;
+  int64_t row_base;
+  int64_t pad_token_id;
+  const int64_t* eos_ids; /* device int64[n_eos]; may be NULL when n_eos == 0 */
+  int32_t n_eos;
+} drl_sampling_params;
+
+int drl_select_tokens(const void* logits, int32_t logits_dtype, int64_t N, int64_t V, int64_t ld,
+                      const drl_sampling_params* params, int32_t* unfinished, int64_t* out_tokens,
+                      int64_t ld_out, void* stream);
+
+/* ------------------------------------------------------------------------------------------------
+ * Rollout bookkeeping (A4/A5).
+ * get_response_mask (torch_functional.py:226-246): mask[b,t] = 1 up to and including the first eos.
+ * compute_position_id_with_mask (utils/model.py:219): pos = clip(cumsum(mask)-1, 0).
+ * response positions (hf_rollout.py:151-155): pos[b, P+t] = pos[b, P-1] + 1 + t.
+ * ---------------------------------------------------------------------------------------------- */
+int drl_response_mask(const int64_t* responses, int64_t B, int64_t R, int64_t ld, const int64_t* eos_ids,
+                      int32_t n_eos, void* mask_out, int32_t mask_dtype, int64_t ld_out, void* stream);
+int drl_position_ids(const void* attention_mask, int32_t mask_dtype, int64_t B, int64_t T, int64_t* position_ids,
+                     void* stream);
+int drl_response_position_ids(int64_t* position_ids, int64_t B, int64_t P, int64_t R, void* stream);
+
+/* ------------------------------------------------------------------------------------------------
+ * A15 — optimizer step on a flat fp32 master buffer: clip_grad_norm_ + skip-if-non-finite + AdamW
+ * (dp_actor.py:282-298; torch.optim.AdamW semantics, fsdp_workers.py:454-459).
+ * drl_grad_norm: out_norm[0] = ||grads||_2 (device float).
+ * drl_adamw_step: applies clip coef min(1, max_norm/(norm+1e-6)) from device `norm`; if norm is not
+ * finite the step is skipped (params/moments untouched). Optionally writes a bf16 compute copy.
+ * ---------------------------------------------------------------------------------------------- */
+size_t drl_grad_norm_workspace_bytes(int64_t n);
+int drl_grad_norm(const float* grads, int64_t n, float* out_norm, void* workspace, size_t workspace_bytes,
+                  void* stream);
+typedef struct drl_adamw_params {
+  float lr;
+  float beta1;
+  float beta2;
+  float eps;
+  float weight_decay;
+  int32_t step;       /* 1-based step count after this update */
+  float max_grad_norm; /* <= 0: no clipping */
+} drl_adamw_params;
+int drl_adamw_step(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, uint16_t* params_bf16,
+                   int64_t n, const drl_adamw_params* hp, const float* grad_norm, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DOTSRL_AMD_H_ */
