@@ -1,0 +1,111 @@
+"""Trainer configuration with the reference's dotted key names (verl/trainer/config/ppo_trainer.yaml,
+actor/actor.yaml, actor/dp_actor.yaml, rollout/rollout.yaml, algorithm section).
+
+Only the keys the actor-learner hot path reads are defined; ``apply_overrides`` accepts the same
+``a.b.c=value`` strings a hydra command line uses (e.g. ``actor_rollout_ref.actor.ppo_mini_batch_size=32``),
+so reference launch scripts map over key for key. ``actor.strategy`` selects this backend: ``"mi355x"``.
+"""
+
+from __future__ import annotations
+
+import ast
+import copy
+
+
+class AttrDict(dict):
+    """dict with attribute access and ``.get`` — the subset of OmegaConf DictConfig in use."""
+
+    def __getattr__(self, k):
+        try:
+            return self[k]
+        except KeyError as e:
+            raise AttributeError(k) from e
+
+    def __setattr__(self, k, v):
+        self[k] = v
+
+    def __deepcopy__(self, memo):
+        return AttrDict({k: copy.deepcopy(v, memo) for k, v in self.items()})
+
+
+def to_attr(d):
+    if isinstance(d, dict):
+        return AttrDict({k: to_attr(v) for k, v in d.items()})
+    if isinstance(d, list):
+        return [to_attr(v) for v in d]
+    return d
+
+
+# Qwen2.5-0.5B architecture (config.json of Qwen/Qwen2.5-0.5B(-Instruct)); weights are random-init (no network)
+QWEN25_05B = dict(
+    vocab_size=151936, hidden_size=896, intermediate_size=4864, num_hidden_layers=24, num_attention_heads=14,
+    num_key_value_heads=2, max_position_embeddings=32768, rope_theta=1000000.0, rms_norm_eps=1e-6,
+    tie_word_embeddings=True, bos_token_id=151643, eos_token_id=151645, pad_token_id=151643,
+)
+
+DEFAULTS = dict(
+    data=dict(train_batch_size=64, max_prompt_length=512, max_response_length=256, seed=1234),
+    actor_rollout_ref=dict(
+        hybrid_engine=True,
+        model=dict(path="random:qwen2.5-0.5b", override_config={}, use_remove_padding=False, use_fused_kernels=False,
+                   enable_gradient_checkpointing=False, external_lib=None, dtype="bfloat16"),
+        actor=dict(
+            strategy="mi355x", ppo_mini_batch_size=32, ppo_micro_batch_size=None, ppo_micro_batch_size_per_gpu=8,
+            use_dynamic_bsz=False, ppo_max_token_len_per_gpu=16384, clip_ratio=0.2, clip_ratio_low=0.2,
+            clip_ratio_high=0.2, clip_ratio_c=3.0, policy_loss=dict(loss_mode="vanilla"), loss_agg_mode="token-mean",
+            entropy_coeff=0.0, use_kl_loss=True, kl_loss_coef=0.001, kl_loss_type="low_var_kl", ppo_epochs=1,
+            shuffle=False, grad_clip=1.0, ulysses_sequence_parallel_size=1,
+            optim=dict(lr=1e-6, lr_warmup_steps_ratio=0.0, total_training_steps=-1, weight_decay=0.01,
+                       lr_warmup_steps=-1, betas=[0.9, 0.999], eps=1e-8, warmup_style="constant", min_lr_ratio=0.0),
+        ),
+        rollout=dict(
+            name="mi355x", mode="sync", temperature=1.0, top_k=-1, top_p=1.0, do_sample=True, n=8,
+            prompt_length=512, response_length=256, ignore_eos=False, log_prob_micro_batch_size=None,
+            log_prob_micro_batch_size_per_gpu=16, log_prob_use_dynamic_bsz=False, micro_batch_size=None,
+            seed=1234, val_kwargs=dict(top_k=-1, top_p=1.0, temperature=0, n=1, do_sample=False),
+        ),
+        ref=dict(log_prob_micro_batch_size=None, log_prob_micro_batch_size_per_gpu=16, log_prob_use_dynamic_bsz=False),
+    ),
+    algorithm=dict(gamma=1.0, lam=1.0, adv_estimator="grpo", norm_adv_by_std_in_grpo=True, use_kl_in_reward=False,
+                   kl_penalty="kl", kl_ctrl=dict(type="fixed", kl_coef=0.001, horizon=10000, target_kl=0.1)),
+    reward_model=dict(enable=False, reward_manager="synthetic_bernoulli", launch_reward_fn_async=False),
+    trainer=dict(balance_batch=False, total_epochs=1, total_training_steps=None, critic_warmup=0, n_gpus_per_node=1,
+                 nnodes=1, save_freq=-1, test_freq=-1, logger=["console"], project_name="dots_rl_amd",
+                 experiment_name="grpo"),
+)
+
+
+def default_config():
+    return to_attr(copy.deepcopy(DEFAULTS))
+
+
+def _parse_value(s: str):
+    low = s.lower()
+    if low in ("true", "false"):
+        return low == "true"
+    if low in ("null", "none", "~"):
+        return None
+    try:
+        return ast.literal_eval(s)
+    except (ValueError, SyntaxError):
+        return s
+
+
+def apply_overrides(cfg: AttrDict, overrides) -> AttrDict:
+    """Apply hydra-style ``a.b.c=value`` overrides in place (``+a.b=v`` adds a new key)."""
+    for ov in overrides or []:
+        key, _, val = ov.partition("=")
+        add = key.startswith("+")
+        key = key.lstrip("+")
+        node = cfg
+        parts = key.split(".")
+        for p in parts[:-1]:
+            if p not in node:
+                if not add:
+                    raise KeyError(f"unknown config key {key}")
+                node[p] = AttrDict()
+            node = node[p]
+        if parts[-1] not in node and not add:
+            raise KeyError(f"unknown config key {key}")
+        node[parts[-1]] = to_attr(_parse_value(val))
+    return cfg

@@ -1,0 +1,218 @@
+"""PPO/GRPO algorithm entry points with the reference's names and registries, computed by the HIP kernels.
+
+Mirror of verl/trainer/ppo/core_algos.py (file:line per function). Registries and signatures are kept
+so reference call sites and custom registrations map over unchanged; the numerics run in
+libdotsrl_amd.so (K1 fused loss, K3 GRPO, K5 GAE).
+"""
+
+from __future__ import annotations
+
+from collections.abc import Callable
+from enum import Enum
+from typing import Any
+
+import numpy as np
+import torch
+
+from . import native
+
+POLICY_LOSS_REGISTRY: dict[str, Callable] = {}
+ADV_ESTIMATOR_REGISTRY: dict[str, Any] = {}
+
+
+def register_policy_loss(name: str):
+    """core_algos.py:51-66."""
+
+    def decorator(func):
+        POLICY_LOSS_REGISTRY[name] = func
+        return func
+
+    return decorator
+
+
+def get_policy_loss_fn(name):
+    """core_algos.py:69-83."""
+    if name not in POLICY_LOSS_REGISTRY:
+        raise ValueError(f"Unsupported loss mode: {name}. Supported modes are: {list(POLICY_LOSS_REGISTRY.keys())}")
+    return POLICY_LOSS_REGISTRY[name]
+
+
+class AdvantageEstimator(str, Enum):
+    """core_algos.py:86-103."""
+
+    GAE = "gae"
+    GRPO = "grpo"
+    REINFORCE_PLUS_PLUS = "reinforce_plus_plus"
+    REINFORCE_PLUS_PLUS_BASELINE = "reinforce_plus_plus_baseline"
+    REMAX = "remax"
+    RLOO = "rloo"
+    OPO = "opo"
+    GRPO_PASSK = "grpo_passk"
+    GPG = "gpg"
+
+
+def register_adv_est(name_or_enum):
+    """core_algos.py:109-126."""
+
+    def decorator(fn):
+        name = name_or_enum.value if isinstance(name_or_enum, Enum) else name_or_enum
+        if name in ADV_ESTIMATOR_REGISTRY and ADV_ESTIMATOR_REGISTRY[name] != fn:
+            raise ValueError(f"Adv estimator {name} has already been registered: {ADV_ESTIMATOR_REGISTRY[name]} vs {fn}")
+        ADV_ESTIMATOR_REGISTRY[name] = fn
+        return fn
+
+    return decorator
+
+
+def get_adv_estimator_fn(name_or_enum):
+    """core_algos.py:129-143."""
+    name = name_or_enum.value if isinstance(name_or_enum, Enum) else name_or_enum
+    if name not in ADV_ESTIMATOR_REGISTRY:
+        raise ValueError(f"Unknown advantage estimator simply: {name}")
+    return ADV_ESTIMATOR_REGISTRY[name]
+
+
+class AdaptiveKLController:
+    """core_algos.py:146-170."""
+
+    def __init__(self, init_kl_coef, target_kl, horizon):
+        self.value = init_kl_coef
+        self.target = target_kl
+        self.horizon = horizon
+
+    def update(self, current_kl, n_steps):
+        proportional_error = np.clip(current_kl / self.target - 1, -0.2, 0.2)
+        self.value *= 1 + proportional_error * n_steps / self.horizon
+
+
+class FixedKLController:
+    """core_algos.py:173-187."""
+
+    def __init__(self, kl_coef):
+        self.value = kl_coef
+
+    def update(self, current_kl, n_steps):
+        pass
+
+
+def get_kl_controller(kl_ctrl):
+    """core_algos.py:190-205."""
+    if kl_ctrl.type == "fixed":
+        return FixedKLController(kl_coef=kl_ctrl.kl_coef)
+    if kl_ctrl.type == "adaptive":
+        assert kl_ctrl.horizon > 0, f"horizon must be larger than 0. Got {kl_ctrl.horizon}"
+        return AdaptiveKLController(init_kl_coef=kl_ctrl.kl_coef, target_kl=kl_ctrl.target_kl, horizon=kl_ctrl.horizon)
+    raise NotImplementedError
+
+
+# ---------------------------------------------------------------------------------------------- advantages
+@register_adv_est(AdvantageEstimator.GAE)
+def compute_gae_advantage_return(token_level_rewards, values, response_mask, gamma, lam):
+    """core_algos.py:208-256 — HIP reverse scan + masked_whiten (K5)."""
+    with torch.no_grad():
+        return native.gae_advantage_return(token_level_rewards, values, response_mask, float(gamma), float(lam))
+
+
+def uid_csr(index, device):
+    """uid array -> (row_group[B], group_offsets[G+1], group_members[B], G): groups in order of first
+    appearance, members in row order (the order core_algos.py:297-309 stacks them)."""
+    keys = {}
+    row_group = np.empty(len(index), np.int32)
+    for i, u in enumerate(index):
+        row_group[i] = keys.setdefault(u, len(keys))
+    G = len(keys)
+    members = np.argsort(row_group, kind="stable").astype(np.int32)
+    offsets = np.zeros(G + 1, np.int32)
+    np.add.at(offsets, row_group + 1, 1)
+    offsets = np.cumsum(offsets).astype(np.int32)
+    t = lambda a: torch.from_numpy(a).to(device, non_blocking=True)  # noqa: E731
+    return t(row_group), t(offsets), t(members), G
+
+
+@register_adv_est(AdvantageEstimator.GRPO)
+def compute_grpo_outcome_advantage(token_level_rewards, response_mask, index, epsilon: float = 1e-6,
+                                   norm_adv_by_std_in_grpo: bool = True, config=None):
+    """core_algos.py:260-324 — scores, group mean/std and the (B, R) broadcast on device (K3)."""
+    row_group, offsets, members, G = uid_csr(index, token_level_rewards.device)
+    with torch.no_grad():
+        return native.grpo_outcome_advantage(token_level_rewards, response_mask, row_group, offsets, members, G,
+                                             epsilon, norm_adv_by_std_in_grpo)
+
+
+# ---------------------------------------------------------------------------------------------- losses
+def agg_loss(loss_mat, loss_mask, loss_agg_mode: str):
+    """core_algos.py:703-736 (forward; gradients flow through fused_actor_loss)."""
+    if loss_mat.requires_grad:
+        raise NotImplementedError("differentiate the actor loss through fused_actor_loss (one HIP pass fwd+bwd)")
+    return native.agg_loss(loss_mat, loss_mask, loss_agg_mode)
+
+
+def kl_penalty(logprob, ref_logprob, kl_penalty):
+    """core_algos.py:1272-1307 (forward; the KL gradient is part of fused_actor_loss)."""
+    if kl_penalty == "full":
+        raise NotImplementedError
+    if logprob.requires_grad:
+        raise NotImplementedError("differentiate the KL term through fused_actor_loss")
+    return native.kl_penalty(logprob, ref_logprob, kl_penalty)
+
+
+class _FusedActorLoss(torch.autograd.Function):
+    """K1: forward AND backward computed in the forward launch; backward only scales the stored grads."""
+
+    @staticmethod
+    def forward(ctx, log_prob, entropy, old_log_prob, advantages, response_mask, ref_log_prob, kw):
+        out, dlogp, dent = native.ppo_loss_fwd_bwd(
+            old_log_prob.detach(), log_prob.detach(), advantages, response_mask,
+            entropy.detach() if entropy is not None else None, ref_log_prob,
+            want_dlogp=log_prob.requires_grad, want_dentropy=entropy is not None and entropy.requires_grad, **kw)
+        ctx.save_for_backward(dlogp if dlogp is not None else out.new_empty(0),
+                              dent if dent is not None else out.new_empty(0))
+        ctx.has = (dlogp is not None, dent is not None)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        dlogp, dent = ctx.saved_tensors
+        scale = g[6]  # only the total loss (DRL_PPO_OUT_LOSS) carries a gradient
+        return (dlogp * scale if ctx.has[0] else None, dent * scale if ctx.has[1] else None,
+                None, None, None, None, None)
+
+
+def fused_actor_loss(log_prob, entropy, old_log_prob, advantages, response_mask, ref_log_prob, *, clip_ratio_low,
+                     clip_ratio_high, clip_ratio_c, entropy_coeff, use_kl_loss, kl_loss_type, kl_loss_coef,
+                     loss_agg_mode, loss_scale_factor):
+    """The whole per-micro-batch loss of dp_actor.py:419-466 in one HIP launch.
+
+    Returns a float32[8] tensor: pg_loss, pg_clipfrac, ppo_kl, pg_clipfrac_lower, entropy_loss, kl_loss,
+    loss (= (pg - c_ent*ent + c_kl*kl) * loss_scale_factor, the backpropagated value), mask_count.
+    """
+    kw = dict(clip_ratio_low=clip_ratio_low, clip_ratio_high=clip_ratio_high, clip_ratio_c=clip_ratio_c,
+              entropy_coeff=entropy_coeff if entropy is not None else 0.0,
+              kl_loss_coef=kl_loss_coef if use_kl_loss else 0.0,
+              kl_loss_type=kl_loss_type if use_kl_loss else None, loss_agg_mode=loss_agg_mode,
+              loss_scale_factor=loss_scale_factor)
+    return _FusedActorLoss.apply(log_prob, entropy, old_log_prob, advantages, response_mask,
+                                 ref_log_prob if use_kl_loss else None, kw)
+
+
+@register_policy_loss("vanilla")
+def compute_policy_loss_vanilla(old_log_prob, log_prob, advantages, response_mask, loss_agg_mode: str = "token-mean",
+                                config=None):
+    """core_algos.py:815-889 — (pg_loss, pg_clipfrac, ppo_kl, pg_clipfrac_lower); pg_loss is differentiable."""
+    assert config is not None
+    clip_ratio = config.clip_ratio
+    lo = config.clip_ratio_low if config.get("clip_ratio_low") is not None else clip_ratio
+    hi = config.clip_ratio_high if config.get("clip_ratio_high") is not None else clip_ratio
+    c = config.get("clip_ratio_c", 3.0)
+    assert c > 1.0, ("The lower bound of the clip_ratio_c for dual-clip PPO should be greater than 1.0,"
+                     + f" but get the value: {c}.")
+    out = fused_actor_loss(log_prob, None, old_log_prob, advantages, response_mask, None, clip_ratio_low=lo,
+                           clip_ratio_high=hi, clip_ratio_c=c, entropy_coeff=0.0, use_kl_loss=False,
+                           kl_loss_type=None, kl_loss_coef=0.0, loss_agg_mode=loss_agg_mode, loss_scale_factor=1.0)
+    # out[6] == pg_loss here (no entropy / KL term, scale 1) and is the differentiable slot
+    return out[6], out[1].detach(), out[2].detach(), out[3].detach()
+
+
+def compute_value_loss(vpreds, returns, values, response_mask, cliprange_value, loss_agg_mode="token-mean"):
+    """core_algos.py:1230-1269 (critic, config #4) — not on the GRPO path yet."""
+    raise NotImplementedError("critic value loss lands with the GAE/critic row (SURVEY §8(f) rank 4)")

@@ -1,0 +1,429 @@
+// Transformer-layer kernels of the Qwen2 actor / reference / rollout model (everything that is not a
+// GEMM; GEMMs run on hipBLASLt): fused QKV split + RoPE + grouped-query re-layout (fwd / bwd),
+// masked softmax over attention scores (fwd / bwd), residual-add + RMSNorm (fwd / bwd), SwiGLU (fwd / bwd).
+// Semantics follow HF Qwen2 (Qwen2RMSNorm fp32 variance, rotate_half RoPE, SiLU(gate) * up, causal +
+// key-padding attention mask) as the reference runs it (verl/workers/actor/dp_actor.py:90-280 model call).
+// All are HBM-bound streaming kernels: 16-B vector loads, fp32 math, one pass.
+#include "common.h"
+
+namespace drl {
+namespace {
+
+// element I/O: E = uint16_t (bf16) or float
+__device__ __forceinline__ float ldf(const uint16_t* p, int64_t i) { return bf16_to_f32(p[i]); }
+__device__ __forceinline__ float ldf(const float* p, int64_t i) { return p[i]; }
+__device__ __forceinline__ void stf(uint16_t* p, int64_t i, float v) { p[i] = f32_to_bf16(v); }
+__device__ __forceinline__ void stf(float* p, int64_t i, float v) { p[i] = v; }
+template <typename E>
+__device__ __forceinline__ float rnd(float v) {  // round through E (models a separate E-typed op)
+  if constexpr (sizeof(E) == 2) return bf16_to_f32(f32_to_bf16(v));
+  else return v;
+}
+
+// ------------------------------------------------------------------------------------------ RoPE + QKV
+// qkv (B, T, (Hq + 2 Hkv) * D) bf16 ->
+//   q  (B, Hkv, G, T, D)   G = Hq / Hkv query heads per KV head, rotated
+//   k  (B, Hkv, Tk, D) at key offset koff (the KV cache when decoding), rotated
+//   v  (B, Hkv, Tk, D) at key offset koff
+// cos/sin tables (maxpos, D/2) fp32 indexed by position_ids (B, T). One thread per (b, t, head, pair).
+template <typename E>
+struct RopeArgs {
+  const E* qkv;
+  const int64_t* pos;
+  const float* cos_t;
+  const float* sin_t;
+  E* q;
+  E* k;
+  E* v;
+  int64_t B, T, Hq, Hkv, D, Tk, koff, maxpos;
+};
+
+template <typename E>
+__global__ __launch_bounds__(256) void rope_qkv_fwd_kernel(RopeArgs<E> a) {
+  const int64_t half = a.D / 2;
+  const int64_t Hall = a.Hq + 2 * a.Hkv;
+  const int64_t n = a.B * a.T * Hall * half;
+  const int64_t G = a.Hq / a.Hkv;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int64_t j = i % half;
+    const int64_t h = (i / half) % Hall;
+    const int64_t bt = i / (half * Hall);
+    const int64_t t = bt % a.T, b = bt / a.T;
+    const E* src = a.qkv + bt * Hall * a.D + h * a.D;
+    const float x1 = ldf(src, j), x2 = ldf(src, j + half);
+    if (h < a.Hq + a.Hkv) {
+      int64_t p = a.pos[b * a.T + t];
+      p = p < 0 ? 0 : (p >= a.maxpos ? a.maxpos - 1 : p);
+      const float c = a.cos_t[p * half + j], s = a.sin_t[p * half + j];
+      // rotate_half: out1 = x1*cos - x2*sin ; out2 = x2*cos + x1*sin
+      const float o1 = x1 * c - x2 * s, o2 = x2 * c + x1 * s;
+      E* dst;
+      if (h < a.Hq) {
+        const int64_t g = h / G, hi = h % G;
+        dst = a.q + (((b * a.Hkv + g) * G + hi) * a.T + t) * a.D;
+      } else {
+        dst = a.k + ((b * a.Hkv + (h - a.Hq)) * a.Tk + a.koff + t) * a.D;
+      }
+      stf(dst, j, o1);
+      stf(dst, j + half, o2);
+    } else {
+      E* dst = a.v + ((b * a.Hkv + (h - a.Hq - a.Hkv)) * a.Tk + a.koff + t) * a.D;
+      dst[j] = src[j];
+      dst[j + half] = src[j + half];
+    }
+  }
+}
+
+// backward: dq (B,Hkv,G,T,D), dk/dv (B,Hkv,T,D) -> dqkv (B,T,(Hq+2Hkv)*D) with the inverse rotation
+template <typename E>
+__global__ __launch_bounds__(256) void rope_qkv_bwd_kernel(RopeArgs<E> a, const E* dq, const E* dk, const E* dv,
+                                                           E* dqkv) {
+  const int64_t half = a.D / 2;
+  const int64_t Hall = a.Hq + 2 * a.Hkv;
+  const int64_t n = a.B * a.T * Hall * half;
+  const int64_t G = a.Hq / a.Hkv;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int64_t j = i % half;
+    const int64_t h = (i / half) % Hall;
+    const int64_t bt = i / (half * Hall);
+    const int64_t t = bt % a.T, b = bt / a.T;
+    E* dst = dqkv + bt * Hall * a.D + h * a.D;
+    if (h < a.Hq + a.Hkv) {
+      const E* src;
+      if (h < a.Hq) {
+        const int64_t g = h / G, hi = h % G;
+        src = dq + (((b * a.Hkv + g) * G + hi) * a.T + t) * a.D;
+      } else {
+        src = dk + ((b * a.Hkv + (h - a.Hq)) * a.T + t) * a.D;
+      }
+      int64_t p = a.pos[b * a.T + t];
+      p = p < 0 ? 0 : (p >= a.maxpos ? a.maxpos - 1 : p);
+      const float c = a.cos_t[p * half + j], s = a.sin_t[p * half + j];
+      const float g1 = ldf(src, j), g2 = ldf(src, j + half);
+      // transpose of [[c, -s], [s, c]]
+      stf(dst, j, g1 * c + g2 * s);
+      stf(dst, j + half, g2 * c - g1 * s);
+    } else {
+      const E* src = dv + ((b * a.Hkv + (h - a.Hq - a.Hkv)) * a.T + t) * a.D;
+      dst[j] = src[j];
+      dst[j + half] = src[j + half];
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------ softmax
+// Rows of attention scores S (rows, Tk) bf16 laid out (B, Hkv, G, Tq, Tk). Row r: q = r % Tq, b = r / (Hkv G Tq).
+// allowed(key j) = valid[b, j] && j <= q + qoff; a row with no allowed key is uniform (HF finfo.min mask)
+// P = softmax(S * scale) written as bf16 (in place allowed). One wave per row.
+template <typename E>
+struct SoftmaxArgs {
+  const float* s;  // fp32 scores (hipBLASLt bf16 x bf16 -> fp32)
+  E* p;
+  const uint8_t* valid;  // (B, ld_valid) 0/1
+  int64_t rows, Tq, Tk, HG, qoff, ld_valid;
+  float scale;
+};
+
+template <typename E>
+__global__ __launch_bounds__(256) void masked_softmax_fwd_kernel(SoftmaxArgs<E> a) {
+  const int64_t row = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= a.rows) return;
+  const int64_t q = row % a.Tq;
+  const int64_t b = row / (a.HG * a.Tq);
+  const int64_t qpos = q + a.qoff;
+  const float* src = a.s + row * a.Tk;
+  E* dst = a.p + row * a.Tk;
+  const uint8_t* vrow = a.valid + b * a.ld_valid;
+  const float sl2 = a.scale * 1.4426950408889634f;  // exp(x*scale) = exp2(x*scale*log2e)
+  float m = -INFINITY;
+  for (int64_t j = lane; j < a.Tk; j += 64) {
+    if (j <= qpos && vrow[j]) m = fmaxf(m, ldf(src, j) * sl2);
+  }
+  m = wave_max(m);
+  if (m == -INFINITY) {
+    // no allowed key (a left-padded query): HF adds finfo.min to every masked score, which makes the
+    // row uniform over all Tk keys; its output only ever reaches padded positions
+    const float u = 1.f / static_cast<float>(a.Tk);
+    for (int64_t j = lane; j < a.Tk; j += 64) stf(dst, j, u);
+    return;
+  }
+  float sum = 0.f;
+  for (int64_t j = lane; j < a.Tk; j += 64) {
+    if (j <= qpos && vrow[j]) sum += __builtin_amdgcn_exp2f(ldf(src, j) * sl2 - m);
+  }
+  sum = wave_sum(sum);
+  const float inv = 1.f / sum;
+  for (int64_t j = lane; j < a.Tk; j += 64) {
+    const bool ok = j <= qpos && vrow[j];
+    const float e = ok ? __builtin_amdgcn_exp2f(ldf(src, j) * sl2 - m) * inv : 0.f;
+    stf(dst, j, e);
+  }
+}
+
+// dS = P * (dP - sum_j P dP) * scale: P (E), dP fp32 -> dS (E). One wave per row.
+template <typename E>
+__global__ __launch_bounds__(256) void masked_softmax_bwd_kernel(const E* p, const float* dp, E* ds, int64_t rows,
+                                                                 int64_t Tk, float scale) {
+  const int64_t row = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const E* pr = p + row * Tk;
+  const float* dr = dp + row * Tk;
+  E* sr = ds + row * Tk;
+  float dot = 0.f;
+  for (int64_t j = lane; j < Tk; j += 64) dot += ldf(pr, j) * dr[j];
+  dot = wave_sum(dot);
+  for (int64_t j = lane; j < Tk; j += 64) stf(sr, j, ldf(pr, j) * (dr[j] - dot) * scale);
+}
+
+// ------------------------------------------------------------------------------------------ RMSNorm
+// x_out = x_in (+ delta) (fp32 residual stream; x_out may alias x_in or be NULL = no write);
+// y = w * x * rsqrt(mean(x^2) + eps) as E; rstd (N) saved for backward. One wave per row.
+template <typename E>
+__global__ __launch_bounds__(256) void add_rmsnorm_fwd_kernel(const float* x_in, const E* delta, float* x_out,
+                                                              const float* w, E* y, float* rstd, int64_t N, int64_t H,
+                                                              float eps) {
+  const int64_t row = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= N) return;
+  const float* xr = x_in + row * H;
+  float* xo = x_out ? x_out + row * H : nullptr;
+  float ss = 0.f;
+  for (int64_t j = lane * 4; j < H; j += 256) {
+    float4 v = *reinterpret_cast<const float4*>(xr + j);
+    if (delta) {
+      v.x += ldf(delta, row * H + j);
+      v.y += ldf(delta, row * H + j + 1);
+      v.z += ldf(delta, row * H + j + 2);
+      v.w += ldf(delta, row * H + j + 3);
+    }
+    if (xo) *reinterpret_cast<float4*>(xo + j) = v;
+    ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+  }
+  ss = wave_sum(ss);
+  const float r = rsqrtf(ss / static_cast<float>(H) + eps);
+  if (lane == 0 && rstd) rstd[row] = r;
+  const float* xs = xo ? xo : xr;
+  for (int64_t j = lane * 4; j < H; j += 256) {
+    float4 v = *reinterpret_cast<const float4*>(xs + j);
+    if (delta && !xo) {
+      v.x += ldf(delta, row * H + j);
+      v.y += ldf(delta, row * H + j + 1);
+      v.z += ldf(delta, row * H + j + 2);
+      v.w += ldf(delta, row * H + j + 3);
+    }
+    const float4 ww = *reinterpret_cast<const float4*>(w + j);
+    stf(y, row * H + j, ww.x * (v.x * r));
+    stf(y, row * H + j + 1, ww.y * (v.y * r));
+    stf(y, row * H + j + 2, ww.z * (v.z * r));
+    stf(y, row * H + j + 3, ww.w * (v.w * r));
+  }
+}
+
+// dx += rstd * (w*dy - xhat * mean(xhat * w*dy)) ; dw partials per block (fixed order) -> dw_part (grid, H)
+template <typename E>
+__global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const float* x, const float* w, const float* rstd,
+                                                          const E* dy, float* dx, float* dw_part, int64_t N,
+                                                          int64_t H) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  extern __shared__ float s_dw[];  // 4 waves x H
+  for (int64_t j = threadIdx.x; j < 4 * H; j += blockDim.x) s_dw[j] = 0.f;
+  __syncthreads();
+  for (int64_t row = static_cast<int64_t>(blockIdx.x) * 4 + wave; row < N; row += static_cast<int64_t>(gridDim.x) * 4) {
+    const float r = rstd[row];
+    const float* xr = x + row * H;
+    float dot = 0.f;
+    for (int64_t j = lane; j < H; j += 64) dot += (w[j] * ldf(dy, row * H + j)) * (xr[j] * r);
+    dot = wave_sum(dot) / static_cast<float>(H);
+    for (int64_t j = lane; j < H; j += 64) {
+      const float g = ldf(dy, row * H + j);
+      const float xh = xr[j] * r;
+      dx[row * H + j] += r * (w[j] * g - xh * dot);
+      s_dw[wave * H + j] += g * xh;
+    }
+  }
+  __syncthreads();
+  for (int64_t j = threadIdx.x; j < H; j += blockDim.x)
+    dw_part[blockIdx.x * H + j] = s_dw[j] + s_dw[H + j] + s_dw[2 * H + j] + s_dw[3 * H + j];
+}
+
+// dw[j] += sum over blocks of dw_part[:, j]  (fixed order)
+__global__ __launch_bounds__(256) void colsum_kernel(const float* part, int64_t nb, int64_t H, float* out) {
+  const int64_t j = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (j >= H) return;
+  float s = 0.f;
+  for (int64_t b = 0; b < nb; ++b) s += part[b * H + j];
+  out[j] += s;
+}
+
+// ------------------------------------------------------------------------------------------ SwiGLU
+// gu (N, 2I) = [gate | up] -> a (N, I) = silu(gate) * up   (two E-typed ops, as F.silu then * in the model)
+template <typename E>
+__global__ __launch_bounds__(256) void swiglu_fwd_kernel(const E* gu, E* out, int64_t N, int64_t I) {
+  const int64_t n = N * I;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int64_t row = i / I, c = i % I;
+    const float g = ldf(gu, row * 2 * I + c), u = ldf(gu, row * 2 * I + I + c);
+    const float sg = rnd<E>(g / (1.f + expf(-g)));
+    stf(out, i, sg * u);
+  }
+}
+
+// d gate = da * up * silu'(gate), d up = da * silu(gate)   ->   dgu (N, 2I)
+template <typename E>
+__global__ __launch_bounds__(256) void swiglu_bwd_kernel(const E* gu, const E* da, E* dgu, int64_t N, int64_t I) {
+  const int64_t n = N * I;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int64_t row = i / I, c = i % I;
+    const float g = ldf(gu, row * 2 * I + c);
+    const float u = ldf(gu, row * 2 * I + I + c);
+    const float d = ldf(da, i);
+    const float sig = 1.f / (1.f + expf(-g));
+    const float silu = rnd<E>(g * sig);
+    stf(dgu, row * 2 * I + c, rnd<E>(d * u) * (sig * (1.f + g * (1.f - sig))));
+    stf(dgu, row * 2 * I + I + c, d * silu);
+  }
+}
+
+int grid_stride(int64_t n, int threads = 256) {
+  return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>((n + threads - 1) / threads, static_cast<int64_t>(cu_count()) * 16)));
+}
+
+}  // namespace
+}  // namespace drl
+
+#define DRL_E_DISPATCH(dt, ...)                                   \
+  do {                                                          \
+    if ((dt) == DRL_BF16) { using E = uint16_t; __VA_ARGS__; }  \
+    else if ((dt) == DRL_F32) { using E = float; __VA_ARGS__; } \
+    else return ::drl::fail(DRL_ERR_INVALID, "dtype must be BF16 or F32"); \
+  } while (0)
+
+extern "C" {
+
+int drl_rope_qkv_fwd(const void* qkv, int32_t dt, const int64_t* position_ids, const float* cos_t, const float* sin_t,
+                     int64_t maxpos, int64_t B, int64_t T, int64_t Hq, int64_t Hkv, int64_t D, void* q, void* k,
+                     void* v, int64_t Tk, int64_t koff, void* stream) {
+  using namespace drl;
+  DRL_CHECK_ARG(qkv && position_ids && cos_t && sin_t && q && k && v, "NULL input");
+  DRL_CHECK_ARG(B >= 1 && T >= 1 && Hq >= 1 && Hkv >= 1 && Hq % Hkv == 0 && D % 2 == 0, "bad shape");
+  DRL_CHECK_ARG(koff >= 0 && koff + T <= Tk, "key offset out of range");
+  const int64_t n = B * T * (Hq + 2 * Hkv) * (D / 2);
+  DRL_E_DISPATCH(dt, {
+    RopeArgs<E> a{static_cast<const E*>(qkv), position_ids, cos_t, sin_t, static_cast<E*>(q), static_cast<E*>(k),
+                  static_cast<E*>(v), B, T, Hq, Hkv, D, Tk, koff, maxpos};
+    hipLaunchKernelGGL(rope_qkv_fwd_kernel<E>, dim3(grid_stride(n)), dim3(256), 0, static_cast<hipStream_t>(stream), a);
+  });
+  DRL_LAUNCH_CHECK();
+  return DRL_OK;
+}
+
+int drl_rope_qkv_bwd(const void* dq, const void* dk, const void* dv, int32_t dt, const int64_t* position_ids,
+                     const float* cos_t, const float* sin_t, int64_t maxpos, int64_t B, int64_t T, int64_t Hq,
+                     int64_t Hkv, int64_t D, void* dqkv, void* stream) {
+  using namespace drl;
+  DRL_CHECK_ARG(dq && dk && dv && position_ids && cos_t && sin_t && dqkv, "NULL input");
+  DRL_CHECK_ARG(B >= 1 && T >= 1 && Hq % Hkv == 0 && D % 2 == 0, "bad shape");
+  const int64_t n = B * T * (Hq + 2 * Hkv) * (D / 2);
+  DRL_E_DISPATCH(dt, {
+    RopeArgs<E> a{nullptr, position_ids, cos_t, sin_t, nullptr, nullptr, nullptr, B, T, Hq, Hkv, D, T, 0, maxpos};
+    hipLaunchKernelGGL(rope_qkv_bwd_kernel<E>, dim3(grid_stride(n)), dim3(256), 0, static_cast<hipStream_t>(stream), a,
+                       static_cast<const E*>(dq), static_cast<const E*>(dk), static_cast<const E*>(dv),
+                       static_cast<E*>(dqkv));
+  });
+  DRL_LAUNCH_CHECK();
+  return DRL_OK;
+}
+
+int drl_masked_softmax_fwd(const float* scores, void* probs, int32_t dt, const uint8_t* key_valid, int64_t ld_valid,
+                           int64_t B, int64_t HG, int64_t Tq, int64_t Tk, int64_t qoff, float scale, void* stream) {
+  using namespace drl;
+  DRL_CHECK_ARG(scores && probs && key_valid, "NULL input");
+  DRL_CHECK_ARG(B >= 1 && HG >= 1 && Tq >= 1 && Tk >= 1 && ld_valid >= Tk && qoff >= 0 && qoff + Tq <= Tk, "bad shape");
+  const int64_t rows = B * HG * Tq;
+  DRL_E_DISPATCH(dt, {
+    SoftmaxArgs<E> a{scores, static_cast<E*>(probs), key_valid, rows, Tq, Tk, HG, qoff, ld_valid, scale};
+    hipLaunchKernelGGL(masked_softmax_fwd_kernel<E>, dim3((rows + 3) / 4), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), a);
+  });
+  DRL_LAUNCH_CHECK();
+  return DRL_OK;
+}
+
+int drl_masked_softmax_bwd(const void* probs, const float* dprobs, void* dscores, int32_t dt, int64_t rows, int64_t Tk,
+                           float scale, void* stream) {
+  using namespace drl;
+  DRL_CHECK_ARG(probs && dprobs && dscores && rows >= 0 && Tk >= 1, "bad input");
+  if (rows == 0) return DRL_OK;
+  DRL_E_DISPATCH(dt, hipLaunchKernelGGL(masked_softmax_bwd_kernel<E>, dim3((rows + 3) / 4), dim3(256), 0,
+                                        static_cast<hipStream_t>(stream), static_cast<const E*>(probs), dprobs,
+                                        static_cast<E*>(dscores), rows, Tk, scale));
+  DRL_LAUNCH_CHECK();
+  return DRL_OK;
+}
+
+int drl_add_rmsnorm_fwd(const float* x_in, const void* delta, float* x_out, const float* weight, void* y, int32_t dt,
+                        float* rstd, int64_t N, int64_t H, float eps, void* stream) {
+  using namespace drl;
+  DRL_CHECK_ARG(x_in && weight && y, "NULL input");
+  DRL_CHECK_ARG(N >= 0 && H >= 4 && H % 4 == 0, "bad shape (H %% 4 == 0 required)");
+  if (N == 0) return DRL_OK;
+  DRL_E_DISPATCH(dt, hipLaunchKernelGGL(add_rmsnorm_fwd_kernel<E>, dim3((N + 3) / 4), dim3(256), 0,
+                                        static_cast<hipStream_t>(stream), x_in, static_cast<const E*>(delta), x_out,
+                                        weight, static_cast<E*>(y), rstd, N, H, eps));
+  DRL_LAUNCH_CHECK();
+  return DRL_OK;
+}
+
+size_t drl_rmsnorm_bwd_workspace_bytes(int64_t N, int64_t H) {
+  (void)N;
+  return static_cast<size_t>(drl::cu_count()) * 2 * static_cast<size_t>(H) * sizeof(float);
+}
+
+int drl_rmsnorm_bwd(const float* x, const float* weight, const float* rstd, const void* dy, int32_t dt, float* dx,
+                    float* dw, int64_t N, int64_t H, void* workspace, size_t workspace_bytes, void* stream) {
+  using namespace drl;
+  DRL_CHECK_ARG(x && weight && rstd && dy && dx && dw, "NULL input");
+  DRL_CHECK_ARG(N >= 1 && H >= 1 && 4 * H * sizeof(float) <= 64 * 1024, "bad shape");
+  const int grid = static_cast<int>(std::min<int64_t>(static_cast<int64_t>(cu_count()) * 2, (N + 3) / 4));
+  if (workspace == nullptr || workspace_bytes < static_cast<size_t>(grid) * H * sizeof(float))
+    return fail(DRL_ERR_WORKSPACE, "workspace too small");
+  float* part = static_cast<float*>(workspace);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  DRL_E_DISPATCH(dt, hipLaunchKernelGGL(rmsnorm_bwd_kernel<E>, dim3(grid), dim3(256), 4 * H * sizeof(float), s, x,
+                                        weight, rstd, static_cast<const E*>(dy), dx, part, N, H));
+  DRL_LAUNCH_CHECK();
+  hipLaunchKernelGGL(colsum_kernel, dim3((H + 255) / 256), dim3(256), 0, s, part, static_cast<int64_t>(grid), H, dw);
+  DRL_LAUNCH_CHECK();
+  return DRL_OK;
+}
+
+int drl_swiglu_fwd(const void* gate_up, void* out, int32_t dt, int64_t N, int64_t I, void* stream) {
+  using namespace drl;
+  DRL_CHECK_ARG(gate_up && out && N >= 0 && I >= 1, "bad input");
+  if (N == 0) return DRL_OK;
+  DRL_E_DISPATCH(dt, hipLaunchKernelGGL(swiglu_fwd_kernel<E>, dim3(grid_stride(N * I)), dim3(256), 0,
+                                        static_cast<hipStream_t>(stream), static_cast<const E*>(gate_up),
+                                        static_cast<E*>(out), N, I));
+  DRL_LAUNCH_CHECK();
+  return DRL_OK;
+}
+
+int drl_swiglu_bwd(const void* gate_up, const void* dout, void* dgate_up, int32_t dt, int64_t N, int64_t I,
+                   void* stream) {
+  using namespace drl;
+  DRL_CHECK_ARG(gate_up && dout && dgate_up && N >= 0 && I >= 1, "bad input");
+  if (N == 0) return DRL_OK;
+  DRL_E_DISPATCH(dt, hipLaunchKernelGGL(swiglu_bwd_kernel<E>, dim3(grid_stride(N * I)), dim3(256), 0,
+                                        static_cast<hipStream_t>(stream), static_cast<const E*>(gate_up),
+                                        static_cast<const E*>(dout), static_cast<E*>(dgate_up), N, I));
+  DRL_LAUNCH_CHECK();
+  return DRL_OK;
+}
+
+}  // extern "C"

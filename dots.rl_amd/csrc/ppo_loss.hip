@@ -1,33 +1,31 @@
 // K1 — fused actor loss (vanilla PPO clip + dual clip, entropy bonus, KL-to-ref), forward AND backward,
 // one pass over HBM. Replaces dp_actor.py:419-466 (+ core_algos.py:703-736, 815-889, 1272-1307).
 //
-// Layout: the (B, R) float32 inputs are flattened to N = B*R tokens; each workgroup of a persistent grid
-// (<= 2 per CU, all co-resident) owns one contiguous token range and walks it 4 tokens per lane
-// (16-B loads, 1 KiB per wave-instruction per input).
-// token-mean needs the global mask count before any gradient can be written, so that mode runs two
-// phases around a grid barrier: phase 1 reads ONLY the mask, counts it and keeps it on chip as a bit
-// image in LDS (one 64-bit ballot per wave and element slot); phase 2 reads the other inputs, takes the
-// mask bits from LDS and writes the gradients. Every input byte crosses HBM once. The other modes know
-// their gradient weights up front (seq-mean-token-mean gets per-row counts from a small pre-pass) and
-// run phase 2 only. Forward scalars: per-workgroup partials (double) reduced by the last workgroup in a
-// fixed order, so results are bitwise reproducible run to run.
+// Layout: the (B, R) float32 inputs are flattened to N = B*R tokens in 1024-token chunks; each workgroup
+// (<= 4 per CU) owns a contiguous run of chunks and walks it 4 tokens per lane (16-B loads, 1 KiB per
+// wave-instruction per input).
+// token-mean needs the global mask count before any gradient can be written. K1a streams ONLY the mask
+// (8 B/token for int64), writes it back as a 1-bit image (N/8 bytes, one 64-bit ballot per wave and
+// element slot) plus fixed-order partial counts; K1b sums those counts, reads the other inputs and the
+// bit image (1/8 B/token instead of 8) and writes the gradients: 36.25 B/token of traffic for 36 B/token
+// of algorithmic bytes, no grid barrier. The other modes know their gradient weights up front
+// (seq-mean-token-mean gets per-row counts from a small pre-pass) and run K1b alone. Forward scalars:
+// per-workgroup partials (double) reduced by the last workgroup in a fixed order, so the results are
+// bitwise reproducible run to run.
 #include "common.h"
 
 namespace drl {
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kTokPerIter = kThreads * 4;      // 1024 tokens per workgroup iteration
-constexpr int kBitWords = 4096;                // LDS bit image: 4096 x 64 bit = 32 KiB = 256 Ki tokens
+constexpr int kChunk = kThreads * 4;  // 1024 tokens: one workgroup iteration, 16 mask words (4 waves x 4 slots)
 constexpr int kNumPartials = 8;
 
-struct Header {          // zeroed on the stream before every launch
-  unsigned barrier;
+
+struct Header {  // zeroed on the stream before every call
   unsigned ticket;
-  unsigned timeout;
-  unsigned pad;
-  double mask_count;     // global sum(mask), published before the barrier
-  double pad2[6];
+  unsigned nonbinary;  // some mask value is not 0/1: K1b reads the original mask instead of the bits
+  unsigned pad[2];
 };
 
 struct Args {
@@ -37,35 +35,36 @@ struct Args {
   const void* mask;
   const float* ent;
   const float* ref;
-  const float* rowcnt;  // seq-mean-token-mean: sum(mask) per row
+  const float* rowcnt;               // seq-mean-token-mean: sum(mask) per row
+  const unsigned long long* bits;    // token-mean: packed mask (nullptr: read `mask`)
+  const double* pack_counts;         // token-mean: n_pack partial sums of the mask
+  int n_pack;
   float* dlp;
   float* dent;
   float* out;
   Header* hdr;
-  double* partials;     // gridDim.x * kNumPartials
+  double* partials;                  // gridDim.x * kNumPartials
   int64_t N, B, R;
   float lo, hi, clip_c, ent_coef, kl_coef, lsf;
   int mode, kl;
 };
 
 template <int MDT>
-__device__ __forceinline__ void load_mask4(const void* m, int64_t t, int64_t N, bool vec, float v[4]) {
-  if (vec && t + 3 < N) {
+__device__ __forceinline__ void load_mask4(const void* m, int64_t t, int64_t N, float v[4]) {
+  if (t + 3 < N) {
     if constexpr (MDT == DRL_I64) {
-      const int4* p = reinterpret_cast<const int4*>(static_cast<const int64_t*>(m) + t);
-      int4 a = p[0], b = p[1];
-      v[0] = static_cast<float>(static_cast<int64_t>((static_cast<uint64_t>(static_cast<uint32_t>(a.y)) << 32) | static_cast<uint32_t>(a.x)));
-      v[1] = static_cast<float>(static_cast<int64_t>((static_cast<uint64_t>(static_cast<uint32_t>(a.w)) << 32) | static_cast<uint32_t>(a.z)));
-      v[2] = static_cast<float>(static_cast<int64_t>((static_cast<uint64_t>(static_cast<uint32_t>(b.y)) << 32) | static_cast<uint32_t>(b.x)));
-      v[3] = static_cast<float>(static_cast<int64_t>((static_cast<uint64_t>(static_cast<uint32_t>(b.w)) << 32) | static_cast<uint32_t>(b.z)));
+      const longlong2* p = reinterpret_cast<const longlong2*>(static_cast<const int64_t*>(m) + t);
+      const longlong2 a = p[0], b = p[1];
+      v[0] = static_cast<float>(a.x); v[1] = static_cast<float>(a.y);
+      v[2] = static_cast<float>(b.x); v[3] = static_cast<float>(b.y);
     } else if constexpr (MDT == DRL_I32) {
-      int4 a = *reinterpret_cast<const int4*>(static_cast<const int32_t*>(m) + t);
+      const int4 a = *reinterpret_cast<const int4*>(static_cast<const int32_t*>(m) + t);
       v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
     } else if constexpr (MDT == DRL_U8) {
-      uint32_t a = *reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(m) + t);
+      const uint32_t a = *reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(m) + t);
       v[0] = a & 0xff; v[1] = (a >> 8) & 0xff; v[2] = (a >> 16) & 0xff; v[3] = a >> 24;
     } else {
-      float4 a = *reinterpret_cast<const float4*>(static_cast<const float*>(m) + t);
+      const float4 a = *reinterpret_cast<const float4*>(static_cast<const float*>(m) + t);
       v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
     }
   } else {
@@ -74,9 +73,9 @@ __device__ __forceinline__ void load_mask4(const void* m, int64_t t, int64_t N, 
   }
 }
 
-__device__ __forceinline__ void load4(const float* p, int64_t t, int64_t N, bool vec, float v[4]) {
-  if (vec && t + 3 < N) {
-    float4 a = *reinterpret_cast<const float4*>(p + t);
+__device__ __forceinline__ void load4(const float* p, int64_t t, int64_t N, float v[4]) {
+  if (t + 3 < N) {
+    const float4 a = *reinterpret_cast<const float4*>(p + t);
     v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
   } else {
 #pragma unroll
@@ -84,8 +83,8 @@ __device__ __forceinline__ void load4(const float* p, int64_t t, int64_t N, bool
   }
 }
 
-__device__ __forceinline__ void store4(float* p, int64_t t, int64_t N, bool vec, const float v[4]) {
-  if (vec && t + 3 < N) {
+__device__ __forceinline__ void store4(float* p, int64_t t, int64_t N, const float v[4]) {
+  if (t + 3 < N) {
     *reinterpret_cast<float4*>(p + t) = make_float4(v[0], v[1], v[2], v[3]);
   } else {
 #pragma unroll
@@ -99,25 +98,25 @@ __device__ __forceinline__ void kl_term(int kl, float lp, float ref, float& val,
   switch (kl) {
     case DRL_KL_K1: val = lp - ref; dval = 1.f; break;
     case DRL_KL_ABS: {
-      float d = lp - ref;
+      const float d = lp - ref;
       val = fabsf(d);
       dval = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
       break;
     }
     case DRL_KL_K2: {
-      float d = lp - ref;
+      const float d = lp - ref;
       val = 0.5f * (d * d);
       dval = d;
       break;
     }
     case DRL_KL_K3: {
-      float raw = ref - lp;
-      float k = fminf(fmaxf(raw, -20.f), 20.f);
-      float g1 = (raw >= -20.f && raw <= 20.f) ? 1.f : 0.f;
-      float r = expf(k);
-      float kld = (r - k) - 1.f;
+      const float raw = ref - lp;
+      const float k = fminf(fmaxf(raw, -20.f), 20.f);
+      const float g1 = (raw >= -20.f && raw <= 20.f) ? 1.f : 0.f;
+      const float r = expf(k);
+      const float kld = (r - k) - 1.f;
       val = fminf(fmaxf(kld, -10.f), 10.f);
-      float g2 = (kld >= -10.f && kld <= 10.f) ? 1.f : 0.f;
+      const float g2 = (kld >= -10.f && kld <= 10.f) ? 1.f : 0.f;
       dval = -(r - 1.f) * g1 * g2;
       break;
     }
@@ -125,82 +124,96 @@ __device__ __forceinline__ void kl_term(int kl, float lp, float ref, float& val,
   }
 }
 
-template <int MDT, bool TWO_PHASE>
-__global__ __launch_bounds__(kThreads) void ppo_loss_kernel(Args a) {
-  __shared__ unsigned long long bits[TWO_PHASE ? kBitWords : 1];
-  __shared__ double red[kThreads / kWave][kNumPartials];
-  __shared__ int wg_flags;  // bit0: keep mask on chip
-
+// K1a (token-mean only): stream the mask once; per 1024-token chunk store one 64-bit ballot per wave and
+// element slot (N/8 bytes in total) and accumulate sum(mask) per workgroup (fixed-order partials).
+template <int MDT>
+__global__ __launch_bounds__(kThreads) void mask_pack_kernel(const void* mask, int64_t N, unsigned long long* bits,
+                                                             double* counts, Header* hdr) {
+  constexpr int kU = 4;  // chunks in flight per lane (8 x 16-B loads for an int64 mask)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int64_t N = a.N;
-  // contiguous range per workgroup, multiple of 4 tokens
-  const int64_t per = ((N + gridDim.x - 1) / gridDim.x + 3) & ~int64_t(3);
-  const int64_t t_begin = min(N, per * blockIdx.x);
-  const int64_t t_end = min(N, t_begin + per);
-  const bool vec = true;  // host guarantees 16-B aligned bases; tails fall back to scalar
-
-  float inv_cnt_global = 0.f;
-  const int64_t n_iter = (t_end - t_begin + kTokPerIter - 1) / kTokPerIter;
-
-  if constexpr (TWO_PHASE) {
-    // ---- phase 1: mask -> count + on-chip bit image
-    if (tid == 0) wg_flags = (n_iter * 16 <= kBitWords) ? 1 : 0;
-    __syncthreads();
-    const bool keep = wg_flags & 1;
-    float cnt = 0.f;
-    bool nonbin = false;
-    for (int64_t it = 0; it < n_iter; ++it) {
-      const int64_t t = t_begin + it * kTokPerIter + tid * 4;
-      float m[4];
-      if (t < t_end) load_mask4<MDT>(a.mask, t, t_end, vec, m);
-      else m[0] = m[1] = m[2] = m[3] = 0.f;
+  const int64_t nchunks = (N + kChunk - 1) / kChunk;
+  float cnt = 0.f;
+  double dcnt = 0.0;
+  bool nonbin = false;
+  for (int64_t c0 = static_cast<int64_t>(blockIdx.x) * kU; c0 < nchunks; c0 += static_cast<int64_t>(gridDim.x) * kU) {
+    float m[kU][4];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int64_t t = (c0 + u) * kChunk + tid * 4;
+      if (c0 + u < nchunks) load_mask4<MDT>(mask, t, N, m[u]);
+      else m[u][0] = m[u][1] = m[u][2] = m[u][3] = 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        cnt += m[j];
-        nonbin |= (m[j] != 0.f && m[j] != 1.f);
-        unsigned long long b = __ballot(m[j] != 0.f);
-        if (keep && lane == 0) bits[(it * 4 + wave) * 4 + j] = b;
+        cnt += m[u][j];
+        nonbin |= (m[u][j] != 0.f && m[u][j] != 1.f);
+        const unsigned long long b = __ballot(m[u][j] != 0.f);
+        if (lane == 0 && c0 + u < nchunks) bits[(c0 + u) * 16 + wave * 4 + j] = b;
       }
     }
-    if (__any(nonbin) && lane == 0) atomicAnd(&wg_flags, ~1);
-    double c = wave_sum(static_cast<double>(cnt));
-    if (lane == 0) red[wave][0] = c;
-    __syncthreads();
-    if (tid == 0) {
-      double s = red[0][0] + red[1][0] + red[2][0] + red[3][0];
-      atomicAdd(&a.hdr->mask_count, s);
-    }
-    grid_barrier(&a.hdr->barrier, gridDim.x, &a.hdr->timeout);
-    const double total = __hip_atomic_load(&a.hdr->mask_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    inv_cnt_global = static_cast<float>(total);  // reuse as the token-mean denominator base
+    if (cnt >= 8388608.f) { dcnt += cnt; cnt = 0.f; }  // keep float partials exact
   }
-  const bool keep_bits = TWO_PHASE && (wg_flags & 1);
+  dcnt += cnt;
+  if (__any(nonbin) && lane == 0) atomicOr(&hdr->nonbinary, 1u);
+  dcnt = wave_sum(dcnt);
+  __shared__ double red[kThreads / kWave];
+  if (lane == 0) red[wave] = dcnt;
+  __syncthreads();
+  if (tid == 0) counts[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
 
-  // ---- phase 2: per-token loss terms, gradients, weighted partial sums
-  const float denom_tm = inv_cnt_global + 1e-8f;  // masked_mean: sum / (mask.sum() + 1e-8)
-  float s_pg = 0.f, s_clip = 0.f, s_kl = 0.f, s_cliplow = 0.f, s_ent = 0.f, s_kld = 0.f, s_cnt = 0.f;
+// K1b: per-token loss terms, gradients and the workgroup's partial sums. One contiguous run of
+// 1024-token chunks per workgroup; 4 tokens per lane per chunk.
+template <int MDT>
+__global__ __launch_bounds__(kThreads) void ppo_loss_kernel(Args a) {
+  __shared__ double red[kThreads / kWave][kNumPartials];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t N = a.N;
+  const int64_t nchunks = (N + kChunk - 1) / kChunk;
+  const int64_t per = (nchunks + gridDim.x - 1) / gridDim.x;
+  const int64_t c_begin = min(nchunks, per * blockIdx.x), c_end = min(nchunks, c_begin + per);
+
+  float cnt_total = 0.f;
+  bool use_bits = false;
+  if (a.mode == DRL_AGG_TOKEN_MEAN && a.bits != nullptr) {
+    // global mask count from the pack kernel's fixed-order partials
+    double v = 0.0;
+    for (int g = tid; g < a.n_pack; g += kThreads) v += a.pack_counts[g];
+    v = wave_sum(v);
+    if (lane == 0) red[wave][0] = v;
+    __syncthreads();
+    cnt_total = static_cast<float>(red[0][0] + red[1][0] + red[2][0] + red[3][0]);
+    use_bits = a.hdr->nonbinary == 0;
+    __syncthreads();
+  }
+  const float denom_tm = cnt_total + 1e-8f;       // masked_mean: sum / (mask.sum() + 1e-8)
+  const float inv_denom_tm = 1.0f / denom_tm;     // upstream / D once, then * mask (MeanBackward style)
+  const float inv_B = 1.0f / static_cast<float>(a.B), inv_R = 1.0f / static_cast<float>(a.R);
   const bool has_ent = a.ent != nullptr, has_kl = a.kl != DRL_KL_NONE;
   const bool want_dlp = a.dlp != nullptr, want_dent = a.dent != nullptr;
+  const bool tm = a.mode == DRL_AGG_TOKEN_MEAN, smtm = a.mode == DRL_AGG_SEQ_MEAN_TOKEN_MEAN;
+  float s_pg = 0.f, s_clip = 0.f, s_kl = 0.f, s_cliplow = 0.f, s_ent = 0.f, s_kld = 0.f, s_cnt = 0.f;
 
-  for (int64_t it = 0; it < n_iter; ++it) {
-    const int64_t t = t_begin + it * kTokPerIter + tid * 4;
-    if (t >= t_end) continue;
+  for (int64_t c = c_begin; c < c_end; ++c) {
+    const int64_t t = c * kChunk + tid * 4;
     float m[4], old[4], lp[4], A[4], en[4], rf[4];
-    if (keep_bits) {
+    if (use_bits) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) m[j] = (bits[(it * 4 + wave) * 4 + j] >> lane) & 1ull ? 1.f : 0.f;
+      for (int j = 0; j < 4; ++j) m[j] = ((a.bits[c * 16 + wave * 4 + j] >> lane) & 1ull) ? 1.f : 0.f;
     } else {
-      load_mask4<MDT>(a.mask, t, t_end, vec, m);
+      load_mask4<MDT>(a.mask, t, N, m);
     }
-    load4(a.old_lp, t, t_end, vec, old);
-    load4(a.lp, t, t_end, vec, lp);
-    load4(a.adv, t, t_end, vec, A);
-    if (has_ent) load4(a.ent, t, t_end, vec, en);
-    if (has_kl) load4(a.ref, t, t_end, vec, rf);
+    load4(a.old_lp, t, N, old);
+    load4(a.lp, t, N, lp);
+    load4(a.adv, t, N, A);
+    if (has_ent) load4(a.ent, t, N, en);
+    if (has_kl) load4(a.ref, t, N, rf);
     float g_lp[4], g_en[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const bool valid = t + j < t_end;
+      const bool valid = t + j < N;
       // compute_policy_loss_vanilla, float32 with the reference's op order
       const float raw = lp[j] - old[j];
       const float nkl = fminf(fmaxf(raw, -20.f), 20.f);
@@ -223,34 +236,26 @@ __global__ __launch_bounds__(kThreads) void ppo_loss_kernel(Args a) {
 
       const float mj = valid ? m[j] : 0.f;
       const bool mb = mj != 0.f;
-      // agg weight of this token (d agg / d loss_mat) and its forward contribution
+      // d agg / d loss_mat of this token, and its forward contribution
+      float rc_inv = 0.f;
+      if (smtm) rc_inv = 1.0f / a.rowcnt[valid ? (t + j) / a.R : 0];
       float w;
-      switch (a.mode) {
-        case DRL_AGG_TOKEN_MEAN: w = mb ? mj / denom_tm : 0.f; break;
-        case DRL_AGG_SEQ_MEAN_TOKEN_SUM: w = mj / static_cast<float>(a.B); break;
-        case DRL_AGG_SEQ_MEAN_TOKEN_MEAN: {
-          const int64_t row = (t + j) / a.R;
-          w = mj / (static_cast<float>(a.B) * a.rowcnt[valid ? row : 0]);
-          break;
-        }
-        default: w = mj / static_cast<float>(a.R); break;
-      }
-      // forward sums: token-mean uses where(mask, x, 0) * mask; the seq modes use x * mask
-      const bool tm = a.mode == DRL_AGG_TOKEN_MEAN;
+      if (tm) w = mb ? inv_denom_tm * mj : 0.f;
+      else if (a.mode == DRL_AGG_SEQ_MEAN_TOKEN_SUM) w = inv_B * mj;
+      else if (smtm) w = mj * (inv_B * rc_inv);
+      else w = inv_R * mj;
+      // token-mean sums where(mask, x, 0) * mask; the seq modes x * mask (core_algos.py:716-733)
       auto agg_val = [&](float x) -> float {
         if (tm) return mb ? x * mj : 0.f;
-        if (a.mode == DRL_AGG_SEQ_MEAN_TOKEN_MEAN) {
-          const int64_t row = (t + j) / a.R;
-          return (x * mj) / a.rowcnt[valid ? row : 0];
-        }
+        if (smtm) return (x * mj) * rc_inv;
         return x * mj;
       };
       if (valid) {
         s_pg += agg_val(pg);
         s_cnt += mj;
-        s_clip += mb ? (L2 > L1 ? mj : 0.f) : 0.f;
+        s_clip += (mb && L2 > L1) ? mj : 0.f;
         s_kl += mb ? -nkl * mj : 0.f;
-        s_cliplow += mb ? ((C1 > L3 && neg) ? mj : 0.f) : 0.f;
+        s_cliplow += (mb && C1 > L3 && neg) ? mj : 0.f;
       }
       float gl = w * dpg;
       if (has_kl) {
@@ -263,50 +268,48 @@ __global__ __launch_bounds__(kThreads) void ppo_loss_kernel(Args a) {
       g_lp[j] = a.lsf * gl;
       g_en[j] = a.ent_coef != 0.f ? a.lsf * (-a.ent_coef * w) : 0.f;
     }
-    if (want_dlp) store4(a.dlp, t, t_end, vec, g_lp);
-    if (want_dent) store4(a.dent, t, t_end, vec, g_en);
+    if (want_dlp) store4(a.dlp, t, N, g_lp);
+    if (want_dent) store4(a.dent, t, N, g_en);
   }
 
-  // ---- workgroup partials -> last workgroup reduces in a fixed order
+  // ---- workgroup partials -> the last workgroup reduces all of them in a fixed order
   const float vals[kNumPartials] = {s_pg, s_clip, s_kl, s_cliplow, s_ent, s_kld, s_cnt, 0.f};
 #pragma unroll
   for (int k = 0; k < kNumPartials; ++k) {
-    double v = wave_sum(static_cast<double>(vals[k]));
+    const double v = wave_sum(static_cast<double>(vals[k]));
     if (lane == 0) red[wave][k] = v;
   }
   __syncthreads();
-  if (tid < kNumPartials) {
-    double s = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
-    a.partials[blockIdx.x * kNumPartials + tid] = s;
-  }
+  if (tid < kNumPartials) a.partials[blockIdx.x * kNumPartials + tid] = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
   if (last_block_ticket(&a.hdr->ticket)) {
-    if (tid < kNumPartials) {
-      double s = 0.0;
-      for (unsigned g = 0; g < gridDim.x; ++g) s += a.partials[g * kNumPartials + tid];
-      red[0][tid] = s;
+#pragma unroll
+    for (int k = 0; k < kNumPartials; ++k) {
+      double v = 0.0;
+      for (unsigned g = tid; g < gridDim.x; g += kThreads) v += a.partials[g * kNumPartials + k];
+      v = wave_sum(v);
+      if (lane == 0) red[wave][k] = v;
     }
     __syncthreads();
     if (tid == 0) {
-      const double cnt = red[0][6];
+      double r[kNumPartials];
+      for (int k = 0; k < kNumPartials; ++k) r[k] = red[0][k] + red[1][k] + red[2][k] + red[3][k];
+      const double cnt = r[6];
       const double dm = static_cast<double>(static_cast<float>(cnt) + 1e-8f);
       auto agg = [&](double s) -> double {
-        switch (a.mode) {
-          case DRL_AGG_TOKEN_MEAN: return s / dm;
-          case DRL_AGG_SEQ_MEAN_TOKEN_SUM: return s / static_cast<double>(a.B);
-          case DRL_AGG_SEQ_MEAN_TOKEN_MEAN: return s / static_cast<double>(a.B);
-          default: return s / static_cast<double>(a.R);
-        }
+        if (a.mode == DRL_AGG_TOKEN_MEAN) return s / dm;
+        if (a.mode == DRL_AGG_SEQ_MEAN_TOKEN_SUM || a.mode == DRL_AGG_SEQ_MEAN_TOKEN_MEAN) return s / static_cast<double>(a.B);
+        return s / static_cast<double>(a.R);
       };
-      const double pg_loss = agg(red[0][0]);
-      const double ent_loss = has_ent ? agg(red[0][4]) : 0.0;
-      const double kl_loss = has_kl ? agg(red[0][5]) : 0.0;
+      const double pg_loss = agg(r[0]);
+      const double ent_loss = has_ent ? agg(r[4]) : 0.0;
+      const double kl_loss = has_kl ? agg(r[5]) : 0.0;
       double total = pg_loss;
       if (a.ent_coef != 0.f) total -= ent_loss * a.ent_coef;
       if (has_kl) total += kl_loss * a.kl_coef;
       a.out[DRL_PPO_OUT_PG_LOSS] = static_cast<float>(pg_loss);
-      a.out[DRL_PPO_OUT_PG_CLIPFRAC] = static_cast<float>(red[0][1] / dm);
-      a.out[DRL_PPO_OUT_PPO_KL] = static_cast<float>(red[0][2] / dm);
-      a.out[DRL_PPO_OUT_PG_CLIPFRAC_LOWER] = static_cast<float>(red[0][3] / dm);
+      a.out[DRL_PPO_OUT_PG_CLIPFRAC] = static_cast<float>(r[1] / dm);
+      a.out[DRL_PPO_OUT_PPO_KL] = static_cast<float>(r[2] / dm);
+      a.out[DRL_PPO_OUT_PG_CLIPFRAC_LOWER] = static_cast<float>(r[3] / dm);
       a.out[DRL_PPO_OUT_ENTROPY_LOSS] = static_cast<float>(ent_loss);
       a.out[DRL_PPO_OUT_KL_LOSS] = static_cast<float>(kl_loss);
       a.out[DRL_PPO_OUT_LOSS] = static_cast<float>(total * a.lsf);
@@ -327,30 +330,48 @@ __global__ __launch_bounds__(256) void row_count_kernel(const void* mask, int64_
   if (lane == 0) rowcnt[row] = c;
 }
 
+int max_grid() { return cu_count() * 4; }
+
+struct Layout {
+  size_t partials, rowcnt, counts, bits, total;
+};
+
+Layout ws_layout(int64_t B, int64_t R) {
+  Layout L{};
+  const size_t grid = static_cast<size_t>(max_grid());
+  const size_t nchunks = static_cast<size_t>((B * R + kChunk - 1) / kChunk);
+  L.partials = round_up(sizeof(Header), 256);
+  L.rowcnt = round_up(L.partials + grid * kNumPartials * sizeof(double), 256);
+  L.counts = round_up(L.rowcnt + static_cast<size_t>(B) * sizeof(float), 256);
+  L.bits = round_up(L.counts + grid * sizeof(double), 256);
+  L.total = round_up(L.bits + nchunks * 16 * sizeof(unsigned long long), 256);
+  return L;
+}
+
 template <int MDT>
-int launch(const Args& base, bool two_phase, int grid, hipStream_t s) {
-  if (base.mode == DRL_AGG_SEQ_MEAN_TOKEN_MEAN) {
-    hipLaunchKernelGGL(row_count_kernel<MDT>, dim3((base.B + 3) / 4), dim3(256), 0, s, base.mask, base.B, base.R,
-                       const_cast<float*>(base.rowcnt));
+int launch(Args a, const Layout& L, char* ws, hipStream_t s) {
+  if (a.mode == DRL_AGG_SEQ_MEAN_TOKEN_MEAN) {
+    hipLaunchKernelGGL(row_count_kernel<MDT>, dim3((a.B + 3) / 4), dim3(256), 0, s, a.mask, a.B, a.R,
+                       const_cast<float*>(a.rowcnt));
     DRL_LAUNCH_CHECK();
   }
-  if (two_phase)
-    hipLaunchKernelGGL((ppo_loss_kernel<MDT, true>), dim3(grid), dim3(kThreads), 0, s, base);
-  else
-    hipLaunchKernelGGL((ppo_loss_kernel<MDT, false>), dim3(grid), dim3(kThreads), 0, s, base);
+  const int64_t nchunks = (a.N + kChunk - 1) / kChunk;
+  if (a.mode == DRL_AGG_TOKEN_MEAN && (a.dlp != nullptr || a.dent != nullptr)) {
+    auto* bits = reinterpret_cast<unsigned long long*>(ws + L.bits);
+    auto* counts = reinterpret_cast<double*>(ws + L.counts);
+    const int g1 = static_cast<int>(std::min<int64_t>(max_grid(), (nchunks + 3) / 4));
+    hipLaunchKernelGGL(mask_pack_kernel<MDT>, dim3(g1), dim3(kThreads), 0, s, a.mask, a.N, bits, counts, a.hdr);
+    DRL_LAUNCH_CHECK();
+    a.bits = bits;
+    a.pack_counts = counts;
+    a.n_pack = g1;
+  }
+  // >= 2 chunks per workgroup before the grid reaches 4 workgroups per CU
+  const int grid = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(max_grid(), (nchunks + 1) / 2)));
+  hipLaunchKernelGGL(ppo_loss_kernel<MDT>, dim3(grid), dim3(kThreads), 0, s, a);
   DRL_LAUNCH_CHECK();
   return DRL_OK;
 }
-
-int max_grid() { return cu_count() * 2; }
-
-size_t ws_layout(int64_t B, size_t* off_partials, size_t* off_rowcnt) {
-  const size_t grid = static_cast<size_t>(max_grid());
-  *off_partials = round_up(sizeof(Header), 256);
-  *off_rowcnt = round_up(*off_partials + grid * kNumPartials * sizeof(double), 256);
-  return round_up(*off_rowcnt + static_cast<size_t>(B) * sizeof(float), 256);
-}
-
 
 __global__ __launch_bounds__(256) void kl_penalty_kernel(const float* lp, const float* ref, int64_t n, int kl, float* out) {
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
@@ -401,7 +422,7 @@ __global__ __launch_bounds__(256) void agg_loss_kernel(const float* x, const voi
 
 template <int MDT>
 int launch_agg(const float* x, const void* mask, int64_t B, int64_t R, int mode, char* ws, size_t off_part,
-               size_t off_row, float* out, hipStream_t s) {
+               size_t off_row, float* out, hipStream_t s) {  // workspace offsets from ws_layout()
   float* rowcnt = reinterpret_cast<float*>(ws + off_row);
   if (mode == DRL_AGG_SEQ_MEAN_TOKEN_MEAN) {
     hipLaunchKernelGGL(row_count_kernel<MDT>, dim3((B + 3) / 4), dim3(256), 0, s, mask, B, R, rowcnt);
@@ -419,11 +440,7 @@ int launch_agg(const float* x, const void* mask, int64_t B, int64_t R, int mode,
 
 extern "C" {
 
-size_t drl_ppo_loss_workspace_bytes(int64_t B, int64_t R) {
-  (void)R;
-  size_t a, b;
-  return drl::ws_layout(B, &a, &b);
-}
+size_t drl_ppo_loss_workspace_bytes(int64_t B, int64_t R) { return drl::ws_layout(B, R).total; }
 
 int drl_ppo_loss_fwd_bwd(const float* old_log_prob, const float* log_prob, const float* advantages,
                          const void* response_mask, int32_t mask_dtype, const float* entropy,
@@ -443,39 +460,35 @@ int drl_ppo_loss_fwd_bwd(const float* old_log_prob, const float* log_prob, const
                 "unsupported mask dtype %d", mask_dtype);
   const void* ptrs[] = {old_log_prob, log_prob, advantages, response_mask, entropy, ref_log_prob, dlog_prob, dentropy};
   for (const void* q : ptrs) DRL_CHECK_ARG(q == nullptr || aligned16(q), "tensor base not 16-byte aligned");
-  size_t off_part, off_row;
-  const size_t need = ws_layout(B, &off_part, &off_row);
-  if (workspace == nullptr || workspace_bytes < need)
-    return fail(DRL_ERR_WORKSPACE, "workspace %zu < %zu bytes", workspace_bytes, need);
+  const Layout L = ws_layout(B, R);
+  if (workspace == nullptr || workspace_bytes < L.total)
+    return fail(DRL_ERR_WORKSPACE, "workspace %zu < %zu bytes", workspace_bytes, L.total);
 
-  const int64_t N = B * R;
-  const int grid = static_cast<int>(std::min<int64_t>(max_grid(), (N + kTokPerIter - 1) / kTokPerIter));
   auto* ws = static_cast<char*>(workspace);
   Args a{};
   a.old_lp = old_log_prob; a.lp = log_prob; a.adv = advantages; a.mask = response_mask;
   a.ent = entropy; a.ref = p->kl_type == DRL_KL_NONE ? nullptr : ref_log_prob;
-  a.rowcnt = reinterpret_cast<const float*>(ws + off_row);
+  a.rowcnt = reinterpret_cast<const float*>(ws + L.rowcnt);
+  a.bits = nullptr; a.pack_counts = nullptr;
   a.dlp = dlog_prob; a.dent = dentropy; a.out = out_scalars;
   a.hdr = reinterpret_cast<Header*>(ws);
-  a.partials = reinterpret_cast<double*>(ws + off_part);
-  a.N = N; a.B = B; a.R = R;
+  a.partials = reinterpret_cast<double*>(ws + L.partials);
+  a.N = B * R; a.B = B; a.R = R;
   // python computes 1 - cliprange_low in double; torch.clamp then casts the bound to float32
   a.lo = static_cast<float>(1.0 - static_cast<double>(p->clip_ratio_low));
   a.hi = static_cast<float>(1.0 + static_cast<double>(p->clip_ratio_high));
   a.clip_c = p->clip_ratio_c; a.ent_coef = p->entropy_coeff; a.kl_coef = p->kl_loss_coef;
   a.lsf = p->loss_scale_factor; a.mode = p->loss_agg_mode; a.kl = p->kl_type;
-  const bool two_phase = (p->loss_agg_mode == DRL_AGG_TOKEN_MEAN) && (dlog_prob != nullptr || dentropy != nullptr);
 
   hipStream_t s = static_cast<hipStream_t>(stream);
   DRL_HIP(hipMemsetAsync(ws, 0, sizeof(Header), s));
   switch (mask_dtype) {
-    case DRL_I64: return launch<DRL_I64>(a, two_phase, grid, s);
-    case DRL_I32: return launch<DRL_I32>(a, two_phase, grid, s);
-    case DRL_U8: return launch<DRL_U8>(a, two_phase, grid, s);
-    default: return launch<DRL_F32>(a, two_phase, grid, s);
+    case DRL_I64: return launch<DRL_I64>(a, L, ws, s);
+    case DRL_I32: return launch<DRL_I32>(a, L, ws, s);
+    case DRL_U8: return launch<DRL_U8>(a, L, ws, s);
+    default: return launch<DRL_F32>(a, L, ws, s);
   }
 }
-
 
 int drl_kl_penalty(const float* log_prob, const float* ref_log_prob, int64_t n, int32_t kl_type, float* out,
                    void* stream) {
@@ -498,9 +511,9 @@ int drl_agg_loss(const float* loss_mat, const void* loss_mask, int32_t mdt, int6
   DRL_CHECK_ARG(loss_mat && loss_mask && out, "NULL input");
   DRL_CHECK_ARG(B >= 1 && R >= 1, "bad shape");
   DRL_CHECK_ARG(mode >= 0 && mode <= 3, "bad loss_agg_mode %d", mode);
-  size_t off_part, off_row;
-  const size_t need = ws_layout(B, &off_part, &off_row);
-  if (workspace == nullptr || workspace_bytes < need) return fail(DRL_ERR_WORKSPACE, "workspace too small");
+  const Layout L = ws_layout(B, R);
+  const size_t off_part = L.partials, off_row = L.rowcnt;
+  if (workspace == nullptr || workspace_bytes < L.total) return fail(DRL_ERR_WORKSPACE, "workspace too small");
   hipStream_t s = static_cast<hipStream_t>(stream);
   char* ws = static_cast<char*>(workspace);
   DRL_HIP(hipMemsetAsync(ws, 0, sizeof(Header), s));

@@ -57,11 +57,33 @@ __device__ __forceinline__ float scale_logit(float x, float temp, bool apply, bo
 // merge two online-softmax states (max m, sum_e s = sum exp(z-m), sum_ez t = sum exp(z-m)*z)
 __device__ __forceinline__ void merge_state(float& m, float& s, float& t, float m2, float s2, float t2) {
   const float mn = fmaxf(m, m2);
-  const float a = (m == -INFINITY) ? 0.f : expf(m - mn);
-  const float b = (m2 == -INFINITY) ? 0.f : expf(m2 - mn);
+  const float a = (m == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f((m - mn) * 1.4426950408889634f);
+  const float b = (m2 == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f((m2 - mn) * 1.4426950408889634f);
   s = s * a + s2 * b;
   t = t * a + t2 * b;
   m = mn;
+}
+
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr int kUnroll = 4;  // 16-B loads in flight per lane per step
+
+__device__ __forceinline__ float fast_exp(float x) { return __builtin_amdgcn_exp2f(x * kLog2e); }
+
+template <bool WANT_T>
+__device__ __forceinline__ void online_update(const float* v, int n, float& m, float& s, float& t) {
+  float mx = -INFINITY;
+  for (int k = 0; k < n; ++k) mx = fmaxf(mx, v[k]);
+  if (mx > m) {
+    const float sc = (m == -INFINITY) ? 0.f : fast_exp(m - mx);
+    s *= sc;
+    if (WANT_T) t *= sc;
+    m = mx;
+  }
+  for (int k = 0; k < n; ++k) {
+    const float e = fast_exp(v[k] - m);
+    s += e;
+    if (WANT_T) t = fmaf(e, v[k], t);
+  }
 }
 
 template <int DT, bool WANT_T, bool ROUND = true>
@@ -70,55 +92,34 @@ __device__ __forceinline__ void row_softmax_state(const void* row, int64_t V, bo
   constexpr int kV = Elem<DT>::kVec;
   m = -INFINITY; s = 0.f; t = 0.f;
   const int tid = threadIdx.x;
+  int64_t done = 0;
   if (vec) {
-    const int64_t nfull = V / kV;
-    for (int64_t c = tid; c < nfull; c += kThreads) {
+    const int64_t nfull = V / kV;  // vectors in the row
+    const int64_t nsteps = nfull / (kThreads * kUnroll);
+    for (int64_t st = 0; st < nsteps; ++st) {
+      float v[kUnroll][kV];
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u)
+        Elem<DT>::load_vec(row, ((st * kUnroll + u) * kThreads + tid) * kV, v[u]);
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {
+#pragma unroll
+        for (int k = 0; k < kV; ++k) v[u][k] = scale_logit<DT>(v[u][k], inv_t, apply_t, ROUND);
+      }
+      online_update<WANT_T>(&v[0][0], kUnroll * kV, m, s, t);
+    }
+    for (int64_t c = nsteps * kUnroll * kThreads + tid; c < nfull; c += kThreads) {
       float v[kV];
       Elem<DT>::load_vec(row, c * kV, v);
-      float mx = -INFINITY;
 #pragma unroll
-      for (int k = 0; k < kV; ++k) {
-        v[k] = scale_logit<DT>(v[k], inv_t, apply_t, ROUND);
-        mx = fmaxf(mx, v[k]);
-      }
-      if (mx > m) {
-        const float sc = (m == -INFINITY) ? 0.f : expf(m - mx);
-        s *= sc;
-        if (WANT_T) t *= sc;
-        m = mx;
-      }
-#pragma unroll
-      for (int k = 0; k < kV; ++k) {
-        const float e = expf(v[k] - m);
-        s += e;
-        if (WANT_T) t = fmaf(e, v[k], t);
-      }
+      for (int k = 0; k < kV; ++k) v[k] = scale_logit<DT>(v[k], inv_t, apply_t, ROUND);
+      online_update<WANT_T>(v, kV, m, s, t);
     }
-    for (int64_t i = nfull * kV + tid; i < V; i += kThreads) {
-      const float z = scale_logit<DT>(Elem<DT>::get(row, i), inv_t, apply_t, ROUND);
-      if (z > m) {
-        const float sc = (m == -INFINITY) ? 0.f : expf(m - z);
-        s *= sc;
-        if (WANT_T) t *= sc;
-        m = z;
-      }
-      const float e = expf(z - m);
-      s += e;
-      if (WANT_T) t = fmaf(e, z, t);
-    }
-  } else {
-    for (int64_t i = tid; i < V; i += kThreads) {
-      const float z = scale_logit<DT>(Elem<DT>::get(row, i), inv_t, apply_t, ROUND);
-      if (z > m) {
-        const float sc = (m == -INFINITY) ? 0.f : expf(m - z);
-        s *= sc;
-        if (WANT_T) t *= sc;
-        m = z;
-      }
-      const float e = expf(z - m);
-      s += e;
-      if (WANT_T) t = fmaf(e, z, t);
-    }
+    done = nfull * kV;
+  }
+  for (int64_t i = done + tid; i < V; i += kThreads) {
+    const float z = scale_logit<DT>(Elem<DT>::get(row, i), inv_t, apply_t, ROUND);
+    online_update<WANT_T>(&z, 1, m, s, t);
   }
   // wave then block merge
 #pragma unroll
@@ -173,7 +174,7 @@ __global__ __launch_bounds__(kThreads) void logprob_bwd_kernel(const void* logit
   auto grad = [&](float x, int64_t i) -> float {
     const float z = scale_logit<DT>(x, inv_t, apply_t);
     const float lp = z - L;
-    const float p = expf(lp);
+    const float p = fast_exp(lp);
     float g = -gl * p - ge * p * (lp + H);
     if (i == y) g += gl;
     return apply_t ? g / inv_t : g;
@@ -183,29 +184,46 @@ __global__ __launch_bounds__(kThreads) void logprob_bwd_kernel(const void* logit
     else static_cast<float*>(dlogits)[r * ld_out + i] = g;
   };
   const int tid = threadIdx.x;
+  auto store_vec = [&](int64_t c, const float* g) {
+    if constexpr (ODT == DRL_BF16) {
+      uint32_t w[kV / 2];
+#pragma unroll
+      for (int k = 0; k < kV / 2; ++k)
+        w[k] = static_cast<uint32_t>(f32_to_bf16(g[2 * k])) | (static_cast<uint32_t>(f32_to_bf16(g[2 * k + 1])) << 16);
+      if constexpr (kV == 8)
+        *reinterpret_cast<uint4*>(static_cast<uint16_t*>(dlogits) + r * ld_out + c * kV) = make_uint4(w[0], w[1], w[2], w[3]);
+      else
+        *reinterpret_cast<uint2*>(static_cast<uint16_t*>(dlogits) + r * ld_out + c * kV) = make_uint2(w[0], w[1]);
+    } else {
+#pragma unroll
+      for (int k = 0; k < kV; k += 4)
+        *reinterpret_cast<float4*>(static_cast<float*>(dlogits) + r * ld_out + c * kV + k) =
+            make_float4(g[k], g[k + 1], g[k + 2], g[k + 3]);
+    }
+  };
   if (vec) {
     const int64_t nfull = V / kV;
-    for (int64_t c = tid; c < nfull; c += kThreads) {
+    const int64_t nsteps = nfull / (kThreads * kUnroll);
+    for (int64_t st = 0; st < nsteps; ++st) {
+      float v[kUnroll][kV];
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) Elem<DT>::load_vec(row, ((st * kUnroll + u) * kThreads + tid) * kV, v[u]);
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {
+        const int64_t c = (st * kUnroll + u) * kThreads + tid;
+        float g[kV];
+#pragma unroll
+        for (int k = 0; k < kV; ++k) g[k] = grad(v[u][k], c * kV + k);
+        store_vec(c, g);
+      }
+    }
+    for (int64_t c = nsteps * kUnroll * kThreads + tid; c < nfull; c += kThreads) {
       float v[kV];
       Elem<DT>::load_vec(row, c * kV, v);
       float g[kV];
 #pragma unroll
       for (int k = 0; k < kV; ++k) g[k] = grad(v[k], c * kV + k);
-      if constexpr (ODT == DRL_BF16) {
-        uint32_t w[kV / 2];
-#pragma unroll
-        for (int k = 0; k < kV / 2; ++k)
-          w[k] = static_cast<uint32_t>(f32_to_bf16(g[2 * k])) | (static_cast<uint32_t>(f32_to_bf16(g[2 * k + 1])) << 16);
-        if constexpr (kV == 8)
-          *reinterpret_cast<uint4*>(static_cast<uint16_t*>(dlogits) + r * ld_out + c * kV) = make_uint4(w[0], w[1], w[2], w[3]);
-        else
-          *reinterpret_cast<uint2*>(static_cast<uint16_t*>(dlogits) + r * ld_out + c * kV) = make_uint2(w[0], w[1]);
-      } else {
-#pragma unroll
-        for (int k = 0; k < kV; k += 4)
-          *reinterpret_cast<float4*>(static_cast<float*>(dlogits) + r * ld_out + c * kV + k) =
-              make_float4(g[k], g[k + 1], g[k + 2], g[k + 3]);
-      }
+      store_vec(c, g);
     }
     for (int64_t i = nfull * kV + tid; i < V; i += kThreads) store(i, grad(Elem<DT>::get(row, i), i));
   } else {
@@ -268,7 +286,33 @@ __global__ __launch_bounds__(kThreads) void select_kernel(SelectArgs a) {
   if (!a.do_sample) {
     float bv = -INFINITY;
     int64_t bi = INT64_MAX;
-    for (int64_t i = tid; i < a.V; i += kThreads) {
+    int64_t done = 0;
+    if (a.vec) {
+      constexpr int kV = Elem<DT>::kVec;
+      const int64_t nfull = a.V / kV;
+      const int64_t nsteps = nfull / (kThreads * kUnroll);
+      for (int64_t st = 0; st < nsteps; ++st) {
+        float v[kUnroll][kV];
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) Elem<DT>::load_vec(row, ((st * kUnroll + u) * kThreads + tid) * kV, v[u]);
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+          const int64_t base = ((st * kUnroll + u) * kThreads + tid) * kV;
+#pragma unroll
+          for (int k = 0; k < kV; ++k)
+            if (argmax_better(v[u][k], base + k, bv, bi)) { bv = v[u][k]; bi = base + k; }
+        }
+      }
+      for (int64_t c = nsteps * kUnroll * kThreads + tid; c < nfull; c += kThreads) {
+        float v[kV];
+        Elem<DT>::load_vec(row, c * kV, v);
+#pragma unroll
+        for (int k = 0; k < kV; ++k)
+          if (argmax_better(v[k], c * kV + k, bv, bi)) { bv = v[k]; bi = c * kV + k; }
+      }
+      done = nfull * kV;
+    }
+    for (int64_t i = done + tid; i < a.V; i += kThreads) {
       const float v = Elem<DT>::get(row, i);
       if (argmax_better(v, i, bv, bi)) { bv = v; bi = i; }
     }

@@ -1,0 +1,181 @@
+"""DataParallelPPOActor on MI355X (mirror of verl/workers/actor/dp_actor.py:53-482).
+
+Same micro-batching, loss composition, gradient accumulation and metric keys as the reference; the
+numerics per micro-batch are: transformer forward (hipBLASLt GEMMs) -> lm_head on the R response
+positions only -> K2 log-prob/entropy over the vocabulary -> K1 fused actor loss (forward + backward in
+one launch) -> backward of the model from (d logp, d entropy). The optimizer step is the flat-buffer
+RCCL all-reduce + HIP grad-norm + HIP AdamW (FlatAdamW). Metric scalars stay on device until the end
+of update_policy (one host sync per call instead of one per micro-batch, dp_actor.py:468-479).
+"""
+
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.distributed as dist
+
+from . import native
+from .core_algos import fused_actor_loss
+from .protocol import DataProto
+from .qwen2 import Qwen2Model
+from .torch_functional import logprobs_and_entropy_from_logits
+
+
+def append_to_dict(data: dict, new: dict):
+    for k, v in new.items():
+        data.setdefault(k, []).append(v)
+
+
+class FlatAdamW:
+    """torch.optim.AdamW over the ParamStore's flat fp32 buffers (fsdp_workers.py:454-459 hyper-parameters),
+    with clip_grad_norm_ + skip-if-non-finite (dp_actor.py:282-298) fused into the HIP step kernel.
+    LR schedule: constant with linear warmup (verl/utils/torch_functional.py get_constant_schedule_with_warmup)."""
+
+    def __init__(self, store, lr, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01, max_grad_norm=1.0,
+                 warmup_steps=0, group=None):
+        self.store = store
+        self.lr = lr
+        self.betas = betas
+        self.eps = eps
+        self.weight_decay = weight_decay
+        self.max_grad_norm = max_grad_norm
+        self.warmup_steps = warmup_steps
+        self.group = group
+        self.exp_avg = torch.zeros_like(store.master)
+        self.exp_avg_sq = torch.zeros_like(store.master)
+        self.step_count = 0
+        self.sched_step = 0
+        self.norm = torch.zeros(1, dtype=torch.float32, device=store.master.device)
+
+    def current_lr(self):
+        if self.warmup_steps > 0 and self.sched_step < self.warmup_steps:
+            return self.lr * float(self.sched_step) / float(max(1, self.warmup_steps))
+        return self.lr
+
+    def zero_grad(self):
+        self.store.zero_grad()
+
+    def step(self):
+        """All-reduce (average) the flat gradient across DP ranks, then norm -> clip -> AdamW in HIP.
+        Returns the device grad-norm tensor (the reference returns clip_grad_norm_'s total norm)."""
+        g = self.store.grad
+        if dist.is_initialized() and dist.get_world_size(self.group) > 1:
+            dist.all_reduce(g, op=dist.ReduceOp.AVG, group=self.group)
+        native.grad_norm(g, out=self.norm)
+        self.step_count += 1
+        params_bf16 = None if self.store.compute is self.store.master else self.store.compute
+        native.adamw_step(self.store.master, g, self.exp_avg, self.exp_avg_sq, lr=self.current_lr(),
+                          beta1=self.betas[0], beta2=self.betas[1], eps=self.eps, weight_decay=self.weight_decay,
+                          step=self.step_count, max_grad_norm=self.max_grad_norm, grad_norm_t=self.norm,
+                          params_bf16=params_bf16)
+        return self.norm
+
+    def state_dict(self):
+        return {"exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq, "step": self.step_count,
+                "sched_step": self.sched_step}
+
+    def load_state_dict(self, sd):
+        self.exp_avg.copy_(sd["exp_avg"])
+        self.exp_avg_sq.copy_(sd["exp_avg_sq"])
+        self.step_count = int(sd["step"])
+        self.sched_step = int(sd.get("sched_step", 0))
+
+
+class DataParallelPPOActor:
+    """dp_actor.py:53-482. ``actor_optimizer`` None -> reference policy."""
+
+    def __init__(self, config, actor_module: Qwen2Model, actor_optimizer: FlatAdamW | None = None):
+        self.config = config
+        self.actor_module = actor_module
+        self.actor_optimizer = actor_optimizer
+        self.use_remove_padding = config.get("use_remove_padding", False)
+        self.use_fused_kernels = config.get("use_fused_kernels", False)
+
+    def _forward_micro_batch(self, micro_batch, temperature, calculate_entropy=False):
+        """dp_actor.py:90-280 (padded path): full-sequence forward, logits only at the R positions that
+        predict the response ([:, -R-1:-1]), then K2. Returns (entropy or None, log_probs), (bs, R) fp32."""
+        m = self.actor_module
+        responses = micro_batch["responses"]
+        B, R = responses.shape
+        h = m.hidden_states(micro_batch["input_ids"], micro_batch["attention_mask"], micro_batch["position_ids"])
+        h = h[:, -R - 1:-1, :].reshape(B * R, h.shape[-1])
+        logits = m.logits(h)
+        logp, ent = logprobs_and_entropy_from_logits(logits, responses.reshape(-1), temperature, calculate_entropy,
+                                                     inplace_backward=True)
+        return (ent.view(B, R) if ent is not None else None), logp.view(B, R)
+
+    @torch.no_grad()
+    def compute_log_prob(self, data: DataProto, calculate_entropy=False):
+        """dp_actor.py:300-359."""
+        self.actor_module.training = False
+        micro_batch_size = data.meta_info["micro_batch_size"]
+        temperature = data.meta_info["temperature"]
+        assert not data.meta_info.get("use_dynamic_bsz", False), "dynamic bsz is not supported yet"
+        data = data.select(batch_keys=["responses", "input_ids", "attention_mask", "position_ids"])
+        lps, ents = [], []
+        for mb in data.split(micro_batch_size):
+            ent, lp = self._forward_micro_batch(mb.batch, temperature, calculate_entropy)
+            lps.append(lp)
+            if calculate_entropy:
+                ents.append(ent)
+        log_probs = torch.cat(lps, 0)
+        return log_probs, (torch.cat(ents, 0) if calculate_entropy else None)
+
+    def update_policy(self, data: DataProto):
+        """dp_actor.py:361-482."""
+        cfg = self.config
+        m = self.actor_module
+        m.training = True
+        temperature = data.meta_info["temperature"]
+        keys = ["responses", "response_mask", "input_ids", "attention_mask", "position_ids", "old_log_probs",
+                "advantages"]
+        if cfg.use_kl_loss:
+            keys.append("ref_log_prob")
+        data = data.select(batch_keys=keys)
+        mini_batches = data.split(cfg.ppo_mini_batch_size)
+        loss_mode = cfg.policy_loss.get("loss_mode", "vanilla")
+        if loss_mode != "vanilla":
+            raise NotImplementedError(f"policy loss {loss_mode}: only the vanilla (PPO clip + dual clip) loss is fused")
+        lo = cfg.clip_ratio_low if cfg.get("clip_ratio_low") is not None else cfg.clip_ratio
+        hi = cfg.clip_ratio_high if cfg.get("clip_ratio_high") is not None else cfg.clip_ratio
+        mb_out, mb_lsf, grad_norms = [], [], []
+        for _ in range(cfg.ppo_epochs):
+            for mini_batch in mini_batches:
+                grad_accum = cfg.ppo_mini_batch_size // cfg.ppo_micro_batch_size_per_gpu
+                micro_batches = mini_batch.split(cfg.ppo_micro_batch_size_per_gpu)
+                self.actor_optimizer.zero_grad()
+                for micro_batch in micro_batches:
+                    mb = micro_batch.batch
+                    lsf = 1.0 / grad_accum
+                    calculate_entropy = cfg.entropy_coeff != 0
+                    entropy, log_prob = self._forward_micro_batch(mb, temperature, calculate_entropy)
+                    out = fused_actor_loss(
+                        log_prob, entropy, mb["old_log_probs"], mb["advantages"], mb["response_mask"],
+                        mb.get("ref_log_prob"), clip_ratio_low=lo, clip_ratio_high=hi,
+                        clip_ratio_c=cfg.get("clip_ratio_c", 3.0), entropy_coeff=cfg.entropy_coeff,
+                        use_kl_loss=cfg.use_kl_loss, kl_loss_type=cfg.kl_loss_type, kl_loss_coef=cfg.kl_loss_coef,
+                        loss_agg_mode=cfg.loss_agg_mode, loss_scale_factor=lsf)
+                    out[6].backward()
+                    mb_out.append(out.detach())
+                    mb_lsf.append(lsf)
+                grad_norms.append(self.actor_optimizer.step().clone())
+        self.actor_optimizer.zero_grad()
+        m.training = False
+        # one device->host copy for every metric of the call
+        stats = torch.stack(mb_out).cpu().tolist() if mb_out else []
+        gn = torch.cat(grad_norms).cpu().tolist() if grad_norms else []
+        metrics: dict = {}
+        for row, lsf in zip(stats, mb_lsf):
+            mbm = {}
+            if cfg.use_kl_loss:
+                mbm["actor/kl_loss"] = row[5] * lsf
+                mbm["actor/kl_coef"] = cfg.kl_loss_coef
+            mbm.update({"actor/pg_loss": row[0] * lsf, "actor/pg_clipfrac": row[1], "actor/ppo_kl": row[2],
+                        "actor/pg_clipfrac_lower": row[3]})
+            append_to_dict(metrics, mbm)
+        for g in gn:
+            if not math.isfinite(g):
+                print(f"WARN: grad_norm is not finite: {g}")
+            append_to_dict(metrics, {"actor/grad_norm": g})
+        return metrics

@@ -1,0 +1,66 @@
+"""Step metrics with the reference's keys (verl/trainer/ppo/metric_utils.py:80-302)."""
+
+from __future__ import annotations
+
+from typing import Any
+
+import numpy as np
+import torch
+
+from .protocol import DataProto
+
+
+def reduce_metrics(metrics: dict) -> dict:
+    """metric_utils.py reduce_metrics: mean of each list."""
+    return {k: float(np.mean(v)) if isinstance(v, (list, tuple)) else v for k, v in metrics.items()}
+
+
+def _response_info(batch: DataProto):
+    R = batch.batch["responses"].shape[-1]
+    am = batch.batch["attention_mask"]
+    return {"prompt_length": am[:, :-R].sum(-1).float(), "response_length": am[:, -R:].sum(-1).float(),
+            "response_mask": am[:, -R:].bool()}
+
+
+def compute_data_metrics(batch: DataProto, use_critic: bool = False) -> dict[str, Any]:
+    """metric_utils.py:80-224 (critic entries only when use_critic)."""
+    b = batch.batch
+    seq_score = b["token_level_scores"].sum(-1)
+    seq_reward = b["token_level_rewards"].sum(-1)
+    R = b["responses"].shape[-1]
+    info = _response_info(batch)
+    rmask = b["response_mask"].bool()
+    adv = torch.masked_select(b["advantages"], rmask)
+    ret = torch.masked_select(b["returns"], rmask)
+    P = b["attention_mask"].shape[-1] - R
+    vals = torch.stack([
+        seq_score.mean(), seq_score.max(), seq_score.min(), seq_reward.mean(), seq_reward.max(), seq_reward.min(),
+        adv.mean(), adv.max(), adv.min(), ret.mean(), ret.max(), ret.min(),
+        info["response_length"].mean(), info["response_length"].max(), info["response_length"].min(),
+        (info["response_length"] == R).float().mean(),
+        info["prompt_length"].mean(), info["prompt_length"].max(), info["prompt_length"].min(),
+        (info["prompt_length"] == P).float().mean()]).cpu().tolist()
+    keys = ["critic/score/mean", "critic/score/max", "critic/score/min", "critic/rewards/mean", "critic/rewards/max",
+            "critic/rewards/min", "critic/advantages/mean", "critic/advantages/max", "critic/advantages/min",
+            "critic/returns/mean", "critic/returns/max", "critic/returns/min", "response_length/mean",
+            "response_length/max", "response_length/min", "response_length/clip_ratio", "prompt_length/mean",
+            "prompt_length/max", "prompt_length/min", "prompt_length/clip_ratio"]
+    return dict(zip(keys, vals))
+
+
+def compute_timing_metrics(batch: DataProto, timing_raw: dict) -> dict[str, Any]:
+    """metric_utils.py:227-266."""
+    info = _response_info(batch)
+    n_prompt = float(info["prompt_length"].sum().item())
+    n_resp = float(info["response_length"].sum().item())
+    n_all = n_prompt + n_resp
+    sec = {"gen": n_resp, **{k: n_all for k in ["ref", "values", "adv", "update_critic", "update_actor"]}}
+    return {**{f"timing_s/{k}": v for k, v in timing_raw.items()},
+            **{f"timing_per_token_ms/{k}": timing_raw[k] * 1000 / sec[k] for k in set(sec) & set(timing_raw)}}
+
+
+def compute_throughout_metrics(batch: DataProto, timing_raw: dict, n_gpus: int) -> dict[str, Any]:
+    """metric_utils.py:269-302: perf/throughput = sum(attention-mask tokens) / (t_step * n_gpus)."""
+    total = sum(batch.meta_info["global_token_num"])
+    t = timing_raw["step"]
+    return {"perf/total_num_tokens": total, "perf/time_per_step": t, "perf/throughput": total / (t * n_gpus)}

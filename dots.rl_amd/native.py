@@ -256,3 +256,63 @@ def adamw_step(params, grads, exp_avg, exp_avg_sq, *, lr, beta1, beta2, eps, wei
                           float(max_grad_norm))
     check(lib().drl_adamw_step(_p(params), _p(grads), _p(exp_avg), _p(exp_avg_sq), _p(params_bf16), params.numel(),
                                ctypes.byref(hp), _p(grad_norm_t), _stream()), "drl_adamw_step")
+
+
+# ----------------------------------------------------------------------------------------------- layers
+def _edt(t):
+    try:
+        return _LOGIT_DTYPES[t.dtype]
+    except KeyError as e:
+        raise ValueError(f"activation dtype {t.dtype} not supported (bfloat16 / float32)") from e
+
+
+def rope_qkv_fwd(qkv, position_ids, cos_t, sin_t, Hq, Hkv, D, q, k, v, koff=0):
+    """qkv (B,T,(Hq+2Hkv)D) -> q (B,Hkv,G,T,D); k, v written at [:, :, koff:koff+T] of (B,Hkv,Tk,D)."""
+    B, T = qkv.shape[0], qkv.shape[1]
+    check(lib().drl_rope_qkv_fwd(_p(qkv), _edt(qkv), _p(position_ids), _p(cos_t), _p(sin_t), cos_t.shape[0], B, T,
+                                 Hq, Hkv, D, _p(q), _p(k), _p(v), k.shape[2], koff, _stream()), "drl_rope_qkv_fwd")
+
+
+def rope_qkv_bwd(dq, dk, dv, position_ids, cos_t, sin_t, Hq, Hkv, D, dqkv):
+    B, T = dqkv.shape[0], dqkv.shape[1]
+    check(lib().drl_rope_qkv_bwd(_p(dq), _p(dk), _p(dv), _edt(dq), _p(position_ids), _p(cos_t), _p(sin_t),
+                                 cos_t.shape[0], B, T, Hq, Hkv, D, _p(dqkv), _stream()), "drl_rope_qkv_bwd")
+
+
+def masked_softmax_fwd(scores_f32, probs, key_valid_u8, B, HG, Tq, Tk, qoff, scale):
+    """fp32 scores (B,Hkv,G,Tq,Tk) -> probs (activation dtype)."""
+    assert scores_f32.dtype == torch.float32
+    check(lib().drl_masked_softmax_fwd(_p(scores_f32), _p(probs), _edt(probs), _p(key_valid_u8),
+                                       key_valid_u8.stride(0), B, HG, Tq, Tk, qoff, float(scale), _stream()),
+          "drl_masked_softmax_fwd")
+
+
+def masked_softmax_bwd(probs, dprobs_f32, dscores, rows, Tk, scale):
+    assert dprobs_f32.dtype == torch.float32
+    check(lib().drl_masked_softmax_bwd(_p(probs), _p(dprobs_f32), _p(dscores), _edt(probs), rows, Tk, float(scale),
+                                       _stream()), "drl_masked_softmax_bwd")
+
+
+def add_rmsnorm_fwd(x_in, delta, x_out, weight, y, rstd, eps):
+    N, H = x_in.numel() // x_in.shape[-1], x_in.shape[-1]
+    check(lib().drl_add_rmsnorm_fwd(_p(x_in), _p(delta), _p(x_out), _p(weight), _p(y), _edt(y), _p(rstd), N, H,
+                                    float(eps), _stream()), "drl_add_rmsnorm_fwd")
+
+
+def rmsnorm_bwd(x, weight, rstd, dy, dx, dw):
+    N, H = x.numel() // x.shape[-1], x.shape[-1]
+    L = lib()
+    ws = _ws.get(L.drl_rmsnorm_bwd_workspace_bytes(N, H), x.device)
+    check(L.drl_rmsnorm_bwd(_p(x), _p(weight), _p(rstd), _p(dy), _edt(dy), _p(dx), _p(dw), N, H, _p(ws), ws.numel(),
+                            _stream()), "drl_rmsnorm_bwd")
+
+
+def swiglu_fwd(gate_up, out):
+    N, I2 = gate_up.numel() // gate_up.shape[-1], gate_up.shape[-1]
+    check(lib().drl_swiglu_fwd(_p(gate_up), _p(out), _edt(gate_up), N, I2 // 2, _stream()), "drl_swiglu_fwd")
+
+
+def swiglu_bwd(gate_up, dout, dgate_up):
+    N, I2 = gate_up.numel() // gate_up.shape[-1], gate_up.shape[-1]
+    check(lib().drl_swiglu_bwd(_p(gate_up), _p(dout), _p(dgate_up), _edt(gate_up), N, I2 // 2, _stream()),
+          "drl_swiglu_bwd")

@@ -1,0 +1,451 @@
+"""Qwen2 decoder (Qwen2.5-0.5B architecture) laid out for MI355X training + decode.
+
+Parameters live in three flat device buffers (``ParamStore``): fp32 master weights, a compute copy (bf16)
+that the GEMMs read, and fp32 gradients. The optimizer (HIP AdamW kernel) updates the master buffer and
+rewrites the bf16 copy in the same pass; data-parallel gradient averaging is a single RCCL all-reduce of
+the flat gradient; GEMM weight gradients accumulate straight into fp32 (hipBLASLt bf16 x bf16 -> fp32),
+so micro-batch accumulation never rounds through bf16.
+
+Per decoder layer the GEMMs run on hipBLASLt and everything else on the HIP kernels of
+``csrc/layers.hip``: residual-add + RMSNorm, QKV split + RoPE + grouped-query re-layout (the 7 query
+heads of a KV head become one GEMM's rows, so K/V are never expanded), causal + key-padding masked
+softmax over fp32 scores, SwiGLU; the backward of a whole layer is hand-written (``_DecoderLayer``).
+Decode uses the same kernels against a preallocated KV cache.
+
+Semantics follow HF ``Qwen2ForCausalLM`` as the reference runs it (dp_actor.py:110 autocast bf16 over
+fp32 master weights): bf16 GEMM inputs with fp32 accumulation, fp32 RMSNorm and residual stream, fp32
+attention scores, bf16 probabilities into the PV GEMM. ``compute_dtype=float32`` runs the same kernels
+in fp32 end to end (the parity model checked against HF / golden greedy tokens).
+"""
+
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import torch
+import torch.nn.functional as F
+
+from . import native
+
+
+@dataclass
+class Qwen2Config:
+    vocab_size: int = 151936
+    hidden_size: int = 896
+    intermediate_size: int = 4864
+    num_hidden_layers: int = 24
+    num_attention_heads: int = 14
+    num_key_value_heads: int = 2
+    rope_theta: float = 1000000.0
+    rms_norm_eps: float = 1e-6
+    tie_word_embeddings: bool = True
+    initializer_range: float = 0.02
+    max_position_embeddings: int = 32768
+    bos_token_id: int = 151643
+    eos_token_id: int = 151645
+    pad_token_id: int = 151643
+    extra: dict = field(default_factory=dict)
+
+    @property
+    def head_dim(self):
+        return self.hidden_size // self.num_attention_heads
+
+    @classmethod
+    def from_dict(cls, d):
+        known = {k: v for k, v in d.items() if k in cls.__dataclass_fields__}
+        return cls(**known)
+
+
+def param_specs(cfg: Qwen2Config):
+    """(name, shape, kind) in buffer order; kind: 'gemm' (read through the compute copy) or 'small' (fp32)."""
+    H, I, hd = cfg.hidden_size, cfg.intermediate_size, cfg.head_dim
+    qkv = (cfg.num_attention_heads + 2 * cfg.num_key_value_heads) * hd
+    specs = [("embed_tokens", (cfg.vocab_size, H), "gemm")]
+    for i in range(cfg.num_hidden_layers):
+        p = f"layers.{i}."
+        specs += [
+            (p + "input_layernorm", (H,), "small"),
+            (p + "qkv_proj.weight", (qkv, H), "gemm"),
+            (p + "qkv_proj.bias", (qkv,), "small"),
+            (p + "o_proj", (H, cfg.num_attention_heads * hd), "gemm"),
+            (p + "post_attention_layernorm", (H,), "small"),
+            (p + "gate_up_proj", (2 * I, H), "gemm"),
+            (p + "down_proj", (H, I), "gemm"),
+        ]
+    specs.append(("norm", (H,), "small"))
+    if not cfg.tie_word_embeddings:
+        specs.append(("lm_head", (cfg.vocab_size, H), "gemm"))
+    return specs
+
+
+class ParamStore:
+    """Flat parameter/gradient buffers with named views (64-element = 256-B aligned offsets)."""
+
+    ALIGN = 64
+
+    def __init__(self, cfg: Qwen2Config, device, compute_dtype=torch.bfloat16, trainable=True):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.compute_dtype = compute_dtype
+        self.trainable = trainable
+        self.specs = param_specs(cfg)
+        self.offsets = {}
+        off = 0
+        for name, shape, kind in self.specs:
+            n = math.prod(shape)
+            self.offsets[name] = (off, shape, kind)
+            off += (n + self.ALIGN - 1) // self.ALIGN * self.ALIGN
+        self.numel = off
+        self.n_params = sum(math.prod(s) for _, s, _ in self.specs)
+        self.master = torch.zeros(off, dtype=torch.float32, device=self.device)
+        self.compute = self.master if compute_dtype == torch.float32 else torch.zeros(off, dtype=compute_dtype,
+                                                                                     device=self.device)
+        self.grad = torch.zeros(off, dtype=torch.float32, device=self.device) if trainable else None
+        self._views = {}
+        for name, (o, shape, kind) in self.offsets.items():
+            n = math.prod(shape)
+            w = (self.master if kind == "small" else self.compute)[o:o + n].view(shape)
+            g = self.grad[o:o + n].view(shape) if trainable else None
+            self._views[name] = (w, g)
+
+    def w(self, name):
+        return self._views[name][0]
+
+    def g(self, name):
+        return self._views[name][1]
+
+    @torch.no_grad()
+    def init_random(self, seed: int):
+        """HF Qwen2 init: N(0, initializer_range) for matrices, ones for norms, zeros for biases."""
+        gen = torch.Generator(device=self.device).manual_seed(seed)
+        for name, (o, shape, kind) in self.offsets.items():
+            dst = self.master[o:o + math.prod(shape)]
+            if name.endswith("layernorm") or name == "norm":
+                dst.fill_(1.0)
+            elif name.endswith("bias"):
+                dst.zero_()
+            else:
+                dst.normal_(0.0, self.cfg.initializer_range, generator=gen)
+        self.refresh_compute()
+
+    @torch.no_grad()
+    def refresh_compute(self):
+        if self.compute is not self.master:
+            self.compute.copy_(self.master)
+
+    @torch.no_grad()
+    def load_state_dict_hf(self, sd: dict):
+        """Load HF Qwen2ForCausalLM weights (q/k/v and gate/up are concatenated into the fused layouts)."""
+        cfg = self.cfg
+
+        def put(name, t):
+            o, shape, _ = self.offsets[name]
+            self.master[o:o + math.prod(shape)].copy_(t.reshape(-1).to(torch.float32))
+
+        put("embed_tokens", sd["model.embed_tokens.weight"])
+        for i in range(cfg.num_hidden_layers):
+            p, q = f"model.layers.{i}.", f"layers.{i}."
+            put(q + "input_layernorm", sd[p + "input_layernorm.weight"])
+            put(q + "qkv_proj.weight", torch.cat([sd[p + f"self_attn.{x}_proj.weight"] for x in "qkv"], 0))
+            put(q + "qkv_proj.bias", torch.cat([sd[p + f"self_attn.{x}_proj.bias"] for x in "qkv"], 0))
+            put(q + "o_proj", sd[p + "self_attn.o_proj.weight"])
+            put(q + "post_attention_layernorm", sd[p + "post_attention_layernorm.weight"])
+            put(q + "gate_up_proj", torch.cat([sd[p + "mlp.gate_proj.weight"], sd[p + "mlp.up_proj.weight"]], 0))
+            put(q + "down_proj", sd[p + "mlp.down_proj.weight"])
+        put("norm", sd["model.norm.weight"])
+        if not cfg.tie_word_embeddings:
+            put("lm_head", sd["lm_head.weight"])
+        self.refresh_compute()
+
+    def zero_grad(self):
+        if self.grad is not None:
+            self.grad.zero_()
+
+
+# --------------------------------------------------------------------------------------------- GEMM helpers
+def acc_wgrad(gw, dy, x):
+    """gw (out, in) fp32 += dy^T x  with dy (N, out), x (N, in) in the compute dtype (hipBLASLt, fp32 out)."""
+    if dy.dtype == torch.float32:
+        gw.addmm_(dy.t(), x)
+    else:
+        gw.copy_(torch.addmm(gw, dy.t(), x, out_dtype=torch.float32))
+
+
+def bmm_f32(a, b):
+    """Batched a @ b (bf16 or fp32 inputs) with an fp32 result (hipBLASLt)."""
+    if a.dtype == torch.float32:
+        return torch.bmm(a, b)
+    return torch.bmm(a, b, out_dtype=torch.float32)
+
+
+class _Linear(torch.autograd.Function):
+    """y = x W^T on hipBLASLt; backward dx = dy W, dW += dy^T x in fp32 (lm_head over the response rows)."""
+
+    @staticmethod
+    def forward(ctx, x, w, gw, dummy):
+        ctx.save_for_backward(x, w)
+        ctx.gw = gw
+        return F.linear(x, w)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dy = dy.contiguous()
+        if ctx.gw is not None:
+            acc_wgrad(ctx.gw, dy.reshape(-1, dy.shape[-1]), x.reshape(-1, x.shape[-1]))
+        return dy @ w, None, None, None
+
+
+class _Embedding(torch.autograd.Function):
+    """fp32 residual stream input; backward scatter-adds into the fp32 embedding gradient."""
+
+    @staticmethod
+    def forward(ctx, ids, w, gw, dummy):
+        ctx.save_for_backward(ids)
+        ctx.gw = gw
+        return F.embedding(ids, w).to(torch.float32)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (ids,) = ctx.saved_tensors
+        if ctx.gw is not None:
+            ctx.gw.index_add_(0, ids.reshape(-1), dy.reshape(-1, dy.shape[-1]).to(torch.float32))
+        return None, None, None, None
+
+
+# --------------------------------------------------------------------------------------------- decoder layer
+def _layer_forward(m, i, x_prev, delta, pos, key_valid, save, cache=None, koff=0):
+    """x = x_prev (+ delta); returns (x2 = x + attn(x), mlp_out) — the next consumer adds them.
+
+    ``save`` (dict or None) receives the activations the hand-written backward needs."""
+    cfg, s, dt = m.cfg, m.store, m.dtype
+    B, T, H = x_prev.shape
+    Hq, Hkv, D = cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim
+    G = Hq // Hkv
+    p = f"layers.{i}."
+    dev = x_prev.device
+    x = torch.empty_like(x_prev) if delta is not None else x_prev
+    h1 = torch.empty(B, T, H, dtype=dt, device=dev)
+    rstd1 = torch.empty(B * T, dtype=torch.float32, device=dev) if save is not None else None
+    native.add_rmsnorm_fwd(x_prev, delta, x if delta is not None else None, s.w(p + "input_layernorm"), h1, rstd1,
+                           cfg.rms_norm_eps)
+    qkv = torch.addmm(s.w(p + "qkv_proj.bias").to(dt), h1.view(B * T, H), s.w(p + "qkv_proj.weight").t())
+    qkv = qkv.view(B, T, -1)
+    q = torch.empty(B, Hkv, G, T, D, dtype=dt, device=dev)
+    if cache is None:
+        kbuf = torch.empty(B, Hkv, T, D, dtype=dt, device=dev)
+        vbuf = torch.empty_like(kbuf)
+        koff = 0
+    else:
+        kbuf, vbuf = cache.k[i], cache.v[i]
+    native.rope_qkv_fwd(qkv, pos, m.cos, m.sin, Hq, Hkv, D, q, kbuf, vbuf, koff)
+    L = koff + T
+    k3 = kbuf[:, :, :L].reshape(B * Hkv, L, D)
+    v3 = vbuf[:, :, :L].reshape(B * Hkv, L, D)
+    q3 = q.view(B * Hkv, G * T, D)
+    S = bmm_f32(q3, k3.transpose(1, 2))  # (B*Hkv, G*T, L) fp32 scores
+    P = torch.empty(B * Hkv, G * T, L, dtype=dt, device=dev)
+    native.masked_softmax_fwd(S, P, key_valid, B, Hkv * G, T, L, L - T, 1.0 / math.sqrt(D))
+    del S
+    O = torch.bmm(P, v3)  # (B*Hkv, G*T, D)
+    if T == 1:
+        attn = O.view(B, 1, Hq * D)
+    else:
+        attn = O.view(B, Hkv, G, T, D).permute(0, 3, 1, 2, 4).reshape(B, T, Hq * D)
+    o = attn.view(B * T, Hq * D) @ s.w(p + "o_proj").t()
+    x2 = torch.empty_like(x)
+    h2 = torch.empty(B, T, H, dtype=dt, device=dev)
+    rstd2 = torch.empty(B * T, dtype=torch.float32, device=dev) if save is not None else None
+    native.add_rmsnorm_fwd(x, o, x2, s.w(p + "post_attention_layernorm"), h2, rstd2, cfg.rms_norm_eps)
+    gu = h2.view(B * T, H) @ s.w(p + "gate_up_proj").t()
+    a = torch.empty(B * T, cfg.intermediate_size, dtype=dt, device=dev)
+    native.swiglu_fwd(gu, a)
+    mlp = (a @ s.w(p + "down_proj").t()).view(B, T, H)
+    if save is not None:
+        save.update(x=x, rstd1=rstd1, h1=h1, q=q, k=kbuf, v=vbuf, P=P, attn=attn, x2=x2, rstd2=rstd2, h2=h2,
+                    gu=gu, a=a)
+    return x2, mlp
+
+
+class _DecoderLayer(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x_prev, delta, m, i, pos, key_valid):
+        save = {}
+        x2, mlp = _layer_forward(m, i, x_prev, delta, pos, key_valid, save)
+        ctx.m, ctx.i, ctx.save, ctx.pos = m, i, save, pos
+        ctx.has_delta = delta is not None
+        return x2, mlp
+
+    @staticmethod
+    def backward(ctx, g_x2, g_mlp):
+        m, i, sv = ctx.m, ctx.i, ctx.save
+        cfg, s, dt = m.cfg, m.store, m.dtype
+        p = f"layers.{i}."
+        B, T, H = sv["x"].shape
+        Hq, Hkv, D = cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim
+        G = Hq // Hkv
+        N = B * T
+        dx2 = g_x2.to(torch.float32).contiguous().clone()
+        dm = g_mlp.to(dt).contiguous().view(N, H)
+        # MLP
+        da = dm @ s.w(p + "down_proj")
+        acc_wgrad(s.g(p + "down_proj"), dm, sv["a"])
+        dgu = torch.empty_like(sv["gu"])
+        native.swiglu_bwd(sv["gu"], da, dgu)
+        dh2 = dgu @ s.w(p + "gate_up_proj")
+        acc_wgrad(s.g(p + "gate_up_proj"), dgu, sv["h2"].view(N, H))
+        native.rmsnorm_bwd(sv["x2"], s.w(p + "post_attention_layernorm"), sv["rstd2"], dh2, dx2,
+                           s.g(p + "post_attention_layernorm"))
+        # attention output projection
+        do = dx2.to(dt).view(N, H)
+        dattn = do @ s.w(p + "o_proj")
+        acc_wgrad(s.g(p + "o_proj"), do, sv["attn"].reshape(N, Hq * D))
+        dO = dattn.view(B, T, Hkv, G, D).permute(0, 2, 3, 1, 4).reshape(B * Hkv, G * T, D)
+        q3 = sv["q"].view(B * Hkv, G * T, D)
+        k3 = sv["k"].view(B * Hkv, T, D)
+        v3 = sv["v"].view(B * Hkv, T, D)
+        P = sv["P"]
+        dP = bmm_f32(dO, v3.transpose(1, 2))  # fp32 (B*Hkv, G*T, T)
+        dv = torch.bmm(P.transpose(1, 2), dO)  # (B*Hkv, T, D): sums the 7 query heads of the group
+        dS = torch.empty_like(P)
+        native.masked_softmax_bwd(P, dP, dS, B * Hkv * G * T, T, 1.0 / math.sqrt(D))
+        del dP
+        dq = torch.bmm(dS, k3)
+        dk = torch.bmm(dS.transpose(1, 2), q3)
+        dqkv = torch.empty(B, T, (Hq + 2 * Hkv) * D, dtype=dt, device=dx2.device)
+        native.rope_qkv_bwd(dq, dk, dv, ctx.pos, m.cos, m.sin, Hq, Hkv, D, dqkv)
+        dqkv2 = dqkv.view(N, -1)
+        dh1 = dqkv2 @ s.w(p + "qkv_proj.weight")
+        acc_wgrad(s.g(p + "qkv_proj.weight"), dqkv2, sv["h1"].view(N, H))
+        s.g(p + "qkv_proj.bias").add_(dqkv2.sum(0, dtype=torch.float32))
+        dx = dx2  # residual: x2 = x + o
+        native.rmsnorm_bwd(sv["x"], s.w(p + "input_layernorm"), sv["rstd1"], dh1, dx, s.g(p + "input_layernorm"))
+        ctx.save = None
+        return dx, (dx.to(g_mlp.dtype) if ctx.has_delta else None), None, None, None, None
+
+
+class _FinalNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x_prev, delta, m):
+        x = torch.empty_like(x_prev)
+        h = torch.empty(x_prev.shape, dtype=m.dtype, device=x_prev.device)
+        rstd = torch.empty(x_prev.numel() // x_prev.shape[-1], dtype=torch.float32, device=x_prev.device)
+        native.add_rmsnorm_fwd(x_prev, delta, x, m.store.w("norm"), h, rstd, m.cfg.rms_norm_eps)
+        ctx.save_for_backward(x, rstd)
+        ctx.m = m
+        ctx.delta_dtype = delta.dtype
+        return h
+
+    @staticmethod
+    def backward(ctx, dh):
+        x, rstd = ctx.saved_tensors
+        m = ctx.m
+        dx = torch.zeros_like(x)
+        native.rmsnorm_bwd(x, m.store.w("norm"), rstd, dh.contiguous(), dx, m.store.g("norm"))
+        return dx, dx.to(ctx.delta_dtype), None
+
+
+class KVCache:
+    """Per-layer K/V for decode: (B, Hkv, Tmax, D) in the compute dtype, plus the key-valid mask (u8)."""
+
+    def __init__(self, cfg: Qwen2Config, B, Tmax, device, dtype):
+        self.k = [torch.empty(B, cfg.num_key_value_heads, Tmax, cfg.head_dim, device=device, dtype=dtype)
+                  for _ in range(cfg.num_hidden_layers)]
+        self.v = [torch.empty_like(t) for t in self.k]
+        self.valid = torch.zeros(B, Tmax, dtype=torch.uint8, device=device)
+        self.len = 0
+
+
+class Qwen2Model:
+    """Functional Qwen2 over a ParamStore (no nn.Module: the parameters are views into flat buffers)."""
+
+    def __init__(self, cfg: Qwen2Config, store: ParamStore):
+        self.cfg = cfg
+        self.store = store
+        self.dtype = store.compute_dtype
+        self.training = False
+        dev = store.device
+        half = cfg.head_dim // 2
+        inv_freq = 1.0 / (cfg.rope_theta ** (torch.arange(0, cfg.head_dim, 2, dtype=torch.int64, device=dev).float()
+                                             / cfg.head_dim))
+        t = torch.arange(cfg.max_position_embeddings, device=dev, dtype=torch.float32)
+        freqs = t[:, None] * inv_freq[None, :half]
+        self.cos = freqs.cos().contiguous()
+        self.sin = freqs.sin().contiguous()
+        self._dummy = torch.empty(0, device=dev, requires_grad=True)
+
+    def _gw(self, name):
+        return self.store.g(name) if (self.training and self.store.trainable) else None
+
+    def lm_head_weight(self):
+        return "embed_tokens" if self.cfg.tie_word_embeddings else "lm_head"
+
+    def logits(self, h):
+        """h (N, H) in the compute dtype -> (N, V) logits in the compute dtype (hipBLASLt)."""
+        name = self.lm_head_weight()
+        if self.training and self.store.trainable:
+            return _Linear.apply(h, self.store.w(name), self.store.g(name), self._dummy)
+        return F.linear(h, self.store.w(name))
+
+    def hidden_states(self, input_ids, attention_mask, position_ids):
+        """Full-sequence forward -> final-norm hidden states (B, T, H) in the compute dtype."""
+        cfg = self.cfg
+        key_valid = attention_mask.to(torch.uint8).contiguous()
+        pos = position_ids.contiguous()
+        if self.training and self.store.trainable:
+            x = _Embedding.apply(input_ids, self.store.w("embed_tokens"), self.store.g("embed_tokens"), self._dummy)
+            delta = None
+            for i in range(cfg.num_hidden_layers):
+                x, delta = _DecoderLayer.apply(x, delta, self, i, pos, key_valid)
+            return _FinalNorm.apply(x, delta, self)
+        with torch.no_grad():
+            x = F.embedding(input_ids, self.store.w("embed_tokens")).to(torch.float32)
+            delta = None
+            for i in range(cfg.num_hidden_layers):
+                x, delta = _layer_forward(self, i, x, delta, pos, key_valid, None)
+            return self._final_norm(x, delta)
+
+    def _final_norm(self, x, delta):
+        h = torch.empty(x.shape, dtype=self.dtype, device=x.device)
+        native.add_rmsnorm_fwd(x, delta, None, self.store.w("norm"), h, None, self.cfg.rms_norm_eps)
+        return h
+
+    # ----------------------------------------------------------------------------------- decode
+    @torch.no_grad()
+    def prefill(self, cache: KVCache, input_ids, attention_mask, position_ids):
+        """Prompt pass writing the KV cache; returns the last position's hidden state (B, H)."""
+        cfg = self.cfg
+        B, T = input_ids.shape
+        cache.valid[:, :T] = attention_mask.to(torch.uint8)
+        pos = position_ids.contiguous()
+        x = F.embedding(input_ids, self.store.w("embed_tokens")).to(torch.float32)
+        delta = None
+        for i in range(cfg.num_hidden_layers):
+            x, delta = _layer_forward(self, i, x, delta, pos, cache.valid, None, cache, 0)
+        cache.len = T
+        return self._final_norm(x[:, -1:].contiguous(), delta[:, -1:].contiguous())[:, 0]
+
+    @torch.no_grad()
+    def decode_step(self, cache: KVCache, tokens, positions):
+        """One token per sequence at cache position cache.len; returns (B, H) hidden."""
+        cfg = self.cfg
+        t = cache.len
+        x = F.embedding(tokens[:, None], self.store.w("embed_tokens")).to(torch.float32)
+        cache.valid[:, t] = 1
+        pos = positions[:, None].contiguous()
+        delta = None
+        for i in range(cfg.num_hidden_layers):
+            x, delta = _layer_forward(self, i, x, delta, pos, cache.valid, None, cache, t)
+        cache.len = t + 1
+        return self._final_norm(x, delta)[:, 0]
+
+
+def flops_per_token(cfg: Qwen2Config, seqlen: int) -> float:
+    """flops_counter.py:135-167 convention: 2 * N_dense per token forward (embedding + lm_head counted)
+    plus attention 2 * 2 * s * d * h * L."""
+    H, I, L, V = cfg.hidden_size, cfg.intermediate_size, cfg.num_hidden_layers, cfg.vocab_size
+    hd = cfg.head_dim
+    q, kv = cfg.num_attention_heads * hd, cfg.num_key_value_heads * hd
+    dense = L * (H * (q + 2 * kv) + q * H + 3 * H * I) + 2 * V * H
+    return 2 * dense + 4 * seqlen * hd * cfg.num_attention_heads * L

@@ -1,0 +1,98 @@
+"""Rollout engine: HFRollout semantics (verl/workers/rollout/hf_rollout.py:39-177) on our own decode loop.
+
+Prefill of the left-padded prompts into a preallocated KV cache, then one decode step per response token
+whose token selection (greedy / temperature sampling, EOS -> pad for finished rows) is the HIP kernel K4
+writing straight into the ``responses`` column. Outputs match HFRollout's keys and post-processing:
+``prompts, responses, input_ids, attention_mask, position_ids`` with responses padded to response_length,
+position ids continuing from the last prompt position and the response attention mask from the first EOS.
+The actor's bf16 compute buffer is read directly: no weight resharding between training and rollout.
+"""
+
+from __future__ import annotations
+
+import time
+
+import torch
+
+from . import native
+from .protocol import DataProto, TensorBatch
+from .qwen2 import KVCache, Qwen2Model
+from .torch_functional import get_response_mask
+
+
+class MI355XRollout:
+    def __init__(self, module: Qwen2Model, config, dp_rank: int = 0):
+        self.module = module
+        self.config = config
+        self.dp_rank = dp_rank
+        self.calls = 0
+
+    def generate_sequences(self, prompts: DataProto) -> DataProto:
+        """hf_rollout.py:45-51: optional micro-batching of the prompt batch."""
+        n = len(prompts)
+        mbs = self.config.get("micro_batch_size") or n
+        chunks = prompts.chunk(max(n // mbs, 1)) if n > mbs else [prompts]
+        outs = [self._generate_minibatch(p, i * len(chunks[0])) for i, p in enumerate(chunks)]
+        self.calls += 1
+        return DataProto.concat(outs) if len(outs) > 1 else outs[0]
+
+    @torch.no_grad()
+    def _generate_minibatch(self, prompts: DataProto, row_offset: int) -> DataProto:
+        cfg = self.config
+        mi = prompts.meta_info
+        do_sample = mi.get("do_sample", cfg.do_sample)
+        is_validate = mi.get("validate", False)
+        temperature = mi.get("temperature", cfg.temperature)
+        response_length = mi.get("response_length", cfg.response_length)
+        top_p = mi.get("top_p", cfg.get("top_p", 1.0))
+        top_k = max(0, mi.get("top_k", cfg.get("top_k", 0)))
+        if is_validate and do_sample:
+            vk = cfg.val_kwargs
+            top_k, top_p, temperature = max(0, vk.top_k), vk.top_p, vk.temperature
+        eos = mi["eos_token_id"]
+        pad_token_id = mi["pad_token_id"]
+        eos_list = eos if isinstance(eos, (list, tuple)) else [eos]
+
+        idx = prompts.batch["input_ids"]
+        attention_mask = prompts.batch["attention_mask"]
+        position_ids = prompts.batch["position_ids"]
+        B, P = idx.shape
+        R = int(response_length)
+        dev = idx.device
+        m = self.module
+        m.training = False
+        cache = KVCache(m.cfg, B, P + R, dev, m.dtype)
+        t0 = time.perf_counter()
+        h = m.prefill(cache, idx, attention_mask, position_ids)
+        torch.cuda.synchronize()
+        self.last_prefill_s = time.perf_counter() - t0
+        responses = torch.empty(B, R, dtype=torch.int64, device=dev)
+        unfinished = torch.ones(B, dtype=torch.int32, device=dev)
+        eos_t = torch.tensor(eos_list, dtype=torch.int64, device=dev)
+        stop_ids = None if cfg.get("ignore_eos", False) else eos_t
+        last_pos = position_ids[:, -1]
+        seed = int(cfg.get("seed", 0)) + 7919 * self.calls
+        row_base = self.dp_rank * (1 << 32) + row_offset
+        for t in range(R):
+            logits = m.logits(h)
+            native.select_tokens(logits, responses[:, t], do_sample=do_sample and temperature > 0,
+                                 temperature=temperature if do_sample else 1.0, top_k=top_k, top_p=top_p, seed=seed,
+                                 step=t, row_base=row_base, pad_token_id=pad_token_id, eos_ids=stop_ids,
+                                 unfinished=unfinished)
+            if t + 1 < R:
+                h = m.decode_step(cache, responses[:, t], last_pos + 1 + t)
+        del cache
+        seq = torch.cat([idx, responses], dim=-1)
+        # hf_rollout.py:151-160: positions continue from the last prompt position; mask up to first EOS
+        full_pos = torch.empty(B, P + R, dtype=torch.int64, device=dev)
+        full_pos[:, :P] = position_ids
+        native.response_position_ids_(full_pos, P)
+        resp_mask = get_response_mask(responses, eos_list, dtype=attention_mask.dtype)
+        batch = TensorBatch({
+            "prompts": idx,
+            "responses": responses,
+            "input_ids": seq,
+            "attention_mask": torch.cat([attention_mask, resp_mask], dim=-1),
+            "position_ids": full_pos,
+        }, batch_size=B)
+        return DataProto(batch=batch)

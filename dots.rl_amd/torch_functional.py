@@ -1,0 +1,81 @@
+"""Vocabulary-side and rollout-bookkeeping functions with the reference's names (verl/utils/torch_functional.py,
+verl/utils/model.py), computed by the HIP kernels K2 (logp/entropy over the vocabulary) and A4/A5.
+"""
+
+from __future__ import annotations
+
+import torch
+
+from . import native
+
+
+class _LogprobEntropy(torch.autograd.Function):
+    """K2 forward (one pass: logp of the label, entropy, logsumexp) and K2 backward (one pass writing
+    d logits, in place over the logits buffer when the caller no longer needs them)."""
+
+    @staticmethod
+    def forward(ctx, logits, labels, temperature, want_entropy, inplace_backward):
+        logp, ent, lse = native.logprob_entropy_fwd(logits, labels, temperature, want_entropy=want_entropy)
+        ctx.save_for_backward(logits, labels, lse, ent if ent is not None else lse.new_empty(0))
+        ctx.temperature = temperature
+        ctx.inplace = inplace_backward
+        ctx.want_entropy = want_entropy
+        shape = labels.shape
+        if ent is None:
+            ent = logp.new_zeros(0)
+        else:
+            ent = ent.view(shape)
+        return logp.view(shape), ent
+
+    @staticmethod
+    def backward(ctx, dlogp, dent):
+        logits, labels, lse, ent = ctx.saved_tensors
+        if not ctx.want_entropy:
+            dent = None
+        out = logits if ctx.inplace and logits.is_contiguous() else None
+        dlogits = native.logprob_entropy_bwd(logits, labels, ctx.temperature, dlogp, dent, lse,
+                                             ent if dent is not None else None, out=out.view(-1, logits.shape[-1])
+                                             if out is not None else None)
+        return dlogits.view(logits.shape), None, None, None, None
+
+
+def logprobs_and_entropy_from_logits(logits, labels, temperature=1.0, calculate_entropy=True, inplace_backward=True):
+    """log p(label) and entropy of softmax(logits / T) — the pair _forward_micro_batch computes
+    (dp_actor.py:195-211, 263-272), in one read of the logits. Returns (log_probs, entropy or None), fp32."""
+    logp, ent = _LogprobEntropy.apply(logits, labels, float(temperature), bool(calculate_entropy), inplace_backward)
+    return logp, (ent if calculate_entropy else None)
+
+
+def logprobs_from_logits(logits, labels, inplace_backward=True):
+    """torch_functional.py:64-92 (flash-attn CE semantics: fp32 result)."""
+    return logprobs_and_entropy_from_logits(logits, labels, 1.0, False, inplace_backward)[0]
+
+
+def entropy_from_logits(logits: torch.Tensor):
+    """torch_functional.py:145-149."""
+    labels = torch.zeros(logits.shape[:-1], dtype=torch.int64, device=logits.device)
+    return logprobs_and_entropy_from_logits(logits, labels, 1.0, True, False)[1]
+
+
+def masked_sum(values, mask, axis=None):
+    """torch_functional.py:163-168."""
+    assert axis is None, "only the full reduction is on the hot path"
+    return masked_mean(values, mask) * (mask.sum() + 1e-8)
+
+
+def masked_mean(values, mask, axis=None):
+    """torch_functional.py:171-185 — token-mean reduction of the agg kernel."""
+    assert axis is None, "only the full reduction is on the hot path"
+    return native.agg_loss(values, mask, "token-mean")
+
+
+def get_response_mask(response_id: torch.Tensor, eos_token=2, dtype=torch.int64):
+    """torch_functional.py:226-246 — 1 up to and including the first EOS."""
+    eos = torch.tensor(eos_token if isinstance(eos_token, (list, tuple)) else [eos_token], dtype=torch.int64,
+                       device=response_id.device)
+    return native.response_mask(response_id.contiguous(), eos, dtype=dtype)
+
+
+def compute_position_id_with_mask(mask):
+    """utils/model.py:219."""
+    return native.position_ids(mask)

@@ -1,0 +1,217 @@
+"""RayPPOTrainer.fit() dataflow on the SPMD single controller (mirror of verl/trainer/ppo/ray_trainer.py).
+
+One PPO step (ray_trainer.py:1104-1399): prompts -> uid -> repeat(n, interleave) -> generate_sequences ->
+union -> response_mask -> (balance_batch) -> global_token_num -> reward -> compute_log_prob (old log-probs
++ entropy) -> compute_ref_log_prob -> advantage (GRPO / GAE on device) -> update_actor -> metrics.
+The "driver" runs on every rank (SPMD); worker-group calls dispatch this rank's DP chunk and all-gather
+the outputs, so the full batch is resident in each rank's HBM between stages (no object-store hops).
+"""
+
+from __future__ import annotations
+
+import time
+import uuid
+from contextlib import contextmanager
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import core_algos
+from .core_algos import AdvantageEstimator, agg_loss
+from .metric_utils import compute_data_metrics, compute_throughout_metrics, compute_timing_metrics, reduce_metrics
+from .protocol import DataProto
+from .reward import SyntheticBernoulliRewardManager, compute_reward
+from .single_controller import SPMDWorkerGroup
+from .workers import ActorRolloutRefWorker
+
+
+@contextmanager
+def marked_timer(name: str, timing_raw: dict):
+    """profiler/performance.py:172 — wall time of a stage (synchronised: stages run on the GPU stream)."""
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    yield
+    torch.cuda.synchronize()
+    timing_raw[name] = timing_raw.get(name, 0.0) + time.perf_counter() - t0
+
+
+def compute_response_mask(data: DataProto):
+    """ray_trainer.py:196-211."""
+    R = data.batch["responses"].size(1)
+    return data.batch["attention_mask"][:, -R:]
+
+
+def apply_kl_penalty(data: DataProto, kl_ctrl, kl_penalty="kl"):
+    """ray_trainer.py:154-193 (use_kl_in_reward)."""
+    mask = data.batch["response_mask"]
+    kld = core_algos.kl_penalty(data.batch["old_log_probs"], data.batch["ref_log_prob"], kl_penalty) * mask
+    beta = kl_ctrl.value
+    data.batch["token_level_rewards"] = data.batch["token_level_scores"] - beta * kld
+    current_kl = float(core_algos.agg_loss(kld, mask, "token-mean"))
+    kl_ctrl.update(current_kl=current_kl, n_steps=len(data))
+    return data, {"actor/reward_kl_penalty": current_kl, "actor/reward_kl_penalty_coeff": beta}
+
+
+def compute_advantage(data: DataProto, adv_estimator, gamma=1.0, lam=1.0, num_repeat=1, norm_adv_by_std_in_grpo=True,
+                      config=None) -> DataProto:
+    """ray_trainer.py:214-291."""
+    if "response_mask" not in data.batch:
+        data.batch["response_mask"] = compute_response_mask(data)
+    if adv_estimator == AdvantageEstimator.GAE:
+        adv, ret = core_algos.compute_gae_advantage_return(data.batch["token_level_rewards"], data.batch["values"],
+                                                           data.batch["response_mask"], gamma, lam)
+    elif adv_estimator == AdvantageEstimator.GRPO:
+        adv, ret = core_algos.compute_grpo_outcome_advantage(
+            token_level_rewards=data.batch["token_level_rewards"], response_mask=data.batch["response_mask"],
+            index=data.non_tensor_batch["uid"], norm_adv_by_std_in_grpo=norm_adv_by_std_in_grpo)
+    else:
+        fn = core_algos.get_adv_estimator_fn(adv_estimator)
+        kw = {"token_level_rewards": data.batch["token_level_rewards"], "response_mask": data.batch["response_mask"],
+              "config": config}
+        if "uid" in data.non_tensor_batch:
+            kw["index"] = data.non_tensor_batch["uid"]
+        adv, ret = fn(**kw)
+    data.batch["advantages"] = adv
+    data.batch["returns"] = ret
+    return data
+
+
+class SyntheticPromptLoader:
+    """Fixed-length synthetic prompts: token ids ~ U[0, 151643), no padding."""
+
+    def __init__(self, batch_size, prompt_length, vocab_limit=151643, seed=1234, device="cuda", left_pad=None):
+        self.batch_size = batch_size
+        self.prompt_length = prompt_length
+        self.vocab_limit = vocab_limit
+        self.seed = seed
+        self.device = device
+        self.left_pad = left_pad  # optional (B,) number of left-pad tokens for variable-length prompts
+        self.step = 0
+
+    def next(self) -> dict:
+        g = torch.Generator(device=self.device).manual_seed(self.seed + self.step)
+        self.step += 1
+        B, P = self.batch_size, self.prompt_length
+        ids = torch.randint(0, self.vocab_limit, (B, P), generator=g, device=self.device)
+        am = torch.ones(B, P, dtype=torch.int64, device=self.device)
+        if self.left_pad is not None:
+            for i, n in enumerate(self.left_pad):
+                am[i, :n] = 0
+                ids[i, :n] = self.vocab_limit  # pad id
+        from .torch_functional import compute_position_id_with_mask
+
+        pos = compute_position_id_with_mask(am)
+        return {"input_ids": ids, "attention_mask": am, "position_ids": pos}
+
+
+class RayPPOTrainer:
+    """The fit() loop of ray_trainer.py:1050-1405 for the GRPO/PPO actor-learner hot path."""
+
+    def __init__(self, config, reward_fn=None, train_dataloader=None, eos_token_id=151645, pad_token_id=151643):
+        self.config = config
+        self.reward_fn = reward_fn or SyntheticBernoulliRewardManager(seed=config.data.get("seed", 1234))
+        self.train_dataloader = train_dataloader or SyntheticPromptLoader(
+            config.data.train_batch_size, config.data.max_prompt_length, seed=config.data.get("seed", 1234))
+        self.eos_token_id = eos_token_id
+        self.pad_token_id = pad_token_id
+        self.use_reference_policy = config.actor_rollout_ref.actor.use_kl_loss or config.algorithm.use_kl_in_reward
+        self.kl_ctrl_in_reward = core_algos.get_kl_controller(config.algorithm.kl_ctrl)
+        self.global_steps = 0
+        self.n_gpus = dist.get_world_size() if dist.is_initialized() else 1
+
+    def init_workers(self):
+        """ray_trainer.py:779-886: one colocated actor/rollout/ref worker per GPU (hybrid engine)."""
+        worker = ActorRolloutRefWorker(self.config.actor_rollout_ref, role="actor_rollout_ref")
+        self.actor_rollout_wg = SPMDWorkerGroup(worker)
+        self.ref_policy_wg = self.actor_rollout_wg
+        self.actor_rollout_wg.init_model()
+
+    def _uids(self, n):
+        # deterministic per step (uuid4 in the reference; only group identity matters)
+        return np.array([str(uuid.UUID(int=(self.global_steps << 32) + i)) for i in range(n)], dtype=object)
+
+    def _balance_batch(self, batch: DataProto, metrics):
+        """ray_trainer.py:1033-1048 (greedy sequence-length balancing across DP ranks)."""
+        am = batch.batch["attention_mask"]
+        seqlens = am.sum(-1).cpu().tolist()
+        k = self.n_gpus
+        order = sorted(range(len(seqlens)), key=lambda i: -seqlens[i])
+        per = len(seqlens) // k
+        buckets = [[] for _ in range(k)]
+        loads = [0] * k
+        for i in order:
+            j = min((j for j in range(k) if len(buckets[j]) < per), key=lambda j: loads[j])
+            buckets[j].append(i)
+            loads[j] += seqlens[i]
+        idx = torch.tensor([i for b in buckets for i in sorted(b)], device=am.device)
+        batch.reorder(idx)
+
+    def step(self, batch_dict: dict) -> dict:
+        """One PPO step — ray_trainer.py:1104-1399 minus validation/checkpoint/logging."""
+        cfg = self.config
+        ar = cfg.actor_rollout_ref
+        metrics, timing_raw = {}, {}
+        batch = DataProto.from_single_dict(batch_dict)
+        batch.non_tensor_batch["uid"] = self._uids(len(batch))
+        gen_batch = batch.pop(batch_keys=["input_ids", "attention_mask", "position_ids"])
+        gen_batch.meta_info.update({"global_steps": self.global_steps, "eos_token_id": self.eos_token_id,
+                                    "pad_token_id": self.pad_token_id})
+        gen_batch = gen_batch.repeat(repeat_times=ar.rollout.n, interleave=True)
+        with marked_timer("step", timing_raw):
+            with marked_timer("gen", timing_raw):
+                gen_out = self.actor_rollout_wg.generate_sequences(gen_batch)
+                timing_raw.update(gen_out.meta_info.pop("timing", {}))
+            batch = batch.repeat(repeat_times=ar.rollout.n, interleave=True)
+            batch = batch.union(gen_out)
+            if "response_mask" not in batch.batch:
+                batch.batch["response_mask"] = compute_response_mask(batch)
+            if cfg.trainer.balance_batch and self.n_gpus > 1:
+                self._balance_batch(batch, metrics)
+            batch.meta_info["global_token_num"] = batch.batch["attention_mask"].sum(-1).tolist()
+            with marked_timer("reward", timing_raw):
+                reward_tensor, _ = compute_reward(batch, self.reward_fn)
+            with marked_timer("old_log_prob", timing_raw):
+                old = self.actor_rollout_wg.compute_log_prob(batch)
+                ent = agg_loss(old.batch["entropys"], batch.batch["response_mask"], ar.actor.loss_agg_mode)
+                metrics["actor/entropy"] = ent
+                old.batch.pop("entropys")
+                batch = batch.union(old)
+            if self.use_reference_policy:
+                with marked_timer("ref", timing_raw):
+                    batch = batch.union(self.ref_policy_wg.compute_ref_log_prob(batch))
+            with marked_timer("adv", timing_raw):
+                batch.batch["token_level_scores"] = reward_tensor
+                if cfg.algorithm.use_kl_in_reward:
+                    batch, klm = apply_kl_penalty(batch, self.kl_ctrl_in_reward, cfg.algorithm.kl_penalty)
+                    metrics.update(klm)
+                else:
+                    batch.batch["token_level_rewards"] = batch.batch["token_level_scores"]
+                batch = compute_advantage(batch, cfg.algorithm.adv_estimator, cfg.algorithm.gamma, cfg.algorithm.lam,
+                                          ar.rollout.n, cfg.algorithm.norm_adv_by_std_in_grpo, cfg.algorithm)
+            if cfg.trainer.critic_warmup <= self.global_steps:
+                with marked_timer("update_actor", timing_raw):
+                    batch.meta_info["multi_turn"] = False
+                    batch.meta_info["temperature"] = ar.rollout.temperature
+                    actor_out = self.actor_rollout_wg.update_actor(batch)
+                metrics.update(reduce_metrics(actor_out.meta_info["metrics"]))
+        metrics["actor/entropy"] = float(metrics["actor/entropy"])
+        metrics.update({"training/global_step": self.global_steps})
+        metrics.update(compute_data_metrics(batch, use_critic=False))
+        metrics.update(compute_timing_metrics(batch, timing_raw))
+        metrics.update(compute_throughout_metrics(batch, timing_raw, self.n_gpus))
+        n_resp = batch.batch["response_mask"].sum().item()
+        metrics["perf/rollout_tokens_per_sec"] = n_resp / timing_raw["gen"]
+        self.last_batch = batch
+        return metrics
+
+    def fit(self, num_steps=None):
+        """ray_trainer.py:1050-1405 training loop (synthetic data; no validation/checkpoint by default)."""
+        total = num_steps or self.config.trainer.get("total_training_steps") or 1
+        self.global_steps = 1
+        history = []
+        for _ in range(total):
+            m = self.step(self.train_dataloader.next())
+            history.append(m)
+            self.global_steps += 1
+        return history

@@ -1,0 +1,199 @@
+"""ActorRolloutRefWorker for ``actor.strategy = "mi355x"`` (mirror of verl/workers/fsdp_workers.py:110-921).
+
+Same registered methods, dispatch modes, batch-size normalisation and output keys as the FSDP worker:
+``init_model``, ``generate_sequences``, ``compute_log_prob`` (-> old_log_probs, entropys),
+``compute_ref_log_prob`` (-> ref_log_prob), ``update_actor`` (-> meta_info["metrics"]),
+``save_checkpoint`` / ``load_checkpoint``. Parallelism is replicated-parameter data parallelism: each
+rank holds the full model (0.5B fits many times over in 288 GB) and gradients are averaged with one
+RCCL all-reduce per optimizer step, instead of FSDP's per-layer all-gather / reduce-scatter.
+Outputs stay on the device (``output_device="cuda"``); ``output_device="cpu"`` reproduces the
+reference's ``.to("cpu")`` convention for callers that need it.
+"""
+
+from __future__ import annotations
+
+import os
+import time
+
+import torch
+import torch.distributed as dist
+
+from .config import QWEN25_05B
+from .dp_actor import DataParallelPPOActor, FlatAdamW
+from .protocol import DataProto
+from .qwen2 import ParamStore, Qwen2Config, Qwen2Model, flops_per_token
+from .rollout import MI355XRollout
+from .single_controller import Dispatch, Worker, make_nd_compute_dataproto_dispatch_fn, register
+
+MI355X_BF16_DENSE_PEAK = 2.5e15  # FLOP/s (MI355X_MICROARCH.md; AMD's 5 PF figure is 2:1 sparse)
+
+
+def resolve_model_config(model_cfg) -> Qwen2Config:
+    path = model_cfg.get("path", "random:qwen2.5-0.5b")
+    over = dict(model_cfg.get("override_config", {}) or {})
+    if path.startswith("random:"):
+        base = dict(QWEN25_05B)
+    else:
+        import json
+
+        with open(os.path.join(path, "config.json")) as f:
+            base = json.load(f)
+    base.update(over)
+    return Qwen2Config.from_dict(base)
+
+
+class ActorRolloutRefWorker(Worker):
+    def __init__(self, config, role: str = "actor_rollout_ref", output_device: str = "cuda"):
+        super().__init__()
+        self.config = config
+        self.role = role
+        self._is_actor = role in ("actor", "actor_rollout", "actor_rollout_ref")
+        self._is_rollout = role in ("rollout", "actor_rollout", "actor_rollout_ref")
+        self._is_ref = role in ("ref", "actor_rollout_ref")
+        self.output_device = output_device
+        self.device = torch.device("cuda", torch.cuda.current_device())
+        dp = dist.get_world_size() if dist.is_initialized() else 1
+        self.dp_size = dp
+        self.dp_rank = dist.get_rank() if dist.is_initialized() else 0
+        for mesh in ("actor", "rollout"):
+            self._register_dispatch_collect_info(mesh, dp_rank=self.dp_rank, is_collect=True)
+        # fsdp_workers.py:209-242 batch-size normalisation (per-GPU sizes)
+        a = config.actor
+        if self._is_actor:
+            a.ppo_mini_batch_size = a.ppo_mini_batch_size * config.rollout.n // dp
+            assert a.ppo_mini_batch_size > 0
+            if a.get("ppo_micro_batch_size") is not None:
+                a.ppo_micro_batch_size_per_gpu = a.ppo_micro_batch_size // dp
+            assert a.ppo_mini_batch_size % a.ppo_micro_batch_size_per_gpu == 0
+        r = config.rollout
+        if self._is_rollout and r.get("log_prob_micro_batch_size") is not None:
+            r.log_prob_micro_batch_size_per_gpu = r.log_prob_micro_batch_size // dp
+        rf = config.ref
+        if self._is_ref and rf.get("log_prob_micro_batch_size") is not None:
+            rf.log_prob_micro_batch_size_per_gpu = rf.log_prob_micro_batch_size // dp
+
+    # ------------------------------------------------------------------------------------------ init
+    @register(dispatch_mode=Dispatch.ONE_TO_ALL)
+    def init_model(self):
+        cfg = self.config
+        mcfg = resolve_model_config(cfg.model)
+        self.model_config = mcfg
+        dtype = torch.float32 if cfg.model.get("dtype", "bfloat16") == "float32" else torch.bfloat16
+        seed = int(cfg.model.get("seed", 1234))
+        self.store = ParamStore(mcfg, self.device, compute_dtype=dtype, trainable=self._is_actor)
+        path = cfg.model.get("path", "random:")
+        if path.startswith("random:"):
+            self.store.init_random(seed)
+        else:
+            self._load_hf_weights(path)
+        self.actor_module = Qwen2Model(mcfg, self.store)
+        if self._is_actor:
+            o = cfg.actor.optim
+            total = o.get("total_training_steps", -1)
+            warm = o.get("lr_warmup_steps", -1)
+            if warm is None or warm < 0:
+                warm = int(o.get("lr_warmup_steps_ratio", 0.0) * max(total, 0))
+            betas = tuple(o.get("betas", (0.9, 0.999)))
+            self.actor_optimizer = FlatAdamW(self.store, lr=o.lr, betas=betas, eps=o.get("eps", 1e-8),
+                                             weight_decay=o.weight_decay, max_grad_norm=cfg.actor.grad_clip,
+                                             warmup_steps=warm)
+            self.actor = DataParallelPPOActor(cfg.actor, self.actor_module, self.actor_optimizer)
+        if self._is_rollout:
+            self.rollout = MI355XRollout(self.actor_module, cfg.rollout, dp_rank=self.dp_rank)
+        if self._is_ref:
+            # reference policy: frozen compute-dtype copy of the initial weights (fsdp_workers.py:648-672)
+            self.ref_store = ParamStore(mcfg, self.device, compute_dtype=dtype, trainable=False)
+            self.ref_store.master.copy_(self.store.master)
+            self.ref_store.refresh_compute()
+            self.ref_module = Qwen2Model(mcfg, self.ref_store)
+            self.ref_policy = DataParallelPPOActor(cfg.ref, self.ref_module)
+
+    def _load_hf_weights(self, path):
+        from safetensors.torch import load_file
+
+        sd = {}
+        for f in sorted(os.listdir(path)):
+            if f.endswith(".safetensors"):
+                sd.update(load_file(os.path.join(path, f)))
+        self.store.load_state_dict_hf(sd)
+
+    def _out(self, d: DataProto):
+        return d.to(self.output_device) if self.output_device != "cuda" else d
+
+    # ------------------------------------------------------------------------------------------ hot path
+    @register(dispatch_mode=make_nd_compute_dataproto_dispatch_fn(mesh_name="rollout"))
+    def generate_sequences(self, prompts: DataProto):
+        """fsdp_workers.py:727-763."""
+        prompts = prompts.to(self.device)
+        t0 = time.perf_counter()
+        output = self.rollout.generate_sequences(prompts)
+        torch.cuda.synchronize()
+        output.meta_info["timing"] = {"generate_sequences": time.perf_counter() - t0,
+                                      "generate_prefill": getattr(self.rollout, "last_prefill_s", 0.0)}
+        return self._out(output)
+
+    @register(dispatch_mode=make_nd_compute_dataproto_dispatch_fn(mesh_name="actor"))
+    def compute_log_prob(self, data: DataProto):
+        """fsdp_workers.py:765-805: old log-probs AND entropy (calculate_entropy=True, :788)."""
+        data = data.to(self.device)
+        r = self.config.rollout
+        data.meta_info["micro_batch_size"] = r.log_prob_micro_batch_size_per_gpu
+        data.meta_info["use_dynamic_bsz"] = r.log_prob_use_dynamic_bsz
+        data.meta_info["temperature"] = r.temperature
+        output, entropys = self.actor.compute_log_prob(data=data, calculate_entropy=True)
+        out = DataProto.from_dict(tensors={"old_log_probs": output, "entropys": entropys},
+                                  meta_info={"temperature": r.temperature})
+        return self._out(out)
+
+    @register(dispatch_mode=make_nd_compute_dataproto_dispatch_fn(mesh_name="actor"))
+    def compute_ref_log_prob(self, data: DataProto):
+        """fsdp_workers.py:807-842."""
+        data = data.to(self.device)
+        rf = self.config.ref
+        data.meta_info["micro_batch_size"] = rf.log_prob_micro_batch_size_per_gpu
+        data.meta_info["temperature"] = self.config.rollout.temperature
+        data.meta_info["use_dynamic_bsz"] = rf.log_prob_use_dynamic_bsz
+        output, _ = self.ref_policy.compute_log_prob(data=data, calculate_entropy=False)
+        return self._out(DataProto.from_dict(tensors={"ref_log_prob": output}))
+
+    @register(dispatch_mode=make_nd_compute_dataproto_dispatch_fn(mesh_name="actor"))
+    def update_actor(self, data: DataProto):
+        """fsdp_workers.py:684-725 (+ MFU with an MI355X peak, lr schedule step)."""
+        data = data.to(self.device)
+        t0 = time.perf_counter()
+        metrics = self.actor.update_policy(data=data)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        ntok = data.meta_info.get("global_token_num")
+        if ntok:
+            T = data.batch["input_ids"].shape[1]
+            est = 3 * flops_per_token(self.model_config, T) * sum(ntok)
+            metrics["perf/mfu/actor"] = est * self.config.actor.ppo_epochs / (dt * MI355X_BF16_DENSE_PEAK * self.dp_size)
+        metrics["perf/max_memory_allocated_gb"] = torch.cuda.max_memory_allocated() / 1024**3
+        metrics["perf/max_memory_reserved_gb"] = torch.cuda.max_memory_reserved() / 1024**3
+        metrics["actor/lr"] = self.actor_optimizer.current_lr()
+        self.actor_optimizer.sched_step += 1
+        return DataProto(meta_info={"metrics": metrics})
+
+    # ------------------------------------------------------------------------------------------ checkpoint
+    @register(dispatch_mode=Dispatch.ONE_TO_ALL)
+    def save_checkpoint(self, local_path, hdfs_path=None, global_step=0, max_ckpt_to_keep=None):
+        """fsdp_workers.py:844-880: replicated params -> rank 0 writes model + optimizer + rng state."""
+        if self.dp_rank == 0:
+            os.makedirs(local_path, exist_ok=True)
+            torch.save({"master": self.store.master.cpu(), "optim": {k: (v.cpu() if torch.is_tensor(v) else v)
+                                                                      for k, v in self.actor_optimizer.state_dict().items()},
+                        "global_step": global_step, "cuda_rng": torch.cuda.get_rng_state(),
+                        "rollout_calls": self.rollout.calls if self._is_rollout else 0},
+                       os.path.join(local_path, "model_optim_rng.pt"))
+        if dist.is_initialized():
+            dist.barrier()
+
+    @register(dispatch_mode=Dispatch.ONE_TO_ALL)
+    def load_checkpoint(self, local_path, hdfs_path=None, del_local_after_load=False):
+        sd = torch.load(os.path.join(local_path, "model_optim_rng.pt"), map_location="cpu", weights_only=True)
+        self.store.master.copy_(sd["master"])
+        self.store.refresh_compute()
+        self.actor_optimizer.load_state_dict(sd["optim"])
+        if self._is_rollout:
+            self.rollout.calls = int(sd.get("rollout_calls", 0))

@@ -208,6 +208,40 @@ typedef struct drl_adamw_params {
 int drl_adamw_step(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, uint16_t* params_bf16,
                    int64_t n, const drl_adamw_params* hp, const float* grad_norm, void* stream);
 
+/* ------------------------------------------------------------------------------------------------
+ * Transformer-layer kernels of the actor / reference / rollout model (HF Qwen2 semantics as the
+ * reference runs them inside _forward_micro_batch, dp_actor.py:90-280, and HF generate,
+ * hf_rollout.py:112-124). `dt` is the element type of the activations (DRL_BF16 in production,
+ * DRL_F32 for the parity model); the residual stream and norm weights are always float32.
+ * ---------------------------------------------------------------------------------------------- */
+/* qkv (B,T,(Hq+2Hkv)*D) -> RoPE'd q in grouped layout (B,Hkv,Hq/Hkv,T,D), RoPE'd k and v written at
+ * key offset koff of (B,Hkv,Tk,D) buffers (the KV cache when decoding). cos/sin: (maxpos, D/2) fp32. */
+int drl_rope_qkv_fwd(const void* qkv, int32_t dt, const int64_t* position_ids, const float* cos_t, const float* sin_t,
+                     int64_t maxpos, int64_t B, int64_t T, int64_t Hq, int64_t Hkv, int64_t D, void* q, void* k,
+                     void* v, int64_t Tk, int64_t koff, void* stream);
+int drl_rope_qkv_bwd(const void* dq, const void* dk, const void* dv, int32_t dt, const int64_t* position_ids,
+                     const float* cos_t, const float* sin_t, int64_t maxpos, int64_t B, int64_t T, int64_t Hq,
+                     int64_t Hkv, int64_t D, void* dqkv, void* stream);
+/* fp32 scores (B,Hkv,G,Tq,Tk) -> probs of type dt: softmax(scale*s) over keys j with
+ * j <= q+qoff && key_valid[b,j] (causal + key padding, HF semantics: a query with no allowed key is
+ * uniform over all Tk keys, as HF's additive finfo.min mask makes it). */
+int drl_masked_softmax_fwd(const float* scores, void* probs, int32_t dt, const uint8_t* key_valid, int64_t ld_valid,
+                           int64_t B, int64_t HG, int64_t Tq, int64_t Tk, int64_t qoff, float scale, void* stream);
+/* dscores = probs * (dprobs - rowsum(probs*dprobs)) * scale  (rows x Tk; dprobs fp32) */
+int drl_masked_softmax_bwd(const void* probs, const float* dprobs, void* dscores, int32_t dt, int64_t rows, int64_t Tk,
+                           float scale, void* stream);
+/* x_out = x_in (+ delta); y = w * x_out * rsqrt(mean(x_out^2) + eps)  (Qwen2RMSNorm); rstd saved. */
+int drl_add_rmsnorm_fwd(const float* x_in, const void* delta, float* x_out, const float* weight, void* y, int32_t dt,
+                        float* rstd, int64_t N, int64_t H, float eps, void* stream);
+size_t drl_rmsnorm_bwd_workspace_bytes(int64_t N, int64_t H);
+/* dx += d norm(x)/dx . dy ; dw += sum_rows dy * xhat */
+int drl_rmsnorm_bwd(const float* x, const float* weight, const float* rstd, const void* dy, int32_t dt, float* dx,
+                    float* dw, int64_t N, int64_t H, void* workspace, size_t workspace_bytes, void* stream);
+/* gate_up (N, 2I) -> out (N, I) = silu(gate) * up ; backward -> d gate_up */
+int drl_swiglu_fwd(const void* gate_up, void* out, int32_t dt, int64_t N, int64_t I, void* stream);
+int drl_swiglu_bwd(const void* gate_up, const void* dout, void* dgate_up, int32_t dt, int64_t N, int64_t I,
+                   void* stream);
+
 #ifdef __cplusplus
 }
 #endif

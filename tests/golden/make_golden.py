@@ -349,7 +349,83 @@ def gen_masks():
     _save("masks.npz", arrays, {"ref": "torch_functional.py:226-246; model.py:219; hf_rollout.py:151-160"})
 
 
+# --------------------------------------------------------------------------------------------
+# A3/A6: tiny random Qwen2 — HF greedy generate post-processed exactly as HFRollout._generate_minibatch
+# (hf_rollout.py:112-171), and teacher-forced log-probs / entropy of the responses as
+# DataParallelPPOActor._forward_micro_batch computes them (dp_actor.py:249-272), all fp32.
+# --------------------------------------------------------------------------------------------
+TINY_QWEN2 = dict(vocab_size=512, hidden_size=64, intermediate_size=128, num_hidden_layers=2, num_attention_heads=4,
+                  num_key_value_heads=2, max_position_embeddings=256, rope_theta=10000.0, rms_norm_eps=1e-6,
+                  tie_word_embeddings=True, initializer_range=0.2, bos_token_id=1, eos_token_id=2, pad_token_id=0)
+
+
+def gen_tiny_qwen2():
+    from safetensors.torch import save_file
+    from transformers import GenerationConfig, Qwen2Config, Qwen2ForCausalLM
+
+    torch.manual_seed(0)
+    cfg = Qwen2Config(**TINY_QWEN2, attn_implementation="eager")
+    model = Qwen2ForCausalLM(cfg).float().eval()
+    with torch.no_grad():  # non-trivial norm weights and biases so those code paths are exercised
+        for n, p in model.named_parameters():
+            if "norm" in n:
+                p.copy_(1.0 + 0.1 * torch.randn_like(p))
+            elif n.endswith("bias"):
+                p.copy_(0.1 * torch.randn_like(p))
+    outdir = os.path.join(HERE, "tiny_qwen2")
+    os.makedirs(outdir, exist_ok=True)
+    sd = {k: v.contiguous() for k, v in model.state_dict().items() if k != "lm_head.weight"}
+    save_file(sd, os.path.join(outdir, "model.safetensors"))
+    with open(os.path.join(outdir, "config.json"), "w") as f:
+        json.dump(TINY_QWEN2, f, indent=1)
+
+    B, P, R = 6, 12, 10
+    g = torch.Generator().manual_seed(42)
+    ids = torch.randint(3, 512, (B, P), generator=g)
+    am = torch.ones(B, P, dtype=torch.int64)
+    for i, npad in enumerate([0, 3, 0, 5, 1, 0]):
+        am[i, :npad] = 0
+        ids[i, :npad] = TINY_QWEN2["pad_token_id"]
+    pos = compute_position_id_with_mask(am)
+
+    def hf_rollout(eos):
+        gc = GenerationConfig(do_sample=False, num_beams=1)
+        with torch.no_grad():
+            out = model.generate(input_ids=ids, attention_mask=am, do_sample=False, max_new_tokens=R,
+                                 eos_token_id=eos, pad_token_id=TINY_QWEN2["pad_token_id"], generation_config=gc,
+                                 output_scores=True, return_dict_in_generate=True, use_cache=True)
+        seq = out.sequences
+        if seq.shape[1] < P + R:  # hf_rollout.py:132-139
+            seq = torch.cat([seq, torch.full((B, P + R - seq.shape[1]), TINY_QWEN2["pad_token_id"])], 1)
+        gaps = [torch.topk(s, 2, dim=-1).values for s in out.scores]
+        gap = min(float((v[:, 0] - v[:, 1]).min()) for v in gaps)
+        return seq, gap
+
+    seq, gap = hf_rollout(eos=[TINY_QWEN2["eos_token_id"]])
+    eos = int(seq[0, P + 4])  # make row 0 hit "EOS" mid-response so the finished-row padding path is exercised
+    seq, gap = hf_rollout(eos=[eos])
+    resp = seq[:, P:]
+    delta = torch.arange(1, R + 1).unsqueeze(0).repeat(B, 1)
+    full_pos = torch.cat([pos, pos[:, -1:] + delta], -1)
+    resp_mask = vF.get_response_mask(resp, eos_token=eos, dtype=am.dtype)
+    full_am = torch.cat([am, resp_mask], -1)
+    with torch.no_grad():
+        logits = model(input_ids=seq, attention_mask=full_am, position_ids=full_pos, use_cache=False).logits
+    logits = logits[:, -R - 1:-1, :]
+    logp = vF.logprobs_from_logits_v2(logits, resp)
+    ent = vF.entropy_from_logits(logits)
+    # temperature 0.7 variant (logits.div_(temperature), dp_actor.py:263)
+    logp_t = vF.logprobs_from_logits_v2(logits / 0.7, resp)
+    arrays = dict(prompt_ids=ids, prompt_attention_mask=am, prompt_position_ids=pos, sequences=seq,
+                  responses=resp, attention_mask=full_am, position_ids=full_pos, log_probs=logp, entropy=ent,
+                  log_probs_t07=logp_t)
+    _save("tiny_qwen2_rollout.npz", arrays, {"eos_token_id": eos, "pad_token_id": TINY_QWEN2["pad_token_id"],
+                                             "response_length": R, "min_top2_logit_gap": gap,
+                                             "hf": "transformers Qwen2ForCausalLM fp32 eager attention",
+                                             "ref": "hf_rollout.py:112-171; dp_actor.py:249-272"})
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["ppo_loss", "masked_mean", "grpo", "gae", "logprob", "fused_linear", "masks"]
+    which = sys.argv[1:] or ["ppo_loss", "masked_mean", "grpo", "gae", "logprob", "fused_linear", "masks", "tiny_qwen2"]
     for w in which:
         globals()[f"gen_{w}"]()

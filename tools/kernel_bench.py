@@ -1,0 +1,110 @@
+"""Per-kernel roofline sweep of the hand-written HIP kernels (HIP events on the launch stream).
+
+Algorithmic bytes per unit:
+  K1 ppo loss fwd+bwd : 36 B / token  (read old, logp, adv, entropy, ref: 5 x 4 B; mask int64 8 B;
+                                       write dlogp, dentropy: 2 x 4 B)
+  K2 logprob fwd      : 2V + 16 B / row (bf16 logits row, label int64, write logp + entropy fp32)
+  K2 logprob bwd      : 4V + 8+16 B / row (read bf16 logits, write bf16 dlogits; per-row scalars)
+  K4 select (greedy)  : 2V + 8 B / row
+  AdamW step          : 28 B / param (+2 B bf16 copy) ; grad norm : 4 B / param
+Usage: python tools/kernel_bench.py [--quick] > out.jsonl
+"""
+
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from dots.rl_amd import native  # noqa: E402
+
+PEAK_HBM = 8.0e12  # MI355X HBM3E spec peak, B/s (MI355X_MICROARCH.md)
+
+
+def time_it(fn, iters=20, warmup=3):
+    s = torch.cuda.current_stream()
+    for _ in range(warmup):
+        fn()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(s)
+    for _ in range(iters):
+        fn()
+    b.record(s)
+    b.synchronize()
+    return a.elapsed_time(b) / iters * 1e-3
+
+
+def k1_sweep(exps):
+    rows = []
+    for e in exps:
+        N = 1 << e
+        R = 1024 if N >= 1024 else N
+        B = N // R
+        g = torch.Generator(device="cuda").manual_seed(e)
+        old = -torch.rand(B, R, device="cuda", generator=g) * 5
+        lp = old + torch.randn(B, R, device="cuda", generator=g) * 0.3
+        adv = torch.randn(B, R, device="cuda", generator=g)
+        mask = (torch.rand(B, R, device="cuda", generator=g) > 0.05).to(torch.int64)
+        ent = torch.rand(B, R, device="cuda", generator=g)
+        ref = lp + 0.1
+        out = torch.empty(8, device="cuda")
+        dlp = torch.empty_like(lp)
+        dent = torch.empty_like(lp)
+        kw = dict(entropy_coeff=0.001, kl_loss_coef=0.001, kl_loss_type="low_var_kl", loss_agg_mode="token-mean",
+                  want_dentropy=True, out=out, dlogp=dlp, dentropy=dent)
+        t = time_it(lambda: native.ppo_loss_fwd_bwd(old, lp, adv, mask, ent, ref, **kw))
+        byt = 36 * N
+        rows.append(dict(kernel="K1_ppo_loss_fwd_bwd", tokens=N, seconds=t, GBps=byt / t / 1e9, frac=byt / t / PEAK_HBM))
+        del old, lp, adv, mask, ent, ref, dlp, dent
+        torch.cuda.empty_cache()
+    return rows
+
+
+def k2(rows_n=4096, V=151936):
+    x = torch.randn(rows_n, V, device="cuda", dtype=torch.bfloat16) * 3
+    lab = torch.randint(0, V, (rows_n,), device="cuda")
+    res = []
+    t = time_it(lambda: native.logprob_entropy_fwd(x, lab))
+    byt = rows_n * (2 * V + 16)
+    res.append(dict(kernel="K2_logprob_entropy_fwd", rows=rows_n, V=V, seconds=t, GBps=byt / t / 1e9, frac=byt / t / PEAK_HBM))
+    lp, ent, lse = native.logprob_entropy_fwd(x, lab)
+    dl = torch.randn(rows_n, device="cuda")
+    out = torch.empty_like(x)
+    t = time_it(lambda: native.logprob_entropy_bwd(x, lab, 1.0, dl, dl, lse, ent, out=out))
+    byt = rows_n * (4 * V + 24)
+    res.append(dict(kernel="K2_logprob_entropy_bwd", rows=rows_n, V=V, seconds=t, GBps=byt / t / 1e9, frac=byt / t / PEAK_HBM))
+    tok = torch.empty(rows_n, dtype=torch.int64, device="cuda")
+    sub = x[:512]
+    t = time_it(lambda: native.select_tokens(sub, tok[:512]))
+    byt = 512 * (2 * V + 8)
+    res.append(dict(kernel="K4_select_greedy", rows=512, V=V, seconds=t, GBps=byt / t / 1e9, frac=byt / t / PEAK_HBM))
+    t = time_it(lambda: native.select_tokens(sub, tok[:512], do_sample=True, temperature=1.0, seed=1), iters=5)
+    res.append(dict(kernel="K4_select_sample", rows=512, V=V, seconds=t, GBps=byt * 3 / t / 1e9, frac=byt * 3 / t / PEAK_HBM))
+    return res
+
+
+def adam(n=494_032_768):
+    p = torch.randn(n, device="cuda")
+    g = torch.randn(n, device="cuda")
+    m = torch.zeros_like(p)
+    v = torch.zeros_like(p)
+    pbf = torch.empty(n, dtype=torch.bfloat16, device="cuda")
+    nrm = torch.empty(1, device="cuda")
+    res = []
+    t = time_it(lambda: native.grad_norm(g, out=nrm))
+    res.append(dict(kernel="A15_grad_norm", params=n, seconds=t, GBps=4 * n / t / 1e9, frac=4 * n / t / PEAK_HBM))
+    t = time_it(lambda: native.adamw_step(p, g, m, v, lr=1e-6, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.01,
+                                          step=1, max_grad_norm=1.0, grad_norm_t=nrm, params_bf16=pbf))
+    res.append(dict(kernel="A15_adamw_step", params=n, seconds=t, GBps=30 * n / t / 1e9, frac=30 * n / t / PEAK_HBM))
+    return res
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--quick", action="store_true")
+    args = ap.parse_args()
+    exps = [17, 20, 22, 24] if args.quick else [17, 18, 20, 22, 23, 24, 25, 26]
+    for r in k1_sweep(exps) + k2(1024 if args.quick else 4096) + adam(1 << 24 if args.quick else 494_032_768):
+        print(json.dumps(r), flush=True)
