@@ -72,12 +72,27 @@ def _union_batch(a: TensorBatch | None, b: TensorBatch | None) -> TensorBatch | 
     return a
 
 
+def _deep_equal(x, y) -> bool:
+    """protocol.py:121-181 semantics: strict type match, NaN == NaN, object arrays compared elementwise."""
+    if type(x) is not type(y):
+        return False
+    if isinstance(x, float):
+        return (x != x and y != y) or x == y
+    if isinstance(x, np.ndarray):
+        if x.dtype != y.dtype or x.shape != y.shape:
+            return False
+        if x.dtype != object:
+            return bool(np.array_equal(x, y, equal_nan=x.dtype.kind in "fc"))
+        return all(_deep_equal(p, q) for p, q in zip(x.flat, y.flat))
+    return bool(x == y)
+
+
 def _union_numpy(a: dict, b: dict) -> dict:
     for k, v in b.items():
         if k in a:
-            assert a[k].shape == v.shape and (a[k] is v or np.array_equal(a[k], v)), f"{k} differs"
-        else:
-            a[k] = v
+            assert isinstance(v, np.ndarray) and isinstance(a[k], np.ndarray)
+            assert a[k] is v or _deep_equal(a[k], v), f"`{k}` in tensor_dict1 and tensor_dict2 are not the same object."
+        a[k] = v
     return a
 
 
