@@ -163,6 +163,118 @@ __global__ __launch_bounds__(256) void masked_softmax_fwd_kernel(SoftmaxArgs<E> 
   }
 }
 
+// Single-pass variants for rows of up to kRegCols keys: the row lives in registers (lane l holds columns
+// 4l + 256k .. +3), so S / dP are read from HBM once with 16-B loads and P / dS written once.
+constexpr int kRegChunks = 16;                 // 16 x 256 columns
+constexpr int64_t kRegCols = kRegChunks * 256;  // 4096 keys
+
+__device__ __forceinline__ void ld4f(const float* p, int64_t j, int64_t n, bool vec, float v[4]) {
+  if (vec && j + 3 < n) {
+    const float4 q = *reinterpret_cast<const float4*>(p + j);
+    v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = j + e < n ? p[j + e] : 0.f;
+  }
+}
+template <typename E>
+__device__ __forceinline__ void ld4e(const E* p, int64_t j, int64_t n, bool vec, float v[4]) {
+  if constexpr (sizeof(E) == 2) {
+    if (vec && j + 3 < n) {
+      const uint2 q = *reinterpret_cast<const uint2*>(p + j);
+      v[0] = __uint_as_float(q.x << 16); v[1] = __uint_as_float(q.x & 0xffff0000u);
+      v[2] = __uint_as_float(q.y << 16); v[3] = __uint_as_float(q.y & 0xffff0000u);
+      return;
+    }
+  } else {
+    if (vec && j + 3 < n) {
+      const float4 q = *reinterpret_cast<const float4*>(p + j);
+      v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+      return;
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) v[e] = j + e < n ? ldf(p, j + e) : 0.f;
+}
+template <typename E>
+__device__ __forceinline__ void st4e(E* p, int64_t j, int64_t n, bool vec, const float v[4]) {
+  if constexpr (sizeof(E) == 2) {
+    if (vec && j + 3 < n) {
+      const uint32_t lo = static_cast<uint32_t>(f32_to_bf16(v[0])) | (static_cast<uint32_t>(f32_to_bf16(v[1])) << 16);
+      const uint32_t hi = static_cast<uint32_t>(f32_to_bf16(v[2])) | (static_cast<uint32_t>(f32_to_bf16(v[3])) << 16);
+      *reinterpret_cast<uint2*>(p + j) = make_uint2(lo, hi);
+      return;
+    }
+  } else {
+    if (vec && j + 3 < n) {
+      *reinterpret_cast<float4*>(p + j) = make_float4(v[0], v[1], v[2], v[3]);
+      return;
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+    if (j + e < n) stf(p, j + e, v[e]);
+}
+
+template <typename E>
+__global__ __launch_bounds__(256) void masked_softmax_fwd_reg_kernel(SoftmaxArgs<E> a) {
+  const int64_t row = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= a.rows) return;
+  const int64_t q = row % a.Tq, b = row / (a.HG * a.Tq), qpos = q + a.qoff, Tk = a.Tk;
+  const bool vec = (Tk & 3) == 0;
+  const float* src = a.s + row * Tk;
+  const uint8_t* vrow = a.valid + b * a.ld_valid;
+  const float sl2 = a.scale * 1.4426950408889634f;
+  const int nchunk = static_cast<int>((Tk + 255) / 256);
+  float v[kRegChunks][4];
+  float m = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < kRegChunks; ++k) {
+    if (k < nchunk) {
+      const int64_t j = 256 * k + 4 * lane;
+      ld4f(src, j, Tk, vec, v[k]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int64_t jj = j + e;
+        const bool ok = jj < Tk && jj <= qpos && vrow[jj];
+        v[k][e] = ok ? v[k][e] * sl2 : -INFINITY;
+        m = fmaxf(m, v[k][e]);
+      }
+    }
+  }
+  m = wave_max(m);
+  E* dst = a.p + row * Tk;
+  if (m == -INFINITY) {  // no allowed key: uniform row (HF finfo.min mask)
+    const float u = 1.f / static_cast<float>(Tk);
+    const float uu[4] = {u, u, u, u};
+#pragma unroll
+    for (int k = 0; k < kRegChunks; ++k)
+      if (k < nchunk) st4e(dst, 256 * k + 4 * lane, Tk, vec, uu);
+    return;
+  }
+  float sum = 0.f;
+#pragma unroll
+  for (int k = 0; k < kRegChunks; ++k) {
+    if (k < nchunk) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[k][e] = __builtin_amdgcn_exp2f(v[k][e] - m);  // exp2(-inf) = 0 for masked keys
+        sum += v[k][e];
+      }
+    }
+  }
+  const float inv = 1.f / wave_sum(sum);
+#pragma unroll
+  for (int k = 0; k < kRegChunks; ++k) {
+    if (k < nchunk) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[k][e] *= inv;
+      st4e(dst, 256 * k + 4 * lane, Tk, vec, v[k]);
+    }
+  }
+}
+
 // dS = P * (dP - sum_j P dP) * scale: P (E), dP fp32 -> dS (E). One wave per row.
 template <typename E>
 __global__ __launch_bounds__(256) void masked_softmax_bwd_kernel(const E* p, const float* dp, E* ds, int64_t rows,
@@ -173,6 +285,32 @@ __global__ __launch_bounds__(256) void masked_softmax_bwd_kernel(const E* p, con
   const E* pr = p + row * Tk;
   const float* dr = dp + row * Tk;
   E* sr = ds + row * Tk;
+  if (Tk <= kRegCols) {
+    const bool vec = (Tk & 3) == 0;
+    const int nchunk = static_cast<int>((Tk + 255) / 256);
+    float pv[kRegChunks][4], dv[kRegChunks][4];
+    float dot = 0.f;
+#pragma unroll
+    for (int k = 0; k < kRegChunks; ++k) {
+      if (k < nchunk) {
+        const int64_t j = 256 * k + 4 * lane;
+        ld4e(pr, j, Tk, vec, pv[k]);
+        ld4f(dr, j, Tk, vec, dv[k]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) dot += pv[k][e] * dv[k][e];
+      }
+    }
+    dot = wave_sum(dot);
+#pragma unroll
+    for (int k = 0; k < kRegChunks; ++k) {
+      if (k < nchunk) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) dv[k][e] = pv[k][e] * (dv[k][e] - dot) * scale;
+        st4e(sr, 256 * k + 4 * lane, Tk, vec, dv[k]);
+      }
+    }
+    return;
+  }
   float dot = 0.f;
   for (int64_t j = lane; j < Tk; j += 64) dot += ldf(pr, j) * dr[j];
   dot = wave_sum(dot);
@@ -250,43 +388,56 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const float* x, const 
     dw_part[blockIdx.x * H + j] = s_dw[j] + s_dw[H + j] + s_dw[2 * H + j] + s_dw[3 * H + j];
 }
 
-// dw[j] += sum over blocks of dw_part[:, j]  (fixed order)
+// dw[j] += sum over blocks of dw_part[:, j]: 64 columns x 4 block-slices per workgroup, fixed order
 __global__ __launch_bounds__(256) void colsum_kernel(const float* part, int64_t nb, int64_t H, float* out) {
-  const int64_t j = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (j >= H) return;
+  __shared__ float red[4][64];
+  const int c = threadIdx.x & 63, sl = threadIdx.x >> 6;
+  const int64_t j = static_cast<int64_t>(blockIdx.x) * 64 + c;
   float s = 0.f;
-  for (int64_t b = 0; b < nb; ++b) s += part[b * H + j];
-  out[j] += s;
+  if (j < H)
+    for (int64_t b = sl; b < nb; b += 4) s += part[b * H + j];
+  red[sl][c] = s;
+  __syncthreads();
+  if (sl == 0 && j < H) out[j] += (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
 }
 
 // ------------------------------------------------------------------------------------------ SwiGLU
 // gu (N, 2I) = [gate | up] -> a (N, I) = silu(gate) * up   (two E-typed ops, as F.silu then * in the model)
+// 4 consecutive columns per thread (I % 4 == 0 on the vector path).
 template <typename E>
 __global__ __launch_bounds__(256) void swiglu_fwd_kernel(const E* gu, E* out, int64_t N, int64_t I) {
-  const int64_t n = N * I;
-  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+  const int64_t n4 = N * I / 4;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n4;
        i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-    const int64_t row = i / I, c = i % I;
-    const float g = ldf(gu, row * 2 * I + c), u = ldf(gu, row * 2 * I + I + c);
-    const float sg = rnd<E>(g / (1.f + expf(-g)));
-    stf(out, i, sg * u);
+    const int64_t row = (4 * i) / I, c = (4 * i) % I;
+    float g[4], u[4], o[4];
+    ld4e(gu, row * 2 * I + c, row * 2 * I + I, true, g);
+    ld4e(gu, row * 2 * I + I + c, row * 2 * I + 2 * I, true, u);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = rnd<E>(g[e] / (1.f + expf(-g[e]))) * u[e];
+    st4e(out, 4 * i, N * I, true, o);
   }
 }
 
 // d gate = da * up * silu'(gate), d up = da * silu(gate)   ->   dgu (N, 2I)
 template <typename E>
 __global__ __launch_bounds__(256) void swiglu_bwd_kernel(const E* gu, const E* da, E* dgu, int64_t N, int64_t I) {
-  const int64_t n = N * I;
-  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+  const int64_t n4 = N * I / 4;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n4;
        i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-    const int64_t row = i / I, c = i % I;
-    const float g = ldf(gu, row * 2 * I + c);
-    const float u = ldf(gu, row * 2 * I + I + c);
-    const float d = ldf(da, i);
-    const float sig = 1.f / (1.f + expf(-g));
-    const float silu = rnd<E>(g * sig);
-    stf(dgu, row * 2 * I + c, rnd<E>(d * u) * (sig * (1.f + g * (1.f - sig))));
-    stf(dgu, row * 2 * I + I + c, d * silu);
+    const int64_t row = (4 * i) / I, c = (4 * i) % I;
+    float g[4], u[4], d[4], dg[4], du[4];
+    ld4e(gu, row * 2 * I + c, row * 2 * I + I, true, g);
+    ld4e(gu, row * 2 * I + I + c, row * 2 * I + 2 * I, true, u);
+    ld4e(da, 4 * i, N * I, true, d);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float sig = 1.f / (1.f + expf(-g[e]));
+      dg[e] = rnd<E>(d[e] * u[e]) * (sig * (1.f + g[e] * (1.f - sig)));
+      du[e] = d[e] * rnd<E>(g[e] * sig);
+    }
+    st4e(dgu, row * 2 * I + c, row * 2 * I + I, true, dg);
+    st4e(dgu, row * 2 * I + I + c, row * 2 * I + 2 * I, true, du);
   }
 }
 
@@ -348,8 +499,12 @@ int drl_masked_softmax_fwd(const float* scores, void* probs, int32_t dt, const u
   const int64_t rows = B * HG * Tq;
   DRL_E_DISPATCH(dt, {
     SoftmaxArgs<E> a{scores, static_cast<E*>(probs), key_valid, rows, Tq, Tk, HG, qoff, ld_valid, scale};
-    hipLaunchKernelGGL(masked_softmax_fwd_kernel<E>, dim3((rows + 3) / 4), dim3(256), 0,
-                       static_cast<hipStream_t>(stream), a);
+    if (Tk <= kRegCols)
+      hipLaunchKernelGGL(masked_softmax_fwd_reg_kernel<E>, dim3((rows + 3) / 4), dim3(256), 0,
+                         static_cast<hipStream_t>(stream), a);
+    else
+      hipLaunchKernelGGL(masked_softmax_fwd_kernel<E>, dim3((rows + 3) / 4), dim3(256), 0,
+                         static_cast<hipStream_t>(stream), a);
   });
   DRL_LAUNCH_CHECK();
   return DRL_OK;
@@ -398,16 +553,16 @@ int drl_rmsnorm_bwd(const float* x, const float* weight, const float* rstd, cons
   DRL_E_DISPATCH(dt, hipLaunchKernelGGL(rmsnorm_bwd_kernel<E>, dim3(grid), dim3(256), 4 * H * sizeof(float), s, x,
                                         weight, rstd, static_cast<const E*>(dy), dx, part, N, H));
   DRL_LAUNCH_CHECK();
-  hipLaunchKernelGGL(colsum_kernel, dim3((H + 255) / 256), dim3(256), 0, s, part, static_cast<int64_t>(grid), H, dw);
+  hipLaunchKernelGGL(colsum_kernel, dim3((H + 63) / 64), dim3(256), 0, s, part, static_cast<int64_t>(grid), H, dw);
   DRL_LAUNCH_CHECK();
   return DRL_OK;
 }
 
 int drl_swiglu_fwd(const void* gate_up, void* out, int32_t dt, int64_t N, int64_t I, void* stream) {
   using namespace drl;
-  DRL_CHECK_ARG(gate_up && out && N >= 0 && I >= 1, "bad input");
+  DRL_CHECK_ARG(gate_up && out && N >= 0 && I >= 4 && I % 4 == 0, "bad input (I %% 4 == 0 required)");
   if (N == 0) return DRL_OK;
-  DRL_E_DISPATCH(dt, hipLaunchKernelGGL(swiglu_fwd_kernel<E>, dim3(grid_stride(N * I)), dim3(256), 0,
+  DRL_E_DISPATCH(dt, hipLaunchKernelGGL(swiglu_fwd_kernel<E>, dim3(grid_stride(N * I / 4)), dim3(256), 0,
                                         static_cast<hipStream_t>(stream), static_cast<const E*>(gate_up),
                                         static_cast<E*>(out), N, I));
   DRL_LAUNCH_CHECK();
@@ -417,9 +572,9 @@ int drl_swiglu_fwd(const void* gate_up, void* out, int32_t dt, int64_t N, int64_
 int drl_swiglu_bwd(const void* gate_up, const void* dout, void* dgate_up, int32_t dt, int64_t N, int64_t I,
                    void* stream) {
   using namespace drl;
-  DRL_CHECK_ARG(gate_up && dout && dgate_up && N >= 0 && I >= 1, "bad input");
+  DRL_CHECK_ARG(gate_up && dout && dgate_up && N >= 0 && I >= 4 && I % 4 == 0, "bad input (I %% 4 == 0 required)");
   if (N == 0) return DRL_OK;
-  DRL_E_DISPATCH(dt, hipLaunchKernelGGL(swiglu_bwd_kernel<E>, dim3(grid_stride(N * I)), dim3(256), 0,
+  DRL_E_DISPATCH(dt, hipLaunchKernelGGL(swiglu_bwd_kernel<E>, dim3(grid_stride(N * I / 4)), dim3(256), 0,
                                         static_cast<hipStream_t>(stream), static_cast<const E*>(gate_up),
                                         static_cast<const E*>(dout), static_cast<E*>(dgate_up), N, I));
   DRL_LAUNCH_CHECK();
