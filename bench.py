@@ -6,6 +6,15 @@ two PPO mini-batch updates (micro 8/GPU) with AdamW. Global batch is fixed (512 
 across the N ranks: "scaling" is strong. Random-init Qwen2.5-0.5B weights, synthetic prompts.
 
   python bench.py [--gpus N] [--steps K] [--warmup W]          (N>1 under torch.distributed.run)
+
+Besides the step rate the JSON line carries
+  roofline     : the dominant hand-written kernel (--roofline-kernel), every launch inside the timed region
+                 bracketed by HIP events on its launch stream; achieved = algorithmic bytes per launch
+                 (ROOFLINE below, DESIGN.md §Kernels) / mean launch duration, against the 8 TB/s HBM peak;
+                 traffic = HBM bytes per launch from the committed rocprofv3 PMC pass
+                 (profiles/pmc_<kernel>.json, FETCH_SIZE doubled per the gfx950 correction + WRITE_SIZE) or null;
+  cpu_baseline : rank 0 at N=1 only — oracle/cpu_baseline.py (the same step restated in eager torch fp32
+                 on the host cores) on a bounded sample, scaled to PPO steps/s.
 """
 
 from __future__ import annotations
@@ -20,6 +29,52 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "PPO steps/sec + rollout tokens/sec, Qwen2.5-0.5B GRPO @1/2/4/8 MI355X"
+PEAK_HBM_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def _softmax_fwd_bytes(a):
+    # drl_masked_softmax_fwd(scores, probs, dt, valid, ld_valid, B, HG, Tq, Tk, qoff, scale, stream):
+    # read fp32 scores + write probs (bf16 / fp32) per element, key-valid row once per (b, key)
+    dt, B, HG, Tq, Tk = a[2], a[5], a[6], a[7], a[8]
+    return B * HG * Tq * Tk * (4 + (2 if dt == 4 else 4)) + B * Tk
+
+
+def _decode_attn_bytes(a):
+    # drl_decode_attention(q, k, v, dt, valid, ld, qpos_ptr, qpos, B, Hkv, G, D, Tk, L, ...): K and V rows
+    # of every allowed key once + q and out rows
+    dt, B, Hkv, G, D, L = a[3], a[8], a[9], a[10], a[11], a[13]
+    e = 2 if dt == 4 else 4
+    return B * Hkv * (2 * L * D + 2 * G * D) * e
+
+
+ROOFLINE = {  # symbol -> (bytes per launch from the call's arguments, per-unit statement)
+    "drl_masked_softmax_fwd": (_softmax_fwd_bytes, "6 B per attention score (fp32 in, bf16 out)"),
+    "drl_decode_attention": (_decode_attn_bytes, "4*D B per cached key (bf16 K+V rows)"),
+}
+
+
+def _pmc_traffic(symbol):
+    path = os.path.join(ROOT, "profiles", f"pmc_{symbol}.json")
+    if not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        d = json.load(f)
+    return d.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
+
+
+def cpu_baseline(cfg):
+    from oracle import cpu_baseline as cb
+
+    from dots.rl_amd.workers import resolve_model_config
+
+    ar = cfg.actor_rollout_ref
+    B = cfg.data.train_batch_size * ar.rollout.n
+    n_mini = max(1, cfg.data.train_batch_size // ar.actor.ppo_mini_batch_size)
+    r = cb.measure(resolve_model_config(ar.model), B, cfg.data.max_prompt_length, cfg.data.max_response_length,
+                   n_optimizer_steps=n_mini)
+    return {"value": 1.0 / r["step_s"], "unit": "PPO steps/s", "cores": r["threads"], "kind": "port",
+            "sample": r["sample"], "est_step_s": r["step_s"],
+            "est_parts_s": {k: v for k, v in r.items() if k.endswith("_s") and k != "step_s"}}
 
 
 def build_config(args):
@@ -54,12 +109,14 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--tiny", action="store_true", help="2-layer model, small batch (bring-up only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--roofline-kernel", default="drl_masked_softmax_fwd", choices=sorted(ROOFLINE))
     ap.add_argument("--override", nargs="*", default=[])
     args = ap.parse_args()
 
     import torch
     import torch.distributed as dist
 
+    from dots.rl_amd import native
     from dots.rl_amd.single_controller import init_process_group_from_env
     from dots.rl_amd.trainer import RayPPOTrainer
 
@@ -74,13 +131,15 @@ def main():
         trainer.step(trainer.train_dataloader.next())
         trainer.global_steps += 1
     prompts = [trainer.train_dataloader.next() for _ in range(args.steps)]
+    timer = native.KernelTimer(args.roofline_kernel, ROOFLINE[args.roofline_kernel][0])
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     hist = []
-    for p in prompts:
-        hist.append(trainer.step(p))
-        trainer.global_steps += 1
+    with timer:
+        for p in prompts:
+            hist.append(trainer.step(p))
+            trainer.global_steps += 1
     torch.cuda.synchronize()
     dist.barrier()
     elapsed = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cuda")
@@ -90,8 +149,16 @@ def main():
     gen_tokens = sum(h["perf/total_num_tokens"] for h in hist)  # prompt + response tokens processed
     resp_tokens = sum(h["perf/rollout_tokens_per_sec"] * h["timing_s/gen"] for h in hist)
     gen_time = sum(h["timing_s/gen"] for h in hist)
+    n_launch, t_launch, b_launch = timer.summary()
     if rank == 0:
         ar = cfg.actor_rollout_ref
+        achieved = b_launch / t_launch / 1e9 if n_launch else None
+        traffic, traffic_src = _pmc_traffic(args.roofline_kernel)
+        roofline = {"kernel": args.roofline_kernel, "bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBPS,
+                    "unit": "GB/s", "frac": achieved / PEAK_HBM_GBPS if achieved else None, "traffic": traffic,
+                    "algorithmic_bytes_per_launch": b_launch if n_launch else None,
+                    "mean_launch_us": t_launch * 1e6 if n_launch else None, "launches": n_launch,
+                    "per_unit": ROOFLINE[args.roofline_kernel][1], "traffic_source": traffic_src}
         line = {
             "metric": METRIC,
             "value": steps_per_s,
@@ -113,7 +180,11 @@ def main():
                        "parallelism": f"dp{world}", "tiny": bool(args.tiny)},
             "timing_s": {k.split("/", 1)[1]: sum(h[k] for h in hist) / len(hist) for k in hist[0] if k.startswith("timing_s/")},
             "mfu_actor": sum(h.get("perf/mfu/actor", 0.0) for h in hist) / len(hist),
+            "roofline": roofline,
+            "cpu_baseline": None,
         }
+        if world == 1 and not args.no_cpu_baseline and not args.tiny:
+            line["cpu_baseline"] = cpu_baseline(cfg)
         print(json.dumps(line), flush=True)
     dist.destroy_process_group()
 

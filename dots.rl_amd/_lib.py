@@ -52,6 +52,7 @@ class SamplingParams(ctypes.Structure):
         ("pad_token_id", ctypes.c_int64),
         ("eos_ids", ctypes.c_void_p),
         ("n_eos", ctypes.c_int32),
+        ("dev_step", ctypes.c_void_p),
     ]
 
 
@@ -97,7 +98,7 @@ SIGNATURES = {
     "drl_grad_norm_workspace_bytes": (SZ, [I64]),
     "drl_grad_norm": (ctypes.c_int, [P, I64, P, P, SZ, P]),
     "drl_adamw_step": (ctypes.c_int, [P, P, P, P, P, I64, ctypes.POINTER(AdamWParams), P, P]),
-    "drl_rope_qkv_fwd": (ctypes.c_int, [P, I32, P, P, P, I64, I64, I64, I64, I64, I64, P, P, P, I64, I64, P]),
+    "drl_rope_qkv_fwd": (ctypes.c_int, [P, I32, P, P, P, I64, I64, I64, I64, I64, I64, P, P, P, I64, I64, P, P]),
     "drl_rope_qkv_bwd": (ctypes.c_int, [P, P, P, I32, P, P, P, I64, I64, I64, I64, I64, I64, P, P]),
     "drl_masked_softmax_fwd": (ctypes.c_int, [P, P, I32, P, I64, I64, I64, I64, I64, I64, F32, P]),
     "drl_masked_softmax_bwd": (ctypes.c_int, [P, P, P, I32, I64, I64, F32, P]),
@@ -106,6 +107,9 @@ SIGNATURES = {
     "drl_rmsnorm_bwd": (ctypes.c_int, [P, P, P, P, I32, P, P, I64, I64, P, SZ, P]),
     "drl_swiglu_fwd": (ctypes.c_int, [P, P, I32, I64, I64, P]),
     "drl_swiglu_bwd": (ctypes.c_int, [P, P, P, I32, I64, I64, P]),
+    "drl_decode_attention_workspace_bytes": (SZ, [I64, I64, I64, I64, I64]),
+    "drl_decode_attention": (ctypes.c_int, [P, P, P, I32, P, I64, P, I64, I64, I64, I64, I64, I64, I64, F32, P, P, SZ,
+                                            P]),
 }
 
 _lib = None

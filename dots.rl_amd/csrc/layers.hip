@@ -36,6 +36,7 @@ struct RopeArgs {
   E* k;
   E* v;
   int64_t B, T, Hq, Hkv, D, Tk, koff, maxpos;
+  const int64_t* koff_dev;  // device key offset (graph-captured decode) overriding koff when non-NULL
 };
 
 template <typename E>
@@ -44,6 +45,8 @@ __global__ __launch_bounds__(256) void rope_qkv_fwd_kernel(RopeArgs<E> a) {
   const int64_t Hall = a.Hq + 2 * a.Hkv;
   const int64_t n = a.B * a.T * Hall * half;
   const int64_t G = a.Hq / a.Hkv;
+  const int64_t koff = a.koff_dev ? *a.koff_dev : a.koff;
+  if (koff < 0 || koff + a.T > a.Tk) return;  // device offset out of range: write nothing
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
        i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
     const int64_t j = i % half;
@@ -63,12 +66,12 @@ __global__ __launch_bounds__(256) void rope_qkv_fwd_kernel(RopeArgs<E> a) {
         const int64_t g = h / G, hi = h % G;
         dst = a.q + (((b * a.Hkv + g) * G + hi) * a.T + t) * a.D;
       } else {
-        dst = a.k + ((b * a.Hkv + (h - a.Hq)) * a.Tk + a.koff + t) * a.D;
+        dst = a.k + ((b * a.Hkv + (h - a.Hq)) * a.Tk + koff + t) * a.D;
       }
       stf(dst, j, o1);
       stf(dst, j + half, o2);
     } else {
-      E* dst = a.v + ((b * a.Hkv + (h - a.Hq - a.Hkv)) * a.Tk + a.koff + t) * a.D;
+      E* dst = a.v + ((b * a.Hkv + (h - a.Hq - a.Hkv)) * a.Tk + koff + t) * a.D;
       dst[j] = src[j];
       dst[j + half] = src[j + half];
     }
@@ -459,7 +462,7 @@ extern "C" {
 
 int drl_rope_qkv_fwd(const void* qkv, int32_t dt, const int64_t* position_ids, const float* cos_t, const float* sin_t,
                      int64_t maxpos, int64_t B, int64_t T, int64_t Hq, int64_t Hkv, int64_t D, void* q, void* k,
-                     void* v, int64_t Tk, int64_t koff, void* stream) {
+                     void* v, int64_t Tk, int64_t koff, const int64_t* koff_dev, void* stream) {
   using namespace drl;
   DRL_CHECK_ARG(qkv && position_ids && cos_t && sin_t && q && k && v, "NULL input");
   DRL_CHECK_ARG(B >= 1 && T >= 1 && Hq >= 1 && Hkv >= 1 && Hq % Hkv == 0 && D % 2 == 0, "bad shape");
@@ -467,7 +470,7 @@ int drl_rope_qkv_fwd(const void* qkv, int32_t dt, const int64_t* position_ids, c
   const int64_t n = B * T * (Hq + 2 * Hkv) * (D / 2);
   DRL_E_DISPATCH(dt, {
     RopeArgs<E> a{static_cast<const E*>(qkv), position_ids, cos_t, sin_t, static_cast<E*>(q), static_cast<E*>(k),
-                  static_cast<E*>(v), B, T, Hq, Hkv, D, Tk, koff, maxpos};
+                  static_cast<E*>(v), B, T, Hq, Hkv, D, Tk, koff, maxpos, koff_dev};
     hipLaunchKernelGGL(rope_qkv_fwd_kernel<E>, dim3(grid_stride(n)), dim3(256), 0, static_cast<hipStream_t>(stream), a);
   });
   DRL_LAUNCH_CHECK();

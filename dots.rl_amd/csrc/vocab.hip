@@ -271,6 +271,7 @@ struct SelectArgs {
   int n_eos;
   int32_t* unfinished;
   int64_t* out;
+  const int64_t* dev_step;
 };
 
 template <int DT>
@@ -335,7 +336,8 @@ __global__ __launch_bounds__(kThreads) void select_kernel(SelectArgs a) {
     // pass 1: max of z = logit / T (HF TemperatureLogitsWarper on fp32 scores)
     float m, sdummy, tdummy;
     row_softmax_state<DT, false, false>(row, a.V, a.vec, a.temp, true, m, sdummy, tdummy);
-    const uint32_t bits = philox_u32(a.seed, a.offset, static_cast<uint64_t>(a.row_base + r));
+    const uint64_t off = a.offset + (a.dev_step ? static_cast<uint64_t>(*a.dev_step) : 0ull);
+    const uint32_t bits = philox_u32(a.seed, off, static_cast<uint64_t>(a.row_base + r));
     const double u = (static_cast<double>(bits >> 8) + 0.5) * (1.0 / 16777216.0);
     // pass 2/3: inverse CDF. Chunks of kThreads*8 elements, 8 contiguous per lane; every sum is taken
     // in the same fixed order in both passes, so the scan ends exactly at the total.
@@ -406,7 +408,7 @@ __global__ __launch_bounds__(kThreads) void select_kernel(SelectArgs a) {
   if (tid == 0) {
     const bool alive = a.unfinished ? a.unfinished[r] != 0 : true;
     const int64_t tok = alive ? choice : a.pad;
-    a.out[r * a.ld_out] = tok;
+    a.out[r * a.ld_out + (a.dev_step ? *a.dev_step : 0)] = tok;
     if (a.unfinished && alive) {
       for (int k = 0; k < a.n_eos; ++k)
         if (tok == a.eos[k]) { a.unfinished[r] = 0; break; }
@@ -493,6 +495,7 @@ int drl_select_tokens(const void* logits, int32_t dt, int64_t N, int64_t V, int6
   a.do_sample = sample; a.temp = sample ? p->temperature : 1.0f;
   a.seed = p->seed; a.offset = p->offset; a.row_base = p->row_base; a.pad = p->pad_token_id;
   a.eos = p->eos_ids; a.n_eos = p->n_eos; a.unfinished = unfinished; a.out = out_tokens;
+  a.dev_step = p->dev_step;
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (dt == DRL_BF16) hipLaunchKernelGGL(select_kernel<DRL_BF16>, dim3(N), dim3(kThreads), 0, s, a);
   else hipLaunchKernelGGL(select_kernel<DRL_F32>, dim3(N), dim3(kThreads), 0, s, a);

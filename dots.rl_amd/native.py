@@ -7,6 +7,7 @@ in the gfx950 kernels of ``libdotsrl_amd.so``. Tensors must live on the GPU; any
 from __future__ import annotations
 
 import ctypes
+import math
 
 import torch
 
@@ -19,7 +20,63 @@ _LOGIT_DTYPES = {torch.float32: _lib.DRL_F32, torch.bfloat16: _lib.DRL_BF16}
 
 
 def lib():
-    return _lib.load()
+    L = _lib.load()
+    return _TimedLib(L) if _TIMERS else L
+
+
+# ----------------------------------------------------------------------------------------------- timing
+_TIMERS: dict = {}
+
+
+class KernelTimer:
+    """Brackets every launch of one C-ABI entry point with HIP events on the stream it is launched on
+    (the current torch stream, which every wrapper passes to the library) while active; launches recorded
+    into a HIP graph are not timed. ``bytes_fn(args)`` gives the algorithmic bytes of one launch from the
+    entry point's own arguments. Used by bench.py for the roofline of the dominant kernel."""
+
+    def __init__(self, symbol: str, bytes_fn):
+        self.symbol, self.bytes_fn = symbol, bytes_fn
+        self.events, self.nbytes = [], []
+
+    def __enter__(self):
+        _TIMERS[self.symbol] = self
+        return self
+
+    def __exit__(self, *exc):
+        _TIMERS.pop(self.symbol, None)
+
+    def wrap(self, fn):
+        def call(*args):
+            if torch.cuda.is_current_stream_capturing():
+                return fn(*args)
+            s = torch.cuda.current_stream()
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(s)
+            rc = fn(*args)
+            b.record(s)
+            self.events.append((a, b))
+            self.nbytes.append(self.bytes_fn(args))
+            return rc
+        return call
+
+    def summary(self):
+        """(launches, mean seconds per launch, mean algorithmic bytes per launch)."""
+        if not self.events:
+            return 0, float("nan"), float("nan")
+        self.events[-1][1].synchronize()
+        tot = sum(a.elapsed_time(b) for a, b in self.events) * 1e-3
+        n = len(self.events)
+        return n, tot / n, sum(self.nbytes) / n
+
+
+class _TimedLib:
+    def __init__(self, real):
+        self._real = real
+
+    def __getattr__(self, name):
+        fn = getattr(self._real, name)
+        t = _TIMERS.get(name)
+        return fn if t is None else t.wrap(fn)
 
 
 def _stream():
@@ -190,8 +247,11 @@ def gae_advantage_return(token_level_rewards, values, response_mask, gamma, lam)
 
 # ----------------------------------------------------------------------------------------------- K4
 def select_tokens(logits, out_tokens, *, do_sample=False, temperature=1.0, top_k=0, top_p=1.0, seed=0, step=0,
-                  row_base=0, pad_token_id=0, eos_ids=None, unfinished=None):
-    """Pick one token per row into ``out_tokens`` (int64 view with any row stride, e.g. responses[:, t])."""
+                  row_base=0, pad_token_id=0, eos_ids=None, unfinished=None, dev_step=None):
+    """Pick one token per row into ``out_tokens`` (int64 view with any row stride, e.g. responses[:, t]).
+
+    ``dev_step`` (device int64 scalar s): the Philox offset becomes step + s and row n's token goes to
+    ``out_tokens[n * stride + s]`` — the graph-captured decode loop passes ``responses[:, 0]`` and s."""
     _dev(logits, out_tokens, eos_ids, unfinished)
     lg = _logits_2d(logits)
     N, V = lg.shape
@@ -200,7 +260,8 @@ def select_tokens(logits, out_tokens, *, do_sample=False, temperature=1.0, top_k
     prm = _lib.SamplingParams(int(bool(do_sample)), float(temperature), int(top_k), float(top_p),
                               int(seed) & 0xFFFFFFFFFFFFFFFF, int(step), int(row_base), int(pad_token_id),
                               None if eos_ids is None else eos_ids.data_ptr(),
-                              0 if eos_ids is None else eos_ids.numel())
+                              0 if eos_ids is None else eos_ids.numel(),
+                              None if dev_step is None else dev_step.data_ptr())
     check(lib().drl_select_tokens(_p(lg), _LOGIT_DTYPES[lg.dtype], N, V, lg.stride(0), ctypes.byref(prm),
                                   _p(unfinished), _p(out_tokens), ld_out, _stream()), "drl_select_tokens")
     return out_tokens
@@ -266,11 +327,14 @@ def _edt(t):
         raise ValueError(f"activation dtype {t.dtype} not supported (bfloat16 / float32)") from e
 
 
-def rope_qkv_fwd(qkv, position_ids, cos_t, sin_t, Hq, Hkv, D, q, k, v, koff=0):
-    """qkv (B,T,(Hq+2Hkv)D) -> q (B,Hkv,G,T,D); k, v written at [:, :, koff:koff+T] of (B,Hkv,Tk,D)."""
+def rope_qkv_fwd(qkv, position_ids, cos_t, sin_t, Hq, Hkv, D, q, k, v, koff=0, koff_dev=None):
+    """qkv (B,T,(Hq+2Hkv)D) -> q (B,Hkv,G,T,D); k, v written at [:, :, koff:koff+T] of (B,Hkv,Tk,D).
+
+    ``koff_dev`` (device int64 scalar) replaces ``koff`` for graph-captured decode steps."""
     B, T = qkv.shape[0], qkv.shape[1]
     check(lib().drl_rope_qkv_fwd(_p(qkv), _edt(qkv), _p(position_ids), _p(cos_t), _p(sin_t), cos_t.shape[0], B, T,
-                                 Hq, Hkv, D, _p(q), _p(k), _p(v), k.shape[2], koff, _stream()), "drl_rope_qkv_fwd")
+                                 Hq, Hkv, D, _p(q), _p(k), _p(v), k.shape[2], koff, _p(koff_dev), _stream()),
+          "drl_rope_qkv_fwd")
 
 
 def rope_qkv_bwd(dq, dk, dv, position_ids, cos_t, sin_t, Hq, Hkv, D, dqkv):
@@ -316,3 +380,20 @@ def swiglu_bwd(gate_up, dout, dgate_up):
     N, I2 = gate_up.numel() // gate_up.shape[-1], gate_up.shape[-1]
     check(lib().drl_swiglu_bwd(_p(gate_up), _p(dout), _p(dgate_up), _edt(gate_up), N, I2 // 2, _stream()),
           "drl_swiglu_bwd")
+
+
+def decode_attention(q, k_cache, v_cache, key_valid, L, out, qpos=None, qpos_dev=None, split=True):
+    """q (B,Hkv,G,D) one token; caches (B,Hkv,Tk,D); keys j < L with key_valid[b,j] and j <= qpos -> out."""
+    _dev(q, k_cache, v_cache, key_valid, out)
+    B, Hkv, G, D = q.shape
+    Tk = k_cache.shape[2]
+    assert k_cache.is_contiguous() and v_cache.is_contiguous() and q.is_contiguous() and out.is_contiguous()
+    assert key_valid.dtype == torch.uint8 and key_valid.stride(1) == 1 and key_valid.shape[0] == B
+    qp = L - 1 if qpos is None else int(qpos)
+    Lb = lib()
+    nb = Lb.drl_decode_attention_workspace_bytes(B, Hkv, G, D, L) if split else 0
+    ws = _ws.get(nb, q.device) if nb else None
+    check(Lb.drl_decode_attention(_p(q), _p(k_cache), _p(v_cache), _edt(q), _p(key_valid), key_valid.stride(0),
+                                  _p(qpos_dev), qp, B, Hkv, G, D, Tk, L, 1.0 / math.sqrt(D), _p(out), _p(ws), nb,
+                                  _stream()), "drl_decode_attention")
+    return out

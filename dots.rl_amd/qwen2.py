@@ -215,10 +215,11 @@ class _Embedding(torch.autograd.Function):
 
 
 # --------------------------------------------------------------------------------------------- decoder layer
-def _layer_forward(m, i, x_prev, delta, pos, key_valid, save, cache=None, koff=0):
+def _layer_forward(m, i, x_prev, delta, pos, key_valid, save, cache=None, koff=0, koff_dev=None):
     """x = x_prev (+ delta); returns (x2 = x + attn(x), mlp_out) — the next consumer adds them.
 
-    ``save`` (dict or None) receives the activations the hand-written backward needs."""
+    ``save`` (dict or None) receives the activations the hand-written backward needs. ``koff_dev`` (device
+    int64 (1,)) is the cache position of a single decode token kept on the device (graph capture)."""
     cfg, s, dt = m.cfg, m.store, m.dtype
     B, T, H = x_prev.shape
     Hq, Hkv, D = cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim
@@ -239,17 +240,29 @@ def _layer_forward(m, i, x_prev, delta, pos, key_valid, save, cache=None, koff=0
         koff = 0
     else:
         kbuf, vbuf = cache.k[i], cache.v[i]
-    native.rope_qkv_fwd(qkv, pos, m.cos, m.sin, Hq, Hkv, D, q, kbuf, vbuf, koff)
+    native.rope_qkv_fwd(qkv, pos, m.cos, m.sin, Hq, Hkv, D, q, kbuf, vbuf, koff, koff_dev)
     L = koff + T
-    k3 = kbuf[:, :, :L].reshape(B * Hkv, L, D)
-    v3 = vbuf[:, :, :L].reshape(B * Hkv, L, D)
-    q3 = q.view(B * Hkv, G * T, D)
-    S = bmm_f32(q3, k3.transpose(1, 2))  # (B*Hkv, G*T, L) fp32 scores
-    P = torch.empty(B * Hkv, G * T, L, dtype=dt, device=dev)
-    native.masked_softmax_fwd(S, P, key_valid, B, Hkv * G, T, L, L - T, 1.0 / math.sqrt(D))
-    del S
-    O = torch.bmm(P, v3)  # (B*Hkv, G*T, D)
-    if T == 1:
+    if cache is not None and T == 1:
+        # one new token: fused GQA decode attention streams the cache once (csrc/attention.hip)
+        attn = torch.empty(B, 1, Hq * D, dtype=dt, device=dev)
+        if koff_dev is None:
+            native.decode_attention(q.view(B, Hkv, G, D), kbuf, vbuf, key_valid, L, attn)
+        else:  # keys [0, koff_dev] of the whole cache; the kernel stops at the device position
+            native.decode_attention(q.view(B, Hkv, G, D), kbuf, vbuf, key_valid, kbuf.shape[2], attn,
+                                    qpos_dev=koff_dev)
+        P = None
+    else:
+        k3 = kbuf[:, :, :L].reshape(B * Hkv, L, D)
+        v3 = vbuf[:, :, :L].reshape(B * Hkv, L, D)
+        q3 = q.view(B * Hkv, G * T, D)
+        S = bmm_f32(q3, k3.transpose(1, 2))  # (B*Hkv, G*T, L) fp32 scores
+        P = torch.empty(B * Hkv, G * T, L, dtype=dt, device=dev)
+        native.masked_softmax_fwd(S, P, key_valid, B, Hkv * G, T, L, L - T, 1.0 / math.sqrt(D))
+        del S
+        O = torch.bmm(P, v3)  # (B*Hkv, G*T, D)
+    if P is None:
+        pass
+    elif T == 1:
         attn = O.view(B, 1, Hq * D)
     else:
         attn = O.view(B, Hkv, G, T, D).permute(0, 3, 1, 2, 4).reshape(B, T, Hq * D)
@@ -438,6 +451,18 @@ class Qwen2Model:
         for i in range(cfg.num_hidden_layers):
             x, delta = _layer_forward(self, i, x, delta, pos, cache.valid, None, cache, t)
         cache.len = t + 1
+        return self._final_norm(x, delta)[:, 0]
+
+    @torch.no_grad()
+    def decode_step_dev(self, cache: KVCache, tokens, positions, kpos_dev):
+        """decode_step with the cache position in device memory (int64 (1,)): every shape and address is
+        static, so the step can be captured once into a HIP graph and replayed for each response token."""
+        x = F.embedding(tokens.view(-1, 1), self.store.w("embed_tokens")).to(torch.float32)
+        cache.valid.index_fill_(1, kpos_dev, 1)
+        pos = positions.view(-1, 1)
+        delta = None
+        for i in range(self.cfg.num_hidden_layers):
+            x, delta = _layer_forward(self, i, x, delta, pos, cache.valid, None, cache, 0, koff_dev=kpos_dev)
         return self._final_norm(x, delta)[:, 0]
 
 

@@ -73,14 +73,16 @@ class MI355XRollout:
         last_pos = position_ids[:, -1]
         seed = int(cfg.get("seed", 0)) + 7919 * self.calls
         row_base = self.dp_rank * (1 << 32) + row_offset
-        for t in range(R):
-            logits = m.logits(h)
-            native.select_tokens(logits, responses[:, t], do_sample=do_sample and temperature > 0,
-                                 temperature=temperature if do_sample else 1.0, top_k=top_k, top_p=top_p, seed=seed,
-                                 step=t, row_base=row_base, pad_token_id=pad_token_id, eos_ids=stop_ids,
-                                 unfinished=unfinished)
-            if t + 1 < R:
-                h = m.decode_step(cache, responses[:, t], last_pos + 1 + t)
+        sel = dict(do_sample=do_sample and temperature > 0, temperature=temperature if do_sample else 1.0, top_k=top_k,
+                   top_p=top_p, seed=seed, row_base=row_base, pad_token_id=pad_token_id, eos_ids=stop_ids,
+                   unfinished=unfinished)
+        native.select_tokens(m.logits(h), responses[:, 0], step=0, **sel)
+        if cfg.get("use_hip_graph", True) and R > 2:
+            self._decode_graphed(cache, responses, last_pos, P, R, sel)
+        else:
+            for t in range(1, R):
+                h = m.decode_step(cache, responses[:, t - 1], last_pos + t)
+                native.select_tokens(m.logits(h), responses[:, t], step=t, **sel)
         del cache
         seq = torch.cat([idx, responses], dim=-1)
         # hf_rollout.py:151-160: positions continue from the last prompt position; mask up to first EOS
@@ -96,3 +98,28 @@ class MI355XRollout:
             "position_ids": full_pos,
         }, batch_size=B)
         return DataProto(batch=batch)
+
+    def _decode_graphed(self, cache, responses, last_pos, P, R, sel):
+        """Response tokens 1..R-1 as replays of ONE captured decode step.
+
+        The step's only changing inputs live in device memory: the step counter t (token t-1 is read from
+        ``responses``, written at cache position P+t-1, rotated at position last_pos+t; token t is selected
+        into ``responses[:, t]`` with Philox offset t), so ~270 kernel launches per token become one graph
+        launch and the host never waits on the device inside the loop. Step 1 runs eagerly (warms the GEMM
+        heuristics for the decode shapes, outside capture); the captured body advances t itself."""
+        m = self.module
+        t_dev = torch.ones(1, dtype=torch.int64, device=responses.device)
+
+        def body():
+            tok = responses.index_select(1, t_dev - 1)
+            h = m.decode_step_dev(cache, tok, last_pos + t_dev, t_dev + (P - 1))
+            native.select_tokens(m.logits(h), responses[:, 0], step=0, dev_step=t_dev, **sel)
+            t_dev.add_(1)
+
+        body()  # t = 1, eager
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            body()
+        for _ in range(2, R):
+            graph.replay()
+        del graph

@@ -168,6 +168,9 @@ typedef struct drl_sampling_params {
   int64_t pad_token_id;
   const int64_t* eos_ids; /* device int64[n_eos]; may be NULL when n_eos == 0 */
   int32_t n_eos;
+  /* optional device int64 scalar s (graph-captured decode loops): when non-NULL the Philox offset is
+   * offset + s and the token is written to out_tokens[n * ld_out + s]. */
+  const int64_t* dev_step;
 } drl_sampling_params;
 
 int drl_select_tokens(const void* logits, int32_t logits_dtype, int64_t N, int64_t V, int64_t ld,
@@ -215,10 +218,12 @@ int drl_adamw_step(float* params, const float* grads, float* exp_avg, float* exp
  * DRL_F32 for the parity model); the residual stream and norm weights are always float32.
  * ---------------------------------------------------------------------------------------------- */
 /* qkv (B,T,(Hq+2Hkv)*D) -> RoPE'd q in grouped layout (B,Hkv,Hq/Hkv,T,D), RoPE'd k and v written at
- * key offset koff of (B,Hkv,Tk,D) buffers (the KV cache when decoding). cos/sin: (maxpos, D/2) fp32. */
+ * key offset koff of (B,Hkv,Tk,D) buffers (the KV cache when decoding). cos/sin: (maxpos, D/2) fp32.
+ * koff_dev (optional device int64 scalar) replaces koff — graph-captured decode steps; an out-of-range
+ * device offset writes nothing. */
 int drl_rope_qkv_fwd(const void* qkv, int32_t dt, const int64_t* position_ids, const float* cos_t, const float* sin_t,
                      int64_t maxpos, int64_t B, int64_t T, int64_t Hq, int64_t Hkv, int64_t D, void* q, void* k,
-                     void* v, int64_t Tk, int64_t koff, void* stream);
+                     void* v, int64_t Tk, int64_t koff, const int64_t* koff_dev, void* stream);
 int drl_rope_qkv_bwd(const void* dq, const void* dk, const void* dv, int32_t dt, const int64_t* position_ids,
                      const float* cos_t, const float* sin_t, int64_t maxpos, int64_t B, int64_t T, int64_t Hq,
                      int64_t Hkv, int64_t D, void* dqkv, void* stream);
@@ -241,6 +246,20 @@ int drl_rmsnorm_bwd(const float* x, const float* weight, const float* rstd, cons
 int drl_swiglu_fwd(const void* gate_up, void* out, int32_t dt, int64_t N, int64_t I, void* stream);
 int drl_swiglu_bwd(const void* gate_up, const void* dout, void* dgate_up, int32_t dt, int64_t N, int64_t I,
                    void* stream);
+
+/* ---- decode attention (rollout engine; replaces the per-token attention of HF generate,
+ *      hf_rollout.py:112-124 -> Qwen2Attention with the KV cache).
+ * q (B, Hkv, G, D) for one new token; k/v cache (B, Hkv, Tk, D), keys [0, L) used; a key j is attended iff
+ * key_valid[b*ld_valid + j] && j <= qpos, where qpos = *qpos_ptr if qpos_ptr != NULL (device scalar, for
+ * graph capture) else qpos. out (B, Hkv, G, D) == (B, Hq*D). A row with no allowed key writes zeros.
+ * With a workspace of drl_decode_attention_workspace_bytes(B, Hkv, G, D, L) and fewer (b, kv head) pairs
+ * than CUs, the key range is split over more workgroups (split-K + fixed-order merge); otherwise a single
+ * pass per (b, kv head) runs. */
+size_t drl_decode_attention_workspace_bytes(int64_t B, int64_t Hkv, int64_t G, int64_t D, int64_t L);
+int drl_decode_attention(const void* q, const void* k_cache, const void* v_cache, int32_t dt, const uint8_t* key_valid,
+                         int64_t ld_valid, const int64_t* qpos_ptr, int64_t qpos, int64_t B, int64_t Hkv, int64_t G,
+                         int64_t D, int64_t Tk, int64_t L, float scale, void* out, void* workspace,
+                         size_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }

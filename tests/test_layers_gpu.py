@@ -1,0 +1,187 @@
+"""Transformer-layer HIP kernels (csrc/layers.hip, csrc/attention.hip) against plain PyTorch fp32 references.
+
+The model-level tests (test_model_gpu.py) check these kernels composed into Qwen2 against HF; this file
+pins each kernel on its own, including ragged masks (left padding, masked-out rows) and sizes that cross
+the kernels' chunk boundaries. fp32 runs must agree to ~1e-5 relative; bf16 runs to bf16 rounding.
+"""
+
+import math
+
+import pytest
+import torch
+
+from dots.rl_amd import native
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _tol(dt):
+    return dict(rtol=1e-5, atol=1e-5) if dt == torch.float32 else dict(rtol=2e-2, atol=2e-2)
+
+
+def _rope_tables(D, maxpos=4096, theta=1e4):
+    inv = 1.0 / (theta ** (torch.arange(0, D, 2, device=DEV).float() / D))
+    f = torch.arange(maxpos, device=DEV).float()[:, None] * inv[None]
+    return f.cos().contiguous(), f.sin().contiguous()
+
+
+def _rot(x, c, s):  # HF rotate_half RoPE; x (..., D), c/s (..., D/2)
+    h = x.shape[-1] // 2
+    x1, x2 = x[..., :h], x[..., h:]
+    return torch.cat([x1 * c - x2 * s, x2 * c + x1 * s], -1)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_rope_qkv_forward_backward(dt):
+    B, T, Hq, Hkv, D, Tk, koff = 3, 37, 14, 2, 64, 50, 9
+    G = Hq // Hkv
+    g = torch.Generator(device=DEV).manual_seed(0)
+    qkv = torch.randn(B, T, (Hq + 2 * Hkv) * D, device=DEV, generator=g).to(dt)
+    pos = torch.randint(0, 4000, (B, T), device=DEV, generator=g)
+    cos, sin = _rope_tables(D)
+    q = torch.empty(B, Hkv, G, T, D, device=DEV, dtype=dt)
+    k = torch.zeros(B, Hkv, Tk, D, device=DEV, dtype=dt)
+    v = torch.zeros_like(k)
+    native.rope_qkv_fwd(qkv, pos, cos, sin, Hq, Hkv, D, q, k, v, koff)
+    if dt == torch.float32:  # device-side key offset (graph-captured decode) writes the same slots
+        k2 = torch.zeros_like(k)
+        v2 = torch.zeros_like(v)
+        native.rope_qkv_fwd(qkv, pos, cos, sin, Hq, Hkv, D, torch.empty_like(q), k2, v2, 0, torch.tensor([koff], device=DEV))
+        assert torch.equal(k2, k) and torch.equal(v2, v)
+    x = qkv.float().view(B, T, Hq + 2 * Hkv, D)
+    c, s = cos[pos][:, :, None], sin[pos][:, :, None]
+    rq = _rot(x[:, :, :Hq], c, s)  # (B,T,Hq,D)
+    rk = _rot(x[:, :, Hq:Hq + Hkv], c, s)
+    torch.testing.assert_close(q.float(), rq.view(B, T, Hkv, G, D).permute(0, 2, 3, 1, 4), **_tol(dt))
+    torch.testing.assert_close(k[:, :, koff:koff + T].float(), rk.permute(0, 2, 1, 3), **_tol(dt))
+    assert torch.equal(v[:, :, koff:koff + T], qkv.view(B, T, -1, D)[:, :, Hq + Hkv:].permute(0, 2, 1, 3))
+    assert not k[:, :, :koff].any() and not k[:, :, koff + T:].any()
+    # backward = transpose rotation; check against autograd of the fp32 reference
+    dq = torch.randn(B, Hkv, G, T, D, device=DEV, generator=g).to(dt)
+    dk = torch.randn(B, Hkv, T, D, device=DEV, generator=g).to(dt)
+    dv = torch.randn(B, Hkv, T, D, device=DEV, generator=g).to(dt)
+    dqkv = torch.empty(B, T, (Hq + 2 * Hkv) * D, device=DEV, dtype=dt)
+    native.rope_qkv_bwd(dq, dk, dv, pos, cos, sin, Hq, Hkv, D, dqkv)
+    xr = qkv.float().requires_grad_(True)
+    xv = xr.view(B, T, Hq + 2 * Hkv, D)
+    oq = _rot(xv[:, :, :Hq], c, s).view(B, T, Hkv, G, D).permute(0, 2, 3, 1, 4)
+    ok = _rot(xv[:, :, Hq:Hq + Hkv], c, s).permute(0, 2, 1, 3)
+    ov = xv[:, :, Hq + Hkv:].permute(0, 2, 1, 3)
+    torch.autograd.backward([oq, ok, ov], [dq.float(), dk.float(), dv.float()])
+    torch.testing.assert_close(dqkv.float(), xr.grad, **_tol(dt))
+
+
+def _ref_masked_softmax(S, valid, Tq, qoff, scale):
+    """HF semantics: allowed = valid[b, j] & (j <= q + qoff); a fully-masked row is uniform over all keys."""
+    B, HG, _, Tk = S.shape
+    j = torch.arange(Tk, device=DEV)
+    qi = torch.arange(Tq, device=DEV)[:, None]
+    allowed = (valid[:, None, None, :].bool()) & (j[None, None, None, :] <= qi[None, None] + qoff)
+    z = torch.where(allowed, S * scale, torch.full_like(S, torch.finfo(torch.float32).min))
+    return torch.softmax(z, -1)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("Tq,Tk,qoff", [(1, 700, 699), (33, 33, 0), (64, 300, 236), (5, 5000, 4995)])
+def test_masked_softmax_forward_backward(dt, Tq, Tk, qoff):
+    B, HG, scale = 3, 4, 0.125
+    g = torch.Generator(device=DEV).manual_seed(Tk)
+    S = torch.randn(B, HG, Tq, Tk, device=DEV, generator=g) * 4
+    valid = torch.ones(B, Tk, dtype=torch.uint8, device=DEV)
+    valid[0, :7] = 0  # left padding
+    valid[1, : Tk // 2] = 0
+    valid[2, :] = 0  # every row of batch 2 fully masked -> uniform
+    P = torch.empty(B, HG, Tq, Tk, device=DEV, dtype=dt)
+    native.masked_softmax_fwd(S, P, valid, B, HG, Tq, Tk, qoff, scale)
+    ref = _ref_masked_softmax(S, valid, Tq, qoff, scale)
+    torch.testing.assert_close(P.float(), ref, rtol=1e-5 if dt == torch.float32 else 1e-2, atol=1e-6 if dt == torch.float32 else 4e-3)
+    dP = torch.randn(B, HG, Tq, Tk, device=DEV, generator=g)
+    dS = torch.empty_like(P)
+    native.masked_softmax_bwd(P, dP, dS, B * HG * Tq, Tk, scale)
+    Pf = P.float()
+    ref_dS = Pf * (dP - (Pf * dP).sum(-1, keepdim=True)) * scale
+    torch.testing.assert_close(dS.float(), ref_dS, **_tol(dt))
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("with_delta", [False, True])
+def test_add_rmsnorm_forward_backward(dt, with_delta):
+    N, H, eps = 77, 896, 1e-6
+    g = torch.Generator(device=DEV).manual_seed(1)
+    x_in = torch.randn(N, H, device=DEV, generator=g)
+    delta = torch.randn(N, H, device=DEV, generator=g).to(dt) if with_delta else None
+    w = torch.rand(H, device=DEV, generator=g) + 0.5
+    x_out = torch.empty_like(x_in) if with_delta else None
+    y = torch.empty(N, H, device=DEV, dtype=dt)
+    rstd = torch.empty(N, device=DEV)
+    native.add_rmsnorm_fwd(x_in, delta, x_out, w, y, rstd, eps)
+    x = x_in + (delta.float() if with_delta else 0)
+    r = torch.rsqrt(x.pow(2).mean(-1, keepdim=True) + eps)
+    torch.testing.assert_close(rstd, r[:, 0], rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(y.float(), (w * (x * r)), **_tol(dt))
+    if with_delta:
+        torch.testing.assert_close(x_out, x, rtol=0, atol=0)
+    # backward accumulates into dx / dw
+    dy = torch.randn(N, H, device=DEV, generator=g).to(dt)
+    dx = torch.ones(N, H, device=DEV)
+    dw = torch.ones(H, device=DEV)
+    native.rmsnorm_bwd(x, w, rstd, dy, dx, dw)
+    xr = x.clone().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    out = wr * (xr * torch.rsqrt(xr.pow(2).mean(-1, keepdim=True) + eps))
+    out.backward(dy.float())
+    torch.testing.assert_close(dx, 1 + xr.grad, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(dw, 1 + wr.grad, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_swiglu_forward_backward(dt):
+    N, I = 131, 4864
+    g = torch.Generator(device=DEV).manual_seed(2)
+    gu = (torch.randn(N, 2 * I, device=DEV, generator=g) * 3).to(dt)
+    a = torch.empty(N, I, device=DEV, dtype=dt)
+    native.swiglu_fwd(gu, a)
+    gr = gu.float().requires_grad_(True)
+    ref = torch.nn.functional.silu(gr[:, :I]) * gr[:, I:]
+    torch.testing.assert_close(a.float(), ref.detach(), **_tol(dt))
+    da = torch.randn(N, I, device=DEV, generator=g).to(dt)
+    dgu = torch.empty_like(gu)
+    native.swiglu_bwd(gu, da, dgu)
+    ref.backward(da.float())
+    torch.testing.assert_close(dgu.float(), gr.grad, **_tol(dt))
+
+
+def _ref_decode(q, k, v, valid, L, qpos):
+    B, Hkv, G, D = q.shape
+    S = torch.einsum("bhgd,bhtd->bhgt", q.float(), k[:, :, :L].float()) / math.sqrt(D)
+    j = torch.arange(L, device=DEV)
+    allowed = valid[:, None, None, :L].bool() & (j <= qpos)
+    S = S.masked_fill(~allowed, float("-inf"))
+    P = torch.softmax(S, -1).nan_to_num(0.0)  # a row with no allowed key: the kernel writes zeros
+    return torch.einsum("bhgt,bhtd->bhgd", P, v[:, :, :L].float())
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B,Hkv,G,D,Tk,L", [(4, 2, 7, 64, 768, 513), (3, 2, 7, 64, 300, 1), (2, 4, 4, 128, 1100, 1100),
+                                            (300, 2, 7, 64, 768, 700),
+                                            (5, 1, 8, 32, 256, 256)])
+def test_decode_attention(dt, B, Hkv, G, D, Tk, L):
+    g = torch.Generator(device=DEV).manual_seed(L)
+    q = torch.randn(B, Hkv, G, D, device=DEV, generator=g).to(dt)
+    k = torch.randn(B, Hkv, Tk, D, device=DEV, generator=g).to(dt)
+    v = torch.randn(B, Hkv, Tk, D, device=DEV, generator=g).to(dt)
+    valid = torch.zeros(B, Tk, dtype=torch.uint8, device=DEV)
+    valid[:, :L] = 1
+    for b in range(B):  # ragged left padding; the newest key (L-1) is always valid
+        valid[b, : min(3 * b, L - 1)] = 0
+    out = torch.empty(B, Hkv, G, D, device=DEV, dtype=dt)
+    ref = _ref_decode(q, k, v, valid, L, L - 1)
+    for split in (True, False):  # split-K + merge (small grids), and the single-pass form
+        native.decode_attention(q, k, v, valid, L, out, split=split)
+        torch.testing.assert_close(out.float(), ref, **_tol(dt))
+    # device-side query position (graph-capturable form) and a position short of L
+    if L > 4:
+        qp = torch.tensor([L - 4], device=DEV)
+        native.decode_attention(q, k, v, valid, L, out, qpos_dev=qp)
+        torch.testing.assert_close(out.float(), _ref_decode(q, k, v, valid, L, L - 4), **_tol(dt))

@@ -131,3 +131,41 @@ def test_masks_and_positions_match_reference(golden):
 def test_greedy_first_index_tie_break():
     # torch.argmax semantics the reference relies on (argmax([3,3,1]) == 0)
     assert oracle.greedy(np.array([[3.0, 3.0, 1.0], [0.0, 1.0, 1.0]])).tolist() == [0, 1]
+
+
+def _tiny_cfg_and_params():
+    import json
+    import os
+    import types
+
+    import torch
+    from safetensors.torch import load_file
+
+    from oracle import qwen2_ref
+
+    d = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "tiny_qwen2")
+    c = json.load(open(os.path.join(d, "config.json")))
+    cfg = types.SimpleNamespace(**c)
+    cfg.head_dim = cfg.hidden_size // cfg.num_attention_heads
+    return cfg, qwen2_ref.load_hf_state_dict(cfg, load_file(os.path.join(d, "model.safetensors")))
+
+
+def test_qwen2_restatement_matches_reference_model(golden):
+    """oracle.qwen2_ref (the CPU model used by GPU parity tests and the CPU baseline) reproduces the
+    reference's HF model: greedy rollout tokens bit-exact, log-probs / entropy to fp32 rounding."""
+    import torch
+
+    from oracle import qwen2_ref
+
+    z, meta = golden("tiny_qwen2_rollout.npz")
+    cfg, P = _tiny_cfg_and_params()
+    t = lambda k: torch.from_numpy(np.ascontiguousarray(z[k]))  # noqa: E731
+    resp = qwen2_ref.generate_greedy(cfg, P, t("prompt_ids"), t("prompt_attention_mask"), t("prompt_position_ids"),
+                                     meta["response_length"], [meta["eos_token_id"]], meta["pad_token_id"])
+    np.testing.assert_array_equal(resp.numpy(), z["responses"])
+    ids, am, pos, r = t("sequences"), t("attention_mask"), t("position_ids"), t("responses")
+    lp, ent = qwen2_ref.logp_entropy(cfg, P, ids, am, pos, r)
+    np.testing.assert_allclose(lp.numpy(), z["log_probs"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(ent.numpy(), z["entropy"], rtol=1e-5, atol=1e-5)
+    lp7, _ = qwen2_ref.logp_entropy(cfg, P, ids, am, pos, r, temperature=0.7)
+    np.testing.assert_allclose(lp7.numpy(), z["log_probs_t07"], rtol=1e-5, atol=1e-5)

@@ -7,6 +7,7 @@ Algorithmic bytes per unit:
   K2 logprob bwd      : 4V + 8+16 B / row (read bf16 logits, write bf16 dlogits; per-row scalars)
   K4 select (greedy)  : 2V + 8 B / row
   AdamW step          : 28 B / param (+2 B bf16 copy) ; grad norm : 4 B / param
+  decode attention    : 4 D B / key (K and V rows, bf16) per (sequence, KV head) + q/out rows
 Usage: python tools/kernel_bench.py [--quick] > out.jsonl
 """
 
@@ -101,10 +102,28 @@ def adam(n=494_032_768):
     return res
 
 
+def decode_attn(B=512, Hkv=2, G=7, D=64, Tk=768, L=640):
+    dev = "cuda"
+    q = torch.randn(B, Hkv, G, D, device=dev, dtype=torch.bfloat16)
+    k = torch.randn(B, Hkv, Tk, D, device=dev, dtype=torch.bfloat16)
+    v = torch.randn_like(k)
+    valid = torch.ones(B, Tk, dtype=torch.uint8, device=dev)
+    out = torch.empty_like(q)
+    t = time_it(lambda: native.decode_attention(q, k, v, valid, L, out), iters=50)
+    nbytes = B * Hkv * (2 * L * D * 2 + 2 * G * D * 2)
+    return [dict(kernel="A3_decode_attention", B=B, L=L, seconds=t, GBps=nbytes / t / 1e9, frac=nbytes / t / PEAK_HBM)]
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--quick", action="store_true")
+    ap.add_argument("--only", default=None)
     args = ap.parse_args()
+    if args.only == "decode":
+        for L in (513, 640, 768):
+            for r in decode_attn(L=L):
+                print(json.dumps(r), flush=True)
+        sys.exit(0)
     exps = [17, 20, 22, 24] if args.quick else [17, 18, 20, 22, 23, 24, 25, 26]
     for r in k1_sweep(exps) + k2(1024 if args.quick else 4096) + adam(1 << 24 if args.quick else 494_032_768):
         print(json.dumps(r), flush=True)
