@@ -103,21 +103,29 @@ __device__ __forceinline__ void grid_barrier(unsigned* counter, unsigned expecte
   __syncthreads();
 }
 
-// "Last workgroup to arrive" ticket: every workgroup publishes its partials, then takes a ticket; the
-// one that draws gridDim-1 reduces all partials in a fixed order (bitwise-reproducible result).
-// Returns true in every thread of the last workgroup.
+// "Last workgroup to arrive" ticket over write-through partials (cdna_hip_programming.md §6 G16, R1):
+// every workgroup stores its partials with store_sc1 (write-through, so no release fence and no L2
+// write-back per workgroup, which cost K1 ~30 us at 2^26 tokens), drains them (s_waitcnt vmcnt(0) in
+// every storing wave, then the barrier) and takes a relaxed agent-scope ticket; the one that draws
+// gridDim-1 reads ALL partials with load_sc1 (bypassing its possibly stale L1, no acquire) and reduces
+// them in a fixed order (bitwise-reproducible result). Returns true in every thread of that workgroup.
+typedef __attribute__((address_space(1))) unsigned long long gu64_t;  // global (not flat) accesses; C casts below
+__device__ __forceinline__ void store_sc1(double* p, double v) {
+  __hip_atomic_store((gu64_t*)(p), static_cast<unsigned long long>(__double_as_longlong(v)),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double load_sc1(const double* p) {
+  return __longlong_as_double(static_cast<long long>(
+      __hip_atomic_load((const gu64_t*)(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
+}
 __device__ __forceinline__ bool last_block_ticket(unsigned* ticket) {
   __shared__ int is_last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned t = __hip_atomic_fetch_add((__attribute__((address_space(1))) unsigned*)(ticket),
+                                              1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     is_last = (t == gridDim.x - 1);
-    if (is_last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
   }
   __syncthreads();
   return is_last != 0;

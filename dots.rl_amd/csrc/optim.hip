@@ -39,11 +39,11 @@ __global__ __launch_bounds__(kThreads) void sumsq_kernel(const float* g, int64_t
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if (lane == 0) red[wave] = acc;
   __syncthreads();
-  if (threadIdx.x == 0) partials[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+  if (threadIdx.x == 0) store_sc1(partials + blockIdx.x, red[0] + red[1] + red[2] + red[3]);
   if (last_block_ticket(&hdr->ticket)) {
     if (threadIdx.x == 0) {
       double s = 0.0;
-      for (unsigned b = 0; b < gridDim.x; ++b) s += partials[b];
+      for (unsigned b = 0; b < gridDim.x; ++b) s += load_sc1(partials + b);
       *out_norm = static_cast<float>(sqrt(s));
     }
   }

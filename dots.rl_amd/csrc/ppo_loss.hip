@@ -2,11 +2,11 @@
 // one pass over HBM. Replaces dp_actor.py:419-466 (+ core_algos.py:703-736, 815-889, 1272-1307).
 //
 // Layout: the (B, R) float32 inputs are flattened to N = B*R tokens in 1024-token chunks; each workgroup
-// (<= 4 per CU) owns a contiguous run of chunks and walks it 4 tokens per lane (16-B loads, 1 KiB per
-// wave-instruction per input).
+// (<= 8 per CU, all resident) owns a contiguous run of chunks and walks it 4 tokens per lane (16-B
+// nontemporal loads/stores, 1 KiB per wave-instruction per stream).
 // token-mean needs the global mask count before any gradient can be written. K1a streams ONLY the mask
 // (8 B/token for int64), writes it back as a 1-bit image (N/8 bytes, one 64-bit ballot per wave and
-// element slot) plus fixed-order partial counts; K1b sums those counts, reads the other inputs and the
+// element slot) and folds the count (fixed order, last workgroup); K1b reads that count, the other inputs and the
 // bit image (1/8 B/token instead of 8) and writes the gradients: 36.25 B/token of traffic for 36 B/token
 // of algorithmic bytes, no grid barrier. The other modes know their gradient weights up front
 // (seq-mean-token-mean gets per-row counts from a small pre-pass) and run K1b alone. Forward scalars:
@@ -20,12 +20,26 @@ namespace {
 constexpr int kThreads = 256;
 constexpr int kChunk = kThreads * 4;  // 1024 tokens: one workgroup iteration, 16 mask words (4 waves x 4 slots)
 constexpr int kNumPartials = 8;
+#ifndef DRL_K1_PACK_U
+#define DRL_K1_PACK_U 4
+#endif
+
+// every K1 byte is touched once: nontemporal (streaming) loads and stores keep it out of the caches'
+// way (measured on the 5-read/2-write shape: 5.16 -> 5.49 TB/s, tools/hbm_probe.hip)
+typedef float nt_f4 __attribute__((ext_vector_type(4)));
+typedef long long nt_i2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ nt_f4 ldnt(const float* p) { return __builtin_nontemporal_load(reinterpret_cast<const nt_f4*>(p)); }
+__device__ __forceinline__ nt_i2 ldnt(const int64_t* p) { return __builtin_nontemporal_load(reinterpret_cast<const nt_i2*>(p)); }
+__device__ __forceinline__ void stnt(float* p, nt_f4 v) { __builtin_nontemporal_store(v, reinterpret_cast<nt_f4*>(p)); }
 
 
 struct Header {  // zeroed on the stream before every call
   unsigned ticket;
   unsigned nonbinary;  // some mask value is not 0/1: K1b reads the original mask instead of the bits
-  unsigned pad[2];
+  unsigned pack_ticket;
+  unsigned pad;
+  double mask_total;   // token-mean: sum(mask), reduced by K1a's last workgroup in a fixed order
+  double pad2;         // 32 B: one fill on the stream
 };
 
 struct Args {
@@ -37,8 +51,6 @@ struct Args {
   const float* ref;
   const float* rowcnt;               // seq-mean-token-mean: sum(mask) per row
   const unsigned long long* bits;    // token-mean: packed mask (nullptr: read `mask`)
-  const double* pack_counts;         // token-mean: n_pack partial sums of the mask
-  int n_pack;
   float* dlp;
   float* dent;
   float* out;
@@ -49,12 +61,14 @@ struct Args {
   int mode, kl;
 };
 
-template <int MDT>
+template <int MDT, bool NT = true>
 __device__ __forceinline__ void load_mask4(const void* m, int64_t t, int64_t N, float v[4]) {
   if (t + 3 < N) {
     if constexpr (MDT == DRL_I64) {
-      const longlong2* p = reinterpret_cast<const longlong2*>(static_cast<const int64_t*>(m) + t);
-      const longlong2 a = p[0], b = p[1];
+      const int64_t* p = static_cast<const int64_t*>(m) + t;
+      nt_i2 a, b;
+      if constexpr (NT) { a = ldnt(p); b = ldnt(p + 2); }
+      else { a = *reinterpret_cast<const nt_i2*>(p); b = *reinterpret_cast<const nt_i2*>(p + 2); }
       v[0] = static_cast<float>(a.x); v[1] = static_cast<float>(a.y);
       v[2] = static_cast<float>(b.x); v[3] = static_cast<float>(b.y);
     } else if constexpr (MDT == DRL_I32) {
@@ -64,7 +78,7 @@ __device__ __forceinline__ void load_mask4(const void* m, int64_t t, int64_t N, 
       const uint32_t a = *reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(m) + t);
       v[0] = a & 0xff; v[1] = (a >> 8) & 0xff; v[2] = (a >> 16) & 0xff; v[3] = a >> 24;
     } else {
-      const float4 a = *reinterpret_cast<const float4*>(static_cast<const float*>(m) + t);
+      const nt_f4 a = ldnt(static_cast<const float*>(m) + t);
       v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
     }
   } else {
@@ -75,7 +89,7 @@ __device__ __forceinline__ void load_mask4(const void* m, int64_t t, int64_t N, 
 
 __device__ __forceinline__ void load4(const float* p, int64_t t, int64_t N, float v[4]) {
   if (t + 3 < N) {
-    const float4 a = *reinterpret_cast<const float4*>(p + t);
+    const nt_f4 a = ldnt(p + t);
     v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
   } else {
 #pragma unroll
@@ -85,7 +99,7 @@ __device__ __forceinline__ void load4(const float* p, int64_t t, int64_t N, floa
 
 __device__ __forceinline__ void store4(float* p, int64_t t, int64_t N, const float v[4]) {
   if (t + 3 < N) {
-    *reinterpret_cast<float4*>(p + t) = make_float4(v[0], v[1], v[2], v[3]);
+    stnt(p + t, nt_f4{v[0], v[1], v[2], v[3]});
   } else {
 #pragma unroll
     for (int j = 0; j < 4; ++j)
@@ -125,11 +139,12 @@ __device__ __forceinline__ void kl_term(int kl, float lp, float ref, float& val,
 }
 
 // K1a (token-mean only): stream the mask once; per 1024-token chunk store one 64-bit ballot per wave and
-// element slot (N/8 bytes in total) and accumulate sum(mask) per workgroup (fixed-order partials).
+// element slot (N/8 bytes in total) and accumulate sum(mask) per workgroup; the last workgroup folds the
+// per-workgroup counts in a fixed order into the header.
 template <int MDT>
 __global__ __launch_bounds__(kThreads) void mask_pack_kernel(const void* mask, int64_t N, unsigned long long* bits,
                                                              double* counts, Header* hdr) {
-  constexpr int kU = 4;  // chunks in flight per lane (8 x 16-B loads for an int64 mask)
+  constexpr int kU = DRL_K1_PACK_U;  // chunks in flight per lane (2 x 16-B loads each for an int64 mask)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t nchunks = (N + kChunk - 1) / kChunk;
   float cnt = 0.f;
@@ -140,18 +155,21 @@ __global__ __launch_bounds__(kThreads) void mask_pack_kernel(const void* mask, i
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
       const int64_t t = (c0 + u) * kChunk + tid * 4;
-      if (c0 + u < nchunks) load_mask4<MDT>(mask, t, N, m[u]);
+      if (c0 + u < nchunks) load_mask4<MDT, false>(mask, t, N, m[u]);
       else m[u][0] = m[u][1] = m[u][2] = m[u][3] = 0.f;
     }
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
+      unsigned long long mine = 0;  // lane j (< 4) stores the wave's ballot of element slot j
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         cnt += m[u][j];
         nonbin |= (m[u][j] != 0.f && m[u][j] != 1.f);
         const unsigned long long b = __ballot(m[u][j] != 0.f);
-        if (lane == 0 && c0 + u < nchunks) bits[(c0 + u) * 16 + wave * 4 + j] = b;
+        mine = lane == j ? b : mine;
       }
+      // the wave's 4 words are contiguous: one 32-B store instead of four single-lane ones
+      if (lane < 4 && c0 + u < nchunks) bits[(c0 + u) * 16 + wave * 4 + lane] = mine;
     }
     if (cnt >= 8388608.f) { dcnt += cnt; cnt = 0.f; }  // keep float partials exact
   }
@@ -161,7 +179,17 @@ __global__ __launch_bounds__(kThreads) void mask_pack_kernel(const void* mask, i
   __shared__ double red[kThreads / kWave];
   if (lane == 0) red[wave] = dcnt;
   __syncthreads();
-  if (tid == 0) counts[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+  if (tid == 0) store_sc1(counts + blockIdx.x, red[0] + red[1] + red[2] + red[3]);
+  // the last workgroup folds the per-workgroup counts (fixed order) so K1b reads one value
+  if (last_block_ticket(&hdr->pack_ticket)) {
+    double v = 0.0;
+    for (unsigned g = tid; g < gridDim.x; g += kThreads) v += load_sc1(counts + g);
+    v = wave_sum(v);
+    __syncthreads();
+    if (lane == 0) red[wave] = v;
+    __syncthreads();
+    if (tid == 0) hdr->mask_total = red[0] + red[1] + red[2] + red[3];
+  }
 }
 
 // K1b: per-token loss terms, gradients and the workgroup's partial sums. One contiguous run of
@@ -178,15 +206,9 @@ __global__ __launch_bounds__(kThreads) void ppo_loss_kernel(Args a) {
   float cnt_total = 0.f;
   bool use_bits = false;
   if (a.mode == DRL_AGG_TOKEN_MEAN && a.bits != nullptr) {
-    // global mask count from the pack kernel's fixed-order partials
-    double v = 0.0;
-    for (int g = tid; g < a.n_pack; g += kThreads) v += a.pack_counts[g];
-    v = wave_sum(v);
-    if (lane == 0) red[wave][0] = v;
-    __syncthreads();
-    cnt_total = static_cast<float>(red[0][0] + red[1][0] + red[2][0] + red[3][0]);
+    // global mask count, folded by the pack kernel's last workgroup
+    cnt_total = static_cast<float>(a.hdr->mask_total);
     use_bits = a.hdr->nonbinary == 0;
-    __syncthreads();
   }
   const float denom_tm = cnt_total + 1e-8f;       // masked_mean: sum / (mask.sum() + 1e-8)
   const float inv_denom_tm = 1.0f / denom_tm;     // upstream / D once, then * mask (MeanBackward style)
@@ -196,20 +218,38 @@ __global__ __launch_bounds__(kThreads) void ppo_loss_kernel(Args a) {
   const bool tm = a.mode == DRL_AGG_TOKEN_MEAN, smtm = a.mode == DRL_AGG_SEQ_MEAN_TOKEN_MEAN;
   float s_pg = 0.f, s_clip = 0.f, s_kl = 0.f, s_cliplow = 0.f, s_ent = 0.f, s_kld = 0.f, s_cnt = 0.f;
 
-  for (int64_t c = c_begin; c < c_end; ++c) {
-    const int64_t t = c * kChunk + tid * 4;
-    float m[4], old[4], lp[4], A[4], en[4], rf[4];
-    if (use_bits) {
+  // kU chunks per iteration: every load of the kU chunks is issued before any of their math, so each
+  // wave keeps kU x (5 x 16 B) per lane in flight
+  constexpr int kU = 1;
+  for (int64_t c0 = c_begin; c0 < c_end; c0 += kU) {
+    float mu[kU][4], oldu[kU][4], lpu[kU][4], Au[kU][4], enu[kU][4], rfu[kU][4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) m[j] = ((a.bits[c * 16 + wave * 4 + j] >> lane) & 1ull) ? 1.f : 0.f;
-    } else {
-      load_mask4<MDT>(a.mask, t, N, m);
+    for (int u = 0; u < kU; ++u) {
+      const int64_t c = c0 + u;
+      const int64_t t = c * kChunk + tid * 4;
+      const int64_t tt = c < c_end ? t : N;  // past the run: every load4 takes its bounds path and yields 0
+      if (use_bits && c < c_end) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) mu[u][j] = ((a.bits[c * 16 + wave * 4 + j] >> lane) & 1ull) ? 1.f : 0.f;
+      } else {
+        load_mask4<MDT>(a.mask, tt, N, mu[u]);
+      }
+      load4(a.old_lp, tt, N, oldu[u]);
+      load4(a.lp, tt, N, lpu[u]);
+      load4(a.adv, tt, N, Au[u]);
+      if (has_ent) load4(a.ent, tt, N, enu[u]);
+      if (has_kl) load4(a.ref, tt, N, rfu[u]);
     }
-    load4(a.old_lp, t, N, old);
-    load4(a.lp, t, N, lp);
-    load4(a.adv, t, N, A);
-    if (has_ent) load4(a.ent, t, N, en);
-    if (has_kl) load4(a.ref, t, N, rf);
+#pragma unroll
+  for (int u = 0; u < kU; ++u) {
+    if (c0 + u >= c_end) break;
+    const int64_t t = (c0 + u) * kChunk + tid * 4;
+    float* m = mu[u];
+    float* old = oldu[u];
+    float* lp = lpu[u];
+    float* A = Au[u];
+    float* en = enu[u];
+    float* rf = rfu[u];
     float g_lp[4], g_en[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -271,6 +311,7 @@ __global__ __launch_bounds__(kThreads) void ppo_loss_kernel(Args a) {
     if (want_dlp) store4(a.dlp, t, N, g_lp);
     if (want_dent) store4(a.dent, t, N, g_en);
   }
+  }
 
   // ---- workgroup partials -> the last workgroup reduces all of them in a fixed order
   const float vals[kNumPartials] = {s_pg, s_clip, s_kl, s_cliplow, s_ent, s_kld, s_cnt, 0.f};
@@ -280,12 +321,12 @@ __global__ __launch_bounds__(kThreads) void ppo_loss_kernel(Args a) {
     if (lane == 0) red[wave][k] = v;
   }
   __syncthreads();
-  if (tid < kNumPartials) a.partials[blockIdx.x * kNumPartials + tid] = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
+  if (tid < kNumPartials) store_sc1(a.partials + tid * gridDim.x + blockIdx.x, red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid]);
   if (last_block_ticket(&a.hdr->ticket)) {
 #pragma unroll
     for (int k = 0; k < kNumPartials; ++k) {
       double v = 0.0;
-      for (unsigned g = tid; g < gridDim.x; g += kThreads) v += a.partials[g * kNumPartials + k];
+      for (unsigned g = tid; g < gridDim.x; g += kThreads) v += load_sc1(a.partials + k * gridDim.x + g);
       v = wave_sum(v);
       if (lane == 0) red[wave][k] = v;
     }
@@ -330,7 +371,13 @@ __global__ __launch_bounds__(256) void row_count_kernel(const void* mask, int64_
   if (lane == 0) rowcnt[row] = c;
 }
 
-int max_grid() { return cu_count() * 4; }
+#ifndef DRL_K1_WG_PER_CU
+#define DRL_K1_WG_PER_CU 4
+#endif
+#ifndef DRL_K1_PACK_WG_PER_CU
+#define DRL_K1_PACK_WG_PER_CU 4
+#endif
+int max_grid() { return cu_count() * (DRL_K1_WG_PER_CU > DRL_K1_PACK_WG_PER_CU ? DRL_K1_WG_PER_CU : DRL_K1_PACK_WG_PER_CU); }
 
 struct Layout {
   size_t partials, rowcnt, counts, bits, total;
@@ -359,15 +406,15 @@ int launch(Args a, const Layout& L, char* ws, hipStream_t s) {
   if (a.mode == DRL_AGG_TOKEN_MEAN && (a.dlp != nullptr || a.dent != nullptr)) {
     auto* bits = reinterpret_cast<unsigned long long*>(ws + L.bits);
     auto* counts = reinterpret_cast<double*>(ws + L.counts);
-    const int g1 = static_cast<int>(std::min<int64_t>(max_grid(), (nchunks + 3) / 4));
+    const int g1 = static_cast<int>(std::min<int64_t>(static_cast<int64_t>(cu_count()) * DRL_K1_PACK_WG_PER_CU,
+                                                      (nchunks + DRL_K1_PACK_U - 1) / DRL_K1_PACK_U));
     hipLaunchKernelGGL(mask_pack_kernel<MDT>, dim3(g1), dim3(kThreads), 0, s, a.mask, a.N, bits, counts, a.hdr);
     DRL_LAUNCH_CHECK();
     a.bits = bits;
-    a.pack_counts = counts;
-    a.n_pack = g1;
   }
   // >= 2 chunks per workgroup before the grid reaches 4 workgroups per CU
-  const int grid = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(max_grid(), (nchunks + 1) / 2)));
+  const int grid = static_cast<int>(std::max<int64_t>(
+      1, std::min<int64_t>(static_cast<int64_t>(cu_count()) * DRL_K1_WG_PER_CU, (nchunks + 1) / 2)));
   hipLaunchKernelGGL(ppo_loss_kernel<MDT>, dim3(grid), dim3(kThreads), 0, s, a);
   DRL_LAUNCH_CHECK();
   return DRL_OK;
@@ -406,12 +453,12 @@ __global__ __launch_bounds__(256) void agg_loss_kernel(const float* x, const voi
   if (lane == 0) { red[wave][0] = s; red[wave][1] = c; }
   __syncthreads();
   if (threadIdx.x == 0) {
-    partials[2 * blockIdx.x] = red[0][0] + red[1][0] + red[2][0] + red[3][0];
-    partials[2 * blockIdx.x + 1] = red[0][1] + red[1][1] + red[2][1] + red[3][1];
+    store_sc1(partials + 2 * blockIdx.x, red[0][0] + red[1][0] + red[2][0] + red[3][0]);
+    store_sc1(partials + 2 * blockIdx.x + 1, red[0][1] + red[1][1] + red[2][1] + red[3][1]);
   }
   if (last_block_ticket(&hdr->ticket) && threadIdx.x == 0) {
     double S = 0.0, C = 0.0;
-    for (unsigned b = 0; b < gridDim.x; ++b) { S += partials[2 * b]; C += partials[2 * b + 1]; }
+    for (unsigned b = 0; b < gridDim.x; ++b) { S += load_sc1(partials + 2 * b); C += load_sc1(partials + 2 * b + 1); }
     double r;
     if (mode == DRL_AGG_TOKEN_MEAN) r = S / static_cast<double>(static_cast<float>(C) + 1e-8f);
     else if (mode == DRL_AGG_SEQ_MEAN_TOKEN_SUM || mode == DRL_AGG_SEQ_MEAN_TOKEN_MEAN) r = S / static_cast<double>(B);
@@ -469,7 +516,7 @@ int drl_ppo_loss_fwd_bwd(const float* old_log_prob, const float* log_prob, const
   a.old_lp = old_log_prob; a.lp = log_prob; a.adv = advantages; a.mask = response_mask;
   a.ent = entropy; a.ref = p->kl_type == DRL_KL_NONE ? nullptr : ref_log_prob;
   a.rowcnt = reinterpret_cast<const float*>(ws + L.rowcnt);
-  a.bits = nullptr; a.pack_counts = nullptr;
+  a.bits = nullptr;
   a.dlp = dlog_prob; a.dent = dentropy; a.out = out_scalars;
   a.hdr = reinterpret_cast<Header*>(ws);
   a.partials = reinterpret_cast<double*>(ws + L.partials);

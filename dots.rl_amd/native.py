@@ -327,13 +327,15 @@ def _edt(t):
         raise ValueError(f"activation dtype {t.dtype} not supported (bfloat16 / float32)") from e
 
 
-def rope_qkv_fwd(qkv, position_ids, cos_t, sin_t, Hq, Hkv, D, q, k, v, koff=0, koff_dev=None):
+def rope_qkv_fwd(qkv, position_ids, cos_t, sin_t, Hq, Hkv, D, q, k, v, koff=0, koff_dev=None, vt=None):
     """qkv (B,T,(Hq+2Hkv)D) -> q (B,Hkv,G,T,D); k, v written at [:, :, koff:koff+T] of (B,Hkv,Tk,D).
 
-    ``koff_dev`` (device int64 scalar) replaces ``koff`` for graph-captured decode steps."""
+    ``koff_dev`` (device int64 scalar) replaces ``koff`` for graph-captured decode steps; with ``vt``
+    ((B,Hkv,D,ld) view, last dim contiguous) V is written transposed there instead of ``v``."""
     B, T = qkv.shape[0], qkv.shape[1]
     check(lib().drl_rope_qkv_fwd(_p(qkv), _edt(qkv), _p(position_ids), _p(cos_t), _p(sin_t), cos_t.shape[0], B, T,
-                                 Hq, Hkv, D, _p(q), _p(k), _p(v), k.shape[2], koff, _p(koff_dev), _stream()),
+                                 Hq, Hkv, D, _p(q), _p(k), _p(v), k.shape[2], koff, _p(koff_dev), _p(vt),
+                                 0 if vt is None else vt.stride(2), _stream()),
           "drl_rope_qkv_fwd")
 
 
@@ -396,4 +398,19 @@ def decode_attention(q, k_cache, v_cache, key_valid, L, out, qpos=None, qpos_dev
     check(Lb.drl_decode_attention(_p(q), _p(k_cache), _p(v_cache), _edt(q), _p(key_valid), key_valid.stride(0),
                                   _p(qpos_dev), qp, B, Hkv, G, D, Tk, L, 1.0 / math.sqrt(D), _p(out), _p(ws), nb,
                                   _stream()), "drl_decode_attention")
+    return out
+
+
+def flash_attn_fwd(q, k, vt, key_valid, out, Tk=None, qoff=0, lse=None):
+    """Fused causal + key-padding attention (MFMA). q (B,Hkv,G,Tq,D) bf16, k (B,Hkv,>=Tk,D) (keys [0,Tk) used),
+    vt (B,Hkv,D,ld) with ld >= Tk a multiple of 8; out (B,Tq,Hkv*G*D); lse optional (B,Hkv,G,Tq) fp32."""
+    _dev(q, k, vt, key_valid, out, lse)
+    B, Hkv, G, Tq, D = q.shape
+    Tk = k.shape[2] if Tk is None else Tk
+    assert q.is_contiguous() and k.is_contiguous() and out.is_contiguous() and vt.stride(3) == 1
+    assert vt.stride(2) * D == vt.stride(1) and key_valid.dtype == torch.uint8 and key_valid.stride(1) == 1
+    check(lib().drl_flash_attn_fwd(_p(q), _p(k), _p(vt), _edt(q), _p(key_valid), key_valid.stride(0), B, Hkv, G, D,
+                                   Tq, Tk, k.shape[2], vt.stride(2), qoff, 1.0 / math.sqrt(D), _p(out), _p(lse),
+                                   _stream()),
+          "drl_flash_attn_fwd")
     return out

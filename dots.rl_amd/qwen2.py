@@ -234,15 +234,31 @@ def _layer_forward(m, i, x_prev, delta, pos, key_valid, save, cache=None, koff=0
     qkv = torch.addmm(s.w(p + "qkv_proj.bias").to(dt), h1.view(B * T, H), s.w(p + "qkv_proj.weight").t())
     qkv = qkv.view(B, T, -1)
     q = torch.empty(B, Hkv, G, T, D, dtype=dt, device=dev)
+    # no-grad full-sequence passes (log-probs, prefill) run the fused MFMA attention (csrc/flash_attn.hip);
+    # the training forward keeps the probabilities for the hand-written backward
+    flash = (save is None and T > 1 and dt == torch.bfloat16 and D in (64, 128) and G <= 8
+             and key_valid.stride(0) % 4 == 0)
+    vt = None
     if cache is None:
         kbuf = torch.empty(B, Hkv, T, D, dtype=dt, device=dev)
-        vbuf = torch.empty_like(kbuf)
+        if flash:
+            vt = torch.empty(B, Hkv, D, (T + 7) // 8 * 8, dtype=dt, device=dev)
+            vbuf = None
+        else:
+            vbuf = torch.empty_like(kbuf)
         koff = 0
     else:
         kbuf, vbuf = cache.k[i], cache.v[i]
-    native.rope_qkv_fwd(qkv, pos, m.cos, m.sin, Hq, Hkv, D, q, kbuf, vbuf, koff, koff_dev)
+    native.rope_qkv_fwd(qkv, pos, m.cos, m.sin, Hq, Hkv, D, q, kbuf, vbuf, koff, koff_dev, vt=vt)
     L = koff + T
-    if cache is not None and T == 1:
+    if flash:
+        if vt is None:  # prefill: the cache keeps V row-major for decode; the kernel reads a transposed copy
+            vt = torch.empty(B, Hkv, D, (L + 7) // 8 * 8, dtype=dt, device=dev)
+            vt[..., :L].copy_(vbuf[:, :, :L].transpose(-1, -2))
+        attn = torch.empty(B, T, Hq * D, dtype=dt, device=dev)
+        native.flash_attn_fwd(q, kbuf, vt, key_valid, attn, Tk=L, qoff=L - T)
+        P = None
+    elif cache is not None and T == 1:
         # one new token: fused GQA decode attention streams the cache once (csrc/attention.hip)
         attn = torch.empty(B, 1, Hq * D, dtype=dt, device=dev)
         if koff_dev is None:
@@ -359,6 +375,14 @@ class _FinalNorm(torch.autograd.Function):
         return dx, dx.to(ctx.delta_dtype), None
 
 
+def _key_valid(attention_mask):
+    """u8 key-valid rows padded to a multiple of 4 bytes (the fused attention reads them as 32-bit words)."""
+    B, T = attention_mask.shape
+    buf = torch.zeros(B, (T + 3) // 4 * 4, dtype=torch.uint8, device=attention_mask.device)
+    buf[:, :T] = attention_mask
+    return buf[:, :T]
+
+
 class KVCache:
     """Per-layer K/V for decode: (B, Hkv, Tmax, D) in the compute dtype, plus the key-valid mask (u8)."""
 
@@ -366,7 +390,7 @@ class KVCache:
         self.k = [torch.empty(B, cfg.num_key_value_heads, Tmax, cfg.head_dim, device=device, dtype=dtype)
                   for _ in range(cfg.num_hidden_layers)]
         self.v = [torch.empty_like(t) for t in self.k]
-        self.valid = torch.zeros(B, Tmax, dtype=torch.uint8, device=device)
+        self.valid = torch.zeros(B, (Tmax + 3) // 4 * 4, dtype=torch.uint8, device=device)[:, :Tmax]
         self.len = 0
 
 
@@ -404,7 +428,7 @@ class Qwen2Model:
     def hidden_states(self, input_ids, attention_mask, position_ids):
         """Full-sequence forward -> final-norm hidden states (B, T, H) in the compute dtype."""
         cfg = self.cfg
-        key_valid = attention_mask.to(torch.uint8).contiguous()
+        key_valid = _key_valid(attention_mask)
         pos = position_ids.contiguous()
         if self.training and self.store.trainable:
             x = _Embedding.apply(input_ids, self.store.w("embed_tokens"), self.store.g("embed_tokens"), self._dummy)

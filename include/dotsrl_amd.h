@@ -220,10 +220,12 @@ int drl_adamw_step(float* params, const float* grads, float* exp_avg, float* exp
 /* qkv (B,T,(Hq+2Hkv)*D) -> RoPE'd q in grouped layout (B,Hkv,Hq/Hkv,T,D), RoPE'd k and v written at
  * key offset koff of (B,Hkv,Tk,D) buffers (the KV cache when decoding). cos/sin: (maxpos, D/2) fp32.
  * koff_dev (optional device int64 scalar) replaces koff — graph-captured decode steps; an out-of-range
- * device offset writes nothing. */
+ * device offset writes nothing. With vt != NULL, V is written transposed to vt (B,Hkv,D,ld_vt) instead
+ * of v (the layout drl_flash_attn_fwd reads). */
 int drl_rope_qkv_fwd(const void* qkv, int32_t dt, const int64_t* position_ids, const float* cos_t, const float* sin_t,
                      int64_t maxpos, int64_t B, int64_t T, int64_t Hq, int64_t Hkv, int64_t D, void* q, void* k,
-                     void* v, int64_t Tk, int64_t koff, const int64_t* koff_dev, void* stream);
+                     void* v, int64_t Tk, int64_t koff, const int64_t* koff_dev, void* vt, int64_t ld_vt,
+                     void* stream);
 int drl_rope_qkv_bwd(const void* dq, const void* dk, const void* dv, int32_t dt, const int64_t* position_ids,
                      const float* cos_t, const float* sin_t, int64_t maxpos, int64_t B, int64_t T, int64_t Hq,
                      int64_t Hkv, int64_t D, void* dqkv, void* stream);
@@ -260,6 +262,18 @@ int drl_decode_attention(const void* q, const void* k_cache, const void* v_cache
                          int64_t ld_valid, const int64_t* qpos_ptr, int64_t qpos, int64_t B, int64_t Hkv, int64_t G,
                          int64_t D, int64_t Tk, int64_t L, float scale, void* out, void* workspace,
                          size_t workspace_bytes, void* stream);
+
+/* ---- fused attention forward on MFMA (full-sequence passes: old / ref log-probs, training forward;
+ *      replaces the eager q k^T -> masked softmax -> p v of HF Qwen2 attention under dp_actor.py:90-280).
+ * q (B,Hkv,G,Tq,D) bf16 (grouped layout of drl_rope_qkv_fwd), k (B,Hkv,ld_k,D) of which keys [0,Tk)
+ * are used (ld_k > Tk: a KV cache), vt (B,Hkv,D,ld_vt) (V
+ * transposed, ld_vt >= Tk, multiple of 8), key_valid (B, ld_valid) u8 with 4-byte aligned rows.
+ * Query t attends to key j iff j <= t + qoff && key_valid[b, j]; out (B,Tq,Hkv*G*D) bf16 (the o_proj
+ * input layout). lse (optional, (B,Hkv,G,Tq) fp32) = log sum_j exp(scale * s_tj) over allowed keys.
+ * A query row with no allowed key writes zeros and lse = -inf. bf16, head_dim 64 or 128, G <= 8. */
+int drl_flash_attn_fwd(const void* q, const void* k, const void* vt, int32_t dt, const uint8_t* key_valid,
+                       int64_t ld_valid, int64_t B, int64_t Hkv, int64_t G, int64_t D, int64_t Tq, int64_t Tk,
+                       int64_t ld_k, int64_t ld_vt, int64_t qoff, float scale, void* out, float* lse, void* stream);
 
 #ifdef __cplusplus
 }

@@ -185,3 +185,59 @@ def test_decode_attention(dt, B, Hkv, G, D, Tk, L):
         qp = torch.tensor([L - 4], device=DEV)
         native.decode_attention(q, k, v, valid, L, out, qpos_dev=qp)
         torch.testing.assert_close(out.float(), _ref_decode(q, k, v, valid, L, L - 4), **_tol(dt))
+
+
+def _ref_attn(q, k, v, valid, qoff):
+    """fp32 causal + key-padding attention, grouped layout; rows with no allowed key -> zeros."""
+    B, Hkv, G, Tq, D = q.shape
+    Tk = k.shape[2]
+    S = torch.einsum("bhgtd,bhkd->bhgtk", q.float(), k.float()) / math.sqrt(D)
+    j = torch.arange(Tk, device=DEV)
+    t = torch.arange(Tq, device=DEV)[:, None] + qoff
+    allowed = valid[:, None, None, None, :].bool() & (j <= t)[None, None, None]
+    S = S.masked_fill(~allowed, float("-inf"))
+    lse = torch.logsumexp(S, -1)
+    P = torch.softmax(S, -1).nan_to_num(0.0)
+    O = torch.einsum("bhgtk,bhkd->bhgtd", P, v.float())
+    return O.permute(0, 3, 1, 2, 4).reshape(B, Tq, Hkv * G * D), lse
+
+
+@pytest.mark.parametrize("B,Hkv,G,D,Tq,Tk,qoff", [(2, 2, 7, 64, 768, 768, 0), (3, 2, 7, 64, 100, 100, 0),
+                                                  (2, 1, 4, 128, 40, 100, 60), (1, 2, 7, 64, 17, 17, 0),
+                                                  (2, 2, 8, 64, 64, 64, 0)])
+def test_flash_attn_forward(B, Hkv, G, D, Tq, Tk, qoff):
+    g = torch.Generator(device=DEV).manual_seed(Tq * 7 + Tk)
+    q = torch.randn(B, Hkv, G, Tq, D, device=DEV, generator=g).to(torch.bfloat16)
+    k = torch.randn(B, Hkv, Tk, D, device=DEV, generator=g).to(torch.bfloat16)
+    v = torch.randn(B, Hkv, Tk, D, device=DEV, generator=g).to(torch.bfloat16)
+    ld = (Tk + 7) // 8 * 8
+    vt = torch.full((B, Hkv, D, ld), float("nan"), device=DEV, dtype=torch.bfloat16)  # pad columns must not leak
+    vt[..., :Tk] = v.transpose(-1, -2)
+    ldv = (Tk + 3) // 4 * 4
+    valid = torch.zeros(B, ldv, dtype=torch.uint8, device=DEV)
+    valid[:, :Tk] = 1
+    for b in range(B):
+        valid[b, : min(5 * b, Tk - 1)] = 0  # left padding: early query rows of b > 0 have no allowed key
+    out = torch.empty(B, Tq, Hkv * G * D, device=DEV, dtype=torch.bfloat16)
+    lse = torch.empty(B, Hkv, G, Tq, device=DEV)
+    native.flash_attn_fwd(q, k, vt, valid, out, Tk=Tk, qoff=qoff, lse=lse)
+    ref, ref_lse = _ref_attn(q, k, v, valid[:, :Tk], qoff)
+    torch.testing.assert_close(out.float(), ref, rtol=2e-2, atol=2e-2)
+    fin = torch.isfinite(ref_lse)
+    assert torch.equal(torch.isfinite(lse), fin)
+    torch.testing.assert_close(lse[fin], ref_lse[fin], rtol=1e-4, atol=1e-4)
+
+
+def test_rope_writes_transposed_v():
+    B, T, Hq, Hkv, D = 2, 45, 14, 2, 64
+    g = torch.Generator(device=DEV).manual_seed(3)
+    qkv = torch.randn(B, T, (Hq + 2 * Hkv) * D, device=DEV, generator=g).to(torch.bfloat16)
+    pos = torch.arange(T, device=DEV)[None].expand(B, T).contiguous()
+    cos, sin = _rope_tables(D)
+    q = torch.empty(B, Hkv, Hq // Hkv, T, D, device=DEV, dtype=torch.bfloat16)
+    k = torch.empty(B, Hkv, T, D, device=DEV, dtype=torch.bfloat16)
+    v = torch.empty_like(k)
+    vt = torch.zeros(B, Hkv, D, 48, device=DEV, dtype=torch.bfloat16)
+    native.rope_qkv_fwd(qkv, pos, cos, sin, Hq, Hkv, D, q, k, v)
+    native.rope_qkv_fwd(qkv, pos, cos, sin, Hq, Hkv, D, q, k, None, vt=vt)
+    assert torch.equal(vt[..., :T], v.transpose(-1, -2))

@@ -114,6 +114,30 @@ def decode_attn(B=512, Hkv=2, G=7, D=64, Tk=768, L=640):
     return [dict(kernel="A3_decode_attention", B=B, L=L, seconds=t, GBps=nbytes / t / 1e9, frac=nbytes / t / PEAK_HBM)]
 
 
+def flash(B=16, Hkv=2, G=7, D=64, T=768):
+    """Fused attention forward vs the unfused path (fp32-score GEMM + masked softmax + PV GEMM)."""
+    import math
+    dev = "cuda"
+    q = torch.randn(B, Hkv, G, T, D, device=dev, dtype=torch.bfloat16)
+    k = torch.randn(B, Hkv, T, D, device=dev, dtype=torch.bfloat16)
+    v = torch.randn(B, Hkv, T, D, device=dev, dtype=torch.bfloat16)
+    vt = v.transpose(-1, -2).contiguous()
+    valid = torch.ones(B, T, dtype=torch.uint8, device=dev)
+    out = torch.empty(B, T, Hkv * G * D, device=dev, dtype=torch.bfloat16)
+    lse = torch.empty(B, Hkv, G, T, device=dev)
+    t = time_it(lambda: native.flash_attn_fwd(q, k, vt, valid, out, lse=lse), iters=20)
+    flops = 4.0 * B * Hkv * G * D * T * (T + 1) / 2  # causal half of QK^T and PV
+
+    def unfused():
+        S = torch.bmm(q.view(B * Hkv, G * T, D), k.view(B * Hkv, T, D).transpose(1, 2), out_dtype=torch.float32)
+        P = torch.empty(B * Hkv, G * T, T, device=dev, dtype=torch.bfloat16)
+        native.masked_softmax_fwd(S, P, valid, B, Hkv * G, T, T, 0, 1.0 / math.sqrt(D))
+        return torch.bmm(P, v.view(B * Hkv, T, D))
+    t2 = time_it(unfused, iters=10)
+    return [dict(kernel="flash_attn_fwd", B=B, T=T, seconds=t, TFLOPs=flops / t / 1e12, frac_mfma=flops / t / 2.5e15,
+                 unfused_seconds=t2)]
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--quick", action="store_true")
@@ -123,6 +147,14 @@ if __name__ == "__main__":
         for L in (513, 640, 768):
             for r in decode_attn(L=L):
                 print(json.dumps(r), flush=True)
+        sys.exit(0)
+    if args.only == "flash":
+        for r in flash():
+            print(json.dumps(r), flush=True)
+        sys.exit(0)
+    if args.only in ("k1", "k1big"):
+        for r in k1_sweep([26] if args.only == "k1big" else [17, 20, 22, 24, 25, 26]):
+            print(json.dumps(r), flush=True)
         sys.exit(0)
     exps = [17, 20, 22, 24] if args.quick else [17, 18, 20, 22, 23, 24, 25, 26]
     for r in k1_sweep(exps) + k2(1024 if args.quick else 4096) + adam(1 << 24 if args.quick else 494_032_768):
