@@ -98,8 +98,8 @@ SIGNATURES = {
     "drl_grad_norm_workspace_bytes": (SZ, [I64]),
     "drl_grad_norm": (ctypes.c_int, [P, I64, P, P, SZ, P]),
     "drl_adamw_step": (ctypes.c_int, [P, P, P, P, P, I64, ctypes.POINTER(AdamWParams), P, P]),
-    "drl_rope_qkv_fwd": (ctypes.c_int, [P, I32, P, P, P, I64, I64, I64, I64, I64, I64, P, P, P, I64, I64, P, P, I64,
-                                        P]),
+    "drl_rope_qkv_fwd": (ctypes.c_int, [P, I32, P, P, P, I64, I64, I64, I64, I64, I64, P, P, P, I64, I64, P, P, P, P,
+                                        I64, P]),
     "drl_rope_qkv_bwd": (ctypes.c_int, [P, P, P, I32, P, P, P, I64, I64, I64, I64, I64, I64, P, P]),
     "drl_masked_softmax_fwd": (ctypes.c_int, [P, P, I32, P, I64, I64, I64, I64, I64, I64, F32, P]),
     "drl_masked_softmax_bwd": (ctypes.c_int, [P, P, P, I32, I64, I64, F32, P]),
@@ -111,6 +111,8 @@ SIGNATURES = {
     "drl_decode_attention_workspace_bytes": (SZ, [I64, I64, I64, I64, I64]),
     "drl_flash_attn_fwd": (ctypes.c_int, [P, P, P, I32, P, I64, I64, I64, I64, I64, I64, I64, I64, I64, I64, F32, P, P,
                                           P]),
+    "drl_flash_attn_bwd": (ctypes.c_int, [P, P, P, P, P, P, P, P, I64, P, I32, P, I64, I64, I64, I64, I64, I64, I64, F32,
+                                          P, P, P, P, P]),
     "drl_decode_attention": (ctypes.c_int, [P, P, P, I32, P, I64, P, I64, I64, I64, I64, I64, I64, I64, F32, P, P, SZ,
                                             P]),
 }

@@ -40,24 +40,91 @@ struct FlashArgs {
 
 __device__ __forceinline__ bf16x8 as_bf16x8(u16x8 v) { return __builtin_bit_cast(bf16x8, v); }
 
-__device__ __forceinline__ uint16_t to_bf16_bits(float f) { return f32_to_bf16(f); }
+// round-to-nearest-even f32 -> bf16 (one v_cvt_pk_bf16_f32; NaN stays NaN)
+__device__ __forceinline__ uint16_t to_bf16_bits(float f) { return __builtin_bit_cast(uint16_t, static_cast<__bf16>(f)); }
+
+// K / V tiles of one 32-key block staged in LDS and shared by the G waves of the workgroup.
+// K: [32 keys][D] rows of D*2 + 16 bytes (16-B aligned, conflict-free ds_read_b128 of a key row slice);
+// V^T: [D][32 keys] rows of 72 bytes (conflict-free ds_read_b64 of 4 keys of one head-dim row).
+template <int D>
+struct KVTile {
+  static constexpr int KROW = D + 8;   // u16 per K row
+  static constexpr int VROW = 36;      // u16 per V^T row
+  static constexpr int KSZ = 32 * KROW, VSZ = D * VROW;
+  static constexpr int NCH = (32 * D + D * 32) * 2 / 16;  // 16-B chunks per block
+  static constexpr int CPT = NCH / 512;                   // chunks per thread (512-thread workgroups)
+};
+
+// global -> registers: chunk c < 32*D/8 is K row c / (D/8), 16-B column c % (D/8); the rest V^T row
+// d = c' / 4, 16-B column c' % 4 (keys 8*col .. 8*col+7). Keys >= Tk load as zero.
+template <int D>
+__device__ __forceinline__ void kv_issue(const uint16_t* kbase, const uint16_t* vtbase, int64_t ld_vt, int64_t k0,
+                                         int64_t Tk, int tid, u16x8 (&r)[KVTile<D>::CPT]) {
+  constexpr int KCH = 32 * D / 8;
+#pragma unroll
+  for (int i = 0; i < KVTile<D>::CPT; ++i) {
+    const int c = tid + 512 * i;
+    if (c < KCH) {
+      const int row = c / (D / 8), col = c % (D / 8);
+      const int64_t key = k0 + row;
+      r[i] = key < Tk ? *reinterpret_cast<const u16x8*>(kbase + key * D + col * 8) : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    } else {
+      const int cc = c - KCH, d = cc / 4, col = cc % 4;
+      const int64_t kk = k0 + col * 8;
+      const uint16_t* src = vtbase + static_cast<int64_t>(d) * ld_vt + kk;
+      if (kk + 7 < Tk) {
+        r[i] = *reinterpret_cast<const u16x8*>(src);
+      } else {
+        u16x8 v = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (kk + j < Tk) v[j] = src[j];
+        r[i] = v;
+      }
+    }
+  }
+}
+
+template <int D>
+__device__ __forceinline__ void kv_store(uint16_t* kl, uint16_t* vl, int tid, const u16x8 (&r)[KVTile<D>::CPT]) {
+  constexpr int KCH = 32 * D / 8;
+#pragma unroll
+  for (int i = 0; i < KVTile<D>::CPT; ++i) {
+    const int c = tid + 512 * i;
+    if (c < KCH) {
+      const int row = c / (D / 8), col = c % (D / 8);
+      *reinterpret_cast<u16x8*>(kl + row * KVTile<D>::KROW + col * 8) = r[i];
+    } else {
+      const int cc = c - KCH, d = cc / 4, col = cc % 4;
+      uint16_t* dst = vl + d * KVTile<D>::VROW + col * 8;  // 8-B aligned: two 8-B stores
+      *reinterpret_cast<u16x4*>(dst) = u16x4{r[i][0], r[i][1], r[i][2], r[i][3]};
+      *reinterpret_cast<u16x4*>(dst + 4) = u16x4{r[i][4], r[i][5], r[i][6], r[i][7]};
+    }
+  }
+}
 
 template <int D>
 __global__ __launch_bounds__(512) void flash_fwd_kernel(FlashArgs a) {
   constexpr int KS = D / 16;  // k-steps of S^T = K Q^T over the head dim
   constexpr int MT = D / 32;  // 32-row tiles of O^T over the head dim
-  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+  using TL = KVTile<D>;
+  __shared__ __attribute__((aligned(16))) uint16_t lds_k[2][TL::KSZ];
+  __shared__ __attribute__((aligned(16))) uint16_t lds_v[2][TL::VSZ];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, g = tid >> 6;
+  const bool computes = g < a.G;  // waves >= G only help staging
   const int qi = lane & 31, h = lane >> 5;
   const int64_t bh = blockIdx.y;
   const int64_t b = bh / a.Hkv;
   const int64_t ntiles = (a.Tq + 31) / 32;
   const int64_t t0 = (ntiles - 1 - static_cast<int64_t>(blockIdx.x)) * 32;
   const int64_t tq = t0 + qi;
-  const bool qvalid = tq < a.Tq;
+  const bool qvalid = computes && tq < a.Tq;
 
   bf16x8 qf[KS];
   {
-    const uint16_t* qrow = a.q + ((bh * a.G + g) * a.Tq + (qvalid ? tq : 0)) * D + 8 * h;
+    const int gg = computes ? g : 0;
+    const uint16_t* qrow = a.q + ((bh * a.G + gg) * a.Tq + (qvalid ? tq : 0)) * D + 8 * h;
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       u16x8 v = *reinterpret_cast<const u16x8*>(qrow + 16 * s);
@@ -74,80 +141,99 @@ __global__ __launch_bounds__(512) void flash_fwd_kernel(FlashArgs a) {
   const uint16_t* vtbase = a.vt + bh * D * a.ld_vt;
   const uint8_t* vrow = a.valid + b * a.ld_valid;
   const int64_t kmax = min(a.Tk, t0 + 31 + a.qoff + 1);  // causal limit of the tile's last query
-  const int64_t qpos = tq + a.qoff;
+  const int64_t nb = (kmax + 31) / 32;
+  const int qpos = static_cast<int>(tq + a.qoff);  // positions fit in 32 bits (host check)
+  const int Tk = static_cast<int>(a.Tk);
+  const int qlo = static_cast<int>(t0 + a.qoff);     // smallest query position of the tile
 
-  for (int64_t k0 = 0; k0 < kmax; k0 += 32) {
-    // ---- S^T (32 keys x 32 queries): A = K rows (lane & 31 = key), B = Q fragments
-    f32x16 st = f32x16{};
-    {
-      const int64_t key = k0 + qi;
-      const bool kin = key < a.Tk;
-      const uint16_t* krow = kbase + (kin ? key : 0) * D + 8 * h;
+  u16x8 stage[TL::CPT];
+  kv_issue<D>(kbase, vtbase, a.ld_vt, 0, a.Tk, tid, stage);
+  kv_store<D>(lds_k[0], lds_v[0], tid, stage);
+  __syncthreads();
+  for (int64_t ib = 0; ib < nb; ++ib) {
+    const int cur = static_cast<int>(ib & 1);
+    const int64_t k0 = ib * 32;
+    if (ib + 1 < nb) kv_issue<D>(kbase, vtbase, a.ld_vt, k0 + 32, a.Tk, tid, stage);  // in flight under compute
+    if (computes) {
+      // ---- S^T (32 keys x 32 queries): A = K rows from LDS (lane & 31 = key), B = Q fragments
+      f32x16 st = f32x16{};
+      const uint16_t* krow = lds_k[cur] + qi * TL::KROW + 8 * h;
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
-        u16x8 kv = *reinterpret_cast<const u16x8*>(krow + 16 * s);
-        if (!kin) kv = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        const u16x8 kv = *reinterpret_cast<const u16x8*>(krow + 16 * s);
         st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(kv), qf[s], st, 0, 0, 0);
       }
-    }
-    // ---- mask + scale; register r holds key k0 + (r & 3) + 8 * (r >> 2) + 4h of query tq
-    float x[16];
-    float mx = -INFINITY;
+      // ---- mask + scale; register r holds key k0 + (r & 3) + 8 * (r >> 2) + 4h of query tq
+      const int kbase0 = static_cast<int>(k0) + 4 * h;
+      uint32_t vw[4];
+      bool allv = true;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const int64_t kb = k0 + 8 * c + 4 * h;
-      uint32_t vb;
-      if (kb + 3 < a.Tk) {
-        vb = *reinterpret_cast<const uint32_t*>(vrow + kb);
+      for (int c = 0; c < 4; ++c) {
+        const int kb = kbase0 + 8 * c;
+        if (kb + 3 < Tk) {
+          vw[c] = *reinterpret_cast<const uint32_t*>(vrow + kb);
+        } else {
+          vw[c] = 0;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) vw[c] |= (kb + j < Tk ? static_cast<uint32_t>(vrow[kb + j]) : 0u) << (8 * j);
+        }
+        allv &= vw[c] == 0x01010101u;
+      }
+      // blocks strictly below the diagonal with every key valid need no mask (wave-uniform test)
+      const bool full = __all(allv) && static_cast<int>(k0) + 31 <= qlo;
+      float x[16];
+      float mx = -INFINITY;
+      if (full) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          x[r] = st[r] * a.scale_log2;
+          mx = fmaxf(mx, x[r]);
+        }
       } else {
-        vb = 0;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) vb |= (kb + j < a.Tk ? static_cast<uint32_t>(vrow[kb + j]) : 0u) << (8 * j);
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int r = 4 * c + j;
-        const bool ok = ((vb >> (8 * j)) & 0xffu) != 0u && kb + j <= qpos;
-        x[r] = ok ? st[r] * a.scale_log2 : -INFINITY;
-        mx = fmaxf(mx, x[r]);
-      }
-    }
-    mx = fmaxf(mx, __shfl_xor(mx, 32, kWave));
-    const float mn = fmaxf(m, mx);
-    const float alpha = (m == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(m - mn);
-    m = mn;
-    float ps = 0.f;
-    u16x8 pb[2];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const float p = (mn == -INFINITY || x[r] == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(x[r] - mn);
-      ps += p;
-      pb[r >> 3][r & 7] = to_bf16_bits(p);
-    }
-    lsum = lsum * alpha + ps;
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) o[mt] *= alpha;
-    // ---- O^T += V^T P^T; k-step s: element j of lane half h is key k0 + 16s + 8(j>>2) + 4h + (j&3)
-    const bool tail = k0 + 32 > a.Tk;
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      const uint16_t* vtrow = vtbase + static_cast<int64_t>(32 * mt + qi) * a.ld_vt;
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const int64_t ka = k0 + 16 * s + 4 * h, kb2 = ka + 8;
-        u16x4 lo = *reinterpret_cast<const u16x4*>(vtrow + ka);
-        u16x4 hi = *reinterpret_cast<const u16x4*>(vtrow + kb2);
-        if (tail) {
+        for (int c = 0; c < 4; ++c) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            if (ka + j >= a.Tk) lo[j] = 0;
-            if (kb2 + j >= a.Tk) hi[j] = 0;
+            const int r = 4 * c + j;
+            const bool ok = ((vw[c] >> (8 * j)) & 0xffu) != 0u && kbase0 + 8 * c + j <= qpos;
+            x[r] = ok ? st[r] * a.scale_log2 : -INFINITY;
+            mx = fmaxf(mx, x[r]);
           }
         }
-        const u16x8 vv = u16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        o[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(vv), as_bf16x8(pb[s]), o[mt], 0, 0, 0);
+      }
+      mx = fmaxf(mx, __shfl_xor(mx, 32, kWave));
+      const float mn = fmaxf(m, mx);
+      const float mref = mn == -INFINITY ? 0.f : mn;  // keeps exp2(-inf - mref) = 0, never NaN
+      const float alpha = __builtin_amdgcn_exp2f(m - mref);
+      m = mn;
+      float ps = 0.f;
+      u16x8 pb[2];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = __builtin_amdgcn_exp2f(x[r] - mref);
+        ps += p;
+        pb[r >> 3][r & 7] = to_bf16_bits(p);
+      }
+      lsum = lsum * alpha + ps;
+      if (!__all(alpha == 1.f)) {
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) o[mt] *= alpha;
+      }
+      // ---- O^T += V^T P^T; k-step s: element j of lane half h is key k0 + 16s + 8(j>>2) + 4h + (j&3)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const uint16_t* vtl = lds_v[cur] + (32 * mt + qi) * TL::VROW + 4 * h;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const u16x4 lo = *reinterpret_cast<const u16x4*>(vtl + 16 * s);
+          const u16x4 hi = *reinterpret_cast<const u16x4*>(vtl + 16 * s + 8);
+          const u16x8 vv = u16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          o[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(vv), as_bf16x8(pb[s]), o[mt], 0, 0, 0);
+        }
       }
     }
+    if (ib + 1 < nb) kv_store<D>(lds_k[cur ^ 1], lds_v[cur ^ 1], tid, stage);  // buffer last read at ib - 1
+    __syncthreads();
   }
   // ---- finalize: O^T register r of tile mt = head-dim row 32mt + (r & 3) + 8(r >> 2) + 4h of query tq
   const float lt = lsum + __shfl_xor(lsum, 32, kWave);
@@ -167,6 +253,359 @@ __global__ __launch_bounds__(512) void flash_fwd_kernel(FlashArgs a) {
     a.lse[(bh * a.G + g) * a.Tq + tq] = lt > 0.f ? (m + __builtin_amdgcn_logf(lt)) * 0.6931471805599453f : -INFINITY;
 }
 
+// ------------------------------------------------------------------------------------------ backward
+// FA2-style backward in two launches, recomputing P from the forward's LSE (nothing of size T x T is
+// stored): (1) dq_kernel, query-tile centric in the forward's S^T orientation (lane = query): dP^T =
+// V dO^T, dS^T = P^T (dP^T - delta), dQ^T += K^T dS^T (K^T from the head-dim-major kt copy); it also
+// writes delta = rowsum(dO * O). (2) dkdv_kernel, key-tile centric in the S orientation (lane = key):
+// S = Q K^T, dP = dO V^T, then dV^T += dO^T P and dK^T += Q^T dS take P / dS straight from the
+// accumulators (dO^T from the transposed o_proj-gradient GEMM, Q^T from qt); the G query heads of a
+// KV group are the G waves of the workgroup and their dK / dV partials are summed in LDS in a fixed
+// order (deterministic). Reference: autograd of the eager attention under dp_actor.py:90-280.
+struct FlashBwdArgs {
+  const uint16_t* q;      // (B, Hkv, G, T, D)
+  const uint16_t* qt;     // (B, Hkv, G, D, ld_t)
+  const uint16_t* k;      // (B, Hkv, T, D)
+  const uint16_t* kt;     // (B, Hkv, D, ld_t)
+  const uint16_t* v;      // (B, Hkv, T, D)
+  const uint16_t* o;      // (B, T, Hkv, G, D)
+  const uint16_t* dout;   // (B, T, Hkv, G, D)
+  const uint16_t* doutt;  // (Hkv * G * D, ld_n), column b * T + t
+  const float* lse;       // (B, Hkv, G, T)
+  const uint8_t* valid;
+  int64_t ld_valid;
+  float* delta;  // (B, Hkv, G, T)
+  uint16_t* dq;  // (B, Hkv, G, T, D)
+  uint16_t* dk;  // (B, Hkv, T, D)
+  uint16_t* dv;  // (B, Hkv, T, D)
+  int64_t Hkv, G, T, ld_t, ld_n;
+  float scale, scale_log2;
+};
+
+__device__ __forceinline__ float bf2f(uint16_t x) { return bf16_to_f32(x); }
+
+// 8 elements of a k-step in the accumulator's permuted k order: positions p0 + 16s + 4h + {0..3} and
+// p0 + 16s + 8 + 4h + {0..3} of a position-contiguous row; positions >= lim read as zero.
+__device__ __forceinline__ u16x8 load_perm8(const uint16_t* row, int64_t pa, int64_t lim) {
+  const int64_t pb = pa + 8;
+  u16x4 lo, hi;
+  if (pb + 3 < lim) {
+    lo = *reinterpret_cast<const u16x4*>(row + pa);
+    hi = *reinterpret_cast<const u16x4*>(row + pb);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      lo[j] = pa + j < lim ? row[pa + j] : 0;
+      hi[j] = pb + j < lim ? row[pb + j] : 0;
+    }
+  }
+  return u16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+// dq_kernel's per-key-block tiles in LDS, shared by the G waves (query heads) of the workgroup:
+// K and V row-major [32 keys][D] (rows padded to D + 8 elements) and K^T [D][32 keys] (rows of 36).
+template <int D>
+struct DqTile {
+  static constexpr int ROW = D + 8, TROW = 36;
+  static constexpr int RSZ = 32 * ROW, TSZ = D * TROW;
+  static constexpr int RCH = 32 * D / 8;        // 16-B chunks of one row-major tile
+  static constexpr int NCH = 2 * RCH + D * 4;   // K, V, K^T
+  static constexpr int CPT = (NCH + 511) / 512;
+};
+
+template <int D>
+__device__ __forceinline__ void dq_issue(const uint16_t* kb, const uint16_t* vb, const uint16_t* ktb, int64_t ld_t,
+                                         int k0, int T, int tid, u16x8 (&r)[DqTile<D>::CPT]) {
+  using TL = DqTile<D>;
+#pragma unroll
+  for (int i = 0; i < TL::CPT; ++i) {
+    const int c = tid + 512 * i;
+    u16x8 v = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    if (c < 2 * TL::RCH) {
+      const int cc = c % TL::RCH, row = cc / (D / 8), col = cc % (D / 8);
+      const int key = k0 + row;
+      if (key < T) v = *reinterpret_cast<const u16x8*>((c < TL::RCH ? kb : vb) + static_cast<int64_t>(key) * D + col * 8);
+    } else if (c < TL::NCH) {
+      const int cc = c - 2 * TL::RCH, d = cc / 4, col = cc % 4;
+      const int kk = k0 + col * 8;
+      const uint16_t* src = ktb + static_cast<int64_t>(d) * ld_t + kk;
+      if (kk + 7 < T) {
+        v = *reinterpret_cast<const u16x8*>(src);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (kk + j < T) v[j] = src[j];
+      }
+    }
+    r[i] = v;
+  }
+}
+
+template <int D>
+__device__ __forceinline__ void dq_store(uint16_t* kl, uint16_t* vl, uint16_t* ktl, int tid,
+                                         const u16x8 (&r)[DqTile<D>::CPT]) {
+  using TL = DqTile<D>;
+#pragma unroll
+  for (int i = 0; i < TL::CPT; ++i) {
+    const int c = tid + 512 * i;
+    if (c < 2 * TL::RCH) {
+      const int cc = c % TL::RCH, row = cc / (D / 8), col = cc % (D / 8);
+      *reinterpret_cast<u16x8*>((c < TL::RCH ? kl : vl) + row * TL::ROW + col * 8) = r[i];
+    } else if (c < TL::NCH) {
+      const int cc = c - 2 * TL::RCH, d = cc / 4, col = cc % 4;
+      uint16_t* dst = ktl + d * TL::TROW + col * 8;
+      *reinterpret_cast<u16x4*>(dst) = u16x4{r[i][0], r[i][1], r[i][2], r[i][3]};
+      *reinterpret_cast<u16x4*>(dst + 4) = u16x4{r[i][4], r[i][5], r[i][6], r[i][7]};
+    }
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(512) void flash_dq_kernel(FlashBwdArgs a) {
+  constexpr int KS = D / 16, MT = D / 32;
+  using TL = DqTile<D>;
+  __shared__ __attribute__((aligned(16))) uint16_t lds_k[2][TL::RSZ];
+  __shared__ __attribute__((aligned(16))) uint16_t lds_v[2][TL::RSZ];
+  __shared__ __attribute__((aligned(16))) uint16_t lds_kt[2][TL::TSZ];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, g = tid >> 6;
+  const bool computes = g < a.G;
+  const int qi = lane & 31, h = lane >> 5;
+  const int64_t bh = blockIdx.y, b = bh / a.Hkv, hkv = bh % a.Hkv;
+  const int T = static_cast<int>(a.T);
+  const int ntiles = (T + 31) / 32;
+  const int t0 = (ntiles - 1 - static_cast<int>(blockIdx.x)) * 32;
+  const int tq = t0 + qi;
+  const bool qvalid = computes && tq < T;
+  const int64_t head = bh * a.G + (computes ? g : 0);
+  bf16x8 qf[KS], dof[KS];
+  float dl = 0.f;
+  {
+    const uint16_t* qrow = a.q + (head * T + (qvalid ? tq : 0)) * D + 8 * h;
+    const int64_t orow_off = (((b * T + (qvalid ? tq : 0)) * a.Hkv + hkv) * a.G + (computes ? g : 0)) * D + 8 * h;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      u16x8 qv = *reinterpret_cast<const u16x8*>(qrow + 16 * s);
+      u16x8 dv = *reinterpret_cast<const u16x8*>(a.dout + orow_off + 16 * s);
+      const u16x8 ov = *reinterpret_cast<const u16x8*>(a.o + orow_off + 16 * s);
+      if (!qvalid) qv = dv = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dl = fmaf(bf2f(dv[j]), bf2f(ov[j]), dl);
+      qf[s] = as_bf16x8(qv);
+      dof[s] = as_bf16x8(dv);
+    }
+  }
+  dl += __shfl_xor(dl, 32, kWave);  // delta = rowsum(dO * O) of query tq
+  if (qvalid && h == 0) a.delta[head * T + tq] = dl;
+  const float lse2 = qvalid ? a.lse[head * T + tq] * 1.4426950408889634f : -INFINITY;
+  const float lref = lse2 == -INFINITY ? INFINITY : lse2;  // exp2(x - inf) = 0 for rows with no allowed key
+  f32x16 dqt[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) dqt[mt] = f32x16{};
+  const uint16_t* kbase = a.k + bh * a.T * D;
+  const uint16_t* vbase = a.v + bh * a.T * D;
+  const uint16_t* ktbase = a.kt + bh * D * a.ld_t;
+  const uint8_t* vrow = a.valid + b * a.ld_valid;
+  const int nb = (min(T, t0 + 32) + 31) / 32;
+  u16x8 stage[TL::CPT];
+  dq_issue<D>(kbase, vbase, ktbase, a.ld_t, 0, T, tid, stage);
+  dq_store<D>(lds_k[0], lds_v[0], lds_kt[0], tid, stage);
+  __syncthreads();
+  for (int ib = 0; ib < nb; ++ib) {
+    const int cur = ib & 1, k0 = ib * 32;
+    if (ib + 1 < nb) dq_issue<D>(kbase, vbase, ktbase, a.ld_t, k0 + 32, T, tid, stage);
+    if (computes) {
+      f32x16 st = f32x16{}, dpt = f32x16{};
+      const uint16_t* kr = lds_k[cur] + qi * TL::ROW + 8 * h;
+      const uint16_t* vr = lds_v[cur] + qi * TL::ROW + 8 * h;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const u16x8 kv = *reinterpret_cast<const u16x8*>(kr + 16 * s);
+        const u16x8 vv = *reinterpret_cast<const u16x8*>(vr + 16 * s);
+        st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(kv), qf[s], st, 0, 0, 0);
+        dpt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(vv), dof[s], dpt, 0, 0, 0);
+      }
+      const int kbase0 = k0 + 4 * h;
+      uint32_t vw[4];
+      bool allv = true;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int kb = kbase0 + 8 * c;
+        if (kb + 3 < T) {
+          vw[c] = *reinterpret_cast<const uint32_t*>(vrow + kb);
+        } else {
+          vw[c] = 0;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) vw[c] |= (kb + j < T ? static_cast<uint32_t>(vrow[kb + j]) : 0u) << (8 * j);
+        }
+        allv &= vw[c] == 0x01010101u;
+      }
+      const bool full = __all(allv) && k0 + 31 <= t0;
+      u16x8 dsb[2];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int r = 4 * c + j;
+          const bool ok = full || (((vw[c] >> (8 * j)) & 0xffu) != 0u && kbase0 + 8 * c + j <= tq);
+          const float p = ok ? __builtin_amdgcn_exp2f(st[r] * a.scale_log2 - lref) : 0.f;
+          dsb[r >> 3][r & 7] = to_bf16_bits(p * (dpt[r] - dl));
+        }
+      }
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const uint16_t* ktl = lds_kt[cur] + (32 * mt + qi) * TL::TROW + 4 * h;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const u16x4 lo = *reinterpret_cast<const u16x4*>(ktl + 16 * s);
+          const u16x4 hi = *reinterpret_cast<const u16x4*>(ktl + 16 * s + 8);
+          const u16x8 kv = u16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          dqt[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(kv), as_bf16x8(dsb[s]), dqt[mt], 0, 0, 0);
+        }
+      }
+    }
+    if (ib + 1 < nb) dq_store<D>(lds_k[cur ^ 1], lds_v[cur ^ 1], lds_kt[cur ^ 1], tid, stage);
+    __syncthreads();
+  }
+  if (!qvalid) return;
+  uint16_t* dqrow = a.dq + (head * T + tq) * D;
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const u16x4 w = u16x4{to_bf16_bits(dqt[mt][4 * c] * a.scale), to_bf16_bits(dqt[mt][4 * c + 1] * a.scale),
+                            to_bf16_bits(dqt[mt][4 * c + 2] * a.scale), to_bf16_bits(dqt[mt][4 * c + 3] * a.scale)};
+      *reinterpret_cast<u16x4*>(dqrow + 32 * mt + 8 * c + 4 * h) = w;
+    }
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(512) void flash_dkdv_kernel(FlashBwdArgs a) {
+  constexpr int KS = D / 16, MT = D / 32;
+  __shared__ float red[2][MT][16][64];  // [dk/dv][tile][register][lane]: conflict-free per register
+  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int li = lane & 31, h = lane >> 5;
+  const int64_t bh = blockIdx.y, b = bh / a.Hkv, hkv = bh % a.Hkv;
+  const int64_t ntiles = (a.T + 31) / 32;
+  const int64_t k0 = (ntiles - 1 - static_cast<int64_t>(blockIdx.x)) * 32;  // short causal columns last
+  const int64_t key = k0 + li;
+  const bool kin = key < a.T;
+  const bool kval = kin && a.valid[b * a.ld_valid + key] != 0;
+  const int64_t head = bh * a.G + g;
+  bf16x8 kf[KS], vf[KS];
+  {
+    const uint16_t* krow = a.k + (bh * a.T + (kin ? key : 0)) * D + 8 * h;
+    const uint16_t* vr = a.v + (bh * a.T + (kin ? key : 0)) * D + 8 * h;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      u16x8 kv = *reinterpret_cast<const u16x8*>(krow + 16 * s);
+      u16x8 vv = *reinterpret_cast<const u16x8*>(vr + 16 * s);
+      if (!kin) kv = vv = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      kf[s] = as_bf16x8(kv);
+      vf[s] = as_bf16x8(vv);
+    }
+  }
+  f32x16 dkt[MT], dvt[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) dkt[mt] = dvt[mt] = f32x16{};
+  const uint16_t* qbase = a.q + head * a.T * D;
+  const uint16_t* qtbase = a.qt + head * D * a.ld_t;
+  const float* lser = a.lse + head * a.T;
+  const float* dlr = a.delta + head * a.T;
+  const int64_t colb = b * a.T;  // this sequence's first column of doutt
+  for (int64_t t0 = k0; t0 < a.T; t0 += 32) {
+    // S = Q K^T and dP = dO V^T: A = rows of query t0 + li; C row r -> query t0 + (r&3) + 8(r>>2) + 4h
+    f32x16 sc = f32x16{}, dp = f32x16{};
+    {
+      const int64_t tr = t0 + li;
+      const bool rin = tr < a.T;
+      const uint16_t* qrow = qbase + (rin ? tr : 0) * D + 8 * h;
+      const uint16_t* dorow = a.dout + (((b * a.T + (rin ? tr : 0)) * a.Hkv + hkv) * a.G + g) * D + 8 * h;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        u16x8 qv = *reinterpret_cast<const u16x8*>(qrow + 16 * s);
+        u16x8 dv = *reinterpret_cast<const u16x8*>(dorow + 16 * s);
+        if (!rin) qv = dv = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        sc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(qv), kf[s], sc, 0, 0, 0);
+        dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(dv), vf[s], dp, 0, 0, 0);
+      }
+    }
+    u16x8 pb[2], dsb[2];
+    // block entirely at or below the diagonal, all keys valid, all queries in range: no mask
+    const bool full = __all(kval) && t0 >= k0 + 31 && t0 + 32 <= a.T;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int64_t qb = t0 + 8 * c + 4 * h;
+      float4 l4, d4;
+      if (qb + 3 < a.T) {
+        l4 = *reinterpret_cast<const float4*>(lser + qb);
+        d4 = *reinterpret_cast<const float4*>(dlr + qb);
+      } else {
+        l4 = make_float4(qb < a.T ? lser[qb] : -INFINITY, qb + 1 < a.T ? lser[qb + 1] : -INFINITY,
+                         qb + 2 < a.T ? lser[qb + 2] : -INFINITY, -INFINITY);
+        d4 = make_float4(qb < a.T ? dlr[qb] : 0.f, qb + 1 < a.T ? dlr[qb + 1] : 0.f, qb + 2 < a.T ? dlr[qb + 2] : 0.f, 0.f);
+      }
+      const float lv[4] = {l4.x, l4.y, l4.z, l4.w}, dv4[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int r = 4 * c + j;
+        const float l2 = lv[j] == -INFINITY ? INFINITY : lv[j] * 1.4426950408889634f;  // no allowed key: p = 0
+        const bool ok = full || (kval && key <= qb + j);
+        const float p = ok ? __builtin_amdgcn_exp2f(sc[r] * a.scale_log2 - l2) : 0.f;
+        pb[r >> 3][r & 7] = to_bf16_bits(p);
+        dsb[r >> 3][r & 7] = to_bf16_bits(p * (dp[r] - dv4[j]));
+      }
+    }
+    // dV^T += dO^T P and dK^T += Q^T dS (A operands: head-dim-major rows, positions permuted per k-step)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int64_t d = 32 * mt + li;
+      const uint16_t* dotrow = a.doutt + ((hkv * a.G + g) * D + d) * a.ld_n + colb;
+      const uint16_t* qtrow = qtbase + d * a.ld_t;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int64_t pa = t0 + 16 * s + 4 * h;
+        const u16x8 dov = load_perm8(dotrow, pa, a.T);
+        const u16x8 qv = load_perm8(qtrow, pa, a.T);
+        dvt[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(dov), as_bf16x8(pb[s]), dvt[mt], 0, 0, 0);
+        dkt[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(qv), as_bf16x8(dsb[s]), dkt[mt], 0, 0, 0);
+      }
+    }
+  }
+  // sum the G heads' partials in LDS in wave order (deterministic), wave 0 writes
+  for (int w = 0; w < a.G; ++w) {
+    if (g == w) {
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          red[0][mt][r][lane] = (w == 0 ? 0.f : red[0][mt][r][lane]) + dkt[mt][r];
+          red[1][mt][r][lane] = (w == 0 ? 0.f : red[1][mt][r][lane]) + dvt[mt][r];
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (g != 0 || !kin) return;
+  uint16_t* dkrow = a.dk + (bh * a.T + key) * D;
+  uint16_t* dvrow = a.dv + (bh * a.T + key) * D;
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      u16x4 wk, wv;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        wk[j] = to_bf16_bits(red[0][mt][4 * c + j][lane] * a.scale);
+        wv[j] = to_bf16_bits(red[1][mt][4 * c + j][lane]);
+      }
+      *reinterpret_cast<u16x4*>(dkrow + 32 * mt + 8 * c + 4 * h) = wk;
+      *reinterpret_cast<u16x4*>(dvrow + 32 * mt + 8 * c + 4 * h) = wv;
+    }
+  }
+}
+
 }  // namespace
 }  // namespace drl
 
@@ -182,6 +621,7 @@ int drl_flash_attn_fwd(const void* q, const void* k, const void* vt, int32_t dt,
   DRL_CHECK_ARG(B >= 1 && Hkv >= 1 && G >= 1 && G <= 8 && Tq >= 1 && Tk >= 1 && qoff >= 0, "bad shape");
   DRL_CHECK_ARG(ld_vt >= Tk && ld_vt % 8 == 0, "ld_vt must be >= Tk and a multiple of 8");
   DRL_CHECK_ARG(ld_k >= Tk, "ld_k < Tk");
+  DRL_CHECK_ARG(Tk + qoff < (int64_t(1) << 30), "positions must fit in 32 bits");
   DRL_CHECK_ARG(ld_valid >= Tk && ld_valid % 4 == 0 && (reinterpret_cast<uintptr_t>(key_valid) & 3u) == 0,
                 "key_valid rows must be 4-byte aligned");
   DRL_CHECK_ARG(aligned16(q) && aligned16(k) && aligned16(vt) && (reinterpret_cast<uintptr_t>(out) & 7u) == 0,
@@ -190,10 +630,44 @@ int drl_flash_attn_fwd(const void* q, const void* k, const void* vt, int32_t dt,
               key_valid, ld_valid, static_cast<uint16_t*>(out), lse, Hkv, G, Tq, Tk, ld_k, ld_vt, qoff,
               scale * 1.4426950408889634f};
   const dim3 grid(static_cast<unsigned>((Tq + 31) / 32), static_cast<unsigned>(B * Hkv));
-  const dim3 block(static_cast<unsigned>(64 * G));
+  const dim3 block(512);  // waves >= G stage K/V only
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (D == 64) hipLaunchKernelGGL(flash_fwd_kernel<64>, grid, block, 0, s, a);
   else hipLaunchKernelGGL(flash_fwd_kernel<128>, grid, block, 0, s, a);
+  DRL_LAUNCH_CHECK();
+  return DRL_OK;
+}
+
+int drl_flash_attn_bwd(const void* q, const void* qt, const void* k, const void* kt, const void* v, const void* o,
+                       const void* dout, const void* doutt, int64_t ld_n, const float* lse, int32_t dt,
+                       const uint8_t* key_valid, int64_t ld_valid, int64_t B, int64_t Hkv, int64_t G, int64_t D,
+                       int64_t T, int64_t ld_t, float scale, float* delta, void* dq, void* dk, void* dv,
+                       void* stream) {
+  using namespace drl;
+  DRL_CHECK_ARG(q && qt && k && kt && v && o && dout && doutt && lse && key_valid && delta && dq && dk && dv,
+                "NULL input");
+  DRL_CHECK_ARG(dt == DRL_BF16, "flash attention runs on bf16 operands");
+  DRL_CHECK_ARG(D == 64 || D == 128, "head_dim must be 64 or 128");
+  DRL_CHECK_ARG(B >= 1 && Hkv >= 1 && G >= 1 && G <= 8 && T >= 1, "bad shape");
+  DRL_CHECK_ARG(T % 4 == 0 && ld_t >= T && ld_t % 4 == 0 && ld_n >= B * T && ld_n % 4 == 0,
+                "T, ld_t and ld_n must be multiples of 4 (8-byte position runs)");
+  DRL_CHECK_ARG(ld_valid >= T, "ld_valid < T");
+  FlashBwdArgs a{static_cast<const uint16_t*>(q), static_cast<const uint16_t*>(qt), static_cast<const uint16_t*>(k),
+                 static_cast<const uint16_t*>(kt), static_cast<const uint16_t*>(v), static_cast<const uint16_t*>(o),
+                 static_cast<const uint16_t*>(dout), static_cast<const uint16_t*>(doutt), lse, key_valid, ld_valid,
+                 delta, static_cast<uint16_t*>(dq), static_cast<uint16_t*>(dk), static_cast<uint16_t*>(dv), Hkv, G, T,
+                 ld_t, ld_n, scale, scale * 1.4426950408889634f};
+  const dim3 grid(static_cast<unsigned>((T + 31) / 32), static_cast<unsigned>(B * Hkv));
+  const dim3 block_dq(512);  // waves >= G only stage K / V / K^T
+  const dim3 block_kv(static_cast<unsigned>(64 * G));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (D == 64) {
+    hipLaunchKernelGGL(flash_dq_kernel<64>, grid, block_dq, 0, s, a);
+    hipLaunchKernelGGL(flash_dkdv_kernel<64>, grid, block_kv, 0, s, a);
+  } else {
+    hipLaunchKernelGGL(flash_dq_kernel<128>, grid, block_dq, 0, s, a);
+    hipLaunchKernelGGL(flash_dkdv_kernel<128>, grid, block_kv, 0, s, a);
+  }
   DRL_LAUNCH_CHECK();
   return DRL_OK;
 }

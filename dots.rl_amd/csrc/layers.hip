@@ -37,8 +37,12 @@ struct RopeArgs {
   E* v;
   int64_t B, T, Hq, Hkv, D, Tk, koff, maxpos;
   const int64_t* koff_dev;  // device key offset (graph-captured decode) overriding koff when non-NULL
-  E* vt;                    // optional: V written transposed (B, Hkv, D, ld_vt) for the flash-attention kernel
-  int64_t ld_vt;
+  // optional head-dim-major copies for the fused attention kernels (row stride ld_t over key positions):
+  // qt (B, Hkv, G, D, ld_t), kt / vt (B, Hkv, D, ld_t)
+  E* qt;
+  E* kt;
+  E* vt;
+  int64_t ld_t;
 };
 
 template <typename E>
@@ -64,22 +68,32 @@ __global__ __launch_bounds__(256) void rope_qkv_fwd_kernel(RopeArgs<E> a) {
       // rotate_half: out1 = x1*cos - x2*sin ; out2 = x2*cos + x1*sin
       const float o1 = x1 * c - x2 * s, o2 = x2 * c + x1 * s;
       E* dst;
+      E* dstt;  // transposed copy (nullptr: not requested)
       if (h < a.Hq) {
         const int64_t g = h / G, hi = h % G;
         dst = a.q + (((b * a.Hkv + g) * G + hi) * a.T + t) * a.D;
+        dstt = a.qt ? a.qt + ((b * a.Hkv + g) * G + hi) * a.D * a.ld_t + t : nullptr;
       } else {
         dst = a.k + ((b * a.Hkv + (h - a.Hq)) * a.Tk + koff + t) * a.D;
+        dstt = a.kt ? a.kt + (b * a.Hkv + (h - a.Hq)) * a.D * a.ld_t + koff + t : nullptr;
       }
       stf(dst, j, o1);
       stf(dst, j + half, o2);
-    } else if (a.vt != nullptr) {
-      E* dst = a.vt + (b * a.Hkv + (h - a.Hq - a.Hkv)) * a.D * a.ld_vt + koff + t;
-      dst[j * a.ld_vt] = src[j];
-      dst[(j + half) * a.ld_vt] = src[j + half];
+      if (dstt) {
+        stf(dstt, j * a.ld_t, o1);
+        stf(dstt, (j + half) * a.ld_t, o2);
+      }
     } else {
-      E* dst = a.v + ((b * a.Hkv + (h - a.Hq - a.Hkv)) * a.Tk + koff + t) * a.D;
-      dst[j] = src[j];
-      dst[j + half] = src[j + half];
+      if (a.vt != nullptr) {
+        E* dst = a.vt + (b * a.Hkv + (h - a.Hq - a.Hkv)) * a.D * a.ld_t + koff + t;
+        dst[j * a.ld_t] = src[j];
+        dst[(j + half) * a.ld_t] = src[j + half];
+      }
+      if (a.v != nullptr) {
+        E* dst = a.v + ((b * a.Hkv + (h - a.Hq - a.Hkv)) * a.Tk + koff + t) * a.D;
+        dst[j] = src[j];
+        dst[j + half] = src[j + half];
+      }
     }
   }
 }
@@ -468,17 +482,18 @@ extern "C" {
 
 int drl_rope_qkv_fwd(const void* qkv, int32_t dt, const int64_t* position_ids, const float* cos_t, const float* sin_t,
                      int64_t maxpos, int64_t B, int64_t T, int64_t Hq, int64_t Hkv, int64_t D, void* q, void* k,
-                     void* v, int64_t Tk, int64_t koff, const int64_t* koff_dev, void* vt, int64_t ld_vt,
-                     void* stream) {
+                     void* v, int64_t Tk, int64_t koff, const int64_t* koff_dev, void* qt, void* kt, void* vt,
+                     int64_t ld_t, void* stream) {
   using namespace drl;
   DRL_CHECK_ARG(qkv && position_ids && cos_t && sin_t && q && k && (v || vt), "NULL input");
-  DRL_CHECK_ARG(vt == nullptr || ld_vt >= Tk, "ld_vt < Tk");
+  DRL_CHECK_ARG((qt == nullptr && kt == nullptr && vt == nullptr) || (ld_t >= Tk && ld_t >= T), "ld_t too small");
   DRL_CHECK_ARG(B >= 1 && T >= 1 && Hq >= 1 && Hkv >= 1 && Hq % Hkv == 0 && D % 2 == 0, "bad shape");
   DRL_CHECK_ARG(koff >= 0 && koff + T <= Tk, "key offset out of range");
   const int64_t n = B * T * (Hq + 2 * Hkv) * (D / 2);
   DRL_E_DISPATCH(dt, {
     RopeArgs<E> a{static_cast<const E*>(qkv), position_ids, cos_t, sin_t, static_cast<E*>(q), static_cast<E*>(k),
-                  static_cast<E*>(v), B, T, Hq, Hkv, D, Tk, koff, maxpos, koff_dev, static_cast<E*>(vt), ld_vt};
+                  static_cast<E*>(v), B, T, Hq, Hkv, D, Tk, koff, maxpos, koff_dev, static_cast<E*>(qt),
+                  static_cast<E*>(kt), static_cast<E*>(vt), ld_t};
     hipLaunchKernelGGL(rope_qkv_fwd_kernel<E>, dim3(grid_stride(n)), dim3(256), 0, static_cast<hipStream_t>(stream), a);
   });
   DRL_LAUNCH_CHECK();

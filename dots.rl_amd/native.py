@@ -327,15 +327,18 @@ def _edt(t):
         raise ValueError(f"activation dtype {t.dtype} not supported (bfloat16 / float32)") from e
 
 
-def rope_qkv_fwd(qkv, position_ids, cos_t, sin_t, Hq, Hkv, D, q, k, v, koff=0, koff_dev=None, vt=None):
+def rope_qkv_fwd(qkv, position_ids, cos_t, sin_t, Hq, Hkv, D, q, k, v, koff=0, koff_dev=None, vt=None, qt=None,
+                 kt=None):
     """qkv (B,T,(Hq+2Hkv)D) -> q (B,Hkv,G,T,D); k, v written at [:, :, koff:koff+T] of (B,Hkv,Tk,D).
 
-    ``koff_dev`` (device int64 scalar) replaces ``koff`` for graph-captured decode steps; with ``vt``
-    ((B,Hkv,D,ld) view, last dim contiguous) V is written transposed there instead of ``v``."""
+    ``koff_dev`` (device int64 scalar) replaces ``koff`` for graph-captured decode steps. ``qt`` (B,Hkv,G,D,ld),
+    ``kt`` / ``vt`` (B,Hkv,D,ld): head-dim-major copies for the fused attention kernels (same ld)."""
     B, T = qkv.shape[0], qkv.shape[1]
+    lds = {t.stride(-2) for t in (qt, kt, vt) if t is not None}
+    assert len(lds) <= 1, "qt / kt / vt must share their row stride"
     check(lib().drl_rope_qkv_fwd(_p(qkv), _edt(qkv), _p(position_ids), _p(cos_t), _p(sin_t), cos_t.shape[0], B, T,
-                                 Hq, Hkv, D, _p(q), _p(k), _p(v), k.shape[2], koff, _p(koff_dev), _p(vt),
-                                 0 if vt is None else vt.stride(2), _stream()),
+                                 Hq, Hkv, D, _p(q), _p(k), _p(v), k.shape[2], koff, _p(koff_dev), _p(qt), _p(kt),
+                                 _p(vt), lds.pop() if lds else 0, _stream()),
           "drl_rope_qkv_fwd")
 
 
@@ -414,3 +417,19 @@ def flash_attn_fwd(q, k, vt, key_valid, out, Tk=None, qoff=0, lse=None):
                                    _stream()),
           "drl_flash_attn_fwd")
     return out
+
+
+def flash_attn_bwd(q, qt, k, kt, v, o, dout, doutt, lse, key_valid, dq, dk, dv):
+    """Backward of flash_attn_fwd (Tq == Tk, qoff 0): q (B,Hkv,G,T,D), qt (B,Hkv,G,D,ld), k/v (B,Hkv,T,D),
+    kt (B,Hkv,D,ld), o/dout (B,T,Hq*D), doutt (Hq*D, >=B*T) = dout transposed, lse (B,Hkv,G,T) ->
+    dq (B,Hkv,G,T,D), dk/dv (B,Hkv,T,D)."""
+    _dev(q, qt, k, kt, v, o, dout, doutt, lse, key_valid, dq, dk, dv)
+    B, Hkv, G, T, D = q.shape
+    assert qt.stride(-2) == kt.stride(-2) and doutt.stride(1) == 1 and qt.stride(-1) == 1 and kt.stride(-1) == 1
+    for t in (q, k, v, o, dout, lse, dq, dk, dv):
+        assert t.is_contiguous()
+    delta = _ws.get(B * Hkv * G * T * 4, q.device)
+    check(lib().drl_flash_attn_bwd(_p(q), _p(qt), _p(k), _p(kt), _p(v), _p(o), _p(dout), _p(doutt), doutt.stride(0),
+                                   _p(lse), _edt(q), _p(key_valid), key_valid.stride(0), B, Hkv, G, D, T,
+                                   qt.stride(-2), 1.0 / math.sqrt(D), _p(delta), _p(dq), _p(dk), _p(dv), _stream()),
+          "drl_flash_attn_bwd")

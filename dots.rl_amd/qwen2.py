@@ -6,11 +6,12 @@ rewrites the bf16 copy in the same pass; data-parallel gradient averaging is a s
 the flat gradient; GEMM weight gradients accumulate straight into fp32 (hipBLASLt bf16 x bf16 -> fp32),
 so micro-batch accumulation never rounds through bf16.
 
-Per decoder layer the GEMMs run on hipBLASLt and everything else on the HIP kernels of
-``csrc/layers.hip``: residual-add + RMSNorm, QKV split + RoPE + grouped-query re-layout (the 7 query
-heads of a KV head become one GEMM's rows, so K/V are never expanded), causal + key-padding masked
-softmax over fp32 scores, SwiGLU; the backward of a whole layer is hand-written (``_DecoderLayer``).
-Decode uses the same kernels against a preallocated KV cache.
+Per decoder layer the GEMMs run on hipBLASLt and everything else on hand-written HIP kernels:
+``csrc/layers.hip`` (residual-add + RMSNorm, QKV split + RoPE + grouped-query re-layout so the 7 query
+heads of a KV head share one K/V stream, SwiGLU), ``csrc/flash_attn.hip`` (fused MFMA attention forward
+and backward for bf16 full sequences; the fp32 parity model uses fp32-score GEMMs + masked softmax) and
+``csrc/attention.hip`` (decode attention over the preallocated KV cache). The backward of a whole layer
+is hand-written (``_DecoderLayer``).
 
 Semantics follow HF ``Qwen2ForCausalLM`` as the reference runs it (dp_actor.py:110 autocast bf16 over
 fp32 master weights): bf16 GEMM inputs with fp32 accumulation, fp32 RMSNorm and residual stream, fp32
@@ -234,10 +235,27 @@ def _layer_forward(m, i, x_prev, delta, pos, key_valid, save, cache=None, koff=0
     qkv = torch.addmm(s.w(p + "qkv_proj.bias").to(dt), h1.view(B * T, H), s.w(p + "qkv_proj.weight").t())
     qkv = qkv.view(B, T, -1)
     q = torch.empty(B, Hkv, G, T, D, dtype=dt, device=dev)
-    # no-grad full-sequence passes (log-probs, prefill) run the fused MFMA attention (csrc/flash_attn.hip);
-    # the training forward keeps the probabilities for the hand-written backward
-    flash = (save is None and T > 1 and dt == torch.bfloat16 and D in (64, 128) and G <= 8
-             and key_valid.stride(0) % 4 == 0)
+    # bf16 full-sequence passes run the fused MFMA attention (csrc/flash_attn.hip): log-probs and prefill
+    # forward-only, the training forward with the LSE its fused backward needs; the unfused path (fp32 scores
+    # GEMM + masked softmax + PV GEMM, probabilities kept for the backward) serves the fp32 parity model
+    flash_ok = T > 1 and dt == torch.bfloat16 and D in (64, 128) and G <= 8 and key_valid.stride(0) % 4 == 0
+    flash = save is None and flash_ok
+    if save is not None and flash_ok and cache is None and T % 8 == 0:
+        # training forward: fused attention that saves only the LSE; the backward (flash_attn_bwd)
+        # recomputes P and needs head-dim-major copies of q and k besides row-major k and v
+        kbuf = torch.empty(B, Hkv, T, D, dtype=dt, device=dev)
+        vbuf = torch.empty_like(kbuf)
+        qt = torch.empty(B, Hkv, G, D, T, dtype=dt, device=dev)
+        kt = torch.empty(B, Hkv, D, T, dtype=dt, device=dev)
+        vt = torch.empty(B, Hkv, D, T, dtype=dt, device=dev)
+        native.rope_qkv_fwd(qkv, pos, m.cos, m.sin, Hq, Hkv, D, q, kbuf, vbuf, qt=qt, kt=kt, vt=vt)
+        attn = torch.empty(B, T, Hq * D, dtype=dt, device=dev)
+        lse = torch.empty(B, Hkv, G, T, dtype=torch.float32, device=dev)
+        native.flash_attn_fwd(q, kbuf, vt, key_valid, attn, lse=lse)
+        del vt
+        save.update(qt=qt, kt=kt, lse=lse, key_valid=key_valid)
+        P = "flash"
+        return _layer_mlp(m, i, x, attn, save, kbuf, vbuf, P, q, h1, rstd1)
     vt = None
     if cache is None:
         kbuf = torch.empty(B, Hkv, T, D, dtype=dt, device=dev)
@@ -282,6 +300,17 @@ def _layer_forward(m, i, x_prev, delta, pos, key_valid, save, cache=None, koff=0
         attn = O.view(B, 1, Hq * D)
     else:
         attn = O.view(B, Hkv, G, T, D).permute(0, 3, 1, 2, 4).reshape(B, T, Hq * D)
+    return _layer_mlp(m, i, x, attn, save, kbuf, vbuf, P, q, h1, rstd1)
+
+
+def _layer_mlp(m, i, x, attn, save, kbuf, vbuf, P, q, h1, rstd1):
+    """o_proj + residual + post-attention RMSNorm + SwiGLU MLP of layer i (shared by both attention paths)."""
+    cfg, s, dt = m.cfg, m.store, m.dtype
+    B, T, H = x.shape
+    Hq = cfg.num_attention_heads
+    D = cfg.head_dim
+    p = f"layers.{i}."
+    dev = x.device
     o = attn.view(B * T, Hq * D) @ s.w(p + "o_proj").t()
     x2 = torch.empty_like(x)
     h2 = torch.empty(B, T, H, dtype=dt, device=dev)
@@ -330,18 +359,28 @@ class _DecoderLayer(torch.autograd.Function):
         do = dx2.to(dt).view(N, H)
         dattn = do @ s.w(p + "o_proj")
         acc_wgrad(s.g(p + "o_proj"), do, sv["attn"].reshape(N, Hq * D))
-        dO = dattn.view(B, T, Hkv, G, D).permute(0, 2, 3, 1, 4).reshape(B * Hkv, G * T, D)
-        q3 = sv["q"].view(B * Hkv, G * T, D)
-        k3 = sv["k"].view(B * Hkv, T, D)
-        v3 = sv["v"].view(B * Hkv, T, D)
-        P = sv["P"]
-        dP = bmm_f32(dO, v3.transpose(1, 2))  # fp32 (B*Hkv, G*T, T)
-        dv = torch.bmm(P.transpose(1, 2), dO)  # (B*Hkv, T, D): sums the 7 query heads of the group
-        dS = torch.empty_like(P)
-        native.masked_softmax_bwd(P, dP, dS, B * Hkv * G * T, T, 1.0 / math.sqrt(D))
-        del dP
-        dq = torch.bmm(dS, k3)
-        dk = torch.bmm(dS.transpose(1, 2), q3)
+        if isinstance(sv["P"], str):  # "flash": fused forward, fused backward
+            # fused attention backward; dO^T comes from the same GEMM with swapped operands
+            dattn_t = torch.mm(s.w(p + "o_proj").t(), do.t())  # (Hq*D, N)
+            dq = torch.empty_like(sv["q"])
+            dk = torch.empty_like(sv["k"])
+            dv = torch.empty_like(sv["v"])
+            native.flash_attn_bwd(sv["q"], sv["qt"], sv["k"], sv["kt"], sv["v"], sv["attn"], dattn.view(B, T, Hq * D),
+                                  dattn_t, sv["lse"], sv["key_valid"], dq, dk, dv)
+            del dattn_t
+        else:
+            dO = dattn.view(B, T, Hkv, G, D).permute(0, 2, 3, 1, 4).reshape(B * Hkv, G * T, D)
+            q3 = sv["q"].view(B * Hkv, G * T, D)
+            k3 = sv["k"].view(B * Hkv, T, D)
+            v3 = sv["v"].view(B * Hkv, T, D)
+            P = sv["P"]
+            dP = bmm_f32(dO, v3.transpose(1, 2))  # fp32 (B*Hkv, G*T, T)
+            dv = torch.bmm(P.transpose(1, 2), dO)  # (B*Hkv, T, D): sums the 7 query heads of the group
+            dS = torch.empty_like(P)
+            native.masked_softmax_bwd(P, dP, dS, B * Hkv * G * T, T, 1.0 / math.sqrt(D))
+            del dP
+            dq = torch.bmm(dS, k3)
+            dk = torch.bmm(dS.transpose(1, 2), q3)
         dqkv = torch.empty(B, T, (Hq + 2 * Hkv) * D, dtype=dt, device=dx2.device)
         native.rope_qkv_bwd(dq, dk, dv, ctx.pos, m.cos, m.sin, Hq, Hkv, D, dqkv)
         dqkv2 = dqkv.view(N, -1)

@@ -220,12 +220,13 @@ int drl_adamw_step(float* params, const float* grads, float* exp_avg, float* exp
 /* qkv (B,T,(Hq+2Hkv)*D) -> RoPE'd q in grouped layout (B,Hkv,Hq/Hkv,T,D), RoPE'd k and v written at
  * key offset koff of (B,Hkv,Tk,D) buffers (the KV cache when decoding). cos/sin: (maxpos, D/2) fp32.
  * koff_dev (optional device int64 scalar) replaces koff — graph-captured decode steps; an out-of-range
- * device offset writes nothing. With vt != NULL, V is written transposed to vt (B,Hkv,D,ld_vt) instead
- * of v (the layout drl_flash_attn_fwd reads). */
+ * device offset writes nothing. Optional head-dim-major copies for the fused attention kernels, row
+ * stride ld_t over positions: qt (B,Hkv,G,D,ld_t), kt and vt (B,Hkv,D,ld_t); v may be NULL when vt
+ * is given. */
 int drl_rope_qkv_fwd(const void* qkv, int32_t dt, const int64_t* position_ids, const float* cos_t, const float* sin_t,
                      int64_t maxpos, int64_t B, int64_t T, int64_t Hq, int64_t Hkv, int64_t D, void* q, void* k,
-                     void* v, int64_t Tk, int64_t koff, const int64_t* koff_dev, void* vt, int64_t ld_vt,
-                     void* stream);
+                     void* v, int64_t Tk, int64_t koff, const int64_t* koff_dev, void* qt, void* kt, void* vt,
+                     int64_t ld_t, void* stream);
 int drl_rope_qkv_bwd(const void* dq, const void* dk, const void* dv, int32_t dt, const int64_t* position_ids,
                      const float* cos_t, const float* sin_t, int64_t maxpos, int64_t B, int64_t T, int64_t Hq,
                      int64_t Hkv, int64_t D, void* dqkv, void* stream);
@@ -274,6 +275,17 @@ int drl_decode_attention(const void* q, const void* k_cache, const void* v_cache
 int drl_flash_attn_fwd(const void* q, const void* k, const void* vt, int32_t dt, const uint8_t* key_valid,
                        int64_t ld_valid, int64_t B, int64_t Hkv, int64_t G, int64_t D, int64_t Tq, int64_t Tk,
                        int64_t ld_k, int64_t ld_vt, int64_t qoff, float scale, void* out, float* lse, void* stream);
+/* Backward of drl_flash_attn_fwd for Tq == Tk == T, qoff = 0 (the training forward), recomputing P from lse:
+ * q (B,Hkv,G,T,D), k / v (B,Hkv,T,D) row-major, qt (B,Hkv,G,D,ld_t) and kt (B,Hkv,D,ld_t) head-dim-major
+ * copies (drl_rope_qkv_fwd writes all of them), o and dout (B,T,Hkv*G*D), doutt = dout transposed
+ * (Hkv*G*D rows of ld_n columns, column b*T + t), lse from the forward. delta: (B,Hkv,G,T) fp32
+ * scratch. Outputs dq (B,Hkv,G,T,D), dk / dv (B,Hkv,T,D) bf16 (the drl_rope_qkv_bwd inputs).
+ * T, ld_t, ld_n multiples of 4. Deterministic (the G heads' dK/dV partials are summed in fixed order). */
+int drl_flash_attn_bwd(const void* q, const void* qt, const void* k, const void* kt, const void* v, const void* o,
+                       const void* dout, const void* doutt, int64_t ld_n, const float* lse, int32_t dt,
+                       const uint8_t* key_valid, int64_t ld_valid, int64_t B, int64_t Hkv, int64_t G, int64_t D,
+                       int64_t T, int64_t ld_t, float scale, float* delta, void* dq, void* dk, void* dv,
+                       void* stream);
 
 #ifdef __cplusplus
 }

@@ -138,6 +138,30 @@ def flash(B=16, Hkv=2, G=7, D=64, T=768):
                  unfused_seconds=t2)]
 
 
+def flash_bwd(B=8, Hkv=2, G=7, D=64, T=768):
+    """Fused attention backward (dq + dkdv launches) at the update micro-batch shape."""
+    dev = "cuda"
+    bf = torch.bfloat16
+    q = torch.randn(B, Hkv, G, T, D, device=dev, dtype=bf)
+    k = torch.randn(B, Hkv, T, D, device=dev, dtype=bf)
+    v = torch.randn(B, Hkv, T, D, device=dev, dtype=bf)
+    qt = q.transpose(-1, -2).contiguous()
+    kt = k.transpose(-1, -2).contiguous()
+    vt = v.transpose(-1, -2).contiguous()
+    valid = torch.ones(B, T, dtype=torch.uint8, device=dev)
+    o = torch.empty(B, T, Hkv * G * D, device=dev, dtype=bf)
+    lse = torch.empty(B, Hkv, G, T, device=dev)
+    native.flash_attn_fwd(q, k, vt, valid, o, lse=lse)
+    dout = torch.randn(B, T, Hkv * G * D, device=dev, dtype=bf)
+    doutt = dout.view(B * T, -1).t().contiguous()
+    dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+    t = time_it(lambda: native.flash_attn_bwd(q, qt, k, kt, v, o, dout, doutt, lse, valid, dq, dk, dv), iters=20)
+    tf = time_it(lambda: native.flash_attn_fwd(q, k, vt, valid, o, lse=lse), iters=20)
+    flops = 4.0 * B * Hkv * G * D * T * (T + 1) / 2
+    return [dict(kernel="flash_attn_bwd", B=B, T=T, seconds=t, TFLOPs=2.5 * flops / t / 1e12,
+                 frac_mfma=2.5 * flops / t / 2.5e15, fwd_seconds=tf)]
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--quick", action="store_true")
@@ -149,7 +173,7 @@ if __name__ == "__main__":
                 print(json.dumps(r), flush=True)
         sys.exit(0)
     if args.only == "flash":
-        for r in flash():
+        for r in flash() + flash_bwd():
             print(json.dumps(r), flush=True)
         sys.exit(0)
     if args.only in ("k1", "k1big"):
