@@ -606,6 +606,166 @@ __global__ __launch_bounds__(512) void flash_dkdv_kernel(FlashBwdArgs a) {
   }
 }
 
+
+// ------------------------------------------------------------------------------------------ decode
+// One new token per sequence against the KV cache, on MFMA: the G query heads of a KV head are the
+// "queries" of the forward kernel's S^T = K Q^T tile (columns >= G are zero padding), so the online
+// softmax stays lane-local and P^T feeds O^T += V^T P^T from the accumulators. Workgroup = (sequence,
+// KV head), 4 waves splitting the cached keys into interleaved 32-key blocks (each wave's next block
+// is loaded while it computes the current one); the 4 partial softmax states are merged in LDS.
+// The cache holds K row-major (B, Hkv, ld_k, D) and V head-dim-major (B, Hkv, D, ld_vt), the layout
+// drl_rope_qkv_fwd writes with koff / koff_dev. HBM-bound: 4 * D bytes per cached key.
+struct DecodeArgs {
+  const uint16_t* q;   // (B, Hkv, G, D)
+  const uint16_t* k;   // (B, Hkv, ld_k, D)
+  const uint16_t* vt;  // (B, Hkv, D, ld_vt)
+  const uint8_t* valid;
+  int64_t ld_valid;
+  const int64_t* qpos_ptr;
+  int64_t qpos;
+  int64_t Hkv, G, ld_k, ld_vt, L;
+  float scale_log2;
+  uint16_t* out;  // (B, Hkv, G, D)
+};
+
+template <int D>
+__device__ __forceinline__ void dec_load(const uint16_t* kb, const uint16_t* vtb, int64_t ld_vt, int k0, int kend,
+                                         int qi, int h, u16x8 (&kf)[D / 16], u16x8 (&vf)[D / 32][2]) {
+  const int key = k0 + qi;
+  const bool kin = key < kend;
+  const uint16_t* krow = kb + static_cast<int64_t>(kin ? key : 0) * D + 8 * h;
+#pragma unroll
+  for (int s = 0; s < D / 16; ++s) {
+    kf[s] = *reinterpret_cast<const u16x8*>(krow + 16 * s);
+    if (!kin) kf[s] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  }
+#pragma unroll
+  for (int mt = 0; mt < D / 32; ++mt) {
+    const uint16_t* vrow = vtb + static_cast<int64_t>(32 * mt + qi) * ld_vt;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) vf[mt][s] = load_perm8(vrow, k0 + 16 * s + 4 * h, kend);
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void decode_mfma_kernel(DecodeArgs a) {
+  constexpr int KS = D / 16, MT = D / 32, NW = 4;
+  __shared__ float s_m[NW][32], s_l[NW][32];
+  __shared__ float s_o[NW][MT][16][64];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int qi = lane & 31, h = lane >> 5;
+  const int64_t bh = blockIdx.x, b = bh / a.Hkv;
+  const int qpos = static_cast<int>(a.qpos_ptr ? *a.qpos_ptr : a.qpos);
+  const int kend = static_cast<int>(min(a.L, static_cast<int64_t>(qpos) + 1));
+  bf16x8 qf[KS];
+  {
+    const bool qv = qi < a.G;
+    const uint16_t* qrow = a.q + (bh * a.G + (qv ? qi : 0)) * D + 8 * h;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      u16x8 v = *reinterpret_cast<const u16x8*>(qrow + 16 * s);
+      if (!qv) v = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      qf[s] = as_bf16x8(v);
+    }
+  }
+  const uint16_t* kb = a.k + bh * a.ld_k * D;
+  const uint16_t* vtb = a.vt + bh * D * a.ld_vt;
+  const uint8_t* vrow = a.valid + b * a.ld_valid;
+  f32x16 o[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) o[mt] = f32x16{};
+  float m = -INFINITY, lsum = 0.f;
+  const int nblk = (kend + 31) / 32;
+  u16x8 kf[KS], vf[MT][2];
+  if (w < nblk) dec_load<D>(kb, vtb, a.ld_vt, 32 * w, kend, qi, h, kf, vf);
+  for (int ib = w; ib < nblk; ib += NW) {
+    const int k0 = 32 * ib;
+    f32x16 st = f32x16{};
+#pragma unroll
+    for (int s = 0; s < KS; ++s) st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(kf[s]), qf[s], st, 0, 0, 0);
+    u16x8 vcur[MT][2];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) vcur[mt][0] = vf[mt][0], vcur[mt][1] = vf[mt][1];
+    if (ib + NW < nblk) dec_load<D>(kb, vtb, a.ld_vt, k0 + 32 * NW, kend, qi, h, kf, vf);  // next block in flight
+    float x[16], mx = -INFINITY;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int kk = k0 + 8 * c + 4 * h;
+      uint32_t vb;
+      if (kk + 3 < kend) {
+        vb = *reinterpret_cast<const uint32_t*>(vrow + kk);
+      } else {
+        vb = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) vb |= (kk + j < kend ? static_cast<uint32_t>(vrow[kk + j]) : 0u) << (8 * j);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int r = 4 * c + j;
+        x[r] = ((vb >> (8 * j)) & 0xffu) != 0u ? st[r] * a.scale_log2 : -INFINITY;
+        mx = fmaxf(mx, x[r]);
+      }
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, kWave));
+    const float mn = fmaxf(m, mx);
+    const float mref = mn == -INFINITY ? 0.f : mn;
+    const float alpha = __builtin_amdgcn_exp2f(m - mref);
+    m = mn;
+    float ps = 0.f;
+    u16x8 pb[2];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float p = __builtin_amdgcn_exp2f(x[r] - mref);
+      ps += p;
+      pb[r >> 3][r & 7] = to_bf16_bits(p);
+    }
+    lsum = lsum * alpha + ps;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      o[mt] *= alpha;
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+        o[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(vcur[mt][s]), as_bf16x8(pb[s]), o[mt], 0, 0, 0);
+    }
+  }
+  // merge the 4 waves' states per query column (head) in a fixed order
+  const float lt = lsum + __shfl_xor(lsum, 32, kWave);
+  if (h == 0) { s_m[w][qi] = m; s_l[w][qi] = lt; }
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s_o[w][mt][r][lane] = o[mt][r];
+  __syncthreads();
+  if (w != 0 || qi >= a.G) return;
+  float mm = -INFINITY;
+#pragma unroll
+  for (int v = 0; v < NW; ++v) mm = fmaxf(mm, s_m[v][qi]);
+  const float mref = mm == -INFINITY ? 0.f : mm;
+  float sc[NW], ll = 0.f;
+#pragma unroll
+  for (int v = 0; v < NW; ++v) {
+    sc[v] = __builtin_amdgcn_exp2f(s_m[v][qi] - mref);
+    ll += s_l[v][qi] * sc[v];
+  }
+  const float inv = ll > 0.f ? 1.f / ll : 0.f;
+  uint16_t* orow = a.out + (bh * a.G + qi) * D;
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      u16x4 wv;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float acc = 0.f;
+#pragma unroll
+        for (int v = 0; v < NW; ++v) acc = fmaf(s_o[v][mt][4 * c + j][lane], sc[v], acc);
+        wv[j] = to_bf16_bits(acc * inv);
+      }
+      *reinterpret_cast<u16x4*>(orow + 32 * mt + 8 * c + 4 * h) = wv;
+    }
+  }
+}
+
 }  // namespace
 }  // namespace drl
 
@@ -668,6 +828,31 @@ int drl_flash_attn_bwd(const void* q, const void* qt, const void* k, const void*
     hipLaunchKernelGGL(flash_dq_kernel<128>, grid, block_dq, 0, s, a);
     hipLaunchKernelGGL(flash_dkdv_kernel<128>, grid, block_kv, 0, s, a);
   }
+  DRL_LAUNCH_CHECK();
+  return DRL_OK;
+}
+
+int drl_decode_attention_vt(const void* q, const void* k_cache, const void* vt_cache, int32_t dt,
+                            const uint8_t* key_valid, int64_t ld_valid, const int64_t* qpos_ptr, int64_t qpos,
+                            int64_t B, int64_t Hkv, int64_t G, int64_t D, int64_t ld_k, int64_t ld_vt, int64_t L,
+                            float scale, void* out, void* stream) {
+  using namespace drl;
+  DRL_CHECK_ARG(q && k_cache && vt_cache && key_valid && out, "NULL input");
+  DRL_CHECK_ARG(dt == DRL_BF16, "MFMA decode attention runs on bf16");
+  DRL_CHECK_ARG(D == 64 || D == 128, "head_dim must be 64 or 128");
+  DRL_CHECK_ARG(B >= 1 && Hkv >= 1 && G >= 1 && G <= 32 && L >= 1 && L <= ld_k && L <= ld_vt, "bad shape");
+  DRL_CHECK_ARG(ld_vt % 4 == 0 && ld_valid % 4 == 0 && (reinterpret_cast<uintptr_t>(key_valid) & 3u) == 0 &&
+                    ld_k < (int64_t(1) << 30),
+                "ld_vt / key_valid rows must be 4-element aligned");
+  DRL_CHECK_ARG(aligned16(q) && aligned16(k_cache) && (reinterpret_cast<uintptr_t>(vt_cache) & 7u) == 0 &&
+                    (reinterpret_cast<uintptr_t>(out) & 7u) == 0,
+                "misaligned operand");
+  DecodeArgs a{static_cast<const uint16_t*>(q), static_cast<const uint16_t*>(k_cache),
+               static_cast<const uint16_t*>(vt_cache), key_valid, ld_valid, qpos_ptr, qpos, Hkv, G, ld_k, ld_vt, L,
+               scale * 1.4426950408889634f, static_cast<uint16_t*>(out)};
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (D == 64) hipLaunchKernelGGL(decode_mfma_kernel<64>, dim3(B * Hkv), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(decode_mfma_kernel<128>, dim3(B * Hkv), dim3(256), 0, s, a);
   DRL_LAUNCH_CHECK();
   return DRL_OK;
 }

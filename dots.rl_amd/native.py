@@ -433,3 +433,16 @@ def flash_attn_bwd(q, qt, k, kt, v, o, dout, doutt, lse, key_valid, dq, dk, dv):
                                    _p(lse), _edt(q), _p(key_valid), key_valid.stride(0), B, Hkv, G, D, T,
                                    qt.stride(-2), 1.0 / math.sqrt(D), _p(delta), _p(dq), _p(dk), _p(dv), _stream()),
           "drl_flash_attn_bwd")
+
+
+def decode_attention_vt(q, k_cache, vt_cache, key_valid, L, out, qpos=None, qpos_dev=None):
+    """MFMA decode attention: q (B,Hkv,G,D) bf16, k_cache (B,Hkv,ld_k,D), vt_cache (B,Hkv,D,ld_vt)."""
+    _dev(q, k_cache, vt_cache, key_valid, out)
+    B, Hkv, G, D = q.shape
+    assert q.is_contiguous() and k_cache.is_contiguous() and out.is_contiguous() and vt_cache.stride(-1) == 1
+    assert vt_cache.stride(-2) * D == vt_cache.stride(1) and key_valid.dtype == torch.uint8
+    qp = L - 1 if qpos is None else int(qpos)
+    check(lib().drl_decode_attention_vt(_p(q), _p(k_cache), _p(vt_cache), _edt(q), _p(key_valid), key_valid.stride(0),
+                                        _p(qpos_dev), qp, B, Hkv, G, D, k_cache.shape[2], vt_cache.stride(-2), L,
+                                        1.0 / math.sqrt(D), _p(out), _stream()), "drl_decode_attention_vt")
+    return out

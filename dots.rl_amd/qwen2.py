@@ -265,25 +265,24 @@ def _layer_forward(m, i, x_prev, delta, pos, key_valid, save, cache=None, koff=0
         else:
             vbuf = torch.empty_like(kbuf)
         koff = 0
-    else:
+    else:  # bf16 caches keep V head-dim-major (cache.vt), the layout of the MFMA prefill / decode kernels
         kbuf, vbuf = cache.k[i], cache.v[i]
+        vt = cache.vt[i]
     native.rope_qkv_fwd(qkv, pos, m.cos, m.sin, Hq, Hkv, D, q, kbuf, vbuf, koff, koff_dev, vt=vt)
     L = koff + T
     if flash:
-        if vt is None:  # prefill: the cache keeps V row-major for decode; the kernel reads a transposed copy
-            vt = torch.empty(B, Hkv, D, (L + 7) // 8 * 8, dtype=dt, device=dev)
-            vt[..., :L].copy_(vbuf[:, :, :L].transpose(-1, -2))
         attn = torch.empty(B, T, Hq * D, dtype=dt, device=dev)
         native.flash_attn_fwd(q, kbuf, vt, key_valid, attn, Tk=L, qoff=L - T)
         P = None
     elif cache is not None and T == 1:
-        # one new token: fused GQA decode attention streams the cache once (csrc/attention.hip)
+        # one new token: decode attention streams the cache once (MFMA kernel over V^T for bf16 caches,
+        # csrc/flash_attn.hip; VALU kernel over row-major V for the fp32 parity model, csrc/attention.hip)
         attn = torch.empty(B, 1, Hq * D, dtype=dt, device=dev)
-        if koff_dev is None:
-            native.decode_attention(q.view(B, Hkv, G, D), kbuf, vbuf, key_valid, L, attn)
-        else:  # keys [0, koff_dev] of the whole cache; the kernel stops at the device position
-            native.decode_attention(q.view(B, Hkv, G, D), kbuf, vbuf, key_valid, kbuf.shape[2], attn,
-                                    qpos_dev=koff_dev)
+        Lk = L if koff_dev is None else kbuf.shape[2]  # device position: the kernel stops at koff_dev
+        if vt is not None:
+            native.decode_attention_vt(q.view(B, Hkv, G, D), kbuf, vt, key_valid, Lk, attn, qpos_dev=koff_dev)
+        else:
+            native.decode_attention(q.view(B, Hkv, G, D), kbuf, vbuf, key_valid, Lk, attn, qpos_dev=koff_dev)
         P = None
     else:
         k3 = kbuf[:, :, :L].reshape(B * Hkv, L, D)
@@ -423,12 +422,20 @@ def _key_valid(attention_mask):
 
 
 class KVCache:
-    """Per-layer K/V for decode: (B, Hkv, Tmax, D) in the compute dtype, plus the key-valid mask (u8)."""
+    """Per-layer K (B, Hkv, Tmax, D) and V (bf16: head-dim-major (B, Hkv, D, Tmax); fp32: row-major) in the
+    compute dtype, plus the key-valid mask (u8)."""
 
     def __init__(self, cfg: Qwen2Config, B, Tmax, device, dtype):
-        self.k = [torch.empty(B, cfg.num_key_value_heads, Tmax, cfg.head_dim, device=device, dtype=dtype)
-                  for _ in range(cfg.num_hidden_layers)]
-        self.v = [torch.empty_like(t) for t in self.k]
+        Hkv, D, L = cfg.num_key_value_heads, cfg.head_dim, cfg.num_hidden_layers
+        self.k = [torch.empty(B, Hkv, Tmax, D, device=device, dtype=dtype) for _ in range(L)]
+        if dtype == torch.bfloat16 and D in (64, 128):
+            # V head-dim-major (B, Hkv, D, Tmax padded to 8): read by the MFMA prefill and decode kernels
+            ld = (Tmax + 7) // 8 * 8
+            self.vt = [torch.zeros(B, Hkv, D, ld, device=device, dtype=dtype)[..., :Tmax] for _ in range(L)]
+            self.v = [None] * L
+        else:
+            self.vt = [None] * L
+            self.v = [torch.empty_like(t) for t in self.k]
         self.valid = torch.zeros(B, (Tmax + 3) // 4 * 4, dtype=torch.uint8, device=device)[:, :Tmax]
         self.len = 0
 

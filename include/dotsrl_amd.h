@@ -275,6 +275,14 @@ int drl_decode_attention(const void* q, const void* k_cache, const void* v_cache
 int drl_flash_attn_fwd(const void* q, const void* k, const void* vt, int32_t dt, const uint8_t* key_valid,
                        int64_t ld_valid, int64_t B, int64_t Hkv, int64_t G, int64_t D, int64_t Tq, int64_t Tk,
                        int64_t ld_k, int64_t ld_vt, int64_t qoff, float scale, void* out, float* lse, void* stream);
+/* Decode attention on MFMA over a cache with V head-dim-major: q (B,Hkv,G,D) bf16 (one token), k_cache
+ * (B,Hkv,ld_k,D), vt_cache (B,Hkv,D,ld_vt); keys j < L with key_valid[b, j] && j <= qpos (device scalar
+ * *qpos_ptr when non-NULL). out (B,Hkv,G,D). G <= 32, head_dim 64 or 128. Same semantics as
+ * drl_decode_attention (the VALU kernel over a row-major V cache used by the fp32 parity model). */
+int drl_decode_attention_vt(const void* q, const void* k_cache, const void* vt_cache, int32_t dt,
+                            const uint8_t* key_valid, int64_t ld_valid, const int64_t* qpos_ptr, int64_t qpos,
+                            int64_t B, int64_t Hkv, int64_t G, int64_t D, int64_t ld_k, int64_t ld_vt, int64_t L,
+                            float scale, void* out, void* stream);
 /* Backward of drl_flash_attn_fwd for Tq == Tk == T, qoff = 0 (the training forward), recomputing P from lse:
  * q (B,Hkv,G,T,D), k / v (B,Hkv,T,D) row-major, qt (B,Hkv,G,D,ld_t) and kt (B,Hkv,D,ld_t) head-dim-major
  * copies (drl_rope_qkv_fwd writes all of them), o and dout (B,T,Hkv*G*D), doutt = dout transposed

@@ -185,6 +185,20 @@ def test_decode_attention(dt, B, Hkv, G, D, Tk, L):
         qp = torch.tensor([L - 4], device=DEV)
         native.decode_attention(q, k, v, valid, L, out, qpos_dev=qp)
         torch.testing.assert_close(out.float(), _ref_decode(q, k, v, valid, L, L - 4), **_tol(dt))
+    if dt == torch.bfloat16 and D in (64, 128):
+        # MFMA kernel over the head-dim-major V cache (the bf16 rollout layout)
+        ldv = (Tk + 7) // 8 * 8
+        vt = torch.full((B, Hkv, D, ldv), float("nan"), device=DEV, dtype=dt)
+        vt[..., :Tk] = v.transpose(-1, -2)
+        ldk = (Tk + 3) // 4 * 4
+        valid4 = torch.zeros(B, ldk, dtype=torch.uint8, device=DEV)
+        valid4[:, :Tk] = valid
+        out2 = torch.empty_like(out)
+        native.decode_attention_vt(q, k, vt, valid4[:, :Tk], L, out2)
+        torch.testing.assert_close(out2.float(), ref, **_tol(dt))
+        if L > 4:
+            native.decode_attention_vt(q, k, vt, valid4[:, :Tk], L, out2, qpos_dev=qp)
+            torch.testing.assert_close(out2.float(), _ref_decode(q, k, v, valid, L, L - 4), **_tol(dt))
 
 
 def _ref_attn(q, k, v, valid, qoff):

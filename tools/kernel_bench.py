@@ -111,7 +111,11 @@ def decode_attn(B=512, Hkv=2, G=7, D=64, Tk=768, L=640):
     out = torch.empty_like(q)
     t = time_it(lambda: native.decode_attention(q, k, v, valid, L, out), iters=50)
     nbytes = B * Hkv * (2 * L * D * 2 + 2 * G * D * 2)
-    return [dict(kernel="A3_decode_attention", B=B, L=L, seconds=t, GBps=nbytes / t / 1e9, frac=nbytes / t / PEAK_HBM)]
+    vt = v.transpose(-1, -2).contiguous()
+    t2 = time_it(lambda: native.decode_attention_vt(q, k, vt, valid, L, out), iters=50)
+    return [dict(kernel="A3_decode_attention", B=B, L=L, seconds=t, GBps=nbytes / t / 1e9, frac=nbytes / t / PEAK_HBM),
+            dict(kernel="A3_decode_attention_vt_mfma", B=B, L=L, seconds=t2, GBps=nbytes / t2 / 1e9,
+                 frac=nbytes / t2 / PEAK_HBM)]
 
 
 def flash(B=16, Hkv=2, G=7, D=64, T=768):
