@@ -66,7 +66,8 @@ __global__ __launch_bounds__(256) void rope_qkv_fwd_kernel(RopeArgs<E> a) {
       p = p < 0 ? 0 : (p >= a.maxpos ? a.maxpos - 1 : p);
       const float c = a.cos_t[p * half + j], s = a.sin_t[p * half + j];
       // rotate_half: out1 = x1*cos - x2*sin ; out2 = x2*cos + x1*sin
-      const float o1 = x1 * c - x2 * s, o2 = x2 * c + x1 * s;
+      // explicit contraction: identical rounding in every kernel that rotates
+      const float o1 = fmaf(x1, c, -(x2 * s)), o2 = fmaf(x2, c, x1 * s);
       E* dst;
       E* dstt;  // transposed copy (nullptr: not requested)
       if (h < a.Hq) {
@@ -94,6 +95,87 @@ __global__ __launch_bounds__(256) void rope_qkv_fwd_kernel(RopeArgs<E> a) {
         dst[j] = src[j];
         dst[j + half] = src[j + half];
       }
+    }
+  }
+}
+
+// Tiled form for full sequences that also want head-dim-major copies: one workgroup per (64-position
+// tile, head, sequence) rotates the tile, writes the row-major output, and writes the transposed copy
+// through an LDS tile so each head-dim row gets 64 contiguous positions (coalesced) instead of one
+// 2-byte store per position. Same results as rope_qkv_fwd_kernel.
+constexpr int kRopeTile = 64;
+
+template <typename E>
+__global__ __launch_bounds__(256) void rope_qkv_fwd_tiled_kernel(RopeArgs<E> a) {
+  __shared__ __attribute__((aligned(16))) E tile[128][kRopeTile + 8];
+  const int half = static_cast<int>(a.D / 2);
+  const int64_t Hall = a.Hq + 2 * a.Hkv;
+  const int64_t G = a.Hq / a.Hkv;
+  const int64_t h = blockIdx.y, b = blockIdx.z;
+  const int64_t t0 = static_cast<int64_t>(blockIdx.x) * kRopeTile;
+  const int64_t koff = a.koff_dev ? *a.koff_dev : a.koff;
+  if (koff < 0 || koff + a.T > a.Tk) return;
+  const bool is_q = h < a.Hq, is_k = !is_q && h < a.Hq + a.Hkv;
+  E* rowdst;   // row-major destination base of this (b, head), indexed [pos][D]
+  E* tdst;     // head-dim-major destination base, indexed [d * ld_t + pos]
+  int64_t pos0;  // position offset of t = 0 in the destinations
+  if (is_q) {
+    const int64_t g = h / G, hi = h % G;
+    rowdst = a.q + ((b * a.Hkv + g) * G + hi) * a.T * a.D;
+    tdst = a.qt ? a.qt + ((b * a.Hkv + g) * G + hi) * a.D * a.ld_t : nullptr;
+    pos0 = 0;
+  } else if (is_k) {
+    rowdst = a.k + (b * a.Hkv + (h - a.Hq)) * a.Tk * a.D;
+    tdst = a.kt ? a.kt + (b * a.Hkv + (h - a.Hq)) * a.D * a.ld_t : nullptr;
+    pos0 = koff;
+  } else {
+    rowdst = a.v ? a.v + (b * a.Hkv + (h - a.Hq - a.Hkv)) * a.Tk * a.D : nullptr;
+    tdst = a.vt ? a.vt + (b * a.Hkv + (h - a.Hq - a.Hkv)) * a.D * a.ld_t : nullptr;
+    pos0 = koff;
+  }
+  const int rows_per_pass = 256 / half;
+  for (int p = threadIdx.x / half; p < kRopeTile; p += rows_per_pass) {
+    const int j = threadIdx.x % half;
+    const int64_t t = t0 + p;
+    if (t >= a.T) break;
+    const E* src = a.qkv + ((b * a.T + t) * Hall + h) * a.D;
+    float o1 = ldf(src, j), o2 = ldf(src, j + half);
+    if (is_q || is_k) {
+      int64_t ps = a.pos[b * a.T + t];
+      ps = ps < 0 ? 0 : (ps >= a.maxpos ? a.maxpos - 1 : ps);
+      const float c = a.cos_t[ps * half + j], s = a.sin_t[ps * half + j];
+      const float x1 = o1, x2 = o2;
+      o1 = fmaf(x1, c, -(x2 * s));
+      o2 = fmaf(x2, c, x1 * s);
+    }
+    if (rowdst) {
+      stf(rowdst + (pos0 + t) * a.D, j, o1);
+      stf(rowdst + (pos0 + t) * a.D, j + half, o2);
+    }
+    if (tdst) {
+      E e1, e2;
+      stf(&e1, 0, o1);
+      stf(&e2, 0, o2);
+      tile[j][p] = e1;
+      tile[j + half][p] = e2;
+    }
+  }
+  if (tdst == nullptr) return;
+  __syncthreads();
+  // transposed rows: D rows x 64 positions, 16 positions (one or two 16-B pieces) per thread
+  constexpr int kPer = 16;
+  const int nvalid = static_cast<int>(min<int64_t>(kRopeTile, a.T - t0));
+  for (int it = threadIdx.x; it < a.D * (kRopeTile / kPer); it += 256) {
+    const int d = it / (kRopeTile / kPer), c = it % (kRopeTile / kPer);
+    E* dst = tdst + d * a.ld_t + pos0 + t0 + c * kPer;
+    const bool aligned = ((reinterpret_cast<uintptr_t>(dst) & 15u) == 0) && sizeof(E) == 2;
+    if (aligned && c * kPer + kPer <= nvalid) {
+      const uint4* srcv = reinterpret_cast<const uint4*>(&tile[d][c * kPer]);
+      uint4* dv = reinterpret_cast<uint4*>(dst);
+      dv[0] = srcv[0];
+      dv[1] = srcv[1];
+    } else {
+      for (int e = 0; e < kPer && c * kPer + e < nvalid; ++e) dst[e] = tile[d][c * kPer + e];
     }
   }
 }
@@ -494,7 +576,14 @@ int drl_rope_qkv_fwd(const void* qkv, int32_t dt, const int64_t* position_ids, c
     RopeArgs<E> a{static_cast<const E*>(qkv), position_ids, cos_t, sin_t, static_cast<E*>(q), static_cast<E*>(k),
                   static_cast<E*>(v), B, T, Hq, Hkv, D, Tk, koff, maxpos, koff_dev, static_cast<E*>(qt),
                   static_cast<E*>(kt), static_cast<E*>(vt), ld_t};
-    hipLaunchKernelGGL(rope_qkv_fwd_kernel<E>, dim3(grid_stride(n)), dim3(256), 0, static_cast<hipStream_t>(stream), a);
+    if ((qt || kt || vt) && T >= 16 && D <= 128 && D % 2 == 0 && 256 % (D / 2) == 0) {
+      const dim3 grid(static_cast<unsigned>((T + kRopeTile - 1) / kRopeTile), static_cast<unsigned>(Hq + 2 * Hkv),
+                      static_cast<unsigned>(B));
+      hipLaunchKernelGGL(rope_qkv_fwd_tiled_kernel<E>, grid, dim3(256), 0, static_cast<hipStream_t>(stream), a);
+    } else {
+      hipLaunchKernelGGL(rope_qkv_fwd_kernel<E>, dim3(grid_stride(n)), dim3(256), 0, static_cast<hipStream_t>(stream),
+                         a);
+    }
   });
   DRL_LAUNCH_CHECK();
   return DRL_OK;

@@ -68,7 +68,7 @@ def param_specs(cfg: Qwen2Config):
         specs += [
             (p + "input_layernorm", (H,), "small"),
             (p + "qkv_proj.weight", (qkv, H), "gemm"),
-            (p + "qkv_proj.bias", (qkv,), "small"),
+            (p + "qkv_proj.bias", (qkv,), "gemm"),  # GEMM epilogue operand: read in the compute dtype
             (p + "o_proj", (H, cfg.num_attention_heads * hd), "gemm"),
             (p + "post_attention_layernorm", (H,), "small"),
             (p + "gate_up_proj", (2 * I, H), "gemm"),
@@ -169,8 +169,8 @@ def acc_wgrad(gw, dy, x):
     """gw (out, in) fp32 += dy^T x  with dy (N, out), x (N, in) in the compute dtype (hipBLASLt, fp32 out)."""
     if dy.dtype == torch.float32:
         gw.addmm_(dy.t(), x)
-    else:
-        gw.copy_(torch.addmm(gw, dy.t(), x, out_dtype=torch.float32))
+    else:  # accumulate in place (C = D, beta = 1): no temporary, no copy of the fp32 gradient
+        torch.addmm(gw, dy.t(), x, out_dtype=torch.float32, out=gw)
 
 
 def bmm_f32(a, b):
@@ -232,7 +232,7 @@ def _layer_forward(m, i, x_prev, delta, pos, key_valid, save, cache=None, koff=0
     rstd1 = torch.empty(B * T, dtype=torch.float32, device=dev) if save is not None else None
     native.add_rmsnorm_fwd(x_prev, delta, x if delta is not None else None, s.w(p + "input_layernorm"), h1, rstd1,
                            cfg.rms_norm_eps)
-    qkv = torch.addmm(s.w(p + "qkv_proj.bias").to(dt), h1.view(B * T, H), s.w(p + "qkv_proj.weight").t())
+    qkv = torch.addmm(s.w(p + "qkv_proj.bias"), h1.view(B * T, H), s.w(p + "qkv_proj.weight").t())
     qkv = qkv.view(B, T, -1)
     q = torch.empty(B, Hkv, G, T, D, dtype=dt, device=dev)
     # bf16 full-sequence passes run the fused MFMA attention (csrc/flash_attn.hip): log-probs and prefill

@@ -242,19 +242,32 @@ def test_flash_attn_forward(B, Hkv, G, D, Tq, Tk, qoff):
     torch.testing.assert_close(lse[fin], ref_lse[fin], rtol=1e-4, atol=1e-4)
 
 
-def test_rope_writes_transposed_v():
-    B, T, Hq, Hkv, D = 2, 45, 14, 2, 64
-    g = torch.Generator(device=DEV).manual_seed(3)
+@pytest.mark.parametrize("T,D", [(45, 64), (130, 64), (8, 64), (77, 128)])
+def test_rope_writes_head_dim_major_copies(T, D):
+    """The tiled kernel (head-dim-major copies through LDS) matches the per-element kernel bit for bit."""
+    B, Hq, Hkv = 2, 14, 2
+    G = Hq // Hkv
+    g = torch.Generator(device=DEV).manual_seed(T)
     qkv = torch.randn(B, T, (Hq + 2 * Hkv) * D, device=DEV, generator=g).to(torch.bfloat16)
-    pos = torch.arange(T, device=DEV)[None].expand(B, T).contiguous()
+    pos = torch.randint(0, 4000, (B, T), device=DEV, generator=g)
     cos, sin = _rope_tables(D)
-    q = torch.empty(B, Hkv, Hq // Hkv, T, D, device=DEV, dtype=torch.bfloat16)
+    q = torch.empty(B, Hkv, G, T, D, device=DEV, dtype=torch.bfloat16)
     k = torch.empty(B, Hkv, T, D, device=DEV, dtype=torch.bfloat16)
     v = torch.empty_like(k)
-    vt = torch.zeros(B, Hkv, D, 48, device=DEV, dtype=torch.bfloat16)
     native.rope_qkv_fwd(qkv, pos, cos, sin, Hq, Hkv, D, q, k, v)
-    native.rope_qkv_fwd(qkv, pos, cos, sin, Hq, Hkv, D, q, k, None, vt=vt)
+    ld = (T + 7) // 8 * 8
+    q2, k2, v2 = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+    qt = torch.zeros(B, Hkv, G, D, ld, device=DEV, dtype=torch.bfloat16)
+    kt = torch.zeros(B, Hkv, D, ld, device=DEV, dtype=torch.bfloat16)
+    vt = torch.zeros_like(kt)
+    native.rope_qkv_fwd(qkv, pos, cos, sin, Hq, Hkv, D, q2, k2, v2, qt=qt, kt=kt, vt=vt)
+    assert torch.equal(q2, q) and torch.equal(k2, k) and torch.equal(v2, v)
+    assert torch.equal(qt[..., :T], q.transpose(-1, -2))
+    assert torch.equal(kt[..., :T], k.transpose(-1, -2))
     assert torch.equal(vt[..., :T], v.transpose(-1, -2))
+    vt2 = torch.zeros_like(vt)  # V only transposed (v = None)
+    native.rope_qkv_fwd(qkv, pos, cos, sin, Hq, Hkv, D, q2, k2, None, vt=vt2)
+    assert torch.equal(vt2, vt)
 
 
 def _ref_attn_autograd(q, k, v, valid, dout):
