@@ -113,8 +113,8 @@ SIGNATURES = {
                                           P]),
     "drl_decode_attention_vt": (ctypes.c_int, [P, P, P, I32, P, I64, P, I64, I64, I64, I64, I64, I64, I64, I64, F32,
                                                P, P]),
-    "drl_flash_attn_bwd": (ctypes.c_int, [P, P, P, P, P, P, P, P, I64, P, I32, P, I64, I64, I64, I64, I64, I64, I64, F32,
-                                          P, P, P, P, P]),
+    "drl_flash_attn_bwd": (ctypes.c_int, [P, P, P, P, P, P, P, I32, P, I64, I64, I64, I64, I64, I64, I64, F32, P, P, P, P,
+                                          P]),
     "drl_decode_attention": (ctypes.c_int, [P, P, P, I32, P, I64, P, I64, I64, I64, I64, I64, I64, I64, F32, P, P, SZ,
                                             P]),
 }

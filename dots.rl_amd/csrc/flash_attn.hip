@@ -40,6 +40,25 @@ struct FlashArgs {
 
 __device__ __forceinline__ bf16x8 as_bf16x8(u16x8 v) { return __builtin_bit_cast(bf16x8, v); }
 
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+// ds_read_b64_tr_b16 (cdna_hip_programming.md §5.5 T10): per 16-lane group, lane 4q+p addresses row q,
+// columns 4p..4p+3 of a 4 x 16 block; lane i receives column i of the 4 rows (row q in element q).
+__device__ __forceinline__ u16x4 lds_tr16(const uint16_t* p) {
+  const s16x4 r = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p));
+  return __builtin_bit_cast(u16x4, r);
+}
+
+// A operand "X^T" (rows = head dim, k = positions in the accumulator order) of a 32-position x D tile X held
+// row-major in LDS ([position][d], row stride rs elements): k-step s, head-dim tile mt. Two transposing reads:
+// element j of lane half h is position 16s + 8(j>>2) + 4h + (j&3), head-dim 32mt + (lane & 31).
+__device__ __forceinline__ u16x8 lds_xt_operand(const uint16_t* x, int rs, int mt, int s, int lane) {
+  const int i = lane & 15, q = i >> 2, p = i & 3, h = lane >> 5;
+  const int col = 32 * mt + (lane & 16) + 4 * p;
+  const u16x4 lo = lds_tr16(x + (16 * s + 4 * h + q) * rs + col);
+  const u16x4 hi = lds_tr16(x + (16 * s + 8 + 4 * h + q) * rs + col);
+  return u16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
 // round-to-nearest-even f32 -> bf16 (one v_cvt_pk_bf16_f32; NaN stays NaN)
 __device__ __forceinline__ uint16_t to_bf16_bits(float f) { return __builtin_bit_cast(uint16_t, static_cast<__bf16>(f)); }
 
@@ -256,21 +275,21 @@ __global__ __launch_bounds__(512) void flash_fwd_kernel(FlashArgs a) {
 // ------------------------------------------------------------------------------------------ backward
 // FA2-style backward in two launches, recomputing P from the forward's LSE (nothing of size T x T is
 // stored): (1) dq_kernel, query-tile centric in the forward's S^T orientation (lane = query): dP^T =
-// V dO^T, dS^T = P^T (dP^T - delta), dQ^T += K^T dS^T (K^T from the head-dim-major kt copy); it also
-// writes delta = rowsum(dO * O). (2) dkdv_kernel, key-tile centric in the S orientation (lane = key):
-// S = Q K^T, dP = dO V^T, then dV^T += dO^T P and dK^T += Q^T dS take P / dS straight from the
-// accumulators (dO^T from the transposed o_proj-gradient GEMM, Q^T from qt); the G query heads of a
-// KV group are the G waves of the workgroup and their dK / dV partials are summed in LDS in a fixed
-// order (deterministic). Reference: autograd of the eager attention under dp_actor.py:90-280.
+// V dO^T, dS^T = P^T (dP^T - delta), dQ^T += K^T dS^T (K, V and the head-dim-major K^T copy staged in
+// LDS, shared by the G query heads of the workgroup); it also writes delta = rowsum(dO * O).
+// (2) dkdv_kernel, key-tile centric in the S orientation (lane = key): S = Q K^T, dP = dO V^T, then
+// dV^T += dO^T P and dK^T += Q^T dS take P / dS straight from the accumulators, and their transposed A
+// operands come from each wave's LDS image of the Q / dO tile through ds_read_b64_tr_b16 (no transposed
+// copies in HBM). The G query heads of a KV group are the G waves of the workgroup; their dK / dV
+// partials are summed in LDS in a fixed order (deterministic). Reference: autograd of the eager attention
+// under dp_actor.py:90-280.
 struct FlashBwdArgs {
   const uint16_t* q;      // (B, Hkv, G, T, D)
-  const uint16_t* qt;     // (B, Hkv, G, D, ld_t)
   const uint16_t* k;      // (B, Hkv, T, D)
   const uint16_t* kt;     // (B, Hkv, D, ld_t)
   const uint16_t* v;      // (B, Hkv, T, D)
   const uint16_t* o;      // (B, T, Hkv, G, D)
   const uint16_t* dout;   // (B, T, Hkv, G, D)
-  const uint16_t* doutt;  // (Hkv * G * D, ld_n), column b * T + t
   const float* lse;       // (B, Hkv, G, T)
   const uint8_t* valid;
   int64_t ld_valid;
@@ -278,7 +297,7 @@ struct FlashBwdArgs {
   uint16_t* dq;  // (B, Hkv, G, T, D)
   uint16_t* dk;  // (B, Hkv, T, D)
   uint16_t* dv;  // (B, Hkv, T, D)
-  int64_t Hkv, G, T, ld_t, ld_n;
+  int64_t Hkv, G, T, ld_t;
   float scale, scale_log2;
 };
 
@@ -481,72 +500,100 @@ __global__ __launch_bounds__(512) void flash_dq_kernel(FlashBwdArgs a) {
 }
 
 template <int D>
+__device__ __forceinline__ void dkdv_rows(const uint16_t* qbase, const uint16_t* dout, int64_t b, int64_t hkv,
+                                          int64_t Hkv, int64_t G, int g, int T, int tr, int h, u16x8 (&qa)[D / 16],
+                                          u16x8 (&da)[D / 16]) {
+  const bool rin = tr < T;
+  const uint16_t* qrow = qbase + static_cast<int64_t>(rin ? tr : 0) * D + 8 * h;
+  const uint16_t* dorow = dout + (((b * T + (rin ? tr : 0)) * Hkv + hkv) * G + g) * D + 8 * h;
+#pragma unroll
+  for (int s = 0; s < D / 16; ++s) {
+    qa[s] = *reinterpret_cast<const u16x8*>(qrow + 16 * s);
+    da[s] = *reinterpret_cast<const u16x8*>(dorow + 16 * s);
+    if (!rin) qa[s] = da[s] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  }
+}
+
+template <int D>
 __global__ __launch_bounds__(512) void flash_dkdv_kernel(FlashBwdArgs a) {
-  constexpr int KS = D / 16, MT = D / 32;
+  constexpr int KS = D / 16, MT = D / 32, KROW = D + 8;
+  // per-wave image of the current query tile's Q and dO rows, row stride 1.5 D elements: the 4 rows of a
+  // transposing read land in disjoint bank ranges
+  constexpr int XROW = D + D / 2;
   __shared__ float red[2][MT][16][64];  // [dk/dv][tile][register][lane]: conflict-free per register
-  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+  __shared__ __attribute__((aligned(16))) uint16_t kv_lds[2][32 * KROW];  // this key tile's K and V rows
+  __shared__ __attribute__((aligned(16))) uint16_t xw[8][2][32 * XROW];    // [wave][Q / dO][position][d]
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, g = tid >> 6;
   const int li = lane & 31, h = lane >> 5;
   const int64_t bh = blockIdx.y, b = bh / a.Hkv, hkv = bh % a.Hkv;
-  const int64_t ntiles = (a.T + 31) / 32;
-  const int64_t k0 = (ntiles - 1 - static_cast<int64_t>(blockIdx.x)) * 32;  // short causal columns last
-  const int64_t key = k0 + li;
-  const bool kin = key < a.T;
+  const int T = static_cast<int>(a.T);
+  const int ntiles = (T + 31) / 32;
+  const int k0 = static_cast<int>(blockIdx.x) * 32;  // key tile 0 has the most query tiles: dispatched first
+  (void)ntiles;
+  const int key = k0 + li;
+  const bool kin = key < T;
   const bool kval = kin && a.valid[b * a.ld_valid + key] != 0;
   const int64_t head = bh * a.G + g;
-  bf16x8 kf[KS], vf[KS];
-  {
-    const uint16_t* krow = a.k + (bh * a.T + (kin ? key : 0)) * D + 8 * h;
-    const uint16_t* vr = a.v + (bh * a.T + (kin ? key : 0)) * D + 8 * h;
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      u16x8 kv = *reinterpret_cast<const u16x8*>(krow + 16 * s);
-      u16x8 vv = *reinterpret_cast<const u16x8*>(vr + 16 * s);
-      if (!kin) kv = vv = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-      kf[s] = as_bf16x8(kv);
-      vf[s] = as_bf16x8(vv);
-    }
+  // stage the key tile's K and V rows once; every wave (query head) reads them from LDS
+  for (int c = tid; c < 2 * 32 * (D / 8); c += blockDim.x) {
+    const int which = c / (32 * (D / 8)), cc = c % (32 * (D / 8)), row = cc / (D / 8), col = cc % (D / 8);
+    const int kk = k0 + row;
+    u16x8 v = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    if (kk < T) v = *reinterpret_cast<const u16x8*>((which ? a.v : a.k) + (bh * a.T + kk) * D + col * 8);
+    *reinterpret_cast<u16x8*>(&kv_lds[which][row * KROW + col * 8]) = v;
   }
+  __syncthreads();
+  const uint16_t* kl = kv_lds[0] + li * KROW + 8 * h;
+  const uint16_t* vl = kv_lds[1] + li * KROW + 8 * h;
   f32x16 dkt[MT], dvt[MT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) dkt[mt] = dvt[mt] = f32x16{};
   const uint16_t* qbase = a.q + head * a.T * D;
-  const uint16_t* qtbase = a.qt + head * D * a.ld_t;
   const float* lser = a.lse + head * a.T;
   const float* dlr = a.delta + head * a.T;
-  const int64_t colb = b * a.T;  // this sequence's first column of doutt
-  for (int64_t t0 = k0; t0 < a.T; t0 += 32) {
-    // S = Q K^T and dP = dO V^T: A = rows of query t0 + li; C row r -> query t0 + (r&3) + 8(r>>2) + 4h
-    f32x16 sc = f32x16{}, dp = f32x16{};
-    {
-      const int64_t tr = t0 + li;
-      const bool rin = tr < a.T;
-      const uint16_t* qrow = qbase + (rin ? tr : 0) * D + 8 * h;
-      const uint16_t* dorow = a.dout + (((b * a.T + (rin ? tr : 0)) * a.Hkv + hkv) * a.G + g) * D + 8 * h;
+  u16x8 qa[KS], da[KS];
+  dkdv_rows<D>(qbase, a.dout, b, hkv, a.Hkv, a.G, g, T, k0 + li, h, qa, da);
+  uint16_t* xq = xw[g][0];
+  uint16_t* xd = xw[g][1];
+  for (int t0 = k0; t0 < T; t0 += 32) {
+    // this tile's Q and dO rows into the wave's LDS image (row li, head dims 16s + 8h .. + 7); the transposed
+    // operands of dV / dK are read back from it after the softmax (no head-dim-major copies in HBM)
 #pragma unroll
-      for (int s = 0; s < KS; ++s) {
-        u16x8 qv = *reinterpret_cast<const u16x8*>(qrow + 16 * s);
-        u16x8 dv = *reinterpret_cast<const u16x8*>(dorow + 16 * s);
-        if (!rin) qv = dv = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-        sc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(qv), kf[s], sc, 0, 0, 0);
-        dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(dv), vf[s], dp, 0, 0, 0);
-      }
+    for (int s = 0; s < KS; ++s) {
+      *reinterpret_cast<u16x8*>(xq + li * XROW + 16 * s + 8 * h) = qa[s];
+      *reinterpret_cast<u16x8*>(xd + li * XROW + 16 * s + 8 * h) = da[s];
     }
-    u16x8 pb[2], dsb[2];
-    // block entirely at or below the diagonal, all keys valid, all queries in range: no mask
-    const bool full = __all(kval) && t0 >= k0 + 31 && t0 + 32 <= a.T;
+    float4 l4[4], d4[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      const int64_t qb = t0 + 8 * c + 4 * h;
-      float4 l4, d4;
-      if (qb + 3 < a.T) {
-        l4 = *reinterpret_cast<const float4*>(lser + qb);
-        d4 = *reinterpret_cast<const float4*>(dlr + qb);
+      const int qb = t0 + 8 * c + 4 * h;
+      if (qb + 3 < T) {
+        l4[c] = *reinterpret_cast<const float4*>(lser + qb);
+        d4[c] = *reinterpret_cast<const float4*>(dlr + qb);
       } else {
-        l4 = make_float4(qb < a.T ? lser[qb] : -INFINITY, qb + 1 < a.T ? lser[qb + 1] : -INFINITY,
-                         qb + 2 < a.T ? lser[qb + 2] : -INFINITY, -INFINITY);
-        d4 = make_float4(qb < a.T ? dlr[qb] : 0.f, qb + 1 < a.T ? dlr[qb + 1] : 0.f, qb + 2 < a.T ? dlr[qb + 2] : 0.f, 0.f);
+        l4[c] = make_float4(qb < T ? lser[qb] : -INFINITY, qb + 1 < T ? lser[qb + 1] : -INFINITY,
+                            qb + 2 < T ? lser[qb + 2] : -INFINITY, -INFINITY);
+        d4[c] = make_float4(qb < T ? dlr[qb] : 0.f, qb + 1 < T ? dlr[qb + 1] : 0.f, qb + 2 < T ? dlr[qb + 2] : 0.f, 0.f);
       }
-      const float lv[4] = {l4.x, l4.y, l4.z, l4.w}, dv4[4] = {d4.x, d4.y, d4.z, d4.w};
+    }
+    // S = Q K^T and dP = dO V^T: A = rows of query t0 + li; C row r -> query t0 + (r&3) + 8(r>>2) + 4h
+    f32x16 sc = f32x16{}, dp = f32x16{};
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const u16x8 kv = *reinterpret_cast<const u16x8*>(kl + 16 * s);
+      const u16x8 vv = *reinterpret_cast<const u16x8*>(vl + 16 * s);
+      sc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(qa[s]), as_bf16x8(kv), sc, 0, 0, 0);
+      dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(da[s]), as_bf16x8(vv), dp, 0, 0, 0);
+    }
+    if (t0 + 32 < T) dkdv_rows<D>(qbase, a.dout, b, hkv, a.Hkv, a.G, g, T, t0 + 32 + li, h, qa, da);  // next tile
+    u16x8 pb[2], dsb[2];
+    // block entirely at or below the diagonal, all keys valid, all queries in range: no mask
+    const bool full = __all(kval) && t0 >= k0 + 31 && t0 + 32 <= T;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int qb = t0 + 8 * c + 4 * h;
+      const float lv[4] = {l4[c].x, l4[c].y, l4[c].z, l4[c].w}, dv4[4] = {d4[c].x, d4[c].y, d4[c].z, d4[c].w};
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int r = 4 * c + j;
@@ -557,19 +604,15 @@ __global__ __launch_bounds__(512) void flash_dkdv_kernel(FlashBwdArgs a) {
         dsb[r >> 3][r & 7] = to_bf16_bits(p * (dp[r] - dv4[j]));
       }
     }
-    // dV^T += dO^T P and dK^T += Q^T dS (A operands: head-dim-major rows, positions permuted per k-step)
+    // dV^T += dO^T P and dK^T += Q^T dS: A operands read transposed from the wave's Q / dO image
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
-      const int64_t d = 32 * mt + li;
-      const uint16_t* dotrow = a.doutt + ((hkv * a.G + g) * D + d) * a.ld_n + colb;
-      const uint16_t* qtrow = qtbase + d * a.ld_t;
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        const int64_t pa = t0 + 16 * s + 4 * h;
-        const u16x8 dov = load_perm8(dotrow, pa, a.T);
-        const u16x8 qv = load_perm8(qtrow, pa, a.T);
+        const u16x8 dov = lds_xt_operand(xd, XROW, mt, s, lane);
+        const u16x8 qtv = lds_xt_operand(xq, XROW, mt, s, lane);
         dvt[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(dov), as_bf16x8(pb[s]), dvt[mt], 0, 0, 0);
-        dkt[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(qv), as_bf16x8(dsb[s]), dkt[mt], 0, 0, 0);
+        dkt[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(qtv), as_bf16x8(dsb[s]), dkt[mt], 0, 0, 0);
       }
     }
   }
@@ -605,7 +648,6 @@ __global__ __launch_bounds__(512) void flash_dkdv_kernel(FlashBwdArgs a) {
     }
   }
 }
-
 
 // ------------------------------------------------------------------------------------------ decode
 // One new token per sequence against the KV cache, on MFMA: the G query heads of a KV head are the
@@ -798,36 +840,28 @@ int drl_flash_attn_fwd(const void* q, const void* k, const void* vt, int32_t dt,
   return DRL_OK;
 }
 
-int drl_flash_attn_bwd(const void* q, const void* qt, const void* k, const void* kt, const void* v, const void* o,
-                       const void* dout, const void* doutt, int64_t ld_n, const float* lse, int32_t dt,
-                       const uint8_t* key_valid, int64_t ld_valid, int64_t B, int64_t Hkv, int64_t G, int64_t D,
-                       int64_t T, int64_t ld_t, float scale, float* delta, void* dq, void* dk, void* dv,
-                       void* stream) {
+int drl_flash_attn_bwd(const void* q, const void* k, const void* kt, const void* v, const void* o, const void* dout,
+                       const float* lse, int32_t dt, const uint8_t* key_valid, int64_t ld_valid, int64_t B,
+                       int64_t Hkv, int64_t G, int64_t D, int64_t T, int64_t ld_t, float scale, float* delta, void* dq,
+                       void* dk, void* dv, void* stream) {
   using namespace drl;
-  DRL_CHECK_ARG(q && qt && k && kt && v && o && dout && doutt && lse && key_valid && delta && dq && dk && dv,
+  DRL_CHECK_ARG(q && k && kt && v && o && dout && lse && key_valid && delta && dq && dk && dv,
                 "NULL input");
   DRL_CHECK_ARG(dt == DRL_BF16, "flash attention runs on bf16 operands");
-  DRL_CHECK_ARG(D == 64 || D == 128, "head_dim must be 64 or 128");
+  DRL_CHECK_ARG(D == 64, "the fused backward is built for head_dim 64 (LDS budget of the per-wave Q / dO images)");
   DRL_CHECK_ARG(B >= 1 && Hkv >= 1 && G >= 1 && G <= 8 && T >= 1, "bad shape");
-  DRL_CHECK_ARG(T % 4 == 0 && ld_t >= T && ld_t % 4 == 0 && ld_n >= B * T && ld_n % 4 == 0,
-                "T, ld_t and ld_n must be multiples of 4 (8-byte position runs)");
+  DRL_CHECK_ARG(T % 8 == 0 && ld_t >= T && ld_t % 8 == 0, "T and ld_t must be multiples of 8");
   DRL_CHECK_ARG(ld_valid >= T, "ld_valid < T");
-  FlashBwdArgs a{static_cast<const uint16_t*>(q), static_cast<const uint16_t*>(qt), static_cast<const uint16_t*>(k),
-                 static_cast<const uint16_t*>(kt), static_cast<const uint16_t*>(v), static_cast<const uint16_t*>(o),
-                 static_cast<const uint16_t*>(dout), static_cast<const uint16_t*>(doutt), lse, key_valid, ld_valid,
-                 delta, static_cast<uint16_t*>(dq), static_cast<uint16_t*>(dk), static_cast<uint16_t*>(dv), Hkv, G, T,
-                 ld_t, ld_n, scale, scale * 1.4426950408889634f};
+  FlashBwdArgs a{static_cast<const uint16_t*>(q), static_cast<const uint16_t*>(k), static_cast<const uint16_t*>(kt),
+                 static_cast<const uint16_t*>(v), static_cast<const uint16_t*>(o), static_cast<const uint16_t*>(dout),
+                 lse, key_valid, ld_valid, delta, static_cast<uint16_t*>(dq), static_cast<uint16_t*>(dk),
+                 static_cast<uint16_t*>(dv), Hkv, G, T, ld_t, scale, scale * 1.4426950408889634f};
   const dim3 grid(static_cast<unsigned>((T + 31) / 32), static_cast<unsigned>(B * Hkv));
   const dim3 block_dq(512);  // waves >= G only stage K / V / K^T
   const dim3 block_kv(static_cast<unsigned>(64 * G));
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (D == 64) {
-    hipLaunchKernelGGL(flash_dq_kernel<64>, grid, block_dq, 0, s, a);
-    hipLaunchKernelGGL(flash_dkdv_kernel<64>, grid, block_kv, 0, s, a);
-  } else {
-    hipLaunchKernelGGL(flash_dq_kernel<128>, grid, block_dq, 0, s, a);
-    hipLaunchKernelGGL(flash_dkdv_kernel<128>, grid, block_kv, 0, s, a);
-  }
+  hipLaunchKernelGGL(flash_dq_kernel<64>, grid, block_dq, 0, s, a);
+  hipLaunchKernelGGL(flash_dkdv_kernel<64>, grid, block_kv, 0, s, a);
   DRL_LAUNCH_CHECK();
   return DRL_OK;
 }

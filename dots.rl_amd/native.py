@@ -419,19 +419,18 @@ def flash_attn_fwd(q, k, vt, key_valid, out, Tk=None, qoff=0, lse=None):
     return out
 
 
-def flash_attn_bwd(q, qt, k, kt, v, o, dout, doutt, lse, key_valid, dq, dk, dv):
-    """Backward of flash_attn_fwd (Tq == Tk, qoff 0): q (B,Hkv,G,T,D), qt (B,Hkv,G,D,ld), k/v (B,Hkv,T,D),
-    kt (B,Hkv,D,ld), o/dout (B,T,Hq*D), doutt (Hq*D, >=B*T) = dout transposed, lse (B,Hkv,G,T) ->
-    dq (B,Hkv,G,T,D), dk/dv (B,Hkv,T,D)."""
-    _dev(q, qt, k, kt, v, o, dout, doutt, lse, key_valid, dq, dk, dv)
+def flash_attn_bwd(q, k, kt, v, o, dout, lse, key_valid, dq, dk, dv):
+    """Backward of flash_attn_fwd (Tq == Tk, qoff 0): q (B,Hkv,G,T,D), k/v (B,Hkv,T,D), kt (B,Hkv,D,ld),
+    o/dout (B,T,Hq*D), lse (B,Hkv,G,T) -> dq (B,Hkv,G,T,D), dk/dv (B,Hkv,T,D)."""
+    _dev(q, k, kt, v, o, dout, lse, key_valid, dq, dk, dv)
     B, Hkv, G, T, D = q.shape
-    assert qt.stride(-2) == kt.stride(-2) and doutt.stride(1) == 1 and qt.stride(-1) == 1 and kt.stride(-1) == 1
+    assert kt.stride(-1) == 1 and kt.stride(-2) * D == kt.stride(1)
     for t in (q, k, v, o, dout, lse, dq, dk, dv):
         assert t.is_contiguous()
     delta = _ws.get(B * Hkv * G * T * 4, q.device)
-    check(lib().drl_flash_attn_bwd(_p(q), _p(qt), _p(k), _p(kt), _p(v), _p(o), _p(dout), _p(doutt), doutt.stride(0),
-                                   _p(lse), _edt(q), _p(key_valid), key_valid.stride(0), B, Hkv, G, D, T,
-                                   qt.stride(-2), 1.0 / math.sqrt(D), _p(delta), _p(dq), _p(dk), _p(dv), _stream()),
+    check(lib().drl_flash_attn_bwd(_p(q), _p(k), _p(kt), _p(v), _p(o), _p(dout), _p(lse), _edt(q), _p(key_valid),
+                                   key_valid.stride(0), B, Hkv, G, D, T, kt.stride(-2), 1.0 / math.sqrt(D), _p(delta),
+                                   _p(dq), _p(dk), _p(dv), _stream()),
           "drl_flash_attn_bwd")
 
 

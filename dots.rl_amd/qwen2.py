@@ -240,20 +240,19 @@ def _layer_forward(m, i, x_prev, delta, pos, key_valid, save, cache=None, koff=0
     # GEMM + masked softmax + PV GEMM, probabilities kept for the backward) serves the fp32 parity model
     flash_ok = T > 1 and dt == torch.bfloat16 and D in (64, 128) and G <= 8 and key_valid.stride(0) % 4 == 0
     flash = save is None and flash_ok
-    if save is not None and flash_ok and cache is None and T % 8 == 0:
+    if save is not None and flash_ok and cache is None and T % 8 == 0 and D == 64:
         # training forward: fused attention that saves only the LSE; the backward (flash_attn_bwd)
-        # recomputes P and needs head-dim-major copies of q and k besides row-major k and v
+        # recomputes P and needs a head-dim-major copy of k besides row-major k and v
         kbuf = torch.empty(B, Hkv, T, D, dtype=dt, device=dev)
         vbuf = torch.empty_like(kbuf)
-        qt = torch.empty(B, Hkv, G, D, T, dtype=dt, device=dev)
         kt = torch.empty(B, Hkv, D, T, dtype=dt, device=dev)
         vt = torch.empty(B, Hkv, D, T, dtype=dt, device=dev)
-        native.rope_qkv_fwd(qkv, pos, m.cos, m.sin, Hq, Hkv, D, q, kbuf, vbuf, qt=qt, kt=kt, vt=vt)
+        native.rope_qkv_fwd(qkv, pos, m.cos, m.sin, Hq, Hkv, D, q, kbuf, vbuf, kt=kt, vt=vt)
         attn = torch.empty(B, T, Hq * D, dtype=dt, device=dev)
         lse = torch.empty(B, Hkv, G, T, dtype=torch.float32, device=dev)
         native.flash_attn_fwd(q, kbuf, vt, key_valid, attn, lse=lse)
         del vt
-        save.update(qt=qt, kt=kt, lse=lse, key_valid=key_valid)
+        save.update(kt=kt, lse=lse, key_valid=key_valid)
         P = "flash"
         return _layer_mlp(m, i, x, attn, save, kbuf, vbuf, P, q, h1, rstd1)
     vt = None
@@ -359,14 +358,12 @@ class _DecoderLayer(torch.autograd.Function):
         dattn = do @ s.w(p + "o_proj")
         acc_wgrad(s.g(p + "o_proj"), do, sv["attn"].reshape(N, Hq * D))
         if isinstance(sv["P"], str):  # "flash": fused forward, fused backward
-            # fused attention backward; dO^T comes from the same GEMM with swapped operands
-            dattn_t = torch.mm(s.w(p + "o_proj").t(), do.t())  # (Hq*D, N)
+            # fused attention backward (P recomputed from the saved LSE)
             dq = torch.empty_like(sv["q"])
             dk = torch.empty_like(sv["k"])
             dv = torch.empty_like(sv["v"])
-            native.flash_attn_bwd(sv["q"], sv["qt"], sv["k"], sv["kt"], sv["v"], sv["attn"], dattn.view(B, T, Hq * D),
-                                  dattn_t, sv["lse"], sv["key_valid"], dq, dk, dv)
-            del dattn_t
+            native.flash_attn_bwd(sv["q"], sv["k"], sv["kt"], sv["v"], sv["attn"], dattn.view(B, T, Hq * D),
+                                  sv["lse"], sv["key_valid"], dq, dk, dv)
         else:
             dO = dattn.view(B, T, Hkv, G, D).permute(0, 2, 3, 1, 4).reshape(B * Hkv, G * T, D)
             q3 = sv["q"].view(B * Hkv, G * T, D)

@@ -284,16 +284,14 @@ int drl_decode_attention_vt(const void* q, const void* k_cache, const void* vt_c
                             int64_t B, int64_t Hkv, int64_t G, int64_t D, int64_t ld_k, int64_t ld_vt, int64_t L,
                             float scale, void* out, void* stream);
 /* Backward of drl_flash_attn_fwd for Tq == Tk == T, qoff = 0 (the training forward), recomputing P from lse:
- * q (B,Hkv,G,T,D), k / v (B,Hkv,T,D) row-major, qt (B,Hkv,G,D,ld_t) and kt (B,Hkv,D,ld_t) head-dim-major
- * copies (drl_rope_qkv_fwd writes all of them), o and dout (B,T,Hkv*G*D), doutt = dout transposed
- * (Hkv*G*D rows of ld_n columns, column b*T + t), lse from the forward. delta: (B,Hkv,G,T) fp32
- * scratch. Outputs dq (B,Hkv,G,T,D), dk / dv (B,Hkv,T,D) bf16 (the drl_rope_qkv_bwd inputs).
- * T, ld_t, ld_n multiples of 4. Deterministic (the G heads' dK/dV partials are summed in fixed order). */
-int drl_flash_attn_bwd(const void* q, const void* qt, const void* k, const void* kt, const void* v, const void* o,
-                       const void* dout, const void* doutt, int64_t ld_n, const float* lse, int32_t dt,
-                       const uint8_t* key_valid, int64_t ld_valid, int64_t B, int64_t Hkv, int64_t G, int64_t D,
-                       int64_t T, int64_t ld_t, float scale, float* delta, void* dq, void* dk, void* dv,
-                       void* stream);
+ * q (B,Hkv,G,T,D), k / v (B,Hkv,T,D) row-major, kt (B,Hkv,D,ld_t) head-dim-major copy of k (written by
+ * drl_rope_qkv_fwd), o and dout (B,T,Hkv*G*D), lse from the forward. delta: (B,Hkv,G,T) fp32 scratch.
+ * Outputs dq (B,Hkv,G,T,D), dk / dv (B,Hkv,T,D) bf16 (the drl_rope_qkv_bwd inputs). T and ld_t multiples
+ * of 8; head_dim 64. Deterministic (the G heads' dK/dV partials are summed in a fixed order). */
+int drl_flash_attn_bwd(const void* q, const void* k, const void* kt, const void* v, const void* o, const void* dout,
+                       const float* lse, int32_t dt, const uint8_t* key_valid, int64_t ld_valid, int64_t B,
+                       int64_t Hkv, int64_t G, int64_t D, int64_t T, int64_t ld_t, float scale, float* delta, void* dq,
+                       void* dk, void* dv, void* stream);
 
 #ifdef __cplusplus
 }

@@ -149,7 +149,6 @@ def flash_bwd(B=8, Hkv=2, G=7, D=64, T=768):
     q = torch.randn(B, Hkv, G, T, D, device=dev, dtype=bf)
     k = torch.randn(B, Hkv, T, D, device=dev, dtype=bf)
     v = torch.randn(B, Hkv, T, D, device=dev, dtype=bf)
-    qt = q.transpose(-1, -2).contiguous()
     kt = k.transpose(-1, -2).contiguous()
     vt = v.transpose(-1, -2).contiguous()
     valid = torch.ones(B, T, dtype=torch.uint8, device=dev)
@@ -157,9 +156,8 @@ def flash_bwd(B=8, Hkv=2, G=7, D=64, T=768):
     lse = torch.empty(B, Hkv, G, T, device=dev)
     native.flash_attn_fwd(q, k, vt, valid, o, lse=lse)
     dout = torch.randn(B, T, Hkv * G * D, device=dev, dtype=bf)
-    doutt = dout.view(B * T, -1).t().contiguous()
     dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
-    t = time_it(lambda: native.flash_attn_bwd(q, qt, k, kt, v, o, dout, doutt, lse, valid, dq, dk, dv), iters=20)
+    t = time_it(lambda: native.flash_attn_bwd(q, k, kt, v, o, dout, lse, valid, dq, dk, dv), iters=20)
     tf = time_it(lambda: native.flash_attn_fwd(q, k, vt, valid, o, lse=lse), iters=20)
     flops = 4.0 * B * Hkv * G * D * T * (T + 1) / 2
     return [dict(kernel="flash_attn_bwd", B=B, T=T, seconds=t, TFLOPs=2.5 * flops / t / 1e12,
