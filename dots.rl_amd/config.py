@@ -48,7 +48,8 @@ DEFAULTS = dict(
     actor_rollout_ref=dict(
         hybrid_engine=True,
         model=dict(path="random:qwen2.5-0.5b", override_config={}, use_remove_padding=False, use_fused_kernels=False,
-                   enable_gradient_checkpointing=False, external_lib=None, dtype="bfloat16"),
+                   enable_gradient_checkpointing=False, external_lib=None, dtype="bfloat16",
+                   gemm_tuning="auto"),  # replay offline GEMM algorithm choices (workers._enable_gemm_tuning)
         actor=dict(
             strategy="mi355x", ppo_mini_batch_size=32, ppo_micro_batch_size=None, ppo_micro_batch_size_per_gpu=8,
             use_dynamic_bsz=False, ppo_max_token_len_per_gpu=16384, clip_ratio=0.2, clip_ratio_low=0.2,

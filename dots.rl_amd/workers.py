@@ -42,6 +42,30 @@ def resolve_model_config(model_cfg) -> Qwen2Config:
     return Qwen2Config.from_dict(base)
 
 
+_TUNING_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuning", "tunableop_gfx950.csv")
+
+
+def _enable_gemm_tuning(setting):
+    """Replay hipBLASLt / rocBLAS algorithm choices measured offline for this model's GEMM shapes on MI355X
+    (PyTorch TunableOp results file, read-only: no tuning at run time). ``setting``: "auto" (the shipped
+    gfx950 file when running on gfx950), a CSV path, or None / "off"."""
+    if setting in (None, "off", False):
+        return
+    path = _TUNING_FILE if setting == "auto" else str(setting)
+    if setting == "auto" and "gfx950" not in torch.cuda.get_device_properties(torch.cuda.current_device()).gcnArchName:
+        return
+    if not os.path.exists(path):
+        return
+    import tempfile
+
+    import torch.cuda.tunable as tunable
+
+    tunable.enable(True)
+    tunable.tuning_enable(False)
+    tunable.set_filename(os.path.join(tempfile.gettempdir(), "dotsrl_tunableop%d.csv"), insert_device_ordinal=False)
+    tunable.read_file(path)
+
+
 class ActorRolloutRefWorker(Worker):
     def __init__(self, config, role: str = "actor_rollout_ref", output_device: str = "cuda"):
         super().__init__()
@@ -76,6 +100,7 @@ class ActorRolloutRefWorker(Worker):
     @register(dispatch_mode=Dispatch.ONE_TO_ALL)
     def init_model(self):
         cfg = self.config
+        _enable_gemm_tuning(cfg.model.get("gemm_tuning", "auto"))
         mcfg = resolve_model_config(cfg.model)
         self.model_config = mcfg
         dtype = torch.float32 if cfg.model.get("dtype", "bfloat16") == "float32" else torch.bfloat16
