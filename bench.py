@@ -8,9 +8,10 @@ across the N ranks: "scaling" is strong. Random-init Qwen2.5-0.5B weights, synth
   python bench.py [--gpus N] [--steps K] [--warmup W]          (N>1 under torch.distributed.run)
 
 Besides the step rate the JSON line carries
-  roofline     : the dominant hand-written kernel (--roofline-kernel), every launch inside the timed region
-                 bracketed by HIP events on its launch stream; achieved = algorithmic bytes per launch
-                 (ROOFLINE below, DESIGN.md §Kernels) / mean launch duration, against the 8 TB/s HBM peak;
+  roofline     : the dominant hand-written kernel (--roofline-kernel, default the fused attention forward),
+                 every launch inside the timed region bracketed by HIP events on its launch stream;
+                 achieved = algorithmic work per launch (ROOFLINE below) / mean launch
+                 duration, against its bound's peak (2.5 PFLOP/s dense bf16 MFMA or 8 TB/s HBM);
                  traffic = HBM bytes per launch from the committed rocprofv3 PMC pass
                  (profiles/pmc_<kernel>.json, FETCH_SIZE doubled per the gfx950 correction + WRITE_SIZE) or null;
   cpu_baseline : rank 0 at N=1 only — oracle/cpu_baseline.py (the same step restated in eager torch fp32
@@ -30,6 +31,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "PPO steps/sec + rollout tokens/sec, Qwen2.5-0.5B GRPO @1/2/4/8 MI355X"
 PEAK_HBM_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA peak (AMD's 5 PF figure counts 2:1 sparsity)
 
 
 def _softmax_fwd_bytes(a):
@@ -47,9 +49,22 @@ def _decode_attn_bytes(a):
     return B * Hkv * (2 * L * D + 2 * G * D) * e
 
 
-ROOFLINE = {  # symbol -> (bytes per launch from the call's arguments, per-unit statement)
-    "drl_masked_softmax_fwd": (_softmax_fwd_bytes, "6 B per attention score (fp32 in, bf16 out)"),
-    "drl_decode_attention": (_decode_attn_bytes, "4*D B per cached key (bf16 K+V rows)"),
+def _flash_fwd_flops(a):
+    # drl_flash_attn_fwd(q, k, vt, dt, valid, ld_valid, B, Hkv, G, D, Tq, Tk, ld_k, ld_vt, qoff, ...):
+    # QK^T and PV over the causally allowed (query, key) pairs: 4 * D FLOP per pair and query head
+    B, Hkv, G, D, Tq, Tk, qoff = a[6], a[7], a[8], a[9], a[10], a[11], a[14]
+    pairs = sum(min(Tk, t + qoff + 1) for t in range(Tq))
+    return 4.0 * B * Hkv * G * D * pairs
+
+
+# symbol -> (work per launch from the call's arguments, per-unit statement, bound, peak, unit)
+ROOFLINE = {
+    "drl_flash_attn_fwd": (_flash_fwd_flops, "4*D FLOP per causal (query, key) pair per query head", "mfma",
+                           PEAK_BF16_TFLOPS, "TFLOP/s"),
+    "drl_masked_softmax_fwd": (_softmax_fwd_bytes, "6 B per attention score (fp32 in, bf16 out)", "hbm",
+                               PEAK_HBM_GBPS, "GB/s"),
+    "drl_decode_attention": (_decode_attn_bytes, "4*D B per cached key (bf16 K+V rows)", "hbm", PEAK_HBM_GBPS,
+                             "GB/s"),
 }
 
 
@@ -109,7 +124,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--tiny", action="store_true", help="2-layer model, small batch (bring-up only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--roofline-kernel", default="drl_masked_softmax_fwd", choices=sorted(ROOFLINE))
+    ap.add_argument("--roofline-kernel", default="drl_flash_attn_fwd", choices=sorted(ROOFLINE))
     ap.add_argument("--override", nargs="*", default=[])
     args = ap.parse_args()
 
@@ -152,13 +167,15 @@ def main():
     n_launch, t_launch, b_launch = timer.summary()
     if rank == 0:
         ar = cfg.actor_rollout_ref
-        achieved = b_launch / t_launch / 1e9 if n_launch else None
+        _, per_unit, bound, peak, unit = ROOFLINE[args.roofline_kernel]
+        scale = 1e12 if unit == "TFLOP/s" else 1e9
+        achieved = b_launch / t_launch / scale if n_launch else None
         traffic, traffic_src = _pmc_traffic(args.roofline_kernel)
-        roofline = {"kernel": args.roofline_kernel, "bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBPS,
-                    "unit": "GB/s", "frac": achieved / PEAK_HBM_GBPS if achieved else None, "traffic": traffic,
-                    "algorithmic_bytes_per_launch": b_launch if n_launch else None,
+        roofline = {"kernel": args.roofline_kernel, "bound": bound, "achieved": achieved, "peak": peak,
+                    "unit": unit, "frac": achieved / peak if achieved else None, "traffic": traffic,
+                    "algorithmic_work_per_launch": b_launch if n_launch else None,
                     "mean_launch_us": t_launch * 1e6 if n_launch else None, "launches": n_launch,
-                    "per_unit": ROOFLINE[args.roofline_kernel][1], "traffic_source": traffic_src}
+                    "per_unit": per_unit, "traffic_source": traffic_src}
         line = {
             "metric": METRIC,
             "value": steps_per_s,

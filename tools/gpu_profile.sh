@@ -4,8 +4,8 @@
 # Usage: bash tools/gpu_profile.sh <round-tag> [roofline-kernel-symbol] [kernel-name-regex]
 set -o pipefail
 TAG=${1:-r01}
-SYM=${2:-drl_masked_softmax_fwd}
-RX=${3:-masked_softmax_fwd}
+SYM=${2:-drl_flash_attn_fwd}
+RX=${3:-flash_fwd_kernel}
 ROOT=$(pwd)
 OUT=$ROOT/gpurun_out/$TAG
 mkdir -p "$OUT"
