@@ -493,17 +493,81 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const float* x, const 
     dw_part[blockIdx.x * H + j] = s_dw[j] + s_dw[H + j] + s_dw[2 * H + j] + s_dw[3 * H + j];
 }
 
-// dw[j] += sum over blocks of dw_part[:, j]: 64 columns x 4 block-slices per workgroup, fixed order
-__global__ __launch_bounds__(256) void colsum_kernel(const float* part, int64_t nb, int64_t H, float* out) {
-  __shared__ float red[4][64];
-  const int c = threadIdx.x & 63, sl = threadIdx.x >> 6;
-  const int64_t j = static_cast<int64_t>(blockIdx.x) * 64 + c;
-  float s = 0.f;
-  if (j < H)
-    for (int64_t b = sl; b < nb; b += 4) s += part[b * H + j];
-  red[sl][c] = s;
+// Vectorised form for H % 128 == 0 (Qwen2: 896): one wave per row, each lane owns the column pairs
+// 2*lane + 128*k; the row's x and dy stay in registers between the dot product and the update (one read).
+template <typename E, int K>
+__global__ __launch_bounds__(256) void rmsnorm_bwd_vec_kernel(const float* x, const float* w, const float* rstd,
+                                                              const E* dy, float* dx, float* dw_part, int64_t N) {
+  constexpr int H = 128 * K;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __shared__ float2 s_dw[4][64 * K];
+  float2 wv[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    wv[k] = *reinterpret_cast<const float2*>(w + 2 * lane + 128 * k);
+    s_dw[wave][lane + 64 * k] = make_float2(0.f, 0.f);
+  }
+  float2 acc[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) acc[k] = make_float2(0.f, 0.f);
+  for (int64_t row = static_cast<int64_t>(blockIdx.x) * 4 + wave; row < N; row += static_cast<int64_t>(gridDim.x) * 4) {
+    const float r = rstd[row];
+    float2 xv[K], gv[K];
+    float dot = 0.f;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int64_t j = row * H + 2 * lane + 128 * k;
+      xv[k] = *reinterpret_cast<const float2*>(x + j);
+      gv[k] = make_float2(ldf(dy, j), ldf(dy, j + 1));
+      dot += (wv[k].x * gv[k].x) * (xv[k].x * r) + (wv[k].y * gv[k].y) * (xv[k].y * r);
+    }
+    dot = wave_sum(dot) / static_cast<float>(H);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int64_t j = row * H + 2 * lane + 128 * k;
+      const float xh0 = xv[k].x * r, xh1 = xv[k].y * r;
+      float2 d = *reinterpret_cast<float2*>(dx + j);
+      d.x += r * (wv[k].x * gv[k].x - xh0 * dot);
+      d.y += r * (wv[k].y * gv[k].y - xh1 * dot);
+      *reinterpret_cast<float2*>(dx + j) = d;
+      acc[k].x += gv[k].x * xh0;
+      acc[k].y += gv[k].y * xh1;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) s_dw[wave][lane + 64 * k] = acc[k];
   __syncthreads();
-  if (sl == 0 && j < H) out[j] += (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
+  for (int j = threadIdx.x; j < 64 * K; j += blockDim.x) {
+    const float2 a = s_dw[0][j], b = s_dw[1][j], c = s_dw[2][j], d = s_dw[3][j];
+    const int col = 2 * (j % 64) + 128 * (j / 64);
+    dw_part[blockIdx.x * H + col] = (a.x + b.x) + (c.x + d.x);
+    dw_part[blockIdx.x * H + col + 1] = (a.y + b.y) + (c.y + d.y);
+  }
+}
+
+// dw[j] += sum over blocks of dw_part[:, j]: 16 columns x 16 block-slices per workgroup (many
+// workgroups, short dependent chains), slices combined in a fixed order
+__global__ __launch_bounds__(256) void colsum_kernel(const float* part, int64_t nb, int64_t H, float* out) {
+  __shared__ float red[16][16];
+  const int c = threadIdx.x & 15, sl = threadIdx.x >> 4;
+  const int64_t j = static_cast<int64_t>(blockIdx.x) * 16 + c;
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
+  if (j < H) {
+    int64_t b = sl;
+    for (; b + 48 < nb; b += 64) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) s[u] += part[(b + 16 * u) * H + j];
+    }
+    for (; b < nb; b += 16) s[0] += part[b * H + j];
+  }
+  red[sl][c] = (s[0] + s[1]) + (s[2] + s[3]);
+  __syncthreads();
+  if (sl == 0 && j < H) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) t += red[k][c];
+    out[j] += t;
+  }
 }
 
 // ------------------------------------------------------------------------------------------ SwiGLU
@@ -665,10 +729,17 @@ int drl_rmsnorm_bwd(const float* x, const float* weight, const float* rstd, cons
     return fail(DRL_ERR_WORKSPACE, "workspace too small");
   float* part = static_cast<float*>(workspace);
   hipStream_t s = static_cast<hipStream_t>(stream);
-  DRL_E_DISPATCH(dt, hipLaunchKernelGGL(rmsnorm_bwd_kernel<E>, dim3(grid), dim3(256), 4 * H * sizeof(float), s, x,
-                                        weight, rstd, static_cast<const E*>(dy), dx, part, N, H));
+  const bool vec = H == 896 && (reinterpret_cast<uintptr_t>(x) & 7u) == 0 && (reinterpret_cast<uintptr_t>(dx) & 7u) == 0 &&
+                   (reinterpret_cast<uintptr_t>(weight) & 7u) == 0;
+  if (vec) {
+    DRL_E_DISPATCH(dt, hipLaunchKernelGGL((rmsnorm_bwd_vec_kernel<E, 7>), dim3(grid), dim3(256), 0, s, x, weight, rstd,
+                                          static_cast<const E*>(dy), dx, part, N));
+  } else {
+    DRL_E_DISPATCH(dt, hipLaunchKernelGGL(rmsnorm_bwd_kernel<E>, dim3(grid), dim3(256), 4 * H * sizeof(float), s, x,
+                                          weight, rstd, static_cast<const E*>(dy), dx, part, N, H));
+  }
   DRL_LAUNCH_CHECK();
-  hipLaunchKernelGGL(colsum_kernel, dim3((H + 63) / 64), dim3(256), 0, s, part, static_cast<int64_t>(grid), H, dw);
+  hipLaunchKernelGGL(colsum_kernel, dim3((H + 15) / 16), dim3(256), 0, s, part, static_cast<int64_t>(grid), H, dw);
   DRL_LAUNCH_CHECK();
   return DRL_OK;
 }

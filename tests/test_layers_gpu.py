@@ -106,8 +106,9 @@ def test_masked_softmax_forward_backward(dt, Tq, Tk, qoff):
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("with_delta", [False, True])
-def test_add_rmsnorm_forward_backward(dt, with_delta):
-    N, H, eps = 77, 896, 1e-6
+@pytest.mark.parametrize("N,H", [(77, 896), (3000, 896), (77, 320)])  # 896: vectorised backward; 320: generic
+def test_add_rmsnorm_forward_backward(dt, with_delta, N, H):
+    eps = 1e-6
     g = torch.Generator(device=DEV).manual_seed(1)
     x_in = torch.randn(N, H, device=DEV, generator=g)
     delta = torch.randn(N, H, device=DEV, generator=g).to(dt) if with_delta else None
