@@ -653,8 +653,8 @@ __global__ __launch_bounds__(512) void flash_dkdv_kernel(FlashBwdArgs a) {
 // One new token per sequence against the KV cache, on MFMA: the G query heads of a KV head are the
 // "queries" of the forward kernel's S^T = K Q^T tile (columns >= G are zero padding), so the online
 // softmax stays lane-local and P^T feeds O^T += V^T P^T from the accumulators. Workgroup = (sequence,
-// KV head), 4 waves splitting the cached keys into interleaved 32-key blocks (each wave's next block
-// is loaded while it computes the current one); the 4 partial softmax states are merged in LDS.
+// KV head), NW waves splitting the cached keys into interleaved 32-key blocks (each wave's next block
+// is loaded while it computes the current one); the NW partial softmax states are merged in LDS.
 // The cache holds K row-major (B, Hkv, ld_k, D) and V head-dim-major (B, Hkv, D, ld_vt), the layout
 // drl_rope_qkv_fwd writes with koff / koff_dev. HBM-bound: 4 * D bytes per cached key.
 struct DecodeArgs {
@@ -689,9 +689,9 @@ __device__ __forceinline__ void dec_load(const uint16_t* kb, const uint16_t* vtb
   }
 }
 
-template <int D>
-__global__ __launch_bounds__(256) void decode_mfma_kernel(DecodeArgs a) {
-  constexpr int KS = D / 16, MT = D / 32, NW = 4;
+template <int D, int NW>
+__global__ __launch_bounds__(64 * NW) void decode_mfma_kernel(DecodeArgs a) {
+  constexpr int KS = D / 16, MT = D / 32;
   __shared__ float s_m[NW][32], s_l[NW][32];
   __shared__ float s_o[NW][MT][16][64];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -885,8 +885,21 @@ int drl_decode_attention_vt(const void* q, const void* k_cache, const void* vt_c
                static_cast<const uint16_t*>(vt_cache), key_valid, ld_valid, qpos_ptr, qpos, Hkv, G, ld_k, ld_vt, L,
                scale * 1.4426950408889634f, static_cast<uint16_t*>(out)};
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (D == 64) hipLaunchKernelGGL(decode_mfma_kernel<64>, dim3(B * Hkv), dim3(256), 0, s, a);
-  else hipLaunchKernelGGL(decode_mfma_kernel<128>, dim3(B * Hkv), dim3(256), 0, s, a);
+  // waves per (sequence, KV head): 2 when the grid alone fills the chip (B=512: 37.9 vs 39.1 us at 4 waves,
+  // tools/kernel_bench.py --only decode), more to spread the keys of small decode batches
+  const int64_t wgs = B * Hkv, cus = cu_count();
+  const int nw = wgs >= 4 * cus ? 2 : (wgs >= cus ? 4 : 8);
+#define DRL_DEC(DD, NN) hipLaunchKernelGGL((decode_mfma_kernel<DD, NN>), dim3(B * Hkv), dim3(64 * NN), 0, s, a)
+  if (D == 64) {
+    if (nw == 2) DRL_DEC(64, 2);
+    else if (nw == 4) DRL_DEC(64, 4);
+    else DRL_DEC(64, 8);
+  } else {
+    if (nw == 2) DRL_DEC(128, 2);
+    else if (nw == 4) DRL_DEC(128, 4);
+    else DRL_DEC(128, 8);
+  }
+#undef DRL_DEC
   DRL_LAUNCH_CHECK();
   return DRL_OK;
 }

@@ -165,7 +165,7 @@ def _ref_decode(q, k, v, valid, L, qpos):
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("B,Hkv,G,D,Tk,L", [(4, 2, 7, 64, 768, 513), (3, 2, 7, 64, 300, 1), (2, 4, 4, 128, 1100, 1100),
-                                            (300, 2, 7, 64, 768, 700),
+                                            (300, 2, 7, 64, 768, 700), (520, 2, 7, 64, 768, 700),
                                             (5, 1, 8, 32, 256, 256)])
 def test_decode_attention(dt, B, Hkv, G, D, Tk, L):
     g = torch.Generator(device=DEV).manual_seed(L)
