@@ -40,6 +40,19 @@ struct FlashArgs {
 
 __device__ __forceinline__ bf16x8 as_bf16x8(u16x8 v) { return __builtin_bit_cast(bf16x8, v); }
 
+// XCD-aware tile order (cdna_hip_programming.md §5.5 T1): workgroups are dealt round-robin to the 8 XCDs,
+// each with its own L2. Remap the linear workgroup id so that all tiles of one (sequence, KV head) land on
+// the same XCD (its K / V stay in that L2) and, within an XCD, run in tile order. Returns (tile, bh).
+// Placement only changes speed, never results.
+__device__ __forceinline__ void xcd_tile_order(int ntiles, int nbh, int& tile, int64_t& bh) {
+  const int64_t n = static_cast<int64_t>(ntiles) * nbh;
+  const int64_t i = static_cast<int64_t>(blockIdx.y) * gridDim.x + blockIdx.x;
+  int64_t c = i;
+  if (n % 8 == 0) c = (i % 8) * (n / 8) + i / 8;
+  bh = c / ntiles;
+  tile = static_cast<int>(c % ntiles);
+}
+
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 // ds_read_b64_tr_b16 (cdna_hip_programming.md §5.5 T10): per 16-lane group, lane 4q+p addresses row q,
 // columns 4p..4p+3 of a 4 x 16 block; lane i receives column i of the 4 rows (row q in element q).
@@ -133,10 +146,12 @@ __global__ __launch_bounds__(512) void flash_fwd_kernel(FlashArgs a) {
   const int lane = tid & 63, g = tid >> 6;
   const bool computes = g < a.G;  // waves >= G only help staging
   const int qi = lane & 31, h = lane >> 5;
-  const int64_t bh = blockIdx.y;
-  const int64_t b = bh / a.Hkv;
   const int64_t ntiles = (a.Tq + 31) / 32;
-  const int64_t t0 = (ntiles - 1 - static_cast<int64_t>(blockIdx.x)) * 32;
+  int tile;
+  int64_t bh;
+  xcd_tile_order(static_cast<int>(ntiles), static_cast<int>(gridDim.y), tile, bh);
+  const int64_t b = bh / a.Hkv;
+  const int64_t t0 = (ntiles - 1 - tile) * 32;  // longest causal rows first
   const int64_t tq = t0 + qi;
   const bool qvalid = computes && tq < a.Tq;
 
@@ -390,10 +405,13 @@ __global__ __launch_bounds__(512) void flash_dq_kernel(FlashBwdArgs a) {
   const int lane = tid & 63, g = tid >> 6;
   const bool computes = g < a.G;
   const int qi = lane & 31, h = lane >> 5;
-  const int64_t bh = blockIdx.y, b = bh / a.Hkv, hkv = bh % a.Hkv;
   const int T = static_cast<int>(a.T);
   const int ntiles = (T + 31) / 32;
-  const int t0 = (ntiles - 1 - static_cast<int>(blockIdx.x)) * 32;
+  int tile;
+  int64_t bh;
+  xcd_tile_order(ntiles, static_cast<int>(gridDim.y), tile, bh);
+  const int64_t b = bh / a.Hkv, hkv = bh % a.Hkv;
+  const int t0 = (ntiles - 1 - tile) * 32;  // longest causal rows first
   const int tq = t0 + qi;
   const bool qvalid = computes && tq < T;
   const int64_t head = bh * a.G + (computes ? g : 0);
@@ -526,11 +544,13 @@ __global__ __launch_bounds__(512) void flash_dkdv_kernel(FlashBwdArgs a) {
   const int tid = threadIdx.x;
   const int lane = tid & 63, g = tid >> 6;
   const int li = lane & 31, h = lane >> 5;
-  const int64_t bh = blockIdx.y, b = bh / a.Hkv, hkv = bh % a.Hkv;
   const int T = static_cast<int>(a.T);
   const int ntiles = (T + 31) / 32;
-  const int k0 = static_cast<int>(blockIdx.x) * 32;  // key tile 0 has the most query tiles: dispatched first
-  (void)ntiles;
+  int tile;
+  int64_t bh;
+  xcd_tile_order(ntiles, static_cast<int>(gridDim.y), tile, bh);
+  const int64_t b = bh / a.Hkv, hkv = bh % a.Hkv;
+  const int k0 = tile * 32;  // key tile 0 has the most query tiles: dispatched first
   const int key = k0 + li;
   const bool kin = key < T;
   const bool kval = kin && a.valid[b * a.ld_valid + key] != 0;
