@@ -61,14 +61,22 @@ __device__ __forceinline__ u16x4 lds_tr16(const uint16_t* p) {
   return __builtin_bit_cast(u16x4, r);
 }
 
-// A operand "X^T" (rows = head dim, k = positions in the accumulator order) of a 32-position x D tile X held
-// row-major in LDS ([position][d], row stride rs elements): k-step s, head-dim tile mt. Two transposing reads:
-// element j of lane half h is position 16s + 8(j>>2) + 4h + (j&3), head-dim 32mt + (lane & 31).
-__device__ __forceinline__ u16x8 lds_xt_operand(const uint16_t* x, int rs, int mt, int s, int lane) {
+// Swizzled [32 positions][64] bf16 image (128-B rows, no padding): the 16-B unit u of row r is stored at
+// unit u ^ f(r). f is a bijection on r & 7 (conflict-free 16-B row writes: 8 consecutive rows cover all 8
+// units) that also flips bit 2 between rows r and r + 2 (the 4 rows of a transposing read never share banks).
+__device__ __forceinline__ int xsw(int r) { return (r & 7) ^ ((r & 2) << 1); }
+__device__ __forceinline__ int ximg_off(int r, int col) {  // element offset of (row r, column col)
+  return r * 64 + 8 * ((col >> 3) ^ xsw(r)) + (col & 7);
+}
+
+// A operand "X^T" (rows = head dim, k = positions in the accumulator order) of a 32-position x 64 tile X in
+// the swizzled image above: k-step s, head-dim tile mt. Two transposing reads: element j of lane half h is
+// position 16s + 8(j>>2) + 4h + (j&3), head-dim 32mt + (lane & 31).
+__device__ __forceinline__ u16x8 lds_xt_operand(const uint16_t* x, int mt, int s, int lane) {
   const int i = lane & 15, q = i >> 2, p = i & 3, h = lane >> 5;
   const int col = 32 * mt + (lane & 16) + 4 * p;
-  const u16x4 lo = lds_tr16(x + (16 * s + 4 * h + q) * rs + col);
-  const u16x4 hi = lds_tr16(x + (16 * s + 8 + 4 * h + q) * rs + col);
+  const u16x4 lo = lds_tr16(x + ximg_off(16 * s + 4 * h + q, col));
+  const u16x4 hi = lds_tr16(x + ximg_off(16 * s + 8 + 4 * h + q, col));
   return u16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
@@ -535,9 +543,9 @@ __device__ __forceinline__ void dkdv_rows(const uint16_t* qbase, const uint16_t*
 template <int D>
 __global__ __launch_bounds__(512) void flash_dkdv_kernel(FlashBwdArgs a) {
   constexpr int KS = D / 16, MT = D / 32, KROW = D + 8;
-  // per-wave image of the current query tile's Q and dO rows, row stride 1.5 D elements: the 4 rows of a
-  // transposing read land in disjoint bank ranges
-  constexpr int XROW = D + D / 2;
+  // per-wave swizzled image of the current query tile's Q and dO rows (ximg_off)
+  constexpr int XROW = 64;
+  static_assert(D == 64, "the Q / dO image is laid out for head_dim 64");
   __shared__ float red[2][MT][16][64];  // [dk/dv][tile][register][lane]: conflict-free per register
   __shared__ __attribute__((aligned(16))) uint16_t kv_lds[2][32 * KROW];  // this key tile's K and V rows
   __shared__ __attribute__((aligned(16))) uint16_t xw[8][2][32 * XROW];    // [wave][Q / dO][position][d]
@@ -581,8 +589,8 @@ __global__ __launch_bounds__(512) void flash_dkdv_kernel(FlashBwdArgs a) {
     // operands of dV / dK are read back from it after the softmax (no head-dim-major copies in HBM)
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
-      *reinterpret_cast<u16x8*>(xq + li * XROW + 16 * s + 8 * h) = qa[s];
-      *reinterpret_cast<u16x8*>(xd + li * XROW + 16 * s + 8 * h) = da[s];
+      *reinterpret_cast<u16x8*>(xq + ximg_off(li, 16 * s + 8 * h)) = qa[s];
+      *reinterpret_cast<u16x8*>(xd + ximg_off(li, 16 * s + 8 * h)) = da[s];
     }
     float4 l4[4], d4[4];
 #pragma unroll
@@ -629,8 +637,8 @@ __global__ __launch_bounds__(512) void flash_dkdv_kernel(FlashBwdArgs a) {
     for (int mt = 0; mt < MT; ++mt) {
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        const u16x8 dov = lds_xt_operand(xd, XROW, mt, s, lane);
-        const u16x8 qtv = lds_xt_operand(xq, XROW, mt, s, lane);
+        const u16x8 dov = lds_xt_operand(xd, mt, s, lane);
+        const u16x8 qtv = lds_xt_operand(xq, mt, s, lane);
         dvt[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(dov), as_bf16x8(pb[s]), dvt[mt], 0, 0, 0);
         dkt[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(qtv), as_bf16x8(dsb[s]), dkt[mt], 0, 0, 0);
       }
