@@ -126,6 +126,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--roofline-kernel", default="drl_flash_attn_fwd", choices=sorted(ROOFLINE))
     ap.add_argument("--override", nargs="*", default=[])
+    ap.add_argument("--dist-backend", default=None,
+                    help="default: nccl (RCCL) on GPU; gloo lets several ranks share one GPU for a rehearsal")
     args = ap.parse_args()
 
     import torch
@@ -135,7 +137,7 @@ def main():
     from dots.rl_amd.single_controller import init_process_group_from_env
     from dots.rl_amd.trainer import RayPPOTrainer
 
-    init_process_group_from_env()
+    init_process_group_from_env(args.dist_backend)
     rank, world = dist.get_rank(), dist.get_world_size()
     assert world == args.gpus, f"--gpus {args.gpus} but WORLD_SIZE {world}"
     cfg = build_config(args)
