@@ -37,6 +37,7 @@ class PPOLossParams(ctypes.Structure):
         ("loss_scale_factor", ctypes.c_float),
         ("loss_agg_mode", ctypes.c_int32),
         ("kl_type", ctypes.c_int32),
+        ("token_count", ctypes.c_void_p),
     ]
 
 
@@ -91,7 +92,8 @@ SIGNATURES = {
     "drl_grpo_outcome_advantage": (ctypes.c_int, [P, P, I32, P, P, P, I64, I64, I64, F32, I32, P, P, P, SZ, P]),
     "drl_gae_workspace_bytes": (SZ, [I64, I64]),
     "drl_gae_advantage_return": (ctypes.c_int, [P, P, P, I32, I64, I64, F32, F32, P, P, P, SZ, P]),
-    "drl_select_tokens": (ctypes.c_int, [P, I32, I64, I64, I64, ctypes.POINTER(SamplingParams), P, P, I64, P]),
+    "drl_select_tokens_workspace_bytes": (SZ, [I64]),
+    "drl_select_tokens": (ctypes.c_int, [P, I32, I64, I64, I64, ctypes.POINTER(SamplingParams), P, P, I64, P, SZ, P]),
     "drl_response_mask": (ctypes.c_int, [P, I64, I64, I64, P, I32, P, I32, I64, P]),
     "drl_position_ids": (ctypes.c_int, [P, I32, I64, I64, P, P]),
     "drl_response_position_ids": (ctypes.c_int, [P, I64, I64, I64, P]),
@@ -111,12 +113,17 @@ SIGNATURES = {
     "drl_decode_attention_workspace_bytes": (SZ, [I64, I64, I64, I64, I64]),
     "drl_flash_attn_fwd": (ctypes.c_int, [P, P, P, I32, P, I64, I64, I64, I64, I64, I64, I64, I64, I64, I64, F32, P, P,
                                           P]),
+    "drl_decode_attention_vt_workspace_bytes": (SZ, [I64, I64, I64, I64]),
+    "drl_decode_attention_set_plan": (None, [I32, I32]),
     "drl_decode_attention_vt": (ctypes.c_int, [P, P, P, I32, P, I64, P, I64, I64, I64, I64, I64, I64, I64, I64, F32,
-                                               P, P]),
+                                               P, P, SZ, P]),
     "drl_flash_attn_bwd": (ctypes.c_int, [P, P, P, P, P, P, P, I32, P, I64, I64, I64, I64, I64, I64, I64, F32, P, P, P, P,
                                           P]),
     "drl_decode_attention": (ctypes.c_int, [P, P, P, I32, P, I64, P, I64, I64, I64, I64, I64, I64, I64, F32, P, P, SZ,
                                             P]),
+    "drl_linear_decode_workspace_bytes": (SZ, [I64, I64, I64, I32]),
+    "drl_linear_decode_set_plan": (None, [I32, I32]),
+    "drl_linear_decode": (ctypes.c_int, [P, I64, P, P, I32, I64, I64, I64, I32, P, I64, P, SZ, P]),
 }
 
 _lib = None

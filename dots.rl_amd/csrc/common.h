@@ -114,6 +114,13 @@ __device__ __forceinline__ void store_sc1(double* p, double v) {
   __hip_atomic_store((gu64_t*)(p), static_cast<unsigned long long>(__double_as_longlong(v)),
                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+typedef __attribute__((address_space(1))) unsigned gu32_t;
+__device__ __forceinline__ void store_f32_sc1(float* p, float v) {
+  __hip_atomic_store((gu32_t*)(p), __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float load_f32_sc1(const float* p) {
+  return __uint_as_float(__hip_atomic_load((const gu32_t*)(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
 __device__ __forceinline__ double load_sc1(const double* p) {
   return __longlong_as_double(static_cast<long long>(
       __hip_atomic_load((const gu64_t*)(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));

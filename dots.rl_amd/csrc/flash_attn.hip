@@ -696,24 +696,87 @@ struct DecodeArgs {
   int64_t Hkv, G, ld_k, ld_vt, L;
   float scale_log2;
   uint16_t* out;  // (B, Hkv, G, D)
+  float* slabs;        // split-K: (B*Hkv, splits, 64 + 32*D) fp32 partial states (m, l, unnormalised o)
+  unsigned* tickets;   // split-K: (B*Hkv) arrival counters, zero between launches
+};
+
+// one 32-key block of the cache for lane (qi, h): K rows (A operand of S^T = K Q^T), V^T columns
+// (A operand of O^T = V^T P^T) and the key-valid bytes of the keys this lane's scores cover
+template <int D>
+struct DecBlock {
+  u16x8 kf[D / 16];
+  u16x8 vf[D / 32][2];
+  uint32_t vb[4];
 };
 
 template <int D>
-__device__ __forceinline__ void dec_load(const uint16_t* kb, const uint16_t* vtb, int64_t ld_vt, int k0, int kend,
-                                         int qi, int h, u16x8 (&kf)[D / 16], u16x8 (&vf)[D / 32][2]) {
+__device__ __forceinline__ void dec_load(const uint16_t* kb, const uint16_t* vtb, const uint8_t* vrow, int64_t ld_vt,
+                                         int k0, int kend, int qi, int h, DecBlock<D>& blk) {
   const int key = k0 + qi;
   const bool kin = key < kend;
   const uint16_t* krow = kb + static_cast<int64_t>(kin ? key : 0) * D + 8 * h;
 #pragma unroll
   for (int s = 0; s < D / 16; ++s) {
-    kf[s] = *reinterpret_cast<const u16x8*>(krow + 16 * s);
-    if (!kin) kf[s] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    blk.kf[s] = *reinterpret_cast<const u16x8*>(krow + 16 * s);
+    if (!kin) blk.kf[s] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
   }
 #pragma unroll
   for (int mt = 0; mt < D / 32; ++mt) {
-    const uint16_t* vrow = vtb + static_cast<int64_t>(32 * mt + qi) * ld_vt;
+    const uint16_t* vr = vtb + static_cast<int64_t>(32 * mt + qi) * ld_vt;
 #pragma unroll
-    for (int s = 0; s < 2; ++s) vf[mt][s] = load_perm8(vrow, k0 + 16 * s + 4 * h, kend);
+    for (int s = 0; s < 2; ++s) blk.vf[mt][s] = load_perm8(vr, k0 + 16 * s + 4 * h, kend);
+  }
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int kk = k0 + 8 * c + 4 * h;
+    if (kk + 3 < kend) {
+      blk.vb[c] = *reinterpret_cast<const uint32_t*>(vrow + kk);
+    } else {
+      uint32_t v = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v |= (kk + j < kend ? static_cast<uint32_t>(vrow[kk + j]) : 0u) << (8 * j);
+      blk.vb[c] = v;
+    }
+  }
+}
+
+// online-softmax step over one loaded block (scores, running max / sum, O^T accumulation)
+template <int D>
+__device__ __forceinline__ void dec_block(const DecBlock<D>& blk, const bf16x8 (&qf)[D / 16], float scale_log2,
+                                          float& m, float& lsum, f32x16 (&o)[D / 32]) {
+  constexpr int KS = D / 16, MT = D / 32;
+  f32x16 st = f32x16{};
+#pragma unroll
+  for (int s = 0; s < KS; ++s) st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(blk.kf[s]), qf[s], st, 0, 0, 0);
+  float x[16], mx = -INFINITY;
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int r = 4 * c + j;
+      x[r] = ((blk.vb[c] >> (8 * j)) & 0xffu) != 0u ? st[r] * scale_log2 : -INFINITY;
+      mx = fmaxf(mx, x[r]);
+    }
+  mx = fmaxf(mx, __shfl_xor(mx, 32, kWave));
+  const float mn = fmaxf(m, mx);
+  const float mref = mn == -INFINITY ? 0.f : mn;
+  const float alpha = __builtin_amdgcn_exp2f(m - mref);
+  m = mn;
+  float ps = 0.f;
+  u16x8 pb[2];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const float p = __builtin_amdgcn_exp2f(x[r] - mref);
+    ps += p;
+    pb[r >> 3][r & 7] = to_bf16_bits(p);
+  }
+  lsum = lsum * alpha + ps;
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    o[mt] *= alpha;
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+      o[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(blk.vf[mt][s]), as_bf16x8(pb[s]), o[mt], 0, 0, 0);
   }
 }
 
@@ -727,6 +790,17 @@ __global__ __launch_bounds__(64 * NW) void decode_mfma_kernel(DecodeArgs a) {
   const int64_t bh = blockIdx.x, b = bh / a.Hkv;
   const int qpos = static_cast<int>(a.qpos_ptr ? *a.qpos_ptr : a.qpos);
   const int kend = static_cast<int>(min(a.L, static_cast<int64_t>(qpos) + 1));
+  const uint16_t* kb = a.k + bh * a.ld_k * D;
+  const uint16_t* vtb = a.vt + bh * D * a.ld_vt;
+  const uint8_t* vrow = a.valid + b * a.ld_valid;
+  // split-K over gridDim.y workgroups: split y takes 32-key blocks [y*n/S, (y+1)*n/S) of the n live blocks;
+  // each wave takes blocks ib0, ib0 + NW, ... and has its first two in flight together with q
+  const int nall = (kend + 31) / 32, S = gridDim.y, y = blockIdx.y;
+  const int bbeg = y * nall / S, nblk = (y + 1) * nall / S;
+  const int ib0 = bbeg + w;
+  DecBlock<D> A, Bn;
+  if (ib0 < nblk) dec_load<D>(kb, vtb, vrow, a.ld_vt, 32 * ib0, kend, qi, h, A);
+  if (ib0 + NW < nblk) dec_load<D>(kb, vtb, vrow, a.ld_vt, 32 * (ib0 + NW), kend, qi, h, Bn);
   bf16x8 qf[KS];
   {
     const bool qv = qi < a.G;
@@ -738,64 +812,16 @@ __global__ __launch_bounds__(64 * NW) void decode_mfma_kernel(DecodeArgs a) {
       qf[s] = as_bf16x8(v);
     }
   }
-  const uint16_t* kb = a.k + bh * a.ld_k * D;
-  const uint16_t* vtb = a.vt + bh * D * a.ld_vt;
-  const uint8_t* vrow = a.valid + b * a.ld_valid;
   f32x16 o[MT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) o[mt] = f32x16{};
   float m = -INFINITY, lsum = 0.f;
-  const int nblk = (kend + 31) / 32;
-  u16x8 kf[KS], vf[MT][2];
-  if (w < nblk) dec_load<D>(kb, vtb, a.ld_vt, 32 * w, kend, qi, h, kf, vf);
-  for (int ib = w; ib < nblk; ib += NW) {
-    const int k0 = 32 * ib;
-    f32x16 st = f32x16{};
-#pragma unroll
-    for (int s = 0; s < KS; ++s) st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(kf[s]), qf[s], st, 0, 0, 0);
-    u16x8 vcur[MT][2];
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) vcur[mt][0] = vf[mt][0], vcur[mt][1] = vf[mt][1];
-    if (ib + NW < nblk) dec_load<D>(kb, vtb, a.ld_vt, k0 + 32 * NW, kend, qi, h, kf, vf);  // next block in flight
-    float x[16], mx = -INFINITY;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const int kk = k0 + 8 * c + 4 * h;
-      uint32_t vb;
-      if (kk + 3 < kend) {
-        vb = *reinterpret_cast<const uint32_t*>(vrow + kk);
-      } else {
-        vb = 0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) vb |= (kk + j < kend ? static_cast<uint32_t>(vrow[kk + j]) : 0u) << (8 * j);
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int r = 4 * c + j;
-        x[r] = ((vb >> (8 * j)) & 0xffu) != 0u ? st[r] * a.scale_log2 : -INFINITY;
-        mx = fmaxf(mx, x[r]);
-      }
-    }
-    mx = fmaxf(mx, __shfl_xor(mx, 32, kWave));
-    const float mn = fmaxf(m, mx);
-    const float mref = mn == -INFINITY ? 0.f : mn;
-    const float alpha = __builtin_amdgcn_exp2f(m - mref);
-    m = mn;
-    float ps = 0.f;
-    u16x8 pb[2];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const float p = __builtin_amdgcn_exp2f(x[r] - mref);
-      ps += p;
-      pb[r >> 3][r & 7] = to_bf16_bits(p);
-    }
-    lsum = lsum * alpha + ps;
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      o[mt] *= alpha;
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-        o[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(vcur[mt][s]), as_bf16x8(pb[s]), o[mt], 0, 0, 0);
+  for (int ib = ib0; ib < nblk; ib += 2 * NW) {
+    dec_block<D>(A, qf, a.scale_log2, m, lsum, o);
+    if (ib + 2 * NW < nblk) dec_load<D>(kb, vtb, vrow, a.ld_vt, 32 * (ib + 2 * NW), kend, qi, h, A);
+    if (ib + NW < nblk) {
+      dec_block<D>(Bn, qf, a.scale_log2, m, lsum, o);
+      if (ib + 3 * NW < nblk) dec_load<D>(kb, vtb, vrow, a.ld_vt, 32 * (ib + 3 * NW), kend, qi, h, Bn);
     }
   }
   // merge the 4 waves' states per query column (head) in a fixed order
@@ -806,6 +832,86 @@ __global__ __launch_bounds__(64 * NW) void decode_mfma_kernel(DecodeArgs a) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) s_o[w][mt][r][lane] = o[mt][r];
   __syncthreads();
+  if (S > 1) {
+    // this split's state -> write-through slab; the last of the S splits merges them in split order
+    float* slab = a.slabs + (bh * S + y) * (64 + 32 * D);
+    if (w == 0) {
+      if (h == 0) {
+        float mm = -INFINITY;
+#pragma unroll
+        for (int v = 0; v < NW; ++v) mm = fmaxf(mm, s_m[v][qi]);
+        const float mref = mm == -INFINITY ? 0.f : mm;
+        float ll = 0.f;
+#pragma unroll
+        for (int v = 0; v < NW; ++v) ll += s_l[v][qi] * __builtin_amdgcn_exp2f(s_m[v][qi] - mref);
+        store_f32_sc1(slab + qi, mm);
+        store_f32_sc1(slab + 32 + qi, ll);
+      }
+      float mm = -INFINITY;
+#pragma unroll
+      for (int v = 0; v < NW; ++v) mm = fmaxf(mm, s_m[v][qi]);
+      const float mref = mm == -INFINITY ? 0.f : mm;
+      float sc[NW];
+#pragma unroll
+      for (int v = 0; v < NW; ++v) sc[v] = __builtin_amdgcn_exp2f(s_m[v][qi] - mref);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float acc = 0.f;
+#pragma unroll
+          for (int v = 0; v < NW; ++v) acc = fmaf(s_o[v][mt][r][lane], sc[v], acc);
+          store_f32_sc1(slab + 64 + (mt * 16 + r) * 64 + lane, acc);  // (row r of tile mt, lane) as held
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    __shared__ int s_last;
+    if (tid == 0) {
+      const unsigned t = __hip_atomic_fetch_add((__attribute__((address_space(1))) unsigned*)(a.tickets + bh), 1u,
+                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_last = t == static_cast<unsigned>(S - 1);
+    }
+    __syncthreads();
+    if (!s_last || w != 0) return;
+    const float* base = a.slabs + bh * S * (64 + 32 * D);
+    float mm = -INFINITY;
+    for (int v = 0; v < S; ++v) mm = fmaxf(mm, load_f32_sc1(base + v * (64 + 32 * D) + qi));
+    const float mref = mm == -INFINITY ? 0.f : mm;
+    float ll = 0.f;
+    for (int v = 0; v < S; ++v) {
+      const float* sl = base + v * (64 + 32 * D);
+      ll += load_f32_sc1(sl + 32 + qi) * __builtin_amdgcn_exp2f(load_f32_sc1(sl + qi) - mref);
+    }
+    const float inv = ll > 0.f ? 1.f / ll : 0.f;
+    float acc[MT][16];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[mt][r] = 0.f;
+    for (int v = 0; v < S; ++v) {
+      const float* sl = base + v * (64 + 32 * D);
+      const float sc = __builtin_amdgcn_exp2f(load_f32_sc1(sl + qi) - mref);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[mt][r] = fmaf(load_f32_sc1(sl + 64 + (mt * 16 + r) * 64 + lane), sc, acc[mt][r]);
+    }
+    if (tid == 0) __hip_atomic_store((__attribute__((address_space(1))) unsigned*)(a.tickets + bh), 0u,
+                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (qi >= a.G) return;
+    uint16_t* orow = a.out + (bh * a.G + qi) * D;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        u16x4 wv;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) wv[j] = to_bf16_bits(acc[mt][4 * c + j] * inv);
+        *reinterpret_cast<u16x4*>(orow + 32 * mt + 8 * c + 4 * h) = wv;
+      }
+    return;
+  }
   if (w != 0 || qi >= a.G) return;
   float mm = -INFINITY;
 #pragma unroll
@@ -837,6 +943,21 @@ __global__ __launch_bounds__(64 * NW) void decode_mfma_kernel(DecodeArgs a) {
 }
 
 }  // namespace
+
+int g_dec_nw = 0, g_dec_splits = 0;  // tuning override (drl_decode_attention_set_plan), 0 = automatic
+
+// key splits for decode attention. Measured (tools/kernel_bench.py --only decode_sweep, B 64..512,
+// L 513..768): a split never beat one workgroup per (sequence, KV head) with 8 waves — the slab hand-off
+// costs more than the extra CUs give back at these cache lengths — so splits are only used when a long
+// cache leaves the grid short of the chip (more than 64 key blocks per wave group of 8).
+int decode_splits(int64_t B, int64_t Hkv, int64_t L) {
+  if (g_dec_splits) return g_dec_splits;
+  const int64_t wgs = B * Hkv, cus = cu_count();
+  int s = 1;
+  while (s < 8 && wgs * s * 2 <= cus && L / (32 * 8 * 2 * s) >= 8) s *= 2;
+  return s;
+}
+
 }  // namespace drl
 
 extern "C" {
@@ -894,10 +1015,22 @@ int drl_flash_attn_bwd(const void* q, const void* k, const void* kt, const void*
   return DRL_OK;
 }
 
+void drl_decode_attention_set_plan(int32_t waves, int32_t splits) {
+  drl::g_dec_nw = (waves == 2 || waves == 4 || waves == 8 || waves == 16) ? waves : 0;
+  drl::g_dec_splits = (splits >= 1 && splits <= 16) ? splits : 0;
+}
+
+size_t drl_decode_attention_vt_workspace_bytes(int64_t B, int64_t Hkv, int64_t D, int64_t L) {
+  const int splits = drl::decode_splits(B, Hkv, L);
+  if (splits == 1) return 0;
+  return drl::round_up(static_cast<size_t>(B * Hkv) * sizeof(unsigned), 256) +
+         static_cast<size_t>(B * Hkv) * splits * (64 + 32 * D) * sizeof(float);
+}
+
 int drl_decode_attention_vt(const void* q, const void* k_cache, const void* vt_cache, int32_t dt,
                             const uint8_t* key_valid, int64_t ld_valid, const int64_t* qpos_ptr, int64_t qpos,
                             int64_t B, int64_t Hkv, int64_t G, int64_t D, int64_t ld_k, int64_t ld_vt, int64_t L,
-                            float scale, void* out, void* stream) {
+                            float scale, void* out, void* workspace, size_t workspace_bytes, void* stream) {
   using namespace drl;
   DRL_CHECK_ARG(q && k_cache && vt_cache && key_valid && out, "NULL input");
   DRL_CHECK_ARG(dt == DRL_BF16, "MFMA decode attention runs on bf16");
@@ -911,21 +1044,29 @@ int drl_decode_attention_vt(const void* q, const void* k_cache, const void* vt_c
                 "misaligned operand");
   DecodeArgs a{static_cast<const uint16_t*>(q), static_cast<const uint16_t*>(k_cache),
                static_cast<const uint16_t*>(vt_cache), key_valid, ld_valid, qpos_ptr, qpos, Hkv, G, ld_k, ld_vt, L,
-               scale * 1.4426950408889634f, static_cast<uint16_t*>(out)};
+               scale * 1.4426950408889634f, static_cast<uint16_t*>(out), nullptr, nullptr};
   hipStream_t s = static_cast<hipStream_t>(stream);
-  // waves per (sequence, KV head): 2 when the grid alone fills the chip (B=512: 37.9 vs 39.1 us at 4 waves,
-  // tools/kernel_bench.py --only decode), more to spread the keys of small decode batches
   const int64_t wgs = B * Hkv, cus = cu_count();
-  const int nw = wgs >= 4 * cus ? 2 : (wgs >= cus ? 4 : 8);
-#define DRL_DEC(DD, NN) hipLaunchKernelGGL((decode_mfma_kernel<DD, NN>), dim3(B * Hkv), dim3(64 * NN), 0, s, a)
+  const int splits = decode_splits(B, Hkv, L);
+  // waves per workgroup (same sweep): 8 while the grid is below the chip, 4 up to 4 workgroups per CU,
+  // then 2 for short caches
+  const int nw = g_dec_nw ? g_dec_nw : (wgs < cus ? 8 : (wgs < 4 * cus || L > 640 ? 4 : 2));
+  if (splits > 1) {
+    const size_t need = drl_decode_attention_vt_workspace_bytes(B, Hkv, D, L);
+    if (!workspace || workspace_bytes < need || (reinterpret_cast<uintptr_t>(workspace) & 255u))
+      return fail(DRL_ERR_WORKSPACE, "decode attention workspace: need %zu bytes, 256-byte aligned, zeroed", need);
+    a.tickets = static_cast<unsigned*>(workspace);
+    a.slabs = reinterpret_cast<float*>(static_cast<char*>(workspace) + round_up(static_cast<size_t>(wgs) * sizeof(unsigned), 256));
+  }
+#define DRL_DEC(DD, NN) hipLaunchKernelGGL((decode_mfma_kernel<DD, NN>), dim3(B * Hkv, splits), dim3(64 * NN), 0, s, a)
   if (D == 64) {
     if (nw == 2) DRL_DEC(64, 2);
     else if (nw == 4) DRL_DEC(64, 4);
-    else DRL_DEC(64, 8);
+    else if (nw == 8) DRL_DEC(64, 8);
+    else DRL_DEC(64, 16);
   } else {
     if (nw == 2) DRL_DEC(128, 2);
-    else if (nw == 4) DRL_DEC(128, 4);
-    else DRL_DEC(128, 8);
+    else DRL_DEC(128, 4);  // D=128 at 8+ waves would spill
   }
 #undef DRL_DEC
   DRL_LAUNCH_CHECK();

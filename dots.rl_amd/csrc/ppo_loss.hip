@@ -8,7 +8,8 @@
 // (8 B/token for int64), writes it back as a 1-bit image (N/8 bytes, one 64-bit ballot per wave and
 // element slot) and folds the count (fixed order, last workgroup); K1b reads that count, the other inputs and the
 // bit image (1/8 B/token instead of 8) and writes the gradients: 36.25 B/token of traffic for 36 B/token
-// of algorithmic bytes, no grid barrier. The other modes know their gradient weights up front
+// of algorithmic bytes, no grid barrier. A caller that already holds sum(mask) (params.token_count) skips
+// K1a: K1b then reads the mask itself and the whole fwd+bwd is one streaming pass. The other modes know their gradient weights up front
 // (seq-mean-token-mean gets per-row counts from a small pre-pass) and run K1b alone. Forward scalars:
 // per-workgroup partials (double) reduced by the last workgroup in a fixed order, so the results are
 // bitwise reproducible run to run.
@@ -22,6 +23,9 @@ constexpr int kChunk = kThreads * 4;  // 1024 tokens: one workgroup iteration, 1
 constexpr int kNumPartials = 8;
 #ifndef DRL_K1_PACK_U
 #define DRL_K1_PACK_U 4
+#endif
+#ifndef DRL_K1_PREFETCH
+#define DRL_K1_PREFETCH 0
 #endif
 
 // every K1 byte is touched once: nontemporal (streaming) loads and stores keep it out of the caches'
@@ -51,6 +55,7 @@ struct Args {
   const float* ref;
   const float* rowcnt;               // seq-mean-token-mean: sum(mask) per row
   const unsigned long long* bits;    // token-mean: packed mask (nullptr: read `mask`)
+  const double* token_count;         // token-mean: caller-provided sum(mask) (one-pass form), or nullptr
   float* dlp;
   float* dent;
   float* out;
@@ -194,9 +199,14 @@ __global__ __launch_bounds__(kThreads) void mask_pack_kernel(const void* mask, i
 
 // K1b: per-token loss terms, gradients and the workgroup's partial sums. One contiguous run of
 // 1024-token chunks per workgroup; 4 tokens per lane per chunk.
-template <int MDT>
+// FMODE / FKL: the aggregation mode and KL type fixed at compile time for the hot configurations
+// (kRuntime = read from Args), so the per-token math carries no mode branches.
+constexpr int kRuntime = -2;
+template <int MDT, int FMODE, int FKL>
 __global__ __launch_bounds__(kThreads) void ppo_loss_kernel(Args a) {
   __shared__ double red[kThreads / kWave][kNumPartials];
+  const int mode = FMODE != kRuntime ? FMODE : a.mode;
+  const int kl = FKL != kRuntime ? FKL : a.kl;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t N = a.N;
   const int64_t nchunks = (N + kChunk - 1) / kChunk;
@@ -205,7 +215,9 @@ __global__ __launch_bounds__(kThreads) void ppo_loss_kernel(Args a) {
 
   float cnt_total = 0.f;
   bool use_bits = false;
-  if (a.mode == DRL_AGG_TOKEN_MEAN && a.bits != nullptr) {
+  if (mode == DRL_AGG_TOKEN_MEAN && a.token_count != nullptr) {
+    cnt_total = static_cast<float>(*a.token_count);  // one-pass form: the caller's count, mask read here
+  } else if (mode == DRL_AGG_TOKEN_MEAN && a.bits != nullptr) {
     // global mask count, folded by the pack kernel's last workgroup
     cnt_total = static_cast<float>(a.hdr->mask_total);
     use_bits = a.hdr->nonbinary == 0;
@@ -213,43 +225,47 @@ __global__ __launch_bounds__(kThreads) void ppo_loss_kernel(Args a) {
   const float denom_tm = cnt_total + 1e-8f;       // masked_mean: sum / (mask.sum() + 1e-8)
   const float inv_denom_tm = 1.0f / denom_tm;     // upstream / D once, then * mask (MeanBackward style)
   const float inv_B = 1.0f / static_cast<float>(a.B), inv_R = 1.0f / static_cast<float>(a.R);
-  const bool has_ent = a.ent != nullptr, has_kl = a.kl != DRL_KL_NONE;
+  const bool has_ent = a.ent != nullptr, has_kl = kl != DRL_KL_NONE;
   const bool want_dlp = a.dlp != nullptr, want_dent = a.dent != nullptr;
-  const bool tm = a.mode == DRL_AGG_TOKEN_MEAN, smtm = a.mode == DRL_AGG_SEQ_MEAN_TOKEN_MEAN;
+  const bool tm = mode == DRL_AGG_TOKEN_MEAN, smtm = mode == DRL_AGG_SEQ_MEAN_TOKEN_MEAN;
   float s_pg = 0.f, s_clip = 0.f, s_kl = 0.f, s_cliplow = 0.f, s_ent = 0.f, s_kld = 0.f, s_cnt = 0.f;
 
-  // kU chunks per iteration: every load of the kU chunks is issued before any of their math, so each
-  // wave keeps kU x (5 x 16 B) per lane in flight
-  constexpr int kU = 1;
-  for (int64_t c0 = c_begin; c0 < c_end; c0 += kU) {
-    float mu[kU][4], oldu[kU][4], lpu[kU][4], Au[kU][4], enu[kU][4], rfu[kU][4];
+  // software pipeline: chunk c+1's loads are issued before chunk c's math (DRL_K1_PREFETCH), so every wave
+  // keeps 5-6 x 16 B per lane in flight while it computes
+  struct Chunk {
+    float m[4], old[4], lp[4], A[4], en[4], rf[4];
+  };
+  auto load_chunk = [&](int64_t c, Chunk& k) {
+    const int64_t t = c * kChunk + tid * 4;
+    const int64_t tt = c < c_end ? t : N;  // past the run: every load4 takes its bounds path and yields 0
+    if (use_bits && c < c_end) {
 #pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const int64_t c = c0 + u;
-      const int64_t t = c * kChunk + tid * 4;
-      const int64_t tt = c < c_end ? t : N;  // past the run: every load4 takes its bounds path and yields 0
-      if (use_bits && c < c_end) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) mu[u][j] = ((a.bits[c * 16 + wave * 4 + j] >> lane) & 1ull) ? 1.f : 0.f;
-      } else {
-        load_mask4<MDT>(a.mask, tt, N, mu[u]);
-      }
-      load4(a.old_lp, tt, N, oldu[u]);
-      load4(a.lp, tt, N, lpu[u]);
-      load4(a.adv, tt, N, Au[u]);
-      if (has_ent) load4(a.ent, tt, N, enu[u]);
-      if (has_kl) load4(a.ref, tt, N, rfu[u]);
+      for (int j = 0; j < 4; ++j) k.m[j] = ((a.bits[c * 16 + wave * 4 + j] >> lane) & 1ull) ? 1.f : 0.f;
+    } else {
+      load_mask4<MDT>(a.mask, tt, N, k.m);
     }
-#pragma unroll
-  for (int u = 0; u < kU; ++u) {
-    if (c0 + u >= c_end) break;
-    const int64_t t = (c0 + u) * kChunk + tid * 4;
-    float* m = mu[u];
-    float* old = oldu[u];
-    float* lp = lpu[u];
-    float* A = Au[u];
-    float* en = enu[u];
-    float* rf = rfu[u];
+    load4(a.old_lp, tt, N, k.old);
+    load4(a.lp, tt, N, k.lp);
+    load4(a.adv, tt, N, k.A);
+    if (has_ent) load4(a.ent, tt, N, k.en);
+    if (has_kl) load4(a.ref, tt, N, k.rf);
+  };
+  Chunk cur;
+#if DRL_K1_PREFETCH
+  Chunk nxt;
+#endif
+  if (c_begin < c_end) load_chunk(c_begin, cur);
+  for (int64_t c0 = c_begin; c0 < c_end; ++c0) {
+#if DRL_K1_PREFETCH
+    if (c0 + 1 < c_end) load_chunk(c0 + 1, nxt);
+#endif
+    const int64_t t = c0 * kChunk + tid * 4;
+    float* m = cur.m;
+    float* old = cur.old;
+    float* lp = cur.lp;
+    float* A = cur.A;
+    float* en = cur.en;
+    float* rf = cur.rf;
     float g_lp[4], g_en[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -281,7 +297,7 @@ __global__ __launch_bounds__(kThreads) void ppo_loss_kernel(Args a) {
       if (smtm) rc_inv = 1.0f / a.rowcnt[valid ? (t + j) / a.R : 0];
       float w;
       if (tm) w = mb ? inv_denom_tm * mj : 0.f;
-      else if (a.mode == DRL_AGG_SEQ_MEAN_TOKEN_SUM) w = inv_B * mj;
+      else if (mode == DRL_AGG_SEQ_MEAN_TOKEN_SUM) w = inv_B * mj;
       else if (smtm) w = mj * (inv_B * rc_inv);
       else w = inv_R * mj;
       // token-mean sums where(mask, x, 0) * mask; the seq modes x * mask (core_algos.py:716-733)
@@ -300,7 +316,7 @@ __global__ __launch_bounds__(kThreads) void ppo_loss_kernel(Args a) {
       float gl = w * dpg;
       if (has_kl) {
         float kv, dk;
-        kl_term(a.kl, lp[j], rf[j], kv, dk);
+        kl_term(kl, lp[j], rf[j], kv, dk);
         if (valid) s_kld += agg_val(kv);
         gl += a.kl_coef * (w * dk);
       }
@@ -310,7 +326,11 @@ __global__ __launch_bounds__(kThreads) void ppo_loss_kernel(Args a) {
     }
     if (want_dlp) store4(a.dlp, t, N, g_lp);
     if (want_dent) store4(a.dent, t, N, g_en);
-  }
+#if DRL_K1_PREFETCH
+    cur = nxt;
+#else
+    if (c0 + 1 < c_end) load_chunk(c0 + 1, cur);
+#endif
   }
 
   // ---- workgroup partials -> the last workgroup reduces all of them in a fixed order
@@ -337,8 +357,8 @@ __global__ __launch_bounds__(kThreads) void ppo_loss_kernel(Args a) {
       const double cnt = r[6];
       const double dm = static_cast<double>(static_cast<float>(cnt) + 1e-8f);
       auto agg = [&](double s) -> double {
-        if (a.mode == DRL_AGG_TOKEN_MEAN) return s / dm;
-        if (a.mode == DRL_AGG_SEQ_MEAN_TOKEN_SUM || a.mode == DRL_AGG_SEQ_MEAN_TOKEN_MEAN) return s / static_cast<double>(a.B);
+        if (mode == DRL_AGG_TOKEN_MEAN) return s / dm;
+        if (mode == DRL_AGG_SEQ_MEAN_TOKEN_SUM || mode == DRL_AGG_SEQ_MEAN_TOKEN_MEAN) return s / static_cast<double>(a.B);
         return s / static_cast<double>(a.R);
       };
       const double pg_loss = agg(r[0]);
@@ -403,7 +423,7 @@ int launch(Args a, const Layout& L, char* ws, hipStream_t s) {
     DRL_LAUNCH_CHECK();
   }
   const int64_t nchunks = (a.N + kChunk - 1) / kChunk;
-  if (a.mode == DRL_AGG_TOKEN_MEAN && (a.dlp != nullptr || a.dent != nullptr)) {
+  if (a.mode == DRL_AGG_TOKEN_MEAN && (a.dlp != nullptr || a.dent != nullptr) && a.token_count == nullptr) {
     auto* bits = reinterpret_cast<unsigned long long*>(ws + L.bits);
     auto* counts = reinterpret_cast<double*>(ws + L.counts);
     const int g1 = static_cast<int>(std::min<int64_t>(static_cast<int64_t>(cu_count()) * DRL_K1_PACK_WG_PER_CU,
@@ -415,7 +435,12 @@ int launch(Args a, const Layout& L, char* ws, hipStream_t s) {
   // >= 2 chunks per workgroup before the grid reaches 4 workgroups per CU
   const int grid = static_cast<int>(std::max<int64_t>(
       1, std::min<int64_t>(static_cast<int64_t>(cu_count()) * DRL_K1_WG_PER_CU, (nchunks + 1) / 2)));
-  hipLaunchKernelGGL(ppo_loss_kernel<MDT>, dim3(grid), dim3(kThreads), 0, s, a);
+  if (a.mode == DRL_AGG_TOKEN_MEAN && a.kl == DRL_KL_K3)
+    hipLaunchKernelGGL((ppo_loss_kernel<MDT, DRL_AGG_TOKEN_MEAN, DRL_KL_K3>), dim3(grid), dim3(kThreads), 0, s, a);
+  else if (a.mode == DRL_AGG_TOKEN_MEAN && a.kl == DRL_KL_NONE)
+    hipLaunchKernelGGL((ppo_loss_kernel<MDT, DRL_AGG_TOKEN_MEAN, DRL_KL_NONE>), dim3(grid), dim3(kThreads), 0, s, a);
+  else
+    hipLaunchKernelGGL((ppo_loss_kernel<MDT, kRuntime, kRuntime>), dim3(grid), dim3(kThreads), 0, s, a);
   DRL_LAUNCH_CHECK();
   return DRL_OK;
 }
@@ -526,6 +551,7 @@ int drl_ppo_loss_fwd_bwd(const float* old_log_prob, const float* log_prob, const
   a.hi = static_cast<float>(1.0 + static_cast<double>(p->clip_ratio_high));
   a.clip_c = p->clip_ratio_c; a.ent_coef = p->entropy_coeff; a.kl_coef = p->kl_loss_coef;
   a.lsf = p->loss_scale_factor; a.mode = p->loss_agg_mode; a.kl = p->kl_type;
+  a.token_count = p->loss_agg_mode == DRL_AGG_TOKEN_MEAN ? p->token_count : nullptr;
 
   hipStream_t s = static_cast<hipStream_t>(stream);
   DRL_HIP(hipMemsetAsync(ws, 0, sizeof(Header), s));

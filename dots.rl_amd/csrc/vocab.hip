@@ -232,15 +232,9 @@ __global__ __launch_bounds__(kThreads) void logprob_bwd_kernel(const void* logit
 }
 
 // ------------------------------------------------------------------------------------------------ K4
-__device__ __forceinline__ bool argmax_better(float v, int64_t i, float bv, int64_t bi) {
-  // torch.argmax: NaN is the maximum; ties -> first index
-  const bool vn = isnan(v), bn = isnan(bv);
-  if (vn != bn) return vn;
-  if (vn) return i < bi;
-  return v > bv || (v == bv && i < bi);
-}
 
-__device__ __forceinline__ uint32_t philox_u32(uint64_t seed, uint64_t offset, uint64_t counter) {
+// Philox4x32-10 block (seed = key, counter (c0,c1) | offset (c2,c3)); four 32-bit outputs
+__device__ __forceinline__ uint4 philox4(uint64_t seed, uint64_t offset, uint64_t counter) {
   uint32_t c0 = static_cast<uint32_t>(counter), c1 = static_cast<uint32_t>(counter >> 32);
   uint32_t c2 = static_cast<uint32_t>(offset), c3 = static_cast<uint32_t>(offset >> 32);
   uint32_t k0 = static_cast<uint32_t>(seed), k1 = static_cast<uint32_t>(seed >> 32);
@@ -256,12 +250,31 @@ __device__ __forceinline__ uint32_t philox_u32(uint64_t seed, uint64_t offset, u
     k0 += 0x9E3779B9u;
     k1 += 0xBB67AE85u;
   }
-  return c0;
+  return make_uint4(c0, c1, c2, c3);
 }
+
+// Sampling as a race of exponential clocks (the Gumbel-max form of the categorical draw): token i wins
+// iff z_i - log(E_i) is the row maximum, E_i = -log(1 - v_i) ~ Exp(1) with v_i a 24-bit Philox uniform
+// in (0, 1). Exactly softmax(z)-distributed, and a single max-reduction: the row splits across
+// workgroups with no scan (the inverse CDF needs a prefix sum over the whole vocabulary).
+__device__ __forceinline__ float race_key(float z, uint32_t bits) {
+  const float v = (static_cast<float>(bits >> 8) + 0.5f) * (1.0f / 16777216.0f);
+  return z - logf(-log1pf(-v));
+}
+
+// (key, index) -> one u64 whose unsigned max is torch.argmax: order-preserving key bits (NaN = maximum)
+// in the high word, ~index in the low word (ties -> lowest index)
+__device__ __forceinline__ uint64_t pack_key(float key, int64_t idx) {
+  uint32_t b = __float_as_uint(key);
+  b = isnan(key) ? 0xFFFFFFFFu : ((b & 0x80000000u) ? ~b : (b | 0x80000000u));
+  return (static_cast<uint64_t>(b) << 32) | (0xFFFFFFFFu - static_cast<uint32_t>(idx));
+}
+
+__device__ __forceinline__ uint64_t max_u64(uint64_t a, uint64_t b) { return a > b ? a : b; }
 
 struct SelectArgs {
   const void* logits;
-  int64_t V, ld, ld_out;
+  int64_t V, ld, ld_out, chunk;  // chunk: elements per workgroup slice (multiple of 8)
   bool vec;
   int do_sample;
   float temp;
@@ -272,147 +285,87 @@ struct SelectArgs {
   int32_t* unfinished;
   int64_t* out;
   const int64_t* dev_step;
+  unsigned long long* best;  // (N) running max per row; zero on entry, reset to zero by the finish kernel
 };
 
-template <int DT>
-__global__ __launch_bounds__(kThreads) void select_kernel(SelectArgs a) {
-  const int64_t r = blockIdx.x;
-  const void* row = static_cast<const typename Elem<DT>::T*>(a.logits) + r * a.ld;
+// Slice s of row r: best packed key over [s*chunk, (s+1)*chunk), merged into best[r] with one atomic max.
+template <int DT, bool SAMPLE>
+__global__ __launch_bounds__(kThreads) void select_slice_kernel(SelectArgs a) {
+  const int64_t r = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  __shared__ float s_val[kThreads / kWave];
-  __shared__ int64_t s_idx[kThreads / kWave];
-  __shared__ double s_scan[kThreads / kWave];
-  __shared__ int64_t s_choice;
-  int64_t choice = 0;
-  if (!a.do_sample) {
-    float bv = -INFINITY;
-    int64_t bi = INT64_MAX;
-    int64_t done = 0;
-    if (a.vec) {
-      constexpr int kV = Elem<DT>::kVec;
-      const int64_t nfull = a.V / kV;
-      const int64_t nsteps = nfull / (kThreads * kUnroll);
-      for (int64_t st = 0; st < nsteps; ++st) {
-        float v[kUnroll][kV];
-#pragma unroll
-        for (int u = 0; u < kUnroll; ++u) Elem<DT>::load_vec(row, ((st * kUnroll + u) * kThreads + tid) * kV, v[u]);
-#pragma unroll
-        for (int u = 0; u < kUnroll; ++u) {
-          const int64_t base = ((st * kUnroll + u) * kThreads + tid) * kV;
-#pragma unroll
-          for (int k = 0; k < kV; ++k)
-            if (argmax_better(v[u][k], base + k, bv, bi)) { bv = v[u][k]; bi = base + k; }
-        }
+  const void* row = static_cast<const typename Elem<DT>::T*>(a.logits) + r * a.ld;
+  const int64_t begin = static_cast<int64_t>(blockIdx.x) * a.chunk;
+  const int64_t end = begin + a.chunk < a.V ? begin + a.chunk : a.V;
+  const uint64_t off = a.offset + (a.dev_step ? static_cast<uint64_t>(*a.dev_step) : 0ull);
+  const uint64_t ctr_row = static_cast<uint64_t>(a.row_base + r) << 32;
+  auto key_of = [&](float x, uint32_t bits) -> float {
+    if constexpr (SAMPLE) return race_key(scale_logit<DT>(x, a.temp, true, false), bits);
+    else return x;
+  };
+  uint64_t best = 0;
+  int64_t done = begin;
+  if (a.vec) {
+    // 8 consecutive elements per lane per step (one 16-B bf16 load / two fp32 loads, two Philox blocks)
+    const int64_t vend = begin + (end - begin) / 8 * 8;
+    for (int64_t i = begin + 8 * tid; i < vend; i += 8 * kThreads) {
+      float v[8];
+      if constexpr (DT == DRL_BF16) {
+        Elem<DT>::load_vec(row, i, v);
+      } else {
+        Elem<DT>::load_vec(row, i, v);
+        Elem<DT>::load_vec(row, i + 4, v + 4);
       }
-      for (int64_t c = nsteps * kUnroll * kThreads + tid; c < nfull; c += kThreads) {
-        float v[kV];
-        Elem<DT>::load_vec(row, c * kV, v);
-#pragma unroll
-        for (int k = 0; k < kV; ++k)
-          if (argmax_better(v[k], c * kV + k, bv, bi)) { bv = v[k]; bi = c * kV + k; }
+      uint32_t bits[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      if constexpr (SAMPLE) {
+        const uint4 p0 = philox4(a.seed, off, ctr_row | static_cast<uint64_t>(i >> 2));
+        const uint4 p1 = philox4(a.seed, off, ctr_row | static_cast<uint64_t>((i >> 2) + 1));
+        bits[0] = p0.x; bits[1] = p0.y; bits[2] = p0.z; bits[3] = p0.w;
+        bits[4] = p1.x; bits[5] = p1.y; bits[6] = p1.z; bits[7] = p1.w;
       }
-      done = nfull * kV;
-    }
-    for (int64_t i = done + tid; i < a.V; i += kThreads) {
-      const float v = Elem<DT>::get(row, i);
-      if (argmax_better(v, i, bv, bi)) { bv = v; bi = i; }
-    }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const float v2 = __shfl_xor(bv, o, kWave);
-      const int64_t i2 = __shfl_xor(bi, o, kWave);
-      if (argmax_better(v2, i2, bv, bi)) { bv = v2; bi = i2; }
+      for (int k = 0; k < 8; ++k) best = max_u64(best, pack_key(key_of(v[k], bits[k]), i + k));
     }
-    if (lane == 0) { s_val[wave] = bv; s_idx[wave] = bi; }
-    __syncthreads();
-    if (tid == 0) {
-      for (int w = 1; w < kThreads / kWave; ++w)
-        if (argmax_better(s_val[w], s_idx[w], bv, bi)) { bv = s_val[w]; bi = s_idx[w]; }
-      s_choice = bi;
-    }
-    __syncthreads();
-    choice = s_choice;
-  } else {
-    // pass 1: max of z = logit / T (HF TemperatureLogitsWarper on fp32 scores)
-    float m, sdummy, tdummy;
-    row_softmax_state<DT, false, false>(row, a.V, a.vec, a.temp, true, m, sdummy, tdummy);
-    const uint64_t off = a.offset + (a.dev_step ? static_cast<uint64_t>(*a.dev_step) : 0ull);
-    const uint32_t bits = philox_u32(a.seed, off, static_cast<uint64_t>(a.row_base + r));
-    const double u = (static_cast<double>(bits >> 8) + 0.5) * (1.0 / 16777216.0);
-    // pass 2/3: inverse CDF. Chunks of kThreads*8 elements, 8 contiguous per lane; every sum is taken
-    // in the same fixed order in both passes, so the scan ends exactly at the total.
-    constexpr int kE = 8;
-    const int64_t chunk = static_cast<int64_t>(kThreads) * kE;
-    auto lane_sum = [&](int64_t base, double e[kE]) -> double {
-      double acc = 0.0;
-#pragma unroll
-      for (int k = 0; k < kE; ++k) {
-        const int64_t i = base + tid * kE + k;
-        e[k] = i < a.V ? static_cast<double>(expf(scale_logit<DT>(Elem<DT>::get(row, i), a.temp, true, false) - m)) : 0.0;
-        acc += e[k];
-      }
-      return acc;
-    };
-    auto block_sum = [&](double v) -> double {
-      v = wave_sum(v);
-      if (lane == 0) s_scan[wave] = v;
-      __syncthreads();
-      const double tot = s_scan[0] + s_scan[1] + s_scan[2] + s_scan[3];
-      __syncthreads();
-      return tot;
-    };
-    double total = 0.0;
-    for (int64_t base = 0; base < a.V; base += chunk) {
-      double e[kE];
-      total += block_sum(lane_sum(base, e));
-    }
-    const double target = u * total;
-    if (tid == 0) s_choice = -1;
-    __syncthreads();
-    double running = 0.0;
-    for (int64_t base = 0; base < a.V; base += chunk) {
-      double e[kE];
-      const double mine = lane_sum(base, e);
-      const double ct = block_sum(mine);
-      if (running + ct > target || base + chunk >= a.V) {
-        // exclusive scan of the lane sums (wave inclusive scan + wave offsets)
-        double inc = mine;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-          const double x = __shfl_up(inc, o, kWave);
-          if (lane >= o) inc += x;
-        }
-        if (lane == 63) s_scan[wave] = inc;
-        __syncthreads();
-        double woff = 0.0;
-        for (int w = 0; w < wave; ++w) woff += s_scan[w];
-        double c = running + woff + inc - mine;
-#pragma unroll
-        for (int k = 0; k < kE; ++k) {
-          const int64_t i = base + tid * kE + k;
-          const double nc = c + e[k];
-          if (i < a.V && e[k] > 0.0 && c <= target && nc > target) s_choice = i;  // unique crossing
-          c = nc;
-        }
-        __syncthreads();
-        break;
-      }
-      running += ct;
-    }
-    __syncthreads();
-    choice = s_choice;
-    if (choice < 0) {  // target beyond the last crossing through rounding: last non-zero-mass token
-      choice = a.V - 1;
-    }
+    done = vend;
   }
-  if (tid == 0) {
-    const bool alive = a.unfinished ? a.unfinished[r] != 0 : true;
-    const int64_t tok = alive ? choice : a.pad;
-    a.out[r * a.ld_out + (a.dev_step ? *a.dev_step : 0)] = tok;
-    if (a.unfinished && alive) {
-      for (int k = 0; k < a.n_eos; ++k)
-        if (tok == a.eos[k]) { a.unfinished[r] = 0; break; }
+  for (int64_t i = done + tid; i < end; i += kThreads) {
+    uint32_t bits = 0;
+    if constexpr (SAMPLE) {
+      const uint4 p = philox4(a.seed, off, ctr_row | static_cast<uint64_t>(i >> 2));
+      const uint32_t w[4] = {p.x, p.y, p.z, p.w};
+      bits = w[i & 3];
     }
+    best = max_u64(best, pack_key(key_of(Elem<DT>::get(row, i), bits), i));
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint64_t other = (static_cast<uint64_t>(__shfl_xor(static_cast<uint32_t>(best >> 32), o, kWave)) << 32) |
+                           __shfl_xor(static_cast<uint32_t>(best), o, kWave);
+    best = max_u64(best, other);
+  }
+  __shared__ uint64_t s_best[kThreads / kWave];
+  if (lane == 0) s_best[wave] = best;
+  __syncthreads();
+  if (tid == 0) {
+#pragma unroll
+    for (int w = 1; w < kThreads / kWave; ++w) best = max_u64(best, s_best[w]);
+    __hip_atomic_fetch_max(a.best + r, static_cast<unsigned long long>(best), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// One thread per row: decode the winning index, reset best[r], apply the finished-row / eos bookkeeping.
+__global__ __launch_bounds__(kThreads) void select_finish_kernel(SelectArgs a, int64_t N) {
+  const int64_t r = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
+  if (r >= N) return;
+  const uint64_t b = a.best[r];
+  a.best[r] = 0;
+  const int64_t choice = static_cast<int64_t>(0xFFFFFFFFu - static_cast<uint32_t>(b));
+  const bool alive = a.unfinished ? a.unfinished[r] != 0 : true;
+  const int64_t tok = alive ? choice : a.pad;
+  a.out[r * a.ld_out + (a.dev_step ? *a.dev_step : 0)] = tok;
+  if (a.unfinished && alive) {
+    for (int k = 0; k < a.n_eos; ++k)
+      if (tok == a.eos[k]) { a.unfinished[r] = 0; break; }
   }
 }
 
@@ -478,27 +431,47 @@ int drl_logprob_entropy_bwd(const void* logits, int32_t dt, int64_t N, int64_t V
   return DRL_OK;
 }
 
+size_t drl_select_tokens_workspace_bytes(int64_t N) { return N > 0 ? static_cast<size_t>(N) * 8 : 0; }
+
 int drl_select_tokens(const void* logits, int32_t dt, int64_t N, int64_t V, int64_t ld,
                       const drl_sampling_params* p, int32_t* unfinished, int64_t* out_tokens, int64_t ld_out,
-                      void* stream) {
+                      void* workspace, size_t workspace_bytes, void* stream) {
   using namespace drl;
   DRL_CHECK_ARG(logits && p && out_tokens, "NULL input");
-  DRL_CHECK_ARG(N >= 0 && V >= 1 && ld >= V, "bad shape");
+  DRL_CHECK_ARG(N >= 0 && V >= 1 && ld >= V && V < (int64_t(1) << 32), "bad shape");
   DRL_CHECK_ARG(dt == DRL_BF16 || dt == DRL_F32, "logits dtype must be F32 or BF16");
   DRL_CHECK_ARG(p->n_eos == 0 || p->eos_ids != nullptr, "n_eos > 0 but eos_ids is NULL");
   const bool sample = p->do_sample && p->temperature > 0.f;
   if (sample && ((p->top_k > 0 && p->top_k < V) || p->top_p < 1.0f))
     return fail(DRL_ERR_UNSUPPORTED, "top-k / top-p filtering is not implemented in this build");
   if (N == 0) return DRL_OK;
+  DRL_CHECK_ARG(N <= 65535, "too many rows for one launch");
+  if (!workspace || workspace_bytes < drl_select_tokens_workspace_bytes(N) || (reinterpret_cast<uintptr_t>(workspace) & 7u))
+    return fail(DRL_ERR_WORKSPACE, "select workspace: need %zu 8-byte aligned bytes", drl_select_tokens_workspace_bytes(N));
   SelectArgs a{};
   a.logits = logits; a.V = V; a.ld = ld; a.ld_out = ld_out; a.vec = rows_aligned(logits, ld, dt);
   a.do_sample = sample; a.temp = sample ? p->temperature : 1.0f;
   a.seed = p->seed; a.offset = p->offset; a.row_base = p->row_base; a.pad = p->pad_token_id;
   a.eos = p->eos_ids; a.n_eos = p->n_eos; a.unfinished = unfinished; a.out = out_tokens;
   a.dev_step = p->dev_step;
+  a.best = static_cast<unsigned long long*>(workspace);
+  // slices per row: ~4 workgroups per CU over the whole launch, >= 2048 elements per slice
+  const int64_t want = (4 * static_cast<int64_t>(cu_count()) + N - 1) / N;
+  const int64_t max_slices = (V + 2047) / 2048;
+  const int64_t slices = want < 1 ? 1 : (want > max_slices ? max_slices : want);
+  a.chunk = ((V + slices - 1) / slices + 7) / 8 * 8;
+  const dim3 grid(static_cast<unsigned>((V + a.chunk - 1) / a.chunk), static_cast<unsigned>(N));
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (dt == DRL_BF16) hipLaunchKernelGGL(select_kernel<DRL_BF16>, dim3(N), dim3(kThreads), 0, s, a);
-  else hipLaunchKernelGGL(select_kernel<DRL_F32>, dim3(N), dim3(kThreads), 0, s, a);
+  if (dt == DRL_BF16) {
+    if (sample) hipLaunchKernelGGL((select_slice_kernel<DRL_BF16, true>), grid, dim3(kThreads), 0, s, a);
+    else hipLaunchKernelGGL((select_slice_kernel<DRL_BF16, false>), grid, dim3(kThreads), 0, s, a);
+  } else {
+    if (sample) hipLaunchKernelGGL((select_slice_kernel<DRL_F32, true>), grid, dim3(kThreads), 0, s, a);
+    else hipLaunchKernelGGL((select_slice_kernel<DRL_F32, false>), grid, dim3(kThreads), 0, s, a);
+  }
+  DRL_LAUNCH_CHECK();
+  hipLaunchKernelGGL(select_finish_kernel, dim3(static_cast<unsigned>((N + kThreads - 1) / kThreads)), dim3(kThreads), 0,
+                     s, a, N);
   DRL_LAUNCH_CHECK();
   return DRL_OK;
 }

@@ -126,8 +126,10 @@ def mask_dtype_code(mask: torch.Tensor) -> int:
 def ppo_loss_fwd_bwd(old_log_prob, log_prob, advantages, response_mask, entropy=None, ref_log_prob=None, *,
                      clip_ratio_low=0.2, clip_ratio_high=0.2, clip_ratio_c=3.0, entropy_coeff=0.0,
                      kl_loss_coef=0.0, kl_loss_type=None, loss_agg_mode="token-mean", loss_scale_factor=1.0,
-                     want_dlogp=True, want_dentropy=False, out=None, dlogp=None, dentropy=None):
-    """One launch: the 8 loss scalars (see DRL_PPO_OUT_*) and d loss / d log_prob, d loss / d entropy."""
+                     want_dlogp=True, want_dentropy=False, out=None, dlogp=None, dentropy=None, token_count=None):
+    """One launch: the 8 loss scalars (see DRL_PPO_OUT_*) and d loss / d log_prob, d loss / d entropy.
+    ``token_count`` (token-mean): device float64 scalar = response_mask.sum() when the caller already has
+    it; K1 then makes one pass over HBM instead of two."""
     _dev(old_log_prob, log_prob, advantages, response_mask, entropy, ref_log_prob)
     old_log_prob, log_prob, advantages = _c(old_log_prob.float()), _c(log_prob.float()), _c(advantages.float())
     response_mask = _c(response_mask)
@@ -136,7 +138,11 @@ def ppo_loss_fwd_bwd(old_log_prob, log_prob, advantages, response_mask, entropy=
     B, R = log_prob.shape
     prm = _lib.PPOLossParams(clip_ratio_low, clip_ratio_high, clip_ratio_c, entropy_coeff, kl_loss_coef,
                              loss_scale_factor, _lib.AGG_MODES[loss_agg_mode],
-                             _lib.KL_NONE if kl_loss_type is None else _lib.KL_TYPES[kl_loss_type])
+                             _lib.KL_NONE if kl_loss_type is None else _lib.KL_TYPES[kl_loss_type], None)
+    if token_count is not None:
+        _dev(token_count)
+        assert token_count.dtype == torch.float64 and token_count.numel() == 1
+        prm.token_count = token_count.data_ptr()
     dev = log_prob.device
     if out is None:
         out = torch.empty(_lib.PPO_OUT_N, dtype=torch.float32, device=dev)
@@ -257,14 +263,32 @@ def select_tokens(logits, out_tokens, *, do_sample=False, temperature=1.0, top_k
     N, V = lg.shape
     assert out_tokens.dtype == torch.int64 and out_tokens.numel() == N
     ld_out = out_tokens.stride(0) if out_tokens.dim() == 1 else 1
+    ws = _select_workspace(lg.device, N)
     prm = _lib.SamplingParams(int(bool(do_sample)), float(temperature), int(top_k), float(top_p),
                               int(seed) & 0xFFFFFFFFFFFFFFFF, int(step), int(row_base), int(pad_token_id),
                               None if eos_ids is None else eos_ids.data_ptr(),
                               0 if eos_ids is None else eos_ids.numel(),
                               None if dev_step is None else dev_step.data_ptr())
     check(lib().drl_select_tokens(_p(lg), _LOGIT_DTYPES[lg.dtype], N, V, lg.stride(0), ctypes.byref(prm),
-                                  _p(unfinished), _p(out_tokens), ld_out, _stream()), "drl_select_tokens")
+                                  _p(unfinished), _p(out_tokens), ld_out, _p(ws), ws.numel() * 8, _stream()),
+          "drl_select_tokens")
     return out_tokens
+
+
+_SELECT_WS = {}
+
+
+def _select_workspace(device, N):
+    """Per-device zeroed int64 buffer (>= N rows) that the selection kernels leave zeroed after each call
+    (valid inside captured graphs: calls on one stream reuse it in order)."""
+    key = str(device)
+    ws = _SELECT_WS.get(key)
+    if ws is None or ws.numel() < N:
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("select_tokens: call once outside graph capture to size its workspace")
+        ws = torch.zeros(max(N, 1024), dtype=torch.int64, device=device)
+        _SELECT_WS[key] = ws
+    return ws
 
 
 def response_mask(responses, eos_ids, dtype=torch.int64, out=None):
@@ -434,6 +458,47 @@ def flash_attn_bwd(q, k, kt, v, o, dout, lse, key_valid, dq, dk, dv):
           "drl_flash_attn_bwd")
 
 
+LINEAR_NONE, LINEAR_BIAS, LINEAR_SWIGLU = 0, 1, 2
+
+
+def linear_decode(x, w, bias=None, swiglu=False, out=None):
+    """Decode-step linear layer (csrc/linear.hip): x (M, K) bf16 @ w (N, K)^T (+ bias) -> (M, N) bf16, or with
+    ``swiglu`` (w = [gate | up]) silu(x Wg^T) * (x Wu^T) -> (M, N/2)."""
+    _dev(x, w)
+    M, K = x.shape
+    N = w.shape[0]
+    assert x.stride(1) == 1 and w.is_contiguous() and w.shape[1] == K and x.dtype == w.dtype
+    epi = LINEAR_SWIGLU if swiglu else (LINEAR_BIAS if bias is not None else LINEAR_NONE)
+    n_out = N // 2 if swiglu else N
+    if out is None:
+        out = torch.empty(M, n_out, dtype=x.dtype, device=x.device)
+    assert out.stride(1) == 1 and out.shape == (M, n_out)
+    if bias is not None:
+        _dev(bias)
+        assert bias.is_contiguous() and bias.numel() == N
+    nws = lib().drl_linear_decode_workspace_bytes(M, N, K, epi)
+    ws = _linear_workspace(x.device, nws) if nws else None
+    check(lib().drl_linear_decode(_p(x), x.stride(0), _p(w), _p(bias), _edt(x), M, N, K, epi, _p(out), out.stride(0),
+                                  _p(ws), nws, _stream()), "drl_linear_decode")
+    return out
+
+
+_LINEAR_WS = {}
+
+
+def _linear_workspace(device, nbytes, kind="linear"):
+    """Per-device zeroed workspace shared by the split-K decode kernels of one kind on one stream (each call
+    leaves its arrival tickets zeroed again, so consecutive calls and graph replays reuse it)."""
+    key = (str(device), kind)
+    ws = _LINEAR_WS.get(key)
+    if ws is None or ws.numel() * 8 < nbytes:
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError(f"{kind}: call once outside graph capture to size its workspace")
+        ws = torch.zeros((max(nbytes, 1 << 22) + 7) // 8, dtype=torch.int64, device=device)
+        _LINEAR_WS[key] = ws
+    return ws
+
+
 def decode_attention_vt(q, k_cache, vt_cache, key_valid, L, out, qpos=None, qpos_dev=None):
     """MFMA decode attention: q (B,Hkv,G,D) bf16, k_cache (B,Hkv,ld_k,D), vt_cache (B,Hkv,D,ld_vt)."""
     _dev(q, k_cache, vt_cache, key_valid, out)
@@ -441,7 +506,9 @@ def decode_attention_vt(q, k_cache, vt_cache, key_valid, L, out, qpos=None, qpos
     assert q.is_contiguous() and k_cache.is_contiguous() and out.is_contiguous() and vt_cache.stride(-1) == 1
     assert vt_cache.stride(-2) * D == vt_cache.stride(1) and key_valid.dtype == torch.uint8
     qp = L - 1 if qpos is None else int(qpos)
+    nws = lib().drl_decode_attention_vt_workspace_bytes(B, Hkv, D, L)
+    ws = _linear_workspace(q.device, nws, "decode_attention") if nws else None
     check(lib().drl_decode_attention_vt(_p(q), _p(k_cache), _p(vt_cache), _edt(q), _p(key_valid), key_valid.stride(0),
                                         _p(qpos_dev), qp, B, Hkv, G, D, k_cache.shape[2], vt_cache.stride(-2), L,
-                                        1.0 / math.sqrt(D), _p(out), _stream()), "drl_decode_attention_vt")
+                                        1.0 / math.sqrt(D), _p(out), _p(ws), nws, _stream()), "drl_decode_attention_vt")
     return out

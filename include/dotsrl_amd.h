@@ -55,6 +55,13 @@ typedef enum drl_kl_type {
   DRL_KL_K3 = 3,    /* "low_var_kl" / "k3" */
 } drl_kl_type;
 
+/* Epilogues of drl_linear_decode */
+typedef enum drl_linear_epilogue {
+  DRL_LINEAR_NONE = 0,   /* y = x W^T */
+  DRL_LINEAR_BIAS = 1,   /* y = x W^T + bias (qkv_proj) */
+  DRL_LINEAR_SWIGLU = 2, /* W = [gate (I rows) | up (I rows)]: y (M, I) = silu(x Wg^T) * (x Wu^T) (Qwen2MLP) */
+} drl_linear_epilogue;
+
 const char* drl_last_error(void);
 int drl_abi_version(void);
 /* Number of compute units of the current device (grid sizing); <0 on error. */
@@ -78,6 +85,11 @@ typedef struct drl_ppo_loss_params {
   float loss_scale_factor; /* 1 / gradient_accumulation (dp_actor.py:415-417) */
   int32_t loss_agg_mode;   /* drl_agg_mode */
   int32_t kl_type;         /* drl_kl_type; NONE = use_kl_loss False */
+  /* optional, token-mean only: device double = sum(response_mask) of this call's tokens (e.g. the per-row
+   * counts the rollout's response-mask step already has, summed over the micro-batch). When given, K1
+   * runs as ONE pass (the mask is read once, in the loss pass) instead of the count pass + loss pass.
+   * NULL = K1 counts the mask itself. */
+  const double* token_count;
 } drl_ppo_loss_params;
 
 enum {
@@ -148,14 +160,19 @@ int drl_gae_advantage_return(const float* token_level_rewards, const float* valu
 
 /* ------------------------------------------------------------------------------------------------
  * K4 — decode-step token selection over the vocabulary (HF generate semantics that HFRollout
- * delegates to, verl/workers/rollout/hf_rollout.py:112-124). One launch per decode step.
+ * delegates to, verl/workers/rollout/hf_rollout.py:112-124). Two launches per decode step (row slices
+ * across workgroups, then one thread per row).
  * logits (N, V) F32/BF16 (row stride ld). unfinished (N) int32 in/out: rows already finished emit
  * pad_token_id (HF: next = next*unfinished + pad*(1-unfinished)) and a row hitting any eos id
  * becomes finished. The chosen token is written to out_tokens[n*ld_out] (int64) — pass a column
  * of the `responses` tensor to fill it in place. temperature <= 0 or do_sample == 0 -> greedy
- * (argmax, first index on ties = torch.argmax). Sampling: temperature, then top-k (top_k <= 0 ->
- * off), then top-p (>= 1 -> off), then the inverse CDF at a Philox4x32-10 uniform
- * (seed, offset = decode step, counter = row_base + n).
+ * (argmax, first index on ties = torch.argmax). Sampling: z = logit / temperature (fp32, HF
+ * TemperatureLogitsWarper), top-k / top-p (not implemented: DRL_ERR_UNSUPPORTED), then the categorical
+ * draw as a race of exponential clocks: argmax_i z_i - log(E_i), E_i = -log(1 - v_i), v_i the 24-bit
+ * uniform ((w >> 8) + 0.5) / 2^24 from word (i & 3) of Philox4x32-10(key = seed,
+ * counter = ((row_base + n) << 32 | i >> 2, offset = decode step)) — softmax(z)-distributed like HF's
+ * torch.multinomial. workspace: drl_select_tokens_workspace_bytes(N) bytes, 8-byte aligned, zero-filled
+ * before the first call; every call leaves it zeroed again (one in-flight call per workspace).
  * ---------------------------------------------------------------------------------------------- */
 typedef struct drl_sampling_params {
   int32_t do_sample;
@@ -173,9 +190,10 @@ typedef struct drl_sampling_params {
   const int64_t* dev_step;
 } drl_sampling_params;
 
+size_t drl_select_tokens_workspace_bytes(int64_t N);
 int drl_select_tokens(const void* logits, int32_t logits_dtype, int64_t N, int64_t V, int64_t ld,
                       const drl_sampling_params* params, int32_t* unfinished, int64_t* out_tokens,
-                      int64_t ld_out, void* stream);
+                      int64_t ld_out, void* workspace, size_t workspace_bytes, void* stream);
 
 /* ------------------------------------------------------------------------------------------------
  * Rollout bookkeeping (A4/A5).
@@ -278,11 +296,17 @@ int drl_flash_attn_fwd(const void* q, const void* k, const void* vt, int32_t dt,
 /* Decode attention on MFMA over a cache with V head-dim-major: q (B,Hkv,G,D) bf16 (one token), k_cache
  * (B,Hkv,ld_k,D), vt_cache (B,Hkv,D,ld_vt); keys j < L with key_valid[b, j] && j <= qpos (device scalar
  * *qpos_ptr when non-NULL). out (B,Hkv,G,D). G <= 32, head_dim 64 or 128. Same semantics as
- * drl_decode_attention (the VALU kernel over a row-major V cache used by the fp32 parity model). */
+ * drl_decode_attention (the VALU kernel over a row-major V cache used by the fp32 parity model).
+ * Small batches split the keys over workgroups (partial softmax states merged in split order by the last
+ * arriving split): workspace of drl_decode_attention_vt_workspace_bytes(B, Hkv, D, L) bytes (0 = none
+ * needed), 256-byte aligned, zero-filled before the first call and left zeroed by every call. */
+size_t drl_decode_attention_vt_workspace_bytes(int64_t B, int64_t Hkv, int64_t D, int64_t L);
+/* Tuning hook (tools/kernel_bench.py): force waves per workgroup (2/4/8/16) and key splits; 0 = automatic. */
+void drl_decode_attention_set_plan(int32_t waves, int32_t splits);
 int drl_decode_attention_vt(const void* q, const void* k_cache, const void* vt_cache, int32_t dt,
                             const uint8_t* key_valid, int64_t ld_valid, const int64_t* qpos_ptr, int64_t qpos,
                             int64_t B, int64_t Hkv, int64_t G, int64_t D, int64_t ld_k, int64_t ld_vt, int64_t L,
-                            float scale, void* out, void* stream);
+                            float scale, void* out, void* workspace, size_t workspace_bytes, void* stream);
 /* Backward of drl_flash_attn_fwd for Tq == Tk == T, qoff = 0 (the training forward), recomputing P from lse:
  * q (B,Hkv,G,T,D), k / v (B,Hkv,T,D) row-major, kt (B,Hkv,D,ld_t) head-dim-major copy of k (written by
  * drl_rope_qkv_fwd), o and dout (B,T,Hkv*G*D), lse from the forward. delta: (B,Hkv,G,T) fp32 scratch.
@@ -292,6 +316,20 @@ int drl_flash_attn_bwd(const void* q, const void* k, const void* kt, const void*
                        const float* lse, int32_t dt, const uint8_t* key_valid, int64_t ld_valid, int64_t B,
                        int64_t Hkv, int64_t G, int64_t D, int64_t T, int64_t ld_t, float scale, float* delta, void* dq,
                        void* dk, void* dv, void* stream);
+/* Linear layer of the decode step (M = one token per sequence, M small): y (M, N or N/2) = epilogue(x W^T).
+ * Replaces the nn.Linear calls of Qwen2Attention / Qwen2MLP / lm_head (transformers modeling_qwen2, run by
+ * hf_rollout.py:112-124 generate) at decode time. x (M, ld_x) bf16, W (N, K) bf16 row-major, bias (N) bf16,
+ * out (M, ld_out) bf16; fp32 accumulation, one rounding to bf16 after the bias (SWIGLU: gate and up rounded
+ * to bf16, silu(gate) rounded, product rounded: the bf16 module semantics). 1 <= M <= 128, K % 16 == 0,
+ * x rows and W 16-byte aligned. Deterministic (fixed-order partial sums). workspace: 256-byte aligned,
+ * drl_linear_decode_workspace_bytes(M, N, K, epilogue) bytes (0 when K is not split over workgroups),
+ * zero-filled before the first call and left zeroed by every call (one in-flight call per workspace). */
+size_t drl_linear_decode_workspace_bytes(int64_t M, int64_t N, int64_t K, int32_t epilogue);
+/* Tuning hook (tools/kernel_bench.py): force waves per workgroup (4/8/16) and the K split; 0 = automatic. */
+void drl_linear_decode_set_plan(int32_t waves, int32_t ksplit);
+int drl_linear_decode(const void* x, int64_t ld_x, const void* w, const void* bias, int32_t dt, int64_t M,
+                      int64_t N, int64_t K, int32_t epilogue, void* out, int64_t ld_out, void* workspace,
+                      size_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }

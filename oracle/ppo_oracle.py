@@ -326,27 +326,55 @@ def greedy(logits):
     return np.asarray(logits).argmax(-1).astype(np.int64)
 
 
-def philox_uniform(seed, offset, counter):
-    """Counter-based uniform in (0,1) matching the HIP sampler (Philox4x32-10, first word, 24-bit mantissa)."""
+def philox4(seed, offset, counter):
+    """Philox4x32-10 block (key = seed; counter words (c0, c1) = counter, (c2, c3) = offset) -> 4 words."""
     M0, M1, W0, W1 = 0xD2511F53, 0xCD9E8D57, 0x9E3779B9, 0xBB67AE85
-    k0, k1 = np.uint64(seed & 0xFFFFFFFF), np.uint64((seed >> 32) & 0xFFFFFFFF)
-    c = [np.uint64(counter & 0xFFFFFFFF), np.uint64((counter >> 32) & 0xFFFFFFFF),
-         np.uint64(offset & 0xFFFFFFFF), np.uint64((offset >> 32) & 0xFFFFFFFF)]
-    mask = np.uint64(0xFFFFFFFF)
+    k0, k1 = seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF
+    c = [counter & 0xFFFFFFFF, (counter >> 32) & 0xFFFFFFFF, offset & 0xFFFFFFFF, (offset >> 32) & 0xFFFFFFFF]
     for _ in range(10):
-        p0 = np.uint64(M0) * c[0]
-        p1 = np.uint64(M1) * c[2]
-        c = [((p1 >> np.uint64(32)) ^ c[1] ^ k0) & mask, p1 & mask, ((p0 >> np.uint64(32)) ^ c[3] ^ k1) & mask, p0 & mask]
-        k0 = (k0 + np.uint64(W0)) & mask
-        k1 = (k1 + np.uint64(W1)) & mask
-    return (float(int(c[0]) >> 8) + 0.5) * (1.0 / 16777216.0)
+        p0 = M0 * c[0]
+        p1 = M1 * c[2]
+        c = [((p1 >> 32) ^ c[1] ^ k0) & 0xFFFFFFFF, p1 & 0xFFFFFFFF, ((p0 >> 32) ^ c[3] ^ k1) & 0xFFFFFFFF,
+             p0 & 0xFFFFFFFF]
+        k0 = (k0 + W0) & 0xFFFFFFFF
+        k1 = (k1 + W1) & 0xFFFFFFFF
+    return c
+
+
+def philox_words(seed, offset, row, V):
+    """Word (i & 3) of block (row << 32 | i >> 2) for i < V (vectorised over the blocks)."""
+    M0, M1, W0, W1 = np.uint64(0xD2511F53), np.uint64(0xCD9E8D57), 0x9E3779B9, 0xBB67AE85
+    mask = np.uint64(0xFFFFFFFF)
+    nb = (V + 3) // 4
+    c0 = np.arange(nb, dtype=np.uint64)
+    c1 = np.full(nb, row & 0xFFFFFFFF, np.uint64)
+    c2 = np.full(nb, offset & 0xFFFFFFFF, np.uint64)
+    c3 = np.full(nb, (offset >> 32) & 0xFFFFFFFF, np.uint64)
+    k0, k1 = seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF
+    for _ in range(10):
+        p0 = M0 * c0
+        p1 = M1 * c2
+        c0, c1, c2, c3 = ((p1 >> np.uint64(32)) ^ c1 ^ np.uint64(k0)) & mask, p1 & mask, \
+            ((p0 >> np.uint64(32)) ^ c3 ^ np.uint64(k1)) & mask, p0 & mask
+        k0 = (k0 + W0) & 0xFFFFFFFF
+        k1 = (k1 + W1) & 0xFFFFFFFF
+    return np.stack([c0, c1, c2, c3], 1).reshape(-1)[:V].astype(np.uint32)
+
+
+def race_keys(z, seed, offset, row):
+    """z_i - log(E_i), E_i = -log(1 - v_i) ~ Exp(1), v_i = ((w_i >> 8) + 0.5) / 2^24 (float32 math, as the
+    HIP sampler); the argmax is a softmax(z) draw (exponential race / Gumbel-max)."""
+    w = philox_words(seed, offset, row, z.shape[0])
+    v = ((w >> np.uint32(8)).astype(np.float32) + np.float32(0.5)) * np.float32(1.0 / 16777216.0)
+    e = -np.log1p(-v)
+    return np.asarray(z, np.float32) - np.log(e)
 
 
 def sample_row(logits, temperature, top_k, top_p, seed, offset, row):
     """Reference semantics of one sampling step: temperature -> top-k -> top-p -> categorical draw.
 
-    The draw uses the inverse CDF of the filtered distribution at a Philox uniform (the HIP sampler's
-    RNG), so HIP and oracle pick the same token; HF uses torch.multinomial (same distribution)."""
+    The draw is the exponential race over the kept tokens with the HIP sampler's Philox stream
+    (race_keys), so HIP and oracle pick the same token; HF uses torch.multinomial (same distribution)."""
     z = np.asarray(logits, np.float32).astype(f64) / temperature
     V = z.shape[0]
     keep = np.ones(V, bool)
@@ -367,6 +395,6 @@ def sample_row(logits, temperature, top_k, top_p, seed, offset, row):
         keep2[order[drop]] = False
         p = np.where(keep2, p, 0.0)
         p /= p.sum()
-    u = philox_uniform(seed, offset, row)
-    cdf = np.cumsum(p)
-    return int(min(np.searchsorted(cdf, u * cdf[-1], side="right"), V - 1))
+    keys = race_keys((np.asarray(logits, np.float32) / np.float32(temperature)).astype(np.float32), seed, offset, row)
+    keys = np.where(p > 0, keys, -np.inf)
+    return int(np.argmax(keys))

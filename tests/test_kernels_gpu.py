@@ -21,15 +21,16 @@ def T(x, dtype=None):
     return t.to(dtype) if dtype is not None else t
 
 
-def run_k1(ins, cfg, mask_dtype=None, want_dent=True):
+def run_k1(ins, cfg, mask_dtype=None, want_dent=True, given_count=False):
     old, lp, adv, mask, ent, ref = ins
     m = T(mask) if mask_dtype is None else T(mask).to(mask_dtype)
+    tc = m.to(torch.float64).sum().reshape(1) if given_count else None
     out, dlp, dent = native.ppo_loss_fwd_bwd(
         T(old), T(lp), T(adv), m, T(ent), T(ref),
         clip_ratio_low=cfg["clip_ratio_low"], clip_ratio_high=cfg["clip_ratio_high"], clip_ratio_c=cfg["clip_ratio_c"],
         entropy_coeff=cfg["entropy_coeff"], kl_loss_coef=cfg["kl_loss_coef"],
         kl_loss_type=cfg["kl_loss_type"] if cfg["use_kl_loss"] else None, loss_agg_mode=cfg["loss_agg_mode"],
-        loss_scale_factor=cfg["loss_scale_factor"], want_dlogp=True, want_dentropy=want_dent)
+        loss_scale_factor=cfg["loss_scale_factor"], want_dlogp=True, want_dentropy=want_dent, token_count=tc)
     torch.cuda.synchronize()
     o = out.cpu().numpy()
     res = dict(zip(OUT_KEYS, o[:7]))
@@ -77,12 +78,15 @@ def rand_inputs(rng, B, R, hole_rows=True):
 @pytest.mark.parametrize("mode", oracle.AGG_MODES)
 @pytest.mark.parametrize("mask_dtype", [torch.int64, torch.int32, torch.uint8, torch.bool, torch.float32])
 @pytest.mark.parametrize("shape", [(3, 7), (8, 256), (37, 513), (64, 1000)])
-def test_ppo_loss_matches_oracle(mode, mask_dtype, shape):
+@pytest.mark.parametrize("given_count", [False, True])  # token-mean: count pass + loss pass, or one pass
+def test_ppo_loss_matches_oracle(mode, mask_dtype, shape, given_count):
+    if given_count and mode != "token-mean":
+        pytest.skip("token_count applies to token-mean")
     rng = np.random.default_rng(hash((mode, str(mask_dtype), shape)) % (2**32))
     ins = rand_inputs(rng, *shape)
     cfg = dict(clip_ratio_low=0.2, clip_ratio_high=0.28, clip_ratio_c=3.0, entropy_coeff=0.01, kl_loss_coef=0.001,
                kl_loss_type="low_var_kl", use_kl_loss=True, loss_agg_mode=mode, loss_scale_factor=0.25)
-    res = run_k1(ins, cfg, mask_dtype)
+    res = run_k1(ins, cfg, mask_dtype, given_count=given_count)
     ref = oracle.actor_loss(*ins, loss_agg_mode=mode, clip_ratio_low=0.2, clip_ratio_high=0.28, clip_ratio_c=3.0,
                             entropy_coeff=0.01, use_kl_loss=True, kl_loss_type="low_var_kl", kl_loss_coef=0.001,
                             loss_scale_factor=0.25)
@@ -122,6 +126,10 @@ def test_ppo_loss_deterministic_and_large():
     o1, d1, e1 = o1.clone(), d1.clone(), e1.clone()
     o2, d2, e2 = native.ppo_loss_fwd_bwd(old, lp, adv, mask, ent, ref, **kw)
     assert torch.equal(o1, o2) and torch.equal(d1, d2) and torch.equal(e1, e2)
+    # one-pass form with the caller's token count: the same bits
+    tc = mask.to(torch.float64).sum().reshape(1)
+    o3, d3, e3 = native.ppo_loss_fwd_bwd(old, lp, adv, mask, ent, ref, token_count=tc, **kw)
+    assert torch.equal(o1, o3) and torch.equal(d1, d3) and torch.equal(e1, e3)
     # plain torch fp32 reference (same formulas as core_algos.py:815-889 / dp_actor.py:419-466)
     x = lp.clone().requires_grad_(True)
     e = ent.clone().requires_grad_(True)
@@ -288,10 +296,14 @@ def test_greedy_writes_strided_column_and_handles_eos():
     assert (responses[:, [0, 1, 3]] == -7).all()
 
 
-@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
-def test_sampling_matches_oracle_inverse_cdf(dt):
+@pytest.mark.parametrize("dt,V", [(torch.float32, 151936), (torch.bfloat16, 151936), (torch.bfloat16, 1001),
+                                  (torch.float32, 77)])
+def test_sampling_matches_oracle_race(dt, V):
+    """Sampled tokens == the oracle's exponential race on the same Philox stream (rows split across
+    workgroup slices on the GPU). A row whose two best oracle keys are within float32 rounding may pick
+    either of them."""
     rng = np.random.default_rng(12)
-    N, V = 48, 151936
+    N = 48
     x = (rng.standard_normal((N, V)) * 2).astype(np.float32)
     logits = T(x).to(dt)
     xs = logits.float().cpu().numpy()
@@ -299,11 +311,44 @@ def test_sampling_matches_oracle_inverse_cdf(dt):
     seed, step, temp = 1234, 17, 0.8
     native.select_tokens(logits, out, do_sample=True, temperature=temp, seed=seed, step=step, row_base=100)
     got = out.cpu().numpy()
-    want = np.array([oracle.sample_row(xs[i], temp, 0, 1.0, seed, step, 100 + i) for i in range(N)])
-    assert (got == want).mean() >= 0.97, (got, want)  # fp32-vs-fp64 CDF rounding may move a boundary draw
-    # every draw must come from the support with non-negligible mass
-    p = np.exp(xs / temp - (xs / temp).max(-1, keepdims=True))
-    assert (p[np.arange(N), got] > 0).all()
+    for i in range(N):
+        keys = oracle.race_keys((xs[i] / np.float32(temp)).astype(np.float32), seed, step, 100 + i)
+        want = oracle.sample_row(xs[i], temp, 0, 1.0, seed, step, 100 + i)
+        if got[i] != want:
+            assert abs(keys[got[i]] - keys[want]) <= 1e-5 * max(1.0, abs(keys[want])), (i, got[i], want)
+
+
+def test_sampling_distribution():
+    """The race draw is softmax-distributed: 8192 rows of the same 6 logits, distinct Philox counters."""
+    z = torch.tensor([2.0, 1.0, 0.5, 0.0, -1.0, -30.0])
+    N = 8192
+    logits = z.repeat(N, 1).to(DEV)
+    out = torch.empty(N, dtype=torch.int64, device=DEV)
+    native.select_tokens(logits, out, do_sample=True, temperature=1.0, seed=99, step=3)
+    freq = np.bincount(out.cpu().numpy(), minlength=6) / N
+    p = torch.softmax(z, 0).numpy()
+    assert np.abs(freq - p).max() < 4 * np.sqrt(p.max() * (1 - p.max()) / N), (freq, p)
+    assert freq[5] == 0
+
+
+@pytest.mark.parametrize("V", [151936, 4099])
+def test_greedy_sliced_ties_and_nan(V):
+    """Greedy across workgroup slices keeps torch.argmax semantics: first index on ties (also across
+    slice boundaries), NaN is the maximum, -inf rows pick index 0; unaligned fp32 rows (scalar path)."""
+    N = 6
+    x = torch.randn(N, V + 1, device=DEV)[:, :V]  # row stride V+1: unaligned rows for fp32
+    x[0, V - 1] = 50.0
+    x[0, 3] = 50.0  # tie: first index wins
+    x[1, V // 2 + 1] = float("nan")
+    x[1, V - 2] = float("nan")
+    x[2] = float("-inf")
+    x[3, V - 1] = 1e30
+    out = torch.empty(N, dtype=torch.int64, device=DEV)
+    for t in (x, x.to(torch.bfloat16)):
+        native.select_tokens(t, out)
+        want = torch.argmax(t.float(), -1)
+        assert out.tolist() == want.tolist()
+        assert out[0].item() == 3 and out[1].item() == V // 2 + 1
 
 
 # ---------------------------------------------------------------------------------------------------- A15

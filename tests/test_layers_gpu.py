@@ -9,6 +9,7 @@ import math
 
 import pytest
 import torch
+import torch.nn.functional as F
 
 from dots.rl_amd import native
 
@@ -315,3 +316,57 @@ def test_flash_attn_backward(B, Hkv, G, D, T):
     dq2, dk2, dv2 = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
     native.flash_attn_bwd(q, k, kt, v, o, dout, lse, valid, dq2, dk2, dv2)
     assert torch.equal(dq, dq2) and torch.equal(dk, dk2) and torch.equal(dv, dv2)
+
+
+@pytest.mark.parametrize("M,N,K,epi", [(1, 1152, 896, "bias"), (7, 896, 896, None), (64, 1152, 896, "bias"),
+                                       (64, 9728, 896, "swiglu"), (64, 896, 4864, None), (100, 1000, 272, None),
+                                       (128, 9728, 896, "swiglu"), (128, 896, 4864, None), (40, 96, 4864, "bias"),
+                                       (64, 2 * 80, 4864, "swiglu"), (33, 151936, 896, None), (128, 64, 16, None)])
+def test_linear_decode(M, N, K, epi):
+    """Decode-step linear (csrc/linear.hip) vs an fp32 reference of the bf16 module: y = bf16(x W^T + b);
+    SwiGLU: bf16(bf16(silu(bf16(g))) * bf16(u)). Tolerance: 1 bf16 ulp of the output (fp32 summation order)
+    for the plain forms, 3 ulp after SwiGLU's three roundings."""
+    g = torch.Generator(device="cuda").manual_seed(M * 7 + N)
+    bf = torch.bfloat16
+    x = torch.randn(M, K, device="cuda", generator=g).to(bf)
+    w = (torch.randn(N, K, device="cuda", generator=g) / math.sqrt(K)).to(bf)
+    bias = torch.randn(N, device="cuda", generator=g).to(bf) if epi == "bias" else None
+    y = native.linear_decode(x, w, bias=bias, swiglu=epi == "swiglu")
+    ref = x.float() @ w.float().t()
+    if bias is not None:
+        ref = ref + bias.float()
+    if epi == "swiglu":
+        gt, up = ref[:, : N // 2].to(bf).float(), ref[:, N // 2:].to(bf).float()
+        ref = F.silu(gt).to(bf).float() * up
+        ulp = 3
+    else:
+        ulp = 1
+    err = (y.float() - ref).abs()
+    bound = ulp * 2.0 ** -7 * ref.abs() + 1e-4
+    assert (err <= bound).all(), f"max err {err.max().item()} at {torch.nonzero(err > bound)[:4].tolist()}"
+    for _ in range(3):  # deterministic; the K-split arrival tickets reset themselves between calls
+        y2 = native.linear_decode(x, w, bias=bias, swiglu=epi == "swiglu")
+        assert torch.equal(y, y2)
+
+
+@pytest.mark.parametrize("waves,splits", [(4, 2), (8, 4), (2, 8), (16, 1)])
+def test_decode_attention_vt_split_plans(waves, splits):
+    """Every forced (waves, key-split) plan of the MFMA decode kernel gives the same result as the default
+    plan up to fp32 merge rounding (split partial states merged by the last arriving workgroup)."""
+    B, Hkv, G, D, Tk = 6, 2, 7, 64, 640
+    g = torch.Generator(device=DEV).manual_seed(waves * 10 + splits)
+    q = torch.randn(B, Hkv, G, D, device=DEV, generator=g).to(torch.bfloat16)
+    k = torch.randn(B, Hkv, Tk, D, device=DEV, generator=g).to(torch.bfloat16)
+    vt = torch.randn(B, Hkv, D, Tk, device=DEV, generator=g).to(torch.bfloat16)
+    valid = (torch.rand(B, Tk, device=DEV, generator=g) > 0.2).to(torch.uint8)
+    valid[0] = 0  # a row with no allowed key
+    ref = native.decode_attention_vt(q, k, vt, valid, 600, torch.empty_like(q))
+    lib = native.lib()
+    lib.drl_decode_attention_set_plan(waves, splits)
+    try:
+        for _ in range(2):  # the arrival tickets reset themselves between calls
+            out = native.decode_attention_vt(q, k, vt, valid, 600, torch.empty_like(q))
+            torch.testing.assert_close(out.float(), ref.float(), rtol=2e-2, atol=2e-3)
+        assert (out[0] == 0).all()
+    finally:
+        lib.drl_decode_attention_set_plan(0, 0)

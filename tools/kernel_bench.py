@@ -37,6 +37,26 @@ def time_it(fn, iters=20, warmup=3):
     return a.elapsed_time(b) / iters * 1e-3
 
 
+def time_graph(fn, n):
+    """GPU time per call of n back-to-back calls captured in one HIP graph (no host launch cost: the decode
+    step replays its kernels from a graph too)."""
+    fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(n):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(3):
+        g.replay()
+    b.record()
+    b.synchronize()
+    return a.elapsed_time(b) / (3 * n) * 1e-3
+
+
 def k1_sweep(exps):
     rows = []
     for e in exps:
@@ -58,6 +78,11 @@ def k1_sweep(exps):
         t = time_it(lambda: native.ppo_loss_fwd_bwd(old, lp, adv, mask, ent, ref, **kw))
         byt = 36 * N
         rows.append(dict(kernel="K1_ppo_loss_fwd_bwd", tokens=N, seconds=t, GBps=byt / t / 1e9, frac=byt / t / PEAK_HBM))
+        # one-pass form: the batch's token count is already known (computed once, outside the timed region)
+        tc = mask.to(torch.float64).sum().reshape(1)
+        t1 = time_it(lambda: native.ppo_loss_fwd_bwd(old, lp, adv, mask, ent, ref, token_count=tc, **kw))
+        rows.append(dict(kernel="K1_ppo_loss_fwd_bwd_one_pass", tokens=N, seconds=t1, GBps=byt / t1 / 1e9,
+                         frac=byt / t1 / PEAK_HBM))
         del old, lp, adv, mask, ent, ref, dlp, dent
         torch.cuda.empty_cache()
     return rows
@@ -109,13 +134,39 @@ def decode_attn(B=512, Hkv=2, G=7, D=64, Tk=768, L=640):
     v = torch.randn_like(k)
     valid = torch.ones(B, Tk, dtype=torch.uint8, device=dev)
     out = torch.empty_like(q)
-    t = time_it(lambda: native.decode_attention(q, k, v, valid, L, out), iters=50)
+    t = time_graph(lambda: native.decode_attention(q, k, v, valid, L, out), 50)
     nbytes = B * Hkv * (2 * L * D * 2 + 2 * G * D * 2)
     vt = v.transpose(-1, -2).contiguous()
-    t2 = time_it(lambda: native.decode_attention_vt(q, k, vt, valid, L, out), iters=50)
+    t2 = time_graph(lambda: native.decode_attention_vt(q, k, vt, valid, L, out), 50)
     return [dict(kernel="A3_decode_attention", B=B, L=L, seconds=t, GBps=nbytes / t / 1e9, frac=nbytes / t / PEAK_HBM),
             dict(kernel="A3_decode_attention_vt_mfma", B=B, L=L, seconds=t2, GBps=nbytes / t2 / 1e9,
                  frac=nbytes / t2 / PEAK_HBM)]
+
+
+def decode_sweep(Bs=(64, 128, 256, 512), Ls=(513, 768), Hkv=2, G=7, D=64):
+    """MFMA decode attention over (waves per workgroup, key splits) plans, graph-timed."""
+    dev = "cuda"
+    res = []
+    for B in Bs:
+        for L in Ls:
+            q = torch.randn(B, Hkv, G, D, device=dev, dtype=torch.bfloat16)
+            k = torch.randn(B, Hkv, 768, D, device=dev, dtype=torch.bfloat16)
+            vt = torch.randn(B, Hkv, D, 768, device=dev, dtype=torch.bfloat16)
+            valid = torch.ones(B, 768, dtype=torch.uint8, device=dev)
+            out = torch.empty_like(q)
+            sweep = {}
+            for nw in (0, 2, 4, 8, 16):
+                for sp in (0, 1, 2, 4, 8):
+                    if (nw == 0) != (sp == 0):
+                        continue
+                    native.lib().drl_decode_attention_set_plan(nw, sp)
+                    sweep[f"{nw}x{sp}"] = round(time_graph(
+                        lambda: native.decode_attention_vt(q, k, vt, valid, L, out), 50) * 1e6, 2)
+            native.lib().drl_decode_attention_set_plan(0, 0)
+            best = min(sweep, key=sweep.get)
+            res.append(dict(kernel="decode_attention_vt_sweep", B=B, L=L, auto_us=sweep["0x0"], best=best,
+                            best_us=sweep[best], sweep_us=sweep))
+    return res
 
 
 def flash(B=16, Hkv=2, G=7, D=64, T=768):
@@ -164,15 +215,93 @@ def flash_bwd(B=8, Hkv=2, G=7, D=64, T=768):
                  frac_mfma=2.5 * flops / t / 2.5e15, fwd_seconds=tf)]
 
 
+def linear(Ms=(64, 128, 256, 512), plans=True):  # ours takes M <= 128
+    """Decode-step linear layers (csrc/linear.hip) vs hipBLASLt (replaying the shipped TunableOp choices) at the
+    Qwen2.5-0.5B projection shapes. Weights rotate over copies totalling > 600 MB so every call streams its
+    weight from HBM, as in a decode step (1 GB of weights between two uses of one layer)."""
+    from dots.rl_amd.workers import _enable_gemm_tuning
+    _enable_gemm_tuning("auto")
+    dev, bf = "cuda", torch.bfloat16
+    shapes = [("qkv_proj", 1152, 896, "bias"), ("o_proj", 896, 896, None), ("gate_up_swiglu", 9728, 896, "swiglu"),
+              ("down_proj", 896, 4864, None), ("lm_head", 151936, 896, None)]
+    res = []
+    for name, N, K, epi in shapes:
+        ncopy = max(2, int(600e6 // (N * K * 2)) + 1)
+        ws = [torch.randn(N, K, device=dev, dtype=bf) * 0.05 for _ in range(ncopy)]
+        bias = torch.randn(N, device=dev, dtype=bf) if epi == "bias" else None
+        for M in Ms:
+            x = torch.randn(M, K, device=dev, dtype=bf)
+            it = iter(range(1 << 30))
+
+            def ours():
+                w = ws[next(it) % ncopy]
+                return native.linear_decode(x, w, bias=bias, swiglu=epi == "swiglu")
+
+            def lib():
+                w = ws[next(it) % ncopy]
+                if epi == "bias":
+                    return torch.addmm(bias, x, w.t())
+                y = x @ w.t()
+                if epi == "swiglu":
+                    a = torch.empty(M, N // 2, device=dev, dtype=bf)
+                    native.swiglu_fwd(y, a)
+                    return a
+                return y
+            t = time_graph(ours, ncopy) if M <= 128 else float("nan")
+            sweep = {}
+            if M <= 128 and plans:
+                for kw in (4, 8, 16):
+                    for ks in (1, 2, 4, 8, 16):
+                        native.lib().drl_linear_decode_set_plan(kw, ks)
+                        sweep[f"{kw}x{ks}"] = round(time_graph(ours, ncopy) * 1e6, 2)
+                native.lib().drl_linear_decode_set_plan(0, 0)
+            t2 = time_graph(lib, ncopy)
+            nbytes = 2 * N * K + 2 * M * K + 2 * M * (N // 2 if epi == "swiglu" else N)
+            best = min(sweep, key=sweep.get) if sweep else None
+            res.append(dict(kernel="linear_decode", layer=name, M=M, N=N, K=K, seconds=t, GBps=nbytes / t / 1e9,
+                            frac=nbytes / t / PEAK_HBM, hipblaslt_seconds=t2, best_plan=best,
+                            best_us=sweep.get(best), sweep_us=sweep))
+    return res
+
+
+def launch_floor(B=64, H=896, I=4864):
+    """Per-call time of tiny kernels replayed back to back from a HIP graph: the launch/dependency floor of a
+    decode step, next to the small hand-written decode kernels at B rows."""
+    dev, bf = "cuda", torch.bfloat16
+    z = torch.zeros(1, device=dev)
+    x = torch.randn(B, 1, H, device=dev)
+    d = torch.randn(B, 1, H, device=dev, dtype=bf)
+    w = torch.ones(H, device=dev)
+    y = torch.empty(B, 1, H, device=dev, dtype=bf)
+    x2 = torch.empty_like(x)
+    gu = torch.randn(B, 2 * I, device=dev, dtype=bf)
+    a = torch.empty(B, I, device=dev, dtype=bf)
+    res = []
+    for name, fn in [("torch_zero_1elem", lambda: z.zero_()),
+                     ("add_rmsnorm_fwd", lambda: native.add_rmsnorm_fwd(x, d, x2, w, y, None, 1e-6)),
+                     ("swiglu_fwd", lambda: native.swiglu_fwd(gu, a))]:
+        res.append(dict(kernel="graph_floor", op=name, B=B, seconds=time_graph(fn, 200)))
+    return res
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--only", default=None)
     args = ap.parse_args()
     if args.only == "decode":
-        for L in (513, 640, 768):
-            for r in decode_attn(L=L):
-                print(json.dumps(r), flush=True)
+        for B in (512, 64):
+            for L in (513, 640, 768):
+                for r in decode_attn(B=B, L=L):
+                    print(json.dumps(r), flush=True)
+        sys.exit(0)
+    if args.only == "decode_sweep":
+        for r in decode_sweep():
+            print(json.dumps(r), flush=True)
+        sys.exit(0)
+    if args.only == "linear":
+        for r in launch_floor() + linear():
+            print(json.dumps(r), flush=True)
         sys.exit(0)
     if args.only == "flash":
         for r in flash() + flash_bwd():
