@@ -124,6 +124,9 @@ SIGNATURES = {
     "drl_linear_decode_workspace_bytes": (SZ, [I64, I64, I64, I32]),
     "drl_linear_decode_set_plan": (None, [I32, I32]),
     "drl_linear_decode": (ctypes.c_int, [P, I64, P, P, I32, I64, I64, I64, I32, P, I64, P, SZ, P]),
+    "drl_linear_logprob_workspace_bytes": (SZ, [I64, I64, I64]),
+    "drl_linear_logprob_fwd": (ctypes.c_int, [P, I64, P, P, I32, I64, I64, I64, F32, P, P, P, P, SZ, P]),
+    "drl_linear_logprob_dlogits": (ctypes.c_int, [P, I64, P, P, I32, I64, I64, I64, F32, P, P, P, P, P, I64, P]),
 }
 
 _lib = None

@@ -100,6 +100,9 @@ class DataParallelPPOActor:
         B, R = responses.shape
         h = m.hidden_states(micro_batch["input_ids"], micro_batch["attention_mask"], micro_batch["position_ids"])
         h = h[:, -R - 1:-1, :].reshape(B * R, h.shape[-1])
+        if self.use_fused_kernels:  # A21: no (B*R, V) logits (dp_actor.py:173-186 fused branch)
+            logp, ent = m.fused_logprob(h, responses.reshape(-1), temperature, calculate_entropy)
+            return (ent.view(B, R) if ent is not None else None), logp.view(B, R)
         logits = m.logits(h)
         logp, ent = logprobs_and_entropy_from_logits(logits, responses.reshape(-1), temperature, calculate_entropy,
                                                      inplace_backward=True)

@@ -223,6 +223,52 @@ def logprob_entropy_bwd(logits, labels, temperature, dlogp, dentropy, lse, entro
     return out
 
 
+# ----------------------------------------------------------------------------------------------- A21
+def _pad_k64(t):
+    """Zero-pad the hidden dimension to a multiple of 64 (the fused kernel's K step; zeros add nothing)."""
+    H = t.shape[-1]
+    return t if H % 64 == 0 else torch.nn.functional.pad(t, (0, 64 - H % 64))
+
+
+def linear_logprob_fwd(hidden, weight, labels, temperature=1.0, want_entropy=True, want_lse=True):
+    """Fused lm_head + log-prob + entropy (csrc/fused_linear.hip): hidden (N, H) bf16, weight (V, H) bf16,
+    labels (N,) -> logp, entropy (or None), lse (or None), (N,) fp32; the (N, V) logits are never stored."""
+    _dev(hidden, weight, labels)
+    h, w = _pad_k64(hidden), _pad_k64(weight)
+    assert h.dim() == 2 and h.stride(1) == 1 and w.is_contiguous() and h.dtype == w.dtype == torch.bfloat16
+    lab = _c(labels.reshape(-1).to(torch.int64))
+    N, H = h.shape
+    V = w.shape[0]
+    dev = h.device
+    logp = torch.empty(N, dtype=torch.float32, device=dev)
+    ent = torch.empty(N, dtype=torch.float32, device=dev) if want_entropy else None
+    lse = torch.empty(N, dtype=torch.float32, device=dev) if want_lse else None
+    nws = lib().drl_linear_logprob_workspace_bytes(N, H, V)
+    ws = _ws.get(nws, dev)
+    check(lib().drl_linear_logprob_fwd(_p(h), h.stride(0), _p(w), _p(lab), _lib.DRL_BF16, N, H, V, float(temperature),
+                                       _p(logp), _p(ent), _p(lse), _p(ws), nws, _stream()), "drl_linear_logprob_fwd")
+    return logp, ent, lse
+
+
+def linear_logprob_dlogits(hidden, weight, labels, temperature, dlogp, dentropy, lse, entropy, out=None):
+    """d_logits^T (V, N) bf16 of the fused lm_head log-prob / entropy (z recomputed on MFMA)."""
+    _dev(hidden, weight, labels, dlogp, lse)
+    h, w = _pad_k64(hidden), _pad_k64(weight)
+    assert h.dim() == 2 and h.stride(1) == 1 and w.is_contiguous() and h.dtype == w.dtype == torch.bfloat16
+    lab = _c(labels.reshape(-1).to(torch.int64))
+    N, H = h.shape
+    V = w.shape[0]
+    if out is None:
+        out = torch.empty(V, N, dtype=torch.bfloat16, device=h.device)
+    assert out.shape == (V, N) and out.stride(1) == 1 and out.dtype == torch.bfloat16
+    dlogp = _c(dlogp.reshape(-1).float())
+    dentropy = _c(dentropy.reshape(-1).float()) if dentropy is not None else None
+    check(lib().drl_linear_logprob_dlogits(_p(h), h.stride(0), _p(w), _p(lab), _lib.DRL_BF16, N, H, V, float(temperature),
+                                           _p(dlogp), _p(dentropy), _p(_c(lse)), _p(_c(entropy)), _p(out),
+                                           out.stride(0), _stream()), "drl_linear_logprob_dlogits")
+    return out
+
+
 # ----------------------------------------------------------------------------------------------- K3/K5
 def grpo_outcome_advantage(token_level_rewards, response_mask, row_group, group_offsets, group_members, G,
                            epsilon=1e-6, norm_adv_by_std_in_grpo=True):

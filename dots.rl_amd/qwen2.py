@@ -28,6 +28,7 @@ import torch
 import torch.nn.functional as F
 
 from . import native
+from .torch_functional import fused_linear_logprob_entropy
 
 
 @dataclass
@@ -467,6 +468,14 @@ class Qwen2Model:
         if self.training and self.store.trainable:
             return _Linear.apply(h, self.store.w(name), self.store.g(name), self._dummy)
         return F.linear(h, self.store.w(name))
+
+    def fused_logprob(self, h, labels, temperature, calculate_entropy):
+        """A21: h (N, H) in bf16 -> (log_probs, entropy or None) over the lm_head without materialising logits
+        (csrc/fused_linear.hip); in training the weight gradient accumulates into the fp32 gradient buffer."""
+        name = self.lm_head_weight()
+        gw = self.store.g(name) if (self.training and self.store.trainable) else None
+        return fused_linear_logprob_entropy(h, self.store.w(name), labels, temperature, calculate_entropy,
+                                            weight_grad=gw)
 
     def hidden_states(self, input_ids, attention_mask, position_ids):
         """Full-sequence forward -> final-norm hidden states (B, T, H) in the compute dtype."""

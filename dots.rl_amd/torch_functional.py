@@ -57,6 +57,48 @@ def entropy_from_logits(logits: torch.Tensor):
     return logprobs_and_entropy_from_logits(logits, labels, 1.0, True, False)[1]
 
 
+class _FusedLinearLogprobEntropy(torch.autograd.Function):
+    """A21: lm_head + log-prob + entropy without materialising logits (FusedLinearForPPOFunction,
+    utils/experimental/torch_functional.py:75-150; linear_cross_entropy.py:41-117 with reduction "none").
+    Backward = the reference's BackwardEnum._Total_Separate: one kernel writes d_logits^T (V, N) bf16 from
+    recomputed logits, then d_hidden = d_logits W and d_W += d_logits^T hidden on hipBLASLt (d_W straight
+    into the fp32 gradient buffer ``weight_grad`` when given)."""
+
+    @staticmethod
+    def forward(ctx, hidden, weight, weight_grad, labels, temperature, want_entropy):
+        logp, ent, lse = native.linear_logprob_fwd(hidden, weight, labels, temperature, want_entropy=want_entropy)
+        ctx.save_for_backward(hidden, weight, labels, lse, ent if ent is not None else lse.new_empty(0))
+        ctx.weight_grad = weight_grad
+        ctx.temperature = temperature
+        ctx.want_entropy = want_entropy
+        return logp, (ent if ent is not None else logp.new_zeros(0))
+
+    @staticmethod
+    def backward(ctx, dlogp, dent):
+        hidden, weight, labels, lse, ent = ctx.saved_tensors
+        if dlogp is None:
+            dlogp = torch.zeros_like(lse)
+        if not ctx.want_entropy:
+            dent = None
+        dlt = native.linear_logprob_dlogits(hidden, weight, labels, ctx.temperature, dlogp, dent, lse,
+                                            ent if dent is not None else None)
+        dh = dlt.t() @ weight
+        dw = None
+        if ctx.weight_grad is not None:
+            torch.addmm(ctx.weight_grad, dlt, hidden, out_dtype=torch.float32, out=ctx.weight_grad)
+        elif ctx.needs_input_grad[1]:
+            dw = dlt @ hidden
+        return dh, dw, None, None, None, None
+
+
+def fused_linear_logprob_entropy(hidden, weight, labels, temperature=1.0, calculate_entropy=True, weight_grad=None):
+    """hidden (N, H) bf16, weight (V, H) bf16 -> (log_probs, entropy or None), (N,) fp32 (A21). With
+    ``weight_grad`` (fp32, (V, H)) the weight gradient accumulates there instead of being returned."""
+    logp, ent = _FusedLinearLogprobEntropy.apply(hidden, weight, weight_grad, labels, float(temperature),
+                                                 bool(calculate_entropy))
+    return logp, (ent if calculate_entropy else None)
+
+
 def masked_sum(values, mask, axis=None):
     """torch_functional.py:163-168."""
     assert axis is None, "only the full reduction is on the hot path"

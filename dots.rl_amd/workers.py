@@ -112,6 +112,11 @@ class ActorRolloutRefWorker(Worker):
         else:
             self._load_hf_weights(path)
         self.actor_module = Qwen2Model(mcfg, self.store)
+        # model.use_fused_kernels reaches the actor and ref configs (fsdp_workers.py:581, :658): A21 fused
+        # lm_head + log-prob + entropy (csrc/fused_linear.hip) instead of logits + K2
+        fused = bool(cfg.model.get("use_fused_kernels", False)) and dtype == torch.bfloat16
+        cfg.actor.use_fused_kernels = fused
+        cfg.ref.use_fused_kernels = fused
         if self._is_actor:
             o = cfg.actor.optim
             total = o.get("total_training_steps", -1)

@@ -331,6 +331,29 @@ int drl_linear_decode(const void* x, int64_t ld_x, const void* w, const void* bi
                       int64_t N, int64_t K, int32_t epilogue, void* out, int64_t ld_out, void* workspace,
                       size_t workspace_bytes, void* stream);
 
+/* A21 fused lm_head + log-prob + entropy (MFMA; logits never written). Replaces FusedLinearForPPO.forward
+ * (verl/utils/experimental/torch_functional.py:20-37, :153-216) and the Triton linear_cross_entropy forward
+ * (verl/utils/kernel/linear_cross_entropy.py:41-84 -> kernels.py:507-696) for reduction "none".
+ * hidden (N, ld_h) bf16, weight (V, H) bf16 row-major, labels (N) int64 in [0, V); H % 64 == 0, 16-B aligned
+ * operands. z = hidden W^T / temperature in fp32 (no bf16 rounding of the logits: the Triton kernel's
+ * numerics); outputs (each may be NULL) logp[t] = z[t, label] - lse[t], entropy[t] = lse[t] - sum_v p z,
+ * lse[t] (natural log), all fp32. workspace: drl_linear_logprob_workspace_bytes(N, H, V) bytes, any content.
+ * Deterministic (fixed tile order, fixed-order merges). */
+size_t drl_linear_logprob_workspace_bytes(int64_t N, int64_t H, int64_t V);
+int drl_linear_logprob_fwd(const void* hidden, int64_t ld_h, const void* weight, const int64_t* labels, int32_t dt,
+                           int64_t N, int64_t H, int64_t V, float temperature, float* logp, float* entropy,
+                           float* lse, void* workspace, size_t workspace_bytes, void* stream);
+/* A21 backward, d_logits stage (the reference's BackwardEnum._Total_Separate, kernels.py:1378-1480 ->
+ * efficient_entropy_backward_kernel_general_d_logits; semantics torch_functional.py:40-72): recomputes z and
+ * writes d_logits TRANSPOSED, dlogits_t (V, ld_dl) bf16 with ld_dl >= N:
+ *   d z[t, v] = (dlogp[t] (1[v == label] - p) - dentropy[t] p (log p + entropy[t])) / temperature.
+ * dentropy may be NULL (no entropy gradient; entropy then unused). d_hidden = dlogits_t^T W and
+ * d_W = dlogits_t hidden are library GEMMs on the caller side. */
+int drl_linear_logprob_dlogits(const void* hidden, int64_t ld_h, const void* weight, const int64_t* labels, int32_t dt,
+                               int64_t N, int64_t H, int64_t V, float temperature, const float* dlogp,
+                               const float* dentropy, const float* lse, const float* entropy, void* dlogits_t,
+                               int64_t ld_dl, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,119 @@
+"""A21 parity: fused lm_head + log-prob + entropy (csrc/fused_linear.hip, through the C-ABI) against the
+CPU oracle (oracle.fused_linear_*, pinned to the reference's FusedLinearForPPO by tests/golden/fused_linear.npz
+in test_oracle_golden.py).
+
+The kernel takes bf16 operands and accumulates the logits in fp32 without rounding them (the Triton
+linear_cross_entropy numerics), so the oracle is evaluated in float64 on the SAME bf16-rounded operands.
+Tolerances (stated per check): logp / entropy 2e-5 relative + 2e-5 absolute (fp32 accumulation over H
+and fp32 online softmax over V); d_logits one bf16 rounding (2^-8 relative of the row's largest entry);
+d_hidden / d_W the bf16 d_logits fed to bf16 GEMMs: 2e-2 of the largest entry.
+"""
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from dots.rl_amd import native
+from dots.rl_amd.torch_functional import fused_linear_logprob_entropy
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def bf16_round(x):
+    return torch.from_numpy(np.ascontiguousarray(x, np.float32)).to(torch.bfloat16).to(torch.float32).numpy()
+
+
+def make(N, H, V, seed, scale=0.5):
+    rng = np.random.default_rng(seed)
+    h = bf16_round((rng.random((N, H), dtype=np.float32) - 0.5) * 2 * scale)
+    w = bf16_round((rng.random((V, H), dtype=np.float32) - 0.5) * 2 * scale)
+    ids = rng.integers(0, V, size=(N,), dtype=np.int64)
+    ids[0], ids[-1] = 0, V - 1  # both ends of the vocabulary
+    return h, w, ids
+
+
+def T(x, dtype=None):
+    t = torch.from_numpy(np.ascontiguousarray(x)).to(DEV)
+    return t.to(dtype) if dtype is not None else t
+
+
+@pytest.mark.parametrize("N,H,V,temp", [(40, 64, 512, 1.0), (130, 96, 1000, 1.5), (300, 896, 151936, 0.7),
+                                        (513, 128, 4099, 1.0), (1, 64, 257, 2.0)])
+def test_forward_matches_oracle(N, H, V, temp):
+    h, w, ids = make(N, H, V, seed=N + V)
+    lp, ent, lse = native.linear_logprob_fwd(T(h, torch.bfloat16), T(w, torch.bfloat16), T(ids), temp)
+    rlp, rent = oracle.fused_linear_logprob_entropy(h, w, ids, temp)
+    np.testing.assert_allclose(lp.cpu().numpy(), rlp, rtol=2e-5, atol=2e-5)
+    np.testing.assert_allclose(ent.cpu().numpy(), rent, rtol=2e-5, atol=2e-5)
+    # lse is consistent with logp: logp = z[label] - lse
+    z_lab = (h.astype(np.float64) * w[ids].astype(np.float64)).sum(-1) / temp
+    np.testing.assert_allclose(lse.cpu().numpy(), z_lab - rlp, rtol=2e-5, atol=2e-5)
+
+
+def test_reference_golden_cases(golden):
+    """The reference's own FusedLinearForPPO vectors (fp32 operands) through the bf16 kernel: equal up to the
+    bf16 rounding of hidden / weight (|h|, |w| < 0.5, H <= 96: logits move by < 1e-2)."""
+    z, meta = golden("fused_linear.npz")
+    for ci, cfg in enumerate(meta["cases"]):
+        g = lambda k: z[f"c{ci}_{k}"]  # noqa: E731
+        lp, ent, _ = native.linear_logprob_fwd(T(g("hidden"), torch.bfloat16), T(g("weight"), torch.bfloat16),
+                                               T(g("input_ids")), cfg["temperature"])
+        np.testing.assert_allclose(lp.cpu().numpy(), g("out_logp"), rtol=0, atol=3e-2)
+        np.testing.assert_allclose(ent.cpu().numpy(), g("out_entropy"), rtol=0, atol=3e-2)
+
+
+@pytest.mark.parametrize("N,H,V,temp,with_ent", [(130, 96, 1000, 1.5, True), (300, 128, 3001, 1.0, False),
+                                                 (64, 896, 151936, 1.0, True)])
+def test_dlogits_matches_oracle(N, H, V, temp, with_ent):
+    h, w, ids = make(N, H, V, seed=7 * N)
+    rng = np.random.default_rng(N)
+    dlp = rng.standard_normal(N).astype(np.float32)
+    den = rng.standard_normal(N).astype(np.float32) if with_ent else np.zeros(N, np.float32)
+    hb, wb = T(h, torch.bfloat16), T(w, torch.bfloat16)
+    lp, ent, lse = native.linear_logprob_fwd(hb, wb, T(ids), temp)
+    dlt = native.linear_logprob_dlogits(hb, wb, T(ids), temp, T(dlp), T(den) if with_ent else None, lse,
+                                        ent if with_ent else None)
+    logits = h.astype(np.float64) @ w.astype(np.float64).T
+    ref = oracle.logprob_entropy_backward(logits, ids, dlp, den, temp)
+    got = dlt.float().cpu().numpy().T
+    tol = np.abs(ref).max(axis=1, keepdims=True) * 2.0 ** -8 + 1e-9
+    assert (np.abs(got - ref) <= tol).all(), float(np.abs(got - ref).max())
+
+
+def test_autograd_grads_match_oracle():
+    N, H, V, temp = 200, 128, 2500, 1.3
+    h, w, ids = make(N, H, V, seed=3)
+    rng = np.random.default_rng(5)
+    dlp = rng.standard_normal(N).astype(np.float32)
+    den = rng.standard_normal(N).astype(np.float32)
+    hb = T(h, torch.bfloat16).requires_grad_(True)
+    wb = T(w, torch.bfloat16).requires_grad_(True)
+    lp, ent = fused_linear_logprob_entropy(hb, wb, T(ids), temp, calculate_entropy=True)
+    ((lp * T(dlp)).sum() + (ent * T(den)).sum()).backward()
+    rdh, rdw = oracle.fused_linear_backward(h, w, ids, dlp, den, temp)
+    for got, ref in ((hb.grad, rdh), (wb.grad, rdw)):
+        err = np.abs(got.float().cpu().numpy() - ref).max() / np.abs(ref).max()
+        assert err < 2e-2, err
+    # fp32 gradient-buffer form (the training path): d_W accumulates into weight_grad
+    gw = torch.full((V, H), 0.25, dtype=torch.float32, device=DEV)
+    hb2 = T(h, torch.bfloat16).requires_grad_(True)
+    lp2, ent2 = fused_linear_logprob_entropy(hb2, T(w, torch.bfloat16), T(ids), temp, True, weight_grad=gw)
+    ((lp2 * T(dlp)).sum() + (ent2 * T(den)).sum()).backward()
+    err = np.abs(gw.cpu().numpy() - 0.25 - rdw).max() / np.abs(rdw).max()
+    assert err < 2e-2, err
+    assert torch.equal(hb2.grad, hb.grad)
+
+
+def test_matches_unfused_path_and_is_deterministic():
+    """Against the unfused path (bf16 logits GEMM + K2): equal up to the bf16 rounding of the logits."""
+    N, H, V = 512, 896, 151936
+    h, w, ids = make(N, H, V, seed=11, scale=0.25)
+    hb, wb, lab = T(h, torch.bfloat16), T(w, torch.bfloat16), T(ids)
+    lp, ent, _ = native.linear_logprob_fwd(hb, wb, lab, 1.0)
+    lp2, ent2, _ = native.linear_logprob_fwd(hb, wb, lab, 1.0)
+    assert torch.equal(lp, lp2) and torch.equal(ent, ent2)
+    ulp, uent, _ = native.logprob_entropy_fwd(hb @ wb.t(), lab, 1.0)
+    np.testing.assert_allclose(lp.cpu().numpy(), ulp.cpu().numpy(), rtol=0, atol=5e-2)
+    np.testing.assert_allclose(ent.cpu().numpy(), uent.cpu().numpy(), rtol=0, atol=5e-2)

@@ -264,6 +264,45 @@ def linear(Ms=(64, 128, 256, 512), plans=True):  # ours takes M <= 128
     return res
 
 
+def fused_linear(Ns=(2048, 4096), H=896, V=151936):
+    """A21 fused lm_head + logp + entropy vs the unfused path (bf16 logits GEMM + K2), forward and backward.
+    MFMA-bound: 2*N*H*V FLOP per forward (and per d_logits recompute)."""
+    dev, bf = "cuda", torch.bfloat16
+    w = torch.randn(V, H, device=dev, dtype=bf) * 0.05
+    gw = torch.zeros(V, H, device=dev, dtype=torch.float32)
+    res = []
+    for N in Ns:
+        h = torch.randn(N, H, device=dev, dtype=bf)
+        lab = torch.randint(0, V, (N,), device=dev)
+        dlp = torch.randn(N, device=dev)
+        fl = 2.0 * N * H * V
+        t_f = time_it(lambda: native.linear_logprob_fwd(h, w, lab, 1.0))
+        t_u = time_it(lambda: native.logprob_entropy_fwd(h @ w.t(), lab, 1.0))
+        _, ent, lse = native.linear_logprob_fwd(h, w, lab, 1.0)
+
+        def fused_bwd():
+            dlt = native.linear_logprob_dlogits(h, w, lab, 1.0, dlp, None, lse, None)
+            dh = dlt.t() @ w
+            torch.addmm(gw, dlt, h, out_dtype=torch.float32, out=gw)
+            return dh
+
+        logits = h @ w.t()
+
+        def unfused_bwd():
+            dl = native.logprob_entropy_bwd(logits, lab, 1.0, dlp, None, lse, None, out=logits)
+            dh = dl @ w
+            torch.addmm(gw, dl.t(), h, out_dtype=torch.float32, out=gw)
+            return dh
+
+        t_dl = time_it(lambda: native.linear_logprob_dlogits(h, w, lab, 1.0, dlp, None, lse, None))
+        t_fb = time_it(fused_bwd)
+        t_ub = time_it(unfused_bwd)
+        res.append(dict(kernel="fused_linear", N=N, H=H, V=V, fwd_us=t_f * 1e6, fwd_TFLOPs=fl / t_f / 1e12,
+                        fwd_frac=fl / t_f / 2.5e15, unfused_fwd_us=t_u * 1e6, dlogits_us=t_dl * 1e6,
+                        dlogits_TFLOPs=fl / t_dl / 1e12, bwd_us=t_fb * 1e6, unfused_bwd_us=t_ub * 1e6))
+    return res
+
+
 def launch_floor(B=64, H=896, I=4864):
     """Per-call time of tiny kernels replayed back to back from a HIP graph: the launch/dependency floor of a
     decode step, next to the small hand-written decode kernels at B rows."""
@@ -301,6 +340,10 @@ if __name__ == "__main__":
         sys.exit(0)
     if args.only == "linear":
         for r in launch_floor() + linear():
+            print(json.dumps(r), flush=True)
+        sys.exit(0)
+    if args.only == "fused_linear":
+        for r in fused_linear():
             print(json.dumps(r), flush=True)
         sys.exit(0)
     if args.only == "flash":
