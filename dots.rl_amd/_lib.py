@@ -116,7 +116,7 @@ SIGNATURES = {
     "drl_decode_attention_vt_workspace_bytes": (SZ, [I64, I64, I64, I64]),
     "drl_decode_attention_set_plan": (None, [I32, I32]),
     "drl_decode_attention_vt": (ctypes.c_int, [P, P, P, I32, P, I64, P, I64, I64, I64, I64, I64, I64, I64, I64, F32,
-                                               P, P, SZ, P]),
+                                               P, I64, P, SZ, P]),
     "drl_flash_attn_bwd": (ctypes.c_int, [P, P, P, P, P, P, P, I32, P, I64, I64, I64, I64, I64, I64, I64, F32, P, P, P, P,
                                           P]),
     "drl_decode_attention": (ctypes.c_int, [P, P, P, I32, P, I64, P, I64, I64, I64, I64, I64, I64, I64, F32, P, P, SZ,
@@ -125,6 +125,13 @@ SIGNATURES = {
     "drl_linear_decode_set_plan": (None, [I32, I32]),
     "drl_linear_decode": (ctypes.c_int, [P, I64, P, P, I32, I64, I64, I64, I32, P, I64, P, SZ, P]),
     "drl_linear_logprob_workspace_bytes": (SZ, [I64, I64, I64]),
+    "drl_decode_gemm_plan": (ctypes.c_int, [I64, I64, I64, I32, P, P]),
+    "drl_decode_gemm_set_plan": (None, [I32, I32]),
+    "drl_decode_pack_weight_elems": (SZ, [I64, I64, I32]),
+    "drl_decode_pack_weight": (ctypes.c_int, [P, I64, I64, I64, I32, P, P]),
+    "drl_decode_gemm": (ctypes.c_int, [P, P, I64, I64, I64, I32, P, P, P]),
+    "drl_decode_rmsnorm": (ctypes.c_int, [P, P, I32, P, P, P, I64, I64, I64, F32, P]),
+    "drl_decode_rope": (ctypes.c_int, [P, I32, P, P, P, P, I64, I64, I64, I64, I64, P, P, P, P, I64, I64, I64, P, P]),
     "drl_linear_logprob_fwd": (ctypes.c_int, [P, I64, P, P, I32, I64, I64, I64, F32, P, P, P, P, SZ, P]),
     "drl_linear_logprob_dlogits": (ctypes.c_int, [P, I64, P, P, I32, I64, I64, I64, F32, P, P, P, P, P, I64, P]),
 }

@@ -1,0 +1,472 @@
+// Decode-step projections on fragment-packed operands (the rollout's per-token GEMMs at M = one token
+// per sequence, 1..128 rows per rank): replaces the nn.Linear calls of Qwen2Attention / Qwen2MLP that HF
+// generate runs once per response token (hf_rollout.py:112-124 -> transformers modeling_qwen2).
+//
+// Why a layout: at M <= 128 a projection is a weight stream (qkv 2 MB ... gate_up 17 MB per layer) plus an
+// activation panel re-read from L2 by every workgroup. Loading MFMA fragments straight from row-major
+// operands touches 32 rows x 32 B per wave-instruction and ran at ~1-2.5 TB/s (tools/wsgemm_probe.hip).
+// Here both operands are stored in v_mfma_f32_32x32x16_bf16 fragment order — the 64 lanes' 16-B pieces
+// of one (32-row block, 16-deep k step) are one contiguous 1 KB — so every load is a fully coalesced 1-KB
+// wave read into registers:
+//   weights: packed once per rollout from the bf16 compute copy (drl_decode_pack_weight);
+//   activations: written packed by their producers (the decode RMSNorm, the decode attention, the SwiGLU
+//   epilogue below), element (m, k) at ((k/16 * MBT + m/32) * 64 + ((k/8)&1) * 32 + m%32) * 8 + k%8 with
+//   MBT the (padded) number of 32-token blocks (1..16: up to 512 rows).
+// Workgroup = 4 waves on one 32-row weight block, one group of MB token blocks and one K slice; every wave
+// issues ALL loads of its KSW k-steps before its first MFMA (one memory round trip), the four partial
+// tiles meet in LDS in a fixed order. Outputs: fp32 partial sums per K slice (summed, in slice order, by
+// the consumer kernel that runs next anyway: decode RoPE, decode RMSNorm), or the SwiGLU activation
+// bf16(bf16(silu(g)) * u) written packed for the down projection (gate / up rows interleaved per block by
+// the weight packing). Deterministic: fixed summation order everywhere.
+#include "common.h"
+
+namespace drl {
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ bf16x8 as_bf16x8(u16x8 v) { return __builtin_bit_cast(bf16x8, v); }
+__device__ __forceinline__ uint16_t to_bf16_bits(float f) { return __builtin_bit_cast(uint16_t, static_cast<__bf16>(f)); }
+__device__ __forceinline__ float bf16r(float f) { return bf16_to_f32(to_bf16_bits(f)); }
+
+// packed activation offset of element (m, k)
+__device__ __forceinline__ int64_t pk_off(int64_t m, int64_t k, int64_t MBT) {
+  return (((k >> 4) * MBT + (m >> 5)) * 64 + ((k >> 3) & 1) * 32 + (m & 31)) * 8 + (k & 7);
+}
+
+// ------------------------------------------------------------------------------------------- packing
+// dst fragment (t, s, lane l): W row rowmap(t, l & 31), k = 16 s + 8 (l >> 5) .. + 7. SwiGLU packing
+// (half = I > 0): block t holds gate rows 16t..16t+15 then up rows I+16t..I+16t+15.
+__global__ __launch_bounds__(256) void pack_weight_kernel(const uint16_t* src, int64_t ld, int64_t N, int64_t K,
+                                                          int64_t half, int64_t tiles, uint16_t* dst) {
+  const int64_t nks = K / 16;
+  const int64_t idx = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (idx >= tiles * nks * 64) return;
+  const int l = static_cast<int>(idx & 63), r = l & 31, h = l >> 5;
+  const int64_t s = (idx >> 6) % nks, t = (idx >> 6) / nks;
+  int64_t row;
+  bool ok;
+  if (half > 0) {
+    const int64_t c = 16 * t + (r & 15);
+    ok = c < half;
+    row = r < 16 ? c : half + c;
+  } else {
+    row = 32 * t + r;
+    ok = row < N;
+  }
+  u16x8 v = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  if (ok) v = *reinterpret_cast<const u16x8*>(src + row * ld + 16 * s + 8 * h);
+  *reinterpret_cast<u16x8*>(dst + idx * 8) = v;
+}
+
+// ------------------------------------------------------------------------------------------- GEMM
+struct DgArgs {
+  const uint16_t* x;  // packed activations, MBT token blocks
+  const uint16_t* w;  // packed weights (tiles, nks)
+  int M, N, K, MBT, nks, tiles, half;
+  float* part;        // EPI_PARTIAL: (ksplit, M, N) fp32
+  uint16_t* out;      // EPI_SWIGLU: packed (MBT blocks, K' = half)
+};
+
+constexpr int EPI_PARTIAL = 0, EPI_SWIGLU = 1;
+
+template <int MB, int KSW, int EPI>
+__global__ __launch_bounds__(256) void decode_gemm_kernel(DgArgs a) {
+  __shared__ float red[4][MB][16][64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tile = blockIdx.x, ks = blockIdx.y, mb0 = blockIdx.z * MB;
+  const int s0 = (ks * 4 + wave) * KSW;
+  u16x8 wv[KSW], xv[KSW][MB];
+  const uint16_t* wp = a.w + (static_cast<int64_t>(tile) * a.nks + s0) * 512 + lane * 8;
+#pragma unroll
+  for (int s = 0; s < KSW; ++s) wv[s] = __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(wp + s * 512));
+#pragma unroll
+  for (int s = 0; s < KSW; ++s)
+#pragma unroll
+    for (int i = 0; i < MB; ++i)
+      xv[s][i] = *reinterpret_cast<const u16x8*>(a.x + ((static_cast<int64_t>(s0 + s) * a.MBT + mb0 + i) * 64 + lane) * 8);
+  __builtin_amdgcn_sched_barrier(0);  // every load of the wave is in flight before the first MFMA
+  f32x16 acc[MB];
+#pragma unroll
+  for (int i = 0; i < MB; ++i) acc[i] = f32x16{};
+#pragma unroll
+  for (int s = 0; s < KSW; ++s)
+#pragma unroll
+    for (int i = 0; i < MB; ++i)
+      acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(wv[s]), as_bf16x8(xv[s][i]), acc[i], 0, 0, 0);
+#pragma unroll
+  for (int i = 0; i < MB; ++i)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) red[wave][i][q][lane] = acc[i][q];
+  __syncthreads();
+  // C row i (weight row of the block) <-> register (i & 3) + 4 (i >> 3), lane half (i >> 2) & 1; column = token
+  if constexpr (EPI == EPI_PARTIAL) {
+    for (int e = tid; e < 1024 * MB; e += 256) {
+      const int tl = e >> 5, i = e & 31, blk = tl >> 5, ml = tl & 31;
+      const int m = (mb0 + blk) * 32 + ml, n = tile * 32 + i;
+      if (m >= a.M || n >= a.N) continue;
+      const int q = (i & 3) + 4 * (i >> 3), ln = ml + 32 * ((i >> 2) & 1);
+      const float v = ((red[0][blk][q][ln] + red[1][blk][q][ln]) + red[2][blk][q][ln]) + red[3][blk][q][ln];
+      a.part[(static_cast<int64_t>(ks) * a.M + m) * a.N + n] = v;
+    }
+  } else {
+    // SwiGLU: rows 0..15 gate, 16..31 up of output columns 16 * tile + c; thread -> (token, 8 columns)
+    for (int e = tid; e < 64 * MB; e += 256) {
+      const int tl = e >> 1, hc = e & 1, blk = tl >> 5, ml = tl & 31;
+      u16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int c = 8 * hc + j, ig = c, iu = c + 16;
+        const int qg = (ig & 3) + 4 * (ig >> 3), lg = ml + 32 * ((ig >> 2) & 1);
+        const int qu = (iu & 3) + 4 * (iu >> 3), lu = ml + 32 * ((iu >> 2) & 1);
+        const float g = bf16r(((red[0][blk][qg][lg] + red[1][blk][qg][lg]) + red[2][blk][qg][lg]) + red[3][blk][qg][lg]);
+        const float u = bf16r(((red[0][blk][qu][lu] + red[1][blk][qu][lu]) + red[2][blk][qu][lu]) + red[3][blk][qu][lu]);
+        o[j] = to_bf16_bits(bf16r(g / (1.f + expf(-g))) * u);
+      }
+      // packed for the next GEMM (K' = half): k step = tile, 8-column half hc, token (mb0 + blk, ml)
+      *reinterpret_cast<u16x8*>(a.out + ((static_cast<int64_t>(tile) * a.MBT + mb0 + blk) * 64 + hc * 32 + ml) * 8) = o;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------- consumers
+// x_out = x_in + bf16(sum_ks part) (fp32 residual stream, bf16 module output: add_rmsnorm_fwd semantics),
+// y = bf16(w * (x_out * rsqrt(mean(x_out^2) + eps))) written packed (MBT blocks) or row-major (MBT = 0).
+// Two waves per row, each lane owns 8-column chunks tid, tid + 128, ...; every load of the row (x and the NS
+// partial slices) is issued before the first add, so the kernel is one dependent memory round trip.
+// NS < 0: runtime slice count (loop).
+template <int CH, int NS>
+__global__ __launch_bounds__(128) void dec_rmsnorm_kernel(const float* x_in, const float* part, int nsplit, float* x_out,
+                                                          const float* w, uint16_t* y, int64_t M, int64_t H, int64_t MBT,
+                                                          float eps) {
+  __shared__ float s_ss[2];
+  const int64_t row = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int64_t nch = H / 8;
+  float4 xv[CH][2];
+  constexpr int NSL = NS > 0 ? NS : 1;
+  float4 pv[CH][NSL][2];
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int64_t ch = tid + 128 * c;
+    if (ch < nch) {
+      xv[c][0] = *reinterpret_cast<const float4*>(x_in + row * H + ch * 8);
+      xv[c][1] = *reinterpret_cast<const float4*>(x_in + row * H + ch * 8 + 4);
+      if constexpr (NS > 0) {
+#pragma unroll
+        for (int k = 0; k < NS; ++k) {
+          const float* p = part + (static_cast<int64_t>(k) * M + row) * H + ch * 8;
+          pv[c][k][0] = *reinterpret_cast<const float4*>(p);
+          pv[c][k][1] = *reinterpret_cast<const float4*>(p + 4);
+        }
+      }
+    }
+  }
+  float v[CH][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int64_t ch = tid + 128 * c;
+    if (ch >= nch) continue;
+    v[c][0] = xv[c][0].x; v[c][1] = xv[c][0].y; v[c][2] = xv[c][0].z; v[c][3] = xv[c][0].w;
+    v[c][4] = xv[c][1].x; v[c][5] = xv[c][1].y; v[c][6] = xv[c][1].z; v[c][7] = xv[c][1].w;
+    if (part) {
+      float d[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if constexpr (NS > 0) {
+#pragma unroll
+        for (int k = 0; k < NS; ++k) {
+          d[0] += pv[c][k][0].x; d[1] += pv[c][k][0].y; d[2] += pv[c][k][0].z; d[3] += pv[c][k][0].w;
+          d[4] += pv[c][k][1].x; d[5] += pv[c][k][1].y; d[6] += pv[c][k][1].z; d[7] += pv[c][k][1].w;
+        }
+      } else {
+        for (int k = 0; k < nsplit; ++k) {
+          const float* p = part + (static_cast<int64_t>(k) * M + row) * H + ch * 8;
+          const float4 b0 = *reinterpret_cast<const float4*>(p), b1 = *reinterpret_cast<const float4*>(p + 4);
+          d[0] += b0.x; d[1] += b0.y; d[2] += b0.z; d[3] += b0.w;
+          d[4] += b1.x; d[5] += b1.y; d[6] += b1.z; d[7] += b1.w;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[c][j] += bf16r(d[j]);
+    }
+    if (x_out) {
+      *reinterpret_cast<float4*>(x_out + row * H + ch * 8) = make_float4(v[c][0], v[c][1], v[c][2], v[c][3]);
+      *reinterpret_cast<float4*>(x_out + row * H + ch * 8 + 4) = make_float4(v[c][4], v[c][5], v[c][6], v[c][7]);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ss += v[c][j] * v[c][j];
+  }
+  ss = wave_sum(ss);
+  if ((tid & 63) == 0) s_ss[tid >> 6] = ss;
+  __syncthreads();
+  const float r = rsqrtf((s_ss[0] + s_ss[1]) / static_cast<float>(H) + eps);
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int64_t ch = tid + 128 * c;
+    if (ch >= nch) continue;
+    u16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = f32_to_bf16(w[ch * 8 + j] * (v[c][j] * r));
+    uint16_t* dst = MBT > 0 ? y + pk_off(row, ch * 8, MBT) : y + row * H + ch * 8;
+    *reinterpret_cast<u16x8*>(dst) = o;
+  }
+}
+
+// qkv = bf16(sum_ks part + bias) of one decode token, then rotary embedding (rope_qkv_fwd_kernel's math and
+// rounding): q -> (B, Hkv, G, 1, D); k -> cache row koff; v -> V^T cache column koff (and/or row-major v).
+struct DecRopeArgs {
+  const float* part;
+  int nsplit;
+  const uint16_t* bias;
+  const int64_t* pos;
+  const float* cos_t;
+  const float* sin_t;
+  uint16_t* q;
+  uint16_t* k;
+  uint16_t* v;
+  uint16_t* vt;
+  int64_t B, Hq, Hkv, D, Tk, ld_vt, maxpos, koff;
+  const int64_t* koff_dev;
+};
+
+__global__ __launch_bounds__(256) void dec_rope_kernel(DecRopeArgs a) {
+  const int64_t half = a.D / 2, Hall = a.Hq + 2 * a.Hkv, NQ = Hall * a.D;
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (i >= a.B * Hall * half) return;
+  const int64_t koff = a.koff_dev ? *a.koff_dev : a.koff;
+  if (koff < 0 || koff >= a.Tk) return;
+  const int64_t j = i % half, h = (i / half) % Hall, b = i / (half * Hall);
+  const int64_t c1 = h * a.D + j, c2 = c1 + half;
+  float s1 = 0.f, s2 = 0.f;
+  for (int k = 0; k < a.nsplit; ++k) {
+    s1 += a.part[(k * a.B + b) * NQ + c1];
+    s2 += a.part[(k * a.B + b) * NQ + c2];
+  }
+  const float x1 = bf16r(s1 + bf16_to_f32(a.bias[c1])), x2 = bf16r(s2 + bf16_to_f32(a.bias[c2]));
+  if (h < a.Hq + a.Hkv) {
+    int64_t p = a.pos[b];
+    p = p < 0 ? 0 : (p >= a.maxpos ? a.maxpos - 1 : p);
+    const float c = a.cos_t[p * half + j], s = a.sin_t[p * half + j];
+    const float o1 = fmaf(x1, c, -(x2 * s)), o2 = fmaf(x2, c, x1 * s);
+    uint16_t* dst;
+    if (h < a.Hq) {
+      const int64_t G = a.Hq / a.Hkv, g = h / G, hi = h % G;
+      dst = a.q + ((b * a.Hkv + g) * G + hi) * a.D;
+    } else {
+      dst = a.k + ((b * a.Hkv + (h - a.Hq)) * a.Tk + koff) * a.D;
+    }
+    dst[j] = to_bf16_bits(o1);
+    dst[j + half] = to_bf16_bits(o2);
+  } else {
+    const int64_t hv = h - a.Hq - a.Hkv;
+    if (a.vt) {
+      uint16_t* dst = a.vt + (b * a.Hkv + hv) * a.D * a.ld_vt + koff;
+      dst[j * a.ld_vt] = to_bf16_bits(x1);
+      dst[(j + half) * a.ld_vt] = to_bf16_bits(x2);
+    }
+    if (a.v) {
+      uint16_t* dst = a.v + ((b * a.Hkv + hv) * a.Tk + koff) * a.D;
+      dst[j] = to_bf16_bits(x1);
+      dst[j + half] = to_bf16_bits(x2);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------- planning
+struct DgPlan {
+  int mb, ksw, ksplit, mgroups, tiles, mbt;
+};
+
+int g_dg_mb = 0, g_dg_ksw = 0;  // tuning override (drl_decode_gemm_set_plan), 0 = automatic
+
+// (token blocks per workgroup, k16 steps per wave) instantiated; registers in flight 4 * ksw * (1 + mb)
+struct DgShape { int mb, ksw; };
+constexpr DgShape kShapes[] = {{2, 14}, {2, 7}, {2, 4}, {2, 2}, {2, 1}, {1, 19}, {1, 14}, {1, 7}, {1, 4}, {1, 2}, {1, 1}};
+
+bool plan_decode_gemm(int64_t M, int64_t N, int64_t K, int epi, DgPlan& p) {
+  if (M < 1 || M > 512 || K % 64 != 0 || N < 1) return false;
+  const int blocks = static_cast<int>((M + 31) / 32);
+  // one panel layout per M for every producer / consumer: blocks padded to the 2-block workgroup granule
+  p.mbt = blocks == 1 ? 1 : (blocks + 1) / 2 * 2;
+  p.tiles = static_cast<int>(epi == EPI_SWIGLU ? (N / 2 + 15) / 16 : (N + 31) / 32);
+  const int nks = static_cast<int>(K / 16);
+  // fewest K slices (partial sums for the consumer) among the shapes that give >= 96 workgroups, then
+  // 2-block workgroups (each weight fragment feeds two MFMAs); otherwise the shape with the most workgroups.
+  // SwiGLU needs the whole K in one workgroup.
+  bool found = false, full = false;
+  int64_t best_wgs = 0;
+  for (const DgShape& c : kShapes) {
+    if (c.mb > p.mbt) continue;
+    if (nks % (4 * c.ksw) != 0) continue;
+    const int ks = nks / (4 * c.ksw);
+    if (epi == EPI_SWIGLU && ks != 1) continue;
+    if ((g_dg_mb && c.mb != g_dg_mb) || (g_dg_ksw && c.ksw != g_dg_ksw)) continue;
+    const int64_t wgs = static_cast<int64_t>(p.tiles) * (p.mbt / c.mb) * ks;
+    const bool ok = wgs >= 96;
+    bool take = !found;
+    if (found) {
+      if (ok && !full) take = true;
+      else if (ok && full) take = ks < p.ksplit || (ks == p.ksplit && c.mb > p.mb);
+      else if (!ok && !full) take = wgs > best_wgs;
+    }
+    if (take) {
+      p.mb = c.mb;
+      p.ksw = c.ksw;
+      p.ksplit = ks;
+      p.mgroups = p.mbt / c.mb;
+      best_wgs = wgs;
+      full = ok;
+      found = true;
+    }
+  }
+  return found;
+}
+
+template <int MB, int EPI>
+void launch_dg(const DgArgs& a, const DgPlan& p, hipStream_t s) {
+  const dim3 grid(p.tiles, p.ksplit, p.mgroups);
+  switch (p.ksw) {
+    case 19:
+      if constexpr (MB == 1) hipLaunchKernelGGL((decode_gemm_kernel<1, 19, EPI>), grid, dim3(256), 0, s, a);
+      break;
+    case 14: hipLaunchKernelGGL((decode_gemm_kernel<MB, 14, EPI>), grid, dim3(256), 0, s, a); break;
+    case 7: hipLaunchKernelGGL((decode_gemm_kernel<MB, 7, EPI>), grid, dim3(256), 0, s, a); break;
+    case 4: hipLaunchKernelGGL((decode_gemm_kernel<MB, 4, EPI>), grid, dim3(256), 0, s, a); break;
+    case 2: hipLaunchKernelGGL((decode_gemm_kernel<MB, 2, EPI>), grid, dim3(256), 0, s, a); break;
+    default: hipLaunchKernelGGL((decode_gemm_kernel<MB, 1, EPI>), grid, dim3(256), 0, s, a); break;
+  }
+}
+
+}  // namespace
+}  // namespace drl
+
+extern "C" {
+
+void drl_decode_gemm_set_plan(int32_t mb, int32_t ksw) {
+  drl::g_dg_mb = (mb == 1 || mb == 2) ? mb : 0;
+  drl::g_dg_ksw = ksw > 0 ? ksw : 0;
+}
+
+int drl_decode_gemm_plan(int64_t M, int64_t N, int64_t K, int32_t epilogue, int32_t* ksplit, int32_t* mbt) {
+  drl::DgPlan p{};
+  if (!drl::plan_decode_gemm(M, N, K, epilogue == DRL_DECODE_SWIGLU ? drl::EPI_SWIGLU : drl::EPI_PARTIAL, p))
+    return drl::fail(DRL_ERR_UNSUPPORTED, "decode GEMM: unsupported shape M=%lld N=%lld K=%lld", (long long)M,
+                     (long long)N, (long long)K);
+  if (ksplit) *ksplit = p.ksplit;
+  if (mbt) *mbt = p.mbt;
+  return DRL_OK;
+}
+
+size_t drl_decode_pack_weight_elems(int64_t N, int64_t K, int32_t swiglu) {
+  if (N < 1 || K < 16 || K % 16) return 0;
+  const int64_t tiles = swiglu ? (N / 2 + 15) / 16 : (N + 31) / 32;
+  return static_cast<size_t>(tiles * (K / 16) * 512);
+}
+
+int drl_decode_pack_weight(const void* w, int64_t ld, int64_t N, int64_t K, int32_t swiglu, void* packed,
+                           void* stream) {
+  using namespace drl;
+  DRL_CHECK_ARG(w && packed, "NULL input");
+  DRL_CHECK_ARG(N >= 1 && K >= 16 && K % 16 == 0 && ld >= K && ld % 8 == 0 && aligned16(w) && aligned16(packed),
+                "bad shape / alignment");
+  DRL_CHECK_ARG(!swiglu || N % 2 == 0, "SwiGLU packing needs W = [gate | up]");
+  const int64_t tiles = swiglu ? (N / 2 + 15) / 16 : (N + 31) / 32;
+  const int64_t n = tiles * (K / 16) * 64;
+  hipLaunchKernelGGL(pack_weight_kernel, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), static_cast<const uint16_t*>(w), ld, N, K,
+                     swiglu ? N / 2 : int64_t(0), tiles, static_cast<uint16_t*>(packed));
+  DRL_LAUNCH_CHECK();
+  return DRL_OK;
+}
+
+int drl_decode_gemm(const void* x_packed, const void* w_packed, int64_t M, int64_t N, int64_t K, int32_t epilogue,
+                    float* partials, void* out_packed, void* stream) {
+  using namespace drl;
+  DRL_CHECK_ARG(x_packed && w_packed, "NULL input");
+  DRL_CHECK_ARG(aligned16(x_packed) && aligned16(w_packed), "packed operands must be 16-byte aligned");
+  const int epi = epilogue == DRL_DECODE_SWIGLU ? EPI_SWIGLU : EPI_PARTIAL;
+  DRL_CHECK_ARG(epilogue == DRL_DECODE_PARTIAL || epilogue == DRL_DECODE_SWIGLU, "unknown epilogue");
+  DRL_CHECK_ARG(epi == EPI_PARTIAL ? partials != nullptr : (out_packed != nullptr && aligned16(out_packed)),
+                "missing output");
+  DRL_CHECK_ARG(epi == EPI_PARTIAL || N % 32 == 0, "SwiGLU needs N % 32 == 0");
+  DgPlan p{};
+  if (!plan_decode_gemm(M, N, K, epi, p))
+    return fail(DRL_ERR_UNSUPPORTED, "decode GEMM: unsupported shape M=%lld N=%lld K=%lld", (long long)M,
+                (long long)N, (long long)K);
+  DgArgs a{static_cast<const uint16_t*>(x_packed), static_cast<const uint16_t*>(w_packed), static_cast<int>(M),
+           static_cast<int>(N), static_cast<int>(K), p.mbt, static_cast<int>(K / 16), p.tiles,
+           static_cast<int>(N / 2), partials, static_cast<uint16_t*>(out_packed)};
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (p.mb == 1) {
+    if (epi == EPI_PARTIAL) launch_dg<1, EPI_PARTIAL>(a, p, s);
+    else launch_dg<1, EPI_SWIGLU>(a, p, s);
+  } else {
+    if (epi == EPI_PARTIAL) launch_dg<2, EPI_PARTIAL>(a, p, s);
+    else launch_dg<2, EPI_SWIGLU>(a, p, s);
+  }
+  DRL_LAUNCH_CHECK();
+  return DRL_OK;
+}
+
+int drl_decode_rmsnorm(const float* x_in, const float* partials, int32_t nsplit, float* x_out, const float* weight,
+                       void* y, int64_t M, int64_t H, int64_t mbt, float eps, void* stream) {
+  using namespace drl;
+  DRL_CHECK_ARG(x_in && weight && y, "NULL input");
+  DRL_CHECK_ARG(M >= 1 && H >= 8 && H % 8 == 0 && H <= 8 * 128 * 4, "bad shape (H %% 8 == 0, H <= 4096)");
+  DRL_CHECK_ARG(partials == nullptr || nsplit >= 1, "nsplit < 1");
+  DRL_CHECK_ARG(mbt == 0 || mbt * 32 >= M, "mbt too small");
+  DRL_CHECK_ARG(aligned16(x_in) && aligned16(y) && (x_out == nullptr || aligned16(x_out)) &&
+                    (partials == nullptr || aligned16(partials)),
+                "16-byte aligned buffers needed");
+  const int ch = static_cast<int>((H / 8 + 127) / 128);
+  const int ns = partials ? nsplit : 0;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const dim3 grid(static_cast<unsigned>(M));
+#define DRL_DRN(C, NS) hipLaunchKernelGGL((dec_rmsnorm_kernel<C, NS>), grid, dim3(128), 0, s, x_in, partials, ns, x_out, \
+                                          weight, static_cast<uint16_t*>(y), M, H, mbt, eps)
+#define DRL_DRN_NS(C)                \
+  switch (ns) {                      \
+    case 0: DRL_DRN(C, 0); break;    \
+    case 1: DRL_DRN(C, 1); break;    \
+    case 2: DRL_DRN(C, 2); break;    \
+    case 4: DRL_DRN(C, 4); break;    \
+    case 7: DRL_DRN(C, 7); break;    \
+    default: DRL_DRN(C, -1); break;  \
+  }
+  if (ch <= 1) {
+    DRL_DRN_NS(1)
+  } else if (ch == 2) {
+    DRL_DRN_NS(2)
+  } else {
+    DRL_DRN(4, -1);
+  }
+#undef DRL_DRN_NS
+#undef DRL_DRN
+  DRL_LAUNCH_CHECK();
+  return DRL_OK;
+}
+
+int drl_decode_rope(const float* partials, int32_t nsplit, const void* bias, const int64_t* position_ids,
+                    const float* cos_t, const float* sin_t, int64_t maxpos, int64_t B, int64_t Hq, int64_t Hkv,
+                    int64_t D, void* q, void* k_cache, void* v_cache, void* vt_cache, int64_t Tk, int64_t ld_vt,
+                    int64_t koff, const int64_t* koff_dev, void* stream) {
+  using namespace drl;
+  DRL_CHECK_ARG(partials && bias && position_ids && cos_t && sin_t && q && k_cache && (v_cache || vt_cache),
+                "NULL input");
+  DRL_CHECK_ARG(nsplit >= 1 && B >= 1 && Hq >= 1 && Hkv >= 1 && Hq % Hkv == 0 && D % 2 == 0 && Tk >= 1, "bad shape");
+  DRL_CHECK_ARG(vt_cache == nullptr || ld_vt >= Tk, "ld_vt < Tk");
+  DRL_CHECK_ARG(koff_dev != nullptr || (koff >= 0 && koff < Tk), "key offset out of range");
+  DecRopeArgs a{partials, nsplit, static_cast<const uint16_t*>(bias), position_ids, cos_t, sin_t,
+                static_cast<uint16_t*>(q), static_cast<uint16_t*>(k_cache), static_cast<uint16_t*>(v_cache),
+                static_cast<uint16_t*>(vt_cache), B, Hq, Hkv, D, Tk, ld_vt, maxpos, koff, koff_dev};
+  const int64_t n = B * (Hq + 2 * Hkv) * (D / 2);
+  hipLaunchKernelGGL(dec_rope_kernel, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), a);
+  DRL_LAUNCH_CHECK();
+  return DRL_OK;
+}
+
+}  // extern "C"

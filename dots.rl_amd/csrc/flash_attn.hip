@@ -695,7 +695,8 @@ struct DecodeArgs {
   int64_t qpos;
   int64_t Hkv, G, ld_k, ld_vt, L;
   float scale_log2;
-  uint16_t* out;  // (B, Hkv, G, D)
+  uint16_t* out;  // (B, Hkv, G, D), or fragment-packed (out_mbt 32-row blocks) for the decode o_proj GEMM
+  int64_t out_mbt;
   float* slabs;        // split-K: (B*Hkv, splits, 64 + 32*D) fp32 partial states (m, l, unnormalised o)
   unsigned* tickets;   // split-K: (B*Hkv) arrival counters, zero between launches
 };
@@ -778,6 +779,12 @@ __device__ __forceinline__ void dec_block(const DecBlock<D>& blk, const bf16x8 (
     for (int s = 0; s < 2; ++s)
       o[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(blk.vf[mt][s]), as_bf16x8(pb[s]), o[mt], 0, 0, 0);
   }
+}
+
+// output element (sequence b, column k of (Hq * D)): row-major or fragment-packed (csrc/decode_gemm.hip layout)
+__device__ __forceinline__ uint16_t* dec_out_ptr(const DecodeArgs& a, int64_t b, int64_t k, int64_t row_off) {
+  if (a.out_mbt == 0) return a.out + row_off;  // row-major: row_off is the (b, k) offset
+  return a.out + ((((k >> 4) * a.out_mbt + (b >> 5)) * 64 + ((k >> 3) & 1) * 32 + (b & 31)) * 8 + (k & 7));
 }
 
 template <int D, int NW>
@@ -900,7 +907,7 @@ __global__ __launch_bounds__(64 * NW) void decode_mfma_kernel(DecodeArgs a) {
     if (tid == 0) __hip_atomic_store((__attribute__((address_space(1))) unsigned*)(a.tickets + bh), 0u,
                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (qi >= a.G) return;
-    uint16_t* orow = a.out + (bh * a.G + qi) * D;
+    const int64_t kq = ((bh % a.Hkv) * a.G + qi) * D;  // column of (b, query head) in (Hq * D)
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -908,7 +915,8 @@ __global__ __launch_bounds__(64 * NW) void decode_mfma_kernel(DecodeArgs a) {
         u16x4 wv;
 #pragma unroll
         for (int j = 0; j < 4; ++j) wv[j] = to_bf16_bits(acc[mt][4 * c + j] * inv);
-        *reinterpret_cast<u16x4*>(orow + 32 * mt + 8 * c + 4 * h) = wv;
+        const int64_t k = kq + 32 * mt + 8 * c + 4 * h;
+        *reinterpret_cast<u16x4*>(dec_out_ptr(a, b, k, (bh * a.G + qi) * D + 32 * mt + 8 * c + 4 * h)) = wv;
       }
     return;
   }
@@ -924,7 +932,7 @@ __global__ __launch_bounds__(64 * NW) void decode_mfma_kernel(DecodeArgs a) {
     ll += s_l[v][qi] * sc[v];
   }
   const float inv = ll > 0.f ? 1.f / ll : 0.f;
-  uint16_t* orow = a.out + (bh * a.G + qi) * D;
+  const int64_t kq = ((bh % a.Hkv) * a.G + qi) * D;  // column of (b, query head) in (Hq * D)
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
 #pragma unroll
@@ -937,7 +945,8 @@ __global__ __launch_bounds__(64 * NW) void decode_mfma_kernel(DecodeArgs a) {
         for (int v = 0; v < NW; ++v) acc = fmaf(s_o[v][mt][4 * c + j][lane], sc[v], acc);
         wv[j] = to_bf16_bits(acc * inv);
       }
-      *reinterpret_cast<u16x4*>(orow + 32 * mt + 8 * c + 4 * h) = wv;
+      const int64_t k = kq + 32 * mt + 8 * c + 4 * h;
+      *reinterpret_cast<u16x4*>(dec_out_ptr(a, b, k, (bh * a.G + qi) * D + 32 * mt + 8 * c + 4 * h)) = wv;
     }
   }
 }
@@ -1030,10 +1039,12 @@ size_t drl_decode_attention_vt_workspace_bytes(int64_t B, int64_t Hkv, int64_t D
 int drl_decode_attention_vt(const void* q, const void* k_cache, const void* vt_cache, int32_t dt,
                             const uint8_t* key_valid, int64_t ld_valid, const int64_t* qpos_ptr, int64_t qpos,
                             int64_t B, int64_t Hkv, int64_t G, int64_t D, int64_t ld_k, int64_t ld_vt, int64_t L,
-                            float scale, void* out, void* workspace, size_t workspace_bytes, void* stream) {
+                            float scale, void* out, int64_t out_mbt, void* workspace, size_t workspace_bytes,
+                            void* stream) {
   using namespace drl;
   DRL_CHECK_ARG(q && k_cache && vt_cache && key_valid && out, "NULL input");
   DRL_CHECK_ARG(dt == DRL_BF16, "MFMA decode attention runs on bf16");
+  DRL_CHECK_ARG(out_mbt == 0 || out_mbt * 32 >= B, "out_mbt too small for B rows");
   DRL_CHECK_ARG(D == 64 || D == 128, "head_dim must be 64 or 128");
   DRL_CHECK_ARG(B >= 1 && Hkv >= 1 && G >= 1 && G <= 32 && L >= 1 && L <= ld_k && L <= ld_vt, "bad shape");
   DRL_CHECK_ARG(ld_vt % 4 == 0 && ld_valid % 4 == 0 && (reinterpret_cast<uintptr_t>(key_valid) & 3u) == 0 &&
@@ -1044,7 +1055,7 @@ int drl_decode_attention_vt(const void* q, const void* k_cache, const void* vt_c
                 "misaligned operand");
   DecodeArgs a{static_cast<const uint16_t*>(q), static_cast<const uint16_t*>(k_cache),
                static_cast<const uint16_t*>(vt_cache), key_valid, ld_valid, qpos_ptr, qpos, Hkv, G, ld_k, ld_vt, L,
-               scale * 1.4426950408889634f, static_cast<uint16_t*>(out), nullptr, nullptr};
+               scale * 1.4426950408889634f, static_cast<uint16_t*>(out), out_mbt, nullptr, nullptr};
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int64_t wgs = B * Hkv, cus = cu_count();
   const int splits = decode_splits(B, Hkv, L);

@@ -545,16 +545,101 @@ def _linear_workspace(device, nbytes, kind="linear"):
     return ws
 
 
-def decode_attention_vt(q, k_cache, vt_cache, key_valid, L, out, qpos=None, qpos_dev=None):
-    """MFMA decode attention: q (B,Hkv,G,D) bf16, k_cache (B,Hkv,ld_k,D), vt_cache (B,Hkv,D,ld_vt)."""
+def decode_attention_vt(q, k_cache, vt_cache, key_valid, L, out, qpos=None, qpos_dev=None, out_mbt=0):
+    """MFMA decode attention: q (B,Hkv,G,D) bf16, k_cache (B,Hkv,ld_k,D), vt_cache (B,Hkv,D,ld_vt). ``out_mbt`` > 0:
+    ``out`` is the fragment-packed (B, Hq*D) panel of the decode o_proj GEMM (decode_gemm layout)."""
     _dev(q, k_cache, vt_cache, key_valid, out)
     B, Hkv, G, D = q.shape
     assert q.is_contiguous() and k_cache.is_contiguous() and out.is_contiguous() and vt_cache.stride(-1) == 1
+    assert out_mbt == 0 or out.numel() >= out_mbt * 32 * Hkv * G * D
     assert vt_cache.stride(-2) * D == vt_cache.stride(1) and key_valid.dtype == torch.uint8
     qp = L - 1 if qpos is None else int(qpos)
     nws = lib().drl_decode_attention_vt_workspace_bytes(B, Hkv, D, L)
     ws = _linear_workspace(q.device, nws, "decode_attention") if nws else None
     check(lib().drl_decode_attention_vt(_p(q), _p(k_cache), _p(vt_cache), _edt(q), _p(key_valid), key_valid.stride(0),
                                         _p(qpos_dev), qp, B, Hkv, G, D, k_cache.shape[2], vt_cache.stride(-2), L,
-                                        1.0 / math.sqrt(D), _p(out), _p(ws), nws, _stream()), "drl_decode_attention_vt")
+                                        1.0 / math.sqrt(D), _p(out), int(out_mbt), _p(ws), nws, _stream()),
+          "drl_decode_attention_vt")
     return out
+
+
+# ------------------------------------------------------------------------------ decode projections (packed)
+DECODE_PARTIAL, DECODE_SWIGLU = 0, 1
+
+
+def decode_gemm_plan(M, N, K, swiglu=False):
+    """(ksplit, mbt) of drl_decode_gemm for this shape, or None when unsupported (K % 64, M > 128)."""
+    ks, mbt = ctypes.c_int32(0), ctypes.c_int32(0)
+    rc = lib().drl_decode_gemm_plan(M, N, K, DECODE_SWIGLU if swiglu else DECODE_PARTIAL, ctypes.byref(ks),
+                                    ctypes.byref(mbt))
+    return (ks.value, mbt.value) if rc == 0 else None
+
+
+def decode_pack_weight(w, swiglu=False, out=None):
+    """Fragment-packed copy of W (N, K) bf16 for drl_decode_gemm (swiglu: W = [gate | up])."""
+    _dev(w)
+    assert w.dim() == 2 and w.stride(1) == 1 and w.dtype == torch.bfloat16
+    N, K = w.shape
+    n = lib().drl_decode_pack_weight_elems(N, K, int(swiglu))
+    if out is None:
+        out = torch.empty(n, dtype=torch.bfloat16, device=w.device)
+    assert out.numel() >= n and out.is_contiguous()
+    check(lib().drl_decode_pack_weight(_p(w), w.stride(0), N, K, int(swiglu), _p(out), _stream()),
+          "drl_decode_pack_weight")
+    return out
+
+
+def pack_activations(x, mbt):
+    """Row-major (M, K) -> fragment-packed panel with mbt 32-row blocks (host-side layout helper for tests:
+    element (m, k) at ((k//16 * mbt + m//32) * 64 + ((k//8) % 2) * 32 + m % 32) * 8 + k % 8)."""
+    M, K = x.shape
+    xp = torch.zeros(mbt * 32, K, dtype=x.dtype, device=x.device)
+    xp[:M] = x
+    return xp.view(mbt, 32, K // 16, 2, 8).permute(2, 0, 3, 1, 4).contiguous().view(-1)
+
+
+def unpack_activations(xp, M, K, mbt):
+    return xp.view(K // 16, mbt, 2, 32, 8).permute(1, 3, 0, 2, 4).reshape(mbt * 32, K)[:M]
+
+
+def decode_gemm(x_packed, w_packed, M, N, K, swiglu=False, partials=None, out_packed=None):
+    """x (packed, M rows) @ W^T (packed): fp32 partials (ksplit, M, N), or with ``swiglu`` the packed activation
+    bf16(bf16(silu(g)) * u) (mbt blocks, N/2 columns)."""
+    _dev(x_packed, w_packed)
+    plan = decode_gemm_plan(M, N, K, swiglu)
+    assert plan is not None, f"decode GEMM does not take M={M} N={N} K={K}"
+    ks, mbt = plan
+    assert x_packed.numel() >= mbt * 32 * K
+    if swiglu:
+        if out_packed is None:
+            out_packed = torch.zeros(mbt * 32 * (N // 2), dtype=torch.bfloat16, device=x_packed.device)
+    elif partials is None:
+        partials = torch.empty(ks, M, N, dtype=torch.float32, device=x_packed.device)
+    if swiglu:
+        assert out_packed.numel() >= mbt * 32 * (N // 2) and out_packed.dtype == torch.bfloat16
+    else:
+        assert partials.numel() >= ks * M * N and partials.dtype == torch.float32 and partials.is_contiguous()
+    check(lib().drl_decode_gemm(_p(x_packed), _p(w_packed), M, N, K, DECODE_SWIGLU if swiglu else DECODE_PARTIAL,
+                                _p(partials), _p(out_packed), _stream()), "drl_decode_gemm")
+    return out_packed if swiglu else partials
+
+
+def decode_rmsnorm(x_in, partials, x_out, weight, y, eps, mbt=0):
+    """x_out = x_in + bf16(sum partials); y = RMSNorm(x_out) * w in bf16, packed (mbt > 0) or row-major."""
+    _dev(x_in, weight, y)
+    M, H = x_in.shape[0], x_in.shape[-1]
+    ns = partials.shape[0] if partials is not None else 0
+    check(lib().drl_decode_rmsnorm(_p(x_in), _p(partials), ns, _p(x_out), _p(weight), _p(y), M, H, int(mbt),
+                                   float(eps), _stream()), "drl_decode_rmsnorm")
+
+
+def decode_rope(partials, bias, position_ids, cos_t, sin_t, Hq, Hkv, D, q, k_cache, vt_cache=None, v_cache=None,
+                koff=0, koff_dev=None):
+    """One decode token: qkv = bf16(sum partials + bias) -> RoPE -> q, k cache row koff, V^T / V cache."""
+    _dev(partials, bias, position_ids, q, k_cache)
+    ns, B = partials.shape[0], partials.shape[1]
+    Tk = k_cache.shape[2]
+    ld_vt = vt_cache.stride(-2) if vt_cache is not None else 0
+    check(lib().drl_decode_rope(_p(partials), ns, _p(bias), _p(position_ids), _p(cos_t), _p(sin_t), cos_t.shape[0], B,
+                                Hq, Hkv, D, _p(q), _p(k_cache), _p(v_cache), _p(vt_cache), Tk, ld_vt, int(koff),
+                                _p(koff_dev), _stream()), "drl_decode_rope")

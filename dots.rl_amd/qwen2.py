@@ -542,6 +542,91 @@ class Qwen2Model:
         return self._final_norm(x, delta)[:, 0]
 
 
+class PackedDecode:
+    """Decode step on fragment-packed operands (csrc/decode_gemm.hip) for one rollout of B <= 256 sequences:
+    per layer decode RMSNorm (packed out) -> qkv GEMM (fp32 K-slice partials) -> decode RoPE (sums the
+    partials + bias, writes q and the caches) -> MFMA decode attention (packed out) -> o_proj GEMM ->
+    decode RMSNorm (adds the o_proj partials) -> gate_up GEMM with the SwiGLU epilogue (packed out) ->
+    down_proj GEMM, whose partials the next layer's RMSNorm adds. Eight launches per layer instead of nine,
+    every projection a one-round-trip weight stream. The weights are packed once per rollout from the bf16
+    compute copy (they change at every optimizer step); every buffer is preallocated so the step is
+    graph-capturable. Module math is the unpacked decode path's (bf16 module outputs, fp32 residual)."""
+
+    @staticmethod
+    def supported(model, B):
+        cfg = model.cfg
+        H, I, D = cfg.hidden_size, cfg.intermediate_size, cfg.head_dim
+        NQ = (cfg.num_attention_heads + 2 * cfg.num_key_value_heads) * D
+        # up to 256 rows: at 512 (one GPU holding the whole batch) hipBLASLt's tiles are as fast and the
+        # unpacked path is kept (tools/kernel_bench.py --only decode_gemm; bench step 1.22 vs 1.55 s rollout)
+        return (B <= 256 and model.dtype == torch.bfloat16 and D in (64, 128) and H % 64 == 0 and I % 64 == 0
+                and (cfg.num_attention_heads * D) % 64 == 0 and I % 16 == 0
+                and all(native.decode_gemm_plan(B, n, k, sw) is not None
+                        for n, k, sw in ((NQ, H, False), (H, cfg.num_attention_heads * D, False), (2 * I, H, True),
+                                         (H, I, False))))
+
+    def __init__(self, model, B):
+        cfg, s, dev = model.cfg, model.store, model.store.device
+        self.model = model
+        self.B = B
+        H, I, D = cfg.hidden_size, cfg.intermediate_size, cfg.head_dim
+        Hq, Hkv = cfg.num_attention_heads, cfg.num_key_value_heads
+        self.NQ = (Hq + 2 * Hkv) * D
+        self.HD = Hq * D
+        self.plans = {"qkv": native.decode_gemm_plan(B, self.NQ, H), "o": native.decode_gemm_plan(B, H, self.HD),
+                      "gu": native.decode_gemm_plan(B, 2 * I, H, True), "d": native.decode_gemm_plan(B, H, I)}
+        self.mbt = self.plans["qkv"][1]
+        assert all(p[1] == self.mbt for p in self.plans.values())
+        bf = torch.bfloat16
+        self.w = []
+        for i in range(cfg.num_hidden_layers):
+            p = f"layers.{i}."
+            self.w.append(dict(qkv=native.decode_pack_weight(s.w(p + "qkv_proj.weight")),
+                               o=native.decode_pack_weight(s.w(p + "o_proj")),
+                               gu=native.decode_pack_weight(s.w(p + "gate_up_proj"), swiglu=True),
+                               d=native.decode_pack_weight(s.w(p + "down_proj"))))
+        rows = self.mbt * 32
+        self.h_p = torch.zeros(rows * H, dtype=bf, device=dev)        # RMSNorm out (packed; pad rows stay 0)
+        self.attn_p = torch.zeros(rows * self.HD, dtype=bf, device=dev)
+        self.a_p = torch.zeros(rows * I, dtype=bf, device=dev)        # SwiGLU out
+        self.part_qkv = torch.empty(self.plans["qkv"][0], B, self.NQ, device=dev)
+        self.part_o = torch.empty(self.plans["o"][0], B, H, device=dev)
+        self.part_d = torch.empty(self.plans["d"][0], B, H, device=dev)
+        self.x = torch.empty(B, H, device=dev)                         # fp32 residual stream
+        self.q = torch.empty(B, Hkv, Hq // Hkv, D, dtype=bf, device=dev)
+        self.h_out = torch.empty(B, H, dtype=bf, device=dev)
+
+    @torch.no_grad()
+    def step(self, cache, tokens, positions, kpos_dev):
+        """One token per sequence at device cache position kpos_dev; returns the final-norm hidden (B, H)."""
+        m = self.model
+        cfg, s = m.cfg, m.store
+        B, H, I = self.B, cfg.hidden_size, cfg.intermediate_size
+        Hq, Hkv, D = cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim
+        eps, mbt = cfg.rms_norm_eps, self.mbt
+        self.x.copy_(F.embedding(tokens.view(-1), s.w("embed_tokens")))
+        cache.valid.index_fill_(1, kpos_dev, 1)
+        pos = positions.view(-1)
+        Lk = cache.k[0].shape[2]
+        prev = None
+        for i in range(cfg.num_hidden_layers):
+            p, w = f"layers.{i}.", self.w[i]
+            native.decode_rmsnorm(self.x, prev, self.x, s.w(p + "input_layernorm"), self.h_p, eps, mbt=mbt)
+            native.decode_gemm(self.h_p, w["qkv"], B, self.NQ, H, partials=self.part_qkv)
+            native.decode_rope(self.part_qkv, s.w(p + "qkv_proj.bias"), pos, m.cos, m.sin, Hq, Hkv, D, self.q,
+                               cache.k[i], vt_cache=cache.vt[i], koff_dev=kpos_dev)
+            native.decode_attention_vt(self.q, cache.k[i], cache.vt[i], cache.valid, Lk, self.attn_p,
+                                       qpos_dev=kpos_dev, out_mbt=mbt)
+            native.decode_gemm(self.attn_p, w["o"], B, H, self.HD, partials=self.part_o)
+            native.decode_rmsnorm(self.x, self.part_o, self.x, s.w(p + "post_attention_layernorm"), self.h_p, eps,
+                                  mbt=mbt)
+            native.decode_gemm(self.h_p, w["gu"], B, 2 * I, H, swiglu=True, out_packed=self.a_p)
+            native.decode_gemm(self.a_p, w["d"], B, H, I, partials=self.part_d)
+            prev = self.part_d
+        native.decode_rmsnorm(self.x, prev, None, s.w("norm"), self.h_out, eps, mbt=0)
+        return self.h_out
+
+
 def flops_per_token(cfg: Qwen2Config, seqlen: int) -> float:
     """flops_counter.py:135-167 convention: 2 * N_dense per token forward (embedding + lm_head counted)
     plus attention 2 * 2 * s * d * h * L."""

@@ -16,7 +16,7 @@ import torch
 
 from . import native
 from .protocol import DataProto, TensorBatch
-from .qwen2 import KVCache, Qwen2Model
+from .qwen2 import KVCache, PackedDecode, Qwen2Model
 from .torch_functional import get_response_mask
 
 
@@ -109,10 +109,16 @@ class MI355XRollout:
         heuristics for the decode shapes, outside capture); the captured body advances t itself."""
         m = self.module
         t_dev = torch.ones(1, dtype=torch.int64, device=responses.device)
+        B = responses.shape[0]
+        packed = PackedDecode(m, B) if self.config.get("packed_decode", True) and PackedDecode.supported(m, B) else None
+        self.last_packed_decode = packed is not None
 
         def body():
             tok = responses.index_select(1, t_dev - 1)
-            h = m.decode_step_dev(cache, tok, last_pos + t_dev, t_dev + (P - 1))
+            if packed is not None:
+                h = packed.step(cache, tok, last_pos + t_dev, t_dev + (P - 1))
+            else:
+                h = m.decode_step_dev(cache, tok, last_pos + t_dev, t_dev + (P - 1))
             native.select_tokens(m.logits(h), responses[:, 0], step=0, dev_step=t_dev, **sel)
             t_dev.add_(1)
 
@@ -122,4 +128,4 @@ class MI355XRollout:
             body()
         for _ in range(2, R):
             graph.replay()
-        del graph
+        del graph, packed

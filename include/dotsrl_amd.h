@@ -295,7 +295,8 @@ int drl_flash_attn_fwd(const void* q, const void* k, const void* vt, int32_t dt,
                        int64_t ld_k, int64_t ld_vt, int64_t qoff, float scale, void* out, float* lse, void* stream);
 /* Decode attention on MFMA over a cache with V head-dim-major: q (B,Hkv,G,D) bf16 (one token), k_cache
  * (B,Hkv,ld_k,D), vt_cache (B,Hkv,D,ld_vt); keys j < L with key_valid[b, j] && j <= qpos (device scalar
- * *qpos_ptr when non-NULL). out (B,Hkv,G,D). G <= 32, head_dim 64 or 128. Same semantics as
+ * *qpos_ptr when non-NULL). out (B,Hkv,G,D), or with out_mbt > 0 the (B, Hq*D) panel fragment-packed for
+ * drl_decode_gemm (out_mbt >= B/32 blocks). G <= 32, head_dim 64 or 128. Same semantics as
  * drl_decode_attention (the VALU kernel over a row-major V cache used by the fp32 parity model).
  * Small batches split the keys over workgroups (partial softmax states merged in split order by the last
  * arriving split): workspace of drl_decode_attention_vt_workspace_bytes(B, Hkv, D, L) bytes (0 = none
@@ -306,7 +307,8 @@ void drl_decode_attention_set_plan(int32_t waves, int32_t splits);
 int drl_decode_attention_vt(const void* q, const void* k_cache, const void* vt_cache, int32_t dt,
                             const uint8_t* key_valid, int64_t ld_valid, const int64_t* qpos_ptr, int64_t qpos,
                             int64_t B, int64_t Hkv, int64_t G, int64_t D, int64_t ld_k, int64_t ld_vt, int64_t L,
-                            float scale, void* out, void* workspace, size_t workspace_bytes, void* stream);
+                            float scale, void* out, int64_t out_mbt, void* workspace, size_t workspace_bytes,
+                            void* stream);
 /* Backward of drl_flash_attn_fwd for Tq == Tk == T, qoff = 0 (the training forward), recomputing P from lse:
  * q (B,Hkv,G,T,D), k / v (B,Hkv,T,D) row-major, kt (B,Hkv,D,ld_t) head-dim-major copy of k (written by
  * drl_rope_qkv_fwd), o and dout (B,T,Hkv*G*D), lse from the forward. delta: (B,Hkv,G,T) fp32 scratch.
@@ -353,6 +355,40 @@ int drl_linear_logprob_dlogits(const void* hidden, int64_t ld_h, const void* wei
                                int64_t N, int64_t H, int64_t V, float temperature, const float* dlogp,
                                const float* dentropy, const float* lse, const float* entropy, void* dlogits_t,
                                int64_t ld_dl, void* stream);
+
+/* ---- Decode-step projections on fragment-packed operands (csrc/decode_gemm.hip). Replace the per-token
+ * nn.Linear / RMSNorm / rotary calls of HF generate (hf_rollout.py:112-124 -> modeling_qwen2) for 1..512
+ * token rows. Packed layout of an activation panel (M rows, K columns, MBT 32-row blocks, MBT >= M/32):
+ * element (m, k) at ((k/16 * MBT + m/32) * 64 + ((k/8) & 1) * 32 + m % 32) * 8 + k % 8; rows >= M must hold
+ * zeros (allocate zero-filled, never write them). */
+typedef enum drl_decode_epilogue {
+  DRL_DECODE_PARTIAL = 0, /* fp32 partial sums per K slice: partials (ksplit, M, N) */
+  DRL_DECODE_SWIGLU = 1   /* W = [gate | up] packed with swiglu=1: bf16(bf16(silu(g)) * u) packed (MBT, N/2) */
+} drl_decode_epilogue;
+/* ksplit (K slices = partial sums the consumer adds) and mbt (token blocks the packed panels need). */
+int drl_decode_gemm_plan(int64_t M, int64_t N, int64_t K, int32_t epilogue, int32_t* ksplit, int32_t* mbt);
+/* Tuning hook (tools/kernel_bench.py): force 32-row token blocks per workgroup (1, 2) and k16 steps per wave
+ * (1, 2, 4, 7, 14; 19 with one block); 0 = automatic. */
+void drl_decode_gemm_set_plan(int32_t mb, int32_t ksw);
+/* Elements of the packed copy of W (N, K) bf16 (swiglu: W = [gate | up], blocks interleave 16 + 16 rows). */
+size_t drl_decode_pack_weight_elems(int64_t N, int64_t K, int32_t swiglu);
+int drl_decode_pack_weight(const void* w, int64_t ld, int64_t N, int64_t K, int32_t swiglu, void* packed, void* stream);
+/* y = x W^T with x packed (M rows), W packed; K % 64 == 0, 1 <= M <= 512. PARTIAL writes fp32 partials,
+ * SWIGLU writes the activation packed for the down projection. */
+int drl_decode_gemm(const void* x_packed, const void* w_packed, int64_t M, int64_t N, int64_t K, int32_t epilogue,
+                    float* partials, void* out_packed, void* stream);
+/* x_out = x_in + bf16(sum of nsplit partials (nsplit, M, H)) (partials may be NULL: no delta), y = bf16(w *
+ * x_out * rsqrt(mean(x_out^2) + eps)) packed with mbt blocks, or row-major (M, H) when mbt == 0
+ * (drl_add_rmsnorm_fwd semantics). H % 8 == 0. */
+int drl_decode_rmsnorm(const float* x_in, const float* partials, int32_t nsplit, float* x_out, const float* weight,
+                       void* y, int64_t M, int64_t H, int64_t mbt, float eps, void* stream);
+/* One decode token per sequence: qkv = bf16(sum of nsplit partials (nsplit, B, (Hq+2Hkv)D) + bias), then
+ * drl_rope_qkv_fwd's rotation: q (B, Hkv, G, D), k_cache (B, Hkv, Tk, D) row koff, V into vt_cache
+ * (B, Hkv, D, ld_vt) column koff and/or v_cache (B, Hkv, Tk, D); koff_dev (device int64) overrides koff. */
+int drl_decode_rope(const float* partials, int32_t nsplit, const void* bias, const int64_t* position_ids,
+                    const float* cos_t, const float* sin_t, int64_t maxpos, int64_t B, int64_t Hq, int64_t Hkv,
+                    int64_t D, void* q, void* k_cache, void* v_cache, void* vt_cache, int64_t Tk, int64_t ld_vt,
+                    int64_t koff, const int64_t* koff_dev, void* stream);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,223 @@
+"""Decode-step projections on fragment-packed operands (csrc/decode_gemm.hip) and their producers /
+consumers, each against a plain PyTorch fp32 reference of the same bf16 module math:
+
+* pack / unpack of the activation panel is a bijection (host helper == device layout, via the GEMM);
+* drl_decode_gemm PARTIAL: sum of the fp32 partial slices == x W^T in fp32 (bf16 operands): 1e-5 relative
+  (fp32 accumulation, different order);
+* SWIGLU: bf16(bf16(silu(bf16 g)) * bf16 u) — within 1 bf16 ulp of the reference on 99.9 % of entries and
+  2^-6 of the panel's largest entry everywhere (the fp32 sums differ in order before the three roundings);
+* drl_decode_rmsnorm == drl_add_rmsnorm_fwd fed the bf16-rounded delta (bit-exact when the delta is the same);
+* drl_decode_rope == drl_rope_qkv_fwd on the same bf16 qkv (bit-exact);
+* decode attention with a packed output == its row-major output, packed (bit-exact).
+"""
+
+import math
+
+import pytest
+import torch
+
+from dots.rl_amd import native
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+BF = torch.bfloat16
+
+
+def rnd(*shape, scale=1.0, seed=0, dtype=BF):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    return (torch.randn(*shape, device=DEV, generator=g) * scale).to(dtype)
+
+
+@pytest.mark.parametrize("M", [1, 7, 32, 33, 64, 100, 128])
+@pytest.mark.parametrize("N,K", [(1152, 896), (896, 896), (896, 4864), (96, 64), (200, 128)])
+def test_decode_gemm_partials(M, N, K):
+    plan = native.decode_gemm_plan(M, N, K)
+    assert plan is not None
+    ks, mbt = plan
+    x = rnd(M, K, seed=M)
+    w = rnd(N, K, scale=0.05, seed=N + K)
+    xp = native.pack_activations(x, mbt)
+    assert torch.equal(native.unpack_activations(xp, M, K, mbt), x)
+    wp = native.decode_pack_weight(w)
+    part = native.decode_gemm(xp, wp, M, N, K)
+    assert part.shape == (ks, M, N)
+    ref = x.float() @ w.float().t()
+    got = part.sum(0)
+    err = (got - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 1e-5, err
+    assert torch.equal(part, native.decode_gemm(xp, wp, M, N, K))  # deterministic
+
+
+@pytest.mark.parametrize("M", [5, 64, 128])
+@pytest.mark.parametrize("I,K", [(4864, 896), (128, 64)])
+def test_decode_gemm_swiglu_packed(M, I, K):
+    ks, mbt = native.decode_gemm_plan(M, 2 * I, K, swiglu=True)
+    assert ks == 1
+    x = rnd(M, K, seed=3)
+    w = rnd(2 * I, K, scale=0.05, seed=4)
+    out = native.decode_gemm(native.pack_activations(x, mbt), native.decode_pack_weight(w, swiglu=True), M, 2 * I, K,
+                             swiglu=True)
+    a = native.unpack_activations(out, M, I, mbt).float()
+    gu = (x.float() @ w.float().t()).to(BF).float()
+    g, u = gu[:, :I], gu[:, I:]
+    ref = ((g / (1 + torch.exp(-g))).to(BF).float() * u).to(BF).float()
+    ulp = ref.abs().clamp_min(1e-30) * 2.0 ** -7
+    bad = (a - ref).abs() > ulp * 1.01
+    assert bad.float().mean().item() < 1e-3
+    # where a differently-ordered fp32 sum rounds g or u to the neighbouring bf16 value the output moves by that
+    # input ulp scaled through silu / the product: bounded relative to the panel's scale
+    assert (a - ref).abs().max().item() <= 2.0 ** -6 * ref.abs().max().item()
+    # rows past M of the packed panel stay zero (the next GEMM reads them)
+    assert torch.count_nonzero(native.unpack_activations(out, mbt * 32, I, mbt)[M:]) == 0
+
+
+@pytest.mark.parametrize("M,H,ns", [(64, 896, 4), (3, 64, 1), (128, 896, 19)])
+def test_decode_rmsnorm_matches_add_rmsnorm(M, H, ns):
+    x = torch.randn(M, H, device=DEV)
+    part = torch.randn(ns, M, H, device=DEV) * 0.3
+    w = torch.rand(H, device=DEV) + 0.5
+    mbt = (M + 31) // 32
+    yp = torch.zeros(mbt * 32 * H, dtype=BF, device=DEV)
+    x_out = torch.empty_like(x)
+    native.decode_rmsnorm(x, part, x_out, w, yp, 1e-6, mbt=mbt)
+    delta = part.sum(0).to(BF)  # same fixed order: k = 0, 1, ...
+    s = part[0].clone()
+    for k in range(1, ns):
+        s += part[k]
+    delta = s.to(BF)
+    x2, y2 = torch.empty_like(x), torch.empty(M, H, dtype=BF, device=DEV)
+    native.add_rmsnorm_fwd(x.view(M, 1, H), delta.view(M, 1, H), x2.view(M, 1, H), w, y2.view(M, 1, H), None, 1e-6)
+    assert torch.equal(x_out, x2)
+    y = native.unpack_activations(yp, M, H, mbt)
+    assert (y.float() - y2.float()).abs().max().item() <= 2.0 ** -7 * y2.float().abs().max().item()
+    # row-major output form, no delta
+    yr = torch.empty(M, H, dtype=BF, device=DEV)
+    native.decode_rmsnorm(x, None, None, w, yr, 1e-6, mbt=0)
+    y3 = torch.empty(M, H, dtype=BF, device=DEV)
+    native.add_rmsnorm_fwd(x.view(M, 1, H), None, None, w, y3.view(M, 1, H), None, 1e-6)
+    assert (yr.float() - y3.float()).abs().max().item() <= 2.0 ** -7 * y3.float().abs().max().item()
+
+
+def test_decode_rope_matches_rope_qkv():
+    B, Hq, Hkv, D, Tk, koff = 64, 14, 2, 64, 40, 17
+    G = Hq // Hkv
+    NQ = (Hq + 2 * Hkv) * D
+    ns = 3
+    part = torch.randn(ns, B, NQ, device=DEV)
+    bias = rnd(NQ, seed=5)
+    pos = torch.randint(0, 1000, (B,), device=DEV)
+    half = D // 2
+    inv = 1.0 / (10000.0 ** (torch.arange(0, D, 2, device=DEV).float() / D))
+    fr = torch.arange(2048, device=DEV).float()[:, None] * inv[None, :half]
+    cos_t, sin_t = fr.cos().contiguous(), fr.sin().contiguous()
+    s = part[0].clone()
+    for k in range(1, ns):
+        s += part[k]
+    qkv = (s + bias.float()).to(BF).view(B, 1, NQ)
+    q1 = torch.empty(B, Hkv, G, 1, D, dtype=BF, device=DEV)
+    k1 = torch.zeros(B, Hkv, Tk, D, dtype=BF, device=DEV)
+    vt1 = torch.zeros(B, Hkv, D, 48, dtype=BF, device=DEV)[..., :Tk]
+    native.rope_qkv_fwd(qkv, pos.view(B, 1), cos_t, sin_t, Hq, Hkv, D, q1, k1, None, koff=koff, vt=vt1)
+    q2 = torch.empty_like(q1)
+    k2 = torch.zeros_like(k1)
+    vt2 = torch.zeros(B, Hkv, D, 48, dtype=BF, device=DEV)[..., :Tk]
+    kd = torch.tensor([koff], device=DEV)
+    native.decode_rope(part, bias, pos, cos_t, sin_t, Hq, Hkv, D, q2, k2, vt_cache=vt2, koff_dev=kd)
+    assert torch.equal(q1, q2) and torch.equal(k1, k2) and torch.equal(vt1, vt2)
+
+
+def test_decode_attention_packed_output():
+    B, Hkv, G, D, Tk, L = 70, 2, 7, 64, 96, 81
+    q = rnd(B, Hkv, G, D, seed=1)
+    k = rnd(B, Hkv, Tk, D, seed=2)
+    vt = rnd(B, Hkv, D, Tk, seed=3)
+    valid = torch.ones(B, Tk, dtype=torch.uint8, device=DEV)
+    valid[:5, :9] = 0
+    out = torch.empty(B, Hkv * G * D, dtype=BF, device=DEV)
+    native.decode_attention_vt(q, k, vt, valid, L, out)
+    mbt = 4
+    outp = torch.zeros(mbt * 32 * Hkv * G * D, dtype=BF, device=DEV)
+    native.decode_attention_vt(q, k, vt, valid, L, outp, out_mbt=mbt)
+    assert torch.equal(native.unpack_activations(outp, B, Hkv * G * D, mbt), out)
+    assert math.isfinite(out.float().sum().item())
+
+
+def _small_model(seed=0, B=48):
+    from dots.rl_amd.qwen2 import KVCache, ParamStore, Qwen2Config, Qwen2Model
+
+    cfg = Qwen2Config.from_dict(dict(vocab_size=512, hidden_size=128, intermediate_size=256, num_hidden_layers=2,
+                                     num_attention_heads=2, num_key_value_heads=1, max_position_embeddings=512,
+                                     rope_theta=10000.0, rms_norm_eps=1e-6, tie_word_embeddings=True))
+    store = ParamStore(cfg, DEV, compute_dtype=BF, trainable=False)
+    store.init_random(seed)
+    return cfg, Qwen2Model(cfg, store)
+
+
+@pytest.mark.parametrize("B", [5, 48, 130])
+def test_packed_decode_step_tracks_unpacked(B):
+    """PackedDecode.step (8 launches per layer on packed operands) against the unpacked decode step on the same
+    prefilled cache and the same teacher-forced tokens: final hidden states and the written K/V agree at bf16
+    level (the projections sum in a different order), step after step."""
+    from dots.rl_amd.qwen2 import KVCache, PackedDecode
+
+    cfg, m = _small_model(B=B)
+    assert PackedDecode.supported(m, B)
+    P, R = 24, 6
+    g = torch.Generator(device=DEV).manual_seed(1)
+    ids = torch.randint(0, 512, (B, P), device=DEV, generator=g)
+    am = torch.ones(B, P, dtype=torch.int64, device=DEV)
+    am[:3, :5] = 0
+    pos = (am.cumsum(-1) - 1).clamp_min(0)
+    caches = []
+    for _ in range(2):
+        c = KVCache(cfg, B, P + R, DEV, BF)
+        m.prefill(c, ids, am, pos)
+        caches.append(c)
+    pk = PackedDecode(m, B)
+    toks = torch.randint(0, 512, (B, R), device=DEV, generator=g)
+    for t in range(1, R):
+        kd = torch.tensor([P + t - 1], device=DEV)
+        h0 = m.decode_step_dev(caches[0], toks[:, t - 1:t], pos[:, -1] + t, kd).float()
+        h1 = pk.step(caches[1], toks[:, t - 1:t], pos[:, -1] + t, kd).float()
+        err = (h0 - h1).abs().max().item() / h0.abs().max().item()
+        assert err < 3e-2, (t, err)
+    n = P + R - 1  # positions written (the last cache slot is never filled here)
+    for i in range(cfg.num_hidden_layers):
+        for a, b in ((caches[0].k[i][:, :, :n], caches[1].k[i][:, :, :n]),
+                     (caches[0].vt[i][..., :n], caches[1].vt[i][..., :n])):
+            assert (a.float() - b.float()).abs().max().item() <= 3e-2 * a.float().abs().max().item()
+    assert torch.equal(caches[0].valid, caches[1].valid)
+
+
+def test_packed_rollout_graph_equals_eager():
+    """The rollout's HIP-graph decode loop on the packed path replays exactly what eager packed steps produce
+    (greedy), and the rollout outputs keep HFRollout's structure."""
+    from dots.rl_amd.config import to_attr
+    from dots.rl_amd.protocol import DataProto
+    from dots.rl_amd.qwen2 import KVCache, PackedDecode
+    from dots.rl_amd.rollout import MI355XRollout
+
+    B, P, R = 40, 16, 12
+    cfg, m = _small_model(seed=3)
+    g = torch.Generator(device=DEV).manual_seed(2)
+    ids = torch.randint(0, 512, (B, P), device=DEV, generator=g)
+    am = torch.ones(B, P, dtype=torch.int64, device=DEV)
+    pos = (am.cumsum(-1) - 1).clamp_min(0)
+    rcfg = to_attr(dict(do_sample=False, temperature=1.0, top_k=-1, top_p=1.0, response_length=R, ignore_eos=True,
+                        seed=0, val_kwargs={}, use_hip_graph=True, packed_decode=True))
+    ro = MI355XRollout(m, rcfg)
+    out = ro.generate_sequences(DataProto.from_dict({"input_ids": ids, "attention_mask": am, "position_ids": pos},
+                                                    meta_info={"eos_token_id": 2, "pad_token_id": 0}))
+    assert ro.last_packed_decode
+    resp = out.batch["responses"]
+    # eager packed greedy loop
+    cache = KVCache(cfg, B, P + R, DEV, BF)
+    h = m.prefill(cache, ids, am, pos)
+    pk = PackedDecode(m, B)
+    toks = [m.logits(h).float().argmax(-1)]
+    for t in range(1, R):
+        kd = torch.tensor([P + t - 1], device=DEV)
+        h = pk.step(cache, toks[-1].view(B, 1), pos[:, -1] + t, kd)
+        toks.append(m.logits(h).float().argmax(-1))
+    assert torch.equal(resp, torch.stack(toks, 1))
+    assert out.batch["input_ids"].shape == (B, P + R)

@@ -303,6 +303,54 @@ def fused_linear(Ns=(2048, 4096), H=896, V=151936):
     return res
 
 
+def decode_gemm(Ms=(32, 64, 128, 256, 512)):
+    """Decode projections on fragment-packed operands (csrc/decode_gemm.hip) vs hipBLASLt at the Qwen2.5-0.5B
+    shapes, weights rotating over > 600 MB of copies (each call streams W from HBM), graph-timed."""
+    from dots.rl_amd.workers import _enable_gemm_tuning
+    _enable_gemm_tuning("auto")
+    dev, bf = "cuda", torch.bfloat16
+    shapes = [("qkv_proj", 1152, 896, False), ("o_proj", 896, 896, False), ("gate_up_swiglu", 9728, 896, True),
+              ("down_proj", 896, 4864, False)]
+    res = []
+    for name, N, K, sw in shapes:
+        ncopy = max(2, int(600e6 // (N * K * 2)) + 1)
+        ws = [torch.randn(N, K, device=dev, dtype=bf) * 0.05 for _ in range(ncopy)]
+        wps = [native.decode_pack_weight(w, swiglu=sw) for w in ws]
+        for M in Ms:
+            ks, mbt = native.decode_gemm_plan(M, N, K, sw)
+            x = torch.randn(M, K, device=dev, dtype=bf)
+            xp = native.pack_activations(x, mbt)
+            part = torch.empty(K // 16, M, N, device=dev)  # room for the deepest K split (1 step per wave)
+            outp = torch.zeros(mbt * 32 * (N // 2), device=dev, dtype=bf)
+            it = iter(range(1 << 30))
+
+            def ours():
+                return native.decode_gemm(xp, wps[next(it) % ncopy], M, N, K, swiglu=sw, partials=part,
+                                          out_packed=outp)
+
+            def lib():
+                y = x @ ws[next(it) % ncopy].t()
+                if sw:
+                    a = torch.empty(M, N // 2, device=dev, dtype=bf)
+                    native.swiglu_fwd(y, a)
+                    return a
+                return y
+            sweep = {}
+            for mbw in (2, 1):
+                for ksw in (19, 14, 7, 4, 2, 1):
+                    native.lib().drl_decode_gemm_set_plan(mbw, ksw)
+                    if native.decode_gemm_plan(M, N, K, sw) is None:
+                        continue
+                    sweep[f"{mbw}x{ksw}"] = round(time_graph(ours, ncopy) * 1e6, 2)
+            native.lib().drl_decode_gemm_set_plan(0, 0)
+            t = time_graph(ours, ncopy)
+            t2 = time_graph(lib, ncopy)
+            nbytes = 2 * N * K + 2 * M * K
+            res.append(dict(kernel="decode_gemm", layer=name, M=M, N=N, K=K, ksplit=ks, us=t * 1e6,
+                            GBps=nbytes / t / 1e9, hipblaslt_us=t2 * 1e6, sweep_us=sweep))
+    return res
+
+
 def launch_floor(B=64, H=896, I=4864):
     """Per-call time of tiny kernels replayed back to back from a HIP graph: the launch/dependency floor of a
     decode step, next to the small hand-written decode kernels at B rows."""
@@ -340,6 +388,10 @@ if __name__ == "__main__":
         sys.exit(0)
     if args.only == "linear":
         for r in launch_floor() + linear():
+            print(json.dumps(r), flush=True)
+        sys.exit(0)
+    if args.only == "decode_gemm":
+        for r in decode_gemm():
             print(json.dumps(r), flush=True)
         sys.exit(0)
     if args.only == "fused_linear":
