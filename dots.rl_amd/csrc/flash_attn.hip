@@ -326,23 +326,6 @@ struct FlashBwdArgs {
 
 __device__ __forceinline__ float bf2f(uint16_t x) { return bf16_to_f32(x); }
 
-// 8 elements of a k-step in the accumulator's permuted k order: positions p0 + 16s + 4h + {0..3} and
-// p0 + 16s + 8 + 4h + {0..3} of a position-contiguous row; positions >= lim read as zero.
-__device__ __forceinline__ u16x8 load_perm8(const uint16_t* row, int64_t pa, int64_t lim) {
-  const int64_t pb = pa + 8;
-  u16x4 lo, hi;
-  if (pb + 3 < lim) {
-    lo = *reinterpret_cast<const u16x4*>(row + pa);
-    hi = *reinterpret_cast<const u16x4*>(row + pb);
-  } else {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      lo[j] = pa + j < lim ? row[pa + j] : 0;
-      hi[j] = pb + j < lim ? row[pb + j] : 0;
-    }
-  }
-  return u16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-}
 
 // dq_kernel's per-key-block tiles in LDS, shared by the G waves (query heads) of the workgroup:
 // K and V row-major [32 keys][D] (rows padded to D + 8 elements) and K^T [D][32 keys] (rows of 36).
@@ -710,35 +693,84 @@ struct DecBlock {
   uint32_t vb[4];
 };
 
+// Coalesced block loader: a 32-key block is 4 KB of contiguous K rows and D rows x 64 B of V^T. A wave
+// fetches it with whole 1-KB instructions (16 B per lane, K: 8 lanes per 128-B row; V^T: 4 lanes per 64-B
+// row segment) instead of fragment-shaped loads that touch 32 rows x 16-32 B per instruction, then
+// re-shapes it through its own LDS slot (no cross-wave sync: the wave writes and reads its slot in order).
 template <int D>
-__device__ __forceinline__ void dec_load(const uint16_t* kb, const uint16_t* vtb, const uint8_t* vrow, int64_t ld_vt,
-                                         int k0, int kend, int qi, int h, DecBlock<D>& blk) {
-  const int key = k0 + qi;
-  const bool kin = key < kend;
-  const uint16_t* krow = kb + static_cast<int64_t>(kin ? key : 0) * D + 8 * h;
+struct DecRaw {
+  u16x8 k[D / 16];
+  u16x8 v[D / 16];
+  uint32_t vb[4];
+};
+
+template <int D>
+__device__ __forceinline__ void dec_load_raw(const uint16_t* kb, const uint16_t* vtb, const uint8_t* vrow,
+                                             int64_t ld_vt, int64_t ld_valid, int k0, int kend, int lane, int h,
+                                             DecRaw<D>& r) {
+  constexpr int UPR = D / 8;  // 16-B units per K row
+  // every load is a whole 16 B at an in-bounds address (rows clamped to kend - 1, V^T columns to the row);
+  // positions >= kend are zeroed after the load, so the tail block costs no extra memory round trip
+  const bool tail = k0 + 32 > kend;
 #pragma unroll
-  for (int s = 0; s < D / 16; ++s) {
-    blk.kf[s] = *reinterpret_cast<const u16x8*>(krow + 16 * s);
-    if (!kin) blk.kf[s] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-  }
+  for (int i = 0; i < D / 16; ++i) {
+    const int c = lane + 64 * i;
+    const int key = k0 + c / UPR;
+    r.k[i] = *reinterpret_cast<const u16x8*>(kb + static_cast<int64_t>(min(key, kend - 1)) * D + 8 * (c % UPR));
+    const int kk = k0 + 8 * (c & 3);
+    r.v[i] = *reinterpret_cast<const u16x8*>(vtb + static_cast<int64_t>(c >> 2) * ld_vt +
+                                             min(static_cast<int64_t>(kk), ld_vt - 8));
+    if (tail) {
+      if (key >= kend) r.k[i] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
-  for (int mt = 0; mt < D / 32; ++mt) {
-    const uint16_t* vr = vtb + static_cast<int64_t>(32 * mt + qi) * ld_vt;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) blk.vf[mt][s] = load_perm8(vr, k0 + 16 * s + 4 * h, kend);
+      for (int j = 0; j < 8; ++j)
+        if (kk + j >= kend) r.v[i][j] = 0;
+    }
   }
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
     const int kk = k0 + 8 * c + 4 * h;
-    if (kk + 3 < kend) {
-      blk.vb[c] = *reinterpret_cast<const uint32_t*>(vrow + kk);
-    } else {
-      uint32_t v = 0;
+    uint32_t v = *reinterpret_cast<const uint32_t*>(vrow + min(static_cast<int64_t>(kk), ld_valid - 4));
+    if (tail) {
+      uint32_t keep = 0;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) v |= (kk + j < kend ? static_cast<uint32_t>(vrow[kk + j]) : 0u) << (8 * j);
-      blk.vb[c] = v;
+      for (int j = 0; j < 4; ++j) keep |= (kk + j < kend ? 0xffu : 0u) << (8 * j);
+      v = kk + 3 < ld_valid ? (v & keep) : 0u;
+    }
+    r.vb[c] = v;
+  }
+}
+
+// raw block -> the wave's LDS slot -> MFMA fragments (the same DecBlock the fragment-shaped loader fills).
+// K slot [32][D]: 16-B unit u of row r at u ^ (r & 7); V^T slot [D][32 keys]: 8-B slot t of row d at
+// t ^ ((d >> 2) & 7) (conflict-free ds_read_b64 over 32 consecutive rows).
+template <int D>
+__device__ __forceinline__ void dec_reshape(const DecRaw<D>& r, uint16_t* ks, uint16_t* vs, int lane, int qi, int h,
+                                            DecBlock<D>& blk) {
+  constexpr int UPR = D / 8;
+#pragma unroll
+  for (int i = 0; i < D / 16; ++i) {
+    const int c = lane + 64 * i, row = c / UPR, u = c % UPR;
+    *reinterpret_cast<u16x8*>(ks + row * D + 8 * (u ^ (row & 7))) = r.k[i];
+    const int d = c >> 2, t0 = 2 * (c & 3), sw = (d >> 2) & 7;
+    *reinterpret_cast<u16x4*>(vs + d * 32 + 4 * (t0 ^ sw)) = u16x4{r.v[i][0], r.v[i][1], r.v[i][2], r.v[i][3]};
+    *reinterpret_cast<u16x4*>(vs + d * 32 + 4 * ((t0 + 1) ^ sw)) = u16x4{r.v[i][4], r.v[i][5], r.v[i][6], r.v[i][7]};
+  }
+#pragma unroll
+  for (int s = 0; s < D / 16; ++s)
+    blk.kf[s] = *reinterpret_cast<const u16x8*>(ks + qi * D + 8 * ((2 * s + h) ^ (qi & 7)));
+#pragma unroll
+  for (int mt = 0; mt < D / 32; ++mt) {
+    const int d = 32 * mt + qi, sw = (d >> 2) & 7;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const u16x4 lo = *reinterpret_cast<const u16x4*>(vs + d * 32 + 4 * ((4 * s + h) ^ sw));
+      const u16x4 hi = *reinterpret_cast<const u16x4*>(vs + d * 32 + 4 * ((4 * s + 2 + h) ^ sw));
+      blk.vf[mt][s] = u16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
     }
   }
+#pragma unroll
+  for (int c = 0; c < 4; ++c) blk.vb[c] = r.vb[c];
 }
 
 // online-softmax step over one loaded block (scores, running max / sum, O^T accumulation)
@@ -791,7 +823,8 @@ template <int D, int NW>
 __global__ __launch_bounds__(64 * NW) void decode_mfma_kernel(DecodeArgs a) {
   constexpr int KS = D / 16, MT = D / 32;
   __shared__ float s_m[NW][32], s_l[NW][32];
-  __shared__ float s_o[NW][MT][16][64];
+  // per wave: its K / V^T staging slot during the key loop, then its partial O^T (same 64*D*2... bytes)
+  __shared__ __attribute__((aligned(16))) float s_o[NW][MT][16][64];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int qi = lane & 31, h = lane >> 5;
   const int64_t bh = blockIdx.x, b = bh / a.Hkv;
@@ -805,9 +838,11 @@ __global__ __launch_bounds__(64 * NW) void decode_mfma_kernel(DecodeArgs a) {
   const int nall = (kend + 31) / 32, S = gridDim.y, y = blockIdx.y;
   const int bbeg = y * nall / S, nblk = (y + 1) * nall / S;
   const int ib0 = bbeg + w;
-  DecBlock<D> A, Bn;
-  if (ib0 < nblk) dec_load<D>(kb, vtb, vrow, a.ld_vt, 32 * ib0, kend, qi, h, A);
-  if (ib0 + NW < nblk) dec_load<D>(kb, vtb, vrow, a.ld_vt, 32 * (ib0 + NW), kend, qi, h, Bn);
+  DecRaw<D> A, Bn;
+  uint16_t* kslot = reinterpret_cast<uint16_t*>(&s_o[w][0][0][0]);  // 32 * D bf16
+  uint16_t* vslot = kslot + 32 * D;                                 // D * 32 bf16
+  if (ib0 < nblk) dec_load_raw<D>(kb, vtb, vrow, a.ld_vt, a.ld_valid, 32 * ib0, kend, lane, h, A);
+  if (ib0 + NW < nblk) dec_load_raw<D>(kb, vtb, vrow, a.ld_vt, a.ld_valid, 32 * (ib0 + NW), kend, lane, h, Bn);
   bf16x8 qf[KS];
   {
     const bool qv = qi < a.G;
@@ -824,11 +859,14 @@ __global__ __launch_bounds__(64 * NW) void decode_mfma_kernel(DecodeArgs a) {
   for (int mt = 0; mt < MT; ++mt) o[mt] = f32x16{};
   float m = -INFINITY, lsum = 0.f;
   for (int ib = ib0; ib < nblk; ib += 2 * NW) {
-    dec_block<D>(A, qf, a.scale_log2, m, lsum, o);
-    if (ib + 2 * NW < nblk) dec_load<D>(kb, vtb, vrow, a.ld_vt, 32 * (ib + 2 * NW), kend, qi, h, A);
+    DecBlock<D> blk;
+    dec_reshape<D>(A, kslot, vslot, lane, qi, h, blk);
+    if (ib + 2 * NW < nblk) dec_load_raw<D>(kb, vtb, vrow, a.ld_vt, a.ld_valid, 32 * (ib + 2 * NW), kend, lane, h, A);
+    dec_block<D>(blk, qf, a.scale_log2, m, lsum, o);
     if (ib + NW < nblk) {
-      dec_block<D>(Bn, qf, a.scale_log2, m, lsum, o);
-      if (ib + 3 * NW < nblk) dec_load<D>(kb, vtb, vrow, a.ld_vt, 32 * (ib + 3 * NW), kend, qi, h, Bn);
+      dec_reshape<D>(Bn, kslot, vslot, lane, qi, h, blk);
+      if (ib + 3 * NW < nblk) dec_load_raw<D>(kb, vtb, vrow, a.ld_vt, a.ld_valid, 32 * (ib + 3 * NW), kend, lane, h, Bn);
+      dec_block<D>(blk, qf, a.scale_log2, m, lsum, o);
     }
   }
   // merge the 4 waves' states per query column (head) in a fixed order
@@ -1047,21 +1085,20 @@ int drl_decode_attention_vt(const void* q, const void* k_cache, const void* vt_c
   DRL_CHECK_ARG(out_mbt == 0 || out_mbt * 32 >= B, "out_mbt too small for B rows");
   DRL_CHECK_ARG(D == 64 || D == 128, "head_dim must be 64 or 128");
   DRL_CHECK_ARG(B >= 1 && Hkv >= 1 && G >= 1 && G <= 32 && L >= 1 && L <= ld_k && L <= ld_vt, "bad shape");
-  DRL_CHECK_ARG(ld_vt % 4 == 0 && ld_valid % 4 == 0 && (reinterpret_cast<uintptr_t>(key_valid) & 3u) == 0 &&
+  DRL_CHECK_ARG(ld_vt % 8 == 0 && ld_valid % 4 == 0 && (reinterpret_cast<uintptr_t>(key_valid) & 3u) == 0 &&
                     ld_k < (int64_t(1) << 30),
-                "ld_vt / key_valid rows must be 4-element aligned");
-  DRL_CHECK_ARG(aligned16(q) && aligned16(k_cache) && (reinterpret_cast<uintptr_t>(vt_cache) & 7u) == 0 &&
-                    (reinterpret_cast<uintptr_t>(out) & 7u) == 0,
-                "misaligned operand");
+                "ld_vt must be a multiple of 8 and key_valid rows 4-byte aligned");
+  DRL_CHECK_ARG(aligned16(q) && aligned16(k_cache) && aligned16(vt_cache) && (reinterpret_cast<uintptr_t>(out) & 7u) == 0,
+                "misaligned operand (q, caches 16-byte aligned)");
   DecodeArgs a{static_cast<const uint16_t*>(q), static_cast<const uint16_t*>(k_cache),
                static_cast<const uint16_t*>(vt_cache), key_valid, ld_valid, qpos_ptr, qpos, Hkv, G, ld_k, ld_vt, L,
                scale * 1.4426950408889634f, static_cast<uint16_t*>(out), out_mbt, nullptr, nullptr};
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int64_t wgs = B * Hkv, cus = cu_count();
   const int splits = decode_splits(B, Hkv, L);
-  // waves per workgroup (same sweep): 8 while the grid is below the chip, 4 up to 4 workgroups per CU,
-  // then 2 for short caches
-  const int nw = g_dec_nw ? g_dec_nw : (wgs < cus ? 8 : (wgs < 4 * cus || L > 640 ? 4 : 2));
+  // waves per workgroup (tools/kernel_bench.py --only decode_sweep, coalesced loader): 8 while the grid fits
+  // the chip, 2 beyond (B=64: 8.9 us, B=512: 36.8 us at L=768)
+  const int nw = g_dec_nw ? g_dec_nw : (wgs <= cus ? 8 : 2);
   if (splits > 1) {
     const size_t need = drl_decode_attention_vt_workspace_bytes(B, Hkv, D, L);
     if (!workspace || workspace_bytes < need || (reinterpret_cast<uintptr_t>(workspace) & 255u))

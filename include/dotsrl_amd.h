@@ -298,6 +298,7 @@ int drl_flash_attn_fwd(const void* q, const void* k, const void* vt, int32_t dt,
  * *qpos_ptr when non-NULL). out (B,Hkv,G,D), or with out_mbt > 0 the (B, Hq*D) panel fragment-packed for
  * drl_decode_gemm (out_mbt >= B/32 blocks). G <= 32, head_dim 64 or 128. Same semantics as
  * drl_decode_attention (the VALU kernel over a row-major V cache used by the fp32 parity model).
+ * q and both caches 16-byte aligned, ld_vt % 8 == 0 (32-key blocks are fetched with whole 16-byte loads).
  * Small batches split the keys over workgroups (partial softmax states merged in split order by the last
  * arriving split): workspace of drl_decode_attention_vt_workspace_bytes(B, Hkv, D, L) bytes (0 = none
  * needed), 256-byte aligned, zero-filled before the first call and left zeroed by every call. */
