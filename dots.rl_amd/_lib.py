@@ -131,6 +131,8 @@ SIGNATURES = {
     "drl_decode_pack_weight": (ctypes.c_int, [P, I64, I64, I64, I32, P, P]),
     "drl_decode_gemm": (ctypes.c_int, [P, P, I64, I64, I64, I32, P, P, P]),
     "drl_decode_rmsnorm": (ctypes.c_int, [P, P, I32, P, P, P, I64, I64, I64, F32, P]),
+    "drl_decode_pack_weight_rope": (ctypes.c_int, [P, I64, I64, I64, I64, P, P]),
+    "drl_decode_qkv_rope": (ctypes.c_int, [P, P, P, P, P, P, I64, I64, I64, I64, I64, I64, P, P, P, I64, I64, P, P]),
     "drl_decode_rope": (ctypes.c_int, [P, I32, P, P, P, P, I64, I64, I64, I64, I64, P, P, P, P, I64, I64, I64, P, P]),
     "drl_linear_logprob_fwd": (ctypes.c_int, [P, I64, P, P, I32, I64, I64, I64, F32, P, P, P, P, SZ, P]),
     "drl_linear_logprob_dlogits": (ctypes.c_int, [P, I64, P, P, I32, I64, I64, I64, F32, P, P, P, P, P, I64, P]),

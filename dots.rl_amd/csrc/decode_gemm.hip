@@ -40,8 +40,12 @@ __device__ __forceinline__ int64_t pk_off(int64_t m, int64_t k, int64_t MBT) {
 // ------------------------------------------------------------------------------------------- packing
 // dst fragment (t, s, lane l): W row rowmap(t, l & 31), k = 16 s + 8 (l >> 5) .. + 7. SwiGLU packing
 // (half = I > 0): block t holds gate rows 16t..16t+15 then up rows I+16t..I+16t+15.
+// RoPE packing (rope_half = D/2 > 0): block t holds rows head*D + 16q + (0..15) and the rotation partners
+// head*D + D/2 + 16q + (0..15), q = t % (D/32), head = t / (D/32), so both halves of a rotated pair meet in one
+// workgroup's epilogue.
 __global__ __launch_bounds__(256) void pack_weight_kernel(const uint16_t* src, int64_t ld, int64_t N, int64_t K,
-                                                          int64_t half, int64_t tiles, uint16_t* dst) {
+                                                          int64_t half, int64_t tiles, uint16_t* dst,
+                                                          int64_t rope_half = 0) {
   const int64_t nks = K / 16;
   const int64_t idx = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
   if (idx >= tiles * nks * 64) return;
@@ -53,6 +57,10 @@ __global__ __launch_bounds__(256) void pack_weight_kernel(const uint16_t* src, i
     const int64_t c = 16 * t + (r & 15);
     ok = c < half;
     row = r < 16 ? c : half + c;
+  } else if (rope_half > 0) {
+    const int64_t per = rope_half / 16, head = t / per, q = t % per;
+    row = head * 2 * rope_half + 16 * q + (r & 15) + (r < 16 ? 0 : rope_half);
+    ok = row < N;
   } else {
     row = 32 * t + r;
     ok = row < N;
@@ -69,9 +77,20 @@ struct DgArgs {
   int M, N, K, MBT, nks, tiles, half;
   float* part;        // EPI_PARTIAL: (ksplit, M, N) fp32
   uint16_t* out;      // EPI_SWIGLU: packed (MBT blocks, K' = half)
+  // EPI_ROPE (qkv_proj of one decode token; weights packed in rotation pairs, whole K per workgroup)
+  const uint16_t* bias;
+  const int64_t* pos;
+  const float* cos_t;
+  const float* sin_t;
+  uint16_t* q;        // (M, Hkv, G, D)
+  uint16_t* kc;       // (M, Hkv, Tk, D)
+  uint16_t* vt;       // (M, Hkv, D, ld_vt)
+  const int64_t* koff_dev;
+  int64_t maxpos, Tk, ld_vt;
+  int Hq, Hkv, D;
 };
 
-constexpr int EPI_PARTIAL = 0, EPI_SWIGLU = 1;
+constexpr int EPI_PARTIAL = 0, EPI_SWIGLU = 1, EPI_ROPE = 2;
 
 template <int MB, int KSW, int EPI>
 __global__ __launch_bounds__(256) void decode_gemm_kernel(DgArgs a) {
@@ -111,6 +130,44 @@ __global__ __launch_bounds__(256) void decode_gemm_kernel(DgArgs a) {
       const int q = (i & 3) + 4 * (i >> 3), ln = ml + 32 * ((i >> 2) & 1);
       const float v = ((red[0][blk][q][ln] + red[1][blk][q][ln]) + red[2][blk][q][ln]) + red[3][blk][q][ln];
       a.part[(static_cast<int64_t>(ks) * a.M + m) * a.N + n] = v;
+    }
+  } else if constexpr (EPI == EPI_ROPE) {
+    // rows 0..15: d = 16 qq + c of head hd, rows 16..31 its partners d + D/2. qkv = bf16(acc + bias), then
+    // rope_qkv_fwd_kernel's rotation (q, k heads) and the cache writes at the device key offset koff
+    const int half = a.D / 2, per = half / 16, hd = tile / per, qq = tile % per;
+    const int64_t koff = *a.koff_dev;
+    for (int e = tid; e < 512 * MB; e += 256) {
+      const int tl = e >> 4, c = e & 15, blk = tl >> 5, ml = tl & 31;
+      const int m = (mb0 + blk) * 32 + ml;
+      if (m >= a.M) continue;
+      const int i1 = c, i2 = c + 16;
+      const int q1 = (i1 & 3) + 4 * (i1 >> 3), l1 = ml + 32 * ((i1 >> 2) & 1);
+      const int q2 = (i2 & 3) + 4 * (i2 >> 3), l2 = ml + 32 * ((i2 >> 2) & 1);
+      const int d1 = 16 * qq + c, d2 = d1 + half;
+      const int n1 = hd * a.D + d1, n2 = n1 + half;
+      const float x1 = bf16r(((red[0][blk][q1][l1] + red[1][blk][q1][l1]) + red[2][blk][q1][l1]) + red[3][blk][q1][l1] +
+                             bf16_to_f32(a.bias[n1]));
+      const float x2 = bf16r(((red[0][blk][q2][l2] + red[1][blk][q2][l2]) + red[2][blk][q2][l2]) + red[3][blk][q2][l2] +
+                             bf16_to_f32(a.bias[n2]));
+      if (hd < a.Hq + a.Hkv) {
+        int64_t p = a.pos[m];
+        p = p < 0 ? 0 : (p >= a.maxpos ? a.maxpos - 1 : p);
+        const float cs = a.cos_t[p * half + d1], sn = a.sin_t[p * half + d1];
+        const float o1 = fmaf(x1, cs, -(x2 * sn)), o2 = fmaf(x2, cs, x1 * sn);
+        uint16_t* dst;
+        if (hd < a.Hq) {
+          const int G = a.Hq / a.Hkv;
+          dst = a.q + ((static_cast<int64_t>(m) * a.Hkv + hd / G) * G + hd % G) * a.D;
+        } else {
+          dst = a.kc + ((static_cast<int64_t>(m) * a.Hkv + (hd - a.Hq)) * a.Tk + koff) * a.D;
+        }
+        dst[d1] = to_bf16_bits(o1);
+        dst[d2] = to_bf16_bits(o2);
+      } else {
+        uint16_t* dst = a.vt + (static_cast<int64_t>(m) * a.Hkv + (hd - a.Hq - a.Hkv)) * a.D * a.ld_vt + koff;
+        dst[static_cast<int64_t>(d1) * a.ld_vt] = to_bf16_bits(x1);
+        dst[static_cast<int64_t>(d2) * a.ld_vt] = to_bf16_bits(x2);
+      }
     }
   } else {
     // SwiGLU: rows 0..15 gate, 16..31 up of output columns 16 * tile + c; thread -> (token, 8 columns)
@@ -295,14 +352,14 @@ bool plan_decode_gemm(int64_t M, int64_t N, int64_t K, int epi, DgPlan& p) {
   const int nks = static_cast<int>(K / 16);
   // fewest K slices (partial sums for the consumer) among the shapes that give >= 96 workgroups, then
   // 2-block workgroups (each weight fragment feeds two MFMAs); otherwise the shape with the most workgroups.
-  // SwiGLU needs the whole K in one workgroup.
+  // The SwiGLU / RoPE epilogues need the whole K in one workgroup.
   bool found = false, full = false;
   int64_t best_wgs = 0;
   for (const DgShape& c : kShapes) {
     if (c.mb > p.mbt) continue;
     if (nks % (4 * c.ksw) != 0) continue;
     const int ks = nks / (4 * c.ksw);
-    if (epi == EPI_SWIGLU && ks != 1) continue;
+    if (epi != EPI_PARTIAL && ks != 1) continue;
     if ((g_dg_mb && c.mb != g_dg_mb) || (g_dg_ksw && c.ksw != g_dg_ksw)) continue;
     const int64_t wgs = static_cast<int64_t>(p.tiles) * (p.mbt / c.mb) * ks;
     const bool ok = wgs >= 96;
@@ -407,6 +464,66 @@ int drl_decode_gemm(const void* x_packed, const void* w_packed, int64_t M, int64
     if (epi == EPI_PARTIAL) launch_dg<2, EPI_PARTIAL>(a, p, s);
     else launch_dg<2, EPI_SWIGLU>(a, p, s);
   }
+  DRL_LAUNCH_CHECK();
+  return DRL_OK;
+}
+
+int drl_decode_pack_weight_rope(const void* w, int64_t ld, int64_t N, int64_t K, int64_t head_dim, void* packed,
+                                void* stream) {
+  using namespace drl;
+  DRL_CHECK_ARG(w && packed, "NULL input");
+  DRL_CHECK_ARG(head_dim % 32 == 0 && head_dim >= 32 && N % head_dim == 0, "rotation-pair packing: head_dim % 32, N % head_dim");
+  DRL_CHECK_ARG(K >= 16 && K % 16 == 0 && ld >= K && ld % 8 == 0 && aligned16(w) && aligned16(packed),
+                "bad shape / alignment");
+  const int64_t tiles = N / 32, n = tiles * (K / 16) * 64;
+  hipLaunchKernelGGL(pack_weight_kernel, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), static_cast<const uint16_t*>(w), ld, N, K, int64_t(0), tiles,
+                     static_cast<uint16_t*>(packed), head_dim / 2);
+  DRL_LAUNCH_CHECK();
+  return DRL_OK;
+}
+
+int drl_decode_qkv_rope(const void* x_packed, const void* w_packed, const void* bias, const int64_t* position_ids,
+                        const float* cos_t, const float* sin_t, int64_t maxpos, int64_t M, int64_t K, int64_t Hq,
+                        int64_t Hkv, int64_t D, void* q, void* k_cache, void* vt_cache, int64_t Tk, int64_t ld_vt,
+                        const int64_t* koff_dev, void* stream) {
+  using namespace drl;
+  DRL_CHECK_ARG(x_packed && w_packed && bias && position_ids && cos_t && sin_t && q && k_cache && vt_cache && koff_dev,
+                "NULL input");
+  DRL_CHECK_ARG(aligned16(x_packed) && aligned16(w_packed), "packed operands must be 16-byte aligned");
+  DRL_CHECK_ARG(Hq >= 1 && Hkv >= 1 && Hq % Hkv == 0 && D % 32 == 0 && ld_vt >= Tk && Tk >= 1 && maxpos >= 1,
+                "bad shape");
+  const int64_t N = (Hq + 2 * Hkv) * D;
+  DgPlan p{};
+  if (!plan_decode_gemm(M, N, K, EPI_ROPE, p))
+    return fail(DRL_ERR_UNSUPPORTED, "decode qkv+rope: unsupported shape M=%lld N=%lld K=%lld", (long long)M,
+                (long long)N, (long long)K);
+  DgArgs a{};
+  a.x = static_cast<const uint16_t*>(x_packed);
+  a.w = static_cast<const uint16_t*>(w_packed);
+  a.M = static_cast<int>(M);
+  a.N = static_cast<int>(N);
+  a.K = static_cast<int>(K);
+  a.MBT = p.mbt;
+  a.nks = static_cast<int>(K / 16);
+  a.tiles = p.tiles;
+  a.bias = static_cast<const uint16_t*>(bias);
+  a.pos = position_ids;
+  a.cos_t = cos_t;
+  a.sin_t = sin_t;
+  a.q = static_cast<uint16_t*>(q);
+  a.kc = static_cast<uint16_t*>(k_cache);
+  a.vt = static_cast<uint16_t*>(vt_cache);
+  a.koff_dev = koff_dev;
+  a.maxpos = maxpos;
+  a.Tk = Tk;
+  a.ld_vt = ld_vt;
+  a.Hq = static_cast<int>(Hq);
+  a.Hkv = static_cast<int>(Hkv);
+  a.D = static_cast<int>(D);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (p.mb == 1) launch_dg<1, EPI_ROPE>(a, p, s);
+  else launch_dg<2, EPI_ROPE>(a, p, s);
   DRL_LAUNCH_CHECK();
   return DRL_OK;
 }

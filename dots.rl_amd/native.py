@@ -643,3 +643,27 @@ def decode_rope(partials, bias, position_ids, cos_t, sin_t, Hq, Hkv, D, q, k_cac
     check(lib().drl_decode_rope(_p(partials), ns, _p(bias), _p(position_ids), _p(cos_t), _p(sin_t), cos_t.shape[0], B,
                                 Hq, Hkv, D, _p(q), _p(k_cache), _p(v_cache), _p(vt_cache), Tk, ld_vt, int(koff),
                                 _p(koff_dev), _stream()), "drl_decode_rope")
+
+
+def decode_pack_weight_rope(w, head_dim, out=None):
+    """Packed qkv_proj weight in RoPE rotation pairs (drl_decode_qkv_rope)."""
+    _dev(w)
+    assert w.dim() == 2 and w.stride(1) == 1 and w.dtype == torch.bfloat16
+    N, K = w.shape
+    n = lib().drl_decode_pack_weight_elems(N, K, 0)
+    if out is None:
+        out = torch.empty(n, dtype=torch.bfloat16, device=w.device)
+    check(lib().drl_decode_pack_weight_rope(_p(w), w.stride(0), N, K, head_dim, _p(out), _stream()),
+          "drl_decode_pack_weight_rope")
+    return out
+
+
+def decode_qkv_rope(x_packed, w_packed, bias, position_ids, cos_t, sin_t, M, K, Hq, Hkv, D, q, k_cache, vt_cache,
+                    koff_dev):
+    """One launch: qkv_proj + bias + RoPE, q (M,Hkv,G,D) out, K / V^T cache rows at the device offset."""
+    _dev(x_packed, w_packed, bias, position_ids, q, k_cache, vt_cache, koff_dev)
+    assert q.is_contiguous() and k_cache.is_contiguous() and vt_cache.stride(-1) == 1
+    check(lib().drl_decode_qkv_rope(_p(x_packed), _p(w_packed), _p(bias), _p(position_ids), _p(cos_t), _p(sin_t),
+                                    cos_t.shape[0], M, K, Hq, Hkv, D, _p(q), _p(k_cache), _p(vt_cache),
+                                    k_cache.shape[2], vt_cache.stride(-2), _p(koff_dev), _stream()),
+          "drl_decode_qkv_rope")

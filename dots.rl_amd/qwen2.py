@@ -544,10 +544,10 @@ class Qwen2Model:
 
 class PackedDecode:
     """Decode step on fragment-packed operands (csrc/decode_gemm.hip) for one rollout of B <= 256 sequences:
-    per layer decode RMSNorm (packed out) -> qkv GEMM (fp32 K-slice partials) -> decode RoPE (sums the
-    partials + bias, writes q and the caches) -> MFMA decode attention (packed out) -> o_proj GEMM ->
+    per layer decode RMSNorm (packed out) -> qkv GEMM with bias + RoPE + cache writes in its epilogue (weights
+    packed in rotation pairs) -> MFMA decode attention (packed out) -> o_proj GEMM (fp32 K-slice partials) ->
     decode RMSNorm (adds the o_proj partials) -> gate_up GEMM with the SwiGLU epilogue (packed out) ->
-    down_proj GEMM, whose partials the next layer's RMSNorm adds. Eight launches per layer instead of nine,
+    down_proj GEMM, whose partials the next layer's RMSNorm adds. Seven launches per layer instead of nine,
     every projection a one-round-trip weight stream. The weights are packed once per rollout from the bf16
     compute copy (they change at every optimizer step); every buffer is preallocated so the step is
     graph-capturable. Module math is the unpacked decode path's (bf16 module outputs, fp32 residual)."""
@@ -573,15 +573,15 @@ class PackedDecode:
         Hq, Hkv = cfg.num_attention_heads, cfg.num_key_value_heads
         self.NQ = (Hq + 2 * Hkv) * D
         self.HD = Hq * D
-        self.plans = {"qkv": native.decode_gemm_plan(B, self.NQ, H), "o": native.decode_gemm_plan(B, H, self.HD),
+        self.plans = {"o": native.decode_gemm_plan(B, H, self.HD),
                       "gu": native.decode_gemm_plan(B, 2 * I, H, True), "d": native.decode_gemm_plan(B, H, I)}
-        self.mbt = self.plans["qkv"][1]
+        self.mbt = self.plans["o"][1]
         assert all(p[1] == self.mbt for p in self.plans.values())
         bf = torch.bfloat16
         self.w = []
         for i in range(cfg.num_hidden_layers):
             p = f"layers.{i}."
-            self.w.append(dict(qkv=native.decode_pack_weight(s.w(p + "qkv_proj.weight")),
+            self.w.append(dict(qkv=native.decode_pack_weight_rope(s.w(p + "qkv_proj.weight"), D),
                                o=native.decode_pack_weight(s.w(p + "o_proj")),
                                gu=native.decode_pack_weight(s.w(p + "gate_up_proj"), swiglu=True),
                                d=native.decode_pack_weight(s.w(p + "down_proj"))))
@@ -589,7 +589,6 @@ class PackedDecode:
         self.h_p = torch.zeros(rows * H, dtype=bf, device=dev)        # RMSNorm out (packed; pad rows stay 0)
         self.attn_p = torch.zeros(rows * self.HD, dtype=bf, device=dev)
         self.a_p = torch.zeros(rows * I, dtype=bf, device=dev)        # SwiGLU out
-        self.part_qkv = torch.empty(self.plans["qkv"][0], B, self.NQ, device=dev)
         self.part_o = torch.empty(self.plans["o"][0], B, H, device=dev)
         self.part_d = torch.empty(self.plans["d"][0], B, H, device=dev)
         self.x = torch.empty(B, H, device=dev)                         # fp32 residual stream
@@ -612,9 +611,8 @@ class PackedDecode:
         for i in range(cfg.num_hidden_layers):
             p, w = f"layers.{i}.", self.w[i]
             native.decode_rmsnorm(self.x, prev, self.x, s.w(p + "input_layernorm"), self.h_p, eps, mbt=mbt)
-            native.decode_gemm(self.h_p, w["qkv"], B, self.NQ, H, partials=self.part_qkv)
-            native.decode_rope(self.part_qkv, s.w(p + "qkv_proj.bias"), pos, m.cos, m.sin, Hq, Hkv, D, self.q,
-                               cache.k[i], vt_cache=cache.vt[i], koff_dev=kpos_dev)
+            native.decode_qkv_rope(self.h_p, w["qkv"], s.w(p + "qkv_proj.bias"), pos, m.cos, m.sin, B, H, Hq, Hkv, D,
+                                   self.q, cache.k[i], cache.vt[i], kpos_dev)
             native.decode_attention_vt(self.q, cache.k[i], cache.vt[i], cache.valid, Lk, self.attn_p,
                                        qpos_dev=kpos_dev, out_mbt=mbt)
             native.decode_gemm(self.attn_p, w["o"], B, H, self.HD, partials=self.part_o)

@@ -378,6 +378,18 @@ int drl_decode_pack_weight(const void* w, int64_t ld, int64_t N, int64_t K, int3
  * SWIGLU writes the activation packed for the down projection. */
 int drl_decode_gemm(const void* x_packed, const void* w_packed, int64_t M, int64_t N, int64_t K, int32_t epilogue,
                     float* partials, void* out_packed, void* stream);
+/* Packed copy of qkv_proj.weight (N = (Hq + 2 Hkv) head_dim rows) in rotation pairs: every 32-row block
+ * holds 16 consecutive head-dim rows and their RoPE partners head_dim/2 further (drl_decode_qkv_rope). */
+int drl_decode_pack_weight_rope(const void* w, int64_t ld, int64_t N, int64_t K, int64_t head_dim, void* packed,
+                                void* stream);
+/* qkv_proj + bias + rotary embedding of one decode token per sequence in ONE launch (replaces
+ * drl_decode_gemm + drl_decode_rope): qkv = bf16(x W^T + bias), q/k rotated as drl_rope_qkv_fwd, q written
+ * (M, Hkv, G, D), k to k_cache (M, Hkv, Tk, D) row *koff_dev, v to vt_cache (M, Hkv, D, ld_vt) column
+ * *koff_dev. x packed (M rows, K % 64 == 0), W packed by drl_decode_pack_weight_rope. */
+int drl_decode_qkv_rope(const void* x_packed, const void* w_packed, const void* bias, const int64_t* position_ids,
+                        const float* cos_t, const float* sin_t, int64_t maxpos, int64_t M, int64_t K, int64_t Hq,
+                        int64_t Hkv, int64_t D, void* q, void* k_cache, void* vt_cache, int64_t Tk, int64_t ld_vt,
+                        const int64_t* koff_dev, void* stream);
 /* x_out = x_in + bf16(sum of nsplit partials (nsplit, M, H)) (partials may be NULL: no delta), y = bf16(w *
  * x_out * rsqrt(mean(x_out^2) + eps)) packed with mbt blocks, or row-major (M, H) when mbt == 0
  * (drl_add_rmsnorm_fwd semantics). H % 8 == 0. */

@@ -221,3 +221,40 @@ def test_packed_rollout_graph_equals_eager():
         toks.append(m.logits(h).float().argmax(-1))
     assert torch.equal(resp, torch.stack(toks, 1))
     assert out.batch["input_ids"].shape == (B, P + R)
+
+
+@pytest.mark.parametrize("M,K,Hq,Hkv,D", [(64, 896, 14, 2, 64), (5, 128, 2, 1, 64), (100, 256, 4, 2, 128)])
+def test_decode_qkv_rope_matches_gemm_then_rope(M, K, Hq, Hkv, D):
+    """One-launch qkv_proj + bias + RoPE (rotation-pair packing) == the two-launch form (decode GEMM with the
+    same single K slice, then decode RoPE) bit for bit: the same fp32 sums in the same order, the same roundings."""
+    NQ = (Hq + 2 * Hkv) * D
+    G, Tk, koff = Hq // Hkv, 32, 9
+    x = rnd(M, K, seed=7)
+    w = rnd(NQ, K, scale=0.05, seed=8)
+    bias = rnd(NQ, seed=9)
+    pos = torch.randint(0, 500, (M,), device=DEV)
+    half = D // 2
+    inv = 1.0 / (10000.0 ** (torch.arange(0, D, 2, device=DEV).float() / D))
+    fr = torch.arange(1024, device=DEV).float()[:, None] * inv[None, :half]
+    cos_t, sin_t = fr.cos().contiguous(), fr.sin().contiguous()
+    kd = torch.tensor([koff], device=DEV)
+    mbt = native.decode_gemm_plan(M, NQ, K)[1]
+    xp = native.pack_activations(x, mbt)
+    outs = []
+    for fused in (True, False):
+        q = torch.zeros(M, Hkv, G, D, dtype=BF, device=DEV)
+        kc = torch.zeros(M, Hkv, Tk, D, dtype=BF, device=DEV)
+        vt = torch.zeros(M, Hkv, D, Tk, dtype=BF, device=DEV)
+        if fused:
+            native.decode_qkv_rope(xp, native.decode_pack_weight_rope(w, D), bias, pos, cos_t, sin_t, M, K, Hq, Hkv, D,
+                                   q, kc, vt, kd)
+        else:
+            # the fused launch's shape: whole K per workgroup (K / 64 k16-steps per wave)
+            native.lib().drl_decode_gemm_set_plan(0, K // 64)
+            part = native.decode_gemm(xp, native.decode_pack_weight(w), M, NQ, K)
+            native.lib().drl_decode_gemm_set_plan(0, 0)
+            assert part.shape[0] == 1
+            native.decode_rope(part, bias, pos, cos_t, sin_t, Hq, Hkv, D, q, kc, vt_cache=vt, koff_dev=kd)
+        outs.append((q, kc, vt))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
