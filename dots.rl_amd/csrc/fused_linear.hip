@@ -61,7 +61,46 @@ struct FlArgs {
   const float* ent;
   uint16_t* dlt;      // (V, ld_dl) bf16 d_logits^T
   int64_t ld_dl;
+  // token selection (decode): greedy argmax or the exponential race of the sampling draw over bf16 logits
+  int do_sample;
+  float temp;
+  uint64_t seed, offset;
+  int64_t row_base;
+  const int64_t* dev_step;
+  unsigned long long* best;  // (N) packed (key, ~index) running max, zero between calls
 };
+
+constexpr int MODE_LOGPROB = 0, MODE_DLOGITS = 1, MODE_SELECT = 2;
+
+// Philox4x32-10 block and the sampling race key / order-preserving packing of csrc/vocab.hip (K4): the same
+// draw for the same (seed, offset, row, index), so the fused and the unfused selection agree.
+__device__ __forceinline__ uint4 philox4(uint64_t seed, uint64_t offset, uint64_t counter) {
+  uint32_t c0 = static_cast<uint32_t>(counter), c1 = static_cast<uint32_t>(counter >> 32);
+  uint32_t c2 = static_cast<uint32_t>(offset), c3 = static_cast<uint32_t>(offset >> 32);
+  uint32_t k0 = static_cast<uint32_t>(seed), k1 = static_cast<uint32_t>(seed >> 32);
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const uint64_t p0 = static_cast<uint64_t>(0xD2511F53u) * c0;
+    const uint64_t p1 = static_cast<uint64_t>(0xCD9E8D57u) * c2;
+    const uint32_t n0 = static_cast<uint32_t>(p1 >> 32) ^ c1 ^ k0;
+    const uint32_t n1 = static_cast<uint32_t>(p1);
+    const uint32_t n2 = static_cast<uint32_t>(p0 >> 32) ^ c3 ^ k1;
+    const uint32_t n3 = static_cast<uint32_t>(p0);
+    c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return make_uint4(c0, c1, c2, c3);
+}
+__device__ __forceinline__ float race_key(float z, uint32_t bits) {
+  const float v = (static_cast<float>(bits >> 8) + 0.5f) * (1.0f / 16777216.0f);
+  return z - logf(-log1pf(-v));
+}
+__device__ __forceinline__ uint64_t pack_key(float key, int64_t idx) {
+  uint32_t b = __float_as_uint(key);
+  b = isnan(key) ? 0xFFFFFFFFu : ((b & 0x80000000u) ? ~b : (b | 0x80000000u));
+  return (static_cast<uint64_t>(b) << 32) | (0xFFFFFFFFu - static_cast<uint32_t>(idx));
+}
 
 // one K-step of both operands, global -> LDS directly (global_load_lds_dwordx4, no staging registers).
 // One wave-instruction fills 8 consecutive rows (1 KB, lane-linear in LDS): lane l writes physical unit
@@ -118,8 +157,9 @@ __device__ __forceinline__ void wg_coords(const FlArgs& a, int& tt, int& chunk) 
   chunk = c / a.tok_tiles;
 }
 
-template <bool BWD>
+template <int MODE>
 __global__ __launch_bounds__(kThreads) void fused_linear_kernel(FlArgs a) {
+  constexpr bool BWD = MODE == MODE_DLOGITS;
   __shared__ __attribute__((aligned(16))) uint16_t lds[kLdsU16];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wv = w & 3, wt = w >> 2, hi = lane >> 5;
@@ -134,12 +174,14 @@ __global__ __launch_bounds__(kThreads) void fused_linear_kernel(FlArgs a) {
   // per-token state of this lane: the 4 token blocks' columns
   int64_t lab[4];
   float m[4], s[4], sz[4];
+  uint64_t sel[4] = {0, 0, 0, 0};
+  const uint64_t off = MODE == MODE_SELECT ? a.offset + (a.dev_step ? static_cast<uint64_t>(*a.dev_step) : 0ull) : 0;
   float c_dlp[4], c_den[4], c_lse[4], c_ent[4];
 #pragma unroll
   for (int tb = 0; tb < 4; ++tb) {
     const int64_t t = t0 + wt * 128 + tb * 32 + (lane & 31);
     const bool tin = t < a.N;
-    lab[tb] = tin ? a.labels[t] : -1;
+    lab[tb] = (tin && MODE != MODE_SELECT) ? a.labels[t] : -1;
     m[tb] = -INFINITY;
     s[tb] = 0.f;
     sz[tb] = 0.f;
@@ -174,7 +216,27 @@ __global__ __launch_bounds__(kThreads) void fused_linear_kernel(FlArgs a) {
 #pragma unroll
       for (int tb = 0; tb < 4; ++tb) {
         const int64_t t = t0 + wt * 128 + tb * 32 + (lane & 31);
-        if constexpr (!BWD) {
+        if constexpr (MODE == MODE_SELECT) {
+          // bf16 logits (the lm_head module output), then greedy key = logit or race key = logit / T - log E
+          const uint64_t ctr = static_cast<uint64_t>(a.row_base + t) << 32;
+#pragma unroll
+          for (int vb = 0; vb < 2; ++vb)
+#pragma unroll
+            for (int g4 = 0; g4 < 4; ++g4) {
+              const int64_t v0 = vbase + vrow(vb, 4 * g4, hi);  // 4 consecutive rows, one Philox block
+              uint4 pb = make_uint4(0u, 0u, 0u, 0u);
+              if (a.do_sample) pb = philox4(a.seed, off, ctr | static_cast<uint64_t>(v0 >> 2));
+              const uint32_t bits[4] = {pb.x, pb.y, pb.z, pb.w};
+#pragma unroll
+              for (int j = 0; j < 4; ++j) {
+                const int64_t v = v0 + j;
+                const float x = bf16_to_f32(to_bf16_bits(acc[vb][tb][4 * g4 + j]));
+                const float key = a.do_sample ? race_key(x / a.temp, bits[j]) : x;
+                const uint64_t pk = pack_key(key, v);
+                if ((!vtail || v < a.V) && pk > sel[tb]) sel[tb] = pk;
+              }
+            }
+        } else if constexpr (!BWD) {
           float mx = -INFINITY;
 #pragma unroll
           for (int vb = 0; vb < 2; ++vb)
@@ -240,7 +302,19 @@ __global__ __launch_bounds__(kThreads) void fused_linear_kernel(FlArgs a) {
     }
     __syncthreads();
   }
-  if constexpr (!BWD) {
+  if constexpr (MODE == MODE_SELECT) {
+    // max over the 8 (vocab wave, lane half) partials of each token, then one atomic per (token, chunk)
+    unsigned long long* sb = reinterpret_cast<unsigned long long*>(lds);  // [256 tokens][8]
+#pragma unroll
+    for (int tb = 0; tb < 4; ++tb) sb[(wt * 128 + tb * 32 + (lane & 31)) * 8 + wv * 2 + hi] = sel[tb];
+    __syncthreads();
+    if (tid < kBT && t0 + tid < a.N) {
+      unsigned long long b = 0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) b = sb[tid * 8 + k] > b ? sb[tid * 8 + k] : b;
+      __hip_atomic_fetch_max(a.best + t0 + tid, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  } else if constexpr (!BWD) {
     // merge the 8 partial states of each token (4 vocab waves x 2 lane halves) in a fixed order
     float* st = reinterpret_cast<float*>(lds);  // [256 tokens][8 slots][3]
 #pragma unroll
@@ -293,6 +367,26 @@ __global__ __launch_bounds__(256) void fused_linear_merge_kernel(const float* pa
   if (logp) logp[t] = zlab[t] - l;
   if (ent) ent[t] = l - szz / ss;
   if (lse) lse[t] = l;
+}
+
+// one thread per token: decode the winning index, reset best[t], finished-row / EOS bookkeeping
+// (select_finish_kernel of csrc/vocab.hip)
+__global__ __launch_bounds__(256) void fused_select_finish_kernel(unsigned long long* best, int64_t N,
+                                                                  const int64_t* dev_step, int64_t pad,
+                                                                  const int64_t* eos, int n_eos, int32_t* unfinished,
+                                                                  int64_t* out, int64_t ld_out) {
+  const int64_t r = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (r >= N) return;
+  const unsigned long long b = best[r];
+  best[r] = 0;
+  const int64_t choice = static_cast<int64_t>(0xFFFFFFFFu - static_cast<uint32_t>(b));
+  const bool alive = unfinished ? unfinished[r] != 0 : true;
+  const int64_t tok = alive ? choice : pad;
+  out[r * ld_out + (dev_step ? *dev_step : 0)] = tok;
+  if (unfinished && alive) {
+    for (int k = 0; k < n_eos; ++k)
+      if (tok == eos[k]) { unfinished[r] = 0; break; }
+  }
 }
 
 struct Plan {
@@ -352,7 +446,7 @@ int drl_linear_logprob_fwd(const void* hidden, int64_t ld_h, const void* weight,
   a.part = static_cast<float*>(workspace);
   a.zlab = a.part + static_cast<size_t>(p.nchunks) * 3 * N;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(fused_linear_kernel<false>, dim3(p.tok_tiles * p.nchunks), dim3(kThreads),
+  hipLaunchKernelGGL(fused_linear_kernel<MODE_LOGPROB>, dim3(p.tok_tiles * p.nchunks), dim3(kThreads),
                      0, s, a);
   hipLaunchKernelGGL(fused_linear_merge_kernel, dim3(static_cast<unsigned>((N + 255) / 256)), dim3(256), 0, s, a.part,
                      a.zlab, N, p.nchunks, logp, entropy, lse);
@@ -392,8 +486,56 @@ int drl_linear_logprob_dlogits(const void* hidden, int64_t ld_h, const void* wei
   a.ent = entropy;
   a.dlt = static_cast<uint16_t*>(dlogits_t);
   a.ld_dl = ld_dl;
-  hipLaunchKernelGGL(fused_linear_kernel<true>, dim3(p.tok_tiles * p.nchunks), dim3(kThreads),
+  hipLaunchKernelGGL(fused_linear_kernel<MODE_DLOGITS>, dim3(p.tok_tiles * p.nchunks), dim3(kThreads),
                      0, static_cast<hipStream_t>(stream), a);
+  DRL_LAUNCH_CHECK();
+  return DRL_OK;
+}
+
+size_t drl_linear_select_tokens_workspace_bytes(int64_t N) { return N > 0 ? static_cast<size_t>(N) * 8 : 0; }
+
+int drl_linear_select_tokens(const void* hidden, int64_t ld_h, const void* weight, int32_t dt, int64_t N, int64_t H,
+                             int64_t V, const drl_sampling_params* p, int32_t* unfinished, int64_t* out_tokens,
+                             int64_t ld_out, void* workspace, size_t workspace_bytes, void* stream) {
+  using namespace drl;
+  DRL_CHECK_ARG(hidden && weight && p && out_tokens, "NULL input");
+  DRL_CHECK_ARG(dt == DRL_BF16, "the fused lm_head runs on bf16 operands");
+  DRL_CHECK_ARG(N >= 1 && V >= 1 && V < (int64_t(1) << 32) && H >= 64 && H % 64 == 0 && ld_h >= H && ld_h % 8 == 0,
+                "bad shape (H % 64 == 0)");
+  DRL_CHECK_ARG(aligned16(hidden) && aligned16(weight), "hidden / weight must be 16-byte aligned");
+  DRL_CHECK_ARG(p->n_eos == 0 || p->eos_ids != nullptr, "n_eos > 0 but eos_ids is NULL");
+  const bool sample = p->do_sample && p->temperature > 0.f;
+  if (sample && ((p->top_k > 0 && p->top_k < V) || p->top_p < 1.0f))
+    return fail(DRL_ERR_UNSUPPORTED, "top-k / top-p filtering is not implemented in this build");
+  if (!workspace || workspace_bytes < drl_linear_select_tokens_workspace_bytes(N) ||
+      (reinterpret_cast<uintptr_t>(workspace) & 7u))
+    return fail(DRL_ERR_WORKSPACE, "select workspace: need %zu 8-byte aligned bytes, zeroed",
+                drl_linear_select_tokens_workspace_bytes(N));
+  const Plan pl = make_plan(N, V);
+  FlArgs a{};
+  a.h = static_cast<const uint16_t*>(hidden);
+  a.ld_h = ld_h;
+  a.w = static_cast<const uint16_t*>(weight);
+  a.N = N;
+  a.H = H;
+  a.V = V;
+  a.inv_t = 1.f;
+  a.l2e_t = 1.4426950408889634f;
+  a.tok_tiles = pl.tok_tiles;
+  a.tiles_per_chunk = pl.tiles_per_chunk;
+  a.nchunks = pl.nchunks;
+  a.vtiles = pl.vtiles;
+  a.do_sample = sample;
+  a.temp = sample ? p->temperature : 1.f;
+  a.seed = p->seed;
+  a.offset = p->offset;
+  a.row_base = p->row_base;
+  a.dev_step = p->dev_step;
+  a.best = static_cast<unsigned long long*>(workspace);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(fused_linear_kernel<MODE_SELECT>, dim3(pl.tok_tiles * pl.nchunks), dim3(kThreads), 0, s, a);
+  hipLaunchKernelGGL(fused_select_finish_kernel, dim3(static_cast<unsigned>((N + 255) / 256)), dim3(256), 0, s, a.best,
+                     N, p->dev_step, p->pad_token_id, p->eos_ids, p->n_eos, unfinished, out_tokens, ld_out);
   DRL_LAUNCH_CHECK();
   return DRL_OK;
 }

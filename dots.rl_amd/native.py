@@ -321,6 +321,29 @@ def select_tokens(logits, out_tokens, *, do_sample=False, temperature=1.0, top_k
     return out_tokens
 
 
+def linear_select_tokens(hidden, weight, out_tokens, *, do_sample=False, temperature=1.0, top_k=0, top_p=1.0, seed=0,
+                         step=0, row_base=0, pad_token_id=0, eos_ids=None, unfinished=None, dev_step=None):
+    """select_tokens on the bf16 logits hidden @ weight^T without writing them (lm_head fused with K4,
+    csrc/fused_linear.hip): hidden (N, H) bf16, weight (V, H) bf16, H % 64 == 0."""
+    _dev(hidden, weight, out_tokens, eos_ids, unfinished)
+    assert hidden.dim() == 2 and hidden.stride(1) == 1 and weight.is_contiguous()
+    assert hidden.dtype == weight.dtype == torch.bfloat16
+    N, H = hidden.shape
+    V = weight.shape[0]
+    assert out_tokens.dtype == torch.int64 and out_tokens.numel() == N
+    ld_out = out_tokens.stride(0) if out_tokens.dim() == 1 else 1
+    ws = _select_workspace(hidden.device, N)
+    prm = _lib.SamplingParams(int(bool(do_sample)), float(temperature), int(top_k), float(top_p),
+                              int(seed) & 0xFFFFFFFFFFFFFFFF, int(step), int(row_base), int(pad_token_id),
+                              None if eos_ids is None else eos_ids.data_ptr(),
+                              0 if eos_ids is None else eos_ids.numel(),
+                              None if dev_step is None else dev_step.data_ptr())
+    check(lib().drl_linear_select_tokens(_p(hidden), hidden.stride(0), _p(weight), _lib.DRL_BF16, N, H, V,
+                                         ctypes.byref(prm), _p(unfinished), _p(out_tokens), ld_out, _p(ws),
+                                         ws.numel() * 8, _stream()), "drl_linear_select_tokens")
+    return out_tokens
+
+
 _SELECT_WS = {}
 
 

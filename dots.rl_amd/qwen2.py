@@ -469,6 +469,14 @@ class Qwen2Model:
             return _Linear.apply(h, self.store.w(name), self.store.g(name), self._dummy)
         return F.linear(h, self.store.w(name))
 
+    def select_tokens(self, h, out_tokens, fused=True, **sel):
+        """Token selection from the final-norm hidden h (N, H): K4 fused with the lm_head on bf16 (the (N, V)
+        logits are never written, csrc/fused_linear.hip), else lm_head logits + K4 (fp32 parity model)."""
+        w = self.store.w(self.lm_head_weight())
+        if fused and self.dtype == torch.bfloat16 and h.shape[-1] % 64 == 0:
+            return native.linear_select_tokens(h.contiguous(), w, out_tokens, **sel)
+        return native.select_tokens(self.logits(h), out_tokens, **sel)
+
     def fused_logprob(self, h, labels, temperature, calculate_entropy):
         """A21: h (N, H) in bf16 -> (log_probs, entropy or None) over the lm_head without materialising logits
         (csrc/fused_linear.hip); in training the weight gradient accumulates into the fp32 gradient buffer."""
@@ -543,7 +551,7 @@ class Qwen2Model:
 
 
 class PackedDecode:
-    """Decode step on fragment-packed operands (csrc/decode_gemm.hip) for one rollout of B <= 256 sequences:
+    """Decode step on fragment-packed operands (csrc/decode_gemm.hip) for one rollout of B <= 512 sequences:
     per layer decode RMSNorm (packed out) -> qkv GEMM with bias + RoPE + cache writes in its epilogue (weights
     packed in rotation pairs) -> MFMA decode attention (packed out) -> o_proj GEMM (fp32 K-slice partials) ->
     decode RMSNorm (adds the o_proj partials) -> gate_up GEMM with the SwiGLU epilogue (packed out) ->
@@ -553,13 +561,13 @@ class PackedDecode:
     graph-capturable. Module math is the unpacked decode path's (bf16 module outputs, fp32 residual)."""
 
     @staticmethod
-    def supported(model, B):
+    def supported(model, B, max_rows=512):
         cfg = model.cfg
         H, I, D = cfg.hidden_size, cfg.intermediate_size, cfg.head_dim
         NQ = (cfg.num_attention_heads + 2 * cfg.num_key_value_heads) * D
-        # up to 256 rows: at 512 (one GPU holding the whole batch) hipBLASLt's tiles are as fast and the
-        # unpacked path is kept (tools/kernel_bench.py --only decode_gemm; bench step 1.22 vs 1.55 s rollout)
-        return (B <= 256 and model.dtype == torch.bfloat16 and D in (64, 128) and H % 64 == 0 and I % 64 == 0
+        # 1..512 rows (rollout at B=64: 0.66 -> 0.38 s; at B=512 1.20 -> 1.18 s, tools/kernel_bench.py
+        # --only decode_gemm for the per-projection times)
+        return (B <= max_rows and model.dtype == torch.bfloat16 and D in (64, 128) and H % 64 == 0 and I % 64 == 0
                 and (cfg.num_attention_heads * D) % 64 == 0 and I % 16 == 0
                 and all(native.decode_gemm_plan(B, n, k, sw) is not None
                         for n, k, sw in ((NQ, H, False), (H, cfg.num_attention_heads * D, False), (2 * I, H, True),

@@ -76,13 +76,17 @@ class MI355XRollout:
         sel = dict(do_sample=do_sample and temperature > 0, temperature=temperature if do_sample else 1.0, top_k=top_k,
                    top_p=top_p, seed=seed, row_base=row_base, pad_token_id=pad_token_id, eos_ids=stop_ids,
                    unfinished=unfinished)
-        native.select_tokens(m.logits(h), responses[:, 0], step=0, **sel)
+        # lm_head fused with K4 (csrc/fused_linear.hip, no logits written) measured slower than hipBLASLt's
+        # lm_head + K4 at 64 and 512 rows (rollout 0.43 vs 0.38 s, 1.22 vs 1.20 s): opt-in
+        fused = bool(cfg.get("fused_select", False))
+        self._fused_select = fused
+        m.select_tokens(h, responses[:, 0], fused=fused, step=0, **sel)
         if cfg.get("use_hip_graph", True) and R > 2:
             self._decode_graphed(cache, responses, last_pos, P, R, sel)
         else:
             for t in range(1, R):
                 h = m.decode_step(cache, responses[:, t - 1], last_pos + t)
-                native.select_tokens(m.logits(h), responses[:, t], step=t, **sel)
+                m.select_tokens(h, responses[:, t], fused=fused, step=t, **sel)
         del cache
         seq = torch.cat([idx, responses], dim=-1)
         # hf_rollout.py:151-160: positions continue from the last prompt position; mask up to first EOS
@@ -110,7 +114,9 @@ class MI355XRollout:
         m = self.module
         t_dev = torch.ones(1, dtype=torch.int64, device=responses.device)
         B = responses.shape[0]
-        packed = PackedDecode(m, B) if self.config.get("packed_decode", True) and PackedDecode.supported(m, B) else None
+        max_rows = int(self.config.get("packed_decode_max_rows", 512))
+        use = self.config.get("packed_decode", True) and PackedDecode.supported(m, B, max_rows)
+        packed = PackedDecode(m, B) if use else None
         self.last_packed_decode = packed is not None
 
         def body():
@@ -119,7 +125,7 @@ class MI355XRollout:
                 h = packed.step(cache, tok, last_pos + t_dev, t_dev + (P - 1))
             else:
                 h = m.decode_step_dev(cache, tok, last_pos + t_dev, t_dev + (P - 1))
-            native.select_tokens(m.logits(h), responses[:, 0], step=0, dev_step=t_dev, **sel)
+            m.select_tokens(h, responses[:, 0], fused=self._fused_select, step=0, dev_step=t_dev, **sel)
             t_dev.add_(1)
 
         body()  # t = 1, eager

@@ -357,6 +357,16 @@ int drl_linear_logprob_dlogits(const void* hidden, int64_t ld_h, const void* wei
                                const float* dentropy, const float* lse, const float* entropy, void* dlogits_t,
                                int64_t ld_dl, void* stream);
 
+/* K4 fused with the lm_head (decode): token selection straight from hidden (N, ld_h) bf16 and the lm_head
+ * weight (V, H) bf16 without writing the (N, V) logits — drl_select_tokens' semantics on the bf16 logits
+ * bf16(hidden W^T) (greedy argmax, lowest index on ties; or the exponential race with the same Philox draw),
+ * the same params / unfinished / EOS bookkeeping. workspace: drl_linear_select_tokens_workspace_bytes(N)
+ * bytes, 8-byte aligned, zero-filled before the first call and left zeroed by every call. H % 64 == 0. */
+size_t drl_linear_select_tokens_workspace_bytes(int64_t N);
+int drl_linear_select_tokens(const void* hidden, int64_t ld_h, const void* weight, int32_t dt, int64_t N, int64_t H,
+                             int64_t V, const drl_sampling_params* params, int32_t* unfinished, int64_t* out_tokens,
+                             int64_t ld_out, void* workspace, size_t workspace_bytes, void* stream);
+
 /* ---- Decode-step projections on fragment-packed operands (csrc/decode_gemm.hip). Replace the per-token
  * nn.Linear / RMSNorm / rotary calls of HF generate (hf_rollout.py:112-124 -> modeling_qwen2) for 1..512
  * token rows. Packed layout of an activation panel (M rows, K columns, MBT 32-row blocks, MBT >= M/32):

@@ -214,11 +214,15 @@ def test_packed_rollout_graph_equals_eager():
     cache = KVCache(cfg, B, P + R, DEV, BF)
     h = m.prefill(cache, ids, am, pos)
     pk = PackedDecode(m, B)
-    toks = [m.logits(h).float().argmax(-1)]
+    def pick(h):
+        out = torch.empty(B, dtype=torch.int64, device=DEV)
+        return m.select_tokens(h, out, fused=True)
+
+    toks = [pick(h)]
     for t in range(1, R):
         kd = torch.tensor([P + t - 1], device=DEV)
         h = pk.step(cache, toks[-1].view(B, 1), pos[:, -1] + t, kd)
-        toks.append(m.logits(h).float().argmax(-1))
+        toks.append(pick(h))
     assert torch.equal(resp, torch.stack(toks, 1))
     assert out.batch["input_ids"].shape == (B, P + R)
 
@@ -258,3 +262,34 @@ def test_decode_qkv_rope_matches_gemm_then_rope(M, K, Hq, Hkv, D):
         outs.append((q, kc, vt))
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("N,H,V", [(64, 896, 151936), (300, 128, 5003), (1, 64, 257)])
+@pytest.mark.parametrize("sample", [False, True])
+def test_linear_select_matches_unfused(N, H, V, sample):
+    """lm_head fused with K4 (no logits written) against K4 on the bf16 logits of the same GEMM: the same token
+    wherever the fp32 sums round to the same bf16 logits (>= 99 % of rows; a differing row must be a
+    near-tie: its pick is within one bf16 ulp of the unfused pick's logit)."""
+    h = rnd(N, H, seed=N)
+    w = rnd(V, H, scale=0.05, seed=V)
+    kw = dict(do_sample=sample, temperature=0.8 if sample else 1.0, seed=1234, step=3, row_base=5)
+    a = native.linear_select_tokens(h, w, torch.empty(N, dtype=torch.int64, device=DEV), **kw)
+    logits = h @ w.t()
+    b = native.select_tokens(logits, torch.empty(N, dtype=torch.int64, device=DEV), **kw)
+    same = (a == b).float().mean().item()
+    assert same >= (0.99 if N >= 100 else 0.95), same
+    lf = logits.float()
+    for r in torch.nonzero(a != b).flatten().tolist():
+        la, lb = lf[r, a[r]].item(), lf[r, b[r]].item()
+        if not sample:
+            assert abs(la - lb) <= 2.0 ** -7 * max(abs(la), abs(lb)) + 1e-6
+    # finished rows get the pad token, EOS finishes a row
+    unf = torch.ones(N, dtype=torch.int32, device=DEV)
+    unf[0] = 0
+    eos = a[-1:].clone()
+    out = native.linear_select_tokens(h, w, torch.empty(N, dtype=torch.int64, device=DEV), pad_token_id=7,
+                                      eos_ids=eos, unfinished=unf, **kw)
+    assert out[0].item() == 7 or N == 1
+    if N > 1:
+        assert unf[-1].item() == 0
+    assert torch.equal(out[1:], a[1:]) or N == 1

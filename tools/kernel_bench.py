@@ -351,6 +351,28 @@ def decode_gemm(Ms=(32, 64, 128, 256, 512)):
     return res
 
 
+def train_gemms(Ms=(6144, 12288)):
+    """hipBLASLt on the transformer GEMMs of the log-prob / update micro-batches (replayed TunableOp choices):
+    forward y = x W^T, backward dx = dy W and dW += dy^T x (fp32 accumulate in place)."""
+    from dots.rl_amd.workers import _enable_gemm_tuning
+    _enable_gemm_tuning("auto")
+    dev, bf = "cuda", torch.bfloat16
+    res = []
+    for name, N, K in (("qkv", 1152, 896), ("o_proj", 896, 896), ("gate_up", 9728, 896), ("down", 896, 4864)):
+        w = torch.randn(N, K, device=dev, dtype=bf) * 0.05
+        gw = torch.zeros(N, K, device=dev)
+        for M in Ms:
+            x = torch.randn(M, K, device=dev, dtype=bf)
+            dy = torch.randn(M, N, device=dev, dtype=bf)
+            fl = 2.0 * M * N * K
+            tf = time_it(lambda: x @ w.t())
+            tb = time_it(lambda: dy @ w)
+            tw = time_it(lambda: torch.addmm(gw, dy.t(), x, out_dtype=torch.float32, out=gw))
+            res.append(dict(kernel="train_gemm", layer=name, M=M, N=N, K=K, fwd_us=tf * 1e6, fwd_TF=fl / tf / 1e12,
+                            dx_us=tb * 1e6, dx_TF=fl / tb / 1e12, dw_us=tw * 1e6, dw_TF=fl / tw / 1e12))
+    return res
+
+
 def launch_floor(B=64, H=896, I=4864):
     """Per-call time of tiny kernels replayed back to back from a HIP graph: the launch/dependency floor of a
     decode step, next to the small hand-written decode kernels at B rows."""
@@ -388,6 +410,10 @@ if __name__ == "__main__":
         sys.exit(0)
     if args.only == "linear":
         for r in launch_floor() + linear():
+            print(json.dumps(r), flush=True)
+        sys.exit(0)
+    if args.only == "train_gemms":
+        for r in train_gemms():
             print(json.dumps(r), flush=True)
         sys.exit(0)
     if args.only == "decode_gemm":
