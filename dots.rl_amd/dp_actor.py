@@ -47,6 +47,7 @@ class FlatAdamW:
         self.step_count = 0
         self.sched_step = 0
         self.norm = torch.zeros(1, dtype=torch.float32, device=store.master.device)
+        self._pending = []
 
     def current_lr(self):
         if self.warmup_steps > 0 and self.sched_step < self.warmup_steps:
@@ -56,12 +57,55 @@ class FlatAdamW:
     def zero_grad(self):
         self.store.zero_grad()
 
+    # ------------------------------------------------------------------ gradient averaging across DP ranks
+    def distributed(self):
+        return dist.is_initialized() and dist.get_world_size(self.group) > 1
+
+    def begin_overlap(self, model):
+        """Before the LAST micro-batch's backward of an optimizer step: every decoder layer's gradient slice
+        is all-reduced (async, RCCL's own stream, ordered after the layer's backward kernels) as soon as its
+        backward finishes, so the 24 slices (73 % of the bytes for Qwen2.5-0.5B) travel under the rest of the
+        backward. The embedding / lm_head and final-norm slices are complete only at the end (allreduce_rest)."""
+        self._pending = []
+        if not self.distributed():
+            return
+
+        def hook(i):
+            a, b = self.store.layer_range(i)
+            self._pending.append((a, b, dist.all_reduce(self.store.grad[a:b], op=dist.ReduceOp.AVG, group=self.group,
+                                                        async_op=True)))
+
+        model.grad_ready_hook = hook
+
+    def end_overlap(self, model):
+        model.grad_ready_hook = None
+
+    def allreduce_grads(self):
+        """AVG-all-reduce every gradient byte not already reduced by begin_overlap's per-layer work, then
+        wait for all of it (the optimizer kernels run after this on the current stream)."""
+        if not self.distributed():
+            self._pending = []
+            return
+        g = self.store.grad
+        done = sorted((a, b) for a, b, _ in getattr(self, "_pending", []))
+        gaps, pos = [], 0
+        for a, b in done:
+            if a > pos:
+                gaps.append((pos, a))
+            pos = max(pos, b)
+        if pos < g.numel():
+            gaps.append((pos, g.numel()))
+        works = [w for _, _, w in getattr(self, "_pending", [])]
+        works += [dist.all_reduce(g[a:b], op=dist.ReduceOp.AVG, group=self.group, async_op=True) for a, b in gaps]
+        for w in works:
+            w.wait()
+        self._pending = []
+
     def step(self):
         """All-reduce (average) the flat gradient across DP ranks, then norm -> clip -> AdamW in HIP.
         Returns the device grad-norm tensor (the reference returns clip_grad_norm_'s total norm)."""
         g = self.store.grad
-        if dist.is_initialized() and dist.get_world_size(self.group) > 1:
-            dist.all_reduce(g, op=dist.ReduceOp.AVG, group=self.group)
+        self.allreduce_grads()
         native.grad_norm(g, out=self.norm)
         self.step_count += 1
         params_bf16 = None if self.store.compute is self.store.master else self.store.compute
@@ -148,7 +192,9 @@ class DataParallelPPOActor:
                 grad_accum = cfg.ppo_mini_batch_size // cfg.ppo_micro_batch_size_per_gpu
                 micro_batches = mini_batch.split(cfg.ppo_micro_batch_size_per_gpu)
                 self.actor_optimizer.zero_grad()
-                for micro_batch in micro_batches:
+                for k, micro_batch in enumerate(micro_batches):
+                    if k == len(micro_batches) - 1:  # gradients final after this backward: overlap the all-reduce
+                        self.actor_optimizer.begin_overlap(m)
                     mb = micro_batch.batch
                     lsf = 1.0 / grad_accum
                     calculate_entropy = cfg.entropy_coeff != 0
@@ -162,6 +208,7 @@ class DataParallelPPOActor:
                     out[6].backward()
                     mb_out.append(out.detach())
                     mb_lsf.append(lsf)
+                self.actor_optimizer.end_overlap(m)
                 grad_norms.append(self.actor_optimizer.step().clone())
         self.actor_optimizer.zero_grad()
         m.training = False

@@ -164,6 +164,13 @@ class ParamStore:
         if self.grad is not None:
             self.grad.zero_()
 
+    def layer_range(self, i):
+        """[start, end) of decoder layer i's parameters in the flat buffers (contiguous, buffer order)."""
+        names = [n for n, _, _ in self.specs if n.startswith(f"layers.{i}.")]
+        start = self.offsets[names[0]][0]
+        last = self.offsets[names[-1]]
+        return start, last[0] + math.prod(last[1])
+
 
 # --------------------------------------------------------------------------------------------- GEMM helpers
 def acc_wgrad(gw, dy, x):
@@ -387,6 +394,8 @@ class _DecoderLayer(torch.autograd.Function):
         dx = dx2  # residual: x2 = x + o
         native.rmsnorm_bwd(sv["x"], s.w(p + "input_layernorm"), sv["rstd1"], dh1, dx, s.g(p + "input_layernorm"))
         ctx.save = None
+        if m.grad_ready_hook is not None:  # layer i's gradient is complete for this micro-batch
+            m.grad_ready_hook(i)
         return dx, (dx.to(g_mlp.dtype) if ctx.has_delta else None), None, None, None, None
 
 
@@ -455,6 +464,8 @@ class Qwen2Model:
         self.cos = freqs.cos().contiguous()
         self.sin = freqs.sin().contiguous()
         self._dummy = torch.empty(0, device=dev, requires_grad=True)
+        # called with layer index i at the end of layer i's backward (FlatAdamW's overlapped all-reduce)
+        self.grad_ready_hook = None
 
     def _gw(self, name):
         return self.store.g(name) if (self.training and self.store.trainable) else None

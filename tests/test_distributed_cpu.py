@@ -4,7 +4,8 @@
   batch in rank order on every rank (decorator.py:213-312 chunk / concat semantics);
 * ONE_TO_ALL / RANK_ZERO dispatch;
 * DataProto.all_gather of tensors + non-tensor (uid) arrays;
-* gradient averaging of the flat buffer (the RCCL all-reduce of FlatAdamW.step, AVG) on gloo.
+* gradient averaging of the flat buffer (the RCCL all-reduce of FlatAdamW.step, AVG) on gloo, and its
+  overlapped per-layer form (async all-reduce per decoder layer from the backward hook).
 """
 
 import os
@@ -97,6 +98,42 @@ def _grad_avg_case(rank, world):
 def test_flat_gradient_average():
     out = spawn(_grad_avg_case)
     assert out[0] == out[1] == [1.5, 1.5, 1.5]
+
+
+def _overlap_case(rank, world):
+    import types
+
+    from dots.rl_amd.dp_actor import FlatAdamW
+    from dots.rl_amd.qwen2 import ParamStore, Qwen2Config
+
+    cfg = Qwen2Config.from_dict(dict(vocab_size=64, hidden_size=32, intermediate_size=64, num_hidden_layers=3,
+                                     num_attention_heads=2, num_key_value_heads=1, max_position_embeddings=64,
+                                     tie_word_embeddings=True))
+    store = ParamStore(cfg, "cpu", compute_dtype=torch.float32, trainable=True)
+    g = torch.Generator().manual_seed(rank)
+    store.grad.copy_(torch.randn(store.grad.shape, generator=g))
+    want = store.grad.clone()
+    dist.all_reduce(want, op=dist.ReduceOp.AVG)  # the monolithic form
+    opt = FlatAdamW(store, lr=1e-3)
+    model = types.SimpleNamespace(grad_ready_hook=None)
+    opt.begin_overlap(model)
+    for i in reversed(range(cfg.num_hidden_layers)):  # backward order: last layer first
+        model.grad_ready_hook(i)
+    opt.end_overlap(model)
+    assert model.grad_ready_hook is None
+    opt.allreduce_grads()
+    ranges = [store.layer_range(i) for i in range(cfg.num_hidden_layers)]
+    return dict(equal=bool(torch.equal(store.grad, want)), ranges=ranges, n=store.grad.numel())
+
+
+def test_overlapped_gradient_allreduce_matches_monolithic():
+    """FlatAdamW's per-layer async all-reduce (started from the layer backward hook of the last micro-batch)
+    plus the rest-of-buffer all-reduce averages exactly what one all-reduce of the flat gradient does."""
+    out = spawn(_overlap_case)
+    assert out[0]["equal"] and out[1]["equal"]
+    ranges = out[0]["ranges"]
+    assert all(a < b for a, b in ranges) and all(ranges[k][1] <= ranges[k + 1][0] for k in range(len(ranges) - 1))
+    assert ranges[0][0] > 0 and ranges[-1][1] < out[0]["n"]  # embedding before, final norm after
 
 
 def test_config_overrides():
