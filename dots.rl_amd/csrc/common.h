@@ -70,6 +70,19 @@ __device__ __forceinline__ uint16_t f32_to_bf16(float f) {
   return static_cast<uint16_t>(u >> 16);
 }
 
+// Sampling as a race of exponential clocks (the Gumbel-max form of the categorical draw): token i wins iff
+// z_i - log(E_i) is the row maximum, E_i = -log(1 - v_i) ~ Exp(1) with v_i = ((bits >> 8) + 0.5) / 2^24 a
+// 24-bit Philox uniform in (0, 1). Hardware log2 (v_log_f32) instead of libm: E from a 4-term series below
+// v = 2^-6 (relative error < 3e-8, where E is small and the key large) and from log2(1 - v) above (1 - v is
+// rounded to 2^-25, i.e. < 2e-6 relative in E at v = 2^-6); log(E) = ln2 * log2(E). Keys stay within 2e-6
+// of the libm / numpy float32 form the oracle uses (oracle.race_keys).
+__device__ __forceinline__ float race_key(float z, uint32_t bits) {
+  const float v = (static_cast<float>(bits >> 8) + 0.5f) * (1.0f / 16777216.0f);
+  const float e = v < 0.015625f ? v * (1.f + v * (0.5f + v * (0.33333334f + v * 0.25f)))
+                                : -0.6931471805599453f * __builtin_amdgcn_logf(1.f - v);
+  return z - 0.6931471805599453f * __builtin_amdgcn_logf(e);
+}
+
 // Mask element -> 0/1 float, for the mask dtypes the boundary accepts.
 template <int DT>
 __device__ __forceinline__ float mask_at(const void* m, int64_t i) {

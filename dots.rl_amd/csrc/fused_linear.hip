@@ -72,7 +72,7 @@ struct FlArgs {
 
 constexpr int MODE_LOGPROB = 0, MODE_DLOGITS = 1, MODE_SELECT = 2;
 
-// Philox4x32-10 block and the sampling race key / order-preserving packing of csrc/vocab.hip (K4): the same
+// Philox4x32-10 block and the order-preserving key packing of csrc/vocab.hip (K4; race_key in common.h): the same
 // draw for the same (seed, offset, row, index), so the fused and the unfused selection agree.
 __device__ __forceinline__ uint4 philox4(uint64_t seed, uint64_t offset, uint64_t counter) {
   uint32_t c0 = static_cast<uint32_t>(counter), c1 = static_cast<uint32_t>(counter >> 32);
@@ -91,10 +91,6 @@ __device__ __forceinline__ uint4 philox4(uint64_t seed, uint64_t offset, uint64_
     k1 += 0xBB67AE85u;
   }
   return make_uint4(c0, c1, c2, c3);
-}
-__device__ __forceinline__ float race_key(float z, uint32_t bits) {
-  const float v = (static_cast<float>(bits >> 8) + 0.5f) * (1.0f / 16777216.0f);
-  return z - logf(-log1pf(-v));
 }
 __device__ __forceinline__ uint64_t pack_key(float key, int64_t idx) {
   uint32_t b = __float_as_uint(key);
@@ -231,7 +227,7 @@ __global__ __launch_bounds__(kThreads) void fused_linear_kernel(FlArgs a) {
               for (int j = 0; j < 4; ++j) {
                 const int64_t v = v0 + j;
                 const float x = bf16_to_f32(to_bf16_bits(acc[vb][tb][4 * g4 + j]));
-                const float key = a.do_sample ? race_key(x / a.temp, bits[j]) : x;
+                const float key = a.do_sample ? race_key(a.temp != 1.f ? x / a.temp : x, bits[j]) : x;
                 const uint64_t pk = pack_key(key, v);
                 if ((!vtail || v < a.V) && pk > sel[tb]) sel[tb] = pk;
               }

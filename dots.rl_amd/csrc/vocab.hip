@@ -253,14 +253,8 @@ __device__ __forceinline__ uint4 philox4(uint64_t seed, uint64_t offset, uint64_
   return make_uint4(c0, c1, c2, c3);
 }
 
-// Sampling as a race of exponential clocks (the Gumbel-max form of the categorical draw): token i wins
-// iff z_i - log(E_i) is the row maximum, E_i = -log(1 - v_i) ~ Exp(1) with v_i a 24-bit Philox uniform
-// in (0, 1). Exactly softmax(z)-distributed, and a single max-reduction: the row splits across
-// workgroups with no scan (the inverse CDF needs a prefix sum over the whole vocabulary).
-__device__ __forceinline__ float race_key(float z, uint32_t bits) {
-  const float v = (static_cast<float>(bits >> 8) + 0.5f) * (1.0f / 16777216.0f);
-  return z - logf(-log1pf(-v));
-}
+// Sampling: race_key (common.h), the exponential race — exactly softmax(z)-distributed and a single
+// max-reduction, so the row splits across workgroups with no scan (the inverse CDF needs a prefix sum).
 
 // (key, index) -> one u64 whose unsigned max is torch.argmax: order-preserving key bits (NaN = maximum)
 // in the high word, ~index in the low word (ties -> lowest index)
@@ -299,7 +293,7 @@ __global__ __launch_bounds__(kThreads) void select_slice_kernel(SelectArgs a) {
   const uint64_t off = a.offset + (a.dev_step ? static_cast<uint64_t>(*a.dev_step) : 0ull);
   const uint64_t ctr_row = static_cast<uint64_t>(a.row_base + r) << 32;
   auto key_of = [&](float x, uint32_t bits) -> float {
-    if constexpr (SAMPLE) return race_key(scale_logit<DT>(x, a.temp, true, false), bits);
+    if constexpr (SAMPLE) return race_key(scale_logit<DT>(x, a.temp, a.temp != 1.0f, false), bits);
     else return x;
   };
   uint64_t best = 0;

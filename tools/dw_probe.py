@@ -43,8 +43,15 @@ def main():
         t2 = time_it(lambda: gw.add_(torch.mm(dy.t(), x)))
         gwt = gw.t()
         t3 = time_it(lambda: torch.addmm(gwt, x.t(), dy, out_dtype=torch.float32, out=gwt))
+        # v4: explicit transposed copies, then the forward's layout (reduction dim contiguous in both operands)
+        t4 = time_it(lambda: torch.addmm(gw, dy.t().contiguous(), x.t().contiguous().t(), out_dtype=torch.float32,
+                                         out=gw))
+        dyt, xt = dy.t().contiguous(), x.t().contiguous()
+        t4g = time_it(lambda: torch.addmm(gw, dyt, xt.t(), out_dtype=torch.float32, out=gw))
+        t4b = time_it(lambda: torch.mm(dyt, xt.t()))
         print(json.dumps(dict(layer=name, M=M, N=N, K=K, v1_us=t1 * 1e6, v1_TF=fl / t1 / 1e12, v2_mm_us=t2m * 1e6,
-                              v2_us=t2 * 1e6, v2_TF=fl / t2 / 1e12, v3_us=t3 * 1e6, v3_TF=fl / t3 / 1e12)), flush=True)
+                              v2_us=t2 * 1e6, v2_TF=fl / t2 / 1e12, v3_us=t3 * 1e6, v3_TF=fl / t3 / 1e12, v4_us=t4 * 1e6,
+                              v4_gemm_us=t4g * 1e6, v4_bf16_gemm_us=t4b * 1e6)), flush=True)
     print("\n".join(",".join(map(str, r)) for r in tunable.get_results()), file=sys.stderr)
 
 
