@@ -127,6 +127,7 @@ SIGNATURES = {
     "drl_linear_logprob_workspace_bytes": (SZ, [I64, I64, I64]),
     "drl_linear_select_tokens_workspace_bytes": (SZ, [I64]),
     "drl_linear_select_tokens": (ctypes.c_int, [P, I64, P, I32, I64, I64, I64, P, P, P, I64, P, SZ, P]),
+    "drl_decode_attention_set_variant": (None, [I32]),
     "drl_decode_gemm_plan": (ctypes.c_int, [I64, I64, I64, I32, P, P]),
     "drl_decode_gemm_set_plan": (None, [I32, I32]),
     "drl_decode_pack_weight_elems": (SZ, [I64, I64, I32]),

@@ -813,13 +813,77 @@ __device__ __forceinline__ void dec_block(const DecBlock<D>& blk, const bf16x8 (
   }
 }
 
+// raw block -> the wave's LDS slot only (fragments are read just in time by dec_block_lds)
+template <int D>
+__device__ __forceinline__ void dec_stage(const DecRaw<D>& r, uint16_t* ks, uint16_t* vs, int lane) {
+  constexpr int UPR = D / 8;
+#pragma unroll
+  for (int i = 0; i < D / 16; ++i) {
+    const int c = lane + 64 * i, row = c / UPR, u = c % UPR;
+    *reinterpret_cast<u16x8*>(ks + row * D + 8 * (u ^ (row & 7))) = r.k[i];
+    const int d = c >> 2, t0 = 2 * (c & 3), sw = (d >> 2) & 7;
+    *reinterpret_cast<u16x4*>(vs + d * 32 + 4 * (t0 ^ sw)) = u16x4{r.v[i][0], r.v[i][1], r.v[i][2], r.v[i][3]};
+    *reinterpret_cast<u16x4*>(vs + d * 32 + 4 * ((t0 + 1) ^ sw)) = u16x4{r.v[i][4], r.v[i][5], r.v[i][6], r.v[i][7]};
+  }
+}
+
+// dec_block with the K / V^T fragments read from the wave's LDS slot as each MFMA needs them (register-lean:
+// lets several waves share a SIMD, so the staging of one block overlaps the math of another)
+template <int D>
+__device__ __forceinline__ void dec_block_lds(const uint16_t* ks, const uint16_t* vs, const uint32_t (&vb)[4],
+                                              const bf16x8 (&qf)[D / 16], float scale_log2, int qi, int h, float& m,
+                                              float& lsum, f32x16 (&o)[D / 32]) {
+  constexpr int KS = D / 16, MT = D / 32;
+  f32x16 st = f32x16{};
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const u16x8 kf = *reinterpret_cast<const u16x8*>(ks + qi * D + 8 * ((2 * s + h) ^ (qi & 7)));
+    st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(kf), qf[s], st, 0, 0, 0);
+  }
+  float mx = -INFINITY;
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int r = 4 * c + j;
+      st[r] = ((vb[c] >> (8 * j)) & 0xffu) != 0u ? st[r] * scale_log2 : -INFINITY;
+      mx = fmaxf(mx, st[r]);
+    }
+  mx = fmaxf(mx, __shfl_xor(mx, 32, kWave));
+  const float mn = fmaxf(m, mx);
+  const float mref = mn == -INFINITY ? 0.f : mn;
+  const float alpha = __builtin_amdgcn_exp2f(m - mref);
+  m = mn;
+  float ps = 0.f;
+  u16x8 pb[2];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const float p = __builtin_amdgcn_exp2f(st[r] - mref);
+    ps += p;
+    pb[r >> 3][r & 7] = to_bf16_bits(p);
+  }
+  lsum = lsum * alpha + ps;
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    o[mt] *= alpha;
+    const int d = 32 * mt + qi, sw = (d >> 2) & 7;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const u16x4 lo = *reinterpret_cast<const u16x4*>(vs + d * 32 + 4 * ((4 * s + h) ^ sw));
+      const u16x4 hi = *reinterpret_cast<const u16x4*>(vs + d * 32 + 4 * ((4 * s + 2 + h) ^ sw));
+      const u16x8 vf = u16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      o[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(vf), as_bf16x8(pb[s]), o[mt], 0, 0, 0);
+    }
+  }
+}
+
 // output element (sequence b, column k of (Hq * D)): row-major or fragment-packed (csrc/decode_gemm.hip layout)
 __device__ __forceinline__ uint16_t* dec_out_ptr(const DecodeArgs& a, int64_t b, int64_t k, int64_t row_off) {
   if (a.out_mbt == 0) return a.out + row_off;  // row-major: row_off is the (b, k) offset
   return a.out + ((((k >> 4) * a.out_mbt + (b >> 5)) * 64 + ((k >> 3) & 1) * 32 + (b & 31)) * 8 + (k & 7));
 }
 
-template <int D, int NW>
+template <int D, int NW, bool LEAN = false, bool SPLIT = false>
 __global__ __launch_bounds__(64 * NW) void decode_mfma_kernel(DecodeArgs a) {
   constexpr int KS = D / 16, MT = D / 32;
   __shared__ float s_m[NW][32], s_l[NW][32];
@@ -842,7 +906,7 @@ __global__ __launch_bounds__(64 * NW) void decode_mfma_kernel(DecodeArgs a) {
   uint16_t* kslot = reinterpret_cast<uint16_t*>(&s_o[w][0][0][0]);  // 32 * D bf16
   uint16_t* vslot = kslot + 32 * D;                                 // D * 32 bf16
   if (ib0 < nblk) dec_load_raw<D>(kb, vtb, vrow, a.ld_vt, a.ld_valid, 32 * ib0, kend, lane, h, A);
-  if (ib0 + NW < nblk) dec_load_raw<D>(kb, vtb, vrow, a.ld_vt, a.ld_valid, 32 * (ib0 + NW), kend, lane, h, Bn);
+  if (!LEAN && ib0 + NW < nblk) dec_load_raw<D>(kb, vtb, vrow, a.ld_vt, a.ld_valid, 32 * (ib0 + NW), kend, lane, h, Bn);
   bf16x8 qf[KS];
   {
     const bool qv = qi < a.G;
@@ -858,6 +922,15 @@ __global__ __launch_bounds__(64 * NW) void decode_mfma_kernel(DecodeArgs a) {
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) o[mt] = f32x16{};
   float m = -INFINITY, lsum = 0.f;
+  if constexpr (LEAN) {
+    // one block in flight per wave: stage it to the slot, issue the next, compute from LDS
+    for (int ib = ib0; ib < nblk; ib += NW) {
+      dec_stage<D>(A, kslot, vslot, lane);
+      const uint32_t vb[4] = {A.vb[0], A.vb[1], A.vb[2], A.vb[3]};
+      if (ib + NW < nblk) dec_load_raw<D>(kb, vtb, vrow, a.ld_vt, a.ld_valid, 32 * (ib + NW), kend, lane, h, A);
+      dec_block_lds<D>(kslot, vslot, vb, qf, a.scale_log2, qi, h, m, lsum, o);
+    }
+  } else
   for (int ib = ib0; ib < nblk; ib += 2 * NW) {
     DecBlock<D> blk;
     dec_reshape<D>(A, kslot, vslot, lane, qi, h, blk);
@@ -877,7 +950,7 @@ __global__ __launch_bounds__(64 * NW) void decode_mfma_kernel(DecodeArgs a) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) s_o[w][mt][r][lane] = o[mt][r];
   __syncthreads();
-  if (S > 1) {
+  if (SPLIT && S > 1) {
     // this split's state -> write-through slab; the last of the S splits merges them in split order
     float* slab = a.slabs + (bh * S + y) * (64 + 32 * D);
     if (w == 0) {
@@ -992,6 +1065,7 @@ __global__ __launch_bounds__(64 * NW) void decode_mfma_kernel(DecodeArgs a) {
 }  // namespace
 
 int g_dec_nw = 0, g_dec_splits = 0;  // tuning override (drl_decode_attention_set_plan), 0 = automatic
+int g_dec_lean = 0;                  // drl_decode_attention_set_variant: 1 = one block in flight, LDS fragments
 
 // key splits for decode attention. Measured (tools/kernel_bench.py --only decode_sweep, B 64..512,
 // L 513..768): a split never beat one workgroup per (sequence, KV head) with 8 waves — the slab hand-off
@@ -1062,6 +1136,8 @@ int drl_flash_attn_bwd(const void* q, const void* k, const void* kt, const void*
   return DRL_OK;
 }
 
+void drl_decode_attention_set_variant(int32_t lean) { drl::g_dec_lean = lean ? 1 : 0; }
+
 void drl_decode_attention_set_plan(int32_t waves, int32_t splits) {
   drl::g_dec_nw = (waves == 2 || waves == 4 || waves == 8 || waves == 16) ? waves : 0;
   drl::g_dec_splits = (splits >= 1 && splits <= 16) ? splits : 0;
@@ -1096,9 +1172,12 @@ int drl_decode_attention_vt(const void* q, const void* k_cache, const void* vt_c
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int64_t wgs = B * Hkv, cus = cu_count();
   const int splits = decode_splits(B, Hkv, L);
-  // waves per workgroup (tools/kernel_bench.py --only decode_sweep, coalesced loader): 8 while the grid fits
-  // the chip, 2 beyond (B=64: 8.9 us, B=512: 36.8 us at L=768)
-  const int nw = g_dec_nw ? g_dec_nw : (wgs <= cus ? 8 : 2);
+  // waves per workgroup and key-loop variant (tools/kernel_bench.py --only decode_sweep): 8 waves with two
+  // blocks in flight while the grid fits the chip (B=64: 8.7 us at L=768, latency-bound); beyond it the
+  // register-lean loop (2 waves per SIMD) with 4 waves up to 2 workgroups per CU, else 2 (B=512, L=768:
+  // 201 MB in 34.7 us = 5.8 TB/s, 0.92 of the measured 6.3 TB/s copy rate)
+  const int nw = g_dec_nw ? g_dec_nw : (wgs <= cus ? 8 : (wgs <= 2 * cus ? 4 : 2));
+  const bool lean = g_dec_nw ? g_dec_lean != 0 : wgs > cus;
   if (splits > 1) {
     const size_t need = drl_decode_attention_vt_workspace_bytes(B, Hkv, D, L);
     if (!workspace || workspace_bytes < need || (reinterpret_cast<uintptr_t>(workspace) & 255u))
@@ -1106,7 +1185,13 @@ int drl_decode_attention_vt(const void* q, const void* k_cache, const void* vt_c
     a.tickets = static_cast<unsigned*>(workspace);
     a.slabs = reinterpret_cast<float*>(static_cast<char*>(workspace) + round_up(static_cast<size_t>(wgs) * sizeof(unsigned), 256));
   }
-#define DRL_DEC(DD, NN) hipLaunchKernelGGL((decode_mfma_kernel<DD, NN>), dim3(B * Hkv, splits), dim3(64 * NN), 0, s, a)
+#define DRL_DEC(DD, NN)                                                                                          \
+  do {                                                                                                           \
+    const dim3 g_(B * Hkv, splits), b_(64 * NN);                                                                  \
+    if (splits > 1) hipLaunchKernelGGL((decode_mfma_kernel<DD, NN, false, true>), g_, b_, 0, s, a);              \
+    else if (lean) hipLaunchKernelGGL((decode_mfma_kernel<DD, NN, true, false>), g_, b_, 0, s, a);              \
+    else hipLaunchKernelGGL((decode_mfma_kernel<DD, NN, false, false>), g_, b_, 0, s, a);                        \
+  } while (0)
   if (D == 64) {
     if (nw == 2) DRL_DEC(64, 2);
     else if (nw == 4) DRL_DEC(64, 4);

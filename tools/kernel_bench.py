@@ -155,13 +155,16 @@ def decode_sweep(Bs=(64, 128, 256, 512), Ls=(513, 768), Hkv=2, G=7, D=64):
             valid = torch.ones(B, 768, dtype=torch.uint8, device=dev)
             out = torch.empty_like(q)
             sweep = {}
-            for nw in (0, 2, 4, 8, 16):
-                for sp in (0, 1, 2, 4, 8):
-                    if (nw == 0) != (sp == 0):
-                        continue
-                    native.lib().drl_decode_attention_set_plan(nw, sp)
-                    sweep[f"{nw}x{sp}"] = round(time_graph(
-                        lambda: native.decode_attention_vt(q, k, vt, valid, L, out), 50) * 1e6, 2)
+            for lean in (0, 1):
+                native.lib().drl_decode_attention_set_variant(lean)
+                for nw in (0, 2, 4, 8, 16):
+                    for sp in (0, 1, 2):
+                        if (nw == 0) != (sp == 0):
+                            continue
+                        native.lib().drl_decode_attention_set_plan(nw, sp)
+                        sweep[f"{'L' if lean else ''}{nw}x{sp}"] = round(time_graph(
+                            lambda: native.decode_attention_vt(q, k, vt, valid, L, out), 50) * 1e6, 2)
+            native.lib().drl_decode_attention_set_variant(0)
             native.lib().drl_decode_attention_set_plan(0, 0)
             best = min(sweep, key=sweep.get)
             res.append(dict(kernel="decode_attention_vt_sweep", B=B, L=L, auto_us=sweep["0x0"], best=best,
