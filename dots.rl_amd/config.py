@@ -65,6 +65,8 @@ DEFAULTS = dict(
             log_prob_micro_batch_size_per_gpu=16, log_prob_use_dynamic_bsz=False, micro_batch_size=None,
             seed=1234, val_kwargs=dict(top_k=-1, top_p=1.0, temperature=0, n=1, do_sample=False),
             use_hip_graph=True,  # decode steps replayed from one captured HIP graph (rollout.py)
+            packed_decode=True, packed_decode_max_rows=512,  # qwen2.PackedDecode (fragment-packed operands)
+            fused_select=False,  # lm_head fused with K4 (csrc/fused_linear.hip)
         ),
         ref=dict(log_prob_micro_batch_size=None, log_prob_micro_batch_size_per_gpu=16, log_prob_use_dynamic_bsz=False),
     ),

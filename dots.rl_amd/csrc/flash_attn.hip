@@ -82,6 +82,13 @@ __device__ __forceinline__ u16x8 lds_xt_operand(const uint16_t* x, int mt, int s
 
 // round-to-nearest-even f32 -> bf16 (one v_cvt_pk_bf16_f32; NaN stays NaN)
 __device__ __forceinline__ uint16_t to_bf16_bits(float f) { return __builtin_bit_cast(uint16_t, static_cast<__bf16>(f)); }
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+// two f32 -> packed bf16 pair (one v_cvt_pk_bf16_f32; the same rounding as to_bf16_bits)
+__device__ __forceinline__ uint32_t pk_bf16(float lo, float hi) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{lo, hi}, bf16x2));
+}
 
 // K / V tiles of one 32-key block staged in LDS and shared by the G waves of the workgroup.
 // K: [32 keys][D] rows of D*2 + 16 bytes (16-B aligned, conflict-free ds_read_b128 of a key row slice);
@@ -143,6 +150,19 @@ __device__ __forceinline__ void kv_store(uint16_t* kl, uint16_t* vl, int tid, co
   }
 }
 
+// key-valid bytes of the 32-key block at k0, staged with the block's K / V: thread tid < 8 holds the word of
+// keys k0 + 4 tid .. k0 + 4 tid + 3 (0 past T). Read from LDS by the compute, so the key loop never waits
+// on a global load of its own.
+__device__ __forceinline__ uint32_t valid_issue(const uint8_t* vrow, int64_t k0, int64_t T, int tid) {
+  if (tid >= 8) return 0u;
+  const int64_t kb = k0 + 4 * tid;
+  if (kb + 3 < T) return *reinterpret_cast<const uint32_t*>(vrow + kb);
+  uint32_t v = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) v |= (kb + j < T ? static_cast<uint32_t>(vrow[kb + j]) : 0u) << (8 * j);
+  return v;
+}
+
 template <int D>
 __global__ __launch_bounds__(512) void flash_fwd_kernel(FlashArgs a) {
   constexpr int KS = D / 16;  // k-steps of S^T = K Q^T over the head dim
@@ -150,6 +170,7 @@ __global__ __launch_bounds__(512) void flash_fwd_kernel(FlashArgs a) {
   using TL = KVTile<D>;
   __shared__ __attribute__((aligned(16))) uint16_t lds_k[2][TL::KSZ];
   __shared__ __attribute__((aligned(16))) uint16_t lds_v[2][TL::VSZ];
+  __shared__ uint32_t lds_vw[2][8];
   const int tid = threadIdx.x;
   const int lane = tid & 63, g = tid >> 6;
   const bool computes = g < a.G;  // waves >= G only help staging
@@ -185,96 +206,102 @@ __global__ __launch_bounds__(512) void flash_fwd_kernel(FlashArgs a) {
   const int64_t kmax = min(a.Tk, t0 + 31 + a.qoff + 1);  // causal limit of the tile's last query
   const int64_t nb = (kmax + 31) / 32;
   const int qpos = static_cast<int>(tq + a.qoff);  // positions fit in 32 bits (host check)
-  const int Tk = static_cast<int>(a.Tk);
   const int qlo = static_cast<int>(t0 + a.qoff);     // smallest query position of the tile
 
+  // one 32-key block: S^T, online softmax, O^T += V^T P^T (LDS buffer cur holds the block at k0)
+  auto block = [&](int cur, int64_t k0) {
+    // ---- S^T (32 keys x 32 queries): A = K rows from LDS (lane & 31 = key), B = Q fragments
+    f32x16 st = f32x16{};
+    const uint16_t* krow = lds_k[cur] + qi * TL::KROW + 8 * h;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const u16x8 kv = *reinterpret_cast<const u16x8*>(krow + 16 * s);
+      st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(kv), qf[s], st, 0, 0, 0);
+    }
+    // ---- mask + scale; register r holds key k0 + (r & 3) + 8 * (r >> 2) + 4h of query tq
+    const int kbase0 = static_cast<int>(k0) + 4 * h;
+    uint32_t vw[4];
+    bool allv = true;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      vw[c] = lds_vw[cur][h + 2 * c];  // keys kbase0 + 8c .. + 3
+      allv &= vw[c] == 0x01010101u;
+    }
+    // blocks strictly below the diagonal with every key valid need no mask (wave-uniform test)
+    const bool full = __all(allv) && static_cast<int>(k0) + 31 <= qlo;
+    // raw-score max (the scale is positive: max(s * scale) = scale * max(s)); masked scores -> -inf
+    float mxr = -INFINITY;
+    if (!full) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int r = 4 * c + j;
+          const bool ok = ((vw[c] >> (8 * j)) & 0xffu) != 0u && kbase0 + 8 * c + j <= qpos;
+          st[r] = ok ? st[r] : -INFINITY;
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) mxr = fmaxf(mxr, st[r]);
+    mxr = fmaxf(mxr, __shfl_xor(mxr, 32, kWave));
+    const float mx = mxr * a.scale_log2;
+    // deferred rescale: the reference max moves only when the block's max exceeds it by more than 8 (log2
+    // units), so p <= 2^8 and most blocks skip the O^T rescale; the final O / l and LSE are exact either way
+    const float mn = mx > m + 8.f ? mx : m;
+    const float mref = mn == -INFINITY ? 0.f : mn;  // keeps exp2(-inf - mref) = 0, never NaN
+    const float alpha = __builtin_amdgcn_exp2f(m - mref);
+    m = mn;
+    float ps0 = 0.f, ps1 = 0.f;
+    uint32_t pw[8];  // P in bf16, element pairs (2k, 2k + 1)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float p0 = __builtin_amdgcn_exp2f(fmaf(st[2 * k], a.scale_log2, -mref));
+      const float p1 = __builtin_amdgcn_exp2f(fmaf(st[2 * k + 1], a.scale_log2, -mref));
+      ps0 += p0;
+      ps1 += p1;
+      pw[k] = pk_bf16(p0, p1);
+    }
+    lsum = lsum * alpha + (ps0 + ps1);
+    if (!__all(alpha == 1.f)) {
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) o[mt] *= alpha;
+    }
+    u16x8 pb[2];
+    pb[0] = __builtin_bit_cast(u16x8, u32x4{pw[0], pw[1], pw[2], pw[3]});
+    pb[1] = __builtin_bit_cast(u16x8, u32x4{pw[4], pw[5], pw[6], pw[7]});
+    // ---- O^T += V^T P^T; k-step s: element j of lane half h is key k0 + 16s + 8(j>>2) + 4h + (j&3)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const uint16_t* vtl = lds_v[cur] + (32 * mt + qi) * TL::VROW + 4 * h;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const u16x4 lo = *reinterpret_cast<const u16x4*>(vtl + 16 * s);
+        const u16x4 hi = *reinterpret_cast<const u16x4*>(vtl + 16 * s + 8);
+        const u16x8 vv = u16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        o[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(vv), as_bf16x8(pb[s]), o[mt], 0, 0, 0);
+      }
+    }
+  };
+  // K/V staging: block ib + 1 is issued into registers at the start of iteration ib (in flight under the
+  // compute) and written to the other LDS buffer at its end; the key-valid words travel with it
   u16x8 stage[TL::CPT];
+  uint32_t vst;
   kv_issue<D>(kbase, vtbase, a.ld_vt, 0, a.Tk, tid, stage);
+  vst = valid_issue(vrow, 0, a.Tk, tid);
   kv_store<D>(lds_k[0], lds_v[0], tid, stage);
+  if (tid < 8) lds_vw[0][tid] = vst;
   __syncthreads();
   for (int64_t ib = 0; ib < nb; ++ib) {
     const int cur = static_cast<int>(ib & 1);
-    const int64_t k0 = ib * 32;
-    if (ib + 1 < nb) kv_issue<D>(kbase, vtbase, a.ld_vt, k0 + 32, a.Tk, tid, stage);  // in flight under compute
-    if (computes) {
-      // ---- S^T (32 keys x 32 queries): A = K rows from LDS (lane & 31 = key), B = Q fragments
-      f32x16 st = f32x16{};
-      const uint16_t* krow = lds_k[cur] + qi * TL::KROW + 8 * h;
-#pragma unroll
-      for (int s = 0; s < KS; ++s) {
-        const u16x8 kv = *reinterpret_cast<const u16x8*>(krow + 16 * s);
-        st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(kv), qf[s], st, 0, 0, 0);
-      }
-      // ---- mask + scale; register r holds key k0 + (r & 3) + 8 * (r >> 2) + 4h of query tq
-      const int kbase0 = static_cast<int>(k0) + 4 * h;
-      uint32_t vw[4];
-      bool allv = true;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const int kb = kbase0 + 8 * c;
-        if (kb + 3 < Tk) {
-          vw[c] = *reinterpret_cast<const uint32_t*>(vrow + kb);
-        } else {
-          vw[c] = 0;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) vw[c] |= (kb + j < Tk ? static_cast<uint32_t>(vrow[kb + j]) : 0u) << (8 * j);
-        }
-        allv &= vw[c] == 0x01010101u;
-      }
-      // blocks strictly below the diagonal with every key valid need no mask (wave-uniform test)
-      const bool full = __all(allv) && static_cast<int>(k0) + 31 <= qlo;
-      float x[16];
-      float mx = -INFINITY;
-      if (full) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          x[r] = st[r] * a.scale_log2;
-          mx = fmaxf(mx, x[r]);
-        }
-      } else {
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int r = 4 * c + j;
-            const bool ok = ((vw[c] >> (8 * j)) & 0xffu) != 0u && kbase0 + 8 * c + j <= qpos;
-            x[r] = ok ? st[r] * a.scale_log2 : -INFINITY;
-            mx = fmaxf(mx, x[r]);
-          }
-        }
-      }
-      mx = fmaxf(mx, __shfl_xor(mx, 32, kWave));
-      const float mn = fmaxf(m, mx);
-      const float mref = mn == -INFINITY ? 0.f : mn;  // keeps exp2(-inf - mref) = 0, never NaN
-      const float alpha = __builtin_amdgcn_exp2f(m - mref);
-      m = mn;
-      float ps = 0.f;
-      u16x8 pb[2];
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float p = __builtin_amdgcn_exp2f(x[r] - mref);
-        ps += p;
-        pb[r >> 3][r & 7] = to_bf16_bits(p);
-      }
-      lsum = lsum * alpha + ps;
-      if (!__all(alpha == 1.f)) {
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) o[mt] *= alpha;
-      }
-      // ---- O^T += V^T P^T; k-step s: element j of lane half h is key k0 + 16s + 8(j>>2) + 4h + (j&3)
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        const uint16_t* vtl = lds_v[cur] + (32 * mt + qi) * TL::VROW + 4 * h;
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          const u16x4 lo = *reinterpret_cast<const u16x4*>(vtl + 16 * s);
-          const u16x4 hi = *reinterpret_cast<const u16x4*>(vtl + 16 * s + 8);
-          const u16x8 vv = u16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-          o[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(vv), as_bf16x8(pb[s]), o[mt], 0, 0, 0);
-        }
-      }
+    if (ib + 1 < nb) {
+      kv_issue<D>(kbase, vtbase, a.ld_vt, (ib + 1) * 32, a.Tk, tid, stage);
+      vst = valid_issue(vrow, (ib + 1) * 32, a.Tk, tid);
     }
-    if (ib + 1 < nb) kv_store<D>(lds_k[cur ^ 1], lds_v[cur ^ 1], tid, stage);  // buffer last read at ib - 1
+    if (computes) block(cur, ib * 32);
+    if (ib + 1 < nb) {
+      kv_store<D>(lds_k[cur ^ 1], lds_v[cur ^ 1], tid, stage);
+      if (tid < 8) lds_vw[cur ^ 1][tid] = vst;
+    }
     __syncthreads();
   }
   // ---- finalize: O^T register r of tile mt = head-dim row 32mt + (r & 3) + 8(r >> 2) + 4h of query tq
@@ -392,6 +419,7 @@ __global__ __launch_bounds__(512) void flash_dq_kernel(FlashBwdArgs a) {
   __shared__ __attribute__((aligned(16))) uint16_t lds_k[2][TL::RSZ];
   __shared__ __attribute__((aligned(16))) uint16_t lds_v[2][TL::RSZ];
   __shared__ __attribute__((aligned(16))) uint16_t lds_kt[2][TL::TSZ];
+  __shared__ uint32_t lds_vw[2][8];
   const int tid = threadIdx.x;
   const int lane = tid & 63, g = tid >> 6;
   const bool computes = g < a.G;
@@ -437,11 +465,16 @@ __global__ __launch_bounds__(512) void flash_dq_kernel(FlashBwdArgs a) {
   const int nb = (min(T, t0 + 32) + 31) / 32;
   u16x8 stage[TL::CPT];
   dq_issue<D>(kbase, vbase, ktbase, a.ld_t, 0, T, tid, stage);
+  uint32_t vst = valid_issue(vrow, 0, T, tid);
   dq_store<D>(lds_k[0], lds_v[0], lds_kt[0], tid, stage);
+  if (tid < 8) lds_vw[0][tid] = vst;
   __syncthreads();
   for (int ib = 0; ib < nb; ++ib) {
     const int cur = ib & 1, k0 = ib * 32;
-    if (ib + 1 < nb) dq_issue<D>(kbase, vbase, ktbase, a.ld_t, k0 + 32, T, tid, stage);
+    if (ib + 1 < nb) {
+      dq_issue<D>(kbase, vbase, ktbase, a.ld_t, k0 + 32, T, tid, stage);
+      vst = valid_issue(vrow, k0 + 32, T, tid);
+    }
     if (computes) {
       f32x16 st = f32x16{}, dpt = f32x16{};
       const uint16_t* kr = lds_k[cur] + qi * TL::ROW + 8 * h;
@@ -458,14 +491,7 @@ __global__ __launch_bounds__(512) void flash_dq_kernel(FlashBwdArgs a) {
       bool allv = true;
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        const int kb = kbase0 + 8 * c;
-        if (kb + 3 < T) {
-          vw[c] = *reinterpret_cast<const uint32_t*>(vrow + kb);
-        } else {
-          vw[c] = 0;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) vw[c] |= (kb + j < T ? static_cast<uint32_t>(vrow[kb + j]) : 0u) << (8 * j);
-        }
+        vw[c] = lds_vw[cur][h + 2 * c];  // keys kbase0 + 8c .. + 3
         allv &= vw[c] == 0x01010101u;
       }
       const bool full = __all(allv) && k0 + 31 <= t0;
@@ -492,7 +518,10 @@ __global__ __launch_bounds__(512) void flash_dq_kernel(FlashBwdArgs a) {
         }
       }
     }
-    if (ib + 1 < nb) dq_store<D>(lds_k[cur ^ 1], lds_v[cur ^ 1], lds_kt[cur ^ 1], tid, stage);
+    if (ib + 1 < nb) {
+      dq_store<D>(lds_k[cur ^ 1], lds_v[cur ^ 1], lds_kt[cur ^ 1], tid, stage);
+      if (tid < 8) lds_vw[cur ^ 1][tid] = vst;
+    }
     __syncthreads();
   }
   if (!qvalid) return;
@@ -883,7 +912,7 @@ __device__ __forceinline__ uint16_t* dec_out_ptr(const DecodeArgs& a, int64_t b,
   return a.out + ((((k >> 4) * a.out_mbt + (b >> 5)) * 64 + ((k >> 3) & 1) * 32 + (b & 31)) * 8 + (k & 7));
 }
 
-template <int D, int NW, bool LEAN = false, bool SPLIT = false>
+template <int D, int NW, bool LEAN = false, bool SPLIT = false, int NB = 2>
 __global__ __launch_bounds__(64 * NW) void decode_mfma_kernel(DecodeArgs a) {
   constexpr int KS = D / 16, MT = D / 32;
   __shared__ float s_m[NW][32], s_l[NW][32];
@@ -898,15 +927,17 @@ __global__ __launch_bounds__(64 * NW) void decode_mfma_kernel(DecodeArgs a) {
   const uint16_t* vtb = a.vt + bh * D * a.ld_vt;
   const uint8_t* vrow = a.valid + b * a.ld_valid;
   // split-K over gridDim.y workgroups: split y takes 32-key blocks [y*n/S, (y+1)*n/S) of the n live blocks;
-  // each wave takes blocks ib0, ib0 + NW, ... and has its first two in flight together with q
+  // each wave takes blocks ib0, ib0 + NW, ... and has its first NB (LEAN: 1) in flight together with q
   const int nall = (kend + 31) / 32, S = gridDim.y, y = blockIdx.y;
   const int bbeg = y * nall / S, nblk = (y + 1) * nall / S;
   const int ib0 = bbeg + w;
-  DecRaw<D> A, Bn;
+  constexpr int NR = LEAN ? 1 : NB;
+  DecRaw<D> R[NR];
   uint16_t* kslot = reinterpret_cast<uint16_t*>(&s_o[w][0][0][0]);  // 32 * D bf16
   uint16_t* vslot = kslot + 32 * D;                                 // D * 32 bf16
-  if (ib0 < nblk) dec_load_raw<D>(kb, vtb, vrow, a.ld_vt, a.ld_valid, 32 * ib0, kend, lane, h, A);
-  if (!LEAN && ib0 + NW < nblk) dec_load_raw<D>(kb, vtb, vrow, a.ld_vt, a.ld_valid, 32 * (ib0 + NW), kend, lane, h, Bn);
+#pragma unroll
+  for (int j = 0; j < NR; ++j)
+    if (ib0 + j * NW < nblk) dec_load_raw<D>(kb, vtb, vrow, a.ld_vt, a.ld_valid, 32 * (ib0 + j * NW), kend, lane, h, R[j]);
   bf16x8 qf[KS];
   {
     const bool qv = qi < a.G;
@@ -925,21 +956,24 @@ __global__ __launch_bounds__(64 * NW) void decode_mfma_kernel(DecodeArgs a) {
   if constexpr (LEAN) {
     // one block in flight per wave: stage it to the slot, issue the next, compute from LDS
     for (int ib = ib0; ib < nblk; ib += NW) {
-      dec_stage<D>(A, kslot, vslot, lane);
-      const uint32_t vb[4] = {A.vb[0], A.vb[1], A.vb[2], A.vb[3]};
-      if (ib + NW < nblk) dec_load_raw<D>(kb, vtb, vrow, a.ld_vt, a.ld_valid, 32 * (ib + NW), kend, lane, h, A);
+      dec_stage<D>(R[0], kslot, vslot, lane);
+      const uint32_t vb[4] = {R[0].vb[0], R[0].vb[1], R[0].vb[2], R[0].vb[3]};
+      if (ib + NW < nblk) dec_load_raw<D>(kb, vtb, vrow, a.ld_vt, a.ld_valid, 32 * (ib + NW), kend, lane, h, R[0]);
       dec_block_lds<D>(kslot, vslot, vb, qf, a.scale_log2, qi, h, m, lsum, o);
     }
   } else
-  for (int ib = ib0; ib < nblk; ib += 2 * NW) {
-    DecBlock<D> blk;
-    dec_reshape<D>(A, kslot, vslot, lane, qi, h, blk);
-    if (ib + 2 * NW < nblk) dec_load_raw<D>(kb, vtb, vrow, a.ld_vt, a.ld_valid, 32 * (ib + 2 * NW), kend, lane, h, A);
-    dec_block<D>(blk, qf, a.scale_log2, m, lsum, o);
-    if (ib + NW < nblk) {
-      dec_reshape<D>(Bn, kslot, vslot, lane, qi, h, blk);
-      if (ib + 3 * NW < nblk) dec_load_raw<D>(kb, vtb, vrow, a.ld_vt, a.ld_valid, 32 * (ib + 3 * NW), kend, lane, h, Bn);
-      dec_block<D>(blk, qf, a.scale_log2, m, lsum, o);
+  // ring of NB raw blocks: block ib + j * NW is reshaped out of R[j], whose next load is issued right after
+  for (int ib = ib0; ib < nblk; ib += NB * NW) {
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int ibj = ib + j * NW;
+      if (ibj < nblk) {
+        DecBlock<D> blk;
+        dec_reshape<D>(R[j], kslot, vslot, lane, qi, h, blk);
+        if (ibj + NB * NW < nblk)
+          dec_load_raw<D>(kb, vtb, vrow, a.ld_vt, a.ld_valid, 32 * (ibj + NB * NW), kend, lane, h, R[j]);
+        dec_block<D>(blk, qf, a.scale_log2, m, lsum, o);
+      }
     }
   }
   // merge the 4 waves' states per query column (head) in a fixed order
@@ -1031,7 +1065,9 @@ __global__ __launch_bounds__(64 * NW) void decode_mfma_kernel(DecodeArgs a) {
       }
     return;
   }
-  if (w != 0 || qi >= a.G) return;
+  // every wave merges its share of the (tile, 4-row group) outputs: NW partial states per element, summed in
+  // wave order (the same fixed order whichever wave does it)
+  if (qi >= a.G) return;
   float mm = -INFINITY;
 #pragma unroll
   for (int v = 0; v < NW; ++v) mm = fmaxf(mm, s_m[v][qi]);
@@ -1044,28 +1080,25 @@ __global__ __launch_bounds__(64 * NW) void decode_mfma_kernel(DecodeArgs a) {
   }
   const float inv = ll > 0.f ? 1.f / ll : 0.f;
   const int64_t kq = ((bh % a.Hkv) * a.G + qi) * D;  // column of (b, query head) in (Hq * D)
+  for (int g = w; g < 4 * MT; g += NW) {
+    const int mt = g >> 2, c = g & 3;
+    u16x4 wv;
 #pragma unroll
-  for (int mt = 0; mt < MT; ++mt) {
+    for (int j = 0; j < 4; ++j) {
+      float acc = 0.f;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      u16x4 wv;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float acc = 0.f;
-#pragma unroll
-        for (int v = 0; v < NW; ++v) acc = fmaf(s_o[v][mt][4 * c + j][lane], sc[v], acc);
-        wv[j] = to_bf16_bits(acc * inv);
-      }
-      const int64_t k = kq + 32 * mt + 8 * c + 4 * h;
-      *reinterpret_cast<u16x4*>(dec_out_ptr(a, b, k, (bh * a.G + qi) * D + 32 * mt + 8 * c + 4 * h)) = wv;
+      for (int v = 0; v < NW; ++v) acc = fmaf(s_o[v][mt][4 * c + j][lane], sc[v], acc);
+      wv[j] = to_bf16_bits(acc * inv);
     }
+    const int64_t k = kq + 32 * mt + 8 * c + 4 * h;
+    *reinterpret_cast<u16x4*>(dec_out_ptr(a, b, k, (bh * a.G + qi) * D + 32 * mt + 8 * c + 4 * h)) = wv;
   }
 }
 
 }  // namespace
 
 int g_dec_nw = 0, g_dec_splits = 0;  // tuning override (drl_decode_attention_set_plan), 0 = automatic
-int g_dec_lean = 0;                  // drl_decode_attention_set_variant: 1 = one block in flight, LDS fragments
+int g_dec_variant = 0;  // drl_decode_attention_set_variant: 1 = one block in flight (LDS fragments), 2..4 = ring depth
 
 // key splits for decode attention. Measured (tools/kernel_bench.py --only decode_sweep, B 64..512,
 // L 513..768): a split never beat one workgroup per (sequence, KV head) with 8 waves — the slab hand-off
@@ -1136,7 +1169,9 @@ int drl_flash_attn_bwd(const void* q, const void* k, const void* kt, const void*
   return DRL_OK;
 }
 
-void drl_decode_attention_set_variant(int32_t lean) { drl::g_dec_lean = lean ? 1 : 0; }
+void drl_decode_attention_set_variant(int32_t variant) {
+  drl::g_dec_variant = (variant >= 1 && variant <= 4) ? variant : 0;
+}
 
 void drl_decode_attention_set_plan(int32_t waves, int32_t splits) {
   drl::g_dec_nw = (waves == 2 || waves == 4 || waves == 8 || waves == 16) ? waves : 0;
@@ -1177,7 +1212,10 @@ int drl_decode_attention_vt(const void* q, const void* k_cache, const void* vt_c
   // register-lean loop (2 waves per SIMD) with 4 waves up to 2 workgroups per CU, else 2 (B=512, L=768:
   // 201 MB in 34.7 us = 5.8 TB/s, 0.92 of the measured 6.3 TB/s copy rate)
   const int nw = g_dec_nw ? g_dec_nw : (wgs <= cus ? 8 : (wgs <= 2 * cus ? 4 : 2));
-  const bool lean = g_dec_nw ? g_dec_lean != 0 : wgs > cus;
+  const bool lean = g_dec_nw ? g_dec_variant == 1 : wgs > cus;
+  // blocks in flight per wave (small grids): all of a wave's blocks at the cache capacity, up to 4
+  const int64_t per_wave = ((L + 31) / 32 + nw - 1) / nw;
+  const int nb = g_dec_nw ? (g_dec_variant > 2 ? g_dec_variant : 2) : (per_wave >= 4 ? 4 : per_wave >= 3 ? 3 : 2);
   if (splits > 1) {
     const size_t need = drl_decode_attention_vt_workspace_bytes(B, Hkv, D, L);
     if (!workspace || workspace_bytes < need || (reinterpret_cast<uintptr_t>(workspace) & 255u))
@@ -1190,7 +1228,15 @@ int drl_decode_attention_vt(const void* q, const void* k_cache, const void* vt_c
     const dim3 g_(B * Hkv, splits), b_(64 * NN);                                                                  \
     if (splits > 1) hipLaunchKernelGGL((decode_mfma_kernel<DD, NN, false, true>), g_, b_, 0, s, a);              \
     else if (lean) hipLaunchKernelGGL((decode_mfma_kernel<DD, NN, true, false>), g_, b_, 0, s, a);              \
-    else hipLaunchKernelGGL((decode_mfma_kernel<DD, NN, false, false>), g_, b_, 0, s, a);                        \
+    else {                                                                                                       \
+      bool done_ = false;                                                                                        \
+      if constexpr (DD == 64 && (NN == 4 || NN == 8)) {                                                          \
+        done_ = nb >= 3;                                                                                         \
+        if (nb == 3) hipLaunchKernelGGL((decode_mfma_kernel<DD, NN, false, false, 3>), g_, b_, 0, s, a);         \
+        else if (nb >= 4) hipLaunchKernelGGL((decode_mfma_kernel<DD, NN, false, false, 4>), g_, b_, 0, s, a);    \
+      }                                                                                                          \
+      if (!done_) hipLaunchKernelGGL((decode_mfma_kernel<DD, NN, false, false>), g_, b_, 0, s, a);               \
+    }                                                                                                            \
   } while (0)
   if (D == 64) {
     if (nw == 2) DRL_DEC(64, 2);

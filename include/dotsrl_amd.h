@@ -305,9 +305,10 @@ int drl_flash_attn_fwd(const void* q, const void* k, const void* vt, int32_t dt,
 size_t drl_decode_attention_vt_workspace_bytes(int64_t B, int64_t Hkv, int64_t D, int64_t L);
 /* Tuning hook (tools/kernel_bench.py): force waves per workgroup (2/4/8/16) and key splits; 0 = automatic. */
 void drl_decode_attention_set_plan(int32_t waves, int32_t splits);
-/* Tuning hook: 1 = register-lean key loop (one block in flight per wave, fragments read from LDS), 0 = two
- * blocks in flight per wave (default). Results are identical. */
-void drl_decode_attention_set_variant(int32_t lean);
+/* Tuning hook for forced plans (set_plan waves != 0): 1 = register-lean key loop (one block in flight per
+ * wave, fragments read from LDS); 2..4 = that many blocks in flight per wave (4 and 8 waves, D = 64; else 2).
+ * Results are identical. */
+void drl_decode_attention_set_variant(int32_t variant);
 int drl_decode_attention_vt(const void* q, const void* k_cache, const void* vt_cache, int32_t dt,
                             const uint8_t* key_valid, int64_t ld_valid, const int64_t* qpos_ptr, int64_t qpos,
                             int64_t B, int64_t Hkv, int64_t G, int64_t D, int64_t ld_k, int64_t ld_vt, int64_t L,

@@ -1,0 +1,12 @@
+# SQ counter passes over tools/flash_probe.py (one rocprofv3 --pmc run per pass; run through gpurun).
+set -o pipefail
+ROOT=$(pwd)
+OUT=$ROOT/gpurun_out/fpmc
+mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp
+i=0
+for pass in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_MFMA" \
+            "SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_SALU"; do
+  i=$((i+1))
+  timeout -s KILL 90 rocprofv3 --pmc $pass -d "$OUT/p$i" -o run -- python3 "$ROOT/tools/flash_probe.py" 5 > "$OUT/p$i.log" 2>&1 || exit 1
+done

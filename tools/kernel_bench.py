@@ -172,6 +172,44 @@ def decode_sweep(Bs=(64, 128, 256, 512), Ls=(513, 768), Hkv=2, G=7, D=64):
     return res
 
 
+def decode_sweep_cold(Bs=(64, 128, 256, 512), L=640, Hkv=2, G=7, D=64, footprint=768 << 20):
+    """As decode_sweep, but each call reads a different cache copy (footprint > the 256 MB MALL), the in-situ
+    pattern of 24 layers' caches per decode step: HBM-cold numbers."""
+    dev = "cuda"
+    res = []
+    for B in Bs:
+        per = B * Hkv * 768 * D * 2 * 2
+        n = max(2, -(-footprint // per))
+        qs = [torch.randn(B, Hkv, G, D, device=dev, dtype=torch.bfloat16) for _ in range(n)]
+        ks = [torch.randn(B, Hkv, 768, D, device=dev, dtype=torch.bfloat16) for _ in range(n)]
+        vts = [torch.randn(B, Hkv, D, 768, device=dev, dtype=torch.bfloat16) for _ in range(n)]
+        valid = torch.ones(B, 768, dtype=torch.uint8, device=dev)
+        out = torch.empty_like(qs[0])
+
+        def run():
+            for i in range(n):
+                native.decode_attention_vt(qs[i], ks[i], vts[i], valid, L, out)
+
+        sweep = {}
+        for var in (0, 1, 3, 4):  # 0: two blocks in flight, 1: lean, 3/4: ring depth
+            native.lib().drl_decode_attention_set_variant(var)
+            for nw in (0, 2, 4, 8):
+                for sp in (0, 1, 2):
+                    if (nw == 0) != (sp == 0) or (var and nw == 0) or (var > 1 and (sp > 1 or nw < 4)):
+                        continue
+                    native.lib().drl_decode_attention_set_plan(nw, sp)
+                    tag = {0: "", 1: "L", 3: "R3_", 4: "R4_"}[var]
+                    sweep[f"{tag}{nw}x{sp}"] = round(time_graph(run, 4) / n * 1e6, 2)
+        native.lib().drl_decode_attention_set_variant(0)
+        native.lib().drl_decode_attention_set_plan(0, 0)
+        best = min(sweep, key=sweep.get)
+        nbytes = B * Hkv * L * D * 4
+        res.append(dict(kernel="decode_attention_vt_cold", B=B, L=L, copies=n, auto_us=sweep["0x0"], best=best,
+                        best_us=sweep[best], best_GBps=round(nbytes / sweep[best] / 1e3, 1), sweep_us=sweep))
+        del qs, ks, vts
+    return res
+
+
 def flash(B=16, Hkv=2, G=7, D=64, T=768):
     """Fused attention forward vs the unfused path (fp32-score GEMM + masked softmax + PV GEMM)."""
     import math
@@ -389,7 +427,10 @@ def launch_floor(B=64, H=896, I=4864):
     gu = torch.randn(B, 2 * I, device=dev, dtype=bf)
     a = torch.empty(B, I, device=dev, dtype=bf)
     res = []
+    xs = torch.randn(B, H, device=dev)
+    hp = torch.zeros(64 * H, device=dev, dtype=bf)
     for name, fn in [("torch_zero_1elem", lambda: z.zero_()),
+                     ("decode_rmsnorm", lambda: native.decode_rmsnorm(xs, None, xs, w, hp, 1e-6, mbt=2)),
                      ("add_rmsnorm_fwd", lambda: native.add_rmsnorm_fwd(x, d, x2, w, y, None, 1e-6)),
                      ("swiglu_fwd", lambda: native.swiglu_fwd(gu, a))]:
         res.append(dict(kernel="graph_floor", op=name, B=B, seconds=time_graph(fn, 200)))
@@ -406,6 +447,19 @@ if __name__ == "__main__":
             for L in (513, 640, 768):
                 for r in decode_attn(B=B, L=L):
                     print(json.dumps(r), flush=True)
+        sys.exit(0)
+    if args.only == "flash":
+        for B in (8, 16):
+            for r in flash(B=B):
+                print(json.dumps(r), flush=True)
+        sys.exit(0)
+    if args.only == "floor":
+        for r in launch_floor():
+            print(json.dumps(r), flush=True)
+        sys.exit(0)
+    if args.only == "decode_cold":
+        for r in decode_sweep_cold():
+            print(json.dumps(r), flush=True)
         sys.exit(0)
     if args.only == "decode_sweep":
         for r in decode_sweep():
