@@ -21,6 +21,7 @@ LIB_PATH = os.environ.get("DOTSRL_AMD_LIB", os.path.join(_HERE, "libdotsrl_amd.s
 DRL_I64, DRL_I32, DRL_U8, DRL_F32, DRL_BF16 = 0, 1, 2, 3, 4
 DRL_OK = 0
 PPO_OUT_N = 8
+VALUE_OUT_N = 8
 
 AGG_MODES = {"token-mean": 0, "seq-mean-token-sum": 1, "seq-mean-token-mean": 2, "seq-mean-token-sum-norm": 3}
 KL_TYPES = {"kl": 0, "k1": 0, "abs": 1, "mse": 2, "k2": 2, "low_var_kl": 3, "k3": 3}
@@ -38,6 +39,15 @@ class PPOLossParams(ctypes.Structure):
         ("loss_agg_mode", ctypes.c_int32),
         ("kl_type", ctypes.c_int32),
         ("token_count", ctypes.c_void_p),
+    ]
+
+
+class ValueLossParams(ctypes.Structure):
+    _fields_ = [
+        ("cliprange_value", ctypes.c_float),
+        ("loss_scale_factor", ctypes.c_float),
+        ("loss_agg_mode", ctypes.c_int32),
+        ("pad", ctypes.c_int32),
     ]
 
 
@@ -91,7 +101,13 @@ SIGNATURES = {
     "drl_grpo_workspace_bytes": (SZ, [I64]),
     "drl_grpo_outcome_advantage": (ctypes.c_int, [P, P, I32, P, P, P, I64, I64, I64, F32, I32, P, P, P, SZ, P]),
     "drl_gae_workspace_bytes": (SZ, [I64, I64]),
-    "drl_gae_advantage_return": (ctypes.c_int, [P, P, P, I32, I64, I64, F32, F32, P, P, P, SZ, P]),
+    "drl_gae_advantage_return": (ctypes.c_int, [P, P, I32, P, I32, I64, I64, F32, F32, P, P, P, SZ, P]),
+    "drl_value_loss_workspace_bytes": (SZ, [I64, I64]),
+    "drl_value_loss_fwd_bwd": (ctypes.c_int, [P, P, I32, P, P, I32, I64, I64, ctypes.POINTER(ValueLossParams), P, P, P,
+                                              SZ, P]),
+    "drl_value_head_fwd": (ctypes.c_int, [P, I64, P, P, I32, I64, I64, P, I32, P]),
+    "drl_value_head_bwd_workspace_bytes": (SZ, [I64, I64]),
+    "drl_value_head_bwd": (ctypes.c_int, [P, I64, P, I32, P, I64, I64, P, I64, P, P, P, SZ, P]),
     "drl_select_tokens_workspace_bytes": (SZ, [I64]),
     "drl_select_tokens": (ctypes.c_int, [P, I32, I64, I64, I64, ctypes.POINTER(SamplingParams), P, P, I64, P, SZ, P]),
     "drl_response_mask": (ctypes.c_int, [P, I64, I64, I64, P, I32, P, I32, I64, P]),

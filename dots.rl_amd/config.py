@@ -70,6 +70,19 @@ DEFAULTS = dict(
         ),
         ref=dict(log_prob_micro_batch_size=None, log_prob_micro_batch_size_per_gpu=16, log_prob_use_dynamic_bsz=False),
     ),
+    # critic.yaml + dp_critic.yaml (used when algorithm.adv_estimator == "gae" or critic.enable)
+    critic=dict(
+        # None = the reference's ${oc.select:actor_rollout_ref...} interpolation (resolve_critic_config)
+        strategy="mi355x", enable=None, rollout_n=None,
+        optim=dict(lr=1e-5, lr_warmup_steps_ratio=0.0, total_training_steps=-1, weight_decay=0.01, lr_warmup_steps=-1,
+                   betas=[0.9, 0.999], eps=1e-8, warmup_style="constant"),
+        model=dict(path="random:qwen2.5-0.5b", override_config={}, use_remove_padding=False, dtype="bfloat16",
+                   gemm_tuning="auto", seed=4321),
+        ppo_mini_batch_size=None, ppo_micro_batch_size=None, ppo_micro_batch_size_per_gpu=8,
+        forward_micro_batch_size=None, forward_micro_batch_size_per_gpu=16, use_dynamic_bsz=None,
+        ppo_max_token_len_per_gpu=32768, forward_max_token_len_per_gpu=32768, ppo_epochs=None, shuffle=None,
+        grad_clip=1.0, cliprange_value=0.5, loss_agg_mode=None, ulysses_sequence_parallel_size=1,
+    ),
     algorithm=dict(gamma=1.0, lam=1.0, adv_estimator="grpo", norm_adv_by_std_in_grpo=True, use_kl_in_reward=False,
                    kl_penalty="kl", kl_ctrl=dict(type="fixed", kl_coef=0.001, horizon=10000, target_kl=0.1)),
     reward_model=dict(enable=False, reward_manager="synthetic_bernoulli", launch_reward_fn_async=False),
@@ -77,6 +90,19 @@ DEFAULTS = dict(
                  nnodes=1, save_freq=-1, test_freq=-1, logger=["console"], project_name="dots_rl_amd",
                  experiment_name="grpo"),
 )
+
+
+def resolve_critic_config(cfg: AttrDict) -> AttrDict:
+    """critic.yaml's interpolations from the actor (rollout_n, ppo_mini_batch_size, use_dynamic_bsz, ppo_epochs,
+    shuffle, loss_agg_mode) for entries left None; returns cfg.critic."""
+    c, a = cfg.critic, cfg.actor_rollout_ref.actor
+    src = {"rollout_n": cfg.actor_rollout_ref.rollout.n, "ppo_mini_batch_size": a.ppo_mini_batch_size,
+           "use_dynamic_bsz": a.use_dynamic_bsz, "ppo_epochs": a.ppo_epochs, "shuffle": a.shuffle,
+           "loss_agg_mode": a.loss_agg_mode}
+    for k, v in src.items():
+        if c.get(k) is None:
+            c[k] = v
+    return c
 
 
 def default_config():

@@ -214,5 +214,12 @@ def compute_policy_loss_vanilla(old_log_prob, log_prob, advantages, response_mas
 
 
 def compute_value_loss(vpreds, returns, values, response_mask, cliprange_value, loss_agg_mode="token-mean"):
-    """core_algos.py:1230-1269 (critic, config #4) — not on the GRPO path yet."""
-    raise NotImplementedError("critic value loss lands with the GAE/critic row (SURVEY §8(f) rank 4)")
+    """core_algos.py:1230-1269 — (vf_loss, vf_clipfrac); vf_loss is differentiable wrt vpreds (K6, one launch
+    for forward and backward, csrc/value_loss.hip)."""
+    from .dp_critic import fused_value_loss
+
+    if loss_agg_mode not in ("token-mean", "seq-mean-token-sum", "seq-mean-token-mean", "seq-mean-token-sum-norm"):
+        raise ValueError(f"Invalid loss_agg_mode: {loss_agg_mode}")
+    out = fused_value_loss(vpreds, values, returns, response_mask, cliprange_value=cliprange_value,
+                           loss_agg_mode=loss_agg_mode, loss_scale_factor=1.0)
+    return out[3], out[1].detach()

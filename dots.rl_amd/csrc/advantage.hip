@@ -57,8 +57,10 @@ __global__ __launch_bounds__(256) void grpo_write_kernel(const float* scores, co
 }
 
 // GAE reverse scan, one thread per row (core_algos.py:237-256); also emits returns = adv + values.
-template <int MDT>
-__global__ __launch_bounds__(256) void gae_scan_kernel(const float* r, const float* v, const void* mask, int64_t B,
+// VDT = DRL_BF16: values are the critic's bf16 output (dp_critic.py:192): the reference's `gamma * nextvalues`
+// is then bf16 tensor arithmetic (rounded to bf16); everything else promotes to fp32 against the fp32 rewards.
+template <int MDT, int VDT>
+__global__ __launch_bounds__(256) void gae_scan_kernel(const float* r, const void* vals, const void* mask, int64_t B,
                                                        int64_t R, float gamma, float lam, float* adv, float* ret) {
   const int64_t row = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (row >= B) return;
@@ -66,12 +68,15 @@ __global__ __launch_bounds__(256) void gae_scan_kernel(const float* r, const flo
   for (int64_t t = R - 1; t >= 0; --t) {
     const int64_t i = row * R + t;
     const float m = mask_at<MDT>(mask, i);
-    const float delta = r[i] + gamma * nextvalues - v[i];
+    const float vi = VDT == DRL_BF16 ? bf16_to_f32(static_cast<const uint16_t*>(vals)[i]) : static_cast<const float*>(vals)[i];
+    float gv = gamma * nextvalues;
+    if (VDT == DRL_BF16) gv = bf16_to_f32(f32_to_bf16(gv));
+    const float delta = r[i] + gv - vi;
     const float lg = delta + gamma * lam * lastgaelam;
-    nextvalues = v[i] * m + (1.f - m) * nextvalues;
+    nextvalues = vi * m + (1.f - m) * nextvalues;
     lastgaelam = lg * m + (1.f - m) * lastgaelam;
     adv[i] = lastgaelam;
-    ret[i] = lastgaelam + v[i];
+    ret[i] = lastgaelam + vi;
   }
 }
 
@@ -154,11 +159,12 @@ size_t drl_gae_workspace_bytes(int64_t B, int64_t R) {
   return 256;
 }
 
-int drl_gae_advantage_return(const float* rewards, const float* values, const void* mask, int32_t mdt, int64_t B,
-                             int64_t R, float gamma, float lam, float* advantages, float* returns, void* workspace,
-                             size_t workspace_bytes, void* stream) {
+int drl_gae_advantage_return(const float* rewards, const void* values, int32_t values_dtype, const void* mask,
+                             int32_t mdt, int64_t B, int64_t R, float gamma, float lam, float* advantages,
+                             float* returns, void* workspace, size_t workspace_bytes, void* stream) {
   using namespace drl;
   DRL_CHECK_ARG(rewards && values && mask && advantages && returns, "NULL input");
+  DRL_CHECK_ARG(values_dtype == DRL_F32 || values_dtype == DRL_BF16, "values dtype must be F32 or BF16");
   DRL_CHECK_ARG(B >= 1 && R >= 1, "bad shape");
   DRL_CHECK_ARG(mdt == DRL_I64 || mdt == DRL_I32 || mdt == DRL_U8 || mdt == DRL_F32, "bad mask dtype");
   if (workspace == nullptr || workspace_bytes < drl_gae_workspace_bytes(B, R))
@@ -167,8 +173,12 @@ int drl_gae_advantage_return(const float* rewards, const float* values, const vo
   int* err = static_cast<int*>(workspace);
   DRL_HIP(hipMemsetAsync(err, 0, sizeof(int), s));
 #define DRL_GAE(MDT)                                                                                               \
-  hipLaunchKernelGGL(gae_scan_kernel<MDT>, dim3((B + 255) / 256), dim3(256), 0, s, rewards, values, mask, B, R,      \
-                     gamma, lam, advantages, returns);                                                              \
+  if (values_dtype == DRL_BF16)                                                                                    \
+    hipLaunchKernelGGL((gae_scan_kernel<MDT, DRL_BF16>), dim3((B + 255) / 256), dim3(256), 0, s, rewards, values,  \
+                       mask, B, R, gamma, lam, advantages, returns);                                               \
+  else                                                                                                             \
+    hipLaunchKernelGGL((gae_scan_kernel<MDT, DRL_F32>), dim3((B + 255) / 256), dim3(256), 0, s, rewards, values,   \
+                       mask, B, R, gamma, lam, advantages, returns);                                               \
   hipLaunchKernelGGL(masked_whiten_kernel<MDT>, dim3(1), dim3(1024), 0, s, advantages, mask, B * R, err)
   switch (mdt) {
     case DRL_I64: DRL_GAE(DRL_I64); break;

@@ -1,0 +1,150 @@
+"""DataParallelPPOCritic on MI355X (mirror of verl/workers/critic/dp_critic.py:46-263).
+
+Same micro-batching, loss scaling, gradient accumulation and metric keys as the reference. Per micro-batch:
+Qwen2 backbone forward (the actor's kernels) -> the value head on the R positions that predict the
+response ([:, -R-1:-1], ``csrc/value_loss.hip`` drl_value_head_fwd, output in the compute dtype like the
+reference's autocast Linear) -> K6 fused clipped value loss, forward + backward in one launch
+(drl_value_loss_fwd_bwd) -> value-head backward (drl_value_head_bwd, weight/bias gradients accumulated in
+fp32) -> the backbone's hand-written backward. Optimizer: the flat-buffer RCCL all-reduce + HIP grad-norm +
+HIP AdamW of the actor (FlatAdamW), with the critic's own hyper-parameters (critic.yaml: lr 1e-5).
+"""
+
+from __future__ import annotations
+
+import math
+
+import torch
+
+from . import native
+from .dp_actor import FlatAdamW, append_to_dict
+from .protocol import DataProto
+from .qwen2 import Qwen2Model
+
+
+class _ValueHead(torch.autograd.Function):
+    """values (N,) = h (N, H) . score.weight + score.bias; backward dh = dv w, dW/db += (fp32, in place)."""
+
+    @staticmethod
+    def forward(ctx, h, w, b, gw, gb, dummy):
+        h = h.contiguous()
+        ctx.save_for_backward(h, w)
+        ctx.gw, ctx.gb = gw, gb
+        return native.value_head_fwd(h, w, b)
+
+    @staticmethod
+    def backward(ctx, dv):
+        h, w = ctx.saved_tensors
+        dh = native.value_head_bwd(h, w, dv, dweight=ctx.gw.reshape(-1) if ctx.gw is not None else None,
+                                   dbias=ctx.gb if ctx.gb is not None else None)
+        return dh, None, None, None, None, None
+
+
+def value_head(m: Qwen2Model, h):
+    """The critic's score head over hidden rows h (N, H) -> (N,) values in the compute dtype."""
+    s = m.store
+    train = m.training and s.trainable
+    return _ValueHead.apply(h, s.w("score.weight"), s.w("score.bias"), s.g("score.weight") if train else None,
+                            s.g("score.bias") if train else None, m._dummy)
+
+
+class DataParallelPPOCritic:
+    """dp_critic.py:46-263 (padded path; use_remove_padding / ulysses SP are out of scope)."""
+
+    def __init__(self, config, critic_module: Qwen2Model, critic_optimizer: FlatAdamW | None = None):
+        self.config = config
+        self.critic_module = critic_module
+        self.critic_optimizer = critic_optimizer
+        self.use_remove_padding = config.model.get("use_remove_padding", False) if "model" in config else False
+
+    def _forward_micro_batch(self, micro_batch):
+        """dp_critic.py:57-145: values = score(h)[:, -R-1:-1] (compute dtype, (bs, R))."""
+        m = self.critic_module
+        R = micro_batch["responses"].size(-1)
+        h = m.hidden_states(micro_batch["input_ids"], micro_batch["attention_mask"], micro_batch["position_ids"])
+        B = h.shape[0]
+        h = h[:, -R - 1:-1, :].reshape(B * R, h.shape[-1])
+        return value_head(m, h).view(B, R)
+
+    @torch.no_grad()
+    def compute_values(self, data: DataProto) -> torch.Tensor:
+        """dp_critic.py:163-197."""
+        self.critic_module.training = False
+        micro_batch_size = data.meta_info["micro_batch_size"]
+        assert not data.meta_info.get("use_dynamic_bsz", False), "dynamic bsz is not supported yet"
+        keys = ["responses", "input_ids", "attention_mask", "position_ids"]
+        if "response_mask" in data.batch:
+            keys.append("response_mask")
+        data = data.select(batch_keys=keys)
+        values = torch.cat([self._forward_micro_batch(mb.batch) for mb in data.split(micro_batch_size)], 0)
+        if "response_mask" in data.batch:
+            values = values * data.batch["response_mask"]  # only action tokens have values (bf16 * int64 -> bf16)
+        return values
+
+    def update_critic(self, data: DataProto):
+        """dp_critic.py:199-263."""
+        cfg = self.config
+        m = self.critic_module
+        m.training = True
+        data = data.select(batch_keys=["input_ids", "responses", "response_mask", "attention_mask", "position_ids",
+                                       "values", "returns"])
+        assert not cfg.get("use_dynamic_bsz", False), "dynamic bsz is not supported yet"
+        mini_batches = data.split(cfg.ppo_mini_batch_size)
+        mb_out, mb_lsf, grad_norms = [], [], []
+        for _ in range(cfg.ppo_epochs):
+            for mini_batch in mini_batches:
+                grad_accum = cfg.ppo_mini_batch_size // cfg.ppo_micro_batch_size_per_gpu
+                micro_batches = mini_batch.split(cfg.ppo_micro_batch_size_per_gpu)
+                self.critic_optimizer.zero_grad()
+                for k, micro_batch in enumerate(micro_batches):
+                    if k == len(micro_batches) - 1:
+                        self.critic_optimizer.begin_overlap(m)
+                    mb = micro_batch.batch
+                    lsf = 1.0 / grad_accum
+                    vpreds = self._forward_micro_batch(mb)
+                    out = fused_value_loss(vpreds, mb["values"], mb["returns"], mb["response_mask"],
+                                           cliprange_value=cfg.cliprange_value, loss_agg_mode=cfg.loss_agg_mode,
+                                           loss_scale_factor=lsf)
+                    out[3].backward()
+                    mb_out.append(out.detach())
+                    mb_lsf.append(lsf)
+                self.critic_optimizer.end_overlap(m)
+                grad_norms.append(self.critic_optimizer.step().clone())
+        self.critic_optimizer.zero_grad()
+        m.training = False
+        stats = torch.stack(mb_out).cpu().tolist() if mb_out else []
+        gn = torch.cat(grad_norms).cpu().tolist() if grad_norms else []
+        metrics: dict = {}
+        for row, lsf in zip(stats, mb_lsf):
+            append_to_dict(metrics, {"critic/vf_loss": row[0] * lsf, "critic/vf_clipfrac": row[1],
+                                     "critic/vpred_mean": row[2]})
+        for g in gn:
+            if not math.isfinite(g):
+                print(f"WARN: grad_norm is not finite: {g}")
+            append_to_dict(metrics, {"critic/grad_norm": g})
+        return metrics
+
+
+class _FusedValueLoss(torch.autograd.Function):
+    """K6: forward AND backward in the forward launch; backward scales the stored d loss / d vpreds."""
+
+    @staticmethod
+    def forward(ctx, vpreds, values, returns, response_mask, kw):
+        out, dv = native.value_loss_fwd_bwd(vpreds.detach(), values, returns, response_mask,
+                                            want_dvpreds=vpreds.requires_grad, **kw)
+        ctx.save_for_backward(dv if dv is not None else out.new_empty(0))
+        ctx.has = dv is not None
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (dv,) = ctx.saved_tensors
+        return (dv * g[3] if ctx.has else None), None, None, None, None
+
+
+def fused_value_loss(vpreds, values, returns, response_mask, *, cliprange_value, loss_agg_mode="token-mean",
+                     loss_scale_factor=1.0):
+    """float32[8]: vf_loss, vf_clipfrac, vpred_mean, loss (= vf_loss * loss_scale_factor, the differentiable
+    slot), mask count (DRL_VALUE_OUT_*)."""
+    return _FusedValueLoss.apply(vpreds, values, returns, response_mask,
+                                 dict(cliprange_value=cliprange_value, loss_agg_mode=loss_agg_mode,
+                                      loss_scale_factor=loss_scale_factor))

@@ -45,7 +45,14 @@ def compute_data_metrics(batch: DataProto, use_critic: bool = False) -> dict[str
             "critic/returns/mean", "critic/returns/max", "critic/returns/min", "response_length/mean",
             "response_length/max", "response_length/min", "response_length/clip_ratio", "prompt_length/mean",
             "prompt_length/max", "prompt_length/min", "prompt_length/clip_ratio"]
-    return dict(zip(keys, vals))
+    out = dict(zip(keys, vals))
+    if use_critic:  # metric_utils.py:138-143, 176-186
+        v = torch.masked_select(b["values"], rmask).float()
+        rdv, rv = torch.var(ret - v), torch.var(ret)
+        cv = torch.stack([v.mean(), v.max(), v.min(), 1.0 - rdv / (rv + 1e-5)]).cpu().tolist()
+        out.update(dict(zip(["critic/values/mean", "critic/values/max", "critic/values/min",
+                             "critic/vf_explained_var"], cv)))
+    return out
 
 
 def compute_timing_metrics(batch: DataProto, timing_raw: dict) -> dict[str, Any]:

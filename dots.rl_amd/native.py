@@ -287,14 +287,78 @@ def grpo_outcome_advantage(token_level_rewards, response_mask, row_group, group_
 
 def gae_advantage_return(token_level_rewards, values, response_mask, gamma, lam):
     _dev(token_level_rewards, values, response_mask)
-    r, v, m = _c(token_level_rewards.float()), _c(values.float()), _c(response_mask)
+    r, m = _c(token_level_rewards.float()), _c(response_mask)
+    v = _c(values if values.dtype == torch.bfloat16 else values.float())  # bf16 critic values read as stored
     B, R = r.shape
     adv, ret = torch.empty_like(r), torch.empty_like(r)
     L = lib()
     ws = _ws.get(L.drl_gae_workspace_bytes(B, R), r.device)
-    check(L.drl_gae_advantage_return(_p(r), _p(v), _p(m), mask_dtype_code(m), B, R, float(gamma), float(lam), _p(adv),
-                                     _p(ret), _p(ws), ws.numel(), _stream()), "drl_gae_advantage_return")
+    check(L.drl_gae_advantage_return(_p(r), _p(v), _VALUE_DTYPES[v.dtype], _p(m), mask_dtype_code(m), B, R, float(gamma),
+                                     float(lam), _p(adv), _p(ret), _p(ws), ws.numel(), _stream()),
+          "drl_gae_advantage_return")
     return adv, ret
+
+
+# ----------------------------------------------------------------------------------------------- K6 critic
+_VALUE_DTYPES = {torch.float32: _lib.DRL_F32, torch.bfloat16: _lib.DRL_BF16}
+
+
+def value_loss_fwd_bwd(vpreds, values, returns, response_mask, *, cliprange_value, loss_agg_mode="token-mean",
+                       loss_scale_factor=1.0, want_dvpreds=True, out=None):
+    """One launch after a row-count pre-pass: float32[8] scalars (DRL_VALUE_OUT_*: vf_loss, vf_clipfrac,
+    vpred_mean, loss = vf_loss * loss_scale_factor, mask count) and d loss / d vpreds (float32)."""
+    _dev(vpreds, values, returns, response_mask)
+    if vpreds.dtype != values.dtype:
+        values = values.to(vpreds.dtype)
+    if vpreds.dtype not in _VALUE_DTYPES:
+        raise TypeError(f"vpreds dtype {vpreds.dtype}: float32 or bfloat16")
+    vp, vo, rt, m = _c(vpreds.detach()), _c(values), _c(returns.float()), _c(response_mask)
+    B, R = vp.shape
+    assert vo.shape == (B, R) and rt.shape == (B, R) and m.shape == (B, R)
+    prm = _lib.ValueLossParams(float(cliprange_value), float(loss_scale_factor), _lib.AGG_MODES[loss_agg_mode], 0)
+    dev = vp.device
+    if out is None:
+        out = torch.empty(_lib.VALUE_OUT_N, dtype=torch.float32, device=dev)
+    dv = torch.empty(B, R, dtype=torch.float32, device=dev) if want_dvpreds else None
+    L = lib()
+    ws = _ws.get(L.drl_value_loss_workspace_bytes(B, R), dev)
+    check(L.drl_value_loss_fwd_bwd(_p(vp), _p(vo), _VALUE_DTYPES[vp.dtype], _p(rt), _p(m), mask_dtype_code(m), B, R,
+                                   ctypes.byref(prm), _p(out), _p(dv), _p(ws), ws.numel(), _stream()),
+          "drl_value_loss_fwd_bwd")
+    return out, dv
+
+
+def value_head_fwd(hidden, weight, bias, out_dtype=None):
+    """values (N,) = hidden (N, H) . weight (H) + bias, fp32 accumulation, stored as ``out_dtype``
+    (default: the hidden dtype, as the reference's autocast Linear)."""
+    _dev(hidden, weight, bias)
+    assert hidden.dim() == 2 and hidden.stride(-1) == 1
+    N, H = hidden.shape
+    dt = _VALUE_DTYPES[hidden.dtype]
+    w = _c(weight.reshape(-1).to(hidden.dtype))
+    b = _c(bias.reshape(-1).to(hidden.dtype)) if bias is not None else None
+    od = out_dtype or hidden.dtype
+    out = torch.empty(N, dtype=od, device=hidden.device)
+    check(lib().drl_value_head_fwd(_p(hidden), hidden.stride(0), _p(w), _p(b), dt, N, H, _p(out), _VALUE_DTYPES[od],
+                                   _stream()), "drl_value_head_fwd")
+    return out
+
+
+def value_head_bwd(hidden, weight, dvalues, dweight=None, dbias=None, want_dhidden=True):
+    """dhidden (N, H) in the hidden dtype; accumulates into the fp32 ``dweight`` (H) / ``dbias`` (1)."""
+    _dev(hidden, weight, dvalues, dweight, dbias)
+    N, H = hidden.shape
+    dt = _VALUE_DTYPES[hidden.dtype]
+    w = _c(weight.reshape(-1).to(hidden.dtype))
+    dv = _c(dvalues.reshape(-1).float())
+    for g in (dweight, dbias):
+        assert g is None or (g.dtype == torch.float32 and g.is_contiguous())
+    dh = torch.empty(N, H, dtype=hidden.dtype, device=hidden.device) if want_dhidden else None
+    L = lib()
+    ws = _ws.get(L.drl_value_head_bwd_workspace_bytes(N, H), hidden.device)
+    check(L.drl_value_head_bwd(_p(hidden), hidden.stride(0), _p(w), dt, _p(dv), N, H, _p(dh), H if dh is not None else 0,
+                               _p(dweight), _p(dbias), _p(ws), ws.numel(), _stream()), "drl_value_head_bwd")
+    return dh
 
 
 # ----------------------------------------------------------------------------------------------- K4

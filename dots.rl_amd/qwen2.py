@@ -47,6 +47,9 @@ class Qwen2Config:
     bos_token_id: int = 151643
     eos_token_id: int = 151645
     pad_token_id: int = 151643
+    # > 0: token-classification head `score` Linear(H, num_labels, bias=True) instead of the lm_head (the
+    # critic the reference loads with AutoModelForTokenClassification, num_labels=1, fsdp_workers.py:1045)
+    num_labels: int = 0
     extra: dict = field(default_factory=dict)
 
     @property
@@ -76,7 +79,9 @@ def param_specs(cfg: Qwen2Config):
             (p + "down_proj", (H, I), "gemm"),
         ]
     specs.append(("norm", (H,), "small"))
-    if not cfg.tie_word_embeddings:
+    if cfg.num_labels > 0:  # critic value head, read in the compute dtype like the autocast Linear
+        specs += [("score.weight", (cfg.num_labels, H), "gemm"), ("score.bias", (cfg.num_labels,), "gemm")]
+    elif not cfg.tie_word_embeddings:
         specs.append(("lm_head", (cfg.vocab_size, H), "gemm"))
     return specs
 
@@ -156,7 +161,10 @@ class ParamStore:
             put(q + "gate_up_proj", torch.cat([sd[p + "mlp.gate_proj.weight"], sd[p + "mlp.up_proj.weight"]], 0))
             put(q + "down_proj", sd[p + "mlp.down_proj.weight"])
         put("norm", sd["model.norm.weight"])
-        if not cfg.tie_word_embeddings:
+        if cfg.num_labels > 0:
+            put("score.weight", sd["score.weight"])
+            put("score.bias", sd["score.bias"] if "score.bias" in sd else torch.zeros(cfg.num_labels))
+        elif not cfg.tie_word_embeddings:
             put("lm_head", sd["lm_head.weight"])
         self.refresh_compute()
 

@@ -23,7 +23,8 @@ from .metric_utils import compute_data_metrics, compute_throughout_metrics, comp
 from .protocol import DataProto
 from .reward import SyntheticBernoulliRewardManager, compute_reward
 from .single_controller import SPMDWorkerGroup
-from .workers import ActorRolloutRefWorker
+from .config import resolve_critic_config
+from .workers import ActorRolloutRefWorker, CriticWorker
 
 
 @contextmanager
@@ -117,6 +118,12 @@ class RayPPOTrainer:
         self.pad_token_id = pad_token_id
         self.use_reference_policy = config.actor_rollout_ref.actor.use_kl_loss or config.algorithm.use_kl_in_reward
         self.kl_ctrl_in_reward = core_algos.get_kl_controller(config.algorithm.kl_ctrl)
+        # ray_trainer.py:340-356: a critic when critic.enable says so, else exactly for GAE
+        enable = config.get("critic", {}).get("enable") if "critic" in config else None
+        if enable is not None:
+            self.use_critic = bool(enable)
+        else:
+            self.use_critic = config.algorithm.adv_estimator == AdvantageEstimator.GAE.value
         self.global_steps = 0
         self.n_gpus = dist.get_world_size() if dist.is_initialized() else 1
 
@@ -125,6 +132,9 @@ class RayPPOTrainer:
         worker = ActorRolloutRefWorker(self.config.actor_rollout_ref, role="actor_rollout_ref")
         self.actor_rollout_wg = SPMDWorkerGroup(worker)
         self.ref_policy_wg = self.actor_rollout_wg
+        if self.use_critic:
+            self.critic_wg = SPMDWorkerGroup(CriticWorker(resolve_critic_config(self.config)))
+            self.critic_wg.init_model()
         self.actor_rollout_wg.init_model()
 
     def _uids(self, n):
@@ -180,6 +190,9 @@ class RayPPOTrainer:
             if self.use_reference_policy:
                 with marked_timer("ref", timing_raw):
                     batch = batch.union(self.ref_policy_wg.compute_ref_log_prob(batch))
+            if self.use_critic:
+                with marked_timer("values", timing_raw):
+                    batch = batch.union(self.critic_wg.compute_values(batch))
             with marked_timer("adv", timing_raw):
                 batch.batch["token_level_scores"] = reward_tensor
                 if cfg.algorithm.use_kl_in_reward:
@@ -189,6 +202,10 @@ class RayPPOTrainer:
                     batch.batch["token_level_rewards"] = batch.batch["token_level_scores"]
                 batch = compute_advantage(batch, cfg.algorithm.adv_estimator, cfg.algorithm.gamma, cfg.algorithm.lam,
                                           ar.rollout.n, cfg.algorithm.norm_adv_by_std_in_grpo, cfg.algorithm)
+            if self.use_critic:
+                with marked_timer("update_critic", timing_raw):
+                    critic_out = self.critic_wg.update_critic(batch)
+                metrics.update(reduce_metrics(critic_out.meta_info["metrics"]))
             if cfg.trainer.critic_warmup <= self.global_steps:
                 with marked_timer("update_actor", timing_raw):
                     batch.meta_info["multi_turn"] = False
@@ -197,7 +214,7 @@ class RayPPOTrainer:
                 metrics.update(reduce_metrics(actor_out.meta_info["metrics"]))
         metrics["actor/entropy"] = float(metrics["actor/entropy"])
         metrics.update({"training/global_step": self.global_steps})
-        metrics.update(compute_data_metrics(batch, use_critic=False))
+        metrics.update(compute_data_metrics(batch, use_critic=self.use_critic))
         metrics.update(compute_timing_metrics(batch, timing_raw))
         metrics.update(compute_throughout_metrics(batch, timing_raw, self.n_gpus))
         n_resp = batch.batch["response_mask"].sum().item()

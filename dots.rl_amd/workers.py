@@ -20,6 +20,7 @@ import torch.distributed as dist
 
 from .config import QWEN25_05B
 from .dp_actor import DataParallelPPOActor, FlatAdamW
+from .dp_critic import DataParallelPPOCritic
 from .protocol import DataProto
 from .qwen2 import ParamStore, Qwen2Config, Qwen2Model, flops_per_token
 from .rollout import MI355XRollout
@@ -227,3 +228,110 @@ class ActorRolloutRefWorker(Worker):
         self.actor_optimizer.load_state_dict(sd["optim"])
         if self._is_rollout:
             self.rollout.calls = int(sd.get("rollout_calls", 0))
+
+
+class CriticWorker(Worker):
+    """fsdp_workers.py:922-1340 for ``critic.strategy = "mi355x"``: Qwen2 backbone + `score` value head
+    (num_labels=1, classifier dropout 0), replicated-parameter DP with one RCCL all-reduce per optimizer step."""
+
+    def __init__(self, config, output_device: str = "cuda"):
+        super().__init__()
+        self.config = config
+        self.output_device = output_device
+        self.device = torch.device("cuda", torch.cuda.current_device())
+        dp = dist.get_world_size() if dist.is_initialized() else 1
+        self.dp_size = dp
+        self.dp_rank = dist.get_rank() if dist.is_initialized() else 0
+        self._register_dispatch_collect_info("critic", dp_rank=self.dp_rank, is_collect=True)
+        # fsdp_workers.py:979-1000 batch-size normalisation
+        c = config
+        c.ppo_mini_batch_size = c.ppo_mini_batch_size * c.get("rollout_n", 1) // dp
+        if c.get("ppo_micro_batch_size") is not None:
+            c.ppo_micro_batch_size_per_gpu = c.ppo_micro_batch_size // dp
+            c.forward_micro_batch_size_per_gpu = c.get("forward_micro_batch_size", c.ppo_micro_batch_size) // dp
+        if c.get("forward_micro_batch_size_per_gpu") is None:
+            c.forward_micro_batch_size_per_gpu = c.ppo_micro_batch_size_per_gpu
+        assert c.ppo_mini_batch_size % c.ppo_micro_batch_size_per_gpu == 0, (
+            f"normalized ppo_mini_batch_size {c.ppo_mini_batch_size} should be divisible by "
+            f"ppo_micro_batch_size_per_gpu {c.ppo_micro_batch_size_per_gpu}")
+
+    @register(dispatch_mode=Dispatch.ONE_TO_ALL)
+    def init_model(self):
+        """fsdp_workers.py:1003-1123 (_build_critic_model_optimizer + DataParallelPPOCritic)."""
+        cfg = self.config
+        _enable_gemm_tuning(cfg.model.get("gemm_tuning", "auto"))
+        mcfg = resolve_model_config(cfg.model)
+        mcfg.num_labels = 1
+        self.model_config = mcfg
+        dtype = torch.float32 if cfg.model.get("dtype", "bfloat16") == "float32" else torch.bfloat16
+        self.store = ParamStore(mcfg, self.device, compute_dtype=dtype, trainable=True)
+        path = cfg.model.get("path", "random:")
+        if path.startswith("random:"):
+            self.store.init_random(int(cfg.model.get("seed", 4321)))
+        else:
+            from safetensors.torch import load_file
+
+            sd = {}
+            for f in sorted(os.listdir(path)):
+                if f.endswith(".safetensors"):
+                    sd.update(load_file(os.path.join(path, f)))
+            self.store.load_state_dict_hf(sd)
+        self.critic_module = Qwen2Model(mcfg, self.store)
+        o = cfg.optim
+        total = o.get("total_training_steps", -1)
+        warm = o.get("lr_warmup_steps", -1)
+        if warm is None or warm < 0:
+            warm = int(o.get("lr_warmup_steps_ratio", 0.0) * max(total, 0))
+        self.critic_optimizer = FlatAdamW(self.store, lr=o.lr, betas=tuple(o.get("betas", (0.9, 0.999))),
+                                          eps=o.get("eps", 1e-8), weight_decay=o.weight_decay,
+                                          max_grad_norm=cfg.grad_clip, warmup_steps=warm)
+        self.critic = DataParallelPPOCritic(cfg, self.critic_module, self.critic_optimizer)
+
+    def _out(self, d: DataProto):
+        return d.to(self.output_device) if self.output_device != "cuda" else d
+
+    @register(dispatch_mode=make_nd_compute_dataproto_dispatch_fn(mesh_name="critic"))
+    def compute_values(self, data: DataProto):
+        """fsdp_workers.py:1237-1258 -> values (bs, R) in the compute dtype."""
+        data = data.to(self.device)
+        data.meta_info["micro_batch_size"] = self.config.forward_micro_batch_size_per_gpu
+        data.meta_info["max_token_len"] = self.config.get("forward_max_token_len_per_gpu", 32768)
+        data.meta_info["use_dynamic_bsz"] = self.config.get("use_dynamic_bsz", False)
+        values = self.critic.compute_values(data=data)
+        return self._out(DataProto.from_dict(tensors={"values": values}))
+
+    @register(dispatch_mode=make_nd_compute_dataproto_dispatch_fn(mesh_name="critic"))
+    def update_critic(self, data: DataProto):
+        """fsdp_workers.py:1260-1292 (+ perf/mfu/critic with the MI355X peak, critic/lr, lr schedule step)."""
+        data = data.to(self.device)
+        t0 = time.perf_counter()
+        metrics = self.critic.update_critic(data=data)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        ntok = data.meta_info.get("global_token_num")
+        if ntok:
+            T = data.batch["input_ids"].shape[1]
+            est = 3 * flops_per_token(self.model_config, T) * sum(ntok)
+            metrics["perf/mfu/critic"] = est * self.config.ppo_epochs / (dt * MI355X_BF16_DENSE_PEAK * self.dp_size)
+        metrics["critic/lr"] = self.critic_optimizer.current_lr()
+        self.critic_optimizer.sched_step += 1
+        return DataProto(meta_info={"metrics": metrics})
+
+    @register(dispatch_mode=Dispatch.ONE_TO_ALL)
+    def save_checkpoint(self, local_path, hdfs_path=None, global_step=0, max_ckpt_to_keep=None):
+        """fsdp_workers.py:1294-1310: replicated params -> rank 0 writes model + optimizer."""
+        if self.dp_rank == 0:
+            os.makedirs(local_path, exist_ok=True)
+            torch.save({"master": self.store.master.cpu(),
+                        "optim": {k: (v.cpu() if torch.is_tensor(v) else v)
+                                  for k, v in self.critic_optimizer.state_dict().items()},
+                        "global_step": global_step}, os.path.join(local_path, "critic_model_optim.pt"))
+        if dist.is_initialized():
+            dist.barrier()
+
+    @register(dispatch_mode=Dispatch.ONE_TO_ALL)
+    def load_checkpoint(self, local_path, hdfs_path=None, del_local_after_load=True):
+        sd = torch.load(os.path.join(local_path, "critic_model_optim.pt"), map_location="cpu", weights_only=True)
+        self.store.master.copy_(sd["master"])
+        self.store.refresh_compute()
+        self.critic_optimizer.load_state_dict(sd["optim"])

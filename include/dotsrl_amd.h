@@ -152,11 +152,59 @@ int drl_grpo_outcome_advantage(const float* token_level_rewards, const void* res
                                int32_t norm_adv_by_std, float* advantages, float* returns, void* workspace,
                                size_t workspace_bytes, void* stream);
 
-/* K5 — GAE + masked_whiten (core_algos.py:208-256, torch_functional.py:206-223). */
+/* K5 — GAE + masked_whiten (core_algos.py:208-256, torch_functional.py:206-223). values (B, R) of
+ * values_dtype: F32, or BF16 = the critic's autocast output as the reference stores it (then gamma * V(t+1)
+ * is rounded to bf16 as the reference's bf16 tensor arithmetic does). */
 size_t drl_gae_workspace_bytes(int64_t B, int64_t R);
-int drl_gae_advantage_return(const float* token_level_rewards, const float* values, const void* response_mask,
-                             int32_t mask_dtype, int64_t B, int64_t R, float gamma, float lam, float* advantages,
-                             float* returns, void* workspace, size_t workspace_bytes, void* stream);
+int drl_gae_advantage_return(const float* token_level_rewards, const void* values, int32_t values_dtype,
+                             const void* response_mask, int32_t mask_dtype, int64_t B, int64_t R, float gamma,
+                             float lam, float* advantages, float* returns, void* workspace, size_t workspace_bytes,
+                             void* stream);
+
+/* ------------------------------------------------------------------------------------------------
+ * K6 — critic: clipped value loss, forward + backward in one launch (after a row-count pre-pass).
+ * Replaces compute_value_loss (verl/trainer/ppo/core_algos.py:1230-1269) + `vf_loss * loss_scale_factor`
+ * + loss.backward() down to d loss / d vpreds (verl/workers/critic/dp_critic.py:218-245) and the
+ * critic/vpred_mean metric (masked_mean, torch_functional.py:171-185).
+ * vpreds / values (B, R) of value_dtype (F32, or BF16 = the reference critic's autocast output: the clip
+ * bounds values -/+ cliprange are rounded to bf16 as the reference's bf16 tensor arithmetic does);
+ * returns (B, R) float32; out_scalars device float[DRL_VALUE_OUT_N]; dvpreds (B, R) float32 or NULL.
+ * ---------------------------------------------------------------------------------------------- */
+typedef struct drl_value_loss_params {
+  float cliprange_value;   /* critic.cliprange_value */
+  float loss_scale_factor; /* 1 / gradient_accumulation (dp_critic.py:236-238) */
+  int32_t loss_agg_mode;   /* drl_agg_mode (critic.loss_agg_mode) */
+  int32_t pad;
+} drl_value_loss_params;
+
+enum {
+  DRL_VALUE_OUT_VF_LOSS = 0,     /* 0.5 * agg_loss(max(vf_losses1, vf_losses2)) */
+  DRL_VALUE_OUT_VF_CLIPFRAC = 1, /* masked_mean(vf_losses2 > vf_losses1) */
+  DRL_VALUE_OUT_VPRED_MEAN = 2,  /* masked_mean(vpreds) */
+  DRL_VALUE_OUT_LOSS = 3,        /* vf_loss * loss_scale_factor — the value backpropagated */
+  DRL_VALUE_OUT_MASK_COUNT = 4,
+  DRL_VALUE_OUT_N = 8
+};
+
+size_t drl_value_loss_workspace_bytes(int64_t B, int64_t R);
+int drl_value_loss_fwd_bwd(const void* vpreds, const void* values, int32_t value_dtype, const float* returns,
+                           const void* response_mask, int32_t mask_dtype, int64_t B, int64_t R,
+                           const drl_value_loss_params* params, float* out_scalars, float* dvpreds, void* workspace,
+                           size_t workspace_bytes, void* stream);
+
+/* Critic value head (HF GenericForTokenClassification.score = Linear(H, 1, bias=True), the critic the
+ * reference loads with AutoModelForTokenClassification, dp_critic.py:57-145): values[n] = hidden[n, :] . w
+ * + b, fp32 accumulation, written as out_dtype (BF16 = the reference's autocast output). hidden (N, H)
+ * row stride ld_h, weight (H) and bias (1, may be NULL) in `dt` (BF16 / F32). H % 8 (bf16) / 4 (fp32). */
+int drl_value_head_fwd(const void* hidden, int64_t ld_h, const void* weight, const void* bias, int32_t dt, int64_t N,
+                       int64_t H, void* values, int32_t out_dtype, void* stream);
+/* Backward: dhidden[n, :] = dvalues[n] * w (in `dt`, may be NULL); dweight[k] += sum_n dvalues[n] hidden[n, k]
+ * and dbias[0] += sum_n dvalues[n] (fp32 gradient buffers, accumulated in place; either may be NULL);
+ * deterministic (fixed-order partials). workspace: drl_value_head_bwd_workspace_bytes(N, H) bytes. */
+size_t drl_value_head_bwd_workspace_bytes(int64_t N, int64_t H);
+int drl_value_head_bwd(const void* hidden, int64_t ld_h, const void* weight, int32_t dt, const float* dvalues,
+                       int64_t N, int64_t H, void* dhidden, int64_t ld_dh, float* dweight, float* dbias,
+                       void* workspace, size_t workspace_bytes, void* stream);
 
 /* ------------------------------------------------------------------------------------------------
  * K4 — decode-step token selection over the vocabulary (HF generate semantics that HFRollout

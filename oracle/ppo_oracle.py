@@ -236,7 +236,9 @@ def group_ids(index):
 # ---------------------------------------------------------------------------------------------
 # compute_gae_advantage_return — core_algos.py:208-256
 # ---------------------------------------------------------------------------------------------
-def gae_advantage_return(token_level_rewards, values, response_mask, gamma, lam):
+def gae_advantage_return(token_level_rewards, values, response_mask, gamma, lam, values_bf16=False):
+    """values_bf16: the values are a bf16 tensor in the reference (critic output, dp_critic.py:192), so
+    `gamma * nextvalues` is bf16 tensor arithmetic there (rounded to bf16; core_algos.py:244)."""
     r = np.asarray(token_level_rewards, f64)
     v = np.asarray(values, f64)
     m = np.asarray(response_mask, f64)
@@ -245,13 +247,63 @@ def gae_advantage_return(token_level_rewards, values, response_mask, gamma, lam)
     lastgaelam = np.zeros(B)
     adv = np.zeros((B, T))
     for t in reversed(range(T)):
-        delta = r[:, t] + gamma * nextvalues - v[:, t]
+        gv = gamma * nextvalues
+        if values_bf16:
+            gv = bf16_round(gv)
+        delta = r[:, t] + gv - v[:, t]
         lg = delta + gamma * lam * lastgaelam
         nextvalues = v[:, t] * m[:, t] + (1 - m[:, t]) * nextvalues
         lastgaelam = lg * m[:, t] + (1 - m[:, t]) * lastgaelam
         adv[:, t] = lastgaelam
     returns = adv + v
     return masked_whiten(adv, response_mask), returns
+
+
+# ---------------------------------------------------------------------------------------------
+# compute_value_loss — core_algos.py:1230-1269 (+ the analytic d/d vpreds of dp_critic.py:237-240)
+# ---------------------------------------------------------------------------------------------
+def bf16_round(x):
+    """Round to the nearest bfloat16 (ties to even), returned as float64."""
+    a = np.ascontiguousarray(np.asarray(x, np.float32))
+    u = a.view(np.uint32).astype(np.uint64)
+    u = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16) << 16
+    return (u.astype(np.uint32).view(np.float32)).astype(f64)
+
+
+def value_loss(vpreds, values, returns, response_mask, cliprange_value, loss_agg_mode="token-mean",
+               loss_scale_factor=1.0, value_bf16=False):
+    """Returns (vf_loss, vf_clipfrac, vpred_mean, d (vf_loss * loss_scale_factor) / d vpreds).
+
+    clip_by_value (torch_functional.py:136-142) = torch.max(torch.min(vpreds, values + c), values - c); with
+    bf16 critic outputs the bounds `values -/+ c` are bf16 tensors (rounded). Squared errors in float32
+    against float32 returns (type promotion), reductions as agg_loss / masked_mean."""
+    f32 = np.float32
+    v = np.asarray(vpreds, f32)
+    old = np.asarray(values, f32)
+    ret = np.asarray(returns, f32)
+    # tensor -/+ python float: float32 arithmetic with the scalar rounded to float32 (torch opmath)
+    hi = old + f32(cliprange_value)
+    lo = old - f32(cliprange_value)
+    if value_bf16:  # bf16 tensor -/+ python float: the scalar is rounded to bf16 too (as torch computes it here)
+        cb = f32(bf16_round(f32(cliprange_value)))
+        hi, lo = bf16_round(old + cb).astype(f32), bf16_round(old - cb).astype(f32)
+    y = np.minimum(v, hi)
+    gy = np.where(v < hi, 1.0, np.where(v == hi, 0.5, 0.0))
+    vc = np.maximum(y, lo)
+    gc = np.where(y > lo, 1.0, np.where(y == lo, 0.5, 0.0))
+    e1, e2 = v - ret, vc - ret
+    l1, l2 = (e1 * e1).astype(f64), (e2 * e2).astype(f64)
+    w1, w2 = _max_grad(l1, l2)
+    lmax = np.maximum(l1, l2)
+    vf_loss = 0.5 * agg_loss(lmax, response_mask, loss_agg_mode)
+    vf_clipfrac = masked_mean((l2 > l1).astype(f64), response_mask)
+    vpred_mean = masked_mean(v.astype(f64), response_mask)
+    if value_bf16:  # masked_mean over a bf16 tensor: the sum is a bf16 tensor, the quotient promotes to fp32
+        m = np.asarray(response_mask, f64)  # against the fp32 (mask.sum() + 1e-8) (torch_functional.py:163-185)
+        vpred_mean = f32(bf16_round((v.astype(f64) * m).sum())) / f32(m.sum() + 1e-8)
+    dl = w1 * 2.0 * e1.astype(f64) + w2 * 2.0 * e2.astype(f64) * gy * gc
+    dv = loss_scale_factor * 0.5 * agg_loss_grad(response_mask, loss_agg_mode) * dl
+    return vf_loss, vf_clipfrac, vpred_mean, dv
 
 
 # ---------------------------------------------------------------------------------------------

@@ -15,6 +15,9 @@ Reference call sites (file:line under /root/reference):
 * fused lm_head -> logp/entropy (+ backward) : verl/utils/experimental/torch_functional.py:20-216
 * response mask / position ids : verl/utils/torch_functional.py:226-246, verl/utils/model.py:219,
   verl/workers/rollout/hf_rollout.py:151-160
+* critic value loss + backward : verl/trainer/ppo/core_algos.py:1230-1269 as dp_critic.py:218-245 scales it
+* critic forward/backward (tiny Qwen2ForTokenClassification, the model fsdp_workers.py:1003-1060 builds) :
+  verl/workers/critic/dp_critic.py:57-145 values slice, compute_value_loss, loss.backward()
 * masked_mean known answers : tests/utils/test_torch_functional.py:55-66 (reference test, reproduced as data)
 """
 
@@ -423,6 +426,104 @@ def gen_tiny_qwen2():
                                              "response_length": R, "min_top2_logit_gap": gap,
                                              "hf": "transformers Qwen2ForCausalLM fp32 eager attention",
                                              "ref": "hf_rollout.py:112-171; dp_actor.py:249-272"})
+
+
+# --------------------------------------------------------------------------------------------
+# K6: critic clipped value loss + backward (core_algos.py:1230-1269; dp_critic.py:218-245)
+# --------------------------------------------------------------------------------------------
+def gen_value_loss():
+    g = torch.Generator().manual_seed(11)
+    arrays, cases = {}, []
+    ci = 0
+    for dt in ["float32", "bfloat16"]:
+        for mode in ["token-mean", "seq-mean-token-sum", "seq-mean-token-mean", "seq-mean-token-sum-norm"]:
+            for clip, lsf in [(0.5, 0.25), (0.2, 1.0)]:
+                B, R = (6, 40) if ci % 2 == 0 else (3, 129)
+                values = torch.randn(B, R, generator=g) * 0.8
+                vpreds = values + torch.randn(B, R, generator=g) * 0.6
+                returns = values + torch.randn(B, R, generator=g)
+                mask = torch.ones(B, R, dtype=torch.int64)
+                for i in range(B):
+                    mask[i, int(torch.randint(1, R + 1, (1,), generator=g)):] = 0
+                tdt = getattr(torch, dt)
+                values, vpreds = values.to(tdt), vpreds.to(tdt)
+                # edges: vpred exactly on the clip bounds (ties in torch.min / torch.max), vpred == value
+                vpreds[0, 0] = (values[0, 0] + clip).to(tdt)
+                vpreds[0, 1] = (values[0, 1] - clip).to(tdt)
+                vpreds[0, 2] = values[0, 2]
+                returns[0, 3] = vpreds[0, 3].float()  # zero error
+                vp = vpreds.clone().requires_grad_(True)
+                vf_loss, vf_clipfrac = ca.compute_value_loss(vpreds=vp, returns=returns, values=values,
+                                                             response_mask=mask, cliprange_value=clip,
+                                                             loss_agg_mode=mode)
+                (vf_loss * lsf).backward()
+                vpred_mean = vF.masked_mean(vpreds, mask)
+                for k, v in dict(vpreds=vpreds, values=values, returns=returns, mask=mask, vf_loss=vf_loss.detach(),
+                                 vf_clipfrac=vf_clipfrac.detach(), vpred_mean=vpred_mean.detach(),
+                                 dvpreds=vp.grad).items():
+                    arrays[f"c{ci}_{k}"] = v.float() if torch.is_tensor(v) and v.is_floating_point() else v
+                cases.append({"dtype": dt, "mode": mode, "cliprange_value": clip, "loss_scale_factor": lsf})
+                ci += 1
+    _save("value_loss.npz", arrays, {"cases": cases, "ref": "core_algos.py:1230-1269; dp_critic.py:218-245"})
+
+
+def gen_gae_bf16():
+    """GAE over bf16 critic values (the dtype dp_critic.compute_values returns under autocast)."""
+    g = torch.Generator().manual_seed(6)
+    arrays, cases = {}, []
+    for ci, (B, R, gamma, lam) in enumerate([(5, 33, 0.99, 0.95), (4, 16, 1.0, 0.9)]):
+        rewards = torch.randn(B, R, generator=g)
+        values = torch.randn(B, R, generator=g).to(torch.bfloat16)
+        mask = torch.ones(B, R, dtype=torch.int64)
+        for i in range(B):
+            mask[i, int(torch.randint(2, R + 1, (1,), generator=g)):] = 0
+        adv, ret = ca.compute_gae_advantage_return(rewards, values, mask, gamma=gamma, lam=lam)
+        arrays.update({f"c{ci}_rewards": rewards, f"c{ci}_values": values.float(), f"c{ci}_mask": mask,
+                       f"c{ci}_adv": adv, f"c{ci}_ret": ret})
+        cases.append({"gamma": gamma, "lam": lam})
+    _save("gae_bf16.npz", arrays, {"cases": cases, "values_dtype": "bfloat16", "ref": "core_algos.py:208-256"})
+
+
+def gen_tiny_critic():
+    """Critic = the tiny backbone + a `score` head (Qwen2ForTokenClassification, num_labels=1, dropout 0, as
+    fsdp_workers.py:1045-1056 configures it), fp32: values over the tiny rollout sequences (dp_critic.py:127-145
+    padded path), then one micro-batch value loss (token-mean, cliprange 0.5, loss_scale_factor 0.5) and its
+    backward; records values and the gradients of the head, the final norm and the first layer norm."""
+    from safetensors.torch import load_file, save_file
+    from transformers import Qwen2Config, Qwen2ForTokenClassification
+
+    cfg = Qwen2Config(**TINY_QWEN2, attn_implementation="eager", num_labels=1, classifier_dropout=0.0)
+    model = Qwen2ForTokenClassification(cfg).float()
+    sd = load_file(os.path.join(HERE, "tiny_qwen2", "model.safetensors"))
+    missing, unexpected = model.load_state_dict(sd, strict=False)
+    assert set(missing) == {"score.weight", "score.bias"} and not unexpected, (missing, unexpected)
+    g = torch.Generator().manual_seed(77)
+    with torch.no_grad():
+        model.score.weight.copy_(torch.randn(model.score.weight.shape, generator=g) * 0.2)
+        model.score.bias.copy_(torch.randn(1, generator=g) * 0.1)
+    save_file({"score.weight": model.score.weight.detach().contiguous(), "score.bias": model.score.bias.detach()},
+              os.path.join(HERE, "tiny_qwen2", "score.safetensors"))
+    z = np.load(os.path.join(HERE, "tiny_qwen2_rollout.npz"))
+    seq, am, pos = (torch.from_numpy(z[k]) for k in ("sequences", "attention_mask", "position_ids"))
+    resp = torch.from_numpy(z["responses"])
+    R = resp.shape[1]
+    rmask = am[:, -R:]
+    model.train()
+    vpreds = model(input_ids=seq, attention_mask=am, position_ids=pos, use_cache=False).logits
+    vpreds = vpreds[:, -R - 1:-1].squeeze(-1)
+    values = (vpreds.detach() + 0.3 * torch.randn(vpreds.shape, generator=g)) * rmask
+    returns = values + torch.randn(vpreds.shape, generator=g)
+    vf_loss, vf_clipfrac = ca.compute_value_loss(vpreds=vpreds, returns=returns, values=values, response_mask=rmask,
+                                                 cliprange_value=0.5, loss_agg_mode="token-mean")
+    (vf_loss * 0.5).backward()
+    arrays = dict(vpreds=vpreds.detach(), values=values, returns=returns, vf_loss=vf_loss.detach(),
+                  vf_clipfrac=vf_clipfrac, d_score_weight=model.score.weight.grad, d_score_bias=model.score.bias.grad,
+                  d_norm=model.model.norm.weight.grad,
+                  d_input_layernorm0=model.model.layers[0].input_layernorm.weight.grad,
+                  d_embed_rows=model.model.embed_tokens.weight.grad.norm(dim=-1))
+    _save("tiny_critic.npz", arrays, {"cliprange_value": 0.5, "loss_agg_mode": "token-mean", "loss_scale_factor": 0.5,
+                                      "hf": "transformers Qwen2ForTokenClassification fp32 eager attention",
+                                      "ref": "dp_critic.py:127-145, 218-245; core_algos.py:1230-1269"})
 
 
 if __name__ == "__main__":

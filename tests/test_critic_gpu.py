@@ -1,0 +1,220 @@
+"""Critic row: K6 value loss, value head, GAE over bf16 values, the tiny
+critic forward/backward, and a GAE PPO step end to end — on MI355X through the C-ABI.
+
+* K6 fused value loss vs the reference's compute_value_loss vectors (tests/golden/value_loss.npz: fp32 and
+  bf16 critic outputs, 4 agg modes, vpreds on the clip bounds) and vs the oracle restatement at size;
+* value head fwd/bwd vs a plain fp32 torch reference of the same Linear(H, 1);
+* GAE with bf16 values vs tests/golden/gae_bf16.npz;
+* the tiny Qwen2ForTokenClassification critic (tests/golden/tiny_critic.npz, fp32): values and the
+  gradients of the head / final norm / first layer norm after value loss + backward;
+* RayPPOTrainer step with adv_estimator=gae (critic worker, values, update_critic) on a tiny random model.
+"""
+
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+TINY = os.path.join(HERE, "golden", "tiny_qwen2")
+
+
+def T(a, dtype=None):
+    t = torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    return t.to(dtype) if dtype is not None else t
+
+
+def test_value_loss_matches_reference_golden(golden):
+    from dots.rl_amd import native
+
+    z, meta = golden("value_loss.npz")
+    for ci, cfg in enumerate(meta["cases"]):
+        bf = cfg["dtype"] == "bfloat16"
+        vdt = torch.bfloat16 if bf else torch.float32
+        out, dv = native.value_loss_fwd_bwd(T(z[f"c{ci}_vpreds"], vdt), T(z[f"c{ci}_values"], vdt),
+                                            T(z[f"c{ci}_returns"]), T(z[f"c{ci}_mask"]),
+                                            cliprange_value=cfg["cliprange_value"], loss_agg_mode=cfg["mode"],
+                                            loss_scale_factor=cfg["loss_scale_factor"])
+        o = out.cpu().numpy()
+        np.testing.assert_allclose(o[0], z[f"c{ci}_vf_loss"], rtol=3e-5, err_msg=str(cfg))
+        np.testing.assert_allclose(o[1], z[f"c{ci}_vf_clipfrac"], rtol=1e-6, atol=1e-7, err_msg=str(cfg))
+        np.testing.assert_allclose(o[2], z[f"c{ci}_vpred_mean"], rtol=2e-6, atol=1e-7, err_msg=str(cfg))
+        np.testing.assert_allclose(o[3], z[f"c{ci}_vf_loss"] * cfg["loss_scale_factor"], rtol=3e-5, err_msg=str(cfg))
+        # gradient: the oracle's analytic d/d vpreds (fp32, tight), and the reference's autograd vectors (bf16
+        # critics: the reference's vpreds gradient is a bf16 tensor, one rounding away)
+        want = oracle.value_loss(z[f"c{ci}_vpreds"], z[f"c{ci}_values"], z[f"c{ci}_returns"], z[f"c{ci}_mask"],
+                                 cfg["cliprange_value"], cfg["mode"], cfg["loss_scale_factor"], value_bf16=bf)[3]
+        got = dv.cpu().numpy()
+        np.testing.assert_allclose(got, want, rtol=2e-5, atol=1e-7 * np.abs(want).max(), err_msg=str(cfg))
+        ref = z[f"c{ci}_dvpreds"]
+        if bf:
+            np.testing.assert_allclose(got, ref, rtol=8e-3, atol=1e-3 * np.abs(ref).max(), err_msg=str(cfg))
+        else:
+            np.testing.assert_allclose(got, ref, rtol=2e-5, atol=1e-7 * np.abs(ref).max(), err_msg=str(cfg))
+
+
+@pytest.mark.parametrize("mode", ["token-mean", "seq-mean-token-mean"])
+def test_value_loss_at_size_matches_oracle(mode):
+    """B=512 R=256 (one PPO batch of config #2): forward scalars and the full gradient vs the oracle."""
+    from dots.rl_amd import native
+
+    rng = np.random.default_rng(3)
+    B, R = 512, 256
+    values = rng.standard_normal((B, R)).astype(np.float32)
+    vpreds = (values + rng.standard_normal((B, R)) * 0.7).astype(np.float32)
+    returns = (values + rng.standard_normal((B, R))).astype(np.float32)
+    mask = (np.arange(R)[None, :] < rng.integers(1, R + 1, (B, 1))).astype(np.int64)
+    out, dv = native.value_loss_fwd_bwd(T(vpreds), T(values), T(returns), T(mask), cliprange_value=0.5,
+                                        loss_agg_mode=mode, loss_scale_factor=0.125)
+    vf, cf, vm, want = oracle.value_loss(vpreds, values, returns, mask, 0.5, mode, 0.125)
+    o = out.cpu().numpy()
+    np.testing.assert_allclose(o[0], vf, rtol=1e-5)
+    np.testing.assert_allclose(o[1], cf, rtol=1e-5)
+    np.testing.assert_allclose(o[2], vm, rtol=1e-5, atol=1e-7)
+    np.testing.assert_allclose(dv.cpu().numpy(), want, rtol=2e-5, atol=1e-7 * np.abs(want).max())
+    # deterministic: fixed-order partials
+    out2, dv2 = native.value_loss_fwd_bwd(T(vpreds), T(values), T(returns), T(mask), cliprange_value=0.5,
+                                          loss_agg_mode=mode, loss_scale_factor=0.125)
+    assert torch.equal(out, out2) and torch.equal(dv, dv2)
+
+
+def test_compute_value_loss_api_is_differentiable(golden):
+    """core_algos.compute_value_loss (the reference's signature) -> (vf_loss, vf_clipfrac) with autograd."""
+    from dots.rl_amd import core_algos
+
+    z, meta = golden("value_loss.npz")
+    ci = 2
+    cfg = meta["cases"][ci]
+    vp = T(z[f"c{ci}_vpreds"]).requires_grad_(True)
+    vf, cf = core_algos.compute_value_loss(vp, T(z[f"c{ci}_returns"]), T(z[f"c{ci}_values"]), T(z[f"c{ci}_mask"]),
+                                           cfg["cliprange_value"], cfg["mode"])
+    (vf * cfg["loss_scale_factor"]).backward()
+    np.testing.assert_allclose(vf.item(), z[f"c{ci}_vf_loss"], rtol=3e-5)
+    np.testing.assert_allclose(cf.item(), z[f"c{ci}_vf_clipfrac"], rtol=1e-6)
+    ref = z[f"c{ci}_dvpreds"]
+    np.testing.assert_allclose(vp.grad.cpu().numpy(), ref, rtol=2e-5, atol=1e-7 * np.abs(ref).max())
+    with pytest.raises(ValueError):
+        core_algos.compute_value_loss(vp, T(z[f"c{ci}_returns"]), T(z[f"c{ci}_values"]), T(z[f"c{ci}_mask"]), 0.5, "bad")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("N,H", [(2048, 896), (77, 64), (1, 4096)])
+def test_value_head_matches_torch(dtype, N, H):
+    from dots.rl_amd import native
+
+    g = torch.Generator(device="cuda").manual_seed(N + H)
+    h = torch.randn(N, H, device="cuda", generator=g).to(dtype)
+    w = (torch.randn(1, H, device="cuda", generator=g) * 0.05).to(dtype)
+    b = torch.randn(1, device="cuda", generator=g).to(dtype)
+    v = native.value_head_fwd(h, w, b)
+    ref = h.float() @ w.float().t() + b.float()
+    tol = dict(rtol=1e-5, atol=1e-5) if dtype == torch.float32 else dict(rtol=8e-3, atol=8e-3)
+    assert v.dtype == dtype
+    torch.testing.assert_close(v.float(), ref.reshape(-1).to(dtype).float(), **tol)
+    dv = torch.randn(N, device="cuda", generator=g)
+    gw = torch.full((H,), 0.5, device="cuda")
+    gb = torch.full((1,), 0.25, device="cuda")
+    dh = native.value_head_bwd(h, w, dv, dweight=gw, dbias=gb)
+    torch.testing.assert_close(dh.float(), (dv[:, None] * w.float()).to(dtype).float(), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(gw, 0.5 + (dv[:, None] * h.float()).sum(0), rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(gb, 0.25 + dv.sum().reshape(1), rtol=1e-4, atol=1e-3)
+
+
+def test_gae_over_bf16_values_matches_reference_golden(golden):
+    from dots.rl_amd import native
+
+    z, meta = golden("gae_bf16.npz")
+    for ci, cfg in enumerate(meta["cases"]):
+        adv, ret = native.gae_advantage_return(T(z[f"c{ci}_rewards"]), T(z[f"c{ci}_values"], torch.bfloat16),
+                                               T(z[f"c{ci}_mask"]), cfg["gamma"], cfg["lam"])
+        np.testing.assert_allclose(adv.cpu().numpy(), z[f"c{ci}_adv"], rtol=1e-4, atol=1e-5)
+        np.testing.assert_allclose(ret.cpu().numpy(), z[f"c{ci}_ret"], rtol=1e-5, atol=1e-5)
+
+
+def _tiny_critic(dtype=torch.float32):
+    from safetensors.torch import load_file
+
+    from dots.rl_amd.qwen2 import ParamStore, Qwen2Config, Qwen2Model
+
+    cfg = Qwen2Config.from_dict(json.load(open(os.path.join(TINY, "config.json"))))
+    cfg.num_labels = 1
+    store = ParamStore(cfg, "cuda", compute_dtype=dtype, trainable=True)
+    sd = load_file(os.path.join(TINY, "model.safetensors"))
+    sd.update(load_file(os.path.join(TINY, "score.safetensors")))
+    store.load_state_dict_hf(sd)
+    return cfg, store, Qwen2Model(cfg, store)
+
+
+def test_tiny_critic_forward_backward_matches_reference(golden):
+    """values = score(h)[:, -R-1:-1] and, after 0.5 * compute_value_loss(...).backward(), the fp32 gradients of
+    score.weight / score.bias / model.norm / layers.0.input_layernorm vs the reference HF critic."""
+    from dots.rl_amd.config import to_attr
+    from dots.rl_amd.dp_critic import DataParallelPPOCritic, fused_value_loss
+
+    zr, _ = golden("tiny_qwen2_rollout.npz")
+    z, meta = golden("tiny_critic.npz")
+    cfg, store, model = _tiny_critic()
+    critic = DataParallelPPOCritic(to_attr({"model": {}}), model)
+    mb = {"input_ids": T(zr["sequences"]), "attention_mask": T(zr["attention_mask"]),
+          "position_ids": T(zr["position_ids"]), "responses": T(zr["responses"])}
+    with torch.no_grad():
+        v = critic._forward_micro_batch(mb)
+    np.testing.assert_allclose(v.cpu().numpy(), z["vpreds"], rtol=1e-4, atol=1e-5)
+    model.training = True
+    store.zero_grad()
+    R = zr["responses"].shape[1]
+    vp = critic._forward_micro_batch(mb)
+    out = fused_value_loss(vp, T(z["values"]), T(z["returns"]), T(zr["attention_mask"][:, -R:]),
+                           cliprange_value=meta["cliprange_value"], loss_agg_mode=meta["loss_agg_mode"],
+                           loss_scale_factor=meta["loss_scale_factor"])
+    out[3].backward()
+    np.testing.assert_allclose(out[0].item(), z["vf_loss"], rtol=1e-5)
+    np.testing.assert_allclose(out[1].item(), z["vf_clipfrac"], rtol=1e-6)
+    g = lambda n: store.g(n).detach().cpu().numpy()  # noqa: E731
+    for name, key in [("score.weight", "d_score_weight"), ("score.bias", "d_score_bias"), ("norm", "d_norm"),
+                      ("layers.0.input_layernorm", "d_input_layernorm0")]:
+        ref = z[key].reshape(g(name).shape)
+        np.testing.assert_allclose(g(name), ref, rtol=2e-4, atol=2e-4 * np.abs(ref).max(), err_msg=name)
+    emb = np.linalg.norm(g("embed_tokens"), axis=-1)
+    np.testing.assert_allclose(emb, z["d_embed_rows"], rtol=2e-4, atol=2e-4 * z["d_embed_rows"].max())
+
+
+def test_gae_ppo_step_end_to_end():
+    """RayPPOTrainer with adv_estimator=gae: critic values -> GAE on bf16 values -> update_critic -> update_actor,
+    on a tiny random Qwen2 (bf16). Metrics carry the reference's critic keys and are finite; the critic moves."""
+    from dots.rl_amd.config import apply_overrides, default_config
+    from dots.rl_amd.trainer import RayPPOTrainer
+
+    tiny = ("{'hidden_size': 128, 'intermediate_size': 256, 'num_hidden_layers': 2, 'num_attention_heads': 2, "
+            "'num_key_value_heads': 1, 'vocab_size': 1024}")
+    cfg = apply_overrides(default_config(), [
+        "data.train_batch_size=4", "data.max_prompt_length=32", "data.max_response_length=16",
+        "actor_rollout_ref.rollout.n=2", "actor_rollout_ref.rollout.response_length=16",
+        "actor_rollout_ref.rollout.prompt_length=32", "actor_rollout_ref.actor.ppo_mini_batch_size=2",
+        "actor_rollout_ref.actor.ppo_micro_batch_size_per_gpu=2", "actor_rollout_ref.rollout.log_prob_micro_batch_size_per_gpu=4",
+        "actor_rollout_ref.ref.log_prob_micro_batch_size_per_gpu=4", "critic.ppo_micro_batch_size_per_gpu=2",
+        "critic.forward_micro_batch_size_per_gpu=4", "algorithm.adv_estimator=gae", "algorithm.gamma=0.99",
+        "algorithm.lam=0.95", "actor_rollout_ref.actor.use_kl_loss=False", "algorithm.use_kl_in_reward=True",
+        f"actor_rollout_ref.model.override_config={tiny}", f"critic.model.override_config={tiny}",
+    ])
+    trainer = RayPPOTrainer(cfg)
+    trainer.train_dataloader.vocab_limit = 1000
+    trainer.init_workers()
+    assert trainer.use_critic
+    w0 = trainer.critic_wg.worker.store.master.clone() if hasattr(trainer.critic_wg, "worker") else None
+    m = trainer.fit(num_steps=2)[-1]
+    for k in ["critic/vf_loss", "critic/vf_clipfrac", "critic/vpred_mean", "critic/grad_norm", "critic/lr",
+              "critic/values/mean", "critic/vf_explained_var", "actor/pg_loss", "actor/reward_kl_penalty",
+              "timing_s/values", "timing_s/update_critic"]:
+        assert k in m, k
+        assert np.isfinite(m[k]), (k, m[k])
+    b = trainer.last_batch.batch
+    assert b["values"].dtype == torch.bfloat16
+    assert torch.isfinite(b["advantages"]).all() and torch.isfinite(b["returns"]).all()
+    if w0 is not None:
+        assert not torch.equal(w0, trainer.critic_wg.worker.store.master)

@@ -61,6 +61,36 @@ def test_gae_matches_reference(golden):
         np.testing.assert_allclose(ret, z[f"c{ci}_ret"], rtol=1e-5, atol=1e-5)
 
 
+def test_gae_bf16_values_matches_reference(golden):
+    """GAE over bf16 critic values: the reference rounds gamma * V(t+1) to bf16 (bf16 tensor arithmetic)."""
+    z, meta = golden("gae_bf16.npz")
+    for ci, cfg in enumerate(meta["cases"]):
+        adv, ret = oracle.gae_advantage_return(z[f"c{ci}_rewards"], z[f"c{ci}_values"], z[f"c{ci}_mask"],
+                                               cfg["gamma"], cfg["lam"], values_bf16=True)
+        np.testing.assert_allclose(adv, z[f"c{ci}_adv"], rtol=1e-4, atol=1e-5)
+        np.testing.assert_allclose(ret, z[f"c{ci}_ret"], rtol=1e-5, atol=1e-5)
+
+
+def test_value_loss_matches_reference(golden):
+    """compute_value_loss (core_algos.py:1230-1269) fwd + d/d vpreds, fp32 and bf16 critic outputs, 4 agg modes,
+    vpreds on the clip bounds. bf16: the reference's vpreds gradient is itself a bf16 tensor (one rounding)."""
+    z, meta = golden("value_loss.npz")
+    assert len(meta["cases"]) == 16
+    for ci, cfg in enumerate(meta["cases"]):
+        bf = cfg["dtype"] == "bfloat16"
+        vf, cf, vm, dv = oracle.value_loss(z[f"c{ci}_vpreds"], z[f"c{ci}_values"], z[f"c{ci}_returns"], z[f"c{ci}_mask"],
+                                           cfg["cliprange_value"], cfg["mode"], cfg["loss_scale_factor"], value_bf16=bf)
+        np.testing.assert_allclose(vf, z[f"c{ci}_vf_loss"], rtol=3e-5, err_msg=str(cfg))  # fp32 sum order
+        np.testing.assert_allclose(cf, z[f"c{ci}_vf_clipfrac"], rtol=1e-6, atol=1e-7, err_msg=str(cfg))
+        np.testing.assert_allclose(vm, z[f"c{ci}_vpred_mean"], rtol=1e-5, atol=1e-6, err_msg=str(cfg))
+        ref = z[f"c{ci}_dvpreds"]
+        if bf:
+            dv = oracle.bf16_round(dv)
+            np.testing.assert_allclose(dv, ref, rtol=8e-3, atol=1e-3 * np.abs(ref).max(), err_msg=str(cfg))
+        else:
+            np.testing.assert_allclose(dv, ref, rtol=2e-5, atol=1e-7 * np.abs(ref).max(), err_msg=str(cfg))
+
+
 def regen_logits(case):
     rng = np.random.default_rng(case["seed"])
     x = (rng.standard_normal((case["N"], case["V"]), dtype=np.float32) * np.float32(case["scale"])).astype(np.float32)
