@@ -30,10 +30,13 @@ from .workers import ActorRolloutRefWorker, CriticWorker
 @contextmanager
 def marked_timer(name: str, timing_raw: dict):
     """profiler/performance.py:172 — wall time of a stage (synchronised: stages run on the GPU stream)."""
-    torch.cuda.synchronize()
+    sync = torch.cuda.is_initialized()  # host-only callers (CPU tests of the driver logic) have no stream
+    if sync:
+        torch.cuda.synchronize()
     t0 = time.perf_counter()
     yield
-    torch.cuda.synchronize()
+    if sync:
+        torch.cuda.synchronize()
     timing_raw[name] = timing_raw.get(name, 0.0) + time.perf_counter() - t0
 
 
@@ -138,8 +141,10 @@ class RayPPOTrainer:
         self.actor_rollout_wg.init_model()
 
     def _uids(self, n):
-        # deterministic per step (uuid4 in the reference; only group identity matters)
-        return np.array([str(uuid.UUID(int=(self.global_steps << 32) + i)) for i in range(n)], dtype=object)
+        # deterministic and unique across generation batches (uuid4 in the reference; only group identity matters)
+        base = getattr(self, "_uid_next", 0)
+        self._uid_next = base + n
+        return np.array([str(uuid.UUID(int=(self.global_steps << 40) + base + i)) for i in range(n)], dtype=object)
 
     def _balance_batch(self, batch: DataProto, metrics):
         """ray_trainer.py:1033-1048 (greedy sequence-length balancing across DP ranks)."""
@@ -157,61 +162,73 @@ class RayPPOTrainer:
         idx = torch.tensor([i for b in buckets for i in sorted(b)], device=am.device)
         batch.reorder(idx)
 
-    def step(self, batch_dict: dict) -> dict:
-        """One PPO step — ray_trainer.py:1104-1399 minus validation/checkpoint/logging."""
-        cfg = self.config
-        ar = cfg.actor_rollout_ref
-        metrics, timing_raw = {}, {}
+    def _rollout(self, batch_dict: dict, timing_raw: dict) -> DataProto:
+        """ray_trainer.py:1104-1170: uid per prompt, repeat(n, interleave), generate_sequences, union."""
+        ar = self.config.actor_rollout_ref
         batch = DataProto.from_single_dict(batch_dict)
         batch.non_tensor_batch["uid"] = self._uids(len(batch))
         gen_batch = batch.pop(batch_keys=["input_ids", "attention_mask", "position_ids"])
         gen_batch.meta_info.update({"global_steps": self.global_steps, "eos_token_id": self.eos_token_id,
                                     "pad_token_id": self.pad_token_id})
         gen_batch = gen_batch.repeat(repeat_times=ar.rollout.n, interleave=True)
-        with marked_timer("step", timing_raw):
-            with marked_timer("gen", timing_raw):
-                gen_out = self.actor_rollout_wg.generate_sequences(gen_batch)
-                timing_raw.update(gen_out.meta_info.pop("timing", {}))
-            batch = batch.repeat(repeat_times=ar.rollout.n, interleave=True)
-            batch = batch.union(gen_out)
-            if "response_mask" not in batch.batch:
-                batch.batch["response_mask"] = compute_response_mask(batch)
-            if cfg.trainer.balance_batch and self.n_gpus > 1:
-                self._balance_batch(batch, metrics)
-            batch.meta_info["global_token_num"] = batch.batch["attention_mask"].sum(-1).tolist()
+        with marked_timer("gen", timing_raw):
+            gen_out = self.actor_rollout_wg.generate_sequences(gen_batch)
+            for k, v in gen_out.meta_info.pop("timing", {}).items():
+                timing_raw[k] = timing_raw.get(k, 0.0) + v
+        batch = batch.repeat(repeat_times=ar.rollout.n, interleave=True)
+        return batch.union(gen_out)
+
+    def _train_on(self, batch: DataProto, metrics: dict, timing_raw: dict) -> DataProto:
+        """ray_trainer.py:1171-1375: response mask, balance, reward (unless the caller already scored the batch),
+        old log-prob + entropy, ref log-prob, values, advantage, update_critic, update_actor."""
+        cfg = self.config
+        ar = cfg.actor_rollout_ref
+        if "response_mask" not in batch.batch:
+            batch.batch["response_mask"] = compute_response_mask(batch)
+        if cfg.trainer.balance_batch and self.n_gpus > 1:
+            self._balance_batch(batch, metrics)
+        batch.meta_info["global_token_num"] = batch.batch["attention_mask"].sum(-1).tolist()
+        reward_tensor = None
+        if "token_level_scores" not in batch.batch:
             with marked_timer("reward", timing_raw):
                 reward_tensor, _ = compute_reward(batch, self.reward_fn)
-            with marked_timer("old_log_prob", timing_raw):
-                old = self.actor_rollout_wg.compute_log_prob(batch)
-                ent = agg_loss(old.batch["entropys"], batch.batch["response_mask"], ar.actor.loss_agg_mode)
-                metrics["actor/entropy"] = ent
-                old.batch.pop("entropys")
-                batch = batch.union(old)
-            if self.use_reference_policy:
-                with marked_timer("ref", timing_raw):
-                    batch = batch.union(self.ref_policy_wg.compute_ref_log_prob(batch))
-            if self.use_critic:
-                with marked_timer("values", timing_raw):
-                    batch = batch.union(self.critic_wg.compute_values(batch))
-            with marked_timer("adv", timing_raw):
+        with marked_timer("old_log_prob", timing_raw):
+            old = self.actor_rollout_wg.compute_log_prob(batch)
+            ent = agg_loss(old.batch["entropys"], batch.batch["response_mask"], ar.actor.loss_agg_mode)
+            metrics["actor/entropy"] = ent
+            old.batch.pop("entropys")
+            batch = batch.union(old)
+        if self.use_reference_policy:
+            with marked_timer("ref", timing_raw):
+                batch = batch.union(self.ref_policy_wg.compute_ref_log_prob(batch))
+        if self.use_critic:
+            with marked_timer("values", timing_raw):
+                batch = batch.union(self.critic_wg.compute_values(batch))
+        with marked_timer("adv", timing_raw):
+            if reward_tensor is not None:
                 batch.batch["token_level_scores"] = reward_tensor
+            if "token_level_rewards" not in batch.batch:
                 if cfg.algorithm.use_kl_in_reward:
                     batch, klm = apply_kl_penalty(batch, self.kl_ctrl_in_reward, cfg.algorithm.kl_penalty)
                     metrics.update(klm)
                 else:
                     batch.batch["token_level_rewards"] = batch.batch["token_level_scores"]
-                batch = compute_advantage(batch, cfg.algorithm.adv_estimator, cfg.algorithm.gamma, cfg.algorithm.lam,
-                                          ar.rollout.n, cfg.algorithm.norm_adv_by_std_in_grpo, cfg.algorithm)
-            if self.use_critic:
-                with marked_timer("update_critic", timing_raw):
-                    critic_out = self.critic_wg.update_critic(batch)
-                metrics.update(reduce_metrics(critic_out.meta_info["metrics"]))
-            if cfg.trainer.critic_warmup <= self.global_steps:
-                with marked_timer("update_actor", timing_raw):
-                    batch.meta_info["multi_turn"] = False
-                    batch.meta_info["temperature"] = ar.rollout.temperature
-                    actor_out = self.actor_rollout_wg.update_actor(batch)
-                metrics.update(reduce_metrics(actor_out.meta_info["metrics"]))
+            batch = compute_advantage(batch, cfg.algorithm.adv_estimator, cfg.algorithm.gamma, cfg.algorithm.lam,
+                                      ar.rollout.n, cfg.algorithm.norm_adv_by_std_in_grpo, cfg.algorithm)
+        if self.use_critic:
+            with marked_timer("update_critic", timing_raw):
+                critic_out = self.critic_wg.update_critic(batch)
+            metrics.update(reduce_metrics(critic_out.meta_info["metrics"]))
+        if cfg.trainer.critic_warmup <= self.global_steps:
+            with marked_timer("update_actor", timing_raw):
+                batch.meta_info["multi_turn"] = False
+                batch.meta_info["temperature"] = ar.rollout.temperature
+                actor_out = self.actor_rollout_wg.update_actor(batch)
+            metrics.update(reduce_metrics(actor_out.meta_info["metrics"]))
+        return batch
+
+    def _finish_metrics(self, batch: DataProto, metrics: dict, timing_raw: dict) -> dict:
+        """ray_trainer.py:1377-1399."""
         metrics["actor/entropy"] = float(metrics["actor/entropy"])
         metrics.update({"training/global_step": self.global_steps})
         metrics.update(compute_data_metrics(batch, use_critic=self.use_critic))
@@ -221,6 +238,14 @@ class RayPPOTrainer:
         metrics["perf/rollout_tokens_per_sec"] = n_resp / timing_raw["gen"]
         self.last_batch = batch
         return metrics
+
+    def step(self, batch_dict: dict) -> dict:
+        """One PPO step — ray_trainer.py:1104-1399 minus validation/checkpoint/logging."""
+        metrics, timing_raw = {}, {}
+        with marked_timer("step", timing_raw):
+            batch = self._rollout(batch_dict, timing_raw)
+            batch = self._train_on(batch, metrics, timing_raw)
+        return self._finish_metrics(batch, metrics, timing_raw)
 
     def fit(self, num_steps=None):
         """ray_trainer.py:1050-1405 training loop (synthetic data; no validation/checkpoint by default)."""

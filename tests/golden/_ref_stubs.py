@@ -33,6 +33,13 @@ def install():
         def keys(self):
             return list(super().keys())
 
+        def __getitem__(self, key):  # str -> tensor; int / slice / index -> the rows (DataProtoItem access)
+            if isinstance(key, str):
+                return super().__getitem__(key)
+            rows = {k: v[key] for k, v in self.items()}
+            n = next(iter(rows.values())).shape[:1] if rows and not isinstance(key, int) else []
+            return TensorDict(rows, batch_size=list(n))
+
     td.TensorDict = TensorDict
     sys.modules["tensordict"] = td
 

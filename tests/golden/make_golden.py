@@ -18,6 +18,7 @@ Reference call sites (file:line under /root/reference):
 * critic value loss + backward : verl/trainer/ppo/core_algos.py:1230-1269 as dp_critic.py:218-245 scales it
 * critic forward/backward (tiny Qwen2ForTokenClassification, the model fsdp_workers.py:1003-1060 builds) :
   verl/workers/critic/dp_critic.py:57-145 values slice, compute_value_loss, loss.backward()
+* DAPO overlong-buffer reward : verl/workers/reward_manager/dapo.py:60-150 (stub tokenizer / preset scores)
 * masked_mean known answers : tests/utils/test_torch_functional.py:55-66 (reference test, reproduced as data)
 """
 
@@ -524,6 +525,45 @@ def gen_tiny_critic():
     _save("tiny_critic.npz", arrays, {"cliprange_value": 0.5, "loss_agg_mode": "token-mean", "loss_scale_factor": 0.5,
                                       "hf": "transformers Qwen2ForTokenClassification fp32 eager attention",
                                       "ref": "dp_critic.py:127-145, 218-245; core_algos.py:1230-1269"})
+
+
+# --------------------------------------------------------------------------------------------
+# DAPO overlong-buffer reward (reward_manager/dapo.py:60-150) with a stub tokenizer / scorer
+# --------------------------------------------------------------------------------------------
+def gen_dapo_reward():
+    from verl import DataProto as RefDataProto
+    from verl.workers.reward_manager.dapo import DAPORewardManager
+
+    class Tok:
+        eos_token = "</s>"
+
+        def decode(self, ids, skip_special_tokens=True):
+            return ",".join(str(int(i)) for i in ids)
+
+    g = torch.Generator().manual_seed(9)
+    arrays, cases = {}, []
+    for ci, (B, P, R, blen, factor) in enumerate([(6, 4, 12, 4, 1.5), (16, 8, 64, 16, 1.0)]):
+        prompts = torch.randint(3, 100, (B, P), generator=g)
+        resp = torch.randint(3, 100, (B, R), generator=g)
+        lens = torch.randint(0, R + 1, (B,), generator=g)
+        lens[0], lens[1] = R, 0
+        am = torch.ones(B, P + R, dtype=torch.int64)
+        for i in range(B):
+            am[i, P + int(lens[i]):] = 0
+        acc = (torch.rand(B, generator=g) > 0.5).float()
+        table = {",".join(str(int(t)) for t in resp[i, : int(lens[i])]): float(acc[i]) for i in range(B)}
+        ob = DictConfig(enable=True, len=blen, penalty_factor=factor, log=True)
+        rm = DAPORewardManager(Tok(), num_examine=0, compute_score=lambda data_source, solution_str, ground_truth,
+                               extra_info=None: table[solution_str], max_resp_len=R, overlong_buffer_cfg=ob)
+        dp = RefDataProto.from_dict(tensors={"prompts": prompts, "responses": resp, "attention_mask": am},
+                                    non_tensors={"reward_model": np.array([{"ground_truth": ""}] * B, dtype=object),
+                                                 "data_source": np.array(["synthetic"] * B, dtype=object)})
+        out = rm(dp, return_dict=True)
+        over = np.array([float(x) for x in out["reward_extra_info"]["overlong_reward"]], np.float32)
+        arrays.update({f"c{ci}_responses": resp, f"c{ci}_attention_mask": am, f"c{ci}_acc": acc,
+                       f"c{ci}_reward_tensor": out["reward_tensor"], f"c{ci}_overlong_reward": over})
+        cases.append({"max_resp_len": R, "overlong_len": blen, "penalty_factor": factor})
+    _save("dapo_reward.npz", arrays, {"cases": cases, "ref": "reward_manager/dapo.py:60-150"})
 
 
 if __name__ == "__main__":

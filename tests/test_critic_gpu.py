@@ -218,3 +218,32 @@ def test_gae_ppo_step_end_to_end():
     assert torch.isfinite(b["advantages"]).all() and torch.isfinite(b["returns"]).all()
     if w0 is not None:
         assert not torch.equal(w0, trainer.critic_wg.worker.store.master)
+
+
+def test_dapo_step_end_to_end():
+    """RayDAPOTrainer (config #5 recipe: clip 0.2/0.28, clip_ratio_c 10, token-mean, overlong buffer, dynamic
+    sampling) on a tiny random Qwen2: the filtered batch is exactly train_batch_size * n, metrics finite."""
+    from dots.rl_amd.config import apply_overrides, default_config
+    from dots.rl_amd.dapo_trainer import RayDAPOTrainer, dapo_overrides
+
+    tiny = ("{'hidden_size': 128, 'intermediate_size': 256, 'num_hidden_layers': 2, 'num_attention_heads': 2, "
+            "'num_key_value_heads': 1, 'vocab_size': 1024}")
+    cfg = apply_overrides(default_config(), dapo_overrides(16, overlong_len=4) + [
+        "data.train_batch_size=4", "data.max_prompt_length=32", "data.max_response_length=16",
+        "actor_rollout_ref.rollout.n=4", "actor_rollout_ref.rollout.response_length=16",
+        "actor_rollout_ref.rollout.prompt_length=32", "actor_rollout_ref.actor.ppo_mini_batch_size=2",
+        "actor_rollout_ref.actor.ppo_micro_batch_size_per_gpu=4",
+        "actor_rollout_ref.rollout.log_prob_micro_batch_size_per_gpu=8", f"actor_rollout_ref.model.override_config={tiny}",
+    ])
+    trainer = RayDAPOTrainer(cfg)
+    trainer.train_dataloader.vocab_limit = 1000
+    trainer.init_workers()
+    m = trainer.fit(num_steps=2)[-1]
+    b = trainer.last_batch
+    assert len(b) == 4 * 4
+    assert m["train/num_gen_batches"] >= 1
+    for k in ["actor/pg_loss", "actor/pg_clipfrac", "actor/grad_norm", "critic/score/mean", "response_length/mean"]:
+        assert np.isfinite(m[k]), k
+    # responses never hit EOS (tiny vocab) -> length 16 = max: overlong penalty -(16 - 12) / 4 * 1.0 = -1
+    np.testing.assert_allclose(b.batch["token_level_scores"].sum(-1).cpu().numpy(),
+                               b.non_tensor_batch["acc"] - 1.0, atol=1e-6)
