@@ -43,6 +43,20 @@ QWEN25_05B = dict(
     tie_word_embeddings=True, bos_token_id=151643, eos_token_id=151645, pad_token_id=151643,
 )
 
+# config #4 / #5 architectures (config.json of meta-llama/Meta-Llama-3-8B and Qwen/Qwen2.5-7B), random init
+LLAMA3_8B = dict(
+    vocab_size=128256, hidden_size=4096, intermediate_size=14336, num_hidden_layers=32, num_attention_heads=32,
+    num_key_value_heads=8, max_position_embeddings=8192, rope_theta=500000.0, rms_norm_eps=1e-5,
+    tie_word_embeddings=False, attention_bias=False, bos_token_id=128000, eos_token_id=128001, pad_token_id=128001,
+    model_type="llama",
+)
+QWEN25_7B = dict(
+    vocab_size=152064, hidden_size=3584, intermediate_size=18944, num_hidden_layers=28, num_attention_heads=28,
+    num_key_value_heads=4, max_position_embeddings=32768, rope_theta=1000000.0, rms_norm_eps=1e-6,
+    tie_word_embeddings=False, bos_token_id=151643, eos_token_id=151643, pad_token_id=151643,
+)
+RANDOM_MODELS = {"qwen2.5-0.5b": QWEN25_05B, "llama-3-8b": LLAMA3_8B, "qwen2.5-7b": QWEN25_7B}
+
 DEFAULTS = dict(
     data=dict(train_batch_size=64, max_prompt_length=512, max_response_length=256, seed=1234),
     actor_rollout_ref=dict(

@@ -50,6 +50,11 @@ class Qwen2Config:
     # > 0: token-classification head `score` Linear(H, num_labels, bias=True) instead of the lm_head (the
     # critic the reference loads with AutoModelForTokenClassification, num_labels=1, fsdp_workers.py:1045)
     num_labels: int = 0
+    # False: Llama-family attention (no q/k/v bias; LlamaForCausalLM, config #4's Llama-3-8B). The kernels are
+    # shared: the qkv GEMM epilogues read a constant zero bias instead of a parameter.
+    attention_bias: bool = True
+    rope_scaling: dict | None = None
+    model_type: str = "qwen2"
     extra: dict = field(default_factory=dict)
 
     @property
@@ -72,7 +77,10 @@ def param_specs(cfg: Qwen2Config):
         specs += [
             (p + "input_layernorm", (H,), "small"),
             (p + "qkv_proj.weight", (qkv, H), "gemm"),
-            (p + "qkv_proj.bias", (qkv,), "gemm"),  # GEMM epilogue operand: read in the compute dtype
+        ]
+        if cfg.attention_bias:
+            specs.append((p + "qkv_proj.bias", (qkv,), "gemm"))  # GEMM epilogue operand: read in the compute dtype
+        specs += [
             (p + "o_proj", (H, cfg.num_attention_heads * hd), "gemm"),
             (p + "post_attention_layernorm", (H,), "small"),
             (p + "gate_up_proj", (2 * I, H), "gemm"),
@@ -155,7 +163,8 @@ class ParamStore:
             p, q = f"model.layers.{i}.", f"layers.{i}."
             put(q + "input_layernorm", sd[p + "input_layernorm.weight"])
             put(q + "qkv_proj.weight", torch.cat([sd[p + f"self_attn.{x}_proj.weight"] for x in "qkv"], 0))
-            put(q + "qkv_proj.bias", torch.cat([sd[p + f"self_attn.{x}_proj.bias"] for x in "qkv"], 0))
+            if cfg.attention_bias:
+                put(q + "qkv_proj.bias", torch.cat([sd[p + f"self_attn.{x}_proj.bias"] for x in "qkv"], 0))
             put(q + "o_proj", sd[p + "self_attn.o_proj.weight"])
             put(q + "post_attention_layernorm", sd[p + "post_attention_layernorm.weight"])
             put(q + "gate_up_proj", torch.cat([sd[p + "mlp.gate_proj.weight"], sd[p + "mlp.up_proj.weight"]], 0))
@@ -248,7 +257,7 @@ def _layer_forward(m, i, x_prev, delta, pos, key_valid, save, cache=None, koff=0
     rstd1 = torch.empty(B * T, dtype=torch.float32, device=dev) if save is not None else None
     native.add_rmsnorm_fwd(x_prev, delta, x if delta is not None else None, s.w(p + "input_layernorm"), h1, rstd1,
                            cfg.rms_norm_eps)
-    qkv = torch.addmm(s.w(p + "qkv_proj.bias"), h1.view(B * T, H), s.w(p + "qkv_proj.weight").t())
+    qkv = torch.addmm(m.qkv_bias(i), h1.view(B * T, H), s.w(p + "qkv_proj.weight").t())
     qkv = qkv.view(B, T, -1)
     q = torch.empty(B, Hkv, G, T, D, dtype=dt, device=dev)
     # bf16 full-sequence passes run the fused MFMA attention (csrc/flash_attn.hip): log-probs and prefill
@@ -398,7 +407,8 @@ class _DecoderLayer(torch.autograd.Function):
         dqkv2 = dqkv.view(N, -1)
         dh1 = dqkv2 @ s.w(p + "qkv_proj.weight")
         acc_wgrad(s.g(p + "qkv_proj.weight"), dqkv2, sv["h1"].view(N, H))
-        s.g(p + "qkv_proj.bias").add_(dqkv2.sum(0, dtype=torch.float32))
+        if m.cfg.attention_bias:
+            s.g(p + "qkv_proj.bias").add_(dqkv2.sum(0, dtype=torch.float32))
         dx = dx2  # residual: x2 = x + o
         native.rmsnorm_bwd(sv["x"], s.w(p + "input_layernorm"), sv["rstd1"], dh1, dx, s.g(p + "input_layernorm"))
         ctx.save = None
@@ -474,6 +484,15 @@ class Qwen2Model:
         self._dummy = torch.empty(0, device=dev, requires_grad=True)
         # called with layer index i at the end of layer i's backward (FlatAdamW's overlapped all-reduce)
         self.grad_ready_hook = None
+        if cfg.rope_scaling:
+            raise NotImplementedError(f"rope_scaling {cfg.rope_scaling} (plain RoPE only: Qwen2 / Llama-3-8B)")
+        self._zero_bias = None
+        if not cfg.attention_bias:  # Llama: the shared qkv epilogues add a constant zero bias
+            nq = (cfg.num_attention_heads + 2 * cfg.num_key_value_heads) * cfg.head_dim
+            self._zero_bias = torch.zeros(nq, dtype=self.dtype, device=dev)
+
+    def qkv_bias(self, i):
+        return self.store.w(f"layers.{i}.qkv_proj.bias") if self.cfg.attention_bias else self._zero_bias
 
     def _gw(self, name):
         return self.store.g(name) if (self.training and self.store.trainable) else None
@@ -638,7 +657,7 @@ class PackedDecode:
         for i in range(cfg.num_hidden_layers):
             p, w = f"layers.{i}.", self.w[i]
             native.decode_rmsnorm(self.x, prev, self.x, s.w(p + "input_layernorm"), self.h_p, eps, mbt=mbt)
-            native.decode_qkv_rope(self.h_p, w["qkv"], s.w(p + "qkv_proj.bias"), pos, m.cos, m.sin, B, H, Hq, Hkv, D,
+            native.decode_qkv_rope(self.h_p, w["qkv"], m.qkv_bias(i), pos, m.cos, m.sin, B, H, Hq, Hkv, D,
                                    self.q, cache.k[i], cache.vt[i], kpos_dev)
             native.decode_attention_vt(self.q, cache.k[i], cache.vt[i], cache.valid, Lk, self.attn_p,
                                        qpos_dev=kpos_dev, out_mbt=mbt)

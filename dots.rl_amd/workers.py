@@ -18,7 +18,7 @@ import time
 import torch
 import torch.distributed as dist
 
-from .config import QWEN25_05B
+from .config import RANDOM_MODELS
 from .dp_actor import DataParallelPPOActor, FlatAdamW
 from .dp_critic import DataParallelPPOCritic
 from .protocol import DataProto
@@ -32,8 +32,8 @@ MI355X_BF16_DENSE_PEAK = 2.5e15  # FLOP/s (MI355X_MICROARCH.md; AMD's 5 PF figur
 def resolve_model_config(model_cfg) -> Qwen2Config:
     path = model_cfg.get("path", "random:qwen2.5-0.5b")
     over = dict(model_cfg.get("override_config", {}) or {})
-    if path.startswith("random:"):
-        base = dict(QWEN25_05B)
+    if path.startswith("random:"):  # "random:<preset>" (config.RANDOM_MODELS), default Qwen2.5-0.5B
+        base = dict(RANDOM_MODELS.get(path[len("random:"):] or "qwen2.5-0.5b", RANDOM_MODELS["qwen2.5-0.5b"]))
     else:
         import json
 

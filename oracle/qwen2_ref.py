@@ -34,7 +34,8 @@ def load_hf_state_dict(cfg, sd, device="cpu"):
         p, q = f"model.layers.{i}.", f"layers.{i}."
         P[q + "input_layernorm"] = sd[p + "input_layernorm.weight"]
         P[q + "qkv_proj.weight"] = torch.cat([sd[p + f"self_attn.{x}_proj.weight"] for x in "qkv"], 0)
-        P[q + "qkv_proj.bias"] = torch.cat([sd[p + f"self_attn.{x}_proj.bias"] for x in "qkv"], 0)
+        if getattr(cfg, "attention_bias", True):  # Llama (LlamaForCausalLM): no q/k/v bias
+            P[q + "qkv_proj.bias"] = torch.cat([sd[p + f"self_attn.{x}_proj.bias"] for x in "qkv"], 0)
         P[q + "o_proj"] = sd[p + "self_attn.o_proj.weight"]
         P[q + "post_attention_layernorm"] = sd[p + "post_attention_layernorm.weight"]
         P[q + "gate_up_proj"] = torch.cat([sd[p + "mlp.gate_proj.weight"], sd[p + "mlp.up_proj.weight"]], 0)
@@ -59,7 +60,8 @@ def init_params(cfg, seed=0, device="cpu"):
         q = f"layers.{i}."
         P[q + "input_layernorm"] = torch.ones(H, device=device)
         P[q + "qkv_proj.weight"] = n(qkv, H)
-        P[q + "qkv_proj.bias"] = torch.zeros(qkv, device=device)
+        if getattr(cfg, "attention_bias", True):
+            P[q + "qkv_proj.bias"] = torch.zeros(qkv, device=device)
         P[q + "o_proj"] = n(H, cfg.num_attention_heads * D)
         P[q + "post_attention_layernorm"] = torch.ones(H, device=device)
         P[q + "gate_up_proj"] = n(2 * I, H)
@@ -96,7 +98,9 @@ def _layers(cfg, P, x, pos, allowed, cache=None, koff=0):
     for i in range(cfg.num_hidden_layers):
         p = f"layers.{i}."
         h = _rms(cfg, x, P[p + "input_layernorm"])
-        qkv = h @ P[p + "qkv_proj.weight"].t() + P[p + "qkv_proj.bias"]
+        qkv = h @ P[p + "qkv_proj.weight"].t()
+        if p + "qkv_proj.bias" in P:
+            qkv = qkv + P[p + "qkv_proj.bias"]
         q, k, v = qkv.split([Hq * D, Hkv * D, Hkv * D], -1)
         q = _rope(q.view(B, T, Hq, D).transpose(1, 2), cos, sin)
         k = _rope(k.view(B, T, Hkv, D).transpose(1, 2), cos, sin)

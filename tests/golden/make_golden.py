@@ -566,6 +566,66 @@ def gen_dapo_reward():
     _save("dapo_reward.npz", arrays, {"cases": cases, "ref": "reward_manager/dapo.py:60-150"})
 
 
+# --------------------------------------------------------------------------------------------
+# Llama family (config #4's Llama-3-8B architecture: no q/k/v bias, untied lm_head, head_dim 128,
+# rope_theta 5e5): tiny LlamaForCausalLM greedy rollout + teacher-forced log-probs (fp32, eager)
+# --------------------------------------------------------------------------------------------
+TINY_LLAMA = dict(vocab_size=512, hidden_size=256, intermediate_size=256, num_hidden_layers=2, num_attention_heads=2,
+                  num_key_value_heads=1, max_position_embeddings=256, rope_theta=500000.0, rms_norm_eps=1e-5,
+                  tie_word_embeddings=False, initializer_range=0.1, bos_token_id=1, eos_token_id=2, pad_token_id=0,
+                  attention_bias=False, mlp_bias=False, model_type="llama")
+
+
+def gen_tiny_llama():
+    from safetensors.torch import save_file
+    from transformers import GenerationConfig, LlamaConfig, LlamaForCausalLM
+
+    torch.manual_seed(1)
+    kw = {k: v for k, v in TINY_LLAMA.items() if k != "model_type"}
+    cfg = LlamaConfig(**kw, attn_implementation="eager")
+    model = LlamaForCausalLM(cfg).float().eval()
+    with torch.no_grad():
+        for n, p in model.named_parameters():
+            if "norm" in n:
+                p.copy_(1.0 + 0.1 * torch.randn_like(p))
+    outdir = os.path.join(HERE, "tiny_llama")
+    os.makedirs(outdir, exist_ok=True)
+    save_file({k: v.contiguous() for k, v in model.state_dict().items()}, os.path.join(outdir, "model.safetensors"))
+    with open(os.path.join(outdir, "config.json"), "w") as f:
+        json.dump(TINY_LLAMA, f, indent=1)
+    B, P, R = 4, 10, 8
+    g = torch.Generator().manual_seed(43)
+    ids = torch.randint(3, 512, (B, P), generator=g)
+    am = torch.ones(B, P, dtype=torch.int64)
+    for i, npad in enumerate([0, 2, 0, 4]):
+        am[i, :npad] = 0
+        ids[i, :npad] = TINY_LLAMA["pad_token_id"]
+    pos = compute_position_id_with_mask(am)
+    gc = GenerationConfig(do_sample=False, num_beams=1)
+    with torch.no_grad():
+        out = model.generate(input_ids=ids, attention_mask=am, do_sample=False, max_new_tokens=R, eos_token_id=[2],
+                             pad_token_id=0, generation_config=gc, output_scores=True, return_dict_in_generate=True,
+                             use_cache=True)
+    seq = out.sequences
+    if seq.shape[1] < P + R:
+        seq = torch.cat([seq, torch.zeros(B, P + R - seq.shape[1], dtype=seq.dtype)], 1)
+    gap = min(float((v[:, 0] - v[:, 1]).min()) for v in (torch.topk(s_, 2, dim=-1).values for s_ in out.scores))
+    resp = seq[:, P:]
+    full_pos = torch.cat([pos, pos[:, -1:] + torch.arange(1, R + 1).unsqueeze(0).repeat(B, 1)], -1)
+    resp_mask = vF.get_response_mask(resp, eos_token=2, dtype=am.dtype)
+    full_am = torch.cat([am, resp_mask], -1)
+    with torch.no_grad():
+        logits = model(input_ids=seq, attention_mask=full_am, position_ids=full_pos, use_cache=False).logits
+    logits = logits[:, -R - 1:-1, :]
+    arrays = dict(prompt_ids=ids, prompt_attention_mask=am, prompt_position_ids=pos, sequences=seq, responses=resp,
+                  attention_mask=full_am, position_ids=full_pos, log_probs=vF.logprobs_from_logits_v2(logits, resp),
+                  entropy=vF.entropy_from_logits(logits))
+    _save("tiny_llama_rollout.npz", arrays, {"eos_token_id": 2, "pad_token_id": 0, "response_length": R,
+                                             "min_top2_logit_gap": gap,
+                                             "hf": "transformers LlamaForCausalLM fp32 eager attention",
+                                             "ref": "hf_rollout.py:112-171; dp_actor.py:249-272"})
+
+
 if __name__ == "__main__":
     which = sys.argv[1:] or ["ppo_loss", "masked_mean", "grpo", "gae", "logprob", "fused_linear", "masks", "tiny_qwen2"]
     for w in which:

@@ -163,7 +163,7 @@ def test_greedy_first_index_tie_break():
     assert oracle.greedy(np.array([[3.0, 3.0, 1.0], [0.0, 1.0, 1.0]])).tolist() == [0, 1]
 
 
-def _tiny_cfg_and_params():
+def _tiny_cfg_and_params(name="tiny_qwen2"):
     import json
     import os
     import types
@@ -173,7 +173,7 @@ def _tiny_cfg_and_params():
 
     from oracle import qwen2_ref
 
-    d = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "tiny_qwen2")
+    d = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", name)
     c = json.load(open(os.path.join(d, "config.json")))
     cfg = types.SimpleNamespace(**c)
     cfg.head_dim = cfg.hidden_size // cfg.num_attention_heads
@@ -199,3 +199,22 @@ def test_qwen2_restatement_matches_reference_model(golden):
     np.testing.assert_allclose(ent.numpy(), z["entropy"], rtol=1e-5, atol=1e-5)
     lp7, _ = qwen2_ref.logp_entropy(cfg, P, ids, am, pos, r, temperature=0.7)
     np.testing.assert_allclose(lp7.numpy(), z["log_probs_t07"], rtol=1e-5, atol=1e-5)
+
+
+def test_llama_restatement_matches_reference_model(golden):
+    """The same restatement with attention_bias=False / untied lm_head / head_dim 128 / rope_theta 5e5
+    reproduces HF LlamaForCausalLM (config #4's architecture): greedy tokens bit-exact, log-probs to fp32."""
+    import torch
+
+    from oracle import qwen2_ref
+
+    z, meta = golden("tiny_llama_rollout.npz")
+    cfg, P = _tiny_cfg_and_params("tiny_llama")
+    assert cfg.head_dim == 128 and not cfg.attention_bias and "layers.0.qkv_proj.bias" not in P
+    t = lambda k: torch.from_numpy(np.ascontiguousarray(z[k]))  # noqa: E731
+    resp = qwen2_ref.generate_greedy(cfg, P, t("prompt_ids"), t("prompt_attention_mask"), t("prompt_position_ids"),
+                                     meta["response_length"], [meta["eos_token_id"]], meta["pad_token_id"])
+    np.testing.assert_array_equal(resp.numpy(), z["responses"])
+    lp, ent = qwen2_ref.logp_entropy(cfg, P, t("sequences"), t("attention_mask"), t("position_ids"), t("responses"))
+    np.testing.assert_allclose(lp.numpy(), z["log_probs"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(ent.numpy(), z["entropy"], rtol=1e-5, atol=1e-5)
