@@ -137,9 +137,10 @@ def test_add_rmsnorm_forward_backward(dt, with_delta, N, H):
     torch.testing.assert_close(dw, 1 + wr.grad, rtol=1e-4, atol=1e-3)
 
 
+@pytest.mark.parametrize("I", [4864, 36])  # bf16: 16-B-per-lane path (I % 8 == 0) and the generic one
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
-def test_swiglu_forward_backward(dt):
-    N, I = 131, 4864
+def test_swiglu_forward_backward(dt, I):
+    N = 131
     g = torch.Generator(device=DEV).manual_seed(2)
     gu = (torch.randn(N, 2 * I, device=DEV, generator=g) * 3).to(dt)
     a = torch.empty(N, I, device=DEV, dtype=dt)

@@ -414,6 +414,24 @@ def train_gemms(Ms=(6144, 12288)):
     return res
 
 
+def swiglu(Ns=(6144, 12288), I=4864):
+    """SwiGLU forward / backward at the training (8 x 768) and log-prob (16 x 768) micro-batch rows, HBM GB/s."""
+    dev, bf = "cuda", torch.bfloat16
+    res = []
+    for N in Ns:
+        gu = torch.randn(N, 2 * I, device=dev, dtype=bf)
+        a = torch.empty(N, I, device=dev, dtype=bf)
+        da = torch.randn(N, I, device=dev, dtype=bf)
+        dgu = torch.empty_like(gu)
+        t = time_it(lambda: native.swiglu_fwd(gu, a))
+        byt = N * I * 6  # read gate + up, write out (bf16)
+        res.append(dict(kernel="swiglu_fwd", N=N, I=I, seconds=t, GBps=byt / t / 1e9, frac=byt / t / PEAK_HBM))
+        t = time_it(lambda: native.swiglu_bwd(gu, da, dgu))
+        byt = N * I * 10  # read gate, up, d out; write d gate, d up
+        res.append(dict(kernel="swiglu_bwd", N=N, I=I, seconds=t, GBps=byt / t / 1e9, frac=byt / t / PEAK_HBM))
+    return res
+
+
 def launch_floor(B=64, H=896, I=4864):
     """Per-call time of tiny kernels replayed back to back from a HIP graph: the launch/dependency floor of a
     decode step, next to the small hand-written decode kernels at B rows."""
@@ -452,6 +470,10 @@ if __name__ == "__main__":
         for B in (8, 16):
             for r in flash(B=B):
                 print(json.dumps(r), flush=True)
+        sys.exit(0)
+    if args.only == "swiglu":
+        for r in swiglu():
+            print(json.dumps(r), flush=True)
         sys.exit(0)
     if args.only == "floor":
         for r in launch_floor():
