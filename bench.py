@@ -8,7 +8,9 @@ across the N ranks: "scaling" is strong. Random-init Qwen2.5-0.5B weights, synth
   python bench.py [--gpus N] [--steps K] [--warmup W]          (N>1 under torch.distributed.run)
 
 Besides the step rate the JSON line carries
-  roofline     : the dominant hand-written kernel (--roofline-kernel, default the fused attention forward),
+  roofline     : the dominant eagerly launched hand-written kernel (--roofline-kernel; default the SwiGLU
+                 forward, the largest hand-written total in profiles/r01_kernel_stats.csv outside the graphed
+                 decode step; the fused attention forward is the MFMA-bound alternative),
                  every launch inside the timed region bracketed by HIP events on its launch stream;
                  achieved = algorithmic work per launch (ROOFLINE below) / mean launch
                  duration, against its bound's peak (2.5 PFLOP/s dense bf16 MFMA or 8 TB/s HBM);
@@ -57,8 +59,16 @@ def _flash_fwd_flops(a):
     return 4.0 * B * Hkv * G * D * pairs
 
 
+def _swiglu_fwd_bytes(a):
+    # drl_swiglu_fwd(gate_up, out, dt, N, I, stream): read gate and up rows, write the product (one element each)
+    dt, N, I = a[2], a[3], a[4]
+    return 3 * N * I * (2 if dt == 4 else 4)
+
+
 # symbol -> (work per launch from the call's arguments, per-unit statement, bound, peak, unit)
 ROOFLINE = {
+    "drl_swiglu_fwd": (_swiglu_fwd_bytes, "6 B per (token, intermediate column): gate + up read, product written (bf16)",
+                       "hbm", PEAK_HBM_GBPS, "GB/s"),
     "drl_flash_attn_fwd": (_flash_fwd_flops, "4*D FLOP per causal (query, key) pair per query head", "mfma",
                            PEAK_BF16_TFLOPS, "TFLOP/s"),
     "drl_masked_softmax_fwd": (_softmax_fwd_bytes, "6 B per attention score (fp32 in, bf16 out)", "hbm",
@@ -124,7 +134,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--tiny", action="store_true", help="2-layer model, small batch (bring-up only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--roofline-kernel", default="drl_flash_attn_fwd", choices=sorted(ROOFLINE))
+    ap.add_argument("--roofline-kernel", default="drl_swiglu_fwd", choices=sorted(ROOFLINE))
     ap.add_argument("--override", nargs="*", default=[])
     ap.add_argument("--dist-backend", default=None,
                     help="default: nccl (RCCL) on GPU; gloo lets several ranks share one GPU for a rehearsal")
