@@ -108,7 +108,6 @@ SIGNATURES = {
     "drl_value_head_fwd": (ctypes.c_int, [P, I64, P, P, I32, I64, I64, P, I32, P]),
     "drl_value_head_bwd_workspace_bytes": (SZ, [I64, I64]),
     "drl_value_head_bwd": (ctypes.c_int, [P, I64, P, I32, P, I64, I64, P, I64, P, P, P, SZ, P]),
-    "drl_prefetch": (ctypes.c_int, [P, SZ, I32, P]),
     "drl_select_tokens_workspace_bytes": (SZ, [I64]),
     "drl_select_tokens": (ctypes.c_int, [P, I32, I64, I64, I64, ctypes.POINTER(SamplingParams), P, P, I64, P, SZ, P]),
     "drl_response_mask": (ctypes.c_int, [P, I64, I64, I64, P, I32, P, I32, I64, P]),

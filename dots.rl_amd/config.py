@@ -81,7 +81,6 @@ DEFAULTS = dict(
             use_hip_graph=True,  # decode steps replayed from one captured HIP graph (rollout.py)
             packed_decode=True, packed_decode_max_rows=512,  # qwen2.PackedDecode (fragment-packed operands)
             fused_select=False,  # lm_head fused with K4 (csrc/fused_linear.hip)
-            decode_prefetch=False, decode_prefetch_wgs=64,  # next layer's operands -> MALL on a side stream
         ),
         ref=dict(log_prob_micro_batch_size=None, log_prob_micro_batch_size_per_gpu=16, log_prob_use_dynamic_bsz=False),
     ),

@@ -400,24 +400,6 @@ void launch_dg(const DgArgs& a, const DgPlan& p, hipStream_t s) {
 }  // namespace
 }  // namespace drl
 
-// ------------------------------------------------------------------------------------------- prefetch
-// Read `bytes` at p (16 B per lane per load, 4 loads in flight per lane) so the next decode layer's weight
-// and KV-cache streams hit the memory-side cache (MALL) instead of HBM: issued on a side stream while the
-// current layer runs. The loads feed a value that is stored only if it equals an impossible sentinel, so
-// the compiler keeps them and nothing is ever written.
-__global__ __launch_bounds__(256) void prefetch_kernel(const uint4* p, int64_t n16, unsigned* sink) {
-  unsigned acc = 0;
-  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
-  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n16; i += 4 * stride) {
-    uint4 v[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) v[k] = i + k * stride < n16 ? p[i + k * stride] : make_uint4(0, 0, 0, 0);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) acc ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
-  }
-  if (sink != nullptr && acc == 0x9e3779b9u) *sink = acc;  // sink is NULL: never taken, not provable
-}
-
 extern "C" {
 
 void drl_decode_gemm_set_plan(int32_t mb, int32_t ksw) {
@@ -600,17 +582,6 @@ int drl_decode_rope(const float* partials, int32_t nsplit, const void* bias, con
   const int64_t n = B * (Hq + 2 * Hkv) * (D / 2);
   hipLaunchKernelGGL(dec_rope_kernel, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0,
                      static_cast<hipStream_t>(stream), a);
-  DRL_LAUNCH_CHECK();
-  return DRL_OK;
-}
-
-int drl_prefetch(const void* ptr, size_t bytes, int32_t workgroups, void* stream) {
-  using namespace drl;
-  DRL_CHECK_ARG(ptr != nullptr && aligned16(ptr), "prefetch pointer must be non-NULL and 16-byte aligned");
-  if (bytes < 16) return DRL_OK;
-  const int g = workgroups > 0 ? workgroups : 64;
-  hipLaunchKernelGGL(prefetch_kernel, dim3(g), dim3(256), 0, static_cast<hipStream_t>(stream),
-                     static_cast<const uint4*>(ptr), static_cast<int64_t>(bytes / 16), nullptr);
   DRL_LAUNCH_CHECK();
   return DRL_OK;
 }

@@ -711,12 +711,6 @@ def decode_gemm(x_packed, w_packed, M, N, K, swiglu=False, partials=None, out_pa
     return out_packed if swiglu else partials
 
 
-def prefetch(t, workgroups=64):
-    """Touch every byte of device tensor t (see drl_prefetch) on the current stream."""
-    _dev(t)
-    check(lib().drl_prefetch(_p(t), t.numel() * t.element_size(), int(workgroups), _stream()), "drl_prefetch")
-
-
 def decode_rmsnorm(x_in, partials, x_out, weight, y, eps, mbt=0):
     """x_out = x_in + bf16(sum partials); y = RMSNorm(x_out) * w in bf16, packed (mbt > 0) or row-major."""
     _dev(x_in, weight, y)

@@ -611,13 +611,10 @@ class PackedDecode:
                         for n, k, sw in ((NQ, H, False), (H, cfg.num_attention_heads * D, False), (2 * I, H, True),
                                          (H, I, False))))
 
-    def __init__(self, model, B, prefetch=False, prefetch_wgs=64):
+    def __init__(self, model, B):
         cfg, s, dev = model.cfg, model.store, model.store.device
         self.model = model
         self.B = B
-        self.prefetch = bool(prefetch)  # rollout.decode_prefetch: next layer's operands -> MALL on a side stream
-        self.prefetch_wgs = int(prefetch_wgs)
-        self.side = torch.cuda.Stream(device=dev) if self.prefetch else None
         H, I, D = cfg.hidden_size, cfg.intermediate_size, cfg.head_dim
         Hq, Hkv = cfg.num_attention_heads, cfg.num_key_value_heads
         self.NQ = (Hq + 2 * Hkv) * D
@@ -657,17 +654,8 @@ class PackedDecode:
         pos = positions.view(-1)
         Lk = cache.k[0].shape[2]
         prev = None
-        main = torch.cuda.current_stream()
         for i in range(cfg.num_hidden_layers):
             p, w = f"layers.{i}.", self.w[i]
-            if self.prefetch and i + 1 < cfg.num_hidden_layers:
-                # side stream: layer i+1's packed weights and KV cache -> MALL while layer i runs (forked from
-                # and joined to the main stream, so the captured graph has the same dependencies)
-                self.side.wait_stream(main)
-                with torch.cuda.stream(self.side):
-                    nw = self.w[i + 1]
-                    for t in (nw["qkv"], cache.k[i + 1], cache.vt[i + 1], nw["o"], nw["gu"], nw["d"]):
-                        native.prefetch(t, self.prefetch_wgs)
             native.decode_rmsnorm(self.x, prev, self.x, s.w(p + "input_layernorm"), self.h_p, eps, mbt=mbt)
             native.decode_qkv_rope(self.h_p, w["qkv"], m.qkv_bias(i), pos, m.cos, m.sin, B, H, Hq, Hkv, D,
                                    self.q, cache.k[i], cache.vt[i], kpos_dev)
@@ -679,8 +667,6 @@ class PackedDecode:
             native.decode_gemm(self.h_p, w["gu"], B, 2 * I, H, swiglu=True, out_packed=self.a_p)
             native.decode_gemm(self.a_p, w["d"], B, H, I, partials=self.part_d)
             prev = self.part_d
-        if self.prefetch:  # join once: a prefetch that falls behind only loses its benefit, never stalls a layer
-            main.wait_stream(self.side)
         native.decode_rmsnorm(self.x, prev, None, s.w("norm"), self.h_out, eps, mbt=0)
         return self.h_out
 

@@ -116,8 +116,7 @@ class MI355XRollout:
         B = responses.shape[0]
         max_rows = int(self.config.get("packed_decode_max_rows", 512))
         use = self.config.get("packed_decode", True) and PackedDecode.supported(m, B, max_rows)
-        packed = PackedDecode(m, B, prefetch=self.config.get("decode_prefetch", False),
-                              prefetch_wgs=self.config.get("decode_prefetch_wgs", 64)) if use else None
+        packed = PackedDecode(m, B) if use else None
         self.last_packed_decode = packed is not None
 
         def body():

@@ -362,11 +362,6 @@ int drl_decode_attention_vt(const void* q, const void* k_cache, const void* vt_c
                             int64_t B, int64_t Hkv, int64_t G, int64_t D, int64_t ld_k, int64_t ld_vt, int64_t L,
                             float scale, void* out, int64_t out_mbt, void* workspace, size_t workspace_bytes,
                             void* stream);
-/* Read `bytes` at ptr (16-B aligned) with `workgroups` workgroups (<= 0: 64) and discard the data: issued on a
- * side stream during decode layer i for layer i+1's packed weights and KV cache, so their streams hit the
- * memory-side cache. No reference equivalent (rollout engine internals, hf_rollout.py:112-124). */
-int drl_prefetch(const void* ptr, size_t bytes, int32_t workgroups, void* stream);
-
 /* Backward of drl_flash_attn_fwd for Tq == Tk == T, qoff = 0 (the training forward), recomputing P from lse:
  * q (B,Hkv,G,T,D), k / v (B,Hkv,T,D) row-major, kt (B,Hkv,D,ld_t) head-dim-major copy of k (written by
  * drl_rope_qkv_fwd), o and dout (B,T,Hkv*G*D), lse from the forward. delta: (B,Hkv,G,T) fp32 scratch.
