@@ -280,6 +280,7 @@ struct SelectArgs {
   int64_t* out;
   const int64_t* dev_step;
   unsigned long long* best;  // (N) running max per row; zero on entry, reset to zero by the finish kernel
+  const float* thr;          // (N) top-k / top-p cut on z = logit / T (tokens below it never win), or nullptr
 };
 
 // Slice s of row r: best packed key over [s*chunk, (s+1)*chunk), merged into best[r] with one atomic max.
@@ -292,9 +293,14 @@ __global__ __launch_bounds__(kThreads) void select_slice_kernel(SelectArgs a) {
   const int64_t end = begin + a.chunk < a.V ? begin + a.chunk : a.V;
   const uint64_t off = a.offset + (a.dev_step ? static_cast<uint64_t>(*a.dev_step) : 0ull);
   const uint64_t ctr_row = static_cast<uint64_t>(a.row_base + r) << 32;
+  const float cut = (SAMPLE && a.thr != nullptr) ? a.thr[r] : -INFINITY;
   auto key_of = [&](float x, uint32_t bits) -> float {
-    if constexpr (SAMPLE) return race_key(scale_logit<DT>(x, a.temp, a.temp != 1.0f, false), bits);
-    else return x;
+    if constexpr (SAMPLE) {
+      const float z = scale_logit<DT>(x, a.temp, a.temp != 1.0f, false);
+      return z >= cut ? race_key(z, bits) : -INFINITY;  // filtered tokens lose to every kept one
+    } else {
+      return x;
+    }
   };
   uint64_t best = 0;
   int64_t done = begin;
@@ -363,6 +369,102 @@ __global__ __launch_bounds__(kThreads) void select_finish_kernel(SelectArgs a, i
   }
 }
 
+// Top-k / top-p (HF TopKLogitsWarper then TopPLogitsWarper, after TemperatureLogitsWarper) as one cut per
+// row on z = logit / T: one workgroup per row, radix select over order-preserving 32-bit keys, 8-bit digits,
+// LDS histograms with integer atomics (so the cut is deterministic, identical in graph replay and eager).
+//   top-k: the k-th largest z (all ties with it kept, as `scores < topk[..., -1]` removes only smaller ones);
+//   top-p: over the top-k survivors, masses e = exp(z - max) in 2^40 fixed point; the cut is the value of the
+//   last token (descending) whose strictly-higher mass is < top_p * sum — the nucleus of
+//   `cumsum(softmax(sorted ascending)) <= 1 - top_p` removed; ties at the cut are all kept (HF's sort order
+//   decides among them). thr[r] = max of the two cuts; the sampler skips tokens with z < thr[r].
+__device__ __forceinline__ uint32_t order_key(float z) {
+  const uint32_t b = __float_as_uint(z);
+  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+__device__ __forceinline__ float key_value(uint32_t k) {
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+
+template <int DT>
+__global__ __launch_bounds__(kThreads) void select_threshold_kernel(SelectArgs a, int top_k, float top_p) {
+  const int64_t r = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const void* row = static_cast<const typename Elem<DT>::T*>(a.logits) + r * a.ld;
+  const int64_t V = a.V;
+  auto zat = [&](int64_t i) { return scale_logit<DT>(Elem<DT>::get(row, i), a.temp, a.temp != 1.0f, false); };
+  __shared__ unsigned long long hist[256];
+  __shared__ float s_red[kThreads / kWave];
+  __shared__ unsigned long long s_u64[kThreads / kWave];
+  __shared__ uint32_t s_prefix;
+  __shared__ unsigned long long s_target;
+
+  // radix select: find the key of the element where the (count or mass) from the top crosses `target`
+  // (returned prefix = full 32-bit key). weight(i) = 1 (top-k) or fixed-point mass (top-p).
+  auto radix = [&](auto weight, unsigned long long target, uint32_t lo_key) -> uint32_t {
+    uint32_t prefix = 0;
+    for (int pass = 0; pass < 4; ++pass) {
+      const int shift = 24 - 8 * pass;
+      for (int b = tid; b < 256; b += kThreads) hist[b] = 0;
+      __syncthreads();
+      for (int64_t i = tid; i < V; i += kThreads) {
+        const float z = zat(i);
+        const uint32_t k = order_key(z);
+        if (k < lo_key) continue;
+        if (pass > 0 && (k >> (shift + 8)) != prefix) continue;
+        const unsigned long long w = weight(z);
+        if (w) atomicAdd(&hist[(k >> shift) & 0xFFu], w);
+      }
+      __syncthreads();
+      if (tid == 0) {
+        unsigned long long above = 0;
+        int b = 255;
+        for (; b > 0; --b) {
+          if (above + hist[b] >= target) break;
+          above += hist[b];
+        }
+        s_prefix = (prefix << 8) | static_cast<uint32_t>(b);
+        s_target = target - above;
+      }
+      __syncthreads();
+      prefix = s_prefix;
+      target = s_target;
+      __syncthreads();
+    }
+    return prefix;
+  };
+
+  uint32_t cut_key = 0;
+  if (top_k > 0 && top_k < V)
+    cut_key = radix([](float) { return 1ull; }, static_cast<unsigned long long>(top_k), 0u);
+  if (top_p < 1.0f) {
+    // max z (the top token always survives top-k)
+    float m = -INFINITY;
+    for (int64_t i = tid; i < V; i += kThreads) m = fmaxf(m, zat(i));
+    m = wave_max(m);
+    if (lane == 0) s_red[wave] = m;
+    __syncthreads();
+    m = fmaxf(fmaxf(s_red[0], s_red[1]), fmaxf(s_red[2], s_red[3]));
+    const float scale = 1099511627776.0f;  // 2^40 fixed point: exact, associative integer sums
+    const uint32_t kk = cut_key;
+    auto mass = [&](float z) -> unsigned long long {
+      return order_key(z) >= kk ? static_cast<unsigned long long>(__expf(z - m) * scale) : 0ull;
+    };
+    unsigned long long tot = 0;
+    for (int64_t i = tid; i < V; i += kThreads) tot += mass(zat(i));
+    tot = wave_sum_u64(tot);
+    if (lane == 0) s_u64[wave] = tot;
+    __syncthreads();
+    tot = s_u64[0] + s_u64[1] + s_u64[2] + s_u64[3];
+    // keep j iff mass strictly above j < top_p * total: the cut token is where the running mass from the top
+    // first reaches that target (a token exactly at it is the last one kept)
+    unsigned long long target = static_cast<unsigned long long>(static_cast<double>(top_p) * static_cast<double>(tot));
+    if (target < 1) target = 1;
+    const uint32_t pk = radix(mass, target, kk);
+    cut_key = pk > cut_key ? pk : cut_key;
+  }
+  if (tid == 0) const_cast<float*>(a.thr)[r] = cut_key ? key_value(cut_key) : -INFINITY;
+}
+
 bool rows_aligned(const void* p, int64_t ld, int dt) {
   const int64_t esz = dt == DRL_BF16 ? 2 : 4;
   return aligned16(p) && ((ld * esz) % 16 == 0);
@@ -425,7 +527,8 @@ int drl_logprob_entropy_bwd(const void* logits, int32_t dt, int64_t N, int64_t V
   return DRL_OK;
 }
 
-size_t drl_select_tokens_workspace_bytes(int64_t N) { return N > 0 ? static_cast<size_t>(N) * 8 : 0; }
+// best (N x u64) + the top-k / top-p cut (N x f32)
+size_t drl_select_tokens_workspace_bytes(int64_t N) { return N > 0 ? static_cast<size_t>(N) * 12 : 0; }
 
 int drl_select_tokens(const void* logits, int32_t dt, int64_t N, int64_t V, int64_t ld,
                       const drl_sampling_params* p, int32_t* unfinished, int64_t* out_tokens, int64_t ld_out,
@@ -436,8 +539,8 @@ int drl_select_tokens(const void* logits, int32_t dt, int64_t N, int64_t V, int6
   DRL_CHECK_ARG(dt == DRL_BF16 || dt == DRL_F32, "logits dtype must be F32 or BF16");
   DRL_CHECK_ARG(p->n_eos == 0 || p->eos_ids != nullptr, "n_eos > 0 but eos_ids is NULL");
   const bool sample = p->do_sample && p->temperature > 0.f;
-  if (sample && ((p->top_k > 0 && p->top_k < V) || p->top_p < 1.0f))
-    return fail(DRL_ERR_UNSUPPORTED, "top-k / top-p filtering is not implemented in this build");
+  const bool filter = sample && ((p->top_k > 0 && p->top_k < V) || p->top_p < 1.0f);
+  DRL_CHECK_ARG(!sample || (p->top_p > 0.f && p->top_p <= 1.0f), "top_p must be in (0, 1], got %f", p->top_p);
   if (N == 0) return DRL_OK;
   DRL_CHECK_ARG(N <= 65535, "too many rows for one launch");
   if (!workspace || workspace_bytes < drl_select_tokens_workspace_bytes(N) || (reinterpret_cast<uintptr_t>(workspace) & 7u))
@@ -449,6 +552,7 @@ int drl_select_tokens(const void* logits, int32_t dt, int64_t N, int64_t V, int6
   a.eos = p->eos_ids; a.n_eos = p->n_eos; a.unfinished = unfinished; a.out = out_tokens;
   a.dev_step = p->dev_step;
   a.best = static_cast<unsigned long long*>(workspace);
+  a.thr = filter ? reinterpret_cast<const float*>(static_cast<char*>(workspace) + static_cast<size_t>(N) * 8) : nullptr;
   // slices per row: ~4 workgroups per CU over the whole launch, >= 2048 elements per slice
   const int64_t want = (4 * static_cast<int64_t>(cu_count()) + N - 1) / N;
   const int64_t max_slices = (V + 2047) / 2048;
@@ -456,6 +560,16 @@ int drl_select_tokens(const void* logits, int32_t dt, int64_t N, int64_t V, int6
   a.chunk = ((V + slices - 1) / slices + 7) / 8 * 8;
   const dim3 grid(static_cast<unsigned>((V + a.chunk - 1) / a.chunk), static_cast<unsigned>(N));
   hipStream_t s = static_cast<hipStream_t>(stream);
+  if (filter) {
+    const int k = (p->top_k > 0 && p->top_k < V) ? p->top_k : 0;
+    if (dt == DRL_BF16)
+      hipLaunchKernelGGL(select_threshold_kernel<DRL_BF16>, dim3(static_cast<unsigned>(N)), dim3(kThreads), 0, s, a, k,
+                         p->top_p);
+    else
+      hipLaunchKernelGGL(select_threshold_kernel<DRL_F32>, dim3(static_cast<unsigned>(N)), dim3(kThreads), 0, s, a, k,
+                         p->top_p);
+    DRL_LAUNCH_CHECK();
+  }
   if (dt == DRL_BF16) {
     if (sample) hipLaunchKernelGGL((select_slice_kernel<DRL_BF16, true>), grid, dim3(kThreads), 0, s, a);
     else hipLaunchKernelGGL((select_slice_kernel<DRL_BF16, false>), grid, dim3(kThreads), 0, s, a);

@@ -215,8 +215,11 @@ int drl_value_head_bwd(const void* hidden, int64_t ld_h, const void* weight, int
  * becomes finished. The chosen token is written to out_tokens[n*ld_out] (int64) — pass a column
  * of the `responses` tensor to fill it in place. temperature <= 0 or do_sample == 0 -> greedy
  * (argmax, first index on ties = torch.argmax). Sampling: z = logit / temperature (fp32, HF
- * TemperatureLogitsWarper), top-k / top-p (not implemented: DRL_ERR_UNSUPPORTED), then the categorical
- * draw as a race of exponential clocks: argmax_i z_i - log(E_i), E_i = -log(1 - v_i), v_i the 24-bit
+ * TemperatureLogitsWarper), then top-k (top_k > 0: tokens below the k-th largest z dropped, ties kept, HF
+ * TopKLogitsWarper) and top-p (top_p < 1: the nucleus of HF TopPLogitsWarper over the top-k survivors — a
+ * token is kept iff the softmax mass of the tokens above it is < top_p; ties at the cut kept) as one cut per
+ * row (a third launch, one workgroup per row, deterministic radix select), then the categorical
+ * draw as a race of exponential clocks over the kept tokens: argmax_i z_i - log(E_i), E_i = -log(1 - v_i), v_i the 24-bit
  * uniform ((w >> 8) + 0.5) / 2^24 from word (i & 3) of Philox4x32-10(key = seed,
  * counter = ((row_base + n) << 32 | i >> 2, offset = decode step)) — softmax(z)-distributed like HF's
  * torch.multinomial. workspace: drl_select_tokens_workspace_bytes(N) bytes, 8-byte aligned, zero-filled

@@ -85,6 +85,17 @@ def test_graphed_sampling_rollout_equals_eager():
     for k in ("responses", "attention_mask", "position_ids"):
         assert torch.equal(outs[0].batch[k], outs[1].batch[k]), k
     assert len(set(outs[0].batch["responses"].flatten().tolist())) > 20  # actually sampled
+    # top-k / top-p sampling (per-row cut kernel) replays identically from the graph
+    tk = []
+    for g in (True, False):
+        rcfg = to_attr(dict(do_sample=True, temperature=0.9, top_k=20, top_p=0.9, response_length=24, ignore_eos=False,
+                            seed=3, val_kwargs={}, use_hip_graph=g))
+        prompts = DataProto.from_dict({"input_ids": T(z["prompt_ids"]), "attention_mask": T(z["prompt_attention_mask"]),
+                                       "position_ids": T(z["prompt_position_ids"])},
+                                      meta_info={"eos_token_id": meta["eos_token_id"], "pad_token_id": meta["pad_token_id"]})
+        tk.append(MI355XRollout(model, rcfg).generate_sequences(prompts))
+    assert torch.equal(tk[0].batch["responses"], tk[1].batch["responses"])
+    assert not torch.equal(tk[0].batch["responses"], outs[0].batch["responses"])
 
 
 @pytest.mark.parametrize("temperature,key", [(1.0, "log_probs"), (0.7, "log_probs_t07")])
