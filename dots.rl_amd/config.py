@@ -77,12 +77,14 @@ DEFAULTS = dict(
             name="mi355x", mode="sync", temperature=1.0, top_k=-1, top_p=1.0, do_sample=True, n=8,
             prompt_length=512, response_length=256, ignore_eos=False, log_prob_micro_batch_size=None,
             log_prob_micro_batch_size_per_gpu=16, log_prob_use_dynamic_bsz=False, micro_batch_size=None,
+            log_prob_max_token_len_per_gpu=16384,
             seed=1234, val_kwargs=dict(top_k=-1, top_p=1.0, temperature=0, n=1, do_sample=False),
             use_hip_graph=True,  # decode steps replayed from one captured HIP graph (rollout.py)
             packed_decode=True, packed_decode_max_rows=512,  # qwen2.PackedDecode (fragment-packed operands)
             fused_select=False,  # lm_head fused with K4 (csrc/fused_linear.hip)
         ),
-        ref=dict(log_prob_micro_batch_size=None, log_prob_micro_batch_size_per_gpu=16, log_prob_use_dynamic_bsz=False),
+        ref=dict(log_prob_micro_batch_size=None, log_prob_micro_batch_size_per_gpu=16, log_prob_use_dynamic_bsz=False,
+                 log_prob_max_token_len_per_gpu=16384),
     ),
     # critic.yaml + dp_critic.yaml (used when algorithm.adv_estimator == "gae" or critic.enable)
     critic=dict(

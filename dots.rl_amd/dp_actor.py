@@ -18,6 +18,7 @@ import torch.distributed as dist
 from . import native
 from .core_algos import fused_actor_loss
 from .protocol import DataProto
+from .seqlen_balancing import prepare_dynamic_batch, restore_dynamic_batch
 from .qwen2 import Qwen2Model
 from .torch_functional import logprobs_and_entropy_from_logits
 
@@ -158,16 +159,25 @@ class DataParallelPPOActor:
         self.actor_module.training = False
         micro_batch_size = data.meta_info["micro_batch_size"]
         temperature = data.meta_info["temperature"]
-        assert not data.meta_info.get("use_dynamic_bsz", False), "dynamic bsz is not supported yet"
+        use_dynamic_bsz = data.meta_info.get("use_dynamic_bsz", False)
         data = data.select(batch_keys=["responses", "input_ids", "attention_mask", "position_ids"])
+        if use_dynamic_bsz:  # token-budget micro-batches (seqlen_balancing.prepare_dynamic_batch)
+            micro_batches, batch_idx_list = prepare_dynamic_batch(data, max_token_len=data.meta_info["max_token_len"])
+        else:
+            micro_batches = data.split(micro_batch_size)
         lps, ents = [], []
-        for mb in data.split(micro_batch_size):
+        for mb in micro_batches:
             ent, lp = self._forward_micro_batch(mb.batch, temperature, calculate_entropy)
             lps.append(lp)
             if calculate_entropy:
                 ents.append(ent)
         log_probs = torch.cat(lps, 0)
-        return log_probs, (torch.cat(ents, 0) if calculate_entropy else None)
+        entropys = torch.cat(ents, 0) if calculate_entropy else None
+        if use_dynamic_bsz:
+            log_probs = restore_dynamic_batch(log_probs, batch_idx_list)
+            if entropys is not None:
+                entropys = restore_dynamic_batch(entropys, batch_idx_list)
+        return log_probs, entropys
 
     def update_policy(self, data: DataProto):
         """dp_actor.py:361-482."""
@@ -189,14 +199,20 @@ class DataParallelPPOActor:
         mb_out, mb_lsf, grad_norms = [], [], []
         for _ in range(cfg.ppo_epochs):
             for mini_batch in mini_batches:
-                grad_accum = cfg.ppo_mini_batch_size // cfg.ppo_micro_batch_size_per_gpu
-                micro_batches = mini_batch.split(cfg.ppo_micro_batch_size_per_gpu)
+                if cfg.get("use_dynamic_bsz", False):
+                    micro_batches, _ = prepare_dynamic_batch(mini_batch, max_token_len=cfg.ppo_max_token_len_per_gpu)
+                else:
+                    grad_accum = cfg.ppo_mini_batch_size // cfg.ppo_micro_batch_size_per_gpu
+                    micro_batches = mini_batch.split(cfg.ppo_micro_batch_size_per_gpu)
                 self.actor_optimizer.zero_grad()
                 for k, micro_batch in enumerate(micro_batches):
                     if k == len(micro_batches) - 1:  # gradients final after this backward: overlap the all-reduce
                         self.actor_optimizer.begin_overlap(m)
                     mb = micro_batch.batch
-                    lsf = 1.0 / grad_accum
+                    if cfg.get("use_dynamic_bsz", False):  # relative to the dynamic bsz (dp_actor.py:413-414)
+                        lsf = mb["response_mask"].shape[0] / cfg.ppo_mini_batch_size
+                    else:
+                        lsf = 1.0 / grad_accum
                     calculate_entropy = cfg.entropy_coeff != 0
                     entropy, log_prob = self._forward_micro_batch(mb, temperature, calculate_entropy)
                     out = fused_actor_loss(

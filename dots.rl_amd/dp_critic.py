@@ -18,6 +18,7 @@ import torch
 from . import native
 from .dp_actor import FlatAdamW, append_to_dict
 from .protocol import DataProto
+from .seqlen_balancing import prepare_dynamic_batch, restore_dynamic_batch
 from .qwen2 import Qwen2Model
 
 
@@ -70,12 +71,18 @@ class DataParallelPPOCritic:
         """dp_critic.py:163-197."""
         self.critic_module.training = False
         micro_batch_size = data.meta_info["micro_batch_size"]
-        assert not data.meta_info.get("use_dynamic_bsz", False), "dynamic bsz is not supported yet"
+        use_dynamic_bsz = data.meta_info.get("use_dynamic_bsz", False)
         keys = ["responses", "input_ids", "attention_mask", "position_ids"]
         if "response_mask" in data.batch:
             keys.append("response_mask")
         data = data.select(batch_keys=keys)
-        values = torch.cat([self._forward_micro_batch(mb.batch) for mb in data.split(micro_batch_size)], 0)
+        if use_dynamic_bsz:
+            micro_batches, batch_idx_list = prepare_dynamic_batch(data, max_token_len=data.meta_info["max_token_len"])
+        else:
+            micro_batches = data.split(micro_batch_size)
+        values = torch.cat([self._forward_micro_batch(mb.batch) for mb in micro_batches], 0)
+        if use_dynamic_bsz:
+            values = restore_dynamic_batch(values, batch_idx_list)
         if "response_mask" in data.batch:
             values = values * data.batch["response_mask"]  # only action tokens have values (bf16 * int64 -> bf16)
         return values
@@ -87,19 +94,24 @@ class DataParallelPPOCritic:
         m.training = True
         data = data.select(batch_keys=["input_ids", "responses", "response_mask", "attention_mask", "position_ids",
                                        "values", "returns"])
-        assert not cfg.get("use_dynamic_bsz", False), "dynamic bsz is not supported yet"
         mini_batches = data.split(cfg.ppo_mini_batch_size)
         mb_out, mb_lsf, grad_norms = [], [], []
         for _ in range(cfg.ppo_epochs):
             for mini_batch in mini_batches:
-                grad_accum = cfg.ppo_mini_batch_size // cfg.ppo_micro_batch_size_per_gpu
-                micro_batches = mini_batch.split(cfg.ppo_micro_batch_size_per_gpu)
+                if cfg.get("use_dynamic_bsz", False):
+                    micro_batches, _ = prepare_dynamic_batch(mini_batch, max_token_len=cfg.ppo_max_token_len_per_gpu)
+                else:
+                    grad_accum = cfg.ppo_mini_batch_size // cfg.ppo_micro_batch_size_per_gpu
+                    micro_batches = mini_batch.split(cfg.ppo_micro_batch_size_per_gpu)
                 self.critic_optimizer.zero_grad()
                 for k, micro_batch in enumerate(micro_batches):
                     if k == len(micro_batches) - 1:
                         self.critic_optimizer.begin_overlap(m)
                     mb = micro_batch.batch
-                    lsf = 1.0 / grad_accum
+                    if cfg.get("use_dynamic_bsz", False):  # dp_critic.py:232-234
+                        lsf = mb["response_mask"].shape[0] / cfg.ppo_mini_batch_size
+                    else:
+                        lsf = 1.0 / grad_accum
                     vpreds = self._forward_micro_batch(mb)
                     out = fused_value_loss(vpreds, mb["values"], mb["returns"], mb["response_mask"],
                                            cliprange_value=cfg.cliprange_value, loss_agg_mode=cfg.loss_agg_mode,

@@ -22,6 +22,7 @@ from .core_algos import AdvantageEstimator, agg_loss
 from .metric_utils import compute_data_metrics, compute_throughout_metrics, compute_timing_metrics, reduce_metrics
 from .protocol import DataProto
 from .reward import SyntheticBernoulliRewardManager, compute_reward
+from .seqlen_balancing import get_seqlen_balanced_partitions, log_seqlen_unbalance
 from .single_controller import SPMDWorkerGroup
 from .config import resolve_critic_config
 from .workers import ActorRolloutRefWorker, CriticWorker
@@ -146,21 +147,14 @@ class RayPPOTrainer:
         self._uid_next = base + n
         return np.array([str(uuid.UUID(int=(self.global_steps << 40) + base + i)) for i in range(n)], dtype=object)
 
-    def _balance_batch(self, batch: DataProto, metrics):
-        """ray_trainer.py:1033-1048 (greedy sequence-length balancing across DP ranks)."""
+    def _balance_batch(self, batch: DataProto, metrics, logging_prefix="global_seqlen"):
+        """ray_trainer.py:1033-1048: reorder rows so every DP rank's contiguous chunk carries a similar token
+        count (Karmarkar-Karp, equal-size partitions)."""
         am = batch.batch["attention_mask"]
-        seqlens = am.sum(-1).cpu().tolist()
-        k = self.n_gpus
-        order = sorted(range(len(seqlens)), key=lambda i: -seqlens[i])
-        per = len(seqlens) // k
-        buckets = [[] for _ in range(k)]
-        loads = [0] * k
-        for i in order:
-            j = min((j for j in range(k) if len(buckets[j]) < per), key=lambda j: loads[j])
-            buckets[j].append(i)
-            loads[j] += seqlens[i]
-        idx = torch.tensor([i for b in buckets for i in sorted(b)], device=am.device)
-        batch.reorder(idx)
+        seqlens = am.view(am.shape[0], -1).sum(-1).tolist()
+        parts = get_seqlen_balanced_partitions(seqlens, k_partitions=self.n_gpus, equal_size=True)
+        batch.reorder(torch.tensor([j for p in parts for j in p], device=am.device))
+        metrics.update(log_seqlen_unbalance(seqlens, parts, logging_prefix))
 
     def _rollout(self, batch_dict: dict, timing_raw: dict) -> DataProto:
         """ray_trainer.py:1104-1170: uid per prompt, repeat(n, interleave), generate_sequences, union."""

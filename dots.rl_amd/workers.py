@@ -89,7 +89,10 @@ class ActorRolloutRefWorker(Worker):
             assert a.ppo_mini_batch_size > 0
             if a.get("ppo_micro_batch_size") is not None:
                 a.ppo_micro_batch_size_per_gpu = a.ppo_micro_batch_size // dp
-            assert a.ppo_mini_batch_size % a.ppo_micro_batch_size_per_gpu == 0
+            if a.get("ppo_micro_batch_size_per_gpu") is not None:  # None with use_dynamic_bsz
+                assert a.ppo_mini_batch_size % a.ppo_micro_batch_size_per_gpu == 0, (
+                    f"normalized ppo_mini_batch_size {a.ppo_mini_batch_size} should be divisible by "
+                    f"ppo_micro_batch_size_per_gpu {a.ppo_micro_batch_size_per_gpu}")
         r = config.rollout
         if self._is_rollout and r.get("log_prob_micro_batch_size") is not None:
             r.log_prob_micro_batch_size_per_gpu = r.log_prob_micro_batch_size // dp
@@ -170,6 +173,7 @@ class ActorRolloutRefWorker(Worker):
         r = self.config.rollout
         data.meta_info["micro_batch_size"] = r.log_prob_micro_batch_size_per_gpu
         data.meta_info["use_dynamic_bsz"] = r.log_prob_use_dynamic_bsz
+        data.meta_info["max_token_len"] = r.get("log_prob_max_token_len_per_gpu", 16384)
         data.meta_info["temperature"] = r.temperature
         output, entropys = self.actor.compute_log_prob(data=data, calculate_entropy=True)
         out = DataProto.from_dict(tensors={"old_log_probs": output, "entropys": entropys},
@@ -184,6 +188,7 @@ class ActorRolloutRefWorker(Worker):
         data.meta_info["micro_batch_size"] = rf.log_prob_micro_batch_size_per_gpu
         data.meta_info["temperature"] = self.config.rollout.temperature
         data.meta_info["use_dynamic_bsz"] = rf.log_prob_use_dynamic_bsz
+        data.meta_info["max_token_len"] = rf.get("log_prob_max_token_len_per_gpu", 16384)
         output, _ = self.ref_policy.compute_log_prob(data=data, calculate_entropy=False)
         return self._out(DataProto.from_dict(tensors={"ref_log_prob": output}))
 
@@ -251,9 +256,10 @@ class CriticWorker(Worker):
             c.forward_micro_batch_size_per_gpu = c.get("forward_micro_batch_size", c.ppo_micro_batch_size) // dp
         if c.get("forward_micro_batch_size_per_gpu") is None:
             c.forward_micro_batch_size_per_gpu = c.ppo_micro_batch_size_per_gpu
-        assert c.ppo_mini_batch_size % c.ppo_micro_batch_size_per_gpu == 0, (
-            f"normalized ppo_mini_batch_size {c.ppo_mini_batch_size} should be divisible by "
-            f"ppo_micro_batch_size_per_gpu {c.ppo_micro_batch_size_per_gpu}")
+        if c.get("ppo_micro_batch_size_per_gpu") is not None:
+            assert c.ppo_mini_batch_size % c.ppo_micro_batch_size_per_gpu == 0, (
+                f"normalized ppo_mini_batch_size {c.ppo_mini_batch_size} should be divisible by "
+                f"ppo_micro_batch_size_per_gpu {c.ppo_micro_batch_size_per_gpu}")
 
     @register(dispatch_mode=Dispatch.ONE_TO_ALL)
     def init_model(self):

@@ -19,6 +19,7 @@ Reference call sites (file:line under /root/reference):
 * critic forward/backward (tiny Qwen2ForTokenClassification, the model fsdp_workers.py:1003-1060 builds) :
   verl/workers/critic/dp_critic.py:57-145 values slice, compute_value_loss, loss.backward()
 * DAPO overlong-buffer reward : verl/workers/reward_manager/dapo.py:60-150 (stub tokenizer / preset scores)
+* Karmarkar-Karp balancing : verl/utils/seqlen_balancing.py:26-239 (partitions + imbalance metrics)
 * masked_mean known answers : tests/utils/test_torch_functional.py:55-66 (reference test, reproduced as data)
 """
 
@@ -624,6 +625,30 @@ def gen_tiny_llama():
                                              "min_top2_logit_gap": gap,
                                              "hf": "transformers LlamaForCausalLM fp32 eager attention",
                                              "ref": "hf_rollout.py:112-171; dp_actor.py:249-272"})
+
+
+# --------------------------------------------------------------------------------------------
+# sequence-length balancing (utils/seqlen_balancing.py:26-239): Karmarkar-Karp partitions used by
+# trainer.balance_batch (equal_size) and dynamic micro-batching (unequal), + the imbalance metrics
+# --------------------------------------------------------------------------------------------
+def gen_seqlen():
+    from verl.utils import seqlen_balancing as sb
+
+    rng = np.random.default_rng(21)
+    cases = []
+    for ci, (B, k, eq) in enumerate([(16, 4, True), (64, 8, True), (512, 8, True), (37, 5, False), (64, 7, False),
+                                     (128, 3, False), (8, 8, True), (12, 1, False)]):
+        lens = [int(x) for x in rng.integers(64, 768, size=B)]
+        if ci == 1:
+            lens[:10] = [500] * 10  # ties
+        parts = sb.get_seqlen_balanced_partitions(lens, k_partitions=k, equal_size=eq)
+        stats = sb.log_seqlen_unbalance(seqlen_list=lens, partitions=parts, prefix="global_seqlen") if eq else {}
+        cases.append({"seqlens": lens, "k": k, "equal_size": eq, "partitions": parts,
+                      "stats": {kk: float(v) for kk, v in stats.items()}})
+    path = os.path.join(HERE, "seqlen_balancing.json")
+    with open(path, "w") as f:
+        json.dump({"cases": cases, "ref": "utils/seqlen_balancing.py:26-239"}, f)
+    print(f"wrote {path} ({os.path.getsize(path)} bytes)")
 
 
 if __name__ == "__main__":

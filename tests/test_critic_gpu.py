@@ -247,3 +247,63 @@ def test_dapo_step_end_to_end():
     # responses never hit EOS (tiny vocab) -> length 16 = max: overlong penalty -(16 - 12) / 4 * 1.0 = -1
     np.testing.assert_allclose(b.batch["token_level_scores"].sum(-1).cpu().numpy(),
                                b.non_tensor_batch["acc"] - 1.0, atol=1e-6)
+
+
+def test_dynamic_bsz_log_prob_matches_fixed_micro_batches(golden):
+    """use_dynamic_bsz (token-budget micro-batches, seqlen_balancing.prepare_dynamic_batch + restore) gives the
+    fixed-size micro-batching's log-probs / entropy and critic values, row for row (fp32 tiny models)."""
+    from dots.rl_amd.config import to_attr
+    from dots.rl_amd.dp_actor import DataParallelPPOActor
+    from dots.rl_amd.dp_critic import DataParallelPPOCritic
+    from dots.rl_amd.protocol import DataProto
+
+    zr, _ = golden("tiny_qwen2_rollout.npz")
+    base = {"input_ids": T(zr["sequences"]), "attention_mask": T(zr["attention_mask"]),
+            "position_ids": T(zr["position_ids"]), "responses": T(zr["responses"])}
+    cfg, store, model = _tiny_critic()
+    critic = DataParallelPPOCritic(to_attr({"model": {}}), model)
+    from safetensors.torch import load_file
+
+    from dots.rl_amd.qwen2 import ParamStore, Qwen2Config, Qwen2Model
+
+    acfg = Qwen2Config.from_dict(json.load(open(os.path.join(TINY, "config.json"))))
+    astore = ParamStore(acfg, "cuda", compute_dtype=torch.float32, trainable=False)
+    astore.load_state_dict_hf(load_file(os.path.join(TINY, "model.safetensors")))
+    actor_model = Qwen2Model(acfg, astore)
+    actor = DataParallelPPOActor(to_attr({}), actor_model)
+    outs = {}
+    for dyn in (False, True):
+        meta = {"micro_batch_size": 2, "temperature": 1.0, "use_dynamic_bsz": dyn, "max_token_len": 40}
+        lp, ent = actor.compute_log_prob(DataProto.from_dict(dict(base), meta_info=dict(meta)), calculate_entropy=True)
+        v = critic.compute_values(DataProto.from_dict(dict(base), meta_info=dict(meta)))
+        outs[dyn] = (lp, ent, v)
+    for a, b in zip(outs[False], outs[True]):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-5)
+
+
+def test_gae_ppo_step_dynamic_bsz():
+    """GAE PPO step with use_dynamic_bsz on the actor, the critic and both log-prob passes (token budgets)."""
+    from dots.rl_amd.config import apply_overrides, default_config
+    from dots.rl_amd.trainer import RayPPOTrainer
+
+    tiny = ("{'hidden_size': 128, 'intermediate_size': 256, 'num_hidden_layers': 2, 'num_attention_heads': 2, "
+            "'num_key_value_heads': 1, 'vocab_size': 1024}")
+    cfg = apply_overrides(default_config(), [
+        "data.train_batch_size=4", "data.max_prompt_length=32", "data.max_response_length=16",
+        "actor_rollout_ref.rollout.n=2", "actor_rollout_ref.rollout.response_length=16",
+        "actor_rollout_ref.rollout.prompt_length=32", "actor_rollout_ref.actor.ppo_mini_batch_size=2",
+        "actor_rollout_ref.actor.use_dynamic_bsz=True", "actor_rollout_ref.actor.ppo_max_token_len_per_gpu=100",
+        "actor_rollout_ref.actor.ppo_micro_batch_size_per_gpu=null", "critic.ppo_micro_batch_size_per_gpu=null",
+        "critic.forward_micro_batch_size_per_gpu=null",
+        "actor_rollout_ref.rollout.log_prob_use_dynamic_bsz=True", "actor_rollout_ref.rollout.log_prob_max_token_len_per_gpu=120",
+        "actor_rollout_ref.ref.log_prob_use_dynamic_bsz=True", "actor_rollout_ref.ref.log_prob_max_token_len_per_gpu=120",
+        "critic.ppo_max_token_len_per_gpu=100", "critic.forward_max_token_len_per_gpu=120",
+        "algorithm.adv_estimator=gae", f"actor_rollout_ref.model.override_config={tiny}",
+        f"critic.model.override_config={tiny}",
+    ])
+    trainer = RayPPOTrainer(cfg)
+    trainer.train_dataloader.vocab_limit = 1000
+    trainer.init_workers()
+    m = trainer.fit(num_steps=1)[-1]
+    for k in ["critic/vf_loss", "actor/pg_loss", "actor/kl_loss", "critic/grad_norm", "actor/grad_norm"]:
+        assert k in m and np.isfinite(m[k]), k
