@@ -139,6 +139,25 @@ def compute_grpo_outcome_advantage(token_level_rewards, response_mask, index, ep
                                              epsilon, norm_adv_by_std_in_grpo)
 
 
+@register_adv_est(AdvantageEstimator.RLOO)
+def compute_rloo_outcome_advantage(token_level_rewards, response_mask, index, epsilon: float = 1e-6, config=None,
+                                   **kwargs):
+    """core_algos.py:444-493 — leave-one-out baseline per uid group (K3, RLOO mode)."""
+    row_group, offsets, members, G = uid_csr(index, token_level_rewards.device)
+    with torch.no_grad():
+        return native.group_outcome_advantage("rloo", token_level_rewards, response_mask, row_group, offsets, members, G)
+
+
+@register_adv_est(AdvantageEstimator.REINFORCE_PLUS_PLUS_BASELINE)
+def compute_reinforce_plus_plus_baseline_outcome_advantage(token_level_rewards, response_mask, index,
+                                                           epsilon: float = 1e-6, config=None, **kwargs):
+    """core_algos.py:392-441 — group-mean baseline, then masked_whiten over the batch (K3 mode + whitening pass)."""
+    row_group, offsets, members, G = uid_csr(index, token_level_rewards.device)
+    with torch.no_grad():
+        return native.group_outcome_advantage("reinforce_plus_plus_baseline", token_level_rewards, response_mask,
+                                              row_group, offsets, members, G)
+
+
 # ---------------------------------------------------------------------------------------------- losses
 def agg_loss(loss_mat, loss_mask, loss_agg_mode: str):
     """core_algos.py:703-736 (forward; gradients flow through fused_actor_loss)."""

@@ -23,10 +23,14 @@ __global__ __launch_bounds__(256) void row_sum_kernel(const float* x, int64_t B,
 
 // per row: group mean/std over the CSR members (float32, torch.mean / unbiased torch.std), then
 // advantages[b, t] = returns[b, t] = norm_score[b] * mask[b, t]
+// estimator: DRL_ADV_GRPO (core_algos.py:260-324), DRL_ADV_RLOO (core_algos.py:444-493: n > 1 ->
+// s * n / (n - 1) - mean * n / (n - 1), a single sample keeps its score), DRL_ADV_REINFORCE_PP_BASELINE
+// (core_algos.py:392-441: s - group mean, then masked_whiten over the batch by the caller's second kernel).
 template <int MDT>
 __global__ __launch_bounds__(256) void grpo_write_kernel(const float* scores, const void* mask, const int32_t* row_group,
                                                          const int32_t* off, const int32_t* mem, int64_t B, int64_t R,
-                                                         float eps, int norm_by_std, float* adv, float* ret) {
+                                                         float eps, int norm_by_std, float* adv, float* ret,
+                                                         int estimator) {
   const int64_t row = blockIdx.x;
   __shared__ float s_val;
   if (threadIdx.x == 0) {
@@ -45,7 +49,14 @@ __global__ __launch_bounds__(256) void grpo_write_kernel(const float* scores, co
       stdv = sqrtf(ss / static_cast<float>(n - 1));
     }
     const float sc = scores[row];
-    s_val = norm_by_std ? (sc - mean) / (stdv + eps) : sc - mean;
+    if (estimator == DRL_ADV_RLOO) {
+      const float fn = static_cast<float>(n), fn1 = static_cast<float>(n - 1);
+      s_val = n > 1 ? (sc * fn) / fn1 - (mean * fn) / fn1 : sc;
+    } else if (estimator == DRL_ADV_REINFORCE_PP_BASELINE) {
+      s_val = sc - mean;
+    } else {
+      s_val = norm_by_std ? (sc - mean) / (stdv + eps) : sc - mean;
+    }
   }
   __syncthreads();
   const float v = s_val;
@@ -83,7 +94,8 @@ __global__ __launch_bounds__(256) void gae_scan_kernel(const float* r, const voi
 // masked_whiten over the whole (B, R) tensor in place: mean, unbiased var, (x - mean) * rsqrt(var + 1e-8).
 // One workgroup (the tensor is one PPO batch of advantages, a few MB); three ordered passes.
 template <int MDT>
-__global__ __launch_bounds__(1024) void masked_whiten_kernel(float* x, const void* mask, int64_t n, int* err) {
+__global__ __launch_bounds__(1024) void masked_whiten_kernel(float* x, const void* mask, int64_t n, int* err,
+                                                             float* copy = nullptr, int times_mask = 0) {
   __shared__ double red[16][2];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   double s = 0.0, c = 0.0;
@@ -114,7 +126,12 @@ __global__ __launch_bounds__(1024) void masked_whiten_kernel(float* x, const voi
   if (tid == 0 && (C == 0.0 || C == 1.0)) *err = 1;  // the reference raises ValueError
   const double var = Q / (C + 1e-8) * (C / (C - 1.0));
   const float rs = static_cast<float>(1.0 / sqrt(var + 1e-8));
-  for (int64_t i = tid; i < n; i += 1024) x[i] = (x[i] - mean) * rs;
+  for (int64_t i = tid; i < n; i += 1024) {
+    float v = (x[i] - mean) * rs;
+    if (times_mask) v *= mask_at<MDT>(mask, i);  // RF++-baseline: masked_whiten(...) * response_mask
+    x[i] = v;
+    if (copy) copy[i] = v;
+  }
 }
 
 }  // namespace
@@ -128,7 +145,25 @@ int drl_grpo_outcome_advantage(const float* rewards, const void* mask, int32_t m
                                const int32_t* group_offsets, const int32_t* group_members, int64_t B, int64_t R,
                                int64_t G, float epsilon, int32_t norm_adv_by_std, float* advantages, float* returns,
                                void* workspace, size_t workspace_bytes, void* stream) {
+  return drl_group_outcome_advantage(rewards, mask, mdt, row_group, group_offsets, group_members, B, R, G, DRL_ADV_GRPO,
+                                     epsilon, norm_adv_by_std, advantages, returns, workspace, workspace_bytes, stream);
+}
+
+size_t drl_group_outcome_advantage_workspace_bytes(int64_t B) {
+  return drl::round_up(static_cast<size_t>(B) * sizeof(float), 256) + 256;
+}
+
+int drl_group_outcome_advantage(const float* rewards, const void* mask, int32_t mdt, const int32_t* row_group,
+                                const int32_t* group_offsets, const int32_t* group_members, int64_t B, int64_t R,
+                                int64_t G, int32_t estimator, float epsilon, int32_t norm_adv_by_std,
+                                float* advantages, float* returns, void* workspace, size_t workspace_bytes,
+                                void* stream) {
   using namespace drl;
+  DRL_CHECK_ARG(estimator == DRL_ADV_GRPO || estimator == DRL_ADV_RLOO || estimator == DRL_ADV_REINFORCE_PP_BASELINE,
+                "unknown group estimator %d", estimator);
+  DRL_CHECK_ARG(estimator != DRL_ADV_REINFORCE_PP_BASELINE ||
+                    workspace_bytes >= drl_group_outcome_advantage_workspace_bytes(B),
+                "workspace too small for the whitening pass");
   DRL_CHECK_ARG(rewards && mask && row_group && group_offsets && group_members && advantages, "NULL input");
   DRL_CHECK_ARG(B >= 1 && R >= 1 && G >= 1 && G <= B, "bad shape B=%lld R=%lld G=%lld", (long long)B, (long long)R,
                 (long long)G);
@@ -137,11 +172,16 @@ int drl_grpo_outcome_advantage(const float* rewards, const void* mask, int32_t m
     return fail(DRL_ERR_WORKSPACE, "workspace too small");
   hipStream_t s = static_cast<hipStream_t>(stream);
   float* scores = static_cast<float*>(workspace);
+  int* err = reinterpret_cast<int*>(static_cast<char*>(workspace) + round_up(static_cast<size_t>(B) * sizeof(float), 256));
+  if (estimator == DRL_ADV_REINFORCE_PP_BASELINE) DRL_HIP(hipMemsetAsync(err, 0, sizeof(int), s));
   hipLaunchKernelGGL(row_sum_kernel, dim3((B + 3) / 4), dim3(256), 0, s, rewards, B, R, scores);
   DRL_LAUNCH_CHECK();
 #define DRL_GRPO(MDT)                                                                                              \
   hipLaunchKernelGGL(grpo_write_kernel<MDT>, dim3(B), dim3(256), 0, s, scores, mask, row_group, group_offsets,       \
-                     group_members, B, R, epsilon, norm_adv_by_std, advantages, returns)
+                     group_members, B, R, epsilon, norm_adv_by_std, advantages,                                   \
+                     estimator == DRL_ADV_REINFORCE_PP_BASELINE ? nullptr : returns, estimator);                   \
+  if (estimator == DRL_ADV_REINFORCE_PP_BASELINE)                                                                  \
+    hipLaunchKernelGGL(masked_whiten_kernel<MDT>, dim3(1), dim3(1024), 0, s, advantages, mask, B * R, err, returns, 1)
   switch (mdt) {
     case DRL_I64: DRL_GRPO(DRL_I64); break;
     case DRL_I32: DRL_GRPO(DRL_I32); break;

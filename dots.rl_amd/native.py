@@ -285,6 +285,25 @@ def grpo_outcome_advantage(token_level_rewards, response_mask, row_group, group_
     return adv, ret
 
 
+_GROUP_ESTIMATORS = {"grpo": 0, "rloo": 1, "reinforce_plus_plus_baseline": 2}
+
+
+def group_outcome_advantage(estimator, token_level_rewards, response_mask, row_group, group_offsets, group_members, G,
+                            epsilon=1e-6, norm_adv_by_std_in_grpo=True):
+    """K3 over the uid-group CSR for GRPO / RLOO / REINFORCE++-baseline (drl_group_outcome_advantage)."""
+    _dev(token_level_rewards, response_mask, row_group, group_offsets, group_members)
+    r, m = _c(token_level_rewards.float()), _c(response_mask)
+    B, R = r.shape
+    adv, ret = torch.empty_like(r), torch.empty_like(r)
+    L = lib()
+    ws = _ws.get(L.drl_group_outcome_advantage_workspace_bytes(B), r.device)
+    check(L.drl_group_outcome_advantage(_p(r), _p(m), mask_dtype_code(m), _p(_c(row_group)), _p(_c(group_offsets)),
+                                        _p(_c(group_members)), B, R, G, _GROUP_ESTIMATORS[estimator], float(epsilon),
+                                        int(bool(norm_adv_by_std_in_grpo)), _p(adv), _p(ret), _p(ws), ws.numel(),
+                                        _stream()), "drl_group_outcome_advantage")
+    return adv, ret
+
+
 def gae_advantage_return(token_level_rewards, values, response_mask, gamma, lam):
     _dev(token_level_rewards, values, response_mask)
     r, m = _c(token_level_rewards.float()), _c(response_mask)

@@ -152,6 +152,19 @@ int drl_grpo_outcome_advantage(const float* token_level_rewards, const void* res
                                int32_t norm_adv_by_std, float* advantages, float* returns, void* workspace,
                                size_t workspace_bytes, void* stream);
 
+/* K3 generalised to the other group-outcome estimators (same CSR of uid groups):
+ * DRL_ADV_RLOO = compute_rloo_outcome_advantage (core_algos.py:444-493),
+ * DRL_ADV_REINFORCE_PP_BASELINE = compute_reinforce_plus_plus_baseline_outcome_advantage (core_algos.py:392-441:
+ * group-mean baseline, then masked_whiten over the batch, times the mask; needs
+ * drl_group_outcome_advantage_workspace_bytes(B)). epsilon / norm_adv_by_std apply to GRPO only. */
+enum { DRL_ADV_GRPO = 0, DRL_ADV_RLOO = 1, DRL_ADV_REINFORCE_PP_BASELINE = 2 };
+size_t drl_group_outcome_advantage_workspace_bytes(int64_t B);
+int drl_group_outcome_advantage(const float* token_level_rewards, const void* response_mask, int32_t mask_dtype,
+                                const int32_t* row_group, const int32_t* group_offsets, const int32_t* group_members,
+                                int64_t B, int64_t R, int64_t G, int32_t estimator, float epsilon,
+                                int32_t norm_adv_by_std, float* advantages, float* returns, void* workspace,
+                                size_t workspace_bytes, void* stream);
+
 /* K5 — GAE + masked_whiten (core_algos.py:208-256, torch_functional.py:206-223). values (B, R) of
  * values_dtype: F32, or BF16 = the critic's autocast output as the reference stores it (then gamma * V(t+1)
  * is rounded to bf16 as the reference's bf16 tensor arithmetic does). */

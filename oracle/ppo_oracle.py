@@ -223,6 +223,37 @@ def grpo_outcome_advantage(token_level_rewards, response_mask, index, epsilon=1e
     return adv, adv
 
 
+def rloo_outcome_advantage(token_level_rewards, response_mask, index):
+    """core_algos.py:444-493: n > 1 -> s * n / (n - 1) - mean * n / (n - 1); a single sample keeps s."""
+    scores = np.asarray(token_level_rewards, np.float32).astype(f64).sum(-1)
+    groups: dict = {}
+    for i, u in enumerate(index):
+        groups.setdefault(u, []).append(i)
+    out = scores.copy()
+    for members in groups.values():
+        n = len(members)
+        if n > 1:
+            s = scores[members]
+            out[members] = s * n / (n - 1) - s.mean() * n / (n - 1)
+    adv = out[:, None] * np.asarray(response_mask, f64)
+    return adv, adv
+
+
+def reinforce_pp_baseline_outcome_advantage(token_level_rewards, response_mask, index):
+    """core_algos.py:392-441: s - group mean (0 for a single sample), broadcast x mask, masked_whiten, x mask."""
+    scores = np.asarray(token_level_rewards, np.float32).astype(f64).sum(-1)
+    groups: dict = {}
+    for i, u in enumerate(index):
+        groups.setdefault(u, []).append(i)
+    out = scores.copy()
+    for members in groups.values():
+        if len(members) > 1:
+            out[members] = scores[members] - scores[members].mean()
+    m = np.asarray(response_mask, f64)
+    adv = masked_whiten(out[:, None] * m, response_mask) * m
+    return adv, adv
+
+
 def group_ids(index):
     """uid strings -> dense int32 group ids in order of first appearance (the CSR the HIP kernel takes)."""
     ids, order = {}, []

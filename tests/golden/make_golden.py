@@ -20,6 +20,7 @@ Reference call sites (file:line under /root/reference):
   verl/workers/critic/dp_critic.py:57-145 values slice, compute_value_loss, loss.backward()
 * DAPO overlong-buffer reward : verl/workers/reward_manager/dapo.py:60-150 (stub tokenizer / preset scores)
 * Karmarkar-Karp balancing : verl/utils/seqlen_balancing.py:26-239 (partitions + imbalance metrics)
+* RLOO / REINFORCE++-baseline advantages : verl/trainer/ppo/core_algos.py:392-493
 * masked_mean known answers : tests/utils/test_torch_functional.py:55-66 (reference test, reproduced as data)
 """
 
@@ -649,6 +650,37 @@ def gen_seqlen():
     with open(path, "w") as f:
         json.dump({"cases": cases, "ref": "utils/seqlen_balancing.py:26-239"}, f)
     print(f"wrote {path} ({os.path.getsize(path)} bytes)")
+
+
+# --------------------------------------------------------------------------------------------
+# RLOO (core_algos.py:444-493) and REINFORCE++-baseline (core_algos.py:392-441) on the GRPO layouts
+# --------------------------------------------------------------------------------------------
+def gen_group_adv():
+    g = torch.Generator().manual_seed(101)
+    arrays, cases = {}, []
+    ci = 0
+    for name, sizes, shuffle in [("n8_interleaved", [8] * 8, False), ("ragged_with_singletons", [3, 1, 5, 1, 2, 4], True),
+                                 ("n4_shuffled", [4] * 6, True)]:
+        B, R = sum(sizes), 20
+        uid = np.concatenate([np.full(s, f"uid-{gi}", dtype=object) for gi, s in enumerate(sizes)])
+        if shuffle:
+            uid = uid[torch.randperm(B, generator=g).numpy()]
+        mask = torch.ones(B, R, dtype=torch.int64)
+        lengths = torch.randint(2, R + 1, (B,), generator=g)
+        for i in range(B):
+            mask[i, lengths[i]:] = 0
+        rewards = torch.zeros(B, R)
+        score = torch.bernoulli(torch.full((B,), 0.5), generator=g) + torch.randn(B, generator=g) * 0.1
+        for i in range(B):
+            rewards[i, lengths[i] - 1] = score[i]
+        for est, fn in [("rloo", ca.compute_rloo_outcome_advantage),
+                        ("reinforce_plus_plus_baseline", ca.compute_reinforce_plus_plus_baseline_outcome_advantage)]:
+            adv, ret = fn(token_level_rewards=rewards.clone(), response_mask=mask, index=uid)
+            arrays.update({f"c{ci}_rewards": rewards, f"c{ci}_mask": mask, f"c{ci}_uid": np.array([str(u) for u in uid]),
+                           f"c{ci}_adv": adv, f"c{ci}_ret": ret})
+            cases.append({"name": name, "estimator": est})
+            ci += 1
+    _save("group_adv.npz", arrays, {"cases": cases, "ref": "core_algos.py:392-493"})
 
 
 if __name__ == "__main__":

@@ -242,6 +242,19 @@ def test_grpo_matches_reference_golden(golden):
         np.testing.assert_allclose(ret.cpu().numpy(), z[f"c{ci}_ret"], rtol=1e-5, atol=1e-6)
 
 
+def test_rloo_and_reinforce_pp_baseline_match_reference_golden(golden):
+    from dots.rl_amd import core_algos
+
+    z, meta = golden("group_adv.npz")
+    fns = {"rloo": core_algos.compute_rloo_outcome_advantage,
+           "reinforce_plus_plus_baseline": core_algos.compute_reinforce_plus_plus_baseline_outcome_advantage}
+    assert core_algos.get_adv_estimator_fn("rloo") is fns["rloo"]
+    for ci, c in enumerate(meta["cases"]):
+        adv, ret = fns[c["estimator"]](T(z[f"c{ci}_rewards"]), T(z[f"c{ci}_mask"]), list(z[f"c{ci}_uid"]))
+        np.testing.assert_allclose(adv.cpu().numpy(), z[f"c{ci}_adv"], rtol=2e-5, atol=2e-6, err_msg=str(c))
+        np.testing.assert_allclose(ret.cpu().numpy(), z[f"c{ci}_ret"], rtol=2e-5, atol=2e-6, err_msg=str(c))
+
+
 def test_gae_matches_reference_golden(golden):
     z, meta = golden("gae.npz")
     for ci, cfg in enumerate(meta["cases"]):

@@ -52,6 +52,15 @@ def test_grpo_matches_reference(golden):
         np.testing.assert_allclose(ret, z[f"c{ci}_ret"], rtol=2e-5, atol=2e-6, err_msg=str(cfg))
 
 
+def test_rloo_and_reinforce_pp_baseline_match_reference(golden):
+    z, meta = golden("group_adv.npz")
+    fns = {"rloo": oracle.rloo_outcome_advantage, "reinforce_plus_plus_baseline": oracle.reinforce_pp_baseline_outcome_advantage}
+    for ci, c in enumerate(meta["cases"]):
+        adv, ret = fns[c["estimator"]](z[f"c{ci}_rewards"], z[f"c{ci}_mask"], list(z[f"c{ci}_uid"]))
+        np.testing.assert_allclose(adv, z[f"c{ci}_adv"], rtol=2e-5, atol=2e-6, err_msg=str(c))
+        np.testing.assert_allclose(ret, z[f"c{ci}_ret"], rtol=2e-5, atol=2e-6, err_msg=str(c))
+
+
 def test_gae_matches_reference(golden):
     z, meta = golden("gae.npz")
     for ci, cfg in enumerate(meta["cases"]):
