@@ -182,7 +182,9 @@ def main():
         _, per_unit, bound, peak, unit = ROOFLINE[args.roofline_kernel]
         scale = 1e12 if unit == "TFLOP/s" else 1e9
         achieved = b_launch / t_launch / scale if n_launch else None
-        traffic, traffic_src = _pmc_traffic(args.roofline_kernel)
+        # the committed PMC pass is of the default workload (N=1 config #2): attach it only to that workload
+        default_workload = not args.tiny and not args.override and args.gpus == 1
+        traffic, traffic_src = _pmc_traffic(args.roofline_kernel) if default_workload else (None, None)
         roofline = {"kernel": args.roofline_kernel, "bound": bound, "achieved": achieved, "peak": peak,
                     "unit": unit, "frac": achieved / peak if achieved else None, "traffic": traffic,
                     "algorithmic_work_per_launch": b_launch if n_launch else None,
