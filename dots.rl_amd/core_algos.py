@@ -158,6 +158,14 @@ def compute_reinforce_plus_plus_baseline_outcome_advantage(token_level_rewards, 
                                               row_group, offsets, members, G)
 
 
+@register_adv_est(AdvantageEstimator.REINFORCE_PLUS_PLUS)
+def compute_reinforce_plus_plus_outcome_advantage(token_level_rewards, response_mask, config=None, **kwargs):
+    """core_algos.py:550-586 — masked discounted return scan + masked_whiten (K5 scan mode)."""
+    assert config is not None
+    with torch.no_grad():
+        return native.reinforce_pp_advantage_return(token_level_rewards, response_mask, float(config.gamma))
+
+
 # ---------------------------------------------------------------------------------------------- losses
 def agg_loss(loss_mat, loss_mask, loss_agg_mode: str):
     """core_algos.py:703-736 (forward; gradients flow through fused_actor_loss)."""

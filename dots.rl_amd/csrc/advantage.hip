@@ -91,6 +91,24 @@ __global__ __launch_bounds__(256) void gae_scan_kernel(const float* r, const voi
   }
 }
 
+// REINFORCE++ discounted return scan, one thread per row (core_algos.py:573-578): running = r + gamma *
+// running, returns[t] = running, then running *= mask[t] (a masked token resets the carry); adv starts as a
+// copy of the returns and is whitened + masked in place by masked_whiten_kernel.
+template <int MDT>
+__global__ __launch_bounds__(256) void rfpp_scan_kernel(const float* r, const void* mask, int64_t B, int64_t R,
+                                                        float gamma, float* adv, float* ret) {
+  const int64_t row = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (row >= B) return;
+  float running = 0.f;
+  for (int64_t t = R - 1; t >= 0; --t) {
+    const int64_t i = row * R + t;
+    running = r[i] + gamma * running;
+    ret[i] = running;
+    adv[i] = running;
+    running = running * mask_at<MDT>(mask, i);
+  }
+}
+
 // masked_whiten over the whole (B, R) tensor in place: mean, unbiased var, (x - mean) * rsqrt(var + 1e-8).
 // One workgroup (the tensor is one PPO batch of advantages, a few MB); three ordered passes.
 template <int MDT>
@@ -227,6 +245,33 @@ int drl_gae_advantage_return(const float* rewards, const void* values, int32_t v
     default: DRL_GAE(DRL_F32); break;
   }
 #undef DRL_GAE
+  DRL_LAUNCH_CHECK();
+  return DRL_OK;
+}
+
+int drl_reinforce_pp_advantage_return(const float* rewards, const void* mask, int32_t mdt, int64_t B, int64_t R,
+                                      float gamma, float* advantages, float* returns, void* workspace,
+                                      size_t workspace_bytes, void* stream) {
+  using namespace drl;
+  DRL_CHECK_ARG(rewards && mask && advantages && returns, "NULL input");
+  DRL_CHECK_ARG(B >= 1 && R >= 1, "bad shape");
+  DRL_CHECK_ARG(mdt == DRL_I64 || mdt == DRL_I32 || mdt == DRL_U8 || mdt == DRL_F32, "bad mask dtype");
+  if (workspace == nullptr || workspace_bytes < drl_gae_workspace_bytes(B, R))
+    return fail(DRL_ERR_WORKSPACE, "workspace too small");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  int* err = static_cast<int*>(workspace);
+  DRL_HIP(hipMemsetAsync(err, 0, sizeof(int), s));
+#define DRL_RFPP(MDT)                                                                                             \
+  hipLaunchKernelGGL(rfpp_scan_kernel<MDT>, dim3((B + 255) / 256), dim3(256), 0, s, rewards, mask, B, R, gamma,     \
+                     advantages, returns);                                                                         \
+  hipLaunchKernelGGL(masked_whiten_kernel<MDT>, dim3(1), dim3(1024), 0, s, advantages, mask, B * R, err, nullptr, 1)
+  switch (mdt) {
+    case DRL_I64: DRL_RFPP(DRL_I64); break;
+    case DRL_I32: DRL_RFPP(DRL_I32); break;
+    case DRL_U8: DRL_RFPP(DRL_U8); break;
+    default: DRL_RFPP(DRL_F32); break;
+  }
+#undef DRL_RFPP
   DRL_LAUNCH_CHECK();
   return DRL_OK;
 }

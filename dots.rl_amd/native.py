@@ -304,6 +304,18 @@ def group_outcome_advantage(estimator, token_level_rewards, response_mask, row_g
     return adv, ret
 
 
+def reinforce_pp_advantage_return(token_level_rewards, response_mask, gamma):
+    _dev(token_level_rewards, response_mask)
+    r, m = _c(token_level_rewards.float()), _c(response_mask)
+    B, R = r.shape
+    adv, ret = torch.empty_like(r), torch.empty_like(r)
+    L = lib()
+    ws = _ws.get(L.drl_gae_workspace_bytes(B, R), r.device)
+    check(L.drl_reinforce_pp_advantage_return(_p(r), _p(m), mask_dtype_code(m), B, R, float(gamma), _p(adv), _p(ret),
+                                              _p(ws), ws.numel(), _stream()), "drl_reinforce_pp_advantage_return")
+    return adv, ret
+
+
 def gae_advantage_return(token_level_rewards, values, response_mask, gamma, lam):
     _dev(token_level_rewards, values, response_mask)
     r, m = _c(token_level_rewards.float()), _c(response_mask)

@@ -165,6 +165,12 @@ int drl_group_outcome_advantage(const float* token_level_rewards, const void* re
                                 int32_t norm_adv_by_std, float* advantages, float* returns, void* workspace,
                                 size_t workspace_bytes, void* stream);
 
+/* REINFORCE++ (core_algos.py:550-586): returns = masked discounted reward-to-go (a masked token resets the
+ * carry), advantages = masked_whiten(returns) * mask. workspace: drl_gae_workspace_bytes(B, R). */
+int drl_reinforce_pp_advantage_return(const float* token_level_rewards, const void* response_mask, int32_t mask_dtype,
+                                      int64_t B, int64_t R, float gamma, float* advantages, float* returns,
+                                      void* workspace, size_t workspace_bytes, void* stream);
+
 /* K5 — GAE + masked_whiten (core_algos.py:208-256, torch_functional.py:206-223). values (B, R) of
  * values_dtype: F32, or BF16 = the critic's autocast output as the reference stores it (then gamma * V(t+1)
  * is rounded to bf16 as the reference's bf16 tensor arithmetic does). */

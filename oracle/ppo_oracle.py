@@ -254,6 +254,21 @@ def reinforce_pp_baseline_outcome_advantage(token_level_rewards, response_mask, 
     return adv, adv
 
 
+def reinforce_pp_advantage_return(token_level_rewards, response_mask, gamma):
+    """core_algos.py:550-586 (float32 scan in the reference's order)."""
+    r = np.asarray(token_level_rewards, np.float32)
+    m = np.asarray(response_mask, np.float32)
+    B, T = r.shape
+    ret = np.zeros((B, T), np.float32)
+    running = np.zeros(B, np.float32)
+    for t in reversed(range(T)):
+        running = r[:, t] + np.float32(gamma) * running
+        ret[:, t] = running
+        running = running * m[:, t]
+    adv = masked_whiten(ret.astype(f64), response_mask) * m
+    return adv, ret.astype(f64)
+
+
 def group_ids(index):
     """uid strings -> dense int32 group ids in order of first appearance (the CSR the HIP kernel takes)."""
     ids, order = {}, []

@@ -683,6 +683,23 @@ def gen_group_adv():
     _save("group_adv.npz", arrays, {"cases": cases, "ref": "core_algos.py:392-493"})
 
 
+def gen_rfpp():
+    """REINFORCE++ (core_algos.py:550-586): masked discounted returns + masked_whiten."""
+    g = torch.Generator().manual_seed(103)
+    arrays, cases = {}, []
+    for ci, (B, R, gamma, obs) in enumerate([(6, 20, 1.0, False), (8, 33, 0.99, True), (3, 9, 0.9, True)]):
+        rewards = torch.randn(B, R, generator=g) * (torch.rand(B, R, generator=g) > 0.7)
+        mask = torch.ones(B, R, dtype=torch.int64)
+        for i in range(B):
+            mask[i, int(torch.randint(2, R + 1, (1,), generator=g)):] = 0
+        if obs:
+            mask[:, 1] = 0  # observation tokens inside the response reset the carry
+        adv, ret = ca.compute_reinforce_plus_plus_outcome_advantage(rewards, mask, config=DictConfig(gamma=gamma))
+        arrays.update({f"c{ci}_rewards": rewards, f"c{ci}_mask": mask, f"c{ci}_adv": adv, f"c{ci}_ret": ret})
+        cases.append({"gamma": gamma})
+    _save("rfpp.npz", arrays, {"cases": cases, "ref": "core_algos.py:550-586"})
+
+
 if __name__ == "__main__":
     which = sys.argv[1:] or ["ppo_loss", "masked_mean", "grpo", "gae", "logprob", "fused_linear", "masks", "tiny_qwen2"]
     for w in which:

@@ -255,6 +255,19 @@ def test_rloo_and_reinforce_pp_baseline_match_reference_golden(golden):
         np.testing.assert_allclose(ret.cpu().numpy(), z[f"c{ci}_ret"], rtol=2e-5, atol=2e-6, err_msg=str(c))
 
 
+def test_reinforce_pp_matches_reference_golden(golden):
+    from dots.rl_amd import core_algos
+    from dots.rl_amd.config import to_attr
+
+    z, meta = golden("rfpp.npz")
+    fn = core_algos.get_adv_estimator_fn("reinforce_plus_plus")
+    for ci, c in enumerate(meta["cases"]):
+        adv, ret = fn(token_level_rewards=T(z[f"c{ci}_rewards"]), response_mask=T(z[f"c{ci}_mask"]),
+                      config=to_attr({"gamma": c["gamma"]}))
+        np.testing.assert_allclose(adv.cpu().numpy(), z[f"c{ci}_adv"], rtol=2e-5, atol=2e-6)
+        np.testing.assert_allclose(ret.cpu().numpy(), z[f"c{ci}_ret"], rtol=1e-6, atol=1e-7)
+
+
 def test_gae_matches_reference_golden(golden):
     z, meta = golden("gae.npz")
     for ci, cfg in enumerate(meta["cases"]):

@@ -61,6 +61,14 @@ def test_rloo_and_reinforce_pp_baseline_match_reference(golden):
         np.testing.assert_allclose(ret, z[f"c{ci}_ret"], rtol=2e-5, atol=2e-6, err_msg=str(c))
 
 
+def test_reinforce_pp_matches_reference(golden):
+    z, meta = golden("rfpp.npz")
+    for ci, c in enumerate(meta["cases"]):
+        adv, ret = oracle.reinforce_pp_advantage_return(z[f"c{ci}_rewards"], z[f"c{ci}_mask"], c["gamma"])
+        np.testing.assert_allclose(adv, z[f"c{ci}_adv"], rtol=2e-5, atol=2e-6)
+        np.testing.assert_allclose(ret, z[f"c{ci}_ret"], rtol=1e-6, atol=1e-7)
+
+
 def test_gae_matches_reference(golden):
     z, meta = golden("gae.npz")
     for ci, cfg in enumerate(meta["cases"]):
