@@ -39,6 +39,7 @@ class PPOLossParams(ctypes.Structure):
         ("loss_agg_mode", ctypes.c_int32),
         ("kl_type", ctypes.c_int32),
         ("token_count", ctypes.c_void_p),
+        ("policy_loss", ctypes.c_int32),
     ]
 
 

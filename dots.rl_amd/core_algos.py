@@ -207,7 +207,7 @@ class _FusedActorLoss(torch.autograd.Function):
 
 def fused_actor_loss(log_prob, entropy, old_log_prob, advantages, response_mask, ref_log_prob, *, clip_ratio_low,
                      clip_ratio_high, clip_ratio_c, entropy_coeff, use_kl_loss, kl_loss_type, kl_loss_coef,
-                     loss_agg_mode, loss_scale_factor):
+                     loss_agg_mode, loss_scale_factor, policy_loss="vanilla"):
     """The whole per-micro-batch loss of dp_actor.py:419-466 in one HIP launch.
 
     Returns a float32[8] tensor: pg_loss, pg_clipfrac, ppo_kl, pg_clipfrac_lower, entropy_loss, kl_loss,
@@ -217,7 +217,7 @@ def fused_actor_loss(log_prob, entropy, old_log_prob, advantages, response_mask,
               entropy_coeff=entropy_coeff if entropy is not None else 0.0,
               kl_loss_coef=kl_loss_coef if use_kl_loss else 0.0,
               kl_loss_type=kl_loss_type if use_kl_loss else None, loss_agg_mode=loss_agg_mode,
-              loss_scale_factor=loss_scale_factor)
+              loss_scale_factor=loss_scale_factor, policy_loss=policy_loss)
     return _FusedActorLoss.apply(log_prob, entropy, old_log_prob, advantages, response_mask,
                                  ref_log_prob if use_kl_loss else None, kw)
 
@@ -237,6 +237,16 @@ def compute_policy_loss_vanilla(old_log_prob, log_prob, advantages, response_mas
                            clip_ratio_high=hi, clip_ratio_c=c, entropy_coeff=0.0, use_kl_loss=False,
                            kl_loss_type=None, kl_loss_coef=0.0, loss_agg_mode=loss_agg_mode, loss_scale_factor=1.0)
     # out[6] == pg_loss here (no entropy / KL term, scale 1) and is the differentiable slot
+    return out[6], out[1].detach(), out[2].detach(), out[3].detach()
+
+
+@register_policy_loss("gpg")
+def compute_policy_loss_gpg(old_log_prob, log_prob, advantages, response_mask, loss_agg_mode="token-mean", config=None):
+    """core_algos.py:957-975 — pg = -log_prob * advantages (K1, GPG mode); clip metrics are 0."""
+    out = fused_actor_loss(log_prob, None, old_log_prob, advantages, response_mask, None, clip_ratio_low=0.2,
+                           clip_ratio_high=0.2, clip_ratio_c=3.0, entropy_coeff=0.0, use_kl_loss=False,
+                           kl_loss_type=None, kl_loss_coef=0.0, loss_agg_mode=loss_agg_mode, loss_scale_factor=1.0,
+                           policy_loss="gpg")
     return out[6], out[1].detach(), out[2].detach(), out[3].detach()
 
 

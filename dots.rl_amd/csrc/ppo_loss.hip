@@ -64,6 +64,7 @@ struct Args {
   int64_t N, B, R;
   float lo, hi, clip_c, ent_coef, kl_coef, lsf;
   int mode, kl;
+  int policy;  // DRL_POLICY_*
 };
 
 template <int MDT, bool NT = true>
@@ -287,8 +288,10 @@ __global__ __launch_bounds__(kThreads) void ppo_loss_kernel(Args a) {
       const float C2 = fminf(L3, C1);
       const float wc = C1 < L3 ? 1.f : (C1 == L3 ? 0.5f : 0.f);
       const bool neg = A[j] < 0.f;
-      const float pg = neg ? C2 : C1;
-      const float dpg = (neg ? wc * dC1 : dC1) * ratio * gate;
+      const bool gpg = a.policy == DRL_POLICY_GPG;  // uniform per launch
+      // GPG (core_algos.py:957-975): pg = -log_prob * advantages, d pg / d log_prob = -A
+      const float pg = gpg ? (-lp[j]) * A[j] : (neg ? C2 : C1);
+      const float dpg = gpg ? -A[j] : (neg ? wc * dC1 : dC1) * ratio * gate;
 
       const float mj = valid ? m[j] : 0.f;
       const bool mb = mj != 0.f;
@@ -309,9 +312,11 @@ __global__ __launch_bounds__(kThreads) void ppo_loss_kernel(Args a) {
       if (valid) {
         s_pg += agg_val(pg);
         s_cnt += mj;
-        s_clip += (mb && L2 > L1) ? mj : 0.f;
-        s_kl += mb ? -nkl * mj : 0.f;
-        s_cliplow += (mb && C1 > L3 && neg) ? mj : 0.f;
+        if (!gpg) {  // GPG reports clipfrac / ppo_kl / clipfrac_lower as 0
+          s_clip += (mb && L2 > L1) ? mj : 0.f;
+          s_kl += mb ? -nkl * mj : 0.f;
+          s_cliplow += (mb && C1 > L3 && neg) ? mj : 0.f;
+        }
       }
       float gl = w * dpg;
       if (has_kl) {
@@ -527,7 +532,8 @@ int drl_ppo_loss_fwd_bwd(const float* old_log_prob, const float* log_prob, const
   DRL_CHECK_ARG(p->kl_type >= DRL_KL_NONE && p->kl_type <= DRL_KL_K3, "bad kl_type %d", p->kl_type);
   DRL_CHECK_ARG(p->kl_type == DRL_KL_NONE || ref_log_prob != nullptr, "kl_type set but ref_log_prob is NULL");
   DRL_CHECK_ARG(p->entropy_coeff == 0.f || entropy != nullptr, "entropy_coeff != 0 but entropy is NULL");
-  DRL_CHECK_ARG(p->clip_ratio_c > 1.f, "clip_ratio_c must be > 1.0 (dual-clip PPO), got %f", p->clip_ratio_c);
+  DRL_CHECK_ARG(p->policy_loss == DRL_POLICY_GPG || p->clip_ratio_c > 1.f,
+                "clip_ratio_c must be > 1.0 (dual-clip PPO), got %f", p->clip_ratio_c);
   DRL_CHECK_ARG(mask_dtype == DRL_I64 || mask_dtype == DRL_I32 || mask_dtype == DRL_U8 || mask_dtype == DRL_F32,
                 "unsupported mask dtype %d", mask_dtype);
   const void* ptrs[] = {old_log_prob, log_prob, advantages, response_mask, entropy, ref_log_prob, dlog_prob, dentropy};
@@ -552,6 +558,9 @@ int drl_ppo_loss_fwd_bwd(const float* old_log_prob, const float* log_prob, const
   a.clip_c = p->clip_ratio_c; a.ent_coef = p->entropy_coeff; a.kl_coef = p->kl_loss_coef;
   a.lsf = p->loss_scale_factor; a.mode = p->loss_agg_mode; a.kl = p->kl_type;
   a.token_count = p->loss_agg_mode == DRL_AGG_TOKEN_MEAN ? p->token_count : nullptr;
+  DRL_CHECK_ARG(p->policy_loss == DRL_POLICY_VANILLA || p->policy_loss == DRL_POLICY_GPG, "bad policy_loss %d",
+                p->policy_loss);
+  a.policy = p->policy_loss;
 
   hipStream_t s = static_cast<hipStream_t>(stream);
   DRL_HIP(hipMemsetAsync(ws, 0, sizeof(Header), s));

@@ -192,8 +192,9 @@ class DataParallelPPOActor:
         data = data.select(batch_keys=keys)
         mini_batches = data.split(cfg.ppo_mini_batch_size)
         loss_mode = cfg.policy_loss.get("loss_mode", "vanilla")
-        if loss_mode != "vanilla":
-            raise NotImplementedError(f"policy loss {loss_mode}: only the vanilla (PPO clip + dual clip) loss is fused")
+        if loss_mode not in ("vanilla", "gpg"):
+            raise NotImplementedError(f"policy loss {loss_mode}: the fused K1 modes are vanilla (PPO clip + dual clip) "
+                                      "and gpg")
         lo = cfg.clip_ratio_low if cfg.get("clip_ratio_low") is not None else cfg.clip_ratio
         hi = cfg.clip_ratio_high if cfg.get("clip_ratio_high") is not None else cfg.clip_ratio
         mb_out, mb_lsf, grad_norms = [], [], []
@@ -220,7 +221,7 @@ class DataParallelPPOActor:
                         mb.get("ref_log_prob"), clip_ratio_low=lo, clip_ratio_high=hi,
                         clip_ratio_c=cfg.get("clip_ratio_c", 3.0), entropy_coeff=cfg.entropy_coeff,
                         use_kl_loss=cfg.use_kl_loss, kl_loss_type=cfg.kl_loss_type, kl_loss_coef=cfg.kl_loss_coef,
-                        loss_agg_mode=cfg.loss_agg_mode, loss_scale_factor=lsf)
+                        loss_agg_mode=cfg.loss_agg_mode, loss_scale_factor=lsf, policy_loss=loss_mode)
                     out[6].backward()
                     mb_out.append(out.detach())
                     mb_lsf.append(lsf)

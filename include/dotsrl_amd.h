@@ -90,7 +90,13 @@ typedef struct drl_ppo_loss_params {
    * runs as ONE pass (the mask is read once, in the loss pass) instead of the count pass + loss pass.
    * NULL = K1 counts the mask itself. */
   const double* token_count;
+  /* policy loss (actor.policy_loss.loss_mode, get_policy_loss_fn core_algos.py:68-83): DRL_POLICY_VANILLA =
+   * compute_policy_loss_vanilla (PPO clip + dual clip, :815-889), DRL_POLICY_GPG = compute_policy_loss_gpg
+   * (pg = -log_prob * advantages, :957-975; clipfrac / ppo_kl / clipfrac_lower reported as 0). */
+  int32_t policy_loss;
 } drl_ppo_loss_params;
+
+enum { DRL_POLICY_VANILLA = 0, DRL_POLICY_GPG = 1 };
 
 enum {
   DRL_PPO_OUT_PG_LOSS = 0,

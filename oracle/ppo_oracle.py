@@ -182,10 +182,20 @@ def clip_boundary_tokens(old_log_prob, log_prob, advantages, response_mask, clip
 
 def actor_loss(old_log_prob, log_prob, advantages, response_mask, entropy, ref_log_prob, *, loss_agg_mode,
                clip_ratio_low, clip_ratio_high, clip_ratio_c, entropy_coeff, use_kl_loss, kl_loss_type,
-               kl_loss_coef, loss_scale_factor):
-    """The per-micro-batch loss of DataParallelPPOActor.update_policy (dp_actor.py:419-466)."""
-    pg_loss, clipfrac, ppo_kl, clipfrac_lower, _, dpg = policy_loss_vanilla(
-        old_log_prob, log_prob, advantages, response_mask, loss_agg_mode, clip_ratio_low, clip_ratio_high, clip_ratio_c)
+               kl_loss_coef, loss_scale_factor, policy_loss="vanilla"):
+    """The per-micro-batch loss of DataParallelPPOActor.update_policy (dp_actor.py:419-466).
+    policy_loss "gpg": compute_policy_loss_gpg (core_algos.py:957-975), pg = -log_prob * advantages."""
+    if policy_loss == "gpg":
+        lp32 = np.asarray(log_prob, np.float32)
+        A32 = np.asarray(advantages, np.float32)
+        pg_losses = ((-lp32) * A32).astype(f64)
+        pg_loss = agg_loss(pg_losses, response_mask, loss_agg_mode)
+        clipfrac = ppo_kl = clipfrac_lower = 0.0
+        dpg = -A32.astype(f64)
+    else:
+        pg_loss, clipfrac, ppo_kl, clipfrac_lower, _, dpg = policy_loss_vanilla(
+            old_log_prob, log_prob, advantages, response_mask, loss_agg_mode, clip_ratio_low, clip_ratio_high,
+            clip_ratio_c)
     w = agg_loss_grad(response_mask, loss_agg_mode)
     entropy_loss = agg_loss(entropy, response_mask, loss_agg_mode)
     total = pg_loss - entropy_loss * entropy_coeff if entropy_coeff != 0 else pg_loss

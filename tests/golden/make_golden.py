@@ -700,6 +700,36 @@ def gen_rfpp():
     _save("rfpp.npz", arrays, {"cases": cases, "ref": "core_algos.py:550-586"})
 
 
+def gen_gpg_loss():
+    """GPG policy loss (core_algos.py:957-975) composed as dp_actor.py:419-466 composes any registered loss."""
+    g = torch.Generator().manual_seed(4321)
+    arrays, cases = {}, []
+    pg_fn = ca.get_policy_loss_fn("gpg")
+    for ci, (shape, kind, mode, kl, ent_c, lsf) in enumerate([((6, 16), "edges", "token-mean", "low_var_kl", 0.001, 0.5),
+                                                              ((8, 64), "random", "seq-mean-token-mean", "kl", 0.0, 1.0),
+                                                              ((5, 33), "edges", "seq-mean-token-sum", "mse", 0.01, 0.25),
+                                                              ((4, 40), "random", "seq-mean-token-sum-norm", "abs", 0.0, 1.0)]):
+        old, logp, adv, mask, ent, ref = ppo_loss_inputs(g, *shape, kind)
+        lp = logp.clone().requires_grad_(True)
+        en = ent.clone().requires_grad_(True)
+        pg_loss, c1, c2, c3 = pg_fn(old_log_prob=old, log_prob=lp, advantages=adv, response_mask=mask,
+                                    loss_agg_mode=mode, config=None)
+        entropy_loss = ca.agg_loss(loss_mat=en, loss_mask=mask, loss_agg_mode=mode)
+        policy_loss = pg_loss - entropy_loss * ent_c if ent_c != 0 else pg_loss
+        kld = ca.kl_penalty(logprob=lp, ref_logprob=ref, kl_penalty=kl)
+        kl_loss = ca.agg_loss(loss_mat=kld, loss_mask=mask, loss_agg_mode=mode)
+        loss = (policy_loss + kl_loss * 0.001) * lsf
+        loss.backward()
+        for k, v in dict(old_log_prob=old, log_prob=logp, advantages=adv, response_mask=mask, entropy=ent,
+                         ref_log_prob=ref, out_pg_loss=pg_loss.detach(), out_loss=loss.detach(),
+                         out_dlogp=lp.grad, out_dentropy=en.grad if en.grad is not None else torch.zeros_like(en),
+                         out_clip=torch.tensor([float(c1), float(c2), float(c3)])).items():
+            arrays[f"c{ci}_{k}"] = v
+        cases.append(dict(loss_agg_mode=mode, kl_loss_type=kl, entropy_coeff=ent_c, kl_loss_coef=0.001,
+                          loss_scale_factor=lsf, use_kl_loss=True))
+    _save("gpg_loss.npz", arrays, {"cases": cases, "ref": "core_algos.py:957-975; dp_actor.py:419-466"})
+
+
 if __name__ == "__main__":
     which = sys.argv[1:] or ["ppo_loss", "masked_mean", "grpo", "gae", "logprob", "fused_linear", "masks", "tiny_qwen2"]
     for w in which:

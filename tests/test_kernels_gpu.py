@@ -268,6 +268,25 @@ def test_reinforce_pp_matches_reference_golden(golden):
         np.testing.assert_allclose(ret.cpu().numpy(), z[f"c{ci}_ret"], rtol=1e-6, atol=1e-7)
 
 
+def test_gpg_actor_loss_matches_reference_golden(golden):
+    """K1 in GPG mode (policy_loss.loss_mode=gpg) vs the reference's compute_policy_loss_gpg composed into the
+    dp_actor total loss (entropy bonus, KL, loss scale) and its autograd gradients."""
+    z, meta = golden("gpg_loss.npz")
+    for ci, c in enumerate(meta["cases"]):
+        g = lambda k: T(z[f"c{ci}_{k}"])  # noqa: E731
+        out, dlp, dent = native.ppo_loss_fwd_bwd(
+            g("old_log_prob"), g("log_prob"), g("advantages"), g("response_mask"), g("entropy"), g("ref_log_prob"),
+            entropy_coeff=c["entropy_coeff"], kl_loss_coef=c["kl_loss_coef"], kl_loss_type=c["kl_loss_type"],
+            loss_agg_mode=c["loss_agg_mode"], loss_scale_factor=c["loss_scale_factor"], want_dentropy=True,
+            policy_loss="gpg")
+        o = out.cpu().numpy()
+        np.testing.assert_allclose(o[0], z[f"c{ci}_out_pg_loss"], rtol=1e-5, atol=1e-7)
+        np.testing.assert_allclose(o[6], z[f"c{ci}_out_loss"], rtol=1e-5, atol=1e-7)
+        assert o[1] == 0 and o[2] == 0 and o[3] == 0
+        np.testing.assert_allclose(dlp.cpu().numpy(), z[f"c{ci}_out_dlogp"], rtol=2e-5, atol=1e-9)
+        np.testing.assert_allclose(dent.cpu().numpy(), z[f"c{ci}_out_dentropy"], rtol=2e-5, atol=1e-9)
+
+
 def test_gae_matches_reference_golden(golden):
     z, meta = golden("gae.npz")
     for ci, cfg in enumerate(meta["cases"]):

@@ -32,6 +32,20 @@ def test_ppo_actor_loss_matches_reference(golden):
         np.testing.assert_allclose(out["kld"], g("out_kld"), rtol=1e-5, atol=1e-6, err_msg=f"case {ci} kld")
 
 
+def test_gpg_actor_loss_matches_reference(golden):
+    z, meta = golden("gpg_loss.npz")
+    for ci, c in enumerate(meta["cases"]):
+        g = lambda k: z[f"c{ci}_{k}"]  # noqa: E731
+        r = oracle.actor_loss(g("old_log_prob"), g("log_prob"), g("advantages"), g("response_mask"), g("entropy"),
+                              g("ref_log_prob"), clip_ratio_low=0.2, clip_ratio_high=0.2, clip_ratio_c=3.0,
+                              policy_loss="gpg", **c)
+        np.testing.assert_allclose(r["pg_loss"], g("out_pg_loss"), rtol=1e-5, atol=1e-7)
+        np.testing.assert_allclose(r["loss"], g("out_loss"), rtol=1e-5, atol=1e-7)
+        np.testing.assert_allclose(r["dlogp"], g("out_dlogp"), rtol=2e-5, atol=1e-9)
+        np.testing.assert_allclose(r["dentropy"], g("out_dentropy"), rtol=2e-5, atol=1e-9)
+        assert (g("out_clip") == 0).all()
+
+
 def test_masked_mean_known_answers(golden):
     z, _ = golden("masked_mean.npz")
     # tests/utils/test_torch_functional.py:55-66 — NaN outside the mask is ignored
