@@ -58,7 +58,8 @@ QWEN25_7B = dict(
 RANDOM_MODELS = {"qwen2.5-0.5b": QWEN25_05B, "llama-3-8b": LLAMA3_8B, "qwen2.5-7b": QWEN25_7B}
 
 DEFAULTS = dict(
-    data=dict(train_batch_size=64, max_prompt_length=512, max_response_length=256, seed=1234),
+    data=dict(train_batch_size=64, max_prompt_length=512, max_response_length=256, seed=1234,
+              reward_fn_key="data_source"),
     actor_rollout_ref=dict(
         hybrid_engine=True,
         model=dict(path="random:qwen2.5-0.5b", override_config={}, use_remove_padding=False, use_fused_kernels=False,

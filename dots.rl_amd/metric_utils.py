@@ -23,35 +23,51 @@ def _response_info(batch: DataProto):
 
 
 def compute_data_metrics(batch: DataProto, use_critic: bool = False) -> dict[str, Any]:
-    """metric_utils.py:80-224 (critic entries only when use_critic)."""
+    """metric_utils.py:80-224: score / reward statistics over the non-aborted rows (response length > 0),
+    advantages / returns (/ values) over the response mask, response and prompt length statistics. Every
+    statistic is reduced on the device and read back in one copy."""
     b = batch.batch
     seq_score = b["token_level_scores"].sum(-1)
     seq_reward = b["token_level_rewards"].sum(-1)
     R = b["responses"].shape[-1]
     info = _response_info(batch)
     rmask = b["response_mask"].bool()
+    resp_len, prompt_len = info["response_length"], info["prompt_length"]
+    non_aborted = resp_len != 0
+    if not bool(non_aborted.any()):
+        raise ValueError("All samples are aborted, this should not happen.")
+    sc, rw, rl = seq_score[non_aborted], seq_reward[non_aborted], resp_len[non_aborted]
     adv = torch.masked_select(b["advantages"], rmask)
     ret = torch.masked_select(b["returns"], rmask)
     P = b["attention_mask"].shape[-1] - R
+
+    def mmm(x):
+        return [x.mean(), x.max(), x.min()]
+
     vals = torch.stack([
-        seq_score.mean(), seq_score.max(), seq_score.min(), seq_reward.mean(), seq_reward.max(), seq_reward.min(),
-        adv.mean(), adv.max(), adv.min(), ret.mean(), ret.max(), ret.min(),
-        info["response_length"].mean(), info["response_length"].max(), info["response_length"].min(),
-        (info["response_length"] == R).float().mean(),
-        info["prompt_length"].mean(), info["prompt_length"].max(), info["prompt_length"].min(),
-        (info["prompt_length"] == P).float().mean()]).cpu().tolist()
+        *mmm(sc), *mmm(rw), *mmm(adv.float()), *mmm(ret.float()),
+        *mmm(resp_len), (resp_len == R).float().mean(),
+        *mmm(rl), (rl == R).float().mean(), (~non_aborted).float().mean(),
+        *mmm(prompt_len), (prompt_len == P).float().mean()]).cpu().tolist()
     keys = ["critic/score/mean", "critic/score/max", "critic/score/min", "critic/rewards/mean", "critic/rewards/max",
             "critic/rewards/min", "critic/advantages/mean", "critic/advantages/max", "critic/advantages/min",
             "critic/returns/mean", "critic/returns/max", "critic/returns/min", "response_length/mean",
-            "response_length/max", "response_length/min", "response_length/clip_ratio", "prompt_length/mean",
+            "response_length/max", "response_length/min", "response_length/clip_ratio",
+            "response_length_non_aborted/mean", "response_length_non_aborted/max", "response_length_non_aborted/min",
+            "response_length_non_aborted/clip_ratio", "response/aborted_ratio", "prompt_length/mean",
             "prompt_length/max", "prompt_length/min", "prompt_length/clip_ratio"]
     out = dict(zip(keys, vals))
     if use_critic:  # metric_utils.py:138-143, 176-186
-        v = torch.masked_select(b["values"], rmask).float()
+        v = torch.masked_select(b["values"], rmask)
         rdv, rv = torch.var(ret - v), torch.var(ret)
-        cv = torch.stack([v.mean(), v.max(), v.min(), 1.0 - rdv / (rv + 1e-5)]).cpu().tolist()
+        cv = torch.stack([v.mean(), v.max(), v.min(), 1.0 - rdv / (rv + 1e-5)]).float().cpu().tolist()
         out.update(dict(zip(["critic/values/mean", "critic/values/max", "critic/values/min",
                              "critic/vf_explained_var"], cv)))
+    for k in ("__num_turns__", "tool_call_counts"):  # metric_utils.py:210-222
+        if k in batch.non_tensor_batch:
+            arr = batch.non_tensor_batch[k]
+            name = "num_turns" if k == "__num_turns__" else k
+            out.update({f"{name}/min": arr.min(), f"{name}/max": arr.max(), f"{name}/mean": arr.mean()})
     return out
 
 

@@ -1,18 +1,113 @@
-"""Reward managers (mirror of verl/workers/reward_manager/naive.py:46-122 placement semantics).
+"""Reward managers (mirror of verl/workers/reward_manager/: registry.py, naive.py:27-122, dapo.py).
 
-The score of each response is written at its last valid response token (naive.py:100); the rest of the
-(B, R) ``token_level_scores`` is zero. ``SyntheticBernoulliRewardManager`` is the benchmark reward of
-BASELINE.md §3 (Bernoulli(0.5) per sequence, seeded) — a rule reward needs a tokenizer and a dataset,
-neither of which exists offline here.
+Every manager writes each response's score at its last valid response token (naive.py:100); the rest of
+the (B, R) ``token_level_scores`` is zero.
+
+* ``NaiveRewardManager`` ("naive"): the reference's rule-reward path — decode prompt and response with the
+  tokenizer, score with ``compute_score`` (default: ``reward_score.default_compute_score``, gsm8k), or return
+  ``rm_scores`` when a reward model already scored the batch (naive.py:55-60).
+* ``SyntheticBernoulliRewardManager`` ("synthetic_bernoulli"): the benchmark reward of BASELINE.md §3
+  (Bernoulli(0.5) per sequence, seeded) — no tokenizer or dataset exists offline.
+* ``DAPOSyntheticRewardManager`` ("dapo_synthetic"): dapo.py's overlong-buffer penalty on the synthetic score.
 """
 
 from __future__ import annotations
 
+from collections import defaultdict
+
+import numpy as np
 import torch
 
 from .protocol import DataProto
+from .reward_score import default_compute_score
+
+REWARD_MANAGER_REGISTRY: dict = {}
 
 
+def register(name: str):
+    """registry.py:24-41."""
+
+    def decorator(cls):
+        if name in REWARD_MANAGER_REGISTRY and REWARD_MANAGER_REGISTRY[name] != cls:
+            raise ValueError(f"Reward manager {name} has already been registered: {REWARD_MANAGER_REGISTRY[name]} vs {cls}")
+        REWARD_MANAGER_REGISTRY[name] = cls
+        return cls
+
+    return decorator
+
+
+def get_reward_manager_cls(name: str):
+    """registry.py:44-55."""
+    if name not in REWARD_MANAGER_REGISTRY:
+        raise ValueError(f"Unknown reward manager: {name}")
+    return REWARD_MANAGER_REGISTRY[name]
+
+
+@register("naive")
+class NaiveRewardManager:
+    """naive.py:27-122. The per-sample decode + score loop runs on the host (as in the reference); the batch
+    tensors it reads are copied device->host once per call, and the reward tensor is returned on the
+    responses' device."""
+
+    def __init__(self, tokenizer, num_examine, compute_score=None, reward_fn_key="data_source"):
+        self.tokenizer = tokenizer
+        self.num_examine = num_examine
+        self.compute_score = compute_score or default_compute_score
+        self.reward_fn_key = reward_fn_key
+
+    def __call__(self, data: DataProto, return_dict: bool = False):
+        if "rm_scores" in data.batch.keys():  # naive.py:55-60
+            if return_dict:
+                return {"reward_tensor": data.batch["rm_scores"]}
+            return data.batch["rm_scores"]
+        responses = data.batch["responses"]
+        B, R = responses.shape
+        prompts = data.batch["prompts"].cpu().numpy()
+        P = prompts.shape[-1]
+        resp = responses.cpu().numpy()
+        am = data.batch["attention_mask"].cpu().numpy()
+        rewards = np.zeros(B, dtype=np.float32)
+        last = np.zeros(B, dtype=np.int64)
+        extra_out = defaultdict(list)
+        printed = {}
+        nt = data.non_tensor_batch
+        for i in range(B):
+            vpl = int(am[i, :P].sum())
+            valid_prompt_ids = prompts[i, -vpl:]  # a zero-length prompt keeps the whole row (python's [-0:])
+            vrl = int(am[i, P:].sum())
+            valid_response_ids = resp[i, :vrl]
+            prompt_str = self.tokenizer.decode(valid_prompt_ids, skip_special_tokens=True)
+            response_str = self.tokenizer.decode(valid_response_ids, skip_special_tokens=True)
+            ground_truth = nt["reward_model"][i]["ground_truth"]
+            data_source = nt[self.reward_fn_key][i]
+            extra_info = nt["extra_info"][i] if "extra_info" in nt else {}
+            extra_info["num_turns"] = nt["__num_turns__"][i] if "__num_turns__" in nt else None
+            score = self.compute_score(data_source=data_source, solution_str=response_str, ground_truth=ground_truth,
+                                       extra_info=extra_info)
+            if isinstance(score, dict):
+                reward = score["score"]
+                for k, v in score.items():
+                    extra_out[k].append(v)
+            else:
+                reward = score
+            rewards[i] = reward
+            last[i] = vrl - 1 if vrl > 0 else R - 1  # reward_tensor[i, -1] for an empty response, as python indexes
+            if printed.get(data_source, 0) < self.num_examine:
+                printed[data_source] = printed.get(data_source, 0) + 1
+                print("[prompt]", prompt_str)
+                print("[response]", response_str)
+                print("[ground_truth]", ground_truth)
+                for k, v in (score.items() if isinstance(score, dict) else [("score", score)]):
+                    print(f"[{k}]", v)
+        out = torch.zeros(B, R, dtype=torch.float32)
+        out[torch.arange(B), torch.from_numpy(last)] = torch.from_numpy(rewards)
+        out = out.to(responses.device)
+        if return_dict:
+            return {"reward_tensor": out, "reward_extra_info": extra_out}
+        return out
+
+
+@register("synthetic_bernoulli")
 class SyntheticBernoulliRewardManager:
     def __init__(self, seed: int = 1234, p: float = 0.5):
         self.seed = seed
@@ -44,6 +139,7 @@ class SyntheticBernoulliRewardManager:
         return scores
 
 
+@register("dapo_synthetic")
 class DAPOSyntheticRewardManager(SyntheticBernoulliRewardManager):
     """reward_manager/dapo.py:26-150 with the synthetic score: reward = score + the overlong-buffer penalty
     min(-(L - (max_resp_len - buffer_len)) / buffer_len * penalty_factor, 0) (dapo.py:114-123), placed at the
@@ -77,6 +173,20 @@ class DAPOSyntheticRewardManager(SyntheticBernoulliRewardManager):
         if return_dict:
             return {"reward_tensor": out, "reward_extra_info": extra}
         return out
+
+
+def load_reward_manager(config, tokenizer=None, num_examine: int = 0, compute_score=None, **reward_kwargs):
+    """trainer/ppo/reward.py:93-148: the manager named by ``reward_model.reward_manager``. "naive" needs a
+    tokenizer (decode) and scores with ``compute_score`` or default_compute_score; the synthetic managers take
+    the data seed."""
+    name = config.reward_model.get("reward_manager", "naive")
+    cls = get_reward_manager_cls(name)
+    if name == "naive":
+        if tokenizer is None:
+            raise ValueError("reward_manager=naive decodes responses: pass the tokenizer")
+        return cls(tokenizer=tokenizer, num_examine=num_examine, compute_score=compute_score,
+                   reward_fn_key=config.data.get("reward_fn_key", "data_source"), **reward_kwargs)
+    return cls(seed=config.data.get("seed", 1234), **reward_kwargs)
 
 
 def compute_reward(data: DataProto, reward_fn):

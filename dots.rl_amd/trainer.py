@@ -21,7 +21,7 @@ from . import core_algos
 from .core_algos import AdvantageEstimator, agg_loss
 from .metric_utils import compute_data_metrics, compute_throughout_metrics, compute_timing_metrics, reduce_metrics
 from .protocol import DataProto
-from .reward import SyntheticBernoulliRewardManager, compute_reward
+from .reward import compute_reward, load_reward_manager
 from .seqlen_balancing import get_seqlen_balanced_partitions, log_seqlen_unbalance
 from .single_controller import SPMDWorkerGroup
 from .config import resolve_critic_config
@@ -113,9 +113,15 @@ class SyntheticPromptLoader:
 class RayPPOTrainer:
     """The fit() loop of ray_trainer.py:1050-1405 for the GRPO/PPO actor-learner hot path."""
 
-    def __init__(self, config, reward_fn=None, train_dataloader=None, eos_token_id=151645, pad_token_id=151643):
+    def __init__(self, config, reward_fn=None, train_dataloader=None, eos_token_id=151645, pad_token_id=151643,
+                 tokenizer=None, rm_wg=None):
         self.config = config
-        self.reward_fn = reward_fn or SyntheticBernoulliRewardManager(seed=config.data.get("seed", 1234))
+        self.tokenizer = tokenizer
+        self.reward_fn = reward_fn or load_reward_manager(config, tokenizer)
+        # reward model scores (ray_trainer.py:1200-1203): a worker group with compute_rm_score(batch) -> DataProto
+        # holding `rm_scores`; the reward model itself is outside this repository's path
+        self.use_rm = bool(config.reward_model.get("enable", False))
+        self.rm_wg = rm_wg
         self.train_dataloader = train_dataloader or SyntheticPromptLoader(
             config.data.train_batch_size, config.data.max_prompt_length, seed=config.data.get("seed", 1234))
         self.eos_token_id = eos_token_id
@@ -182,10 +188,14 @@ class RayPPOTrainer:
         if cfg.trainer.balance_batch and self.n_gpus > 1:
             self._balance_batch(batch, metrics)
         batch.meta_info["global_token_num"] = batch.batch["attention_mask"].sum(-1).tolist()
-        reward_tensor = None
+        reward_tensor, reward_extra = None, {}
         if "token_level_scores" not in batch.batch:
             with marked_timer("reward", timing_raw):
-                reward_tensor, _ = compute_reward(batch, self.reward_fn)
+                if self.use_rm:
+                    if self.rm_wg is None:
+                        raise NotImplementedError("reward_model.enable=True needs an rm_wg (compute_rm_score)")
+                    batch = batch.union(self.rm_wg.compute_rm_score(batch))
+                reward_tensor, reward_extra = compute_reward(batch, self.reward_fn)
         with marked_timer("old_log_prob", timing_raw):
             old = self.actor_rollout_wg.compute_log_prob(batch)
             ent = agg_loss(old.batch["entropys"], batch.batch["response_mask"], ar.actor.loss_agg_mode)
@@ -201,6 +211,8 @@ class RayPPOTrainer:
         with marked_timer("adv", timing_raw):
             if reward_tensor is not None:
                 batch.batch["token_level_scores"] = reward_tensor
+            if reward_extra:
+                batch.non_tensor_batch.update({k: np.array(v) for k, v in reward_extra.items()})
             if "token_level_rewards" not in batch.batch:
                 if cfg.algorithm.use_kl_in_reward:
                     batch, klm = apply_kl_penalty(batch, self.kl_ctrl_in_reward, cfg.algorithm.kl_penalty)

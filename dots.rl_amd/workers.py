@@ -15,19 +15,18 @@ from __future__ import annotations
 import os
 import time
 
+import psutil
 import torch
 import torch.distributed as dist
 
 from .config import RANDOM_MODELS
 from .dp_actor import DataParallelPPOActor, FlatAdamW
 from .dp_critic import DataParallelPPOCritic
+from .flops_counter import FlopsCounter
 from .protocol import DataProto
-from .qwen2 import ParamStore, Qwen2Config, Qwen2Model, flops_per_token
+from .qwen2 import ParamStore, Qwen2Config, Qwen2Model
 from .rollout import MI355XRollout
 from .single_controller import Dispatch, Worker, make_nd_compute_dataproto_dispatch_fn, register
-
-MI355X_BF16_DENSE_PEAK = 2.5e15  # FLOP/s (MI355X_MICROARCH.md; AMD's 5 PF figure is 2:1 sparse)
-
 
 def resolve_model_config(model_cfg) -> Qwen2Config:
     path = model_cfg.get("path", "random:qwen2.5-0.5b")
@@ -107,6 +106,7 @@ class ActorRolloutRefWorker(Worker):
         _enable_gemm_tuning(cfg.model.get("gemm_tuning", "auto"))
         mcfg = resolve_model_config(cfg.model)
         self.model_config = mcfg
+        self.flops_counter = FlopsCounter(mcfg)
         dtype = torch.float32 if cfg.model.get("dtype", "bfloat16") == "float32" else torch.bfloat16
         seed = int(cfg.model.get("seed", 1234))
         self.store = ParamStore(mcfg, self.device, compute_dtype=dtype, trainable=self._is_actor)
@@ -201,12 +201,12 @@ class ActorRolloutRefWorker(Worker):
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         ntok = data.meta_info.get("global_token_num")
-        if ntok:
-            T = data.batch["input_ids"].shape[1]
-            est = 3 * flops_per_token(self.model_config, T) * sum(ntok)
-            metrics["perf/mfu/actor"] = est * self.config.actor.ppo_epochs / (dt * MI355X_BF16_DENSE_PEAK * self.dp_size)
+        if ntok:  # fsdp_workers.py:697-701
+            est, promised = self.flops_counter.estimate_flops(ntok, dt)
+            metrics["perf/mfu/actor"] = est * self.config.actor.ppo_epochs / promised / self.dp_size
         metrics["perf/max_memory_allocated_gb"] = torch.cuda.max_memory_allocated() / 1024**3
         metrics["perf/max_memory_reserved_gb"] = torch.cuda.max_memory_reserved() / 1024**3
+        metrics["perf/cpu_memory_used_gb"] = psutil.virtual_memory().used / 1024**3
         metrics["actor/lr"] = self.actor_optimizer.current_lr()
         self.actor_optimizer.sched_step += 1
         return DataProto(meta_info={"metrics": metrics})
@@ -269,6 +269,7 @@ class CriticWorker(Worker):
         mcfg = resolve_model_config(cfg.model)
         mcfg.num_labels = 1
         self.model_config = mcfg
+        self.flops_counter = FlopsCounter(mcfg)
         dtype = torch.float32 if cfg.model.get("dtype", "bfloat16") == "float32" else torch.bfloat16
         self.store = ParamStore(mcfg, self.device, compute_dtype=dtype, trainable=True)
         path = cfg.model.get("path", "random:")
@@ -315,10 +316,9 @@ class CriticWorker(Worker):
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         ntok = data.meta_info.get("global_token_num")
-        if ntok:
-            T = data.batch["input_ids"].shape[1]
-            est = 3 * flops_per_token(self.model_config, T) * sum(ntok)
-            metrics["perf/mfu/critic"] = est * self.config.ppo_epochs / (dt * MI355X_BF16_DENSE_PEAK * self.dp_size)
+        if ntok:  # fsdp_workers.py:1275-1279
+            est, promised = self.flops_counter.estimate_flops(ntok, dt)
+            metrics["perf/mfu/critic"] = est * self.config.ppo_epochs / promised / self.dp_size
         metrics["critic/lr"] = self.critic_optimizer.current_lr()
         self.critic_optimizer.sched_step += 1
         return DataProto(meta_info={"metrics": metrics})

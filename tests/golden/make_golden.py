@@ -730,6 +730,279 @@ def gen_gpg_loss():
     _save("gpg_loss.npz", arrays, {"cases": cases, "ref": "core_algos.py:957-975; dp_actor.py:419-466"})
 
 
+# --------------------------------------------------------------------------------------------
+# SURVEY §8(c) golden #7: the reference DataParallelPPOActor (dp_actor.py:300-482) on the tiny Qwen2, fp32:
+# compute_log_prob (old log-probs + entropy) then update_policy over 2 mini-batches x 2 micro-batches with
+# torch AdamW + clip_grad_norm_ (fsdp_workers.py:454-459, dp_actor.py:282-298). Records every actor/* metric
+# list, the grad norms and the post-step parameters.
+# --------------------------------------------------------------------------------------------
+def _tiny_hf_causal():
+    from safetensors.torch import load_file
+    from transformers import Qwen2Config, Qwen2ForCausalLM
+
+    cfg = Qwen2Config(**TINY_QWEN2, attn_implementation="eager")
+    model = Qwen2ForCausalLM(cfg).float()
+    sd = load_file(os.path.join(HERE, "tiny_qwen2", "model.safetensors"))
+    missing, unexpected = model.load_state_dict(sd, strict=False)
+    assert set(missing) <= {"lm_head.weight"} and not unexpected, (missing, unexpected)
+    model.tie_weights()
+    assert model.lm_head.weight.data_ptr() == model.model.embed_tokens.weight.data_ptr()
+    return model
+
+
+def _gloo_world1():
+    import torch.distributed as dist
+
+    if not dist.is_initialized():
+        import socket
+
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+
+
+def _ref_actor(model, cfgd, lr):
+    """A reference DataParallelPPOActor in fp32: its torch.autocast(device_type=get_device_name()) is 'cpu' here,
+    which would run the CPU bf16 autocast; the actor's device name is set to 'cuda' so autocast is disabled
+    (no CUDA in this container) and the model runs in fp32 - the reference math without the bf16 casts."""
+    import verl.workers.actor.dp_actor as ref_dp
+
+    _gloo_world1()
+    opt = torch.optim.AdamW(model.parameters(), lr=lr, betas=(0.9, 0.999), weight_decay=0.01) if lr else None
+    actor = ref_dp.DataParallelPPOActor(DictConfig(cfgd), model, opt)
+    actor.device_name = "cuda"
+    return actor, opt
+
+
+def _actor_cfg(**kw):
+    d = dict(use_remove_padding=False, use_fused_kernels=False, ulysses_sequence_parallel_size=1,
+             entropy_from_logits_with_chunking=False, use_torch_compile=False, entropy_checkpointing=False,
+             ppo_mini_batch_size=4, ppo_micro_batch_size_per_gpu=2, ppo_epochs=1, use_dynamic_bsz=False,
+             entropy_coeff=0.0, loss_agg_mode="token-mean", policy_loss=DictConfig(loss_mode="vanilla"),
+             clip_ratio=0.2, clip_ratio_low=0.2, clip_ratio_high=0.2, clip_ratio_c=3.0, use_kl_loss=True,
+             kl_loss_type="low_var_kl", kl_loss_coef=0.001, grad_clip=1.0)
+    d.update(kw)
+    return d
+
+
+def _params(model):
+    return {k: v.detach().clone() for k, v in model.state_dict().items() if k != "lm_head.weight"}
+
+
+ACTOR_UPDATE_CASES = [
+    # (name, actor config overrides, lr)
+    ("grpo_k3", dict(), 1e-4),
+    ("ent_seqmean_kl", dict(entropy_coeff=0.01, loss_agg_mode="seq-mean-token-mean", kl_loss_type="kl",
+                            clip_ratio_high=0.28, clip_ratio_c=10.0), 1e-4),
+]
+
+
+def gen_actor_update():
+    from verl import DataProto as RefDataProto
+
+    z = np.load(os.path.join(HERE, "tiny_qwen2_rollout.npz"))
+    seq, am, pos, resp = (torch.from_numpy(z[k]) for k in ("sequences", "attention_mask", "position_ids", "responses"))
+    B, R = resp.shape
+    B = 8  # 6 golden rows + 2 repeated rows with a shifted mask -> 2 mini-batches of 4 (2 micro-batches of 2)
+    seq, am, pos, resp = (torch.cat([t, t[:2]], 0) for t in (seq, am, pos, resp))
+    am[6, -3:] = 0  # shorter responses for the repeated rows
+    am[7, -R + 1:] = 0
+    g = torch.Generator().manual_seed(2024)
+    arrays, cases = {}, []
+    for ci, (name, over, lr) in enumerate(ACTOR_UPDATE_CASES):
+        model = _tiny_hf_causal()
+        before = _params(model)
+        actor, opt = _ref_actor(model, _actor_cfg(**over), lr)
+        data = RefDataProto.from_dict(tensors={"input_ids": seq, "attention_mask": am, "position_ids": pos,
+                                               "responses": resp},
+                                      meta_info={"micro_batch_size": 4, "temperature": 1.0, "use_dynamic_bsz": False})
+        logp, ent = actor.compute_log_prob(data, calculate_entropy=True)
+        rmask = am[:, -R:]
+        old = (logp + 0.3 * torch.randn(B, R, generator=g)).detach()  # ratios across the clip bounds
+        ref = (logp + 0.2 * torch.randn(B, R, generator=g)).detach()
+        adv = torch.randn(B, 1, generator=g).expand(B, R) * rmask  # sequence-level advantages, +-
+        adv = adv.contiguous()
+        udata = RefDataProto.from_dict(tensors={"input_ids": seq, "attention_mask": am, "position_ids": pos,
+                                                "responses": resp, "response_mask": rmask, "old_log_probs": old,
+                                                "advantages": adv, "ref_log_prob": ref},
+                                       meta_info={"temperature": 1.0})
+        metrics = actor.update_policy(udata)
+        after = _params(model)
+        pre = f"c{ci}_"
+        for k, v in dict(input_ids=seq, attention_mask=am, position_ids=pos, responses=resp, response_mask=rmask,
+                         log_probs=logp, entropys=ent, old_log_probs=old, ref_log_prob=ref, advantages=adv).items():
+            arrays[pre + k] = v
+        for k, v in after.items():
+            arrays[pre + "after." + k] = v
+        cases.append(dict(name=name, config=_actor_cfg(**over), lr=lr, metrics=metrics,
+                          param_sums={k: float(v.double().sum()) for k, v in after.items()},
+                          delta_abs_sums={k: float((after[k] - before[k]).double().abs().sum()) for k in after}))
+    for c in cases:
+        c["config"]["policy_loss"] = dict(c["config"]["policy_loss"])
+    _save("actor_update.npz", arrays, {"cases": cases, "weights": "tiny_qwen2/model.safetensors",
+                                       "ref": "dp_actor.py:282-298, 300-359, 361-482; fsdp_workers.py:454-459",
+                                       "precision": "fp32 (autocast disabled: actor.device_name='cuda' on a CPU box)"})
+
+
+# --------------------------------------------------------------------------------------------
+# One GRPO fit() step composed from the reference's own functions (ray_trainer.py:1104-1399) on the tiny
+# Qwen2, fp32, greedy: HFRollout (hf_rollout.py:53-177) -> union -> compute_response_mask -> global_token_num
+# -> reward (reward-model scores through NaiveRewardManager, naive.py:46-60; plus the gsm8k rule score of the
+# same responses with a stub tokenizer, naive.py:62-122 + gsm8k.py) -> compute_log_prob (old + entropy ->
+# actor/entropy) -> ref log-prob -> compute_advantage (GRPO) -> update_policy -> compute_data_metrics /
+# compute_timing_metrics / compute_throughout_metrics (metric_utils.py) -> FlopsCounter MFU.
+# --------------------------------------------------------------------------------------------
+from stub_tokenizer import StubTokenizer  # noqa: E402  (shared with the tests)
+
+
+GRPO_STEP_CASES = [
+    # n = 2: real groups. Greedy copies of a prompt are identical, so the group-normalised advantages (+-1/sqrt 2)
+    # cancel inside each micro-batch: the policy gradient is ~0 (the reference's too) and only the rollout,
+    # reward, log-prob, advantage and metric composition is compared.
+    dict(name="n2", n_prompts=4, n=2, P=12, R=10, pads=[0, 3, 0, 5], lr=1e-4, mini_prompts=2, micro=2,
+         rm_scores=[1.0, 0.0, 0.5, 1.0, 0.0, 0.0, 1.0, 0.25], seed=99, compare_update=False),
+    # n = 1: singleton groups (mean 0, std 1 -> A = score / (1 + 1e-6)): a real policy-gradient update
+    dict(name="n1", n_prompts=8, n=1, P=12, R=10, pads=[0, 3, 0, 5, 1, 0, 2, 0], lr=1e-4, mini_prompts=4, micro=2,
+         rm_scores=[1.0, 0.0, 0.5, 1.0, 0.0, -0.5, 1.0, 0.25], seed=7, compare_update=True),
+]
+GRPO_TIMING = {"gen": 0.5, "reward": 0.01, "old_log_prob": 0.2, "ref": 0.2, "adv": 0.01, "update_actor": 0.8,
+               "step": 1.75}
+
+
+def gen_grpo_step():
+    arrays, metas = {}, []
+    for ci, S in enumerate(GRPO_STEP_CASES):
+        a, m = _grpo_step_case(S)
+        arrays.update({f"c{ci}_{k}": v for k, v in a.items()})
+        metas.append(m)
+    _save("grpo_step.npz", arrays, {"cases": metas})
+
+
+def _grpo_step_case(S):
+    import verl.trainer.ppo.ray_trainer as rt
+    import verl.workers.rollout.hf_rollout as ref_hf
+    from verl import DataProto as RefDataProto
+    from verl.trainer.ppo.metric_utils import (compute_data_metrics, compute_throughout_metrics,
+                                               compute_timing_metrics)
+    from verl.utils.flops_counter import FlopsCounter
+    from verl.workers.reward_manager.naive import NaiveRewardManager
+
+    model = _tiny_hf_causal()
+    before = _params(model)
+    g = torch.Generator().manual_seed(S["seed"])
+    Np, P, R, n = S["n_prompts"], S["P"], S["R"], S["n"]
+    ids = torch.randint(3, 512, (Np, P), generator=g)
+    am = torch.ones(Np, P, dtype=torch.int64)
+    for i, npad in enumerate(S["pads"]):
+        am[i, :npad] = 0
+        ids[i, :npad] = TINY_QWEN2["pad_token_id"]
+    pos = compute_position_id_with_mask(am)
+
+    ref_hf.get_device_name = lambda: "cuda"  # fp32 generate (autocast disabled on this CPU box)
+    if not hasattr(torch.cpu, "empty_cache"):  # hf_rollout.py:174 calls the device's empty_cache (a no-op here)
+        torch.cpu.empty_cache = lambda: None
+    rollout = ref_hf.HFRollout(model, DictConfig(do_sample=False, temperature=1.0, response_length=R, top_p=1.0,
+                                                 top_k=-1, val_kwargs=DictConfig()))
+
+    def run_rollout(eos):
+        batch = RefDataProto.from_single_dict({"input_ids": ids, "attention_mask": am, "position_ids": pos,
+                                               "data_source": np.array(["openai/gsm8k"] * Np, dtype=object),
+                                               "reward_model": np.array([{"ground_truth": None} for _ in range(Np)],
+                                                                        dtype=object)})
+        batch.non_tensor_batch["uid"] = np.array([f"uid{i}" for i in range(Np)], dtype=object)
+        gen_batch = batch.pop(batch_keys=["input_ids", "attention_mask", "position_ids"])
+        gen_batch.meta_info.update({"eos_token_id": eos, "pad_token_id": TINY_QWEN2["pad_token_id"]})
+        gen_batch = gen_batch.repeat(repeat_times=n, interleave=True)
+        out = rollout.generate_sequences(gen_batch)
+        batch = batch.repeat(repeat_times=n, interleave=True)
+        return batch.union(out)
+
+    batch = run_rollout(TINY_QWEN2["eos_token_id"])
+    eos = int(batch.batch["responses"][2 if n > 1 else 1, 3])  # some rows stop mid-response
+    batch = run_rollout(eos)
+    B = Np * n
+    batch.batch["response_mask"] = rt.compute_response_mask(batch)
+    batch.meta_info["global_token_num"] = torch.sum(batch.batch["attention_mask"], dim=-1).tolist()
+
+    # rule reward (gsm8k strict) on the same responses: ground truth = the extracted answer for even prompts,
+    # a different digit for odd ones
+    from verl.utils.reward_score import gsm8k
+
+    tok = StubTokenizer()
+    gts = []
+    for i in range(Np):
+        r = batch.batch["responses"][i * n]
+        vl = int(batch.batch["attention_mask"][i * n, P:].sum())
+        ans = gsm8k.extract_solution(tok.decode(r[:vl]), "strict")
+        gts.append(str(ans) if (i % 2 == 0 and ans is not None) else "9")
+    for i in range(B):
+        batch.non_tensor_batch["reward_model"][i] = {"ground_truth": gts[i // n]}
+    rule = NaiveRewardManager(tokenizer=tok, num_examine=0)(batch, return_dict=True)
+    rule_scores = rule["reward_tensor"]
+
+    # reward-model scores (preset per row) placed at the last valid response token; the naive manager returns
+    # rm_scores as the reward tensor (naive.py:55-60)
+    vl = batch.batch["attention_mask"][:, P:].sum(-1)
+    rm = torch.zeros(B, R)
+    rm[torch.arange(B), vl - 1] = torch.tensor(S["rm_scores"])
+    batch.batch["rm_scores"] = rm
+    reward_tensor = NaiveRewardManager(tokenizer=tok, num_examine=0)(batch, return_dict=True)["reward_tensor"]
+
+    mini = S["mini_prompts"] * n  # fsdp_workers.py:209-214 normalisation at dp=1
+    actor, opt = _ref_actor(model, _actor_cfg(ppo_mini_batch_size=mini, ppo_micro_batch_size_per_gpu=S["micro"]),
+                            S["lr"])
+    batch.meta_info["micro_batch_size"] = 4
+    batch.meta_info["temperature"] = 1.0
+    batch.meta_info["use_dynamic_bsz"] = False
+    old, ent = actor.compute_log_prob(batch, calculate_entropy=True)
+    actor_entropy = ca.agg_loss(loss_mat=ent, loss_mask=batch.batch["response_mask"], loss_agg_mode="token-mean")
+    ref_model = _tiny_hf_causal()
+    ref_actor, _ = _ref_actor(ref_model, _actor_cfg(), None)
+    ref_lp, _ = ref_actor.compute_log_prob(batch, calculate_entropy=False)
+    batch.batch["old_log_probs"] = old
+    batch.batch["ref_log_prob"] = ref_lp
+    batch.batch["token_level_scores"] = reward_tensor
+    batch.batch["token_level_rewards"] = batch.batch["token_level_scores"]
+    batch = rt.compute_advantage(batch, adv_estimator="grpo", norm_adv_by_std_in_grpo=True, num_repeat=n)
+    batch.meta_info.pop("micro_batch_size")
+    metrics = actor.update_policy(batch)
+    after = _params(model)
+    timing = dict(GRPO_TIMING)
+    dm = compute_data_metrics(batch, use_critic=False)
+    tm = compute_timing_metrics(batch, timing)
+    th = compute_throughout_metrics(batch, timing, n_gpus=1)
+    from transformers import Qwen2Config
+
+    fc = FlopsCounter(Qwen2Config(**TINY_QWEN2))
+    est, _ = fc.estimate_flops(batch.meta_info["global_token_num"], timing["update_actor"])
+    big = FlopsCounter(Qwen2Config(vocab_size=151936, hidden_size=896, intermediate_size=4864, num_hidden_layers=24,
+                                   num_attention_heads=14, num_key_value_heads=2))
+    est_big, _ = big.estimate_flops([768] * 512, 1.0)
+    arrays = dict(prompt_ids=ids, prompt_attention_mask=am, prompt_position_ids=pos, rm_scores_preset=torch.tensor(
+        S["rm_scores"]), rule_scores=rule_scores, token_level_scores=reward_tensor)
+    for k in ("prompts", "responses", "input_ids", "attention_mask", "position_ids", "response_mask",
+              "old_log_probs", "ref_log_prob", "advantages", "returns"):
+        arrays[k] = batch.batch[k]
+    arrays["entropys"] = ent
+    for k, v in after.items():
+        arrays["after." + k] = v
+    meta = dict(S, eos_token_id=eos, pad_token_id=TINY_QWEN2["pad_token_id"], ground_truths=gts,
+                uid_groups=[i // n for i in range(B)], actor_entropy=float(actor_entropy), update_metrics=metrics,
+                data_metrics={k: float(v) for k, v in dm.items()}, timing_metrics={k: float(v) for k, v in tm.items()},
+                throughput_metrics={k: float(v) for k, v in th.items()}, flops_tiny_tflops=float(est),
+                flops_qwen05b_768x512_tflops=float(est_big),
+                param_sums={k: float(v.double().sum()) for k, v in after.items()},
+                delta_abs_sums={k: float((after[k] - before[k]).double().abs().sum()) for k in after},
+                actor_config=dict(_actor_cfg(ppo_mini_batch_size=mini, ppo_micro_batch_size_per_gpu=S["micro"]),
+                                  policy_loss={"loss_mode": "vanilla"}),
+                ref="ray_trainer.py:196-291,1104-1399; hf_rollout.py:53-177; naive.py:46-122; gsm8k.py:52; "
+                    "dp_actor.py:300-482; metric_utils.py:80-302; flops_counter.py:135-167",
+                precision="fp32 (autocast disabled)")
+    return arrays, meta
+
+
 if __name__ == "__main__":
     which = sys.argv[1:] or ["ppo_loss", "masked_mean", "grpo", "gae", "logprob", "fused_linear", "masks", "tiny_qwen2"]
     for w in which:
