@@ -1003,6 +1003,70 @@ def _grpo_step_case(S):
     return arrays, meta
 
 
+# --------------------------------------------------------------------------------------------
+# Config #2 at full depth: the reference HF Qwen2ForCausalLM (what the FSDP/HF path loads for Qwen2.5-0.5B)
+# on deterministic CPU-seeded weights (tests/golden/full_depth.py; never committed), fp32: greedy generate of
+# 4 x 64-token prompts for 64 tokens post-processed as HFRollout (hf_rollout.py:112-171) with the top-2 logit
+# margin of every step, teacher-forced log-probs / entropy as dp_actor.py:249-272 computes them, and the size
+# of the CPU bf16-autocast logit error on the same sequences (the bf16 margin bound the test uses).
+# --------------------------------------------------------------------------------------------
+def gen_full_depth():
+    import full_depth as fd
+    from transformers import Qwen2Config, Qwen2ForCausalLM
+
+    cfg = Qwen2Config(**fd.QWEN25_05B, attn_implementation="eager")
+    model = Qwen2ForCausalLM(cfg).float()  # built on the CPU (a meta-device build leaves RoPE's inv_freq unset)
+    sd = fd.make_state_dict()
+    missing, unexpected = model.load_state_dict(sd, strict=False)
+    assert set(missing) == {"lm_head.weight"} and not unexpected
+    model.tie_weights()
+    model.eval()
+    ids, am, pos = fd.prompts()
+    B, P = ids.shape
+    R = 64
+    eos, pad = fd.QWEN25_05B["eos_token_id"], fd.QWEN25_05B["pad_token_id"]
+    with torch.no_grad():
+        out = model.generate(input_ids=ids, attention_mask=am, position_ids=pos, do_sample=False, num_beams=1,
+                             max_new_tokens=R, eos_token_id=eos, pad_token_id=pad, output_scores=True,
+                             return_dict_in_generate=True, use_cache=True)
+    seq = out.sequences
+    if seq.shape[1] < P + R:
+        seq = torch.cat([seq, torch.full((B, P + R - seq.shape[1]), pad)], 1)
+    top2 = torch.stack([torch.topk(s, 2, -1).values for s in out.scores], 1)  # (B, steps, 2)
+    gaps = torch.full((B, R), float("inf"))
+    gaps[:, :top2.shape[1]] = top2[..., 0] - top2[..., 1]
+    resp = seq[:, P:]
+    rmask = vF.get_response_mask(resp, eos_token=eos, dtype=am.dtype)
+    full_am = torch.cat([am, rmask], -1)
+    full_pos = torch.cat([pos, pos[:, -1:] + torch.arange(1, R + 1).unsqueeze(0)], -1)
+    with torch.no_grad():
+        logits = model(input_ids=seq, attention_mask=full_am, position_ids=full_pos, use_cache=False).logits
+        lg = logits[:, -R - 1:-1]
+        logp = vF.logprobs_from_logits_v2(lg, resp)
+        ent = vF.entropy_from_logits(lg)
+        with torch.autocast("cpu", dtype=torch.bfloat16):
+            lb = model(input_ids=seq, attention_mask=full_am, position_ids=full_pos, use_cache=False).logits
+        lbr = lb.float()[:, -R - 1:-1]
+        err = (lbr - lg).abs()
+        err_max_row = err.amax(-1)  # (B, R): worst logit error of the bf16 model at each response step
+        t2 = torch.topk(lg, 2, -1).indices  # the fp32 reference's top-2 tokens of each teacher-forced step
+        d32 = lg.gather(-1, t2[..., :1]) - lg.gather(-1, t2[..., 1:])
+        d16 = lbr.gather(-1, t2[..., :1]) - lbr.gather(-1, t2[..., 1:])
+        gap_err = (d16 - d32).abs().squeeze(-1)  # (B, R): bf16 error of the top-2 margin itself
+        logp_bf16 = vF.logprobs_from_logits_v2(lb.float()[:, -R - 1:-1], resp)
+    arrays = dict(prompt_ids=ids, prompt_attention_mask=am, prompt_position_ids=pos, sequences=seq, responses=resp,
+                  attention_mask=full_am, position_ids=full_pos, top2_gap=gaps, log_probs=logp, entropy=ent,
+                  cpu_bf16_logit_err=err_max_row, cpu_bf16_gap_err=gap_err, cpu_bf16_log_probs=logp_bf16)
+    _save("full_depth.npz", arrays, {
+        "eos_token_id": eos, "pad_token_id": pad, "response_length": R, "weights": "full_depth.make_state_dict()",
+        "scales": fd.SCALES, "seed": fd.SEED, "weight_checksum": fd.checksum(sd), "min_top2_gap": float(gaps.min()),
+        "median_top2_gap": float(gaps[torch.isfinite(gaps)].median()),
+        "cpu_bf16_logit_err_max": float(err_max_row.max()), "cpu_bf16_logit_err_median": float(err_max_row.median()),
+        "cpu_bf16_logp_err_max": float((logp_bf16 - logp).abs().max()),
+        "cpu_bf16_gap_err_max": float(gap_err.max()), "cpu_bf16_gap_err_median": float(gap_err.median()),
+        "hf": "transformers Qwen2ForCausalLM fp32 eager attention", "ref": "hf_rollout.py:112-171; dp_actor.py:249-272"})
+
+
 if __name__ == "__main__":
     which = sys.argv[1:] or ["ppo_loss", "masked_mean", "grpo", "gae", "logprob", "fused_linear", "masks", "tiny_qwen2"]
     for w in which:
