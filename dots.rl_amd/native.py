@@ -97,6 +97,15 @@ def _c(t):
     return None if t is None else t.contiguous()
 
 
+def _c16(t):
+    """Contiguous with a 16-byte aligned base (the vectorised kernels' requirement): a row slice of a larger
+    batch (e.g. a micro-batch of one sequence) is copied once into a fresh allocation."""
+    if t is None:
+        return None
+    t = t.contiguous()
+    return t if t.data_ptr() % 16 == 0 else t.clone()
+
+
 class _Workspace:
     """Per-device scratch buffer, grown on demand; stream-ordered reuse on the current stream."""
 
@@ -132,10 +141,10 @@ def ppo_loss_fwd_bwd(old_log_prob, log_prob, advantages, response_mask, entropy=
     ``token_count`` (token-mean): device float64 scalar = response_mask.sum() when the caller already has
     it; K1 then makes one pass over HBM instead of two."""
     _dev(old_log_prob, log_prob, advantages, response_mask, entropy, ref_log_prob)
-    old_log_prob, log_prob, advantages = _c(old_log_prob.float()), _c(log_prob.float()), _c(advantages.float())
-    response_mask = _c(response_mask)
-    entropy = _c(entropy.float()) if entropy is not None else None
-    ref_log_prob = _c(ref_log_prob.float()) if ref_log_prob is not None else None
+    old_log_prob, log_prob, advantages = _c16(old_log_prob.float()), _c16(log_prob.float()), _c16(advantages.float())
+    response_mask = _c16(response_mask)
+    entropy = _c16(entropy.float()) if entropy is not None else None
+    ref_log_prob = _c16(ref_log_prob.float()) if ref_log_prob is not None else None
     B, R = log_prob.shape
     prm = _lib.PPOLossParams(clip_ratio_low, clip_ratio_high, clip_ratio_c, entropy_coeff, kl_loss_coef,
                              loss_scale_factor, _lib.AGG_MODES[loss_agg_mode],
