@@ -87,6 +87,58 @@ def _pmc_traffic(symbol):
     return d.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
 
 
+K1_TOKENS = 1 << 26
+K1_PER_UNIT = ("36 B per token: old_log_prob, log_prob, advantages, entropy, ref_log_prob read (5 x 4 B fp32), "
+               "response_mask read (8 B int64), dlog_prob and dentropy written (2 x 4 B fp32)")
+
+
+def k1_roofline(form="two_pass", reps=20, warmup=3):
+    """North-star kernel K1 (fused PPO loss fwd+bwd, drl_ppo_loss_fwd_bwd) at 2^26 tokens, token-mean, low_var_kl,
+    entropy bonus, int64 mask: every launch bracketed by HIP events on its stream. ``two_pass`` is the form the
+    actor runs (mask count folded by the K1a pre-pass inside the same call); ``one_pass`` hands over sum(mask)."""
+    import torch
+
+    from dots.rl_amd import native
+
+    N, R = K1_TOKENS, 1024
+    B = N // R
+    g = torch.Generator(device="cuda").manual_seed(26)
+    old = -torch.rand(B, R, device="cuda", generator=g) * 5
+    lp = old + torch.randn(B, R, device="cuda", generator=g) * 0.3
+    adv = torch.randn(B, R, device="cuda", generator=g)
+    mask = (torch.rand(B, R, device="cuda", generator=g) > 0.05).to(torch.int64)
+    ent = torch.rand(B, R, device="cuda", generator=g)
+    ref = lp + 0.1
+    out = torch.empty(8, device="cuda")
+    dlp, dent = torch.empty_like(lp), torch.empty_like(lp)
+    kw = dict(entropy_coeff=0.001, kl_loss_coef=0.001, kl_loss_type="low_var_kl", loss_agg_mode="token-mean",
+              want_dentropy=True, out=out, dlogp=dlp, dentropy=dent)
+    if form == "one_pass":
+        kw["token_count"] = mask.to(torch.float64).sum().reshape(1)
+    for _ in range(warmup):
+        native.ppo_loss_fwd_bwd(old, lp, adv, mask, ent, ref, **kw)
+    # one HIP event pair on the launch stream around `reps` back-to-back calls (per-call event pairs would add
+    # their own gaps to a ~450 us kernel): mean call duration, kernel boundaries included
+    s = torch.cuda.current_stream()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(s)
+    for _ in range(reps):
+        native.ppo_loss_fwd_bwd(old, lp, adv, mask, ent, ref, **kw)
+    b.record(s)
+    b.synchronize()
+    t = a.elapsed_time(b) * 1e-3 / reps
+    work = 36.0 * N
+    sym = "drl_ppo_loss_fwd_bwd" + ("_one_pass" if form == "one_pass" else "")
+    traffic, src = _pmc_traffic(sym)
+    achieved = work / t / 1e9
+    del old, lp, adv, mask, ent, ref, dlp, dent
+    torch.cuda.empty_cache()
+    return {"kernel": "drl_ppo_loss_fwd_bwd", "form": form, "tokens": N, "bound": "hbm", "achieved": achieved,
+            "peak": PEAK_HBM_GBPS, "unit": "GB/s", "frac": achieved / PEAK_HBM_GBPS, "traffic": traffic,
+            "algorithmic_work_per_launch": work, "mean_launch_us": t * 1e6, "launches": reps, "per_unit": K1_PER_UNIT,
+            "traffic_source": src}
+
+
 def cpu_baseline(cfg):
     from oracle import cpu_baseline as cb
 
@@ -136,6 +188,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--roofline-kernel", default="drl_swiglu_fwd", choices=sorted(ROOFLINE))
     ap.add_argument("--override", nargs="*", default=[])
+    ap.add_argument("--k1-only", choices=["two_pass", "one_pass"], default=None,
+                    help="only the K1 roofline at 2^26 tokens (rocprofv3 PMC passes for profiles/pmc_drl_ppo_loss_*)")
     ap.add_argument("--dist-backend", default=None,
                     help="default: nccl (RCCL) on GPU; gloo lets several ranks share one GPU for a rehearsal")
     args = ap.parse_args()
@@ -144,6 +198,10 @@ def main():
     import torch.distributed as dist
 
     from dots.rl_amd import native
+
+    if args.k1_only:
+        print(json.dumps(k1_roofline(args.k1_only)), flush=True)
+        return
     from dots.rl_amd.single_controller import init_process_group_from_env
     from dots.rl_amd.trainer import RayPPOTrainer
 
@@ -212,8 +270,12 @@ def main():
             "timing_s": {k.split("/", 1)[1]: sum(h[k] for h in hist) / len(hist) for k in hist[0] if k.startswith("timing_s/")},
             "mfu_actor": sum(h.get("perf/mfu/actor", 0.0) for h in hist) / len(hist),
             "roofline": roofline,
+            "roofline_k1": None,
             "cpu_baseline": None,
         }
+        if not args.tiny:
+            line["roofline_k1"] = k1_roofline("two_pass")
+            line["roofline_k1_one_pass"] = k1_roofline("one_pass")
         if world == 1 and not args.no_cpu_baseline and not args.tiny:
             line["cpu_baseline"] = cpu_baseline(cfg)
         print(json.dumps(line), flush=True)

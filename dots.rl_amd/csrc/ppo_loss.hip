@@ -1,9 +1,11 @@
 // K1 — fused actor loss (vanilla PPO clip + dual clip, entropy bonus, KL-to-ref), forward AND backward,
 // one pass over HBM. Replaces dp_actor.py:419-466 (+ core_algos.py:703-736, 815-889, 1272-1307).
 //
-// Layout: the (B, R) float32 inputs are flattened to N = B*R tokens in 1024-token chunks; each workgroup
-// (<= 8 per CU, all resident) owns a contiguous run of chunks and walks it 4 tokens per lane (16-B
-// nontemporal loads/stores, 1 KiB per wave-instruction per stream).
+// Layout: the (B, R) float32 inputs are flattened to N = B*R tokens in 1024-token chunks, 4 tokens per lane
+// (16-B nontemporal loads/stores, 1 KiB per wave-instruction per stream). Chunks are dealt to the workgroups
+// grid-stride (chunk = base + u * grid): at any moment the whole grid sweeps one window of every stream, which
+// keeps DRAM pages open; 2 workgroups per CU with 2 chunks in flight per lane (measured on K1's exact shape,
+// tools/probes/k1_stream_probe.hip: 6.1 TB/s vs 5.4 TB/s for contiguous per-workgroup runs at 4 per CU).
 // token-mean needs the global mask count before any gradient can be written. K1a streams ONLY the mask
 // (8 B/token for int64), writes it back as a 1-bit image (N/8 bytes, one 64-bit ballot per wave and
 // element slot) and folds the count (fixed order, last workgroup); K1b reads that count, the other inputs and the
@@ -24,8 +26,11 @@ constexpr int kNumPartials = 8;
 #ifndef DRL_K1_PACK_U
 #define DRL_K1_PACK_U 4
 #endif
-#ifndef DRL_K1_PREFETCH
-#define DRL_K1_PREFETCH 0
+#ifndef DRL_K1_U
+#define DRL_K1_U 1
+#endif
+#ifndef DRL_K1_PIPE
+#define DRL_K1_PIPE 1
 #endif
 
 // every K1 byte is touched once: nontemporal (streaming) loads and stores keep it out of the caches'
@@ -37,7 +42,12 @@ __device__ __forceinline__ nt_i2 ldnt(const int64_t* p) { return __builtin_nonte
 __device__ __forceinline__ void stnt(float* p, nt_f4 v) { __builtin_nontemporal_store(v, reinterpret_cast<nt_f4*>(p)); }
 
 
-struct Header {  // zeroed on the stream before every call
+// Zero before the first call (the caller zeroes the workspace once at allocation); K1b's last workgroup
+// zeroes it again after every other workgroup has finished with it, so a workspace reused on one stream
+// needs no per-call memset (a fill kernel + a kernel boundary, ~6 us per call). Every read of a header
+// field is an agent-scope atomic (sc1: never served from a stale L2 line of another XCD), every write a
+// write-through atomic store or RMW.
+struct Header {
   unsigned ticket;
   unsigned nonbinary;  // some mask value is not 0/1: K1b reads the original mask instead of the bits
   unsigned pack_ticket;
@@ -93,6 +103,37 @@ __device__ __forceinline__ void load_mask4(const void* m, int64_t t, int64_t N, 
   }
 }
 
+// 4 mask values at t (all inside N), unguarded. int64 -> float through the low word unless some lane holds a
+// value outside int32 (then the exact 64-bit conversion, wave-uniform branch): the general conversion costs
+// ~10 VALU instructions per value, a third of K1's per-token work
+template <int MDT>
+__device__ __forceinline__ void load_mask4_full(const void* m, int64_t t, float v[4]) {
+  if constexpr (MDT == DRL_I64) {
+    const int64_t* p = static_cast<const int64_t*>(m) + t;
+    const nt_i2 a = ldnt(p), b = ldnt(p + 2);
+    const long long x[4] = {a.x, a.y, b.x, b.y};
+    bool big = false;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) big |= x[j] != static_cast<long long>(static_cast<int32_t>(x[j]));
+    if (__builtin_expect(__any(big), 0)) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = static_cast<float>(x[j]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = static_cast<float>(static_cast<int32_t>(x[j]));
+    }
+  } else if constexpr (MDT == DRL_I32) {
+    const int4 a = *reinterpret_cast<const int4*>(static_cast<const int32_t*>(m) + t);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  } else if constexpr (MDT == DRL_U8) {
+    const uint32_t a = *reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(m) + t);
+    v[0] = a & 0xff; v[1] = (a >> 8) & 0xff; v[2] = (a >> 16) & 0xff; v[3] = a >> 24;
+  } else {
+    const nt_f4 a = ldnt(static_cast<const float*>(m) + t);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  }
+}
+
 __device__ __forceinline__ void load4(const float* p, int64_t t, int64_t N, float v[4]) {
   if (t + 3 < N) {
     const nt_f4 a = ldnt(p + t);
@@ -111,6 +152,20 @@ __device__ __forceinline__ void store4(float* p, int64_t t, int64_t N, const flo
     for (int j = 0; j < 4; ++j)
       if (t + j < N) p[t + j] = v[j];
   }
+}
+
+#ifndef DRL_K1_FASTEXP
+#define DRL_K1_FASTEXP 1
+#endif
+// exp of the clamped K3 log-ratio (|x| <= 20; no decision is taken on its value): v_exp_f32(x * log2 e) is within ~|x| * 2^-24 relative of the
+// correctly rounded value (<= 1.2e-6 at the clamp, ~1e-7 for the usual |x| < 1), 2 VALU instructions
+// instead of ocml's ~10 (range reduction + ldexp + overflow selects)
+__device__ __forceinline__ float k1_exp(float x) {
+#if DRL_K1_FASTEXP
+  return __expf(x);
+#else
+  return expf(x);
+#endif
 }
 
 // kl_penalty value and d/d logprob (core_algos.py:1272-1307)
@@ -133,7 +188,7 @@ __device__ __forceinline__ void kl_term(int kl, float lp, float ref, float& val,
       const float raw = ref - lp;
       const float k = fminf(fmaxf(raw, -20.f), 20.f);
       const float g1 = (raw >= -20.f && raw <= 20.f) ? 1.f : 0.f;
-      const float r = expf(k);
+      const float r = k1_exp(k);
       const float kld = (r - k) - 1.f;
       val = fminf(fmaxf(kld, -10.f), 10.f);
       const float g2 = (kld >= -10.f && kld <= 10.f) ? 1.f : 0.f;
@@ -156,16 +211,18 @@ __global__ __launch_bounds__(kThreads) void mask_pack_kernel(const void* mask, i
   float cnt = 0.f;
   double dcnt = 0.0;
   bool nonbin = false;
-  for (int64_t c0 = static_cast<int64_t>(blockIdx.x) * kU; c0 < nchunks; c0 += static_cast<int64_t>(gridDim.x) * kU) {
+  const int64_t G = gridDim.x;
+  for (int64_t c0 = blockIdx.x; c0 < nchunks; c0 += G * kU) {
     float m[kU][4];
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
-      const int64_t t = (c0 + u) * kChunk + tid * 4;
-      if (c0 + u < nchunks) load_mask4<MDT, false>(mask, t, N, m[u]);
+      const int64_t t = (c0 + u * G) * kChunk + tid * 4;
+      if (c0 + u * G < nchunks) load_mask4<MDT>(mask, t, N, m[u]);
       else m[u][0] = m[u][1] = m[u][2] = m[u][3] = 0.f;
     }
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
+      const int64_t cu = c0 + u * G;
       unsigned long long mine = 0;  // lane j (< 4) stores the wave's ballot of element slot j
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -175,7 +232,7 @@ __global__ __launch_bounds__(kThreads) void mask_pack_kernel(const void* mask, i
         mine = lane == j ? b : mine;
       }
       // the wave's 4 words are contiguous: one 32-B store instead of four single-lane ones
-      if (lane < 4 && c0 + u < nchunks) bits[(c0 + u) * 16 + wave * 4 + lane] = mine;
+      if (lane < 4 && cu < nchunks) bits[cu * 16 + wave * 4 + lane] = mine;
     }
     if (cnt >= 8388608.f) { dcnt += cnt; cnt = 0.f; }  // keep float partials exact
   }
@@ -194,52 +251,58 @@ __global__ __launch_bounds__(kThreads) void mask_pack_kernel(const void* mask, i
     __syncthreads();
     if (lane == 0) red[wave] = v;
     __syncthreads();
-    if (tid == 0) hdr->mask_total = red[0] + red[1] + red[2] + red[3];
+    if (tid == 0) store_sc1(&hdr->mask_total, red[0] + red[1] + red[2] + red[3]);
   }
 }
 
-// K1b: per-token loss terms, gradients and the workgroup's partial sums. One contiguous run of
-// 1024-token chunks per workgroup; 4 tokens per lane per chunk.
+// K1b: per-token loss terms, gradients and the workgroup's partial sums. Grid-stride 1024-token chunks,
+// DRL_K1_U in flight per workgroup; 4 tokens per lane per chunk.
 // FMODE / FKL: the aggregation mode and KL type fixed at compile time for the hot configurations
-// (kRuntime = read from Args), so the per-token math carries no mode branches.
+// (kRuntime = read from Args), so the per-token math carries no mode branches. The chunk loop itself is
+// instantiated per (mask source, entropy present, KL present) and runs branch-free over the chunks that lie
+// wholly inside N: a bounds-checked load is a branch, and hipcc waits vmcnt(0) at the join of every such
+// branch, which serialised the 6-7 loads per chunk (measured 0.54 -> see DESIGN.md §4).
 constexpr int kRuntime = -2;
-template <int MDT, int FMODE, int FKL>
-__global__ __launch_bounds__(kThreads) void ppo_loss_kernel(Args a) {
-  __shared__ double red[kThreads / kWave][kNumPartials];
-  const int mode = FMODE != kRuntime ? FMODE : a.mode;
-  const int kl = FKL != kRuntime ? FKL : a.kl;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int64_t N = a.N;
-  const int64_t nchunks = (N + kChunk - 1) / kChunk;
-  const int64_t per = (nchunks + gridDim.x - 1) / gridDim.x;
-  const int64_t c_begin = min(nchunks, per * blockIdx.x), c_end = min(nchunks, c_begin + per);
 
-  float cnt_total = 0.f;
-  bool use_bits = false;
-  if (mode == DRL_AGG_TOKEN_MEAN && a.token_count != nullptr) {
-    cnt_total = static_cast<float>(*a.token_count);  // one-pass form: the caller's count, mask read here
-  } else if (mode == DRL_AGG_TOKEN_MEAN && a.bits != nullptr) {
-    // global mask count, folded by the pack kernel's last workgroup
-    cnt_total = static_cast<float>(a.hdr->mask_total);
-    use_bits = a.hdr->nonbinary == 0;
-  }
-  const float denom_tm = cnt_total + 1e-8f;       // masked_mean: sum / (mask.sum() + 1e-8)
-  const float inv_denom_tm = 1.0f / denom_tm;     // upstream / D once, then * mask (MeanBackward style)
-  const float inv_B = 1.0f / static_cast<float>(a.B), inv_R = 1.0f / static_cast<float>(a.R);
-  const bool has_ent = a.ent != nullptr, has_kl = kl != DRL_KL_NONE;
-  const bool want_dlp = a.dlp != nullptr, want_dent = a.dent != nullptr;
-  const bool tm = mode == DRL_AGG_TOKEN_MEAN, smtm = mode == DRL_AGG_SEQ_MEAN_TOKEN_MEAN;
-  float s_pg = 0.f, s_clip = 0.f, s_kl = 0.f, s_cliplow = 0.f, s_ent = 0.f, s_kld = 0.f, s_cnt = 0.f;
+struct Chunk {
+  float m[4], old[4], lp[4], A[4], en[4], rf[4];
+};
 
-  // software pipeline: chunk c+1's loads are issued before chunk c's math (DRL_K1_PREFETCH), so every wave
-  // keeps 5-6 x 16 B per lane in flight while it computes
-  struct Chunk {
-    float m[4], old[4], lp[4], A[4], en[4], rf[4];
-  };
-  auto load_chunk = [&](int64_t c, Chunk& k) {
-    const int64_t t = c * kChunk + tid * 4;
-    const int64_t tt = c < c_end ? t : N;  // past the run: every load4 takes its bounds path and yields 0
-    if (use_bits && c < c_end) {
+struct Sums {
+  float pg = 0.f, clip = 0.f, kl = 0.f, cliplow = 0.f, ent = 0.f, kld = 0.f, cnt = 0.f;
+};
+
+// FULL: the chunk lies wholly inside N (no bounds checks, no branches); else every access is guarded
+template <int MDT, bool BITS, bool ENT, bool KL, bool FULL>
+__device__ __forceinline__ void load_chunk(const Args& a, int64_t c, int64_t N, int tid, int lane, int wave, Chunk& k) {
+  const int64_t t = c * kChunk + tid * 4;
+  if constexpr (FULL) {
+    if constexpr (BITS) {
+      // the wave's four 64-bit ballots (32 contiguous bytes, the same address on every lane)
+      const nt_i2* bp = reinterpret_cast<const nt_i2*>(a.bits + c * 16 + wave * 4);
+      const nt_i2 b0 = bp[0], b1 = bp[1];
+      const unsigned long long w[4] = {static_cast<unsigned long long>(b0.x), static_cast<unsigned long long>(b0.y),
+                                       static_cast<unsigned long long>(b1.x), static_cast<unsigned long long>(b1.y)};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) k.m[j] = ((w[j] >> lane) & 1ull) ? 1.f : 0.f;
+    } else {
+      load_mask4_full<MDT>(a.mask, t, k.m);
+    }
+    const nt_f4 o = ldnt(a.old_lp + t), l = ldnt(a.lp + t), A = ldnt(a.adv + t);
+    k.old[0] = o.x; k.old[1] = o.y; k.old[2] = o.z; k.old[3] = o.w;
+    k.lp[0] = l.x; k.lp[1] = l.y; k.lp[2] = l.z; k.lp[3] = l.w;
+    k.A[0] = A.x; k.A[1] = A.y; k.A[2] = A.z; k.A[3] = A.w;
+    if constexpr (ENT) {
+      const nt_f4 e = ldnt(a.ent + t);
+      k.en[0] = e.x; k.en[1] = e.y; k.en[2] = e.z; k.en[3] = e.w;
+    }
+    if constexpr (KL) {
+      const nt_f4 r = ldnt(a.ref + t);
+      k.rf[0] = r.x; k.rf[1] = r.y; k.rf[2] = r.z; k.rf[3] = r.w;
+    }
+  } else {
+    const int64_t tt = c * kChunk < N ? t : N;  // past the end: every load4 takes its bounds path and yields 0
+    if (BITS && c * kChunk < N) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) k.m[j] = ((a.bits[c * 16 + wave * 4 + j] >> lane) & 1ull) ? 1.f : 0.f;
     } else {
@@ -248,95 +311,193 @@ __global__ __launch_bounds__(kThreads) void ppo_loss_kernel(Args a) {
     load4(a.old_lp, tt, N, k.old);
     load4(a.lp, tt, N, k.lp);
     load4(a.adv, tt, N, k.A);
-    if (has_ent) load4(a.ent, tt, N, k.en);
-    if (has_kl) load4(a.ref, tt, N, k.rf);
-  };
-  Chunk cur;
-#if DRL_K1_PREFETCH
-  Chunk nxt;
-#endif
-  if (c_begin < c_end) load_chunk(c_begin, cur);
-  for (int64_t c0 = c_begin; c0 < c_end; ++c0) {
-#if DRL_K1_PREFETCH
-    if (c0 + 1 < c_end) load_chunk(c0 + 1, nxt);
-#endif
-    const int64_t t = c0 * kChunk + tid * 4;
-    float* m = cur.m;
-    float* old = cur.old;
-    float* lp = cur.lp;
-    float* A = cur.A;
-    float* en = cur.en;
-    float* rf = cur.rf;
-    float g_lp[4], g_en[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const bool valid = t + j < N;
-      // compute_policy_loss_vanilla, float32 with the reference's op order
-      const float raw = lp[j] - old[j];
-      const float nkl = fminf(fmaxf(raw, -20.f), 20.f);
-      const float gate = (raw >= -20.f && raw <= 20.f) ? 1.f : 0.f;
-      const float ratio = expf(nkl);
-      const float negA = -A[j];
-      const float L1 = negA * ratio;
-      const float rc = fminf(fmaxf(ratio, a.lo), a.hi);
-      const float gc = (ratio >= a.lo && ratio <= a.hi) ? 1.f : 0.f;
-      const float L2 = negA * rc;
-      const float C1 = fmaxf(L1, L2);
-      const float w1 = L1 > L2 ? 1.f : (L1 == L2 ? 0.5f : 0.f);  // torch.maximum splits ties
-      const float dC1 = (w1 + (1.f - w1) * gc) * negA;
-      const float L3 = negA * a.clip_c;
-      const float C2 = fminf(L3, C1);
-      const float wc = C1 < L3 ? 1.f : (C1 == L3 ? 0.5f : 0.f);
-      const bool neg = A[j] < 0.f;
-      const bool gpg = a.policy == DRL_POLICY_GPG;  // uniform per launch
-      // GPG (core_algos.py:957-975): pg = -log_prob * advantages, d pg / d log_prob = -A
-      const float pg = gpg ? (-lp[j]) * A[j] : (neg ? C2 : C1);
-      const float dpg = gpg ? -A[j] : (neg ? wc * dC1 : dC1) * ratio * gate;
-
-      const float mj = valid ? m[j] : 0.f;
-      const bool mb = mj != 0.f;
-      // d agg / d loss_mat of this token, and its forward contribution
-      float rc_inv = 0.f;
-      if (smtm) rc_inv = 1.0f / a.rowcnt[valid ? (t + j) / a.R : 0];
-      float w;
-      if (tm) w = mb ? inv_denom_tm * mj : 0.f;
-      else if (mode == DRL_AGG_SEQ_MEAN_TOKEN_SUM) w = inv_B * mj;
-      else if (smtm) w = mj * (inv_B * rc_inv);
-      else w = inv_R * mj;
-      // token-mean sums where(mask, x, 0) * mask; the seq modes x * mask (core_algos.py:716-733)
-      auto agg_val = [&](float x) -> float {
-        if (tm) return mb ? x * mj : 0.f;
-        if (smtm) return (x * mj) * rc_inv;
-        return x * mj;
-      };
-      if (valid) {
-        s_pg += agg_val(pg);
-        s_cnt += mj;
-        if (!gpg) {  // GPG reports clipfrac / ppo_kl / clipfrac_lower as 0
-          s_clip += (mb && L2 > L1) ? mj : 0.f;
-          s_kl += mb ? -nkl * mj : 0.f;
-          s_cliplow += (mb && C1 > L3 && neg) ? mj : 0.f;
-        }
-      }
-      float gl = w * dpg;
-      if (has_kl) {
-        float kv, dk;
-        kl_term(kl, lp[j], rf[j], kv, dk);
-        if (valid) s_kld += agg_val(kv);
-        gl += a.kl_coef * (w * dk);
-      }
-      if (has_ent && valid) s_ent += agg_val(en[j]);
-      g_lp[j] = a.lsf * gl;
-      g_en[j] = a.ent_coef != 0.f ? a.lsf * (-a.ent_coef * w) : 0.f;
-    }
-    if (want_dlp) store4(a.dlp, t, N, g_lp);
-    if (want_dent) store4(a.dent, t, N, g_en);
-#if DRL_K1_PREFETCH
-    cur = nxt;
-#else
-    if (c0 + 1 < c_end) load_chunk(c0 + 1, cur);
-#endif
+    if constexpr (ENT) load4(a.ent, tt, N, k.en);
+    if constexpr (KL) load4(a.ref, tt, N, k.rf);
   }
+}
+
+// per-token loss terms + gradients of one chunk (past the end, t >= N: nothing counted or stored)
+template <int MODE, int KLT, bool ENT, bool KL, bool FULL>
+__device__ __forceinline__ void process_chunk(const Args& a, const Chunk& k, int64_t c, int64_t N, int tid,
+                                              float inv_denom_tm, Sums& S) {
+  const int mode = MODE != kRuntime ? MODE : a.mode;
+  const int kl = KLT != kRuntime ? KLT : a.kl;
+  const float inv_B = 1.0f / static_cast<float>(a.B), inv_R = 1.0f / static_cast<float>(a.R);
+  const bool tm = mode == DRL_AGG_TOKEN_MEAN, smtm = mode == DRL_AGG_SEQ_MEAN_TOKEN_MEAN;
+  const int64_t t = c * kChunk + tid * 4;
+  const float* m = k.m;
+  const float* old = k.old;
+  const float* lp = k.lp;
+  const float* A = k.A;
+  float g_lp[4], g_en[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const bool valid = FULL || t + j < N;
+    // compute_policy_loss_vanilla, float32 with the reference's op order
+    const float raw = lp[j] - old[j];
+    const float nkl = fminf(fmaxf(raw, -20.f), 20.f);
+    const float gate = (raw >= -20.f && raw <= 20.f) ? 1.f : 0.f;
+    const float ratio = expf(nkl);  // exact: the clip / tie decisions on ratio must match torch.exp
+    const float negA = -A[j];
+    const float L1 = negA * ratio;
+    const float rc = fminf(fmaxf(ratio, a.lo), a.hi);
+    const float gc = (ratio >= a.lo && ratio <= a.hi) ? 1.f : 0.f;
+    const float L2 = negA * rc;
+    const float C1 = fmaxf(L1, L2);
+    const float w1 = L1 > L2 ? 1.f : (L1 == L2 ? 0.5f : 0.f);  // torch.maximum splits ties
+    const float dC1 = (w1 + (1.f - w1) * gc) * negA;
+    const float L3 = negA * a.clip_c;
+    const float C2 = fminf(L3, C1);
+    const float wc = C1 < L3 ? 1.f : (C1 == L3 ? 0.5f : 0.f);
+    const bool neg = A[j] < 0.f;
+    const bool gpg = a.policy == DRL_POLICY_GPG;  // uniform per launch
+    // GPG (core_algos.py:957-975): pg = -log_prob * advantages, d pg / d log_prob = -A
+    const float pg = gpg ? (-lp[j]) * A[j] : (neg ? C2 : C1);
+    const float dpg = gpg ? -A[j] : (neg ? wc * dC1 : dC1) * ratio * gate;
+
+    const float mj = valid ? m[j] : 0.f;
+    const bool mb = mj != 0.f;
+    // d agg / d loss_mat of this token, and its forward contribution
+    float rc_inv = 0.f;
+    if (smtm) rc_inv = 1.0f / a.rowcnt[valid ? (t + j) / a.R : 0];
+    float w;
+    if (tm) w = mb ? inv_denom_tm * mj : 0.f;
+    else if (mode == DRL_AGG_SEQ_MEAN_TOKEN_SUM) w = inv_B * mj;
+    else if (smtm) w = mj * (inv_B * rc_inv);
+    else w = inv_R * mj;
+    // token-mean sums where(mask, x, 0) * mask; the seq modes x * mask (core_algos.py:716-733)
+    auto agg_val = [&](float x) -> float {
+      if (tm) return mb ? x * mj : 0.f;
+      if (smtm) return (x * mj) * rc_inv;
+      return x * mj;
+    };
+    if (valid) {
+      S.pg += agg_val(pg);
+      S.cnt += mj;
+      if (!gpg) {  // GPG reports clipfrac / ppo_kl / clipfrac_lower as 0
+        S.clip += (mb && L2 > L1) ? mj : 0.f;
+        S.kl += mb ? -nkl * mj : 0.f;
+        S.cliplow += (mb && C1 > L3 && neg) ? mj : 0.f;
+      }
+    }
+    float gl = w * dpg;
+    if constexpr (KL) {
+      float kv, dk;
+      kl_term(kl, lp[j], k.rf[j], kv, dk);
+      if (valid) S.kld += agg_val(kv);
+      gl += a.kl_coef * (w * dk);
+    }
+    if constexpr (ENT) {
+      if (valid) S.ent += agg_val(k.en[j]);
+    }
+    g_lp[j] = a.lsf * gl;
+    g_en[j] = a.ent_coef != 0.f ? a.lsf * (-a.ent_coef * w) : 0.f;
+  }
+  if constexpr (FULL) {
+    if (a.dlp != nullptr) stnt(a.dlp + t, nt_f4{g_lp[0], g_lp[1], g_lp[2], g_lp[3]});
+    if (a.dent != nullptr) stnt(a.dent + t, nt_f4{g_en[0], g_en[1], g_en[2], g_en[3]});
+  } else {
+    if (a.dlp != nullptr) store4(a.dlp, t, N, g_lp);
+    if (a.dent != nullptr) store4(a.dent, t, N, g_en);
+  }
+}
+
+// the workgroup's chunks: blockIdx.x, +G, +2G, ...; kU full chunks loaded before any is computed, then the
+// remainder (at most kU - 1 full chunks and the partial last chunk) one at a time
+template <int MDT, int MODE, int KLT, bool BITS, bool ENT, bool KL>
+__device__ __forceinline__ void stream_chunks(const Args& a, float inv_denom_tm, Sums& S) {
+  constexpr int kU = DRL_K1_U;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t N = a.N, G = gridDim.x;
+  const int64_t nfull = N / kChunk, nchunks = (N + kChunk - 1) / kChunk;
+  int64_t c0 = blockIdx.x;
+  auto load_group = [&](int64_t c, Chunk* ck) {
+#pragma unroll
+    for (int u = 0; u < kU; ++u) load_chunk<MDT, BITS, ENT, KL, true>(a, c + u * G, N, tid, lane, wave, ck[u]);
+  };
+  auto process_group = [&](int64_t c, const Chunk* ck) {
+#pragma unroll
+    for (int u = 0; u < kU; ++u) process_chunk<MODE, KLT, ENT, KL, true>(a, ck[u], c + u * G, N, tid, inv_denom_tm, S);
+  };
+#if DRL_K1_PIPE
+  // software pipeline, ping-pong register sets: the next group's loads are in flight while this group computes
+  if (c0 + (kU - 1) * G < nfull) {
+    Chunk x[kU], y[kU];
+    load_group(c0, x);
+    for (;;) {
+      int64_t cn = c0 + G * kU;
+      bool more = cn + (kU - 1) * G < nfull;
+      if (more) load_group(cn, y);
+      process_group(c0, x);
+      c0 = cn;
+      if (!more) break;
+      cn = c0 + G * kU;
+      more = cn + (kU - 1) * G < nfull;
+      if (more) load_group(cn, x);
+      process_group(c0, y);
+      c0 = cn;
+      if (!more) break;
+    }
+  }
+#else
+  for (; c0 + (kU - 1) * G < nfull; c0 += G * kU) {
+    Chunk ck[kU];
+    load_group(c0, ck);
+    process_group(c0, ck);
+  }
+#endif
+  for (; c0 < nchunks; c0 += G) {
+    Chunk ck;
+    if (c0 < nfull) {
+      load_chunk<MDT, BITS, ENT, KL, true>(a, c0, N, tid, lane, wave, ck);
+      process_chunk<MODE, KLT, ENT, KL, true>(a, ck, c0, N, tid, inv_denom_tm, S);
+    } else {
+      load_chunk<MDT, BITS, ENT, KL, false>(a, c0, N, tid, lane, wave, ck);
+      process_chunk<MODE, KLT, ENT, KL, false>(a, ck, c0, N, tid, inv_denom_tm, S);
+    }
+  }
+}
+
+template <int MDT, int MODE, int KLT, bool BITS>
+__device__ __forceinline__ void stream_dispatch(const Args& a, bool has_ent, bool has_kl, float inv_denom_tm, Sums& S) {
+  if constexpr (KLT == DRL_KL_NONE) {
+    if (has_ent) stream_chunks<MDT, MODE, KLT, BITS, true, false>(a, inv_denom_tm, S);
+    else stream_chunks<MDT, MODE, KLT, BITS, false, false>(a, inv_denom_tm, S);
+  } else if constexpr (KLT != kRuntime) {
+    if (has_ent) stream_chunks<MDT, MODE, KLT, BITS, true, true>(a, inv_denom_tm, S);
+    else stream_chunks<MDT, MODE, KLT, BITS, false, true>(a, inv_denom_tm, S);
+  } else {
+    if (has_ent && has_kl) stream_chunks<MDT, MODE, KLT, BITS, true, true>(a, inv_denom_tm, S);
+    else if (has_ent) stream_chunks<MDT, MODE, KLT, BITS, true, false>(a, inv_denom_tm, S);
+    else if (has_kl) stream_chunks<MDT, MODE, KLT, BITS, false, true>(a, inv_denom_tm, S);
+    else stream_chunks<MDT, MODE, KLT, BITS, false, false>(a, inv_denom_tm, S);
+  }
+}
+
+template <int MDT, int FMODE, int FKL>
+__global__ __launch_bounds__(kThreads) void ppo_loss_kernel(Args a) {
+  __shared__ double red[kThreads / kWave][kNumPartials];
+  const int mode = FMODE != kRuntime ? FMODE : a.mode;
+  const int kl = FKL != kRuntime ? FKL : a.kl;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+
+  float cnt_total = 0.f;
+  bool use_bits = false;
+  if (mode == DRL_AGG_TOKEN_MEAN && a.token_count != nullptr) {
+    cnt_total = static_cast<float>(*a.token_count);  // one-pass form: the caller's count, mask read here
+  } else if (mode == DRL_AGG_TOKEN_MEAN && a.bits != nullptr) {
+    // global mask count, folded by the pack kernel's last workgroup
+    cnt_total = static_cast<float>(load_sc1(&a.hdr->mask_total));
+    use_bits = __hip_atomic_load(&a.hdr->nonbinary, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0;
+  }
+  const float denom_tm = cnt_total + 1e-8f;       // masked_mean: sum / (mask.sum() + 1e-8)
+  const float inv_denom_tm = 1.0f / denom_tm;     // upstream / D once, then * mask (MeanBackward style)
+  const bool has_ent = a.ent != nullptr, has_kl = kl != DRL_KL_NONE;
+  Sums S;
+  if (use_bits) stream_dispatch<MDT, FMODE, FKL, true>(a, has_ent, has_kl, inv_denom_tm, S);
+  else stream_dispatch<MDT, FMODE, FKL, false>(a, has_ent, has_kl, inv_denom_tm, S);
+  const float s_pg = S.pg, s_clip = S.clip, s_kl = S.kl, s_cliplow = S.cliplow, s_ent = S.ent, s_kld = S.kld,
+              s_cnt = S.cnt;
 
   // ---- workgroup partials -> the last workgroup reduces all of them in a fixed order
   const float vals[kNumPartials] = {s_pg, s_clip, s_kl, s_cliplow, s_ent, s_kld, s_cnt, 0.f};
@@ -380,6 +541,11 @@ __global__ __launch_bounds__(kThreads) void ppo_loss_kernel(Args a) {
       a.out[DRL_PPO_OUT_KL_LOSS] = static_cast<float>(kl_loss);
       a.out[DRL_PPO_OUT_LOSS] = static_cast<float>(total * a.lsf);
       a.out[DRL_PPO_OUT_MASK_COUNT] = static_cast<float>(cnt);
+      // every other workgroup has taken its ticket, i.e. is past its last header read: leave the header zero
+      __hip_atomic_store(&a.hdr->ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&a.hdr->pack_ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&a.hdr->nonbinary, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      store_sc1(&a.hdr->mask_total, 0.0);
     }
   }
 }
@@ -397,7 +563,7 @@ __global__ __launch_bounds__(256) void row_count_kernel(const void* mask, int64_
 }
 
 #ifndef DRL_K1_WG_PER_CU
-#define DRL_K1_WG_PER_CU 4
+#define DRL_K1_WG_PER_CU 2
 #endif
 #ifndef DRL_K1_PACK_WG_PER_CU
 #define DRL_K1_PACK_WG_PER_CU 4
@@ -437,9 +603,9 @@ int launch(Args a, const Layout& L, char* ws, hipStream_t s) {
     DRL_LAUNCH_CHECK();
     a.bits = bits;
   }
-  // >= 2 chunks per workgroup before the grid reaches 4 workgroups per CU
+  // one chunk per workgroup until the grid reaches DRL_K1_WG_PER_CU workgroups per CU
   const int grid = static_cast<int>(std::max<int64_t>(
-      1, std::min<int64_t>(static_cast<int64_t>(cu_count()) * DRL_K1_WG_PER_CU, (nchunks + 1) / 2)));
+      1, std::min<int64_t>(static_cast<int64_t>(cu_count()) * DRL_K1_WG_PER_CU, nchunks)));
   if (a.mode == DRL_AGG_TOKEN_MEAN && a.kl == DRL_KL_K3)
     hipLaunchKernelGGL((ppo_loss_kernel<MDT, DRL_AGG_TOKEN_MEAN, DRL_KL_K3>), dim3(grid), dim3(kThreads), 0, s, a);
   else if (a.mode == DRL_AGG_TOKEN_MEAN && a.kl == DRL_KL_NONE)
@@ -562,8 +728,7 @@ int drl_ppo_loss_fwd_bwd(const float* old_log_prob, const float* log_prob, const
                 p->policy_loss);
   a.policy = p->policy_loss;
 
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  DRL_HIP(hipMemsetAsync(ws, 0, sizeof(Header), s));
+  hipStream_t s = static_cast<hipStream_t>(stream);  // the header is zero on entry (see Header)
   switch (mask_dtype) {
     case DRL_I64: return launch<DRL_I64>(a, L, ws, s);
     case DRL_I32: return launch<DRL_I32>(a, L, ws, s);

@@ -124,6 +124,22 @@ class _Workspace:
 _ws = _Workspace()
 
 
+class _ZeroHeaderWorkspace(_Workspace):
+    """K1's scratch: zeroed at allocation; the kernel leaves its 256-byte header zero after every call
+    (include/dotsrl_amd.h, drl_ppo_loss_fwd_bwd), so no per-call memset."""
+
+    def get(self, nbytes: int, device) -> torch.Tensor:
+        key = (device.index if device.index is not None else torch.cuda.current_device())
+        b = self.buf.get(key)
+        if b is None or b.numel() < nbytes:
+            b = torch.zeros(max(nbytes, 1 << 16), dtype=torch.uint8, device=device)
+            self.buf[key] = b
+        return b
+
+
+_ws_k1 = _ZeroHeaderWorkspace()
+
+
 def mask_dtype_code(mask: torch.Tensor) -> int:
     try:
         return _MASK_DTYPES[mask.dtype]
@@ -163,7 +179,7 @@ def ppo_loss_fwd_bwd(old_log_prob, log_prob, advantages, response_mask, entropy=
         dentropy = torch.empty_like(log_prob)
     L = lib()
     nb = L.drl_ppo_loss_workspace_bytes(B, R)
-    ws = _ws.get(nb, dev)
+    ws = _ws_k1.get(nb, dev)
     check(L.drl_ppo_loss_fwd_bwd(_p(old_log_prob), _p(log_prob), _p(advantages), _p(response_mask),
                                  mask_dtype_code(response_mask), _p(entropy), _p(ref_log_prob), B, R,
                                  ctypes.byref(prm), _p(out), _p(dlogp if want_dlogp else None),

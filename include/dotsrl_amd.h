@@ -75,6 +75,9 @@ int drl_device_cu_count(void);
  * Inputs (B, R) float32, response_mask (B, R) of `mask_dtype` (I64/I32/U8/F32).
  * entropy may be NULL (entropy_coeff must then be 0); ref_log_prob may be NULL (kl_type must be NONE).
  * out_scalars: device float[DRL_PPO_OUT_N], see the enum. dlog_prob / dentropy may be NULL.
+ * workspace: drl_ppo_loss_workspace_bytes(B, R) bytes whose first 256 bytes are ZERO before the first call
+ * (hipMemset once at allocation); every call leaves them zero again, so a workspace reused by calls on one
+ * stream needs no per-call memset. Use it for K1 only (drl_agg_loss keeps its own).
  * ---------------------------------------------------------------------------------------------- */
 typedef struct drl_ppo_loss_params {
   float clip_ratio_low;    /* actor.clip_ratio_low (defaults to clip_ratio) */
