@@ -71,6 +71,9 @@ DEFAULTS = dict(
             clip_ratio_high=0.2, clip_ratio_c=3.0, policy_loss=dict(loss_mode="vanilla"), loss_agg_mode="token-mean",
             entropy_coeff=0.0, use_kl_loss=True, kl_loss_coef=0.001, kl_loss_type="low_var_kl", ppo_epochs=1,
             shuffle=False, grad_clip=1.0, ulysses_sequence_parallel_size=1,
+            # shard: fp32 master + AdamW moments split over the DP ranks (ZeRO-style; FSDP FULL_SHARD in the
+            # reference); "auto" = when replicated state would exceed 64 GB per GPU (workers._shard_spec)
+            fsdp_config=dict(shard="auto", fsdp_size=-1, param_offload=False, optimizer_offload=False),
             optim=dict(lr=1e-6, lr_warmup_steps_ratio=0.0, total_training_steps=-1, weight_decay=0.01,
                        lr_warmup_steps=-1, betas=[0.9, 0.999], eps=1e-8, warmup_style="constant", min_lr_ratio=0.0),
         ),
@@ -91,6 +94,7 @@ DEFAULTS = dict(
     critic=dict(
         # None = the reference's ${oc.select:actor_rollout_ref...} interpolation (resolve_critic_config)
         strategy="mi355x", enable=None, rollout_n=None,
+        fsdp_config=dict(shard="auto", fsdp_size=-1, param_offload=False, optimizer_offload=False),
         optim=dict(lr=1e-5, lr_warmup_steps_ratio=0.0, total_training_steps=-1, weight_decay=0.01, lr_warmup_steps=-1,
                    betas=[0.9, 0.999], eps=1e-8, warmup_style="constant"),
         model=dict(path="random:qwen2.5-0.5b", override_config={}, use_remove_padding=False, dtype="bfloat16",

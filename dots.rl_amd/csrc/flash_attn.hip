@@ -65,18 +65,22 @@ __device__ __forceinline__ u16x4 lds_tr16(const uint16_t* p) {
 // unit u ^ f(r). f is a bijection on r & 7 (conflict-free 16-B row writes: 8 consecutive rows cover all 8
 // units) that also flips bit 2 between rows r and r + 2 (the 4 rows of a transposing read never share banks).
 __device__ __forceinline__ int xsw(int r) { return (r & 7) ^ ((r & 2) << 1); }
+// XR = row length in elements (the head dim: 64 -> 128-B rows, 128 -> 256-B rows; the swizzle permutes the
+// 16-B units within each aligned group of 8)
+template <int XR = 64>
 __device__ __forceinline__ int ximg_off(int r, int col) {  // element offset of (row r, column col)
-  return r * 64 + 8 * ((col >> 3) ^ xsw(r)) + (col & 7);
+  return r * XR + 8 * ((col >> 3) ^ xsw(r)) + (col & 7);
 }
 
 // A operand "X^T" (rows = head dim, k = positions in the accumulator order) of a 32-position x 64 tile X in
 // the swizzled image above: k-step s, head-dim tile mt. Two transposing reads: element j of lane half h is
 // position 16s + 8(j>>2) + 4h + (j&3), head-dim 32mt + (lane & 31).
+template <int XR = 64>
 __device__ __forceinline__ u16x8 lds_xt_operand(const uint16_t* x, int mt, int s, int lane) {
   const int i = lane & 15, q = i >> 2, p = i & 3, h = lane >> 5;
   const int col = 32 * mt + (lane & 16) + 4 * p;
-  const u16x4 lo = lds_tr16(x + ximg_off(16 * s + 4 * h + q, col));
-  const u16x4 hi = lds_tr16(x + ximg_off(16 * s + 8 + 4 * h + q, col));
+  const u16x4 lo = lds_tr16(x + ximg_off<XR>(16 * s + 4 * h + q, col));
+  const u16x4 hi = lds_tr16(x + ximg_off<XR>(16 * s + 8 + 4 * h + q, col));
   return u16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
@@ -552,17 +556,23 @@ __device__ __forceinline__ void dkdv_rows(const uint16_t* qbase, const uint16_t*
   }
 }
 
-template <int D>
-__global__ __launch_bounds__(512) void flash_dkdv_kernel(FlashBwdArgs a) {
+// NW waves per workgroup; wave w handles query heads w, w + NW, ... of the KV head (its dK / dV partials
+// accumulate over them in registers). head_dim 64: NW = 8 (one head per wave, G <= 8); head_dim 128: NW = 4,
+// one wave per SIMD, so the 128 accumulator registers of dK^T / dV^T and the Q / dO rows fit without spilling.
+template <int D, int NW>
+__global__ __launch_bounds__(64 * NW) void flash_dkdv_kernel(FlashBwdArgs a) {
   constexpr int KS = D / 16, MT = D / 32, KROW = D + 8;
-  // per-wave swizzled image of the current query tile's Q and dO rows (ximg_off)
-  constexpr int XROW = 64;
-  static_assert(D == 64, "the Q / dO image is laid out for head_dim 64");
-  __shared__ float red[2][MT][16][64];  // [dk/dv][tile][register][lane]: conflict-free per register
+  // per-wave swizzled image of the current query tile's Q and dO rows (ximg_off); after the key loop the same
+  // LDS holds the cross-wave dK / dV reduction
+  constexpr int XROW = D;
+  static_assert(D == 64 || D == 128, "head_dim 64 or 128");
+  static_assert(2 * MT * 16 * 64 * 4 <= NW * 2 * 32 * XROW * 2, "reduction buffer must fit the image space");
   __shared__ __attribute__((aligned(16))) uint16_t kv_lds[2][32 * KROW];  // this key tile's K and V rows
-  __shared__ __attribute__((aligned(16))) uint16_t xw[8][2][32 * XROW];    // [wave][Q / dO][position][d]
+  __shared__ __attribute__((aligned(16))) uint16_t xw[NW][2][32 * XROW];   // [wave][Q / dO][position][d]
+  // [dk/dv][tile][register][lane]: conflict-free per register; aliases xw after the loop
+  auto red = reinterpret_cast<float (*)[MT][16][64]>(&xw[0][0][0]);
   const int tid = threadIdx.x;
-  const int lane = tid & 63, g = tid >> 6;
+  const int lane = tid & 63, wv = tid >> 6;
   const int li = lane & 31, h = lane >> 5;
   const int T = static_cast<int>(a.T);
   const int ntiles = (T + 31) / 32;
@@ -574,7 +584,6 @@ __global__ __launch_bounds__(512) void flash_dkdv_kernel(FlashBwdArgs a) {
   const int key = k0 + li;
   const bool kin = key < T;
   const bool kval = kin && a.valid[b * a.ld_valid + key] != 0;
-  const int64_t head = bh * a.G + g;
   // stage the key tile's K and V rows once; every wave (query head) reads them from LDS
   for (int c = tid; c < 2 * 32 * (D / 8); c += blockDim.x) {
     const int which = c / (32 * (D / 8)), cc = c % (32 * (D / 8)), row = cc / (D / 8), col = cc % (D / 8);
@@ -589,20 +598,24 @@ __global__ __launch_bounds__(512) void flash_dkdv_kernel(FlashBwdArgs a) {
   f32x16 dkt[MT], dvt[MT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) dkt[mt] = dvt[mt] = f32x16{};
+  uint16_t* xq = xw[wv][0];
+  uint16_t* xd = xw[wv][1];
+  // NW = 8 >= G: the block has exactly G waves, one head each (a one-trip loop the compiler folds)
+  const int g_end = NW >= 8 ? wv + 1 : static_cast<int>(a.G);
+  for (int g = wv; g < g_end; g += NW) {
+  const int64_t head = bh * a.G + g;
   const uint16_t* qbase = a.q + head * a.T * D;
   const float* lser = a.lse + head * a.T;
   const float* dlr = a.delta + head * a.T;
   u16x8 qa[KS], da[KS];
   dkdv_rows<D>(qbase, a.dout, b, hkv, a.Hkv, a.G, g, T, k0 + li, h, qa, da);
-  uint16_t* xq = xw[g][0];
-  uint16_t* xd = xw[g][1];
   for (int t0 = k0; t0 < T; t0 += 32) {
     // this tile's Q and dO rows into the wave's LDS image (row li, head dims 16s + 8h .. + 7); the transposed
     // operands of dV / dK are read back from it after the softmax (no head-dim-major copies in HBM)
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
-      *reinterpret_cast<u16x8*>(xq + ximg_off(li, 16 * s + 8 * h)) = qa[s];
-      *reinterpret_cast<u16x8*>(xd + ximg_off(li, 16 * s + 8 * h)) = da[s];
+      *reinterpret_cast<u16x8*>(xq + ximg_off<XROW>(li, 16 * s + 8 * h)) = qa[s];
+      *reinterpret_cast<u16x8*>(xd + ximg_off<XROW>(li, 16 * s + 8 * h)) = da[s];
     }
     float4 l4[4], d4[4];
 #pragma unroll
@@ -649,16 +662,20 @@ __global__ __launch_bounds__(512) void flash_dkdv_kernel(FlashBwdArgs a) {
     for (int mt = 0; mt < MT; ++mt) {
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        const u16x8 dov = lds_xt_operand(xd, mt, s, lane);
-        const u16x8 qtv = lds_xt_operand(xq, mt, s, lane);
+        const u16x8 dov = lds_xt_operand<XROW>(xd, mt, s, lane);
+        const u16x8 qtv = lds_xt_operand<XROW>(xq, mt, s, lane);
         dvt[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(dov), as_bf16x8(pb[s]), dvt[mt], 0, 0, 0);
         dkt[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(qtv), as_bf16x8(dsb[s]), dkt[mt], 0, 0, 0);
       }
     }
   }
-  // sum the G heads' partials in LDS in wave order (deterministic), wave 0 writes
-  for (int w = 0; w < a.G; ++w) {
-    if (g == w) {
+  }  // query heads of this wave
+  // sum the waves' partials in LDS in wave order (deterministic), wave 0 writes; the buffer overlays the
+  // Q / dO images, so every wave must be past its key loop first
+  __syncthreads();
+  const int nw = a.G < NW ? static_cast<int>(a.G) : NW;
+  for (int w = 0; w < nw; ++w) {
+    if (wv == w) {
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
 #pragma unroll
@@ -670,7 +687,7 @@ __global__ __launch_bounds__(512) void flash_dkdv_kernel(FlashBwdArgs a) {
     }
     __syncthreads();
   }
-  if (g != 0 || !kin) return;
+  if (wv != 0 || !kin) return;
   uint16_t* dkrow = a.dk + (bh * a.T + key) * D;
   uint16_t* dvrow = a.dv + (bh * a.T + key) * D;
 #pragma unroll
@@ -1151,7 +1168,7 @@ int drl_flash_attn_bwd(const void* q, const void* k, const void* kt, const void*
   DRL_CHECK_ARG(q && k && kt && v && o && dout && lse && key_valid && delta && dq && dk && dv,
                 "NULL input");
   DRL_CHECK_ARG(dt == DRL_BF16, "flash attention runs on bf16 operands");
-  DRL_CHECK_ARG(D == 64, "the fused backward is built for head_dim 64 (LDS budget of the per-wave Q / dO images)");
+  DRL_CHECK_ARG(D == 64 || D == 128, "the fused backward supports head_dim 64 and 128");
   DRL_CHECK_ARG(B >= 1 && Hkv >= 1 && G >= 1 && G <= 8 && T >= 1, "bad shape");
   DRL_CHECK_ARG(T % 8 == 0 && ld_t >= T && ld_t % 8 == 0, "T and ld_t must be multiples of 8");
   DRL_CHECK_ARG(ld_valid >= T, "ld_valid < T");
@@ -1161,10 +1178,15 @@ int drl_flash_attn_bwd(const void* q, const void* k, const void* kt, const void*
                  static_cast<uint16_t*>(dv), Hkv, G, T, ld_t, scale, scale * 1.4426950408889634f};
   const dim3 grid(static_cast<unsigned>((T + 31) / 32), static_cast<unsigned>(B * Hkv));
   const dim3 block_dq(512);  // waves >= G only stage K / V / K^T
-  const dim3 block_kv(static_cast<unsigned>(64 * G));
+  const dim3 block_kv(static_cast<unsigned>(64 * (D == 64 ? G : std::min<int64_t>(G, 4))));
   hipStream_t s = static_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(flash_dq_kernel<64>, grid, block_dq, 0, s, a);
-  hipLaunchKernelGGL(flash_dkdv_kernel<64>, grid, block_kv, 0, s, a);
+  if (D == 64) {
+    hipLaunchKernelGGL(flash_dq_kernel<64>, grid, block_dq, 0, s, a);
+    hipLaunchKernelGGL((flash_dkdv_kernel<64, 8>), grid, block_kv, 0, s, a);
+  } else {
+    hipLaunchKernelGGL(flash_dq_kernel<128>, grid, block_dq, 0, s, a);
+    hipLaunchKernelGGL((flash_dkdv_kernel<128, 4>), grid, block_kv, 0, s, a);
+  }
   DRL_LAUNCH_CHECK();
   return DRL_OK;
 }

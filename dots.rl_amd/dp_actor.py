@@ -43,12 +43,15 @@ class FlatAdamW:
         self.max_grad_norm = max_grad_norm
         self.warmup_steps = warmup_steps
         self.group = group
+        # moments cover what the master holds: everything (replicated) or [small region | own shard]
         self.exp_avg = torch.zeros_like(store.master)
         self.exp_avg_sq = torch.zeros_like(store.master)
         self.step_count = 0
         self.sched_step = 0
         self.norm = torch.zeros(1, dtype=torch.float32, device=store.master.device)
         self._pending = []
+        # sharded store: the reduce-scattered gradient of [small region | own shard], aligned with the master
+        self.grad_work = torch.zeros_like(store.master) if store.sharded else None
 
     def current_lr(self):
         if self.warmup_steps > 0 and self.sched_step < self.warmup_steps:
@@ -68,7 +71,7 @@ class FlatAdamW:
         backward finishes, so the 24 slices (73 % of the bytes for Qwen2.5-0.5B) travel under the rest of the
         backward. The embedding / lm_head and final-norm slices are complete only at the end (allreduce_rest)."""
         self._pending = []
-        if not self.distributed():
+        if not self.distributed() or self.store.sharded:  # sharded: one reduce-scatter in step()
             return
 
         def hook(i):
@@ -105,6 +108,8 @@ class FlatAdamW:
     def step(self):
         """All-reduce (average) the flat gradient across DP ranks, then norm -> clip -> AdamW in HIP.
         Returns the device grad-norm tensor (the reference returns clip_grad_norm_'s total norm)."""
+        if self.store.sharded:
+            return self._step_sharded()
         g = self.store.grad
         self.allreduce_grads()
         native.grad_norm(g, out=self.norm)
@@ -114,6 +119,41 @@ class FlatAdamW:
                           beta1=self.betas[0], beta2=self.betas[1], eps=self.eps, weight_decay=self.weight_decay,
                           step=self.step_count, max_grad_norm=self.max_grad_norm, grad_norm_t=self.norm,
                           params_bf16=params_bf16)
+        return self.norm
+
+    def _step_sharded(self):
+        """ZeRO-style step over a sharded store (what FSDP FULL_SHARD's optimizer step does for the reference,
+        fsdp_workers.py:397-418 + dp_actor.py:282-298): AVG reduce-scatter of the GEMM region's gradient into
+        this rank's shard, AVG all-reduce of the (replicated, tiny) small region; clip_grad_norm_'s total norm
+        = sqrt(|small|^2 + sum over ranks |shard|^2) (FSDP's sharded norm: local squares, SUM all-reduce);
+        HIP AdamW on [small | shard] (bf16 compute shard written in the same pass); all-gather of the
+        compute copy's GEMM region."""
+        st, g, gw = self.store, self.store.grad, self.grad_work
+        ns = st.n_small
+        lo, hi = st.master_range()
+        dist.all_reduce(g[:ns], op=dist.ReduceOp.AVG, group=self.group)
+        if dist.get_backend(self.group) == "nccl" or g.device.type == "cpu":
+            dist.reduce_scatter_tensor(gw[ns:], g[ns:], op=dist.ReduceOp.AVG, group=self.group)
+        else:  # gloo on device tensors (ranks sharing one GPU in a test): AVG all-reduce, own shard kept
+            dist.all_reduce(g[ns:], op=dist.ReduceOp.AVG, group=self.group)
+            gw[ns:].copy_(g[lo:hi])
+        gw[:ns].copy_(g[:ns])
+        n_small = native.grad_norm(gw[:ns])
+        n_shard = native.grad_norm(gw[ns:])
+        sq = n_shard * n_shard
+        dist.all_reduce(sq, op=dist.ReduceOp.SUM, group=self.group)
+        torch.sqrt(sq + n_small * n_small, out=self.norm)
+        self.step_count += 1
+        bf16 = st.compute is not st.master and st.compute.dtype == torch.bfloat16
+        hp = dict(lr=self.current_lr(), beta1=self.betas[0], beta2=self.betas[1], eps=self.eps,
+                  weight_decay=self.weight_decay, step=self.step_count, max_grad_norm=self.max_grad_norm,
+                  grad_norm_t=self.norm)
+        m, v, p = self.exp_avg, self.exp_avg_sq, st.master
+        native.adamw_step(p[:ns], gw[:ns], m[:ns], v[:ns], params_bf16=None, **hp)
+        native.adamw_step(p[ns:], gw[ns:], m[ns:], v[ns:], params_bf16=st.compute[lo:hi] if bf16 else None, **hp)
+        if not bf16:
+            st.compute[lo:hi].copy_(p[ns:])
+        st.all_gather_compute()
         return self.norm
 
     def state_dict(self):

@@ -25,6 +25,7 @@ import math
 from dataclasses import dataclass, field
 
 import torch
+import torch.distributed as dist
 import torch.nn.functional as F
 
 from . import native
@@ -95,32 +96,70 @@ def param_specs(cfg: Qwen2Config):
 
 
 class ParamStore:
-    """Flat parameter/gradient buffers with named views (64-element = 256-B aligned offsets)."""
+    """Flat parameter/gradient buffers with named views (64-element = 256-B aligned offsets).
+
+    Layout: the fp32 'small' parameters (norm weights, read by the kernels straight from the fp32 master) come
+    first, then the GEMM parameters (read through the compute-dtype copy), each group in param_specs order.
+    Buffers by mode:
+      * trainable, replicated   : fp32 master (numel), compute copy (numel; the master itself in fp32 mode),
+                                  fp32 grad (numel);
+      * trainable, ``shard=(rank, world)`` (ZeRO-style, what FSDP FULL_SHARD gives the reference,
+        fsdp_workers.py:397-418): the GEMM region's fp32 master and the optimizer moments are split into
+        `world` equal contiguous shards; master = [small region | this rank's shard], the compute copy and
+        the fp32 gradient stay full (all-gathered after every optimizer step / reduce-scattered before it);
+      * frozen (trainable=False) bf16: fp32 master of the small region only + the bf16 compute copy.
+    ``small`` is always master[:n_small]."""
 
     ALIGN = 64
 
-    def __init__(self, cfg: Qwen2Config, device, compute_dtype=torch.bfloat16, trainable=True):
+    def __init__(self, cfg: Qwen2Config, device, compute_dtype=torch.bfloat16, trainable=True, shard=None,
+                 group=None):
         self.cfg = cfg
         self.device = torch.device(device)
         self.compute_dtype = compute_dtype
         self.trainable = trainable
         self.specs = param_specs(cfg)
-        self.offsets = {}
-        off = 0
+        self.rank, self.world = (int(shard[0]), int(shard[1])) if shard is not None else (0, 1)
+        self.sharded = trainable and self.world > 1
+        self.group = group
+        A = self.ALIGN
+
+        def padded(n):
+            return (n + A - 1) // A * A
+
+        pos, off = {}, 0
         for name, shape, kind in self.specs:
-            n = math.prod(shape)
-            self.offsets[name] = (off, shape, kind)
-            off += (n + self.ALIGN - 1) // self.ALIGN * self.ALIGN
-        self.numel = off
+            if kind == "small":
+                pos[name] = off
+                off += padded(math.prod(shape))
+        self.n_small = off
+        for name, shape, kind in self.specs:
+            if kind != "small":
+                pos[name] = off
+                off += padded(math.prod(shape))
+        gemm_len = off - self.n_small
+        gemm_len = (gemm_len + A * self.world - 1) // (A * self.world) * (A * self.world)
+        self.numel = self.n_small + gemm_len
+        self.shard_len = gemm_len // self.world
+        self.offsets = {name: (pos[name], shape, kind) for name, shape, kind in self.specs}  # spec order
         self.n_params = sum(math.prod(s) for _, s, _ in self.specs)
-        self.master = torch.zeros(off, dtype=torch.float32, device=self.device)
-        self.compute = self.master if compute_dtype == torch.float32 else torch.zeros(off, dtype=compute_dtype,
-                                                                                     device=self.device)
-        self.grad = torch.zeros(off, dtype=torch.float32, device=self.device) if trainable else None
+        f32 = torch.float32
+        if self.sharded:
+            self.master = torch.zeros(self.n_small + self.shard_len, dtype=f32, device=self.device)
+            self.compute = torch.zeros(self.numel, dtype=compute_dtype, device=self.device)
+        elif not trainable and compute_dtype != f32:
+            self.master = torch.zeros(self.n_small, dtype=f32, device=self.device)
+            self.compute = torch.zeros(self.numel, dtype=compute_dtype, device=self.device)
+        else:
+            self.master = torch.zeros(self.numel, dtype=f32, device=self.device)
+            self.compute = self.master if compute_dtype == f32 else torch.zeros(self.numel, dtype=compute_dtype,
+                                                                               device=self.device)
+        self.small = self.master[:self.n_small]
+        self.grad = torch.zeros(self.numel, dtype=f32, device=self.device) if trainable else None
         self._views = {}
         for name, (o, shape, kind) in self.offsets.items():
             n = math.prod(shape)
-            w = (self.master if kind == "small" else self.compute)[o:o + n].view(shape)
+            w = (self.small if kind == "small" else self.compute)[o:o + n].view(shape)
             g = self.grad[o:o + n].view(shape) if trainable else None
             self._views[name] = (w, g)
 
@@ -130,24 +169,84 @@ class ParamStore:
     def g(self, name):
         return self._views[name][1]
 
+    def master_range(self):
+        """[lo, hi) of the flat layout held by master[n_small:] (the GEMM region, or this rank's shard of it)."""
+        if self.master.numel() == self.n_small:
+            return self.n_small, self.n_small
+        if self.sharded:
+            lo = self.n_small + self.rank * self.shard_len
+            return lo, lo + self.shard_len
+        return self.n_small, self.numel
+
+    def _put(self, name, vals):
+        """Write one parameter's fp32 values (flat) into the master (the part this rank holds) and the
+        compute copy."""
+        o, shape, kind = self.offsets[name]
+        n = math.prod(shape)
+        if kind == "small":
+            self.small[o:o + n].copy_(vals)
+            return
+        lo, hi = self.master_range()
+        a, b = max(o, lo), min(o + n, hi)
+        if a < b:
+            self.master[self.n_small + a - lo:self.n_small + b - lo].copy_(vals[a - o:b - o])
+        if self.compute is not self.master:
+            self.compute[o:o + n].copy_(vals)
+
     @torch.no_grad()
     def init_random(self, seed: int):
-        """HF Qwen2 init: N(0, initializer_range) for matrices, ones for norms, zeros for biases."""
+        """HF Qwen2 init: N(0, initializer_range) for matrices, ones for norms, zeros for biases. Values are
+        drawn per parameter in param_specs order (the same numbers in every layout / sharding)."""
         gen = torch.Generator(device=self.device).manual_seed(seed)
         for name, (o, shape, kind) in self.offsets.items():
-            dst = self.master[o:o + math.prod(shape)]
+            vals = torch.empty(math.prod(shape), dtype=torch.float32, device=self.device)
             if name.endswith("layernorm") or name == "norm":
-                dst.fill_(1.0)
+                vals.fill_(1.0)
             elif name.endswith("bias"):
-                dst.zero_()
+                vals.zero_()
             else:
-                dst.normal_(0.0, self.cfg.initializer_range, generator=gen)
+                vals.normal_(0.0, self.cfg.initializer_range, generator=gen)
+            self._put(name, vals)
         self.refresh_compute()
 
     @torch.no_grad()
     def refresh_compute(self):
+        """compute copy <- master (GEMM region); sharded: this rank's shard, then an all-gather."""
+        if self.compute is self.master:
+            return
+        lo, hi = self.master_range()
+        if hi > lo:
+            self.compute[lo:hi].copy_(self.master[self.n_small:])
+        if self.sharded:
+            self.all_gather_compute()
+
+    def all_gather_compute(self):
+        """Every rank's shard of the compute copy's GEMM region -> the full region on every rank (RCCL
+        all-gather, in place)."""
+        lo, hi = self.master_range()
+        full = self.compute[self.n_small:]
+        if dist.get_backend(self.group) == "nccl" or full.device.type == "cpu":
+            dist.all_gather_into_tensor(full, self.compute[lo:hi], group=self.group)
+        else:  # gloo on device tensors (ranks sharing one GPU in a test): zero the other shards + SUM, exact
+            mine = self.compute[lo:hi].clone()
+            full.zero_()
+            self.compute[lo:hi].copy_(mine)
+            dist.all_reduce(full, op=dist.ReduceOp.SUM, group=self.group)
+
+    @torch.no_grad()
+    def copy_from(self, other: "ParamStore"):
+        """This store's weights := other's (same config): the small fp32 region and the compute copy; a
+        replicated fp32 master gets the full values (sharded other: gathered through its compute copy)."""
+        self.small.copy_(other.small)
         if self.compute is not self.master:
-            self.compute.copy_(self.master)
+            self.compute.copy_(other.compute.to(self.compute.dtype))
+        lo, hi = self.master_range()
+        if hi > lo:
+            olo, ohi = other.master_range()
+            if (olo, ohi) == (lo, hi):
+                self.master[self.n_small:].copy_(other.master[other.n_small:])
+            else:
+                self.master[self.n_small:].copy_(other.compute[lo:hi].to(torch.float32))
 
     @torch.no_grad()
     def load_state_dict_hf(self, sd: dict):
@@ -155,8 +254,7 @@ class ParamStore:
         cfg = self.cfg
 
         def put(name, t):
-            o, shape, _ = self.offsets[name]
-            self.master[o:o + math.prod(shape)].copy_(t.reshape(-1).to(torch.float32))
+            self._put(name, t.reshape(-1).to(device=self.device, dtype=torch.float32))
 
         put("embed_tokens", sd["model.embed_tokens.weight"])
         for i in range(cfg.num_hidden_layers):
@@ -175,15 +273,20 @@ class ParamStore:
             put("score.bias", sd["score.bias"] if "score.bias" in sd else torch.zeros(cfg.num_labels))
         elif not cfg.tie_word_embeddings:
             put("lm_head", sd["lm_head.weight"])
-        self.refresh_compute()
 
     def zero_grad(self):
         if self.grad is not None:
             self.grad.zero_()
 
+    def memory_bytes(self):
+        """Bytes of device memory held by this store's buffers."""
+        bufs = {id(t): t for t in (self.master, self.compute, self.grad) if t is not None}
+        return sum(t.numel() * t.element_size() for t in bufs.values())
+
     def layer_range(self, i):
-        """[start, end) of decoder layer i's parameters in the flat buffers (contiguous, buffer order)."""
-        names = [n for n, _, _ in self.specs if n.startswith(f"layers.{i}.")]
+        """[start, end) of decoder layer i's GEMM parameters in the flat buffers (contiguous; its two norm
+        weights live in the small region at the front)."""
+        names = [n for n, _, k in self.specs if n.startswith(f"layers.{i}.") and k != "small"]
         start = self.offsets[names[0]][0]
         last = self.offsets[names[-1]]
         return start, last[0] + math.prod(last[1])
@@ -265,7 +368,7 @@ def _layer_forward(m, i, x_prev, delta, pos, key_valid, save, cache=None, koff=0
     # GEMM + masked softmax + PV GEMM, probabilities kept for the backward) serves the fp32 parity model
     flash_ok = T > 1 and dt == torch.bfloat16 and D in (64, 128) and G <= 8 and key_valid.stride(0) % 4 == 0
     flash = save is None and flash_ok
-    if save is not None and flash_ok and cache is None and T % 8 == 0 and D == 64:
+    if save is not None and flash_ok and cache is None and T % 8 == 0:
         # training forward: fused attention that saves only the LSE; the backward (flash_attn_bwd)
         # recomputes P and needs a head-dim-major copy of k besides row-major k and v
         kbuf = torch.empty(B, Hkv, T, D, dtype=dt, device=dev)

@@ -12,6 +12,7 @@ reference's ``.to("cpu")`` convention for callers that need it.
 
 from __future__ import annotations
 
+import math
 import os
 import time
 
@@ -24,7 +25,7 @@ from .dp_actor import DataParallelPPOActor, FlatAdamW
 from .dp_critic import DataParallelPPOCritic
 from .flops_counter import FlopsCounter
 from .protocol import DataProto
-from .qwen2 import ParamStore, Qwen2Config, Qwen2Model
+from .qwen2 import param_specs, ParamStore, Qwen2Config, Qwen2Model
 from .rollout import MI355XRollout
 from .single_controller import Dispatch, Worker, make_nd_compute_dataproto_dispatch_fn, register
 
@@ -109,7 +110,8 @@ class ActorRolloutRefWorker(Worker):
         self.flops_counter = FlopsCounter(mcfg)
         dtype = torch.float32 if cfg.model.get("dtype", "bfloat16") == "float32" else torch.bfloat16
         seed = int(cfg.model.get("seed", 1234))
-        self.store = ParamStore(mcfg, self.device, compute_dtype=dtype, trainable=self._is_actor)
+        shard = _shard_spec(cfg.actor, mcfg, self.dp_rank, self.dp_size) if self._is_actor else None
+        self.store = ParamStore(mcfg, self.device, compute_dtype=dtype, trainable=self._is_actor, shard=shard)
         path = cfg.model.get("path", "random:")
         if path.startswith("random:"):
             self.store.init_random(seed)
@@ -137,8 +139,7 @@ class ActorRolloutRefWorker(Worker):
         if self._is_ref:
             # reference policy: frozen compute-dtype copy of the initial weights (fsdp_workers.py:648-672)
             self.ref_store = ParamStore(mcfg, self.device, compute_dtype=dtype, trainable=False)
-            self.ref_store.master.copy_(self.store.master)
-            self.ref_store.refresh_compute()
+            self.ref_store.copy_from(self.store)
             self.ref_module = Qwen2Model(mcfg, self.ref_store)
             self.ref_policy = DataParallelPPOActor(cfg.ref, self.ref_module)
 
@@ -214,25 +215,56 @@ class ActorRolloutRefWorker(Worker):
     # ------------------------------------------------------------------------------------------ checkpoint
     @register(dispatch_mode=Dispatch.ONE_TO_ALL)
     def save_checkpoint(self, local_path, hdfs_path=None, global_step=0, max_ckpt_to_keep=None):
-        """fsdp_workers.py:844-880: replicated params -> rank 0 writes model + optimizer + rng state."""
-        if self.dp_rank == 0:
-            os.makedirs(local_path, exist_ok=True)
-            torch.save({"master": self.store.master.cpu(), "optim": {k: (v.cpu() if torch.is_tensor(v) else v)
-                                                                      for k, v in self.actor_optimizer.state_dict().items()},
-                        "global_step": global_step, "cuda_rng": torch.cuda.get_rng_state(),
-                        "rollout_calls": self.rollout.calls if self._is_rollout else 0},
-                       os.path.join(local_path, "model_optim_rng.pt"))
-        if dist.is_initialized():
-            dist.barrier()
+        """fsdp_workers.py:844-880: model + optimizer + rng state (one file, or one shard file per rank)."""
+        _save_store(self.store, self.actor_optimizer, local_path, "model_optim_rng",
+                    {"global_step": global_step, "cuda_rng": torch.cuda.get_rng_state(),
+                     "rollout_calls": self.rollout.calls if self._is_rollout else 0}, self.dp_rank)
 
     @register(dispatch_mode=Dispatch.ONE_TO_ALL)
     def load_checkpoint(self, local_path, hdfs_path=None, del_local_after_load=False):
-        sd = torch.load(os.path.join(local_path, "model_optim_rng.pt"), map_location="cpu", weights_only=True)
-        self.store.master.copy_(sd["master"])
-        self.store.refresh_compute()
-        self.actor_optimizer.load_state_dict(sd["optim"])
+        sd = _load_store(self.store, self.actor_optimizer, local_path, "model_optim_rng")
         if self._is_rollout:
             self.rollout.calls = int(sd.get("rollout_calls", 0))
+
+
+def _shard_spec(section, mcfg, dp_rank, dp_size):
+    """(rank, world) to shard the fp32 master + AdamW moments over (ParamStore(shard=...)), or None.
+    ``fsdp_config.shard``: True / False, or "auto" = shard when DP > 1 and the replicated fp32 master +
+    gradient + moments (16 B/param) would take more than 64 GB per GPU (configs #4 / #5: 7-8 B params)."""
+    fc = section.get("fsdp_config", {}) or {}
+    mode = fc.get("shard", "auto")
+    if dp_size <= 1 or mode is False or mode == "false":
+        return None
+    if mode == "auto":
+        n = sum(math.prod(shape) for _, shape, _ in param_specs(mcfg))
+        if 16 * n <= 64 * 1024**3:
+            return None
+    return (dp_rank, dp_size)
+
+
+def _save_store(store, optim, path_dir, name, extra, dp_rank):
+    """Replicated store: rank 0 writes one file. Sharded: every rank writes its shard (the reference's
+    FSDP sharded checkpoint: model_world_size_{w}_rank_{r}.pt, fsdp_checkpoint_manager.py)."""
+    payload = dict(extra)
+    payload.update({"master": store.master.cpu(), "n_small": store.n_small, "world": store.world,
+                    "optim": {k: (v.cpu() if torch.is_tensor(v) else v) for k, v in optim.state_dict().items()}})
+    if store.sharded:
+        os.makedirs(path_dir, exist_ok=True)
+        torch.save(payload, os.path.join(path_dir, f"{name}_world_size_{store.world}_rank_{store.rank}.pt"))
+    elif dp_rank == 0:
+        os.makedirs(path_dir, exist_ok=True)
+        torch.save(payload, os.path.join(path_dir, f"{name}.pt"))
+    if dist.is_initialized():
+        dist.barrier()
+
+
+def _load_store(store, optim, path_dir, name):
+    f = (f"{name}_world_size_{store.world}_rank_{store.rank}.pt" if store.sharded else f"{name}.pt")
+    sd = torch.load(os.path.join(path_dir, f), map_location="cpu", weights_only=True)
+    store.master.copy_(sd["master"])
+    store.refresh_compute()
+    optim.load_state_dict(sd["optim"])
+    return sd
 
 
 class CriticWorker(Worker):
@@ -271,7 +303,8 @@ class CriticWorker(Worker):
         self.model_config = mcfg
         self.flops_counter = FlopsCounter(mcfg)
         dtype = torch.float32 if cfg.model.get("dtype", "bfloat16") == "float32" else torch.bfloat16
-        self.store = ParamStore(mcfg, self.device, compute_dtype=dtype, trainable=True)
+        shard = _shard_spec(cfg, mcfg, self.dp_rank, self.dp_size)
+        self.store = ParamStore(mcfg, self.device, compute_dtype=dtype, trainable=True, shard=shard)
         path = cfg.model.get("path", "random:")
         if path.startswith("random:"):
             self.store.init_random(int(cfg.model.get("seed", 4321)))
@@ -325,19 +358,10 @@ class CriticWorker(Worker):
 
     @register(dispatch_mode=Dispatch.ONE_TO_ALL)
     def save_checkpoint(self, local_path, hdfs_path=None, global_step=0, max_ckpt_to_keep=None):
-        """fsdp_workers.py:1294-1310: replicated params -> rank 0 writes model + optimizer."""
-        if self.dp_rank == 0:
-            os.makedirs(local_path, exist_ok=True)
-            torch.save({"master": self.store.master.cpu(),
-                        "optim": {k: (v.cpu() if torch.is_tensor(v) else v)
-                                  for k, v in self.critic_optimizer.state_dict().items()},
-                        "global_step": global_step}, os.path.join(local_path, "critic_model_optim.pt"))
-        if dist.is_initialized():
-            dist.barrier()
+        """fsdp_workers.py:1294-1310: model + optimizer (one file, or one shard file per rank)."""
+        _save_store(self.store, self.critic_optimizer, local_path, "critic_model_optim", {"global_step": global_step},
+                    self.dp_rank)
 
     @register(dispatch_mode=Dispatch.ONE_TO_ALL)
     def load_checkpoint(self, local_path, hdfs_path=None, del_local_after_load=True):
-        sd = torch.load(os.path.join(local_path, "critic_model_optim.pt"), map_location="cpu", weights_only=True)
-        self.store.master.copy_(sd["master"])
-        self.store.refresh_compute()
-        self.critic_optimizer.load_state_dict(sd["optim"])
+        _load_store(self.store, self.critic_optimizer, local_path, "critic_model_optim")

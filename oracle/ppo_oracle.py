@@ -506,3 +506,32 @@ def sample_row(logits, temperature, top_k, top_p, seed, offset, row):
     keys = race_keys((np.asarray(logits, np.float32) / np.float32(temperature)).astype(np.float32), seed, offset, row)
     keys = np.where(p > 0, keys, -np.inf)
     return int(np.argmax(keys))
+
+
+# ------------------------------------------------------------------------------------ A15 clip + AdamW
+def grad_norm(g):
+    """torch.nn.utils.clip_grad_norm_'s total 2-norm (dp_actor.py:282-298), accumulated in float64."""
+    g = np.asarray(g, np.float64)
+    return np.float32(np.sqrt(np.sum(g * g)))
+
+
+def adamw_step(p, g, m, v, *, lr, beta1, beta2, eps, weight_decay, step, max_grad_norm, grad_norm_value):
+    """In place on float32 arrays: clip_grad_norm_ (coef = max_norm / (norm + 1e-6), clamped to 1; a
+    non-finite norm skips the step, dp_actor.py:292-297) then torch.optim.AdamW (decoupled weight decay,
+    lerp first moment, bias-corrected denominator; fsdp_workers.py:454-459), in the float32 operation order of
+    csrc/optim.hip's adam_one."""
+    f = np.float32
+    if not np.isfinite(grad_norm_value):
+        return
+    coef = f(1.0)
+    if max_grad_norm > 0:
+        coef = min(f(f(max_grad_norm) / (f(grad_norm_value) + f(1e-6))), f(1.0))
+    step_size = f(lr / (1.0 - beta1 ** step))
+    bc2_sqrt = f(np.sqrt(1.0 - beta2 ** step))
+    gg = (g * coef).astype(f)
+    p *= f(1.0) - f(lr) * f(weight_decay)
+    m += (f(1.0) - f(beta1)) * (gg - m)
+    v *= f(beta2)
+    v += (f(1.0) - f(beta2)) * (gg * gg)
+    denom = np.sqrt(v) / bc2_sqrt + f(eps)
+    p += (-step_size) * (m / denom)

@@ -14,10 +14,11 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(HERE))
 
 
-def build_config(world):
+def build_config(world, shard=False):
     from dots.rl_amd.config import apply_overrides, default_config
 
     return apply_overrides(default_config(), [
+        f"actor_rollout_ref.actor.fsdp_config.shard={'true' if shard else 'false'}",
         "actor_rollout_ref.rollout.n=1", "actor_rollout_ref.actor.ppo_mini_batch_size=4",
         "actor_rollout_ref.actor.ppo_micro_batch_size_per_gpu=1", "actor_rollout_ref.actor.optim.lr=1e-4",
         f"actor_rollout_ref.model.path={os.path.join(HERE, 'golden', 'tiny_qwen2')}",
@@ -35,7 +36,7 @@ def batch(device):
                                meta_info={"temperature": 1.0})
 
 
-def main(out_path):
+def main(out_path, shard=False):
     import torch.distributed as dist
 
     from dots.rl_amd.single_controller import SPMDWorkerGroup, init_process_group_from_env
@@ -44,12 +45,15 @@ def main(out_path):
     torch.cuda.set_device(0)
     init_process_group_from_env("gloo")
     world, rank = dist.get_world_size(), dist.get_rank()
-    wg = SPMDWorkerGroup(ActorRolloutRefWorker(build_config(world), role="actor"))
+    wg = SPMDWorkerGroup(ActorRolloutRefWorker(build_config(world, shard), role="actor"))
     wg.init_model()
     w = wg.worker
     out = wg.update_actor(batch("cuda"))
     torch.cuda.synchronize()
-    torch.save({"master": w.store.master.cpu(), "metrics": json.dumps(out.meta_info["metrics"]),
+    st = w.store
+    # full fp32 parameters in flat layout order: the small region + the (all-gathered) GEMM region
+    params = torch.cat([st.small, st.compute[st.n_small:].float()]).cpu() if st.sharded else st.master.cpu()
+    torch.save({"master": params, "sharded": st.sharded, "metrics": json.dumps(out.meta_info["metrics"]),
                 "mini_batch_size": w.config.actor.ppo_mini_batch_size, "rank": rank, "world": world},
                out_path)
     dist.barrier()
@@ -57,4 +61,4 @@ def main(out_path):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], shard=len(sys.argv) > 2 and sys.argv[2] == "shard")

@@ -84,15 +84,15 @@ def _restated_dp1(world=2):
     return w.store.master.detach().cpu(), per_rank_metrics
 
 
-def test_dp2_update_equals_mean_of_rank_gradients(tmp_path):
+def _run_pair(tmp_path, tag, extra=()):
     port = _free_port()
     procs, outs = [], []
     for r in range(2):
         env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(r), WORLD_SIZE="2",
                    LOCAL_RANK="0")
-        out = str(tmp_path / f"rank{r}.pt")
+        out = str(tmp_path / f"{tag}_rank{r}.pt")
         outs.append(out)
-        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "dp2_child.py"), out], env=env,
+        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "dp2_child.py"), out, *extra], env=env,
                                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
     logs = []
     for p in procs:
@@ -104,7 +104,31 @@ def test_dp2_update_equals_mean_of_rank_gradients(tmp_path):
             raise
     for p, log in zip(procs, logs):
         assert p.returncode == 0, log[-3000:]
-    res = [torch.load(o, weights_only=True) for o in outs]
+    return [torch.load(o, weights_only=True) for o in outs]
+
+
+def test_dp2_sharded_optimizer_equals_replicated(tmp_path):
+    """ZeRO-style sharding (fsdp_config.shard=true: fp32 master + AdamW moments split over the 2 ranks, AVG
+    reduce-scatter of the gradient, all-gather of the compute copy) against the replicated optimizer
+    (all-reduce) on the same DP=2 update, real HIP kernels: the same parameters on both ranks, equal to the
+    replicated run's up to the total-norm summation order (AdamW is elementwise)."""
+    rep = _run_pair(tmp_path, "rep")
+    sh = _run_pair(tmp_path, "shard", ("shard",))
+    assert sh[0]["sharded"] and not rep[0]["sharded"]
+    assert torch.equal(sh[0]["master"], sh[1]["master"])
+    n = rep[0]["master"].numel()  # the sharded layout pads the GEMM region to a multiple of world * 64
+    assert sh[0]["master"].numel() >= n and not sh[0]["master"][n:].any()
+    d = (sh[0]["master"][:n] - rep[0]["master"]).abs().max().item()
+    step = (rep[0]["master"]).abs().max().item()
+    assert d <= 1e-6 * max(step, 1.0), d
+    for r in range(2):
+        a, b = json.loads(sh[r]["metrics"]), json.loads(rep[r]["metrics"])
+        np.testing.assert_allclose(a["actor/grad_norm"], b["actor/grad_norm"], rtol=1e-5)
+        np.testing.assert_allclose(a["actor/pg_loss"], b["actor/pg_loss"], rtol=1e-6, atol=1e-7)
+
+
+def test_dp2_update_equals_mean_of_rank_gradients(tmp_path):
+    res = _run_pair(tmp_path, "rep")
     assert res[0]["mini_batch_size"] == res[1]["mini_batch_size"] == 2
     assert torch.equal(res[0]["master"], res[1]["master"])
     want_master, want_metrics = _restated_dp1()

@@ -288,7 +288,10 @@ def _ref_attn_autograd(q, k, v, valid, dout):
     return Ob.detach(), qf.grad, kf.grad, vf.grad
 
 
-@pytest.mark.parametrize("B,Hkv,G,D,T", [(2, 2, 7, 64, 256), (1, 2, 7, 64, 104), (2, 1, 4, 64, 64), (3, 2, 8, 64, 96)])
+@pytest.mark.parametrize("B,Hkv,G,D,T", [(2, 2, 7, 64, 256), (1, 2, 7, 64, 104), (2, 1, 4, 64, 64), (3, 2, 8, 64, 96),
+                                         # head_dim 128: Llama-3-8B (G 4), Qwen2.5-7B (G 7), G > 4 heads per wave
+                                         (2, 2, 4, 128, 128), (1, 2, 7, 128, 104), (2, 1, 8, 128, 64),
+                                         (1, 1, 1, 128, 40)])
 def test_flash_attn_backward(B, Hkv, G, D, T):
     g = torch.Generator(device=DEV).manual_seed(T + G)
     q = torch.randn(B, Hkv, G, T, D, device=DEV, generator=g).to(torch.bfloat16)
