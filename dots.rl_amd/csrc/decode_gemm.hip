@@ -189,6 +189,145 @@ __global__ __launch_bounds__(256) void decode_gemm_kernel(DgArgs a) {
   }
 }
 
+// ------------------------------------------------------------------------------------------- tiled GEMM
+// The same packed operands at 97..512 rows, where a projection is an MFMA problem (gate_up at 512 rows:
+// 8.9 GFLOP against a 17 MB weight stream), not a weight stream: every wave owns a WB x TB tile of 32 x 32
+// output blocks (weight rows x tokens) over the workgroup's whole K slice, so each weight fragment feeds TB
+// MFMAs and each activation fragment WB (the one-round-trip kernel above re-reads the activation panel per
+// 32-row weight block and reduces 4 K slices through LDS). Fragments are loaded straight into registers
+// (1-KB coalesced wave loads) through a DEPTH-deep ring, branch-free (the last loads of a slice repeat its
+// last k-step instead of branching), so DEPTH * (WB + TB) loads are always in flight. Workgroup = WW x WT
+// waves; the 4 waves' overlapping fragments are served by L1 / L2. Epilogues straight from the
+// accumulators: fp32 partials (K slice = gridDim.y), SwiGLU (gate row i and up row i + 16 of a block sit in
+// registers r and r + 8 of the same lane; one lane-half exchange forms the packed 16-B pieces), or bias +
+// RoPE + KV-cache writes (rotation pairs likewise lane-local).
+template <int WB, int TB, int WW, int WT, int EPI>
+__global__ __launch_bounds__(256) void decode_gemm_tiled_kernel(DgArgs a) {
+  constexpr int DEPTH = 4;
+  static_assert(WW * WT == 4, "4 waves per workgroup");
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int ww = wave % WW, wt = wave / WW;
+  const int rb0 = (blockIdx.x * WW + ww) * WB;  // first 32-row weight block of this wave
+  const int tb0 = (blockIdx.z * WT + wt) * TB;  // first 32-token block
+  const int per = a.nks / static_cast<int>(gridDim.y);  // k16 steps of this K slice (a multiple of DEPTH)
+  const int s0 = static_cast<int>(blockIdx.y) * per, s1 = s0 + per;
+  const uint16_t* wp[WB];
+  const uint16_t* xp[TB];
+#pragma unroll
+  for (int b = 0; b < WB; ++b)  // blocks past the end re-read the last one (never stored)
+    wp[b] = a.w + static_cast<int64_t>(min(rb0 + b, a.tiles - 1)) * a.nks * 512 + lane * 8;
+  const int64_t xstep = static_cast<int64_t>(a.MBT) * 512;
+#pragma unroll
+  for (int t = 0; t < TB; ++t) xp[t] = a.x + (static_cast<int64_t>(min(tb0 + t, a.MBT - 1)) * 64 + lane) * 8;
+  u16x8 rw[DEPTH][WB], rx[DEPTH][TB];
+  auto load = [&](int d, int st) {
+#pragma unroll
+    for (int b = 0; b < WB; ++b) rw[d][b] = __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(wp[b] + st * 512));
+#pragma unroll
+    for (int t = 0; t < TB; ++t) rx[d][t] = *reinterpret_cast<const u16x8*>(xp[t] + st * xstep);
+  };
+#pragma unroll
+  for (int d = 0; d < DEPTH; ++d) load(d, s0 + d);
+  __builtin_amdgcn_sched_barrier(0);
+  f32x16 acc[WB][TB];
+#pragma unroll
+  for (int b = 0; b < WB; ++b)
+#pragma unroll
+    for (int t = 0; t < TB; ++t) acc[b][t] = f32x16{};
+  for (int st = s0; st < s1; st += DEPTH) {
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d) {
+#pragma unroll
+      for (int b = 0; b < WB; ++b)
+#pragma unroll
+        for (int t = 0; t < TB; ++t)
+          acc[b][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(rw[d][b]), as_bf16x8(rx[d][t]), acc[b][t], 0, 0, 0);
+      load(d, min(st + d + DEPTH, s1 - 1));
+      // keep the refill here: left alone, hipcc sinks every load next to its MFMAs (fewest live registers)
+      // and the ring degenerates to one k-step in flight behind a vmcnt(0)
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  // C row i of a block <-> register (i & 3) + 4 (i >> 3), lane half (i >> 2) & 1; column = token lane & 31
+  const int hh = lane >> 5, ml = lane & 31;
+#pragma unroll
+  for (int b = 0; b < WB; ++b) {
+    const int rb = rb0 + b;
+#pragma unroll
+    for (int t = 0; t < TB; ++t) {
+      const int tb = tb0 + t;
+      if (rb >= a.tiles || tb >= a.MBT) continue;
+      const int m = tb * 32 + ml;
+      const f32x16& c = acc[b][t];
+      if constexpr (EPI == EPI_PARTIAL) {
+        if (m >= a.M) continue;
+        float* dst = a.part + (static_cast<int64_t>(blockIdx.y) * a.M + m) * a.N;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int n = rb * 32 + 8 * g + 4 * hh;  // registers 4g .. 4g+3: rows n .. n+3
+          if (n + 3 < a.N) {
+            *reinterpret_cast<float4*>(dst + n) = make_float4(c[4 * g], c[4 * g + 1], c[4 * g + 2], c[4 * g + 3]);
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (n + j < a.N) dst[n + j] = c[4 * g + j];
+          }
+        }
+      } else if constexpr (EPI == EPI_SWIGLU) {
+        // registers r < 8: gate of output column cc(r) = (r & 3) + 8 (r >> 2) + 4 hh; r + 8: its up row
+        uint16_t o[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const float g = bf16r(c[r]), u = bf16r(c[r + 8]);
+          o[r] = to_bf16_bits(bf16r(g / (1.f + expf(-g))) * u);
+        }
+        // half 0 holds columns 0-3 | 8-11, half 1 4-7 | 12-15: swap the middle quads so each half owns 8
+        // consecutive columns (half 0: 0-7, half 1: 8-15)
+        const uint32_t s_lo = hh ? (o[0] | (uint32_t(o[1]) << 16)) : (o[4] | (uint32_t(o[5]) << 16));
+        const uint32_t s_hi = hh ? (o[2] | (uint32_t(o[3]) << 16)) : (o[6] | (uint32_t(o[7]) << 16));
+        const uint32_t r_lo = __shfl_xor(s_lo, 32, kWave), r_hi = __shfl_xor(s_hi, 32, kWave);
+        u16x8 piece;
+        if (hh == 0) {
+          piece = u16x8{o[0], o[1], o[2], o[3], static_cast<uint16_t>(r_lo), static_cast<uint16_t>(r_lo >> 16),
+                        static_cast<uint16_t>(r_hi), static_cast<uint16_t>(r_hi >> 16)};
+        } else {
+          piece = u16x8{static_cast<uint16_t>(r_lo), static_cast<uint16_t>(r_lo >> 16), static_cast<uint16_t>(r_hi),
+                        static_cast<uint16_t>(r_hi >> 16), o[4], o[5], o[6], o[7]};
+        }
+        // packed for the next GEMM (K' = half): k step = rb, 8-column half hh, token m
+        *reinterpret_cast<u16x8*>(a.out + ((static_cast<int64_t>(rb) * a.MBT + tb) * 64 + hh * 32 + ml) * 8) = piece;
+      } else {  // EPI_ROPE: rows 0..15 = d 16 qq + cc of head hd, rows 16..31 its partners d + D/2
+        if (m >= a.M) continue;
+        const int half = a.D / 2, per_h = half / 16, hd = rb / per_h, qq = rb % per_h;
+        const int64_t koff = *a.koff_dev;
+        int64_t p = a.pos[m];
+        p = p < 0 ? 0 : (p >= a.maxpos ? a.maxpos - 1 : p);
+        const int G = a.Hq / a.Hkv;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const int cc = (r & 3) + 8 * (r >> 2) + 4 * hh;
+          const int d1 = 16 * qq + cc, d2 = d1 + half;
+          const int n1 = hd * a.D + d1, n2 = n1 + half;
+          const float x1 = bf16r(c[r] + bf16_to_f32(a.bias[n1]));
+          const float x2 = bf16r(c[r + 8] + bf16_to_f32(a.bias[n2]));
+          if (hd < a.Hq + a.Hkv) {
+            const float cs = a.cos_t[p * half + d1], sn = a.sin_t[p * half + d1];
+            const float o1 = fmaf(x1, cs, -(x2 * sn)), o2 = fmaf(x2, cs, x1 * sn);
+            uint16_t* dst = hd < a.Hq ? a.q + ((static_cast<int64_t>(m) * a.Hkv + hd / G) * G + hd % G) * a.D
+                                      : a.kc + ((static_cast<int64_t>(m) * a.Hkv + (hd - a.Hq)) * a.Tk + koff) * a.D;
+            dst[d1] = to_bf16_bits(o1);
+            dst[d2] = to_bf16_bits(o2);
+          } else {
+            uint16_t* dst = a.vt + (static_cast<int64_t>(m) * a.Hkv + (hd - a.Hq - a.Hkv)) * a.D * a.ld_vt + koff;
+            dst[static_cast<int64_t>(d1) * a.ld_vt] = to_bf16_bits(x1);
+            dst[static_cast<int64_t>(d2) * a.ld_vt] = to_bf16_bits(x2);
+          }
+        }
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------------- consumers
 // x_out = x_in + bf16(sum_ks part) (fp32 residual stream, bf16 module output: add_rmsnorm_fwd semantics),
 // y = bf16(w * (x_out * rsqrt(mean(x_out^2) + eps))) written packed (MBT blocks) or row-major (MBT = 0).
@@ -382,6 +521,75 @@ bool plan_decode_gemm(int64_t M, int64_t N, int64_t K, int epi, DgPlan& p) {
   return found;
 }
 
+// tiled path (97..512 rows): (WB, TB, WW, WT) configurations instantiated, largest wave tile first
+struct DtShape { int wb, tb, ww, wt; };
+constexpr DtShape kTiled[] = {{2, 2, 2, 2}, {2, 2, 4, 1}, {1, 2, 2, 2}, {1, 2, 4, 1}, {1, 1, 2, 2}};
+// 0 = never the tiled path (drl_decode_gemm_set_tiled), 1 = automatic, 2 = automatic with one K slice (tests:
+// the partial form in the fused qkv + RoPE launch's summation order)
+int g_dt_mode = 1;
+
+// the tiled plan when the shape is in its range: K slices only for the partial epilogue (each a multiple of
+// 4 k-steps, at most 4 slices); the biggest wave tile that still gives >= 160 workgroups with the fewest
+// slices, else the most workgroups. p.mb = 0 marks a tiled plan; p.ksw = index into kTiled.
+bool plan_decode_tiled(int64_t M, int64_t N, int64_t K, int epi, DgPlan& p) {
+  // measured (tools/kernel_bench.py --only decode_gemm): faster than the one-round-trip form from 256 rows for
+  // the partial projections (qkv 7.6 -> 6.6 us, o 7.5 -> 6.5, down 13.4 -> 12.2 at 256; 11.9 -> 8.6, 7.8 -> 6.7,
+  // 22.8 -> 14.4 at 512), slower below and for the SwiGLU gate_up (29.3 -> 31.9 us at 512)
+  if (g_dt_mode == 0 || M < 192 || M > 512 || K % 64 != 0 || N < 1 || epi == EPI_SWIGLU) return false;
+  const int blocks = static_cast<int>((M + 31) / 32);
+  p.mbt = (blocks + 1) / 2 * 2;
+  p.tiles = static_cast<int>(epi == EPI_SWIGLU ? (N / 2 + 15) / 16 : (N + 31) / 32);
+  const int nks = static_cast<int>(K / 16);
+  bool found = false, full = false;
+  int64_t best_wgs = 0;
+  int best_area = 0;
+  for (int ci = 0; ci < static_cast<int>(sizeof(kTiled) / sizeof(kTiled[0])); ++ci) {
+    const DtShape& c = kTiled[ci];
+    const int rows = c.wb * c.ww, toks = c.tb * c.wt;
+    const int64_t base = static_cast<int64_t>((p.tiles + rows - 1) / rows) * ((p.mbt + toks - 1) / toks);
+    for (int ks = 1; ks <= (epi == EPI_PARTIAL && g_dt_mode == 1 ? 4 : 1); ++ks) {
+      if (nks % ks != 0 || (nks / ks) % 4 != 0) continue;
+      const int64_t wgs = base * ks;
+      const bool ok = wgs >= 160;
+      const int area = c.wb * c.tb;
+      bool take = !found;
+      if (found) {
+        if (ok && !full) take = true;
+        else if (ok && full) take = area > best_area || (area == best_area && ks < p.ksplit);
+        else if (!ok && !full) take = wgs > best_wgs;
+      }
+      if (take) {
+        p.mb = 0;
+        p.ksw = ci;
+        p.ksplit = ks;
+        p.mgroups = static_cast<int>((p.mbt + toks - 1) / toks);
+        best_wgs = wgs;
+        best_area = area;
+        full = ok;
+        found = true;
+      }
+    }
+  }
+  return found;
+}
+
+template <int EPI>
+void launch_dt(const DgArgs& a, const DgPlan& p, hipStream_t s) {
+  const DtShape c = kTiled[p.ksw];
+  const dim3 grid((p.tiles + c.wb * c.ww - 1) / (c.wb * c.ww), p.ksplit, p.mgroups);
+  switch (p.ksw) {
+    case 0: hipLaunchKernelGGL((decode_gemm_tiled_kernel<2, 2, 2, 2, EPI>), grid, dim3(256), 0, s, a); break;
+    case 1: hipLaunchKernelGGL((decode_gemm_tiled_kernel<2, 2, 4, 1, EPI>), grid, dim3(256), 0, s, a); break;
+    case 2: hipLaunchKernelGGL((decode_gemm_tiled_kernel<1, 2, 2, 2, EPI>), grid, dim3(256), 0, s, a); break;
+    case 3: hipLaunchKernelGGL((decode_gemm_tiled_kernel<1, 2, 4, 1, EPI>), grid, dim3(256), 0, s, a); break;
+    default: hipLaunchKernelGGL((decode_gemm_tiled_kernel<1, 1, 2, 2, EPI>), grid, dim3(256), 0, s, a); break;
+  }
+}
+
+bool plan_any(int64_t M, int64_t N, int64_t K, int epi, DgPlan& p) {
+  return plan_decode_tiled(M, N, K, epi, p) || plan_decode_gemm(M, N, K, epi, p);
+}
+
 template <int MB, int EPI>
 void launch_dg(const DgArgs& a, const DgPlan& p, hipStream_t s) {
   const dim3 grid(p.tiles, p.ksplit, p.mgroups);
@@ -402,6 +610,8 @@ void launch_dg(const DgArgs& a, const DgPlan& p, hipStream_t s) {
 
 extern "C" {
 
+void drl_decode_gemm_set_tiled(int32_t mode) { drl::g_dt_mode = (mode >= 0 && mode <= 2) ? mode : 1; }
+
 void drl_decode_gemm_set_plan(int32_t mb, int32_t ksw) {
   drl::g_dg_mb = (mb == 1 || mb == 2) ? mb : 0;
   drl::g_dg_ksw = ksw > 0 ? ksw : 0;
@@ -409,7 +619,7 @@ void drl_decode_gemm_set_plan(int32_t mb, int32_t ksw) {
 
 int drl_decode_gemm_plan(int64_t M, int64_t N, int64_t K, int32_t epilogue, int32_t* ksplit, int32_t* mbt) {
   drl::DgPlan p{};
-  if (!drl::plan_decode_gemm(M, N, K, epilogue == DRL_DECODE_SWIGLU ? drl::EPI_SWIGLU : drl::EPI_PARTIAL, p))
+  if (!drl::plan_any(M, N, K, epilogue == DRL_DECODE_SWIGLU ? drl::EPI_SWIGLU : drl::EPI_PARTIAL, p))
     return drl::fail(DRL_ERR_UNSUPPORTED, "decode GEMM: unsupported shape M=%lld N=%lld K=%lld", (long long)M,
                      (long long)N, (long long)K);
   if (ksplit) *ksplit = p.ksplit;
@@ -450,14 +660,17 @@ int drl_decode_gemm(const void* x_packed, const void* w_packed, int64_t M, int64
                 "missing output");
   DRL_CHECK_ARG(epi == EPI_PARTIAL || N % 32 == 0, "SwiGLU needs N % 32 == 0");
   DgPlan p{};
-  if (!plan_decode_gemm(M, N, K, epi, p))
+  if (!plan_any(M, N, K, epi, p))
     return fail(DRL_ERR_UNSUPPORTED, "decode GEMM: unsupported shape M=%lld N=%lld K=%lld", (long long)M,
                 (long long)N, (long long)K);
   DgArgs a{static_cast<const uint16_t*>(x_packed), static_cast<const uint16_t*>(w_packed), static_cast<int>(M),
            static_cast<int>(N), static_cast<int>(K), p.mbt, static_cast<int>(K / 16), p.tiles,
            static_cast<int>(N / 2), partials, static_cast<uint16_t*>(out_packed)};
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (p.mb == 1) {
+  if (p.mb == 0) {
+    if (epi == EPI_PARTIAL) launch_dt<EPI_PARTIAL>(a, p, s);
+    else launch_dt<EPI_SWIGLU>(a, p, s);
+  } else if (p.mb == 1) {
     if (epi == EPI_PARTIAL) launch_dg<1, EPI_PARTIAL>(a, p, s);
     else launch_dg<1, EPI_SWIGLU>(a, p, s);
   } else {
@@ -495,7 +708,7 @@ int drl_decode_qkv_rope(const void* x_packed, const void* w_packed, const void* 
                 "bad shape");
   const int64_t N = (Hq + 2 * Hkv) * D;
   DgPlan p{};
-  if (!plan_decode_gemm(M, N, K, EPI_ROPE, p))
+  if (!plan_any(M, N, K, EPI_ROPE, p))
     return fail(DRL_ERR_UNSUPPORTED, "decode qkv+rope: unsupported shape M=%lld N=%lld K=%lld", (long long)M,
                 (long long)N, (long long)K);
   DgArgs a{};
@@ -522,7 +735,8 @@ int drl_decode_qkv_rope(const void* x_packed, const void* w_packed, const void* 
   a.Hkv = static_cast<int>(Hkv);
   a.D = static_cast<int>(D);
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (p.mb == 1) launch_dg<1, EPI_ROPE>(a, p, s);
+  if (p.mb == 0) launch_dt<EPI_ROPE>(a, p, s);
+  else if (p.mb == 1) launch_dg<1, EPI_ROPE>(a, p, s);
   else launch_dg<2, EPI_ROPE>(a, p, s);
   DRL_LAUNCH_CHECK();
   return DRL_OK;

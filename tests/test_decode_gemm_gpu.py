@@ -28,7 +28,7 @@ def rnd(*shape, scale=1.0, seed=0, dtype=BF):
     return (torch.randn(*shape, device=DEV, generator=g) * scale).to(dtype)
 
 
-@pytest.mark.parametrize("M", [1, 7, 32, 33, 64, 100, 128])
+@pytest.mark.parametrize("M", [1, 7, 32, 33, 64, 100, 128, 257, 512])  # >= 192 rows: the MFMA-tiled form
 @pytest.mark.parametrize("N,K", [(1152, 896), (896, 896), (896, 4864), (96, 64), (200, 128)])
 def test_decode_gemm_partials(M, N, K):
     plan = native.decode_gemm_plan(M, N, K)
@@ -48,7 +48,7 @@ def test_decode_gemm_partials(M, N, K):
     assert torch.equal(part, native.decode_gemm(xp, wp, M, N, K))  # deterministic
 
 
-@pytest.mark.parametrize("M", [5, 64, 128])
+@pytest.mark.parametrize("M", [5, 64, 128, 300, 512])
 @pytest.mark.parametrize("I,K", [(4864, 896), (128, 64)])
 def test_decode_gemm_swiglu_packed(M, I, K):
     ks, mbt = native.decode_gemm_plan(M, 2 * I, K, swiglu=True)
@@ -153,7 +153,7 @@ def _small_model(seed=0, B=48):
     return cfg, Qwen2Model(cfg, store)
 
 
-@pytest.mark.parametrize("B", [5, 48, 130])
+@pytest.mark.parametrize("B", [5, 48, 130, 512])
 def test_packed_decode_step_tracks_unpacked(B):
     """PackedDecode.step (8 launches per layer on packed operands) against the unpacked decode step on the same
     prefilled cache and the same teacher-forced tokens: final hidden states and the written K/V agree at bf16
@@ -227,7 +227,8 @@ def test_packed_rollout_graph_equals_eager():
     assert out.batch["input_ids"].shape == (B, P + R)
 
 
-@pytest.mark.parametrize("M,K,Hq,Hkv,D", [(64, 896, 14, 2, 64), (5, 128, 2, 1, 64), (100, 256, 4, 2, 128)])
+@pytest.mark.parametrize("M,K,Hq,Hkv,D", [(64, 896, 14, 2, 64), (5, 128, 2, 1, 64), (100, 256, 4, 2, 128),
+                                           (512, 896, 14, 2, 64), (200, 256, 4, 2, 128)])
 def test_decode_qkv_rope_matches_gemm_then_rope(M, K, Hq, Hkv, D):
     """One-launch qkv_proj + bias + RoPE (rotation-pair packing) == the two-launch form (decode GEMM with the
     same single K slice, then decode RoPE) bit for bit: the same fp32 sums in the same order, the same roundings."""
@@ -255,7 +256,9 @@ def test_decode_qkv_rope_matches_gemm_then_rope(M, K, Hq, Hkv, D):
         else:
             # the fused launch's shape: whole K per workgroup (K / 64 k16-steps per wave)
             native.lib().drl_decode_gemm_set_plan(0, K // 64)
+            native.lib().drl_decode_gemm_set_tiled(2)  # from 192 rows: the tiled form, one K slice
             part = native.decode_gemm(xp, native.decode_pack_weight(w), M, NQ, K)
+            native.lib().drl_decode_gemm_set_tiled(1)
             native.lib().drl_decode_gemm_set_plan(0, 0)
             assert part.shape[0] == 1
             native.decode_rope(part, bias, pos, cos_t, sin_t, Hq, Hkv, D, q, kc, vt_cache=vt, koff_dev=kd)

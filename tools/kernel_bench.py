@@ -377,6 +377,7 @@ def decode_gemm(Ms=(32, 64, 128, 256, 512)):
                     return a
                 return y
             sweep = {}
+            native.lib().drl_decode_gemm_set_tiled(0)  # the one-round-trip form's plans
             for mbw in (2, 1):
                 for ksw in (19, 14, 7, 4, 2, 1):
                     native.lib().drl_decode_gemm_set_plan(mbw, ksw)
@@ -384,11 +385,15 @@ def decode_gemm(Ms=(32, 64, 128, 256, 512)):
                         continue
                     sweep[f"{mbw}x{ksw}"] = round(time_graph(ours, ncopy) * 1e6, 2)
             native.lib().drl_decode_gemm_set_plan(0, 0)
-            t = time_graph(ours, ncopy)
+            t_rt = time_graph(ours, ncopy)
+            native.lib().drl_decode_gemm_set_tiled(1)
+            ks, _ = native.decode_gemm_plan(M, N, K, sw)
+            t = time_graph(ours, ncopy)  # the automatic plan (MFMA-tiled form from 192 rows)
             t2 = time_graph(lib, ncopy)
             nbytes = 2 * N * K + 2 * M * K
             res.append(dict(kernel="decode_gemm", layer=name, M=M, N=N, K=K, ksplit=ks, us=t * 1e6,
-                            GBps=nbytes / t / 1e9, hipblaslt_us=t2 * 1e6, sweep_us=sweep))
+                            one_round_trip_us=t_rt * 1e6, GBps=nbytes / t / 1e9, TFLOPs=2 * M * N * K / t / 1e12,
+                            hipblaslt_us=t2 * 1e6, sweep_us=sweep))
     return res
 
 
