@@ -151,6 +151,7 @@ SIGNATURES = {
     "drl_decode_gemm_plan": (ctypes.c_int, [I64, I64, I64, I32, P, P]),
     "drl_decode_gemm_set_plan": (None, [I32, I32]),
     "drl_decode_gemm_set_tiled": (None, [I32]),
+    "drl_decode_gemm_force_tiled": (None, [I32, I32]),
     "drl_decode_pack_weight_elems": (SZ, [I64, I64, I32]),
     "drl_decode_pack_weight": (ctypes.c_int, [P, I64, I64, I64, I32, P, P]),
     "drl_decode_gemm": (ctypes.c_int, [P, P, I64, I64, I64, I32, P, P, P]),

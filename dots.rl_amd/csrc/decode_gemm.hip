@@ -190,65 +190,12 @@ __global__ __launch_bounds__(256) void decode_gemm_kernel(DgArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------- tiled GEMM
-// The same packed operands at 97..512 rows, where a projection is an MFMA problem (gate_up at 512 rows:
-// 8.9 GFLOP against a 17 MB weight stream), not a weight stream: every wave owns a WB x TB tile of 32 x 32
-// output blocks (weight rows x tokens) over the workgroup's whole K slice, so each weight fragment feeds TB
-// MFMAs and each activation fragment WB (the one-round-trip kernel above re-reads the activation panel per
-// 32-row weight block and reduces 4 K slices through LDS). Fragments are loaded straight into registers
-// (1-KB coalesced wave loads) through a DEPTH-deep ring, branch-free (the last loads of a slice repeat its
-// last k-step instead of branching), so DEPTH * (WB + TB) loads are always in flight. Workgroup = WW x WT
-// waves; the 4 waves' overlapping fragments are served by L1 / L2. Epilogues straight from the
-// accumulators: fp32 partials (K slice = gridDim.y), SwiGLU (gate row i and up row i + 16 of a block sit in
-// registers r and r + 8 of the same lane; one lane-half exchange forms the packed 16-B pieces), or bias +
-// RoPE + KV-cache writes (rotation pairs likewise lane-local).
-template <int WB, int TB, int WW, int WT, int EPI>
-__global__ __launch_bounds__(256) void decode_gemm_tiled_kernel(DgArgs a) {
-  constexpr int DEPTH = 4;
-  static_assert(WW * WT == 4, "4 waves per workgroup");
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int ww = wave % WW, wt = wave / WW;
-  const int rb0 = (blockIdx.x * WW + ww) * WB;  // first 32-row weight block of this wave
-  const int tb0 = (blockIdx.z * WT + wt) * TB;  // first 32-token block
-  const int per = a.nks / static_cast<int>(gridDim.y);  // k16 steps of this K slice (a multiple of DEPTH)
-  const int s0 = static_cast<int>(blockIdx.y) * per, s1 = s0 + per;
-  const uint16_t* wp[WB];
-  const uint16_t* xp[TB];
-#pragma unroll
-  for (int b = 0; b < WB; ++b)  // blocks past the end re-read the last one (never stored)
-    wp[b] = a.w + static_cast<int64_t>(min(rb0 + b, a.tiles - 1)) * a.nks * 512 + lane * 8;
-  const int64_t xstep = static_cast<int64_t>(a.MBT) * 512;
-#pragma unroll
-  for (int t = 0; t < TB; ++t) xp[t] = a.x + (static_cast<int64_t>(min(tb0 + t, a.MBT - 1)) * 64 + lane) * 8;
-  u16x8 rw[DEPTH][WB], rx[DEPTH][TB];
-  auto load = [&](int d, int st) {
-#pragma unroll
-    for (int b = 0; b < WB; ++b) rw[d][b] = __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(wp[b] + st * 512));
-#pragma unroll
-    for (int t = 0; t < TB; ++t) rx[d][t] = *reinterpret_cast<const u16x8*>(xp[t] + st * xstep);
-  };
-#pragma unroll
-  for (int d = 0; d < DEPTH; ++d) load(d, s0 + d);
-  __builtin_amdgcn_sched_barrier(0);
-  f32x16 acc[WB][TB];
-#pragma unroll
-  for (int b = 0; b < WB; ++b)
-#pragma unroll
-    for (int t = 0; t < TB; ++t) acc[b][t] = f32x16{};
-  for (int st = s0; st < s1; st += DEPTH) {
-#pragma unroll
-    for (int d = 0; d < DEPTH; ++d) {
-#pragma unroll
-      for (int b = 0; b < WB; ++b)
-#pragma unroll
-        for (int t = 0; t < TB; ++t)
-          acc[b][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(rw[d][b]), as_bf16x8(rx[d][t]), acc[b][t], 0, 0, 0);
-      load(d, min(st + d + DEPTH, s1 - 1));
-      // keep the refill here: left alone, hipcc sinks every load next to its MFMAs (fewest live registers)
-      // and the ring degenerates to one k-step in flight behind a vmcnt(0)
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-  // C row i of a block <-> register (i & 3) + 4 (i >> 3), lane half (i >> 2) & 1; column = token lane & 31
+// epilogue of the tiled forms, straight from a wave's WB x TB accumulator blocks (rb0 / tb0: its first weight /
+// token block, ks: its K slice)
+// C row i of a block <-> register (i & 3) + 4 (i >> 3), lane half (i >> 2) & 1; column = token lane & 31
+template <int WB, int TB, int EPI>
+__device__ __forceinline__ void tiled_epilogue(const DgArgs& a, const f32x16 (&acc)[WB][TB], int rb0, int tb0, int lane,
+                                               int ks) {
   const int hh = lane >> 5, ml = lane & 31;
 #pragma unroll
   for (int b = 0; b < WB; ++b) {
@@ -261,7 +208,7 @@ __global__ __launch_bounds__(256) void decode_gemm_tiled_kernel(DgArgs a) {
       const f32x16& c = acc[b][t];
       if constexpr (EPI == EPI_PARTIAL) {
         if (m >= a.M) continue;
-        float* dst = a.part + (static_cast<int64_t>(blockIdx.y) * a.M + m) * a.N;
+        float* dst = a.part + (static_cast<int64_t>(ks) * a.M + m) * a.N;
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const int n = rb * 32 + 8 * g + 4 * hh;  // registers 4g .. 4g+3: rows n .. n+3
@@ -326,6 +273,152 @@ __global__ __launch_bounds__(256) void decode_gemm_tiled_kernel(DgArgs a) {
       }
     }
   }
+}
+
+
+// The same packed operands at 97..512 rows, where a projection is an MFMA problem (gate_up at 512 rows:
+// 8.9 GFLOP against a 17 MB weight stream), not a weight stream: every wave owns a WB x TB tile of 32 x 32
+// output blocks (weight rows x tokens) over the workgroup's whole K slice, so each weight fragment feeds TB
+// MFMAs and each activation fragment WB (the one-round-trip kernel above re-reads the activation panel per
+// 32-row weight block and reduces 4 K slices through LDS). Fragments are loaded straight into registers
+// (1-KB coalesced wave loads) through a DEPTH-deep ring, branch-free (the last loads of a slice repeat its
+// last k-step instead of branching), so DEPTH * (WB + TB) loads are always in flight. Workgroup = WW x WT
+// waves; the 4 waves' overlapping fragments are served by L1 / L2. Epilogues straight from the
+// accumulators: fp32 partials (K slice = gridDim.y), SwiGLU (gate row i and up row i + 16 of a block sit in
+// registers r and r + 8 of the same lane; one lane-half exchange forms the packed 16-B pieces), or bias +
+// RoPE + KV-cache writes (rotation pairs likewise lane-local).
+template <int WB, int TB, int WW, int WT, int EPI>
+__global__ __launch_bounds__(256) void decode_gemm_tiled_kernel(DgArgs a) {
+  constexpr int DEPTH = 4;
+  static_assert(WW * WT == 4, "4 waves per workgroup");
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int ww = wave % WW, wt = wave / WW;
+  const int rb0 = (blockIdx.x * WW + ww) * WB;  // first 32-row weight block of this wave
+  const int tb0 = (blockIdx.z * WT + wt) * TB;  // first 32-token block
+  const int per = a.nks / static_cast<int>(gridDim.y);  // k16 steps of this K slice (a multiple of DEPTH)
+  const int s0 = static_cast<int>(blockIdx.y) * per, s1 = s0 + per;
+  const uint16_t* wp[WB];
+  const uint16_t* xp[TB];
+#pragma unroll
+  for (int b = 0; b < WB; ++b)  // blocks past the end re-read the last one (never stored)
+    wp[b] = a.w + static_cast<int64_t>(min(rb0 + b, a.tiles - 1)) * a.nks * 512 + lane * 8;
+  const int64_t xstep = static_cast<int64_t>(a.MBT) * 512;
+#pragma unroll
+  for (int t = 0; t < TB; ++t) xp[t] = a.x + (static_cast<int64_t>(min(tb0 + t, a.MBT - 1)) * 64 + lane) * 8;
+  u16x8 rw[DEPTH][WB], rx[DEPTH][TB];
+  auto load = [&](int d, int st) {
+#pragma unroll
+    for (int b = 0; b < WB; ++b) rw[d][b] = __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(wp[b] + st * 512));
+#pragma unroll
+    for (int t = 0; t < TB; ++t) rx[d][t] = *reinterpret_cast<const u16x8*>(xp[t] + st * xstep);
+  };
+#pragma unroll
+  for (int d = 0; d < DEPTH; ++d) load(d, s0 + d);
+  __builtin_amdgcn_sched_barrier(0);
+  f32x16 acc[WB][TB];
+#pragma unroll
+  for (int b = 0; b < WB; ++b)
+#pragma unroll
+    for (int t = 0; t < TB; ++t) acc[b][t] = f32x16{};
+  for (int st = s0; st < s1; st += DEPTH) {
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d) {
+#pragma unroll
+      for (int b = 0; b < WB; ++b)
+#pragma unroll
+        for (int t = 0; t < TB; ++t)
+          acc[b][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(rw[d][b]), as_bf16x8(rx[d][t]), acc[b][t], 0, 0, 0);
+      load(d, min(st + d + DEPTH, s1 - 1));
+      // keep the refill here: left alone, hipcc sinks every load next to its MFMAs (fewest live registers)
+      // and the ring degenerates to one k-step in flight behind a vmcnt(0)
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  tiled_epilogue<WB, TB, EPI>(a, acc, rb0, tb0, lane, static_cast<int>(blockIdx.y));
+}
+
+// LDS-staged tiled form: the workgroup's fragments (RB = WR * WB weight blocks + TT = WT * TB token blocks per
+// k16 step) are copied global -> LDS by LDS-DMA (global_load_lds_dwordx4: one 1-KB fragment per wave
+// instruction, lane-linear, so the image needs no swizzle and every ds_read_b128 of a fragment is
+// conflict-free) in stages of KST k-steps through NBUF buffers, STAGES_AHEAD stages in flight; each fragment
+// leaves L2 once per workgroup instead of once per wave. Order per stage (cdna_hip_programming.md §5,
+// "Pipelining across barriers"): counted vmcnt (own copies of this stage landed, the next stages' still in
+// flight) -> lgkmcnt(0) + raw s_barrier (everyone's copies landed; everyone's reads of the buffer about to be
+// refilled are done) -> refill the oldest buffer -> MFMAs from this stage's buffer. One __shared__ array.
+template <int WR, int WT, int WB, int TB, int EPI>
+__global__ __launch_bounds__(64 * WR * WT) void decode_gemm_lds_kernel(DgArgs a) {
+  constexpr int NW = WR * WT, RB = WR * WB, TT = WT * TB, FR = RB + TT;
+  constexpr int KST = 2, NBUF = 3;
+  constexpr int PER_WAVE = KST * FR / NW;  // LDS-DMA instructions per wave and stage
+  static_assert(KST * FR % NW == 0, "copies must divide evenly over the waves");
+  __shared__ __attribute__((aligned(16))) uint16_t lds[NBUF * KST * FR * 512];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wr = wave % WR, wt = wave / WR;
+  const int rbw = blockIdx.x * RB, tbw = blockIdx.z * TT;  // workgroup's first weight / token block
+  const int per = a.nks / static_cast<int>(gridDim.y);
+  const int s0 = static_cast<int>(blockIdx.y) * per;
+  const int nst = per / KST;  // stages of this K slice
+  const int64_t xstep = static_cast<int64_t>(a.MBT) * 512;
+  // this wave's copies: fragment slots idx = wave + NW * c of a stage (slot = j * FR + f)
+  const uint16_t* src[PER_WAVE];
+  int64_t sstep[PER_WAVE];
+  int dsto[PER_WAVE];
+#pragma unroll
+  for (int c = 0; c < PER_WAVE; ++c) {
+    const int idx = wave + NW * c, j = idx / FR, f = idx % FR;
+    if (f < RB) {
+      src[c] = a.w + (static_cast<int64_t>(min(rbw + f, a.tiles - 1)) * a.nks + j) * 512 + lane * 8;
+      sstep[c] = 512;
+    } else {
+      src[c] = a.x + (static_cast<int64_t>(j) * a.MBT + min(tbw + f - RB, a.MBT - 1)) * 512 + lane * 8;
+      sstep[c] = xstep;
+    }
+    dsto[c] = idx * 512;
+  }
+  auto issue = [&](int stage) {
+    const int st = s0 + min(stage, nst - 1) * KST;  // past the end: repeat the last stage (never read)
+    uint16_t* buf = lds + (stage % NBUF) * (KST * FR * 512);
+#pragma unroll
+    for (int c = 0; c < PER_WAVE; ++c)
+      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src[c] + st * sstep[c]),
+                                       (__attribute__((address_space(3))) void*)(buf + dsto[c]), 16, 0, 0);
+  };
+  f32x16 acc[WB][TB];
+#pragma unroll
+  for (int b = 0; b < WB; ++b)
+#pragma unroll
+    for (int t = 0; t < TB; ++t) acc[b][t] = f32x16{};
+  issue(0);
+  issue(1);
+  for (int i = 0; i < nst; ++i) {
+    // own copies of stage i landed (stage i + 1's PER_WAVE may still be in flight)
+    if constexpr (PER_WAVE == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else if constexpr (PER_WAVE == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    else if constexpr (PER_WAVE == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if constexpr (PER_WAVE == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else static_assert(PER_WAVE == 2 || PER_WAVE == 3 || PER_WAVE == 4 || PER_WAVE == 6, "vmcnt table");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    issue(i + 2);  // into the buffer read in iteration i - 1 (every wave is past it)
+    const uint16_t* buf = lds + (i % NBUF) * (KST * FR * 512);
+#pragma unroll
+    for (int j = 0; j < KST; ++j) {
+      u16x8 wf[WB], xf[TB];
+#pragma unroll
+      for (int b = 0; b < WB; ++b)
+        wf[b] = *reinterpret_cast<const u16x8*>(buf + (j * FR + wr * WB + b) * 512 + lane * 8);
+#pragma unroll
+      for (int t = 0; t < TB; ++t)
+        xf[t] = *reinterpret_cast<const u16x8*>(buf + (j * FR + RB + wt * TB + t) * 512 + lane * 8);
+#pragma unroll
+      for (int b = 0; b < WB; ++b)
+#pragma unroll
+        for (int t = 0; t < TB; ++t)
+          acc[b][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(wf[b]), as_bf16x8(xf[t]), acc[b][t], 0, 0, 0);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the two repeated stages' copies
+  tiled_epilogue<WB, TB, EPI>(a, acc, rbw + wr * WB, tbw + wt * TB, lane, static_cast<int>(blockIdx.y));
 }
 
 // ------------------------------------------------------------------------------------------- consumers
@@ -521,53 +614,52 @@ bool plan_decode_gemm(int64_t M, int64_t N, int64_t K, int epi, DgPlan& p) {
   return found;
 }
 
-// tiled path (97..512 rows): (WB, TB, WW, WT) configurations instantiated, largest wave tile first
-struct DtShape { int wb, tb, ww, wt; };
-constexpr DtShape kTiled[] = {{2, 2, 2, 2}, {2, 2, 4, 1}, {1, 2, 2, 2}, {1, 2, 4, 1}, {1, 1, 2, 2}};
+// tiled path: (WB, TB, WW, WT, lds) configurations instantiated (lds: the LDS-staged kernel, WW x WT waves)
+struct DtShape { int wb, tb, ww, wt, lds; };
+constexpr DtShape kTiled[] = {{2, 2, 4, 2, 1}, {2, 2, 2, 2, 1}, {1, 2, 2, 2, 1}, {2, 1, 2, 2, 1},
+                              {2, 2, 2, 2, 0}, {2, 2, 4, 1, 0}, {1, 2, 2, 2, 0}, {1, 2, 4, 1, 0}, {1, 1, 2, 2, 0}};
+constexpr int kNumTiled = static_cast<int>(sizeof(kTiled) / sizeof(kTiled[0]));
+int g_dt_force = -1;  // tuning: force configuration index (drl_decode_gemm_force_tiled), -1 = planner
+int g_dt_min_rows = 192;  // tuning: smallest M for the tiled path
 // 0 = never the tiled path (drl_decode_gemm_set_tiled), 1 = automatic, 2 = automatic with one K slice (tests:
 // the partial form in the fused qkv + RoPE launch's summation order)
 int g_dt_mode = 1;
 
-// the tiled plan when the shape is in its range: K slices only for the partial epilogue (each a multiple of
-// 4 k-steps, at most 4 slices); the biggest wave tile that still gives >= 160 workgroups with the fewest
-// slices, else the most workgroups. p.mb = 0 marks a tiled plan; p.ksw = index into kTiled.
+// the tiled plan when the shape is in its range. Configuration by shape class, from the sweep of every
+// configuration at 128 / 256 / 512 rows (tools/kernel_bench.py --only decode_gemm, profiles/r02_decode_gemm.jsonl):
+//   SwiGLU gate_up from 192 rows: LDS-staged, 64 x 128 workgroup tile (512 rows: 29.1 -> 19.0 us);
+//   partials with a long K (down_proj, K 4864) from 384 rows: register ring, 64 x 128 (23.3 -> 14.6 us);
+//   partials / qkv + RoPE with a short K from 192 rows: register ring, 64 x 64 (o_proj 7.7 -> 6.7 us,
+//   qkv 11.9 -> 8.6 us at 512).
+// K slices (partials only, each a multiple of 4 k-steps, <= 4): the fewest that give >= 160 workgroups, else the
+// most workgroups. p.mb = 0 marks a tiled plan; p.ksw = index into kTiled.
 bool plan_decode_tiled(int64_t M, int64_t N, int64_t K, int epi, DgPlan& p) {
-  // measured (tools/kernel_bench.py --only decode_gemm): faster than the one-round-trip form from 256 rows for
-  // the partial projections (qkv 7.6 -> 6.6 us, o 7.5 -> 6.5, down 13.4 -> 12.2 at 256; 11.9 -> 8.6, 7.8 -> 6.7,
-  // 22.8 -> 14.4 at 512), slower below and for the SwiGLU gate_up (29.3 -> 31.9 us at 512)
-  if (g_dt_mode == 0 || M < 192 || M > 512 || K % 64 != 0 || N < 1 || epi == EPI_SWIGLU) return false;
+  if (g_dt_mode == 0 || M < g_dt_min_rows || M > 512 || K % 64 != 0 || N < 1) return false;
+  int ci;
+  if (g_dt_force >= 0) ci = g_dt_force;
+  else if (epi == EPI_SWIGLU) ci = 2;
+  else if (K >= 2048) { if (M < 384 && g_dt_min_rows >= 192) return false; ci = 6; }
+  else ci = 8;
   const int blocks = static_cast<int>((M + 31) / 32);
   p.mbt = (blocks + 1) / 2 * 2;
   p.tiles = static_cast<int>(epi == EPI_SWIGLU ? (N / 2 + 15) / 16 : (N + 31) / 32);
   const int nks = static_cast<int>(K / 16);
-  bool found = false, full = false;
+  const DtShape& c = kTiled[ci];
+  const int rows = c.wb * c.ww, toks = c.tb * c.wt;
+  const int64_t base = static_cast<int64_t>((p.tiles + rows - 1) / rows) * ((p.mbt + toks - 1) / toks);
+  bool found = false;
   int64_t best_wgs = 0;
-  int best_area = 0;
-  for (int ci = 0; ci < static_cast<int>(sizeof(kTiled) / sizeof(kTiled[0])); ++ci) {
-    const DtShape& c = kTiled[ci];
-    const int rows = c.wb * c.ww, toks = c.tb * c.wt;
-    const int64_t base = static_cast<int64_t>((p.tiles + rows - 1) / rows) * ((p.mbt + toks - 1) / toks);
-    for (int ks = 1; ks <= (epi == EPI_PARTIAL && g_dt_mode == 1 ? 4 : 1); ++ks) {
-      if (nks % ks != 0 || (nks / ks) % 4 != 0) continue;
-      const int64_t wgs = base * ks;
-      const bool ok = wgs >= 160;
-      const int area = c.wb * c.tb;
-      bool take = !found;
-      if (found) {
-        if (ok && !full) take = true;
-        else if (ok && full) take = area > best_area || (area == best_area && ks < p.ksplit);
-        else if (!ok && !full) take = wgs > best_wgs;
-      }
-      if (take) {
-        p.mb = 0;
-        p.ksw = ci;
-        p.ksplit = ks;
-        p.mgroups = static_cast<int>((p.mbt + toks - 1) / toks);
-        best_wgs = wgs;
-        best_area = area;
-        full = ok;
-        found = true;
-      }
+  for (int ks = 1; ks <= (epi == EPI_PARTIAL && g_dt_mode == 1 ? 4 : 1); ++ks) {
+    if (nks % ks != 0 || (nks / ks) % 4 != 0) continue;  // register ring: DEPTH 4; LDS stages: 2 k-steps
+    const int64_t wgs = base * ks;
+    if (found && best_wgs >= 160) break;  // the fewest slices that fill the chip
+    if (!found || wgs > best_wgs) {
+      p.mb = 0;
+      p.ksw = ci;
+      p.ksplit = ks;
+      p.mgroups = static_cast<int>((p.mbt + toks - 1) / toks);
+      best_wgs = wgs;
+      found = true;
     }
   }
   return found;
@@ -578,10 +670,14 @@ void launch_dt(const DgArgs& a, const DgPlan& p, hipStream_t s) {
   const DtShape c = kTiled[p.ksw];
   const dim3 grid((p.tiles + c.wb * c.ww - 1) / (c.wb * c.ww), p.ksplit, p.mgroups);
   switch (p.ksw) {
-    case 0: hipLaunchKernelGGL((decode_gemm_tiled_kernel<2, 2, 2, 2, EPI>), grid, dim3(256), 0, s, a); break;
-    case 1: hipLaunchKernelGGL((decode_gemm_tiled_kernel<2, 2, 4, 1, EPI>), grid, dim3(256), 0, s, a); break;
-    case 2: hipLaunchKernelGGL((decode_gemm_tiled_kernel<1, 2, 2, 2, EPI>), grid, dim3(256), 0, s, a); break;
-    case 3: hipLaunchKernelGGL((decode_gemm_tiled_kernel<1, 2, 4, 1, EPI>), grid, dim3(256), 0, s, a); break;
+    case 0: hipLaunchKernelGGL((decode_gemm_lds_kernel<4, 2, 2, 2, EPI>), grid, dim3(512), 0, s, a); break;
+    case 1: hipLaunchKernelGGL((decode_gemm_lds_kernel<2, 2, 2, 2, EPI>), grid, dim3(256), 0, s, a); break;
+    case 2: hipLaunchKernelGGL((decode_gemm_lds_kernel<2, 2, 1, 2, EPI>), grid, dim3(256), 0, s, a); break;
+    case 3: hipLaunchKernelGGL((decode_gemm_lds_kernel<2, 2, 2, 1, EPI>), grid, dim3(256), 0, s, a); break;
+    case 4: hipLaunchKernelGGL((decode_gemm_tiled_kernel<2, 2, 2, 2, EPI>), grid, dim3(256), 0, s, a); break;
+    case 5: hipLaunchKernelGGL((decode_gemm_tiled_kernel<2, 2, 4, 1, EPI>), grid, dim3(256), 0, s, a); break;
+    case 6: hipLaunchKernelGGL((decode_gemm_tiled_kernel<1, 2, 2, 2, EPI>), grid, dim3(256), 0, s, a); break;
+    case 7: hipLaunchKernelGGL((decode_gemm_tiled_kernel<1, 2, 4, 1, EPI>), grid, dim3(256), 0, s, a); break;
     default: hipLaunchKernelGGL((decode_gemm_tiled_kernel<1, 1, 2, 2, EPI>), grid, dim3(256), 0, s, a); break;
   }
 }
@@ -609,6 +705,11 @@ void launch_dg(const DgArgs& a, const DgPlan& p, hipStream_t s) {
 }  // namespace drl
 
 extern "C" {
+
+void drl_decode_gemm_force_tiled(int32_t config, int32_t min_rows) {
+  drl::g_dt_force = (config >= 0 && config < drl::kNumTiled) ? config : -1;
+  drl::g_dt_min_rows = min_rows > 0 ? min_rows : 192;
+}
 
 void drl_decode_gemm_set_tiled(int32_t mode) { drl::g_dt_mode = (mode >= 0 && mode <= 2) ? mode : 1; }
 

@@ -467,6 +467,8 @@ void drl_decode_gemm_set_plan(int32_t mb, int32_t ksw);
 /* 192..512 rows run the MFMA-tiled form (2-D wave tiles over weight rows x tokens) for the partial and qkv + RoPE
  * projections: mode 1 (default); 0 = never (A/B tuning); 2 = tiled with one K slice (tests). */
 void drl_decode_gemm_set_tiled(int32_t mode);
+/* Tuning hook: force tiled configuration `config` (-1 = planner) and the smallest M of the tiled path (0 = 192). */
+void drl_decode_gemm_force_tiled(int32_t config, int32_t min_rows);
 /* Elements of the packed copy of W (N, K) bf16 (swiglu: W = [gate | up], blocks interleave 16 + 16 rows). */
 size_t drl_decode_pack_weight_elems(int64_t N, int64_t K, int32_t swiglu);
 int drl_decode_pack_weight(const void* w, int64_t ld, int64_t N, int64_t K, int32_t swiglu, void* packed, void* stream);

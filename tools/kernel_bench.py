@@ -387,13 +387,19 @@ def decode_gemm(Ms=(32, 64, 128, 256, 512)):
             native.lib().drl_decode_gemm_set_plan(0, 0)
             t_rt = time_graph(ours, ncopy)
             native.lib().drl_decode_gemm_set_tiled(1)
+            tiled = {}
+            for ci in range(9):  # every tiled configuration (0-3 LDS-staged, 4-8 register ring), from 97 rows
+                native.lib().drl_decode_gemm_force_tiled(ci, 97)
+                if native.decode_gemm_plan(M, N, K, sw) is not None and M >= 97:
+                    tiled[ci] = round(time_graph(ours, ncopy) * 1e6, 2)
+            native.lib().drl_decode_gemm_force_tiled(-1, 0)
             ks, _ = native.decode_gemm_plan(M, N, K, sw)
             t = time_graph(ours, ncopy)  # the automatic plan (MFMA-tiled form from 192 rows)
             t2 = time_graph(lib, ncopy)
             nbytes = 2 * N * K + 2 * M * K
             res.append(dict(kernel="decode_gemm", layer=name, M=M, N=N, K=K, ksplit=ks, us=t * 1e6,
                             one_round_trip_us=t_rt * 1e6, GBps=nbytes / t / 1e9, TFLOPs=2 * M * N * K / t / 1e12,
-                            hipblaslt_us=t2 * 1e6, sweep_us=sweep))
+                            hipblaslt_us=t2 * 1e6, sweep_us=sweep, tiled_us=tiled))
     return res
 
 
