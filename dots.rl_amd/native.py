@@ -649,6 +649,31 @@ def flash_attn_bwd(q, k, kt, v, o, dout, lse, key_valid, dq, dk, dv):
           "drl_flash_attn_bwd")
 
 
+GEMM_PLAIN, GEMM_BIAS, GEMM_SWIGLU = 0, 1, 2
+
+
+def gemm_nt(x, w, bias=None, swiglu=False, out=None, out_gu=None):
+    """Full-sequence projection (csrc/gemm.hip): x (M, K) bf16 @ w (N, K)^T -> (M, N) bf16 (+ bias); with
+    ``swiglu`` (w = [gate | up], N = 2I) -> a (M, I) = bf16(bf16(silu(g)) * u), and ``out_gu`` (M, N) receives
+    [g | u] (bf16) for the backward."""
+    _dev(x, w, bias, out, out_gu)
+    assert x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x.dim() == 2 and w.dim() == 2
+    assert x.stride(1) == 1 and w.stride(1) == 1 and x.shape[1] == w.shape[1]
+    M, K = x.shape
+    N = w.shape[0]
+    n_out = N // 2 if swiglu else N
+    if out is None:
+        out = torch.empty(M, n_out, dtype=torch.bfloat16, device=x.device)
+    assert out.shape == (M, n_out) and out.stride(1) == 1 and out.dtype == torch.bfloat16
+    if out_gu is not None:
+        assert swiglu and out_gu.shape == (M, N) and out_gu.stride(1) == 1
+    epi = GEMM_SWIGLU if swiglu else (GEMM_BIAS if bias is not None else GEMM_PLAIN)
+    check(lib().drl_gemm_bf16_nt(_p(x), x.stride(0), _p(w), w.stride(0), _p(out), out.stride(0), M, N, K,
+                                 _p(bias), epi, _p(out_gu), out_gu.stride(0) if out_gu is not None else 0, _stream()),
+          "drl_gemm_bf16_nt")
+    return out
+
+
 LINEAR_NONE, LINEAR_BIAS, LINEAR_SWIGLU = 0, 1, 2
 
 

@@ -501,6 +501,21 @@ int drl_decode_rope(const float* partials, int32_t nsplit, const void* bias, con
                     int64_t D, void* q, void* k_cache, void* v_cache, void* vt_cache, int64_t Tk, int64_t ld_vt,
                     int64_t koff, const int64_t* koff_dev, void* stream);
 
+
+/* ------------------------------------------------------------------------------------------------
+ * Full-sequence projection GEMMs (csrc/gemm.hip): y = x W^T with x (M, K) and W (N, K) row-major bf16, fp32
+ * accumulation, bf16 out — the nn.Linear calls of HF Qwen2 / Llama under autocast in the reference's FSDP actor
+ * (dp_actor.py:110 -> modeling_qwen2 / modeling_llama: q/k/v, o, gate/up, down, lm_head).
+ * PLAIN: c (M, N) = bf16(x W^T). BIAS: c = bf16(x W^T + bias) (addmm: one rounding). SWIGLU: W = [gate | up]
+ * (N = 2I rows), c (M, I) = bf16(bf16(silu(g)) * u) with g, u the bf16-rounded gate / up sums (swiglu_fwd's
+ * semantics); c2 (M, 2I) = [g | u] when not NULL (the backward's saved activation). K % 64 == 0; A / B rows
+ * 16-byte aligned. */
+enum { DRL_GEMM_PLAIN = 0, DRL_GEMM_BIAS = 1, DRL_GEMM_SWIGLU = 2 };
+int drl_gemm_bf16_nt(const void* a, int64_t lda, const void* b, int64_t ldb, void* c, int64_t ldc, int64_t M,
+                     int64_t N, int64_t K, const void* bias, int32_t epilogue, void* c2, int64_t ldc2, void* stream);
+/* Tuning hook: 0 = automatic tile, 1 = 256 x 128, 2 = 128 x 128. */
+void drl_gemm_set_tile(int32_t tile);
+
 #ifdef __cplusplus
 }
 #endif

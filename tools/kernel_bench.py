@@ -425,6 +425,40 @@ def train_gemms(Ms=(6144, 12288)):
     return res
 
 
+def our_gemms(Ms=(6144, 12288)):
+    """csrc/gemm.hip (drl_gemm_bf16_nt, both tiles) vs hipBLASLt on the forward projections of the log-prob /
+    update micro-batches; gate_up with the SwiGLU epilogue vs hipBLASLt + swiglu_fwd."""
+    from dots.rl_amd.workers import _enable_gemm_tuning
+    _enable_gemm_tuning("auto")
+    dev, bf = "cuda", torch.bfloat16
+    res = []
+    for name, N, K in (("qkv", 1152, 896), ("o_proj", 896, 896), ("gate_up", 9728, 896), ("down", 896, 4864),
+                       ("lm_head", 151936, 896)):
+        w = torch.randn(N, K, device=dev, dtype=bf) * 0.05
+        b = torch.randn(N, device=dev, dtype=bf) if name == "qkv" else None
+        for M in (Ms if name != "lm_head" else (2048, 4096)):
+            x = torch.randn(M, K, device=dev, dtype=bf)
+            fl = 2.0 * M * N * K
+            sw = name == "gate_up"
+            if sw:
+                a = torch.empty(M, N // 2, device=dev, dtype=bf)
+                tl = time_it(lambda: native.swiglu_fwd(x @ w.t(), a))
+            elif b is not None:
+                tl = time_it(lambda: torch.addmm(b, x, w.t()))
+            else:
+                tl = time_it(lambda: x @ w.t())
+            row = dict(kernel="gemm_nt", layer=name, M=M, N=N, K=K, hipblaslt_us=tl * 1e6, hipblaslt_TF=fl / tl / 1e12)
+            for tile in (0, 1, 2, 3, 4, 5):
+                native.lib().drl_gemm_set_tile(tile)
+                t = time_it(lambda: native.gemm_nt(x, w, bias=b, swiglu=sw))
+                row[f"tile{tile}_us"] = t * 1e6
+                row[f"tile{tile}_TF"] = fl / t / 1e12
+            native.lib().drl_gemm_set_tile(0)
+            res.append(row)
+            del x
+    return res
+
+
 def swiglu(Ns=(6144, 12288), I=4864):
     """SwiGLU forward / backward at the training (8 x 768) and log-prob (16 x 768) micro-batch rows, HBM GB/s."""
     dev, bf = "cuda", torch.bfloat16
@@ -504,6 +538,10 @@ if __name__ == "__main__":
         sys.exit(0)
     if args.only == "train_gemms":
         for r in train_gemms():
+            print(json.dumps(r), flush=True)
+        sys.exit(0)
+    if args.only == "gemm":
+        for r in our_gemms():
             print(json.dumps(r), flush=True)
         sys.exit(0)
     if args.only == "decode_gemm":
