@@ -237,6 +237,11 @@ def main():
     n_launch, t_launch, b_launch = timer.summary()
     if rank == 0:
         ar = cfg.actor_rollout_ref
+        preset = str(ar.model.get("path", "random:qwen2.5-0.5b"))
+        model_name = {"random:qwen2.5-0.5b": "Qwen2.5-0.5B", "random:llama-3-8b": "Llama-3-8B",
+                      "random:qwen2.5-7b": "Qwen2.5-7B", "random:": "Qwen2.5-0.5B"}.get(preset, preset)
+        if args.tiny:
+            model_name += " (2 layers)"
         _, per_unit, bound, peak, unit = ROOFLINE[args.roofline_kernel]
         scale = 1e12 if unit == "TFLOP/s" else 1e9
         achieved = b_launch / t_launch / scale if n_launch else None
@@ -263,8 +268,9 @@ def main():
             "vs_baseline": None,
             "dtype": "bf16",
             "data": "synthetic",
-            "config": {"workload": "Qwen2.5-0.5B GRPO, 64 prompts x n=8, 512-tok prompts / 256-tok responses",
-                       "model": "Qwen2.5-0.5B (random init)", "global_batch": cfg.data.train_batch_size * ar.rollout.n,
+            "config": {"workload": (f"{model_name} GRPO, {cfg.data.train_batch_size} prompts x n={ar.rollout.n}, "
+                                    f"{cfg.data.max_prompt_length}-tok prompts / {cfg.data.max_response_length}-tok responses"),
+                       "model": f"{model_name} (random init)", "global_batch": cfg.data.train_batch_size * ar.rollout.n,
                        "seq_len": cfg.data.max_prompt_length + cfg.data.max_response_length,
                        "parallelism": f"dp{world}", "tiny": bool(args.tiny)},
             "timing_s": {k.split("/", 1)[1]: sum(h[k] for h in hist) / len(hist) for k in hist[0] if k.startswith("timing_s/")},

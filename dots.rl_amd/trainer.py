@@ -83,7 +83,8 @@ def compute_advantage(data: DataProto, adv_estimator, gamma=1.0, lam=1.0, num_re
 
 
 class SyntheticPromptLoader:
-    """Fixed-length synthetic prompts: token ids ~ U[0, 151643), no padding."""
+    """Fixed-length synthetic prompts: token ids ~ U[0, vocab_limit), no padding (vocab_limit is
+    also the pad id of left-padded rows, so it must be a valid embedding row)."""
 
     def __init__(self, batch_size, prompt_length, vocab_limit=151643, seed=1234, device="cuda", left_pad=None):
         self.batch_size = batch_size
@@ -122,8 +123,15 @@ class RayPPOTrainer:
         # holding `rm_scores`; the reward model itself is outside this repository's path
         self.use_rm = bool(config.reward_model.get("enable", False))
         self.rm_wg = rm_wg
-        self.train_dataloader = train_dataloader or SyntheticPromptLoader(
-            config.data.train_batch_size, config.data.max_prompt_length, seed=config.data.get("seed", 1234))
+        if train_dataloader is None:
+            # token ids below the model's vocabulary (Qwen2.5: its 151643 text tokens; Llama-3: 128256 rows)
+            from .workers import resolve_model_config
+
+            vocab = resolve_model_config(config.actor_rollout_ref.model).vocab_size
+            train_dataloader = SyntheticPromptLoader(config.data.train_batch_size, config.data.max_prompt_length,
+                                                     vocab_limit=min(151643, vocab - 1),
+                                                     seed=config.data.get("seed", 1234))
+        self.train_dataloader = train_dataloader
         self.eos_token_id = eos_token_id
         self.pad_token_id = pad_token_id
         self.use_reference_policy = config.actor_rollout_ref.actor.use_kl_loss or config.algorithm.use_kl_in_reward
