@@ -1233,8 +1233,12 @@ int drl_decode_attention_vt(const void* q, const void* k_cache, const void* vt_c
   // blocks in flight while the grid fits the chip (B=64: 8.7 us at L=768, latency-bound); beyond it the
   // register-lean loop (2 waves per SIMD) with 4 waves up to 2 workgroups per CU, else 2 (B=512, L=768:
   // 201 MB in 34.7 us = 5.8 TB/s, 0.92 of the measured 6.3 TB/s copy rate)
+  // round 2, caches cold as in the rollout (24 layers' caches >> the 256 MB MALL; tools/kernel_bench.py --only
+  // decode_cold, L=640): the register-lean loop at every grid, 8 waves up to one workgroup per CU (B=64:
+  // 11.5 -> 9.7 us, B=128: 15.0 -> 12.0); 4 waves measured 35.8 vs 37.3 us at B=512 in isolation but 41.9 vs
+  // 39.3 in the rollout (rocprof), so 2 waves beyond two workgroups per CU
   const int nw = g_dec_nw ? g_dec_nw : (wgs <= cus ? 8 : (wgs <= 2 * cus ? 4 : 2));
-  const bool lean = g_dec_nw ? g_dec_variant == 1 : wgs > cus;
+  const bool lean = g_dec_nw ? g_dec_variant == 1 : true;
   // blocks in flight per wave (small grids): all of a wave's blocks at the cache capacity, up to 4
   const int64_t per_wave = ((L + 31) / 32 + nw - 1) / nw;
   const int nb = g_dec_nw ? (g_dec_variant > 2 ? g_dec_variant : 2) : (per_wave >= 4 ? 4 : per_wave >= 3 ? 3 : 2);

@@ -115,6 +115,7 @@ class FlatAdamW:
         native.grad_norm(g, out=self.norm)
         self.step_count += 1
         params_bf16 = None if self.store.compute is self.store.master else self.store.compute
+        self.store.version += 1  # the compute copy changes below
         native.adamw_step(self.store.master, g, self.exp_avg, self.exp_avg_sq, lr=self.current_lr(),
                           beta1=self.betas[0], beta2=self.betas[1], eps=self.eps, weight_decay=self.weight_decay,
                           step=self.step_count, max_grad_norm=self.max_grad_norm, grad_norm_t=self.norm,
@@ -148,6 +149,7 @@ class FlatAdamW:
         hp = dict(lr=self.current_lr(), beta1=self.betas[0], beta2=self.betas[1], eps=self.eps,
                   weight_decay=self.weight_decay, step=self.step_count, max_grad_norm=self.max_grad_norm,
                   grad_norm_t=self.norm)
+        st.version += 1  # the compute copy changes below
         m, v, p = self.exp_avg, self.exp_avg_sq, st.master
         native.adamw_step(p[:ns], gw[:ns], m[:ns], v[:ns], params_bf16=None, **hp)
         native.adamw_step(p[ns:], gw[ns:], m[ns:], v[ns:], params_bf16=st.compute[lo:hi] if bf16 else None, **hp)

@@ -649,6 +649,19 @@ def flash_attn_bwd(q, k, kt, v, o, dout, lse, key_valid, dq, dk, dv):
           "drl_flash_attn_bwd")
 
 
+def transpose16(src, out=None):
+    """(rows, cols) 16-bit (bf16) -> (cols, rows) contiguous (csrc/layers.hip transpose16_kernel)."""
+    _dev(src, out)
+    assert src.dim() == 2 and src.stride(1) == 1 and src.element_size() == 2
+    rows, cols = src.shape
+    if out is None:
+        out = torch.empty(cols, rows, dtype=src.dtype, device=src.device)
+    assert out.shape == (cols, rows) and out.stride(1) == 1 and out.dtype == src.dtype
+    check(lib().drl_transpose16(_p(src), src.stride(0), rows, cols, _p(out), out.stride(0), _stream()),
+          "drl_transpose16")
+    return out
+
+
 GEMM_PLAIN, GEMM_BIAS, GEMM_SWIGLU = 0, 1, 2
 
 

@@ -156,6 +156,7 @@ class ParamStore:
                                                                                device=self.device)
         self.small = self.master[:self.n_small]
         self.grad = torch.zeros(self.numel, dtype=f32, device=self.device) if trainable else None
+        self.version = 0  # bumped whenever the compute copy changes (derived copies, e.g. Qwen2Model.wt, refresh)
         self._views = {}
         for name, (o, shape, kind) in self.offsets.items():
             n = math.prod(shape)
@@ -181,6 +182,7 @@ class ParamStore:
     def _put(self, name, vals):
         """Write one parameter's fp32 values (flat) into the master (the part this rank holds) and the
         compute copy."""
+        self.version += 1
         o, shape, kind = self.offsets[name]
         n = math.prod(shape)
         if kind == "small":
@@ -212,6 +214,7 @@ class ParamStore:
     @torch.no_grad()
     def refresh_compute(self):
         """compute copy <- master (GEMM region); sharded: this rank's shard, then an all-gather."""
+        self.version += 1
         if self.compute is self.master:
             return
         lo, hi = self.master_range()
@@ -237,6 +240,7 @@ class ParamStore:
     def copy_from(self, other: "ParamStore"):
         """This store's weights := other's (same config): the small fp32 region and the compute copy; a
         replicated fp32 master gets the full values (sharded other: gathered through its compute copy)."""
+        self.version += 1
         self.small.copy_(other.small)
         if self.compute is not self.master:
             self.compute.copy_(other.compute.to(self.compute.dtype))
@@ -473,17 +477,18 @@ class _DecoderLayer(torch.autograd.Function):
         dx2 = g_x2.to(torch.float32).contiguous().clone()
         dm = g_mlp.to(dt).contiguous().view(N, H)
         # MLP
-        da = dm @ s.w(p + "down_proj")
+        tn = dt == torch.bfloat16  # dgrad as the TN product with the transposed weight copy (see Qwen2Model.wt)
+        da = dm @ m.wt(p + "down_proj").t() if tn else dm @ s.w(p + "down_proj")
         acc_wgrad(s.g(p + "down_proj"), dm, sv["a"])
         dgu = torch.empty_like(sv["gu"])
         native.swiglu_bwd(sv["gu"], da, dgu)
-        dh2 = dgu @ s.w(p + "gate_up_proj")
+        dh2 = dgu @ m.wt(p + "gate_up_proj").t() if tn else dgu @ s.w(p + "gate_up_proj")
         acc_wgrad(s.g(p + "gate_up_proj"), dgu, sv["h2"].view(N, H))
         native.rmsnorm_bwd(sv["x2"], s.w(p + "post_attention_layernorm"), sv["rstd2"], dh2, dx2,
                            s.g(p + "post_attention_layernorm"))
         # attention output projection
         do = dx2.to(dt).view(N, H)
-        dattn = do @ s.w(p + "o_proj")
+        dattn = do @ m.wt(p + "o_proj").t() if tn else do @ s.w(p + "o_proj")
         acc_wgrad(s.g(p + "o_proj"), do, sv["attn"].reshape(N, Hq * D))
         if isinstance(sv["P"], str):  # "flash": fused forward, fused backward
             # fused attention backward (P recomputed from the saved LSE)
@@ -508,7 +513,7 @@ class _DecoderLayer(torch.autograd.Function):
         dqkv = torch.empty(B, T, (Hq + 2 * Hkv) * D, dtype=dt, device=dx2.device)
         native.rope_qkv_bwd(dq, dk, dv, ctx.pos, m.cos, m.sin, Hq, Hkv, D, dqkv)
         dqkv2 = dqkv.view(N, -1)
-        dh1 = dqkv2 @ s.w(p + "qkv_proj.weight")
+        dh1 = dqkv2 @ m.wt(p + "qkv_proj.weight").t() if tn else dqkv2 @ s.w(p + "qkv_proj.weight")
         acc_wgrad(s.g(p + "qkv_proj.weight"), dqkv2, sv["h1"].view(N, H))
         if m.cfg.attention_bias:
             s.g(p + "qkv_proj.bias").add_(dqkv2.sum(0, dtype=torch.float32))
@@ -590,9 +595,25 @@ class Qwen2Model:
         if cfg.rope_scaling:
             raise NotImplementedError(f"rope_scaling {cfg.rope_scaling} (plain RoPE only: Qwen2 / Llama-3-8B)")
         self._zero_bias = None
+        self._wt = {}  # name -> (store version, transposed weight), see wt()
         if not cfg.attention_bias:  # Llama: the shared qkv epilogues add a constant zero bias
             nq = (cfg.num_attention_heads + 2 * cfg.num_key_value_heads) * cfg.head_dim
             self._zero_bias = torch.zeros(nq, dtype=self.dtype, device=dev)
+
+    def wt(self, name):
+        """Transposed bf16 copy (in, out) of GEMM weight ``name`` for the backward's dgrad dx = dy W, run as the TN
+        product dy @ wt.t(): tuned (tools/tune_dgrad.py, shipped tuning file) at 6144 rows qkv 22.1 -> 19.8 us,
+        o 20.8 -> 19.6, gate_up 96.3 -> 88.8, down 55.3 -> 44.4 against the NN form dy @ W; re-transposed
+        (csrc/layers.hip transpose16) when the weights changed (once per optimizer step)."""
+        ver = self.store.version
+        hit = self._wt.get(name)
+        if hit is not None and hit[0] == ver:
+            return hit[1]
+        w = self.store.w(name)
+        buf = hit[1] if hit is not None else torch.empty(w.shape[1], w.shape[0], dtype=w.dtype, device=w.device)
+        native.transpose16(w, out=buf)
+        self._wt[name] = (ver, buf)
+        return buf
 
     def qkv_bias(self, i):
         return self.store.w(f"layers.{i}.qkv_proj.bias") if self.cfg.attention_bias else self._zero_bias

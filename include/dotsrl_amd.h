@@ -516,6 +516,13 @@ int drl_gemm_bf16_nt(const void* a, int64_t lda, const void* b, int64_t ldb, voi
 /* Tuning hook: 0 = automatic tile, 1 = 256 x 128, 2 = 128 x 128. */
 void drl_gemm_set_tile(int32_t tile);
 
+
+/* 16-bit transpose: dst (cols, rows) = src (rows, cols)^T (row strides in elements). The weights' transposed
+ * copies for the backward dgrad (dx = dy W run as the TN product dy (W^T)^T: gate_up 129 -> 105 us, down 57 -> 47 us
+ * at 6144 rows on hipBLASLt), refreshed after each optimizer step. */
+int drl_transpose16(const void* src, int64_t ld_src, int64_t rows, int64_t cols, void* dst, int64_t ld_dst,
+                    void* stream);
+
 #ifdef __cplusplus
 }
 #endif
