@@ -585,8 +585,6 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_vec_kernel(const float* x, co
   }
 }
 
-// dw[j] += sum over blocks of dw_part[:, j]: 16 columns x 16 block-slices per workgroup (many
-// workgroups, short dependent chains), slices combined in a fixed order
 // 16-bit transpose dst (cols, rows) = src (rows, cols)^T through a 64 x 64 LDS tile (rows padded by one
 // element: conflict-free column reads); 16-B row loads, 8-B column stores of 4 consecutive elements. Used for the
 // weights' transposed copies (dgrad dx = dy W as the TN product dy (W^T)^T), refreshed after every optimizer step.
@@ -635,6 +633,47 @@ __global__ __launch_bounds__(256) void transpose16_kernel(const uint16_t* src, i
   }
 }
 
+// Column sums of a bf16 (N, C) matrix (the qkv bias gradient = dqkv summed over tokens), phase 1: workgroup
+// (64-column stripe, row slice) -> fp32 partials (slices, C); thread = 8 columns (one 16-B load) x every 32nd row
+// of the slice, combined in LDS in a fixed order. Phase 2 is colsum_kernel (fixed slice order): deterministic.
+__global__ __launch_bounds__(256) void colsum_bf16_partial_kernel(const uint16_t* x, int64_t ld, int64_t N, int64_t C,
+                                                                  int64_t rows_per_slice, float* part) {
+  __shared__ float red[32][65];
+  const int t = threadIdx.x, cg = t & 7, rl = t >> 3;
+  const int64_t c0 = static_cast<int64_t>(blockIdx.x) * 64 + cg * 8;
+  const int64_t r_begin = static_cast<int64_t>(blockIdx.y) * rows_per_slice;
+  const int64_t r_end = min(N, r_begin + rows_per_slice);
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c0 + 7 < C) {
+    for (int64_t r = r_begin + rl; r < r_end; r += 32) {
+      const uint4 u = *reinterpret_cast<const uint4*>(x + r * ld + c0);
+      const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        acc[2 * e] += __uint_as_float(w[e] << 16);
+        acc[2 * e + 1] += __uint_as_float(w[e] & 0xffff0000u);
+      }
+    }
+  } else {
+    for (int64_t r = r_begin + rl; r < r_end; r += 32)
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (c0 + e < C) acc[e] += __uint_as_float(static_cast<uint32_t>(x[r * ld + c0 + e]) << 16);
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) red[rl][cg * 8 + e] = acc[e];
+  __syncthreads();
+  if (t < 64) {
+    const int64_t c = static_cast<int64_t>(blockIdx.x) * 64 + t;
+    float v = 0.f;
+#pragma unroll
+    for (int k = 0; k < 32; ++k) v += red[k][t];
+    if (c < C) part[static_cast<int64_t>(blockIdx.y) * C + c] = v;
+  }
+}
+
+// dw[j] += sum over blocks of dw_part[:, j]: 16 columns x 16 block-slices per workgroup (many
+// workgroups, short dependent chains), slices combined in a fixed order
 __global__ __launch_bounds__(256) void colsum_kernel(const float* part, int64_t nb, int64_t H, float* out) {
   __shared__ float red[16][16];
   const int c = threadIdx.x & 15, sl = threadIdx.x >> 4;
@@ -909,6 +948,29 @@ int drl_rmsnorm_bwd(const float* x, const float* weight, const float* rstd, cons
   }
   DRL_LAUNCH_CHECK();
   hipLaunchKernelGGL(colsum_kernel, dim3((H + 15) / 16), dim3(256), 0, s, part, static_cast<int64_t>(grid), H, dw);
+  DRL_LAUNCH_CHECK();
+  return DRL_OK;
+}
+
+size_t drl_colsum_bf16_workspace_bytes(int64_t N, int64_t C) {
+  (void)N;
+  return static_cast<size_t>(16) * static_cast<size_t>(C) * sizeof(float);
+}
+
+int drl_colsum_bf16_acc(const void* x, int64_t ld, int64_t N, int64_t C, float* out, void* workspace,
+                        size_t workspace_bytes, void* stream) {
+  using namespace drl;
+  DRL_CHECK_ARG(x && out && N >= 1 && C >= 1 && ld >= C && ld % 8 == 0 && aligned16(x), "bad colsum input");
+  if (workspace == nullptr || workspace_bytes < drl_colsum_bf16_workspace_bytes(N, C))
+    return fail(DRL_ERR_WORKSPACE, "colsum workspace too small");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int64_t slices = std::min<int64_t>(16, (N + 31) / 32);
+  const int64_t per = (N + slices - 1) / slices;
+  float* part = static_cast<float*>(workspace);
+  hipLaunchKernelGGL(colsum_bf16_partial_kernel, dim3(static_cast<unsigned>((C + 63) / 64), static_cast<unsigned>(slices)),
+                     dim3(256), 0, s, static_cast<const uint16_t*>(x), ld, N, C, per, part);
+  DRL_LAUNCH_CHECK();
+  hipLaunchKernelGGL(colsum_kernel, dim3(static_cast<unsigned>((C + 15) / 16)), dim3(256), 0, s, part, slices, C, out);
   DRL_LAUNCH_CHECK();
   return DRL_OK;
 }

@@ -662,6 +662,18 @@ def transpose16(src, out=None):
     return out
 
 
+def colsum_bf16_acc(x, out):
+    """out (C,) fp32 += x (N, C) bf16 summed over rows (csrc/layers.hip, deterministic)."""
+    _dev(x, out)
+    assert x.dim() == 2 and x.stride(1) == 1 and x.dtype == torch.bfloat16 and out.dtype == torch.float32
+    N, C = x.shape
+    assert out.numel() == C and out.is_contiguous()
+    L = lib()
+    ws = _ws.get(L.drl_colsum_bf16_workspace_bytes(N, C), x.device)
+    check(L.drl_colsum_bf16_acc(_p(x), x.stride(0), N, C, _p(out), _p(ws), ws.numel(), _stream()), "drl_colsum_bf16_acc")
+    return out
+
+
 GEMM_PLAIN, GEMM_BIAS, GEMM_SWIGLU = 0, 1, 2
 
 

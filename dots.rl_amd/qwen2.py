@@ -516,7 +516,10 @@ class _DecoderLayer(torch.autograd.Function):
         dh1 = dqkv2 @ m.wt(p + "qkv_proj.weight").t() if tn else dqkv2 @ s.w(p + "qkv_proj.weight")
         acc_wgrad(s.g(p + "qkv_proj.weight"), dqkv2, sv["h1"].view(N, H))
         if m.cfg.attention_bias:
-            s.g(p + "qkv_proj.bias").add_(dqkv2.sum(0, dtype=torch.float32))
+            if dqkv2.dtype == torch.bfloat16:
+                native.colsum_bf16_acc(dqkv2, s.g(p + "qkv_proj.bias"))
+            else:
+                s.g(p + "qkv_proj.bias").add_(dqkv2.sum(0, dtype=torch.float32))
         dx = dx2  # residual: x2 = x + o
         native.rmsnorm_bwd(sv["x"], s.w(p + "input_layernorm"), sv["rstd1"], dh1, dx, s.g(p + "input_layernorm"))
         ctx.save = None

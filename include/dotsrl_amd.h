@@ -523,6 +523,13 @@ void drl_gemm_set_tile(int32_t tile);
 int drl_transpose16(const void* src, int64_t ld_src, int64_t rows, int64_t cols, void* dst, int64_t ld_dst,
                     void* stream);
 
+
+/* out (C,) fp32 += column sums of x (N, C) bf16 (row stride ld): the qkv bias gradient, dqkv summed over tokens
+ * (replaces the autograd of `+ bias` in Qwen2Attention's q/k/v Linear). Deterministic (fixed order). */
+size_t drl_colsum_bf16_workspace_bytes(int64_t N, int64_t C);
+int drl_colsum_bf16_acc(const void* x, int64_t ld, int64_t N, int64_t C, float* out, void* workspace,
+                        size_t workspace_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -374,3 +374,22 @@ def test_decode_attention_vt_split_plans(waves, splits):
         assert (out[0] == 0).all()
     finally:
         lib.drl_decode_attention_set_plan(0, 0)
+
+
+@pytest.mark.parametrize("N,C", [(6144, 1152), (100, 200), (1, 64), (12288, 1152)])
+def test_colsum_bf16_acc(N, C):
+    """qkv bias gradient: column sums of bf16 dqkv accumulated into the fp32 gradient, deterministic."""
+    g = torch.Generator(device=DEV).manual_seed(N + C)
+    x = torch.randn(N, C, device=DEV, generator=g).to(torch.bfloat16)
+    out = torch.randn(C, device=DEV, generator=g)
+    want = out.double() + x.double().sum(0)
+    got = native.colsum_bf16_acc(x, out.clone())
+    assert (got.double() - want).abs().max().item() <= 1e-5 * (x.double().abs().sum(0).max().item() + 1)
+    assert torch.equal(got, native.colsum_bf16_acc(x, out.clone()))
+
+
+def test_transpose16():
+    g = torch.Generator(device=DEV).manual_seed(3)
+    for rows, cols in ((896, 1152), (4864, 896), (100, 37 * 8), (65, 130)):
+        x = torch.randn(rows, cols, device=DEV, generator=g).to(torch.bfloat16)
+        assert torch.equal(native.transpose16(x), x.t().contiguous())
