@@ -112,7 +112,7 @@ SIGNATURES = {
     "drl_value_head_fwd": (ctypes.c_int, [P, I64, P, P, I32, I64, I64, P, I32, P]),
     "drl_value_head_bwd_workspace_bytes": (SZ, [I64, I64]),
     "drl_value_head_bwd": (ctypes.c_int, [P, I64, P, I32, P, I64, I64, P, I64, P, P, P, SZ, P]),
-    "drl_select_tokens_workspace_bytes": (SZ, [I64]),
+    "drl_select_tokens_workspace_bytes": (SZ, [I64, I64]),
     "drl_select_tokens": (ctypes.c_int, [P, I32, I64, I64, I64, ctypes.POINTER(SamplingParams), P, P, I64, P, SZ, P]),
     "drl_response_mask": (ctypes.c_int, [P, I64, I64, I64, P, I32, P, I32, I64, P]),
     "drl_position_ids": (ctypes.c_int, [P, I32, I64, I64, P, P]),
@@ -194,7 +194,7 @@ def load(path: str | None = None):
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
-        if lib.drl_abi_version() != 1:
+        if lib.drl_abi_version() != 2:
             raise NativeLibraryError(f"ABI mismatch: library reports {lib.drl_abi_version()}")
         _lib = lib
     return _lib

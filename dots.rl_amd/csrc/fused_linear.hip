@@ -61,37 +61,14 @@ struct FlArgs {
   const float* ent;
   uint16_t* dlt;      // (V, ld_dl) bf16 d_logits^T
   int64_t ld_dl;
-  // token selection (decode): greedy argmax or the exponential race of the sampling draw over bf16 logits
-  int do_sample;
-  float temp;
-  uint64_t seed, offset;
-  int64_t row_base;
+  // token selection (decode): greedy argmax over the bf16 logits
   const int64_t* dev_step;
   unsigned long long* best;  // (N) packed (key, ~index) running max, zero between calls
 };
 
 constexpr int MODE_LOGPROB = 0, MODE_DLOGITS = 1, MODE_SELECT = 2;
 
-// Philox4x32-10 block and the order-preserving key packing of csrc/vocab.hip (K4; race_key in common.h): the same
-// draw for the same (seed, offset, row, index), so the fused and the unfused selection agree.
-__device__ __forceinline__ uint4 philox4(uint64_t seed, uint64_t offset, uint64_t counter) {
-  uint32_t c0 = static_cast<uint32_t>(counter), c1 = static_cast<uint32_t>(counter >> 32);
-  uint32_t c2 = static_cast<uint32_t>(offset), c3 = static_cast<uint32_t>(offset >> 32);
-  uint32_t k0 = static_cast<uint32_t>(seed), k1 = static_cast<uint32_t>(seed >> 32);
-#pragma unroll
-  for (int i = 0; i < 10; ++i) {
-    const uint64_t p0 = static_cast<uint64_t>(0xD2511F53u) * c0;
-    const uint64_t p1 = static_cast<uint64_t>(0xCD9E8D57u) * c2;
-    const uint32_t n0 = static_cast<uint32_t>(p1 >> 32) ^ c1 ^ k0;
-    const uint32_t n1 = static_cast<uint32_t>(p1);
-    const uint32_t n2 = static_cast<uint32_t>(p0 >> 32) ^ c3 ^ k1;
-    const uint32_t n3 = static_cast<uint32_t>(p0);
-    c0 = n0; c1 = n1; c2 = n2; c3 = n3;
-    k0 += 0x9E3779B9u;
-    k1 += 0xBB67AE85u;
-  }
-  return make_uint4(c0, c1, c2, c3);
-}
+// order-preserving (key, ~index) packing of csrc/vocab.hip: unsigned max == torch.argmax (first index on ties)
 __device__ __forceinline__ uint64_t pack_key(float key, int64_t idx) {
   uint32_t b = __float_as_uint(key);
   b = isnan(key) ? 0xFFFFFFFFu : ((b & 0x80000000u) ? ~b : (b | 0x80000000u));
@@ -171,7 +148,6 @@ __global__ __launch_bounds__(kThreads) void fused_linear_kernel(FlArgs a) {
   int64_t lab[4];
   float m[4], s[4], sz[4];
   uint64_t sel[4] = {0, 0, 0, 0};
-  const uint64_t off = MODE == MODE_SELECT ? a.offset + (a.dev_step ? static_cast<uint64_t>(*a.dev_step) : 0ull) : 0;
   float c_dlp[4], c_den[4], c_lse[4], c_ent[4];
 #pragma unroll
   for (int tb = 0; tb < 4; ++tb) {
@@ -213,24 +189,14 @@ __global__ __launch_bounds__(kThreads) void fused_linear_kernel(FlArgs a) {
       for (int tb = 0; tb < 4; ++tb) {
         const int64_t t = t0 + wt * 128 + tb * 32 + (lane & 31);
         if constexpr (MODE == MODE_SELECT) {
-          // bf16 logits (the lm_head module output), then greedy key = logit or race key = logit / T - log E
-          const uint64_t ctr = static_cast<uint64_t>(a.row_base + t) << 32;
+          // greedy key = the bf16 logit (the lm_head module output)
 #pragma unroll
           for (int vb = 0; vb < 2; ++vb)
 #pragma unroll
-            for (int g4 = 0; g4 < 4; ++g4) {
-              const int64_t v0 = vbase + vrow(vb, 4 * g4, hi);  // 4 consecutive rows, one Philox block
-              uint4 pb = make_uint4(0u, 0u, 0u, 0u);
-              if (a.do_sample) pb = philox4(a.seed, off, ctr | static_cast<uint64_t>(v0 >> 2));
-              const uint32_t bits[4] = {pb.x, pb.y, pb.z, pb.w};
-#pragma unroll
-              for (int j = 0; j < 4; ++j) {
-                const int64_t v = v0 + j;
-                const float x = bf16_to_f32(to_bf16_bits(acc[vb][tb][4 * g4 + j]));
-                const float key = a.do_sample ? race_key(a.temp != 1.f ? x / a.temp : x, bits[j]) : x;
-                const uint64_t pk = pack_key(key, v);
-                if ((!vtail || v < a.V) && pk > sel[tb]) sel[tb] = pk;
-              }
+            for (int i = 0; i < 16; ++i) {
+              const int64_t v = vbase + vrow(vb, i, hi);
+              const uint64_t pk = pack_key(bf16_to_f32(to_bf16_bits(acc[vb][tb][i])), v);
+              if ((!vtail || v < a.V) && pk > sel[tb]) sel[tb] = pk;
             }
         } else if constexpr (!BWD) {
           float mx = -INFINITY;
@@ -500,9 +466,9 @@ int drl_linear_select_tokens(const void* hidden, int64_t ld_h, const void* weigh
                 "bad shape (H % 64 == 0)");
   DRL_CHECK_ARG(aligned16(hidden) && aligned16(weight), "hidden / weight must be 16-byte aligned");
   DRL_CHECK_ARG(p->n_eos == 0 || p->eos_ids != nullptr, "n_eos > 0 but eos_ids is NULL");
-  const bool sample = p->do_sample && p->temperature > 0.f;
-  if (sample && ((p->top_k > 0 && p->top_k < V) || p->top_p < 1.0f))
-    return fail(DRL_ERR_UNSUPPORTED, "top-k / top-p filtering is not implemented in this build");
+  if (p->do_sample && p->temperature > 0.f)
+    return fail(DRL_ERR_UNSUPPORTED, "sampling draws slice masses then races inside one slice of the logits row: "
+                                     "use drl_select_tokens on the lm_head logits");
   if (!workspace || workspace_bytes < drl_linear_select_tokens_workspace_bytes(N) ||
       (reinterpret_cast<uintptr_t>(workspace) & 7u))
     return fail(DRL_ERR_WORKSPACE, "select workspace: need %zu 8-byte aligned bytes, zeroed",
@@ -521,11 +487,6 @@ int drl_linear_select_tokens(const void* hidden, int64_t ld_h, const void* weigh
   a.tiles_per_chunk = pl.tiles_per_chunk;
   a.nchunks = pl.nchunks;
   a.vtiles = pl.vtiles;
-  a.do_sample = sample;
-  a.temp = sample ? p->temperature : 1.f;
-  a.seed = p->seed;
-  a.offset = p->offset;
-  a.row_base = p->row_base;
   a.dev_step = p->dev_step;
   a.best = static_cast<unsigned long long*>(workspace);
   hipStream_t s = static_cast<hipStream_t>(stream);

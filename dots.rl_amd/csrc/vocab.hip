@@ -253,8 +253,15 @@ __device__ __forceinline__ uint4 philox4(uint64_t seed, uint64_t offset, uint64_
   return make_uint4(c0, c1, c2, c3);
 }
 
-// Sampling: race_key (common.h), the exponential race — exactly softmax(z)-distributed and a single
-// max-reduction, so the row splits across workgroups with no scan (the inverse CDF needs a prefix sum).
+// Sampling: the categorical draw as a race of exponential clocks (race_key, common.h), run in two levels.
+// The row is cut into fixed slices of kSlice tokens. Pass 1 reduces every slice to its mass
+// (m_s = max kept logit, l_s = sum over kept tokens of exp((x_i - m_s) / T)); pass 2 races the slices with
+// keys ln(mass_s) - ln(E_s) (one Philox word per slice), then races the tokens of the winning slice only.
+// The min of independent clocks E_i / p_i over a slice is an Exp(mass_s) clock, so this is the flat race's
+// distribution (softmax(z) over the kept tokens) exactly, while the per-token Philox + log work — which made
+// the flat race VALU-bound at ~1.3 TB/s — is spent on kSlice tokens per row instead of V.
+
+constexpr int kSlice = 2048;  // tokens per slice: one wave's stream in pass 1 (32 per lane)
 
 // (key, index) -> one u64 whose unsigned max is torch.argmax: order-preserving key bits (NaN = maximum)
 // in the high word, ~index in the low word (ties -> lowest index)
@@ -266,9 +273,31 @@ __device__ __forceinline__ uint64_t pack_key(float key, int64_t idx) {
 
 __device__ __forceinline__ uint64_t max_u64(uint64_t a, uint64_t b) { return a > b ? a : b; }
 
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint64_t other = (static_cast<uint64_t>(__shfl_xor(static_cast<uint32_t>(v >> 32), o, kWave)) << 32) |
+                           __shfl_xor(static_cast<uint32_t>(v), o, kWave);
+    v = max_u64(v, other);
+  }
+  return v;
+}
+
+// workgroup max; every thread gets the result (LDS slot array owned by the caller's call site)
+__device__ __forceinline__ uint64_t block_max_u64(uint64_t v, uint64_t* s_slot) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  v = wave_max_u64(v);
+  if (lane == 0) s_slot[wave] = v;
+  __syncthreads();
+  v = s_slot[0];
+#pragma unroll
+  for (int w = 1; w < kThreads / kWave; ++w) v = max_u64(v, s_slot[w]);
+  return v;
+}
+
 struct SelectArgs {
   const void* logits;
-  int64_t V, ld, ld_out, chunk;  // chunk: elements per workgroup slice (multiple of 8)
+  int64_t V, ld, ld_out, chunk;  // chunk: elements per workgroup slice of the greedy pass (multiple of 8)
   bool vec;
   int do_sample;
   float temp;
@@ -279,77 +308,150 @@ struct SelectArgs {
   int32_t* unfinished;
   int64_t* out;
   const int64_t* dev_step;
-  unsigned long long* best;  // (N) running max per row; zero on entry, reset to zero by the finish kernel
+  unsigned long long* best;  // (N) greedy running max per row; zero on entry, reset to zero by the finish kernel
   const float* thr;          // (N) top-k / top-p cut on z = logit / T (tokens below it never win), or nullptr
+  float2* mass;              // (N, S) sampling slice masses (m_s, l_s)
+  int64_t S;                 // slices per row, ceil(V / kSlice)
 };
 
-// Slice s of row r: best packed key over [s*chunk, (s+1)*chunk), merged into best[r] with one atomic max.
-template <int DT, bool SAMPLE>
+// Greedy: best packed logit over [blockIdx.x * chunk, ...) of row blockIdx.y, merged into best[r] with one
+// atomic max (a handful of VALU ops per token: HBM-bound).
+template <int DT>
 __global__ __launch_bounds__(kThreads) void select_slice_kernel(SelectArgs a) {
   const int64_t r = blockIdx.y;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x;
   const void* row = static_cast<const typename Elem<DT>::T*>(a.logits) + r * a.ld;
   const int64_t begin = static_cast<int64_t>(blockIdx.x) * a.chunk;
   const int64_t end = begin + a.chunk < a.V ? begin + a.chunk : a.V;
-  const uint64_t off = a.offset + (a.dev_step ? static_cast<uint64_t>(*a.dev_step) : 0ull);
-  const uint64_t ctr_row = static_cast<uint64_t>(a.row_base + r) << 32;
-  const float cut = (SAMPLE && a.thr != nullptr) ? a.thr[r] : -INFINITY;
-  auto key_of = [&](float x, uint32_t bits) -> float {
-    if constexpr (SAMPLE) {
-      const float z = scale_logit<DT>(x, a.temp, a.temp != 1.0f, false);
-      return z >= cut ? race_key(z, bits) : -INFINITY;  // filtered tokens lose to every kept one
-    } else {
-      return x;
-    }
-  };
   uint64_t best = 0;
   int64_t done = begin;
   if (a.vec) {
-    // 8 consecutive elements per lane per step (one 16-B bf16 load / two fp32 loads, two Philox blocks)
     const int64_t vend = begin + (end - begin) / 8 * 8;
     for (int64_t i = begin + 8 * tid; i < vend; i += 8 * kThreads) {
       float v[8];
-      if constexpr (DT == DRL_BF16) {
-        Elem<DT>::load_vec(row, i, v);
-      } else {
-        Elem<DT>::load_vec(row, i, v);
-        Elem<DT>::load_vec(row, i + 4, v + 4);
-      }
-      uint32_t bits[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      if constexpr (SAMPLE) {
-        const uint4 p0 = philox4(a.seed, off, ctr_row | static_cast<uint64_t>(i >> 2));
-        const uint4 p1 = philox4(a.seed, off, ctr_row | static_cast<uint64_t>((i >> 2) + 1));
-        bits[0] = p0.x; bits[1] = p0.y; bits[2] = p0.z; bits[3] = p0.w;
-        bits[4] = p1.x; bits[5] = p1.y; bits[6] = p1.z; bits[7] = p1.w;
-      }
+      Elem<DT>::load_vec(row, i, v);
+      if constexpr (DT == DRL_F32) Elem<DT>::load_vec(row, i + 4, v + 4);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) best = max_u64(best, pack_key(key_of(v[k], bits[k]), i + k));
+      for (int k = 0; k < 8; ++k) best = max_u64(best, pack_key(v[k], i + k));
     }
     done = vend;
   }
-  for (int64_t i = done + tid; i < end; i += kThreads) {
-    uint32_t bits = 0;
-    if constexpr (SAMPLE) {
-      const uint4 p = philox4(a.seed, off, ctr_row | static_cast<uint64_t>(i >> 2));
-      const uint32_t w[4] = {p.x, p.y, p.z, p.w};
-      bits = w[i & 3];
-    }
-    best = max_u64(best, pack_key(key_of(Elem<DT>::get(row, i), bits), i));
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const uint64_t other = (static_cast<uint64_t>(__shfl_xor(static_cast<uint32_t>(best >> 32), o, kWave)) << 32) |
-                           __shfl_xor(static_cast<uint32_t>(best), o, kWave);
-    best = max_u64(best, other);
-  }
+  for (int64_t i = done + tid; i < end; i += kThreads) best = max_u64(best, pack_key(Elem<DT>::get(row, i), i));
   __shared__ uint64_t s_best[kThreads / kWave];
-  if (lane == 0) s_best[wave] = best;
-  __syncthreads();
-  if (tid == 0) {
-#pragma unroll
-    for (int w = 1; w < kThreads / kWave; ++w) best = max_u64(best, s_best[w]);
+  best = block_max_u64(best, s_best);
+  if (tid == 0)
     __hip_atomic_fetch_max(a.best + r, static_cast<unsigned long long>(best), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Sampling pass 1: wave w of workgroup (x, r) reduces slice s = 4x + w of row r to (m_s, l_s) over the kept
+// tokens (z = x / T >= thr[r]); l_s = 0 for a slice with no kept token. 32 tokens per lane held in
+// registers: one max, then one exp2 per token — no Philox, no log.
+template <int DT, bool FILTER>
+__global__ __launch_bounds__(kThreads) void select_mass_kernel(SelectArgs a) {
+  constexpr int kV = Elem<DT>::kVec, kPer = kSlice / kWave;
+  const int64_t r = blockIdx.y;
+  const int lane = threadIdx.x & 63;
+  const int64_t s = static_cast<int64_t>(blockIdx.x) * (kThreads / kWave) + (threadIdx.x >> 6);
+  if (s >= a.S) return;  // no barrier in this kernel
+  const void* row = static_cast<const typename Elem<DT>::T*>(a.logits) + r * a.ld;
+  const int64_t begin = s * kSlice;
+  float v[kPer];
+  if (a.vec && begin + kSlice <= a.V) {
+#pragma unroll
+    for (int j = 0; j < kPer / kV; ++j) Elem<DT>::load_vec(row, begin + (j * kWave + lane) * kV, v + j * kV);
+  } else {
+#pragma unroll
+    for (int j = 0; j < kPer / kV; ++j)
+#pragma unroll
+      for (int k = 0; k < kV; ++k) {
+        const int64_t i = begin + (j * kWave + lane) * kV + k;
+        v[j * kV + k] = i < a.V ? Elem<DT>::get(row, i) : -INFINITY;
+      }
+  }
+  const bool apply_t = a.temp != 1.0f;
+  if constexpr (FILTER) {
+    const float cut = a.thr[r];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) v[k] = scale_logit<DT>(v[k], a.temp, apply_t, false) >= cut ? v[k] : -INFINITY;
+  }
+  float m = v[0];
+#pragma unroll
+  for (int k = 1; k < kPer; ++k) m = fmaxf(m, v[k]);
+  m = wave_max(m);
+  float l = 0.f;
+  if (m != -INFINITY) {
+    const float c = kLog2e / a.temp, mc = m * c;  // exp((x - m) / T) = exp2(x c - m c)
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) l += __builtin_amdgcn_exp2f(fmaf(v[k], c, -mc));
+  }
+  l = wave_sum(l);
+  if (lane == 0) a.mass[r * a.S + s] = make_float2(m, l);
+}
+
+// Sampling pass 2, one workgroup per row: race the slices (key ln(mass_s) - ln(E_s), E_s from Philox word
+// s & 3 of counter (row << 32 | 2^31 | s >> 2) — disjoint from the token counters i >> 2 < 2^30), then race
+// the kept tokens of the winning slice (token keys z_i - ln(E_i) on counter (row << 32 | i >> 2), word i & 3),
+// then the finished-row / eos bookkeeping of select_finish_kernel.
+template <int DT, bool FILTER>
+__global__ __launch_bounds__(kThreads) void select_pick_kernel(SelectArgs a) {
+  const int64_t r = blockIdx.x;
+  const int tid = threadIdx.x;
+  const uint64_t off = a.offset + (a.dev_step ? static_cast<uint64_t>(*a.dev_step) : 0ull);
+  const uint64_t ctr_row = static_cast<uint64_t>(a.row_base + r) << 32;
+  const bool apply_t = a.temp != 1.0f;
+  __shared__ uint64_t s_slot[2][kThreads / kWave];
+  uint64_t best = 0;
+  for (int64_t s = tid; s < a.S; s += kThreads) {
+    const float2 ms = a.mass[r * a.S + s];
+    float key = -INFINITY;
+    if (!(ms.y <= 0.f)) {  // NaN mass races (and wins) like a NaN token in the flat race
+      const uint4 p = philox4(a.seed, off, ctr_row | 0x80000000ull | static_cast<uint64_t>(s >> 2));
+      const uint32_t w[4] = {p.x, p.y, p.z, p.w};
+      const float lnmass = scale_logit<DT>(ms.x, a.temp, apply_t, false) + 0.6931471805599453f * __builtin_amdgcn_logf(ms.y);
+      key = race_key(lnmass, w[s & 3]);
+    }
+    best = max_u64(best, pack_key(key, s));
+  }
+  best = block_max_u64(best, s_slot[0]);
+  const int64_t win = static_cast<int64_t>(0xFFFFFFFFu - static_cast<uint32_t>(best));
+  const void* row = static_cast<const typename Elem<DT>::T*>(a.logits) + r * a.ld;
+  const float cut = FILTER ? a.thr[r] : -INFINITY;
+  auto key_of = [&](float x, uint32_t bits) -> float {
+    const float z = scale_logit<DT>(x, a.temp, apply_t, false);
+    return (!FILTER || z >= cut) ? race_key(z, bits) : -INFINITY;
+  };
+  const int64_t begin = win * kSlice;
+  const int64_t end = begin + kSlice < a.V ? begin + kSlice : a.V;
+  best = 0;
+  static_assert(kSlice == 8 * kThreads, "one 8-token group per thread");
+  if (a.vec && end - begin == kSlice) {
+    const int64_t i = begin + 8 * tid;
+    float v[8];
+    Elem<DT>::load_vec(row, i, v);
+    if constexpr (DT == DRL_F32) Elem<DT>::load_vec(row, i + 4, v + 4);
+    const uint4 p0 = philox4(a.seed, off, ctr_row | static_cast<uint64_t>(i >> 2));
+    const uint4 p1 = philox4(a.seed, off, ctr_row | static_cast<uint64_t>((i >> 2) + 1));
+    const uint32_t bits[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) best = max_u64(best, pack_key(key_of(v[k], bits[k]), i + k));
+  } else {
+    for (int64_t i = begin + tid; i < end; i += kThreads) {
+      const uint4 p = philox4(a.seed, off, ctr_row | static_cast<uint64_t>(i >> 2));
+      const uint32_t w[4] = {p.x, p.y, p.z, p.w};
+      best = max_u64(best, pack_key(key_of(Elem<DT>::get(row, i), w[i & 3]), i));
+    }
+  }
+  best = block_max_u64(best, s_slot[1]);
+  if (tid == 0) {
+    const int64_t choice = static_cast<int64_t>(0xFFFFFFFFu - static_cast<uint32_t>(best));
+    const bool alive = a.unfinished ? a.unfinished[r] != 0 : true;
+    const int64_t tok = alive ? choice : a.pad;
+    a.out[r * a.ld_out + (a.dev_step ? *a.dev_step : 0)] = tok;
+    if (a.unfinished && alive) {
+      for (int k = 0; k < a.n_eos; ++k)
+        if (tok == a.eos[k]) { a.unfinished[r] = 0; break; }
+    }
   }
 }
 
@@ -527,8 +629,12 @@ int drl_logprob_entropy_bwd(const void* logits, int32_t dt, int64_t N, int64_t V
   return DRL_OK;
 }
 
-// best (N x u64) + the top-k / top-p cut (N x f32)
-size_t drl_select_tokens_workspace_bytes(int64_t N) { return N > 0 ? static_cast<size_t>(N) * 12 : 0; }
+// best (N x u64) + the top-k / top-p cut (N x f32, padded to 8 B) + the sampling slice masses (N x S x float2)
+size_t drl_select_tokens_workspace_bytes(int64_t N, int64_t V) {
+  if (N <= 0 || V <= 0) return 0;
+  const int64_t S = (V + drl::kSlice - 1) / drl::kSlice;
+  return static_cast<size_t>(N) * 16 + static_cast<size_t>(N) * static_cast<size_t>(S) * 8;
+}
 
 int drl_select_tokens(const void* logits, int32_t dt, int64_t N, int64_t V, int64_t ld,
                       const drl_sampling_params* p, int32_t* unfinished, int64_t* out_tokens, int64_t ld_out,
@@ -543,8 +649,8 @@ int drl_select_tokens(const void* logits, int32_t dt, int64_t N, int64_t V, int6
   DRL_CHECK_ARG(!sample || (p->top_p > 0.f && p->top_p <= 1.0f), "top_p must be in (0, 1], got %f", p->top_p);
   if (N == 0) return DRL_OK;
   DRL_CHECK_ARG(N <= 65535, "too many rows for one launch");
-  if (!workspace || workspace_bytes < drl_select_tokens_workspace_bytes(N) || (reinterpret_cast<uintptr_t>(workspace) & 7u))
-    return fail(DRL_ERR_WORKSPACE, "select workspace: need %zu 8-byte aligned bytes", drl_select_tokens_workspace_bytes(N));
+  if (!workspace || workspace_bytes < drl_select_tokens_workspace_bytes(N, V) || (reinterpret_cast<uintptr_t>(workspace) & 7u))
+    return fail(DRL_ERR_WORKSPACE, "select workspace: need %zu 8-byte aligned bytes", drl_select_tokens_workspace_bytes(N, V));
   SelectArgs a{};
   a.logits = logits; a.V = V; a.ld = ld; a.ld_out = ld_out; a.vec = rows_aligned(logits, ld, dt);
   a.do_sample = sample; a.temp = sample ? p->temperature : 1.0f;
@@ -553,6 +659,8 @@ int drl_select_tokens(const void* logits, int32_t dt, int64_t N, int64_t V, int6
   a.dev_step = p->dev_step;
   a.best = static_cast<unsigned long long*>(workspace);
   a.thr = filter ? reinterpret_cast<const float*>(static_cast<char*>(workspace) + static_cast<size_t>(N) * 8) : nullptr;
+  a.S = (V + kSlice - 1) / kSlice;
+  a.mass = reinterpret_cast<float2*>(static_cast<char*>(workspace) + static_cast<size_t>(N) * 16);
   // slices per row: ~4 workgroups per CU over the whole launch, >= 2048 elements per slice
   const int64_t want = (4 * static_cast<int64_t>(cu_count()) + N - 1) / N;
   const int64_t max_slices = (V + 2047) / 2048;
@@ -570,13 +678,23 @@ int drl_select_tokens(const void* logits, int32_t dt, int64_t N, int64_t V, int6
                          p->top_p);
     DRL_LAUNCH_CHECK();
   }
-  if (dt == DRL_BF16) {
-    if (sample) hipLaunchKernelGGL((select_slice_kernel<DRL_BF16, true>), grid, dim3(kThreads), 0, s, a);
-    else hipLaunchKernelGGL((select_slice_kernel<DRL_BF16, false>), grid, dim3(kThreads), 0, s, a);
-  } else {
-    if (sample) hipLaunchKernelGGL((select_slice_kernel<DRL_F32, true>), grid, dim3(kThreads), 0, s, a);
-    else hipLaunchKernelGGL((select_slice_kernel<DRL_F32, false>), grid, dim3(kThreads), 0, s, a);
+  if (sample) {
+    const dim3 g1(static_cast<unsigned>((a.S + kThreads / kWave - 1) / (kThreads / kWave)), static_cast<unsigned>(N));
+    const dim3 g2(static_cast<unsigned>(N));
+#define DRL_SAMPLE(DT, F)                                                                   \
+  do {                                                                                      \
+    hipLaunchKernelGGL((select_mass_kernel<DT, F>), g1, dim3(kThreads), 0, s, a);           \
+    DRL_LAUNCH_CHECK();                                                                     \
+    hipLaunchKernelGGL((select_pick_kernel<DT, F>), g2, dim3(kThreads), 0, s, a);           \
+  } while (0)
+    if (dt == DRL_BF16) { if (filter) DRL_SAMPLE(DRL_BF16, true); else DRL_SAMPLE(DRL_BF16, false); }
+    else { if (filter) DRL_SAMPLE(DRL_F32, true); else DRL_SAMPLE(DRL_F32, false); }
+#undef DRL_SAMPLE
+    DRL_LAUNCH_CHECK();
+    return DRL_OK;
   }
+  if (dt == DRL_BF16) hipLaunchKernelGGL((select_slice_kernel<DRL_BF16>), grid, dim3(kThreads), 0, s, a);
+  else hipLaunchKernelGGL((select_slice_kernel<DRL_F32>), grid, dim3(kThreads), 0, s, a);
   DRL_LAUNCH_CHECK();
   hipLaunchKernelGGL(select_finish_kernel, dim3(static_cast<unsigned>((N + kThreads - 1) / kThreads)), dim3(kThreads), 0,
                      s, a, N);

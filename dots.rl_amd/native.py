@@ -431,7 +431,8 @@ def select_tokens(logits, out_tokens, *, do_sample=False, temperature=1.0, top_k
     N, V = lg.shape
     assert out_tokens.dtype == torch.int64 and out_tokens.numel() == N
     ld_out = out_tokens.stride(0) if out_tokens.dim() == 1 else 1
-    ws = _select_workspace(lg.device, (3 * N + 1) // 2)  # N u64 running maxima + N f32 top-k / top-p cuts
+    # N u64 greedy maxima + N f32 top-k / top-p cuts + (N, ceil(V / 2048)) sampling slice masses
+    ws = _select_workspace(lg.device, (lib().drl_select_tokens_workspace_bytes(N, V) + 7) // 8)
     prm = _lib.SamplingParams(int(bool(do_sample)), float(temperature), int(top_k), float(top_p),
                               int(seed) & 0xFFFFFFFFFFFFFFFF, int(step), int(row_base), int(pad_token_id),
                               None if eos_ids is None else eos_ids.data_ptr(),

@@ -637,10 +637,9 @@ class Qwen2Model:
     def select_tokens(self, h, out_tokens, fused=True, **sel):
         """Token selection from the final-norm hidden h (N, H): K4 fused with the lm_head on bf16 (the (N, V)
         logits are never written, csrc/fused_linear.hip), else lm_head logits + K4 (fp32 parity model, and
-        top-k / top-p sampling, whose per-row cut needs the logits row)."""
+        sampling: the slice race and the top-k / top-p cut read the logits row)."""
         w = self.store.w(self.lm_head_weight())
-        filtered = sel.get("do_sample") and (0 < sel.get("top_k", 0) < self.cfg.vocab_size or sel.get("top_p", 1.0) < 1.0)
-        if fused and not filtered and self.dtype == torch.bfloat16 and h.shape[-1] % 64 == 0:
+        if fused and not sel.get("do_sample") and self.dtype == torch.bfloat16 and h.shape[-1] % 64 == 0:
             return native.linear_select_tokens(h.contiguous(), w, out_tokens, **sel)
         return native.select_tokens(self.logits(h), out_tokens, **sel)
 

@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define DRL_ABI_VERSION 1
+#define DRL_ABI_VERSION 2
 
 #define DRL_OK 0
 #define DRL_ERR_INVALID (-1)     /* bad argument (shape, dtype, null pointer, alignment) */
@@ -236,22 +236,25 @@ int drl_value_head_bwd(const void* hidden, int64_t ld_h, const void* weight, int
 
 /* ------------------------------------------------------------------------------------------------
  * K4 — decode-step token selection over the vocabulary (HF generate semantics that HFRollout
- * delegates to, verl/workers/rollout/hf_rollout.py:112-124). Two launches per decode step (row slices
- * across workgroups, then one thread per row).
+ * delegates to, verl/workers/rollout/hf_rollout.py:112-124). Two launches per decode step.
  * logits (N, V) F32/BF16 (row stride ld). unfinished (N) int32 in/out: rows already finished emit
  * pad_token_id (HF: next = next*unfinished + pad*(1-unfinished)) and a row hitting any eos id
  * becomes finished. The chosen token is written to out_tokens[n*ld_out] (int64) — pass a column
  * of the `responses` tensor to fill it in place. temperature <= 0 or do_sample == 0 -> greedy
- * (argmax, first index on ties = torch.argmax). Sampling: z = logit / temperature (fp32, HF
- * TemperatureLogitsWarper), then top-k (top_k > 0: tokens below the k-th largest z dropped, ties kept, HF
- * TopKLogitsWarper) and top-p (top_p < 1: the nucleus of HF TopPLogitsWarper over the top-k survivors — a
- * token is kept iff the softmax mass of the tokens above it is < top_p; ties at the cut kept) as one cut per
- * row (a third launch, one workgroup per row, deterministic radix select), then the categorical
- * draw as a race of exponential clocks over the kept tokens: argmax_i z_i - log(E_i), E_i = -log(1 - v_i), v_i the 24-bit
- * uniform ((w >> 8) + 0.5) / 2^24 from word (i & 3) of Philox4x32-10(key = seed,
- * counter = ((row_base + n) << 32 | i >> 2, offset = decode step)) — softmax(z)-distributed like HF's
- * torch.multinomial. workspace: drl_select_tokens_workspace_bytes(N) bytes, 8-byte aligned, zero-filled
- * before the first call; every call leaves it zeroed again (one in-flight call per workspace).
+ * (argmax, first index on ties = torch.argmax; row slices across workgroups, then one thread per row).
+ * Sampling: z = logit / temperature (fp32, HF TemperatureLogitsWarper), then top-k (top_k > 0: tokens
+ * below the k-th largest z dropped, ties kept, HF TopKLogitsWarper) and top-p (top_p < 1: the nucleus of
+ * HF TopPLogitsWarper over the top-k survivors — a token is kept iff the softmax mass of the tokens above
+ * it is < top_p; ties at the cut kept) as one cut per row (a third launch, one workgroup per row,
+ * deterministic radix select), then the categorical draw over the kept tokens as a two-level race of
+ * exponential clocks — softmax(z)-distributed like HF's torch.multinomial (whose one-sample path is the
+ * same race, argmax p_i / E_i): the row is cut into slices of 2048 tokens; slice s races with key
+ * ln(sum_{kept i in s} exp z_i) - ln(E_s), then the tokens i of the winning slice race with key
+ * z_i - ln(E_i). E = -ln(1 - v), v = ((w >> 8) + 0.5) / 2^24, w = word (c & 3) of Philox4x32-10(key = seed,
+ * counter = ((row_base + n) << 32 | c >> 2), offset = decode step) with c = i for tokens and
+ * c = 2^33 + s for slices (counter low word 2^31 | s >> 2).
+ * workspace: drl_select_tokens_workspace_bytes(N, V) bytes, 8-byte aligned, zero-filled before the first
+ * call; every call leaves its greedy maxima zeroed again (one in-flight call per workspace).
  * ---------------------------------------------------------------------------------------------- */
 typedef struct drl_sampling_params {
   int32_t do_sample;
@@ -269,7 +272,7 @@ typedef struct drl_sampling_params {
   const int64_t* dev_step;
 } drl_sampling_params;
 
-size_t drl_select_tokens_workspace_bytes(int64_t N);
+size_t drl_select_tokens_workspace_bytes(int64_t N, int64_t V);
 int drl_select_tokens(const void* logits, int32_t logits_dtype, int64_t N, int64_t V, int64_t ld,
                       const drl_sampling_params* params, int32_t* unfinished, int64_t* out_tokens,
                       int64_t ld_out, void* workspace, size_t workspace_bytes, void* stream);
@@ -442,8 +445,8 @@ int drl_linear_logprob_dlogits(const void* hidden, int64_t ld_h, const void* wei
 
 /* K4 fused with the lm_head (decode): token selection straight from hidden (N, ld_h) bf16 and the lm_head
  * weight (V, H) bf16 without writing the (N, V) logits — drl_select_tokens' semantics on the bf16 logits
- * bf16(hidden W^T) (greedy argmax, lowest index on ties; or the exponential race with the same Philox draw),
- * the same params / unfinished / EOS bookkeeping. workspace: drl_linear_select_tokens_workspace_bytes(N)
+ * bf16(hidden W^T), greedy only (argmax, lowest index on ties; do_sample returns DRL_ERR_UNSUPPORTED: the
+ * two-level draw races inside one slice of the logits row), the same params / unfinished / EOS bookkeeping. workspace: drl_linear_select_tokens_workspace_bytes(N)
  * bytes, 8-byte aligned, zero-filled before the first call and left zeroed by every call. H % 64 == 0. */
 size_t drl_linear_select_tokens_workspace_bytes(int64_t N);
 int drl_linear_select_tokens(const void* hidden, int64_t ld_h, const void* weight, int32_t dt, int64_t N, int64_t H,

@@ -449,12 +449,13 @@ def philox4(seed, offset, counter):
     return c
 
 
-def philox_words(seed, offset, row, V):
-    """Word (i & 3) of block (row << 32 | i >> 2) for i < V (vectorised over the blocks)."""
+def philox_blocks(seed, offset, row, c0):
+    """Philox4x32-10 blocks (key = seed; counter (c0, row), offset words (c2, c3)) for an array of counter low
+    words c0 -> (len(c0), 4) uint32 (vectorised philox4)."""
     M0, M1, W0, W1 = np.uint64(0xD2511F53), np.uint64(0xCD9E8D57), 0x9E3779B9, 0xBB67AE85
     mask = np.uint64(0xFFFFFFFF)
-    nb = (V + 3) // 4
-    c0 = np.arange(nb, dtype=np.uint64)
+    c0 = np.asarray(c0, np.uint64)
+    nb = c0.shape[0]
     c1 = np.full(nb, row & 0xFFFFFFFF, np.uint64)
     c2 = np.full(nb, offset & 0xFFFFFFFF, np.uint64)
     c3 = np.full(nb, (offset >> 32) & 0xFFFFFFFF, np.uint64)
@@ -466,23 +467,55 @@ def philox_words(seed, offset, row, V):
             ((p0 >> np.uint64(32)) ^ c3 ^ np.uint64(k1)) & mask, p0 & mask
         k0 = (k0 + W0) & 0xFFFFFFFF
         k1 = (k1 + W1) & 0xFFFFFFFF
-    return np.stack([c0, c1, c2, c3], 1).reshape(-1)[:V].astype(np.uint32)
+    return np.stack([c0, c1, c2, c3], 1).astype(np.uint32)
+
+
+def philox_words(seed, offset, row, V):
+    """Word (i & 3) of block (row << 32 | i >> 2) for i < V (vectorised over the blocks)."""
+    return philox_blocks(seed, offset, row, np.arange((V + 3) // 4, dtype=np.uint64)).reshape(-1)[:V]
+
+
+def _log_clock(w):
+    """ln(E) for E = -ln(1 - v) ~ Exp(1), v = ((w >> 8) + 0.5) / 2^24 (float32 uniform, as the HIP sampler)."""
+    v = ((w >> np.uint32(8)).astype(np.float32) + np.float32(0.5)) * np.float32(1.0 / 16777216.0)
+    return np.log(-np.log1p(-v))
 
 
 def race_keys(z, seed, offset, row):
     """z_i - log(E_i), E_i = -log(1 - v_i) ~ Exp(1), v_i = ((w_i >> 8) + 0.5) / 2^24 (float32 math, as the
     HIP sampler); the argmax is a softmax(z) draw (exponential race / Gumbel-max)."""
     w = philox_words(seed, offset, row, z.shape[0])
-    v = ((w >> np.uint32(8)).astype(np.float32) + np.float32(0.5)) * np.float32(1.0 / 16777216.0)
-    e = -np.log1p(-v)
-    return np.asarray(z, np.float32) - np.log(e)
+    return np.asarray(z, np.float32) - _log_clock(w).astype(np.float32)
 
 
-def sample_row(logits, temperature, top_k, top_p, seed, offset, row):
+SELECT_SLICE = 2048  # tokens per slice of the two-level race (csrc/vocab.hip kSlice)
+
+
+def slice_race_keys(z, keep, seed, offset, row):
+    """Level 1 of the two-level race: slice s (tokens [2048 s, 2048 (s + 1))) has key
+    ln(sum_{kept i in s} exp z_i) - ln(E_s), E_s from word (s & 3) of Philox block (row << 32 | 2^31 | s >> 2);
+    -inf for a slice without kept tokens. float64 masses (the kernel sums float32 in a fixed order)."""
+    z = np.asarray(z, np.float64)
+    V = z.shape[0]
+    S = -(-V // SELECT_SLICE)
+    zz = np.full(S * SELECT_SLICE, -np.inf)
+    zz[:V] = np.where(keep, z, -np.inf)
+    zz = zz.reshape(S, SELECT_SLICE)
+    m = zz.max(1)
+    fin = np.isfinite(m)
+    lnmass = np.full(S, -np.inf)
+    lnmass[fin] = m[fin] + np.log(np.exp(zz[fin] - m[fin, None]).sum(1))
+    w = philox_blocks(seed, offset, row, (1 << 31) + np.arange((S + 3) // 4, dtype=np.uint64)).reshape(-1)[:S]
+    return lnmass - _log_clock(w)
+
+
+def sample_row(logits, temperature, top_k, top_p, seed, offset, row, return_keys=False):
     """Reference semantics of one sampling step: temperature -> top-k -> top-p -> categorical draw.
 
-    The draw is the exponential race over the kept tokens with the HIP sampler's Philox stream
-    (race_keys), so HIP and oracle pick the same token; HF uses torch.multinomial (same distribution)."""
+    The draw is the HIP sampler's two-level exponential race over the kept tokens (slice_race_keys picks the
+    slice, race_keys the token inside it; same Philox stream), so HIP and oracle pick the same token. HF uses
+    torch.multinomial, whose one-sample path is the flat race argmax p_i / E_i: the same distribution (the
+    first-arriving clock of a slice is an Exp(slice mass) clock)."""
     z = np.asarray(logits, np.float32).astype(f64) / temperature
     V = z.shape[0]
     keep = np.ones(V, bool)
@@ -503,9 +536,14 @@ def sample_row(logits, temperature, top_k, top_p, seed, offset, row):
         keep2[order[drop]] = False
         p = np.where(keep2, p, 0.0)
         p /= p.sum()
-    keys = race_keys((np.asarray(logits, np.float32) / np.float32(temperature)).astype(np.float32), seed, offset, row)
-    keys = np.where(p > 0, keys, -np.inf)
-    return int(np.argmax(keys))
+    z32 = (np.asarray(logits, np.float32) / np.float32(temperature)).astype(np.float32)
+    kept = p > 0
+    skeys = slice_race_keys(z32, kept, seed, offset, row)
+    s = int(np.argmax(skeys))
+    keys = np.where(kept, race_keys(z32, seed, offset, row), -np.inf)
+    lo, hi = s * SELECT_SLICE, min(V, (s + 1) * SELECT_SLICE)
+    tok = lo + int(np.argmax(keys[lo:hi]))
+    return (tok, skeys, keys) if return_keys else tok
 
 
 # ------------------------------------------------------------------------------------ A15 clip + AdamW

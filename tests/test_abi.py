@@ -47,7 +47,7 @@ def test_python_binding_signatures_cover_the_header(built_lib):
 
     assert set(_lib.SIGNATURES) == set(declared_functions())
     lib = _lib.load(built_lib)
-    assert lib.drl_abi_version() == 1
+    assert lib.drl_abi_version() == 2
 
 
 def test_library_is_gfx950_code(built_lib):

@@ -268,14 +268,18 @@ def test_decode_qkv_rope_matches_gemm_then_rope(M, K, Hq, Hkv, D):
 
 
 @pytest.mark.parametrize("N,H,V", [(64, 896, 151936), (300, 128, 5003), (1, 64, 257)])
-@pytest.mark.parametrize("sample", [False, True])
-def test_linear_select_matches_unfused(N, H, V, sample):
-    """lm_head fused with K4 (no logits written) against K4 on the bf16 logits of the same GEMM: the same token
-    wherever the fp32 sums round to the same bf16 logits (>= 99 % of rows; a differing row must be a
-    near-tie: its pick is within one bf16 ulp of the unfused pick's logit)."""
+def test_linear_select_matches_unfused(N, H, V):
+    """lm_head fused with greedy K4 (no logits written) against K4 on the bf16 logits of the same GEMM: the same
+    token wherever the fp32 sums round to the same bf16 logits (>= 99 % of rows; a differing row must be a
+    near-tie: its pick is within one bf16 ulp of the unfused pick's logit). Sampling is refused (the two-level
+    race reads one slice of the logits row)."""
     h = rnd(N, H, seed=N)
     w = rnd(V, H, scale=0.05, seed=V)
-    kw = dict(do_sample=sample, temperature=0.8 if sample else 1.0, seed=1234, step=3, row_base=5)
+    with pytest.raises(RuntimeError, match="drl_select_tokens"):
+        native.linear_select_tokens(h, w, torch.empty(N, dtype=torch.int64, device=DEV), do_sample=True,
+                                    temperature=0.8)
+    sample = False
+    kw = dict(do_sample=sample, temperature=1.0, seed=1234, step=3, row_base=5)
     a = native.linear_select_tokens(h, w, torch.empty(N, dtype=torch.int64, device=DEV), **kw)
     logits = h @ w.t()
     b = native.select_tokens(logits, torch.empty(N, dtype=torch.int64, device=DEV), **kw)
