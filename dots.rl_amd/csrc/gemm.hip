@@ -226,14 +226,14 @@ int launch(GemmArgs& g, int epi, hipStream_t s) {
   return DRL_OK;
 }
 
-int g_gemm_tile = 0;  // tuning: 0 = automatic, 1..5 = the configurations of drl_gemm_bf16_nt
+int g_gemm_tile = 0;  // tuning: 0 = automatic, 1..8 = the configurations of drl_gemm_bf16_nt
 
 }  // namespace
 }  // namespace drl
 
 extern "C" {
 
-void drl_gemm_set_tile(int32_t tile) { drl::g_gemm_tile = (tile >= 0 && tile <= 5) ? tile : 0; }
+void drl_gemm_set_tile(int32_t tile) { drl::g_gemm_tile = (tile >= 0 && tile <= 8) ? tile : 0; }
 
 int drl_gemm_bf16_nt(const void* a, int64_t lda, const void* b, int64_t ldb, void* c, int64_t ldc, int64_t M,
                      int64_t N, int64_t K, const void* bias, int32_t epilogue, void* c2, int64_t ldc2, void* stream) {
@@ -270,6 +270,11 @@ int drl_gemm_bf16_nt(const void* a, int64_t lda, const void* b, int64_t ldb, voi
     case 2: return launch<128, 128, 64, 3, 4, 2>(g, epi, s);
     case 3: return launch<256, 128, 32, 3, 4, 2>(g, epi, s);
     case 4: return launch<128, 128, 32, 3, 4, 2>(g, epi, s);
+    // 256 x 256, 2 x 4 waves of 128 x 64 (6 fragment reads per 8 MFMAs: half the LDS traffic per FLOP of the
+    // 64 x 64 wave tiles above), 128 / 128 / 96 KB of LDS
+    case 6: return launch<256, 256, 64, 2, 2, 4>(g, epi, s);
+    case 7: return launch<256, 256, 32, 4, 2, 4>(g, epi, s);
+    case 8: return launch<256, 256, 32, 3, 2, 4>(g, epi, s);
     default: return launch<128, 128, 64, 2, 4, 2>(g, epi, s);
   }
 }
