@@ -158,6 +158,53 @@ def compute_reinforce_plus_plus_baseline_outcome_advantage(token_level_rewards, 
                                               row_group, offsets, members, G)
 
 
+@register_adv_est(AdvantageEstimator.GRPO_PASSK)
+def compute_grpo_passk_outcome_advantage(token_level_rewards, response_mask, index, epsilon: float = 1e-6,
+                                         norm_adv_by_std_in_grpo: bool = True, config=None, **kwargs):
+    """core_algos.py:327-386 — only the best sample of a uid group gets r_max - r_second_max (/ (std + eps)); K3
+    pass@k mode. Groups of one sample raise, as the reference does."""
+    assert config is not None
+    norm = config.get("norm_adv_by_std_in_grpo", True)
+    counts = {}
+    for u in index:
+        counts[u] = counts.get(u, 0) + 1
+    for u, c in counts.items():
+        if c < 2:
+            raise ValueError(f"Pass@k requires at least 2 samples per group. Got {c} for group {u}.")
+    row_group, offsets, members, G = uid_csr(index, token_level_rewards.device)
+    with torch.no_grad():
+        return native.group_outcome_advantage("grpo_passk", token_level_rewards, response_mask, row_group, offsets,
+                                              members, G, epsilon, norm)
+
+
+@register_adv_est(AdvantageEstimator.OPO)
+def compute_opo_outcome_advantage(token_level_rewards, response_mask, index, epsilon: float = 1e-6, config=None,
+                                  **kwargs):
+    """core_algos.py:495-546 — score minus the length-weighted group mean (sum(len * s) / sum(len)); K3 OPO mode."""
+    row_group, offsets, members, G = uid_csr(index, token_level_rewards.device)
+    with torch.no_grad():
+        return native.group_outcome_advantage("opo", token_level_rewards, response_mask, row_group, offsets, members, G)
+
+
+@register_adv_est(AdvantageEstimator.GPG)
+def compute_gpg_outcome_advantage(token_level_rewards, response_mask, index, epsilon: float = 1e-6, f_norm: float = 1.0,
+                                  alpha: float = 1.0, config=None, **kwargs):
+    """core_algos.py:624-684 — alpha * (s - group mean) / f_norm with alpha = B / max(#nonzero scores, 1) (the
+    reference recomputes alpha and ignores the argument; f_norm = 1 as every caller passes); K3 GPG mode."""
+    if f_norm != 1.0:
+        raise NotImplementedError("GPG advantage with f_norm != 1")
+    row_group, offsets, members, G = uid_csr(index, token_level_rewards.device)
+    with torch.no_grad():
+        return native.group_outcome_advantage("gpg", token_level_rewards, response_mask, row_group, offsets, members, G)
+
+
+@register_adv_est(AdvantageEstimator.REMAX)
+def compute_remax_outcome_advantage(token_level_rewards, reward_baselines, response_mask, config=None, **kwargs):
+    """core_algos.py:588-621 — reverse cumsum of the masked rewards minus the greedy-rollout baseline score."""
+    with torch.no_grad():
+        return native.remax_advantage_return(token_level_rewards, reward_baselines, response_mask)
+
+
 @register_adv_est(AdvantageEstimator.REINFORCE_PLUS_PLUS)
 def compute_reinforce_plus_plus_outcome_advantage(token_level_rewards, response_mask, config=None, **kwargs):
     """core_algos.py:550-586 — masked discounted return scan + masked_whiten (K5 scan mode)."""

@@ -312,12 +312,13 @@ def grpo_outcome_advantage(token_level_rewards, response_mask, row_group, group_
     return adv, ret
 
 
-_GROUP_ESTIMATORS = {"grpo": 0, "rloo": 1, "reinforce_plus_plus_baseline": 2}
+_GROUP_ESTIMATORS = {"grpo": 0, "rloo": 1, "reinforce_plus_plus_baseline": 2, "opo": 3, "gpg": 4, "grpo_passk": 5}
 
 
 def group_outcome_advantage(estimator, token_level_rewards, response_mask, row_group, group_offsets, group_members, G,
                             epsilon=1e-6, norm_adv_by_std_in_grpo=True):
-    """K3 over the uid-group CSR for GRPO / RLOO / REINFORCE++-baseline (drl_group_outcome_advantage)."""
+    """K3 over the uid-group CSR for GRPO / RLOO / REINFORCE++-baseline / OPO / GPG / GRPO pass@k
+    (drl_group_outcome_advantage)."""
     _dev(token_level_rewards, response_mask, row_group, group_offsets, group_members)
     r, m = _c(token_level_rewards.float()), _c(response_mask)
     B, R = r.shape
@@ -328,6 +329,19 @@ def group_outcome_advantage(estimator, token_level_rewards, response_mask, row_g
                                         _p(_c(group_members)), B, R, G, _GROUP_ESTIMATORS[estimator], float(epsilon),
                                         int(bool(norm_adv_by_std_in_grpo)), _p(adv), _p(ret), _p(ws), ws.numel(),
                                         _stream()), "drl_group_outcome_advantage")
+    return adv, ret
+
+
+def remax_advantage_return(token_level_rewards, reward_baselines, response_mask):
+    """ReMax: reverse cumsum of masked rewards minus the greedy baseline (drl_remax_advantage_return)."""
+    _dev(token_level_rewards, reward_baselines, response_mask)
+    r, m = _c(token_level_rewards.float()), _c(response_mask)
+    bl = _c(reward_baselines.float().reshape(-1))
+    B, R = r.shape
+    assert bl.numel() == B
+    adv, ret = torch.empty_like(r), torch.empty_like(r)
+    check(lib().drl_remax_advantage_return(_p(r), _p(bl), _p(m), mask_dtype_code(m), B, R, _p(adv), _p(ret), _stream()),
+          "drl_remax_advantage_return")
     return adv, ret
 
 

@@ -76,6 +76,8 @@ def compute_advantage(data: DataProto, adv_estimator, gamma=1.0, lam=1.0, num_re
               "config": config}
         if "uid" in data.non_tensor_batch:
             kw["index"] = data.non_tensor_batch["uid"]
+        if "reward_baselines" in data.batch:
+            kw["reward_baselines"] = data.batch["reward_baselines"]
         adv, ret = fn(**kw)
     data.batch["advantages"] = adv
     data.batch["returns"] = ret
@@ -178,11 +180,27 @@ class RayPPOTrainer:
         gen_batch = batch.pop(batch_keys=["input_ids", "attention_mask", "position_ids"])
         gen_batch.meta_info.update({"global_steps": self.global_steps, "eos_token_id": self.eos_token_id,
                                     "pad_token_id": self.pad_token_id})
+        base_batch = gen_batch
         gen_batch = gen_batch.repeat(repeat_times=ar.rollout.n, interleave=True)
         with marked_timer("gen", timing_raw):
             gen_out = self.actor_rollout_wg.generate_sequences(gen_batch)
             for k, v in gen_out.meta_info.pop("timing", {}).items():
                 timing_raw[k] = timing_raw.get(k, 0.0) + v
+        if str(getattr(self.config.algorithm.adv_estimator, "value", self.config.algorithm.adv_estimator)) == "remax":
+            # ray_trainer.py:1160-1180: one greedy response per prompt, scored by the reward function; its sum is the
+            # prompt's baseline, repeated with the batch below
+            if self.reward_fn is None:
+                raise ValueError("A reward_fn is required for REMAX advantage estimation.")
+            with marked_timer("gen_max", timing_raw):
+                base_batch.meta_info["do_sample"] = False
+                base_out = self.actor_rollout_wg.generate_sequences(base_batch)
+                base_out.meta_info.pop("timing", None)
+                batch = batch.union(base_out)  # in place, as the reference's
+                rb = self.reward_fn(batch)
+                rb = rb["reward_tensor"] if isinstance(rb, dict) else rb
+                batch.pop(batch_keys=list(base_out.batch.keys()))
+                batch.batch["reward_baselines"] = rb.sum(dim=-1)
+                del base_out
         batch = batch.repeat(repeat_times=ar.rollout.n, interleave=True)
         return batch.union(gen_out)
 

@@ -165,8 +165,16 @@ int drl_grpo_outcome_advantage(const float* token_level_rewards, const void* res
  * DRL_ADV_RLOO = compute_rloo_outcome_advantage (core_algos.py:444-493),
  * DRL_ADV_REINFORCE_PP_BASELINE = compute_reinforce_plus_plus_baseline_outcome_advantage (core_algos.py:392-441:
  * group-mean baseline, then masked_whiten over the batch, times the mask; needs
- * drl_group_outcome_advantage_workspace_bytes(B)). epsilon / norm_adv_by_std apply to GRPO only. */
-enum { DRL_ADV_GRPO = 0, DRL_ADV_RLOO = 1, DRL_ADV_REINFORCE_PP_BASELINE = 2 };
+ * drl_group_outcome_advantage_workspace_bytes(B)),
+ * DRL_ADV_OPO = compute_opo_outcome_advantage (core_algos.py:495-546: length-weighted group baseline; needs the
+ * workspace above for the response lengths),
+ * DRL_ADV_GPG = compute_gpg_outcome_advantage (core_algos.py:624-684: alpha * (s - group mean), alpha = B / max(#nonzero
+ * scores, 1), f_norm = 1),
+ * DRL_ADV_GRPO_PASSK = compute_grpo_passk_outcome_advantage (core_algos.py:327-386: the best sample of a group gets
+ * r_max - r_second_max, divided by std + epsilon when norm_adv_by_std; every group must have >= 2 samples).
+ * epsilon / norm_adv_by_std apply to GRPO and GRPO_PASSK only. */
+enum { DRL_ADV_GRPO = 0, DRL_ADV_RLOO = 1, DRL_ADV_REINFORCE_PP_BASELINE = 2, DRL_ADV_OPO = 3, DRL_ADV_GPG = 4,
+       DRL_ADV_GRPO_PASSK = 5 };
 size_t drl_group_outcome_advantage_workspace_bytes(int64_t B);
 int drl_group_outcome_advantage(const float* token_level_rewards, const void* response_mask, int32_t mask_dtype,
                                 const int32_t* row_group, const int32_t* group_offsets, const int32_t* group_members,
@@ -176,6 +184,10 @@ int drl_group_outcome_advantage(const float* token_level_rewards, const void* re
 
 /* REINFORCE++ (core_algos.py:550-586): returns = masked discounted reward-to-go (a masked token resets the
  * carry), advantages = masked_whiten(returns) * mask. workspace: drl_gae_workspace_bytes(B, R). */
+/* ReMax (core_algos.py:588-621): returns = reverse cumulative sum of rewards * mask along the response, advantages
+ * = returns - reward_baselines[b] * mask; reward_baselines (B) float32 (the greedy baseline's scores). */
+int drl_remax_advantage_return(const float* token_level_rewards, const float* reward_baselines, const void* response_mask,
+                               int32_t mask_dtype, int64_t B, int64_t R, float* advantages, float* returns, void* stream);
 int drl_reinforce_pp_advantage_return(const float* token_level_rewards, const void* response_mask, int32_t mask_dtype,
                                       int64_t B, int64_t R, float gamma, float* advantages, float* returns,
                                       void* workspace, size_t workspace_bytes, void* stream);

@@ -264,6 +264,67 @@ def reinforce_pp_baseline_outcome_advantage(token_level_rewards, response_mask, 
     return adv, adv
 
 
+def _groups(index):
+    groups: dict = {}
+    for i, u in enumerate(index):
+        groups.setdefault(u, []).append(i)
+    return groups
+
+
+def opo_outcome_advantage(token_level_rewards, response_mask, index):
+    """core_algos.py:495-546: s - sum(len * s) / sum(len) over the uid group (baseline 0 for a single sample),
+    len = response_mask row sum; broadcast x mask."""
+    scores = np.asarray(token_level_rewards, np.float32).astype(f64).sum(-1)
+    lens = np.asarray(response_mask, f64).sum(-1)
+    out = scores.copy()
+    for members in _groups(index).values():
+        if len(members) > 1:
+            out[members] = scores[members] - (lens[members] * scores[members]).sum() / lens[members].sum()
+    adv = out[:, None] * np.asarray(response_mask, f64)
+    return adv, adv
+
+
+def gpg_outcome_advantage(token_level_rewards, response_mask, index, f_norm=1.0):
+    """core_algos.py:624-684: alpha * (s - group mean) / f_norm, alpha = B / max(#nonzero scores, 1) (group mean 0
+    for a single sample); broadcast x mask."""
+    scores = np.asarray(token_level_rewards, np.float32).astype(f64).sum(-1)
+    B = scores.shape[0]
+    alpha = B / max(int(np.count_nonzero(scores.astype(np.float32))), 1)
+    out = np.empty_like(scores)
+    for members in _groups(index).values():
+        mean = scores[members].mean() if len(members) > 1 else 0.0
+        out[members] = alpha * (scores[members] - mean) / f_norm
+    adv = out[:, None] * np.asarray(response_mask, f64)
+    return adv, adv
+
+
+def grpo_passk_outcome_advantage(token_level_rewards, response_mask, index, epsilon=1e-6, norm_adv_by_std_in_grpo=True):
+    """core_algos.py:327-386: per uid group (>= 2 samples, else ValueError), the best sample gets r_max - r_2nd
+    (divided by the unbiased std + epsilon when normalising), every other sample 0; broadcast x mask."""
+    scores = np.asarray(token_level_rewards, np.float32).astype(f64).sum(-1)
+    out = np.zeros_like(scores)
+    for u, members in _groups(index).items():
+        if len(members) < 2:
+            raise ValueError(f"Pass@k requires at least 2 samples per group. Got {len(members)} for group {u}.")
+        s = scores[members]
+        order = np.argsort(-s, kind="stable")
+        a = s[order[0]] - s[order[1]]
+        if norm_adv_by_std_in_grpo:
+            a = a / (np.sqrt(((s - s.mean()) ** 2).sum() / (len(s) - 1)) + epsilon)
+        out[members[order[0]]] = a
+    adv = out[:, None] * np.asarray(response_mask, f64)
+    return adv, adv
+
+
+def remax_advantage_return(token_level_rewards, reward_baselines, response_mask):
+    """core_algos.py:588-621: returns = reverse cumsum of rewards * mask (float32, from the last token); advantages
+    = returns - baseline x mask."""
+    r = np.asarray(token_level_rewards, np.float32) * np.asarray(response_mask, np.float32)
+    ret = np.flip(np.cumsum(np.flip(r, -1), -1, dtype=np.float32), -1)
+    adv = ret - np.asarray(reward_baselines, np.float32)[:, None] * np.asarray(response_mask, np.float32)
+    return adv.astype(f64), ret.astype(f64)
+
+
 def reinforce_pp_advantage_return(token_level_rewards, response_mask, gamma):
     """core_algos.py:550-586 (float32 scan in the reference's order)."""
     r = np.asarray(token_level_rewards, np.float32)

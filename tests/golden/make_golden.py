@@ -21,6 +21,7 @@ Reference call sites (file:line under /root/reference):
 * DAPO overlong-buffer reward : verl/workers/reward_manager/dapo.py:60-150 (stub tokenizer / preset scores)
 * Karmarkar-Karp balancing : verl/utils/seqlen_balancing.py:26-239 (partitions + imbalance metrics)
 * RLOO / REINFORCE++-baseline advantages : verl/trainer/ppo/core_algos.py:392-493
+* OPO / GPG / GRPO pass@k / ReMax advantages : verl/trainer/ppo/core_algos.py:327-386, 495-546, 588-684
 * masked_mean known answers : tests/utils/test_torch_functional.py:55-66 (reference test, reproduced as data)
 """
 
@@ -681,6 +682,65 @@ def gen_group_adv():
             cases.append({"name": name, "estimator": est})
             ci += 1
     _save("group_adv.npz", arrays, {"cases": cases, "ref": "core_algos.py:392-493"})
+
+
+def gen_more_adv():
+    """OPO (core_algos.py:495-546), GPG (:624-684), GRPO pass@k (:327-386) on uid-group layouts, and ReMax
+    (:588-621) with per-row baselines."""
+    g = torch.Generator().manual_seed(107)
+    arrays, cases = {}, []
+    ci = 0
+    for name, sizes, shuffle in [("n8_interleaved", [8] * 8, False), ("ragged", [3, 2, 5, 2, 4], True),
+                                 ("n4_shuffled", [4] * 6, True), ("with_singletons", [3, 1, 4, 1, 2], True)]:
+        B, R = sum(sizes), 20
+        uid = np.concatenate([np.full(s, f"uid-{gi}", dtype=object) for gi, s in enumerate(sizes)])
+        if shuffle:
+            uid = uid[torch.randperm(B, generator=g).numpy()]
+        mask = torch.ones(B, R, dtype=torch.int64)
+        lengths = torch.randint(2, R + 1, (B,), generator=g)
+        for i in range(B):
+            mask[i, lengths[i]:] = 0
+        rewards = torch.zeros(B, R)
+        score = torch.bernoulli(torch.full((B,), 0.5), generator=g) + torch.randn(B, generator=g) * 0.1
+        score[::3] = torch.round(score[::3]).clamp(0, 1)  # exact 0 / 1 scores: GPG's nonzero count, pass@k ties
+        for i in range(B):
+            rewards[i, lengths[i] - 1] = score[i]
+        ests = [("opo", lambda r, m, u: ca.compute_opo_outcome_advantage(token_level_rewards=r, response_mask=m, index=u)),
+                ("gpg", lambda r, m, u: ca.compute_gpg_outcome_advantage(token_level_rewards=r, response_mask=m, index=u))]
+        if min(sizes) >= 2:
+            for norm in (True, False):
+                ests.append((f"grpo_passk_{'std' if norm else 'nostd'}",
+                             lambda r, m, u, norm=norm: ca.compute_grpo_passk_outcome_advantage(
+                                 token_level_rewards=r, response_mask=m, index=u,
+                                 config=DictConfig(norm_adv_by_std_in_grpo=norm))))
+        for est, fn in ests:
+            adv, ret = fn(rewards.clone(), mask, uid)
+            arrays.update({f"c{ci}_rewards": rewards, f"c{ci}_mask": mask, f"c{ci}_uid": np.array([str(u) for u in uid]),
+                           f"c{ci}_adv": adv, f"c{ci}_ret": ret})
+            cases.append({"name": name, "estimator": est})
+            ci += 1
+    for name, (B, R) in [("remax_a", (7, 12)), ("remax_b", (16, 33))]:
+        rewards = torch.randn(B, R, generator=g) * (torch.rand(B, R, generator=g) > 0.6)
+        mask = torch.ones(B, R, dtype=torch.int64)
+        for i in range(B):
+            mask[i, int(torch.randint(1, R + 1, (1,), generator=g)):] = 0
+        base = torch.randn(B, generator=g)
+        adv, ret = ca.compute_remax_outcome_advantage(token_level_rewards=rewards, reward_baselines=base,
+                                                      response_mask=mask)
+        arrays.update({f"c{ci}_rewards": rewards, f"c{ci}_mask": mask, f"c{ci}_baselines": base, f"c{ci}_adv": adv,
+                       f"c{ci}_ret": ret})
+        cases.append({"name": name, "estimator": "remax"})
+        ci += 1
+    # pass@k rejects singleton groups
+    try:
+        ca.compute_grpo_passk_outcome_advantage(token_level_rewards=torch.ones(3, 4), response_mask=torch.ones(3, 4),
+                                                index=np.array(["a", "a", "b"], dtype=object),
+                                                config=DictConfig(norm_adv_by_std_in_grpo=True))
+        passk_error = ""
+    except ValueError as e:
+        passk_error = str(e)
+    _save("more_adv.npz", arrays, {"cases": cases, "passk_singleton_error": passk_error,
+                                   "ref": "core_algos.py:327-386, 495-546, 588-621, 624-684"})
 
 
 def gen_rfpp():

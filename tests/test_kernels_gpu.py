@@ -255,6 +255,34 @@ def test_rloo_and_reinforce_pp_baseline_match_reference_golden(golden):
         np.testing.assert_allclose(ret.cpu().numpy(), z[f"c{ci}_ret"], rtol=2e-5, atol=2e-6, err_msg=str(c))
 
 
+def test_opo_gpg_passk_remax_match_reference_golden(golden):
+    """K3 OPO / GPG / pass@k modes and the ReMax scan, through the registry the trainer uses, against the
+    reference estimators (more_adv.npz); pass@k refuses a singleton group with the reference's message."""
+    from dots.rl_amd import core_algos
+    from dots.rl_amd.config import to_attr
+
+    z, meta = golden("more_adv.npz")
+    for ci, c in enumerate(meta["cases"]):
+        est = c["estimator"]
+        r, m = T(z[f"c{ci}_rewards"]), T(z[f"c{ci}_mask"])
+        if est == "remax":
+            fn = core_algos.get_adv_estimator_fn("remax")
+            adv, ret = fn(token_level_rewards=r, reward_baselines=T(z[f"c{ci}_baselines"]), response_mask=m,
+                          config=None)
+        else:
+            name = "grpo_passk" if est.startswith("grpo_passk") else est
+            fn = core_algos.get_adv_estimator_fn(name)
+            cfg = to_attr({"norm_adv_by_std_in_grpo": est.endswith("_std")})
+            adv, ret = fn(token_level_rewards=r, response_mask=m, index=list(z[f"c{ci}_uid"]), config=cfg)
+        np.testing.assert_allclose(adv.cpu().numpy(), z[f"c{ci}_adv"], rtol=2e-5, atol=2e-6, err_msg=str(c))
+        np.testing.assert_allclose(ret.cpu().numpy(), z[f"c{ci}_ret"], rtol=2e-5, atol=2e-6, err_msg=str(c))
+    with pytest.raises(ValueError) as e:
+        core_algos.get_adv_estimator_fn("grpo_passk")(
+            token_level_rewards=torch.ones(3, 4, device=DEV), response_mask=torch.ones(3, 4, device=DEV),
+            index=["a", "a", "b"], config=to_attr({"norm_adv_by_std_in_grpo": True}))
+    assert str(e.value) == meta["passk_singleton_error"]
+
+
 def test_reinforce_pp_matches_reference_golden(golden):
     from dots.rl_amd import core_algos
     from dots.rl_amd.config import to_attr

@@ -75,6 +75,29 @@ def test_rloo_and_reinforce_pp_baseline_match_reference(golden):
         np.testing.assert_allclose(ret, z[f"c{ci}_ret"], rtol=2e-5, atol=2e-6, err_msg=str(c))
 
 
+def _more_adv_oracle(z, ci, est):
+    r, m, uid = z[f"c{ci}_rewards"], z[f"c{ci}_mask"], list(z[f"c{ci}_uid"]) if f"c{ci}_uid" in z else None
+    if est == "opo":
+        return oracle.opo_outcome_advantage(r, m, uid)
+    if est == "gpg":
+        return oracle.gpg_outcome_advantage(r, m, uid)
+    if est == "remax":
+        return oracle.remax_advantage_return(r, z[f"c{ci}_baselines"], m)
+    return oracle.grpo_passk_outcome_advantage(r, m, uid, norm_adv_by_std_in_grpo=est.endswith("_std"))
+
+
+def test_opo_gpg_passk_remax_match_reference(golden):
+    """The oracle's OPO / GPG / GRPO pass@k / ReMax restatements against the reference's estimators."""
+    z, meta = golden("more_adv.npz")
+    for ci, c in enumerate(meta["cases"]):
+        adv, ret = _more_adv_oracle(z, ci, c["estimator"])
+        np.testing.assert_allclose(adv, z[f"c{ci}_adv"], rtol=2e-5, atol=2e-6, err_msg=str(c))
+        np.testing.assert_allclose(ret, z[f"c{ci}_ret"], rtol=2e-5, atol=2e-6, err_msg=str(c))
+    with pytest.raises(ValueError) as e:
+        oracle.grpo_passk_outcome_advantage(np.ones((3, 4)), np.ones((3, 4)), ["a", "a", "b"])
+    assert str(e.value) == meta["passk_singleton_error"]
+
+
 def test_reinforce_pp_matches_reference(golden):
     z, meta = golden("rfpp.npz")
     for ci, c in enumerate(meta["cases"]):
