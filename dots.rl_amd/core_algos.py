@@ -297,6 +297,38 @@ def compute_policy_loss_gpg(old_log_prob, log_prob, advantages, response_mask, l
     return out[6], out[1].detach(), out[2].detach(), out[3].detach()
 
 
+def _clip_lo_hi(config):
+    lo = config.clip_ratio_low if config.get("clip_ratio_low") is not None else config.clip_ratio
+    hi = config.clip_ratio_high if config.get("clip_ratio_high") is not None else config.clip_ratio
+    return lo, hi
+
+
+@register_policy_loss("gspo")
+def compute_policy_loss_gspo(old_log_prob, log_prob, advantages, response_mask, loss_agg_mode="seq-mean-token-mean",
+                             config=None):
+    """core_algos.py:892-954 — sequence-level importance ratio, PPO clip, seq-mean-token-mean (K1's GSPO path)."""
+    assert config is not None
+    lo, hi = _clip_lo_hi(config)
+    out = fused_actor_loss(log_prob, None, old_log_prob, advantages, response_mask, None, clip_ratio_low=lo,
+                           clip_ratio_high=hi, clip_ratio_c=3.0, entropy_coeff=0.0, use_kl_loss=False,
+                           kl_loss_type=None, kl_loss_coef=0.0, loss_agg_mode=loss_agg_mode, loss_scale_factor=1.0,
+                           policy_loss="gspo")
+    return out[6], out[1].detach(), out[2].detach(), out[3].detach()
+
+
+@register_policy_loss("geo_mean")
+def compute_policy_loss_geo_mean(old_log_prob, log_prob, advantages, response_mask, loss_agg_mode="token-mean",
+                                 config=None):
+    """core_algos.py:1143-1210 — GMPO geometric-mean ratio per sequence (K1's GMPO path); loss_agg_mode unused."""
+    assert config is not None
+    lo, hi = _clip_lo_hi(config)
+    out = fused_actor_loss(log_prob, None, old_log_prob, advantages, response_mask, None, clip_ratio_low=lo,
+                           clip_ratio_high=hi, clip_ratio_c=3.0, entropy_coeff=0.0, use_kl_loss=False,
+                           kl_loss_type=None, kl_loss_coef=0.0, loss_agg_mode=loss_agg_mode, loss_scale_factor=1.0,
+                           policy_loss="geo_mean")
+    return out[6], out[1].detach(), out[2].detach(), out[3].detach()
+
+
 def compute_value_loss(vpreds, returns, values, response_mask, cliprange_value, loss_agg_mode="token-mean"):
     """core_algos.py:1230-1269 — (vf_loss, vf_clipfrac); vf_loss is differentiable wrt vpreds (K6, one launch
     for forward and backward, csrc/value_loss.hip)."""

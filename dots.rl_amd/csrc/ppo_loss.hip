@@ -571,7 +571,7 @@ __global__ __launch_bounds__(256) void row_count_kernel(const void* mask, int64_
 int max_grid() { return cu_count() * (DRL_K1_WG_PER_CU > DRL_K1_PACK_WG_PER_CU ? DRL_K1_WG_PER_CU : DRL_K1_PACK_WG_PER_CU); }
 
 struct Layout {
-  size_t partials, rowcnt, counts, bits, total;
+  size_t partials, rowcnt, counts, bits, seqrow, seqpart, total;
 };
 
 Layout ws_layout(int64_t B, int64_t R) {
@@ -582,7 +582,9 @@ Layout ws_layout(int64_t B, int64_t R) {
   L.rowcnt = round_up(L.partials + grid * kNumPartials * sizeof(double), 256);
   L.counts = round_up(L.rowcnt + static_cast<size_t>(B) * sizeof(float), 256);
   L.bits = round_up(L.counts + grid * sizeof(double), 256);
-  L.total = round_up(L.bits + nchunks * 16 * sizeof(unsigned long long), 256);
+  L.seqrow = round_up(L.bits + nchunks * 16 * sizeof(unsigned long long), 256);
+  L.seqpart = round_up(L.seqrow + static_cast<size_t>(B) * 4 * sizeof(float), 256);
+  L.total = round_up(L.seqpart + static_cast<size_t>(B) * kNumPartials * sizeof(double), 256);
   return L;
 }
 
@@ -678,6 +680,209 @@ int launch_agg(const float* x, const void* mask, int64_t B, int64_t R, int mode,
   return DRL_OK;
 }
 
+// ------------------------------------------------------------------------------------------------------------
+// Sequence-level policy losses: GSPO (core_algos.py:892-954) and GMPO geo_mean (core_algos.py:1143-1210), composed
+// with the entropy bonus / KL term / loss scale of dp_actor.py:419-466 like K1. Their pg terms need per-row sums
+// before any token's gradient, so they run as three small launches instead of K1's stream: (S1) per-row sums,
+// one wave per row; (S2) one workgroup per row: per-token loss terms, d loss / d log_prob, d loss / d entropy and
+// the row's partial forward sums; (S3) one workgroup folds the rows' partials in row order (deterministic).
+// rowstat[b] = {sum(mask), sum(nak * mask), sum(nak_min * mask), sum(A * mask)}, nak = log_prob - old_log_prob.
+struct SeqArgs {
+  const float* old_lp;
+  const float* lp;
+  const float* adv;
+  const void* mask;
+  const float* ent;
+  const float* ref;
+  float* dlp;
+  float* dent;
+  float* out;
+  float* rowstat;   // (B, 4)
+  double* rowpart;  // (B, kNumPartials)
+  int64_t B, R;
+  float lo, hi;          // GSPO: 1 - clip_ratio_low, 1 + clip_ratio_high (ratio space)
+  float llo, lhi;        // GMPO: clip_ratio_low, clip_ratio_high (log-ratio space)
+  float ent_coef, kl_coef, lsf;
+  int mode, kl, policy;
+};
+
+// GMPO: nak clipped toward sign(A) (value) and d value / d nak (torch.min / torch.clamp backward)
+__device__ __forceinline__ void geo_clip(float nak, float A, float llo, float lhi, float& v, float& d) {
+  const float sg = A > 0.f ? 1.f : (A < 0.f ? -1.f : 0.f);
+  const float ncl = fminf(fmaxf(nak, -llo), lhi);
+  const float gc = (nak >= -llo && nak <= lhi) ? 1.f : 0.f;
+  const float x = sg * nak, y = sg * ncl;
+  v = sg * fminf(x, y);
+  const float wa = x < y ? 1.f : (x == y ? 0.5f : 0.f);
+  d = sg * sg * (wa + (1.f - wa) * gc);
+}
+
+template <int MDT>
+__global__ __launch_bounds__(256) void seq_row_kernel(SeqArgs a) {
+  const int64_t row = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= a.B) return;
+  float c = 0.f, sk = 0.f, sm = 0.f, sa = 0.f;
+  for (int64_t t = lane; t < a.R; t += 64) {
+    const int64_t i = row * a.R + t;
+    const float m = mask_at<MDT>(a.mask, i);
+    const float nak = a.lp[i] - a.old_lp[i];
+    c += m;
+    sk += nak * m;
+    if (a.policy == DRL_POLICY_GEO_MEAN) {
+      float v, d;
+      geo_clip(nak, a.adv[i], a.llo, a.lhi, v, d);
+      sm += v * m;
+      sa += a.adv[i] * m;
+    }
+  }
+  c = wave_sum(c); sk = wave_sum(sk); sm = wave_sum(sm); sa = wave_sum(sa);
+  if (lane == 0) {
+    a.rowstat[4 * row] = c; a.rowstat[4 * row + 1] = sk; a.rowstat[4 * row + 2] = sm; a.rowstat[4 * row + 3] = sa;
+  }
+}
+
+template <int MDT>
+__global__ __launch_bounds__(256) void seq_token_kernel(SeqArgs a) {
+  const int64_t row = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  __shared__ float s_cnt[4];
+  __shared__ double red[4][kNumPartials];
+  // sum(mask) over the whole micro-batch (token-mean weights), the same fixed order in every workgroup
+  float c = 0.f;
+  for (int64_t b = tid; b < a.B; b += 256) c += a.rowstat[4 * b];
+  c = wave_sum(c);
+  if (lane == 0) s_cnt[wave] = c;
+  __syncthreads();
+  const float cnt = (s_cnt[0] + s_cnt[1]) + (s_cnt[2] + s_cnt[3]);
+  const float inv_denom_tm = 1.0f / (cnt + 1e-8f);
+  const float rowcnt = a.rowstat[4 * row];
+  const float inv_B = 1.0f / static_cast<float>(a.B), inv_R = 1.0f / static_cast<float>(a.R);
+  const bool tm = a.mode == DRL_AGG_TOKEN_MEAN, smtm = a.mode == DRL_AGG_SEQ_MEAN_TOKEN_MEAN;
+  const bool gspo = a.policy == DRL_POLICY_GSPO;
+  // per-row scalars
+  float ratio, gate = 1.f, geo_scale = 0.f, pg_row = 0.f;
+  if (gspo) {  // seq log-ratio = sum(nak * mask) / clamp(len, 1), clamped at 10 (clamp passes the gradient at 10)
+    const float seq_kl = a.rowstat[4 * row + 1] / fmaxf(rowcnt, 1.f);
+    gate = seq_kl <= 10.f ? 1.f : 0.f;
+    ratio = expf(fminf(seq_kl, 10.f));
+  } else {  // GMPO: exp(mean clipped log-ratio), mean advantage; pg_row = -adv * ratio
+    const float msum = rowcnt + 1e-8f;
+    ratio = expf(a.rowstat[4 * row + 2] / msum);
+    const float adv = a.rowstat[4 * row + 3] / msum;
+    pg_row = -adv * ratio;
+    geo_scale = ((-adv * ratio) / msum) * inv_B;  // d pg_loss / d nak_min_t = geo_scale * mask_t
+  }
+  float S[kNumPartials] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int64_t t = tid; t < a.R; t += 256) {
+    const int64_t i = row * a.R + t;
+    const float mj = mask_at<MDT>(a.mask, i);
+    const bool mb = mj != 0.f;
+    const float lpv = a.lp[i], A = a.adv[i];
+    const float nak = lpv - a.old_lp[i];
+    float w;  // d agg / d loss_mat for the entropy / KL terms (loss_agg_mode)
+    if (tm) w = mb ? inv_denom_tm * mj : 0.f;
+    else if (a.mode == DRL_AGG_SEQ_MEAN_TOKEN_SUM) w = inv_B * mj;
+    else if (smtm) w = mj * (inv_B * (1.0f / rowcnt));
+    else w = inv_R * mj;
+    auto agg_val = [&](float x) -> float {
+      if (tm) return mb ? x * mj : 0.f;
+      if (smtm) return (x * mj) * (1.0f / rowcnt);
+      return x * mj;
+    };
+    float dpg;
+    if (gspo) {  // PPO clip on the sequence ratio, no dual clip; pg aggregated seq-mean-token-mean
+      const float negA = -A;
+      const float L1 = negA * ratio;
+      const float rc = fminf(fmaxf(ratio, a.lo), a.hi);
+      const float gc = (ratio >= a.lo && ratio <= a.hi) ? 1.f : 0.f;
+      const float L2 = negA * rc;
+      const float pg = fmaxf(L1, L2);
+      const float w1 = L1 > L2 ? 1.f : (L1 == L2 ? 0.5f : 0.f);
+      dpg = (mj * (inv_B * (1.0f / rowcnt))) * ((w1 + (1.f - w1) * gc) * negA * ratio * gate);
+      S[0] += (pg * mj) * (1.0f / rowcnt);
+      S[1] += (mb && L2 > L1) ? mj : 0.f;
+    } else {
+      float v, d;
+      geo_clip(nak, A, a.llo, a.lhi, v, d);
+      dpg = geo_scale * mj * d;
+      const float ncl = fminf(fmaxf(nak, -a.llo), a.lhi);
+      const bool clipped = nak != ncl;
+      S[1] += (mb && clipped && A > 0.f) ? mj : 0.f;
+      S[3] += (mb && clipped && A < 0.f) ? mj : 0.f;
+    }
+    S[2] += mb ? -nak * mj : 0.f;
+    S[6] += mj;
+    float gl = dpg;
+    if (a.kl != DRL_KL_NONE) {
+      float kv, dk;
+      kl_term(a.kl, lpv, a.ref[i], kv, dk);
+      S[5] += agg_val(kv);
+      gl += a.kl_coef * (w * dk);
+    }
+    if (a.ent != nullptr) S[4] += agg_val(a.ent[i]);
+    if (a.dlp != nullptr) a.dlp[i] = a.lsf * gl;
+    if (a.dent != nullptr) a.dent[i] = a.ent_coef != 0.f ? a.lsf * (-a.ent_coef * w) : 0.f;
+  }
+  if (!gspo && tid == 0) S[0] = pg_row;  // GMPO: one sequence-level term per row
+#pragma unroll
+  for (int k = 0; k < kNumPartials; ++k) {
+    const double v = wave_sum(static_cast<double>(S[k]));
+    if (lane == 0) red[wave][k] = v;
+  }
+  __syncthreads();
+  if (tid < kNumPartials) a.rowpart[row * kNumPartials + tid] = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
+}
+
+__global__ __launch_bounds__(256) void seq_final_kernel(SeqArgs a) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  __shared__ double red[4][kNumPartials];
+#pragma unroll
+  for (int k = 0; k < kNumPartials; ++k) {
+    double v = 0.0;
+    for (int64_t b = tid; b < a.B; b += 256) v += a.rowpart[b * kNumPartials + k];
+    v = wave_sum(v);
+    if (lane == 0) red[wave][k] = v;
+  }
+  __syncthreads();
+  if (tid != 0) return;
+  double r[kNumPartials];
+  for (int k = 0; k < kNumPartials; ++k) r[k] = (red[0][k] + red[1][k]) + (red[2][k] + red[3][k]);
+  const double cnt = r[6];
+  const double dm = static_cast<double>(static_cast<float>(cnt) + 1e-8f);
+  auto agg = [&](double x) -> double {
+    if (a.mode == DRL_AGG_TOKEN_MEAN) return x / dm;
+    if (a.mode == DRL_AGG_SEQ_MEAN_TOKEN_SUM || a.mode == DRL_AGG_SEQ_MEAN_TOKEN_MEAN) return x / static_cast<double>(a.B);
+    return x / static_cast<double>(a.R);
+  };
+  const double pg_loss = r[0] / static_cast<double>(a.B);  // GSPO: seq-mean of token-means; GMPO: mean over rows
+  const bool has_ent = a.ent != nullptr, has_kl = a.kl != DRL_KL_NONE;
+  const double ent_loss = has_ent ? agg(r[4]) : 0.0;
+  const double kl_loss = has_kl ? agg(r[5]) : 0.0;
+  double total = pg_loss;
+  if (a.ent_coef != 0.f) total -= ent_loss * a.ent_coef;
+  if (has_kl) total += kl_loss * a.kl_coef;
+  a.out[DRL_PPO_OUT_PG_LOSS] = static_cast<float>(pg_loss);
+  a.out[DRL_PPO_OUT_PG_CLIPFRAC] = static_cast<float>(r[1] / dm);
+  a.out[DRL_PPO_OUT_PPO_KL] = static_cast<float>(r[2] / dm);
+  a.out[DRL_PPO_OUT_PG_CLIPFRAC_LOWER] = static_cast<float>(r[3] / dm);
+  a.out[DRL_PPO_OUT_ENTROPY_LOSS] = static_cast<float>(ent_loss);
+  a.out[DRL_PPO_OUT_KL_LOSS] = static_cast<float>(kl_loss);
+  a.out[DRL_PPO_OUT_LOSS] = static_cast<float>(total * a.lsf);
+  a.out[DRL_PPO_OUT_MASK_COUNT] = static_cast<float>(cnt);
+}
+
+template <int MDT>
+int launch_seq(const SeqArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(seq_row_kernel<MDT>, dim3(static_cast<unsigned>((a.B + 3) / 4)), dim3(256), 0, s, a);
+  DRL_LAUNCH_CHECK();
+  hipLaunchKernelGGL(seq_token_kernel<MDT>, dim3(static_cast<unsigned>(a.B)), dim3(256), 0, s, a);
+  DRL_LAUNCH_CHECK();
+  hipLaunchKernelGGL(seq_final_kernel, dim3(1), dim3(256), 0, s, a);
+  DRL_LAUNCH_CHECK();
+  return DRL_OK;
+}
+
 }  // namespace
 }  // namespace drl
 
@@ -698,8 +903,10 @@ int drl_ppo_loss_fwd_bwd(const float* old_log_prob, const float* log_prob, const
   DRL_CHECK_ARG(p->kl_type >= DRL_KL_NONE && p->kl_type <= DRL_KL_K3, "bad kl_type %d", p->kl_type);
   DRL_CHECK_ARG(p->kl_type == DRL_KL_NONE || ref_log_prob != nullptr, "kl_type set but ref_log_prob is NULL");
   DRL_CHECK_ARG(p->entropy_coeff == 0.f || entropy != nullptr, "entropy_coeff != 0 but entropy is NULL");
-  DRL_CHECK_ARG(p->policy_loss == DRL_POLICY_GPG || p->clip_ratio_c > 1.f,
+  DRL_CHECK_ARG(p->policy_loss != DRL_POLICY_VANILLA || p->clip_ratio_c > 1.f,
                 "clip_ratio_c must be > 1.0 (dual-clip PPO), got %f", p->clip_ratio_c);
+  DRL_CHECK_ARG(p->policy_loss >= DRL_POLICY_VANILLA && p->policy_loss <= DRL_POLICY_GEO_MEAN, "bad policy_loss %d",
+                p->policy_loss);
   DRL_CHECK_ARG(mask_dtype == DRL_I64 || mask_dtype == DRL_I32 || mask_dtype == DRL_U8 || mask_dtype == DRL_F32,
                 "unsupported mask dtype %d", mask_dtype);
   const void* ptrs[] = {old_log_prob, log_prob, advantages, response_mask, entropy, ref_log_prob, dlog_prob, dentropy};
@@ -709,6 +916,27 @@ int drl_ppo_loss_fwd_bwd(const float* old_log_prob, const float* log_prob, const
     return fail(DRL_ERR_WORKSPACE, "workspace %zu < %zu bytes", workspace_bytes, L.total);
 
   auto* ws = static_cast<char*>(workspace);
+  if (p->policy_loss == DRL_POLICY_GSPO || p->policy_loss == DRL_POLICY_GEO_MEAN) {
+    SeqArgs q{};
+    q.old_lp = old_log_prob; q.lp = log_prob; q.adv = advantages; q.mask = response_mask;
+    q.ent = entropy; q.ref = p->kl_type == DRL_KL_NONE ? nullptr : ref_log_prob;
+    q.dlp = dlog_prob; q.dent = dentropy; q.out = out_scalars;
+    q.rowstat = reinterpret_cast<float*>(ws + L.seqrow);
+    q.rowpart = reinterpret_cast<double*>(ws + L.seqpart);
+    q.B = B; q.R = R;
+    q.lo = static_cast<float>(1.0 - static_cast<double>(p->clip_ratio_low));
+    q.hi = static_cast<float>(1.0 + static_cast<double>(p->clip_ratio_high));
+    q.llo = p->clip_ratio_low; q.lhi = p->clip_ratio_high;
+    q.ent_coef = p->entropy_coeff; q.kl_coef = p->kl_loss_coef; q.lsf = p->loss_scale_factor;
+    q.mode = p->loss_agg_mode; q.kl = p->kl_type; q.policy = p->policy_loss;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    switch (mask_dtype) {
+      case DRL_I64: return launch_seq<DRL_I64>(q, s);
+      case DRL_I32: return launch_seq<DRL_I32>(q, s);
+      case DRL_U8: return launch_seq<DRL_U8>(q, s);
+      default: return launch_seq<DRL_F32>(q, s);
+    }
+  }
   Args a{};
   a.old_lp = old_log_prob; a.lp = log_prob; a.adv = advantages; a.mask = response_mask;
   a.ent = entropy; a.ref = p->kl_type == DRL_KL_NONE ? nullptr : ref_log_prob;
@@ -724,8 +952,6 @@ int drl_ppo_loss_fwd_bwd(const float* old_log_prob, const float* log_prob, const
   a.clip_c = p->clip_ratio_c; a.ent_coef = p->entropy_coeff; a.kl_coef = p->kl_loss_coef;
   a.lsf = p->loss_scale_factor; a.mode = p->loss_agg_mode; a.kl = p->kl_type;
   a.token_count = p->loss_agg_mode == DRL_AGG_TOKEN_MEAN ? p->token_count : nullptr;
-  DRL_CHECK_ARG(p->policy_loss == DRL_POLICY_VANILLA || p->policy_loss == DRL_POLICY_GPG, "bad policy_loss %d",
-                p->policy_loss);
   a.policy = p->policy_loss;
 
   hipStream_t s = static_cast<hipStream_t>(stream);  // the header is zero on entry (see Header)

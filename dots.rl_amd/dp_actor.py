@@ -234,9 +234,9 @@ class DataParallelPPOActor:
         data = data.select(batch_keys=keys)
         mini_batches = data.split(cfg.ppo_mini_batch_size)
         loss_mode = cfg.policy_loss.get("loss_mode", "vanilla")
-        if loss_mode not in ("vanilla", "gpg"):
-            raise NotImplementedError(f"policy loss {loss_mode}: the fused K1 modes are vanilla (PPO clip + dual clip) "
-                                      "and gpg")
+        if loss_mode not in ("vanilla", "gpg", "gspo", "geo_mean"):
+            raise NotImplementedError(f"policy loss {loss_mode}: the fused K1 modes are vanilla (PPO clip + dual clip), "
+                                      "gpg, gspo and geo_mean (clip_cov / kl_cov are not built)")
         lo = cfg.clip_ratio_low if cfg.get("clip_ratio_low") is not None else cfg.clip_ratio
         hi = cfg.clip_ratio_high if cfg.get("clip_ratio_high") is not None else cfg.clip_ratio
         mb_out, mb_lsf, grad_norms = [], [], []

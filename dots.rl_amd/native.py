@@ -165,7 +165,7 @@ def ppo_loss_fwd_bwd(old_log_prob, log_prob, advantages, response_mask, entropy=
     prm = _lib.PPOLossParams(clip_ratio_low, clip_ratio_high, clip_ratio_c, entropy_coeff, kl_loss_coef,
                              loss_scale_factor, _lib.AGG_MODES[loss_agg_mode],
                              _lib.KL_NONE if kl_loss_type is None else _lib.KL_TYPES[kl_loss_type], None,
-                             {"vanilla": 0, "gpg": 1}[policy_loss])
+                             {"vanilla": 0, "gpg": 1, "gspo": 2, "geo_mean": 3}[policy_loss])
     if token_count is not None:
         _dev(token_count)
         assert token_count.dtype == torch.float64 and token_count.numel() == 1

@@ -95,11 +95,17 @@ typedef struct drl_ppo_loss_params {
   const double* token_count;
   /* policy loss (actor.policy_loss.loss_mode, get_policy_loss_fn core_algos.py:68-83): DRL_POLICY_VANILLA =
    * compute_policy_loss_vanilla (PPO clip + dual clip, :815-889), DRL_POLICY_GPG = compute_policy_loss_gpg
-   * (pg = -log_prob * advantages, :957-975; clipfrac / ppo_kl / clipfrac_lower reported as 0). */
+   * (pg = -log_prob * advantages, :957-975; clipfrac / ppo_kl / clipfrac_lower reported as 0),
+   * DRL_POLICY_GSPO = compute_policy_loss_gspo (:892-954: the row's mean log-ratio as every token's ratio, clamped
+   * at 10, PPO clip without dual clip, pg aggregated seq-mean-token-mean whatever loss_agg_mode is;
+   * pg_clipfrac_lower 0), DRL_POLICY_GEO_MEAN = compute_policy_loss_geo_mean (:1143-1210, GMPO: log-ratios clipped
+   * to [-clip_ratio_low, clip_ratio_high] toward sign(A), geometric-mean ratio and mean advantage per row, pg =
+   * mean over rows). The two sequence-level losses run as three small launches (per-row sums, per-token terms,
+   * row fold) instead of K1's stream, and ignore token_count and clip_ratio_c. */
   int32_t policy_loss;
 } drl_ppo_loss_params;
 
-enum { DRL_POLICY_VANILLA = 0, DRL_POLICY_GPG = 1 };
+enum { DRL_POLICY_VANILLA = 0, DRL_POLICY_GPG = 1, DRL_POLICY_GSPO = 2, DRL_POLICY_GEO_MEAN = 3 };
 
 enum {
   DRL_PPO_OUT_PG_LOSS = 0,

@@ -180,12 +180,77 @@ def clip_boundary_tokens(old_log_prob, log_prob, advantages, response_mask, clip
     return int((amb & m).sum())
 
 
+def policy_loss_gspo(old_log_prob, log_prob, advantages, response_mask, clip_ratio_low=0.2, clip_ratio_high=0.2):
+    """compute_policy_loss_gspo (core_algos.py:892-954): the sequence-mean log-ratio (length clamped at 1) as every
+    token's log importance ratio (clamped at 10; d/d log_prob through the log_prob - sg(log_prob) term), PPO clip
+    without dual clip, pg aggregated seq-mean-token-mean whatever loss_agg_mode says. Returns (pg_loss,
+    pg_clipfrac, ppo_kl, pg_clipfrac_lower, d pg_loss / d log_prob)."""
+    f32 = np.float32
+    m32 = np.asarray(response_mask, f32)
+    nak = np.asarray(log_prob, f32) - np.asarray(old_log_prob, f32)
+    seq_len = np.maximum(m32.sum(-1), f32(1.0))
+    seq_kl = ((nak * m32).sum(-1) / seq_len).astype(f32)
+    lsr = np.minimum(seq_kl, f32(10.0))[:, None] * np.ones_like(nak)
+    gate = (seq_kl <= 10.0)[:, None].astype(f64)
+    ratio = np.exp(lsr.astype(f64)).astype(f32)
+    A = np.asarray(advantages, f32)
+    L1 = -A * ratio
+    lo, hi = f32(1.0 - clip_ratio_low), f32(1.0 + clip_ratio_high)
+    gc = ((ratio >= lo) & (ratio <= hi)).astype(f64)
+    L2 = -A * np.clip(ratio, lo, hi)
+    w1, w2 = _max_grad(L1, L2)
+    dpg = (w1 + w2 * gc) * (-A.astype(f64)) * ratio.astype(f64) * gate
+    pg_losses = np.maximum(L1, L2).astype(f64)
+    mode = "seq-mean-token-mean"
+    pg_loss = agg_loss(pg_losses, response_mask, mode)
+    dpg = dpg * agg_loss_grad(response_mask, mode)
+    return (pg_loss, masked_mean((L2 > L1).astype(f64), response_mask), masked_mean(-nak.astype(f64), response_mask),
+            0.0, dpg)
+
+
+def policy_loss_geo_mean(old_log_prob, log_prob, advantages, response_mask, clip_ratio_low=0.2, clip_ratio_high=0.2):
+    """compute_policy_loss_geo_mean (core_algos.py:1143-1210, GMPO): token log-ratios clipped toward the advantage's
+    sign (clamp to [-clip_ratio_low, clip_ratio_high] in log space, min under sign(A)), the row's geometric-mean
+    ratio exp(mean over the row), the row's mean advantage, pg = mean over rows of -adv * ratio. Returns (pg_loss,
+    pg_clipfrac, ppo_kl, pg_clipfrac_lower, d pg_loss / d log_prob)."""
+    f32 = np.float32
+    m32 = np.asarray(response_mask, f32)
+    nak = np.asarray(log_prob, f32) - np.asarray(old_log_prob, f32)
+    A = np.asarray(advantages, f32)
+    sgn = np.sign(A)
+    lo, hi = f32(clip_ratio_low), f32(clip_ratio_high)
+    ncl = np.clip(nak, -lo, hi)
+    gc = ((nak >= -lo) & (nak <= hi)).astype(f64)
+    a, b = sgn * nak, sgn * ncl
+    wa, wb = _max_grad(-a, -b)  # min backward
+    nmin = sgn * np.minimum(a, b)
+    dnmin = (sgn.astype(f64) ** 2) * (wa + wb * gc)
+    msum = m32.sum(-1) + f32(1e-8)
+    ratio = np.exp(((nmin * m32).sum(-1) / msum).astype(f64)).astype(f32)
+    adv = ((A * m32).sum(-1) / msum).astype(f32)
+    pg_rows = (-adv * ratio).astype(f64)
+    B = A.shape[0]
+    pg_loss = pg_rows.mean()
+    dpg = ((-adv.astype(f64) * ratio.astype(f64) / msum.astype(f64)) / B)[:, None] * m32.astype(f64) * dnmin
+    clipped = (nak != ncl).astype(f64)
+    return (pg_loss, masked_mean(clipped * (A > 0), response_mask), masked_mean(-nak.astype(f64), response_mask),
+            masked_mean(clipped * (A < 0), response_mask), dpg)
+
+
 def actor_loss(old_log_prob, log_prob, advantages, response_mask, entropy, ref_log_prob, *, loss_agg_mode,
                clip_ratio_low, clip_ratio_high, clip_ratio_c, entropy_coeff, use_kl_loss, kl_loss_type,
                kl_loss_coef, loss_scale_factor, policy_loss="vanilla"):
     """The per-micro-batch loss of DataParallelPPOActor.update_policy (dp_actor.py:419-466).
-    policy_loss "gpg": compute_policy_loss_gpg (core_algos.py:957-975), pg = -log_prob * advantages."""
-    if policy_loss == "gpg":
+    policy_loss "gpg": compute_policy_loss_gpg (core_algos.py:957-975), pg = -log_prob * advantages; "gspo" /
+    "geo_mean": policy_loss_gspo / policy_loss_geo_mean (sequence-level ratios)."""
+    w = agg_loss_grad(response_mask, loss_agg_mode)
+    if policy_loss in ("gspo", "geo_mean"):  # the pg gradient carries its own aggregation weights
+        fn = policy_loss_gspo if policy_loss == "gspo" else policy_loss_geo_mean
+        pg_loss, clipfrac, ppo_kl, clipfrac_lower, dpg_w = fn(old_log_prob, log_prob, advantages, response_mask,
+                                                               clip_ratio_low, clip_ratio_high)
+        with np.errstate(divide="ignore", invalid="ignore"):
+            dpg = np.where(w != 0, dpg_w / np.where(w != 0, w, 1.0), 0.0)
+    elif policy_loss == "gpg":
         lp32 = np.asarray(log_prob, np.float32)
         A32 = np.asarray(advantages, np.float32)
         pg_losses = ((-lp32) * A32).astype(f64)
@@ -196,12 +261,11 @@ def actor_loss(old_log_prob, log_prob, advantages, response_mask, entropy, ref_l
         pg_loss, clipfrac, ppo_kl, clipfrac_lower, _, dpg = policy_loss_vanilla(
             old_log_prob, log_prob, advantages, response_mask, loss_agg_mode, clip_ratio_low, clip_ratio_high,
             clip_ratio_c)
-    w = agg_loss_grad(response_mask, loss_agg_mode)
     entropy_loss = agg_loss(entropy, response_mask, loss_agg_mode)
     total = pg_loss - entropy_loss * entropy_coeff if entropy_coeff != 0 else pg_loss
     kld, dkld = kl_penalty(log_prob, ref_log_prob, kl_loss_type)
     kl_loss = agg_loss(kld, response_mask, loss_agg_mode)
-    dlogp = w * dpg
+    dlogp = dpg_w if policy_loss in ("gspo", "geo_mean") else w * dpg
     if use_kl_loss:
         total = total + kl_loss * kl_loss_coef
         dlogp = dlogp + kl_loss_coef * w * dkld

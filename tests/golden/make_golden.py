@@ -22,6 +22,7 @@ Reference call sites (file:line under /root/reference):
 * Karmarkar-Karp balancing : verl/utils/seqlen_balancing.py:26-239 (partitions + imbalance metrics)
 * RLOO / REINFORCE++-baseline advantages : verl/trainer/ppo/core_algos.py:392-493
 * OPO / GPG / GRPO pass@k / ReMax advantages : verl/trainer/ppo/core_algos.py:327-386, 495-546, 588-684
+* GSPO / GMPO (geo_mean) policy losses : verl/trainer/ppo/core_algos.py:892-954, 1143-1210
 * masked_mean known answers : tests/utils/test_torch_functional.py:55-66 (reference test, reproduced as data)
 """
 
@@ -788,6 +789,54 @@ def gen_gpg_loss():
         cases.append(dict(loss_agg_mode=mode, kl_loss_type=kl, entropy_coeff=ent_c, kl_loss_coef=0.001,
                           loss_scale_factor=lsf, use_kl_loss=True))
     _save("gpg_loss.npz", arrays, {"cases": cases, "ref": "core_algos.py:957-975; dp_actor.py:419-466"})
+
+
+def gen_seq_loss():
+    """Sequence-level policy losses composed as dp_actor.py:419-466 composes any registered loss: GSPO
+    (core_algos.py:892-954, sequence-mean log-ratio, seq-mean-token-mean pg aggregation) and GMPO geo_mean
+    (:1143-1210, geometric-mean ratio of sign-clipped token log-ratios, mean over rows)."""
+    from verl.workers.config import ActorConfig
+    from verl.workers.config.optimizer import OptimizerConfig
+
+    g = torch.Generator().manual_seed(5151)
+    arrays, cases = {}, []
+    specs = [("gspo", (6, 16), "edges", "token-mean", "low_var_kl", 0.001, 0.5, (0.2, 0.2)),
+             ("gspo", (8, 40), "random", "seq-mean-token-sum", "kl", 0.0, 1.0, (0.2, 0.28)),
+             ("gspo", (5, 33), "big", "seq-mean-token-mean", "abs", 0.01, 0.25, (0.0003, 0.0004)),
+             ("geo_mean", (6, 16), "edges", "token-mean", "low_var_kl", 0.001, 0.5, (0.2, 0.2)),
+             ("geo_mean", (8, 40), "random", "seq-mean-token-mean", "mse", 0.0, 1.0, (0.4, 0.4)),
+             ("geo_mean", (5, 33), "big", "seq-mean-token-sum-norm", "kl", 0.01, 0.25, (0.05, 0.1))]
+    for ci, (loss, shape, kind, mode, kl, ent_c, lsf, (clo, chi)) in enumerate(specs):
+        old, logp, adv, mask, ent, ref = ppo_loss_inputs(g, *shape, "edges" if kind == "edges" else "random")
+        if kind == "big":  # sequence log-ratios past GSPO's clamp at 10, every sign of advantage
+            logp = logp + torch.randn(shape[0], 1, generator=g) * 12.0
+            adv[1] = 0.0
+        if loss == "geo_mean":  # GMPO uses a per-sequence advantage (outcome estimators): constant per row
+            adv = adv[:, :1].expand_as(adv).clone()
+        cfg = ActorConfig(strategy="fsdp", clip_ratio=0.2, clip_ratio_low=clo, clip_ratio_high=chi,
+                          loss_agg_mode=mode, optim=OptimizerConfig(lr=1e-6), ppo_micro_batch_size_per_gpu=2,
+                          ppo_mini_batch_size=4)
+        pg_fn = ca.get_policy_loss_fn(loss)
+        lp = logp.clone().requires_grad_(True)
+        en = ent.clone().requires_grad_(True)
+        pg_loss, c1, c2, c3 = pg_fn(old_log_prob=old, log_prob=lp, advantages=adv, response_mask=mask,
+                                    loss_agg_mode=mode, config=cfg)
+        entropy_loss = ca.agg_loss(loss_mat=en, loss_mask=mask, loss_agg_mode=mode)
+        policy_loss = pg_loss - entropy_loss * ent_c if ent_c != 0 else pg_loss
+        kld = ca.kl_penalty(logprob=lp, ref_logprob=ref, kl_penalty=kl)
+        kl_loss = ca.agg_loss(loss_mat=kld, loss_mask=mask, loss_agg_mode=mode)
+        loss_v = (policy_loss + kl_loss * 0.001) * lsf
+        loss_v.backward()
+        for k, v in dict(old_log_prob=old, log_prob=logp, advantages=adv, response_mask=mask, entropy=ent,
+                         ref_log_prob=ref, out_pg_loss=pg_loss.detach(), out_loss=loss_v.detach(),
+                         out_entropy_loss=entropy_loss.detach(), out_kl_loss=kl_loss.detach(),
+                         out_dlogp=lp.grad, out_dentropy=en.grad if en.grad is not None else torch.zeros_like(en),
+                         out_clip=torch.tensor([float(c1), float(c2), float(c3)])).items():
+            arrays[f"c{ci}_{k}"] = v
+        cases.append(dict(policy_loss=loss, loss_agg_mode=mode, kl_loss_type=kl, entropy_coeff=ent_c,
+                          kl_loss_coef=0.001, loss_scale_factor=lsf, use_kl_loss=True, clip_ratio_low=clo,
+                          clip_ratio_high=chi))
+    _save("seq_loss.npz", arrays, {"cases": cases, "ref": "core_algos.py:892-954, 1143-1210; dp_actor.py:419-466"})
 
 
 # --------------------------------------------------------------------------------------------

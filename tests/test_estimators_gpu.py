@@ -12,7 +12,7 @@ TINY = ("{'hidden_size': 128, 'intermediate_size': 256, 'num_hidden_layers': 2, 
         "'num_key_value_heads': 1, 'vocab_size': 1024}")
 
 
-def _trainer(estimator):
+def _trainer(estimator, extra=()):
     from dots.rl_amd.config import apply_overrides, default_config
     from dots.rl_amd.trainer import RayPPOTrainer
 
@@ -23,7 +23,7 @@ def _trainer(estimator):
         "actor_rollout_ref.actor.ppo_micro_batch_size_per_gpu=4",
         "actor_rollout_ref.rollout.log_prob_micro_batch_size_per_gpu=8",
         "actor_rollout_ref.ref.log_prob_micro_batch_size_per_gpu=8", f"algorithm.adv_estimator={estimator}",
-        f"actor_rollout_ref.model.override_config={TINY}",
+        f"actor_rollout_ref.model.override_config={TINY}", *extra,
     ])
     trainer = RayPPOTrainer(cfg)
     trainer.train_dataloader.vocab_limit = 1000
@@ -55,3 +55,17 @@ def test_estimator_step_end_to_end(estimator):
         # one non-zero advantage row at most per group of n
         nz = (adv.abs().sum(-1) != 0).view(-1, 4).sum(-1)
         assert (nz <= 1).all()
+
+
+@pytest.mark.parametrize("loss_mode", ["gspo", "geo_mean", "gpg"])
+def test_policy_loss_modes_step_end_to_end(loss_mode):
+    """actor.policy_loss.loss_mode selects the registered loss inside update_policy (dp_actor.py:419-466): one GRPO
+    step per mode, finite metrics, the policy moves."""
+    trainer = _trainer("grpo", [f"actor_rollout_ref.actor.policy_loss.loss_mode={loss_mode}"])
+    w0 = trainer.actor_rollout_wg.worker.actor_store.master.clone() if hasattr(trainer.actor_rollout_wg, "worker") \
+        and hasattr(trainer.actor_rollout_wg.worker, "actor_store") else None
+    m = trainer.fit(num_steps=1)[-1]
+    for k in ["actor/pg_loss", "actor/pg_clipfrac", "actor/ppo_kl", "actor/grad_norm"]:
+        assert k in m and np.isfinite(m[k]), (k, m.get(k))
+    if w0 is not None:
+        assert not torch.equal(w0, trainer.actor_rollout_wg.worker.actor_store.master)

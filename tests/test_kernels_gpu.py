@@ -315,6 +315,61 @@ def test_gpg_actor_loss_matches_reference_golden(golden):
         np.testing.assert_allclose(dent.cpu().numpy(), z[f"c{ci}_out_dentropy"], rtol=2e-5, atol=1e-9)
 
 
+def test_gspo_geo_mean_actor_loss_matches_reference_golden(golden):
+    """The sequence-level losses (policy_loss.loss_mode gspo / geo_mean) through the K1 entry point vs the reference's
+    losses composed into the dp_actor total loss and its autograd gradients (seq_loss.npz): sequence ratios past
+    GSPO's clamp at 10, zero advantages, clip edges, every aggregation mode for the entropy / KL terms."""
+    z, meta = golden("seq_loss.npz")
+    for ci, c in enumerate(meta["cases"]):
+        g = lambda k: T(z[f"c{ci}_{k}"])  # noqa: E731
+        out, dlp, dent = native.ppo_loss_fwd_bwd(
+            g("old_log_prob"), g("log_prob"), g("advantages"), g("response_mask"), g("entropy"), g("ref_log_prob"),
+            clip_ratio_low=c["clip_ratio_low"], clip_ratio_high=c["clip_ratio_high"],
+            entropy_coeff=c["entropy_coeff"], kl_loss_coef=c["kl_loss_coef"], kl_loss_type=c["kl_loss_type"],
+            loss_agg_mode=c["loss_agg_mode"], loss_scale_factor=c["loss_scale_factor"], want_dentropy=True,
+            policy_loss=c["policy_loss"])
+        o = out.cpu().numpy()
+        np.testing.assert_allclose(o[0], z[f"c{ci}_out_pg_loss"], rtol=2e-5, atol=1e-6, err_msg=str(c))
+        np.testing.assert_allclose(o[6], z[f"c{ci}_out_loss"], rtol=2e-5, atol=1e-6, err_msg=str(c))
+        np.testing.assert_allclose(o[[1, 2, 3]], z[f"c{ci}_out_clip"], rtol=2e-5, atol=1e-6, err_msg=str(c))
+        np.testing.assert_allclose(o[4], z[f"c{ci}_out_entropy_loss"], rtol=1e-5, atol=1e-7)
+        np.testing.assert_allclose(o[5], z[f"c{ci}_out_kl_loss"], rtol=1e-5, atol=1e-7)
+        d = z[f"c{ci}_out_dlogp"]
+        np.testing.assert_allclose(dlp.cpu().numpy(), d, rtol=2e-4, atol=1e-6 * np.abs(d).max(), err_msg=str(c))
+        np.testing.assert_allclose(dent.cpu().numpy(), z[f"c{ci}_out_dentropy"], rtol=2e-5, atol=1e-9)
+
+
+@pytest.mark.parametrize("policy", ["gspo", "geo_mean"])
+@pytest.mark.parametrize("mode", ["token-mean", "seq-mean-token-mean"])
+def test_seq_policy_loss_at_size_matches_oracle(policy, mode):
+    """GSPO / GMPO at a micro-batch shape (64 x 1024, ragged rows) vs the oracle; deterministic run to run."""
+    rng = np.random.default_rng(17)
+    B, R = 64, 1024
+    old = (-rng.random((B, R)) * 5).astype(np.float32)
+    lp = (old + rng.standard_normal((B, R)) * 0.05 + rng.standard_normal((B, 1)) * 0.1).astype(np.float32)
+    adv = np.repeat(rng.standard_normal((B, 1)), R, 1).astype(np.float32)
+    mask = (np.arange(R)[None, :] < rng.integers(1, R + 1, (B, 1))).astype(np.int64)
+    ent = rng.random((B, R)).astype(np.float32)
+    ref = (lp + rng.standard_normal((B, R)) * 0.1).astype(np.float32)
+    kw = dict(clip_ratio_low=0.2, clip_ratio_high=0.28, entropy_coeff=0.001, kl_loss_coef=0.001,
+              kl_loss_type="low_var_kl", loss_agg_mode=mode, loss_scale_factor=0.5, want_dentropy=True,
+              policy_loss=policy)
+    out, dlp, dent = native.ppo_loss_fwd_bwd(T(old), T(lp), T(adv), T(mask), T(ent), T(ref), **kw)
+    want = oracle.actor_loss(old, lp, adv, mask, ent, ref, loss_agg_mode=mode, clip_ratio_low=0.2,
+                             clip_ratio_high=0.28, clip_ratio_c=3.0, entropy_coeff=0.001, use_kl_loss=True,
+                             kl_loss_type="low_var_kl", kl_loss_coef=0.001, loss_scale_factor=0.5, policy_loss=policy)
+    o = out.cpu().numpy()
+    np.testing.assert_allclose(o[0], want["pg_loss"], rtol=2e-5, atol=1e-7)
+    np.testing.assert_allclose(o[6], want["loss"], rtol=2e-5, atol=1e-7)
+    np.testing.assert_allclose(o[[1, 2, 3]], [want["pg_clipfrac"], want["ppo_kl"], want["pg_clipfrac_lower"]],
+                               rtol=1e-4, atol=1e-6)
+    d = want["dlogp"]
+    np.testing.assert_allclose(dlp.cpu().numpy(), d, rtol=2e-4, atol=1e-6 * np.abs(d).max())
+    np.testing.assert_allclose(dent.cpu().numpy(), want["dentropy"], rtol=2e-5, atol=1e-12)
+    out2, dlp2, _ = native.ppo_loss_fwd_bwd(T(old), T(lp), T(adv), T(mask), T(ent), T(ref), **kw)
+    assert torch.equal(out, out2) and torch.equal(dlp, dlp2)
+
+
 def test_gae_matches_reference_golden(golden):
     z, meta = golden("gae.npz")
     for ci, cfg in enumerate(meta["cases"]):

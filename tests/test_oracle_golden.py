@@ -46,6 +46,25 @@ def test_gpg_actor_loss_matches_reference(golden):
         assert (g("out_clip") == 0).all()
 
 
+def test_gspo_geo_mean_actor_loss_matches_reference(golden):
+    """The oracle's GSPO / GMPO restatements composed as dp_actor does, against the reference's autograd."""
+    z, meta = golden("seq_loss.npz")
+    for ci, c in enumerate(meta["cases"]):
+        g = lambda k: z[f"c{ci}_{k}"]  # noqa: E731
+        want = oracle.actor_loss(g("old_log_prob"), g("log_prob"), g("advantages"), g("response_mask"), g("entropy"),
+                                 g("ref_log_prob"), loss_agg_mode=c["loss_agg_mode"], clip_ratio_low=c["clip_ratio_low"],
+                                 clip_ratio_high=c["clip_ratio_high"], clip_ratio_c=3.0, entropy_coeff=c["entropy_coeff"],
+                                 use_kl_loss=True, kl_loss_type=c["kl_loss_type"], kl_loss_coef=c["kl_loss_coef"],
+                                 loss_scale_factor=c["loss_scale_factor"], policy_loss=c["policy_loss"])
+        np.testing.assert_allclose(want["pg_loss"], g("out_pg_loss"), rtol=2e-5, atol=1e-6, err_msg=str(c))
+        np.testing.assert_allclose(want["loss"], g("out_loss"), rtol=2e-5, atol=1e-6, err_msg=str(c))
+        np.testing.assert_allclose([want["pg_clipfrac"], want["ppo_kl"], want["pg_clipfrac_lower"]], g("out_clip"),
+                                   rtol=2e-5, atol=1e-6, err_msg=str(c))
+        d = g("out_dlogp")
+        np.testing.assert_allclose(want["dlogp"], d, rtol=2e-4, atol=1e-6 * np.abs(d).max(), err_msg=str(c))
+        np.testing.assert_allclose(want["dentropy"], g("out_dentropy"), rtol=1e-5, atol=1e-9, err_msg=str(c))
+
+
 def test_masked_mean_known_answers(golden):
     z, _ = golden("masked_mean.npz")
     # tests/utils/test_torch_functional.py:55-66 — NaN outside the mask is ignored
