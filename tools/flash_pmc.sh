@@ -1,4 +1,4 @@
-# SQ counter passes over tools/flash_probe.py (one rocprofv3 --pmc run per pass; run through gpurun).
+# SQ counter passes over tools/probes/flash_probe.py (one rocprofv3 --pmc run per pass; run through gpurun).
 set -o pipefail
 ROOT=$(pwd)
 OUT=$ROOT/gpurun_out/fpmc
@@ -8,5 +8,16 @@ i=0
 for pass in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_MFMA" \
             "SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_SALU"; do
   i=$((i+1))
-  timeout -s KILL 90 rocprofv3 --pmc $pass -d "$OUT/p$i" -o run -- python3 "$ROOT/tools/flash_probe.py" 5 > "$OUT/p$i.log" 2>&1 || exit 1
+  timeout -s KILL 90 rocprofv3 --pmc $pass -d "$OUT/p$i" -o run -- python3 "$ROOT/tools/probes/flash_probe.py" 5 > "$OUT/p$i.log" 2>&1 || { tail -5 "$OUT/p$i.log"; exit 1; }
 done
+cd "$ROOT"
+python3 - <<'PY'
+import csv, glob, collections
+acc = collections.defaultdict(list)
+for f in glob.glob("gpurun_out/fpmc/p*/**/*counter_collection.csv", recursive=True):
+    for r in csv.DictReader(open(f)):
+        if "flash_fwd" in r["Kernel_Name"]:
+            acc[r["Counter_Name"]].append(float(r["Counter_Value"]))
+for k, v in sorted(acc.items()):
+    print(f"{k:28s} {sum(v) / len(v):16.1f}  (n={len(v)})")
+PY
