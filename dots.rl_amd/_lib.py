@@ -105,6 +105,8 @@ SIGNATURES = {
     "drl_group_outcome_advantage": (ctypes.c_int, [P, P, I32, P, P, P, I64, I64, I64, I32, F32, I32, P, P, P, SZ, P]),
     "drl_reinforce_pp_advantage_return": (ctypes.c_int, [P, P, I32, I64, I64, F32, P, P, P, SZ, P]),
     "drl_remax_advantage_return": (ctypes.c_int, [P, P, P, I32, I64, I64, P, P, P]),
+    "drl_decode_step_prologue_workspace_bytes": (SZ, []),
+    "drl_decode_step_prologue": (ctypes.c_int, [P, I64, P, P, P, I64, P, I32, I64, I64, I64, P, P, P, P, I64, P, SZ, P]),
     "drl_gae_workspace_bytes": (SZ, [I64, I64]),
     "drl_gae_advantage_return": (ctypes.c_int, [P, P, I32, P, I32, I64, I64, F32, F32, P, P, P, SZ, P]),
     "drl_value_loss_workspace_bytes": (SZ, [I64, I64]),

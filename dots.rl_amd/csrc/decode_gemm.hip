@@ -564,6 +564,43 @@ __global__ __launch_bounds__(256) void dec_rope_kernel(DecRopeArgs a) {
   }
 }
 
+// ------------------------------------------------------------------------------------------- step prologue
+// The per-token bookkeeping of the graphed decode step in one launch (was ~8 torch launches): with t = *t_dev,
+// row b's previous token responses[b, t - 1] -> x[b] = float(embed[token]) (the fp32 residual stream input,
+// F.embedding), pos[b] = last_pos[b] + t (its rotary position), key_valid[b, t + P - 1] = 1 (the new cache
+// slot, index_fill_). The last workgroup to arrive (every other one has read t_dev) publishes *kpos = t + P - 1
+// and *t_cur = t for the rest of the step and advances *t_dev to t + 1 for the next replay.
+__global__ __launch_bounds__(128) void decode_prologue_kernel(const int64_t* responses, int64_t ld_r, int64_t* t_dev,
+                                                              int64_t* t_cur, const int64_t* last_pos, int64_t P,
+                                                              const uint16_t* embed, int64_t V, int64_t H, float* x,
+                                                              int64_t* pos, int64_t* kpos, uint8_t* valid,
+                                                              int64_t ld_valid, unsigned* ticket) {
+  const int64_t b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int64_t t = *t_dev;
+  int64_t tok = responses[b * ld_r + t - 1];
+  tok = tok < 0 ? 0 : (tok >= V ? V - 1 : tok);
+  const uint16_t* e = embed + tok * H;
+  float* xr = x + b * H;
+  for (int64_t c = tid; c < H / 8; c += 128) {
+    const u16x8 v = *reinterpret_cast<const u16x8*>(e + 8 * c);
+    *reinterpret_cast<float4*>(xr + 8 * c) = make_float4(bf16_to_f32(v[0]), bf16_to_f32(v[1]), bf16_to_f32(v[2]),
+                                                         bf16_to_f32(v[3]));
+    *reinterpret_cast<float4*>(xr + 8 * c + 4) = make_float4(bf16_to_f32(v[4]), bf16_to_f32(v[5]),
+                                                             bf16_to_f32(v[6]), bf16_to_f32(v[7]));
+  }
+  if (tid == 0) {
+    pos[b] = last_pos[b] + t;
+    valid[b * ld_valid + t + P - 1] = 1;
+  }
+  if (last_block_ticket(ticket) && tid == 0) {
+    *kpos = t + P - 1;
+    *t_cur = t;
+    *t_dev = t + 1;
+    __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // ------------------------------------------------------------------------------------------- planning
 struct DgPlan {
   int mb, ksw, ksplit, mgroups, tiles, mbt;
@@ -897,6 +934,28 @@ int drl_decode_rope(const float* partials, int32_t nsplit, const void* bias, con
   const int64_t n = B * (Hq + 2 * Hkv) * (D / 2);
   hipLaunchKernelGGL(dec_rope_kernel, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0,
                      static_cast<hipStream_t>(stream), a);
+  DRL_LAUNCH_CHECK();
+  return DRL_OK;
+}
+
+size_t drl_decode_step_prologue_workspace_bytes(void) { return 256; }
+
+int drl_decode_step_prologue(const int64_t* responses, int64_t ld_responses, int64_t* t_dev, int64_t* t_cur,
+                             const int64_t* last_pos, int64_t prompt_len, const void* embed, int32_t dt, int64_t V,
+                             int64_t H, int64_t B, float* x, int64_t* positions, int64_t* kpos, uint8_t* key_valid,
+                             int64_t ld_valid, void* workspace, size_t workspace_bytes, void* stream) {
+  using namespace drl;
+  DRL_CHECK_ARG(responses && t_dev && t_cur && last_pos && embed && x && positions && kpos && key_valid,
+                "NULL input");
+  DRL_CHECK_ARG(dt == DRL_BF16, "the decode step prologue reads a bf16 embedding");
+  DRL_CHECK_ARG(B >= 1 && H >= 8 && H % 8 == 0 && V >= 1 && prompt_len >= 0, "bad shape (H %% 8 == 0)");
+  DRL_CHECK_ARG(aligned16(embed) && aligned16(x), "embedding / x must be 16-byte aligned");
+  if (!workspace || workspace_bytes < drl_decode_step_prologue_workspace_bytes())
+    return fail(DRL_ERR_WORKSPACE, "prologue workspace: need 256 zero-filled bytes");
+  hipLaunchKernelGGL(decode_prologue_kernel, dim3(static_cast<unsigned>(B)), dim3(128), 0,
+                     static_cast<hipStream_t>(stream), responses, ld_responses, t_dev, t_cur, last_pos, prompt_len,
+                     static_cast<const uint16_t*>(embed), V, H, x, positions, kpos, key_valid, ld_valid,
+                     static_cast<unsigned*>(workspace));
   DRL_LAUNCH_CHECK();
   return DRL_OK;
 }

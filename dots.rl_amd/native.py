@@ -773,6 +773,24 @@ def decode_attention_vt(q, k_cache, vt_cache, key_valid, L, out, qpos=None, qpos
     return out
 
 
+def decode_step_prologue(responses, t_dev, t_cur, last_pos, prompt_len, embed, x, positions, kpos, key_valid):
+    """One launch of the graphed decode step's bookkeeping (drl_decode_step_prologue): x = float(embed[previous
+    token]), positions = last_pos + t, key_valid[:, t + P - 1] = 1, kpos = t + P - 1, t_cur = t, t_dev += 1."""
+    _dev(responses, t_dev, t_cur, last_pos, embed, x, positions, kpos, key_valid)
+    assert responses.dtype == t_dev.dtype == t_cur.dtype == last_pos.dtype == positions.dtype == kpos.dtype == torch.int64
+    assert embed.dtype == torch.bfloat16 and embed.is_contiguous() and x.dtype == torch.float32 and x.is_contiguous()
+    assert key_valid.dtype == torch.uint8 and key_valid.stride(1) == 1 and responses.stride(1) == 1
+    B, H = x.shape
+    V = embed.shape[0]
+    assert last_pos.is_contiguous() and last_pos.numel() == B and positions.numel() == B and embed.shape[1] == H
+    L = lib()
+    ws = _linear_workspace(x.device, L.drl_decode_step_prologue_workspace_bytes(), "decode_prologue")
+    check(L.drl_decode_step_prologue(_p(responses), responses.stride(0), _p(t_dev), _p(t_cur), _p(last_pos),
+                                     int(prompt_len), _p(embed), _lib.DRL_BF16, V, H, B, _p(x), _p(positions), _p(kpos),
+                                     _p(key_valid), key_valid.stride(0), _p(ws), ws.numel() * 8, _stream()),
+          "drl_decode_step_prologue")
+
+
 # ------------------------------------------------------------------------------ decode projections (packed)
 DECODE_PARTIAL, DECODE_SWIGLU = 0, 1
 

@@ -768,18 +768,33 @@ class PackedDecode:
         self.x = torch.empty(B, H, device=dev)                         # fp32 residual stream
         self.q = torch.empty(B, Hkv, Hq // Hkv, D, dtype=bf, device=dev)
         self.h_out = torch.empty(B, H, dtype=bf, device=dev)
+        self.pos = torch.empty(B, dtype=torch.int64, device=dev)   # step_from: rotary positions of the new token
+        self.kpos = torch.empty(1, dtype=torch.int64, device=dev)  # step_from: its cache slot
+        self.t_cur = torch.empty(1, dtype=torch.int64, device=dev)  # step_from: the step's t (Philox offset / column)
+
+    @torch.no_grad()
+    def step_from(self, cache, responses, t_dev, last_pos, P):
+        """One graphed decode step driven by the device counter t_dev: the previous token of every row is
+        responses[:, t - 1]; one prologue launch embeds it, sets positions / the cache slot / key_valid, publishes
+        t (self.t_cur, the selection's step) and advances t_dev. Returns the final-norm hidden (B, H)."""
+        native.decode_step_prologue(responses, t_dev, self.t_cur, last_pos.reshape(-1).contiguous(), P,
+                                    self.model.store.w("embed_tokens"), self.x, self.pos, self.kpos, cache.valid)
+        return self._layers(cache, self.pos, self.kpos)
 
     @torch.no_grad()
     def step(self, cache, tokens, positions, kpos_dev):
         """One token per sequence at device cache position kpos_dev; returns the final-norm hidden (B, H)."""
+        s = self.model.store
+        self.x.copy_(F.embedding(tokens.view(-1), s.w("embed_tokens")))
+        cache.valid.index_fill_(1, kpos_dev, 1)
+        return self._layers(cache, positions.view(-1), kpos_dev)
+
+    def _layers(self, cache, pos, kpos_dev):
         m = self.model
         cfg, s = m.cfg, m.store
         B, H, I = self.B, cfg.hidden_size, cfg.intermediate_size
         Hq, Hkv, D = cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim
         eps, mbt = cfg.rms_norm_eps, self.mbt
-        self.x.copy_(F.embedding(tokens.view(-1), s.w("embed_tokens")))
-        cache.valid.index_fill_(1, kpos_dev, 1)
-        pos = positions.view(-1)
         Lk = cache.k[0].shape[2]
         prev = None
         for i in range(cfg.num_hidden_layers):

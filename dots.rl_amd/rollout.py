@@ -119,7 +119,15 @@ class MI355XRollout:
         packed = PackedDecode(m, B) if use else None
         self.last_packed_decode = packed is not None
 
+        prologue = packed is not None and m.store.w("embed_tokens").dtype == torch.bfloat16 and \
+            self.config.get("decode_prologue", True)
+        last_pos_flat = last_pos.reshape(-1).contiguous()
+
         def body():
+            if prologue:  # one launch: embedding, positions, cache slot, key_valid, t_cur, t_dev += 1
+                h = packed.step_from(cache, responses, t_dev, last_pos_flat, P)
+                m.select_tokens(h, responses[:, 0], fused=self._fused_select, step=0, dev_step=packed.t_cur, **sel)
+                return
             tok = responses.index_select(1, t_dev - 1)
             if packed is not None:
                 h = packed.step(cache, tok, last_pos + t_dev, t_dev + (P - 1))

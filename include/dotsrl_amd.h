@@ -403,6 +403,16 @@ int drl_flash_attn_fwd(const void* q, const void* k, const void* vt, int32_t dt,
  * arriving split): workspace of drl_decode_attention_vt_workspace_bytes(B, Hkv, D, L) bytes (0 = none
  * needed), 256-byte aligned, zero-filled before the first call and left zeroed by every call. */
 size_t drl_decode_attention_vt_workspace_bytes(int64_t B, int64_t Hkv, int64_t D, int64_t L);
+/* Graphed decode step prologue (hf_rollout.py:112-124's per-token bookkeeping for a device step counter): with
+ * t = *t_dev, for every row b: x[b, :] = float(embed[responses[b, t - 1], :]) (bf16 embedding (V, H) -> fp32
+ * residual stream), positions[b] = last_pos[b] + t, key_valid[b, t + prompt_len - 1] = 1; then *kpos =
+ * t + prompt_len - 1, *t_cur = t and *t_dev = t + 1 (the last workgroup, after every row has read t_dev).
+ * workspace: drl_decode_step_prologue_workspace_bytes() bytes, zero-filled once (left zeroed by every call). */
+size_t drl_decode_step_prologue_workspace_bytes(void);
+int drl_decode_step_prologue(const int64_t* responses, int64_t ld_responses, int64_t* t_dev, int64_t* t_cur,
+                             const int64_t* last_pos, int64_t prompt_len, const void* embed, int32_t dt, int64_t V,
+                             int64_t H, int64_t B, float* x, int64_t* positions, int64_t* kpos, uint8_t* key_valid,
+                             int64_t ld_valid, void* workspace, size_t workspace_bytes, void* stream);
 /* Tuning hook (tools/kernel_bench.py): force waves per workgroup (2/4/8/16) and key splits; 0 = automatic. */
 void drl_decode_attention_set_plan(int32_t waves, int32_t splits);
 /* Tuning hook for forced plans (set_plan waves != 0): 1 = register-lean key loop (one block in flight per

@@ -227,6 +227,38 @@ def test_packed_rollout_graph_equals_eager():
     assert out.batch["input_ids"].shape == (B, P + R)
 
 
+@pytest.mark.parametrize("do_sample", [False, True])
+def test_decode_prologue_equals_torch_bookkeeping(do_sample):
+    """The graphed step's one-launch prologue (embedding, rotary positions, cache slot, key_valid, step counter)
+    replays exactly what the torch bookkeeping does: identical responses, sampled or greedy, on left-padded prompts
+    (per-row positions) with EOS stops; the device step counter ends at R."""
+    from dots.rl_amd.config import to_attr
+    from dots.rl_amd.protocol import DataProto
+    from dots.rl_amd.rollout import MI355XRollout
+
+    B, P, R = 24, 16, 14
+    cfg, m = _small_model(seed=5)
+    g = torch.Generator(device=DEV).manual_seed(9)
+    ids = torch.randint(3, 512, (B, P), device=DEV, generator=g)
+    am = torch.ones(B, P, dtype=torch.int64, device=DEV)
+    for b in range(0, B, 3):
+        am[b, : (b % 7)] = 0  # left padding
+    ids = torch.where(am == 0, torch.zeros_like(ids), ids)
+    pos = (am.cumsum(-1) - 1).clamp_min(0)
+    outs = []
+    for prologue in (True, False):
+        rcfg = to_attr(dict(do_sample=do_sample, temperature=0.9, top_k=-1, top_p=1.0, response_length=R,
+                            ignore_eos=False, seed=11, val_kwargs={}, use_hip_graph=True, packed_decode=True,
+                            decode_prologue=prologue))
+        ro = MI355XRollout(m, rcfg)
+        out = ro.generate_sequences(DataProto.from_dict({"input_ids": ids, "attention_mask": am, "position_ids": pos},
+                                                        meta_info={"eos_token_id": 2, "pad_token_id": 0}))
+        assert ro.last_packed_decode
+        outs.append(out.batch)
+    for k in ("responses", "attention_mask", "position_ids"):
+        assert torch.equal(outs[0][k], outs[1][k]), k
+
+
 @pytest.mark.parametrize("M,K,Hq,Hkv,D", [(64, 896, 14, 2, 64), (5, 128, 2, 1, 64), (100, 256, 4, 2, 128),
                                            (512, 896, 14, 2, 64), (200, 256, 4, 2, 128)])
 def test_decode_qkv_rope_matches_gemm_then_rope(M, K, Hq, Hkv, D):
