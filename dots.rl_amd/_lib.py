@@ -40,6 +40,11 @@ class PPOLossParams(ctypes.Structure):
         ("kl_type", ctypes.c_int32),
         ("token_count", ctypes.c_void_p),
         ("policy_loss", ctypes.c_int32),
+        ("cov_ratio", ctypes.c_float),
+        ("clip_cov_lb", ctypes.c_float),
+        ("clip_cov_ub", ctypes.c_float),
+        ("ppo_kl_coef", ctypes.c_float),
+        ("cov_seed", ctypes.c_uint64),
     ]
 
 

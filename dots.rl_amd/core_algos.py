@@ -254,7 +254,7 @@ class _FusedActorLoss(torch.autograd.Function):
 
 def fused_actor_loss(log_prob, entropy, old_log_prob, advantages, response_mask, ref_log_prob, *, clip_ratio_low,
                      clip_ratio_high, clip_ratio_c, entropy_coeff, use_kl_loss, kl_loss_type, kl_loss_coef,
-                     loss_agg_mode, loss_scale_factor, policy_loss="vanilla"):
+                     loss_agg_mode, loss_scale_factor, policy_loss="vanilla", cov_kw=None):
     """The whole per-micro-batch loss of dp_actor.py:419-466 in one HIP launch.
 
     Returns a float32[8] tensor: pg_loss, pg_clipfrac, ppo_kl, pg_clipfrac_lower, entropy_loss, kl_loss,
@@ -264,7 +264,7 @@ def fused_actor_loss(log_prob, entropy, old_log_prob, advantages, response_mask,
               entropy_coeff=entropy_coeff if entropy is not None else 0.0,
               kl_loss_coef=kl_loss_coef if use_kl_loss else 0.0,
               kl_loss_type=kl_loss_type if use_kl_loss else None, loss_agg_mode=loss_agg_mode,
-              loss_scale_factor=loss_scale_factor, policy_loss=policy_loss)
+              loss_scale_factor=loss_scale_factor, policy_loss=policy_loss, **(cov_kw or {}))
     return _FusedActorLoss.apply(log_prob, entropy, old_log_prob, advantages, response_mask,
                                  ref_log_prob if use_kl_loss else None, kw)
 
@@ -326,6 +326,47 @@ def compute_policy_loss_geo_mean(old_log_prob, log_prob, advantages, response_ma
                            clip_ratio_high=hi, clip_ratio_c=3.0, entropy_coeff=0.0, use_kl_loss=False,
                            kl_loss_type=None, kl_loss_coef=0.0, loss_agg_mode=loss_agg_mode, loss_scale_factor=1.0,
                            policy_loss="geo_mean")
+    return out[6], out[1].detach(), out[2].detach(), out[3].detach()
+
+
+_COV_SEED = [0]
+
+
+def cov_loss_kw(policy_loss_cfg, mode):
+    """clip_cov / kl_cov knobs from actor.policy_loss (PolicyLossConfig defaults, workers/config/actor.py:45-50) and a
+    fresh subset seed per call (the reference draws clip_cov's subset from torch's global RNG each call)."""
+    pc = policy_loss_cfg or {}
+    get = (lambda k, d: pc.get(k) if pc.get(k) is not None else d)
+    _COV_SEED[0] += 1
+    ratio = get("clip_cov_ratio", 0.0002) if mode == "clip_cov" else get("kl_cov_ratio", 0.0002)
+    return dict(cov_ratio=ratio, clip_cov_lb=get("clip_cov_lb", 1.0), clip_cov_ub=get("clip_cov_ub", 5.0),
+                ppo_kl_coef=get("ppo_kl_coef", 0.1), cov_seed=_COV_SEED[0] * 0x9E3779B97F4A7C15)
+
+
+@register_policy_loss("clip_cov")
+def compute_policy_loss_clip_cov(old_log_prob, log_prob, advantages, response_mask, loss_agg_mode="token-mean",
+                                 config=None):
+    """core_algos.py:978-1069 — PPO clip with the loss of a random subset of high-covariance tokens zeroed (K1's
+    covariance path; the subset is our seeded draw, see include/dotsrl_amd.h)."""
+    assert config is not None and config.get("policy_loss") is not None
+    lo, hi = _clip_lo_hi(config)
+    out = fused_actor_loss(log_prob, None, old_log_prob, advantages, response_mask, None, clip_ratio_low=lo,
+                           clip_ratio_high=hi, clip_ratio_c=3.0, entropy_coeff=0.0, use_kl_loss=False,
+                           kl_loss_type=None, kl_loss_coef=0.0, loss_agg_mode=loss_agg_mode, loss_scale_factor=1.0,
+                           policy_loss="clip_cov", cov_kw=cov_loss_kw(config.policy_loss, "clip_cov"))
+    return out[6], out[1].detach(), out[2].detach(), out[3].detach()
+
+
+@register_policy_loss("kl_cov")
+def compute_policy_loss_kl_cov(old_log_prob, log_prob, advantages, response_mask, loss_agg_mode="token-mean",
+                               config=None):
+    """core_algos.py:1072-1140 — -A r, plus ppo_kl_coef |log_prob - old| on the top-k covariance tokens (K1's
+    covariance path)."""
+    assert config is not None and config.get("policy_loss") is not None
+    out = fused_actor_loss(log_prob, None, old_log_prob, advantages, response_mask, None, clip_ratio_low=0.2,
+                           clip_ratio_high=0.2, clip_ratio_c=3.0, entropy_coeff=0.0, use_kl_loss=False,
+                           kl_loss_type=None, kl_loss_coef=0.0, loss_agg_mode=loss_agg_mode, loss_scale_factor=1.0,
+                           policy_loss="kl_cov", cov_kw=cov_loss_kw(config.policy_loss, "kl_cov"))
     return out[6], out[1].detach(), out[2].detach(), out[3].detach()
 
 

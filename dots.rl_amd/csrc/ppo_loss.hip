@@ -571,7 +571,7 @@ __global__ __launch_bounds__(256) void row_count_kernel(const void* mask, int64_
 int max_grid() { return cu_count() * (DRL_K1_WG_PER_CU > DRL_K1_PACK_WG_PER_CU ? DRL_K1_WG_PER_CU : DRL_K1_PACK_WG_PER_CU); }
 
 struct Layout {
-  size_t partials, rowcnt, counts, bits, seqrow, seqpart, total;
+  size_t partials, rowcnt, counts, bits, seqrow, seqpart, seqsel, total;
 };
 
 Layout ws_layout(int64_t B, int64_t R) {
@@ -583,8 +583,9 @@ Layout ws_layout(int64_t B, int64_t R) {
   L.counts = round_up(L.rowcnt + static_cast<size_t>(B) * sizeof(float), 256);
   L.bits = round_up(L.counts + grid * sizeof(double), 256);
   L.seqrow = round_up(L.bits + nchunks * 16 * sizeof(unsigned long long), 256);
-  L.seqpart = round_up(L.seqrow + static_cast<size_t>(B) * 4 * sizeof(float), 256);
-  L.total = round_up(L.seqpart + static_cast<size_t>(B) * kNumPartials * sizeof(double), 256);
+  L.seqpart = round_up(L.seqrow + static_cast<size_t>(B) * 8 * sizeof(float), 256);
+  L.seqsel = round_up(L.seqpart + static_cast<size_t>(B) * kNumPartials * sizeof(double), 256);
+  L.total = round_up(L.seqsel + 256, 256);
   return L;
 }
 
@@ -697,8 +698,11 @@ struct SeqArgs {
   float* dlp;
   float* dent;
   float* out;
-  float* rowstat;   // (B, 4)
+  float* rowstat;   // (B, 8)
   double* rowpart;  // (B, kNumPartials)
+  unsigned* sel;    // covariance selection: {key threshold, flat-index cutoff at the threshold, take-all flag}
+  float cov_ratio, cov_lb, cov_ub, ppo_kl_coef;
+  uint32_t cov_seed;
   int64_t B, R;
   float lo, hi;          // GSPO: 1 - clip_ratio_low, 1 + clip_ratio_high (ratio space)
   float llo, lhi;        // GMPO: clip_ratio_low, clip_ratio_high (log-ratio space)
@@ -717,12 +721,182 @@ __device__ __forceinline__ void geo_clip(float nak, float A, float llo, float lh
   d = sg * sg * (wa + (1.f - wa) * gc);
 }
 
+// ---- clip_cov / kl_cov token selection (core_algos.py:978-1140). Both rank tokens by the covariance
+// cov = (A - mean A) (log_prob - mean log_prob) over the batch:
+//   kl_cov: means over the valid tokens (plain means of the selected entries); the k = max(1, int(n_valid *
+//   kl_cov_ratio)) largest covariances (torch.topk; equal values at the k-th taken lowest flat index first)
+//   get the loss -A r + ppo_kl_coef |log_prob - old|;
+//   clip_cov: masked means (sum(x m) / (sum(m) + 1e-8)); candidates are valid tokens with lb < cov < ub that the
+//   PPO clip did not already clip; min(clip_num, #candidates) of them (clip_num = max(int(clip_cov_ratio *
+//   sum(m)), 1)) get corr = 0. The reference draws that subset with torch.randperm; here it is the candidates
+//   with the smallest keys of a bijective 32-bit hash of (flat index ^ seed): uniformly random subsets, a
+//   different draw (all candidates when they fit, which is deterministic in both).
+__device__ __forceinline__ uint32_t cov_hash(uint32_t i, uint32_t seed) {  // murmur3 fmix32: a bijection
+  uint32_t h = i ^ seed;
+  h ^= h >> 16; h *= 0x85ebca6bu; h ^= h >> 13; h *= 0xc2b2ae35u; h ^= h >> 16;
+  return h;
+}
+__device__ __forceinline__ uint32_t fkey(float v) {  // order-preserving key of a float
+  const uint32_t b = __float_as_uint(v);
+  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+
+struct CovSel {
+  float mean_a, mean_lp;
+  uint32_t thr, cut;  // threshold key, flat-index cutoff among keys equal to it
+  int all;            // take every eligible token (clip_cov: the candidates fit into clip_num)
+  int none;           // nothing selected
+};
+
+// batch means from the per-row sums (fixed order; every caller computes the same values)
+__device__ __forceinline__ void cov_means(const SeqArgs& a, float& mean_a, float& mean_lp, float& n_valid,
+                                          float& msum) {
+  float s[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int64_t b = 0; b < a.B; ++b) {
+    const float* r = a.rowstat + 8 * b;
+    s[0] += r[4]; s[1] += r[5]; s[2] += r[6]; s[3] += r[0]; s[4] += r[3]; s[5] += r[7];
+  }
+  n_valid = s[0];
+  msum = s[3];
+  if (a.policy == DRL_POLICY_KL_COV) { mean_a = s[1] / s[0]; mean_lp = s[2] / s[0]; }
+  else { mean_a = s[4] / (s[3] + 1e-8f); mean_lp = s[5] / (s[3] + 1e-8f); }
+}
+
+// eligibility and ranking key of token i (larger key = picked first)
+__device__ __forceinline__ bool cov_key(const SeqArgs& a, float mean_a, float mean_lp, int64_t i, float A, float lpv,
+                                        float nak, float r, float m, uint32_t& key) {
+  if (!(m > 0.f)) return false;
+  const float c = (A - mean_a) * (lpv - mean_lp);
+  if (a.policy == DRL_POLICY_KL_COV) { key = fkey(c); return true; }
+  const float negA = -A;
+  const float L1 = negA * r, L2 = negA * fminf(fmaxf(r, a.lo), a.hi);
+  if (L2 > L1) return false;  // clip_by_origin
+  if (!(c < a.cov_ub && c > a.cov_lb)) return false;
+  key = ~cov_hash(static_cast<uint32_t>(i), a.cov_seed);  // smallest hash first
+  return true;
+}
+
+__device__ __forceinline__ CovSel cov_selection(const SeqArgs& a) {
+  CovSel cs{};
+  float nv, msum;
+  cov_means(a, cs.mean_a, cs.mean_lp, nv, msum);
+  cs.thr = a.sel[0]; cs.cut = a.sel[1]; cs.all = static_cast<int>(a.sel[2] & 1u); cs.none = static_cast<int>(a.sel[2] >> 1);
+  return cs;
+}
+
+__device__ __forceinline__ bool cov_picked(const SeqArgs& a, const CovSel& cs, int64_t i, float A, float lpv, float nak,
+                                           float r, float m) {
+  if (cs.none) return false;
+  uint32_t key;
+  if (!cov_key(a, cs.mean_a, cs.mean_lp, i, A, lpv, nak, r, m, key)) return false;
+  if (cs.all) return true;
+  return key > cs.thr || (key == cs.thr && static_cast<uint32_t>(i) <= cs.cut);
+}
+
+// One workgroup: the k-th largest key over the eligible tokens by an 8-bit radix select (4 passes, integer LDS
+// histograms: deterministic), then the flat-index cutoff among the tokens equal to it (contiguous thread ranges +
+// an exclusive scan). Writes sel = {threshold, cutoff, flags}.
+__global__ __launch_bounds__(256) void cov_select_kernel(SeqArgs a, const void* mask, int mdt) {
+  const int tid = threadIdx.x;
+  __shared__ unsigned hist[256];
+  __shared__ unsigned s_prefix, s_need;
+  __shared__ unsigned s_cnt[256];
+  float mean_a, mean_lp, nv, msum;
+  cov_means(a, mean_a, mean_lp, nv, msum);
+  const int64_t N = a.B * a.R;
+  auto mask_of = [&](int64_t i) -> float {
+    switch (mdt) {
+      case DRL_I64: return mask_at<DRL_I64>(mask, i);
+      case DRL_I32: return mask_at<DRL_I32>(mask, i);
+      case DRL_U8: return mask_at<DRL_U8>(mask, i);
+      default: return mask_at<DRL_F32>(mask, i);
+    }
+  };
+  auto key_at = [&](int64_t i, uint32_t& key) -> bool {
+    const float lpv = a.lp[i], nak = lpv - a.old_lp[i];
+    return cov_key(a, mean_a, mean_lp, i, a.adv[i], lpv, nak, expf(nak), mask_of(i), key);
+  };
+  // how many to take
+  unsigned cnt = 0;
+  for (int64_t i = tid; i < N; i += 256) { uint32_t k; cnt += key_at(i, k) ? 1u : 0u; }
+  s_cnt[tid] = cnt;
+  __syncthreads();
+  if (tid == 0) {
+    unsigned tot = 0;
+    for (int t = 0; t < 256; ++t) tot += s_cnt[t];
+    unsigned need;
+    if (a.policy == DRL_POLICY_KL_COV) {
+      const unsigned kk = static_cast<unsigned>(static_cast<double>(nv) * static_cast<double>(a.cov_ratio));
+      need = nv > 0.f ? (kk > 1u ? kk : 1u) : 0u;
+    } else {
+      const unsigned cn = static_cast<unsigned>(static_cast<double>(a.cov_ratio) * static_cast<double>(msum));
+      need = cn > 1u ? cn : 1u;
+    }
+    unsigned flags = 0;
+    if (need == 0 || tot == 0) flags = 2u;             // none
+    else if (need >= tot) flags = 1u;                  // all eligible
+    a.sel[2] = flags;
+    s_need = (flags == 0) ? need : 0u;
+  }
+  __syncthreads();
+  unsigned need = s_need;
+  if (need == 0) return;  // uniform
+  // radix select of the need-th largest key
+  uint32_t prefix = 0;
+  for (int pass = 0; pass < 4; ++pass) {
+    const int shift = 24 - 8 * pass;
+    hist[tid] = 0;
+    __syncthreads();
+    for (int64_t i = tid; i < N; i += 256) {
+      uint32_t k;
+      if (!key_at(i, k)) continue;
+      if (pass > 0 && (k >> (shift + 8)) != prefix) continue;
+      atomicAdd(&hist[(k >> shift) & 0xFFu], 1u);
+    }
+    __syncthreads();
+    if (tid == 0) {
+      unsigned above = 0;
+      int b = 255;
+      for (; b > 0; --b) {
+        if (above + hist[b] >= need) break;
+        above += hist[b];
+      }
+      s_prefix = (prefix << 8) | static_cast<uint32_t>(b);
+      s_need = need - above;
+    }
+    __syncthreads();
+    prefix = s_prefix;
+    need = s_need;
+    __syncthreads();
+  }
+  // prefix = threshold key; take `need` of the tokens equal to it, lowest flat index first
+  const int64_t per = (N + 255) / 256, lo = tid * per, hi = lo + per < N ? lo + per : N;
+  unsigned eq = 0;
+  for (int64_t i = lo; i < hi; ++i) { uint32_t k; eq += (key_at(i, k) && k == prefix) ? 1u : 0u; }
+  s_cnt[tid] = eq;
+  __syncthreads();
+  if (tid == 0) {
+    unsigned run = 0;
+    for (int t = 0; t < 256; ++t) { const unsigned c = s_cnt[t]; s_cnt[t] = run; run += c; }
+  }
+  __syncthreads();
+  const unsigned before = s_cnt[tid];
+  if (before < need && before + eq >= need) {
+    unsigned seen = before;
+    for (int64_t i = lo; i < hi; ++i) {
+      uint32_t k;
+      if (key_at(i, k) && k == prefix && ++seen == need) { a.sel[1] = static_cast<unsigned>(i); break; }
+    }
+  }
+  if (tid == 0) a.sel[0] = prefix;
+}
+
 template <int MDT>
 __global__ __launch_bounds__(256) void seq_row_kernel(SeqArgs a) {
   const int64_t row = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= a.B) return;
-  float c = 0.f, sk = 0.f, sm = 0.f, sa = 0.f;
+  float c = 0.f, sk = 0.f, sm = 0.f, sa = 0.f, nv = 0.f, sav = 0.f, slv = 0.f, slm = 0.f;
   for (int64_t t = lane; t < a.R; t += 64) {
     const int64_t i = row * a.R + t;
     const float m = mask_at<MDT>(a.mask, i);
@@ -733,12 +907,16 @@ __global__ __launch_bounds__(256) void seq_row_kernel(SeqArgs a) {
       float v, d;
       geo_clip(nak, a.adv[i], a.llo, a.lhi, v, d);
       sm += v * m;
-      sa += a.adv[i] * m;
     }
+    sa += a.adv[i] * m;
+    slm += a.lp[i] * m;
+    if (m > 0.f) { nv += 1.f; sav += a.adv[i]; slv += a.lp[i]; }  // kl_cov: plain means over the valid tokens
   }
   c = wave_sum(c); sk = wave_sum(sk); sm = wave_sum(sm); sa = wave_sum(sa);
+  nv = wave_sum(nv); sav = wave_sum(sav); slv = wave_sum(slv); slm = wave_sum(slm);
   if (lane == 0) {
-    a.rowstat[4 * row] = c; a.rowstat[4 * row + 1] = sk; a.rowstat[4 * row + 2] = sm; a.rowstat[4 * row + 3] = sa;
+    float* r = a.rowstat + 8 * row;
+    r[0] = c; r[1] = sk; r[2] = sm; r[3] = sa; r[4] = nv; r[5] = sav; r[6] = slv; r[7] = slm;
   }
 }
 
@@ -750,26 +928,30 @@ __global__ __launch_bounds__(256) void seq_token_kernel(SeqArgs a) {
   __shared__ double red[4][kNumPartials];
   // sum(mask) over the whole micro-batch (token-mean weights), the same fixed order in every workgroup
   float c = 0.f;
-  for (int64_t b = tid; b < a.B; b += 256) c += a.rowstat[4 * b];
+  for (int64_t b = tid; b < a.B; b += 256) c += a.rowstat[8 * b];
   c = wave_sum(c);
   if (lane == 0) s_cnt[wave] = c;
   __syncthreads();
   const float cnt = (s_cnt[0] + s_cnt[1]) + (s_cnt[2] + s_cnt[3]);
   const float inv_denom_tm = 1.0f / (cnt + 1e-8f);
-  const float rowcnt = a.rowstat[4 * row];
+  const float rowcnt = a.rowstat[8 * row];
   const float inv_B = 1.0f / static_cast<float>(a.B), inv_R = 1.0f / static_cast<float>(a.R);
   const bool tm = a.mode == DRL_AGG_TOKEN_MEAN, smtm = a.mode == DRL_AGG_SEQ_MEAN_TOKEN_MEAN;
   const bool gspo = a.policy == DRL_POLICY_GSPO;
+  const bool cov = a.policy == DRL_POLICY_CLIP_COV || a.policy == DRL_POLICY_KL_COV;
   // per-row scalars
-  float ratio, gate = 1.f, geo_scale = 0.f, pg_row = 0.f;
-  if (gspo) {  // seq log-ratio = sum(nak * mask) / clamp(len, 1), clamped at 10 (clamp passes the gradient at 10)
-    const float seq_kl = a.rowstat[4 * row + 1] / fmaxf(rowcnt, 1.f);
+  float ratio = 1.f, gate = 1.f, geo_scale = 0.f, pg_row = 0.f;
+  CovSel cs{};
+  if (cov) {
+    cs = cov_selection(a);
+  } else if (gspo) {  // seq log-ratio = sum(nak * mask) / clamp(len, 1), clamped at 10 (clamp passes the gradient at 10)
+    const float seq_kl = a.rowstat[8 * row + 1] / fmaxf(rowcnt, 1.f);
     gate = seq_kl <= 10.f ? 1.f : 0.f;
     ratio = expf(fminf(seq_kl, 10.f));
   } else {  // GMPO: exp(mean clipped log-ratio), mean advantage; pg_row = -adv * ratio
     const float msum = rowcnt + 1e-8f;
-    ratio = expf(a.rowstat[4 * row + 2] / msum);
-    const float adv = a.rowstat[4 * row + 3] / msum;
+    ratio = expf(a.rowstat[8 * row + 2] / msum);
+    const float adv = a.rowstat[8 * row + 3] / msum;
     pg_row = -adv * ratio;
     geo_scale = ((-adv * ratio) / msum) * inv_B;  // d pg_loss / d nak_min_t = geo_scale * mask_t
   }
@@ -791,7 +973,29 @@ __global__ __launch_bounds__(256) void seq_token_kernel(SeqArgs a) {
       return x * mj;
     };
     float dpg;
-    if (gspo) {  // PPO clip on the sequence ratio, no dual clip; pg aggregated seq-mean-token-mean
+    if (cov) {  // token-level: ratio = exp(log_prob - old) unclamped, pg aggregated by loss_agg_mode
+      const float r = expf(nak);
+      const float negA = -A;
+      const float L1 = negA * r;
+      const bool picked = cov_picked(a, cs, i, A, lpv, nak, r, mj);
+      if (a.policy == DRL_POLICY_KL_COV) {  // picked tokens: -A r + ppo_kl_coef |nak|
+        const float pg = picked ? L1 + a.ppo_kl_coef * fabsf(nak) : L1;
+        dpg = w * (negA * r + (picked ? a.ppo_kl_coef * (nak > 0.f ? 1.f : (nak < 0.f ? -1.f : 0.f)) : 0.f));
+        S[0] += agg_val(pg);
+        S[2] += mb ? fabsf(nak) * mj : 0.f;  // ppo_kl reported as masked_mean(|nak|)
+      } else {  // clip_cov: PPO clip (no dual clip), picked tokens' loss zeroed (corr = 0)
+        const float rc = fminf(fmaxf(r, a.lo), a.hi);
+        const float gc = (r >= a.lo && r <= a.hi) ? 1.f : 0.f;
+        const float L2 = negA * rc;
+        const float corr = picked ? 0.f : 1.f;
+        const float pg = fmaxf(L1, L2) * corr;
+        const float w1 = L1 > L2 ? 1.f : (L1 == L2 ? 0.5f : 0.f);
+        dpg = w * corr * ((w1 + (1.f - w1) * gc) * negA * r);
+        S[0] += agg_val(pg);
+        S[1] += (mb && picked) ? mj : 0.f;  // pg_clipfrac = masked_mean(corr == 0)
+        S[2] += mb ? -nak * mj : 0.f;
+      }
+    } else if (gspo) {  // PPO clip on the sequence ratio, no dual clip; pg aggregated seq-mean-token-mean
       const float negA = -A;
       const float L1 = negA * ratio;
       const float rc = fminf(fmaxf(ratio, a.lo), a.hi);
@@ -811,7 +1015,7 @@ __global__ __launch_bounds__(256) void seq_token_kernel(SeqArgs a) {
       S[1] += (mb && clipped && A > 0.f) ? mj : 0.f;
       S[3] += (mb && clipped && A < 0.f) ? mj : 0.f;
     }
-    S[2] += mb ? -nak * mj : 0.f;
+    if (!cov) S[2] += mb ? -nak * mj : 0.f;
     S[6] += mj;
     float gl = dpg;
     if (a.kl != DRL_KL_NONE) {
@@ -824,7 +1028,7 @@ __global__ __launch_bounds__(256) void seq_token_kernel(SeqArgs a) {
     if (a.dlp != nullptr) a.dlp[i] = a.lsf * gl;
     if (a.dent != nullptr) a.dent[i] = a.ent_coef != 0.f ? a.lsf * (-a.ent_coef * w) : 0.f;
   }
-  if (!gspo && tid == 0) S[0] = pg_row;  // GMPO: one sequence-level term per row
+  if (!gspo && !cov && tid == 0) S[0] = pg_row;  // GMPO: one sequence-level term per row
 #pragma unroll
   for (int k = 0; k < kNumPartials; ++k) {
     const double v = wave_sum(static_cast<double>(S[k]));
@@ -855,7 +1059,9 @@ __global__ __launch_bounds__(256) void seq_final_kernel(SeqArgs a) {
     if (a.mode == DRL_AGG_SEQ_MEAN_TOKEN_SUM || a.mode == DRL_AGG_SEQ_MEAN_TOKEN_MEAN) return x / static_cast<double>(a.B);
     return x / static_cast<double>(a.R);
   };
-  const double pg_loss = r[0] / static_cast<double>(a.B);  // GSPO: seq-mean of token-means; GMPO: mean over rows
+  const bool cov = a.policy == DRL_POLICY_CLIP_COV || a.policy == DRL_POLICY_KL_COV;
+  // GSPO: seq-mean of token-means; GMPO: mean over rows; clip_cov / kl_cov: agg_loss(loss_agg_mode)
+  const double pg_loss = cov ? agg(r[0]) : r[0] / static_cast<double>(a.B);
   const bool has_ent = a.ent != nullptr, has_kl = a.kl != DRL_KL_NONE;
   const double ent_loss = has_ent ? agg(r[4]) : 0.0;
   const double kl_loss = has_kl ? agg(r[5]) : 0.0;
@@ -876,6 +1082,10 @@ template <int MDT>
 int launch_seq(const SeqArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(seq_row_kernel<MDT>, dim3(static_cast<unsigned>((a.B + 3) / 4)), dim3(256), 0, s, a);
   DRL_LAUNCH_CHECK();
+  if (a.policy == DRL_POLICY_CLIP_COV || a.policy == DRL_POLICY_KL_COV) {
+    hipLaunchKernelGGL(cov_select_kernel, dim3(1), dim3(256), 0, s, a, a.mask, MDT);
+    DRL_LAUNCH_CHECK();
+  }
   hipLaunchKernelGGL(seq_token_kernel<MDT>, dim3(static_cast<unsigned>(a.B)), dim3(256), 0, s, a);
   DRL_LAUNCH_CHECK();
   hipLaunchKernelGGL(seq_final_kernel, dim3(1), dim3(256), 0, s, a);
@@ -905,7 +1115,7 @@ int drl_ppo_loss_fwd_bwd(const float* old_log_prob, const float* log_prob, const
   DRL_CHECK_ARG(p->entropy_coeff == 0.f || entropy != nullptr, "entropy_coeff != 0 but entropy is NULL");
   DRL_CHECK_ARG(p->policy_loss != DRL_POLICY_VANILLA || p->clip_ratio_c > 1.f,
                 "clip_ratio_c must be > 1.0 (dual-clip PPO), got %f", p->clip_ratio_c);
-  DRL_CHECK_ARG(p->policy_loss >= DRL_POLICY_VANILLA && p->policy_loss <= DRL_POLICY_GEO_MEAN, "bad policy_loss %d",
+  DRL_CHECK_ARG(p->policy_loss >= DRL_POLICY_VANILLA && p->policy_loss <= DRL_POLICY_KL_COV, "bad policy_loss %d",
                 p->policy_loss);
   DRL_CHECK_ARG(mask_dtype == DRL_I64 || mask_dtype == DRL_I32 || mask_dtype == DRL_U8 || mask_dtype == DRL_F32,
                 "unsupported mask dtype %d", mask_dtype);
@@ -916,7 +1126,7 @@ int drl_ppo_loss_fwd_bwd(const float* old_log_prob, const float* log_prob, const
     return fail(DRL_ERR_WORKSPACE, "workspace %zu < %zu bytes", workspace_bytes, L.total);
 
   auto* ws = static_cast<char*>(workspace);
-  if (p->policy_loss == DRL_POLICY_GSPO || p->policy_loss == DRL_POLICY_GEO_MEAN) {
+  if (p->policy_loss >= DRL_POLICY_GSPO) {
     SeqArgs q{};
     q.old_lp = old_log_prob; q.lp = log_prob; q.adv = advantages; q.mask = response_mask;
     q.ent = entropy; q.ref = p->kl_type == DRL_KL_NONE ? nullptr : ref_log_prob;
@@ -929,6 +1139,11 @@ int drl_ppo_loss_fwd_bwd(const float* old_log_prob, const float* log_prob, const
     q.llo = p->clip_ratio_low; q.lhi = p->clip_ratio_high;
     q.ent_coef = p->entropy_coeff; q.kl_coef = p->kl_loss_coef; q.lsf = p->loss_scale_factor;
     q.mode = p->loss_agg_mode; q.kl = p->kl_type; q.policy = p->policy_loss;
+    q.sel = reinterpret_cast<unsigned*>(ws + L.seqsel);
+    q.cov_ratio = p->cov_ratio; q.cov_lb = p->clip_cov_lb; q.cov_ub = p->clip_cov_ub; q.ppo_kl_coef = p->ppo_kl_coef;
+    q.cov_seed = static_cast<uint32_t>(p->cov_seed ^ (p->cov_seed >> 32));
+    DRL_CHECK_ARG(p->policy_loss < DRL_POLICY_CLIP_COV || p->cov_ratio > 0.f, "clip_cov / kl_cov ratio must be > 0");
+    DRL_CHECK_ARG(B * R < (int64_t(1) << 32), "clip_cov / kl_cov: more than 2^32 tokens");
     hipStream_t s = static_cast<hipStream_t>(stream);
     switch (mask_dtype) {
       case DRL_I64: return launch_seq<DRL_I64>(q, s);

@@ -16,7 +16,7 @@ import torch
 import torch.distributed as dist
 
 from . import native
-from .core_algos import fused_actor_loss
+from .core_algos import cov_loss_kw, fused_actor_loss
 from .protocol import DataProto
 from .seqlen_balancing import prepare_dynamic_batch, restore_dynamic_batch
 from .qwen2 import Qwen2Model
@@ -234,9 +234,9 @@ class DataParallelPPOActor:
         data = data.select(batch_keys=keys)
         mini_batches = data.split(cfg.ppo_mini_batch_size)
         loss_mode = cfg.policy_loss.get("loss_mode", "vanilla")
-        if loss_mode not in ("vanilla", "gpg", "gspo", "geo_mean"):
+        if loss_mode not in ("vanilla", "gpg", "gspo", "geo_mean", "clip_cov", "kl_cov"):
             raise NotImplementedError(f"policy loss {loss_mode}: the fused K1 modes are vanilla (PPO clip + dual clip), "
-                                      "gpg, gspo and geo_mean (clip_cov / kl_cov are not built)")
+                                      "gpg, gspo, geo_mean, clip_cov and kl_cov")
         lo = cfg.clip_ratio_low if cfg.get("clip_ratio_low") is not None else cfg.clip_ratio
         hi = cfg.clip_ratio_high if cfg.get("clip_ratio_high") is not None else cfg.clip_ratio
         mb_out, mb_lsf, grad_norms = [], [], []
@@ -263,7 +263,8 @@ class DataParallelPPOActor:
                         mb.get("ref_log_prob"), clip_ratio_low=lo, clip_ratio_high=hi,
                         clip_ratio_c=cfg.get("clip_ratio_c", 3.0), entropy_coeff=cfg.entropy_coeff,
                         use_kl_loss=cfg.use_kl_loss, kl_loss_type=cfg.kl_loss_type, kl_loss_coef=cfg.kl_loss_coef,
-                        loss_agg_mode=cfg.loss_agg_mode, loss_scale_factor=lsf, policy_loss=loss_mode)
+                        loss_agg_mode=cfg.loss_agg_mode, loss_scale_factor=lsf, policy_loss=loss_mode,
+                        cov_kw=cov_loss_kw(cfg.policy_loss, loss_mode) if loss_mode in ("clip_cov", "kl_cov") else None)
                     out[6].backward()
                     mb_out.append(out.detach())
                     mb_lsf.append(lsf)

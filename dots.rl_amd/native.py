@@ -152,7 +152,8 @@ def ppo_loss_fwd_bwd(old_log_prob, log_prob, advantages, response_mask, entropy=
                      clip_ratio_low=0.2, clip_ratio_high=0.2, clip_ratio_c=3.0, entropy_coeff=0.0,
                      kl_loss_coef=0.0, kl_loss_type=None, loss_agg_mode="token-mean", loss_scale_factor=1.0,
                      want_dlogp=True, want_dentropy=False, out=None, dlogp=None, dentropy=None, token_count=None,
-                     policy_loss="vanilla"):
+                     policy_loss="vanilla", cov_ratio=0.0002, clip_cov_lb=1.0, clip_cov_ub=5.0, ppo_kl_coef=0.1,
+                     cov_seed=0):
     """One launch: the 8 loss scalars (see DRL_PPO_OUT_*) and d loss / d log_prob, d loss / d entropy.
     ``token_count`` (token-mean): device float64 scalar = response_mask.sum() when the caller already has
     it; K1 then makes one pass over HBM instead of two."""
@@ -165,7 +166,9 @@ def ppo_loss_fwd_bwd(old_log_prob, log_prob, advantages, response_mask, entropy=
     prm = _lib.PPOLossParams(clip_ratio_low, clip_ratio_high, clip_ratio_c, entropy_coeff, kl_loss_coef,
                              loss_scale_factor, _lib.AGG_MODES[loss_agg_mode],
                              _lib.KL_NONE if kl_loss_type is None else _lib.KL_TYPES[kl_loss_type], None,
-                             {"vanilla": 0, "gpg": 1, "gspo": 2, "geo_mean": 3}[policy_loss])
+                             {"vanilla": 0, "gpg": 1, "gspo": 2, "geo_mean": 3, "clip_cov": 4, "kl_cov": 5}[policy_loss],
+                             float(cov_ratio), float(clip_cov_lb), float(clip_cov_ub), float(ppo_kl_coef),
+                             int(cov_seed) & 0xFFFFFFFFFFFFFFFF)
     if token_count is not None:
         _dev(token_count)
         assert token_count.dtype == torch.float64 and token_count.numel() == 1

@@ -101,11 +101,25 @@ typedef struct drl_ppo_loss_params {
    * pg_clipfrac_lower 0), DRL_POLICY_GEO_MEAN = compute_policy_loss_geo_mean (:1143-1210, GMPO: log-ratios clipped
    * to [-clip_ratio_low, clip_ratio_high] toward sign(A), geometric-mean ratio and mean advantage per row, pg =
    * mean over rows). The two sequence-level losses run as three small launches (per-row sums, per-token terms,
-   * row fold) instead of K1's stream, and ignore token_count and clip_ratio_c. */
+   * row fold) instead of K1's stream, and ignore token_count and clip_ratio_c.
+   * DRL_POLICY_CLIP_COV = compute_policy_loss_clip_cov (:978-1069) and DRL_POLICY_KL_COV = compute_policy_loss_kl_cov
+   * (:1072-1140): token covariances (A - mean A)(log_prob - mean log_prob) over the micro-batch select tokens by a
+   * one-workgroup radix select — kl_cov: the max(1, int(n_valid * cov_ratio)) largest (lowest flat index first
+   * among equal values) get -A r + ppo_kl_coef |log_prob - old| (ratio r = exp(log_prob - old), unclamped);
+   * clip_cov: of the valid, not already clipped tokens with clip_cov_lb < cov < clip_cov_ub, min(max(1,
+   * int(cov_ratio * sum(mask))), #candidates) get their clipped loss zeroed — the reference draws that subset with
+   * torch.randperm, here the candidates with the smallest fmix32(flat index ^ seed) (a uniformly random subset on
+   * cov_seed; every candidate when they fit). */
   int32_t policy_loss;
+  float cov_ratio;    /* policy_loss.clip_cov_ratio / kl_cov_ratio */
+  float clip_cov_lb;  /* policy_loss.clip_cov_lb */
+  float clip_cov_ub;  /* policy_loss.clip_cov_ub */
+  float ppo_kl_coef;  /* policy_loss.ppo_kl_coef */
+  uint64_t cov_seed;  /* clip_cov's subset draw */
 } drl_ppo_loss_params;
 
-enum { DRL_POLICY_VANILLA = 0, DRL_POLICY_GPG = 1, DRL_POLICY_GSPO = 2, DRL_POLICY_GEO_MEAN = 3 };
+enum { DRL_POLICY_VANILLA = 0, DRL_POLICY_GPG = 1, DRL_POLICY_GSPO = 2, DRL_POLICY_GEO_MEAN = 3, DRL_POLICY_CLIP_COV = 4,
+       DRL_POLICY_KL_COV = 5 };
 
 enum {
   DRL_PPO_OUT_PG_LOSS = 0,

@@ -237,17 +237,108 @@ def policy_loss_geo_mean(old_log_prob, log_prob, advantages, response_mask, clip
             masked_mean(clipped * (A < 0), response_mask), dpg)
 
 
+def fmix32(x):
+    """murmur3's 32-bit finalizer (a bijection), vectorised over uint32 — clip_cov's subset ranking."""
+    h = np.asarray(x, np.uint64) & np.uint64(0xFFFFFFFF)
+    h ^= h >> np.uint64(16)
+    h = (h * np.uint64(0x85EBCA6B)) & np.uint64(0xFFFFFFFF)
+    h ^= h >> np.uint64(13)
+    h = (h * np.uint64(0xC2B2AE35)) & np.uint64(0xFFFFFFFF)
+    h ^= h >> np.uint64(16)
+    return h.astype(np.uint32)
+
+
+def policy_loss_kl_cov(old_log_prob, log_prob, advantages, response_mask, loss_agg_mode="token-mean",
+                       kl_cov_ratio=0.0002, ppo_kl_coef=0.1):
+    """compute_policy_loss_kl_cov (core_algos.py:1072-1140): pg = -A r (r = exp(log_prob - old), unclamped), plus
+    ppo_kl_coef |log_prob - old| on the max(1, int(n_valid * kl_cov_ratio)) valid tokens with the largest
+    covariance (A - mean A)(log_prob - mean log_prob) (means over the valid tokens; equal values: lowest flat index
+    first). Returns (pg_loss, 0, ppo_kl = masked_mean(|nak|), 0, d pg_loss / d log_prob)."""
+    f32 = np.float32
+    nak = np.asarray(log_prob, f32) - np.asarray(old_log_prob, f32)
+    r = np.exp(nak.astype(f64)).astype(f32)
+    A = np.asarray(advantages, f32)
+    lp = np.asarray(log_prob, f32)
+    valid = np.asarray(response_mask) > 0
+    pg = (-A * r).astype(f64)
+    dpg = (-A * r).astype(f64)
+    n = int(valid.sum())
+    if n > 0:
+        ma = f32(A[valid].astype(f64).mean())
+        ml = f32(lp[valid].astype(f64).mean())
+        flat = np.flatnonzero(valid.reshape(-1))
+        cov = ((A.reshape(-1)[flat] - ma) * (lp.reshape(-1)[flat] - ml)).astype(f32)
+        k = max(1, int(n * kl_cov_ratio))
+        pick = flat[np.argsort(-cov.astype(f64), kind="stable")[:k]]
+        nk = nak.reshape(-1)
+        pg.reshape(-1)[pick] += ppo_kl_coef * np.abs(nk[pick])
+        dpg.reshape(-1)[pick] += ppo_kl_coef * np.sign(nk[pick])
+    pg_loss = agg_loss(pg, response_mask, loss_agg_mode)
+    return pg_loss, 0.0, masked_mean(np.abs(nak).astype(f64), response_mask), 0.0, \
+        dpg * agg_loss_grad(response_mask, loss_agg_mode)
+
+
+def policy_loss_clip_cov(old_log_prob, log_prob, advantages, response_mask, loss_agg_mode="token-mean",
+                         clip_ratio_low=0.2, clip_ratio_high=0.2, clip_cov_ratio=0.0002, clip_cov_lb=1.0,
+                         clip_cov_ub=5.0, cov_seed=0, return_selected=False):
+    """compute_policy_loss_clip_cov (core_algos.py:978-1069): PPO clip (no dual clip) with corr = 0 on
+    min(clip_num, #candidates) candidates (valid, not clipped by the PPO clip, lb < cov < ub; cov with masked means),
+    clip_num = max(int(clip_cov_ratio * sum(mask)), 1). The reference draws the subset with torch.randperm; the HIP
+    path (and this restatement) takes the candidates with the smallest fmix32(flat index ^ seed32) — the same
+    result whenever every candidate fits. Returns (pg_loss, pg_clipfrac, ppo_kl, 0, d pg_loss / d log_prob)."""
+    f32 = np.float32
+    nak = np.asarray(log_prob, f32) - np.asarray(old_log_prob, f32)
+    r = np.exp(nak.astype(f64)).astype(f32)
+    A = np.asarray(advantages, f32)
+    lp = np.asarray(log_prob, f32)
+    m32 = np.asarray(response_mask, f32)
+    L1 = -A * r
+    lo, hi = f32(1.0 - clip_ratio_low), f32(1.0 + clip_ratio_high)
+    L2 = -A * np.clip(r, lo, hi)
+    gc = ((r >= lo) & (r <= hi)).astype(f64)
+    msum = m32.sum()
+    ma = f32((A * m32).sum() / (msum + f32(1e-8)))
+    ml = f32((lp * m32).sum() / (msum + f32(1e-8)))
+    cov = ((A - ma) * (lp - ml)).astype(f32)
+    cand = (m32 > 0) & ~(L2 > L1) & (cov < f32(clip_cov_ub)) & (cov > f32(clip_cov_lb))
+    clip_num = max(int(clip_cov_ratio * float(msum)), 1)
+    flat = np.flatnonzero(cand.reshape(-1))
+    if len(flat) > clip_num:
+        seed32 = (cov_seed ^ (cov_seed >> 32)) & 0xFFFFFFFF
+        flat = flat[np.argsort(fmix32(flat.astype(np.uint64) ^ np.uint64(seed32)), kind="stable")[:clip_num]]
+    sel = np.zeros(A.size, bool)
+    sel[flat] = True
+    sel = sel.reshape(A.shape)
+    corr = (~sel).astype(f64)
+    w1, w2 = _max_grad(L1, L2)
+    pg = np.maximum(L1, L2).astype(f64) * corr
+    dpg = corr * (w1 + w2 * gc) * (-A.astype(f64)) * r.astype(f64)
+    pg_loss = agg_loss(pg, response_mask, loss_agg_mode)
+    out = (pg_loss, masked_mean(sel.astype(f64), response_mask), masked_mean(-nak.astype(f64), response_mask), 0.0,
+           dpg * agg_loss_grad(response_mask, loss_agg_mode))
+    return out + (sel,) if return_selected else out
+
+
 def actor_loss(old_log_prob, log_prob, advantages, response_mask, entropy, ref_log_prob, *, loss_agg_mode,
                clip_ratio_low, clip_ratio_high, clip_ratio_c, entropy_coeff, use_kl_loss, kl_loss_type,
-               kl_loss_coef, loss_scale_factor, policy_loss="vanilla"):
+               kl_loss_coef, loss_scale_factor, policy_loss="vanilla", cov_ratio=0.0002, clip_cov_lb=1.0,
+               clip_cov_ub=5.0, ppo_kl_coef=0.1, cov_seed=0):
     """The per-micro-batch loss of DataParallelPPOActor.update_policy (dp_actor.py:419-466).
     policy_loss "gpg": compute_policy_loss_gpg (core_algos.py:957-975), pg = -log_prob * advantages; "gspo" /
     "geo_mean": policy_loss_gspo / policy_loss_geo_mean (sequence-level ratios)."""
     w = agg_loss_grad(response_mask, loss_agg_mode)
-    if policy_loss in ("gspo", "geo_mean"):  # the pg gradient carries its own aggregation weights
-        fn = policy_loss_gspo if policy_loss == "gspo" else policy_loss_geo_mean
-        pg_loss, clipfrac, ppo_kl, clipfrac_lower, dpg_w = fn(old_log_prob, log_prob, advantages, response_mask,
-                                                               clip_ratio_low, clip_ratio_high)
+    if policy_loss in ("gspo", "geo_mean", "clip_cov", "kl_cov"):  # the pg gradient carries its own agg weights
+        if policy_loss == "kl_cov":
+            pg_loss, clipfrac, ppo_kl, clipfrac_lower, dpg_w = policy_loss_kl_cov(
+                old_log_prob, log_prob, advantages, response_mask, loss_agg_mode, cov_ratio, ppo_kl_coef)
+        elif policy_loss == "clip_cov":
+            pg_loss, clipfrac, ppo_kl, clipfrac_lower, dpg_w = policy_loss_clip_cov(
+                old_log_prob, log_prob, advantages, response_mask, loss_agg_mode, clip_ratio_low, clip_ratio_high,
+                cov_ratio, clip_cov_lb, clip_cov_ub, cov_seed)
+        else:
+            fn = policy_loss_gspo if policy_loss == "gspo" else policy_loss_geo_mean
+            pg_loss, clipfrac, ppo_kl, clipfrac_lower, dpg_w = fn(old_log_prob, log_prob, advantages, response_mask,
+                                                                   clip_ratio_low, clip_ratio_high)
         with np.errstate(divide="ignore", invalid="ignore"):
             dpg = np.where(w != 0, dpg_w / np.where(w != 0, w, 1.0), 0.0)
     elif policy_loss == "gpg":
@@ -265,7 +356,7 @@ def actor_loss(old_log_prob, log_prob, advantages, response_mask, entropy, ref_l
     total = pg_loss - entropy_loss * entropy_coeff if entropy_coeff != 0 else pg_loss
     kld, dkld = kl_penalty(log_prob, ref_log_prob, kl_loss_type)
     kl_loss = agg_loss(kld, response_mask, loss_agg_mode)
-    dlogp = dpg_w if policy_loss in ("gspo", "geo_mean") else w * dpg
+    dlogp = dpg_w if policy_loss in ("gspo", "geo_mean", "clip_cov", "kl_cov") else w * dpg
     if use_kl_loss:
         total = total + kl_loss * kl_loss_coef
         dlogp = dlogp + kl_loss_coef * w * dkld

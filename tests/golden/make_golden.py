@@ -23,6 +23,7 @@ Reference call sites (file:line under /root/reference):
 * RLOO / REINFORCE++-baseline advantages : verl/trainer/ppo/core_algos.py:392-493
 * OPO / GPG / GRPO pass@k / ReMax advantages : verl/trainer/ppo/core_algos.py:327-386, 495-546, 588-684
 * GSPO / GMPO (geo_mean) policy losses : verl/trainer/ppo/core_algos.py:892-954, 1143-1210
+* Clip-Cov / KL-Cov policy losses : verl/trainer/ppo/core_algos.py:978-1140
 * masked_mean known answers : tests/utils/test_torch_functional.py:55-66 (reference test, reproduced as data)
 """
 
@@ -837,6 +838,55 @@ def gen_seq_loss():
                           kl_loss_coef=0.001, loss_scale_factor=lsf, use_kl_loss=True, clip_ratio_low=clo,
                           clip_ratio_high=chi))
     _save("seq_loss.npz", arrays, {"cases": cases, "ref": "core_algos.py:892-954, 1143-1210; dp_actor.py:419-466"})
+
+
+def gen_cov_loss():
+    """Clip-Cov (core_algos.py:978-1069) and KL-Cov (:1072-1140) composed as dp_actor does. Clip-Cov's token subset
+    comes from torch.randperm; these cases keep clip_num >= #candidates, where every candidate is taken and the
+    result is deterministic (the subset draw itself is not reproducible outside torch's RNG)."""
+    from verl.workers.config import ActorConfig
+    from verl.workers.config.actor import PolicyLossConfig
+    from verl.workers.config.optimizer import OptimizerConfig
+
+    g = torch.Generator().manual_seed(6262)
+    arrays, cases = {}, []
+    specs = [("kl_cov", (6, 16), "token-mean", "low_var_kl", 0.001, 0.5, dict(kl_cov_ratio=0.05, ppo_kl_coef=0.1)),
+             ("kl_cov", (8, 40), "seq-mean-token-mean", "kl", 0.0, 1.0, dict(kl_cov_ratio=0.0002, ppo_kl_coef=1.0)),
+             ("kl_cov", (5, 33), "seq-mean-token-sum", "abs", 0.01, 0.25, dict(kl_cov_ratio=0.2, ppo_kl_coef=0.3)),
+             ("clip_cov", (6, 16), "token-mean", "low_var_kl", 0.001, 0.5,
+              dict(clip_cov_ratio=0.5, clip_cov_lb=1.0, clip_cov_ub=5.0)),
+             ("clip_cov", (8, 40), "seq-mean-token-mean", "mse", 0.0, 1.0,
+              dict(clip_cov_ratio=0.4, clip_cov_lb=0.5, clip_cov_ub=3.0)),
+             ("clip_cov", (5, 33), "seq-mean-token-sum-norm", "kl", 0.01, 0.25,
+              dict(clip_cov_ratio=0.9, clip_cov_lb=-1.0, clip_cov_ub=2.0))]
+    for ci, (loss, shape, mode, kl, ent_c, lsf, pl) in enumerate(specs):
+        old, logp, adv, mask, ent, ref = ppo_loss_inputs(g, *shape, "random")
+        pcfg = PolicyLossConfig(loss_mode=loss, **pl)
+        cfg = ActorConfig(strategy="fsdp", clip_ratio=0.2, clip_ratio_low=0.2, clip_ratio_high=0.28, loss_agg_mode=mode,
+                          optim=OptimizerConfig(lr=1e-6), ppo_micro_batch_size_per_gpu=2, ppo_mini_batch_size=4,
+                          policy_loss=pcfg)
+        pg_fn = ca.get_policy_loss_fn(loss)
+        lp = logp.clone().requires_grad_(True)
+        en = ent.clone().requires_grad_(True)
+        pg_loss, c1, c2, c3 = pg_fn(old_log_prob=old, log_prob=lp, advantages=adv, response_mask=mask,
+                                    loss_agg_mode=mode, config=cfg)
+        entropy_loss = ca.agg_loss(loss_mat=en, loss_mask=mask, loss_agg_mode=mode)
+        policy_loss = pg_loss - entropy_loss * ent_c if ent_c != 0 else pg_loss
+        kld = ca.kl_penalty(logprob=lp, ref_logprob=ref, kl_penalty=kl)
+        kl_loss = ca.agg_loss(loss_mat=kld, loss_mask=mask, loss_agg_mode=mode)
+        loss_v = (policy_loss + kl_loss * 0.001) * lsf
+        loss_v.backward()
+        for k, v in dict(old_log_prob=old, log_prob=logp, advantages=adv, response_mask=mask, entropy=ent,
+                         ref_log_prob=ref, out_pg_loss=pg_loss.detach(), out_loss=loss_v.detach(),
+                         out_dlogp=lp.grad, out_dentropy=en.grad if en.grad is not None else torch.zeros_like(en),
+                         out_clip=torch.tensor([float(c1), float(c2), float(c3)])).items():
+            arrays[f"c{ci}_{k}"] = v
+        cases.append(dict(policy_loss=loss, loss_agg_mode=mode, kl_loss_type=kl, entropy_coeff=ent_c,
+                          kl_loss_coef=0.001, loss_scale_factor=lsf, clip_ratio_low=0.2, clip_ratio_high=0.28,
+                          cov_ratio=pl.get("clip_cov_ratio", pl.get("kl_cov_ratio")),
+                          clip_cov_lb=pl.get("clip_cov_lb", 1.0), clip_cov_ub=pl.get("clip_cov_ub", 5.0),
+                          ppo_kl_coef=pl.get("ppo_kl_coef", 0.1)))
+    _save("cov_loss.npz", arrays, {"cases": cases, "ref": "core_algos.py:978-1140; dp_actor.py:419-466"})
 
 
 # --------------------------------------------------------------------------------------------

@@ -57,7 +57,7 @@ def test_estimator_step_end_to_end(estimator):
         assert (nz <= 1).all()
 
 
-@pytest.mark.parametrize("loss_mode", ["gspo", "geo_mean", "gpg"])
+@pytest.mark.parametrize("loss_mode", ["gspo", "geo_mean", "gpg", "clip_cov", "kl_cov"])
 def test_policy_loss_modes_step_end_to_end(loss_mode):
     """actor.policy_loss.loss_mode selects the registered loss inside update_policy (dp_actor.py:419-466): one GRPO
     step per mode, finite metrics, the policy moves."""

@@ -370,6 +370,65 @@ def test_seq_policy_loss_at_size_matches_oracle(policy, mode):
     assert torch.equal(out, out2) and torch.equal(dlp, dlp2)
 
 
+def test_cov_actor_loss_matches_reference_golden(golden):
+    """Clip-Cov / KL-Cov through the K1 entry point vs the reference losses composed into the dp_actor total loss
+    (cov_loss.npz; clip_cov where every candidate is taken, so the reference's torch.randperm draw is moot)."""
+    z, meta = golden("cov_loss.npz")
+    for ci, c in enumerate(meta["cases"]):
+        g = lambda k: T(z[f"c{ci}_{k}"])  # noqa: E731
+        out, dlp, dent = native.ppo_loss_fwd_bwd(
+            g("old_log_prob"), g("log_prob"), g("advantages"), g("response_mask"), g("entropy"), g("ref_log_prob"),
+            clip_ratio_low=c["clip_ratio_low"], clip_ratio_high=c["clip_ratio_high"],
+            entropy_coeff=c["entropy_coeff"], kl_loss_coef=c["kl_loss_coef"], kl_loss_type=c["kl_loss_type"],
+            loss_agg_mode=c["loss_agg_mode"], loss_scale_factor=c["loss_scale_factor"], want_dentropy=True,
+            policy_loss=c["policy_loss"], cov_ratio=c["cov_ratio"], clip_cov_lb=c["clip_cov_lb"],
+            clip_cov_ub=c["clip_cov_ub"], ppo_kl_coef=c["ppo_kl_coef"], cov_seed=123)
+        o = out.cpu().numpy()
+        np.testing.assert_allclose(o[0], z[f"c{ci}_out_pg_loss"], rtol=2e-5, atol=1e-6, err_msg=str(c))
+        np.testing.assert_allclose(o[6], z[f"c{ci}_out_loss"], rtol=2e-5, atol=1e-6, err_msg=str(c))
+        np.testing.assert_allclose(o[[1, 2, 3]], z[f"c{ci}_out_clip"], rtol=2e-5, atol=1e-6, err_msg=str(c))
+        d = z[f"c{ci}_out_dlogp"]
+        np.testing.assert_allclose(dlp.cpu().numpy(), d, rtol=2e-4, atol=1e-6 * np.abs(d).max(), err_msg=str(c))
+        np.testing.assert_allclose(dent.cpu().numpy(), z[f"c{ci}_out_dentropy"], rtol=2e-5, atol=1e-9)
+
+
+@pytest.mark.parametrize("policy,ratio", [("kl_cov", 0.0002), ("kl_cov", 0.01), ("clip_cov", 0.0002), ("clip_cov", 0.002)])
+def test_cov_policy_loss_at_size_matches_oracle(policy, ratio):
+    """Clip-Cov / KL-Cov at 64 x 1024 (ragged rows) vs the oracle: the same top-k tokens (kl_cov) and the same
+    seeded random subset of the candidates (clip_cov, many more candidates than clip_num); deterministic; a new
+    seed draws another clip_cov subset of the same size."""
+    rng = np.random.default_rng(23)
+    B, R = 64, 1024
+    old = (-rng.random((B, R)) * 5).astype(np.float32)
+    lp = (old + rng.standard_normal((B, R)) * 0.3).astype(np.float32)
+    adv = (rng.standard_normal((B, R)) * 2).astype(np.float32)
+    mask = (np.arange(R)[None, :] < rng.integers(1, R + 1, (B, 1))).astype(np.int64)
+    kw = dict(clip_ratio_low=0.2, clip_ratio_high=0.28, loss_agg_mode="token-mean", loss_scale_factor=1.0,
+              policy_loss=policy, cov_ratio=ratio, clip_cov_lb=1.0, clip_cov_ub=5.0, ppo_kl_coef=0.1, cov_seed=77)
+    out, dlp, _ = native.ppo_loss_fwd_bwd(T(old), T(lp), T(adv), T(mask), **kw)
+    want = oracle.actor_loss(old, lp, adv, mask, np.zeros_like(old), lp, loss_agg_mode="token-mean",
+                             clip_ratio_low=0.2, clip_ratio_high=0.28, clip_ratio_c=3.0, entropy_coeff=0.0,
+                             use_kl_loss=False, kl_loss_type="kl", kl_loss_coef=0.0, loss_scale_factor=1.0,
+                             policy_loss=policy, cov_ratio=ratio, clip_cov_lb=1.0, clip_cov_ub=5.0, ppo_kl_coef=0.1,
+                             cov_seed=77)
+    o = out.cpu().numpy()
+    np.testing.assert_allclose(o[0], want["pg_loss"], rtol=2e-5, atol=1e-7)
+    np.testing.assert_allclose(o[[1, 2, 3]], [want["pg_clipfrac"], want["ppo_kl"], want["pg_clipfrac_lower"]],
+                               rtol=1e-4, atol=1e-7)
+    d = want["dlogp"]
+    np.testing.assert_allclose(dlp.cpu().numpy(), d, rtol=2e-4, atol=1e-6 * np.abs(d).max())
+    out2, dlp2, _ = native.ppo_loss_fwd_bwd(T(old), T(lp), T(adv), T(mask), **kw)
+    assert torch.equal(out, out2) and torch.equal(dlp, dlp2)
+    if policy == "clip_cov":
+        _, _, _, _, _, sel = oracle.policy_loss_clip_cov(old, lp, adv, mask, "token-mean", 0.2, 0.28, ratio, 1.0, 5.0,
+                                                         77, return_selected=True)
+        assert sel.sum() == max(int(ratio * mask.sum()), 1)
+        kw["cov_seed"] = 78
+        out3, _, _ = native.ppo_loss_fwd_bwd(T(old), T(lp), T(adv), T(mask), **kw)
+        assert out3[1].item() == out[1].item()  # same subset size (pg_clipfrac), another draw
+        assert out3[0].item() != out[0].item()
+
+
 def test_gae_matches_reference_golden(golden):
     z, meta = golden("gae.npz")
     for ci, cfg in enumerate(meta["cases"]):

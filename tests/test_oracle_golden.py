@@ -65,6 +65,27 @@ def test_gspo_geo_mean_actor_loss_matches_reference(golden):
         np.testing.assert_allclose(want["dentropy"], g("out_dentropy"), rtol=1e-5, atol=1e-9, err_msg=str(c))
 
 
+def test_cov_actor_loss_matches_reference(golden):
+    """The oracle's Clip-Cov / KL-Cov restatements composed as dp_actor does, against the reference's autograd
+    (clip_cov in the regime where every candidate is taken: the reference's subset draw is torch.randperm)."""
+    z, meta = golden("cov_loss.npz")
+    for ci, c in enumerate(meta["cases"]):
+        g = lambda k: z[f"c{ci}_{k}"]  # noqa: E731
+        want = oracle.actor_loss(g("old_log_prob"), g("log_prob"), g("advantages"), g("response_mask"), g("entropy"),
+                                 g("ref_log_prob"), loss_agg_mode=c["loss_agg_mode"], clip_ratio_low=c["clip_ratio_low"],
+                                 clip_ratio_high=c["clip_ratio_high"], clip_ratio_c=3.0, entropy_coeff=c["entropy_coeff"],
+                                 use_kl_loss=True, kl_loss_type=c["kl_loss_type"], kl_loss_coef=c["kl_loss_coef"],
+                                 loss_scale_factor=c["loss_scale_factor"], policy_loss=c["policy_loss"],
+                                 cov_ratio=c["cov_ratio"], clip_cov_lb=c["clip_cov_lb"], clip_cov_ub=c["clip_cov_ub"],
+                                 ppo_kl_coef=c["ppo_kl_coef"])
+        np.testing.assert_allclose(want["pg_loss"], g("out_pg_loss"), rtol=2e-5, atol=1e-6, err_msg=str(c))
+        np.testing.assert_allclose(want["loss"], g("out_loss"), rtol=2e-5, atol=1e-6, err_msg=str(c))
+        np.testing.assert_allclose([want["pg_clipfrac"], want["ppo_kl"], want["pg_clipfrac_lower"]], g("out_clip"),
+                                   rtol=2e-5, atol=1e-6, err_msg=str(c))
+        d = g("out_dlogp")
+        np.testing.assert_allclose(want["dlogp"], d, rtol=2e-4, atol=1e-6 * np.abs(d).max(), err_msg=str(c))
+
+
 def test_masked_mean_known_answers(golden):
     z, _ = golden("masked_mean.npz")
     # tests/utils/test_torch_functional.py:55-66 — NaN outside the mask is ignored
