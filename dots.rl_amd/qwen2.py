@@ -22,6 +22,7 @@ in fp32 end to end (the parity model checked against HF / golden greedy tokens).
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 
 import torch
@@ -348,6 +349,16 @@ class _Embedding(torch.autograd.Function):
 
 
 # --------------------------------------------------------------------------------------------- decoder layer
+# Full-sequence projections through csrc/gemm.hip's ping-pong GEMM (bias / SwiGLU fused in the epilogue) where
+# it measured at or above hipBLASLt (profiles/r02_gemm_pingpong.jsonl): bf16, >= 2048 rows, K <= 1152 — qkv_proj,
+# o_proj, gate_up_proj; the long-K down_proj and the lm_head stay on hipBLASLt. DRL_HIP_GEMM=0 turns it off (A/B).
+HIP_GEMM = os.environ.get("DRL_HIP_GEMM", "1") != "0"
+
+
+def _hip_gemm(x, rows, K):
+    return HIP_GEMM and x.dtype == torch.bfloat16 and x.is_cuda and rows >= 2048 and K % 128 == 0 and K <= 1152
+
+
 def _layer_forward(m, i, x_prev, delta, pos, key_valid, save, cache=None, koff=0, koff_dev=None):
     """x = x_prev (+ delta); returns (x2 = x + attn(x), mlp_out) — the next consumer adds them.
 
@@ -364,7 +375,10 @@ def _layer_forward(m, i, x_prev, delta, pos, key_valid, save, cache=None, koff=0
     rstd1 = torch.empty(B * T, dtype=torch.float32, device=dev) if save is not None else None
     native.add_rmsnorm_fwd(x_prev, delta, x if delta is not None else None, s.w(p + "input_layernorm"), h1, rstd1,
                            cfg.rms_norm_eps)
-    qkv = torch.addmm(m.qkv_bias(i), h1.view(B * T, H), s.w(p + "qkv_proj.weight").t())
+    if _hip_gemm(h1, B * T, H):
+        qkv = native.gemm_nt(h1.view(B * T, H), s.w(p + "qkv_proj.weight"), bias=m.qkv_bias(i))
+    else:
+        qkv = torch.addmm(m.qkv_bias(i), h1.view(B * T, H), s.w(p + "qkv_proj.weight").t())
     qkv = qkv.view(B, T, -1)
     q = torch.empty(B, Hkv, G, T, D, dtype=dt, device=dev)
     # bf16 full-sequence passes run the fused MFMA attention (csrc/flash_attn.hip): log-probs and prefill
@@ -441,14 +455,22 @@ def _layer_mlp(m, i, x, attn, save, kbuf, vbuf, P, q, h1, rstd1):
     D = cfg.head_dim
     p = f"layers.{i}."
     dev = x.device
-    o = attn.view(B * T, Hq * D) @ s.w(p + "o_proj").t()
+    if _hip_gemm(attn, B * T, Hq * D):
+        o = native.gemm_nt(attn.reshape(B * T, Hq * D), s.w(p + "o_proj"))
+    else:
+        o = attn.view(B * T, Hq * D) @ s.w(p + "o_proj").t()
     x2 = torch.empty_like(x)
     h2 = torch.empty(B, T, H, dtype=dt, device=dev)
     rstd2 = torch.empty(B * T, dtype=torch.float32, device=dev) if save is not None else None
     native.add_rmsnorm_fwd(x, o, x2, s.w(p + "post_attention_layernorm"), h2, rstd2, cfg.rms_norm_eps)
-    gu = h2.view(B * T, H) @ s.w(p + "gate_up_proj").t()
-    a = torch.empty(B * T, cfg.intermediate_size, dtype=dt, device=dev)
-    native.swiglu_fwd(gu, a)
+    if _hip_gemm(h2, B * T, H):
+        # SwiGLU fused into the gate_up GEMM's epilogue; gu = [g | u] written only when the backward needs it
+        gu = torch.empty(B * T, 2 * cfg.intermediate_size, dtype=dt, device=dev) if save is not None else None
+        a = native.gemm_nt(h2.view(B * T, H), s.w(p + "gate_up_proj"), swiglu=True, out_gu=gu)
+    else:
+        gu = h2.view(B * T, H) @ s.w(p + "gate_up_proj").t()
+        a = torch.empty(B * T, cfg.intermediate_size, dtype=dt, device=dev)
+        native.swiglu_fwd(gu, a)
     mlp = (a @ s.w(p + "down_proj").t()).view(B, T, H)
     if save is not None:
         save.update(x=x, rstd1=rstd1, h1=h1, q=q, k=kbuf, v=vbuf, P=P, attn=attn, x2=x2, rstd2=rstd2, h2=h2,

@@ -433,7 +433,8 @@ def our_gemms(Ms=(6144, 12288)):
     dev, bf = "cuda", torch.bfloat16
     res = []
     for name, N, K in (("qkv", 1152, 896), ("o_proj", 896, 896), ("gate_up", 9728, 896), ("down", 896, 4864),
-                       ("lm_head", 151936, 896)):
+                       ("lm_head", 151936, 896), ("qkv_dgrad", 896, 1152), ("gate_up_dgrad", 896, 9728),
+                       ("down_dgrad", 4864, 896)):
         w = torch.randn(N, K, device=dev, dtype=bf) * 0.05
         b = torch.randn(N, device=dev, dtype=bf) if name == "qkv" else None
         for M in (Ms if name != "lm_head" else (2048, 4096)):
@@ -448,7 +449,7 @@ def our_gemms(Ms=(6144, 12288)):
             else:
                 tl = time_it(lambda: x @ w.t())
             row = dict(kernel="gemm_nt", layer=name, M=M, N=N, K=K, hipblaslt_us=tl * 1e6, hipblaslt_TF=fl / tl / 1e12)
-            for tile in (0, 1, 3, 5, 6, 7, 8):
+            for tile in (0, 9):
                 native.lib().drl_gemm_set_tile(tile)
                 t = time_it(lambda: native.gemm_nt(x, w, bias=b, swiglu=sw))
                 row[f"tile{tile}_us"] = t * 1e6
