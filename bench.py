@@ -8,9 +8,9 @@ across the N ranks: "scaling" is strong. Random-init Qwen2.5-0.5B weights, synth
   python bench.py [--gpus N] [--steps K] [--warmup W]          (N>1 under torch.distributed.run)
 
 Besides the step rate the JSON line carries
-  roofline     : the dominant eagerly launched hand-written kernel (--roofline-kernel; default the SwiGLU
-                 forward, the largest hand-written total in profiles/r01_kernel_stats.csv outside the graphed
-                 decode step; the fused attention forward is the MFMA-bound alternative),
+  roofline     : the dominant eagerly launched hand-written kernel (--roofline-kernel; default the ping-pong
+                 projection GEMM drl_gemm_bf16_nt, MFMA-bound — it absorbed the SwiGLU forward, the round-1
+                 choice; the fused attention forward is the other MFMA-bound kernel),
                  every launch inside the timed region bracketed by HIP events on its launch stream;
                  achieved = algorithmic work per launch (ROOFLINE below) / mean launch
                  duration, against its bound's peak (2.5 PFLOP/s dense bf16 MFMA or 8 TB/s HBM);
@@ -65,8 +65,16 @@ def _swiglu_fwd_bytes(a):
     return 3 * N * I * (2 if dt == 4 else 4)
 
 
+def _gemm_flops(a):
+    # drl_gemm_bf16_nt(a, lda, b, ldb, c, ldc, M, N, K, bias, epilogue, c2, ldc2, stream): 2 M N K
+    return 2.0 * a[6] * a[7] * a[8]
+
+
 # symbol -> (work per launch from the call's arguments, per-unit statement, bound, peak, unit)
 ROOFLINE = {
+    "drl_gemm_bf16_nt": (_gemm_flops, "2*M*N*K FLOP per launch (bf16 operands, fp32 accumulation; qkv + bias, "
+                         "o_proj, gate_up + fused SwiGLU of every full-sequence forward)", "mfma", PEAK_BF16_TFLOPS,
+                         "TFLOP/s"),
     "drl_swiglu_fwd": (_swiglu_fwd_bytes, "6 B per (token, intermediate column): gate + up read, product written (bf16)",
                        "hbm", PEAK_HBM_GBPS, "GB/s"),
     "drl_flash_attn_fwd": (_flash_fwd_flops, "4*D FLOP per causal (query, key) pair per query head", "mfma",
@@ -186,7 +194,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--tiny", action="store_true", help="2-layer model, small batch (bring-up only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--roofline-kernel", default="drl_swiglu_fwd", choices=sorted(ROOFLINE))
+    ap.add_argument("--roofline-kernel", default="drl_gemm_bf16_nt", choices=sorted(ROOFLINE))
     ap.add_argument("--override", nargs="*", default=[])
     ap.add_argument("--k1-only", choices=["two_pass", "one_pass"], default=None,
                     help="only the K1 roofline at 2^26 tokens (rocprofv3 PMC passes for profiles/pmc_drl_ppo_loss_*)")
