@@ -168,13 +168,15 @@ __device__ __forceinline__ uint32_t valid_issue(const uint8_t* vrow, int64_t k0,
 }
 
 template <int D>
-__global__ __launch_bounds__(512) void flash_fwd_kernel(FlashArgs a) {
+__global__ __launch_bounds__(512, D == 64 ? 4 : 1) void flash_fwd_kernel(FlashArgs a) {
   constexpr int KS = D / 16;  // k-steps of S^T = K Q^T over the head dim
   constexpr int MT = D / 32;  // 32-row tiles of O^T over the head dim
   using TL = KVTile<D>;
-  __shared__ __attribute__((aligned(16))) uint16_t lds_k[2][TL::KSZ];
-  __shared__ __attribute__((aligned(16))) uint16_t lds_v[2][TL::VSZ];
-  __shared__ uint32_t lds_vw[2][8];
+  // two 32-key blocks per LDS buffer and per barrier: the two S^T chains of an iteration are independent, so
+  // one block's softmax overlaps the other's MFMAs, and the per-block barrier / staging round trip is halved
+  __shared__ __attribute__((aligned(16))) uint16_t lds_k[2][2][TL::KSZ];
+  __shared__ __attribute__((aligned(16))) uint16_t lds_v[2][2][TL::VSZ];
+  __shared__ uint32_t lds_vw[2][2][8];
   const int tid = threadIdx.x;
   const int lane = tid & 63, g = tid >> 6;
   const bool computes = g < a.G;  // waves >= G only help staging
@@ -213,10 +215,10 @@ __global__ __launch_bounds__(512) void flash_fwd_kernel(FlashArgs a) {
   const int qlo = static_cast<int>(t0 + a.qoff);     // smallest query position of the tile
 
   // one 32-key block: S^T, online softmax, O^T += V^T P^T (LDS buffer cur holds the block at k0)
-  auto block = [&](int cur, int64_t k0) {
+  auto block = [&](int cur, int sl, int64_t k0) {
     // ---- S^T (32 keys x 32 queries): A = K rows from LDS (lane & 31 = key), B = Q fragments
     f32x16 st = f32x16{};
-    const uint16_t* krow = lds_k[cur] + qi * TL::KROW + 8 * h;
+    const uint16_t* krow = lds_k[cur][sl] + qi * TL::KROW + 8 * h;
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       const u16x8 kv = *reinterpret_cast<const u16x8*>(krow + 16 * s);
@@ -228,7 +230,7 @@ __global__ __launch_bounds__(512) void flash_fwd_kernel(FlashArgs a) {
     bool allv = true;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      vw[c] = lds_vw[cur][h + 2 * c];  // keys kbase0 + 8c .. + 3
+      vw[c] = lds_vw[cur][sl][h + 2 * c];  // keys kbase0 + 8c .. + 3
       allv &= vw[c] == 0x01010101u;
     }
     // blocks strictly below the diagonal with every key valid need no mask (wave-uniform test)
@@ -276,7 +278,7 @@ __global__ __launch_bounds__(512) void flash_fwd_kernel(FlashArgs a) {
     // ---- O^T += V^T P^T; k-step s: element j of lane half h is key k0 + 16s + 8(j>>2) + 4h + (j&3)
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
-      const uint16_t* vtl = lds_v[cur] + (32 * mt + qi) * TL::VROW + 4 * h;
+      const uint16_t* vtl = lds_v[cur][sl] + (32 * mt + qi) * TL::VROW + 4 * h;
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const u16x4 lo = *reinterpret_cast<const u16x4*>(vtl + 16 * s);
@@ -286,26 +288,38 @@ __global__ __launch_bounds__(512) void flash_fwd_kernel(FlashArgs a) {
       }
     }
   };
-  // K/V staging: block ib + 1 is issued into registers at the start of iteration ib (in flight under the
-  // compute) and written to the other LDS buffer at its end; the key-valid words travel with it
-  u16x8 stage[TL::CPT];
-  uint32_t vst;
-  kv_issue<D>(kbase, vtbase, a.ld_vt, 0, a.Tk, tid, stage);
-  vst = valid_issue(vrow, 0, a.Tk, tid);
-  kv_store<D>(lds_k[0], lds_v[0], tid, stage);
-  if (tid < 8) lds_vw[0][tid] = vst;
+  // K/V staging: blocks ib + 2, ib + 3 are issued into registers at the start of the iteration over blocks
+  // ib, ib + 1 (in flight under the compute) and written to the other LDS buffer at its end; the key-valid
+  // words travel with them
+  u16x8 stage[2][TL::CPT];
+  uint32_t vst[2] = {0u, 0u};
+#pragma unroll
+  for (int sl = 0; sl < 2; ++sl)
+    if (sl < nb) {
+      kv_issue<D>(kbase, vtbase, a.ld_vt, sl * 32, a.Tk, tid, stage[sl]);
+      vst[sl] = valid_issue(vrow, sl * 32, a.Tk, tid);
+      kv_store<D>(lds_k[0][sl], lds_v[0][sl], tid, stage[sl]);
+      if (tid < 8) lds_vw[0][sl][tid] = vst[sl];
+    }
   __syncthreads();
-  for (int64_t ib = 0; ib < nb; ++ib) {
-    const int cur = static_cast<int>(ib & 1);
-    if (ib + 1 < nb) {
-      kv_issue<D>(kbase, vtbase, a.ld_vt, (ib + 1) * 32, a.Tk, tid, stage);
-      vst = valid_issue(vrow, (ib + 1) * 32, a.Tk, tid);
+  for (int64_t ib = 0; ib < nb; ib += 2) {
+    const int cur = static_cast<int>((ib >> 1) & 1);
+#pragma unroll
+    for (int sl = 0; sl < 2; ++sl)
+      if (ib + 2 + sl < nb) {
+        kv_issue<D>(kbase, vtbase, a.ld_vt, (ib + 2 + sl) * 32, a.Tk, tid, stage[sl]);
+        vst[sl] = valid_issue(vrow, (ib + 2 + sl) * 32, a.Tk, tid);
+      }
+    if (computes) {
+      block(cur, 0, ib * 32);
+      if (ib + 1 < nb) block(cur, 1, (ib + 1) * 32);
     }
-    if (computes) block(cur, ib * 32);
-    if (ib + 1 < nb) {
-      kv_store<D>(lds_k[cur ^ 1], lds_v[cur ^ 1], tid, stage);
-      if (tid < 8) lds_vw[cur ^ 1][tid] = vst;
-    }
+#pragma unroll
+    for (int sl = 0; sl < 2; ++sl)
+      if (ib + 2 + sl < nb) {
+        kv_store<D>(lds_k[cur ^ 1][sl], lds_v[cur ^ 1][sl], tid, stage[sl]);
+        if (tid < 8) lds_vw[cur ^ 1][sl][tid] = vst[sl];
+      }
     __syncthreads();
   }
   // ---- finalize: O^T register r of tile mt = head-dim row 32mt + (r & 3) + 8(r >> 2) + 4h of query tq
