@@ -558,7 +558,10 @@ int drl_decode_rope(const float* partials, int32_t nsplit, const void* bias, con
 enum { DRL_GEMM_PLAIN = 0, DRL_GEMM_BIAS = 1, DRL_GEMM_SWIGLU = 2 };
 int drl_gemm_bf16_nt(const void* a, int64_t lda, const void* b, int64_t ldb, void* c, int64_t ldc, int64_t M,
                      int64_t N, int64_t K, const void* bias, int32_t epilogue, void* c2, int64_t ldc2, void* stream);
-/* Tuning hook: 0 = automatic tile, 1 = 256 x 128, 2 = 128 x 128. */
+/* Tuning hook: 0 = automatic (the 256 x 256 ping-pong form when K % 128 == 0 and the 256 x 256 grid has >= 64
+ * tiles, else 256 x 128 / 128 x 128), 1 = 256 x 128, 2 = 128 x 128, 3-8 = the other one-barrier tiles,
+ * 9 = ping-pong (falls back to 256 x 256 x 64 when K % 128 != 0). Every choice gives the same result within one
+ * bf16 rounding (different fp32 summation orders). */
 void drl_gemm_set_tile(int32_t tile);
 
 
