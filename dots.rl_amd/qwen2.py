@@ -353,10 +353,12 @@ class _Embedding(torch.autograd.Function):
 # it measured at or above hipBLASLt (profiles/r02_gemm_pingpong.jsonl): bf16, >= 2048 rows, K <= 1152 — qkv_proj,
 # o_proj, gate_up_proj; the long-K down_proj and the lm_head stay on hipBLASLt. DRL_HIP_GEMM=0 turns it off (A/B).
 HIP_GEMM = os.environ.get("DRL_HIP_GEMM", "1") != "0"
+HIP_GEMM_MIN_ROWS = 2048  # below it the 256 x 256 grid leaves most CUs idle (tests lower it to pin the path)
 
 
 def _hip_gemm(x, rows, K):
-    return HIP_GEMM and x.dtype == torch.bfloat16 and x.is_cuda and rows >= 2048 and K % 128 == 0 and K <= 1152
+    return (HIP_GEMM and x.dtype == torch.bfloat16 and x.is_cuda and rows >= HIP_GEMM_MIN_ROWS and K % 128 == 0
+            and K <= 1152)
 
 
 def _layer_forward(m, i, x_prev, delta, pos, key_valid, save, cache=None, koff=0, koff_dev=None):

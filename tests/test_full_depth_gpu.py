@@ -105,8 +105,14 @@ def test_fp32_full_depth_matches_reference(ref, weights):
     np.testing.assert_allclose(ent, z["entropy"], rtol=1e-4, atol=1e-4)
 
 
-@pytest.mark.parametrize("packed", [True, False])
-def test_bf16_full_depth_margin_checked(ref, weights, packed):
+@pytest.mark.parametrize("packed,hip_gemm_rows", [(True, None), (False, None), (True, 1), (False, 1)])
+def test_bf16_full_depth_margin_checked(ref, weights, packed, hip_gemm_rows, monkeypatch):
+    """hip_gemm_rows=1: every full-sequence qkv / o_proj / gate_up projection (prefill, teacher-forced pass, the
+    unpacked decode step) on csrc/gemm.hip's ping-pong GEMM, held to the same reference margins"""
+    from dots.rl_amd import qwen2
+
+    if hip_gemm_rows is not None:
+        monkeypatch.setattr(qwen2, "HIP_GEMM_MIN_ROWS", hip_gemm_rows)
     z, meta = ref
     bound = 2.0 * meta["cpu_bf16_gap_err_max"]
     gaps = z["top2_gap"]

@@ -210,6 +210,36 @@ def decode_sweep_cold(Bs=(64, 128, 256, 512), L=640, Hkv=2, G=7, D=64, footprint
     return res
 
 
+def decode_split_sweep(Bs=(64, 128), L=640, Hkv=2, G=7, D=64, footprint=768 << 20):
+    """Key-split plans for small decode grids (HBM-cold as decode_sweep_cold): workgroups = B x Hkv x splits."""
+    dev = "cuda"
+    res = []
+    for B in Bs:
+        per = B * Hkv * 768 * D * 2 * 2
+        n = max(2, -(-footprint // per))
+        qs = [torch.randn(B, Hkv, G, D, device=dev, dtype=torch.bfloat16) for _ in range(n)]
+        ks = [torch.randn(B, Hkv, 768, D, device=dev, dtype=torch.bfloat16) for _ in range(n)]
+        vts = [torch.randn(B, Hkv, D, 768, device=dev, dtype=torch.bfloat16) for _ in range(n)]
+        valid = torch.ones(B, 768, dtype=torch.uint8, device=dev)
+        out = torch.empty_like(qs[0])
+
+        def run():
+            for i in range(n):
+                native.decode_attention_vt(qs[i], ks[i], vts[i], valid, L, out)
+
+        sweep = {"auto": round(time_graph(run, 4) / n * 1e6, 2)}
+        for nw in (2, 4, 8):
+            for sp in (1, 2, 4, 8):
+                native.lib().drl_decode_attention_set_plan(nw, sp)
+                sweep[f"{nw}x{sp}"] = round(time_graph(run, 4) / n * 1e6, 2)
+        native.lib().drl_decode_attention_set_plan(0, 0)
+        best = min(sweep, key=sweep.get)
+        res.append(dict(kernel="decode_attention_split_sweep", B=B, L=L, best=best, best_us=sweep[best],
+                        sweep_us=sweep))
+        del qs, ks, vts
+    return res
+
+
 def flash(B=16, Hkv=2, G=7, D=64, T=768):
     """Fused attention forward vs the unfused path (fp32-score GEMM + masked softmax + PV GEMM)."""
     import math
@@ -523,6 +553,10 @@ if __name__ == "__main__":
         sys.exit(0)
     if args.only == "floor":
         for r in launch_floor():
+            print(json.dumps(r), flush=True)
+        sys.exit(0)
+    if args.only == "decode_split":
+        for r in decode_split_sweep():
             print(json.dumps(r), flush=True)
         sys.exit(0)
     if args.only == "decode_cold":
