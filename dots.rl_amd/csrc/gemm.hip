@@ -49,6 +49,7 @@ struct GemmArgs {
   int64_t lda, ldb, ldc, ldc2;
   int M, N, K;        // SwiGLU: N = 2I (weight rows)
   int tm, tn;         // tiles along M and along the weight rows
+  int gm;             // ping-pong form: M-tiles per rasterization group
 };
 
 // LDS image [rows][BK] with the 16-B unit u of row r at u ^ swz(r): conflict-free ds_read_b128 fragment reads
@@ -240,11 +241,10 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs g) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wr = wave >> 2, wc = wave & 3;
   // tile order: the 32 workgroups an XCD runs at once get consecutive ids (xcd_remap) and consecutive ids walk
-  // groups of kGM M-tiles column by column, so those 32 tiles are 4 M-tiles x 8 N-tiles: 12 operand panels
-  // through the XCD's L2 instead of 33 (1 A panel + 32 weight panels) for a row-major walk
-  constexpr int kGM = 4;
+  // groups of g.gm M-tiles column by column, so with g.gm = 4 those 32 tiles are 4 M-tiles x 8 N-tiles: 12
+  // operand panels through the XCD's L2 instead of 33 (1 A panel + 32 weight panels) for a row-major walk
   const int t = xcd_remap(blockIdx.x, gridDim.x);
-  const int grp = t / (kGM * g.tn), first = grp * kGM, gm = min(g.tm - first, kGM), r = t % (kGM * g.tn);
+  const int grp = t / (g.gm * g.tn), first = grp * g.gm, gm = min(g.tm - first, g.gm), r = t % (g.gm * g.tn);
   const int m0 = (first + r % gm) * 256, n0 = (r / gm) * 256;
   const int half = g.N / 2;
 
@@ -475,9 +475,12 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs g) {
   }
 }
 
+int g_gemm_group = 0;  // tuning: M-tiles per rasterization group of the ping-pong form, 0 = automatic (4)
+
 int launch_pp(GemmArgs& g, int epi, hipStream_t s) {
   g.tm = (g.M + 255) / 256;
   g.tn = (g.N + 255) / 256;
+  g.gm = g_gemm_group > 0 ? g_gemm_group : 4;
   const dim3 grid(static_cast<unsigned>(g.tm * g.tn));
   if (epi == EPI_NONE) hipLaunchKernelGGL(gemm_pp_kernel<EPI_NONE>, grid, dim3(512), 0, s, g);
   else if (epi == EPI_BIAS) hipLaunchKernelGGL(gemm_pp_kernel<EPI_BIAS>, grid, dim3(512), 0, s, g);
@@ -504,6 +507,8 @@ int g_gemm_tile = 0;  // tuning: 0 = automatic, 1..9 = the configurations of drl
 }  // namespace drl
 
 extern "C" {
+
+void drl_gemm_set_group(int32_t group_m) { drl::g_gemm_group = (group_m >= 1 && group_m <= 64) ? group_m : 0; }
 
 void drl_gemm_set_tile(int32_t tile) { drl::g_gemm_tile = (tile >= 0 && tile <= 9) ? tile : 0; }
 

@@ -563,6 +563,9 @@ int drl_gemm_bf16_nt(const void* a, int64_t lda, const void* b, int64_t ldb, voi
  * 9 = ping-pong (falls back to 256 x 256 x 64 when K % 128 != 0). Every choice gives the same result within one
  * bf16 rounding (different fp32 summation orders). */
 void drl_gemm_set_tile(int32_t tile);
+/* Tuning hook: M-tiles per rasterization group of the ping-pong form (consecutive tiles walk a group column by
+ * column), 0 = automatic. Changes the schedule only, never the result. */
+void drl_gemm_set_group(int32_t group_m);
 
 
 /* 16-bit transpose: dst (cols, rows) = src (rows, cols)^T (row strides in elements). The weights' transposed

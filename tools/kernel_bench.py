@@ -484,6 +484,11 @@ def our_gemms(Ms=(6144, 12288)):
                 t = time_it(lambda: native.gemm_nt(x, w, bias=b, swiglu=sw))
                 row[f"tile{tile}_us"] = t * 1e6
                 row[f"tile{tile}_TF"] = fl / t / 1e12
+            native.lib().drl_gemm_set_tile(9)
+            for gm in (2, 8, 16):  # rasterization group of the ping-pong form (automatic: 4)
+                native.lib().drl_gemm_set_group(gm)
+                row[f"pp_g{gm}_us"] = time_it(lambda: native.gemm_nt(x, w, bias=b, swiglu=sw)) * 1e6
+            native.lib().drl_gemm_set_group(0)
             native.lib().drl_gemm_set_tile(0)
             res.append(row)
             del x
