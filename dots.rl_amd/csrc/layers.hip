@@ -180,6 +180,110 @@ __global__ __launch_bounds__(256) void rope_qkv_fwd_tiled_kernel(RopeArgs<E> a) 
   }
 }
 
+typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
+// 4-element vector load / store with the fp32 compute conversion (8 B for bf16, 16 B for fp32)
+__device__ __forceinline__ void ld4(const uint16_t* p, float (&f)[4]) {
+  const u16x4 v = *reinterpret_cast<const u16x4*>(p);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) f[e] = bf16_to_f32(v[e]);
+}
+__device__ __forceinline__ void ld4(const float* p, float (&f)[4]) {
+  const float4 v = *reinterpret_cast<const float4*>(p);
+  f[0] = v.x; f[1] = v.y; f[2] = v.z; f[3] = v.w;
+}
+__device__ __forceinline__ void st4(uint16_t* p, const float (&f)[4]) {
+  *reinterpret_cast<u16x4*>(p) = u16x4{f32_to_bf16(f[0]), f32_to_bf16(f[1]), f32_to_bf16(f[2]), f32_to_bf16(f[3])};
+}
+__device__ __forceinline__ void st4(float* p, const float (&f)[4]) {
+  *reinterpret_cast<float4*>(p) = make_float4(f[0], f[1], f[2], f[3]);
+}
+
+template <typename E>
+__global__ __launch_bounds__(256) void rope_qkv_fwd_tiled4_kernel(RopeArgs<E> a) {
+  __shared__ __attribute__((aligned(16))) E tile[128][kRopeTile + 8];
+  const int half = static_cast<int>(a.D / 2);
+  const int64_t Hall = a.Hq + 2 * a.Hkv;
+  const int64_t G = a.Hq / a.Hkv;
+  const int64_t h = blockIdx.y, b = blockIdx.z;
+  const int64_t t0 = static_cast<int64_t>(blockIdx.x) * kRopeTile;
+  const int64_t koff = a.koff_dev ? *a.koff_dev : a.koff;
+  if (koff < 0 || koff + a.T > a.Tk) return;
+  const bool is_q = h < a.Hq, is_k = !is_q && h < a.Hq + a.Hkv;
+  E* rowdst;   // row-major destination base of this (b, head), indexed [pos][D]
+  E* tdst;     // head-dim-major destination base, indexed [d * ld_t + pos]
+  int64_t pos0;  // position offset of t = 0 in the destinations
+  if (is_q) {
+    const int64_t g = h / G, hi = h % G;
+    rowdst = a.q + ((b * a.Hkv + g) * G + hi) * a.T * a.D;
+    tdst = a.qt ? a.qt + ((b * a.Hkv + g) * G + hi) * a.D * a.ld_t : nullptr;
+    pos0 = 0;
+  } else if (is_k) {
+    rowdst = a.k + (b * a.Hkv + (h - a.Hq)) * a.Tk * a.D;
+    tdst = a.kt ? a.kt + (b * a.Hkv + (h - a.Hq)) * a.D * a.ld_t : nullptr;
+    pos0 = koff;
+  } else {
+    rowdst = a.v ? a.v + (b * a.Hkv + (h - a.Hq - a.Hkv)) * a.Tk * a.D : nullptr;
+    tdst = a.vt ? a.vt + (b * a.Hkv + (h - a.Hq - a.Hkv)) * a.D * a.ld_t : nullptr;
+    pos0 = koff;
+  }
+  // 4 consecutive head-dim pairs per thread: 8-B (bf16) / 16-B (fp32) loads and stores instead of 2-B ones
+  const int tpr = half / 4, rows_per_pass = 256 / tpr;
+  const int j0 = 4 * (threadIdx.x % tpr);
+  for (int p = threadIdx.x / tpr; p < kRopeTile; p += rows_per_pass) {
+    const int64_t t = t0 + p;
+    if (t >= a.T) break;
+    const E* src = a.qkv + ((b * a.T + t) * Hall + h) * a.D;
+    float o1[4], o2[4];
+    ld4(src + j0, o1);
+    ld4(src + j0 + half, o2);
+    if (is_q || is_k) {
+      int64_t ps = a.pos[b * a.T + t];
+      ps = ps < 0 ? 0 : (ps >= a.maxpos ? a.maxpos - 1 : ps);
+      const float4 c = *reinterpret_cast<const float4*>(a.cos_t + ps * half + j0);
+      const float4 sn = *reinterpret_cast<const float4*>(a.sin_t + ps * half + j0);
+      const float cc[4] = {c.x, c.y, c.z, c.w}, ss[4] = {sn.x, sn.y, sn.z, sn.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float x1 = o1[e], x2 = o2[e];
+        o1[e] = fmaf(x1, cc[e], -(x2 * ss[e]));
+        o2[e] = fmaf(x2, cc[e], x1 * ss[e]);
+      }
+    }
+    if (rowdst) {
+      st4(rowdst + (pos0 + t) * a.D + j0, o1);
+      st4(rowdst + (pos0 + t) * a.D + j0 + half, o2);
+    }
+    if (tdst) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        E e1, e2;
+        stf(&e1, 0, o1[e]);
+        stf(&e2, 0, o2[e]);
+        tile[j0 + e][p] = e1;
+        tile[j0 + e + half][p] = e2;
+      }
+    }
+  }
+  if (tdst == nullptr) return;
+  __syncthreads();
+  // transposed rows: D rows x 64 positions, 16 positions (one or two 16-B pieces) per thread
+  constexpr int kPer = 16;
+  const int nvalid = static_cast<int>(min<int64_t>(kRopeTile, a.T - t0));
+  for (int it = threadIdx.x; it < a.D * (kRopeTile / kPer); it += 256) {
+    const int d = it / (kRopeTile / kPer), c = it % (kRopeTile / kPer);
+    E* dst = tdst + d * a.ld_t + pos0 + t0 + c * kPer;
+    const bool aligned = ((reinterpret_cast<uintptr_t>(dst) & 15u) == 0) && sizeof(E) == 2;
+    if (aligned && c * kPer + kPer <= nvalid) {
+      const uint4* srcv = reinterpret_cast<const uint4*>(&tile[d][c * kPer]);
+      uint4* dv = reinterpret_cast<uint4*>(dst);
+      dv[0] = srcv[0];
+      dv[1] = srcv[1];
+    } else {
+      for (int e = 0; e < kPer && c * kPer + e < nvalid; ++e) dst[e] = tile[d][c * kPer + e];
+    }
+  }
+}
+
 // backward: dq (B,Hkv,G,T,D), dk/dv (B,Hkv,T,D) -> dqkv (B,T,(Hq+2Hkv)*D) with the inverse rotation
 template <typename E>
 __global__ __launch_bounds__(256) void rope_qkv_bwd_kernel(RopeArgs<E> a, const E* dq, const E* dk, const E* dv,
@@ -841,10 +945,15 @@ int drl_rope_qkv_fwd(const void* qkv, int32_t dt, const int64_t* position_ids, c
     RopeArgs<E> a{static_cast<const E*>(qkv), position_ids, cos_t, sin_t, static_cast<E*>(q), static_cast<E*>(k),
                   static_cast<E*>(v), B, T, Hq, Hkv, D, Tk, koff, maxpos, koff_dev, static_cast<E*>(qt),
                   static_cast<E*>(kt), static_cast<E*>(vt), ld_t};
+    const bool vec4 = D % 8 == 0 && 256 % (D / 8) == 0 && aligned16(qkv) && aligned16(cos_t) && aligned16(sin_t) &&
+                      (q == nullptr || aligned16(q)) && (k == nullptr || aligned16(k)) && (v == nullptr || aligned16(v));
     if ((qt || kt || vt) && T >= 16 && D <= 128 && D % 2 == 0 && 256 % (D / 2) == 0) {
       const dim3 grid(static_cast<unsigned>((T + kRopeTile - 1) / kRopeTile), static_cast<unsigned>(Hq + 2 * Hkv),
                       static_cast<unsigned>(B));
-      hipLaunchKernelGGL(rope_qkv_fwd_tiled_kernel<E>, grid, dim3(256), 0, static_cast<hipStream_t>(stream), a);
+      if (vec4)
+        hipLaunchKernelGGL(rope_qkv_fwd_tiled4_kernel<E>, grid, dim3(256), 0, static_cast<hipStream_t>(stream), a);
+      else
+        hipLaunchKernelGGL(rope_qkv_fwd_tiled_kernel<E>, grid, dim3(256), 0, static_cast<hipStream_t>(stream), a);
     } else {
       hipLaunchKernelGGL(rope_qkv_fwd_kernel<E>, dim3(grid_stride(n)), dim3(256), 0, static_cast<hipStream_t>(stream),
                          a);

@@ -240,6 +240,30 @@ def decode_split_sweep(Bs=(64, 128), L=640, Hkv=2, G=7, D=64, footprint=768 << 2
     return res
 
 
+def rope(B=16, T=768, Hq=14, Hkv=2, D=64):
+    """RoPE + head split of the qkv projection (rope_qkv_fwd) at the log-prob (V^T copy) and training (k, v, K^T,
+    V^T copies) micro-batch shapes; bytes = qkv read + every output written once."""
+    dev, bf = "cuda", torch.bfloat16
+    G = Hq // Hkv
+    qkv = torch.randn(B, T, (Hq + 2 * Hkv) * D, device=dev, dtype=bf)
+    pos = torch.arange(T, device=dev).expand(B, T).contiguous()
+    inv = 1.0 / (1e6 ** (torch.arange(0, D, 2, device=dev).float() / D))
+    ang = torch.arange(32768, device=dev).float()[:, None] * inv[None]
+    cos, sin = ang.cos().contiguous(), ang.sin().contiguous()
+    q = torch.empty(B, Hkv, G, T, D, device=dev, dtype=bf)
+    k = torch.empty(B, Hkv, T, D, device=dev, dtype=bf)
+    v = torch.empty_like(k)
+    kt, vt = torch.empty(B, Hkv, D, T, device=dev, dtype=bf), torch.empty(B, Hkv, D, T, device=dev, dtype=bf)
+    res = []
+    for name, kw in (("logprob", dict(v=None, vt=vt)), ("train", dict(v=v, kt=kt, vt=vt))):
+        vv = kw.pop("v")
+        t = time_it(lambda: native.rope_qkv_fwd(qkv, pos, cos, sin, Hq, Hkv, D, q, k, vv, **kw))
+        nbytes = B * T * D * 2 * (Hq + 2 * Hkv) + B * T * D * 2 * (Hq + Hkv * (4 if name == "train" else 2))
+        res.append(dict(kernel="rope_qkv_fwd", form=name, B=B, T=T, us=t * 1e6, GBps=nbytes / t / 1e9,
+                        frac=nbytes / t / PEAK_HBM))
+    return res
+
+
 def flash(B=16, Hkv=2, G=7, D=64, T=768):
     """Fused attention forward vs the unfused path (fp32-score GEMM + masked softmax + PV GEMM)."""
     import math
@@ -558,6 +582,10 @@ if __name__ == "__main__":
         sys.exit(0)
     if args.only == "floor":
         for r in launch_floor():
+            print(json.dumps(r), flush=True)
+        sys.exit(0)
+    if args.only == "rope":
+        for r in rope() + rope(B=8):
             print(json.dumps(r), flush=True)
         sys.exit(0)
     if args.only == "decode_split":
