@@ -322,6 +322,56 @@ __global__ __launch_bounds__(256) void rope_qkv_bwd_kernel(RopeArgs<E> a, const 
   }
 }
 
+// 4 consecutive head-dim pairs per lane (8-B / 16-B accesses; the index arithmetic once per 4 pairs). Same
+// per-element math as rope_qkv_bwd_kernel.
+template <typename E>
+__global__ __launch_bounds__(256) void rope_qkv_bwd4_kernel(RopeArgs<E> a, const E* dq, const E* dk, const E* dv,
+                                                            E* dqkv) {
+  const int64_t half = a.D / 2, q4 = half / 4;
+  const int64_t Hall = a.Hq + 2 * a.Hkv;
+  const int64_t n = a.B * a.T * Hall * q4;
+  const int64_t G = a.Hq / a.Hkv;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int64_t j0 = 4 * (i % q4);
+    const int64_t h = (i / q4) % Hall;
+    const int64_t bt = i / (q4 * Hall);
+    const int64_t t = bt % a.T, b = bt / a.T;
+    E* dst = dqkv + bt * Hall * a.D + h * a.D;
+    float g1[4], g2[4];
+    if (h < a.Hq + a.Hkv) {
+      const E* src;
+      if (h < a.Hq) {
+        const int64_t g = h / G, hi = h % G;
+        src = dq + (((b * a.Hkv + g) * G + hi) * a.T + t) * a.D;
+      } else {
+        src = dk + ((b * a.Hkv + (h - a.Hq)) * a.T + t) * a.D;
+      }
+      int64_t p = a.pos[b * a.T + t];
+      p = p < 0 ? 0 : (p >= a.maxpos ? a.maxpos - 1 : p);
+      const float4 c4 = *reinterpret_cast<const float4*>(a.cos_t + p * half + j0);
+      const float4 s4 = *reinterpret_cast<const float4*>(a.sin_t + p * half + j0);
+      const float c[4] = {c4.x, c4.y, c4.z, c4.w}, sn[4] = {s4.x, s4.y, s4.z, s4.w};
+      ld4(src + j0, g1);
+      ld4(src + j0 + half, g2);
+      float o1[4], o2[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {  // transpose of [[c, -s], [s, c]]
+        o1[e] = g1[e] * c[e] + g2[e] * sn[e];
+        o2[e] = g2[e] * c[e] - g1[e] * sn[e];
+      }
+      st4(dst + j0, o1);
+      st4(dst + j0 + half, o2);
+    } else {
+      const E* src = dv + ((b * a.Hkv + (h - a.Hq - a.Hkv)) * a.T + t) * a.D;
+      ld4(src + j0, g1);
+      ld4(src + j0 + half, g2);
+      st4(dst + j0, g1);
+      st4(dst + j0 + half, g2);
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------------ softmax
 // Rows of attention scores S (rows, Tk) bf16 laid out (B, Hkv, G, Tq, Tk). Row r: q = r % Tq, b = r / (Hkv G Tq).
 // allowed(key j) = valid[b, j] && j <= q + qoff; a row with no allowed key is uniform (HF finfo.min mask)
@@ -972,9 +1022,15 @@ int drl_rope_qkv_bwd(const void* dq, const void* dk, const void* dv, int32_t dt,
   const int64_t n = B * T * (Hq + 2 * Hkv) * (D / 2);
   DRL_E_DISPATCH(dt, {
     RopeArgs<E> a{nullptr, position_ids, cos_t, sin_t, nullptr, nullptr, nullptr, B, T, Hq, Hkv, D, T, 0, maxpos};
-    hipLaunchKernelGGL(rope_qkv_bwd_kernel<E>, dim3(grid_stride(n)), dim3(256), 0, static_cast<hipStream_t>(stream), a,
-                       static_cast<const E*>(dq), static_cast<const E*>(dk), static_cast<const E*>(dv),
-                       static_cast<E*>(dqkv));
+    if (D % 8 == 0 && aligned16(dq) && aligned16(dk) && aligned16(dv) && aligned16(dqkv) && aligned16(cos_t) &&
+        aligned16(sin_t))
+      hipLaunchKernelGGL(rope_qkv_bwd4_kernel<E>, dim3(grid_stride(n / 4)), dim3(256), 0,
+                         static_cast<hipStream_t>(stream), a, static_cast<const E*>(dq), static_cast<const E*>(dk),
+                         static_cast<const E*>(dv), static_cast<E*>(dqkv));
+    else
+      hipLaunchKernelGGL(rope_qkv_bwd_kernel<E>, dim3(grid_stride(n)), dim3(256), 0, static_cast<hipStream_t>(stream),
+                         a, static_cast<const E*>(dq), static_cast<const E*>(dk), static_cast<const E*>(dv),
+                         static_cast<E*>(dqkv));
   });
   DRL_LAUNCH_CHECK();
   return DRL_OK;

@@ -261,6 +261,11 @@ def rope(B=16, T=768, Hq=14, Hkv=2, D=64):
         nbytes = B * T * D * 2 * (Hq + 2 * Hkv) + B * T * D * 2 * (Hq + Hkv * (4 if name == "train" else 2))
         res.append(dict(kernel="rope_qkv_fwd", form=name, B=B, T=T, us=t * 1e6, GBps=nbytes / t / 1e9,
                         frac=nbytes / t / PEAK_HBM))
+    dqkv = torch.empty_like(qkv)
+    t = time_it(lambda: native.rope_qkv_bwd(q, k, v, pos, cos, sin, Hq, Hkv, D, dqkv))
+    nbytes = 2 * B * T * D * 2 * (Hq + 2 * Hkv)
+    res.append(dict(kernel="rope_qkv_bwd", form="train", B=B, T=T, us=t * 1e6, GBps=nbytes / t / 1e9,
+                    frac=nbytes / t / PEAK_HBM))
     return res
 
 
