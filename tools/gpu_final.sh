@@ -6,4 +6,4 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout
 tail -2 gpurun_out/final/gputests.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/final/smoke.log 2>&1 || { tail -30 gpurun_out/final/smoke.log; exit 1; }
 tail -1 gpurun_out/final/smoke.log
-bash tools/gpu_profile.sh final drl_swiglu_fwd swiglu_fwd
+bash tools/gpu_profile.sh final drl_gemm_bf16_nt gemm_pp_kernel
