@@ -102,8 +102,9 @@ K1_PER_UNIT = ("36 B per token: old_log_prob, log_prob, advantages, entropy, ref
 
 def k1_roofline(form="two_pass", reps=20, warmup=3):
     """North-star kernel K1 (fused PPO loss fwd+bwd, drl_ppo_loss_fwd_bwd) at 2^26 tokens, token-mean, low_var_kl,
-    entropy bonus, int64 mask: every launch bracketed by HIP events on its stream. ``two_pass`` is the form the
-    actor runs (mask count folded by the K1a pre-pass inside the same call); ``one_pass`` hands over sum(mask)."""
+    entropy bonus, int64 mask: every launch bracketed by HIP events on its stream. ``one_pass`` is the form the
+    actor runs (dp_actor.update_policy hands over every micro-batch's sum(mask)); ``two_pass`` folds the count by
+    the K1a pre-pass inside the same call (callers without the count)."""
     import torch
 
     from dots.rl_amd import native
@@ -183,6 +184,18 @@ def build_config(args):
                               "actor_rollout_ref.actor.ppo_micro_batch_size_per_gpu=4",
                               "data.max_response_length=32", "actor_rollout_ref.rollout.response_length=32",
                               "data.max_prompt_length=64", "actor_rollout_ref.rollout.prompt_length=64"])
+    if args.dapo:
+        # BASELINE config #5 on one GPU: Qwen2.5-7B, the DAPO recipe (clip-higher, token-mean, dynamic sampling with
+        # filter_groups on acc, overlong buffer), group size 8, 1024-token responses; 8 prompts x 8 per step
+        from dots.rl_amd.dapo_trainer import dapo_overrides
+
+        apply_overrides(cfg, dapo_overrides(1024) + [
+            "actor_rollout_ref.model.path=random:qwen2.5-7b", "data.train_batch_size=8",
+            "data.max_response_length=1024", "actor_rollout_ref.rollout.response_length=1024",
+            "actor_rollout_ref.actor.ppo_mini_batch_size=4", "actor_rollout_ref.actor.ppo_micro_batch_size_per_gpu=2",
+            "actor_rollout_ref.rollout.log_prob_micro_batch_size_per_gpu=8",
+            "actor_rollout_ref.ref.log_prob_micro_batch_size_per_gpu=8",
+            "reward_model.reward_manager=dapo_synthetic"])
     apply_overrides(cfg, args.override)
     return cfg
 
@@ -196,6 +209,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--roofline-kernel", default="drl_gemm_bf16_nt", choices=sorted(ROOFLINE))
     ap.add_argument("--override", nargs="*", default=[])
+    ap.add_argument("--dapo", action="store_true",
+                    help="BASELINE config #5 on one GPU: Qwen2.5-7B DAPO, n=8, 1024-token responses (RayDAPOTrainer)")
     ap.add_argument("--k1-only", choices=["two_pass", "one_pass"], default=None,
                     help="only the K1 roofline at 2^26 tokens (rocprofv3 PMC passes for profiles/pmc_drl_ppo_loss_*)")
     ap.add_argument("--dist-backend", default=None,
@@ -217,13 +232,19 @@ def main():
     rank, world = dist.get_rank(), dist.get_world_size()
     assert world == args.gpus, f"--gpus {args.gpus} but WORLD_SIZE {world}"
     cfg = build_config(args)
-    trainer = RayPPOTrainer(cfg)
+    if args.dapo:
+        from dots.rl_amd.dapo_trainer import RayDAPOTrainer
+
+        trainer = RayDAPOTrainer(cfg)
+    else:
+        trainer = RayPPOTrainer(cfg)
     trainer.init_workers()
     trainer.global_steps = 1
     for _ in range(args.warmup):
-        trainer.step(trainer.train_dataloader.next())
+        trainer.step(None if args.dapo else trainer.train_dataloader.next())
         trainer.global_steps += 1
-    prompts = [trainer.train_dataloader.next() for _ in range(args.steps)]
+    # DAPO draws its own generation batches inside step() (dynamic sampling)
+    prompts = [None if args.dapo else trainer.train_dataloader.next() for _ in range(args.steps)]
     timer = native.KernelTimer(args.roofline_kernel, ROOFLINE[args.roofline_kernel][0])
     dist.barrier()
     torch.cuda.synchronize()
@@ -250,6 +271,11 @@ def main():
                       "random:qwen2.5-7b": "Qwen2.5-7B", "random:": "Qwen2.5-0.5B"}.get(preset, preset)
         if args.tiny:
             model_name += " (2 layers)"
+        algo = {"grpo": "GRPO", "gae": "PPO"}.get(str(cfg.algorithm.adv_estimator), str(cfg.algorithm.adv_estimator))
+        if args.dapo:
+            algo = "DAPO"
+        # BASELINE.json's metric for the default workload; the same sentence with the model / algorithm that ran
+        metric = METRIC.replace("Qwen2.5-0.5B GRPO", f"{model_name} {algo}")
         _, per_unit, bound, peak, unit = ROOFLINE[args.roofline_kernel]
         scale = 1e12 if unit == "TFLOP/s" else 1e9
         achieved = b_launch / t_launch / scale if n_launch else None
@@ -262,7 +288,7 @@ def main():
                     "mean_launch_us": t_launch * 1e6 if n_launch else None, "launches": n_launch,
                     "per_unit": per_unit, "traffic_source": traffic_src}
         line = {
-            "metric": METRIC,
+            "metric": metric,
             "value": steps_per_s,
             "unit": "PPO steps/s",
             "rollout_tokens_per_sec": resp_tokens / gen_time,
@@ -276,7 +302,7 @@ def main():
             "vs_baseline": None,
             "dtype": "bf16",
             "data": "synthetic",
-            "config": {"workload": (f"{model_name} GRPO, {cfg.data.train_batch_size} prompts x n={ar.rollout.n}, "
+            "config": {"workload": (f"{model_name} {algo}, {cfg.data.train_batch_size} prompts x n={ar.rollout.n}, "
                                     f"{cfg.data.max_prompt_length}-tok prompts / {cfg.data.max_response_length}-tok responses"),
                        "model": f"{model_name} (random init)", "global_batch": cfg.data.train_batch_size * ar.rollout.n,
                        "seq_len": cfg.data.max_prompt_length + cfg.data.max_response_length,
@@ -288,8 +314,9 @@ def main():
             "cpu_baseline": None,
         }
         if not args.tiny:
-            line["roofline_k1"] = k1_roofline("two_pass")
-            line["roofline_k1_one_pass"] = k1_roofline("one_pass")
+            # the actor's form: update_policy hands K1 every micro-batch's sum(response_mask) (one pass over HBM)
+            line["roofline_k1"] = k1_roofline("one_pass")
+            line["roofline_k1_two_pass"] = k1_roofline("two_pass")
         if world == 1 and not args.no_cpu_baseline and not args.tiny:
             line["cpu_baseline"] = cpu_baseline(cfg)
         print(json.dumps(line), flush=True)

@@ -92,6 +92,8 @@ F32 = ctypes.c_float
 SZ = ctypes.c_size_t
 
 # name -> (restype, argtypes); must match include/dotsrl_amd.h exactly
+ABI_VERSION = 3  # include/dotsrl_amd.h DRL_ABI_VERSION: the layouts below (PPOLossParams) are of this version
+
 SIGNATURES = {
     "drl_last_error": (ctypes.c_char_p, []),
     "drl_abi_version": (ctypes.c_int, []),
@@ -203,7 +205,7 @@ def load(path: str | None = None):
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
-        if lib.drl_abi_version() != 2:
+        if lib.drl_abi_version() != ABI_VERSION:
             raise NativeLibraryError(f"ABI mismatch: library reports {lib.drl_abi_version()}")
         _lib = lib
     return _lib

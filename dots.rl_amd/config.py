@@ -75,7 +75,8 @@ DEFAULTS = dict(
             # reference); "auto" = when replicated state would exceed 64 GB per GPU (workers._shard_spec)
             fsdp_config=dict(shard="auto", fsdp_size=-1, param_offload=False, optimizer_offload=False),
             optim=dict(lr=1e-6, lr_warmup_steps_ratio=0.0, total_training_steps=-1, weight_decay=0.01,
-                       lr_warmup_steps=-1, betas=[0.9, 0.999], eps=1e-8, warmup_style="constant", min_lr_ratio=0.0),
+                       lr_warmup_steps=-1, betas=[0.9, 0.999], eps=1e-8, warmup_style="constant", min_lr_ratio=0.0,
+                       num_cycles=0.5),
         ),
         rollout=dict(
             name="mi355x", mode="sync", temperature=1.0, top_k=-1, top_p=1.0, do_sample=True, n=8,
@@ -96,7 +97,7 @@ DEFAULTS = dict(
         strategy="mi355x", enable=None, rollout_n=None,
         fsdp_config=dict(shard="auto", fsdp_size=-1, param_offload=False, optimizer_offload=False),
         optim=dict(lr=1e-5, lr_warmup_steps_ratio=0.0, total_training_steps=-1, weight_decay=0.01, lr_warmup_steps=-1,
-                   betas=[0.9, 0.999], eps=1e-8, warmup_style="constant"),
+                   betas=[0.9, 0.999], eps=1e-8, warmup_style="constant", min_lr_ratio=0.0, num_cycles=0.5),
         model=dict(path="random:qwen2.5-0.5b", override_config={}, use_remove_padding=False, dtype="bfloat16",
                    gemm_tuning="auto", seed=4321),
         ppo_mini_batch_size=None, ppo_micro_batch_size=None, ppo_micro_batch_size_per_gpu=8,

@@ -254,17 +254,21 @@ class _FusedActorLoss(torch.autograd.Function):
 
 def fused_actor_loss(log_prob, entropy, old_log_prob, advantages, response_mask, ref_log_prob, *, clip_ratio_low,
                      clip_ratio_high, clip_ratio_c, entropy_coeff, use_kl_loss, kl_loss_type, kl_loss_coef,
-                     loss_agg_mode, loss_scale_factor, policy_loss="vanilla", cov_kw=None):
+                     loss_agg_mode, loss_scale_factor, policy_loss="vanilla", cov_kw=None, token_count=None):
     """The whole per-micro-batch loss of dp_actor.py:419-466 in one HIP launch.
 
     Returns a float32[8] tensor: pg_loss, pg_clipfrac, ppo_kl, pg_clipfrac_lower, entropy_loss, kl_loss,
     loss (= (pg - c_ent*ent + c_kl*kl) * loss_scale_factor, the backpropagated value), mask_count.
+    ``token_count`` (device float64 (1,), token-mean with the vanilla / gpg loss): sum(response_mask) of this
+    micro-batch, computed by the caller for all micro-batches at once — K1 then reads the mask once (one pass).
     """
     kw = dict(clip_ratio_low=clip_ratio_low, clip_ratio_high=clip_ratio_high, clip_ratio_c=clip_ratio_c,
               entropy_coeff=entropy_coeff if entropy is not None else 0.0,
               kl_loss_coef=kl_loss_coef if use_kl_loss else 0.0,
               kl_loss_type=kl_loss_type if use_kl_loss else None, loss_agg_mode=loss_agg_mode,
               loss_scale_factor=loss_scale_factor, policy_loss=policy_loss, **(cov_kw or {}))
+    if token_count is not None and loss_agg_mode == "token-mean" and policy_loss in ("vanilla", "gpg"):
+        kw["token_count"] = token_count
     return _FusedActorLoss.apply(log_prob, entropy, old_log_prob, advantages, response_mask,
                                  ref_log_prob if use_kl_loss else None, kw)
 
@@ -332,15 +336,31 @@ def compute_policy_loss_geo_mean(old_log_prob, log_prob, advantages, response_ma
 _COV_SEED = [0]
 
 
-def cov_loss_kw(policy_loss_cfg, mode):
-    """clip_cov / kl_cov knobs from actor.policy_loss (PolicyLossConfig defaults, workers/config/actor.py:45-50) and a
-    fresh subset seed per call (the reference draws clip_cov's subset from torch's global RNG each call)."""
+def _mix64(x):
+    """splitmix64 finaliser (a fixed bijection of 64-bit words)."""
+    x = (x + 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF
+    x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & 0xFFFFFFFFFFFFFFFF
+    x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & 0xFFFFFFFFFFFFFFFF
+    return x ^ (x >> 31)
+
+
+def cov_loss_kw(policy_loss_cfg, mode, seed_key=None):
+    """clip_cov / kl_cov knobs from actor.policy_loss (PolicyLossConfig defaults, workers/config/actor.py:45-50) and
+    the clip_cov subset seed. The reference draws the subset from torch's global RNG, whose state its checkpoint
+    restores; here the seed is a function of ``seed_key`` = (policy_loss.seed, optimizer step, micro-batch index),
+    all of which a checkpoint restores, so a resumed run draws the same subsets as an uninterrupted one. Without a
+    key (direct registry calls) a per-process call counter stands in."""
     pc = policy_loss_cfg or {}
     get = (lambda k, d: pc.get(k) if pc.get(k) is not None else d)
-    _COV_SEED[0] += 1
+    if seed_key is None:
+        _COV_SEED[0] += 1
+        seed_key = (0x5EED, _COV_SEED[0])
+    seed = 0
+    for part in seed_key:
+        seed = _mix64(seed ^ (int(part) & 0xFFFFFFFFFFFFFFFF))
     ratio = get("clip_cov_ratio", 0.0002) if mode == "clip_cov" else get("kl_cov_ratio", 0.0002)
     return dict(cov_ratio=ratio, clip_cov_lb=get("clip_cov_lb", 1.0), clip_cov_ub=get("clip_cov_ub", 5.0),
-                ppo_kl_coef=get("ppo_kl_coef", 0.1), cov_seed=_COV_SEED[0] * 0x9E3779B97F4A7C15)
+                ppo_kl_coef=get("ppo_kl_coef", 0.1), cov_seed=seed)
 
 
 @register_policy_loss("clip_cov")

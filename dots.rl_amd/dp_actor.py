@@ -28,13 +28,50 @@ def append_to_dict(data: dict, new: dict):
         data.setdefault(k, []).append(v)
 
 
+def lr_schedule(optim_cfg):
+    """The LambdaLR multiplier fsdp_workers.py:461-486 builds from an optim config section: warmup steps from
+    ``lr_warmup_steps`` (or ``lr_warmup_steps_ratio`` x ``total_training_steps`` when negative / None), then
+    ``warmup_style`` "constant" (get_constant_schedule_with_warmup, torch_functional.py:553-575) or "cosine"
+    (get_cosine_schedule_with_warmup with ``min_lr_ratio`` / ``num_cycles``, torch_functional.py:509-550).
+    Any other style raises NotImplementedError, as the reference does."""
+    total = optim_cfg.get("total_training_steps", 0)
+    total = 0 if total is None else int(total)
+    warm = optim_cfg.get("lr_warmup_steps", -1)
+    warm = -1 if warm is None else int(warm)
+    if warm < 0:
+        warm = int(optim_cfg.get("lr_warmup_steps_ratio", 0.0) * total)
+    style = optim_cfg.get("warmup_style", "constant")
+    if style == "constant":
+        def lam(step):
+            if step < warm:
+                return float(step) / float(max(1.0, warm))
+            return 1.0
+    elif style == "cosine":
+        min_lr_ratio = optim_cfg.get("min_lr_ratio", 0.0)
+        min_lr_ratio = 0.0 if min_lr_ratio is None else float(min_lr_ratio)
+        assert 0.0 <= min_lr_ratio <= 1.0
+        num_cycles = float(optim_cfg.get("num_cycles", 0.5))
+        coef, intercept = (1 - min_lr_ratio) * 0.5, (1 + min_lr_ratio) * 0.5
+
+        def lam(step):
+            if step < warm:
+                return min_lr_ratio + (1.0 - min_lr_ratio) * (float(step) / float(max(1, warm)))
+            progress = float(step - warm) / float(max(1, total - warm))
+            return max(min_lr_ratio, math.cos(math.pi * num_cycles * 2.0 * progress) * coef + intercept)
+    else:
+        raise NotImplementedError(f"Warmup style {style} is not supported")
+    return lam
+
+
 class FlatAdamW:
     """torch.optim.AdamW over the ParamStore's flat fp32 buffers (fsdp_workers.py:454-459 hyper-parameters),
     with clip_grad_norm_ + skip-if-non-finite (dp_actor.py:282-298) fused into the HIP step kernel.
-    LR schedule: constant with linear warmup (verl/utils/torch_functional.py get_constant_schedule_with_warmup)."""
+    LR schedule: ``lr_lambda`` (``lr_schedule(optim_cfg)``: constant or cosine with warmup, as LambdaLR) evaluated
+    at ``sched_step``, which the worker advances once per update call (fsdp_workers.py:717-719); default: constant
+    with ``warmup_steps`` of linear warmup."""
 
     def __init__(self, store, lr, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01, max_grad_norm=1.0,
-                 warmup_steps=0, group=None):
+                 warmup_steps=0, group=None, lr_lambda=None):
         self.store = store
         self.lr = lr
         self.betas = betas
@@ -42,6 +79,7 @@ class FlatAdamW:
         self.weight_decay = weight_decay
         self.max_grad_norm = max_grad_norm
         self.warmup_steps = warmup_steps
+        self.lr_lambda = lr_lambda or lr_schedule({"lr_warmup_steps": warmup_steps})
         self.group = group
         # moments cover what the master holds: everything (replicated) or [small region | own shard]
         self.exp_avg = torch.zeros_like(store.master)
@@ -54,9 +92,7 @@ class FlatAdamW:
         self.grad_work = torch.zeros_like(store.master) if store.sharded else None
 
     def current_lr(self):
-        if self.warmup_steps > 0 and self.sched_step < self.warmup_steps:
-            return self.lr * float(self.sched_step) / float(max(1, self.warmup_steps))
-        return self.lr
+        return self.lr * self.lr_lambda(self.sched_step)
 
     def zero_grad(self):
         self.store.zero_grad()
@@ -248,6 +284,16 @@ class DataParallelPPOActor:
                     grad_accum = cfg.ppo_mini_batch_size // cfg.ppo_micro_batch_size_per_gpu
                     micro_batches = mini_batch.split(cfg.ppo_micro_batch_size_per_gpu)
                 self.actor_optimizer.zero_grad()
+                counts = None
+                if cfg.loss_agg_mode == "token-mean" and loss_mode in ("vanilla", "gpg"):
+                    # every micro-batch's sum(response_mask) in one launch (exact in fp64): K1 runs one-pass
+                    sizes = {len(mb) for mb in micro_batches}
+                    if cfg.get("use_dynamic_bsz", False) or len(sizes) != 1:
+                        counts = torch.stack([mb.batch["response_mask"].sum(dtype=torch.float64)
+                                              for mb in micro_batches])
+                    else:
+                        rm = mini_batch.batch["response_mask"]
+                        counts = rm.reshape(len(micro_batches), -1).sum(-1, dtype=torch.float64)
                 for k, micro_batch in enumerate(micro_batches):
                     if k == len(micro_batches) - 1:  # gradients final after this backward: overlap the all-reduce
                         self.actor_optimizer.begin_overlap(m)
@@ -264,7 +310,11 @@ class DataParallelPPOActor:
                         clip_ratio_c=cfg.get("clip_ratio_c", 3.0), entropy_coeff=cfg.entropy_coeff,
                         use_kl_loss=cfg.use_kl_loss, kl_loss_type=cfg.kl_loss_type, kl_loss_coef=cfg.kl_loss_coef,
                         loss_agg_mode=cfg.loss_agg_mode, loss_scale_factor=lsf, policy_loss=loss_mode,
-                        cov_kw=cov_loss_kw(cfg.policy_loss, loss_mode) if loss_mode in ("clip_cov", "kl_cov") else None)
+                        token_count=counts[k:k + 1] if counts is not None else None,
+                        cov_kw=(cov_loss_kw(cfg.policy_loss, loss_mode,
+                                            seed_key=(cfg.policy_loss.get("seed", 1234),
+                                                      self.actor_optimizer.step_count, k))
+                                if loss_mode in ("clip_cov", "kl_cov") else None))
                     out[6].backward()
                     mb_out.append(out.detach())
                     mb_lsf.append(lsf)

@@ -116,9 +116,17 @@ class SyntheticPromptLoader:
 class RayPPOTrainer:
     """The fit() loop of ray_trainer.py:1050-1405 for the GRPO/PPO actor-learner hot path."""
 
-    def __init__(self, config, reward_fn=None, train_dataloader=None, eos_token_id=151645, pad_token_id=151643,
+    def __init__(self, config, reward_fn=None, train_dataloader=None, eos_token_id=None, pad_token_id=None,
                  tokenizer=None, rm_wg=None):
         self.config = config
+        if eos_token_id is None or pad_token_id is None:
+            # the model's own special ids (Qwen2.5: 151645 / 151643; Llama-3-8B: 128001 / 128001), as the
+            # reference takes them from the tokenizer / generation config of the loaded model
+            from .workers import resolve_model_config
+
+            mc = resolve_model_config(config.actor_rollout_ref.model)
+            eos_token_id = mc.eos_token_id if eos_token_id is None else eos_token_id
+            pad_token_id = mc.pad_token_id if pad_token_id is None else pad_token_id
         self.tokenizer = tokenizer
         self.reward_fn = reward_fn or load_reward_manager(config, tokenizer)
         # reward model scores (ray_trainer.py:1200-1203): a worker group with compute_rm_score(batch) -> DataProto
@@ -146,6 +154,12 @@ class RayPPOTrainer:
             self.use_critic = config.algorithm.adv_estimator == AdvantageEstimator.GAE.value
         self.global_steps = 0
         self.n_gpus = dist.get_world_size() if dist.is_initialized() else 1
+        # ray_trainer.py:557-571: the schedule horizon of the actor / critic LR schedules
+        total = config.trainer.get("total_training_steps")
+        if total is not None:
+            config.actor_rollout_ref.actor.optim.total_training_steps = int(total)
+            if "critic" in config:
+                config.critic.optim.total_training_steps = int(total)
 
     def init_workers(self):
         """ray_trainer.py:779-886: one colocated actor/rollout/ref worker per GPU (hybrid engine)."""

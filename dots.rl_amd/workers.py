@@ -21,7 +21,7 @@ import torch
 import torch.distributed as dist
 
 from .config import RANDOM_MODELS
-from .dp_actor import DataParallelPPOActor, FlatAdamW
+from .dp_actor import DataParallelPPOActor, FlatAdamW, lr_schedule
 from .dp_critic import DataParallelPPOCritic
 from .flops_counter import FlopsCounter
 from .protocol import DataProto
@@ -125,14 +125,10 @@ class ActorRolloutRefWorker(Worker):
         cfg.ref.use_fused_kernels = fused
         if self._is_actor:
             o = cfg.actor.optim
-            total = o.get("total_training_steps", -1)
-            warm = o.get("lr_warmup_steps", -1)
-            if warm is None or warm < 0:
-                warm = int(o.get("lr_warmup_steps_ratio", 0.0) * max(total, 0))
             betas = tuple(o.get("betas", (0.9, 0.999)))
             self.actor_optimizer = FlatAdamW(self.store, lr=o.lr, betas=betas, eps=o.get("eps", 1e-8),
                                              weight_decay=o.weight_decay, max_grad_norm=cfg.actor.grad_clip,
-                                             warmup_steps=warm)
+                                             lr_lambda=lr_schedule(o))
             self.actor = DataParallelPPOActor(cfg.actor, self.actor_module, self.actor_optimizer)
         if self._is_rollout:
             self.rollout = MI355XRollout(self.actor_module, cfg.rollout, dp_rank=self.dp_rank)
@@ -242,11 +238,24 @@ def _shard_spec(section, mcfg, dp_rank, dp_size):
     return (dp_rank, dp_size)
 
 
+# Flat-buffer layout of a checkpoint's 'master' / moment tensors. 2: the fp32 'small' region (norm weights) first,
+# then the GEMM parameters in param_specs order, 64-element alignment (ParamStore); 1 (unversioned files): the
+# parameters interleaved in param_specs order — loading one into a version-2 store would permute weights.
+CKPT_LAYOUT_VERSION = 2
+
+
+def _layout_signature(store):
+    """What a checkpoint's flat tensors must agree on to be copied into ``store`` element for element."""
+    return {"layout_version": CKPT_LAYOUT_VERSION, "n_small": store.n_small, "world": store.world,
+            "rank": store.rank, "numel": store.numel, "master_numel": store.master.numel(),
+            "offsets": [[n, int(o)] for n, (o, _, _) in store.offsets.items()]}
+
+
 def _save_store(store, optim, path_dir, name, extra, dp_rank):
     """Replicated store: rank 0 writes one file. Sharded: every rank writes its shard (the reference's
     FSDP sharded checkpoint: model_world_size_{w}_rank_{r}.pt, fsdp_checkpoint_manager.py)."""
     payload = dict(extra)
-    payload.update({"master": store.master.cpu(), "n_small": store.n_small, "world": store.world,
+    payload.update({"master": store.master.cpu(), "layout": _layout_signature(store),
                     "optim": {k: (v.cpu() if torch.is_tensor(v) else v) for k, v in optim.state_dict().items()}})
     if store.sharded:
         os.makedirs(path_dir, exist_ok=True)
@@ -261,6 +270,17 @@ def _save_store(store, optim, path_dir, name, extra, dp_rank):
 def _load_store(store, optim, path_dir, name):
     f = (f"{name}_world_size_{store.world}_rank_{store.rank}.pt" if store.sharded else f"{name}.pt")
     sd = torch.load(os.path.join(path_dir, f), map_location="cpu", weights_only=True)
+    want = _layout_signature(store)
+    got = sd.get("layout")
+    if got is None:
+        raise ValueError(f"{f}: checkpoint without a layout record (written before layout version "
+                         f"{CKPT_LAYOUT_VERSION}); its flat buffers would load permuted into this store")
+    bad = [k for k in want if got.get(k) != want[k]]
+    if bad:
+        raise ValueError(f"{f}: flat-buffer layout differs from this store in {bad} "
+                         f"(checkpoint layout_version {got.get('layout_version')}, store {CKPT_LAYOUT_VERSION})")
+    if sd["master"].shape != store.master.shape or sd["optim"]["exp_avg"].shape != optim.exp_avg.shape:
+        raise ValueError(f"{f}: buffer shapes {tuple(sd['master'].shape)} do not match {tuple(store.master.shape)}")
     store.master.copy_(sd["master"])
     store.refresh_compute()
     optim.load_state_dict(sd["optim"])
@@ -318,13 +338,9 @@ class CriticWorker(Worker):
             self.store.load_state_dict_hf(sd)
         self.critic_module = Qwen2Model(mcfg, self.store)
         o = cfg.optim
-        total = o.get("total_training_steps", -1)
-        warm = o.get("lr_warmup_steps", -1)
-        if warm is None or warm < 0:
-            warm = int(o.get("lr_warmup_steps_ratio", 0.0) * max(total, 0))
         self.critic_optimizer = FlatAdamW(self.store, lr=o.lr, betas=tuple(o.get("betas", (0.9, 0.999))),
                                           eps=o.get("eps", 1e-8), weight_decay=o.weight_decay,
-                                          max_grad_norm=cfg.grad_clip, warmup_steps=warm)
+                                          max_grad_norm=cfg.grad_clip, lr_lambda=lr_schedule(o))
         self.critic = DataParallelPPOCritic(cfg, self.critic_module, self.critic_optimizer)
 
     def _out(self, d: DataProto):

@@ -22,7 +22,9 @@
 extern "C" {
 #endif
 
-#define DRL_ABI_VERSION 2
+/* 3: drl_ppo_loss_params gained policy_loss, cov_ratio, clip_cov_lb, clip_cov_ub, ppo_kl_coef, cov_seed (a caller
+ * built against version 2 passes a shorter struct); drl_gemm_bf16 (operand layouts, fp32 epilogues, split-K) */
+#define DRL_ABI_VERSION 3
 
 #define DRL_OK 0
 #define DRL_ERR_INVALID (-1)     /* bad argument (shape, dtype, null pointer, alignment) */

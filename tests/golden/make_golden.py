@@ -1226,6 +1226,46 @@ def gen_full_depth():
         "hf": "transformers Qwen2ForCausalLM fp32 eager attention", "ref": "hf_rollout.py:112-171; dp_actor.py:249-272"})
 
 
+# --------------------------------------------------------------------------------------------
+# LR schedules (fsdp_workers.py:461-486): the reference's LambdaLR over a real torch optimizer, the lr read with
+# get_last_lr() before each lr_scheduler.step() as update_actor does (fsdp_workers.py:717-719)
+# --------------------------------------------------------------------------------------------
+def gen_lr_schedule():
+    cases = [dict(warmup_style="constant", lr_warmup_steps=-1, lr_warmup_steps_ratio=0.0, total_training_steps=20),
+             dict(warmup_style="constant", lr_warmup_steps=5, total_training_steps=20),
+             dict(warmup_style="constant", lr_warmup_steps=-1, lr_warmup_steps_ratio=0.25, total_training_steps=20),
+             dict(warmup_style="cosine", lr_warmup_steps=-1, lr_warmup_steps_ratio=0.0, total_training_steps=20),
+             dict(warmup_style="cosine", lr_warmup_steps=4, total_training_steps=30, min_lr_ratio=0.1),
+             dict(warmup_style="cosine", lr_warmup_steps=3, total_training_steps=25, min_lr_ratio=0.0, num_cycles=1.5),
+             dict(warmup_style="cosine", lr_warmup_steps=-1, lr_warmup_steps_ratio=0.1, total_training_steps=40,
+                  min_lr_ratio=0.05, num_cycles=0.5)]
+    lrs = []
+    for c in cases:
+        total = c.get("total_training_steps", 0)
+        warm = int(c.get("lr_warmup_steps", -1))
+        if warm < 0:
+            warm = int(c.get("lr_warmup_steps_ratio", 0.0) * total)
+        opt = torch.optim.AdamW([torch.nn.Parameter(torch.zeros(1))], lr=1e-6)
+        if c["warmup_style"] == "constant":
+            sch = vF.get_constant_schedule_with_warmup(optimizer=opt, num_warmup_steps=warm)
+        else:
+            sch = vF.get_cosine_schedule_with_warmup(optimizer=opt, num_warmup_steps=warm, num_training_steps=total,
+                                                     min_lr_ratio=c.get("min_lr_ratio", 0.0),
+                                                     num_cycles=c.get("num_cycles", 0.5))
+        seq = []
+        for _ in range(total + 5):
+            seq.append(sch.get_last_lr()[0])
+            opt.step()
+            sch.step()
+        lrs.append(seq)
+    width = max(len(s) for s in lrs)
+    arr = np.full((len(cases), width), np.nan)
+    for i, s in enumerate(lrs):
+        arr[i, :len(s)] = s
+    _save("lr_schedule.npz", dict(lr=arr), {"cases": cases, "base_lr": 1e-6,
+                                            "ref": "fsdp_workers.py:461-486, torch_functional.py:509-575"})
+
+
 if __name__ == "__main__":
     which = sys.argv[1:] or ["ppo_loss", "masked_mean", "grpo", "gae", "logprob", "fused_linear", "masks", "tiny_qwen2"]
     for w in which:

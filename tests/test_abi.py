@@ -26,6 +26,30 @@ def declared_functions():
     return sorted(set(re.findall(r"\b(drl_[a-z0-9_]+)\s*\(", src)))
 
 
+def header_abi_version():
+    return int(re.search(r"#define DRL_ABI_VERSION (\d+)", open(HEADER).read()).group(1))
+
+
+def header_struct_fields(name):
+    """Field names of `typedef struct name {...} name;` in the header, in order."""
+    src = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    body = re.search(r"typedef struct %s \{(.*?)\} %s;" % (name, name), src, flags=re.S).group(1)
+    return re.findall(r"(\w+)\s*;", body)
+
+
+def test_ppo_loss_params_layout_agrees_everywhere():
+    """The K1 parameter struct: header == ctypes binding (_lib.PPOLossParams) == the binding INTEGRATION.md §3
+    shows a verl maintainer (a short struct there would be read past its end by the library)."""
+    from dots.rl_amd import _lib
+
+    fields = header_struct_fields("drl_ppo_loss_params")
+    assert [f for f, _ in _lib.PPOLossParams._fields_] == fields
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    block = re.search(r"class PPOLossParams\(ctypes.Structure\):(.*?)\]\n", doc, flags=re.S).group(1)
+    assert re.findall(r'\("(\w+)", ctypes', block) == fields
+    assert f"drl_abi_version() == {header_abi_version()}" in doc
+
+
 def test_header_declares_the_boundary():
     names = declared_functions()
     for must in ["drl_ppo_loss_fwd_bwd", "drl_logprob_entropy_fwd", "drl_logprob_entropy_bwd",
@@ -47,7 +71,7 @@ def test_python_binding_signatures_cover_the_header(built_lib):
 
     assert set(_lib.SIGNATURES) == set(declared_functions())
     lib = _lib.load(built_lib)
-    assert lib.drl_abi_version() == 2
+    assert lib.drl_abi_version() == _lib.ABI_VERSION == header_abi_version()
 
 
 def test_library_is_gfx950_code(built_lib):
