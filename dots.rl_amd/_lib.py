@@ -164,6 +164,9 @@ SIGNATURES = {
     "drl_gemm_bf16_nt": (ctypes.c_int, [P, I64, P, I64, P, I64, I64, I64, I64, P, I32, P, I64, P]),
     "drl_gemm_set_tile": (None, [I32]),
     "drl_gemm_set_group": (None, [I32]),
+    "drl_gemm": (ctypes.c_int, [P, I64, I32, P, I64, I32, P, I64, I32, I32, I64, I64, I64, P, I32, P, I64, P, I64, P]),
+    "drl_gemm_workspace_bytes": (ctypes.c_int64, []),
+    "drl_gemm_set_sk_tuning": (None, [I32, I32, I32, I32]),
     "drl_transpose16": (ctypes.c_int, [P, I64, I64, I64, P, I64, P]),
     "drl_colsum_bf16_workspace_bytes": (SZ, [I64, I64]),
     "drl_colsum_bf16_acc": (ctypes.c_int, [P, I64, I64, I64, P, P, SZ, P]),

@@ -1,0 +1,633 @@
+// Every transformer GEMM of the actor's full-sequence passes on one kernel family: forward (y = x W^T), dgrad
+// (dx = dy W, the weight read in its stored (out, in) layout — no transposed copy) and wgrad (dW += dy^T x, fp32
+// accumulation in place), for the hipBLASLt calls behind nn.Linear's forward and autograd in HF Qwen2 / Llama under
+// the reference's autocast (dp_actor.py:110, fsdp_workers.py FSDP + HF path).
+//
+//   C(m, n) = sum_k A(m, k) B(n, k)     A(m, k) = a[m * lda + k] (layout "K": row-major (M, K))
+//                                                 a[k * lda + m] (layout "T": row-major (K, M))
+//                                       B(n, k) likewise over (N, K) / (K, N)
+//   forward  A = x (K),  B = W (K)                    bf16 out, + bias / SwiGLU epilogues (as csrc/gemm.hip)
+//   dgrad    A = dy (K), B = W (T: W is (out, in) = (K, N))   bf16 out
+//   wgrad    A = dy (T), B = x (T)                    fp32 out, C (+)= acc
+//
+// Main loop: the 256 x 256 x (2 x 64) ping-pong of csrc/gemm.hip (8 phases per k-tile pair, upper wave group one
+// barrier behind, counted vmcnt, 2 LDS buffers of 4 half-tiles), with every operand half-tile copied global -> LDS
+// by buffer_load ... lds (one 1-KB wave instruction per 16-B lane): reads outside the operand's byte range return
+// zeros, so row / column / k tails need no clamping (a k tail is zero in a T operand; K operands need K % 128 == 0).
+// LDS images per half-tile (16 KB): layout K = [128 rows][64 k] (128-B rows, 16-B unit u of row r at u ^ ((r>>1)&7):
+// conflict-free ds_read_b128 fragment reads); layout T = [64 k][128 m|n] (256-B rows, 16-B chunk c of row r at
+// c ^ 2((r & 3) | ((r >> 1) & 4))), read as the MFMA operand with ds_read_b64_tr_b16 (4 k-rows x 16 columns per
+// 16-lane group; the XOR puts the 8 rows a 32-lane half reads on 8 distinct 32-B bank windows: conflict-free).
+//
+// Work decomposition: stream-K over (tile, k-pair) iterations (cdna_hip_programming.md §5 "Decomposition first"),
+// grid = at most one workgroup per CU. The first `dp_tiles` tiles are dealt whole (tile wg, wg + G, ...); the rest
+// form one iteration space split into G contiguous, balanced ranges. A range's first segment that starts inside a
+// tile (a "tail") stores its fp32 partial tile to the workgroup's slab and publishes a flag (agent-scope release);
+// the workgroup that holds the tile's k = 0 segment (its "head", always the LAST segment of that workgroup's range,
+// so the tails it waits for were computed first) adds its own accumulator and the tails' slabs in k order — a fixed
+// order, so results are bit-reproducible — and runs the epilogue. The flag is reset by its consumer: every launch
+// starts and ends with the flag words zero (graph-replay safe). Co-residency: the grid never exceeds the CU count
+// (one 128-KB-LDS workgroup per CU), and a consumer only ever waits for workgroups with a larger index, which the
+// dispatcher has started no later than itself.
+#include "common.h"
+
+namespace drl {
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ bf16x8 as_bf16x8(u16x8 v) { return __builtin_bit_cast(bf16x8, v); }
+__device__ __forceinline__ uint16_t to_bf16_bits(float f) { return __builtin_bit_cast(uint16_t, static_cast<__bf16>(f)); }
+__device__ __forceinline__ float bf16r(float f) { return bf16_to_f32(to_bf16_bits(f)); }
+
+constexpr int EPI_NONE = 0, EPI_BIAS = 1, EPI_SWIGLU = 2, EPI_F32 = 3;
+constexpr int HT = 128 * 64, BUF = 4 * HT;  // half-tile, k-tile buffer (elements)
+constexpr int SLAB = 256 * 256;              // fp32 elements of one partial tile
+
+struct SkArgs {
+  const uint16_t* a;
+  const uint16_t* b;
+  uint16_t* c;         // bf16 out (M, N) or SwiGLU (M, N / 2)
+  uint16_t* c2;        // SwiGLU: optional gu (M, N)
+  float* c32;          // EPI_F32 out (M, N)
+  const uint16_t* bias;
+  float* ws;           // stream-K slabs, gridDim.x x SLAB
+  unsigned* flags;     // gridDim.x publish flags + 1 timeout word (zero between launches)
+  int64_t lda, ldb, ldc, ldc2;
+  uint32_t a_bytes, b_bytes;
+  int M, N, K;
+  int tm, tn, gm;      // tiles along M and N; M-tiles per rasterization group
+  int P;               // k-tile pairs per tile
+  int dp_tiles;        // tiles dealt whole before the stream-K region
+  int n_tiles;
+  int beta;            // EPI_F32: 1 = C += acc
+};
+
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  const int q = nwg / 8, r = nwg % 8, xcd = orig % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+}
+
+__device__ __forceinline__ int swz_k(int r) { return (r >> 1) & 7; }                 // layout K, 16-B units
+__device__ __forceinline__ int swz_t(int r) { return 2 * ((r & 3) | ((r >> 1) & 4)); }  // layout T, 16-B chunks
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+// ds_read_b64_tr_b16: lane 4q+p of each 16-lane group addresses row q, columns 4p..4p+3 of a 4 x 16 block; lane i
+// of the group receives column i of the 4 rows (cdna_hip_programming.md §5.5 T10). Inline asm: hipcc's own form
+// makes the compiler drain every LDS-DMA in flight (vmcnt(0)) before each read, which serialises the pipeline; the
+// asm read is waited for by the schedule's own lgkmcnt, with sched_barrier(0) after it (§5.4 rule 18) and the
+// 64-bit halves joined only behind that barrier.
+__device__ __forceinline__ uint64_t ds_read_tr(uint32_t addr, const int off) {  // off: constant after unrolling
+  uint64_t r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(off));
+  return r;
+}
+__device__ __forceinline__ u16x8 join(uint64_t lo, uint64_t hi) {
+  typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(u16x8, u64x2{lo, hi});
+}
+
+// LDS map (elements): operand region (A: 0, B: 32768) + k-tile buffer * 16384 + half * 8192, so every read of one
+// operand sits within 64 KB of one base address (the DS offset field is 16 bits)
+__device__ __forceinline__ constexpr int lds_half(int h, int buf) { return (h >> 1) * 32768 + buf * 16384 + (h & 1) * 8192; }
+
+template <int EPI, int AT, int BT>
+__global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
+  static_assert(EPI != EPI_SWIGLU || BT == 0, "SwiGLU pairs gate / up weight rows (layout K)");
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * BUF];
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int G = gridDim.x;
+  const int wg = xcd_remap(blockIdx.x, G);
+  const int half = g.N / 2;
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)g.a, (short)0, (int)g.a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)g.b, (short)0, (int)g.b_bytes, 0x00020000);
+
+  // per-lane byte offsets of this wave's two copy instructions of each half-tile h (0 A0, 1 A1, 2 B0, 3 B1) for the
+  // current tile, and the byte advance of one k-tile per operand
+  uint32_t voff[4][2];
+  const uint32_t kstep_a = AT ? static_cast<uint32_t>(64 * g.lda * 2) : 128u;
+  const uint32_t kstep_b = BT ? static_cast<uint32_t>(64 * g.ldb * 2) : 128u;
+
+  auto setup_tile = [&](int m0, int n0) {
+#pragma unroll
+    for (int h = 0; h < 4; ++h)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int q = wave + 8 * c;
+        const bool is_a = h < 2;
+        const bool tr = is_a ? AT : BT;
+        if (!tr) {
+          const int hr = 8 * q + (lane >> 3), up = lane & 7;
+          int grow;
+          if (is_a) {
+            grow = m0 + (h & 1) * 128 + hr;
+          } else if constexpr (EPI == EPI_SWIGLU) {
+            // tile row blocks of 16 alternate gate / up rows of the same 16 output columns
+            const int row = (hr >> 5) * 64 + (h & 1) * 32 + (hr & 31);
+            const int bb = row >> 4, col = min(n0 / 2 + 16 * (bb >> 1) + (row & 15), half - 1);
+            grow = (bb & 1) ? half + col : col;
+          } else {
+            grow = n0 + (hr >> 5) * 64 + (h & 1) * 32 + (hr & 31);
+          }
+          const int64_t ld = is_a ? g.lda : g.ldb;
+          voff[h][c] = static_cast<uint32_t>((static_cast<int64_t>(grow) * ld + 8 * (up ^ swz_k(hr))) * 2);
+        } else {
+          const int row = 4 * q + (lane >> 4), ch = (lane & 15) ^ swz_t(row);
+          const int col = is_a ? m0 + (h & 1) * 128 + 8 * ch : n0 + (ch >> 2) * 64 + (h & 1) * 32 + (ch & 3) * 8;
+          const int64_t ld = is_a ? g.lda : g.ldb;
+          voff[h][c] = static_cast<uint32_t>((static_cast<int64_t>(row) * ld + col) * 2);
+        }
+      }
+  };
+  // buf = kt & 1, passed as a constant of the unrolled schedule (segments start at even k-tiles)
+  auto issue = [&](int h, int buf, int kt, int kt_end) {
+    // past the segment's end: repeat its last k-tile into a buffer nobody reads again (keeps vmcnt counts static)
+    const int k = min(kt, kt_end - 1);
+    uint16_t* dst = lds + lds_half(h, buf);
+    const bool is_a = h < 2;
+    const uint32_t soff = static_cast<uint32_t>(k) * (is_a ? kstep_a : kstep_b);
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(is_a ? ra : rb, (lds_void*)(dst + (wave + 8 * c) * 512 + lane * 8), 16,
+                                               voff[h][c], soff, 0, 0);
+  };
+  auto bar = [] {
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  f32x4 acc[2][2][4][2];
+  u16x8 af[4][2], bq[2][2][2];  // layout-K fragments
+  uint64_t at[4][2][2], bt[2][2][2][2];  // layout-T fragment halves (i|j, kb, h2), joined at the MFMA
+
+  // fragment reads. Layout K: one ds_read_b128 (rows fr, k 8 fq .. 8 fq + 7 of a 32-deep k block). Layout T: two
+  // transposed reads (k rows 8 fq + 4 h2 + [0, 4)), lane 4q+p addressing row q, columns 4p .. 4p + 3.
+  const int tq = (lane & 15) >> 2, tp = lane & 3;
+  const int tsw = 2 * (tq | 4 * (fq & 1));  // swz_t of every row this lane addresses
+  const uint32_t lds32 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(
+      (__attribute__((address_space(3))) uint16_t*)lds));
+  auto tr_addr = [&](int region, int col0) {  // byte address of (row 8 fq + tq, 16-column block col0) of a T image
+    const int chunk = (col0 >> 3) + (tp >> 1);
+    return lds32 + 2 * (region + (8 * fq + tq) * 128 + 8 * (chunk ^ tsw) + 4 * (tp & 1));
+  };
+  uint32_t ta[4], tb[2];
+  if constexpr (AT) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ta[i] = tr_addr(0, wr * 64 + i * 16);
+  }
+  if constexpr (BT) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) tb[j] = tr_addr(32768, wc * 32 + j * 16);
+  }
+  // half-tile h of k-tile buffer `buf` (compile-time after unrolling)
+  auto read_a = [&](int buf, int h) {
+    const uint16_t* Ah = lds + lds_half(h, buf);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if constexpr (!AT) {
+        const int row = wr * 64 + i * 16 + fr;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+          af[i][kb] = *reinterpret_cast<const u16x8*>(Ah + row * 64 + 8 * ((4 * kb + fq) ^ swz_k(row)));
+      } else {
+#define DRL_TRA(KB, H2) at[i][KB][H2] = ds_read_tr(ta[i], 2 * (lds_half(h, buf) + KB * 32 * 128 + H2 * 4 * 128))
+        DRL_TRA(0, 0); DRL_TRA(0, 1); DRL_TRA(1, 0); DRL_TRA(1, 1);
+#undef DRL_TRA
+      }
+    }
+  };
+  auto read_b = [&](int buf, int h, int qn) {
+    const uint16_t* Bh = lds + lds_half(h, buf);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      if constexpr (!BT) {
+        const int row = wc * 32 + j * 16 + fr;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+          bq[qn][j][kb] = *reinterpret_cast<const u16x8*>(Bh + row * 64 + 8 * ((4 * kb + fq) ^ swz_k(row)));
+      } else {
+#define DRL_TRB(KB, H2) \
+  bt[qn][j][KB][H2] = ds_read_tr(tb[j], 2 * (lds_half(h, buf) - 32768 + KB * 32 * 128 + H2 * 4 * 128))
+        DRL_TRB(0, 0); DRL_TRB(0, 1); DRL_TRB(1, 0); DRL_TRB(1, 1);
+#undef DRL_TRB
+      }
+    }
+  };
+  constexpr int NB_READS = BT ? 8 : 4;   // LDS instructions of one B sub-tile read
+  constexpr int NA_READS = AT ? 16 : 8;  // of one A sub-tile read
+
+  // one segment: k-tile pairs [p0, p1) of the current tile accumulated into acc (zeroed first)
+  auto run = [&](int p0, int p1) {
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4{};
+    const int k0 = 2 * p0, k1 = 2 * p1;  // k-tiles [k0, k1)
+    issue(2, 0, k0, k1); issue(0, 0, k0, k1); issue(3, 0, k0, k1); issue(1, 0, k0, k1);
+    issue(2, 1, k0 + 1, k1); issue(0, 1, k0 + 1, k1); issue(3, 1, k0 + 1, k1);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    bar();
+    if (wr == 1) bar();  // the upper group runs one barrier behind
+    for (int kt = k0; kt < k1; kt += 2) {
+      const bool last = kt + 2 >= k1;
+#pragma unroll
+      for (int p = 0; p < 8; ++p) {
+        const int lp = p & 3, qm = lp >> 1, qn = (lp == 1 || lp == 2) ? 1 : 0;
+        const int buf = p >> 2;
+        if (lp == 0) {
+          read_b(buf, 2, 0);
+          __builtin_amdgcn_sched_barrier(0);
+          read_a(buf, 0);
+        } else if (lp == 1) {
+          read_b(buf, 3, 1);
+        } else if (lp == 2) {
+          read_a(buf, 1);
+        }
+        constexpr int kH[8] = {1, 2, 0, 3, 1, 2, 0, 3};
+        constexpr int kD[8] = {1, 2, 2, 2, 2, 3, 3, 3};
+        if (p == 0 || !last) issue(kH[p], kD[p] & 1, kt + kD[p], k1);
+        if (lp == 0) {  // the B0 reads (issued first) retired before the barrier (WAR of the next copies)
+          if constexpr (NA_READS >= 15) asm volatile("s_waitcnt lgkmcnt(15)" ::: "memory");
+          else if constexpr (NA_READS == 8) asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
+        }
+        if (p == 3) {
+          if (last) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        }
+        if (p == 7 && !last) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        bar();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);  // nothing that uses an asm read's result moves above its wait
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb) {
+              const u16x8 fa = AT ? join(at[i][kb][0], at[i][kb][1]) : af[i][kb];
+              const u16x8 fb = BT ? join(bt[qn][j][kb][0], bt[qn][j][kb][1]) : bq[qn][j][kb];
+              acc[qm][qn][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(fa), as_bf16x8(fb),
+                                                                          acc[qm][qn][i][j], 0, 0, 0);
+            }
+        __builtin_amdgcn_s_setprio(0);
+        bar();
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (wr == 0) bar();  // balance the upper group's extra barrier
+  };
+  (void)NB_READS;
+
+  // ------------------------------------------------------------------------------------------ epilogues
+  // accumulator block (i, j) of quadrant (qm, qn): tile row qm * 128 + wr * 64 + i * 16 + 4 fq + r, tile column
+  // wc * 64 + qn * 32 + j * 16 + fr (SwiGLU: output column wc * 32 + qn * 16 + fr, j = 0 gate, 1 up)
+  auto epilogue = [&](int m0, int n0) {
+    bar();  // every fragment read retired and every copy drained: LDS is free for staging
+    if constexpr (EPI == EPI_F32) {
+#pragma unroll
+      for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+        for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const int col = n0 + wc * 64 + qn * 32 + j * 16 + fr;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const int m = m0 + qm * 128 + wr * 64 + i * 16 + 4 * fq + r;
+                if (m < g.M && col < g.N) {
+                  float* p = g.c32 + static_cast<int64_t>(m) * g.ldc + col;
+                  *p = g.beta ? *p + acc[qm][qn][i][j][r] : acc[qm][qn][i][j][r];
+                }
+              }
+          }
+    } else if constexpr (EPI == EPI_SWIGLU) {
+      constexpr int SLD = 40, REG = 64 * SLD;
+      uint16_t* st = lds + wave * 3 * REG;
+      const int ch = lane & 3, col = n0 / 2 + wc * 32 + ch * 8;
+      const bool vec = col + 8 <= half && (g.ldc & 7) == 0 && (reinterpret_cast<uintptr_t>(g.c) & 15) == 0 &&
+                       (!g.c2 || ((g.ldc2 & 7) == 0 && (half & 7) == 0 && (reinterpret_cast<uintptr_t>(g.c2) & 15) == 0));
+#pragma unroll
+      for (int qm = 0; qm < 2; ++qm) {
+#pragma unroll
+        for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int o = (i * 16 + fq * 4 + r) * SLD + qn * 16 + fr;
+              const float gg = bf16r(acc[qm][qn][i][0][r]), uu = bf16r(acc[qm][qn][i][1][r]);
+              st[o] = to_bf16_bits(bf16r(gg / (1.f + expf(-gg))) * uu);
+              if (g.c2) {
+                st[REG + o] = to_bf16_bits(gg);
+                st[2 * REG + o] = to_bf16_bits(uu);
+              }
+            }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int it = 0; it < 4; ++it) {
+          const int lr = it * 16 + (lane >> 2);
+          const int m = m0 + qm * 128 + wr * 64 + lr;
+          const int o = lr * SLD + ch * 8;
+          const u16x8 va = *reinterpret_cast<const u16x8*>(st + o);
+          u16x8 vg, vu;
+          if (g.c2) {
+            vg = *reinterpret_cast<const u16x8*>(st + REG + o);
+            vu = *reinterpret_cast<const u16x8*>(st + 2 * REG + o);
+          }
+          if (m >= g.M || col >= half) continue;
+          uint16_t* pa = g.c + static_cast<int64_t>(m) * g.ldc + col;
+          uint16_t* pg = g.c2 ? g.c2 + static_cast<int64_t>(m) * g.ldc2 + col : nullptr;
+          if (vec) {
+            *reinterpret_cast<u16x8*>(pa) = va;
+            if (pg) {
+              *reinterpret_cast<u16x8*>(pg) = vg;
+              *reinterpret_cast<u16x8*>(pg + half) = vu;
+            }
+          } else {
+            for (int e = 0; e < 8 && col + e < half; ++e) {
+              pa[e] = va[e];
+              if (pg) {
+                pg[e] = vg[e];
+                pg[half + e] = vu[e];
+              }
+            }
+          }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      }
+    } else {
+      constexpr int SLD = 72;
+      uint16_t* st = lds + wave * 64 * SLD;
+      const int ch = lane & 7, col = n0 + wc * 64 + ch * 8;
+      const bool vec = col + 8 <= g.N && (g.ldc & 7) == 0 && (reinterpret_cast<uintptr_t>(g.c) & 15) == 0;
+#pragma unroll
+      for (int qm = 0; qm < 2; ++qm) {
+#pragma unroll
+        for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const int lc = qn * 32 + j * 16 + fr;
+            const float bv = EPI == EPI_BIAS ? bf16_to_f32(g.bias[min(n0 + wc * 64 + lc, g.N - 1)]) : 0.f;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                st[(i * 16 + fq * 4 + r) * SLD + lc] = to_bf16_bits(acc[qm][qn][i][j][r] + bv);
+          }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int it = 0; it < 8; ++it) {
+          const int lr = it * 8 + (lane >> 3);
+          const int m = m0 + qm * 128 + wr * 64 + lr;
+          const u16x8 v = *reinterpret_cast<const u16x8*>(st + lr * SLD + ch * 8);
+          if (m >= g.M || col >= g.N) continue;
+          uint16_t* dstp = g.c + static_cast<int64_t>(m) * g.ldc + col;
+          if (vec) {
+            *reinterpret_cast<u16x8*>(dstp) = v;
+          } else {
+            for (int e = 0; e < 8 && col + e < g.N; ++e) dstp[e] = v[e];
+          }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      }
+    }
+    bar();  // staging reads done before the next segment's copies land in LDS
+  };
+
+  auto tile_origin = [&](int t, int& m0, int& n0) {
+    const int grp = t / (g.gm * g.tn), first = grp * g.gm, gm = min(g.tm - first, g.gm), r = t % (g.gm * g.tn);
+    m0 = (first + r % gm) * 256;
+    n0 = (r / gm) * 256;
+  };
+
+  // ------------------------------------------------------------------------------------------ whole tiles
+  for (int t = wg; t < g.dp_tiles; t += G) {
+    int m0, n0;
+    tile_origin(t, m0, n0);
+    setup_tile(m0, n0);
+    run(0, g.P);
+    epilogue(m0, n0);
+  }
+
+  // ------------------------------------------------------------------------------------------ stream-K region
+  // 32-bit iteration arithmetic (the host keeps the iteration space below 2^23)
+  const int I = (g.n_tiles - g.dp_tiles) * g.P;
+  if (I == 0) return;
+  auto range_begin = [&](int w) { return static_cast<int>((static_cast<unsigned>(w) * static_cast<unsigned>(I)) /
+                                                          static_cast<unsigned>(G)); };
+  int it = range_begin(wg);
+  const int end = range_begin(wg + 1);
+  const __amdgpu_buffer_rsrc_t rws = __builtin_amdgcn_make_buffer_rsrc((void*)g.ws, (short)0, G * SLAB * 4, 0x00020000);
+  while (it < end) {
+    const int ts = it / g.P;
+    const int kb = it - ts * g.P;
+    const int ke = min(g.P, end - ts * g.P);
+    const int t = g.dp_tiles + ts;
+    int m0, n0;
+    tile_origin(t, m0, n0);
+    setup_tile(m0, n0);
+    run(kb, ke);
+    if (kb != 0) {
+      // tail: publish the partial tile (register order: coalesced 16-B lanes)
+      // buffer stores: per-lane voffset + a constant soffset per register (no 64-bit address per register for the
+      // compiler to hoist out of the loop and spill)
+      const uint32_t vo = static_cast<uint32_t>(wg) * SLAB * 4 + threadIdx.x * 16;
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[a][b][i][j]), rws, vo,
+                                                     (((a * 2 + b) * 4 + i) * 2 + j) * 8192, 0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(g.flags + wg, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    } else {
+      if (ke < g.P) {
+        // head of a split tile: add the tails of the workgroups that follow, in k order
+        const int tile_end = (ts + 1) * g.P;
+        for (int w2 = wg + 1; w2 < G && range_begin(w2) < tile_end; ++w2) {
+          if (threadIdx.x == 0) {
+            unsigned spins = 0;
+            while (__hip_atomic_load(g.flags + w2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+              __builtin_amdgcn_s_sleep(1);
+              if (++spins > (1u << 28)) {  // residency violated: record it and finish (wrong tile) instead of hanging
+                __hip_atomic_store(g.flags + G, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+              }
+            }
+            __hip_atomic_store(g.flags + w2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          }
+          __syncthreads();
+          const uint32_t vo = static_cast<uint32_t>(w2) * SLAB * 4 + threadIdx.x * 16;
+          // 2 loads in flight at a time: the 128 accumulator registers leave no room for more
+#pragma unroll
+          for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+#pragma unroll
+              for (int i = 0; i < 4; ++i) {
+                const int reg = ((a * 2 + b) * 4 + i) * 2;
+                const u32x4 s0 = __builtin_amdgcn_raw_buffer_load_b128(rws, vo, reg * 8192, 0);
+                const u32x4 s1 = __builtin_amdgcn_raw_buffer_load_b128(rws, vo, (reg + 1) * 8192, 0);
+                acc[a][b][i][0] += __builtin_bit_cast(f32x4, s0);
+                acc[a][b][i][1] += __builtin_bit_cast(f32x4, s1);
+                __builtin_amdgcn_sched_barrier(0);
+              }
+        }
+      }
+      epilogue(m0, n0);
+    }
+    it = ts * g.P + ke;
+    bar();  // LDS free (the tail path stages nothing, but the next segment's copies must not pass slower waves)
+  }
+}
+
+struct SkTuning {
+  int grid = 0;      // 0 = CU count
+  int group = 4;     // M-tiles per rasterization group
+  int dp_mode = 0;   // 0 automatic, 1 all stream-K, 2 all whole tiles (grid = tiles, no stream-K)
+  int min_iters = 0; // minimum k-pairs per workgroup in the stream-K region (0 automatic)
+};
+SkTuning g_sk;
+
+template <int AT, int BT>
+int launch_sk_layout(SkArgs& g, int epi, int grid, hipStream_t s) {
+  const dim3 gr(static_cast<unsigned>(grid));
+  switch (epi) {
+    case EPI_NONE: hipLaunchKernelGGL((gemm_sk_kernel<EPI_NONE, AT, BT>), gr, dim3(512), 0, s, g); break;
+    case EPI_F32: hipLaunchKernelGGL((gemm_sk_kernel<EPI_F32, AT, BT>), gr, dim3(512), 0, s, g); break;
+    case EPI_BIAS:
+      if constexpr (AT == 0 && BT == 0) hipLaunchKernelGGL((gemm_sk_kernel<EPI_BIAS, 0, 0>), gr, dim3(512), 0, s, g);
+      break;
+    case EPI_SWIGLU:
+      if constexpr (AT == 0 && BT == 0) hipLaunchKernelGGL((gemm_sk_kernel<EPI_SWIGLU, 0, 0>), gr, dim3(512), 0, s, g);
+      break;
+  }
+  DRL_LAUNCH_CHECK();
+  return DRL_OK;
+}
+
+}  // namespace
+}  // namespace drl
+
+extern "C" {
+
+int64_t drl_gemm_workspace_bytes(void) {
+  const int cus = drl::cu_count();
+  if (cus <= 0) return -1;
+  return static_cast<int64_t>(cus) * drl::SLAB * 4 + static_cast<int64_t>(cus + 1) * 4 + 256;
+}
+
+void drl_gemm_set_sk_tuning(int32_t grid, int32_t group, int32_t dp_mode, int32_t min_iters) {
+  drl::g_sk.grid = grid > 0 ? grid : 0;
+  drl::g_sk.group = (group >= 1 && group <= 64) ? group : 4;
+  drl::g_sk.dp_mode = (dp_mode >= 0 && dp_mode <= 2) ? dp_mode : 0;
+  drl::g_sk.min_iters = min_iters > 0 ? min_iters : 0;
+}
+
+int drl_gemm(const void* a, int64_t lda, int32_t a_layout, const void* b, int64_t ldb, int32_t b_layout, void* c,
+             int64_t ldc, int32_t c_dtype, int32_t beta, int64_t M, int64_t N, int64_t K, const void* bias,
+             int32_t epilogue, void* c2, int64_t ldc2, void* workspace, int64_t workspace_bytes, void* stream) {
+  using namespace drl;
+  DRL_CHECK_ARG(a && b && c, "NULL operand");
+  DRL_CHECK_ARG(a_layout == DRL_LAYOUT_K || a_layout == DRL_LAYOUT_T, "a_layout");
+  DRL_CHECK_ARG(b_layout == DRL_LAYOUT_K || b_layout == DRL_LAYOUT_T, "b_layout");
+  DRL_CHECK_ARG(M >= 1 && N >= 1 && K >= 1 && M < (1ll << 30) && N < (1ll << 30) && K < (1ll << 30),
+                "bad shape M=%lld N=%lld K=%lld", (long long)M, (long long)N, (long long)K);
+  DRL_CHECK_ARG(epilogue >= DRL_GEMM_PLAIN && epilogue <= DRL_GEMM_SWIGLU, "unknown epilogue %d", epilogue);
+  DRL_CHECK_ARG(c_dtype == DRL_BF16 || (c_dtype == DRL_F32 && epilogue == DRL_GEMM_PLAIN),
+                "fp32 output takes the plain epilogue");
+  DRL_CHECK_ARG(epilogue == DRL_GEMM_PLAIN || (a_layout == DRL_LAYOUT_K && b_layout == DRL_LAYOUT_K),
+                "bias / SwiGLU epilogues need layout-K operands (the forward)");
+  DRL_CHECK_ARG(epilogue != DRL_GEMM_BIAS || bias != nullptr, "bias epilogue without bias");
+  DRL_CHECK_ARG(epilogue != DRL_GEMM_SWIGLU || N % 64 == 0, "SwiGLU: N = 2I with I %% 32 == 0");
+  // a layout-K operand has K contiguous: its k tail would read the next row, so whole k-tile pairs only
+  DRL_CHECK_ARG((a_layout == DRL_LAYOUT_T && b_layout == DRL_LAYOUT_T) || K % 128 == 0,
+                "K %% 128 == 0 unless both operands are layout T (K=%lld)", (long long)K);
+  const int64_t a_rows = a_layout == DRL_LAYOUT_K ? M : K, a_cols = a_layout == DRL_LAYOUT_K ? K : M;
+  const int64_t b_rows = b_layout == DRL_LAYOUT_K ? N : K, b_cols = b_layout == DRL_LAYOUT_K ? K : N;
+  DRL_CHECK_ARG(lda >= a_cols && ldb >= b_cols && lda % 8 == 0 && ldb % 8 == 0 && aligned16(a) && aligned16(b),
+                "A / B: 16-byte aligned rows with ld %% 8 == 0 and ld >= the contiguous extent");
+  // 32-bit buffer offsets: the byte range plus one tile of overhang must stay below 2^32
+  const int64_t a_bytes = a_rows * lda * 2, b_bytes = b_rows * ldb * 2;
+  DRL_CHECK_ARG(a_bytes + 320ll * lda * 2 < (1ll << 32) && b_bytes + 320ll * ldb * 2 < (1ll << 32),
+                "operand larger than the 4 GB buffer range");
+  const int64_t ncols = epilogue == DRL_GEMM_SWIGLU ? N / 2 : N;
+  DRL_CHECK_ARG(ldc >= ncols && (c2 == nullptr || ldc2 >= N), "ldc");
+  const int64_t need = drl_gemm_workspace_bytes();
+  DRL_CHECK_ARG(workspace != nullptr && workspace_bytes >= need && aligned16(workspace),
+                "workspace: drl_gemm_workspace_bytes() = %lld bytes, flag words zeroed once", (long long)need);
+
+  SkArgs g{};
+  g.a = static_cast<const uint16_t*>(a);
+  g.b = static_cast<const uint16_t*>(b);
+  if (c_dtype == DRL_F32) g.c32 = static_cast<float*>(c);
+  else g.c = static_cast<uint16_t*>(c);
+  g.c2 = static_cast<uint16_t*>(c2);
+  g.bias = static_cast<const uint16_t*>(bias);
+  g.lda = lda; g.ldb = ldb; g.ldc = ldc; g.ldc2 = ldc2;
+  g.a_bytes = static_cast<uint32_t>(a_bytes);
+  g.b_bytes = static_cast<uint32_t>(b_bytes);
+  g.M = static_cast<int>(M); g.N = static_cast<int>(N); g.K = static_cast<int>(K);
+  g.beta = beta ? 1 : 0;
+  g.tm = static_cast<int>((M + 255) / 256);
+  g.tn = static_cast<int>((N + 255) / 256);
+  g.gm = g_sk.group;
+  g.P = static_cast<int>((K + 127) / 128);
+  g.n_tiles = g.tm * g.tn;
+  const int cus = cu_count();
+  g.ws = static_cast<float*>(workspace);
+  g.flags = reinterpret_cast<unsigned*>(static_cast<char*>(workspace) + static_cast<int64_t>(cus) * SLAB * 4);
+
+  // decomposition: whole-tile rounds while they fill the machine, stream-K over the rest (at most two rounds' worth
+  // of tiles, so the split region balances the tail); the grid never exceeds the CU count (co-residency)
+  int grid = g_sk.grid > 0 ? std::min(g_sk.grid, cus) : cus;
+  const int min_iters = g_sk.min_iters > 0 ? g_sk.min_iters : 2;
+  if (g_sk.dp_mode == 2) {
+    g.dp_tiles = g.n_tiles;
+    grid = std::min(grid, g.n_tiles);
+  } else {
+    int dp = 0;
+    if (g_sk.dp_mode == 0) {
+      const int full = g.n_tiles / grid;
+      dp = (g.n_tiles % grid == 0) ? g.n_tiles : std::max(0, full - 1) * grid;
+    }
+    g.dp_tiles = dp;
+    const int64_t I = static_cast<int64_t>(g.n_tiles - dp) * g.P;
+    if (dp == 0 && I > 0) grid = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(grid, I / min_iters)));
+  }
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int epi = epilogue == DRL_GEMM_PLAIN ? (c_dtype == DRL_F32 ? EPI_F32 : EPI_NONE)
+                                             : (epilogue == DRL_GEMM_BIAS ? EPI_BIAS : EPI_SWIGLU);
+  if (a_layout == DRL_LAYOUT_K && b_layout == DRL_LAYOUT_K) return launch_sk_layout<0, 0>(g, epi, grid, s);
+  if (a_layout == DRL_LAYOUT_K) return launch_sk_layout<0, 1>(g, epi, grid, s);
+  if (b_layout == DRL_LAYOUT_K) return launch_sk_layout<1, 0>(g, epi, grid, s);
+  return launch_sk_layout<1, 1>(g, epi, grid, s);
+}
+
+}  // extern "C"

@@ -717,6 +717,81 @@ def gemm_nt(x, w, bias=None, swiglu=False, out=None, out_gu=None):
     return out
 
 
+LAYOUT_K, LAYOUT_T = 0, 1
+
+
+class _GemmWorkspace:
+    """drl_gemm's stream-K slabs + flag words, one per device, zeroed once at allocation (every call leaves the
+    flag words zero again); calls share it in stream order on the current stream."""
+
+    def __init__(self):
+        self.buf = {}
+
+    def get(self, device):
+        key = device.index if device.index is not None else torch.cuda.current_device()
+        b = self.buf.get(key)
+        if b is None:
+            n = lib().drl_gemm_workspace_bytes()
+            if n <= 0:
+                raise RuntimeError(f"drl_gemm_workspace_bytes: {n}")
+            b = torch.zeros(n, dtype=torch.uint8, device=device)
+            self.buf[key] = b
+        return b
+
+
+_ws_gemm = _GemmWorkspace()
+
+
+def gemm(a, a_layout, b, b_layout, M, N, K, out, beta=False, bias=None, swiglu=False, out_gu=None):
+    """drl_gemm (csrc/gemm_sk.hip): out (M, N) (+)= sum_k A(m, k) B(n, k) with A(m, k) = a[m, k] (LAYOUT_K) or
+    a[k, m] (LAYOUT_T), B likewise; bf16 operands, fp32 accumulation; ``out`` bf16 (+ bias / SwiGLU epilogues) or
+    fp32 (``beta``: accumulate into it)."""
+    _dev(a, b, out, bias, out_gu)
+    assert a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and a.dim() == 2 and b.dim() == 2
+    assert a.stride(1) == 1 and b.stride(1) == 1 and out.stride(1) == 1
+    assert (a.shape == (M, K) if a_layout == LAYOUT_K else a.shape == (K, M)), (a.shape, M, K)
+    assert (b.shape == (N, K) if b_layout == LAYOUT_K else b.shape == (K, N)), (b.shape, N, K)
+    c_dt = _lib.DRL_F32 if out.dtype == torch.float32 else _lib.DRL_BF16
+    assert out.dtype in (torch.float32, torch.bfloat16)
+    assert out.shape == (M, N // 2 if swiglu else N), (out.shape, M, N)
+    if out_gu is not None:
+        assert swiglu and out_gu.shape == (M, N) and out_gu.stride(1) == 1
+    if bias is not None:
+        assert bias.is_contiguous() and bias.numel() == N
+    epi = GEMM_SWIGLU if swiglu else (GEMM_BIAS if bias is not None else GEMM_PLAIN)
+    ws = _ws_gemm.get(out.device)
+    check(lib().drl_gemm(_p(a), a.stride(0), a_layout, _p(b), b.stride(0), b_layout, _p(out), out.stride(0), c_dt,
+                         1 if beta else 0, M, N, K, _p(bias), epi, _p(out_gu),
+                         out_gu.stride(0) if out_gu is not None else 0, _p(ws), ws.numel(), _stream()), "drl_gemm")
+    return out
+
+
+def linear_fwd(x, w, bias=None, swiglu=False, out=None, out_gu=None):
+    """y = x W^T (+ bias) / SwiGLU(x [Wg | Wu]^T): x (M, K), w (N, K) -> (M, N) or (M, N / 2) bf16."""
+    M, K = x.shape
+    N = w.shape[0]
+    if out is None:
+        out = torch.empty(M, N // 2 if swiglu else N, dtype=torch.bfloat16, device=x.device)
+    return gemm(x, LAYOUT_K, w, LAYOUT_K, M, N, K, out, bias=bias, swiglu=swiglu, out_gu=out_gu)
+
+
+def linear_dgrad(dy, w, out=None):
+    """dx = dy W (F.linear's grad_input): dy (M, N_out) bf16, w (N_out, N_in) read in place -> (M, N_in) bf16."""
+    M, K = dy.shape
+    N = w.shape[1]
+    if out is None:
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=dy.device)
+    return gemm(dy, LAYOUT_K, w, LAYOUT_T, M, N, K, out)
+
+
+def linear_wgrad(gw, dy, x, accumulate=True):
+    """gw (N_out, N_in) fp32 (+)= dy^T x (F.linear's grad_weight, accumulated in fp32): dy (T, N_out), x (T, N_in)."""
+    T, M = dy.shape
+    N = x.shape[1]
+    assert x.shape[0] == T and gw.shape == (M, N) and gw.dtype == torch.float32
+    return gemm(dy, LAYOUT_T, x, LAYOUT_T, M, N, T, gw, beta=accumulate)
+
+
 LINEAR_NONE, LINEAR_BIAS, LINEAR_SWIGLU = 0, 1, 2
 
 

@@ -569,6 +569,29 @@ void drl_gemm_set_tile(int32_t tile);
  * column), 0 = automatic. Changes the schedule only, never the result. */
 void drl_gemm_set_group(int32_t group_m);
 
+/* ------------------------------------------------------------------------------------------------
+ * Every transformer GEMM of the actor's passes (csrc/gemm_sk.hip): the forward projections, their dgrad and their
+ * wgrad — replaces hipBLASLt behind nn.Linear's forward AND its autograd backward in HF Qwen2 / Llama under the
+ * reference's FSDP autocast (dp_actor.py:110; loss.backward() at dp_actor.py:466): dx = dy W (F.linear's grad_input),
+ * dW += dy^T x (grad_weight, accumulated over micro-batches in fp32 as FSDP's fp32 gradient).
+ *   C(m, n) (+)= sum_k A(m, k) B(n, k),  A(m, k) = a[m*lda + k] (DRL_LAYOUT_K) or a[k*lda + m] (DRL_LAYOUT_T),
+ *                                        B(n, k) = b[n*ldb + k] (DRL_LAYOUT_K) or b[k*ldb + n] (DRL_LAYOUT_T).
+ * bf16 operands, fp32 accumulation. c_dtype DRL_BF16: epilogues as drl_gemm_bf16_nt (bias / SwiGLU need both
+ * operands layout K); DRL_F32 (plain epilogue): c = acc, or c += acc when beta != 0. K % 128 == 0 unless both
+ * operands are layout T (then any K: the k tail reads as zeros). A / B 16-byte aligned, ld % 8 == 0, each operand
+ * < 4 GB. Work is split stream-K over at most one workgroup per CU; split tiles are summed in a fixed order
+ * (bit-reproducible). workspace: drl_gemm_workspace_bytes() bytes, 16-byte aligned, zeroed once at allocation
+ * (every call leaves its flag words zero again); calls sharing a workspace must be ordered on one stream. */
+enum { DRL_LAYOUT_K = 0, DRL_LAYOUT_T = 1 };
+int drl_gemm(const void* a, int64_t lda, int32_t a_layout, const void* b, int64_t ldb, int32_t b_layout, void* c,
+             int64_t ldc, int32_t c_dtype, int32_t beta, int64_t M, int64_t N, int64_t K, const void* bias,
+             int32_t epilogue, void* c2, int64_t ldc2, void* workspace, int64_t workspace_bytes, void* stream);
+int64_t drl_gemm_workspace_bytes(void);
+/* Tuning hook of drl_gemm: grid (0 = CU count), M-tiles per rasterization group, dp_mode (0 automatic: whole-tile
+ * rounds while they fill the grid, stream-K for the last one or two; 1 = all stream-K; 2 = whole tiles only),
+ * min_iters (minimum k-tile pairs per workgroup of an all-stream-K grid, 0 = 2). Schedule only, same result. */
+void drl_gemm_set_sk_tuning(int32_t grid, int32_t group, int32_t dp_mode, int32_t min_iters);
+
 
 /* 16-bit transpose: dst (cols, rows) = src (rows, cols)^T (row strides in elements). The weights' transposed
  * copies for the backward dgrad (dx = dy W run as the TN product dy (W^T)^T: gate_up 129 -> 105 us, down 57 -> 47 us

@@ -1,0 +1,100 @@
+"""drl_gemm (csrc/gemm_sk.hip) vs hipBLASLt on every GEMM of the actor's passes at config #2 (Qwen2.5-0.5B):
+forward (y = x W^T), dgrad (dx = dy W) and wgrad (dW += dy^T x, fp32) of qkv / o / gate_up / down at the update
+(8 x 768) and log-prob (16 x 768) micro-batch rows, and the lm_head over the response rows. One JSON line per
+shape: microseconds and TFLOP/s of both, interleaved rounds in one process (cdna_hip_programming.md §5.4 rule 24).
+
+  python tools/gemm_sk_bench.py [--quick] [--tune]
+"""
+
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from dots.rl_amd import native  # noqa: E402
+
+
+def bench(fn, iters=20, warmup=3, rounds=3):
+    for _ in range(warmup):
+        fn()
+    best = []
+    for _ in range(rounds):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(iters):
+            fn()
+        b.record()
+        b.synchronize()
+        best.append(a.elapsed_time(b) * 1e3 / iters)
+    best.sort()
+    return best[len(best) // 2]
+
+
+def shapes(quick):
+    H, I, NQ, V = 896, 4864, 1152, 151936
+    out = []
+    for M in ((6144,) if quick else (6144, 12288)):
+        out += [("qkv_fwd", "fwd", M, NQ, H), ("o_fwd", "fwd", M, H, H), ("gate_up_fwd_swiglu", "swiglu", M, 2 * I, H),
+                ("down_fwd", "fwd", M, H, I)]
+        if M == 6144:
+            out += [("qkv_dgrad", "dgrad", M, H, NQ), ("o_dgrad", "dgrad", M, H, H), ("gate_up_dgrad", "dgrad", M, H, 2 * I),
+                    ("down_dgrad", "dgrad", M, I, H), ("qkv_wgrad", "wgrad", NQ, H, M), ("o_wgrad", "wgrad", H, H, M),
+                    ("gate_up_wgrad", "wgrad", 2 * I, H, M), ("down_wgrad", "wgrad", H, I, M)]
+    out += [("lm_head_fwd", "fwd", 2048, V, H), ("lm_head_dgrad", "dgrad", 2048, H, V), ("lm_head_wgrad", "wgrad", V, H, 2048)]
+    if not quick:
+        out += [("lm_head_fwd_4096", "fwd", 4096, V, H)]
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--quick", action="store_true")
+    ap.add_argument("--tune", action="store_true", help="also sweep grid / dp_mode / group of drl_gemm")
+    args = ap.parse_args()
+    from dots.rl_amd.workers import _enable_gemm_tuning
+    _enable_gemm_tuning("auto")
+    dev, bf = "cuda", torch.bfloat16
+    g = torch.Generator(device=dev).manual_seed(0)
+    for name, kind, M, N, K in shapes(args.quick):
+        fl = 2.0 * M * N * K
+        if kind in ("fwd", "swiglu"):
+            x = torch.randn(M, K, generator=g, device=dev).to(bf)
+            w = (torch.randn(N, K, generator=g, device=dev) * 0.05).to(bf)
+            sw = kind == "swiglu"
+            a = torch.empty(M, N // 2, device=dev, dtype=bf)
+            ours = lambda: native.linear_fwd(x, w, swiglu=sw)  # noqa: E731
+            lib = (lambda: native.swiglu_fwd(x @ w.t(), a)) if sw else (lambda: x @ w.t())  # noqa: E731
+        elif kind == "dgrad":  # dx (M, N) = dy (M, K) @ W (K, N)
+            dy = torch.randn(M, K, generator=g, device=dev).to(bf)
+            w = (torch.randn(K, N, generator=g, device=dev) * 0.05).to(bf)
+            ours = lambda: native.linear_dgrad(dy, w)  # noqa: E731
+            lib = lambda: dy @ w  # noqa: E731
+        else:  # gw (M=out, N=in) += dy^T x, dy (K, M), x (K, N)
+            dy = torch.randn(K, M, generator=g, device=dev).to(bf)
+            x = torch.randn(K, N, generator=g, device=dev).to(bf)
+            gw = torch.zeros(M, N, device=dev)
+            ours = lambda: native.linear_wgrad(gw, dy, x)  # noqa: E731
+            lib = lambda: torch.addmm(gw, dy.t(), x, out_dtype=torch.float32, out=gw)  # noqa: E731
+        row = dict(shape=name, M=M, N=N, K=K)
+        t_lib = bench(lib)
+        t_ours = bench(ours)
+        row.update(hipblaslt_us=t_lib, hipblaslt_TF=fl / t_lib / 1e6, ours_us=t_ours, ours_TF=fl / t_ours / 1e6)
+        if args.tune:
+            sweep = {}
+            for grid in (0, 192, 224):
+                for dp in (0, 1, 2):
+                    for mi in (0, 4):
+                        if dp == 2 and mi:
+                            continue
+                        native.lib().drl_gemm_set_sk_tuning(grid, 0, dp, mi)
+                        sweep[f"g{grid}_dp{dp}_mi{mi}"] = round(bench(ours, iters=10, rounds=2), 2)
+            native.lib().drl_gemm_set_sk_tuning(0, 0, 0, 0)
+            row["sweep_us"] = sweep
+        print(json.dumps(row), flush=True)
+
+
+if __name__ == "__main__":
+    main()
