@@ -22,7 +22,7 @@
 // Work decomposition: stream-K over (tile, k-pair) iterations (cdna_hip_programming.md §5 "Decomposition first"),
 // grid = at most one workgroup per CU. The first `dp_tiles` tiles are dealt whole (tile wg, wg + G, ...); the rest
 // form one iteration space split into G contiguous, balanced ranges. A range's first segment that starts inside a
-// tile (a "tail") stores its fp32 partial tile to the workgroup's slab and publishes a flag (agent-scope release);
+// tile (a "tail") stores its fp32 partial tile to the workgroup's slab write-through (sc1) and publishes a flag;
 // the workgroup that holds the tile's k = 0 segment (its "head", always the LAST segment of that workgroup's range,
 // so the tails it waits for were computed first) adds its own accumulator and the tails' slabs in k order — a fixed
 // order, so results are bit-reproducible — and runs the epilogue. The flag is reset by its consumer: every launch
@@ -62,9 +62,11 @@ struct SkArgs {
   int M, N, K;
   int tm, tn, gm;      // tiles along M and N; M-tiles per rasterization group
   int P;               // k-tile pairs per tile
+  int nkt;             // k-tiles holding data (ceil(K / 64)); a pair's second tile past it reads as zeros
   int dp_tiles;        // tiles dealt whole before the stream-K region
   int n_tiles;
   int beta;            // EPI_F32: 1 = C += acc
+  int splits;          // > 1: uniform split-K, workgroup wg = split (wg % splits) of tile (wg / splits)
 };
 
 __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
@@ -153,7 +155,9 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
     const int k = min(kt, kt_end - 1);
     uint16_t* dst = lds + lds_half(h, buf);
     const bool is_a = h < 2;
-    const uint32_t soff = static_cast<uint32_t>(k) * (is_a ? kstep_a : kstep_b);
+    // k-tile past the data (K % 128 == 64): an soffset of the whole byte range puts every lane out of range (zeros)
+    const uint32_t soff = k >= g.nkt ? (is_a ? g.a_bytes : g.b_bytes)
+                                     : static_cast<uint32_t>(k) * (is_a ? kstep_a : kstep_b);
 #pragma unroll
     for (int c = 0; c < 2; ++c)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(is_a ? ra : rb, (lds_void*)(dst + (wave + 8 * c) * 512 + lane * 8), 16,
@@ -297,24 +301,39 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
   auto epilogue = [&](int m0, int n0) {
     bar();  // every fragment read retired and every copy drained: LDS is free for staging
     if constexpr (EPI == EPI_F32) {
+      // through LDS per quadrant: the wave's 64 x 32 fp32 block (row stride 36 floats), read back as 16-B row pieces
+      // (8 lanes per 128-B row) for a coalesced read-modify-write of the fp32 output
+      constexpr int SLD = 36;
+      float* st = reinterpret_cast<float*>(lds) + wave * 64 * SLD;
+      const int ch = lane & 7;
+      const bool vec = (g.ldc & 3) == 0 && (reinterpret_cast<uintptr_t>(g.c32) & 15) == 0;
 #pragma unroll
       for (int qm = 0; qm < 2; ++qm)
 #pragma unroll
-        for (int qn = 0; qn < 2; ++qn)
+        for (int qn = 0; qn < 2; ++qn) {
 #pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            const int col = n0 + wc * 64 + qn * 32 + j * 16 + fr;
+          for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int i = 0; i < 4; ++i)
 #pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                const int m = m0 + qm * 128 + wr * 64 + i * 16 + 4 * fq + r;
-                if (m < g.M && col < g.N) {
-                  float* p = g.c32 + static_cast<int64_t>(m) * g.ldc + col;
-                  *p = g.beta ? *p + acc[qm][qn][i][j][r] : acc[qm][qn][i][j][r];
-                }
-              }
+              for (int r = 0; r < 4; ++r) st[(i * 16 + 4 * fq + r) * SLD + j * 16 + fr] = acc[qm][qn][i][j][r];
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          const int col = n0 + wc * 64 + qn * 32 + 4 * ch;
+#pragma unroll
+          for (int it = 0; it < 8; ++it) {
+            const int lr = it * 8 + (lane >> 3);
+            const int m = m0 + qm * 128 + wr * 64 + lr;
+            const f32x4 v = *reinterpret_cast<const f32x4*>(st + lr * SLD + 4 * ch);
+            if (m >= g.M || col >= g.N) continue;
+            float* p = g.c32 + static_cast<int64_t>(m) * g.ldc + col;
+            if (vec && col + 4 <= g.N) {
+              *reinterpret_cast<f32x4*>(p) = g.beta ? *reinterpret_cast<const f32x4*>(p) + v : v;
+            } else {
+              for (int e = 0; e < 4 && col + e < g.N; ++e) p[e] = g.beta ? p[e] + v[e] : v[e];
+            }
           }
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next quadrant's writes
+        }
     } else if constexpr (EPI == EPI_SWIGLU) {
       constexpr int SLD = 40, REG = 64 * SLD;
       uint16_t* st = lds + wave * 3 * REG;
@@ -415,6 +434,93 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
     n0 = (r / gm) * 256;
   };
 
+  typedef __attribute__((address_space(1))) unsigned gflag;
+  // ------------------------------------------------------------------------------------------ uniform split-K
+  // Few tiles, long K (the weight gradients of the small projections, down_proj, the N = H dgrads, the lm_head
+  // dgrad): the S workgroups of a tile each accumulate a k-pair range, publish it (sc1 slab + arrival count), wait for
+  // all S arrivals, then each reduces 1/S of the tile's registers over the S slabs in split order (a fixed order:
+  // bit-reproducible) and writes that share through the epilogue — the combine runs on all S workgroups at once.
+  if (g.splits > 1) {
+    const int S = g.splits, t = wg / S, sp = wg - t * S;
+    int m0, n0;
+    {
+      const int grp = t / (g.gm * g.tn), first = grp * g.gm, gmm = min(g.tm - first, g.gm), r = t % (g.gm * g.tn);
+      m0 = (first + r % gmm) * 256;
+      n0 = (r / gmm) * 256;
+    }
+    setup_tile(m0, n0);
+    run(sp * g.P / S, (sp + 1) * g.P / S);
+    const __amdgpu_buffer_rsrc_t rws = __builtin_amdgcn_make_buffer_rsrc((void*)g.ws, (short)0, G * SLAB * 4, 0x00020000);
+    const uint32_t vo = static_cast<uint32_t>(wg) * SLAB * 4 + threadIdx.x * 16;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[a][b][i][j]), rws, vo,
+                                                   (((a * 2 + b) * 4 + i) * 2 + j) * 8192, 16 /* sc1 */);
+    // arrival: every storing wave drains its sc1 stores, the barrier, ONE lane's agent-scope add; then ONE lane polls
+    // the count (sc1 loads) until all S slices arrived (MI355X_MICROARCH.md § visibility, first row of the sc1 table)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    gflag* cnt = (gflag*)(g.flags + t);
+    if (threadIdx.x == 0) {
+      __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      unsigned spins = 0;
+      while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < static_cast<unsigned>(S)) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > (1u << 28)) {  // residency violated: record it and finish (wrong tile) instead of hanging
+          __hip_atomic_store((gflag*)(g.flags + G), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+    }
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the barrier
+    // this slice's share of the tile: register groups [32 sp / S, 32 (sp + 1) / S)
+    const int r0 = 32 * sp / S, r1 = 32 * (sp + 1) / S;
+    const uint32_t vt = static_cast<uint32_t>(t * S) * SLAB * 4 + threadIdx.x * 16;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const int reg = ((a * 2 + b) * 4 + i) * 2 + j;
+            if (reg < r0 || reg >= r1) continue;
+            f32x4 v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rws, vt, reg * 8192, 16));
+            for (int s2 = 1; s2 < S; ++s2)
+              v += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rws, vt + s2 * SLAB * 4, reg * 8192, 16));
+            const int col = n0 + wc * 64 + b * 32 + j * 16 + fr;
+            if (col >= g.N) continue;
+            const float bv = EPI == EPI_BIAS ? bf16_to_f32(g.bias[col]) : 0.f;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int m = m0 + a * 128 + wr * 64 + i * 16 + 4 * fq + r;
+              if (m >= g.M) continue;
+              if constexpr (EPI == EPI_F32) {
+                float* p = g.c32 + static_cast<int64_t>(m) * g.ldc + col;
+                *p = g.beta ? *p + v[r] : v[r];
+              } else if constexpr (EPI != EPI_SWIGLU) {
+                g.c[static_cast<int64_t>(m) * g.ldc + col] = to_bf16_bits(v[r] + bv);
+              }
+            }
+          }
+    // departure: the last of the S slices to finish reading resets the count (every launch ends with it at zero)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned prev = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (prev == static_cast<unsigned>(2 * S - 1)) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return;
+  }
+
   // ------------------------------------------------------------------------------------------ whole tiles
   for (int t = wg; t < g.dp_tiles; t += G) {
     int m0, n0;
@@ -456,33 +562,35 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
 #pragma unroll
             for (int j = 0; j < 2; ++j)
               __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[a][b][i][j]), rws, vo,
-                                                     (((a * 2 + b) * 4 + i) * 2 + j) * 8192, 0);
+                                                     (((a * 2 + b) * 4 + i) * 2 + j) * 8192, 16 /* sc1 */);
+      // publish (MI355X_MICROARCH.md § visibility, first row of the sc1 table; cdna_hip_programming.md §6 G16 R1):
+      // write-through (sc1) 16-B payload stores drained by EVERY storing wave, the workgroup barrier, then ONE lane's
+      // agent-scope flag store — no release fence (a buffer_wbl2 would write back the whole XCD L2 mid-GEMM)
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(g.flags + wg, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
+      if (threadIdx.x == 0)
+        __hip_atomic_store((__attribute__((address_space(1))) unsigned*)(g.flags + wg), 1u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
     } else {
       if (ke < g.P) {
         // head of a split tile: add the tails of the workgroups that follow, in k order
         const int tile_end = (ts + 1) * g.P;
         for (int w2 = wg + 1; w2 < G && range_begin(w2) < tile_end; ++w2) {
+          // consume: ONE lane polls the flag (relaxed agent = sc1 load), the workgroup barrier, then every load of
+          // the slab is an sc1 buffer load (no acquire: it would invalidate the XCD's L2 under the running GEMM)
           if (threadIdx.x == 0) {
             unsigned spins = 0;
-            while (__hip_atomic_load(g.flags + w2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+            while (__hip_atomic_load((gflag*)(g.flags + w2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
               __builtin_amdgcn_s_sleep(1);
               if (++spins > (1u << 28)) {  // residency violated: record it and finish (wrong tile) instead of hanging
-                __hip_atomic_store(g.flags + G, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store((gflag*)(g.flags + G), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 break;
               }
             }
-            __hip_atomic_store(g.flags + w2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store((gflag*)(g.flags + w2), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           }
           __syncthreads();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the barrier
           const uint32_t vo = static_cast<uint32_t>(w2) * SLAB * 4 + threadIdx.x * 16;
           // 2 loads in flight at a time: the 128 accumulator registers leave no room for more
 #pragma unroll
@@ -492,8 +600,8 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
 #pragma unroll
               for (int i = 0; i < 4; ++i) {
                 const int reg = ((a * 2 + b) * 4 + i) * 2;
-                const u32x4 s0 = __builtin_amdgcn_raw_buffer_load_b128(rws, vo, reg * 8192, 0);
-                const u32x4 s1 = __builtin_amdgcn_raw_buffer_load_b128(rws, vo, (reg + 1) * 8192, 0);
+                const u32x4 s0 = __builtin_amdgcn_raw_buffer_load_b128(rws, vo, reg * 8192, 16 /* sc1 */);
+                const u32x4 s1 = __builtin_amdgcn_raw_buffer_load_b128(rws, vo, (reg + 1) * 8192, 16 /* sc1 */);
                 acc[a][b][i][0] += __builtin_bit_cast(f32x4, s0);
                 acc[a][b][i][1] += __builtin_bit_cast(f32x4, s1);
                 __builtin_amdgcn_sched_barrier(0);
@@ -507,11 +615,14 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
   }
 }
 
+inline bool epi_is_swiglu(int epilogue) { return epilogue == DRL_GEMM_SWIGLU; }
+
 struct SkTuning {
   int grid = 0;      // 0 = CU count
   int group = 4;     // M-tiles per rasterization group
-  int dp_mode = 0;   // 0 automatic, 1 all stream-K, 2 all whole tiles (grid = tiles, no stream-K)
-  int min_iters = 0; // minimum k-pairs per workgroup in the stream-K region (0 automatic)
+  int mode = 0;      // 0 automatic (whole tiles, or uniform split-K for few long-K tiles), 1 stream-K (whole-tile
+                     // rounds + a stream-K tail), 2 whole tiles only, 3 uniform split-K
+  int param = 0;     // mode 1: minimum k-pairs per workgroup; mode 3: splits per tile (0 automatic)
 };
 SkTuning g_sk;
 
@@ -543,11 +654,11 @@ int64_t drl_gemm_workspace_bytes(void) {
   return static_cast<int64_t>(cus) * drl::SLAB * 4 + static_cast<int64_t>(cus + 1) * 4 + 256;
 }
 
-void drl_gemm_set_sk_tuning(int32_t grid, int32_t group, int32_t dp_mode, int32_t min_iters) {
+void drl_gemm_set_sk_tuning(int32_t grid, int32_t group, int32_t mode, int32_t param) {
   drl::g_sk.grid = grid > 0 ? grid : 0;
   drl::g_sk.group = (group >= 1 && group <= 64) ? group : 4;
-  drl::g_sk.dp_mode = (dp_mode >= 0 && dp_mode <= 2) ? dp_mode : 0;
-  drl::g_sk.min_iters = min_iters > 0 ? min_iters : 0;
+  drl::g_sk.mode = (mode >= 0 && mode <= 3) ? mode : 0;
+  drl::g_sk.param = param > 0 ? param : 0;
 }
 
 int drl_gemm(const void* a, int64_t lda, int32_t a_layout, const void* b, int64_t ldb, int32_t b_layout, void* c,
@@ -566,17 +677,19 @@ int drl_gemm(const void* a, int64_t lda, int32_t a_layout, const void* b, int64_
                 "bias / SwiGLU epilogues need layout-K operands (the forward)");
   DRL_CHECK_ARG(epilogue != DRL_GEMM_BIAS || bias != nullptr, "bias epilogue without bias");
   DRL_CHECK_ARG(epilogue != DRL_GEMM_SWIGLU || N % 64 == 0, "SwiGLU: N = 2I with I %% 32 == 0");
-  // a layout-K operand has K contiguous: its k tail would read the next row, so whole k-tile pairs only
-  DRL_CHECK_ARG((a_layout == DRL_LAYOUT_T && b_layout == DRL_LAYOUT_T) || K % 128 == 0,
-                "K %% 128 == 0 unless both operands are layout T (K=%lld)", (long long)K);
+  // a layout-K operand has K contiguous: a partial k-tile would read the next row, so whole 64-deep k-tiles (a
+  // missing second tile of the last pair reads as zeros)
+  DRL_CHECK_ARG((a_layout == DRL_LAYOUT_T && b_layout == DRL_LAYOUT_T) || K % 64 == 0,
+                "K %% 64 == 0 unless both operands are layout T (K=%lld)", (long long)K);
   const int64_t a_rows = a_layout == DRL_LAYOUT_K ? M : K, a_cols = a_layout == DRL_LAYOUT_K ? K : M;
   const int64_t b_rows = b_layout == DRL_LAYOUT_K ? N : K, b_cols = b_layout == DRL_LAYOUT_K ? K : N;
   DRL_CHECK_ARG(lda >= a_cols && ldb >= b_cols && lda % 8 == 0 && ldb % 8 == 0 && aligned16(a) && aligned16(b),
                 "A / B: 16-byte aligned rows with ld %% 8 == 0 and ld >= the contiguous extent");
   // 32-bit buffer offsets: the byte range plus one tile of overhang must stay below 2^32
   const int64_t a_bytes = a_rows * lda * 2, b_bytes = b_rows * ldb * 2;
-  DRL_CHECK_ARG(a_bytes + 320ll * lda * 2 < (1ll << 32) && b_bytes + 320ll * ldb * 2 < (1ll << 32),
-                "operand larger than the 4 GB buffer range");
+  // (below 2 GB: voffset + a whole-range soffset must not wrap around 2^32)
+  DRL_CHECK_ARG(a_bytes + 320ll * lda * 2 < (1ll << 31) && b_bytes + 320ll * ldb * 2 < (1ll << 31),
+                "operand larger than the 2 GB buffer range");
   const int64_t ncols = epilogue == DRL_GEMM_SWIGLU ? N / 2 : N;
   DRL_CHECK_ARG(ldc >= ncols && (c2 == nullptr || ldc2 >= N), "ldc");
   const int64_t need = drl_gemm_workspace_bytes();
@@ -599,26 +712,44 @@ int drl_gemm(const void* a, int64_t lda, int32_t a_layout, const void* b, int64_
   g.tn = static_cast<int>((N + 255) / 256);
   g.gm = g_sk.group;
   g.P = static_cast<int>((K + 127) / 128);
+  g.nkt = static_cast<int>((K + 63) / 64);
   g.n_tiles = g.tm * g.tn;
   const int cus = cu_count();
   g.ws = static_cast<float*>(workspace);
   g.flags = reinterpret_cast<unsigned*>(static_cast<char*>(workspace) + static_cast<int64_t>(cus) * SLAB * 4);
 
-  // decomposition: whole-tile rounds while they fill the machine, stream-K over the rest (at most two rounds' worth
-  // of tiles, so the split region balances the tail); the grid never exceeds the CU count (co-residency)
-  int grid = g_sk.grid > 0 ? std::min(g_sk.grid, cus) : cus;
-  const int min_iters = g_sk.min_iters > 0 ? g_sk.min_iters : 2;
-  if (g_sk.dp_mode == 2) {
+  // decomposition (grid never above the CU count: co-residency). Automatic: uniform split-K when the tiles fill at
+  // most half the CUs and K is long enough to split (S = the most splits that fit the CUs, >= 2 k-pairs each, <= 16;
+  // the SwiGLU epilogue pairs whole tiles, never split), else whole tiles in rounds.
+  const int cap = g_sk.grid > 0 ? std::min(g_sk.grid, cus) : cus;
+  int grid = cap;
+  int mode = g_sk.mode;
+  int S = 1;
+  if (mode == 0 && g.n_tiles * 2 <= cap && g.P >= 256 && !epi_is_swiglu(epilogue)) {
+    mode = 1;  // very long K over few tiles (the lm_head dgrad: 32 tiles x 1187 k-pairs): stream-K measured best
+  } else if (mode == 0 || mode == 3) {
+    // at most 8 splits of >= 6 k-pairs each (profiles/r03_gemm_sk_sweep.jsonl: more or shorter splits lose to the
+    // slab traffic and the per-split pipeline fill)
+    S = mode == 3 && g_sk.param > 0 ? g_sk.param : std::min({cap / std::max(1, g.n_tiles), 8, g.P / 6});
+    S = std::max(1, std::min({S, g.P, 32, cap / std::max(1, g.n_tiles)}));
+    if (epi_is_swiglu(epilogue) || g.n_tiles * 2 > cap) S = 1;
+    mode = S > 1 ? 3 : 2;
+  }
+  g.splits = 1;
+  if (mode == 3) {
+    g.splits = S;
+    g.dp_tiles = 0;
+    grid = g.n_tiles * S;
+  } else if (mode == 2) {
     g.dp_tiles = g.n_tiles;
-    grid = std::min(grid, g.n_tiles);
+    grid = std::min(cap, g.n_tiles);
   } else {
-    int dp = 0;
-    if (g_sk.dp_mode == 0) {
-      const int full = g.n_tiles / grid;
-      dp = (g.n_tiles % grid == 0) ? g.n_tiles : std::max(0, full - 1) * grid;
-    }
+    const int full = g.n_tiles / grid;
+    const int dp = (g.n_tiles % grid == 0) ? g.n_tiles : std::max(0, full - 1) * grid;
     g.dp_tiles = dp;
     const int64_t I = static_cast<int64_t>(g.n_tiles - dp) * g.P;
+    const int min_iters = g_sk.param > 0 ? g_sk.param : 2;
+    DRL_CHECK_ARG(I < (1 << 23), "stream-K iteration space too large");
     if (dp == 0 && I > 0) grid = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(grid, I / min_iters)));
   }
   hipStream_t s = static_cast<hipStream_t>(stream);

@@ -298,9 +298,36 @@ class ParamStore:
 
 
 # --------------------------------------------------------------------------------------------- GEMM helpers
+# Every bf16 GEMM of the full-sequence passes — forward, dgrad and wgrad of each projection and of the lm_head — runs
+# on csrc/gemm_sk.hip (drl_gemm: stream-K 256 x 256 ping-pong, weights read in their stored layout for the dgrad,
+# fp32 accumulation into the gradient buffer for the wgrad). DRL_GEMM=hipblaslt routes them to hipBLASLt instead (A/B
+# measurements only); the fp32 parity model (compute_dtype=float32) uses torch's fp32 GEMMs.
+GEMM_BACKEND = os.environ.get("DRL_GEMM", "hip")
+
+
+def _sk(*ts):
+    return GEMM_BACKEND == "hip" and all(t.dtype == torch.bfloat16 and t.is_cuda for t in ts)
+
+
+def linear(x, w, bias=None):
+    """y = x W^T (+ bias) for x (N, in), w (out, in) in the compute dtype (bias added before the single rounding)."""
+    if _sk(x, w) and x.shape[1] % 64 == 0:
+        return native.linear_fwd(x, w, bias=bias)
+    return torch.addmm(bias, x, w.t()) if bias is not None else x @ w.t()
+
+
+def dgrad(dy, w):
+    """dx = dy W (F.linear's grad_input) for dy (N, out), w (out, in)."""
+    if _sk(dy, w) and dy.shape[1] % 64 == 0:
+        return native.linear_dgrad(dy, w)
+    return dy @ w
+
+
 def acc_wgrad(gw, dy, x):
-    """gw (out, in) fp32 += dy^T x  with dy (N, out), x (N, in) in the compute dtype (hipBLASLt, fp32 out)."""
-    if dy.dtype == torch.float32:
+    """gw (out, in) fp32 += dy^T x  with dy (N, out), x (N, in) in the compute dtype (fp32 accumulation in place)."""
+    if _sk(dy, x):
+        native.linear_wgrad(gw, dy, x)
+    elif dy.dtype == torch.float32:
         gw.addmm_(dy.t(), x)
     else:  # accumulate in place (C = D, beta = 1): no temporary, no copy of the fp32 gradient
         torch.addmm(gw, dy.t(), x, out_dtype=torch.float32, out=gw)
@@ -314,21 +341,21 @@ def bmm_f32(a, b):
 
 
 class _Linear(torch.autograd.Function):
-    """y = x W^T on hipBLASLt; backward dx = dy W, dW += dy^T x in fp32 (lm_head over the response rows)."""
+    """y = x W^T; backward dx = dy W, dW += dy^T x in fp32 (lm_head over the response rows)."""
 
     @staticmethod
     def forward(ctx, x, w, gw, dummy):
         ctx.save_for_backward(x, w)
         ctx.gw = gw
-        return F.linear(x, w)
+        return linear(x.reshape(-1, x.shape[-1]), w).view(*x.shape[:-1], w.shape[0])
 
     @staticmethod
     def backward(ctx, dy):
         x, w = ctx.saved_tensors
-        dy = dy.contiguous()
+        dy = dy.contiguous().reshape(-1, dy.shape[-1])
         if ctx.gw is not None:
-            acc_wgrad(ctx.gw, dy.reshape(-1, dy.shape[-1]), x.reshape(-1, x.shape[-1]))
-        return dy @ w, None, None, None
+            acc_wgrad(ctx.gw, dy, x.reshape(-1, x.shape[-1]))
+        return dgrad(dy, w).view(*x.shape), None, None, None
 
 
 class _Embedding(torch.autograd.Function):
@@ -349,16 +376,12 @@ class _Embedding(torch.autograd.Function):
 
 
 # --------------------------------------------------------------------------------------------- decoder layer
-# Full-sequence projections through csrc/gemm.hip's ping-pong GEMM (bias / SwiGLU fused in the epilogue) where
-# it measured at or above hipBLASLt (profiles/r02_gemm_pingpong.jsonl): bf16, >= 2048 rows, K <= 1152 — qkv_proj,
-# o_proj, gate_up_proj; the long-K down_proj and the lm_head stay on hipBLASLt. DRL_HIP_GEMM=0 turns it off (A/B).
-HIP_GEMM = os.environ.get("DRL_HIP_GEMM", "1") != "0"
-HIP_GEMM_MIN_ROWS = 2048  # below it the 256 x 256 grid leaves most CUs idle (tests lower it to pin the path)
+# Full-sequence projections (bias / SwiGLU fused in the epilogue) on drl_gemm (above) for every row count.
+HIP_GEMM_MIN_ROWS = 1  # kept for tests that pin the path
 
 
 def _hip_gemm(x, rows, K):
-    return (HIP_GEMM and x.dtype == torch.bfloat16 and x.is_cuda and rows >= HIP_GEMM_MIN_ROWS and K % 128 == 0
-            and K <= 1152)
+    return _sk(x) and rows >= HIP_GEMM_MIN_ROWS and K % 64 == 0
 
 
 def _layer_forward(m, i, x_prev, delta, pos, key_valid, save, cache=None, koff=0, koff_dev=None):
@@ -378,7 +401,7 @@ def _layer_forward(m, i, x_prev, delta, pos, key_valid, save, cache=None, koff=0
     native.add_rmsnorm_fwd(x_prev, delta, x if delta is not None else None, s.w(p + "input_layernorm"), h1, rstd1,
                            cfg.rms_norm_eps)
     if _hip_gemm(h1, B * T, H):
-        qkv = native.gemm_nt(h1.view(B * T, H), s.w(p + "qkv_proj.weight"), bias=m.qkv_bias(i))
+        qkv = native.linear_fwd(h1.view(B * T, H), s.w(p + "qkv_proj.weight"), bias=m.qkv_bias(i))
     else:
         qkv = torch.addmm(m.qkv_bias(i), h1.view(B * T, H), s.w(p + "qkv_proj.weight").t())
     qkv = qkv.view(B, T, -1)
@@ -458,7 +481,7 @@ def _layer_mlp(m, i, x, attn, save, kbuf, vbuf, P, q, h1, rstd1):
     p = f"layers.{i}."
     dev = x.device
     if _hip_gemm(attn, B * T, Hq * D):
-        o = native.gemm_nt(attn.reshape(B * T, Hq * D), s.w(p + "o_proj"))
+        o = native.linear_fwd(attn.reshape(B * T, Hq * D), s.w(p + "o_proj"))
     else:
         o = attn.view(B * T, Hq * D) @ s.w(p + "o_proj").t()
     x2 = torch.empty_like(x)
@@ -468,12 +491,12 @@ def _layer_mlp(m, i, x, attn, save, kbuf, vbuf, P, q, h1, rstd1):
     if _hip_gemm(h2, B * T, H):
         # SwiGLU fused into the gate_up GEMM's epilogue; gu = [g | u] written only when the backward needs it
         gu = torch.empty(B * T, 2 * cfg.intermediate_size, dtype=dt, device=dev) if save is not None else None
-        a = native.gemm_nt(h2.view(B * T, H), s.w(p + "gate_up_proj"), swiglu=True, out_gu=gu)
+        a = native.linear_fwd(h2.view(B * T, H), s.w(p + "gate_up_proj"), swiglu=True, out_gu=gu)
     else:
         gu = h2.view(B * T, H) @ s.w(p + "gate_up_proj").t()
         a = torch.empty(B * T, cfg.intermediate_size, dtype=dt, device=dev)
         native.swiglu_fwd(gu, a)
-    mlp = (a @ s.w(p + "down_proj").t()).view(B, T, H)
+    mlp = linear(a, s.w(p + "down_proj")).view(B, T, H)
     if save is not None:
         save.update(x=x, rstd1=rstd1, h1=h1, q=q, k=kbuf, v=vbuf, P=P, attn=attn, x2=x2, rstd2=rstd2, h2=h2,
                     gu=gu, a=a)
@@ -501,18 +524,17 @@ class _DecoderLayer(torch.autograd.Function):
         dx2 = g_x2.to(torch.float32).contiguous().clone()
         dm = g_mlp.to(dt).contiguous().view(N, H)
         # MLP
-        tn = dt == torch.bfloat16  # dgrad as the TN product with the transposed weight copy (see Qwen2Model.wt)
-        da = dm @ m.wt(p + "down_proj").t() if tn else dm @ s.w(p + "down_proj")
+        da = dgrad(dm, s.w(p + "down_proj"))
         acc_wgrad(s.g(p + "down_proj"), dm, sv["a"])
         dgu = torch.empty_like(sv["gu"])
         native.swiglu_bwd(sv["gu"], da, dgu)
-        dh2 = dgu @ m.wt(p + "gate_up_proj").t() if tn else dgu @ s.w(p + "gate_up_proj")
+        dh2 = dgrad(dgu, s.w(p + "gate_up_proj"))
         acc_wgrad(s.g(p + "gate_up_proj"), dgu, sv["h2"].view(N, H))
         native.rmsnorm_bwd(sv["x2"], s.w(p + "post_attention_layernorm"), sv["rstd2"], dh2, dx2,
                            s.g(p + "post_attention_layernorm"))
         # attention output projection
         do = dx2.to(dt).view(N, H)
-        dattn = do @ m.wt(p + "o_proj").t() if tn else do @ s.w(p + "o_proj")
+        dattn = dgrad(do, s.w(p + "o_proj"))
         acc_wgrad(s.g(p + "o_proj"), do, sv["attn"].reshape(N, Hq * D))
         if isinstance(sv["P"], str):  # "flash": fused forward, fused backward
             # fused attention backward (P recomputed from the saved LSE)
@@ -537,7 +559,7 @@ class _DecoderLayer(torch.autograd.Function):
         dqkv = torch.empty(B, T, (Hq + 2 * Hkv) * D, dtype=dt, device=dx2.device)
         native.rope_qkv_bwd(dq, dk, dv, ctx.pos, m.cos, m.sin, Hq, Hkv, D, dqkv)
         dqkv2 = dqkv.view(N, -1)
-        dh1 = dqkv2 @ m.wt(p + "qkv_proj.weight").t() if tn else dqkv2 @ s.w(p + "qkv_proj.weight")
+        dh1 = dgrad(dqkv2, s.w(p + "qkv_proj.weight"))
         acc_wgrad(s.g(p + "qkv_proj.weight"), dqkv2, sv["h1"].view(N, H))
         if m.cfg.attention_bias:
             if dqkv2.dtype == torch.bfloat16:
@@ -622,25 +644,9 @@ class Qwen2Model:
         if cfg.rope_scaling:
             raise NotImplementedError(f"rope_scaling {cfg.rope_scaling} (plain RoPE only: Qwen2 / Llama-3-8B)")
         self._zero_bias = None
-        self._wt = {}  # name -> (store version, transposed weight), see wt()
         if not cfg.attention_bias:  # Llama: the shared qkv epilogues add a constant zero bias
             nq = (cfg.num_attention_heads + 2 * cfg.num_key_value_heads) * cfg.head_dim
             self._zero_bias = torch.zeros(nq, dtype=self.dtype, device=dev)
-
-    def wt(self, name):
-        """Transposed bf16 copy (in, out) of GEMM weight ``name`` for the backward's dgrad dx = dy W, run as the TN
-        product dy @ wt.t(): tuned (tools/tune_dgrad.py, shipped tuning file) at 6144 rows qkv 22.1 -> 19.8 us,
-        o 20.8 -> 19.6, gate_up 96.3 -> 88.8, down 55.3 -> 44.4 against the NN form dy @ W; re-transposed
-        (csrc/layers.hip transpose16) when the weights changed (once per optimizer step)."""
-        ver = self.store.version
-        hit = self._wt.get(name)
-        if hit is not None and hit[0] == ver:
-            return hit[1]
-        w = self.store.w(name)
-        buf = hit[1] if hit is not None else torch.empty(w.shape[1], w.shape[0], dtype=w.dtype, device=w.device)
-        native.transpose16(w, out=buf)
-        self._wt[name] = (ver, buf)
-        return buf
 
     def qkv_bias(self, i):
         return self.store.w(f"layers.{i}.qkv_proj.bias") if self.cfg.attention_bias else self._zero_bias
@@ -652,11 +658,11 @@ class Qwen2Model:
         return "embed_tokens" if self.cfg.tie_word_embeddings else "lm_head"
 
     def logits(self, h):
-        """h (N, H) in the compute dtype -> (N, V) logits in the compute dtype (hipBLASLt)."""
+        """h (N, H) in the compute dtype -> (N, V) logits in the compute dtype."""
         name = self.lm_head_weight()
         if self.training and self.store.trainable:
             return _Linear.apply(h, self.store.w(name), self.store.g(name), self._dummy)
-        return F.linear(h, self.store.w(name))
+        return linear(h.reshape(-1, h.shape[-1]), self.store.w(name)).view(*h.shape[:-1], -1)
 
     def select_tokens(self, h, out_tokens, fused=True, **sel):
         """Token selection from the final-norm hidden h (N, H): K4 fused with the lm_head on bf16 (the (N, V)

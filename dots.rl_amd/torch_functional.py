@@ -61,8 +61,8 @@ class _FusedLinearLogprobEntropy(torch.autograd.Function):
     """A21: lm_head + log-prob + entropy without materialising logits (FusedLinearForPPOFunction,
     utils/experimental/torch_functional.py:75-150; linear_cross_entropy.py:41-117 with reduction "none").
     Backward = the reference's BackwardEnum._Total_Separate: one kernel writes d_logits^T (V, N) bf16 from
-    recomputed logits, then d_hidden = d_logits W and d_W += d_logits^T hidden on hipBLASLt (d_W straight
-    into the fp32 gradient buffer ``weight_grad`` when given)."""
+    recomputed logits, then d_hidden = d_logits W and d_W += d_logits^T hidden on drl_gemm (csrc/gemm_sk.hip;
+    d_W straight into the fp32 gradient buffer ``weight_grad`` when given)."""
 
     @staticmethod
     def forward(ctx, hidden, weight, weight_grad, labels, temperature, want_entropy):
@@ -82,10 +82,20 @@ class _FusedLinearLogprobEntropy(torch.autograd.Function):
             dent = None
         dlt = native.linear_logprob_dlogits(hidden, weight, labels, ctx.temperature, dlogp, dent, lse,
                                             ent if dent is not None else None)
-        dh = dlt.t() @ weight
+        V, N = dlt.shape
+        H = weight.shape[1]
+        hip = dlt.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16 and dlt.is_contiguous()
+        if hip:  # dh (N, H) = dlt^T W on drl_gemm: both operands read in place (layout T), any V
+            dh = native.gemm(dlt, native.LAYOUT_T, weight, native.LAYOUT_T, N, H, V,
+                             torch.empty(N, H, dtype=torch.bfloat16, device=dlt.device))
+        else:
+            dh = dlt.t() @ weight
         dw = None
         if ctx.weight_grad is not None:
-            torch.addmm(ctx.weight_grad, dlt, hidden, out_dtype=torch.float32, out=ctx.weight_grad)
+            if hip and N % 64 == 0 and hidden.is_contiguous():  # dW (V, H) += dlt hidden, fp32 in place
+                native.gemm(dlt, native.LAYOUT_K, hidden, native.LAYOUT_T, V, H, N, ctx.weight_grad, beta=True)
+            else:
+                torch.addmm(ctx.weight_grad, dlt, hidden, out_dtype=torch.float32, out=ctx.weight_grad)
         elif ctx.needs_input_grad[1]:
             dw = dlt @ hidden
         return dh, dw, None, None, None, None

@@ -23,7 +23,7 @@ extern "C" {
 #endif
 
 /* 3: drl_ppo_loss_params gained policy_loss, cov_ratio, clip_cov_lb, clip_cov_ub, ppo_kl_coef, cov_seed (a caller
- * built against version 2 passes a shorter struct); drl_gemm_bf16 (operand layouts, fp32 epilogues, split-K) */
+ * built against version 2 passes a shorter struct); drl_gemm (operand layouts, fp32 epilogues, stream-K) */
 #define DRL_ABI_VERSION 3
 
 #define DRL_OK 0
@@ -577,9 +577,9 @@ void drl_gemm_set_group(int32_t group_m);
  *   C(m, n) (+)= sum_k A(m, k) B(n, k),  A(m, k) = a[m*lda + k] (DRL_LAYOUT_K) or a[k*lda + m] (DRL_LAYOUT_T),
  *                                        B(n, k) = b[n*ldb + k] (DRL_LAYOUT_K) or b[k*ldb + n] (DRL_LAYOUT_T).
  * bf16 operands, fp32 accumulation. c_dtype DRL_BF16: epilogues as drl_gemm_bf16_nt (bias / SwiGLU need both
- * operands layout K); DRL_F32 (plain epilogue): c = acc, or c += acc when beta != 0. K % 128 == 0 unless both
+ * operands layout K); DRL_F32 (plain epilogue): c = acc, or c += acc when beta != 0. K % 64 == 0 unless both
  * operands are layout T (then any K: the k tail reads as zeros). A / B 16-byte aligned, ld % 8 == 0, each operand
- * < 4 GB. Work is split stream-K over at most one workgroup per CU; split tiles are summed in a fixed order
+ * < 2 GB. Work is split stream-K over at most one workgroup per CU; split tiles are summed in a fixed order
  * (bit-reproducible). workspace: drl_gemm_workspace_bytes() bytes, 16-byte aligned, zeroed once at allocation
  * (every call leaves its flag words zero again); calls sharing a workspace must be ordered on one stream. */
 enum { DRL_LAYOUT_K = 0, DRL_LAYOUT_T = 1 };

@@ -1025,6 +1025,10 @@ GRPO_STEP_CASES = [
     # n = 1: singleton groups (mean 0, std 1 -> A = score / (1 + 1e-6)): a real policy-gradient update
     dict(name="n1", n_prompts=8, n=1, P=12, R=10, pads=[0, 3, 0, 5, 1, 0, 2, 0], lr=1e-4, mini_prompts=4, micro=2,
          rm_scores=[1.0, 0.0, 0.5, 1.0, 0.0, -0.5, 1.0, 0.25], seed=7, compare_update=True),
+    # groups of 2 DISTINCT responses (uid pairs over 8 different prompts, n = 1): the group-normalised advantages
+    # (+-1/sqrt 2 by score order, 0 for a tie) do not cancel, so the post-update parameters are compared too
+    dict(name="pairs", n_prompts=8, n=1, P=12, R=10, pads=[2, 0, 0, 4, 0, 1, 3, 0], lr=1e-4, mini_prompts=4, micro=2,
+         rm_scores=[1.0, 0.0, 0.25, 0.75, 0.5, 0.5, -1.0, 1.0], seed=23, compare_update=True, uid_pairs=True),
 ]
 GRPO_TIMING = {"gen": 0.5, "reward": 0.01, "old_log_prob": 0.2, "ref": 0.2, "adv": 0.01, "update_actor": 0.8,
                "step": 1.75}
@@ -1081,6 +1085,8 @@ def _grpo_step_case(S):
     batch = run_rollout(TINY_QWEN2["eos_token_id"])
     eos = int(batch.batch["responses"][2 if n > 1 else 1, 3])  # some rows stop mid-response
     batch = run_rollout(eos)
+    if S.get("uid_pairs"):  # rows (2i, 2i + 1) form one GRPO group
+        batch.non_tensor_batch["uid"] = np.array([f"pair{i // 2}" for i in range(Np * n)], dtype=object)
     B = Np * n
     batch.batch["response_mask"] = rt.compute_response_mask(batch)
     batch.meta_info["global_token_num"] = torch.sum(batch.batch["attention_mask"], dim=-1).tolist()
@@ -1213,9 +1219,15 @@ def gen_full_depth():
         d16 = lbr.gather(-1, t2[..., :1]) - lbr.gather(-1, t2[..., 1:])
         gap_err = (d16 - d32).abs().squeeze(-1)  # (B, R): bf16 error of the top-2 margin itself
         logp_bf16 = vF.logprobs_from_logits_v2(lb.float()[:, -R - 1:-1], resp)
+        # the teacher-forced reference logits of every response step, summarised (the full (4, 64, V) block is
+        # 155 MB): the 32 largest with their token ids, the logsumexp, and the CPU bf16 model's values at those ids
+        topv, topi = torch.topk(lg, 32, -1)
+        lse = torch.logsumexp(lg.double(), -1).float()
+        bf_at_top = lbr.gather(-1, topi)
     arrays = dict(prompt_ids=ids, prompt_attention_mask=am, prompt_position_ids=pos, sequences=seq, responses=resp,
                   attention_mask=full_am, position_ids=full_pos, top2_gap=gaps, log_probs=logp, entropy=ent,
-                  cpu_bf16_logit_err=err_max_row, cpu_bf16_gap_err=gap_err, cpu_bf16_log_probs=logp_bf16)
+                  cpu_bf16_logit_err=err_max_row, cpu_bf16_gap_err=gap_err, cpu_bf16_log_probs=logp_bf16,
+                  ref_top32_ids=topi, ref_top32_logits=topv, ref_lse=lse, cpu_bf16_top32_logits=bf_at_top)
     _save("full_depth.npz", arrays, {
         "eos_token_id": eos, "pad_token_id": pad, "response_length": R, "weights": "full_depth.make_state_dict()",
         "scales": fd.SCALES, "seed": fd.SEED, "weight_checksum": fd.checksum(sd), "min_top2_gap": float(gaps.min()),

@@ -165,7 +165,7 @@ class _PresetRM:
         return DataProto.from_dict({"rm_scores": rm})
 
 
-@pytest.mark.parametrize("ci", [0, 1])
+@pytest.mark.parametrize("ci", [0, 1, 2])
 def test_grpo_fit_step_matches_reference(ci):
     from stub_tokenizer import StubTokenizer
 
@@ -191,6 +191,8 @@ def test_grpo_fit_step_matches_reference(ci):
     trainer = RayPPOTrainer(cfg, tokenizer=StubTokenizer(), rm_wg=_PresetRM(m["rm_scores"]),
                             eos_token_id=m["eos_token_id"], pad_token_id=m["pad_token_id"])
     trainer.init_workers()
+    if m.get("uid_pairs"):  # the reference case groups rows (2i, 2i + 1): distinct responses in one GRPO group
+        trainer._uids = lambda k: np.array([f"pair{i // 2}" for i in range(k)], dtype=object)
     store = trainer.actor_rollout_wg.worker.store
     before = store.master.detach().cpu().clone()
     trainer.global_steps = 1

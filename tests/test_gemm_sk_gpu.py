@@ -20,7 +20,7 @@ def _op(shape, layout, g, scale=1.0):
     if layout == K_:
         buf = torch.randn(r, k + 8, generator=g, device="cuda") * scale
         return buf.to(torch.bfloat16)[:, :k], lambda t: t.float()
-    buf = torch.randn(k, r + 8, generator=g, device="cuda") * scale
+    buf = torch.randn(k, (r + 15) // 8 * 8, generator=g, device="cuda") * scale  # ld % 8 == 0, > r
     return buf.to(torch.bfloat16)[:, :r], lambda t: t.float().t()
 
 
@@ -32,7 +32,8 @@ def _default_tuning():
 
 
 @pytest.mark.parametrize("al,bl", [(K_, K_), (K_, T_), (T_, K_), (T_, T_)])
-@pytest.mark.parametrize("M,N,K", [(300, 520, 256), (1024, 896, 1152), (96, 200, 4864), (2304, 2304, 384)])
+@pytest.mark.parametrize("M,N,K", [(300, 520, 256), (1024, 896, 1152), (96, 200, 4864), (2304, 2304, 384),
+                                   (130, 700, 192)])
 def test_layouts_bf16_and_f32(al, bl, M, N, K):
     g = torch.Generator(device="cuda").manual_seed(M * 7 + N + K + 3 * al + bl)
     a, fa = _op((M, K), al, g)
@@ -93,24 +94,33 @@ def test_forward_epilogues(M):
     assert (a.float() - want.float()).abs().max() < 0.05 * want.float().abs().max()
 
 
-@pytest.mark.parametrize("mode", [(0, 0), (1, 0), (2, 0), (1, 37), (1, 7)])
-def test_decompositions_agree(mode):
-    """Whole tiles, all stream-K, odd grids: the same GEMM within fp32 summation-order differences."""
-    dp_mode, grid = mode
+@pytest.mark.parametrize("mode", [(0, 0, 0), (1, 0, 0), (2, 0, 0), (3, 0, 0), (3, 0, 5), (3, 0, 32), (1, 37, 0),
+                                  (1, 7, 0)])
+@pytest.mark.parametrize("out_dtype", [torch.float32, torch.bfloat16])
+def test_decompositions_agree(mode, out_dtype):
+    """Automatic, stream-K, whole tiles, uniform split-K (automatic / 5 / 32 splits), odd grids: the same GEMM
+    within fp32 summation-order differences."""
+    dp_mode, grid, param = mode
     g = torch.Generator(device="cuda").manual_seed(11)
     a = torch.randn(1000, 4864, generator=g, device="cuda").to(torch.bfloat16)
     b = torch.randn(896, 4864, generator=g, device="cuda").to(torch.bfloat16)
-    ref = a.double() @ b.double().t()
-    native.lib().drl_gemm_set_sk_tuning(grid, 0, dp_mode, 0)
-    out = torch.empty(1000, 896, device="cuda")
-    native.gemm(a, K_, b, K_, 1000, 896, 4864, out)
-    torch.testing.assert_close(out.double(), ref, rtol=1e-6, atol=4e-6 * 4864 ** 0.5)
+    bias = torch.randn(896, generator=g, device="cuda").to(torch.bfloat16) if out_dtype == torch.bfloat16 else None
+    ref = a.double() @ b.double().t() + (bias.double() if bias is not None else 0)
+    native.lib().drl_gemm_set_sk_tuning(grid, 0, dp_mode, param)
+    out = torch.empty(1000, 896, device="cuda", dtype=out_dtype)
+    native.gemm(a, K_, b, K_, 1000, 896, 4864, out, bias=bias)
+    if out_dtype == torch.float32:
+        torch.testing.assert_close(out.double(), ref, rtol=1e-6, atol=4e-6 * 4864 ** 0.5)
+    else:
+        torch.testing.assert_close(out.double(), ref.to(torch.bfloat16).double(), rtol=8e-3, atol=4e-6 * 4864 ** 0.5)
 
 
-@pytest.mark.parametrize("al,bl,M,N,K", [(K_, K_, 6144, 896, 4864), (K_, T_, 2048, 896, 151936 // 4),
+@pytest.mark.parametrize("al,bl,M,N,K", [(K_, K_, 6144, 896, 4864), (K_, T_, 2048, 896, 37888),
                                          (T_, T_, 896, 896, 6144), (K_, K_, 6144, 9728, 896)])
-def test_race_screen(al, bl, M, N, K):
+@pytest.mark.parametrize("mode", [(0, 0), (1, 0), (3, 4)])
+def test_race_screen(al, bl, M, N, K, mode):
     """16 launches bit-identical (split tiles are reduced in k order, whatever the arrival order)."""
+    native.lib().drl_gemm_set_sk_tuning(0, 0, mode[0], mode[1])
     g = torch.Generator(device="cuda").manual_seed(M + N + K)
     a, _ = _op((M, K), al, g)
     b, _ = _op((N, K), bl, g)

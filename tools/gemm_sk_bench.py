@@ -84,13 +84,12 @@ def main():
         row.update(hipblaslt_us=t_lib, hipblaslt_TF=fl / t_lib / 1e6, ours_us=t_ours, ours_TF=fl / t_ours / 1e6)
         if args.tune:
             sweep = {}
-            for grid in (0, 192, 224):
-                for dp in (0, 1, 2):
-                    for mi in (0, 4):
-                        if dp == 2 and mi:
-                            continue
-                        native.lib().drl_gemm_set_sk_tuning(grid, 0, dp, mi)
-                        sweep[f"g{grid}_dp{dp}_mi{mi}"] = round(bench(ours, iters=10, rounds=2), 2)
+            for grid, mode, param in [(0, 1, 0), (192, 1, 0), (0, 2, 0), (0, 3, 0), (0, 3, 2), (0, 3, 4), (0, 3, 8),
+                                      (0, 3, 16), (192, 3, 0)]:
+                if mode == 3 and param and param * (M + 255) // 256 * ((N + 255) // 256) > 256:
+                    continue
+                native.lib().drl_gemm_set_sk_tuning(grid, 0, mode, param)
+                sweep[f"g{grid}_m{mode}_p{param}"] = round(bench(ours, iters=10, rounds=2), 2)
             native.lib().drl_gemm_set_sk_tuning(0, 0, 0, 0)
             row["sweep_us"] = sweep
         print(json.dumps(row), flush=True)
