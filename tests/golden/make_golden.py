@@ -1239,6 +1239,90 @@ def gen_full_depth():
 
 
 # --------------------------------------------------------------------------------------------
+# Configs #4 / #5 at full width, 2 decoder layers (tests/golden/wide.py weights, never committed), fp32 on the CPU:
+# config #4 (Llama-3-8B): actor log-probs / entropy (dp_actor.py:249-272), the vanilla PPO loss's backward (per-tensor
+# gradient norms), the critic (LlamaForTokenClassification, num_labels 1: dp_critic.py:127-145 values slice), its
+# value-loss backward (dp_critic.py:218-245) and GAE over its values (core_algos.py:208-256); config #5 (Qwen2.5-7B):
+# actor log-probs / entropy / loss backward. The CPU bf16-autocast model's log-probs and values size the bf16 bound.
+# --------------------------------------------------------------------------------------------
+def gen_wide():
+    import wide
+    from transformers import LlamaConfig, LlamaForCausalLM, LlamaForTokenClassification, Qwen2Config, Qwen2ForCausalLM
+
+    arrays, meta = {}, {}
+    for which in ("llama", "qwen7b"):
+        cfgd = wide.LLAMA3_8B_W if which == "llama" else wide.QWEN25_7B_W
+        sd = wide.make_state_dict(which)
+        ids, am, pos, R = wide.sequences(which)
+        resp = ids[:, -R:]
+        rmask = am[:, -R:]
+        if which == "llama":
+            cfg = LlamaConfig(**cfgd, attn_implementation="eager", mlp_bias=False)
+            actor = LlamaForCausalLM(cfg).float()
+        else:
+            cfg = Qwen2Config(**cfgd, attn_implementation="eager")
+            actor = Qwen2ForCausalLM(cfg).float()
+        missing, unexpected = actor.load_state_dict({k: v for k, v in sd.items() if not k.startswith("score")},
+                                                    strict=True), None
+        g = torch.Generator().manual_seed(4 if which == "llama" else 5)
+        lg = actor(input_ids=ids, attention_mask=am, position_ids=pos, use_cache=False).logits[:, -R - 1:-1]
+        logp = vF.logprobs_from_logits_v2(lg, resp)
+        ent = vF.entropy_from_logits(lg)
+        old = logp.detach() + 0.05 * torch.randn(logp.shape, generator=g)
+        adv = torch.randn(logp.shape, generator=g)
+        pg, _, _, _ = ca.compute_policy_loss_vanilla(old_log_prob=old, log_prob=logp, advantages=adv,
+                                                     response_mask=rmask, loss_agg_mode="token-mean",
+                                                     config=DictConfig(_actor_cfg()))
+        pg.backward()
+        gnorm = {k: float(p.grad.double().norm()) for k, p in actor.named_parameters()}
+        with torch.no_grad(), torch.autocast("cpu", dtype=torch.bfloat16):
+            lb = actor(input_ids=ids, attention_mask=am, position_ids=pos, use_cache=False).logits
+        logp_bf16 = vF.logprobs_from_logits_v2(lb.float()[:, -R - 1:-1], resp)
+        p = f"{which}_"
+        arrays.update({p + "input_ids": ids, p + "attention_mask": am, p + "position_ids": pos, p + "log_probs": logp,
+                       p + "entropy": ent, p + "old_log_probs": old, p + "advantages": adv, p + "pg_loss": pg.detach(),
+                       p + "cpu_bf16_log_probs": logp_bf16})
+        meta[which] = {"grad_norms": gnorm, "response_length": R, "weight_checksum": wide.checksum(sd),
+                       "cpu_bf16_logp_err_max": float((logp_bf16 - logp).abs().max())}
+        del actor, lg, lb
+        if which == "llama":
+            cfgc = LlamaConfig(**cfgd, attn_implementation="eager", mlp_bias=False, num_labels=1,
+                               classifier_dropout=0.0)
+            critic = LlamaForTokenClassification(cfgc).float()
+            csd = {k: v for k, v in sd.items() if not k.startswith("lm_head")}
+            critic.load_state_dict(csd, strict=True)
+            critic.train()
+            vpreds = critic(input_ids=ids, attention_mask=am, position_ids=pos, use_cache=False).logits
+            vpreds = vpreds[:, -R - 1:-1].squeeze(-1)
+            with torch.no_grad(), torch.autocast("cpu", dtype=torch.bfloat16):
+                vb = critic(input_ids=ids, attention_mask=am, position_ids=pos, use_cache=False).logits
+            vb = vb.float()[:, -R - 1:-1].squeeze(-1)
+            # token-level rewards: a score at the last valid response token (GAE over the critic's own values)
+            scores = torch.tensor([1.0, -0.5])
+            vl = rmask.sum(-1)
+            rewards = torch.zeros(ids.shape[0], R)
+            rewards[torch.arange(ids.shape[0]), vl - 1] = scores
+            adv_g, ret_g = ca.compute_gae_advantage_return(rewards, vpreds.detach(), rmask, gamma=1.0, lam=0.95)
+            values_old = (vpreds.detach() + 0.1 * torch.randn(vpreds.shape, generator=g)) * rmask
+            vf_loss, vf_clipfrac = ca.compute_value_loss(vpreds=vpreds, returns=ret_g, values=values_old,
+                                                         response_mask=rmask, cliprange_value=0.5,
+                                                         loss_agg_mode="token-mean")
+            (vf_loss * 0.5).backward()
+            cnorm = {k: float(q.grad.double().norm()) for k, q in critic.named_parameters()}
+            arrays.update({p + "values": vpreds.detach(), p + "cpu_bf16_values": vb, p + "token_level_rewards": rewards,
+                           p + "gae_advantages": adv_g, p + "gae_returns": ret_g, p + "values_old": values_old,
+                           p + "vf_loss": vf_loss.detach(), p + "vf_clipfrac": vf_clipfrac})
+            meta[which].update(critic_grad_norms=cnorm, gamma=1.0, lam=0.95, cliprange_value=0.5,
+                               cpu_bf16_value_err_max=float((vb - vpreds.detach()).abs().max()))
+            del critic
+        del sd
+    meta["ref"] = ("dp_actor.py:249-272, core_algos.py:815-889 (vanilla, token-mean), dp_critic.py:127-145, 218-245, "
+                   "core_algos.py:208-256, 1230-1269; HF LlamaForCausalLM / LlamaForTokenClassification / "
+                   "Qwen2ForCausalLM fp32 eager attention")
+    _save("wide.npz", arrays, meta)
+
+
+# --------------------------------------------------------------------------------------------
 # LR schedules (fsdp_workers.py:461-486): the reference's LambdaLR over a real torch optimizer, the lr read with
 # get_last_lr() before each lr_scheduler.step() as update_actor does (fsdp_workers.py:717-719)
 # --------------------------------------------------------------------------------------------

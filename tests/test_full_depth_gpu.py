@@ -106,8 +106,11 @@ def test_fp32_full_depth_matches_reference(ref, weights):
                  ("position_ids", "position_ids")]:
         np.testing.assert_array_equal(out.batch[k].cpu().numpy(), z[r], err_msg=k)
     lp, ent, _ = _teacher_forced(model, z)
-    np.testing.assert_allclose(lp, z["log_probs"], rtol=1e-4, atol=1e-4)
-    np.testing.assert_allclose(ent, z["entropy"], rtol=1e-4, atol=1e-4)
+    # fp32 summation-order differences scale with the logits (up to 170 with these weights: 2e-6 relative over the
+    # 896-term lm_head sums); 1e-4 floor as for O(10) logits
+    atol = max(1e-4, 2e-6 * float(np.abs(z["ref_top32_logits"]).max()))
+    np.testing.assert_allclose(lp, z["log_probs"], rtol=1e-4, atol=atol)
+    np.testing.assert_allclose(ent, z["entropy"], rtol=1e-4, atol=atol)
 
 
 @pytest.mark.parametrize("packed,hip_gemm_rows", [(True, None), (False, None), (True, 1), (False, 1)])
