@@ -160,6 +160,7 @@ def cpu_baseline(cfg):
                    n_optimizer_steps=n_mini)
     return {"value": 1.0 / r["step_s"], "unit": "PPO steps/s", "cores": r["threads"], "kind": "port",
             "sample": r["sample"], "est_step_s": r["step_s"],
+            "value_range": [1.0 / r["step_s_range"][1], 1.0 / r["step_s_range"][0]],
             "est_parts_s": {k: v for k, v in r.items() if k.endswith("_s") and k != "step_s"}}
 
 
