@@ -665,6 +665,22 @@ int drl_gemm(const void* a, int64_t lda, int32_t a_layout, const void* b, int64_
              int64_t ldc, int32_t c_dtype, int32_t beta, int64_t M, int64_t N, int64_t K, const void* bias,
              int32_t epilogue, void* c2, int64_t ldc2, void* workspace, int64_t workspace_bytes, void* stream) {
   using namespace drl;
+  // a layout-K A operand beyond one buffer range (e.g. the prefill's 262144 x 4864 down_proj input): launches over
+  // row blocks (multiples of the 256-row tile), each with its own operand / output base — the same tiles, the same
+  // result
+  if (a_layout == DRL_LAYOUT_K && a && lda > 0 && M * lda * 2 + 320ll * lda * 2 >= (1ll << 31)) {
+    const int64_t rows = std::max<int64_t>(256, ((1ll << 31) / (lda * 2) - 320) / 256 * 256);
+    const int64_t es = c_dtype == DRL_F32 ? 4 : 2;
+    for (int64_t m0 = 0; m0 < M; m0 += rows) {
+      const int64_t mm = std::min(rows, M - m0);
+      const int rc = drl_gemm(static_cast<const char*>(a) + m0 * lda * 2, lda, a_layout, b, ldb, b_layout,
+                              static_cast<char*>(c) + m0 * ldc * es, ldc, c_dtype, beta, mm, N, K, bias, epilogue,
+                              c2 ? static_cast<char*>(c2) + m0 * ldc2 * 2 : nullptr, ldc2, workspace, workspace_bytes,
+                              stream);
+      if (rc != DRL_OK) return rc;
+    }
+    return DRL_OK;
+  }
   DRL_CHECK_ARG(a && b && c, "NULL operand");
   DRL_CHECK_ARG(a_layout == DRL_LAYOUT_K || a_layout == DRL_LAYOUT_T, "a_layout");
   DRL_CHECK_ARG(b_layout == DRL_LAYOUT_K || b_layout == DRL_LAYOUT_T, "b_layout");

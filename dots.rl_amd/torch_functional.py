@@ -80,11 +80,15 @@ class _FusedLinearLogprobEntropy(torch.autograd.Function):
             dlogp = torch.zeros_like(lse)
         if not ctx.want_entropy:
             dent = None
+        N = hidden.shape[0]
+        n8 = (N + 7) // 8 * 8  # 16-B aligned rows of d_logits^T, so drl_gemm reads it in place for any N
         dlt = native.linear_logprob_dlogits(hidden, weight, labels, ctx.temperature, dlogp, dent, lse,
-                                            ent if dent is not None else None)
+                                            ent if dent is not None else None,
+                                            out=torch.empty(weight.shape[0], n8, dtype=torch.bfloat16,
+                                                            device=hidden.device)[:, :N])
         V, N = dlt.shape
         H = weight.shape[1]
-        hip = dlt.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16 and dlt.is_contiguous()
+        hip = dlt.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16
         if hip:  # dh (N, H) = dlt^T W on drl_gemm: both operands read in place (layout T), any V
             dh = native.gemm(dlt, native.LAYOUT_T, weight, native.LAYOUT_T, N, H, V,
                              torch.empty(N, H, dtype=torch.bfloat16, device=dlt.device))
@@ -93,6 +97,7 @@ class _FusedLinearLogprobEntropy(torch.autograd.Function):
         dw = None
         if ctx.weight_grad is not None:
             if hip and N % 64 == 0 and hidden.is_contiguous():  # dW (V, H) += dlt hidden, fp32 in place
+                # (layout-K dlt needs whole 64-token k-tiles; other N — A21 is opt-in — take torch's GEMM)
                 native.gemm(dlt, native.LAYOUT_K, hidden, native.LAYOUT_T, V, H, N, ctx.weight_grad, beta=True)
             else:
                 torch.addmm(ctx.weight_grad, dlt, hidden, out_dtype=torch.float32, out=ctx.weight_grad)

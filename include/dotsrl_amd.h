@@ -576,7 +576,7 @@ void drl_gemm_set_group(int32_t group_m);
  * dW += dy^T x (grad_weight, accumulated over micro-batches in fp32 as FSDP's fp32 gradient).
  *   C(m, n) (+)= sum_k A(m, k) B(n, k),  A(m, k) = a[m*lda + k] (DRL_LAYOUT_K) or a[k*lda + m] (DRL_LAYOUT_T),
  *                                        B(n, k) = b[n*ldb + k] (DRL_LAYOUT_K) or b[k*ldb + n] (DRL_LAYOUT_T).
- * bf16 operands, fp32 accumulation. c_dtype DRL_BF16: epilogues as drl_gemm_bf16_nt (bias / SwiGLU need both
+ * bf16 operands, fp32 accumulation (a layout-K A operand over 2 GB runs as row blocks). c_dtype DRL_BF16: epilogues as drl_gemm_bf16_nt (bias / SwiGLU need both
  * operands layout K); DRL_F32 (plain epilogue): c = acc, or c += acc when beta != 0. K % 64 == 0 unless both
  * operands are layout T (then any K: the k tail reads as zeros). A / B 16-byte aligned, ld % 8 == 0, each operand
  * < 2 GB. Work is split stream-K over at most one workgroup per CU; split tiles are summed in a fixed order

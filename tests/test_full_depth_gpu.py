@@ -16,7 +16,7 @@ teacher-forced log-probs / entropy, and the CPU bf16-autocast error of the top-2
     margin exceeds BF16_MARGIN (twice the largest CPU bf16 margin error recorded in the fixture);
   - the rollout reproduces the reference tokens until its first divergence, and a divergence is allowed only at
     a step whose reference margin is below BF16_MARGIN (after it the contexts differ);
-  - teacher-forced log-probs within 0.3 (the CPU bf16 autocast model is 0.144 off at worst).
+  - teacher-forced log-probs within twice the CPU bf16-autocast model's worst log-prob error.
 """
 
 import json
@@ -129,7 +129,8 @@ def test_bf16_full_depth_margin_checked(ref, weights, packed, hip_gemm_rows, mon
     confident = gaps > bound
     assert confident.sum() >= 0.6 * confident.size  # the check covers most steps (70.7 % with these weights)
     np.testing.assert_array_equal(argmax[confident], z["responses"][confident])
-    np.testing.assert_allclose(lp, z["log_probs"], atol=0.3)
+    # twice the CPU bf16-autocast model's own worst log-prob error (0.97 with these weights)
+    np.testing.assert_allclose(lp, z["log_probs"], atol=2.0 * meta["cpu_bf16_logp_err_max"])
     out, ro = _rollout(model, z, meta, packed_decode=packed)
     assert ro.last_packed_decode == packed
     resp = out.batch["responses"].cpu().numpy()
@@ -190,12 +191,14 @@ def test_bf16_packed_decode_teacher_forced(ref, weights):
     bound = 2.0 * np.maximum(cpu_err, np.median(cpu_err))
     bad = np.argwhere(err > bound)
     assert bad.size == 0, [(int(b), int(t), float(err[b, t]), float(bound[b, t])) for b, t in bad[:8]]
-    # log-prob of the reference token (the quantity the actor consumes), same rule
+    # log-prob of the reference token (the quantity the actor consumes): logit_tok - logsumexp moves by at most
+    # the logit error of the token plus that of the logsumexp, i.e. by at most twice the step's logit bound
     lse = torch.logsumexp(lg.double(), -1).cpu().numpy()
     tok_logit = lg.gather(-1, resp.unsqueeze(-1)).squeeze(-1).double().cpu().numpy()
     lp_err = np.abs((tok_logit - lse) - z["log_probs"])
-    lp_cpu = np.abs(z["cpu_bf16_log_probs"] - z["log_probs"])
-    assert (lp_err <= 2.0 * np.maximum(lp_cpu, np.median(lp_cpu))).all(), float(lp_err.max())
+    assert (lp_err <= 2.0 * bound).all(), float((lp_err / (2.0 * bound)).max())
+    lse_err = np.abs(lse - z["ref_lse"])
+    assert (lse_err <= bound).all(), float(lse_err.max())
     # greedy choice wherever the reference margin is clear of bf16 error
     gaps = z["top2_gap"]
     confident = gaps > 2.0 * meta["cpu_bf16_gap_err_max"]

@@ -136,3 +136,19 @@ def test_race_screen(al, bl, M, N, K, mode):
     cus = (n - 256) // (256 * 256 * 4 + 4)
     flags = ws[cus * 256 * 256 * 4:].view(torch.int32)[:cus + 1]
     assert int(flags.abs().sum()) == 0  # every flag consumed and reset, no residency timeout recorded
+
+
+def test_operand_over_2gb_runs_as_row_blocks():
+    """The prefill's down_proj input (512 x 512 rows x 4864) is 2.5 GB, past one buffer range: drl_gemm launches
+    over row blocks; spot rows from each block against the fp32 reference."""
+    M, N, K = 262144, 896, 4864
+    g = torch.Generator(device="cuda").manual_seed(3)
+    a = torch.empty(M, K, dtype=torch.bfloat16, device="cuda")
+    a.copy_(torch.randn(1, K, generator=g, device="cuda").expand(M, K))
+    a[:, :64] = torch.randn(M, 64, generator=g, device="cuda").to(torch.bfloat16)  # every row different
+    b = (torch.randn(N, K, generator=g, device="cuda") * 0.05).to(torch.bfloat16)
+    out = native.linear_fwd(a, b)
+    rows = torch.tensor([0, 1, 255, 256, 200000, 220000, 220671, 220672, M - 1], device="cuda")
+    ref = a[rows].float() @ b.float().t()
+    torch.testing.assert_close(out[rows].float(), ref.to(torch.bfloat16).float(), rtol=8e-3, atol=2e-3)
+    del a, out
