@@ -8,9 +8,10 @@ across the N ranks: "scaling" is strong. Random-init Qwen2.5-0.5B weights, synth
   python bench.py [--gpus N] [--steps K] [--warmup W]          (N>1 under torch.distributed.run)
 
 Besides the step rate the JSON line carries
-  roofline     : the dominant eagerly launched hand-written kernel (--roofline-kernel; default the ping-pong
-                 projection GEMM drl_gemm_bf16_nt, MFMA-bound — it absorbed the SwiGLU forward, the round-1
-                 choice; the fused attention forward is the other MFMA-bound kernel),
+  roofline     : the dominant eagerly launched hand-written kernel (--roofline-kernel; default drl_gemm, the
+                 stream-K ping-pong GEMM that runs every projection of the full-sequence passes — forward,
+                 dgrad and wgrad — and the lm_head; MFMA-bound; the fused attention forward is the other
+                 MFMA-bound kernel),
                  every launch inside the timed region bracketed by HIP events on its launch stream;
                  achieved = algorithmic work per launch (ROOFLINE below) / mean launch
                  duration, against its bound's peak (2.5 PFLOP/s dense bf16 MFMA or 8 TB/s HBM);
@@ -70,8 +71,16 @@ def _gemm_flops(a):
     return 2.0 * a[6] * a[7] * a[8]
 
 
+def _gemm_sk_flops(a):
+    # drl_gemm(a, lda, a_layout, b, ldb, b_layout, c, ldc, c_dtype, beta, M, N, K, bias, epilogue, ...): 2 M N K
+    return 2.0 * a[10] * a[11] * a[12]
+
+
 # symbol -> (work per launch from the call's arguments, per-unit statement, bound, peak, unit)
 ROOFLINE = {
+    "drl_gemm": (_gemm_sk_flops, "2*M*N*K FLOP per launch (bf16 operands, fp32 accumulation): every projection GEMM "
+                 "of the full-sequence passes — forward (bias / SwiGLU epilogues), dgrad, wgrad into the fp32 "
+                 "gradient, lm_head forward and backward", "mfma", PEAK_BF16_TFLOPS, "TFLOP/s"),
     "drl_gemm_bf16_nt": (_gemm_flops, "2*M*N*K FLOP per launch (bf16 operands, fp32 accumulation; qkv + bias, "
                          "o_proj, gate_up + fused SwiGLU of every full-sequence forward)", "mfma", PEAK_BF16_TFLOPS,
                          "TFLOP/s"),
@@ -208,7 +217,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--tiny", action="store_true", help="2-layer model, small batch (bring-up only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--roofline-kernel", default="drl_gemm_bf16_nt", choices=sorted(ROOFLINE))
+    ap.add_argument("--roofline-kernel", default="drl_gemm", choices=sorted(ROOFLINE))
     ap.add_argument("--override", nargs="*", default=[])
     ap.add_argument("--dapo", action="store_true",
                     help="BASELINE config #5 on one GPU: Qwen2.5-7B DAPO, n=8, 1024-token responses (RayDAPOTrainer)")

@@ -19,7 +19,7 @@ from . import native
 from .core_algos import cov_loss_kw, fused_actor_loss
 from .protocol import DataProto
 from .seqlen_balancing import prepare_dynamic_batch, restore_dynamic_batch
-from .qwen2 import Qwen2Model
+from .qwen2 import Qwen2Model, RmPad, gather_rows
 from .torch_functional import logprobs_and_entropy_from_logits
 
 
@@ -216,20 +216,39 @@ class DataParallelPPOActor:
         self.use_fused_kernels = config.get("use_fused_kernels", False)
 
     def _forward_micro_batch(self, micro_batch, temperature, calculate_entropy=False):
-        """dp_actor.py:90-280 (padded path): full-sequence forward, logits only at the R positions that
-        predict the response ([:, -R-1:-1]), then K2. Returns (entropy or None, log_probs), (bs, R) fp32."""
+        """dp_actor.py:90-280: full-sequence forward, logits only at the R positions that predict the response
+        ([:, -R-1:-1]), then K2. Returns (entropy or None, log_probs), (bs, R) fp32.
+
+        use_remove_padding (dp_actor.py:119-247): the backbone runs on the nnz attended tokens only (RmPad), the R
+        predicting rows are gathered from the packed hidden states and the outputs at pad positions are 0 (the
+        reference's pad_input). The reference takes the label of the last attended token from the next packed
+        sequence; that position is outside the response mask in both."""
         m = self.actor_module
         responses = micro_batch["responses"]
         B, R = responses.shape
-        h = m.hidden_states(micro_batch["input_ids"], micro_batch["attention_mask"], micro_batch["position_ids"])
-        h = h[:, -R - 1:-1, :].reshape(B * R, h.shape[-1])
+        am = micro_batch["attention_mask"]
+        keep = None
+        if self.use_remove_padding:
+            T = am.shape[1]
+            rm = RmPad(am)
+            h = m.hidden_states(micro_batch["input_ids"], am, micro_batch["position_ids"], rm=rm)
+            sel = rm.inv.view(B, T)[:, T - R - 1:T - 1].reshape(-1).contiguous()
+            h = gather_rows(h.view(rm.nnz, h.shape[-1]), sel)
+            keep = (sel >= 0).view(B, R)
+        else:
+            h = m.hidden_states(micro_batch["input_ids"], am, micro_batch["position_ids"])
+            h = h[:, -R - 1:-1, :].reshape(B * R, h.shape[-1])
         if self.use_fused_kernels:  # A21: no (B*R, V) logits (dp_actor.py:173-186 fused branch)
             logp, ent = m.fused_logprob(h, responses.reshape(-1), temperature, calculate_entropy)
-            return (ent.view(B, R) if ent is not None else None), logp.view(B, R)
-        logits = m.logits(h)
-        logp, ent = logprobs_and_entropy_from_logits(logits, responses.reshape(-1), temperature, calculate_entropy,
-                                                     inplace_backward=True)
-        return (ent.view(B, R) if ent is not None else None), logp.view(B, R)
+        else:
+            logits = m.logits(h)
+            logp, ent = logprobs_and_entropy_from_logits(logits, responses.reshape(-1), temperature,
+                                                         calculate_entropy, inplace_backward=True)
+        logp, ent = logp.view(B, R), (ent.view(B, R) if ent is not None else None)
+        if keep is not None:
+            logp = torch.where(keep, logp, 0.0)
+            ent = torch.where(keep, ent, 0.0) if ent is not None else None
+        return ent, logp
 
     @torch.no_grad()
     def compute_log_prob(self, data: DataProto, calculate_entropy=False):

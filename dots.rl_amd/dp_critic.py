@@ -19,7 +19,7 @@ from . import native
 from .dp_actor import FlatAdamW, append_to_dict
 from .protocol import DataProto
 from .seqlen_balancing import prepare_dynamic_batch, restore_dynamic_batch
-from .qwen2 import Qwen2Model
+from .qwen2 import Qwen2Model, RmPad, gather_rows
 
 
 class _ValueHead(torch.autograd.Function):
@@ -49,7 +49,7 @@ def value_head(m: Qwen2Model, h):
 
 
 class DataParallelPPOCritic:
-    """dp_critic.py:46-263 (padded path; use_remove_padding / ulysses SP are out of scope)."""
+    """dp_critic.py:46-263 (padded and use_remove_padding paths; ulysses SP is out of scope)."""
 
     def __init__(self, config, critic_module: Qwen2Model, critic_optimizer: FlatAdamW | None = None):
         self.config = config
@@ -58,11 +58,19 @@ class DataParallelPPOCritic:
         self.use_remove_padding = config.model.get("use_remove_padding", False) if "model" in config else False
 
     def _forward_micro_batch(self, micro_batch):
-        """dp_critic.py:57-145: values = score(h)[:, -R-1:-1] (compute dtype, (bs, R))."""
+        """dp_critic.py:57-145: values = score(h)[:, -R-1:-1] (compute dtype, (bs, R)); use_remove_padding
+        (dp_critic.py:69-107) runs the backbone on the attended tokens only and gives 0 at pad positions."""
         m = self.critic_module
         R = micro_batch["responses"].size(-1)
-        h = m.hidden_states(micro_batch["input_ids"], micro_batch["attention_mask"], micro_batch["position_ids"])
-        B = h.shape[0]
+        am = micro_batch["attention_mask"]
+        B, T = am.shape
+        if self.use_remove_padding:
+            rm = RmPad(am)
+            h = m.hidden_states(micro_batch["input_ids"], am, micro_batch["position_ids"], rm=rm)
+            sel = rm.inv.view(B, T)[:, T - R - 1:T - 1].reshape(-1).contiguous()
+            v = value_head(m, gather_rows(h.view(rm.nnz, h.shape[-1]), sel)).view(B, R)
+            return torch.where((sel >= 0).view(B, R), v, 0.0)
+        h = m.hidden_states(micro_batch["input_ids"], am, micro_batch["position_ids"])
         h = h[:, -R - 1:-1, :].reshape(B * R, h.shape[-1])
         return value_head(m, h).view(B, R)
 

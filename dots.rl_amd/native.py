@@ -717,6 +717,22 @@ def gemm_nt(x, w, bias=None, swiglu=False, out=None, out_gu=None):
     return out
 
 
+def copy_rows(src, dst, src_idx=None, dst_idx=None, n=None):
+    """dst[dst_idx[i]] = src[src_idx[i]] row by row (identity where an index is None; a negative index skips the row)
+    — the remove-padding gathers / scatters (csrc/rows.hip)."""
+    _dev(src, dst, src_idx, dst_idx)
+    assert src.dim() == 2 and dst.dim() == 2 and src.stride(1) == 1 and dst.stride(1) == 1
+    assert src.dtype == dst.dtype and src.shape[1] == dst.shape[1]
+    if n is None:
+        n = (src_idx if src_idx is not None else dst_idx if dst_idx is not None else src).shape[0]
+    for ix in (src_idx, dst_idx):
+        assert ix is None or (ix.dtype == torch.int64 and ix.is_contiguous() and ix.numel() >= n)
+    es = src.element_size()
+    check(lib().drl_copy_rows(_p(src), src.stride(0) * es, _p(src_idx), _p(dst), dst.stride(0) * es, _p(dst_idx), n,
+                              src.shape[1] * es, _stream()), "drl_copy_rows")
+    return dst
+
+
 LAYOUT_K, LAYOUT_T = 0, 1
 
 

@@ -384,11 +384,13 @@ def _hip_gemm(x, rows, K):
     return _sk(x) and rows >= HIP_GEMM_MIN_ROWS and K % 64 == 0
 
 
-def _layer_forward(m, i, x_prev, delta, pos, key_valid, save, cache=None, koff=0, koff_dev=None):
+def _layer_forward(m, i, x_prev, delta, pos, key_valid, save, cache=None, koff=0, koff_dev=None, rm=None):
     """x = x_prev (+ delta); returns (x2 = x + attn(x), mlp_out) — the next consumer adds them.
 
     ``save`` (dict or None) receives the activations the hand-written backward needs. ``koff_dev`` (device
-    int64 (1,)) is the cache position of a single decode token kept on the device (graph capture)."""
+    int64 (1,)) is the cache position of a single decode token kept on the device (graph capture). With ``rm``
+    (RmPad) x_prev / delta hold only the attended tokens (1, nnz, H): norms and GEMMs run on the nnz rows, q / k / v
+    are scattered into the padded (B, T) layout for RoPE + attention and the attention output is gathered back."""
     cfg, s, dt = m.cfg, m.store, m.dtype
     B, T, H = x_prev.shape
     Hq, Hkv, D = cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim
@@ -404,6 +406,9 @@ def _layer_forward(m, i, x_prev, delta, pos, key_valid, save, cache=None, koff=0
         qkv = native.linear_fwd(h1.view(B * T, H), s.w(p + "qkv_proj.weight"), bias=m.qkv_bias(i))
     else:
         qkv = torch.addmm(m.qkv_bias(i), h1.view(B * T, H), s.w(p + "qkv_proj.weight").t())
+    if rm is not None:
+        qkv = rm.unpack(qkv)
+        B, T = rm.B, rm.T
     qkv = qkv.view(B, T, -1)
     q = torch.empty(B, Hkv, G, T, D, dtype=dt, device=dev)
     # bf16 full-sequence passes run the fused MFMA attention (csrc/flash_attn.hip): log-probs and prefill
@@ -425,7 +430,7 @@ def _layer_forward(m, i, x_prev, delta, pos, key_valid, save, cache=None, koff=0
         del vt
         save.update(kt=kt, lse=lse, key_valid=key_valid)
         P = "flash"
-        return _layer_mlp(m, i, x, attn, save, kbuf, vbuf, P, q, h1, rstd1)
+        return _layer_mlp(m, i, x, _repack(rm, attn, save), save, kbuf, vbuf, P, q, h1, rstd1)
     vt = None
     if cache is None:
         kbuf = torch.empty(B, Hkv, T, D, dtype=dt, device=dev)
@@ -469,7 +474,17 @@ def _layer_forward(m, i, x_prev, delta, pos, key_valid, save, cache=None, koff=0
         attn = O.view(B, 1, Hq * D)
     else:
         attn = O.view(B, Hkv, G, T, D).permute(0, 3, 1, 2, 4).reshape(B, T, Hq * D)
-    return _layer_mlp(m, i, x, attn, save, kbuf, vbuf, P, q, h1, rstd1)
+    return _layer_mlp(m, i, x, _repack(rm, attn, save), save, kbuf, vbuf, P, q, h1, rstd1)
+
+
+def _repack(rm, attn, save):
+    """Padded attention output (B, T, Hq*D) -> the packed rows (1, nnz, Hq*D) under remove-padding (the padded
+    copy is kept for the fused attention backward)."""
+    if rm is None:
+        return attn
+    if save is not None:
+        save["attn_pad"] = attn
+    return rm.pack(attn.view(rm.B * rm.T, -1)).view(1, rm.nnz, -1)
 
 
 def _layer_mlp(m, i, x, attn, save, kbuf, vbuf, P, q, h1, rstd1):
@@ -505,10 +520,10 @@ def _layer_mlp(m, i, x, attn, save, kbuf, vbuf, P, q, h1, rstd1):
 
 class _DecoderLayer(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x_prev, delta, m, i, pos, key_valid):
+    def forward(ctx, x_prev, delta, m, i, pos, key_valid, rm=None):
         save = {}
-        x2, mlp = _layer_forward(m, i, x_prev, delta, pos, key_valid, save)
-        ctx.m, ctx.i, ctx.save, ctx.pos = m, i, save, pos
+        x2, mlp = _layer_forward(m, i, x_prev, delta, pos, key_valid, save, rm=rm)
+        ctx.m, ctx.i, ctx.save, ctx.pos, ctx.rm = m, i, save, pos, rm
         ctx.has_delta = delta is not None
         return x2, mlp
 
@@ -536,12 +551,18 @@ class _DecoderLayer(torch.autograd.Function):
         do = dx2.to(dt).view(N, H)
         dattn = dgrad(do, s.w(p + "o_proj"))
         acc_wgrad(s.g(p + "o_proj"), do, sv["attn"].reshape(N, Hq * D))
+        rm = ctx.rm
+        attn = sv["attn"]
+        if rm is not None:  # attention backward in the padded layout (zero gradient at the pad rows)
+            dattn = rm.unpack(dattn)
+            attn = sv["attn_pad"]
+            B, T = rm.B, rm.T
         if isinstance(sv["P"], str):  # "flash": fused forward, fused backward
             # fused attention backward (P recomputed from the saved LSE)
             dq = torch.empty_like(sv["q"])
             dk = torch.empty_like(sv["k"])
             dv = torch.empty_like(sv["v"])
-            native.flash_attn_bwd(sv["q"], sv["k"], sv["kt"], sv["v"], sv["attn"], dattn.view(B, T, Hq * D),
+            native.flash_attn_bwd(sv["q"], sv["k"], sv["kt"], sv["v"], attn, dattn.view(B, T, Hq * D),
                                   sv["lse"], sv["key_valid"], dq, dk, dv)
         else:
             dO = dattn.view(B, T, Hkv, G, D).permute(0, 2, 3, 1, 4).reshape(B * Hkv, G * T, D)
@@ -558,7 +579,7 @@ class _DecoderLayer(torch.autograd.Function):
             dk = torch.bmm(dS.transpose(1, 2), q3)
         dqkv = torch.empty(B, T, (Hq + 2 * Hkv) * D, dtype=dt, device=dx2.device)
         native.rope_qkv_bwd(dq, dk, dv, ctx.pos, m.cos, m.sin, Hq, Hkv, D, dqkv)
-        dqkv2 = dqkv.view(N, -1)
+        dqkv2 = dqkv.view(B * T, -1) if rm is None else rm.pack(dqkv.view(B * T, -1))
         dh1 = dgrad(dqkv2, s.w(p + "qkv_proj.weight"))
         acc_wgrad(s.g(p + "qkv_proj.weight"), dqkv2, sv["h1"].view(N, H))
         if m.cfg.attention_bias:
@@ -571,7 +592,7 @@ class _DecoderLayer(torch.autograd.Function):
         ctx.save = None
         if m.grad_ready_hook is not None:  # layer i's gradient is complete for this micro-batch
             m.grad_ready_hook(i)
-        return dx, (dx.to(g_mlp.dtype) if ctx.has_delta else None), None, None, None, None
+        return dx, (dx.to(g_mlp.dtype) if ctx.has_delta else None), None, None, None, None, None
 
 
 class _FinalNorm(torch.autograd.Function):
@@ -593,6 +614,56 @@ class _FinalNorm(torch.autograd.Function):
         dx = torch.zeros_like(x)
         native.rmsnorm_bwd(x, m.store.w("norm"), rstd, dh.contiguous(), dx, m.store.g("norm"))
         return dx, dx.to(ctx.delta_dtype), None
+
+
+class RmPad:
+    """Remove-padding index maps of one (B, T) micro-batch — the reference's unpad_input / pad_input
+    (flash_attn.bert_padding, dp_actor.py:119-247, dp_critic.py:69-107 under use_remove_padding=True): ``idx``
+    (nnz,) the flat positions b*T+t of the attended tokens in order, ``inv`` (B*T,) the packed row of each padded
+    position (-1 at pads). Building it reads nnz back to the host once (the packed tensors' size)."""
+
+    def __init__(self, attention_mask):
+        B, T = attention_mask.shape
+        dev = attention_mask.device
+        self.B, self.T = B, T
+        self.idx = torch.nonzero(attention_mask.reshape(-1)).reshape(-1).contiguous()
+        self.nnz = int(self.idx.numel())
+        self.inv = torch.full((B * T,), -1, dtype=torch.int64, device=dev)
+        self.inv[self.idx] = torch.arange(self.nnz, dtype=torch.int64, device=dev)
+
+    def pack(self, x):
+        """(B*T, C) padded rows -> (nnz, C) (index_first_axis)."""
+        out = torch.empty(self.nnz, x.shape[1], dtype=x.dtype, device=x.device)
+        return native.copy_rows(x, out, src_idx=self.idx)
+
+    def unpack(self, x):
+        """(nnz, C) packed rows -> (B*T, C) with zero rows at the pads (pad_input)."""
+        out = torch.zeros(self.B * self.T, x.shape[1], dtype=x.dtype, device=x.device)
+        return native.copy_rows(x, out, dst_idx=self.idx)
+
+    def tokens(self, t):
+        """(B, T) per-token tensor (ids, positions) -> (1, nnz)."""
+        return t.reshape(-1).index_select(0, self.idx).view(1, -1)
+
+
+class _GatherRows(torch.autograd.Function):
+    """out[j] = x[idx[j]] for x (n, C) and idx (m,) with -1 -> a zero row; every source row is selected at most once,
+    so the backward is the inverse scatter (no accumulation)."""
+
+    @staticmethod
+    def forward(ctx, x, idx):
+        ctx.idx, ctx.n = idx, x.shape[0]
+        out = torch.zeros(idx.shape[0], x.shape[1], dtype=x.dtype, device=x.device)
+        return native.copy_rows(x, out, src_idx=idx)
+
+    @staticmethod
+    def backward(ctx, dy):
+        dx = torch.zeros(ctx.n, dy.shape[1], dtype=dy.dtype, device=dy.device)
+        return native.copy_rows(dy.contiguous(), dx, dst_idx=ctx.idx), None
+
+
+def gather_rows(x, idx):
+    return _GatherRows.apply(x, idx)
 
 
 def _key_valid(attention_mask):
@@ -681,22 +752,25 @@ class Qwen2Model:
         return fused_linear_logprob_entropy(h, self.store.w(name), labels, temperature, calculate_entropy,
                                             weight_grad=gw)
 
-    def hidden_states(self, input_ids, attention_mask, position_ids):
-        """Full-sequence forward -> final-norm hidden states (B, T, H) in the compute dtype."""
+    def hidden_states(self, input_ids, attention_mask, position_ids, rm=None):
+        """Full-sequence forward -> final-norm hidden states (B, T, H) in the compute dtype; with ``rm`` (RmPad of
+        attention_mask) only the attended tokens run through the norms / GEMMs / MLP and the result is the packed
+        (1, nnz, H) (the reference's use_remove_padding forward)."""
         cfg = self.cfg
         key_valid = _key_valid(attention_mask)
         pos = position_ids.contiguous()
+        ids = input_ids if rm is None else rm.tokens(input_ids)
         if self.training and self.store.trainable:
-            x = _Embedding.apply(input_ids, self.store.w("embed_tokens"), self.store.g("embed_tokens"), self._dummy)
+            x = _Embedding.apply(ids, self.store.w("embed_tokens"), self.store.g("embed_tokens"), self._dummy)
             delta = None
             for i in range(cfg.num_hidden_layers):
-                x, delta = _DecoderLayer.apply(x, delta, self, i, pos, key_valid)
+                x, delta = _DecoderLayer.apply(x, delta, self, i, pos, key_valid, rm)
             return _FinalNorm.apply(x, delta, self)
         with torch.no_grad():
-            x = F.embedding(input_ids, self.store.w("embed_tokens")).to(torch.float32)
+            x = F.embedding(ids, self.store.w("embed_tokens")).to(torch.float32)
             delta = None
             for i in range(cfg.num_hidden_layers):
-                x, delta = _layer_forward(self, i, x, delta, pos, key_valid, None)
+                x, delta = _layer_forward(self, i, x, delta, pos, key_valid, None, rm=rm)
             return self._final_norm(x, delta)
 
     def _final_norm(self, x, delta):

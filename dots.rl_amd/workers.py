@@ -123,6 +123,8 @@ class ActorRolloutRefWorker(Worker):
         fused = bool(cfg.model.get("use_fused_kernels", False)) and dtype == torch.bfloat16
         cfg.actor.use_fused_kernels = fused
         cfg.ref.use_fused_kernels = fused
+        # model.use_remove_padding likewise (fsdp_workers.py sets actor / ref use_remove_padding from the model)
+        cfg.actor.use_remove_padding = cfg.ref.use_remove_padding = bool(cfg.model.get("use_remove_padding", False))
         if self._is_actor:
             o = cfg.actor.optim
             betas = tuple(o.get("betas", (0.9, 0.999)))

@@ -593,6 +593,13 @@ int64_t drl_gemm_workspace_bytes(void);
 void drl_gemm_set_sk_tuning(int32_t grid, int32_t group, int32_t dp_mode, int32_t min_iters);
 
 
+/* Row gather / scatter of the remove-padding passes (flash_attn.bert_padding unpad_input / pad_input /
+ * index_first_axis under dp_actor.py:119-247, dp_critic.py:69-107 with use_remove_padding=True): for i < n_rows,
+ * row src_idx[i] (or i when NULL) of src -> row dst_idx[i] (or i) of dst, row_bytes each (a multiple of 16, rows
+ * 16-byte aligned); a negative index skips the row. */
+int drl_copy_rows(const void* src, int64_t ld_src_bytes, const int64_t* src_idx, void* dst, int64_t ld_dst_bytes,
+                  const int64_t* dst_idx, int64_t n_rows, int64_t row_bytes, void* stream);
+
 /* 16-bit transpose: dst (cols, rows) = src (rows, cols)^T (row strides in elements). The weights' transposed
  * copies for the backward dgrad (dx = dy W run as the TN product dy (W^T)^T: gate_up 129 -> 105 us, down 57 -> 47 us
  * at 6144 rows on hipBLASLt), refreshed after each optimizer step. */
