@@ -737,14 +737,15 @@ LAYOUT_K, LAYOUT_T = 0, 1
 
 
 class _GemmWorkspace:
-    """drl_gemm's stream-K slabs + flag words, one per device, zeroed once at allocation (every call leaves the
-    flag words zero again); calls share it in stream order on the current stream."""
+    """drl_gemm's stream-K slabs + flag words, one per (device, slot), zeroed once at allocation (every call leaves
+    the flag words zero again); calls of one slot share it in stream order. Slot 1 belongs to the side stream of
+    qwen2.dgrad_wgrad (a weight gradient running concurrently with its input gradient)."""
 
     def __init__(self):
         self.buf = {}
 
-    def get(self, device):
-        key = device.index if device.index is not None else torch.cuda.current_device()
+    def get(self, device, slot=0):
+        key = (device.index if device.index is not None else torch.cuda.current_device(), slot)
         b = self.buf.get(key)
         if b is None:
             n = lib().drl_gemm_workspace_bytes()
@@ -758,7 +759,7 @@ class _GemmWorkspace:
 _ws_gemm = _GemmWorkspace()
 
 
-def gemm(a, a_layout, b, b_layout, M, N, K, out, beta=False, bias=None, swiglu=False, out_gu=None):
+def gemm(a, a_layout, b, b_layout, M, N, K, out, beta=False, bias=None, swiglu=False, out_gu=None, ws_slot=0):
     """drl_gemm (csrc/gemm_sk.hip): out (M, N) (+)= sum_k A(m, k) B(n, k) with A(m, k) = a[m, k] (LAYOUT_K) or
     a[k, m] (LAYOUT_T), B likewise; bf16 operands, fp32 accumulation; ``out`` bf16 (+ bias / SwiGLU epilogues) or
     fp32 (``beta``: accumulate into it)."""
@@ -775,7 +776,7 @@ def gemm(a, a_layout, b, b_layout, M, N, K, out, beta=False, bias=None, swiglu=F
     if bias is not None:
         assert bias.is_contiguous() and bias.numel() == N
     epi = GEMM_SWIGLU if swiglu else (GEMM_BIAS if bias is not None else GEMM_PLAIN)
-    ws = _ws_gemm.get(out.device)
+    ws = _ws_gemm.get(out.device, ws_slot)
     check(lib().drl_gemm(_p(a), a.stride(0), a_layout, _p(b), b.stride(0), b_layout, _p(out), out.stride(0), c_dt,
                          1 if beta else 0, M, N, K, _p(bias), epi, _p(out_gu),
                          out_gu.stride(0) if out_gu is not None else 0, _p(ws), ws.numel(), _stream()), "drl_gemm")
@@ -800,12 +801,12 @@ def linear_dgrad(dy, w, out=None):
     return gemm(dy, LAYOUT_K, w, LAYOUT_T, M, N, K, out)
 
 
-def linear_wgrad(gw, dy, x, accumulate=True):
+def linear_wgrad(gw, dy, x, accumulate=True, ws_slot=0):
     """gw (N_out, N_in) fp32 (+)= dy^T x (F.linear's grad_weight, accumulated in fp32): dy (T, N_out), x (T, N_in)."""
     T, M = dy.shape
     N = x.shape[1]
     assert x.shape[0] == T and gw.shape == (M, N) and gw.dtype == torch.float32
-    return gemm(dy, LAYOUT_T, x, LAYOUT_T, M, N, T, gw, beta=accumulate)
+    return gemm(dy, LAYOUT_T, x, LAYOUT_T, M, N, T, gw, beta=accumulate, ws_slot=ws_slot)
 
 
 LINEAR_NONE, LINEAR_BIAS, LINEAR_SWIGLU = 0, 1, 2

@@ -333,6 +333,38 @@ def acc_wgrad(gw, dy, x):
         torch.addmm(gw, dy.t(), x, out_dtype=torch.float32, out=gw)
 
 
+# The weight gradient of a projection runs on a side stream while its input gradient runs on the current one: the
+# pair's workgroups share the CUs (at 6144 rows: qkv 160 + 96, gate_up 152 + 96 of 256) where each alone leaves most
+# of them idle. DRL_CONCURRENT_WGRAD=0 serialises them (A/B measurements).
+CONCURRENT_WGRAD = os.environ.get("DRL_CONCURRENT_WGRAD", "1") != "0"
+_SIDE_STREAMS = {}
+
+
+def _side_stream(dev):
+    s = _SIDE_STREAMS.get(dev.index)
+    if s is None:
+        s = _SIDE_STREAMS[dev.index] = torch.cuda.Stream(device=dev)
+    return s
+
+
+def dgrad_wgrad(dy, w, gw, x):
+    """dx = dy W and gw (fp32) += dy^T x for one projection (dy (N, out), w (out, in), x (N, in)); returns dx. On
+    drl_gemm the weight gradient is launched first on the side stream (its own workspace slot) and joined before
+    returning, so callers see plain stream order."""
+    if not (CONCURRENT_WGRAD and _sk(dy, w, x) and dy.shape[1] % 64 == 0):
+        dx = dgrad(dy, w)
+        acc_wgrad(gw, dy, x)
+        return dx
+    main = torch.cuda.current_stream()
+    side = _side_stream(dy.device)
+    side.wait_stream(main)
+    with torch.cuda.stream(side):
+        native.linear_wgrad(gw, dy, x, ws_slot=1)
+    dx = native.linear_dgrad(dy, w)
+    main.wait_stream(side)
+    return dx
+
+
 def bmm_f32(a, b):
     """Batched a @ b (bf16 or fp32 inputs) with an fp32 result (hipBLASLt)."""
     if a.dtype == torch.float32:
@@ -539,18 +571,15 @@ class _DecoderLayer(torch.autograd.Function):
         dx2 = g_x2.to(torch.float32).contiguous().clone()
         dm = g_mlp.to(dt).contiguous().view(N, H)
         # MLP
-        da = dgrad(dm, s.w(p + "down_proj"))
-        acc_wgrad(s.g(p + "down_proj"), dm, sv["a"])
+        da = dgrad_wgrad(dm, s.w(p + "down_proj"), s.g(p + "down_proj"), sv["a"])
         dgu = torch.empty_like(sv["gu"])
         native.swiglu_bwd(sv["gu"], da, dgu)
-        dh2 = dgrad(dgu, s.w(p + "gate_up_proj"))
-        acc_wgrad(s.g(p + "gate_up_proj"), dgu, sv["h2"].view(N, H))
+        dh2 = dgrad_wgrad(dgu, s.w(p + "gate_up_proj"), s.g(p + "gate_up_proj"), sv["h2"].view(N, H))
         native.rmsnorm_bwd(sv["x2"], s.w(p + "post_attention_layernorm"), sv["rstd2"], dh2, dx2,
                            s.g(p + "post_attention_layernorm"))
         # attention output projection
         do = dx2.to(dt).view(N, H)
-        dattn = dgrad(do, s.w(p + "o_proj"))
-        acc_wgrad(s.g(p + "o_proj"), do, sv["attn"].reshape(N, Hq * D))
+        dattn = dgrad_wgrad(do, s.w(p + "o_proj"), s.g(p + "o_proj"), sv["attn"].reshape(N, Hq * D))
         rm = ctx.rm
         attn = sv["attn"]
         if rm is not None:  # attention backward in the padded layout (zero gradient at the pad rows)
@@ -580,8 +609,7 @@ class _DecoderLayer(torch.autograd.Function):
         dqkv = torch.empty(B, T, (Hq + 2 * Hkv) * D, dtype=dt, device=dx2.device)
         native.rope_qkv_bwd(dq, dk, dv, ctx.pos, m.cos, m.sin, Hq, Hkv, D, dqkv)
         dqkv2 = dqkv.view(B * T, -1) if rm is None else rm.pack(dqkv.view(B * T, -1))
-        dh1 = dgrad(dqkv2, s.w(p + "qkv_proj.weight"))
-        acc_wgrad(s.g(p + "qkv_proj.weight"), dqkv2, sv["h1"].view(N, H))
+        dh1 = dgrad_wgrad(dqkv2, s.w(p + "qkv_proj.weight"), s.g(p + "qkv_proj.weight"), sv["h1"].view(N, H))
         if m.cfg.attention_bias:
             if dqkv2.dtype == torch.bfloat16:
                 native.colsum_bf16_acc(dqkv2, s.g(p + "qkv_proj.bias"))
