@@ -71,6 +71,11 @@ DEFAULTS = dict(
             clip_ratio_high=0.2, clip_ratio_c=3.0, policy_loss=dict(loss_mode="vanilla"), loss_agg_mode="token-mean",
             entropy_coeff=0.0, use_kl_loss=True, kl_loss_coef=0.001, kl_loss_type="low_var_kl", ppo_epochs=1,
             shuffle=False, grad_clip=1.0, ulysses_sequence_parallel_size=1,
+            # micro-batches run through the model together (one forward / backward over their concatenated rows; the
+            # loss, its scale and the metrics stay per micro-batch): 0 = as many as fit exec_activation_gb of saved
+            # activations, 1 = the reference's one micro-batch per pass (dp_actor.DataParallelPPOActor.update_policy)
+            exec_micro_batches=0, exec_activation_gb=40,
+            exec_log_prob_tokens=65536,  # forward-only log-prob passes: micro-batches per pass up to this many tokens
             # shard: fp32 master + AdamW moments split over the DP ranks (ZeRO-style; FSDP FULL_SHARD in the
             # reference); "auto" = when replicated state would exceed 64 GB per GPU (workers._shard_spec)
             fsdp_config=dict(shard="auto", fsdp_size=-1, param_offload=False, optimizer_offload=False),
@@ -89,7 +94,7 @@ DEFAULTS = dict(
             fused_select=False,  # lm_head fused with K4 (csrc/fused_linear.hip)
         ),
         ref=dict(log_prob_micro_batch_size=None, log_prob_micro_batch_size_per_gpu=16, log_prob_use_dynamic_bsz=False,
-                 log_prob_max_token_len_per_gpu=16384),
+                 log_prob_max_token_len_per_gpu=16384, exec_log_prob_tokens=65536),
     ),
     # critic.yaml + dp_critic.yaml (used when algorithm.adv_estimator == "gae" or critic.enable)
     critic=dict(

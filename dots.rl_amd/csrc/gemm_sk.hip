@@ -681,6 +681,25 @@ int drl_gemm(const void* a, int64_t lda, int32_t a_layout, const void* b, int64_
     }
     return DRL_OK;
   }
+  // a layout-T operand beyond one buffer range has K along its rows (the weight gradient over a long token batch, e.g.
+  // the lm_head's d_logits^T at 8192 rows x 151936): K blocks of whole 128-deep k-pairs accumulated into the fp32
+  // output (the first block with the caller's beta, the rest with beta = 1)
+  const auto t_bytes = [&](int32_t layout, int64_t ld) { return layout == DRL_LAYOUT_T ? K * ld * 2 + 320ll * ld * 2 : 0; };
+  if (a && b && lda > 0 && ldb > 0 && (t_bytes(a_layout, lda) >= (1ll << 31) || t_bytes(b_layout, ldb) >= (1ll << 31))) {
+    DRL_CHECK_ARG(c_dtype == DRL_F32 && epilogue == DRL_GEMM_PLAIN,
+                  "a layout-T operand over 2 GB needs the fp32 accumulating output (K split)");
+    const int64_t ld = std::max(a_layout == DRL_LAYOUT_T ? lda : 0, b_layout == DRL_LAYOUT_T ? ldb : 0);
+    const int64_t kb = std::max<int64_t>(128, ((1ll << 31) / (ld * 2) - 320) / 128 * 128);
+    for (int64_t k0 = 0; k0 < K; k0 += kb) {
+      const int64_t kk = std::min(kb, K - k0);
+      const char* ak = static_cast<const char*>(a) + (a_layout == DRL_LAYOUT_T ? k0 * lda : k0) * 2;
+      const char* bk = static_cast<const char*>(b) + (b_layout == DRL_LAYOUT_T ? k0 * ldb : k0) * 2;
+      const int rc = drl_gemm(ak, lda, a_layout, bk, ldb, b_layout, c, ldc, c_dtype, k0 == 0 ? beta : 1, M, N, kk,
+                              bias, epilogue, c2, ldc2, workspace, workspace_bytes, stream);
+      if (rc != DRL_OK) return rc;
+    }
+    return DRL_OK;
+  }
   DRL_CHECK_ARG(a && b && c, "NULL operand");
   DRL_CHECK_ARG(a_layout == DRL_LAYOUT_K || a_layout == DRL_LAYOUT_T, "a_layout");
   DRL_CHECK_ARG(b_layout == DRL_LAYOUT_K || b_layout == DRL_LAYOUT_T, "b_layout");

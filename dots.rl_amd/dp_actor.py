@@ -205,6 +205,14 @@ class FlatAdamW:
         self.sched_step = int(sd.get("sched_step", 0))
 
 
+def _concat_rows(group):
+    """The forward inputs of consecutive micro-batches as one batch of rows (all share the padded width T)."""
+    if len(group) == 1:
+        return group[0].batch
+    return {k: torch.cat([mb.batch[k] for mb in group], 0)
+            for k in ("input_ids", "attention_mask", "position_ids", "responses")}
+
+
 class DataParallelPPOActor:
     """dp_actor.py:53-482. ``actor_optimizer`` None -> reference policy."""
 
@@ -250,6 +258,43 @@ class DataParallelPPOActor:
             ent = torch.where(keep, ent, 0.0) if ent is not None else None
         return ent, logp
 
+    def _exec_groups(self, micro_batches):
+        """Micro-batches that run through the model in one pass. The reference runs one per forward / backward
+        (dp_actor.py:392-466); their gradients only add up (each micro-batch's loss carries its own scale factor and
+        token count), so consecutive micro-batches may share one pass over their concatenated rows: the GEMMs see
+        2-4x the rows (at 6144 rows the N = 896 projections fill 96 of 256 CUs). ``exec_micro_batches`` fixes the
+        group size; 0 groups as many as keep the saved activations under ``exec_activation_gb``."""
+        cfg = self.config
+        n = int(cfg.get("exec_micro_batches", 1) or 0)
+        if n <= 0:
+            mc = self.actor_module.cfg
+            H, I, L = mc.hidden_size, mc.intermediate_size, mc.num_hidden_layers
+            nq = (mc.num_attention_heads + 2 * mc.num_key_value_heads) * mc.head_dim
+            # saved per token and layer: x, x2 (fp32), h1, h2, attn (bf16), q / k / v / k^T, gate|up and SwiGLU out
+            per_tok = L * (8 * H + 6 * H + 4 * nq + 6 * I)
+            budget = float(cfg.get("exec_activation_gb", 40)) * 2 ** 30
+            toks = max(mb.batch["input_ids"].numel() for mb in micro_batches)
+            n = max(1, int(budget // max(1, per_tok * toks)))
+        return [micro_batches[i:i + n] for i in range(0, len(micro_batches), n)]
+
+    def _log_prob_groups(self, micro_batches):
+        """Forward-only passes: rows are independent, so consecutive micro-batches run as one pass of at most
+        ``exec_log_prob_tokens`` tokens (0: one micro-batch per pass, as the reference) — bigger GEMMs, same rows."""
+        budget = int(self.config.get("exec_log_prob_tokens", 0) or 0)
+        if budget <= 0:
+            return [[mb] for mb in micro_batches]
+        groups, cur, toks = [], [], 0
+        for mb in micro_batches:
+            t = mb.batch["input_ids"].numel()
+            if cur and toks + t > budget:
+                groups.append(cur)
+                cur, toks = [], 0
+            cur.append(mb)
+            toks += t
+        if cur:
+            groups.append(cur)
+        return groups
+
     @torch.no_grad()
     def compute_log_prob(self, data: DataProto, calculate_entropy=False):
         """dp_actor.py:300-359."""
@@ -263,8 +308,8 @@ class DataParallelPPOActor:
         else:
             micro_batches = data.split(micro_batch_size)
         lps, ents = [], []
-        for mb in micro_batches:
-            ent, lp = self._forward_micro_batch(mb.batch, temperature, calculate_entropy)
+        for group in self._log_prob_groups(micro_batches):
+            ent, lp = self._forward_micro_batch(_concat_rows(group), temperature, calculate_entropy)
             lps.append(lp)
             if calculate_entropy:
                 ents.append(ent)
@@ -313,30 +358,41 @@ class DataParallelPPOActor:
                     else:
                         rm = mini_batch.batch["response_mask"]
                         counts = rm.reshape(len(micro_batches), -1).sum(-1, dtype=torch.float64)
-                for k, micro_batch in enumerate(micro_batches):
-                    if k == len(micro_batches) - 1:  # gradients final after this backward: overlap the all-reduce
+                groups = self._exec_groups(micro_batches)
+                k = 0
+                for gi, group in enumerate(groups):
+                    if gi == len(groups) - 1:  # gradients final after this backward: overlap the all-reduce
                         self.actor_optimizer.begin_overlap(m)
-                    mb = micro_batch.batch
-                    if cfg.get("use_dynamic_bsz", False):  # relative to the dynamic bsz (dp_actor.py:413-414)
-                        lsf = mb["response_mask"].shape[0] / cfg.ppo_mini_batch_size
-                    else:
-                        lsf = 1.0 / grad_accum
                     calculate_entropy = cfg.entropy_coeff != 0
-                    entropy, log_prob = self._forward_micro_batch(mb, temperature, calculate_entropy)
-                    out = fused_actor_loss(
-                        log_prob, entropy, mb["old_log_probs"], mb["advantages"], mb["response_mask"],
-                        mb.get("ref_log_prob"), clip_ratio_low=lo, clip_ratio_high=hi,
-                        clip_ratio_c=cfg.get("clip_ratio_c", 3.0), entropy_coeff=cfg.entropy_coeff,
-                        use_kl_loss=cfg.use_kl_loss, kl_loss_type=cfg.kl_loss_type, kl_loss_coef=cfg.kl_loss_coef,
-                        loss_agg_mode=cfg.loss_agg_mode, loss_scale_factor=lsf, policy_loss=loss_mode,
-                        token_count=counts[k:k + 1] if counts is not None else None,
-                        cov_kw=(cov_loss_kw(cfg.policy_loss, loss_mode,
-                                            seed_key=(cfg.policy_loss.get("seed", 1234),
-                                                      self.actor_optimizer.step_count, k))
-                                if loss_mode in ("clip_cov", "kl_cov") else None))
-                    out[6].backward()
-                    mb_out.append(out.detach())
-                    mb_lsf.append(lsf)
+                    entropy_all, log_prob_all = self._forward_micro_batch(_concat_rows(group), temperature,
+                                                                          calculate_entropy)
+                    total, r0 = None, 0
+                    for micro_batch in group:
+                        mb = micro_batch.batch
+                        n = mb["responses"].shape[0]
+                        if cfg.get("use_dynamic_bsz", False):  # relative to the dynamic bsz (dp_actor.py:413-414)
+                            lsf = mb["response_mask"].shape[0] / cfg.ppo_mini_batch_size
+                        else:
+                            lsf = 1.0 / grad_accum
+                        log_prob = log_prob_all[r0:r0 + n] if len(group) > 1 else log_prob_all
+                        entropy = entropy_all[r0:r0 + n] if (entropy_all is not None and len(group) > 1) else entropy_all
+                        r0 += n
+                        out = fused_actor_loss(
+                            log_prob, entropy, mb["old_log_probs"], mb["advantages"], mb["response_mask"],
+                            mb.get("ref_log_prob"), clip_ratio_low=lo, clip_ratio_high=hi,
+                            clip_ratio_c=cfg.get("clip_ratio_c", 3.0), entropy_coeff=cfg.entropy_coeff,
+                            use_kl_loss=cfg.use_kl_loss, kl_loss_type=cfg.kl_loss_type, kl_loss_coef=cfg.kl_loss_coef,
+                            loss_agg_mode=cfg.loss_agg_mode, loss_scale_factor=lsf, policy_loss=loss_mode,
+                            token_count=counts[k:k + 1] if counts is not None else None,
+                            cov_kw=(cov_loss_kw(cfg.policy_loss, loss_mode,
+                                                seed_key=(cfg.policy_loss.get("seed", 1234),
+                                                          self.actor_optimizer.step_count, k))
+                                    if loss_mode in ("clip_cov", "kl_cov") else None))
+                        total = out[6] if total is None else total + out[6]
+                        mb_out.append(out.detach())
+                        mb_lsf.append(lsf)
+                        k += 1
+                    total.backward()
                 self.actor_optimizer.end_overlap(m)
                 grad_norms.append(self.actor_optimizer.step().clone())
         self.actor_optimizer.zero_grad()

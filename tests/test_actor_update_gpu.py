@@ -120,8 +120,11 @@ def _metric_lists_close(got, want):
             np.testing.assert_allclose(g, r, rtol=1e-4, atol=1e-4, err_msg=k)
 
 
+@pytest.mark.parametrize("exec_mb", [1, 0])
 @pytest.mark.parametrize("ci", [0, 1])
-def test_update_policy_matches_reference(ci):
+def test_update_policy_matches_reference(ci, exec_mb):
+    """exec_mb = 1: one micro-batch per forward / backward as the reference; 0 (auto): both micro-batches of a
+    mini-batch in one pass with their losses kept per micro-batch — the same fixture, the same tolerances."""
     from dots.rl_amd.config import to_attr
     from dots.rl_amd.dp_actor import DataParallelPPOActor, FlatAdamW
     from dots.rl_amd.protocol import DataProto
@@ -131,7 +134,7 @@ def test_update_policy_matches_reference(ci):
     c = lambda k: T(z[f"c{ci}_{k}"])  # noqa: E731
     cfg, store, model = _tiny()
     before = store.master.detach().cpu().clone()
-    acfg = to_attr(case["config"])
+    acfg = to_attr(dict(case["config"], exec_micro_batches=exec_mb))
     opt = FlatAdamW(store, lr=case["lr"], betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01,
                     max_grad_norm=acfg.grad_clip)
     actor = DataParallelPPOActor(acfg, model, opt)

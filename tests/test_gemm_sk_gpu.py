@@ -154,6 +154,22 @@ def test_operand_over_2gb_runs_as_row_blocks():
     del a, out
 
 
+def test_wgrad_operand_over_2gb_splits_k():
+    """The fused-micro-batch lm_head weight gradient: d_logits (8448 tokens x 131072 vocab, bf16, 2.2 GB) read as a
+    layout-T operand past one buffer range: drl_gemm accumulates K blocks into the fp32 gradient. Spot rows of the
+    result against fp32 torch, starting from a non-zero gradient (beta = 1)."""
+    T_, V, H = 8448, 131072, 64
+    g = torch.Generator(device="cuda").manual_seed(5)
+    dy = torch.randn(T_, V, generator=g, device="cuda").to(torch.bfloat16)
+    x = torch.randn(T_, H, generator=g, device="cuda").to(torch.bfloat16)
+    gw = torch.ones(V, H, device="cuda")
+    native.linear_wgrad(gw, dy, x)
+    rows = torch.tensor([0, 1, 77, 65535, 65536, V - 1], device="cuda")
+    ref = 1.0 + dy[:, rows].float().t() @ x.float()
+    torch.testing.assert_close(gw[rows], ref, rtol=1e-4, atol=1e-3)
+    del dy, gw
+
+
 @pytest.mark.parametrize("M,N_out,N_in", [(6144, 1152, 896), (6144, 9728, 896), (6144, 896, 4864), (777, 896, 896)])
 def test_concurrent_dgrad_wgrad_matches_serial(M, N_out, N_in):
     """qwen2.dgrad_wgrad: the weight gradient on the side stream (workspace slot 1) while the input gradient runs on

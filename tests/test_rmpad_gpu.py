@@ -81,7 +81,7 @@ def test_update_policy_rmpad_matches_reference(ci):
     c = lambda k: T(z[f"c{ci}_{k}"])  # noqa: E731
     cfg, store, model = _tiny()
     before = store.master.detach().cpu().clone()
-    acfg = to_attr(dict(case["config"], use_remove_padding=True))
+    acfg = to_attr(dict(case["config"], use_remove_padding=True, exec_micro_batches=0))
     opt = FlatAdamW(store, lr=case["lr"], betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01,
                     max_grad_norm=acfg.grad_clip)
     actor = DataParallelPPOActor(acfg, model, opt)

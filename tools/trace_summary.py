@@ -21,7 +21,7 @@ def main():
         durs[(name, key)] += d
     for name, t in tot.most_common(top):
         print(f"{t / 1e6:9.1f} ms  {name[:110]}")
-        for key, n in shapes[name].most_common(6):
+        for key, n in shapes[name].most_common(int(sys.argv[3]) if len(sys.argv) > 3 else 6):
             print(f"      grid={key[0]}x{key[1]} wg={key[2]}  calls={n}  mean={durs[(name, key)] / n / 1e3:.1f} us")
 
 
