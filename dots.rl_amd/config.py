@@ -109,6 +109,7 @@ DEFAULTS = dict(
         forward_micro_batch_size=None, forward_micro_batch_size_per_gpu=16, use_dynamic_bsz=None,
         ppo_max_token_len_per_gpu=32768, forward_max_token_len_per_gpu=32768, ppo_epochs=None, shuffle=None,
         grad_clip=1.0, cliprange_value=0.5, loss_agg_mode=None, ulysses_sequence_parallel_size=1,
+        exec_micro_batches=0, exec_activation_gb=40,  # as the actor's (dp_actor.exec_groups)
     ),
     algorithm=dict(gamma=1.0, lam=1.0, adv_estimator="grpo", norm_adv_by_std_in_grpo=True, use_kl_in_reward=False,
                    kl_penalty="kl", kl_ctrl=dict(type="fixed", kl_coef=0.001, horizon=10000, target_kl=0.1)),

@@ -213,6 +213,25 @@ def _concat_rows(group):
             for k in ("input_ids", "attention_mask", "position_ids", "responses")}
 
 
+def exec_groups(cfg, model_cfg, micro_batches):
+    """Micro-batches that run through the model in one pass. The reference runs one per forward / backward
+    (dp_actor.py:392-466, dp_critic.py:214-250); their gradients only add up (each micro-batch's loss carries its own
+    scale factor and token count), so consecutive micro-batches may share one pass over their concatenated rows: the
+    GEMMs see 2-4x the rows (at 6144 rows the N = 896 projections fill 96 of 256 CUs). ``exec_micro_batches`` fixes
+    the group size (1 = the reference's schedule); 0 groups as many as keep the saved activations under
+    ``exec_activation_gb``."""
+    n = int(cfg.get("exec_micro_batches", 1) or 0)
+    if n <= 0:
+        H, I, L = model_cfg.hidden_size, model_cfg.intermediate_size, model_cfg.num_hidden_layers
+        nq = (model_cfg.num_attention_heads + 2 * model_cfg.num_key_value_heads) * model_cfg.head_dim
+        # saved per token and layer: x, x2 (fp32), h1, h2, attn (bf16), q / k / v / k^T, gate|up and SwiGLU out
+        per_tok = L * (8 * H + 6 * H + 4 * nq + 6 * I)
+        budget = float(cfg.get("exec_activation_gb", 40)) * 2 ** 30
+        toks = max(mb.batch["input_ids"].numel() for mb in micro_batches)
+        n = max(1, int(budget // max(1, per_tok * toks)))
+    return [micro_batches[i:i + n] for i in range(0, len(micro_batches), n)]
+
+
 class DataParallelPPOActor:
     """dp_actor.py:53-482. ``actor_optimizer`` None -> reference policy."""
 
@@ -259,23 +278,7 @@ class DataParallelPPOActor:
         return ent, logp
 
     def _exec_groups(self, micro_batches):
-        """Micro-batches that run through the model in one pass. The reference runs one per forward / backward
-        (dp_actor.py:392-466); their gradients only add up (each micro-batch's loss carries its own scale factor and
-        token count), so consecutive micro-batches may share one pass over their concatenated rows: the GEMMs see
-        2-4x the rows (at 6144 rows the N = 896 projections fill 96 of 256 CUs). ``exec_micro_batches`` fixes the
-        group size; 0 groups as many as keep the saved activations under ``exec_activation_gb``."""
-        cfg = self.config
-        n = int(cfg.get("exec_micro_batches", 1) or 0)
-        if n <= 0:
-            mc = self.actor_module.cfg
-            H, I, L = mc.hidden_size, mc.intermediate_size, mc.num_hidden_layers
-            nq = (mc.num_attention_heads + 2 * mc.num_key_value_heads) * mc.head_dim
-            # saved per token and layer: x, x2 (fp32), h1, h2, attn (bf16), q / k / v / k^T, gate|up and SwiGLU out
-            per_tok = L * (8 * H + 6 * H + 4 * nq + 6 * I)
-            budget = float(cfg.get("exec_activation_gb", 40)) * 2 ** 30
-            toks = max(mb.batch["input_ids"].numel() for mb in micro_batches)
-            n = max(1, int(budget // max(1, per_tok * toks)))
-        return [micro_batches[i:i + n] for i in range(0, len(micro_batches), n)]
+        return exec_groups(self.config, self.actor_module.cfg, micro_batches)
 
     def _log_prob_groups(self, micro_batches):
         """Forward-only passes: rows are independent, so consecutive micro-batches run as one pass of at most

@@ -16,7 +16,7 @@ import math
 import torch
 
 from . import native
-from .dp_actor import FlatAdamW, append_to_dict
+from .dp_actor import FlatAdamW, _concat_rows, append_to_dict, exec_groups
 from .protocol import DataProto
 from .seqlen_balancing import prepare_dynamic_batch, restore_dynamic_batch
 from .qwen2 import Qwen2Model, RmPad, gather_rows
@@ -112,21 +112,28 @@ class DataParallelPPOCritic:
                     grad_accum = cfg.ppo_mini_batch_size // cfg.ppo_micro_batch_size_per_gpu
                     micro_batches = mini_batch.split(cfg.ppo_micro_batch_size_per_gpu)
                 self.critic_optimizer.zero_grad()
-                for k, micro_batch in enumerate(micro_batches):
-                    if k == len(micro_batches) - 1:
+                groups = exec_groups(cfg, m.cfg, micro_batches)  # micro-batches sharing one pass (dp_actor)
+                for gi, group in enumerate(groups):
+                    if gi == len(groups) - 1:
                         self.critic_optimizer.begin_overlap(m)
-                    mb = micro_batch.batch
-                    if cfg.get("use_dynamic_bsz", False):  # dp_critic.py:232-234
-                        lsf = mb["response_mask"].shape[0] / cfg.ppo_mini_batch_size
-                    else:
-                        lsf = 1.0 / grad_accum
-                    vpreds = self._forward_micro_batch(mb)
-                    out = fused_value_loss(vpreds, mb["values"], mb["returns"], mb["response_mask"],
-                                           cliprange_value=cfg.cliprange_value, loss_agg_mode=cfg.loss_agg_mode,
-                                           loss_scale_factor=lsf)
-                    out[3].backward()
-                    mb_out.append(out.detach())
-                    mb_lsf.append(lsf)
+                    vpreds_all = self._forward_micro_batch(_concat_rows(group))
+                    total, r0 = None, 0
+                    for micro_batch in group:
+                        mb = micro_batch.batch
+                        n = mb["responses"].shape[0]
+                        if cfg.get("use_dynamic_bsz", False):  # dp_critic.py:232-234
+                            lsf = mb["response_mask"].shape[0] / cfg.ppo_mini_batch_size
+                        else:
+                            lsf = 1.0 / grad_accum
+                        vpreds = vpreds_all[r0:r0 + n] if len(group) > 1 else vpreds_all
+                        r0 += n
+                        out = fused_value_loss(vpreds, mb["values"], mb["returns"], mb["response_mask"],
+                                               cliprange_value=cfg.cliprange_value, loss_agg_mode=cfg.loss_agg_mode,
+                                               loss_scale_factor=lsf)
+                        total = out[3] if total is None else total + out[3]
+                        mb_out.append(out.detach())
+                        mb_lsf.append(lsf)
+                    total.backward()
                 self.critic_optimizer.end_overlap(m)
                 grad_norms.append(self.critic_optimizer.step().clone())
         self.critic_optimizer.zero_grad()

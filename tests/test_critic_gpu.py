@@ -307,3 +307,33 @@ def test_gae_ppo_step_dynamic_bsz():
     m = trainer.fit(num_steps=1)[-1]
     for k in ["critic/vf_loss", "actor/pg_loss", "actor/kl_loss", "critic/grad_norm", "actor/grad_norm"]:
         assert k in m and np.isfinite(m[k]), k
+
+
+def test_update_critic_fused_micro_batches_match_per_micro_batch(golden):
+    """update_critic with both micro-batches of a mini-batch in one pass (exec_micro_batches=0) equals the
+    reference's one-pass-per-micro-batch schedule (exec_micro_batches=1): metrics and post-step parameters, fp32."""
+    from dots.rl_amd.config import to_attr
+    from dots.rl_amd.dp_actor import FlatAdamW
+    from dots.rl_amd.dp_critic import DataParallelPPOCritic
+    from dots.rl_amd.protocol import DataProto
+
+    zr, _ = golden("tiny_qwen2_rollout.npz")
+    z, _ = golden("tiny_critic.npz")
+    R = zr["responses"].shape[1]
+    base = {"input_ids": T(zr["sequences"]), "attention_mask": T(zr["attention_mask"]),
+            "position_ids": T(zr["position_ids"]), "responses": T(zr["responses"]),
+            "response_mask": T(zr["attention_mask"][:, -R:]), "values": T(z["values"]), "returns": T(z["returns"])}
+    res = {}
+    for ex in (1, 0):
+        cfg, store, model = _tiny_critic()
+        ccfg = to_attr({"model": {}, "ppo_mini_batch_size": 6, "ppo_micro_batch_size_per_gpu": 2, "ppo_epochs": 1,
+                        "cliprange_value": 0.5, "loss_agg_mode": "token-mean", "exec_micro_batches": ex,
+                        "use_dynamic_bsz": False})
+        opt = FlatAdamW(store, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01, max_grad_norm=1.0)
+        critic = DataParallelPPOCritic(ccfg, model, opt)
+        m = critic.update_critic(DataProto.from_dict(dict(base)))
+        res[ex] = (m, store.master.detach().clone())
+    for k in res[1][0]:
+        np.testing.assert_allclose(res[0][0][k], res[1][0][k], rtol=1e-5, atol=1e-6, err_msg=k)
+    d = res[0][1] - res[1][1]
+    assert (d.norm() / res[1][1].norm()).item() < 1e-6
