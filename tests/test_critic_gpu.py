@@ -331,9 +331,13 @@ def test_update_critic_fused_micro_batches_match_per_micro_batch(golden):
                         "use_dynamic_bsz": False})
         opt = FlatAdamW(store, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01, max_grad_norm=1.0)
         critic = DataParallelPPOCritic(ccfg, model, opt)
+        before = store.master.detach().clone()
         m = critic.update_critic(DataProto.from_dict(dict(base)))
-        res[ex] = (m, store.master.detach().clone())
+        res[ex] = (m, store.master.detach() - before)
     for k in res[1][0]:
         np.testing.assert_allclose(res[0][0][k], res[1][0][k], rtol=1e-5, atol=1e-6, err_msg=k)
-    d = res[0][1] - res[1][1]
-    assert (d.norm() / res[1][1].norm()).item() < 1e-6
+    # the updates themselves (AdamW's first step moves an element by ~lr * sign(g): elements whose gradient sits at
+    # fp32 noise may flip, as in test_actor_update_gpu._check_params)
+    d0, d1 = res[0][1], res[1][1]
+    bad = (d0 - d1).abs() > 0.02 * torch.clamp(d1.abs(), min=d1.abs()[d1 != 0].median().item())
+    assert bad.float().mean().item() < 1e-3

@@ -32,7 +32,19 @@ def store_bytes(cfg, world, trainable, sharded):
             "adam_moments_fp32": 8 * master}
 
 
-def plan(name, arch, world, critic, seqs_per_rank, seq_len):
+def activation_bytes(cfg, micro_seqs, mini_seqs, seq_len, budget_gb=40):
+    """Saved activations of one update pass under dp_actor.exec_groups (micro-batches per pass chosen to stay under
+    exec_activation_gb, at least one): per token and layer x, x2 fp32; h1, h2, attn bf16; q / k / v / k^T; gate|up and
+    the SwiGLU output. The weights are read in place by drl_gemm (no transposed copies)."""
+    nq = (cfg.num_attention_heads + 2 * cfg.num_key_value_heads) * cfg.head_dim
+    H, I = cfg.hidden_size, cfg.intermediate_size
+    per_tok = cfg.num_hidden_layers * (8 * H + 6 * H + 4 * nq + 6 * I)
+    toks = micro_seqs * seq_len
+    n = max(1, min(mini_seqs // micro_seqs, int(budget_gb * 2 ** 30 // (per_tok * toks))))
+    return per_tok * toks * n
+
+
+def plan(name, arch, world, critic, seqs_per_rank, seq_len, micro=8, mini=32):
     actor = Qwen2Config.from_dict(arch)
     sec = {"fsdp_config": {"shard": "auto"}}
     sh = _shard_spec(sec, actor, 0, world) is not None
@@ -46,20 +58,22 @@ def plan(name, arch, world, critic, seqs_per_rank, seq_len):
         if csh:
             rows["critic"]["grad_shard_fp32"] = rows["critic"]["master_fp32"]
     kv = 2 * actor.num_key_value_heads * actor.head_dim * 2 * actor.num_hidden_layers * seqs_per_rank * seq_len
-    total = sum(sum(r.values()) for r in rows.values()) + kv
-    return name, world, sh, rows, kv, total
+    act = activation_bytes(actor, micro, mini, seq_len)  # the actor's and the critic's updates run one after another
+    total = sum(sum(r.values()) for r in rows.values()) + max(kv, act)
+    return name, world, sh, rows, kv, act, total
 
 
 def main():
     cases = [plan("#2/#3 Qwen2.5-0.5B GRPO", QWEN25_05B, 8, False, 64, 768),
              plan("#4 Llama-3-8B PPO (actor+critic)", LLAMA3_8B, 8, True, 64, 768),
-             plan("#5 Qwen2.5-7B DAPO", QWEN25_7B, 8, False, 64, 512 + 1024)]
-    print("| config (DP=8, per GPU) | sharded | actor | ref | critic | rollout KV cache | total state |")
-    print("|---|---|---|---|---|---|---|")
-    for name, world, sh, rows, kv, total in cases:
+             plan("#5 Qwen2.5-7B DAPO", QWEN25_7B, 8, False, 64, 512 + 1024, micro=2, mini=4)]
+    print("| config (DP=8, per GPU) | sharded | actor | ref | critic | rollout KV cache | update activations | "
+          "peak (state + max(KV, activations)) |")
+    print("|---|---|---|---|---|---|---|---|")
+    for name, world, sh, rows, kv, act, total in cases:
         fmt = lambda r: f"{sum(r.values()) / GB:.1f} GB" if r else "—"  # noqa: E731
         print(f"| {name} | {'yes' if sh else 'no'} | {fmt(rows['actor'])} | {fmt(rows['ref'])} | "
-              f"{fmt(rows.get('critic'))} | {kv / GB:.1f} GB | **{total / GB:.1f} GB** of 288 |")
+              f"{fmt(rows.get('critic'))} | {kv / GB:.1f} GB | {act / GB:.1f} GB | **{total / GB:.1f} GB** of 288 |")
     # the same configs replicated (what fails)
     for arch, name, critic in ((LLAMA3_8B, "#4 replicated", True), (QWEN25_7B, "#5 replicated", False)):
         a = Qwen2Config.from_dict(arch)
