@@ -63,6 +63,14 @@ __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v)
 
 // bf16 <-> f32 (bit-level; bf16 stored as uint16_t)
 __device__ __forceinline__ float bf16_to_f32(uint16_t h) { return __uint_as_float(static_cast<uint32_t>(h) << 16); }
+// logistic sigmoid and SiLU (F.silu: x * sigmoid(x)) on the hardware exp2 / reciprocal (v_exp_f32, v_rcp_f32, ~1 ulp
+// each): one form for every SwiGLU in the library (GEMM / decode epilogues, the elementwise kernels) so the paths
+// agree with each other bit for bit; against expf + IEEE division it differs by a few fp32 ulp, below the bf16
+// rounding every caller applies next. exp2(+inf) -> rcp(inf) = 0: silu(-large) = -0, silu(+large) = x, NaN stays NaN.
+__device__ __forceinline__ float sigmoid_fast(float x) {
+  return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-1.4426950408889634f * x));
+}
+__device__ __forceinline__ float silu_fast(float x) { return x * sigmoid_fast(x); }
 __device__ __forceinline__ uint16_t f32_to_bf16(float f) {
   // round-to-nearest-even; NaN stays NaN (quiet bit forced)
   uint32_t u = __float_as_uint(f);

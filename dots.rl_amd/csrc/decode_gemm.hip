@@ -181,7 +181,7 @@ __global__ __launch_bounds__(256) void decode_gemm_kernel(DgArgs a) {
         const int qu = (iu & 3) + 4 * (iu >> 3), lu = ml + 32 * ((iu >> 2) & 1);
         const float g = bf16r(((red[0][blk][qg][lg] + red[1][blk][qg][lg]) + red[2][blk][qg][lg]) + red[3][blk][qg][lg]);
         const float u = bf16r(((red[0][blk][qu][lu] + red[1][blk][qu][lu]) + red[2][blk][qu][lu]) + red[3][blk][qu][lu]);
-        o[j] = to_bf16_bits(bf16r(g / (1.f + expf(-g))) * u);
+        o[j] = to_bf16_bits(bf16r(silu_fast(g)) * u);
       }
       // packed for the next GEMM (K' = half): k step = tile, 8-column half hc, token (mb0 + blk, ml)
       *reinterpret_cast<u16x8*>(a.out + ((static_cast<int64_t>(tile) * a.MBT + mb0 + blk) * 64 + hc * 32 + ml) * 8) = o;
@@ -226,7 +226,7 @@ __device__ __forceinline__ void tiled_epilogue(const DgArgs& a, const f32x16 (&a
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
           const float g = bf16r(c[r]), u = bf16r(c[r + 8]);
-          o[r] = to_bf16_bits(bf16r(g / (1.f + expf(-g))) * u);
+          o[r] = to_bf16_bits(bf16r(silu_fast(g)) * u);
         }
         // half 0 holds columns 0-3 | 8-11, half 1 4-7 | 12-15: swap the middle quads so each half owns 8
         // consecutive columns (half 0: 0-7, half 1: 8-15)

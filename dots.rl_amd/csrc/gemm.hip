@@ -196,7 +196,7 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(GemmArgs g) {
           const int m = m0 + (wm * MB + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
           if (m >= g.M) continue;
           const float gg = bf16r(acc[i][j][r]), uu = bf16r(acc[i][j + 1][r]);
-          g.c[static_cast<int64_t>(m) * g.ldc + col] = to_bf16_bits(bf16r(gg / (1.f + expf(-gg))) * uu);
+          g.c[static_cast<int64_t>(m) * g.ldc + col] = to_bf16_bits(bf16r(silu_fast(gg)) * uu);
           if (g.c2) {
             g.c2[static_cast<int64_t>(m) * g.ldc2 + col] = to_bf16_bits(gg);
             g.c2[static_cast<int64_t>(m) * g.ldc2 + half + col] = to_bf16_bits(uu);
@@ -394,7 +394,7 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs g) {
           for (int r = 0; r < 4; ++r) {
             const int o = (i * 16 + fq * 4 + r) * SLD + qn * 16 + fr;
             const float gg = bf16r(acc[qm][qn][i][0][r]), uu = bf16r(acc[qm][qn][i][1][r]);
-            st[o] = to_bf16_bits(bf16r(gg / (1.f + expf(-gg))) * uu);
+            st[o] = to_bf16_bits(bf16r(silu_fast(gg)) * uu);
             if (g.c2) {
               st[REG + o] = to_bf16_bits(gg);
               st[2 * REG + o] = to_bf16_bits(uu);

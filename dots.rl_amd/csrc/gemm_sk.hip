@@ -44,7 +44,7 @@ __device__ __forceinline__ bf16x8 as_bf16x8(u16x8 v) { return __builtin_bit_cast
 __device__ __forceinline__ uint16_t to_bf16_bits(float f) { return __builtin_bit_cast(uint16_t, static_cast<__bf16>(f)); }
 __device__ __forceinline__ float bf16r(float f) { return bf16_to_f32(to_bf16_bits(f)); }
 
-constexpr int EPI_NONE = 0, EPI_BIAS = 1, EPI_SWIGLU = 2, EPI_F32 = 3;
+constexpr int EPI_NONE = 0, EPI_BIAS = 1, EPI_SWIGLU = 2, EPI_F32 = 3, EPI_SWIGLU_BWD = 4;
 constexpr int HT = 128 * 64, BUF = 4 * HT;  // half-tile, k-tile buffer (elements)
 constexpr int SLAB = 256 * 256;              // fp32 elements of one partial tile
 
@@ -52,7 +52,7 @@ struct SkArgs {
   const uint16_t* a;
   const uint16_t* b;
   uint16_t* c;         // bf16 out (M, N) or SwiGLU (M, N / 2)
-  uint16_t* c2;        // SwiGLU: optional gu (M, N)
+  uint16_t* c2;        // SwiGLU: optional gu (M, N) written; SwiGLU backward: gu (M, 2N) read
   float* c32;          // EPI_F32 out (M, N)
   const uint16_t* bias;
   float* ws;           // stream-K slabs, gridDim.x x SLAB
@@ -350,7 +350,7 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
             for (int r = 0; r < 4; ++r) {
               const int o = (i * 16 + fq * 4 + r) * SLD + qn * 16 + fr;
               const float gg = bf16r(acc[qm][qn][i][0][r]), uu = bf16r(acc[qm][qn][i][1][r]);
-              st[o] = to_bf16_bits(bf16r(gg / (1.f + expf(-gg))) * uu);
+              st[o] = to_bf16_bits(bf16r(silu_fast(gg)) * uu);
               if (g.c2) {
                 st[REG + o] = to_bf16_bits(gg);
                 st[2 * REG + o] = to_bf16_bits(uu);
@@ -393,7 +393,9 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
       constexpr int SLD = 72;
       uint16_t* st = lds + wave * 64 * SLD;
       const int ch = lane & 7, col = n0 + wc * 64 + ch * 8;
-      const bool vec = col + 8 <= g.N && (g.ldc & 7) == 0 && (reinterpret_cast<uintptr_t>(g.c) & 15) == 0;
+      const bool vec = col + 8 <= g.N && (g.ldc & 7) == 0 && (reinterpret_cast<uintptr_t>(g.c) & 15) == 0 &&
+                       (EPI != EPI_SWIGLU_BWD || ((g.ldc2 & 7) == 0 && (g.N & 7) == 0 &&
+                                                  (reinterpret_cast<uintptr_t>(g.c2) & 15) == 0));
 #pragma unroll
       for (int qm = 0; qm < 2; ++qm) {
 #pragma unroll
@@ -416,7 +418,38 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
           const u16x8 v = *reinterpret_cast<const u16x8*>(st + lr * SLD + ch * 8);
           if (m >= g.M || col >= g.N) continue;
           uint16_t* dstp = g.c + static_cast<int64_t>(m) * g.ldc + col;
-          if (vec) {
+          if constexpr (EPI == EPI_SWIGLU_BWD) {
+            // v = bf16(d a) of columns col..col+7; gate / up of the same columns from the saved gu row -> dgu
+            // (swiglu_bwd's math and roundings: dg = bf16(d*u) * sig (1 + g (1 - sig)), du = d * bf16(g sig))
+            const uint16_t* gp = g.c2 + static_cast<int64_t>(m) * g.ldc2 + col;
+            u16x8 gq, uq;
+            if (vec) {
+              gq = *reinterpret_cast<const u16x8*>(gp);
+              uq = *reinterpret_cast<const u16x8*>(gp + g.N);
+            } else {
+              for (int e = 0; e < 8; ++e) {
+                gq[e] = col + e < g.N ? gp[e] : 0;
+                uq[e] = col + e < g.N ? gp[g.N + e] : 0;
+              }
+            }
+            u16x8 dg, du;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float d = bf16_to_f32(v[e]), gg = bf16_to_f32(gq[e]), uu = bf16_to_f32(uq[e]);
+              const float sig = sigmoid_fast(gg);
+              dg[e] = to_bf16_bits(bf16r(d * uu) * (sig * (1.f + gg * (1.f - sig))));
+              du[e] = to_bf16_bits(d * bf16r(gg * sig));
+            }
+            if (vec) {
+              *reinterpret_cast<u16x8*>(dstp) = dg;
+              *reinterpret_cast<u16x8*>(dstp + g.N) = du;
+            } else {
+              for (int e = 0; e < 8 && col + e < g.N; ++e) {
+                dstp[e] = dg[e];
+                dstp[g.N + e] = du[e];
+              }
+            }
+          } else if (vec) {
             *reinterpret_cast<u16x8*>(dstp) = v;
           } else {
             for (int e = 0; e < 8 && col + e < g.N; ++e) dstp[e] = v[e];
@@ -616,6 +649,8 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
 }
 
 inline bool epi_is_swiglu(int epilogue) { return epilogue == DRL_GEMM_SWIGLU; }
+// epilogues that need whole tiles (no uniform split-K: its combine stores element by element)
+inline bool epi_whole_tiles(int epilogue) { return epilogue == DRL_GEMM_SWIGLU || epilogue == DRL_GEMM_SWIGLU_BWD; }
 
 struct SkTuning {
   int grid = 0;      // 0 = CU count
@@ -637,6 +672,9 @@ int launch_sk_layout(SkArgs& g, int epi, int grid, hipStream_t s) {
       break;
     case EPI_SWIGLU:
       if constexpr (AT == 0 && BT == 0) hipLaunchKernelGGL((gemm_sk_kernel<EPI_SWIGLU, 0, 0>), gr, dim3(512), 0, s, g);
+      break;
+    case EPI_SWIGLU_BWD:
+      if constexpr (AT == 0 && BT == 1) hipLaunchKernelGGL((gemm_sk_kernel<EPI_SWIGLU_BWD, 0, 1>), gr, dim3(512), 0, s, g);
       break;
   }
   DRL_LAUNCH_CHECK();
@@ -705,11 +743,15 @@ int drl_gemm(const void* a, int64_t lda, int32_t a_layout, const void* b, int64_
   DRL_CHECK_ARG(b_layout == DRL_LAYOUT_K || b_layout == DRL_LAYOUT_T, "b_layout");
   DRL_CHECK_ARG(M >= 1 && N >= 1 && K >= 1 && M < (1ll << 30) && N < (1ll << 30) && K < (1ll << 30),
                 "bad shape M=%lld N=%lld K=%lld", (long long)M, (long long)N, (long long)K);
-  DRL_CHECK_ARG(epilogue >= DRL_GEMM_PLAIN && epilogue <= DRL_GEMM_SWIGLU, "unknown epilogue %d", epilogue);
+  DRL_CHECK_ARG(epilogue >= DRL_GEMM_PLAIN && epilogue <= DRL_GEMM_SWIGLU_BWD, "unknown epilogue %d", epilogue);
   DRL_CHECK_ARG(c_dtype == DRL_BF16 || (c_dtype == DRL_F32 && epilogue == DRL_GEMM_PLAIN),
                 "fp32 output takes the plain epilogue");
-  DRL_CHECK_ARG(epilogue == DRL_GEMM_PLAIN || (a_layout == DRL_LAYOUT_K && b_layout == DRL_LAYOUT_K),
+  DRL_CHECK_ARG(epilogue == DRL_GEMM_PLAIN || epilogue == DRL_GEMM_SWIGLU_BWD ||
+                (a_layout == DRL_LAYOUT_K && b_layout == DRL_LAYOUT_K),
                 "bias / SwiGLU epilogues need layout-K operands (the forward)");
+  DRL_CHECK_ARG(epilogue != DRL_GEMM_SWIGLU_BWD ||
+                (a_layout == DRL_LAYOUT_K && b_layout == DRL_LAYOUT_T && c2 != nullptr && ldc2 >= 2 * N && ldc >= 2 * N),
+                "SwiGLU backward: the down_proj dgrad (A layout K, B layout T) with c2 = gu (M, 2N), c = dgu (M, 2N)");
   DRL_CHECK_ARG(epilogue != DRL_GEMM_BIAS || bias != nullptr, "bias epilogue without bias");
   DRL_CHECK_ARG(epilogue != DRL_GEMM_SWIGLU || N % 64 == 0, "SwiGLU: N = 2I with I %% 32 == 0");
   // a layout-K operand has K contiguous: a partial k-tile would read the next row, so whole 64-deep k-tiles (a
@@ -767,10 +809,11 @@ int drl_gemm(const void* a, int64_t lda, int32_t a_layout, const void* b, int64_
     // slab traffic and the per-split pipeline fill)
     S = mode == 3 && g_sk.param > 0 ? g_sk.param : std::min({cap / std::max(1, g.n_tiles), 8, g.P / 6});
     S = std::max(1, std::min({S, g.P, 32, cap / std::max(1, g.n_tiles)}));
-    if (epi_is_swiglu(epilogue) || g.n_tiles * 2 > cap) S = 1;
+    if (epi_whole_tiles(epilogue) || g.n_tiles * 2 > cap) S = 1;
     mode = S > 1 ? 3 : 2;
   }
   g.splits = 1;
+  if (mode == 3 && epi_whole_tiles(epilogue)) mode = 2;  // a forced split-K tuning: whole tiles instead
   if (mode == 3) {
     g.splits = S;
     g.dp_tiles = 0;
@@ -789,7 +832,7 @@ int drl_gemm(const void* a, int64_t lda, int32_t a_layout, const void* b, int64_
   }
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int epi = epilogue == DRL_GEMM_PLAIN ? (c_dtype == DRL_F32 ? EPI_F32 : EPI_NONE)
-                                             : (epilogue == DRL_GEMM_BIAS ? EPI_BIAS : EPI_SWIGLU);
+                  : epilogue == DRL_GEMM_BIAS ? EPI_BIAS : epilogue == DRL_GEMM_SWIGLU ? EPI_SWIGLU : EPI_SWIGLU_BWD;
   if (a_layout == DRL_LAYOUT_K && b_layout == DRL_LAYOUT_K) return launch_sk_layout<0, 0>(g, epi, grid, s);
   if (a_layout == DRL_LAYOUT_K) return launch_sk_layout<0, 1>(g, epi, grid, s);
   if (b_layout == DRL_LAYOUT_K) return launch_sk_layout<1, 0>(g, epi, grid, s);

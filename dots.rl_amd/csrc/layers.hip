@@ -864,7 +864,7 @@ __global__ __launch_bounds__(256) void swiglu_fwd_kernel(const E* gu, E* out, in
     ld4e(gu, row * 2 * I + c, row * 2 * I + I, true, g);
     ld4e(gu, row * 2 * I + I + c, row * 2 * I + 2 * I, true, u);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) o[e] = rnd<E>(g[e] / (1.f + expf(-g[e]))) * u[e];
+    for (int e = 0; e < 4; ++e) o[e] = rnd<E>(silu_fast(g[e])) * u[e];
     st4e(out, 4 * i, N * I, true, o);
   }
 }
@@ -882,7 +882,7 @@ __global__ __launch_bounds__(256) void swiglu_bwd_kernel(const E* gu, const E* d
     ld4e(da, 4 * i, N * I, true, d);
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const float sig = 1.f / (1.f + expf(-g[e]));
+      const float sig = sigmoid_fast(g[e]);
       dg[e] = rnd<E>(d[e] * u[e]) * (sig * (1.f + g[e] * (1.f - sig)));
       du[e] = d[e] * rnd<E>(g[e] * sig);
     }
@@ -935,7 +935,7 @@ __global__ __launch_bounds__(256) void swiglu_fwd_bf16x8_kernel(const uint16_t* 
       unpack8(gq[k], g);
       unpack8(uq[k], u);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = rnd<uint16_t>(g[e] / (1.f + expf(-g[e]))) * u[e];
+      for (int e = 0; e < 8; ++e) o[e] = rnd<uint16_t>(silu_fast(g[e])) * u[e];
       *reinterpret_cast<uint4*>(out + static_cast<size_t>(i + k * stride) * 8) = pack8(o);
     }
   }
@@ -956,7 +956,7 @@ __global__ __launch_bounds__(256) void swiglu_bwd_bf16x8_kernel(const uint16_t* 
     unpack8(dq, d);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const float sig = 1.f / (1.f + expf(-g[e]));
+      const float sig = sigmoid_fast(g[e]);
       dg[e] = rnd<uint16_t>(d[e] * u[e]) * (sig * (1.f + g[e] * (1.f - sig)));
       du[e] = d[e] * rnd<uint16_t>(g[e] * sig);
     }

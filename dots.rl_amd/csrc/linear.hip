@@ -53,7 +53,7 @@ __device__ __forceinline__ void store_out(const LinearArgs& a, int tile, int m, 
     const int n = tile * 16 + i;
     if (n >= a.half) return;
     const float g = bf16r(v), u = bf16r(v_up);
-    a.out[static_cast<int64_t>(m) * a.ld_out + n] = to_bf16_bits(bf16r(g / (1.f + expf(-g))) * u);
+    a.out[static_cast<int64_t>(m) * a.ld_out + n] = to_bf16_bits(bf16r(silu_fast(g)) * u);
   } else {
     const int n = tile * 32 + i;
     if (n >= a.N) return;

@@ -692,7 +692,7 @@ def colsum_bf16_acc(x, out):
     return out
 
 
-GEMM_PLAIN, GEMM_BIAS, GEMM_SWIGLU = 0, 1, 2
+GEMM_PLAIN, GEMM_BIAS, GEMM_SWIGLU, GEMM_SWIGLU_BWD = 0, 1, 2, 3
 
 
 def gemm_nt(x, w, bias=None, swiglu=False, out=None, out_gu=None):
@@ -799,6 +799,24 @@ def linear_dgrad(dy, w, out=None):
     if out is None:
         out = torch.empty(M, N, dtype=torch.bfloat16, device=dy.device)
     return gemm(dy, LAYOUT_K, w, LAYOUT_T, M, N, K, out)
+
+
+def linear_dgrad_swiglu_bwd(dy, w, gu, out=None):
+    """The down_proj input gradient fused with the SwiGLU backward: da = bf16(dy W) (dy (M, H), w (H, I) read in
+    place) -> dgu (M, 2I) = swiglu_bwd(gu, da) with gu (M, 2I) = the forward's [gate | up] (csrc/gemm_sk.hip)."""
+    _dev(dy, w, gu)
+    M, K = dy.shape
+    N = w.shape[1]
+    assert dy.dtype == w.dtype == gu.dtype == torch.bfloat16 and dy.stride(1) == 1 and w.stride(1) == 1
+    assert gu.shape == (M, 2 * N) and gu.stride(1) == 1 and w.shape[0] == K
+    if out is None:
+        out = torch.empty(M, 2 * N, dtype=torch.bfloat16, device=dy.device)
+    assert out.shape == (M, 2 * N) and out.stride(1) == 1
+    ws = _ws_gemm.get(out.device)
+    check(lib().drl_gemm(_p(dy), dy.stride(0), LAYOUT_K, _p(w), w.stride(0), LAYOUT_T, _p(out), out.stride(0),
+                         _lib.DRL_BF16, 0, M, N, K, None, GEMM_SWIGLU_BWD, _p(gu), gu.stride(0), _p(ws), ws.numel(),
+                         _stream()), "drl_gemm")
+    return out
 
 
 def linear_wgrad(gw, dy, x, accumulate=True, ws_slot=0):

@@ -335,8 +335,9 @@ def acc_wgrad(gw, dy, x):
 
 # The weight gradient of a projection runs on a side stream while its input gradient runs on the current one: the
 # pair's workgroups share the CUs (at 6144 rows: qkv 160 + 96, gate_up 152 + 96 of 256) where each alone leaves most
-# of them idle. DRL_CONCURRENT_WGRAD=0 serialises them (A/B measurements).
-CONCURRENT_WGRAD = os.environ.get("DRL_CONCURRENT_WGRAD", "1") != "0"
+# of them idle. Measured no faster under fused micro-batch execution (3.385 vs 3.388 s per step,
+# tools/gpu_r03k.sh): off by default, DRL_CONCURRENT_WGRAD=1 turns it on.
+CONCURRENT_WGRAD = os.environ.get("DRL_CONCURRENT_WGRAD", "0") != "0"
 _SIDE_STREAMS = {}
 
 
@@ -571,9 +572,14 @@ class _DecoderLayer(torch.autograd.Function):
         dx2 = g_x2.to(torch.float32).contiguous().clone()
         dm = g_mlp.to(dt).contiguous().view(N, H)
         # MLP
-        da = dgrad_wgrad(dm, s.w(p + "down_proj"), s.g(p + "down_proj"), sv["a"])
-        dgu = torch.empty_like(sv["gu"])
-        native.swiglu_bwd(sv["gu"], da, dgu)
+        if _sk(dm, sv["gu"]) and dm.shape[1] % 64 == 0:
+            # down_proj dgrad with the SwiGLU backward in its epilogue (d a never written)
+            acc_wgrad(s.g(p + "down_proj"), dm, sv["a"])
+            dgu = native.linear_dgrad_swiglu_bwd(dm, s.w(p + "down_proj"), sv["gu"])
+        else:
+            da = dgrad_wgrad(dm, s.w(p + "down_proj"), s.g(p + "down_proj"), sv["a"])
+            dgu = torch.empty_like(sv["gu"])
+            native.swiglu_bwd(sv["gu"], da, dgu)
         dh2 = dgrad_wgrad(dgu, s.w(p + "gate_up_proj"), s.g(p + "gate_up_proj"), sv["h2"].view(N, H))
         native.rmsnorm_bwd(sv["x2"], s.w(p + "post_attention_layernorm"), sv["rstd2"], dh2, dx2,
                            s.g(p + "post_attention_layernorm"))

@@ -557,7 +557,7 @@ int drl_decode_rope(const float* partials, int32_t nsplit, const void* bias, con
  * (N = 2I rows), c (M, I) = bf16(bf16(silu(g)) * u) with g, u the bf16-rounded gate / up sums (swiglu_fwd's
  * semantics); c2 (M, 2I) = [g | u] when not NULL (the backward's saved activation). K % 64 == 0; A / B rows
  * 16-byte aligned. */
-enum { DRL_GEMM_PLAIN = 0, DRL_GEMM_BIAS = 1, DRL_GEMM_SWIGLU = 2 };
+enum { DRL_GEMM_PLAIN = 0, DRL_GEMM_BIAS = 1, DRL_GEMM_SWIGLU = 2, DRL_GEMM_SWIGLU_BWD = 3 };
 int drl_gemm_bf16_nt(const void* a, int64_t lda, const void* b, int64_t ldb, void* c, int64_t ldc, int64_t M,
                      int64_t N, int64_t K, const void* bias, int32_t epilogue, void* c2, int64_t ldc2, void* stream);
 /* Tuning hook: 0 = automatic (the 256 x 256 ping-pong form when K % 128 == 0 and the 256 x 256 grid has >= 64
@@ -579,7 +579,9 @@ void drl_gemm_set_group(int32_t group_m);
  * bf16 operands, fp32 accumulation (a layout-K A operand over 2 GB runs as row blocks). c_dtype DRL_BF16: epilogues as drl_gemm_bf16_nt (bias / SwiGLU need both
  * operands layout K); DRL_F32 (plain epilogue): c = acc, or c += acc when beta != 0. K % 64 == 0 unless both
  * operands are layout T (then any K: the k tail reads as zeros). A / B 16-byte aligned, ld % 8 == 0, each operand
- * < 2 GB. Work is split stream-K over at most one workgroup per CU; split tiles are summed in a fixed order
+ * < 2 GB. DRL_GEMM_SWIGLU_BWD (drl_gemm only): the down_proj dgrad fused with the SwiGLU backward (swiglu_bwd's
+ * math on d a = bf16(acc)): A = dy layout K, B = W_down layout T, c2 = gu (M, 2N) read, c = dgu (M, 2N) written.
+ * Work is split stream-K over at most one workgroup per CU; split tiles are summed in a fixed order
  * (bit-reproducible). workspace: drl_gemm_workspace_bytes() bytes, 16-byte aligned, zeroed once at allocation
  * (every call leaves its flag words zero again); calls sharing a workspace must be ordered on one stream. */
 enum { DRL_LAYOUT_K = 0, DRL_LAYOUT_T = 1 };

@@ -171,10 +171,12 @@ def test_wgrad_operand_over_2gb_splits_k():
 
 
 @pytest.mark.parametrize("M,N_out,N_in", [(6144, 1152, 896), (6144, 9728, 896), (6144, 896, 4864), (777, 896, 896)])
-def test_concurrent_dgrad_wgrad_matches_serial(M, N_out, N_in):
+def test_concurrent_dgrad_wgrad_matches_serial(M, N_out, N_in, monkeypatch):
     """qwen2.dgrad_wgrad: the weight gradient on the side stream (workspace slot 1) while the input gradient runs on
     the current stream gives bit-identical results to the serial pair, repeated back to back (slots reused)."""
     from dots.rl_amd import qwen2
+
+    monkeypatch.setattr(qwen2, "CONCURRENT_WGRAD", True)
 
     g = torch.Generator(device="cuda").manual_seed(M + N_out)
     dy = torch.randn(M, N_out, device="cuda", generator=g).to(torch.bfloat16)
@@ -189,3 +191,27 @@ def test_concurrent_dgrad_wgrad_matches_serial(M, N_out, N_in):
     torch.cuda.synchronize()
     assert torch.equal(dx_s, dx_c)
     assert torch.equal(gw_s, gw_c)
+
+
+@pytest.mark.parametrize("M", [6144, 777, 24576])
+def test_dgrad_swiglu_bwd_epilogue_matches_unfused(M):
+    """The down_proj dgrad with the SwiGLU backward in its epilogue (dgu straight from the accumulators and the saved
+    gu) equals dgrad -> bf16 d a -> swiglu_bwd bit for bit (K = 896: both run whole tiles, one summation order)."""
+    I, H = 4864, 896
+    g = torch.Generator(device="cuda").manual_seed(M)
+    dm = torch.randn(M, H, generator=g, device="cuda").to(torch.bfloat16)
+    w = (torch.randn(H, I, generator=g, device="cuda") * 0.05).to(torch.bfloat16)
+    gu = (torch.randn(M, 2 * I, generator=g, device="cuda") * 2).to(torch.bfloat16)
+    da = native.linear_dgrad(dm, w)
+    want = torch.empty_like(gu)
+    native.swiglu_bwd(gu, da, want)
+    got = native.linear_dgrad_swiglu_bwd(dm, w, gu)
+    assert torch.equal(got, want)
+    # strided / ragged: a view of wider rows, I not a multiple of the tile
+    I2 = 4864 - 96
+    w2 = w[:, :I2].contiguous()
+    gu2 = torch.cat([gu[:, :I2], gu[:, I:I + I2]], 1)
+    da2 = native.linear_dgrad(dm, w2)
+    want2 = torch.empty_like(gu2)
+    native.swiglu_bwd(gu2, da2, want2)
+    assert torch.equal(native.linear_dgrad_swiglu_bwd(dm, w2, gu2), want2)

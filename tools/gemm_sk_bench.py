@@ -33,19 +33,23 @@ def bench(fn, iters=20, warmup=3, rounds=3):
     return best[len(best) // 2]
 
 
-def shapes(quick):
+def shapes(quick, rows=None, decode=None):
     H, I, NQ, V = 896, 4864, 1152, 151936
     out = []
-    for M in ((6144,) if quick else (6144, 12288)):
+    if decode:  # the decode step's projections at `decode` rows (one token per sequence)
+        M = decode
+        return [("dec_qkv", "fwd", M, NQ, H), ("dec_o", "fwd", M, H, H), ("dec_gate_up_swiglu", "swiglu", M, 2 * I, H),
+                ("dec_down", "fwd", M, H, I), ("dec_lm_head", "fwd", M, V, H)]
+    train = rows or [6144]
+    for M in sorted(set(train + ([] if quick else [12288]))):
         out += [("qkv_fwd", "fwd", M, NQ, H), ("o_fwd", "fwd", M, H, H), ("gate_up_fwd_swiglu", "swiglu", M, 2 * I, H),
                 ("down_fwd", "fwd", M, H, I)]
-        if M == 6144:
+        if M in train:
             out += [("qkv_dgrad", "dgrad", M, H, NQ), ("o_dgrad", "dgrad", M, H, H), ("gate_up_dgrad", "dgrad", M, H, 2 * I),
                     ("down_dgrad", "dgrad", M, I, H), ("qkv_wgrad", "wgrad", NQ, H, M), ("o_wgrad", "wgrad", H, H, M),
                     ("gate_up_wgrad", "wgrad", 2 * I, H, M), ("down_wgrad", "wgrad", H, I, M)]
-    out += [("lm_head_fwd", "fwd", 2048, V, H), ("lm_head_dgrad", "dgrad", 2048, H, V), ("lm_head_wgrad", "wgrad", V, H, 2048)]
-    if not quick:
-        out += [("lm_head_fwd_4096", "fwd", 4096, V, H)]
+    R = (max(train) // 768) * 256  # response rows of the pass (256 of every 768-token sequence)
+    out += [("lm_head_fwd", "fwd", R, V, H), ("lm_head_dgrad", "dgrad", R, H, V), ("lm_head_wgrad", "wgrad", V, H, R)]
     return out
 
 
@@ -53,14 +57,28 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--tune", action="store_true", help="also sweep grid / dp_mode / group of drl_gemm")
+    ap.add_argument("--rows", type=int, nargs="*", default=None, help="token rows of the training passes")
+    ap.add_argument("--no-lib", action="store_true", help="skip the hipBLASLt timing")
+    ap.add_argument("--decode", type=int, default=None, help="only the decode-step shapes at this many rows")
     args = ap.parse_args()
     from dots.rl_amd.workers import _enable_gemm_tuning
     _enable_gemm_tuning("auto")
     dev, bf = "cuda", torch.bfloat16
     g = torch.Generator(device=dev).manual_seed(0)
-    for name, kind, M, N, K in shapes(args.quick):
+    for name, kind, M, N, K in shapes(args.quick, args.rows, args.decode):
         fl = 2.0 * M * N * K
-        if kind in ("fwd", "swiglu"):
+        if kind in ("fwd", "swiglu") and args.decode:
+            # decode: weights rotate over > 600 MB of copies (each call streams W from HBM, as in the step)
+            x = torch.randn(M, K, generator=g, device=dev).to(bf)
+            nc = max(2, int(600e6 // (N * K * 2)) + 1)
+            ws = [(torch.randn(N, K, generator=g, device=dev) * 0.05).to(bf) for _ in range(nc)]
+            sw = kind == "swiglu"
+            a = torch.empty(M, N // 2, device=dev, dtype=bf)
+            ctr = iter(range(1 << 40))
+            ours = lambda: native.linear_fwd(x, ws[next(ctr) % nc], swiglu=sw)  # noqa: E731
+            lib = ((lambda: native.swiglu_fwd(x @ ws[next(ctr) % nc].t(), a)) if sw
+                   else (lambda: x @ ws[next(ctr) % nc].t()))  # noqa: E731
+        elif kind in ("fwd", "swiglu"):
             x = torch.randn(M, K, generator=g, device=dev).to(bf)
             w = (torch.randn(N, K, generator=g, device=dev) * 0.05).to(bf)
             sw = kind == "swiglu"
@@ -79,13 +97,13 @@ def main():
             ours = lambda: native.linear_wgrad(gw, dy, x)  # noqa: E731
             lib = lambda: torch.addmm(gw, dy.t(), x, out_dtype=torch.float32, out=gw)  # noqa: E731
         row = dict(shape=name, M=M, N=N, K=K)
-        t_lib = bench(lib)
+        t_lib = float("nan") if args.no_lib else bench(lib)
         t_ours = bench(ours)
         row.update(hipblaslt_us=t_lib, hipblaslt_TF=fl / t_lib / 1e6, ours_us=t_ours, ours_TF=fl / t_ours / 1e6)
         if args.tune:
             sweep = {}
-            for grid, mode, param in [(0, 1, 0), (192, 1, 0), (0, 2, 0), (0, 3, 0), (0, 3, 2), (0, 3, 4), (0, 3, 8),
-                                      (0, 3, 16), (192, 3, 0)]:
+            for grid, mode, param in [(0, 1, 0), (0, 1, 8), (0, 1, 32), (0, 2, 0), (0, 3, 2), (0, 3, 4), (0, 3, 8),
+                                      (0, 3, 16)]:
                 if mode == 3 and param and param * (M + 255) // 256 * ((N + 255) // 256) > 256:
                     continue
                 native.lib().drl_gemm_set_sk_tuning(grid, 0, mode, param)

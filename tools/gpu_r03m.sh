@@ -1,0 +1,8 @@
+#!/bin/bash
+# Full GPU suite + bench after the SwiGLU changes (hardware exp2 / rcp; the backward fused into the down dgrad).
+set -o pipefail
+OUT=gpurun_out/r03m; mkdir -p $OUT
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/gputests.log 2>&1; rc=$?; tail -4 $OUT/gputests.log; [ $rc = 0 ] || { grep -E "FAIL|Error|assert" $OUT/gputests.log | head -30; exit 1; }
+summ() { grep '^{' $1 | python -c "import json,sys; d=json.loads(sys.stdin.read()); t=d['timing_s']; print('$2', round(d['value'],4), 'gen', round(t['gen'],3), 'logp', round(t['old_log_prob'],3), 'upd', round(t['update_actor'],3), 'step', round(t['step'],3))"; }
+timeout -k 10 400 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --roofline-kernel drl_flash_attn_fwd > $OUT/bench.log 2>&1 || { tail -30 $OUT/bench.log; exit 1; }
+summ $OUT/bench.log after
