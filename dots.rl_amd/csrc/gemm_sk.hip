@@ -67,6 +67,8 @@ struct SkArgs {
   int n_tiles;
   int beta;            // EPI_F32: 1 = C += acc
   int splits;          // > 1: uniform split-K, workgroup wg = split (wg % splits) of tile (wg / splits)
+  int dbg;             // measurement only (drl_gemm_set_debug): 1 = whole tiles skip their epilogue, 2 = the plain
+                       // bf16 epilogue stages but does not store
 };
 
 __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
@@ -283,7 +285,9 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
             for (int kb = 0; kb < 2; ++kb) {
               const u16x8 fa = AT ? join(at[i][kb][0], at[i][kb][1]) : af[i][kb];
               const u16x8 fb = BT ? join(bt[qn][j][kb][0], bt[qn][j][kb][1]) : bq[qn][j][kb];
-              acc[qm][qn][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(fa), as_bf16x8(fb),
+              // operands swapped: the 16 x 16 block is accumulated transposed, so lane (fq, fr) holds output row
+              // fr, columns 4 fq .. 4 fq + 3 — the epilogue stores straight from registers
+              acc[qm][qn][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(fb), as_bf16x8(fa),
                                                                           acc[qm][qn][i][j], 0, 0, 0);
             }
         __builtin_amdgcn_s_setprio(0);
@@ -296,13 +300,22 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
   (void)NB_READS;
 
   // ------------------------------------------------------------------------------------------ epilogues
-  // accumulator block (i, j) of quadrant (qm, qn): tile row qm * 128 + wr * 64 + i * 16 + 4 fq + r, tile column
-  // wc * 64 + qn * 32 + j * 16 + fr (SwiGLU: output column wc * 32 + qn * 16 + fr, j = 0 gate, 1 up)
+  // accumulator block (i, j) of quadrant (qm, qn), transposed (the MFMA's operands are swapped): lane (fq, fr) holds
+  // tile row qm * 128 + wr * 64 + i * 16 + fr, tile columns wc * 64 + qn * 32 + j * 16 + 4 fq + (0..3) (SwiGLU: output
+  // columns wc * 32 + qn * 16 + 4 fq + (0..3), j = 0 gate, 1 up). Staged through LDS as one 8-B (bf16) / 16-B (fp32)
+  // write per block and lane — a quarter of the 2-byte writes the untransposed layout needs (that staging cost
+  // 3.7 us per 256 x 256 tile, profiles/r03_gemm_fixed_cost.jsonl) — then read back as 16-B row pieces for coalesced
+  // 128-B row stores (storing the 8-B pieces straight from the registers, 16 rows x 32 B per wave instruction,
+  // measured 3x slower).
   auto epilogue = [&](int m0, int n0) {
     bar();  // every fragment read retired and every copy drained: LDS is free for staging
+    if (g.dbg & 4) {  // measurement: the epilogue's two barriers only
+      bar();
+      return;
+    }
     if constexpr (EPI == EPI_F32) {
-      // through LDS per quadrant: the wave's 64 x 32 fp32 block (row stride 36 floats), read back as 16-B row pieces
-      // (8 lanes per 128-B row) for a coalesced read-modify-write of the fp32 output
+      // per quadrant: the wave's 64 x 32 fp32 block (row stride 36 floats), read back as 16-B row pieces (8 lanes per
+      // 128-B row) for a coalesced read-modify-write of the fp32 output
       constexpr int SLD = 36;
       float* st = reinterpret_cast<float*>(lds) + wave * 64 * SLD;
       const int ch = lane & 7;
@@ -315,8 +328,7 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
           for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int i = 0; i < 4; ++i)
-#pragma unroll
-              for (int r = 0; r < 4; ++r) st[(i * 16 + 4 * fq + r) * SLD + j * 16 + fr] = acc[qm][qn][i][j][r];
+              *reinterpret_cast<f32x4*>(st + (i * 16 + fr) * SLD + j * 16 + 4 * fq) = acc[qm][qn][i][j];
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
           const int col = n0 + wc * 64 + qn * 32 + 4 * ch;
 #pragma unroll
@@ -345,17 +357,22 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
 #pragma unroll
         for (int qn = 0; qn < 2; ++qn)
 #pragma unroll
-          for (int i = 0; i < 4; ++i)
+          for (int i = 0; i < 4; ++i) {
+            const int o = (i * 16 + fr) * SLD + qn * 16 + 4 * fq;
+            u16x4 a4, g4, u4;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              const int o = (i * 16 + fq * 4 + r) * SLD + qn * 16 + fr;
               const float gg = bf16r(acc[qm][qn][i][0][r]), uu = bf16r(acc[qm][qn][i][1][r]);
-              st[o] = to_bf16_bits(bf16r(silu_fast(gg)) * uu);
-              if (g.c2) {
-                st[REG + o] = to_bf16_bits(gg);
-                st[2 * REG + o] = to_bf16_bits(uu);
-              }
+              a4[r] = to_bf16_bits(bf16r(silu_fast(gg)) * uu);
+              g4[r] = to_bf16_bits(gg);
+              u4[r] = to_bf16_bits(uu);
             }
+            *reinterpret_cast<u16x4*>(st + o) = a4;
+            if (g.c2) {
+              *reinterpret_cast<u16x4*>(st + REG + o) = g4;
+              *reinterpret_cast<u16x4*>(st + 2 * REG + o) = u4;
+            }
+          }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
         for (int it = 0; it < 4; ++it) {
@@ -402,13 +419,19 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
         for (int qn = 0; qn < 2; ++qn)
 #pragma unroll
           for (int j = 0; j < 2; ++j) {
-            const int lc = qn * 32 + j * 16 + fr;
-            const float bv = EPI == EPI_BIAS ? bf16_to_f32(g.bias[min(n0 + wc * 64 + lc, g.N - 1)]) : 0.f;
+            const int lc = qn * 32 + j * 16 + 4 * fq;
+            float bb[4] = {0.f, 0.f, 0.f, 0.f};
+            if constexpr (EPI == EPI_BIAS) {
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
+              for (int e = 0; e < 4; ++e) bb[e] = bf16_to_f32(g.bias[min(n0 + wc * 64 + lc + e, g.N - 1)]);
+            }
 #pragma unroll
-              for (int r = 0; r < 4; ++r)
-                st[(i * 16 + fq * 4 + r) * SLD + lc] = to_bf16_bits(acc[qm][qn][i][j][r] + bv);
+            for (int i = 0; i < 4; ++i) {
+              u16x4 w4;
+#pragma unroll
+              for (int e = 0; e < 4; ++e) w4[e] = to_bf16_bits(acc[qm][qn][i][j][e] + bb[e]);
+              *reinterpret_cast<u16x4*>(st + (i * 16 + fr) * SLD + lc) = w4;
+            }
           }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
@@ -449,6 +472,8 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
                 dstp[g.N + e] = du[e];
               }
             }
+          } else if (g.dbg & 2) {  // measurement: staging without the output stores
+            if (v[0] == 0x7fffu && v[1] == 0x1234u) dstp[0] = 0;
           } else if (vec) {
             *reinterpret_cast<u16x8*>(dstp) = v;
           } else {
@@ -529,17 +554,18 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
             f32x4 v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rws, vt, reg * 8192, 16));
             for (int s2 = 1; s2 < S; ++s2)
               v += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rws, vt + s2 * SLAB * 4, reg * 8192, 16));
-            const int col = n0 + wc * 64 + b * 32 + j * 16 + fr;
-            if (col >= g.N) continue;
-            const float bv = EPI == EPI_BIAS ? bf16_to_f32(g.bias[col]) : 0.f;
+            // transposed block (see the epilogue): row fr, columns 4 fq + r
+            const int m = m0 + a * 128 + wr * 64 + i * 16 + fr;
+            if (m >= g.M) continue;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              const int m = m0 + a * 128 + wr * 64 + i * 16 + 4 * fq + r;
-              if (m >= g.M) continue;
+              const int col = n0 + wc * 64 + b * 32 + j * 16 + 4 * fq + r;
+              if (col >= g.N) continue;
               if constexpr (EPI == EPI_F32) {
                 float* p = g.c32 + static_cast<int64_t>(m) * g.ldc + col;
                 *p = g.beta ? *p + v[r] : v[r];
-              } else if constexpr (EPI != EPI_SWIGLU) {
+              } else if constexpr (EPI != EPI_SWIGLU && EPI != EPI_SWIGLU_BWD) {
+                const float bv = EPI == EPI_BIAS ? bf16_to_f32(g.bias[col]) : 0.f;
                 g.c[static_cast<int64_t>(m) * g.ldc + col] = to_bf16_bits(v[r] + bv);
               }
             }
@@ -560,7 +586,7 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
     tile_origin(t, m0, n0);
     setup_tile(m0, n0);
     run(0, g.P);
-    epilogue(m0, n0);
+    if (!(g.dbg & 1)) epilogue(m0, n0);
   }
 
   // ------------------------------------------------------------------------------------------ stream-K region
@@ -660,6 +686,7 @@ struct SkTuning {
   int param = 0;     // mode 1: minimum k-pairs per workgroup; mode 3: splits per tile (0 automatic)
 };
 SkTuning g_sk;
+int g_sk_dbg = 0;
 
 template <int AT, int BT>
 int launch_sk_layout(SkArgs& g, int epi, int grid, hipStream_t s) {
@@ -691,6 +718,8 @@ int64_t drl_gemm_workspace_bytes(void) {
   if (cus <= 0) return -1;
   return static_cast<int64_t>(cus) * drl::SLAB * 4 + static_cast<int64_t>(cus + 1) * 4 + 256;
 }
+
+void drl_gemm_set_debug(int32_t flags) { drl::g_sk_dbg = flags; }
 
 void drl_gemm_set_sk_tuning(int32_t grid, int32_t group, int32_t mode, int32_t param) {
   drl::g_sk.grid = grid > 0 ? grid : 0;
@@ -785,6 +814,7 @@ int drl_gemm(const void* a, int64_t lda, int32_t a_layout, const void* b, int64_
   g.b_bytes = static_cast<uint32_t>(b_bytes);
   g.M = static_cast<int>(M); g.N = static_cast<int>(N); g.K = static_cast<int>(K);
   g.beta = beta ? 1 : 0;
+  g.dbg = g_sk_dbg;
   g.tm = static_cast<int>((M + 255) / 256);
   g.tn = static_cast<int>((N + 255) / 256);
   g.gm = g_sk.group;

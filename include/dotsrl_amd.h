@@ -593,6 +593,9 @@ int64_t drl_gemm_workspace_bytes(void);
  * rounds while they fill the grid, stream-K for the last one or two; 1 = all stream-K; 2 = whole tiles only),
  * min_iters (minimum k-tile pairs per workgroup of an all-stream-K grid, 0 = 2). Schedule only, same result. */
 void drl_gemm_set_sk_tuning(int32_t grid, int32_t group, int32_t dp_mode, int32_t min_iters);
+/* Measurement hook (never set in the product path): 1 = whole tiles skip their epilogue (no output written), to time
+ * the main loop and the per-tile fixed cost apart; 0 = normal. */
+void drl_gemm_set_debug(int32_t flags);
 
 
 /* Row gather / scatter of the remove-padding passes (flash_attn.bert_padding unpad_input / pad_input /

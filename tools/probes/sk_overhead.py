@@ -13,12 +13,19 @@ from dots.rl_amd import native  # noqa: E402
 
 bf = torch.bfloat16
 for M, N in ((24576, 9728), (24576, 896), (61440, 9728)):
-    for K in (896, 1792, 3584):
+    for K in (896,):
         x = torch.randn(M, K, device="cuda", dtype=bf)
         w = torch.randn(N, K, device="cuda", dtype=bf) * 0.05
         b = torch.randn(N, device="cuda", dtype=bf)
         row = dict(M=M, N=N, K=K)
         row["plain_us"] = round(bench(lambda: native.linear_fwd(x, w)), 1)
+        native.lib().drl_gemm_set_debug(1)
+        row["no_epilogue_us"] = round(bench(lambda: native.linear_fwd(x, w)), 1)
+        native.lib().drl_gemm_set_debug(4)
+        row["barriers_only_us"] = round(bench(lambda: native.linear_fwd(x, w)), 1)
+        native.lib().drl_gemm_set_debug(2)
+        row["stage_no_store_us"] = round(bench(lambda: native.linear_fwd(x, w)), 1)
+        native.lib().drl_gemm_set_debug(0)
         row["bias_us"] = round(bench(lambda: native.linear_fwd(x, w, bias=b)), 1)
         if N % 64 == 0 and N > 1000:
             row["swiglu_us"] = round(bench(lambda: native.linear_fwd(x, w, swiglu=True)), 1)
