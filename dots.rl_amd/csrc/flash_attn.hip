@@ -40,6 +40,22 @@ struct FlashArgs {
 
 __device__ __forceinline__ bf16x8 as_bf16x8(u16x8 v) { return __builtin_bit_cast(bf16x8, v); }
 
+// lane i and lane i ^ 32 combined on both (one v_permlane32_swap, no LDS round trip): swapping the upper half
+// of one copy of x with the lower half of another leaves, on every lane, the lower half's value in the first
+// and the upper half's in the second, so both lanes of a pair see the same operands in the same order. Inline
+// asm: the builtin's two results are folded into one by this compiler (measured: the max vanished), and the
+// s_nops cover the VALU -> permlane -> VALU wait states.
+__device__ __forceinline__ float pair_max(float x) {
+  float lo = x, hi = x;
+  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1\n\ts_nop 1\n\tv_max_f32 %0, %0, %1" : "+v"(lo), "+v"(hi));
+  return lo;
+}
+__device__ __forceinline__ float pair_sum(float x) {
+  float lo = x, hi = x;
+  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1\n\ts_nop 1\n\tv_add_f32 %0, %0, %1" : "+v"(lo), "+v"(hi));
+  return lo;
+}
+
 // XCD-aware tile order (cdna_hip_programming.md §5.5 T1): workgroups are dealt round-robin to the 8 XCDs,
 // each with its own L2. Remap the linear workgroup id so that all tiles of one (sequence, KV head) land on
 // the same XCD (its K / V stay in that L2) and, within an XCD, run in tile order. Returns (tile, bh).
@@ -96,11 +112,13 @@ __device__ __forceinline__ uint32_t pk_bf16(float lo, float hi) {
 
 // K / V tiles of one 32-key block staged in LDS and shared by the G waves of the workgroup.
 // K: [32 keys][D] rows of D*2 + 16 bytes (16-B aligned, conflict-free ds_read_b128 of a key row slice);
-// V^T: [D][32 keys] rows of 72 bytes (conflict-free ds_read_b64 of 4 keys of one head-dim row).
+// V^T: [D][32 keys] rows of 80 bytes, keys permuted within each 16-key group as 0-3, 8-11, 4-7, 12-15 so that
+// the 8 keys one lane half needs for a k-step of O^T += V^T P^T (16s + 4h + {0..3, 8..11}) are one
+// conflict-free ds_read_b128 (80-B rows: 16 consecutive rows cover all 64 banks).
 template <int D>
 struct KVTile {
   static constexpr int KROW = D + 8;   // u16 per K row
-  static constexpr int VROW = 36;      // u16 per V^T row
+  static constexpr int VROW = 40;      // u16 per V^T row
   static constexpr int KSZ = 32 * KROW, VSZ = D * VROW;
   static constexpr int NCH = (32 * D + D * 32) * 2 / 16;  // 16-B chunks per block
   static constexpr int CPT = NCH / 512;                   // chunks per thread (512-thread workgroups)
@@ -108,6 +126,25 @@ struct KVTile {
 
 // global -> registers: chunk c < 32*D/8 is K row c / (D/8), 16-B column c % (D/8); the rest V^T row
 // d = c' / 4, 16-B column c' % 4 (keys 8*col .. 8*col+7). Keys >= Tk load as zero.
+// the same for a block wholly below Tk (the caller's test is on k0 alone, so it is uniform over the
+// workgroup): no per-key bounds tests in the steady-state key loop
+template <int D>
+__device__ __forceinline__ void kv_issue_full(const uint16_t* kbase, const uint16_t* vtbase, int64_t ld_vt,
+                                              int64_t k0, int tid, u16x8 (&r)[KVTile<D>::CPT]) {
+  constexpr int KCH = 32 * D / 8;
+#pragma unroll
+  for (int i = 0; i < KVTile<D>::CPT; ++i) {
+    const int c = tid + 512 * i;
+    if (c < KCH) {
+      const int row = c / (D / 8), col = c % (D / 8);
+      r[i] = *reinterpret_cast<const u16x8*>(kbase + (k0 + row) * D + col * 8);
+    } else {
+      const int cc = c - KCH, d = cc / 4, col = cc % 4;
+      r[i] = *reinterpret_cast<const u16x8*>(vtbase + static_cast<int64_t>(d) * ld_vt + k0 + col * 8);
+    }
+  }
+}
+
 template <int D>
 __device__ __forceinline__ void kv_issue(const uint16_t* kbase, const uint16_t* vtbase, int64_t ld_vt, int64_t k0,
                                          int64_t Tk, int tid, u16x8 (&r)[KVTile<D>::CPT]) {
@@ -147,9 +184,10 @@ __device__ __forceinline__ void kv_store(uint16_t* kl, uint16_t* vl, int tid, co
       *reinterpret_cast<u16x8*>(kl + row * KVTile<D>::KROW + col * 8) = r[i];
     } else {
       const int cc = c - KCH, d = cc / 4, col = cc % 4;
-      uint16_t* dst = vl + d * KVTile<D>::VROW + col * 8;  // 8-B aligned: two 8-B stores
+      // keys 8col .. 8col+3 and 8col+4 .. 8col+7 to their permuted places (KVTile): two 8-B stores
+      uint16_t* dst = vl + d * KVTile<D>::VROW + (col >> 1) * 16 + (col & 1) * 4;
       *reinterpret_cast<u16x4*>(dst) = u16x4{r[i][0], r[i][1], r[i][2], r[i][3]};
-      *reinterpret_cast<u16x4*>(dst + 4) = u16x4{r[i][4], r[i][5], r[i][6], r[i][7]};
+      *reinterpret_cast<u16x4*>(dst + 8) = u16x4{r[i][4], r[i][5], r[i][6], r[i][7]};
     }
   }
 }
@@ -249,7 +287,7 @@ __global__ __launch_bounds__(512, D == 64 ? 4 : 1) void flash_fwd_kernel(FlashAr
     }
 #pragma unroll
     for (int r = 0; r < 16; ++r) mxr = fmaxf(mxr, st[r]);
-    mxr = fmaxf(mxr, __shfl_xor(mxr, 32, kWave));
+    mxr = pair_max(mxr);
     const float mx = mxr * a.scale_log2;
     // deferred rescale: the reference max moves only when the block's max exceeds it by more than 8 (log2
     // units), so p <= 2^8 and most blocks skip the O^T rescale; the final O / l and LSE are exact either way
@@ -278,12 +316,10 @@ __global__ __launch_bounds__(512, D == 64 ? 4 : 1) void flash_fwd_kernel(FlashAr
     // ---- O^T += V^T P^T; k-step s: element j of lane half h is key k0 + 16s + 8(j>>2) + 4h + (j&3)
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
-      const uint16_t* vtl = lds_v[cur][sl] + (32 * mt + qi) * TL::VROW + 4 * h;
+      const uint16_t* vtl = lds_v[cur][sl] + (32 * mt + qi) * TL::VROW + 8 * h;
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        const u16x4 lo = *reinterpret_cast<const u16x4*>(vtl + 16 * s);
-        const u16x4 hi = *reinterpret_cast<const u16x4*>(vtl + 16 * s + 8);
-        const u16x8 vv = u16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        const u16x8 vv = *reinterpret_cast<const u16x8*>(vtl + 16 * s);
         o[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(vv), as_bf16x8(pb[s]), o[mt], 0, 0, 0);
       }
     }
@@ -307,8 +343,14 @@ __global__ __launch_bounds__(512, D == 64 ? 4 : 1) void flash_fwd_kernel(FlashAr
 #pragma unroll
     for (int sl = 0; sl < 2; ++sl)
       if (ib + 2 + sl < nb) {
-        kv_issue<D>(kbase, vtbase, a.ld_vt, (ib + 2 + sl) * 32, a.Tk, tid, stage[sl]);
-        vst[sl] = valid_issue(vrow, (ib + 2 + sl) * 32, a.Tk, tid);
+        const int64_t k0 = (ib + 2 + sl) * 32;
+        if (k0 + 32 <= a.Tk) {
+          kv_issue_full<D>(kbase, vtbase, a.ld_vt, k0, tid, stage[sl]);
+          if (tid < 8) vst[sl] = *reinterpret_cast<const uint32_t*>(vrow + k0 + 4 * tid);
+        } else {
+          kv_issue<D>(kbase, vtbase, a.ld_vt, k0, a.Tk, tid, stage[sl]);
+          vst[sl] = valid_issue(vrow, k0, a.Tk, tid);
+        }
       }
     if (computes) {
       block(cur, 0, ib * 32);
@@ -323,7 +365,7 @@ __global__ __launch_bounds__(512, D == 64 ? 4 : 1) void flash_fwd_kernel(FlashAr
     __syncthreads();
   }
   // ---- finalize: O^T register r of tile mt = head-dim row 32mt + (r & 3) + 8(r >> 2) + 4h of query tq
-  const float lt = lsum + __shfl_xor(lsum, 32, kWave);
+  const float lt = pair_sum(lsum);
   const float inv = lt > 0.f ? 1.f / lt : 0.f;
   if (!qvalid) return;
   uint16_t* orow = a.out + (((b * a.Tq + tq) * a.Hkv + (bh % a.Hkv)) * a.G + g) * D;
@@ -373,10 +415,11 @@ __device__ __forceinline__ float bf2f(uint16_t x) { return bf16_to_f32(x); }
 
 
 // dq_kernel's per-key-block tiles in LDS, shared by the G waves (query heads) of the workgroup:
-// K and V row-major [32 keys][D] (rows padded to D + 8 elements) and K^T [D][32 keys] (rows of 36).
+// K and V row-major [32 keys][D] (rows padded to D + 8 elements) and K^T [D][32 keys] (rows of 40, keys
+// permuted within each 16-key group as in KVTile's V^T: one ds_read_b128 per k-step of dQ^T += K^T dS^T).
 template <int D>
 struct DqTile {
-  static constexpr int ROW = D + 8, TROW = 36;
+  static constexpr int ROW = D + 8, TROW = 40;
   static constexpr int RSZ = 32 * ROW, TSZ = D * TROW;
   static constexpr int RCH = 32 * D / 8;        // 16-B chunks of one row-major tile
   static constexpr int NCH = 2 * RCH + D * 4;   // K, V, K^T
@@ -411,6 +454,26 @@ __device__ __forceinline__ void dq_issue(const uint16_t* kb, const uint16_t* vb,
   }
 }
 
+// dq_issue for a block wholly below T (uniform test on k0 by the caller): no per-key bounds tests
+template <int D>
+__device__ __forceinline__ void dq_issue_full(const uint16_t* kb, const uint16_t* vb, const uint16_t* ktb,
+                                              int64_t ld_t, int k0, int tid, u16x8 (&r)[DqTile<D>::CPT]) {
+  using TL = DqTile<D>;
+#pragma unroll
+  for (int i = 0; i < TL::CPT; ++i) {
+    const int c = tid + 512 * i;
+    u16x8 v = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    if (c < 2 * TL::RCH) {
+      const int cc = c % TL::RCH, row = cc / (D / 8), col = cc % (D / 8);
+      v = *reinterpret_cast<const u16x8*>((c < TL::RCH ? kb : vb) + static_cast<int64_t>(k0 + row) * D + col * 8);
+    } else if (c < TL::NCH) {
+      const int cc = c - 2 * TL::RCH, d = cc / 4, col = cc % 4;
+      v = *reinterpret_cast<const u16x8*>(ktb + static_cast<int64_t>(d) * ld_t + k0 + col * 8);
+    }
+    r[i] = v;
+  }
+}
+
 template <int D>
 __device__ __forceinline__ void dq_store(uint16_t* kl, uint16_t* vl, uint16_t* ktl, int tid,
                                          const u16x8 (&r)[DqTile<D>::CPT]) {
@@ -423,9 +486,9 @@ __device__ __forceinline__ void dq_store(uint16_t* kl, uint16_t* vl, uint16_t* k
       *reinterpret_cast<u16x8*>((c < TL::RCH ? kl : vl) + row * TL::ROW + col * 8) = r[i];
     } else if (c < TL::NCH) {
       const int cc = c - 2 * TL::RCH, d = cc / 4, col = cc % 4;
-      uint16_t* dst = ktl + d * TL::TROW + col * 8;
+      uint16_t* dst = ktl + d * TL::TROW + (col >> 1) * 16 + (col & 1) * 4;  // permuted (DqTile)
       *reinterpret_cast<u16x4*>(dst) = u16x4{r[i][0], r[i][1], r[i][2], r[i][3]};
-      *reinterpret_cast<u16x4*>(dst + 4) = u16x4{r[i][4], r[i][5], r[i][6], r[i][7]};
+      *reinterpret_cast<u16x4*>(dst + 8) = u16x4{r[i][4], r[i][5], r[i][6], r[i][7]};
     }
   }
 }
@@ -469,7 +532,7 @@ __global__ __launch_bounds__(512) void flash_dq_kernel(FlashBwdArgs a) {
       dof[s] = as_bf16x8(dv);
     }
   }
-  dl += __shfl_xor(dl, 32, kWave);  // delta = rowsum(dO * O) of query tq
+  dl = pair_sum(dl);  // delta = rowsum(dO * O) of query tq
   if (qvalid && h == 0) a.delta[head * T + tq] = dl;
   const float lse2 = qvalid ? a.lse[head * T + tq] * 1.4426950408889634f : -INFINITY;
   const float lref = lse2 == -INFINITY ? INFINITY : lse2;  // exp2(x - inf) = 0 for rows with no allowed key
@@ -490,8 +553,13 @@ __global__ __launch_bounds__(512) void flash_dq_kernel(FlashBwdArgs a) {
   for (int ib = 0; ib < nb; ++ib) {
     const int cur = ib & 1, k0 = ib * 32;
     if (ib + 1 < nb) {
-      dq_issue<D>(kbase, vbase, ktbase, a.ld_t, k0 + 32, T, tid, stage);
-      vst = valid_issue(vrow, k0 + 32, T, tid);
+      if (k0 + 64 <= T) {
+        dq_issue_full<D>(kbase, vbase, ktbase, a.ld_t, k0 + 32, tid, stage);
+        if (tid < 8) vst = *reinterpret_cast<const uint32_t*>(vrow + k0 + 32 + 4 * tid);
+      } else {
+        dq_issue<D>(kbase, vbase, ktbase, a.ld_t, k0 + 32, T, tid, stage);
+        vst = valid_issue(vrow, k0 + 32, T, tid);
+      }
     }
     if (computes) {
       f32x16 st = f32x16{}, dpt = f32x16{};
@@ -514,24 +582,30 @@ __global__ __launch_bounds__(512) void flash_dq_kernel(FlashBwdArgs a) {
       }
       const bool full = __all(allv) && k0 + 31 <= t0;
       u16x8 dsb[2];
+      if (full) {  // uniform: the unmasked form (a full block's rows all have an allowed key: lref finite)
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int r = 4 * c + j;
-          const bool ok = full || (((vw[c] >> (8 * j)) & 0xffu) != 0u && kbase0 + 8 * c + j <= tq);
-          const float p = ok ? __builtin_amdgcn_exp2f(st[r] * a.scale_log2 - lref) : 0.f;
+        for (int r = 0; r < 16; ++r) {
+          const float p = __builtin_amdgcn_exp2f(fmaf(st[r], a.scale_log2, -lref));
           dsb[r >> 3][r & 7] = to_bf16_bits(p * (dpt[r] - dl));
+        }
+      } else {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int r = 4 * c + j;
+            const bool ok = ((vw[c] >> (8 * j)) & 0xffu) != 0u && kbase0 + 8 * c + j <= tq;
+            const float p = ok ? __builtin_amdgcn_exp2f(fmaf(st[r], a.scale_log2, -lref)) : 0.f;
+            dsb[r >> 3][r & 7] = to_bf16_bits(p * (dpt[r] - dl));
+          }
         }
       }
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
-        const uint16_t* ktl = lds_kt[cur] + (32 * mt + qi) * TL::TROW + 4 * h;
+        const uint16_t* ktl = lds_kt[cur] + (32 * mt + qi) * TL::TROW + 8 * h;
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
-          const u16x4 lo = *reinterpret_cast<const u16x4*>(ktl + 16 * s);
-          const u16x4 hi = *reinterpret_cast<const u16x4*>(ktl + 16 * s + 8);
-          const u16x8 kv = u16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          const u16x8 kv = *reinterpret_cast<const u16x8*>(ktl + 16 * s);
           dqt[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(kv), as_bf16x8(dsb[s]), dqt[mt], 0, 0, 0);
         }
       }
@@ -552,6 +626,20 @@ __global__ __launch_bounds__(512) void flash_dq_kernel(FlashBwdArgs a) {
                             to_bf16_bits(dqt[mt][4 * c + 2] * a.scale), to_bf16_bits(dqt[mt][4 * c + 3] * a.scale)};
       *reinterpret_cast<u16x4*>(dqrow + 32 * mt + 8 * c + 4 * h) = w;
     }
+  }
+}
+
+// dkdv_rows for a tile wholly below T (uniform test by the caller): no per-row range selects
+template <int D>
+__device__ __forceinline__ void dkdv_rows_full(const uint16_t* qbase, const uint16_t* dout, int64_t b, int64_t hkv,
+                                               int64_t Hkv, int64_t G, int g, int T, int tr, int h,
+                                               u16x8 (&qa)[D / 16], u16x8 (&da)[D / 16]) {
+  const uint16_t* qrow = qbase + static_cast<int64_t>(tr) * D + 8 * h;
+  const uint16_t* dorow = dout + (((b * T + tr) * Hkv + hkv) * G + g) * D + 8 * h;
+#pragma unroll
+  for (int s = 0; s < D / 16; ++s) {
+    qa[s] = *reinterpret_cast<const u16x8*>(qrow + 16 * s);
+    da[s] = *reinterpret_cast<const u16x8*>(dorow + 16 * s);
   }
 }
 
@@ -632,16 +720,18 @@ __global__ __launch_bounds__(64 * NW) void flash_dkdv_kernel(FlashBwdArgs a) {
       *reinterpret_cast<u16x8*>(xd + ximg_off<XROW>(li, 16 * s + 8 * h)) = da[s];
     }
     float4 l4[4], d4[4];
+    const bool rows_in = t0 + 32 <= T;  // uniform
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       const int qb = t0 + 8 * c + 4 * h;
-      if (qb + 3 < T) {
+      if (rows_in) {
         l4[c] = *reinterpret_cast<const float4*>(lser + qb);
         d4[c] = *reinterpret_cast<const float4*>(dlr + qb);
       } else {
         l4[c] = make_float4(qb < T ? lser[qb] : -INFINITY, qb + 1 < T ? lser[qb + 1] : -INFINITY,
-                            qb + 2 < T ? lser[qb + 2] : -INFINITY, -INFINITY);
-        d4[c] = make_float4(qb < T ? dlr[qb] : 0.f, qb + 1 < T ? dlr[qb + 1] : 0.f, qb + 2 < T ? dlr[qb + 2] : 0.f, 0.f);
+                            qb + 2 < T ? lser[qb + 2] : -INFINITY, qb + 3 < T ? lser[qb + 3] : -INFINITY);
+        d4[c] = make_float4(qb < T ? dlr[qb] : 0.f, qb + 1 < T ? dlr[qb + 1] : 0.f, qb + 2 < T ? dlr[qb + 2] : 0.f,
+                            qb + 3 < T ? dlr[qb + 3] : 0.f);
       }
     }
     // S = Q K^T and dP = dO V^T: A = rows of query t0 + li; C row r -> query t0 + (r&3) + 8(r>>2) + 4h
@@ -653,10 +743,27 @@ __global__ __launch_bounds__(64 * NW) void flash_dkdv_kernel(FlashBwdArgs a) {
       sc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(qa[s]), as_bf16x8(kv), sc, 0, 0, 0);
       dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(da[s]), as_bf16x8(vv), dp, 0, 0, 0);
     }
-    if (t0 + 32 < T) dkdv_rows<D>(qbase, a.dout, b, hkv, a.Hkv, a.G, g, T, t0 + 32 + li, h, qa, da);  // next tile
+    if (t0 + 64 <= T) dkdv_rows_full<D>(qbase, a.dout, b, hkv, a.Hkv, a.G, g, T, t0 + 32 + li, h, qa, da);
+    else if (t0 + 32 < T) dkdv_rows<D>(qbase, a.dout, b, hkv, a.Hkv, a.G, g, T, t0 + 32 + li, h, qa, da);  // next tile
     u16x8 pb[2], dsb[2];
-    // block entirely at or below the diagonal, all keys valid, all queries in range: no mask
-    const bool full = __all(kval) && t0 >= k0 + 31 && t0 + 32 <= T;
+    // block entirely at or below the diagonal, all keys valid, all queries in range: no mask, and every query
+    // row has an allowed key (finite LSE)
+    const bool full = __all(kval) && t0 >= k0 + 31 && rows_in;
+    if (full) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float nl[4] = {-l4[c].x * 1.4426950408889634f, -l4[c].y * 1.4426950408889634f,
+                             -l4[c].z * 1.4426950408889634f, -l4[c].w * 1.4426950408889634f};
+        const float dv4[4] = {d4[c].x, d4[c].y, d4[c].z, d4[c].w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int r = 4 * c + j;
+          const float p = __builtin_amdgcn_exp2f(fmaf(sc[r], a.scale_log2, nl[j]));
+          pb[r >> 3][r & 7] = to_bf16_bits(p);
+          dsb[r >> 3][r & 7] = to_bf16_bits(p * (dp[r] - dv4[j]));
+        }
+      }
+    } else {
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       const int qb = t0 + 8 * c + 4 * h;
@@ -665,11 +772,12 @@ __global__ __launch_bounds__(64 * NW) void flash_dkdv_kernel(FlashBwdArgs a) {
       for (int j = 0; j < 4; ++j) {
         const int r = 4 * c + j;
         const float l2 = lv[j] == -INFINITY ? INFINITY : lv[j] * 1.4426950408889634f;  // no allowed key: p = 0
-        const bool ok = full || (kval && key <= qb + j);
-        const float p = ok ? __builtin_amdgcn_exp2f(sc[r] * a.scale_log2 - l2) : 0.f;
+        const bool ok = kval && key <= qb + j;
+        const float p = ok ? __builtin_amdgcn_exp2f(fmaf(sc[r], a.scale_log2, -l2)) : 0.f;
         pb[r >> 3][r & 7] = to_bf16_bits(p);
         dsb[r >> 3][r & 7] = to_bf16_bits(p * (dp[r] - dv4[j]));
       }
+    }
     }
     // dV^T += dO^T P and dK^T += Q^T dS: A operands read transposed from the wave's Q / dO image
 #pragma unroll
