@@ -74,8 +74,8 @@ DEFAULTS = dict(
             # micro-batches run through the model together (one forward / backward over their concatenated rows; the
             # loss, its scale and the metrics stay per micro-batch): 0 = as many as fit exec_activation_gb of saved
             # activations, 1 = the reference's one micro-batch per pass (dp_actor.DataParallelPPOActor.update_policy)
-            exec_micro_batches=0, exec_activation_gb=40,
-            exec_log_prob_tokens=65536,  # forward-only log-prob passes: micro-batches per pass up to this many tokens
+            exec_micro_batches=0, exec_activation_gb=110,
+            exec_log_prob_tokens=196608,  # forward-only log-prob passes: micro-batches per pass up to this many tokens
             # shard: fp32 master + AdamW moments split over the DP ranks (ZeRO-style; FSDP FULL_SHARD in the
             # reference); "auto" = when replicated state would exceed 64 GB per GPU (workers._shard_spec)
             fsdp_config=dict(shard="auto", fsdp_size=-1, param_offload=False, optimizer_offload=False),
@@ -94,7 +94,7 @@ DEFAULTS = dict(
             fused_select=False,  # lm_head fused with K4 (csrc/fused_linear.hip)
         ),
         ref=dict(log_prob_micro_batch_size=None, log_prob_micro_batch_size_per_gpu=16, log_prob_use_dynamic_bsz=False,
-                 log_prob_max_token_len_per_gpu=16384, exec_log_prob_tokens=65536),
+                 log_prob_max_token_len_per_gpu=16384, exec_log_prob_tokens=196608),
     ),
     # critic.yaml + dp_critic.yaml (used when algorithm.adv_estimator == "gae" or critic.enable)
     critic=dict(
@@ -109,7 +109,7 @@ DEFAULTS = dict(
         forward_micro_batch_size=None, forward_micro_batch_size_per_gpu=16, use_dynamic_bsz=None,
         ppo_max_token_len_per_gpu=32768, forward_max_token_len_per_gpu=32768, ppo_epochs=None, shuffle=None,
         grad_clip=1.0, cliprange_value=0.5, loss_agg_mode=None, ulysses_sequence_parallel_size=1,
-        exec_micro_batches=0, exec_activation_gb=40,  # as the actor's (dp_actor.exec_groups)
+        exec_micro_batches=0, exec_activation_gb=110,  # as the actor's (dp_actor.exec_groups)
     ),
     algorithm=dict(gamma=1.0, lam=1.0, adv_estimator="grpo", norm_adv_by_std_in_grpo=True, use_kl_in_reward=False,
                    kl_penalty="kl", kl_ctrl=dict(type="fixed", kl_coef=0.001, horizon=10000, target_kl=0.1)),

@@ -226,10 +226,28 @@ def exec_groups(cfg, model_cfg, micro_batches):
         nq = (model_cfg.num_attention_heads + 2 * model_cfg.num_key_value_heads) * model_cfg.head_dim
         # saved per token and layer: x, x2 (fp32), h1, h2, attn (bf16), q / k / v / k^T, gate|up and SwiGLU out
         per_tok = L * (8 * H + 6 * H + 4 * nq + 6 * I)
-        budget = float(cfg.get("exec_activation_gb", 40)) * 2 ** 30
+        budget = float(cfg.get("exec_activation_gb", 110)) * 2 ** 30
+        if torch.cuda.is_available():  # never plan past half of what is free (the device's + torch's cached pool)
+            avail = torch.cuda.mem_get_info()[0] + torch.cuda.memory_reserved() - torch.cuda.memory_allocated()
+            budget = min(budget, 0.5 * avail)
         toks = max(mb.batch["input_ids"].numel() for mb in micro_batches)
         n = max(1, int(budget // max(1, per_tok * toks)))
-    return [micro_batches[i:i + n] for i in range(0, len(micro_batches), n)]
+    return balanced_groups(micro_batches, n)
+
+
+def balanced_groups(items, n):
+    """Consecutive groups of at most n items, as few as possible and of near-equal size (32 items at n = 17 -> two
+    groups of 16, not 17 + 15): every pass's GEMMs then see about the same row count."""
+    if not items:
+        return []
+    k = -(-len(items) // max(1, n))
+    base, extra = divmod(len(items), k)
+    out, i = [], 0
+    for j in range(k):
+        m = base + (1 if j < extra else 0)
+        out.append(items[i:i + m])
+        i += m
+    return out
 
 
 class DataParallelPPOActor:
@@ -286,17 +304,8 @@ class DataParallelPPOActor:
         budget = int(self.config.get("exec_log_prob_tokens", 0) or 0)
         if budget <= 0:
             return [[mb] for mb in micro_batches]
-        groups, cur, toks = [], [], 0
-        for mb in micro_batches:
-            t = mb.batch["input_ids"].numel()
-            if cur and toks + t > budget:
-                groups.append(cur)
-                cur, toks = [], 0
-            cur.append(mb)
-            toks += t
-        if cur:
-            groups.append(cur)
-        return groups
+        toks = max(mb.batch["input_ids"].numel() for mb in micro_batches) if micro_batches else 1
+        return balanced_groups(micro_batches, max(1, budget // toks))
 
     @torch.no_grad()
     def compute_log_prob(self, data: DataProto, calculate_entropy=False):
