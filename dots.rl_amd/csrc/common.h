@@ -37,6 +37,17 @@ int cu_count();  // cached per device
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 inline size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
+// V^T (head-dim-major V) of one (sequence, KV head): rows of ld_vt keys, or with ld_vt == DRL_VT_BLOCKED the
+// key-blocked cache layout [ceil(cap / 32)][D][32] (one 32-key block's V^T is 32 * D contiguous elements, so
+// a decode / prefill block fetch is one contiguous 4-KB (D = 64) run instead of D row pieces). cap = the K
+// capacity (ld_k / Tk) the panel is sized for.
+__host__ __device__ __forceinline__ int64_t vt_index(int64_t d, int64_t key, int64_t ld_vt, int64_t D) {
+  return ld_vt == DRL_VT_BLOCKED ? (key >> 5) * (32 * D) + d * 32 + (key & 31) : d * ld_vt + key;
+}
+__host__ __device__ __forceinline__ int64_t vt_panel(int64_t ld_vt, int64_t D, int64_t cap) {
+  return ld_vt == DRL_VT_BLOCKED ? (cap + 31) / 32 * 32 * D : D * ld_vt;
+}
+
 // ---------------------------------------------------------------- device: wave/block reductions
 constexpr int kWave = 64;
 

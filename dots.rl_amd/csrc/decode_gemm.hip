@@ -164,9 +164,9 @@ __global__ __launch_bounds__(256) void decode_gemm_kernel(DgArgs a) {
         dst[d1] = to_bf16_bits(o1);
         dst[d2] = to_bf16_bits(o2);
       } else {
-        uint16_t* dst = a.vt + (static_cast<int64_t>(m) * a.Hkv + (hd - a.Hq - a.Hkv)) * a.D * a.ld_vt + koff;
-        dst[static_cast<int64_t>(d1) * a.ld_vt] = to_bf16_bits(x1);
-        dst[static_cast<int64_t>(d2) * a.ld_vt] = to_bf16_bits(x2);
+        uint16_t* dst = a.vt + (static_cast<int64_t>(m) * a.Hkv + (hd - a.Hq - a.Hkv)) * vt_panel(a.ld_vt, a.D, a.Tk);
+        dst[vt_index(d1, koff, a.ld_vt, a.D)] = to_bf16_bits(x1);
+        dst[vt_index(d2, koff, a.ld_vt, a.D)] = to_bf16_bits(x2);
       }
     }
   } else {
@@ -265,9 +265,9 @@ __device__ __forceinline__ void tiled_epilogue(const DgArgs& a, const f32x16 (&a
             dst[d1] = to_bf16_bits(o1);
             dst[d2] = to_bf16_bits(o2);
           } else {
-            uint16_t* dst = a.vt + (static_cast<int64_t>(m) * a.Hkv + (hd - a.Hq - a.Hkv)) * a.D * a.ld_vt + koff;
-            dst[static_cast<int64_t>(d1) * a.ld_vt] = to_bf16_bits(x1);
-            dst[static_cast<int64_t>(d2) * a.ld_vt] = to_bf16_bits(x2);
+            uint16_t* dst = a.vt + (static_cast<int64_t>(m) * a.Hkv + (hd - a.Hq - a.Hkv)) * vt_panel(a.ld_vt, a.D, a.Tk);
+            dst[vt_index(d1, koff, a.ld_vt, a.D)] = to_bf16_bits(x1);
+            dst[vt_index(d2, koff, a.ld_vt, a.D)] = to_bf16_bits(x2);
           }
         }
       }
@@ -552,9 +552,9 @@ __global__ __launch_bounds__(256) void dec_rope_kernel(DecRopeArgs a) {
   } else {
     const int64_t hv = h - a.Hq - a.Hkv;
     if (a.vt) {
-      uint16_t* dst = a.vt + (b * a.Hkv + hv) * a.D * a.ld_vt + koff;
-      dst[j * a.ld_vt] = to_bf16_bits(x1);
-      dst[(j + half) * a.ld_vt] = to_bf16_bits(x2);
+      uint16_t* dst = a.vt + (b * a.Hkv + hv) * vt_panel(a.ld_vt, a.D, a.Tk);
+      dst[vt_index(j, koff, a.ld_vt, a.D)] = to_bf16_bits(x1);
+      dst[vt_index(j + half, koff, a.ld_vt, a.D)] = to_bf16_bits(x2);
     }
     if (a.v) {
       uint16_t* dst = a.v + ((b * a.Hkv + hv) * a.Tk + koff) * a.D;
@@ -842,7 +842,7 @@ int drl_decode_qkv_rope(const void* x_packed, const void* w_packed, const void* 
   DRL_CHECK_ARG(x_packed && w_packed && bias && position_ids && cos_t && sin_t && q && k_cache && vt_cache && koff_dev,
                 "NULL input");
   DRL_CHECK_ARG(aligned16(x_packed) && aligned16(w_packed), "packed operands must be 16-byte aligned");
-  DRL_CHECK_ARG(Hq >= 1 && Hkv >= 1 && Hq % Hkv == 0 && D % 32 == 0 && ld_vt >= Tk && Tk >= 1 && maxpos >= 1,
+  DRL_CHECK_ARG(Hq >= 1 && Hkv >= 1 && Hq % Hkv == 0 && D % 32 == 0 && (ld_vt >= Tk || ld_vt == DRL_VT_BLOCKED) && Tk >= 1 && maxpos >= 1,
                 "bad shape");
   const int64_t N = (Hq + 2 * Hkv) * D;
   DgPlan p{};
@@ -926,7 +926,7 @@ int drl_decode_rope(const float* partials, int32_t nsplit, const void* bias, con
   DRL_CHECK_ARG(partials && bias && position_ids && cos_t && sin_t && q && k_cache && (v_cache || vt_cache),
                 "NULL input");
   DRL_CHECK_ARG(nsplit >= 1 && B >= 1 && Hq >= 1 && Hkv >= 1 && Hq % Hkv == 0 && D % 2 == 0 && Tk >= 1, "bad shape");
-  DRL_CHECK_ARG(vt_cache == nullptr || ld_vt >= Tk, "ld_vt < Tk");
+  DRL_CHECK_ARG(vt_cache == nullptr || ld_vt >= Tk || ld_vt == DRL_VT_BLOCKED, "ld_vt < Tk");
   DRL_CHECK_ARG(koff_dev != nullptr || (koff >= 0 && koff < Tk), "key offset out of range");
   DecRopeArgs a{partials, nsplit, static_cast<const uint16_t*>(bias), position_ids, cos_t, sin_t,
                 static_cast<uint16_t*>(q), static_cast<uint16_t*>(k_cache), static_cast<uint16_t*>(v_cache),

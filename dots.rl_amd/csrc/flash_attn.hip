@@ -140,7 +140,7 @@ __device__ __forceinline__ void kv_issue_full(const uint16_t* kbase, const uint1
       r[i] = *reinterpret_cast<const u16x8*>(kbase + (k0 + row) * D + col * 8);
     } else {
       const int cc = c - KCH, d = cc / 4, col = cc % 4;
-      r[i] = *reinterpret_cast<const u16x8*>(vtbase + static_cast<int64_t>(d) * ld_vt + k0 + col * 8);
+      r[i] = *reinterpret_cast<const u16x8*>(vtbase + vt_index(d, k0 + col * 8, ld_vt, D));
     }
   }
 }
@@ -159,7 +159,7 @@ __device__ __forceinline__ void kv_issue(const uint16_t* kbase, const uint16_t* 
     } else {
       const int cc = c - KCH, d = cc / 4, col = cc % 4;
       const int64_t kk = k0 + col * 8;
-      const uint16_t* src = vtbase + static_cast<int64_t>(d) * ld_vt + kk;
+      const uint16_t* src = vtbase + vt_index(d, kk, ld_vt, D);  // 8 keys inside one 32-key block
       if (kk + 7 < Tk) {
         r[i] = *reinterpret_cast<const u16x8*>(src);
       } else {
@@ -245,7 +245,7 @@ __global__ __launch_bounds__(512, D == 64 ? 4 : 1) void flash_fwd_kernel(FlashAr
   float m = -INFINITY, lsum = 0.f;
 
   const uint16_t* kbase = a.k + bh * a.ld_k * D;
-  const uint16_t* vtbase = a.vt + bh * D * a.ld_vt;
+  const uint16_t* vtbase = a.vt + bh * vt_panel(a.ld_vt, D, a.ld_k);
   const uint8_t* vrow = a.valid + b * a.ld_valid;
   const int64_t kmax = min(a.Tk, t0 + 31 + a.qoff + 1);  // causal limit of the tile's last query
   const int64_t nb = (kmax + 31) / 32;
@@ -886,8 +886,9 @@ __device__ __forceinline__ void dec_load_raw(const uint16_t* kb, const uint16_t*
     const int key = k0 + c / UPR;
     r.k[i] = *reinterpret_cast<const u16x8*>(kb + static_cast<int64_t>(min(key, kend - 1)) * D + 8 * (c % UPR));
     const int kk = k0 + 8 * (c & 3);
-    r.v[i] = *reinterpret_cast<const u16x8*>(vtb + static_cast<int64_t>(c >> 2) * ld_vt +
-                                             min(static_cast<int64_t>(kk), ld_vt - 8));
+    r.v[i] = *reinterpret_cast<const u16x8*>(
+        vtb + (ld_vt == DRL_VT_BLOCKED ? vt_index(c >> 2, kk, ld_vt, D)
+                                       : static_cast<int64_t>(c >> 2) * ld_vt + min(static_cast<int64_t>(kk), ld_vt - 8)));
     if (tail) {
       if (key >= kend) r.k[i] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
@@ -1063,7 +1064,7 @@ __global__ __launch_bounds__(64 * NW) void decode_mfma_kernel(DecodeArgs a) {
   const int qpos = static_cast<int>(a.qpos_ptr ? *a.qpos_ptr : a.qpos);
   const int kend = static_cast<int>(min(a.L, static_cast<int64_t>(qpos) + 1));
   const uint16_t* kb = a.k + bh * a.ld_k * D;
-  const uint16_t* vtb = a.vt + bh * D * a.ld_vt;
+  const uint16_t* vtb = a.vt + bh * vt_panel(a.ld_vt, D, a.ld_k);
   const uint8_t* vrow = a.valid + b * a.ld_valid;
   // split-K over gridDim.y workgroups: split y takes 32-key blocks [y*n/S, (y+1)*n/S) of the n live blocks;
   // each wave takes blocks ib0, ib0 + NW, ... and has its first NB (LEAN: 1) in flight together with q
@@ -1263,7 +1264,8 @@ int drl_flash_attn_fwd(const void* q, const void* k, const void* vt, int32_t dt,
   DRL_CHECK_ARG(dt == DRL_BF16, "flash attention runs on bf16 operands");
   DRL_CHECK_ARG(D == 64 || D == 128, "head_dim must be 64 or 128");
   DRL_CHECK_ARG(B >= 1 && Hkv >= 1 && G >= 1 && G <= 8 && Tq >= 1 && Tk >= 1 && qoff >= 0, "bad shape");
-  DRL_CHECK_ARG(ld_vt >= Tk && ld_vt % 8 == 0, "ld_vt must be >= Tk and a multiple of 8");
+  DRL_CHECK_ARG(ld_vt == DRL_VT_BLOCKED || (ld_vt >= Tk && ld_vt % 8 == 0),
+                "ld_vt must be >= Tk and a multiple of 8 (or DRL_VT_BLOCKED)");
   DRL_CHECK_ARG(ld_k >= Tk, "ld_k < Tk");
   DRL_CHECK_ARG(Tk + qoff < (int64_t(1) << 30), "positions must fit in 32 bits");
   DRL_CHECK_ARG(ld_valid >= Tk && ld_valid % 4 == 0 && (reinterpret_cast<uintptr_t>(key_valid) & 3u) == 0,
@@ -1339,7 +1341,8 @@ int drl_decode_attention_vt(const void* q, const void* k_cache, const void* vt_c
   DRL_CHECK_ARG(dt == DRL_BF16, "MFMA decode attention runs on bf16");
   DRL_CHECK_ARG(out_mbt == 0 || out_mbt * 32 >= B, "out_mbt too small for B rows");
   DRL_CHECK_ARG(D == 64 || D == 128, "head_dim must be 64 or 128");
-  DRL_CHECK_ARG(B >= 1 && Hkv >= 1 && G >= 1 && G <= 32 && L >= 1 && L <= ld_k && L <= ld_vt, "bad shape");
+  DRL_CHECK_ARG(B >= 1 && Hkv >= 1 && G >= 1 && G <= 32 && L >= 1 && L <= ld_k &&
+                    (ld_vt == DRL_VT_BLOCKED || L <= ld_vt), "bad shape");
   DRL_CHECK_ARG(ld_vt % 8 == 0 && ld_valid % 4 == 0 && (reinterpret_cast<uintptr_t>(key_valid) & 3u) == 0 &&
                     ld_k < (int64_t(1) << 30),
                 "ld_vt must be a multiple of 8 and key_valid rows 4-byte aligned");

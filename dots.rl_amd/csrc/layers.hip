@@ -86,9 +86,9 @@ __global__ __launch_bounds__(256) void rope_qkv_fwd_kernel(RopeArgs<E> a) {
       }
     } else {
       if (a.vt != nullptr) {
-        E* dst = a.vt + (b * a.Hkv + (h - a.Hq - a.Hkv)) * a.D * a.ld_t + koff + t;
-        dst[j * a.ld_t] = src[j];
-        dst[(j + half) * a.ld_t] = src[j + half];
+        E* dst = a.vt + (b * a.Hkv + (h - a.Hq - a.Hkv)) * vt_panel(a.ld_t, a.D, a.Tk);
+        dst[vt_index(j, koff + t, a.ld_t, a.D)] = src[j];
+        dst[vt_index(j + half, koff + t, a.ld_t, a.D)] = src[j + half];
       }
       if (a.v != nullptr) {
         E* dst = a.v + ((b * a.Hkv + (h - a.Hq - a.Hkv)) * a.Tk + koff + t) * a.D;
@@ -130,7 +130,7 @@ __global__ __launch_bounds__(256) void rope_qkv_fwd_tiled_kernel(RopeArgs<E> a) 
     pos0 = koff;
   } else {
     rowdst = a.v ? a.v + (b * a.Hkv + (h - a.Hq - a.Hkv)) * a.Tk * a.D : nullptr;
-    tdst = a.vt ? a.vt + (b * a.Hkv + (h - a.Hq - a.Hkv)) * a.D * a.ld_t : nullptr;
+    tdst = a.vt ? a.vt + (b * a.Hkv + (h - a.Hq - a.Hkv)) * vt_panel(a.ld_t, a.D, a.Tk) : nullptr;
     pos0 = koff;
   }
   const int rows_per_pass = 256 / half;
@@ -167,15 +167,18 @@ __global__ __launch_bounds__(256) void rope_qkv_fwd_tiled_kernel(RopeArgs<E> a) 
   const int nvalid = static_cast<int>(min<int64_t>(kRopeTile, a.T - t0));
   for (int it = threadIdx.x; it < a.D * (kRopeTile / kPer); it += 256) {
     const int d = it / (kRopeTile / kPer), c = it % (kRopeTile / kPer);
-    E* dst = tdst + d * a.ld_t + pos0 + t0 + c * kPer;
+    const int64_t p0 = pos0 + t0 + c * kPer;  // first position of this thread's piece
+    E* dst = tdst + vt_index(d, p0, a.ld_t, a.D);
+    // the 16 positions are contiguous unless the key-blocked layout splits them over two 32-key blocks
+    const bool contig = a.ld_t != DRL_VT_BLOCKED || (p0 & 31) + kPer <= 32;
     const bool aligned = ((reinterpret_cast<uintptr_t>(dst) & 15u) == 0) && sizeof(E) == 2;
-    if (aligned && c * kPer + kPer <= nvalid) {
+    if (contig && aligned && c * kPer + kPer <= nvalid) {
       const uint4* srcv = reinterpret_cast<const uint4*>(&tile[d][c * kPer]);
       uint4* dv = reinterpret_cast<uint4*>(dst);
       dv[0] = srcv[0];
       dv[1] = srcv[1];
     } else {
-      for (int e = 0; e < kPer && c * kPer + e < nvalid; ++e) dst[e] = tile[d][c * kPer + e];
+      for (int e = 0; e < kPer && c * kPer + e < nvalid; ++e) tdst[vt_index(d, p0 + e, a.ld_t, a.D)] = tile[d][c * kPer + e];
     }
   }
 }
@@ -223,7 +226,7 @@ __global__ __launch_bounds__(256) void rope_qkv_fwd_tiled4_kernel(RopeArgs<E> a)
     pos0 = koff;
   } else {
     rowdst = a.v ? a.v + (b * a.Hkv + (h - a.Hq - a.Hkv)) * a.Tk * a.D : nullptr;
-    tdst = a.vt ? a.vt + (b * a.Hkv + (h - a.Hq - a.Hkv)) * a.D * a.ld_t : nullptr;
+    tdst = a.vt ? a.vt + (b * a.Hkv + (h - a.Hq - a.Hkv)) * vt_panel(a.ld_t, a.D, a.Tk) : nullptr;
     pos0 = koff;
   }
   // 4 consecutive head-dim pairs per thread: 8-B (bf16) / 16-B (fp32) loads and stores instead of 2-B ones
@@ -271,15 +274,18 @@ __global__ __launch_bounds__(256) void rope_qkv_fwd_tiled4_kernel(RopeArgs<E> a)
   const int nvalid = static_cast<int>(min<int64_t>(kRopeTile, a.T - t0));
   for (int it = threadIdx.x; it < a.D * (kRopeTile / kPer); it += 256) {
     const int d = it / (kRopeTile / kPer), c = it % (kRopeTile / kPer);
-    E* dst = tdst + d * a.ld_t + pos0 + t0 + c * kPer;
+    const int64_t p0 = pos0 + t0 + c * kPer;  // first position of this thread's piece
+    E* dst = tdst + vt_index(d, p0, a.ld_t, a.D);
+    // the 16 positions are contiguous unless the key-blocked layout splits them over two 32-key blocks
+    const bool contig = a.ld_t != DRL_VT_BLOCKED || (p0 & 31) + kPer <= 32;
     const bool aligned = ((reinterpret_cast<uintptr_t>(dst) & 15u) == 0) && sizeof(E) == 2;
-    if (aligned && c * kPer + kPer <= nvalid) {
+    if (contig && aligned && c * kPer + kPer <= nvalid) {
       const uint4* srcv = reinterpret_cast<const uint4*>(&tile[d][c * kPer]);
       uint4* dv = reinterpret_cast<uint4*>(dst);
       dv[0] = srcv[0];
       dv[1] = srcv[1];
     } else {
-      for (int e = 0; e < kPer && c * kPer + e < nvalid; ++e) dst[e] = tile[d][c * kPer + e];
+      for (int e = 0; e < kPer && c * kPer + e < nvalid; ++e) tdst[vt_index(d, p0 + e, a.ld_t, a.D)] = tile[d][c * kPer + e];
     }
   }
 }
@@ -987,7 +993,9 @@ int drl_rope_qkv_fwd(const void* qkv, int32_t dt, const int64_t* position_ids, c
                      int64_t ld_t, void* stream) {
   using namespace drl;
   DRL_CHECK_ARG(qkv && position_ids && cos_t && sin_t && q && k && (v || vt), "NULL input");
-  DRL_CHECK_ARG((qt == nullptr && kt == nullptr && vt == nullptr) || (ld_t >= Tk && ld_t >= T), "ld_t too small");
+  DRL_CHECK_ARG((qt == nullptr && kt == nullptr && vt == nullptr) || (ld_t >= Tk && ld_t >= T) ||
+                    (ld_t == DRL_VT_BLOCKED && qt == nullptr && kt == nullptr),
+                "ld_t too small (DRL_VT_BLOCKED only for a vt cache alone)");
   DRL_CHECK_ARG(B >= 1 && T >= 1 && Hq >= 1 && Hkv >= 1 && Hq % Hkv == 0 && D % 2 == 0, "bad shape");
   DRL_CHECK_ARG(koff >= 0 && koff + T <= Tk, "key offset out of range");
   const int64_t n = B * T * (Hq + 2 * Hkv) * (D / 2);

@@ -567,7 +567,9 @@ def rope_qkv_fwd(qkv, position_ids, cos_t, sin_t, Hq, Hkv, D, q, k, v, koff=0, k
     ``koff_dev`` (device int64 scalar) replaces ``koff`` for graph-captured decode steps. ``qt`` (B,Hkv,G,D,ld),
     ``kt`` / ``vt`` (B,Hkv,D,ld): head-dim-major copies for the fused attention kernels (same ld)."""
     B, T = qkv.shape[0], qkv.shape[1]
-    lds = {t.stride(-2) for t in (qt, kt, vt) if t is not None}
+    lds = {(vt_ld(t) if t is vt else t.stride(-2)) for t in (qt, kt, vt) if t is not None}
+    if vt is not None:
+        _vt_cap_ok(vt, k.shape[2])
     assert len(lds) <= 1, "qt / kt / vt must share their row stride"
     check(lib().drl_rope_qkv_fwd(_p(qkv), _edt(qkv), _p(position_ids), _p(cos_t), _p(sin_t), cos_t.shape[0], B, T,
                                  Hq, Hkv, D, _p(q), _p(k), _p(v), k.shape[2], koff, _p(koff_dev), _p(qt), _p(kt),
@@ -637,16 +639,40 @@ def decode_attention(q, k_cache, v_cache, key_valid, L, out, qpos=None, qpos_dev
     return out
 
 
+DRL_VT_BLOCKED = -32  # include/dotsrl_amd.h: ld_vt of the key-blocked V^T cache layout
+
+
+def vt_ld(vt):
+    """ld_vt of a V^T operand: its row stride (B, Hkv, D, ld), or DRL_VT_BLOCKED for the key-blocked cache layout
+    (B, Hkv, ceil(cap / 32), D, 32) that KVCache keeps (one 32-key block's V^T contiguous)."""
+    if vt.dim() == 5:
+        assert vt.shape[-1] == 32 and vt.is_contiguous(), "key-blocked V^T must be a contiguous (B, Hkv, NB, D, 32)"
+        return DRL_VT_BLOCKED
+    assert vt.stride(-1) == 1 and vt.stride(-2) * vt.shape[-2] == vt.stride(-3)
+    return vt.stride(-2)
+
+
+def vt_blocked_to_plain(vt):
+    """(B, Hkv, NB, D, 32) key-blocked V^T -> (B, Hkv, D, NB * 32) head-dim-major copy (tests / inspection)."""
+    B, Hkv, NB, D, _ = vt.shape
+    return vt.permute(0, 1, 3, 2, 4).reshape(B, Hkv, D, NB * 32)
+
+
+def _vt_cap_ok(vt, cap):
+    assert vt.dim() != 5 or vt.shape[2] == (cap + 31) // 32, "key-blocked V^T must hold ceil(K capacity / 32) blocks"
+
+
 def flash_attn_fwd(q, k, vt, key_valid, out, Tk=None, qoff=0, lse=None):
     """Fused causal + key-padding attention (MFMA). q (B,Hkv,G,Tq,D) bf16, k (B,Hkv,>=Tk,D) (keys [0,Tk) used),
     vt (B,Hkv,D,ld) with ld >= Tk a multiple of 8; out (B,Tq,Hkv*G*D); lse optional (B,Hkv,G,Tq) fp32."""
     _dev(q, k, vt, key_valid, out, lse)
     B, Hkv, G, Tq, D = q.shape
     Tk = k.shape[2] if Tk is None else Tk
-    assert q.is_contiguous() and k.is_contiguous() and out.is_contiguous() and vt.stride(3) == 1
-    assert vt.stride(2) * D == vt.stride(1) and key_valid.dtype == torch.uint8 and key_valid.stride(1) == 1
+    assert q.is_contiguous() and k.is_contiguous() and out.is_contiguous()
+    assert key_valid.dtype == torch.uint8 and key_valid.stride(1) == 1
+    _vt_cap_ok(vt, k.shape[2])
     check(lib().drl_flash_attn_fwd(_p(q), _p(k), _p(vt), _edt(q), _p(key_valid), key_valid.stride(0), B, Hkv, G, D,
-                                   Tq, Tk, k.shape[2], vt.stride(2), qoff, 1.0 / math.sqrt(D), _p(out), _p(lse),
+                                   Tq, Tk, k.shape[2], vt_ld(vt), qoff, 1.0 / math.sqrt(D), _p(out), _p(lse),
                                    _stream()),
           "drl_flash_attn_fwd")
     return out
@@ -873,14 +899,15 @@ def decode_attention_vt(q, k_cache, vt_cache, key_valid, L, out, qpos=None, qpos
     ``out`` is the fragment-packed (B, Hq*D) panel of the decode o_proj GEMM (decode_gemm layout)."""
     _dev(q, k_cache, vt_cache, key_valid, out)
     B, Hkv, G, D = q.shape
-    assert q.is_contiguous() and k_cache.is_contiguous() and out.is_contiguous() and vt_cache.stride(-1) == 1
+    assert q.is_contiguous() and k_cache.is_contiguous() and out.is_contiguous()
     assert out_mbt == 0 or out.numel() >= out_mbt * 32 * Hkv * G * D
-    assert vt_cache.stride(-2) * D == vt_cache.stride(1) and key_valid.dtype == torch.uint8
+    assert key_valid.dtype == torch.uint8
+    _vt_cap_ok(vt_cache, k_cache.shape[2])
     qp = L - 1 if qpos is None else int(qpos)
     nws = lib().drl_decode_attention_vt_workspace_bytes(B, Hkv, D, L)
     ws = _linear_workspace(q.device, nws, "decode_attention") if nws else None
     check(lib().drl_decode_attention_vt(_p(q), _p(k_cache), _p(vt_cache), _edt(q), _p(key_valid), key_valid.stride(0),
-                                        _p(qpos_dev), qp, B, Hkv, G, D, k_cache.shape[2], vt_cache.stride(-2), L,
+                                        _p(qpos_dev), qp, B, Hkv, G, D, k_cache.shape[2], vt_ld(vt_cache), L,
                                         1.0 / math.sqrt(D), _p(out), int(out_mbt), _p(ws), nws, _stream()),
           "drl_decode_attention_vt")
     return out
@@ -980,7 +1007,9 @@ def decode_rope(partials, bias, position_ids, cos_t, sin_t, Hq, Hkv, D, q, k_cac
     _dev(partials, bias, position_ids, q, k_cache)
     ns, B = partials.shape[0], partials.shape[1]
     Tk = k_cache.shape[2]
-    ld_vt = vt_cache.stride(-2) if vt_cache is not None else 0
+    ld_vt = vt_ld(vt_cache) if vt_cache is not None else 0
+    if vt_cache is not None:
+        _vt_cap_ok(vt_cache, k_cache.shape[2])
     check(lib().drl_decode_rope(_p(partials), ns, _p(bias), _p(position_ids), _p(cos_t), _p(sin_t), cos_t.shape[0], B,
                                 Hq, Hkv, D, _p(q), _p(k_cache), _p(v_cache), _p(vt_cache), Tk, ld_vt, int(koff),
                                 _p(koff_dev), _stream()), "drl_decode_rope")
@@ -1003,8 +1032,9 @@ def decode_qkv_rope(x_packed, w_packed, bias, position_ids, cos_t, sin_t, M, K, 
                     koff_dev):
     """One launch: qkv_proj + bias + RoPE, q (M,Hkv,G,D) out, K / V^T cache rows at the device offset."""
     _dev(x_packed, w_packed, bias, position_ids, q, k_cache, vt_cache, koff_dev)
-    assert q.is_contiguous() and k_cache.is_contiguous() and vt_cache.stride(-1) == 1
+    assert q.is_contiguous() and k_cache.is_contiguous()
+    _vt_cap_ok(vt_cache, k_cache.shape[2])
     check(lib().drl_decode_qkv_rope(_p(x_packed), _p(w_packed), _p(bias), _p(position_ids), _p(cos_t), _p(sin_t),
                                     cos_t.shape[0], M, K, Hq, Hkv, D, _p(q), _p(k_cache), _p(vt_cache),
-                                    k_cache.shape[2], vt_cache.stride(-2), _p(koff_dev), _stream()),
+                                    k_cache.shape[2], vt_ld(vt_cache), _p(koff_dev), _stream()),
           "drl_decode_qkv_rope")

@@ -709,22 +709,28 @@ def _key_valid(attention_mask):
 
 
 class KVCache:
-    """Per-layer K (B, Hkv, Tmax, D) and V (bf16: head-dim-major (B, Hkv, D, Tmax); fp32: row-major) in the
-    compute dtype, plus the key-valid mask (u8)."""
+    """Per-layer K (B, Hkv, Tmax, D) and V (bf16: head-dim-major in 32-key blocks (B, Hkv, ceil(Tmax / 32), D, 32);
+    fp32: row-major) in the compute dtype, plus the key-valid mask (u8)."""
 
     def __init__(self, cfg: Qwen2Config, B, Tmax, device, dtype):
         Hkv, D, L = cfg.num_key_value_heads, cfg.head_dim, cfg.num_hidden_layers
         self.k = [torch.empty(B, Hkv, Tmax, D, device=device, dtype=dtype) for _ in range(L)]
         if dtype == torch.bfloat16 and D in (64, 128):
-            # V head-dim-major (B, Hkv, D, Tmax padded to 8): read by the MFMA prefill and decode kernels
-            ld = (Tmax + 7) // 8 * 8
-            self.vt = [torch.zeros(B, Hkv, D, ld, device=device, dtype=dtype)[..., :Tmax] for _ in range(L)]
+            # V^T key-blocked (native.DRL_VT_BLOCKED): a 32-key block of V^T is one contiguous 32 * D run, the unit
+            # the MFMA prefill and decode kernels fetch (the K block is one contiguous run already)
+            self.vt = [torch.zeros(B, Hkv, (Tmax + 31) // 32, D, 32, device=device, dtype=dtype) for _ in range(L)]
             self.v = [None] * L
         else:
             self.vt = [None] * L
             self.v = [torch.empty_like(t) for t in self.k]
         self.valid = torch.zeros(B, (Tmax + 3) // 4 * 4, dtype=torch.uint8, device=device)[:, :Tmax]
         self.len = 0
+        self.Tmax = Tmax
+
+    def vt_plain(self, i):
+        """Layer i's V^T as a head-dim-major (B, Hkv, D, Tmax) copy (tests / inspection)."""
+        from . import native
+        return native.vt_blocked_to_plain(self.vt[i])[..., :self.Tmax]
 
 
 class Qwen2Model:

@@ -26,6 +26,12 @@ extern "C" {
  * built against version 2 passes a shorter struct); drl_gemm (operand layouts, fp32 epilogues, stream-K) */
 #define DRL_ABI_VERSION 3
 
+/* ld_vt value selecting the key-blocked V^T cache layout (B, Hkv, ceil(cap / 32), D, 32) wherever a V^T
+ * operand with a leading dimension ld_vt is taken (flash / decode attention, the rope and decode-projection
+ * cache writers): element (d, key) of a (sequence, KV head) panel sits at (key / 32) * 32 * D + d * 32 +
+ * key % 32, and cap is the K capacity of the same call (ld_k or Tk). */
+#define DRL_VT_BLOCKED (-32)
+
 #define DRL_OK 0
 #define DRL_ERR_INVALID (-1)     /* bad argument (shape, dtype, null pointer, alignment) */
 #define DRL_ERR_HIP (-2)         /* a HIP runtime call failed */

@@ -184,7 +184,7 @@ def test_packed_decode_step_tracks_unpacked(B):
     n = P + R - 1  # positions written (the last cache slot is never filled here)
     for i in range(cfg.num_hidden_layers):
         for a, b in ((caches[0].k[i][:, :, :n], caches[1].k[i][:, :, :n]),
-                     (caches[0].vt[i][..., :n], caches[1].vt[i][..., :n])):
+                     (caches[0].vt_plain(i)[..., :n], caches[1].vt_plain(i)[..., :n])):
             assert (a.float() - b.float()).abs().max().item() <= 3e-2 * a.float().abs().max().item()
     assert torch.equal(caches[0].valid, caches[1].valid)
 
