@@ -138,6 +138,7 @@ SIGNATURES = {
     "drl_add_rmsnorm_fwd": (ctypes.c_int, [P, P, P, P, P, I32, P, I64, I64, F32, P]),
     "drl_rmsnorm_bwd_workspace_bytes": (SZ, [I64, I64]),
     "drl_rmsnorm_bwd": (ctypes.c_int, [P, P, P, P, I32, P, P, I64, I64, P, SZ, P]),
+    "drl_rmsnorm_bwd_ex": (ctypes.c_int, [P, P, P, P, I32, P, P, P, P, I64, I64, P, SZ, P]),
     "drl_swiglu_fwd": (ctypes.c_int, [P, P, I32, I64, I64, P]),
     "drl_swiglu_bwd": (ctypes.c_int, [P, P, P, I32, I64, I64, P]),
     "drl_decode_attention_workspace_bytes": (SZ, [I64, I64, I64, I64, I64]),

@@ -669,8 +669,8 @@ __global__ __launch_bounds__(256) void add_rmsnorm_fwd_vec_kernel(const float* x
 // dx += rstd * (w*dy - xhat * mean(xhat * w*dy)) ; dw partials per block (fixed order) -> dw_part (grid, H)
 template <typename E>
 __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const float* x, const float* w, const float* rstd,
-                                                          const E* dy, float* dx, float* dw_part, int64_t N,
-                                                          int64_t H) {
+                                                          const E* dy, const float* dx_in, float* dx, uint16_t* dx_lp,
+                                                          float* dw_part, int64_t N, int64_t H) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   extern __shared__ float s_dw[];  // 4 waves x H
   for (int64_t j = threadIdx.x; j < 4 * H; j += blockDim.x) s_dw[j] = 0.f;
@@ -684,7 +684,9 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const float* x, const 
     for (int64_t j = lane; j < H; j += 64) {
       const float g = ldf(dy, row * H + j);
       const float xh = xr[j] * r;
-      dx[row * H + j] += r * (w[j] * g - xh * dot);
+      const float d = (dx_in ? dx_in[row * H + j] : 0.f) + r * (w[j] * g - xh * dot);
+      dx[row * H + j] = d;
+      if (dx_lp) dx_lp[row * H + j] = f32_to_bf16(d);
       s_dw[wave * H + j] += g * xh;
     }
   }
@@ -697,7 +699,8 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const float* x, const 
 // 2*lane + 128*k; the row's x and dy stay in registers between the dot product and the update (one read).
 template <typename E, int K>
 __global__ __launch_bounds__(256) void rmsnorm_bwd_vec_kernel(const float* x, const float* w, const float* rstd,
-                                                              const E* dy, float* dx, float* dw_part, int64_t N) {
+                                                              const E* dy, const float* dx_in, float* dx,
+                                                              uint16_t* dx_lp, float* dw_part, int64_t N) {
   constexpr int H = 128 * K;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   __shared__ float2 s_dw[4][64 * K];
@@ -726,10 +729,13 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_vec_kernel(const float* x, co
     for (int k = 0; k < K; ++k) {
       const int64_t j = row * H + 2 * lane + 128 * k;
       const float xh0 = xv[k].x * r, xh1 = xv[k].y * r;
-      float2 d = *reinterpret_cast<float2*>(dx + j);
+      float2 d = dx_in ? *reinterpret_cast<const float2*>(dx_in + j) : make_float2(0.f, 0.f);
       d.x += r * (wv[k].x * gv[k].x - xh0 * dot);
       d.y += r * (wv[k].y * gv[k].y - xh1 * dot);
       *reinterpret_cast<float2*>(dx + j) = d;
+      if (dx_lp)  // the bf16 copy the next dgrad consumes, in the same pass
+        *reinterpret_cast<uint32_t*>(dx_lp + j) = static_cast<uint32_t>(f32_to_bf16(d.x)) |
+                                                  (static_cast<uint32_t>(f32_to_bf16(d.y)) << 16);
       acc[k].x += gv[k].x * xh0;
       acc[k].y += gv[k].y * xh1;
     }
@@ -1102,8 +1108,15 @@ size_t drl_rmsnorm_bwd_workspace_bytes(int64_t N, int64_t H) {
 
 int drl_rmsnorm_bwd(const float* x, const float* weight, const float* rstd, const void* dy, int32_t dt, float* dx,
                     float* dw, int64_t N, int64_t H, void* workspace, size_t workspace_bytes, void* stream) {
+  return drl_rmsnorm_bwd_ex(x, weight, rstd, dy, dt, dx, dx, nullptr, dw, N, H, workspace, workspace_bytes, stream);
+}
+
+int drl_rmsnorm_bwd_ex(const float* x, const float* weight, const float* rstd, const void* dy, int32_t dt,
+                       const float* dx_in, float* dx, void* dx_bf16, float* dw, int64_t N, int64_t H, void* workspace,
+                       size_t workspace_bytes, void* stream) {
   using namespace drl;
   DRL_CHECK_ARG(x && weight && rstd && dy && dx && dw, "NULL input");
+  uint16_t* dx_lp = static_cast<uint16_t*>(dx_bf16);
   DRL_CHECK_ARG(N >= 1 && H >= 1 && 4 * H * sizeof(float) <= 64 * 1024, "bad shape");
   const int grid = static_cast<int>(std::min<int64_t>(static_cast<int64_t>(cu_count()) * 2, (N + 3) / 4));
   if (workspace == nullptr || workspace_bytes < static_cast<size_t>(grid) * H * sizeof(float))
@@ -1111,13 +1124,14 @@ int drl_rmsnorm_bwd(const float* x, const float* weight, const float* rstd, cons
   float* part = static_cast<float*>(workspace);
   hipStream_t s = static_cast<hipStream_t>(stream);
   const bool vec = H == 896 && (reinterpret_cast<uintptr_t>(x) & 7u) == 0 && (reinterpret_cast<uintptr_t>(dx) & 7u) == 0 &&
+                   (reinterpret_cast<uintptr_t>(dx_in) & 7u) == 0 && (reinterpret_cast<uintptr_t>(dx_lp) & 3u) == 0 &&
                    (reinterpret_cast<uintptr_t>(weight) & 7u) == 0;
   if (vec) {
     DRL_E_DISPATCH(dt, hipLaunchKernelGGL((rmsnorm_bwd_vec_kernel<E, 7>), dim3(grid), dim3(256), 0, s, x, weight, rstd,
-                                          static_cast<const E*>(dy), dx, part, N));
+                                          static_cast<const E*>(dy), dx_in, dx, dx_lp, part, N));
   } else {
     DRL_E_DISPATCH(dt, hipLaunchKernelGGL(rmsnorm_bwd_kernel<E>, dim3(grid), dim3(256), 4 * H * sizeof(float), s, x,
-                                          weight, rstd, static_cast<const E*>(dy), dx, part, N, H));
+                                          weight, rstd, static_cast<const E*>(dy), dx_in, dx, dx_lp, part, N, H));
   }
   DRL_LAUNCH_CHECK();
   hipLaunchKernelGGL(colsum_kernel, dim3((H + 15) / 16), dim3(256), 0, s, part, static_cast<int64_t>(grid), H, dw);

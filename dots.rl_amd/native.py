@@ -603,12 +603,18 @@ def add_rmsnorm_fwd(x_in, delta, x_out, weight, y, rstd, eps):
                                     float(eps), _stream()), "drl_add_rmsnorm_fwd")
 
 
-def rmsnorm_bwd(x, weight, rstd, dy, dx, dw):
+def rmsnorm_bwd(x, weight, rstd, dy, dx, dw, dx_in="inplace", dx_bf16=None):
+    """dx = dx_in + RMSNorm backward of dy (dx_in "inplace": dx itself, None: zero); dw += its weight gradient;
+    dx_bf16 (optional) receives bf16(dx) from the same pass."""
     N, H = x.numel() // x.shape[-1], x.shape[-1]
     L = lib()
     ws = _ws.get(L.drl_rmsnorm_bwd_workspace_bytes(N, H), x.device)
-    check(L.drl_rmsnorm_bwd(_p(x), _p(weight), _p(rstd), _p(dy), _edt(dy), _p(dx), _p(dw), N, H, _p(ws), ws.numel(),
-                            _stream()), "drl_rmsnorm_bwd")
+    src = dx if isinstance(dx_in, str) else dx_in
+    for t in (src, dx_bf16):
+        assert t is None or (t.is_contiguous() and t.numel() == dx.numel())
+    assert dx_bf16 is None or dx_bf16.dtype == torch.bfloat16
+    check(L.drl_rmsnorm_bwd_ex(_p(x), _p(weight), _p(rstd), _p(dy), _edt(dy), _p(src), _p(dx), _p(dx_bf16), _p(dw), N,
+                               H, _p(ws), ws.numel(), _stream()), "drl_rmsnorm_bwd_ex")
 
 
 def swiglu_fwd(gate_up, out):

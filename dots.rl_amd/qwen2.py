@@ -569,7 +569,10 @@ class _DecoderLayer(torch.autograd.Function):
         Hq, Hkv, D = cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim
         G = Hq // Hkv
         N = B * T
-        dx2 = g_x2.to(torch.float32).contiguous().clone()
+        # the residual gradient passes through the first RMSNorm backward into a fresh buffer (no clone pass)
+        g_res = g_x2.to(torch.float32).contiguous()
+        dx2 = torch.empty_like(g_res)
+        lowp = dt == torch.bfloat16  # the bf16 operand of the next dgrad comes out of the norm backward's pass
         dm = g_mlp.to(dt).contiguous().view(N, H)
         # MLP
         if _sk(dm, sv["gu"]) and dm.shape[1] % 64 == 0:
@@ -581,10 +584,12 @@ class _DecoderLayer(torch.autograd.Function):
             dgu = torch.empty_like(sv["gu"])
             native.swiglu_bwd(sv["gu"], da, dgu)
         dh2 = dgrad_wgrad(dgu, s.w(p + "gate_up_proj"), s.g(p + "gate_up_proj"), sv["h2"].view(N, H))
+        do = torch.empty(dx2.shape, dtype=dt, device=dx2.device) if lowp else None
         native.rmsnorm_bwd(sv["x2"], s.w(p + "post_attention_layernorm"), sv["rstd2"], dh2, dx2,
-                           s.g(p + "post_attention_layernorm"))
+                           s.g(p + "post_attention_layernorm"), dx_in=g_res, dx_bf16=do)
+        del g_res
         # attention output projection
-        do = dx2.to(dt).view(N, H)
+        do = (do if lowp else dx2.to(dt)).view(N, H)
         dattn = dgrad_wgrad(do, s.w(p + "o_proj"), s.g(p + "o_proj"), sv["attn"].reshape(N, Hq * D))
         rm = ctx.rm
         attn = sv["attn"]
@@ -622,11 +627,17 @@ class _DecoderLayer(torch.autograd.Function):
             else:
                 s.g(p + "qkv_proj.bias").add_(dqkv2.sum(0, dtype=torch.float32))
         dx = dx2  # residual: x2 = x + o
-        native.rmsnorm_bwd(sv["x"], s.w(p + "input_layernorm"), sv["rstd1"], dh1, dx, s.g(p + "input_layernorm"))
+        # the previous layer's bf16 delta gets bf16(dx): written by the same pass
+        ddelta = torch.empty(dx.shape, dtype=torch.bfloat16, device=dx.device) \
+            if ctx.has_delta and g_mlp.dtype == torch.bfloat16 else None
+        native.rmsnorm_bwd(sv["x"], s.w(p + "input_layernorm"), sv["rstd1"], dh1, dx, s.g(p + "input_layernorm"),
+                           dx_bf16=ddelta)
         ctx.save = None
         if m.grad_ready_hook is not None:  # layer i's gradient is complete for this micro-batch
             m.grad_ready_hook(i)
-        return dx, (dx.to(g_mlp.dtype) if ctx.has_delta else None), None, None, None, None, None
+        if ctx.has_delta and ddelta is None:
+            ddelta = dx.to(g_mlp.dtype)
+        return dx, ddelta, None, None, None, None, None
 
 
 class _FinalNorm(torch.autograd.Function):
@@ -645,9 +656,12 @@ class _FinalNorm(torch.autograd.Function):
     def backward(ctx, dh):
         x, rstd = ctx.saved_tensors
         m = ctx.m
-        dx = torch.zeros_like(x)
-        native.rmsnorm_bwd(x, m.store.w("norm"), rstd, dh.contiguous(), dx, m.store.g("norm"))
-        return dx, dx.to(ctx.delta_dtype), None
+        dx = torch.empty_like(x)
+        ddelta = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device) \
+            if ctx.delta_dtype == torch.bfloat16 else None
+        native.rmsnorm_bwd(x, m.store.w("norm"), rstd, dh.contiguous(), dx, m.store.g("norm"), dx_in=None,
+                           dx_bf16=ddelta)
+        return dx, (ddelta if ddelta is not None else dx.to(ctx.delta_dtype)), None
 
 
 class RmPad:

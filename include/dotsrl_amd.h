@@ -385,6 +385,12 @@ size_t drl_rmsnorm_bwd_workspace_bytes(int64_t N, int64_t H);
 /* dx += d norm(x)/dx . dy ; dw += sum_rows dy * xhat */
 int drl_rmsnorm_bwd(const float* x, const float* weight, const float* rstd, const void* dy, int32_t dt, float* dx,
                     float* dw, int64_t N, int64_t H, void* workspace, size_t workspace_bytes, void* stream);
+/* drl_rmsnorm_bwd with the residual gradient passed through: dx = dx_in + d norm(x)/dx . dy (dx_in NULL: zero;
+ * dx_in == dx: in place), and, when dx_bf16 is not NULL, its bf16 rounding written in the same pass (the operand of
+ * the next dgrad, and the gradient of a bf16 residual delta). Workspace as drl_rmsnorm_bwd. */
+int drl_rmsnorm_bwd_ex(const float* x, const float* weight, const float* rstd, const void* dy, int32_t dt,
+                       const float* dx_in, float* dx, void* dx_bf16, float* dw, int64_t N, int64_t H, void* workspace,
+                       size_t workspace_bytes, void* stream);
 /* gate_up (N, 2I) -> out (N, I) = silu(gate) * up ; backward -> d gate_up */
 int drl_swiglu_fwd(const void* gate_up, void* out, int32_t dt, int64_t N, int64_t I, void* stream);
 int drl_swiglu_bwd(const void* gate_up, const void* dout, void* dgate_up, int32_t dt, int64_t N, int64_t I,

@@ -135,6 +135,18 @@ def test_add_rmsnorm_forward_backward(dt, with_delta, N, H):
     out.backward(dy.float())
     torch.testing.assert_close(dx, 1 + xr.grad, rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(dw, 1 + wr.grad, rtol=1e-4, atol=1e-3)
+    # pass-through form (drl_rmsnorm_bwd_ex): dx_in read, dx written, bf16 copy from the same pass — bit-identical
+    # to the in-place form and to torch's bf16 rounding of it
+    res = torch.randn(N, H, device=DEV, generator=g)
+    ref = res.clone()
+    native.rmsnorm_bwd(x, w, rstd, dy, ref, torch.zeros(H, device=DEV))
+    out, lp, dw2 = torch.empty_like(res), torch.empty(N, H, device=DEV, dtype=torch.bfloat16), torch.zeros(H, device=DEV)
+    native.rmsnorm_bwd(x, w, rstd, dy, out, dw2, dx_in=res, dx_bf16=lp)
+    assert torch.equal(out, ref) and torch.equal(lp, ref.to(torch.bfloat16))
+    zero = torch.zeros_like(res)
+    native.rmsnorm_bwd(x, w, rstd, dy, zero, torch.zeros(H, device=DEV))
+    native.rmsnorm_bwd(x, w, rstd, dy, out, dw2, dx_in=None)
+    assert torch.equal(out, zero)
 
 
 @pytest.mark.parametrize("I", [4864, 36])  # bf16: 16-B-per-lane path (I % 8 == 0) and the generic one

@@ -182,7 +182,9 @@ def decode_sweep_cold(Bs=(64, 128, 256, 512), L=640, Hkv=2, G=7, D=64, footprint
         n = max(2, -(-footprint // per))
         qs = [torch.randn(B, Hkv, G, D, device=dev, dtype=torch.bfloat16) for _ in range(n)]
         ks = [torch.randn(B, Hkv, 768, D, device=dev, dtype=torch.bfloat16) for _ in range(n)]
-        vts = [torch.randn(B, Hkv, D, 768, device=dev, dtype=torch.bfloat16) for _ in range(n)]
+        # the rollout's key-blocked V^T cache (KVCache); DECODE_VT_PLAIN=1 for the head-dim-major layout
+        vshape = (B, Hkv, D, 768) if os.environ.get("DECODE_VT_PLAIN") == "1" else (B, Hkv, 24, D, 32)
+        vts = [torch.randn(*vshape, device=dev, dtype=torch.bfloat16) for _ in range(n)]
         valid = torch.ones(B, 768, dtype=torch.uint8, device=dev)
         out = torch.empty_like(qs[0])
 
@@ -219,7 +221,9 @@ def decode_split_sweep(Bs=(64, 128), L=640, Hkv=2, G=7, D=64, footprint=768 << 2
         n = max(2, -(-footprint // per))
         qs = [torch.randn(B, Hkv, G, D, device=dev, dtype=torch.bfloat16) for _ in range(n)]
         ks = [torch.randn(B, Hkv, 768, D, device=dev, dtype=torch.bfloat16) for _ in range(n)]
-        vts = [torch.randn(B, Hkv, D, 768, device=dev, dtype=torch.bfloat16) for _ in range(n)]
+        # the rollout's key-blocked V^T cache (KVCache); DECODE_VT_PLAIN=1 for the head-dim-major layout
+        vshape = (B, Hkv, D, 768) if os.environ.get("DECODE_VT_PLAIN") == "1" else (B, Hkv, 24, D, 32)
+        vts = [torch.randn(*vshape, device=dev, dtype=torch.bfloat16) for _ in range(n)]
         valid = torch.ones(B, 768, dtype=torch.uint8, device=dev)
         out = torch.empty_like(qs[0])
 
