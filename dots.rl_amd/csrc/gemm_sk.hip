@@ -43,6 +43,12 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ bf16x8 as_bf16x8(u16x8 v) { return __builtin_bit_cast(bf16x8, v); }
 __device__ __forceinline__ uint16_t to_bf16_bits(float f) { return __builtin_bit_cast(uint16_t, static_cast<__bf16>(f)); }
 __device__ __forceinline__ float bf16r(float f) { return bf16_to_f32(to_bf16_bits(f)); }
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+// two f32 -> packed bf16 pair (one v_cvt_pk_bf16_f32; the rounding of to_bf16_bits)
+__device__ __forceinline__ uint32_t pk_bf16(float lo, float hi) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_t{lo, hi}, bf16x2_t));
+}
 
 constexpr int EPI_NONE = 0, EPI_BIAS = 1, EPI_SWIGLU = 2, EPI_F32 = 3, EPI_SWIGLU_BWD = 4;
 constexpr int HT = 128 * 64, BUF = 4 * HT;  // half-tile, k-tile buffer (elements)
@@ -352,6 +358,9 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
       const int ch = lane & 3, col = n0 / 2 + wc * 32 + ch * 8;
       const bool vec = col + 8 <= half && (g.ldc & 7) == 0 && (reinterpret_cast<uintptr_t>(g.c) & 15) == 0 &&
                        (!g.c2 || ((g.ldc2 & 7) == 0 && (half & 7) == 0 && (reinterpret_cast<uintptr_t>(g.c2) & 15) == 0));
+      const bool interior = m0 + 256 <= g.M && n0 / 2 + 128 <= half && (g.ldc & 7) == 0 &&
+                            (reinterpret_cast<uintptr_t>(g.c) & 15) == 0 &&
+                            (!g.c2 || ((g.ldc2 & 7) == 0 && (half & 7) == 0 && (reinterpret_cast<uintptr_t>(g.c2) & 15) == 0));
 #pragma unroll
       for (int qm = 0; qm < 2; ++qm) {
 #pragma unroll
@@ -374,6 +383,22 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
             }
           }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (interior) {  // whole tile inside (uniform): one row base per output, rows 16 apart, no per-row tests
+          const int64_t m = m0 + qm * 128 + wr * 64 + (lane >> 2);
+          uint16_t* pa = g.c + m * g.ldc + col;
+          uint16_t* pg = g.c2 ? g.c2 + m * g.ldc2 + col : nullptr;
+#pragma unroll
+          for (int it = 0; it < 4; ++it) {
+            const int o = (it * 16 + (lane >> 2)) * SLD + ch * 8;
+            *reinterpret_cast<u16x8*>(pa + it * 16 * g.ldc) = *reinterpret_cast<const u16x8*>(st + o);
+            if (pg) {
+              *reinterpret_cast<u16x8*>(pg + it * 16 * g.ldc2) = *reinterpret_cast<const u16x8*>(st + REG + o);
+              *reinterpret_cast<u16x8*>(pg + it * 16 * g.ldc2 + half) = *reinterpret_cast<const u16x8*>(st + 2 * REG + o);
+            }
+          }
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          continue;
+        }
 #pragma unroll
         for (int it = 0; it < 4; ++it) {
           const int lr = it * 16 + (lane >> 2);
@@ -413,6 +438,8 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
       const bool vec = col + 8 <= g.N && (g.ldc & 7) == 0 && (reinterpret_cast<uintptr_t>(g.c) & 15) == 0 &&
                        (EPI != EPI_SWIGLU_BWD || ((g.ldc2 & 7) == 0 && (g.N & 7) == 0 &&
                                                   (reinterpret_cast<uintptr_t>(g.c2) & 15) == 0));
+      const bool interior = m0 + 256 <= g.M && n0 + 256 <= g.N && (g.ldc & 7) == 0 &&
+                            (reinterpret_cast<uintptr_t>(g.c) & 15) == 0;
 #pragma unroll
       for (int qm = 0; qm < 2; ++qm) {
 #pragma unroll
@@ -427,13 +454,31 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
             }
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-              u16x4 w4;
-#pragma unroll
-              for (int e = 0; e < 4; ++e) w4[e] = to_bf16_bits(acc[qm][qn][i][j][e] + bb[e]);
-              *reinterpret_cast<u16x4*>(st + (i * 16 + fr) * SLD + lc) = w4;
+              const f32x4 v = acc[qm][qn][i][j];
+              // two v_cvt_pk_bf16_f32 per block (no bias: no +0.0 adds, which the compiler must keep for -0.0)
+              uint2 w;
+              if constexpr (EPI == EPI_BIAS) {
+                w.x = pk_bf16(v[0] + bb[0], v[1] + bb[1]);
+                w.y = pk_bf16(v[2] + bb[2], v[3] + bb[3]);
+              } else {
+                w.x = pk_bf16(v[0], v[1]);
+                w.y = pk_bf16(v[2], v[3]);
+              }
+              *reinterpret_cast<uint2*>(st + (i * 16 + fr) * SLD + lc) = w;
             }
           }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (EPI != EPI_SWIGLU_BWD && interior && !(g.dbg & 2)) {
+          // whole tile inside C (uniform): one row base, rows 8 apart, no per-row tests
+          uint16_t* dst = g.c + static_cast<int64_t>(m0 + qm * 128 + wr * 64 + (lane >> 3)) * g.ldc + col;
+          const int64_t step = 8 * g.ldc;
+#pragma unroll
+          for (int it = 0; it < 8; ++it)
+            *reinterpret_cast<u16x8*>(dst + it * step) =
+                *reinterpret_cast<const u16x8*>(st + (it * 8 + (lane >> 3)) * SLD + ch * 8);
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          continue;
+        }
 #pragma unroll
         for (int it = 0; it < 8; ++it) {
           const int lr = it * 8 + (lane >> 3);
