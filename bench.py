@@ -322,6 +322,11 @@ def main():
             "roofline": roofline,
             "roofline_k1": None,
             "cpu_baseline": None,
+            # device memory of this rank over the run (caching allocator): a high retry count means the passes are
+            # sized past what the pool can serve without freeing and re-allocating
+            "memory": {"max_allocated_gb": torch.cuda.max_memory_allocated() / 2 ** 30,
+                       "max_reserved_gb": torch.cuda.max_memory_reserved() / 2 ** 30,
+                       "alloc_retries": torch.cuda.memory_stats().get("num_alloc_retries", 0)},
         }
         if not args.tiny:
             # the actor's form: update_policy hands K1 every micro-batch's sum(response_mask) (one pass over HBM)
