@@ -274,6 +274,10 @@ def main():
     resp_tokens = sum(h["perf/rollout_tokens_per_sec"] * h["timing_s/gen"] for h in hist)
     gen_time = sum(h["timing_s/gen"] for h in hist)
     n_launch, t_launch, b_launch = timer.summary()
+    # the rate of the kernel's work while any of its launches runs: launches on the side stream (weight gradients)
+    # overlap the current stream's, so the mean per-launch interval (mean_launch_us, comparable to rocprof's
+    # per-kernel average) counts shared time twice; achieved uses the union of the intervals instead
+    t_busy = timer.busy_seconds() / n_launch if n_launch else None
     if rank == 0:
         ar = cfg.actor_rollout_ref
         preset = str(ar.model.get("path", "random:qwen2.5-0.5b"))
@@ -288,7 +292,7 @@ def main():
         metric = METRIC.replace("Qwen2.5-0.5B GRPO", f"{model_name} {algo}")
         _, per_unit, bound, peak, unit = ROOFLINE[args.roofline_kernel]
         scale = 1e12 if unit == "TFLOP/s" else 1e9
-        achieved = b_launch / t_launch / scale if n_launch else None
+        achieved = b_launch / t_busy / scale if n_launch else None
         # the committed PMC pass is of the default workload (N=1 config #2): attach it only to that workload
         default_workload = not args.tiny and not args.override and args.gpus == 1
         traffic, traffic_src = _pmc_traffic(args.roofline_kernel) if default_workload else (None, None)
@@ -296,6 +300,7 @@ def main():
                     "unit": unit, "frac": achieved / peak if achieved else None, "traffic": traffic,
                     "algorithmic_work_per_launch": b_launch if n_launch else None,
                     "mean_launch_us": t_launch * 1e6 if n_launch else None, "launches": n_launch,
+                    "busy_us_per_launch": t_busy * 1e6 if n_launch else None,
                     "per_unit": per_unit, "traffic_source": traffic_src}
         line = {
             "metric": metric,

@@ -287,9 +287,14 @@ __device__ __forceinline__ void tiled_epilogue(const DgArgs& a, const f32x16 (&a
 // accumulators: fp32 partials (K slice = gridDim.y), SwiGLU (gate row i and up row i + 16 of a block sit in
 // registers r and r + 8 of the same lane; one lane-half exchange forms the packed 16-B pieces), or bias +
 // RoPE + KV-cache writes (rotation pairs likewise lane-local).
+// ring depth: 8 k-steps in flight for qkv + RoPE's 1-2-fragment wave tiles (one K slice, so its 56-step k chain
+// per wave is latency-bound: 15.2 -> 14.3 us at 512 rows, tools/decode_cfg_sweep.py), 4 elsewhere (a deeper ring
+// there rules out the K slices those shapes need to fill the chip: o_proj 6.9 -> 10.0 us, down 14.5 -> 26.3)
+constexpr int dt_depth(int wb, int tb, int epi) { return epi == EPI_ROPE && wb * tb <= 2 ? 8 : 4; }
+
 template <int WB, int TB, int WW, int WT, int EPI>
 __global__ __launch_bounds__(256) void decode_gemm_tiled_kernel(DgArgs a) {
-  constexpr int DEPTH = 4;
+  constexpr int DEPTH = dt_depth(WB, TB, EPI);
   static_assert(WW * WT == 4, "4 waves per workgroup");
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int ww = wave % WW, wt = wave / WW;
@@ -687,7 +692,8 @@ bool plan_decode_tiled(int64_t M, int64_t N, int64_t K, int epi, DgPlan& p) {
   bool found = false;
   int64_t best_wgs = 0;
   for (int ks = 1; ks <= (epi == EPI_PARTIAL && g_dt_mode == 1 ? 4 : 1); ++ks) {
-    if (nks % ks != 0 || (nks / ks) % 4 != 0) continue;  // register ring: DEPTH 4; LDS stages: 2 k-steps
+    // register ring: dt_depth k-steps per refill round; LDS stages: 2 k-steps
+    if (nks % ks != 0 || (nks / ks) % (c.lds ? 4 : dt_depth(c.wb, c.tb, epi)) != 0) continue;
     const int64_t wgs = base * ks;
     if (found && best_wgs >= 160) break;  // the fewest slices that fill the chip
     if (!found || wgs > best_wgs) {

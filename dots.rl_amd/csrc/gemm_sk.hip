@@ -894,8 +894,11 @@ int drl_gemm(const void* a, int64_t lda, int32_t a_layout, const void* b, int64_
     g.dp_tiles = 0;
     grid = g.n_tiles * S;
   } else if (mode == 2) {
+    // whole tiles, one workgroup per tile (no workgroup waits on another, so no co-residency is needed): the hardware
+    // deals tiles to CUs as they free up, so a kernel on a second stream (the weight gradient beside its input
+    // gradient) fills the CUs a short grid leaves idle instead of waiting behind a persistent grid's static rounds
     g.dp_tiles = g.n_tiles;
-    grid = std::min(cap, g.n_tiles);
+    grid = g_sk.grid > 0 ? std::min(cap, g.n_tiles) : g.n_tiles;
   } else {
     const int full = g.n_tiles / grid;
     const int dp = (g.n_tiles % grid == 0) ? g.n_tiles : std::max(0, full - 1) * grid;

@@ -63,10 +63,27 @@ class KernelTimer:
         """(launches, mean seconds per launch, mean algorithmic bytes per launch)."""
         if not self.events:
             return 0, float("nan"), float("nan")
-        self.events[-1][1].synchronize()
+        torch.cuda.synchronize()
         tot = sum(a.elapsed_time(b) for a, b in self.events) * 1e-3
         n = len(self.events)
         return n, tot / n, sum(self.nbytes) / n
+
+    def busy_seconds(self):
+        """Length of the union of the launch intervals: launches on two streams (a weight gradient beside its input
+        gradient) overlap, and each one's own interval then includes the time it shared the CUs."""
+        if not self.events:
+            return float("nan")
+        torch.cuda.synchronize()
+        t0 = self.events[0][0]
+        iv = sorted((t0.elapsed_time(a), t0.elapsed_time(b)) for a, b in self.events)
+        busy, cur_s, cur_e = 0.0, iv[0][0], iv[0][1]
+        for s_, e_ in iv[1:]:
+            if s_ > cur_e:
+                busy += cur_e - cur_s
+                cur_s, cur_e = s_, e_
+            else:
+                cur_e = max(cur_e, e_)
+        return (busy + cur_e - cur_s) * 1e-3
 
 
 class _TimedLib:

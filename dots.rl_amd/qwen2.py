@@ -334,10 +334,11 @@ def acc_wgrad(gw, dy, x):
 
 
 # The weight gradient of a projection runs on a side stream while its input gradient runs on the current one: the
-# pair's workgroups share the CUs (at 6144 rows: qkv 160 + 96, gate_up 152 + 96 of 256) where each alone leaves most
-# of them idle. Measured no faster under fused micro-batch execution (3.385 vs 3.388 s per step,
-# tools/gpu_r03k.sh): off by default, DRL_CONCURRENT_WGRAD=1 turns it on.
-CONCURRENT_WGRAD = os.environ.get("DRL_CONCURRENT_WGRAD", "0") != "0"
+# pair's workgroups share the CUs (gate_up's weight gradient is 152 tiles of 256 x 256 at any row count, the other
+# 104 CUs otherwise idle for its ~2 ms). It pays since whole-tile drl_gemm launches one workgroup per tile (the
+# hardware deals tiles to CUs as they free up; a persistent grid's static rounds could not take the idle CUs):
+# update 1.44 -> 1.38 s (tools/gpu_r03aa.sh). DRL_CONCURRENT_WGRAD=0 turns it off.
+CONCURRENT_WGRAD = os.environ.get("DRL_CONCURRENT_WGRAD", "1") != "0"
 _SIDE_STREAMS = {}
 
 

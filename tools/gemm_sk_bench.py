@@ -60,12 +60,15 @@ def main():
     ap.add_argument("--rows", type=int, nargs="*", default=None, help="token rows of the training passes")
     ap.add_argument("--no-lib", action="store_true", help="skip the hipBLASLt timing")
     ap.add_argument("--decode", type=int, default=None, help="only the decode-step shapes at this many rows")
+    ap.add_argument("--only", nargs="*", default=None, help="only these shape names (e.g. gate_up_wgrad o_wgrad)")
     args = ap.parse_args()
     from dots.rl_amd.workers import _enable_gemm_tuning
     _enable_gemm_tuning("auto")
     dev, bf = "cuda", torch.bfloat16
     g = torch.Generator(device=dev).manual_seed(0)
     for name, kind, M, N, K in shapes(args.quick, args.rows, args.decode):
+        if args.only and name not in args.only:
+            continue
         fl = 2.0 * M * N * K
         if kind in ("fwd", "swiglu") and args.decode:
             # decode: weights rotate over > 600 MB of copies (each call streams W from HBM, as in the step)
@@ -103,7 +106,7 @@ def main():
         if args.tune:
             sweep = {}
             for grid, mode, param in [(0, 1, 0), (0, 1, 8), (0, 1, 32), (0, 2, 0), (0, 3, 2), (0, 3, 4), (0, 3, 8),
-                                      (0, 3, 16)]:
+                                      (0, 3, 16), (0, 3, 32)]:
                 if mode == 3 and param and param * (M + 255) // 256 * ((N + 255) // 256) > 256:
                     continue
                 native.lib().drl_gemm_set_sk_tuning(grid, 0, mode, param)
