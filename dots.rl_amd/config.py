@@ -92,6 +92,7 @@ DEFAULTS = dict(
             use_hip_graph=True,  # decode steps replayed from one captured HIP graph (rollout.py)
             packed_decode=True, packed_decode_max_rows=512,  # qwen2.PackedDecode (fragment-packed operands)
             fused_select=False,  # lm_head fused with K4 (csrc/fused_linear.hip)
+            decode_lanes=1,  # row groups of the graphed decode step on concurrent streams (rollout._decode_lanes)
         ),
         ref=dict(log_prob_micro_batch_size=None, log_prob_micro_batch_size_per_gpu=16, log_prob_use_dynamic_bsz=False,
                  log_prob_max_token_len_per_gpu=16384, exec_log_prob_tokens=196608),

@@ -440,7 +440,7 @@ __global__ __launch_bounds__(128) void dec_rmsnorm_kernel(const float* x_in, con
   const int64_t row = blockIdx.x;
   const int tid = threadIdx.x;
   const int64_t nch = H / 8;
-  float4 xv[CH][2];
+  float4 xv[CH][2], wv[CH][2];
   constexpr int NSL = NS > 0 ? NS : 1;
   float4 pv[CH][NSL][2];
 #pragma unroll
@@ -449,6 +449,9 @@ __global__ __launch_bounds__(128) void dec_rmsnorm_kernel(const float* x_in, con
     if (ch < nch) {
       xv[c][0] = *reinterpret_cast<const float4*>(x_in + row * H + ch * 8);
       xv[c][1] = *reinterpret_cast<const float4*>(x_in + row * H + ch * 8 + 4);
+      // the norm weight with the row's first loads: no second memory round trip after the row sum
+      wv[c][0] = *reinterpret_cast<const float4*>(w + ch * 8);
+      wv[c][1] = *reinterpret_cast<const float4*>(w + ch * 8 + 4);
       if constexpr (NS > 0) {
 #pragma unroll
         for (int k = 0; k < NS; ++k) {
@@ -501,9 +504,10 @@ __global__ __launch_bounds__(128) void dec_rmsnorm_kernel(const float* x_in, con
   for (int c = 0; c < CH; ++c) {
     const int64_t ch = tid + 128 * c;
     if (ch >= nch) continue;
+    const float wj[8] = {wv[c][0].x, wv[c][0].y, wv[c][0].z, wv[c][0].w, wv[c][1].x, wv[c][1].y, wv[c][1].z, wv[c][1].w};
     u16x8 o;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = f32_to_bf16(w[ch * 8 + j] * (v[c][j] * r));
+    for (int j = 0; j < 8; ++j) o[j] = f32_to_bf16(wj[j] * (v[c][j] * r));
     uint16_t* dst = MBT > 0 ? y + pk_off(row, ch * 8, MBT) : y + row * H + ch * 8;
     *reinterpret_cast<u16x8*>(dst) = o;
   }
@@ -893,7 +897,7 @@ int drl_decode_rmsnorm(const float* x_in, const float* partials, int32_t nsplit,
   DRL_CHECK_ARG(M >= 1 && H >= 8 && H % 8 == 0 && H <= 8 * 128 * 4, "bad shape (H %% 8 == 0, H <= 4096)");
   DRL_CHECK_ARG(partials == nullptr || nsplit >= 1, "nsplit < 1");
   DRL_CHECK_ARG(mbt == 0 || mbt * 32 >= M, "mbt too small");
-  DRL_CHECK_ARG(aligned16(x_in) && aligned16(y) && (x_out == nullptr || aligned16(x_out)) &&
+  DRL_CHECK_ARG(aligned16(x_in) && aligned16(y) && aligned16(weight) && (x_out == nullptr || aligned16(x_out)) &&
                     (partials == nullptr || aligned16(partials)),
                 "16-byte aligned buffers needed");
   const int ch = static_cast<int>((H / 8 + 127) / 128);

@@ -440,6 +440,115 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
                                                   (reinterpret_cast<uintptr_t>(g.c2) & 15) == 0));
       const bool interior = m0 + 256 <= g.M && n0 + 256 <= g.N && (g.ldc & 7) == 0 &&
                             (reinterpret_cast<uintptr_t>(g.c) & 15) == 0;
+      if constexpr (EPI == EPI_SWIGLU_BWD) {
+        // the down_proj dgrad fused with the SwiGLU backward. Per quadrant: stage bf16(d a) through LDS, then read
+        // the saved gate / up of the same columns and write dgu. Lambdas called with constants (not loops): the
+        // accumulator indices stay static (a loop here left them in scratch).
+        auto stage = [&](const int qm) __attribute__((always_inline)) {
+#pragma unroll
+            for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+              for (int j = 0; j < 2; ++j) {
+                const int lc = qn * 32 + j * 16 + 4 * fq;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                  const f32x4 v = acc[qm][qn][i][j];
+                  uint2 w;
+                  w.x = pk_bf16(v[0], v[1]);
+                  w.y = pk_bf16(v[2], v[3]);
+                  *reinterpret_cast<uint2*>(st + (i * 16 + fr) * SLD + lc) = w;
+                }
+              }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        };
+        // whole tile inside (uniform): the 8 row pieces' gate / up loads go out in two batches of 4 (8 x 16 B in
+        // flight per lane, one row base per operand) instead of 2 loads behind each row's bounds test
+        auto fast = [&](const int qm) __attribute__((always_inline)) {
+            const int64_t m = m0 + qm * 128 + wr * 64 + (lane >> 3);
+            const uint16_t* gp = g.c2 + m * g.ldc2 + col;
+            uint16_t* dp = g.c + m * g.ldc + col;
+            const int64_t sg = 8 * g.ldc2, sd = 8 * g.ldc;
+            auto one = [&](int it, u32x4 gw, u32x4 uw) __attribute__((always_inline)) {
+              const u16x8 v = *reinterpret_cast<const u16x8*>(st + (it * 8 + (lane >> 3)) * SLD + ch * 8);
+              const u16x8 gv = __builtin_bit_cast(u16x8, gw), uv = __builtin_bit_cast(u16x8, uw);
+              u16x8 dg, du;
+#pragma unroll
+              for (int e = 0; e < 8; ++e) {  // swiglu_bwd's math and roundings (as the row path below)
+                const float d = bf16_to_f32(v[e]), gg = bf16_to_f32(gv[e]), uu = bf16_to_f32(uv[e]);
+                const float sig = sigmoid_fast(gg);
+                dg[e] = to_bf16_bits(bf16r(d * uu) * (sig * (1.f + gg * (1.f - sig))));
+                du[e] = to_bf16_bits(d * bf16r(gg * sig));
+              }
+              *reinterpret_cast<u16x8*>(dp + it * sd) = dg;
+              *reinterpret_cast<u16x8*>(dp + it * sd + g.N) = du;
+            };
+#pragma unroll
+            for (int hb = 0; hb < 2; ++hb) {
+              const u32x4 g0 = *reinterpret_cast<const u32x4*>(gp + (4 * hb + 0) * sg);
+              const u32x4 u0 = *reinterpret_cast<const u32x4*>(gp + (4 * hb + 0) * sg + g.N);
+              const u32x4 g1 = *reinterpret_cast<const u32x4*>(gp + (4 * hb + 1) * sg);
+              const u32x4 u1 = *reinterpret_cast<const u32x4*>(gp + (4 * hb + 1) * sg + g.N);
+              const u32x4 g2 = *reinterpret_cast<const u32x4*>(gp + (4 * hb + 2) * sg);
+              const u32x4 u2 = *reinterpret_cast<const u32x4*>(gp + (4 * hb + 2) * sg + g.N);
+              const u32x4 g3 = *reinterpret_cast<const u32x4*>(gp + (4 * hb + 3) * sg);
+              const u32x4 u3 = *reinterpret_cast<const u32x4*>(gp + (4 * hb + 3) * sg + g.N);
+              one(4 * hb + 0, g0, u0);
+              one(4 * hb + 1, g1, u1);
+              one(4 * hb + 2, g2, u2);
+              one(4 * hb + 3, g3, u3);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        };
+        // any tile: row by row with bounds tests
+        auto rows = [&](const int qm) __attribute__((always_inline)) {
+#pragma unroll
+          for (int it = 0; it < 8; ++it) {
+            const int lr = it * 8 + (lane >> 3);
+            const int m = m0 + qm * 128 + wr * 64 + lr;
+            const u16x8 v = *reinterpret_cast<const u16x8*>(st + lr * SLD + ch * 8);
+            if (m >= g.M || col >= g.N) continue;
+            uint16_t* dstp = g.c + static_cast<int64_t>(m) * g.ldc + col;
+            // v = bf16(d a) of columns col..col+7; gate / up of the same columns from the saved gu row -> dgu
+            // (swiglu_bwd's math and roundings: dg = bf16(d*u) * sig (1 + g (1 - sig)), du = d * bf16(g sig))
+            const uint16_t* gp = g.c2 + static_cast<int64_t>(m) * g.ldc2 + col;
+            u16x8 gq, uq;
+            if (vec) {
+              gq = *reinterpret_cast<const u16x8*>(gp);
+              uq = *reinterpret_cast<const u16x8*>(gp + g.N);
+            } else {
+              for (int e = 0; e < 8; ++e) {
+                gq[e] = col + e < g.N ? gp[e] : 0;
+                uq[e] = col + e < g.N ? gp[g.N + e] : 0;
+              }
+            }
+            u16x8 dg, du;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float d = bf16_to_f32(v[e]), gg = bf16_to_f32(gq[e]), uu = bf16_to_f32(uq[e]);
+              const float sig = sigmoid_fast(gg);
+              dg[e] = to_bf16_bits(bf16r(d * uu) * (sig * (1.f + gg * (1.f - sig))));
+              du[e] = to_bf16_bits(d * bf16r(gg * sig));
+            }
+            if (vec) {
+              *reinterpret_cast<u16x8*>(dstp) = dg;
+              *reinterpret_cast<u16x8*>(dstp + g.N) = du;
+            } else {
+              for (int e = 0; e < 8 && col + e < g.N; ++e) {
+                dstp[e] = dg[e];
+                dstp[g.N + e] = du[e];
+              }
+            }
+          }
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        };
+        const bool whole = interior && vec;
+        stage(0);
+        if (whole) fast(0);
+        else rows(0);
+        stage(1);
+        if (whole) fast(1);
+        else rows(1);
+      } else {
 #pragma unroll
       for (int qm = 0; qm < 2; ++qm) {
 #pragma unroll
@@ -486,38 +595,7 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
           const u16x8 v = *reinterpret_cast<const u16x8*>(st + lr * SLD + ch * 8);
           if (m >= g.M || col >= g.N) continue;
           uint16_t* dstp = g.c + static_cast<int64_t>(m) * g.ldc + col;
-          if constexpr (EPI == EPI_SWIGLU_BWD) {
-            // v = bf16(d a) of columns col..col+7; gate / up of the same columns from the saved gu row -> dgu
-            // (swiglu_bwd's math and roundings: dg = bf16(d*u) * sig (1 + g (1 - sig)), du = d * bf16(g sig))
-            const uint16_t* gp = g.c2 + static_cast<int64_t>(m) * g.ldc2 + col;
-            u16x8 gq, uq;
-            if (vec) {
-              gq = *reinterpret_cast<const u16x8*>(gp);
-              uq = *reinterpret_cast<const u16x8*>(gp + g.N);
-            } else {
-              for (int e = 0; e < 8; ++e) {
-                gq[e] = col + e < g.N ? gp[e] : 0;
-                uq[e] = col + e < g.N ? gp[g.N + e] : 0;
-              }
-            }
-            u16x8 dg, du;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-              const float d = bf16_to_f32(v[e]), gg = bf16_to_f32(gq[e]), uu = bf16_to_f32(uq[e]);
-              const float sig = sigmoid_fast(gg);
-              dg[e] = to_bf16_bits(bf16r(d * uu) * (sig * (1.f + gg * (1.f - sig))));
-              du[e] = to_bf16_bits(d * bf16r(gg * sig));
-            }
-            if (vec) {
-              *reinterpret_cast<u16x8*>(dstp) = dg;
-              *reinterpret_cast<u16x8*>(dstp + g.N) = du;
-            } else {
-              for (int e = 0; e < 8 && col + e < g.N; ++e) {
-                dstp[e] = dg[e];
-                dstp[g.N + e] = du[e];
-              }
-            }
-          } else if (g.dbg & 2) {  // measurement: staging without the output stores
+          if (g.dbg & 2) {  // measurement: staging without the output stores
             if (v[0] == 0x7fffu && v[1] == 0x1234u) dstp[0] = 0;
           } else if (vec) {
             *reinterpret_cast<u16x8*>(dstp) = v;
@@ -526,6 +604,7 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
           }
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      }
       }
     }
     bar();  // staging reads done before the next segment's copies land in LDS

@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import threading
 
 import torch
 
@@ -100,6 +101,39 @@ def _stream():
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 
+# Workspace lane: the graphed decode step can run independent row groups ("lanes") of one rollout on separate
+# streams inside one graph (rollout.MI355XRollout._decode_graphed). Every stateful workspace (zero-state flag /
+# ticket words, the selection scratch, drl_gemm's stream-K slabs) is keyed by the lane, so concurrent lanes never
+# share one; lane 0 is the default everywhere else.
+# The lane is thread-local: concurrent passes issued from two host threads (trainer: old and ref log-probs) each
+# carry their own.
+class _LaneState(threading.local):
+    lane = 0
+
+
+_LANE_STATE = _LaneState()
+
+
+def _lane():
+    return _LANE_STATE.lane
+
+
+class workspace_lane:
+    """Context manager: calls inside (on this host thread) use lane ``j``'s workspaces."""
+
+    def __init__(self, j):
+        self.j = int(j)
+
+    def __enter__(self):
+        self.prev = _LANE_STATE.lane
+        _LANE_STATE.lane = self.j
+        return self
+
+    def __exit__(self, *exc):
+        _LANE_STATE.lane = self.prev
+        return False
+
+
 def _p(t):
     return None if t is None else ctypes.c_void_p(t.data_ptr())
 
@@ -130,7 +164,7 @@ class _Workspace:
         self.buf = {}
 
     def get(self, nbytes: int, device) -> torch.Tensor:
-        key = (device.index if device.index is not None else torch.cuda.current_device())
+        key = (device.index if device.index is not None else torch.cuda.current_device(), _lane())
         b = self.buf.get(key)
         if b is None or b.numel() < nbytes:
             b = torch.empty(max(nbytes, 1 << 16), dtype=torch.uint8, device=device)
@@ -146,7 +180,7 @@ class _ZeroHeaderWorkspace(_Workspace):
     (include/dotsrl_amd.h, drl_ppo_loss_fwd_bwd), so no per-call memset."""
 
     def get(self, nbytes: int, device) -> torch.Tensor:
-        key = (device.index if device.index is not None else torch.cuda.current_device())
+        key = (device.index if device.index is not None else torch.cuda.current_device(), _lane())
         b = self.buf.get(key)
         if b is None or b.numel() < nbytes:
             b = torch.zeros(max(nbytes, 1 << 16), dtype=torch.uint8, device=device)
@@ -507,7 +541,7 @@ _SELECT_WS = {}
 def _select_workspace(device, N):
     """Per-device zeroed int64 buffer (>= N rows) that the selection kernels leave zeroed after each call
     (valid inside captured graphs: calls on one stream reuse it in order)."""
-    key = str(device)
+    key = (str(device), _lane())
     ws = _SELECT_WS.get(key)
     if ws is None or ws.numel() < N:
         if torch.cuda.is_current_stream_capturing():
@@ -794,6 +828,8 @@ class _GemmWorkspace:
         self.buf = {}
 
     def get(self, device, slot=0):
+        if slot == 0 and _lane():
+            slot = ("lane", _lane())
         key = (device.index if device.index is not None else torch.cuda.current_device(), slot)
         b = self.buf.get(key)
         if b is None:
@@ -907,7 +943,7 @@ _LINEAR_WS = {}
 def _linear_workspace(device, nbytes, kind="linear"):
     """Per-device zeroed workspace shared by the split-K decode kernels of one kind on one stream (each call
     leaves its arrival tickets zeroed again, so consecutive calls and graph replays reuse it)."""
-    key = (str(device), kind)
+    key = (str(device), kind, _lane())
     ws = _LINEAR_WS.get(key)
     if ws is None or ws.numel() * 8 < nbytes:
         if torch.cuda.is_current_stream_capturing():

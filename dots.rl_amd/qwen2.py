@@ -393,7 +393,10 @@ class _Linear(torch.autograd.Function):
 
 
 class _Embedding(torch.autograd.Function):
-    """fp32 residual stream input; backward scatter-adds into the fp32 embedding gradient."""
+    """fp32 residual stream input; backward accumulates into the fp32 embedding gradient through aten's
+    embedding_dense_backward (sorted ids, segment sums: deterministic — the nn.Embedding backward the reference runs).
+    An index_add_ scatter is atomic on the GPU: its summation order changed run to run (tools/probes/det_probe2.py:
+    ~1500 of the 131072 tiny-model embedding-gradient entries differed between identical steps)."""
 
     @staticmethod
     def forward(ctx, ids, w, gw, dummy):
@@ -405,7 +408,9 @@ class _Embedding(torch.autograd.Function):
     def backward(ctx, dy):
         (ids,) = ctx.saved_tensors
         if ctx.gw is not None:
-            ctx.gw.index_add_(0, ids.reshape(-1), dy.reshape(-1, dy.shape[-1]).to(torch.float32))
+            g = torch.ops.aten.embedding_dense_backward(dy.reshape(-1, dy.shape[-1]).to(torch.float32),
+                                                        ids.reshape(-1), ctx.gw.shape[0], -1, False)
+            ctx.gw.add_(g)
         return None, None, None, None
 
 
@@ -723,6 +728,19 @@ def _key_valid(attention_mask):
     return buf[:, :T]
 
 
+class KVCacheRows:
+    """Rows [r0, r1) of a KVCache as a KVCache-shaped view (dim-0 slices: contiguous, the same strides), for one
+    row lane of the graphed decode step."""
+
+    def __init__(self, cache, r0, r1):
+        self.k = [t[r0:r1] for t in cache.k]
+        self.vt = [None if t is None else t[r0:r1] for t in cache.vt]
+        self.v = [None if t is None else t[r0:r1] for t in cache.v]
+        self.valid = cache.valid[r0:r1]
+        self.len = cache.len
+        self.Tmax = cache.Tmax
+
+
 class KVCache:
     """Per-layer K (B, Hkv, Tmax, D) and V (bf16: head-dim-major in 32-key blocks (B, Hkv, ceil(Tmax / 32), D, 32);
     fp32: row-major) in the compute dtype, plus the key-valid mask (u8)."""
@@ -898,7 +916,9 @@ class PackedDecode:
                         for n, k, sw in ((NQ, H, False), (H, cfg.num_attention_heads * D, False), (2 * I, H, True),
                                          (H, I, False))))
 
-    def __init__(self, model, B):
+    def __init__(self, model, B, weights=None):
+        """``weights``: another PackedDecode's packed weights (the layout does not depend on B), shared by the
+        row lanes of one rollout instead of packed again."""
         cfg, s, dev = model.cfg, model.store, model.store.device
         self.model = model
         self.B = B
@@ -911,8 +931,8 @@ class PackedDecode:
         self.mbt = self.plans["o"][1]
         assert all(p[1] == self.mbt for p in self.plans.values())
         bf = torch.bfloat16
-        self.w = []
-        for i in range(cfg.num_hidden_layers):
+        self.w = weights if weights is not None else []
+        for i in range(0 if weights is not None else cfg.num_hidden_layers):
             p = f"layers.{i}."
             self.w.append(dict(qkv=native.decode_pack_weight_rope(s.w(p + "qkv_proj.weight"), D),
                                o=native.decode_pack_weight(s.w(p + "o_proj")),

@@ -16,7 +16,7 @@ import torch
 
 from . import native
 from .protocol import DataProto, TensorBatch
-from .qwen2 import KVCache, PackedDecode, Qwen2Model
+from .qwen2 import KVCache, KVCacheRows, PackedDecode, Qwen2Model
 from .torch_functional import get_response_mask
 
 
@@ -115,6 +115,9 @@ class MI355XRollout:
         t_dev = torch.ones(1, dtype=torch.int64, device=responses.device)
         B = responses.shape[0]
         max_rows = int(self.config.get("packed_decode_max_rows", 512))
+        lanes = self._decode_lanes(B, max_rows)
+        if lanes > 1:
+            return self._decode_graphed_lanes(cache, responses, last_pos, P, R, sel, lanes)
         use = self.config.get("packed_decode", True) and PackedDecode.supported(m, B, max_rows)
         packed = PackedDecode(m, B) if use else None
         self.last_packed_decode = packed is not None
@@ -143,3 +146,66 @@ class MI355XRollout:
         for _ in range(2, R):
             graph.replay()
         del graph, packed
+
+    def _decode_lanes(self, B, max_rows):
+        """Row lanes of the graphed decode step (config ``decode_lanes``): the rows split into equal groups of
+        whole 32-row blocks, each group's decode step on its own stream of one graph. Every per-token kernel is
+        row-independent (per-row attention, per-row GEMM outputs, per-row selection), so the lanes compute the
+        same tokens as one B-row step; their latency-bound kernels overlap instead of running back to back."""
+        m = self.module
+        lanes = int(self.config.get("decode_lanes", 1) or 1)
+        if lanes <= 1 or B % (32 * lanes) != 0:
+            return 1
+        if not (self.config.get("packed_decode", True) and self.config.get("decode_prologue", True)
+                and m.store.w("embed_tokens").dtype == torch.bfloat16
+                and PackedDecode.supported(m, B // lanes, max_rows)):
+            return 1
+        return lanes
+
+    def _decode_graphed_lanes(self, cache, responses, last_pos, P, R, sel, lanes):
+        """_decode_graphed over ``lanes`` row groups: lane j owns rows [j * B / lanes, (j + 1) * B / lanes) — its
+        KV-cache rows, responses rows, step counter, PackedDecode buffers (the packed weights are shared) and
+        workspaces (native.workspace_lane) — and its step is captured on its own stream, forked from and joined
+        to the capture stream, so one replay runs all lanes' steps concurrently. Sampling stays row-identical:
+        lane j's Philox rows start at row_base + j * B / lanes."""
+        m = self.module
+        B = responses.shape[0]
+        rows = B // lanes
+        dev = responses.device
+        last_pos_flat = last_pos.reshape(-1).contiguous()
+        lane_state = []
+        shared_w = None
+        for j in range(lanes):
+            r0, r1 = j * rows, (j + 1) * rows
+            pk = PackedDecode(m, rows, weights=shared_w)
+            shared_w = pk.w
+            sel_j = dict(sel, row_base=sel["row_base"] + r0, unfinished=sel["unfinished"][r0:r1])
+            lane_state.append(dict(cache=KVCacheRows(cache, r0, r1), resp=responses[r0:r1], pk=pk, sel=sel_j,
+                                   last_pos=last_pos_flat[r0:r1].contiguous(),
+                                   t_dev=torch.ones(1, dtype=torch.int64, device=dev)))
+        self.last_packed_decode = True
+
+        def body(j):
+            st = lane_state[j]
+            with native.workspace_lane(j):
+                h = st["pk"].step_from(st["cache"], st["resp"], st["t_dev"], st["last_pos"], P)
+                m.select_tokens(h, st["resp"][:, 0], fused=self._fused_select, step=0, dev_step=st["pk"].t_cur,
+                                **st["sel"])
+
+        for j in range(lanes):  # t = 1, eager (sizes every lane's workspaces outside capture)
+            body(j)
+        side = [torch.cuda.Stream(device=dev) for _ in range(lanes - 1)]
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            main = torch.cuda.current_stream()
+            for s in side:
+                s.wait_stream(main)
+            body(0)
+            for j, s in enumerate(side, start=1):
+                with torch.cuda.stream(s):
+                    body(j)
+            for s in side:
+                main.wait_stream(s)
+        for _ in range(2, R):
+            graph.replay()
+        del graph, lane_state

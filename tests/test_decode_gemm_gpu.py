@@ -332,3 +332,51 @@ def test_linear_select_matches_unfused(N, H, V):
     if N > 1:
         assert unf[-1].item() == 0
     assert torch.equal(out[1:], a[1:]) or N == 1
+
+
+@pytest.mark.parametrize("lanes,do_sample", [(2, False), (2, True), (4, True)])
+def test_decode_lanes_equal_per_lane_eager_steps(lanes, do_sample):
+    """Row lanes of the graphed decode step (rollout.decode_lanes: each row group's step on its own stream of one
+    graph, packed weights shared, workspaces per lane) produce exactly what eager packed steps of each row group
+    produce on the same prefilled cache: identical responses, greedy or sampled (lane j's Philox rows start at
+    row_base + j * B / lanes)."""
+    from dots.rl_amd.config import to_attr
+    from dots.rl_amd.protocol import DataProto
+    from dots.rl_amd.qwen2 import KVCache, KVCacheRows, PackedDecode
+    from dots.rl_amd.rollout import MI355XRollout
+
+    B, P, R = 32 * lanes, 16, 12
+    cfg, m = _small_model(seed=4)
+    g = torch.Generator(device=DEV).manual_seed(6)
+    ids = torch.randint(3, 512, (B, P), device=DEV, generator=g)
+    am = torch.ones(B, P, dtype=torch.int64, device=DEV)
+    for b in range(0, B, 5):
+        am[b, : (b % 6)] = 0
+    ids = torch.where(am == 0, torch.zeros_like(ids), ids)
+    pos = (am.cumsum(-1) - 1).clamp_min(0)
+    seed, temp = 21, 0.8
+    rcfg = to_attr(dict(do_sample=do_sample, temperature=temp, top_k=-1, top_p=1.0, response_length=R,
+                        ignore_eos=True, seed=seed, val_kwargs={}, use_hip_graph=True, packed_decode=True,
+                        decode_lanes=lanes))
+    ro = MI355XRollout(m, rcfg)
+    assert ro._decode_lanes(B, 512) == lanes
+    out = ro.generate_sequences(DataProto.from_dict({"input_ids": ids, "attention_mask": am, "position_ids": pos},
+                                                    meta_info={"eos_token_id": 2, "pad_token_id": 0}))
+    resp = out.batch["responses"]
+    # eager reference: one prefill of all B rows, then each row group stepped by its own PackedDecode
+    cache = KVCache(cfg, B, P + R, DEV, BF)
+    h = m.prefill(cache, ids, am, pos)
+    sel = dict(do_sample=do_sample, temperature=temp if do_sample else 1.0, top_k=0, top_p=1.0, seed=seed,
+               pad_token_id=0)
+    toks = torch.empty(B, R, dtype=torch.int64, device=DEV)
+    m.select_tokens(h, toks[:, 0], fused=False, step=0, row_base=0, **sel)
+    rows = B // lanes
+    pks = [PackedDecode(m, rows) for _ in range(lanes)]
+    for t in range(1, R):
+        kd = torch.tensor([P + t - 1], device=DEV)
+        for j in range(lanes):
+            r0, r1 = j * rows, (j + 1) * rows
+            cj = KVCacheRows(cache, r0, r1)
+            hj = pks[j].step(cj, toks[r0:r1, t - 1:t], pos[r0:r1, -1] + t, kd)
+            m.select_tokens(hj, toks[r0:r1, t], fused=False, step=t, row_base=r0, **sel)
+    assert torch.equal(resp, toks)

@@ -69,3 +69,16 @@ def test_policy_loss_modes_step_end_to_end(loss_mode):
         assert k in m and np.isfinite(m[k]), (k, m.get(k))
     if w0 is not None:
         assert not torch.equal(w0, trainer.actor_rollout_wg.worker.actor_store.master)
+
+
+
+def test_update_step_bit_reproducible():
+    """Two identical trainer steps (fresh trainers, same seeds) end with bit-identical parameters: every kernel of
+    the update is deterministic, including the embedding backward (tied lm_head) and the weight gradients that run
+    on a side stream concurrently with their input gradients."""
+    masters = []
+    for _ in range(2):
+        trainer = _trainer("grpo", ["actor_rollout_ref.actor.use_kl_loss=True"])
+        trainer.fit(num_steps=1)
+        masters.append(trainer.actor_rollout_wg.worker.store.master.clone())
+    assert torch.equal(masters[0], masters[1]), (masters[0] - masters[1]).abs().max().item()
