@@ -643,8 +643,13 @@ bool plan_decode_gemm(int64_t M, int64_t N, int64_t K, int epi, DgPlan& p) {
     const bool ok = wgs >= 96;
     bool take = !found;
     if (found) {
+      // among shapes that fill the chip: the fewest K slices, then one-block workgroups (twice the workgroups on the
+      // same K slices) — measured faster at 64 / 256 / 512 rows for qkv + RoPE (512 rows: 10.7 -> 9.7 us), o_proj
+      // (256 rows: 7.7 -> 5.5) and down_proj (13.4 vs 37.3), profiles/r03_decode_cfg_sweep2.jsonl — except the
+      // SwiGLU gate_up, whose 2-block workgroups feed each weight fragment to two MFMAs (64 rows: 8.1 vs 9.0 us)
+      const bool more_blocks = epi == EPI_SWIGLU ? c.mb > p.mb : c.mb < p.mb;
       if (ok && !full) take = true;
-      else if (ok && full) take = ks < p.ksplit || (ks == p.ksplit && c.mb > p.mb);
+      else if (ok && full) take = ks < p.ksplit || (ks == p.ksplit && more_blocks);
       else if (!ok && !full) take = wgs > best_wgs;
     }
     if (take) {
@@ -681,11 +686,19 @@ int g_dt_mode = 1;
 // most workgroups. p.mb = 0 marks a tiled plan; p.ksw = index into kTiled.
 bool plan_decode_tiled(int64_t M, int64_t N, int64_t K, int epi, DgPlan& p) {
   if (g_dt_mode == 0 || M < g_dt_min_rows || M > 512 || K % 64 != 0 || N < 1) return false;
+  // qkv + RoPE (whole K per output block): the one-round-trip kernel's 4 waves on K quarters beat every tiled
+  // configuration from 192 rows on (512 rows: 14.2 -> 9.7 us, 256 rows: 14.3 -> 7.3;
+  // profiles/r03_decode_cfg_sweep2.jsonl), unless a configuration is forced
+  if (epi == EPI_ROPE && g_dt_force < 0) return false;
   int ci;
   if (g_dt_force >= 0) ci = g_dt_force;
   else if (epi == EPI_SWIGLU) ci = 2;
   else if (K >= 2048) { if (M < 384 && g_dt_min_rows >= 192) return false; ci = 6; }
-  else ci = 8;
+  else {
+    // short-K partials (o_proj): the one-round-trip kernel below 384 rows (256 rows: 6.75 -> 5.5 us)
+    if (epi == EPI_PARTIAL && M < 384 && g_dt_force < 0 && g_dt_min_rows >= 192) return false;
+    ci = 8;
+  }
   const int blocks = static_cast<int>((M + 31) / 32);
   p.mbt = (blocks + 1) / 2 * 2;
   p.tiles = static_cast<int>(epi == EPI_SWIGLU ? (N / 2 + 15) / 16 : (N + 31) / 32);

@@ -286,9 +286,10 @@ def test_decode_qkv_rope_matches_gemm_then_rope(M, K, Hq, Hkv, D):
             native.decode_qkv_rope(xp, native.decode_pack_weight_rope(w, D), bias, pos, cos_t, sin_t, M, K, Hq, Hkv, D,
                                    q, kc, vt, kd)
         else:
-            # the fused launch's shape: whole K per workgroup (K / 64 k16-steps per wave)
-            native.lib().drl_decode_gemm_set_plan(0, K // 64)
-            native.lib().drl_decode_gemm_set_tiled(2)  # from 192 rows: the tiled form, one K slice
+            # the fused launch's shape at every row count: the one-round-trip kernel, one-block workgroups, whole
+            # K per workgroup (K / 64 k16-steps per wave)
+            native.lib().drl_decode_gemm_set_plan(1, K // 64)
+            native.lib().drl_decode_gemm_set_tiled(0)
             part = native.decode_gemm(xp, native.decode_pack_weight(w), M, NQ, K)
             native.lib().drl_decode_gemm_set_tiled(1)
             native.lib().drl_decode_gemm_set_plan(0, 0)

@@ -89,6 +89,16 @@ def main():
                 except RuntimeError as e:  # a configuration that does not take this shape
                     row["planner" if ci < 0 else f"cfg{ci}"] = str(e)[:40]
             lib.drl_decode_gemm_force_tiled(-1, 0)
+            # the one-round-trip kernel (4 waves per workgroup each on a K quarter, reduced in LDS) at these rows
+            for mb in (1, 2):
+                lib.drl_decode_gemm_set_tiled(0)
+                lib.drl_decode_gemm_set_plan(mb, 0)
+                try:
+                    row[f"untiled_mb{mb}"] = round(graph_time(lambda: [fn(i) for i in range(L)]) / L, 2)
+                except (RuntimeError, AssertionError) as e:
+                    row[f"untiled_mb{mb}"] = str(e)[:40]
+                lib.drl_decode_gemm_set_plan(0, 0)
+                lib.drl_decode_gemm_set_tiled(1)
             print(json.dumps(row), flush=True)
 
 
