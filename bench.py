@@ -213,8 +213,10 @@ def build_config(args):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    # two warmup steps: after a single one, the first timed step's old_log_prob stage measured 1.2-1.4 s instead of
+    # 0.36 s (profiles/r03_decode_lanes.jsonl, warmup-1 runs)
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--tiny", action="store_true", help="2-layer model, small batch (bring-up only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--roofline-kernel", default="drl_gemm", choices=sorted(ROOFLINE))
@@ -258,6 +260,7 @@ def main():
     timer = native.KernelTimer(args.roofline_kernel, ROOFLINE[args.roofline_kernel][0])
     dist.barrier()
     torch.cuda.synchronize()
+    ms0 = torch.cuda.memory_stats()
     t0 = time.perf_counter()
     hist = []
     with timer:
@@ -266,6 +269,7 @@ def main():
             trainer.global_steps += 1
     torch.cuda.synchronize()
     dist.barrier()
+    ms1 = torch.cuda.memory_stats()
     elapsed = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cuda")
     dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     elapsed = float(elapsed.item())
@@ -331,7 +335,10 @@ def main():
             # sized past what the pool can serve without freeing and re-allocating
             "memory": {"max_allocated_gb": torch.cuda.max_memory_allocated() / 2 ** 30,
                        "max_reserved_gb": torch.cuda.max_memory_reserved() / 2 ** 30,
-                       "alloc_retries": torch.cuda.memory_stats().get("num_alloc_retries", 0)},
+                       "alloc_retries": torch.cuda.memory_stats().get("num_alloc_retries", 0),
+                       # device allocations / frees by torch's caching allocator inside the timed region
+                       "timed_device_allocs": ms1.get("num_device_alloc", 0) - ms0.get("num_device_alloc", 0),
+                       "timed_device_frees": ms1.get("num_device_free", 0) - ms0.get("num_device_free", 0)},
         }
         if not args.tiny:
             # the actor's form: update_policy hands K1 every micro-batch's sum(response_mask) (one pass over HBM)
