@@ -9,6 +9,7 @@ the outputs, so the full batch is resident in each rank's HBM between stages (no
 
 from __future__ import annotations
 
+import os
 import time
 import uuid
 from contextlib import contextmanager
@@ -28,17 +29,25 @@ from .config import resolve_critic_config
 from .workers import ActorRolloutRefWorker, CriticWorker
 
 
+_ALLOC_TRACE = os.environ.get("DRL_ALLOC_TRACE", "0") == "1"
+
+
 @contextmanager
 def marked_timer(name: str, timing_raw: dict):
     """profiler/performance.py:172 — wall time of a stage (synchronised: stages run on the GPU stream)."""
     sync = torch.cuda.is_initialized()  # host-only callers (CPU tests of the driver logic) have no stream
     if sync:
         torch.cuda.synchronize()
+    trace = sync and _ALLOC_TRACE
+    a0 = torch.cuda.memory_stats().get("num_device_alloc", 0) if trace else 0
     t0 = time.perf_counter()
     yield
     if sync:
         torch.cuda.synchronize()
     timing_raw[name] = timing_raw.get(name, 0.0) + time.perf_counter() - t0
+    if trace:  # DRL_ALLOC_TRACE=1: device allocations of torch's caching allocator inside the stage
+        key = name + "_device_allocs"
+        timing_raw[key] = timing_raw.get(key, 0) + torch.cuda.memory_stats().get("num_device_alloc", 0) - a0
 
 
 def compute_response_mask(data: DataProto):
