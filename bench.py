@@ -76,6 +76,30 @@ def _gemm_sk_flops(a):
     return 2.0 * a[10] * a[11] * a[12]
 
 
+def _gemm_sk_dispatches(a):
+    """Kernel dispatches of one drl_gemm call (rocprof counts these; the KernelTimer counts calls): an operand past
+    the 2 GB buffer range is split over several dispatches (csrc/gemm_sk.hip, drl_gemm: row blocks of a layout-K A,
+    K blocks of a layout-T operand)."""
+    lda, a_layout, ldb, b_layout, M, N, K = a[1], a[2], a[4], a[5], a[10], a[11], a[12]
+    lim = 1 << 31
+    if a_layout == 0 and lda > 0 and M * lda * 2 + 320 * lda * 2 >= lim:
+        rows = max(256, (lim // (lda * 2) - 320) // 256 * 256)
+        return sum(_gemm_sk_dispatches(a[:10] + (min(rows, M - m0),) + a[11:]) for m0 in range(0, M, rows))
+    tb = [K * ld * 2 + 320 * ld * 2 if lay == 1 else 0 for lay, ld in ((a_layout, lda), (b_layout, ldb))]
+    if max(tb) >= lim:
+        ld = max(lda if a_layout == 1 else 0, ldb if b_layout == 1 else 0)
+        kb = max(128, (lim // (ld * 2) - 320) // 128 * 128)
+        return -(-K // kb)
+    return 1
+
+
+def _gemm_sk_tag(a):
+    # (M, N, K, a_layout, b_layout, c_dtype, epilogue, dispatches)
+    return (a[10], a[11], a[12], a[2], a[5], a[8], a[14], _gemm_sk_dispatches(a))
+
+
+TAGS = {"drl_gemm": _gemm_sk_tag}
+
 # symbol -> (work per launch from the call's arguments, per-unit statement, bound, peak, unit)
 ROOFLINE = {
     "drl_gemm": (_gemm_sk_flops, "2*M*N*K FLOP per launch (bf16 operands, fp32 accumulation): every projection GEMM "
@@ -225,6 +249,10 @@ def main():
                     help="BASELINE config #5 on one GPU: Qwen2.5-7B DAPO, n=8, 1024-token responses (RayDAPOTrainer)")
     ap.add_argument("--k1-only", choices=["two_pass", "one_pass"], default=None,
                     help="only the K1 roofline at 2^26 tokens (rocprofv3 PMC passes for profiles/pmc_drl_ppo_loss_*)")
+    ap.add_argument("--launch-log", default=None,
+                    help="write every timed launch of the roofline kernel in the LAST timed step (start / end us, "
+                         "stream, work, shape) as JSON lines to this path: the roofline's per-dispatch and union "
+                         "fractions recompute from it")
     ap.add_argument("--dist-backend", default=None,
                     help="default: nccl (RCCL) on GPU; gloo lets several ranks share one GPU for a rehearsal")
     args = ap.parse_args()
@@ -257,14 +285,16 @@ def main():
         trainer.global_steps += 1
     # DAPO draws its own generation batches inside step() (dynamic sampling)
     prompts = [None if args.dapo else trainer.train_dataloader.next() for _ in range(args.steps)]
-    timer = native.KernelTimer(args.roofline_kernel, ROOFLINE[args.roofline_kernel][0])
+    timer = native.KernelTimer(args.roofline_kernel, ROOFLINE[args.roofline_kernel][0], TAGS.get(args.roofline_kernel))
     dist.barrier()
     torch.cuda.synchronize()
     ms0 = torch.cuda.memory_stats()
     t0 = time.perf_counter()
     hist = []
+    last_step_first_launch = 0
     with timer:
         for p in prompts:
+            last_step_first_launch = len(timer.events)
             hist.append(trainer.step(p))
             trainer.global_steps += 1
     torch.cuda.synchronize()
@@ -282,6 +312,12 @@ def main():
     # overlap the current stream's, so the mean per-launch interval (mean_launch_us, comparable to rocprof's
     # per-kernel average) counts shared time twice; achieved uses the union of the intervals instead
     t_busy = timer.busy_seconds() / n_launch if n_launch else None
+    dispatches = sum(t[-1] for t in timer.tags) if timer.tags and n_launch else None
+    if args.launch_log and rank == 0 and n_launch:
+        with open(args.launch_log, "w") as f:
+            for st, en, stream, work, tag in timer.intervals()[last_step_first_launch:]:
+                f.write(json.dumps({"start_us": round(st, 3), "end_us": round(en, 3), "stream": stream, "work": work,
+                                    "tag": tag}) + "\n")
     if rank == 0:
         ar = cfg.actor_rollout_ref
         preset = str(ar.model.get("path", "random:qwen2.5-0.5b"))
@@ -296,14 +332,23 @@ def main():
         metric = METRIC.replace("Qwen2.5-0.5B GRPO", f"{model_name} {algo}")
         _, per_unit, bound, peak, unit = ROOFLINE[args.roofline_kernel]
         scale = 1e12 if unit == "TFLOP/s" else 1e9
-        achieved = b_launch / t_busy / scale if n_launch else None
+        # frac: the work over the summed launch durations (each call's HIP-event interval; the rocprof view: the
+        # mean kernel duration x dispatches); frac_union: over the union of those intervals (launches on the side
+        # stream — weight gradients beside their input gradients — share the CUs with the current stream's)
+        achieved = b_launch / t_launch / scale if n_launch else None
+        achieved_union = b_launch / t_busy / scale if n_launch else None
         # the committed PMC pass is of the default workload (N=1 config #2): attach it only to that workload
         default_workload = not args.tiny and not args.override and args.gpus == 1
         traffic, traffic_src = _pmc_traffic(args.roofline_kernel) if default_workload else (None, None)
         roofline = {"kernel": args.roofline_kernel, "bound": bound, "achieved": achieved, "peak": peak,
-                    "unit": unit, "frac": achieved / peak if achieved else None, "traffic": traffic,
+                    "unit": unit, "frac": achieved / peak if achieved else None,
+                    "frac_per_dispatch": achieved / peak if achieved else None,
+                    "achieved_union": achieved_union, "frac_union": achieved_union / peak if achieved_union else None,
+                    "traffic": traffic,
                     "algorithmic_work_per_launch": b_launch if n_launch else None,
                     "mean_launch_us": t_launch * 1e6 if n_launch else None, "launches": n_launch,
+                    "dispatches": dispatches,
+                    "mean_dispatch_us": t_launch * n_launch / dispatches * 1e6 if dispatches else None,
                     "busy_us_per_launch": t_busy * 1e6 if n_launch else None,
                     "per_unit": per_unit, "traffic_source": traffic_src}
         line = {
@@ -327,6 +372,10 @@ def main():
                        "seq_len": cfg.data.max_prompt_length + cfg.data.max_response_length,
                        "parallelism": f"dp{world}", "tiny": bool(args.tiny)},
             "timing_s": {k.split("/", 1)[1]: sum(h[k] for h in hist) / len(hist) for k in hist[0] if k.startswith("timing_s/")},
+            # per stage over the timed steps: [min, median, max] seconds (a bimodal stage shows as max >> median)
+            "timing_spread_s": {k.split("/", 1)[1]: [min(v), sorted(v)[len(v) // 2], max(v)]
+                                for k in hist[0] if k.startswith("timing_s/")
+                                for v in [[h[k] for h in hist]]},
             "mfu_actor": sum(h.get("perf/mfu/actor", 0.0) for h in hist) / len(hist),
             "roofline": roofline,
             "roofline_k1": None,

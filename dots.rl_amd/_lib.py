@@ -105,6 +105,7 @@ SIGNATURES = {
     "drl_agg_loss_workspace_bytes": (SZ, [I64, I64]),
     "drl_agg_loss": (ctypes.c_int, [P, P, I32, I64, I64, I32, P, P, SZ, P]),
     "drl_logprob_entropy_fwd": (ctypes.c_int, [P, I32, I64, I64, I64, P, F32, P, P, P, P]),
+    "drl_token_logprob": (ctypes.c_int, [P, I32, I64, I64, I64, P, I64, P, F32, P, I64, P]),
     "drl_logprob_entropy_bwd": (ctypes.c_int, [P, I32, I64, I64, I64, P, F32, P, P, P, P, P, I32, I64, P]),
     "drl_grpo_workspace_bytes": (SZ, [I64]),
     "drl_grpo_outcome_advantage": (ctypes.c_int, [P, P, I32, P, P, P, I64, I64, I64, F32, I32, P, P, P, SZ, P]),

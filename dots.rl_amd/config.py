@@ -71,6 +71,10 @@ DEFAULTS = dict(
             clip_ratio_high=0.2, clip_ratio_c=3.0, policy_loss=dict(loss_mode="vanilla"), loss_agg_mode="token-mean",
             entropy_coeff=0.0, use_kl_loss=True, kl_loss_coef=0.001, kl_loss_type="low_var_kl", ppo_epochs=1,
             shuffle=False, grad_clip=1.0, ulysses_sequence_parallel_size=1,
+            # dp_actor.yaml:30-33: chunked / recomputed entropy bound the reference's (N, V) logits temporaries; K2
+            # computes the entropy in the same single pass over the logits as the log-prob and keeps no temporaries,
+            # so both are accepted and change nothing (dp_actor.DataParallelPPOActor)
+            entropy_from_logits_with_chunking=False, entropy_checkpointing=False,
             # micro-batches run through the model together (one forward / backward over their concatenated rows; the
             # loss, its scale and the metrics stay per micro-batch): 0 = as many as fit exec_activation_gb of saved
             # activations, 1 = the reference's one micro-batch per pass (dp_actor.DataParallelPPOActor.update_policy)
@@ -93,9 +97,13 @@ DEFAULTS = dict(
             packed_decode=True, packed_decode_max_rows=512,  # qwen2.PackedDecode (fragment-packed operands)
             fused_select=False,  # lm_head fused with K4 (csrc/fused_linear.hip)
             decode_lanes=1,  # row groups of the graphed decode step on concurrent streams (rollout._decode_lanes)
+            # rollout.yaml:177: emit `rollout_log_probs` (log p of each sampled token under the decode step's own
+            # logits, -1 past the response) -> training/rollout_probs_diff_* metrics (ray_trainer.py:1221-1225)
+            calculate_log_probs=False,
         ),
         ref=dict(log_prob_micro_batch_size=None, log_prob_micro_batch_size_per_gpu=16, log_prob_use_dynamic_bsz=False,
-                 log_prob_max_token_len_per_gpu=16384, exec_log_prob_tokens=196608),
+                 log_prob_max_token_len_per_gpu=16384, exec_log_prob_tokens=196608,
+                 entropy_from_logits_with_chunking=False, entropy_checkpointing=False),  # dp_ref.yaml:43-46
     ),
     # critic.yaml + dp_critic.yaml (used when algorithm.adv_estimator == "gae" or critic.enable)
     critic=dict(

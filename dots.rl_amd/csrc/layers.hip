@@ -1,5 +1,5 @@
 // Transformer-layer kernels of the Qwen2 actor / reference / rollout model (everything that is not a
-// GEMM; GEMMs run on hipBLASLt): fused QKV split + RoPE + grouped-query re-layout (fwd / bwd),
+// GEMM; GEMMs run on drl_gemm, csrc/gemm_sk.hip): fused QKV split + RoPE + grouped-query re-layout (fwd / bwd),
 // masked softmax over attention scores (fwd / bwd), residual-add + RMSNorm (fwd / bwd), SwiGLU (fwd / bwd).
 // Semantics follow HF Qwen2 (Qwen2RMSNorm fp32 variance, rotate_half RoPE, SiLU(gate) * up, causal +
 // key-padding attention mask) as the reference runs it (verl/workers/actor/dp_actor.py:90-280 model call).

@@ -156,6 +156,26 @@ __global__ __launch_bounds__(kThreads) void logprob_fwd_kernel(const void* logit
   }
 }
 
+// rollout.calculate_log_probs: log p(token) of the token the decode step just selected, under the actor's
+// compute_log_prob definition (logits / temperature as logprob_fwd_kernel), read from out-of-band token columns
+// (the graph-captured decode loop: column *dev_step of tokens / out)
+template <int DT>
+__global__ __launch_bounds__(kThreads) void token_logprob_kernel(const void* logits, int64_t V, int64_t ld,
+                                                                 const int64_t* tokens, int64_t ld_tok,
+                                                                 const int64_t* dev_step, float inv_t, int apply_t,
+                                                                 bool vec, float* out, int64_t ld_out) {
+  const int64_t r = blockIdx.x;
+  const void* row = static_cast<const typename Elem<DT>::T*>(logits) + r * ld;
+  float m, s, t;
+  row_softmax_state<DT, false>(row, V, vec, inv_t, apply_t, m, s, t);
+  if (threadIdx.x == 0) {
+    const int64_t col = dev_step ? *dev_step : 0;
+    const int64_t y = tokens[r * ld_tok + col];
+    const float lse = m + logf(s);
+    out[r * ld_out + col] = (y >= 0 && y < V) ? scale_logit<DT>(Elem<DT>::get(row, y), inv_t, apply_t) - lse : -INFINITY;
+  }
+}
+
 template <int DT, int ODT>
 __global__ __launch_bounds__(kThreads) void logprob_bwd_kernel(const void* logits, int64_t V, int64_t ld,
                                                                const int64_t* labels, float inv_t, int apply_t,
@@ -596,6 +616,29 @@ int drl_logprob_entropy_fwd(const void* logits, int32_t dt, int64_t N, int64_t V
   else
     hipLaunchKernelGGL(logprob_fwd_kernel<DRL_F32>, dim3(N), dim3(kThreads), 0, s, logits, V, ld, labels, inv_t,
                        apply_t, vec, log_prob, entropy, lse_out);
+  DRL_LAUNCH_CHECK();
+  return DRL_OK;
+}
+
+int drl_token_logprob(const void* logits, int32_t dt, int64_t N, int64_t V, int64_t ld, const int64_t* tokens,
+                      int64_t ld_tok, const int64_t* dev_step, float temperature, float* out, int64_t ld_out,
+                      void* stream) {
+  using namespace drl;
+  DRL_CHECK_ARG(logits && tokens && out, "NULL input");
+  DRL_CHECK_ARG(N >= 0 && V >= 1 && ld >= V && ld_tok >= 1 && ld_out >= 1, "bad shape");
+  DRL_CHECK_ARG(dt == DRL_BF16 || dt == DRL_F32, "logits dtype must be F32 or BF16");
+  DRL_CHECK_ARG(temperature > 0.f, "temperature must be > 0");
+  DRL_CHECK_ARG(N <= 0x7fffffff, "too many rows");
+  if (N == 0) return DRL_OK;
+  const bool vec = rows_aligned(logits, ld, dt);
+  const int apply_t = temperature != 1.0f;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (dt == DRL_BF16)
+    hipLaunchKernelGGL(token_logprob_kernel<DRL_BF16>, dim3(N), dim3(kThreads), 0, s, logits, V, ld, tokens, ld_tok,
+                       dev_step, temperature, apply_t, vec, out, ld_out);
+  else
+    hipLaunchKernelGGL(token_logprob_kernel<DRL_F32>, dim3(N), dim3(kThreads), 0, s, logits, V, ld, tokens, ld_tok,
+                       dev_step, temperature, apply_t, vec, out, ld_out);
   DRL_LAUNCH_CHECK();
   return DRL_OK;
 }

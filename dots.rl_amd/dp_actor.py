@@ -1,7 +1,7 @@
 """DataParallelPPOActor on MI355X (mirror of verl/workers/actor/dp_actor.py:53-482).
 
 Same micro-batching, loss composition, gradient accumulation and metric keys as the reference; the
-numerics per micro-batch are: transformer forward (hipBLASLt GEMMs) -> lm_head on the R response
+numerics per micro-batch are: transformer forward (drl_gemm GEMMs) -> lm_head on the R response
 positions only -> K2 log-prob/entropy over the vocabulary -> K1 fused actor loss (forward + backward in
 one launch) -> backward of the model from (d logp, d entropy). The optimizer step is the flat-buffer
 RCCL all-reduce + HIP grad-norm + HIP AdamW (FlatAdamW). Metric scalars stay on device until the end
@@ -38,9 +38,17 @@ def lr_schedule(optim_cfg):
     total = 0 if total is None else int(total)
     warm = optim_cfg.get("lr_warmup_steps", -1)
     warm = -1 if warm is None else int(warm)
-    if warm < 0:
-        warm = int(optim_cfg.get("lr_warmup_steps_ratio", 0.0) * total)
+    ratio = float(optim_cfg.get("lr_warmup_steps_ratio", 0.0) or 0.0)
     style = optim_cfg.get("warmup_style", "constant")
+    # the reference always hands the schedule a positive horizon (ray_trainer.py:557-571: the dataloader length x
+    # total_epochs unless trainer.total_training_steps overrides it); without one a cosine schedule would flip
+    # between lr and min_lr every step and a ratio warmup would silently be zero steps
+    if total <= 0 and (style == "cosine" or (warm < 0 and ratio > 0)):
+        raise ValueError(f"warmup_style={style!r} / lr_warmup_steps_ratio={ratio} need a positive "
+                         f"total_training_steps (set trainer.total_training_steps, or give the trainer a "
+                         f"train_dataloader with a length)")
+    if warm < 0:
+        warm = int(ratio * total)
     if style == "constant":
         def lam(step):
             if step < warm:

@@ -87,3 +87,30 @@ def compute_throughout_metrics(batch: DataProto, timing_raw: dict, n_gpus: int) 
     total = sum(batch.meta_info["global_token_num"])
     t = timing_raw["step"]
     return {"perf/total_num_tokens": total, "perf/time_per_step": t, "perf/throughput": total / (t * n_gpus)}
+
+
+def calculate_debug_metrics(data: DataProto) -> dict:
+    """utils/debug/metrics.py:63-108 (ray_trainer.py:1221-1225, when the rollout emitted ``rollout_log_probs``):
+    rollout-vs-actor probabilities p = exp(log p) over the response mask (``response_mask``, else the response part
+    of ``attention_mask``) — |p_actor - p_rollout| max / mean / std (unbiased) and their Pearson correlation."""
+    b = data.batch
+    rlp, alp = b["rollout_log_probs"], b["old_log_probs"]
+    if "response_mask" in b:
+        mask = b["response_mask"]
+    elif "attention_mask" in b:
+        mask = b["attention_mask"]
+    else:
+        mask = torch.ones_like(rlp)
+    R = b["responses"].size(1)
+    m = mask[:, -R:].bool()
+    pa, pr = torch.exp(alp), torch.exp(rlp)
+    if pa.shape == pr.shape == m.shape:
+        a, r = torch.masked_select(pa, m), torch.masked_select(pr, m)
+        corr = torch.corrcoef(torch.stack([a, r], dim=0))[0][1]
+    else:  # metrics.py:47-49
+        corr = torch.zeros(())
+    diff = torch.masked_select(torch.abs(pa - pr), m)
+    vals = torch.stack([diff.max(), diff.mean(), diff.std(), corr.to(diff.device, diff.dtype)]).tolist()
+    return {"training/rollout_probs_diff_valid": 1, "training/rollout_probs_diff_max": vals[0],
+            "training/rollout_probs_diff_mean": vals[1], "training/rollout_probs_diff_std": vals[2],
+            "training/rollout_actor_probs_pearson_corr": vals[3]}

@@ -35,9 +35,9 @@ class KernelTimer:
     into a HIP graph are not timed. ``bytes_fn(args)`` gives the algorithmic bytes of one launch from the
     entry point's own arguments. Used by bench.py for the roofline of the dominant kernel."""
 
-    def __init__(self, symbol: str, bytes_fn):
-        self.symbol, self.bytes_fn = symbol, bytes_fn
-        self.events, self.nbytes = [], []
+    def __init__(self, symbol: str, bytes_fn, tag_fn=None):
+        self.symbol, self.bytes_fn, self.tag_fn = symbol, bytes_fn, tag_fn
+        self.events, self.nbytes, self.tags, self.streams = [], [], [], []
 
     def __enter__(self):
         _TIMERS[self.symbol] = self
@@ -57,6 +57,9 @@ class KernelTimer:
             b.record(s)
             self.events.append((a, b))
             self.nbytes.append(self.bytes_fn(args))
+            self.streams.append(s.cuda_stream)
+            if self.tag_fn is not None:
+                self.tags.append(self.tag_fn(args))
             return rc
         return call
 
@@ -68,6 +71,19 @@ class KernelTimer:
         tot = sum(a.elapsed_time(b) for a, b in self.events) * 1e-3
         n = len(self.events)
         return n, tot / n, sum(self.nbytes) / n
+
+    def intervals(self):
+        """Per launch: (start_us, end_us) relative to the first launch's start, the stream handle, the algorithmic
+        work and the tag (``tag_fn(args)``, e.g. the GEMM shape)."""
+        if not self.events:
+            return []
+        torch.cuda.synchronize()
+        t0 = self.events[0][0]
+        out = []
+        for i, (a, b) in enumerate(self.events):
+            out.append((t0.elapsed_time(a) * 1e3, t0.elapsed_time(b) * 1e3, self.streams[i], self.nbytes[i],
+                        self.tags[i] if self.tags else None))
+        return out
 
     def busy_seconds(self):
         """Length of the union of the launch intervals: launches on two streams (a weight gradient beside its input
@@ -533,6 +549,21 @@ def linear_select_tokens(hidden, weight, out_tokens, *, do_sample=False, tempera
                                          ctypes.byref(prm), _p(unfinished), _p(out_tokens), ld_out, _p(ws),
                                          ws.numel() * 8, _stream()), "drl_linear_select_tokens")
     return out_tokens
+
+
+def token_logprob(logits, tokens, out, temperature=1.0, dev_step=None):
+    """rollout.calculate_log_probs: out[n, s] = log softmax(logits[n] / T)[tokens[n, s]] for the column s =
+    ``dev_step`` (device int64 scalar; 0 when None) of the (N, *) int64 ``tokens`` / fp32 ``out`` views."""
+    _dev(logits, tokens, out, dev_step)
+    lg = _logits_2d(logits)
+    N, V = lg.shape
+    assert tokens.dtype == torch.int64 and out.dtype == torch.float32
+    assert tokens.shape[0] == N and out.shape[0] == N
+    ld_tok = tokens.stride(0) if tokens.dim() > 1 or tokens.numel() > 1 else 1
+    ld_out = out.stride(0) if out.dim() > 1 or out.numel() > 1 else 1
+    check(lib().drl_token_logprob(_p(lg), _LOGIT_DTYPES[lg.dtype], N, V, lg.stride(0), _p(tokens), ld_tok,
+                                  _p(dev_step), float(temperature), _p(out), ld_out, _stream()), "drl_token_logprob")
+    return out
 
 
 _SELECT_WS = {}

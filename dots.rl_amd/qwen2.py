@@ -3,10 +3,11 @@
 Parameters live in three flat device buffers (``ParamStore``): fp32 master weights, a compute copy (bf16)
 that the GEMMs read, and fp32 gradients. The optimizer (HIP AdamW kernel) updates the master buffer and
 rewrites the bf16 copy in the same pass; data-parallel gradient averaging is a single RCCL all-reduce of
-the flat gradient; GEMM weight gradients accumulate straight into fp32 (hipBLASLt bf16 x bf16 -> fp32),
-so micro-batch accumulation never rounds through bf16.
+the flat gradient; GEMM weight gradients accumulate straight into fp32 (drl_gemm bf16 x bf16 -> fp32 with
+beta = 1), so micro-batch accumulation never rounds through bf16.
 
-Per decoder layer the GEMMs run on hipBLASLt and everything else on hand-written HIP kernels:
+Per decoder layer every bf16 GEMM (forward, input gradient, weight gradient, lm_head) runs on the hand-written
+stream-K GEMM ``drl_gemm`` (``csrc/gemm_sk.hip``) and everything else on hand-written HIP kernels:
 ``csrc/layers.hip`` (residual-add + RMSNorm, QKV split + RoPE + grouped-query re-layout so the 7 query
 heads of a KV head share one K/V stream, SwiGLU), ``csrc/flash_attn.hip`` (fused MFMA attention forward
 and backward for bf16 full sequences; the fp32 parity model uses fp32-score GEMMs + masked softmax) and
@@ -337,7 +338,7 @@ def acc_wgrad(gw, dy, x):
 # pair's workgroups share the CUs (gate_up's weight gradient is 152 tiles of 256 x 256 at any row count, the other
 # 104 CUs otherwise idle for its ~2 ms). It pays since whole-tile drl_gemm launches one workgroup per tile (the
 # hardware deals tiles to CUs as they free up; a persistent grid's static rounds could not take the idle CUs):
-# update 1.44 -> 1.38 s (tools/gpu_r03aa.sh). DRL_CONCURRENT_WGRAD=0 turns it off.
+# update 1.44 -> 1.38 s (round 3). DRL_CONCURRENT_WGRAD=0 turns it off.
 CONCURRENT_WGRAD = os.environ.get("DRL_CONCURRENT_WGRAD", "1") != "0"
 _SIDE_STREAMS = {}
 
@@ -368,7 +369,8 @@ def dgrad_wgrad(dy, w, gw, x):
 
 
 def bmm_f32(a, b):
-    """Batched a @ b (bf16 or fp32 inputs) with an fp32 result (hipBLASLt)."""
+    """Batched a @ b (bf16 or fp32 inputs) with an fp32 result: the fp32 parity model's attention scores (torch
+    bmm); the bf16 model runs the fused attention kernels instead (csrc/flash_attn.hip)."""
     if a.dtype == torch.float32:
         return torch.bmm(a, b)
     return torch.bmm(a, b, out_dtype=torch.float32)
@@ -808,14 +810,21 @@ class Qwen2Model:
             return _Linear.apply(h, self.store.w(name), self.store.g(name), self._dummy)
         return linear(h.reshape(-1, h.shape[-1]), self.store.w(name)).view(*h.shape[:-1], -1)
 
-    def select_tokens(self, h, out_tokens, fused=True, **sel):
+    def select_tokens(self, h, out_tokens, fused=True, logprob_out=None, logprob_temperature=1.0, **sel):
         """Token selection from the final-norm hidden h (N, H): K4 fused with the lm_head on bf16 (the (N, V)
         logits are never written, csrc/fused_linear.hip), else lm_head logits + K4 (fp32 parity model, and
-        sampling: the slice race and the top-k / top-p cut read the logits row)."""
+        sampling: the slice race and the top-k / top-p cut read the logits row). With ``logprob_out`` (the
+        rollout's calculate_log_probs) the selected token's log p under logits / ``logprob_temperature`` is written
+        to the same column of it (native.token_logprob, one more pass over the logits rows)."""
         w = self.store.w(self.lm_head_weight())
-        if fused and not sel.get("do_sample") and self.dtype == torch.bfloat16 and h.shape[-1] % 64 == 0:
+        if logprob_out is None and fused and not sel.get("do_sample") and self.dtype == torch.bfloat16 and \
+                h.shape[-1] % 64 == 0:
             return native.linear_select_tokens(h.contiguous(), w, out_tokens, **sel)
-        return native.select_tokens(self.logits(h), out_tokens, **sel)
+        logits = self.logits(h)
+        native.select_tokens(logits, out_tokens, **sel)
+        if logprob_out is not None:
+            native.token_logprob(logits, out_tokens, logprob_out, logprob_temperature, dev_step=sel.get("dev_step"))
+        return out_tokens
 
     def fused_logprob(self, h, labels, temperature, calculate_entropy):
         """A21: h (N, H) in bf16 -> (log_probs, entropy or None) over the lm_head without materialising logits

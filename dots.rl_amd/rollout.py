@@ -20,12 +20,46 @@ from .qwen2 import KVCache, KVCacheRows, PackedDecode, Qwen2Model
 from .torch_functional import get_response_mask
 
 
+_CAPTURE_STREAM = None
+
+
+def capture_graph(body, pool):
+    """Capture ``body()`` into a new HIP graph whose allocations come from the private pool ``pool``.
+
+    This is torch.cuda.graph without its ``torch.cuda.empty_cache()`` on entry: that call handed every cached
+    block of the step (~130 GB at config #2) back to the driver once per rollout, so the next stages re-allocated
+    them (160 device allocations per step, each cleared by the driver before first use) and the old log-prob pass
+    after the rollout ran up to 3x slow. The pool is the rollout's own and outlives each graph (the caller keeps
+    the previous graph until the next one is captured), so its blocks are reused capture after capture."""
+    global _CAPTURE_STREAM
+    if _CAPTURE_STREAM is None:
+        _CAPTURE_STREAM = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(_CAPTURE_STREAM):
+        graph.capture_begin(pool=pool)
+        try:
+            body()
+        finally:
+            graph.capture_end()
+    return graph
+
+
 class MI355XRollout:
     def __init__(self, module: Qwen2Model, config, dp_rank: int = 0):
         self.module = module
         self.config = config
         self.dp_rank = dp_rank
         self.calls = 0
+        self._graph_pool = None  # private memory pool of the captured decode step, kept across rollouts
+        self._graph = None  # the last captured decode step (released when the next one is captured)
+
+    def _capture(self, body):
+        if self._graph_pool is None:
+            self._graph_pool = torch.cuda.graph_pool_handle()
+        graph = capture_graph(body, self._graph_pool)
+        self._graph = graph  # the previous graph goes only now, so the pool's use count never drops to zero
+        return graph
 
     def generate_sequences(self, prompts: DataProto) -> DataProto:
         """hf_rollout.py:45-51: optional micro-batching of the prompt batch."""
@@ -80,13 +114,17 @@ class MI355XRollout:
         # lm_head + K4 at 64 and 512 rows (rollout 0.43 vs 0.38 s, 1.22 vs 1.20 s): opt-in
         fused = bool(cfg.get("fused_select", False))
         self._fused_select = fused
-        m.select_tokens(h, responses[:, 0], fused=fused, step=0, **sel)
+        # rollout.calculate_log_probs: log p of each selected token from the decode step's own logits, under the
+        # temperature the actor's compute_log_prob divides by (rollout.temperature, ray_trainer.py:1281)
+        rollout_lp = torch.empty(B, R, dtype=torch.float32, device=dev) if cfg.get("calculate_log_probs") else None
+        self._lp = dict(logprob_temperature=float(cfg.temperature)) if rollout_lp is not None else {}
+        m.select_tokens(h, responses[:, 0], fused=fused, step=0, **self._lp_col(rollout_lp, 0), **sel)
         if cfg.get("use_hip_graph", True) and R > 2:
-            self._decode_graphed(cache, responses, last_pos, P, R, sel)
+            self._decode_graphed(cache, responses, last_pos, P, R, sel, rollout_lp)
         else:
             for t in range(1, R):
                 h = m.decode_step(cache, responses[:, t - 1], last_pos + t)
-                m.select_tokens(h, responses[:, t], fused=fused, step=t, **sel)
+                m.select_tokens(h, responses[:, t], fused=fused, step=t, **self._lp_col(rollout_lp, t), **sel)
         del cache
         seq = torch.cat([idx, responses], dim=-1)
         # hf_rollout.py:151-160: positions continue from the last prompt position; mask up to first EOS
@@ -94,16 +132,21 @@ class MI355XRollout:
         full_pos[:, :P] = position_ids
         native.response_position_ids_(full_pos, P)
         resp_mask = get_response_mask(responses, eos_list, dtype=attention_mask.dtype)
-        batch = TensorBatch({
+        tensors = {
             "prompts": idx,
             "responses": responses,
             "input_ids": seq,
             "attention_mask": torch.cat([attention_mask, resp_mask], dim=-1),
             "position_ids": full_pos,
-        }, batch_size=B)
-        return DataProto(batch=batch)
+        }
+        if rollout_lp is not None:  # vllm_rollout_spmd.py:359-362: -1 past each response
+            tensors["rollout_log_probs"] = torch.where(resp_mask.bool(), rollout_lp, rollout_lp.new_full((), -1.0))
+        return DataProto(batch=TensorBatch(tensors, batch_size=B))
 
-    def _decode_graphed(self, cache, responses, last_pos, P, R, sel):
+    def _lp_col(self, rollout_lp, t):
+        return dict(self._lp, logprob_out=rollout_lp[:, t]) if rollout_lp is not None else {}
+
+    def _decode_graphed(self, cache, responses, last_pos, P, R, sel, rollout_lp=None):
         """Response tokens 1..R-1 as replays of ONE captured decode step.
 
         The step's only changing inputs live in device memory: the step counter t (token t-1 is read from
@@ -115,7 +158,7 @@ class MI355XRollout:
         t_dev = torch.ones(1, dtype=torch.int64, device=responses.device)
         B = responses.shape[0]
         max_rows = int(self.config.get("packed_decode_max_rows", 512))
-        lanes = self._decode_lanes(B, max_rows)
+        lanes = self._decode_lanes(B, max_rows) if rollout_lp is None else 1
         if lanes > 1:
             return self._decode_graphed_lanes(cache, responses, last_pos, P, R, sel, lanes)
         use = self.config.get("packed_decode", True) and PackedDecode.supported(m, B, max_rows)
@@ -129,20 +172,20 @@ class MI355XRollout:
         def body():
             if prologue:  # one launch: embedding, positions, cache slot, key_valid, t_cur, t_dev += 1
                 h = packed.step_from(cache, responses, t_dev, last_pos_flat, P)
-                m.select_tokens(h, responses[:, 0], fused=self._fused_select, step=0, dev_step=packed.t_cur, **sel)
+                m.select_tokens(h, responses[:, 0], fused=self._fused_select, step=0, dev_step=packed.t_cur,
+                                **self._lp_col(rollout_lp, 0), **sel)
                 return
             tok = responses.index_select(1, t_dev - 1)
             if packed is not None:
                 h = packed.step(cache, tok, last_pos + t_dev, t_dev + (P - 1))
             else:
                 h = m.decode_step_dev(cache, tok, last_pos + t_dev, t_dev + (P - 1))
-            m.select_tokens(h, responses[:, 0], fused=self._fused_select, step=0, dev_step=t_dev, **sel)
+            m.select_tokens(h, responses[:, 0], fused=self._fused_select, step=0, dev_step=t_dev,
+                            **self._lp_col(rollout_lp, 0), **sel)
             t_dev.add_(1)
 
         body()  # t = 1, eager
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            body()
+        graph = self._capture(body)
         for _ in range(2, R):
             graph.replay()
         del graph, packed
@@ -195,8 +238,8 @@ class MI355XRollout:
         for j in range(lanes):  # t = 1, eager (sizes every lane's workspaces outside capture)
             body(j)
         side = [torch.cuda.Stream(device=dev) for _ in range(lanes - 1)]
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
+
+        def lanes_body():
             main = torch.cuda.current_stream()
             for s in side:
                 s.wait_stream(main)
@@ -206,6 +249,8 @@ class MI355XRollout:
                     body(j)
             for s in side:
                 main.wait_stream(s)
+
+        graph = self._capture(lanes_body)
         for _ in range(2, R):
             graph.replay()
         del graph, lane_state

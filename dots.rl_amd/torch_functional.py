@@ -57,12 +57,27 @@ def entropy_from_logits(logits: torch.Tensor):
     return logprobs_and_entropy_from_logits(logits, labels, 1.0, True, False)[1]
 
 
+_BUFFER_RANGE = 1 << 31  # drl_gemm's operands stay below one 2 GB buffer range
+
+
+def fused_linear_vocab_block(V, n_cols):
+    """Vocabulary rows per d_logits^T block of the fused lm_head backward: the (block, n_cols) bf16 block plus one
+    tile of overhang stays below the 2 GB buffer range drl_gemm reads in place (256-row multiples)."""
+    rows = (_BUFFER_RANGE // (2 * n_cols) - 320) // 256 * 256
+    assert rows >= 256, f"{n_cols} tokens: a 256-row d_logits block exceeds the 2 GB operand range"
+    return min(V, rows)
+
+
 class _FusedLinearLogprobEntropy(torch.autograd.Function):
     """A21: lm_head + log-prob + entropy without materialising logits (FusedLinearForPPOFunction,
     utils/experimental/torch_functional.py:75-150; linear_cross_entropy.py:41-117 with reduction "none").
-    Backward = the reference's BackwardEnum._Total_Separate: one kernel writes d_logits^T (V, N) bf16 from
-    recomputed logits, then d_hidden = d_logits W and d_W += d_logits^T hidden on drl_gemm (csrc/gemm_sk.hip;
-    d_W straight into the fp32 gradient buffer ``weight_grad`` when given)."""
+
+    Backward = the reference's BackwardEnum._Split_Dlogits_N (kernels.py:1519-1580) on this repo's kernels: the
+    vocabulary in blocks whose d_logits^T (block, N) bf16 stays below the 2 GB operand range; per block
+    ``drl_linear_logprob_dlogits`` recomputes z on MFMA and writes d_logits^T, then d_hidden (+)= d_logits W_blk and
+    d_W[blk] (+)= d_logits^T hidden on drl_gemm (csrc/gemm_sk.hip, fp32 accumulation; d_W straight into the fp32
+    gradient buffer ``weight_grad`` when given). d_hidden accumulates in fp32 across blocks and is rounded to bf16
+    once, as the reference's single bf16 matmul over the whole vocabulary rounds its fp32 sum once."""
 
     @staticmethod
     def forward(ctx, hidden, weight, weight_grad, labels, temperature, want_entropy):
@@ -80,30 +95,44 @@ class _FusedLinearLogprobEntropy(torch.autograd.Function):
             dlogp = torch.zeros_like(lse)
         if not ctx.want_entropy:
             dent = None
-        N = hidden.shape[0]
-        n8 = (N + 7) // 8 * 8  # 16-B aligned rows of d_logits^T, so drl_gemm reads it in place for any N
-        dlt = native.linear_logprob_dlogits(hidden, weight, labels, ctx.temperature, dlogp, dent, lse,
-                                            ent if dent is not None else None,
-                                            out=torch.empty(weight.shape[0], n8, dtype=torch.bfloat16,
-                                                            device=hidden.device)[:, :N])
-        V, N = dlt.shape
-        H = weight.shape[1]
-        hip = dlt.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16
-        if hip:  # dh (N, H) = dlt^T W on drl_gemm: both operands read in place (layout T), any V
-            dh = native.gemm(dlt, native.LAYOUT_T, weight, native.LAYOUT_T, N, H, V,
-                             torch.empty(N, H, dtype=torch.bfloat16, device=dlt.device))
-        else:
-            dh = dlt.t() @ weight
+        assert hidden.dtype == weight.dtype == torch.bfloat16, "the fused lm_head runs on bf16 operands"
+        N, H = hidden.shape
+        V = weight.shape[0]
+        dev = hidden.device
+        weight = weight.contiguous()
+        labels = labels.reshape(-1)
+        # d_W's GEMM reads d_logits^T with the tokens along K (layout K): whole 64-token k-tiles, so the block has
+        # 64-aligned rows whose columns past N stay zero, and hidden is read through a zero-padded copy when N is
+        # ragged (zero rows x zero columns: the padding adds exact zeros)
+        n64 = (N + 63) // 64 * 64
+        hid = hidden.contiguous()
+        if n64 != N:
+            hid = torch.zeros(n64, H, dtype=hidden.dtype, device=dev)
+            hid[:N] = hidden
+        vb = fused_linear_vocab_block(V, n64)
+        blk = torch.empty(vb, n64, dtype=torch.bfloat16, device=dev)
+        if n64 != N:
+            blk[:, N:].zero_()
+        one_block = vb >= V
+        dh = torch.empty(N, H, dtype=torch.bfloat16 if one_block else torch.float32, device=dev)
+        wg = ctx.weight_grad
         dw = None
-        if ctx.weight_grad is not None:
-            if hip and N % 64 == 0 and hidden.is_contiguous():  # dW (V, H) += dlt hidden, fp32 in place
-                # (layout-K dlt needs whole 64-token k-tiles; other N — A21 is opt-in — take torch's GEMM)
-                native.gemm(dlt, native.LAYOUT_K, hidden, native.LAYOUT_T, V, H, N, ctx.weight_grad, beta=True)
-            else:
-                torch.addmm(ctx.weight_grad, dlt, hidden, out_dtype=torch.float32, out=ctx.weight_grad)
-        elif ctx.needs_input_grad[1]:
-            dw = dlt @ hidden
-        return dh, dw, None, None, None, None
+        if wg is None and ctx.needs_input_grad[1]:
+            dw = torch.empty(V, H, dtype=torch.float32, device=dev)
+        for v0 in range(0, V, vb):
+            rows = min(vb, V - v0)
+            w_blk = weight[v0:v0 + rows]
+            dlt = native.linear_logprob_dlogits(hidden, w_blk, labels - v0 if v0 else labels, ctx.temperature, dlogp,
+                                                dent, lse, ent if dent is not None else None, out=blk[:rows, :N])
+            # d_hidden (N, H) (+)= d_logits (N, rows) W_blk: A = d_logits^T read as layout T, B = W_blk layout T
+            native.gemm(dlt, native.LAYOUT_T, w_blk, native.LAYOUT_T, N, H, rows, dh, beta=v0 > 0)
+            # d_W[blk] (rows, H) (+)= d_logits^T hidden: A = the block (layout K over n64 tokens), B = hidden layout T
+            tgt = wg[v0:v0 + rows] if wg is not None else (dw[v0:v0 + rows] if dw is not None else None)
+            if tgt is not None:
+                native.gemm(blk[:rows], native.LAYOUT_K, hid, native.LAYOUT_T, rows, H, n64, tgt, beta=wg is not None)
+        if not one_block:
+            dh = dh.to(torch.bfloat16)
+        return dh, (dw.to(weight.dtype) if dw is not None else None), None, None, None, None
 
 
 def fused_linear_logprob_entropy(hidden, weight, labels, temperature=1.0, calculate_entropy=True, weight_grad=None):

@@ -20,7 +20,8 @@ import torch.distributed as dist
 
 from . import core_algos
 from .core_algos import AdvantageEstimator, agg_loss
-from .metric_utils import compute_data_metrics, compute_throughout_metrics, compute_timing_metrics, reduce_metrics
+from .metric_utils import (calculate_debug_metrics, compute_data_metrics, compute_throughout_metrics,
+                           compute_timing_metrics, reduce_metrics)
 from .protocol import DataProto
 from .reward import compute_reward, load_reward_manager
 from .seqlen_balancing import get_seqlen_balanced_partitions, log_seqlen_unbalance
@@ -163,8 +164,12 @@ class RayPPOTrainer:
             self.use_critic = config.algorithm.adv_estimator == AdvantageEstimator.GAE.value
         self.global_steps = 0
         self.n_gpus = dist.get_world_size() if dist.is_initialized() else 1
-        # ray_trainer.py:557-571: the schedule horizon of the actor / critic LR schedules
+        # ray_trainer.py:557-571: the schedule horizon of the actor / critic LR schedules — the dataloader's length x
+        # total_epochs, unless trainer.total_training_steps overrides it (the synthetic loader is endless: no length)
         total = config.trainer.get("total_training_steps")
+        if total is None and hasattr(train_dataloader, "__len__"):
+            total = len(train_dataloader) * int(config.trainer.get("total_epochs", 1))
+        self.total_training_steps = total
         if total is not None:
             config.actor_rollout_ref.actor.optim.total_training_steps = int(total)
             if "critic" in config:
@@ -251,6 +256,8 @@ class RayPPOTrainer:
             metrics["actor/entropy"] = ent
             old.batch.pop("entropys")
             batch = batch.union(old)
+            if "rollout_log_probs" in batch.batch:  # rollout.calculate_log_probs (ray_trainer.py:1221-1225)
+                metrics.update(calculate_debug_metrics(batch))
         if self.use_reference_policy:
             with marked_timer("ref", timing_raw):
                 batch = batch.union(self.ref_policy_wg.compute_ref_log_prob(batch))
@@ -304,7 +311,7 @@ class RayPPOTrainer:
 
     def fit(self, num_steps=None):
         """ray_trainer.py:1050-1405 training loop (synthetic data; no validation/checkpoint by default)."""
-        total = num_steps or self.config.trainer.get("total_training_steps") or 1
+        total = num_steps or self.total_training_steps or 1
         self.global_steps = 1
         history = []
         for _ in range(total):

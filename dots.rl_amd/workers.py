@@ -40,7 +40,18 @@ def resolve_model_config(model_cfg) -> Qwen2Config:
         with open(os.path.join(path, "config.json")) as f:
             base = json.load(f)
     base.update(over)
-    return Qwen2Config.from_dict(base)
+    # tokenizer.py:21-33 (set_pad_token_id): no pad id -> the eos id (the first one of a list); Meta-Llama-3-8B's
+    # config.json has none, and the Qwen default (151643) is past its 128256-row vocabulary
+    eos = base.get("eos_token_id")
+    eos0 = eos[0] if isinstance(eos, (list, tuple)) else eos
+    if base.get("pad_token_id") is None and eos0 is not None:
+        base["pad_token_id"] = eos0
+    cfg = Qwen2Config.from_dict(base)
+    for name, ids in (("pad_token_id", cfg.pad_token_id), ("eos_token_id", cfg.eos_token_id)):
+        for i in (ids if isinstance(ids, (list, tuple)) else [ids]):
+            if not (isinstance(i, int) and 0 <= i < cfg.vocab_size):
+                raise ValueError(f"{name}={ids!r} is not a token of the {cfg.vocab_size}-row vocabulary ({path})")
+    return cfg
 
 
 _TUNING_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuning", "tunableop_gfx950.csv")

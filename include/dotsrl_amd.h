@@ -169,6 +169,13 @@ int drl_agg_loss(const float* loss_mat, const void* loss_mask, int32_t mask_dtyp
 int drl_logprob_entropy_fwd(const void* logits, int32_t logits_dtype, int64_t N, int64_t V, int64_t ld,
                             const int64_t* labels, float temperature, float* log_prob, float* entropy,
                             float* lse_out, void* stream);
+/* rollout.calculate_log_probs (vllm_rollout_spmd.py:350-395 `rollout_log_probs`; compared with the actor's
+ * old_log_probs by ray_trainer.py:1221-1225 -> utils/debug/metrics.py:63-108): out[n * ld_out + c] =
+ * log softmax(logits[n] / T)[tokens[n * ld_tok + c]] with c = *dev_step (0 when dev_step is NULL), the
+ * temperature applied as drl_logprob_entropy_fwd applies it. One launch per decode step, graph-capturable. */
+int drl_token_logprob(const void* logits, int32_t logits_dtype, int64_t N, int64_t V, int64_t ld, const int64_t* tokens,
+                      int64_t ld_tok, const int64_t* dev_step, float temperature, float* out, int64_t ld_out,
+                      void* stream);
 /* d logits = (dlogp*(onehot - p) - dent*p*(log p + H)) / T   (experimental/torch_functional.py:40-72)
  * dlog_prob / dentropy may be NULL (treated as 0). dlogits (N, V) of dlogits_dtype (F32/BF16), row stride
  * ld_out; dlogits may alias logits (in-place backward, torch_functional.py:81 inplace_backward). */

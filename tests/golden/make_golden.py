@@ -25,6 +25,8 @@ Reference call sites (file:line under /root/reference):
 * GSPO / GMPO (geo_mean) policy losses : verl/trainer/ppo/core_algos.py:892-954, 1143-1210
 * Clip-Cov / KL-Cov policy losses : verl/trainer/ppo/core_algos.py:978-1140
 * masked_mean known answers : tests/utils/test_torch_functional.py:55-66 (reference test, reproduced as data)
+* rollout-vs-actor debug metrics : verl/utils/debug/metrics.py:63-108
+* bf16 production-path update (fp32 and autocast-bf16 reference runs) : verl/workers/actor/dp_actor.py:110, 300-482
 """
 
 import hashlib
@@ -1360,6 +1362,114 @@ def gen_lr_schedule():
         arr[i, :len(s)] = s
     _save("lr_schedule.npz", dict(lr=arr), {"cases": cases, "base_lr": 1e-6,
                                             "ref": "fsdp_workers.py:461-486, torch_functional.py:509-575"})
+
+
+def gen_bf16_update():
+    """The reference DataParallelPPOActor (dp_actor.py:300-482) at Qwen2.5-0.5B width (4 layers, full vocabulary,
+    tied lm_head; tests/golden/bf16_update.py) run twice on the same inputs: in fp32 (autocast disabled, as
+    _ref_actor) and under its own torch.autocast(bf16) (dp_actor.py:110; on this CPU box the device name is 'cpu',
+    so the CPU bf16 autocast runs). SDPA attention (fp32 score accumulation like the GPU's flash-attn). Recorded for
+    both runs: log-probs / entropy, every update metric, per-tensor gradient norms and a fixed sample of gradient
+    elements (captured when the optimizer steps: the accumulated gradient of the 2 micro-batches, before clipping),
+    and the same sample of the parameter update. The bf16-vs-fp32 difference of the reference itself is the
+    yardstick the production bf16 path is held to (tests/test_bf16_update_gpu.py)."""
+    import bf16_update as bu
+    import verl.workers.actor.dp_actor as ref_dp
+    from transformers import Qwen2Config, Qwen2ForCausalLM
+    from verl import DataProto as RefDataProto
+
+    # the GPU reference computes log-probs with flash-attn's cross-entropy (torch_functional.py:81-88: fp32 math over
+    # the bf16 logits, fp32 result); this CPU box has no flash-attn, and the torch fallback (logprobs_from_logits_v2)
+    # would run log_softmax in bf16 and return bf16 log-probs. The fp32-math fallback stands in for flash-attn here.
+    ref_dp.logprobs_from_logits = lambda logits, labels, inplace_backward=True: vF.logprobs_from_logits_v2(
+        logits.float(), labels)
+    sd = bu.make_state_dict()
+    bt = bu.batch()
+    lr = 1e-5
+    acfg = _actor_cfg(entropy_coeff=0.001, ppo_mini_batch_size=bu.B, ppo_micro_batch_size_per_gpu=bu.B // 2)
+    arrays = {k: v for k, v in bt.items() if not k.startswith("noise")}
+    meta = {"config": dict(acfg, policy_loss=dict(acfg["policy_loss"])), "lr": lr, "model": bu.CFG,
+            "weight_checksum": bu.checksum(sd), "runs": {}}
+    old = ref = None
+    embed_idx = bu.embed_rows_index(bt["input_ids"].numpy())
+    for mode in ("fp32", "bf16"):
+        torch.manual_seed(0)
+        model = Qwen2ForCausalLM(Qwen2Config(**bu.CFG, attn_implementation="sdpa")).float()
+        missing, unexpected = model.load_state_dict(sd, strict=False)
+        assert set(missing) <= {"lm_head.weight"} and not unexpected, (missing, unexpected)
+        model.tie_weights()
+        actor, opt = _ref_actor(model, acfg, lr)
+        actor.device_name = "cuda" if mode == "fp32" else "cpu"  # "cpu": the reference's autocast(bf16) on CPU
+        grads = {}
+        step0 = opt.step
+
+        def step(*a, _g=grads, _m=model, _s=step0, **k):
+            for n, prm in _m.named_parameters():
+                _g[n] = prm.grad.detach().clone()
+            return _s(*a, **k)
+
+        opt.step = step
+        data = RefDataProto.from_dict(tensors={k: bt[k] for k in ("input_ids", "attention_mask", "position_ids",
+                                                                   "responses")},
+                                      meta_info={"micro_batch_size": bu.B // 2, "temperature": 1.0,
+                                                 "use_dynamic_bsz": False})
+        logp, ent = actor.compute_log_prob(data, calculate_entropy=True)
+        assert torch.isfinite(logp).all() and torch.isfinite(ent).all()
+        if mode == "fp32":
+            rm = bt["response_mask"]
+            old = ((logp + 0.3 * bt["noise_old"]) * rm).detach()
+            ref = ((logp + 0.2 * bt["noise_ref"]) * rm).detach()
+        before = {n: q.detach().clone() for n, q in model.named_parameters()}
+        udata = RefDataProto.from_dict(tensors={**{k: bt[k] for k in ("input_ids", "attention_mask", "position_ids",
+                                                                      "responses", "response_mask", "advantages")},
+                                                "old_log_probs": old, "ref_log_prob": ref},
+                                       meta_info={"temperature": 1.0})
+        metrics = actor.update_policy(udata)
+        assert len(grads) > 0
+        run = {"metrics": {k: [float(x) for x in v] for k, v in metrics.items()},
+               "grad_norms": {n: float(g.double().norm()) for n, g in grads.items()},
+               "delta_abs_sums": {n: float((q.detach() - before[n]).double().abs().sum())
+                                  for n, q in model.named_parameters()}}
+        meta["runs"][mode] = run
+        arrays[f"{mode}_log_probs"] = logp.detach().float()
+        arrays[f"{mode}_entropys"] = ent.detach().float()  # bf16 in the autocast run (entropy_from_logits on bf16)
+        for n, g in grads.items():
+            idx = embed_idx if n == "model.embed_tokens.weight" else bu.sample_index(n, g.numel())
+            arrays[f"{mode}_grad.{n}"] = g.reshape(-1)[torch.from_numpy(idx)]
+            arrays[f"{mode}_delta.{n}"] = (dict(model.named_parameters())[n].detach() - before[n]).reshape(-1)[
+                torch.from_numpy(idx)]
+        del model, actor, opt, grads
+    arrays["old_log_probs"], arrays["ref_log_prob"] = old, ref
+    meta["ref"] = ("dp_actor.py:110 (autocast bf16), 300-482 (compute_log_prob, update_policy), 282-298 (clip + step); "
+                   "fsdp_workers.py:454-459 (AdamW); HF Qwen2ForCausalLM, SDPA attention")
+    _save("bf16_update.npz", arrays, meta)
+
+
+def gen_debug_metrics():
+    """utils/debug/metrics.py:63-108 calculate_debug_metrics (ray_trainer.py:1221-1225) on seeded rollout / actor
+    log-probs: with a response_mask, and with only an attention_mask (prompt + response columns)."""
+    from types import SimpleNamespace
+
+    import verl.utils.debug.metrics as dm
+
+    g = torch.Generator().manual_seed(63)
+    cases, arrays = [], {}
+    for ci, (B, P, R, key) in enumerate([(6, 5, 12, "response_mask"), (4, 3, 9, "attention_mask")]):
+        old = -torch.rand(B, R, generator=g) * 4
+        roll = old + torch.randn(B, R, generator=g) * 0.05
+        lens = torch.randint(1, R + 1, (B,), generator=g)
+        rmask = (torch.arange(R)[None, :] < lens[:, None]).to(torch.int64)
+        roll = torch.where(rmask.bool(), roll, torch.full_like(roll, -1.0))
+        batch = {"rollout_log_probs": roll, "old_log_probs": old, "responses": torch.zeros(B, R, dtype=torch.int64)}
+        if key == "response_mask":
+            batch["response_mask"] = rmask
+        else:
+            batch["attention_mask"] = torch.cat([torch.ones(B, P, dtype=torch.int64), rmask], -1)
+        out = dm.calculate_debug_metrics(SimpleNamespace(batch=batch))
+        for k, v in batch.items():
+            arrays[f"c{ci}_{k}"] = v
+        cases.append({"mask_key": key, "metrics": {k: float(v) for k, v in out.items()}})
+    _save("debug_metrics.npz", arrays, {"cases": cases, "ref": "verl/utils/debug/metrics.py:63-108"})
 
 
 if __name__ == "__main__":

@@ -144,17 +144,24 @@ def test_bf16_full_depth_margin_checked(ref, weights, packed, hip_gemm_rows, mon
     print(f"bf16 {'packed' if packed else 'unpacked'} rollout: tokens matching the fp32 reference per row {matched}")
 
 
-def test_bf16_packed_decode_teacher_forced(ref, weights):
+@pytest.mark.parametrize("rows", [4, 512])
+def test_bf16_packed_decode_teacher_forced(ref, weights, rows):
     """The decode path the bench runs — prefill, then qwen2.PackedDecode's graphed step (decode_gemm.hip projections,
     decode_mfma_kernel attention, dec_rmsnorm, the step prologue) — fed the reference's own tokens (teacher forcing,
     hf_rollout.py:112-171 generate's inputs), so every step sees the reference context; its lm_head logits against
-    the reference HF fp32 logits of the same step."""
+    the reference HF fp32 logits of the same step. rows = 512: the fixture's 4 rows tiled 128 times, so the decode
+    planner picks the bench's 512-row kernels (decode_gemm_lds / decode_gemm_tiled / decode_mfma_kernel<64, 2>,
+    profiles/r03_decode_step_512rows.txt); every row is held to the bound of its own source row."""
     from dots.rl_amd.qwen2 import KVCache, PackedDecode
 
-    z, meta = ref
+    z0, meta = ref
+    rep = rows // z0["prompt_ids"].shape[0]
+    z = {k: (np.concatenate([z0[k]] * rep, 0) if z0[k].ndim >= 1 and z0[k].shape[0] == z0["prompt_ids"].shape[0]
+             else z0[k]) for k in z0.files if k != "__meta__"}
     model = _model(weights, torch.bfloat16)
     ids, am, pos = T(z["prompt_ids"]), T(z["prompt_attention_mask"]), T(z["prompt_position_ids"])
     B, P = ids.shape
+    assert B == rows
     R = int(meta["response_length"])
     assert PackedDecode.supported(model, B)
     resp = T(z["responses"])

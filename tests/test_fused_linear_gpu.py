@@ -117,3 +117,67 @@ def test_matches_unfused_path_and_is_deterministic():
     ulp, uent, _ = native.logprob_entropy_fwd(hb @ wb.t(), lab, 1.0)
     np.testing.assert_allclose(lp.cpu().numpy(), ulp.cpu().numpy(), rtol=0, atol=5e-2)
     np.testing.assert_allclose(ent.cpu().numpy(), uent.cpu().numpy(), rtol=0, atol=5e-2)
+
+
+def test_backward_vocab_blocks_equal_one_block(monkeypatch):
+    """The backward's vocabulary blocks (the reference's _Split_Dlogits_N, kernels.py:1519-1580) against one block:
+    d_W bit-identical (each block's rows are the same GEMM), d_hidden within one bf16 rounding (fp32 partial sums
+    over the blocks, rounded once); ragged N (200: the zero-padded 64-token k-tiles of the d_W GEMM)."""
+    import dots.rl_amd.torch_functional as tf
+
+    N, H, V, temp = 200, 128, 2500, 1.3
+    h, w, ids = make(N, H, V, seed=31)
+    rng = np.random.default_rng(9)
+    dlp, den = rng.standard_normal(N).astype(np.float32), rng.standard_normal(N).astype(np.float32)
+
+    def grads():
+        hb = T(h, torch.bfloat16).requires_grad_(True)
+        gw = torch.zeros((V, H), dtype=torch.float32, device=DEV)
+        lp, ent = fused_linear_logprob_entropy(hb, T(w, torch.bfloat16), T(ids), temp, True, weight_grad=gw)
+        ((lp * T(dlp)).sum() + (ent * T(den)).sum()).backward()
+        return hb.grad.float(), gw
+
+    dh1, dw1 = grads()
+    assert tf.fused_linear_vocab_block(V, 256) == V
+    monkeypatch.setattr(tf, "_BUFFER_RANGE", 2 * 256 * (512 + 320))  # 512-row blocks: 5 blocks, the last ragged
+    assert tf.fused_linear_vocab_block(V, 256) == 512
+    dh5, dw5 = grads()
+    assert torch.equal(dw1, dw5)
+    assert (dh1 - dh5).abs().max().item() <= dh1.abs().max().item() * 2.0 ** -7
+    rdh, rdw = oracle.fused_linear_backward(h, w, ids, dlp, den, temp)
+    assert np.abs(dh5.cpu().numpy() - rdh).max() / np.abs(rdh).max() < 2e-2
+
+
+def test_backward_long_batch_over_2gb():
+    """N = 8192 tokens x V = 151936: d_logits^T (2.5 GB bf16) is past the 2 GB operand range, so the backward runs
+    two vocabulary blocks (the ADVICE r03 failure: one layout-T operand over 2 GB with a bf16 d_hidden). Checked
+    against torch fp32 on the GPU (fp32 logits, softmax, the d_logits formula of torch_functional.py:40-72 rounded
+    to bf16, fp32 GEMMs): 2e-2 of the largest entry, as the oracle check above."""
+    import dots.rl_amd.torch_functional as tf
+
+    N, H, V, temp = 8192, 896, 151936, 1.0
+    assert tf.fused_linear_vocab_block(V, N) < V
+    g = torch.Generator(device=DEV).manual_seed(4)
+    hb = ((torch.rand(N, H, device=DEV, generator=g) - 0.5) * 0.5).to(torch.bfloat16)
+    wb = ((torch.rand(V, H, device=DEV, generator=g) - 0.5) * 0.5).to(torch.bfloat16)
+    ids = torch.randint(0, V, (N,), device=DEV, generator=g)
+    dlp, den = torch.randn(N, device=DEV, generator=g), torch.randn(N, device=DEV, generator=g)
+    h = hb.clone().requires_grad_(True)
+    gw = torch.zeros(V, H, dtype=torch.float32, device=DEV)
+    lp, ent = fused_linear_logprob_entropy(h, wb, ids, temp, True, weight_grad=gw)
+    ((lp * dlp).sum() + (ent * den).sum()).backward()
+    assert torch.isfinite(h.grad.float()).all() and torch.isfinite(gw).all()
+    with torch.no_grad():
+        z = hb.float() @ wb.float().t()
+        logp = torch.log_softmax(z, -1)
+        p = logp.exp()
+        entr = -(p * logp).sum(-1, keepdim=True)
+        dz = -p * (dlp[:, None] + den[:, None] * (logp + entr))
+        dz[torch.arange(N, device=DEV), ids] += dlp
+        del z, logp, p
+        dz = dz.to(torch.bfloat16).float()
+        rdh = dz @ wb.float()
+        rdw = dz.t() @ hb.float()
+    for got, ref in ((h.grad.float(), rdh), (gw, rdw)):
+        err = ((got - ref).abs().max() / ref.abs().max()).item()
+        assert err < 2e-2, err

@@ -98,6 +98,56 @@ def test_graphed_sampling_rollout_equals_eager():
     assert not torch.equal(tk[0].batch["responses"], outs[0].batch["responses"])
 
 
+@pytest.mark.parametrize("use_hip_graph", [True, False])
+def test_rollout_calculate_log_probs(use_hip_graph):
+    """rollout.calculate_log_probs (vllm_rollout_spmd.py:350-395): the fp32 greedy rollout's rollout_log_probs are
+    the reference HF model's log-probs of the same tokens (golden log_probs, 1e-4) inside the response and -1 past
+    it; a bf16 sampled rollout's (T = 0.9) track the actor's compute_log_prob at that temperature (the decode step's
+    bf16 logits vs the full-sequence pass: 0.05) and feed the reference's debug metrics."""
+    from dots.rl_amd.config import to_attr
+    from dots.rl_amd.dp_actor import DataParallelPPOActor
+    from dots.rl_amd.metric_utils import calculate_debug_metrics
+    from dots.rl_amd.protocol import DataProto
+    from dots.rl_amd.rollout import MI355XRollout
+
+    z, meta = golden()
+
+    def prompts():
+        return DataProto.from_dict({"input_ids": T(z["prompt_ids"]), "attention_mask": T(z["prompt_attention_mask"]),
+                                    "position_ids": T(z["prompt_position_ids"])},
+                                   meta_info={"eos_token_id": meta["eos_token_id"], "pad_token_id": meta["pad_token_id"]})
+
+    cfg, store, model = build()
+    rcfg = to_attr(dict(do_sample=False, temperature=1.0, top_k=-1, top_p=1.0, response_length=meta["response_length"],
+                        ignore_eos=False, seed=0, val_kwargs={}, use_hip_graph=use_hip_graph, calculate_log_probs=True))
+    out = MI355XRollout(model, rcfg).generate_sequences(prompts())
+    np.testing.assert_array_equal(out.batch["responses"].cpu().numpy(), z["responses"])
+    R = z["responses"].shape[1]
+    mask = z["attention_mask"][:, -R:].astype(bool)
+    got = out.batch["rollout_log_probs"].cpu().numpy()
+    np.testing.assert_allclose(got[mask], z["log_probs"][mask], rtol=1e-4, atol=1e-4)
+    assert (got[~mask] == -1.0).all()
+
+    cfg, store, model = build(torch.bfloat16, trainable=False)
+    rcfg = to_attr(dict(do_sample=True, temperature=0.9, top_k=-1, top_p=1.0, response_length=24, ignore_eos=False,
+                        seed=5, val_kwargs={}, use_hip_graph=use_hip_graph, calculate_log_probs=True))
+    out = MI355XRollout(model, rcfg).generate_sequences(prompts())
+    plain = MI355XRollout(model, to_attr(dict(rcfg, calculate_log_probs=False))).generate_sequences(prompts())
+    assert torch.equal(out.batch["responses"], plain.batch["responses"])  # the log-probs change no token
+    actor = DataParallelPPOActor(to_attr({}), model)
+    data = out.select(["input_ids", "attention_mask", "position_ids", "responses"])
+    data.meta_info.update({"micro_batch_size": 4, "temperature": 0.9, "use_dynamic_bsz": False})
+    lp, _ = actor.compute_log_prob(data, calculate_entropy=False)
+    m = out.batch["attention_mask"][:, -24:].bool()
+    rl = out.batch["rollout_log_probs"]
+    assert (rl[~m] == -1.0).all()
+    assert (rl[m] - lp[m]).abs().max().item() < 0.05
+    out.batch["old_log_probs"] = lp
+    out.batch["response_mask"] = m.to(torch.int64)
+    dm = calculate_debug_metrics(out)
+    assert dm["training/rollout_probs_diff_max"] < 0.05 and dm["training/rollout_actor_probs_pearson_corr"] > 0.99
+
+
 @pytest.mark.parametrize("temperature,key", [(1.0, "log_probs"), (0.7, "log_probs_t07")])
 def test_log_prob_matches_reference(temperature, key):
     from dots.rl_amd.config import to_attr

@@ -121,3 +121,18 @@ def test_flops_counter_matches_reference():
     np.testing.assert_allclose(est, meta["flops_tiny_tflops"], rtol=1e-6)
     est, _ = FlopsCounter(Qwen2Config.from_dict(QWEN25_05B)).estimate_flops([768] * 512, 1.0)
     np.testing.assert_allclose(est, meta["flops_qwen05b_768x512_tflops"], rtol=1e-12)
+
+
+def test_rollout_debug_metrics_match_reference(golden):
+    """rollout.calculate_log_probs' monitor: training/rollout_probs_diff_* and the Pearson correlation against the
+    reference's calculate_debug_metrics (utils/debug/metrics.py:63-108) on golden debug_metrics.npz, with a
+    response_mask and with only an attention_mask."""
+    from dots.rl_amd.metric_utils import calculate_debug_metrics
+
+    z, meta = golden("debug_metrics.npz")
+    for ci, case in enumerate(meta["cases"]):
+        keys = [k[len(f"c{ci}_"):] for k in z.files if k.startswith(f"c{ci}_")]
+        got = calculate_debug_metrics(DataProto.from_dict({k: torch.from_numpy(z[f"c{ci}_{k}"]) for k in keys}))
+        assert set(got) == set(case["metrics"])
+        for k, v in case["metrics"].items():
+            assert got[k] == pytest.approx(v, rel=1e-5, abs=1e-7), k

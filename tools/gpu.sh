@@ -1,0 +1,77 @@
+#!/bin/bash
+# One MI355X job through gpurun: a chain of named steps, each under its own time limit; the chain stops at the
+# first failure (a GPU fault, abort or time-limit kill ends the job, nothing is retried).
+#   usage: bash tools/gpu.sh <tag> <step> [<step> ...]        (outputs under gpurun_out/<tag>/)
+# steps:
+#   tests                       the whole -m gpu suite
+#   tests:<a>,<b>,...           the named pytest targets (files or node ids), -m gpu, verbose
+#   bench[:<steps>[:<warmup>]]  the default bench line (no CPU baseline) + the last step's drl_gemm launch log
+#   benchfull                   the driver's bench command (python bench.py, CPU baseline included)
+#   bench64                     the per-rank workload of N = 8 (64 sequences) ; bench128 / bench256 likewise
+#   profile                     rocprofv3 kernel stats of a 2-step bench + trace summary
+#   pmc_gemm                    FETCH_SIZE / WRITE_SIZE passes over drl_gemm -> profiles/pmc_drl_gemm.json
+#   py:<script>[:<args>]        python -u <script> <args> (args split on ':')
+set -o pipefail
+TAG=${1:?tag}; shift
+ROOT=$(pwd)
+OUT=$ROOT/gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+
+run_tests() {  # $1 = log name, rest = pytest targets
+  local log=$OUT/$1; shift
+  timeout -k 10 900 python -u -m pytest "$@" -m gpu -x -q --timeout 300 --timeout-method thread > "$log" 2>&1
+  local rc=$?
+  tail -3 "$log"
+  [ $rc = 0 ] || { grep -E "FAIL|Error|assert" "$log" | head -30; return 1; }
+}
+
+bench_rows() {  # $1 = sequences per step
+  local b=$(( $1 / 8 )); local mini=$(( b / 2 < 4 ? 4 : b / 2 ))
+  timeout -k 10 400 python -u bench.py --steps 3 --warmup 2 --no-cpu-baseline --override data.train_batch_size=$b \
+    actor_rollout_ref.actor.ppo_mini_batch_size=$mini > "$OUT/bench$1.json" 2> "$OUT/bench$1.err" \
+    || { tail -20 "$OUT/bench$1.err"; return 1; }
+  cut -c1-700 "$OUT/bench$1.json"
+}
+
+for step in "$@"; do
+  echo "== $step"
+  case "$step" in
+    tests) run_tests tests.log tests || exit 1 ;;
+    tests:*) IFS=',' read -ra T <<< "${step#tests:}"; run_tests "tests_$(date +%s).log" -v "${T[@]}" || exit 1 ;;
+    bench|bench:*)
+      IFS=':' read -ra A <<< "$step"; K=${A[1]:-5}; W=${A[2]:-2}
+      timeout -k 10 500 python -u bench.py --steps "$K" --warmup "$W" --no-cpu-baseline \
+        --launch-log "$OUT/gemm_launches.jsonl" > "$OUT/bench.json" 2> "$OUT/bench.err" \
+        || { tail -20 "$OUT/bench.err"; exit 1; }
+      cat "$OUT/bench.json" ;;
+    benchfull)
+      timeout -k 10 600 python -u bench.py > "$OUT/benchfull.json" 2> "$OUT/benchfull.err" \
+        || { tail -20 "$OUT/benchfull.err"; exit 1; }
+      cat "$OUT/benchfull.json" ;;
+    bench64) bench_rows 64 || exit 1 ;;
+    bench128) bench_rows 128 || exit 1 ;;
+    bench256) bench_rows 256 || exit 1 ;;
+    profile)
+      timeout -k 10 500 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/prof" -o run -- python3 "$ROOT/bench.py" \
+        --steps 2 --warmup 2 --no-cpu-baseline > "$OUT/prof.log" 2>&1 || { tail -20 "$OUT/prof.log"; exit 1; }
+      TR=$(find "$OUT/prof" -name "*kernel_trace.csv" | head -1)
+      python3 tools/trace_summary.py "$TR" 30 > "$OUT/trace_summary.txt" || exit 1
+      find "$OUT/prof" -name "*kernel_trace.csv" -delete
+      head -40 "$OUT/trace_summary.txt" ;;
+    pmc_gemm)
+      for c in FETCH_SIZE WRITE_SIZE; do
+        timeout -s KILL 400 rocprofv3 --pmc $c --kernel-include-regex gemm_sk_kernel -f csv -d "$OUT/pmc_$c" -o p \
+          -- python3 "$ROOT/bench.py" --steps 1 --warmup 1 --no-cpu-baseline > "$OUT/pmc_$c.log" 2>&1 \
+          || { tail -5 "$OUT/pmc_$c.log"; exit 1; }
+      done
+      python3 tools/pmc_traffic.py drl_gemm "$OUT/pmc_FETCH_SIZE" "$OUT/pmc_WRITE_SIZE" || exit 1
+      cp profiles/pmc_drl_gemm.json "$OUT/"
+      find "$OUT" -name "*.csv" -size +20M -delete ;;
+    py:*)
+      IFS=':' read -ra A <<< "${step#py:}"
+      timeout -k 10 600 python -u "${A[@]}" > "$OUT/$(basename "${A[0]}" .py).out" 2>&1; rc=$?
+      tail -40 "$OUT/$(basename "${A[0]}" .py).out"; [ $rc = 0 ] || exit 1 ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
