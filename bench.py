@@ -66,11 +66,6 @@ def _swiglu_fwd_bytes(a):
     return 3 * N * I * (2 if dt == 4 else 4)
 
 
-def _gemm_flops(a):
-    # drl_gemm_bf16_nt(a, lda, b, ldb, c, ldc, M, N, K, bias, epilogue, c2, ldc2, stream): 2 M N K
-    return 2.0 * a[6] * a[7] * a[8]
-
-
 def _gemm_sk_flops(a):
     # drl_gemm(a, lda, a_layout, b, ldb, b_layout, c, ldc, c_dtype, beta, M, N, K, bias, epilogue, ...): 2 M N K
     return 2.0 * a[10] * a[11] * a[12]
@@ -105,9 +100,6 @@ ROOFLINE = {
     "drl_gemm": (_gemm_sk_flops, "2*M*N*K FLOP per launch (bf16 operands, fp32 accumulation): every projection GEMM "
                  "of the full-sequence passes — forward (bias / SwiGLU epilogues), dgrad, wgrad into the fp32 "
                  "gradient, lm_head forward and backward", "mfma", PEAK_BF16_TFLOPS, "TFLOP/s"),
-    "drl_gemm_bf16_nt": (_gemm_flops, "2*M*N*K FLOP per launch (bf16 operands, fp32 accumulation; qkv + bias, "
-                         "o_proj, gate_up + fused SwiGLU of every full-sequence forward)", "mfma", PEAK_BF16_TFLOPS,
-                         "TFLOP/s"),
     "drl_swiglu_fwd": (_swiglu_fwd_bytes, "6 B per (token, intermediate column): gate + up read, product written (bf16)",
                        "hbm", PEAK_HBM_GBPS, "GB/s"),
     "drl_flash_attn_fwd": (_flash_fwd_flops, "4*D FLOP per causal (query, key) pair per query head", "mfma",

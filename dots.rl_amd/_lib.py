@@ -153,9 +153,6 @@ SIGNATURES = {
                                           P]),
     "drl_decode_attention": (ctypes.c_int, [P, P, P, I32, P, I64, P, I64, I64, I64, I64, I64, I64, I64, F32, P, P, SZ,
                                             P]),
-    "drl_linear_decode_workspace_bytes": (SZ, [I64, I64, I64, I32]),
-    "drl_linear_decode_set_plan": (None, [I32, I32]),
-    "drl_linear_decode": (ctypes.c_int, [P, I64, P, P, I32, I64, I64, I64, I32, P, I64, P, SZ, P]),
     "drl_linear_logprob_workspace_bytes": (SZ, [I64, I64, I64]),
     "drl_linear_select_tokens_workspace_bytes": (SZ, [I64]),
     "drl_linear_select_tokens": (ctypes.c_int, [P, I64, P, I32, I64, I64, I64, P, P, P, I64, P, SZ, P]),
@@ -163,14 +160,10 @@ SIGNATURES = {
     "drl_decode_gemm_plan": (ctypes.c_int, [I64, I64, I64, I32, P, P]),
     "drl_decode_gemm_set_plan": (None, [I32, I32]),
     "drl_decode_gemm_set_tiled": (None, [I32]),
-    "drl_gemm_bf16_nt": (ctypes.c_int, [P, I64, P, I64, P, I64, I64, I64, I64, P, I32, P, I64, P]),
-    "drl_gemm_set_tile": (None, [I32]),
-    "drl_gemm_set_group": (None, [I32]),
     "drl_gemm": (ctypes.c_int, [P, I64, I32, P, I64, I32, P, I64, I32, I32, I64, I64, I64, P, I32, P, I64, P, I64, P]),
     "drl_gemm_workspace_bytes": (ctypes.c_int64, []),
     "drl_gemm_set_sk_tuning": (None, [I32, I32, I32, I32]),
     "drl_gemm_set_debug": (None, [I32]),
-    "drl_transpose16": (ctypes.c_int, [P, I64, I64, I64, P, I64, P]),
     "drl_copy_rows": (ctypes.c_int, [P, I64, P, P, I64, P, I64, I64, P]),
     "drl_colsum_bf16_workspace_bytes": (SZ, [I64, I64]),
     "drl_colsum_bf16_acc": (ctypes.c_int, [P, I64, I64, I64, P, P, SZ, P]),

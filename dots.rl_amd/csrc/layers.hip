@@ -751,54 +751,6 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_vec_kernel(const float* x, co
   }
 }
 
-// 16-bit transpose dst (cols, rows) = src (rows, cols)^T through a 64 x 64 LDS tile (rows padded by one
-// element: conflict-free column reads); 16-B row loads, 8-B column stores of 4 consecutive elements. Used for the
-// weights' transposed copies (dgrad dx = dy W as the TN product dy (W^T)^T), refreshed after every optimizer step.
-__global__ __launch_bounds__(256) void transpose16_kernel(const uint16_t* src, int64_t lds_, int64_t rows, int64_t cols,
-                                                          uint16_t* dst, int64_t ldd) {
-  __shared__ uint16_t tile[64][65];
-  const int64_t r0 = static_cast<int64_t>(blockIdx.y) * 64, c0 = static_cast<int64_t>(blockIdx.x) * 64;
-  const int t = threadIdx.x;
-  // load: 64 rows x 64 cols = 512 chunks of 8 elements, 2 per thread
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int ch = t + 256 * i, r = ch >> 3, cc = (ch & 7) * 8;
-    const int64_t gr = r0 + r, gc = c0 + cc;
-    uint16_t v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (gr < rows) {
-      if (gc + 7 < cols && ((lds_ & 7) == 0)) {
-        const uint4 u = *reinterpret_cast<const uint4*>(src + gr * lds_ + gc);
-        v[0] = u.x & 0xffff; v[1] = u.x >> 16; v[2] = u.y & 0xffff; v[3] = u.y >> 16;
-        v[4] = u.z & 0xffff; v[5] = u.z >> 16; v[6] = u.w & 0xffff; v[7] = u.w >> 16;
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if (gc + j < cols) v[j] = src[gr * lds_ + gc + j];
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) tile[r][cc + j] = v[j];
-  }
-  __syncthreads();
-  // store: dst row = source column c0 + c, 4 consecutive source rows per thread
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int ch = t + 256 * i, c = ch >> 4, rr = (ch & 15) * 4;
-    const int64_t gc = c0 + c, gr = r0 + rr;
-    if (gc >= cols) continue;
-    uint16_t* d = dst + gc * ldd + gr;
-    if (gr + 3 < rows && ((ldd & 3) == 0)) {
-      const uint2 u = make_uint2(static_cast<uint32_t>(tile[rr][c]) | (static_cast<uint32_t>(tile[rr + 1][c]) << 16),
-                                 static_cast<uint32_t>(tile[rr + 2][c]) | (static_cast<uint32_t>(tile[rr + 3][c]) << 16));
-      *reinterpret_cast<uint2*>(d) = u;
-    } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (gr + j < rows) d[j] = tile[rr + j][c];
-    }
-  }
-}
-
 // Column sums of a bf16 (N, C) matrix (the qkv bias gradient = dqkv summed over tokens), phase 1: workgroup
 // (64-column stripe, row slice) -> fp32 partials (slices, C); thread = 8 columns (one 16-B load) x every 32nd row
 // of the slice, combined in LDS in a fixed order. Phase 2 is colsum_kernel (fixed slice order): deterministic.
@@ -1158,18 +1110,6 @@ int drl_colsum_bf16_acc(const void* x, int64_t ld, int64_t N, int64_t C, float* 
                      dim3(256), 0, s, static_cast<const uint16_t*>(x), ld, N, C, per, part);
   DRL_LAUNCH_CHECK();
   hipLaunchKernelGGL(colsum_kernel, dim3(static_cast<unsigned>((C + 15) / 16)), dim3(256), 0, s, part, slices, C, out);
-  DRL_LAUNCH_CHECK();
-  return DRL_OK;
-}
-
-int drl_transpose16(const void* src, int64_t ld_src, int64_t rows, int64_t cols, void* dst, int64_t ld_dst,
-                    void* stream) {
-  using namespace drl;
-  DRL_CHECK_ARG(src && dst && rows >= 1 && cols >= 1 && ld_src >= cols && ld_dst >= rows, "bad transpose shape");
-  DRL_CHECK_ARG(aligned16(src) && (reinterpret_cast<uintptr_t>(dst) & 7u) == 0, "src 16-byte / dst 8-byte aligned");
-  const dim3 grid(static_cast<unsigned>((cols + 63) / 64), static_cast<unsigned>((rows + 63) / 64));
-  hipLaunchKernelGGL(transpose16_kernel, grid, dim3(256), 0, static_cast<hipStream_t>(stream),
-                     static_cast<const uint16_t*>(src), ld_src, rows, cols, static_cast<uint16_t*>(dst), ld_dst);
   DRL_LAUNCH_CHECK();
   return DRL_OK;
 }

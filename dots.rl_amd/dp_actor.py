@@ -235,9 +235,11 @@ def exec_groups(cfg, model_cfg, micro_batches):
         # saved per token and layer: x, x2 (fp32), h1, h2, attn (bf16), q / k / v / k^T, gate|up and SwiGLU out
         per_tok = L * (8 * H + 6 * H + 4 * nq + 6 * I)
         budget = float(cfg.get("exec_activation_gb", 110)) * 2 ** 30
-        if torch.cuda.is_available():  # never plan past half of what is free (the device's + torch's cached pool)
-            avail = torch.cuda.mem_get_info()[0] + torch.cuda.memory_reserved() - torch.cuda.memory_allocated()
-            budget = min(budget, 0.5 * avail)
+        if torch.cuda.is_available():
+            # never plan past 40 % of the device — a static bound (not what happens to be free at the call), so the
+            # group size, and with it the GEMM shapes and the fp32 gradient summation order, is the same on every
+            # rank, run and resume
+            budget = min(budget, 0.4 * torch.cuda.get_device_properties(torch.cuda.current_device()).total_memory)
         toks = max(mb.batch["input_ids"].numel() for mb in micro_batches)
         n = max(1, int(budget // max(1, per_tok * toks)))
     return balanced_groups(micro_batches, n)

@@ -781,19 +781,6 @@ def flash_attn_bwd(q, k, kt, v, o, dout, lse, key_valid, dq, dk, dv):
           "drl_flash_attn_bwd")
 
 
-def transpose16(src, out=None):
-    """(rows, cols) 16-bit (bf16) -> (cols, rows) contiguous (csrc/layers.hip transpose16_kernel)."""
-    _dev(src, out)
-    assert src.dim() == 2 and src.stride(1) == 1 and src.element_size() == 2
-    rows, cols = src.shape
-    if out is None:
-        out = torch.empty(cols, rows, dtype=src.dtype, device=src.device)
-    assert out.shape == (cols, rows) and out.stride(1) == 1 and out.dtype == src.dtype
-    check(lib().drl_transpose16(_p(src), src.stride(0), rows, cols, _p(out), out.stride(0), _stream()),
-          "drl_transpose16")
-    return out
-
-
 def colsum_bf16_acc(x, out):
     """out (C,) fp32 += x (N, C) bf16 summed over rows (csrc/layers.hip, deterministic)."""
     _dev(x, out)
@@ -807,28 +794,6 @@ def colsum_bf16_acc(x, out):
 
 
 GEMM_PLAIN, GEMM_BIAS, GEMM_SWIGLU, GEMM_SWIGLU_BWD = 0, 1, 2, 3
-
-
-def gemm_nt(x, w, bias=None, swiglu=False, out=None, out_gu=None):
-    """Full-sequence projection (csrc/gemm.hip): x (M, K) bf16 @ w (N, K)^T -> (M, N) bf16 (+ bias); with
-    ``swiglu`` (w = [gate | up], N = 2I) -> a (M, I) = bf16(bf16(silu(g)) * u), and ``out_gu`` (M, N) receives
-    [g | u] (bf16) for the backward."""
-    _dev(x, w, bias, out, out_gu)
-    assert x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x.dim() == 2 and w.dim() == 2
-    assert x.stride(1) == 1 and w.stride(1) == 1 and x.shape[1] == w.shape[1]
-    M, K = x.shape
-    N = w.shape[0]
-    n_out = N // 2 if swiglu else N
-    if out is None:
-        out = torch.empty(M, n_out, dtype=torch.bfloat16, device=x.device)
-    assert out.shape == (M, n_out) and out.stride(1) == 1 and out.dtype == torch.bfloat16
-    if out_gu is not None:
-        assert swiglu and out_gu.shape == (M, N) and out_gu.stride(1) == 1
-    epi = GEMM_SWIGLU if swiglu else (GEMM_BIAS if bias is not None else GEMM_PLAIN)
-    check(lib().drl_gemm_bf16_nt(_p(x), x.stride(0), _p(w), w.stride(0), _p(out), out.stride(0), M, N, K,
-                                 _p(bias), epi, _p(out_gu), out_gu.stride(0) if out_gu is not None else 0, _stream()),
-          "drl_gemm_bf16_nt")
-    return out
 
 
 def copy_rows(src, dst, src_idx=None, dst_idx=None, n=None):
@@ -941,31 +906,6 @@ def linear_wgrad(gw, dy, x, accumulate=True, ws_slot=0):
     N = x.shape[1]
     assert x.shape[0] == T and gw.shape == (M, N) and gw.dtype == torch.float32
     return gemm(dy, LAYOUT_T, x, LAYOUT_T, M, N, T, gw, beta=accumulate, ws_slot=ws_slot)
-
-
-LINEAR_NONE, LINEAR_BIAS, LINEAR_SWIGLU = 0, 1, 2
-
-
-def linear_decode(x, w, bias=None, swiglu=False, out=None):
-    """Decode-step linear layer (csrc/linear.hip): x (M, K) bf16 @ w (N, K)^T (+ bias) -> (M, N) bf16, or with
-    ``swiglu`` (w = [gate | up]) silu(x Wg^T) * (x Wu^T) -> (M, N/2)."""
-    _dev(x, w)
-    M, K = x.shape
-    N = w.shape[0]
-    assert x.stride(1) == 1 and w.is_contiguous() and w.shape[1] == K and x.dtype == w.dtype
-    epi = LINEAR_SWIGLU if swiglu else (LINEAR_BIAS if bias is not None else LINEAR_NONE)
-    n_out = N // 2 if swiglu else N
-    if out is None:
-        out = torch.empty(M, n_out, dtype=x.dtype, device=x.device)
-    assert out.stride(1) == 1 and out.shape == (M, n_out)
-    if bias is not None:
-        _dev(bias)
-        assert bias.is_contiguous() and bias.numel() == N
-    nws = lib().drl_linear_decode_workspace_bytes(M, N, K, epi)
-    ws = _linear_workspace(x.device, nws) if nws else None
-    check(lib().drl_linear_decode(_p(x), x.stride(0), _p(w), _p(bias), _edt(x), M, N, K, epi, _p(out), out.stride(0),
-                                  _p(ws), nws, _stream()), "drl_linear_decode")
-    return out
 
 
 _LINEAR_WS = {}

@@ -63,12 +63,6 @@ typedef enum drl_kl_type {
   DRL_KL_K3 = 3,    /* "low_var_kl" / "k3" */
 } drl_kl_type;
 
-/* Epilogues of drl_linear_decode */
-typedef enum drl_linear_epilogue {
-  DRL_LINEAR_NONE = 0,   /* y = x W^T */
-  DRL_LINEAR_BIAS = 1,   /* y = x W^T + bias (qkv_proj) */
-  DRL_LINEAR_SWIGLU = 2, /* W = [gate (I rows) | up (I rows)]: y (M, I) = silu(x Wg^T) * (x Wu^T) (Qwen2MLP) */
-} drl_linear_epilogue;
 
 const char* drl_last_error(void);
 int drl_abi_version(void);
@@ -468,20 +462,6 @@ int drl_flash_attn_bwd(const void* q, const void* k, const void* kt, const void*
                        const float* lse, int32_t dt, const uint8_t* key_valid, int64_t ld_valid, int64_t B,
                        int64_t Hkv, int64_t G, int64_t D, int64_t T, int64_t ld_t, float scale, float* delta, void* dq,
                        void* dk, void* dv, void* stream);
-/* Linear layer of the decode step (M = one token per sequence, M small): y (M, N or N/2) = epilogue(x W^T).
- * Replaces the nn.Linear calls of Qwen2Attention / Qwen2MLP / lm_head (transformers modeling_qwen2, run by
- * hf_rollout.py:112-124 generate) at decode time. x (M, ld_x) bf16, W (N, K) bf16 row-major, bias (N) bf16,
- * out (M, ld_out) bf16; fp32 accumulation, one rounding to bf16 after the bias (SWIGLU: gate and up rounded
- * to bf16, silu(gate) rounded, product rounded: the bf16 module semantics). 1 <= M <= 128, K % 16 == 0,
- * x rows and W 16-byte aligned. Deterministic (fixed-order partial sums). workspace: 256-byte aligned,
- * drl_linear_decode_workspace_bytes(M, N, K, epilogue) bytes (0 when K is not split over workgroups),
- * zero-filled before the first call and left zeroed by every call (one in-flight call per workspace). */
-size_t drl_linear_decode_workspace_bytes(int64_t M, int64_t N, int64_t K, int32_t epilogue);
-/* Tuning hook (tools/kernel_bench.py): force waves per workgroup (4/8/16) and the K split; 0 = automatic. */
-void drl_linear_decode_set_plan(int32_t waves, int32_t ksplit);
-int drl_linear_decode(const void* x, int64_t ld_x, const void* w, const void* bias, int32_t dt, int64_t M,
-                      int64_t N, int64_t K, int32_t epilogue, void* out, int64_t ld_out, void* workspace,
-                      size_t workspace_bytes, void* stream);
 
 /* A21 fused lm_head + log-prob + entropy (MFMA; logits never written). Replaces FusedLinearForPPO.forward
  * (verl/utils/experimental/torch_functional.py:20-37, :153-216) and the Triton linear_cross_entropy forward
@@ -568,25 +548,6 @@ int drl_decode_rope(const float* partials, int32_t nsplit, const void* bias, con
                     int64_t koff, const int64_t* koff_dev, void* stream);
 
 
-/* ------------------------------------------------------------------------------------------------
- * Full-sequence projection GEMMs (csrc/gemm.hip): y = x W^T with x (M, K) and W (N, K) row-major bf16, fp32
- * accumulation, bf16 out — the nn.Linear calls of HF Qwen2 / Llama under autocast in the reference's FSDP actor
- * (dp_actor.py:110 -> modeling_qwen2 / modeling_llama: q/k/v, o, gate/up, down, lm_head).
- * PLAIN: c (M, N) = bf16(x W^T). BIAS: c = bf16(x W^T + bias) (addmm: one rounding). SWIGLU: W = [gate | up]
- * (N = 2I rows), c (M, I) = bf16(bf16(silu(g)) * u) with g, u the bf16-rounded gate / up sums (swiglu_fwd's
- * semantics); c2 (M, 2I) = [g | u] when not NULL (the backward's saved activation). K % 64 == 0; A / B rows
- * 16-byte aligned. */
-enum { DRL_GEMM_PLAIN = 0, DRL_GEMM_BIAS = 1, DRL_GEMM_SWIGLU = 2, DRL_GEMM_SWIGLU_BWD = 3 };
-int drl_gemm_bf16_nt(const void* a, int64_t lda, const void* b, int64_t ldb, void* c, int64_t ldc, int64_t M,
-                     int64_t N, int64_t K, const void* bias, int32_t epilogue, void* c2, int64_t ldc2, void* stream);
-/* Tuning hook: 0 = automatic (the 256 x 256 ping-pong form when K % 128 == 0 and the 256 x 256 grid has >= 64
- * tiles, else 256 x 128 / 128 x 128), 1 = 256 x 128, 2 = 128 x 128, 3-8 = the other one-barrier tiles,
- * 9 = ping-pong (falls back to 256 x 256 x 64 when K % 128 != 0). Every choice gives the same result within one
- * bf16 rounding (different fp32 summation orders). */
-void drl_gemm_set_tile(int32_t tile);
-/* Tuning hook: M-tiles per rasterization group of the ping-pong form (consecutive tiles walk a group column by
- * column), 0 = automatic. Changes the schedule only, never the result. */
-void drl_gemm_set_group(int32_t group_m);
 
 /* ------------------------------------------------------------------------------------------------
  * Every transformer GEMM of the actor's passes (csrc/gemm_sk.hip): the forward projections, their dgrad and their
@@ -595,14 +556,17 @@ void drl_gemm_set_group(int32_t group_m);
  * dW += dy^T x (grad_weight, accumulated over micro-batches in fp32 as FSDP's fp32 gradient).
  *   C(m, n) (+)= sum_k A(m, k) B(n, k),  A(m, k) = a[m*lda + k] (DRL_LAYOUT_K) or a[k*lda + m] (DRL_LAYOUT_T),
  *                                        B(n, k) = b[n*ldb + k] (DRL_LAYOUT_K) or b[k*ldb + n] (DRL_LAYOUT_T).
- * bf16 operands, fp32 accumulation (a layout-K A operand over 2 GB runs as row blocks). c_dtype DRL_BF16: epilogues as drl_gemm_bf16_nt (bias / SwiGLU need both
- * operands layout K); DRL_F32 (plain epilogue): c = acc, or c += acc when beta != 0. K % 64 == 0 unless both
+ * bf16 operands, fp32 accumulation (a layout-K A operand over 2 GB runs as row blocks). c_dtype DRL_BF16 epilogues
+ * (bias / SwiGLU need both operands layout K): PLAIN c (M, N) = bf16(acc); BIAS c = bf16(acc + bias) (addmm: one
+ * rounding); SWIGLU: B = [gate | up] (N = 2I rows), c (M, I) = bf16(bf16(silu(g)) * u) with g, u the bf16-rounded
+ * gate / up sums, c2 (M, 2I) = [g | u] when not NULL (the backward's saved activation); DRL_F32 (plain epilogue): c = acc, or c += acc when beta != 0. K % 64 == 0 unless both
  * operands are layout T (then any K: the k tail reads as zeros). A / B 16-byte aligned, ld % 8 == 0, each operand
  * < 2 GB. DRL_GEMM_SWIGLU_BWD (drl_gemm only): the down_proj dgrad fused with the SwiGLU backward (swiglu_bwd's
  * math on d a = bf16(acc)): A = dy layout K, B = W_down layout T, c2 = gu (M, 2N) read, c = dgu (M, 2N) written.
  * Work is split stream-K over at most one workgroup per CU; split tiles are summed in a fixed order
  * (bit-reproducible). workspace: drl_gemm_workspace_bytes() bytes, 16-byte aligned, zeroed once at allocation
  * (every call leaves its flag words zero again); calls sharing a workspace must be ordered on one stream. */
+enum { DRL_GEMM_PLAIN = 0, DRL_GEMM_BIAS = 1, DRL_GEMM_SWIGLU = 2, DRL_GEMM_SWIGLU_BWD = 3 };
 enum { DRL_LAYOUT_K = 0, DRL_LAYOUT_T = 1 };
 int drl_gemm(const void* a, int64_t lda, int32_t a_layout, const void* b, int64_t ldb, int32_t b_layout, void* c,
              int64_t ldc, int32_t c_dtype, int32_t beta, int64_t M, int64_t N, int64_t K, const void* bias,
@@ -624,11 +588,6 @@ void drl_gemm_set_debug(int32_t flags);
 int drl_copy_rows(const void* src, int64_t ld_src_bytes, const int64_t* src_idx, void* dst, int64_t ld_dst_bytes,
                   const int64_t* dst_idx, int64_t n_rows, int64_t row_bytes, void* stream);
 
-/* 16-bit transpose: dst (cols, rows) = src (rows, cols)^T (row strides in elements). The weights' transposed
- * copies for the backward dgrad (dx = dy W run as the TN product dy (W^T)^T: gate_up 129 -> 105 us, down 57 -> 47 us
- * at 6144 rows on hipBLASLt), refreshed after each optimizer step. */
-int drl_transpose16(const void* src, int64_t ld_src, int64_t rows, int64_t cols, void* dst, int64_t ld_dst,
-                    void* stream);
 
 
 /* out (C,) fp32 += column sums of x (N, C) bf16 (row stride ld): the qkv bias gradient, dqkv summed over tokens

@@ -334,37 +334,6 @@ def test_flash_attn_backward(B, Hkv, G, D, T):
     assert torch.equal(dq, dq2) and torch.equal(dk, dk2) and torch.equal(dv, dv2)
 
 
-@pytest.mark.parametrize("M,N,K,epi", [(1, 1152, 896, "bias"), (7, 896, 896, None), (64, 1152, 896, "bias"),
-                                       (64, 9728, 896, "swiglu"), (64, 896, 4864, None), (100, 1000, 272, None),
-                                       (128, 9728, 896, "swiglu"), (128, 896, 4864, None), (40, 96, 4864, "bias"),
-                                       (64, 2 * 80, 4864, "swiglu"), (33, 151936, 896, None), (128, 64, 16, None)])
-def test_linear_decode(M, N, K, epi):
-    """Decode-step linear (csrc/linear.hip) vs an fp32 reference of the bf16 module: y = bf16(x W^T + b);
-    SwiGLU: bf16(bf16(silu(bf16(g))) * bf16(u)). Tolerance: 1 bf16 ulp of the output (fp32 summation order)
-    for the plain forms, 3 ulp after SwiGLU's three roundings."""
-    g = torch.Generator(device="cuda").manual_seed(M * 7 + N)
-    bf = torch.bfloat16
-    x = torch.randn(M, K, device="cuda", generator=g).to(bf)
-    w = (torch.randn(N, K, device="cuda", generator=g) / math.sqrt(K)).to(bf)
-    bias = torch.randn(N, device="cuda", generator=g).to(bf) if epi == "bias" else None
-    y = native.linear_decode(x, w, bias=bias, swiglu=epi == "swiglu")
-    ref = x.float() @ w.float().t()
-    if bias is not None:
-        ref = ref + bias.float()
-    if epi == "swiglu":
-        gt, up = ref[:, : N // 2].to(bf).float(), ref[:, N // 2:].to(bf).float()
-        ref = F.silu(gt).to(bf).float() * up
-        ulp = 3
-    else:
-        ulp = 1
-    err = (y.float() - ref).abs()
-    bound = ulp * 2.0 ** -7 * ref.abs() + 1e-4
-    assert (err <= bound).all(), f"max err {err.max().item()} at {torch.nonzero(err > bound)[:4].tolist()}"
-    for _ in range(3):  # deterministic; the K-split arrival tickets reset themselves between calls
-        y2 = native.linear_decode(x, w, bias=bias, swiglu=epi == "swiglu")
-        assert torch.equal(y, y2)
-
-
 @pytest.mark.parametrize("waves,splits", [(4, 2), (8, 4), (2, 8), (16, 1)])
 def test_decode_attention_vt_split_plans(waves, splits):
     """Every forced (waves, key-split) plan of the MFMA decode kernel gives the same result as the default
@@ -398,10 +367,3 @@ def test_colsum_bf16_acc(N, C):
     got = native.colsum_bf16_acc(x, out.clone())
     assert (got.double() - want).abs().max().item() <= 1e-5 * (x.double().abs().sum(0).max().item() + 1)
     assert torch.equal(got, native.colsum_bf16_acc(x, out.clone()))
-
-
-def test_transpose16():
-    g = torch.Generator(device=DEV).manual_seed(3)
-    for rows, cols in ((896, 1152), (4864, 896), (100, 37 * 8), (65, 130)):
-        x = torch.randn(rows, cols, device=DEV, generator=g).to(torch.bfloat16)
-        assert torch.equal(native.transpose16(x), x.t().contiguous())

@@ -319,55 +319,6 @@ def flash_bwd(B=8, Hkv=2, G=7, D=64, T=768):
                  frac_mfma=2.5 * flops / t / 2.5e15, fwd_seconds=tf)]
 
 
-def linear(Ms=(64, 128, 256, 512), plans=True):  # ours takes M <= 128
-    """Decode-step linear layers (csrc/linear.hip) vs hipBLASLt (replaying the shipped TunableOp choices) at the
-    Qwen2.5-0.5B projection shapes. Weights rotate over copies totalling > 600 MB so every call streams its
-    weight from HBM, as in a decode step (1 GB of weights between two uses of one layer)."""
-    from dots.rl_amd.workers import _enable_gemm_tuning
-    _enable_gemm_tuning("auto")
-    dev, bf = "cuda", torch.bfloat16
-    shapes = [("qkv_proj", 1152, 896, "bias"), ("o_proj", 896, 896, None), ("gate_up_swiglu", 9728, 896, "swiglu"),
-              ("down_proj", 896, 4864, None), ("lm_head", 151936, 896, None)]
-    res = []
-    for name, N, K, epi in shapes:
-        ncopy = max(2, int(600e6 // (N * K * 2)) + 1)
-        ws = [torch.randn(N, K, device=dev, dtype=bf) * 0.05 for _ in range(ncopy)]
-        bias = torch.randn(N, device=dev, dtype=bf) if epi == "bias" else None
-        for M in Ms:
-            x = torch.randn(M, K, device=dev, dtype=bf)
-            it = iter(range(1 << 30))
-
-            def ours():
-                w = ws[next(it) % ncopy]
-                return native.linear_decode(x, w, bias=bias, swiglu=epi == "swiglu")
-
-            def lib():
-                w = ws[next(it) % ncopy]
-                if epi == "bias":
-                    return torch.addmm(bias, x, w.t())
-                y = x @ w.t()
-                if epi == "swiglu":
-                    a = torch.empty(M, N // 2, device=dev, dtype=bf)
-                    native.swiglu_fwd(y, a)
-                    return a
-                return y
-            t = time_graph(ours, ncopy) if M <= 128 else float("nan")
-            sweep = {}
-            if M <= 128 and plans:
-                for kw in (4, 8, 16):
-                    for ks in (1, 2, 4, 8, 16):
-                        native.lib().drl_linear_decode_set_plan(kw, ks)
-                        sweep[f"{kw}x{ks}"] = round(time_graph(ours, ncopy) * 1e6, 2)
-                native.lib().drl_linear_decode_set_plan(0, 0)
-            t2 = time_graph(lib, ncopy)
-            nbytes = 2 * N * K + 2 * M * K + 2 * M * (N // 2 if epi == "swiglu" else N)
-            best = min(sweep, key=sweep.get) if sweep else None
-            res.append(dict(kernel="linear_decode", layer=name, M=M, N=N, K=K, seconds=t, GBps=nbytes / t / 1e9,
-                            frac=nbytes / t / PEAK_HBM, hipblaslt_seconds=t2, best_plan=best,
-                            best_us=sweep.get(best), sweep_us=sweep))
-    return res
-
-
 def fused_linear(Ns=(2048, 4096), H=896, V=151936):
     """A21 fused lm_head + logp + entropy vs the unfused path (bf16 logits GEMM + K2), forward and backward.
     MFMA-bound: 2*N*H*V FLOP per forward (and per d_logits recompute)."""
@@ -488,46 +439,6 @@ def train_gemms(Ms=(6144, 12288)):
     return res
 
 
-def our_gemms(Ms=(6144, 12288)):
-    """csrc/gemm.hip (drl_gemm_bf16_nt, both tiles) vs hipBLASLt on the forward projections of the log-prob /
-    update micro-batches; gate_up with the SwiGLU epilogue vs hipBLASLt + swiglu_fwd."""
-    from dots.rl_amd.workers import _enable_gemm_tuning
-    _enable_gemm_tuning("auto")
-    dev, bf = "cuda", torch.bfloat16
-    res = []
-    for name, N, K in (("qkv", 1152, 896), ("o_proj", 896, 896), ("gate_up", 9728, 896), ("down", 896, 4864),
-                       ("lm_head", 151936, 896), ("qkv_dgrad", 896, 1152), ("gate_up_dgrad", 896, 9728),
-                       ("down_dgrad", 4864, 896)):
-        w = torch.randn(N, K, device=dev, dtype=bf) * 0.05
-        b = torch.randn(N, device=dev, dtype=bf) if name == "qkv" else None
-        for M in (Ms if name != "lm_head" else (2048, 4096)):
-            x = torch.randn(M, K, device=dev, dtype=bf)
-            fl = 2.0 * M * N * K
-            sw = name == "gate_up"
-            if sw:
-                a = torch.empty(M, N // 2, device=dev, dtype=bf)
-                tl = time_it(lambda: native.swiglu_fwd(x @ w.t(), a))
-            elif b is not None:
-                tl = time_it(lambda: torch.addmm(b, x, w.t()))
-            else:
-                tl = time_it(lambda: x @ w.t())
-            row = dict(kernel="gemm_nt", layer=name, M=M, N=N, K=K, hipblaslt_us=tl * 1e6, hipblaslt_TF=fl / tl / 1e12)
-            for tile in (0, 9):
-                native.lib().drl_gemm_set_tile(tile)
-                t = time_it(lambda: native.gemm_nt(x, w, bias=b, swiglu=sw))
-                row[f"tile{tile}_us"] = t * 1e6
-                row[f"tile{tile}_TF"] = fl / t / 1e12
-            native.lib().drl_gemm_set_tile(9)
-            for gm in (2, 8, 16):  # rasterization group of the ping-pong form (automatic: 4)
-                native.lib().drl_gemm_set_group(gm)
-                row[f"pp_g{gm}_us"] = time_it(lambda: native.gemm_nt(x, w, bias=b, swiglu=sw)) * 1e6
-            native.lib().drl_gemm_set_group(0)
-            native.lib().drl_gemm_set_tile(0)
-            res.append(row)
-            del x
-    return res
-
-
 def swiglu(Ns=(6144, 12288), I=4864):
     """SwiGLU forward / backward at the training (8 x 768) and log-prob (16 x 768) micro-batch rows, HBM GB/s."""
     dev, bf = "cuda", torch.bfloat16
@@ -609,16 +520,8 @@ if __name__ == "__main__":
         for r in decode_sweep():
             print(json.dumps(r), flush=True)
         sys.exit(0)
-    if args.only == "linear":
-        for r in launch_floor() + linear():
-            print(json.dumps(r), flush=True)
-        sys.exit(0)
     if args.only == "train_gemms":
         for r in train_gemms():
-            print(json.dumps(r), flush=True)
-        sys.exit(0)
-    if args.only == "gemm":
-        for r in our_gemms():
             print(json.dumps(r), flush=True)
         sys.exit(0)
     if args.only == "decode_gemm":
