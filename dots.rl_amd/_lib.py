@@ -92,7 +92,7 @@ F32 = ctypes.c_float
 SZ = ctypes.c_size_t
 
 # name -> (restype, argtypes); must match include/dotsrl_amd.h exactly
-ABI_VERSION = 3  # include/dotsrl_amd.h DRL_ABI_VERSION: the layouts below (PPOLossParams) are of this version
+ABI_VERSION = 4  # include/dotsrl_amd.h DRL_ABI_VERSION: the layouts below (PPOLossParams) are of this version
 
 SIGNATURES = {
     "drl_last_error": (ctypes.c_char_p, []),

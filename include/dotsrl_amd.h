@@ -24,7 +24,7 @@ extern "C" {
 
 /* 3: drl_ppo_loss_params gained policy_loss, cov_ratio, clip_cov_lb, clip_cov_ub, ppo_kl_coef, cov_seed (a caller
  * built against version 2 passes a shorter struct); drl_gemm (operand layouts, fp32 epilogues, stream-K) */
-#define DRL_ABI_VERSION 3
+#define DRL_ABI_VERSION 4
 
 /* ld_vt value selecting the key-blocked V^T cache layout (B, Hkv, ceil(cap / 32), D, 32) wherever a V^T
  * operand with a leading dimension ld_vt is taken (flash / decode attention, the rope and decode-projection
