@@ -160,6 +160,7 @@ SIGNATURES = {
     "drl_decode_gemm_plan": (ctypes.c_int, [I64, I64, I64, I32, P, P]),
     "drl_decode_gemm_set_plan": (None, [I32, I32]),
     "drl_decode_gemm_set_tiled": (None, [I32]),
+    "drl_decode_gemm_set_max_splits": (None, [I32]),
     "drl_gemm": (ctypes.c_int, [P, I64, I32, P, I64, I32, P, I64, I32, I32, I64, I64, I64, P, I32, P, I64, P, I64, P]),
     "drl_gemm_workspace_bytes": (ctypes.c_int64, []),
     "drl_gemm_set_sk_tuning": (None, [I32, I32, I32, I32]),

@@ -400,8 +400,11 @@ __global__ __launch_bounds__(64 * WR * WT) void decode_gemm_lds_kernel(DgArgs a)
     if constexpr (PER_WAVE == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
     else if constexpr (PER_WAVE == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
     else if constexpr (PER_WAVE == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if constexpr (PER_WAVE == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
     else if constexpr (PER_WAVE == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    else static_assert(PER_WAVE == 2 || PER_WAVE == 3 || PER_WAVE == 4 || PER_WAVE == 6, "vmcnt table");
+    else if constexpr (PER_WAVE == 9) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+    else static_assert(PER_WAVE == 2 || PER_WAVE == 3 || PER_WAVE == 4 || PER_WAVE == 5 || PER_WAVE == 6 ||
+                       PER_WAVE == 9, "vmcnt table");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     issue(i + 2);  // into the buffer read in iteration i - 1 (every wave is past it)
@@ -667,14 +670,17 @@ bool plan_decode_gemm(int64_t M, int64_t N, int64_t K, int epi, DgPlan& p) {
 
 // tiled path: (WB, TB, WW, WT, lds) configurations instantiated (lds: the LDS-staged kernel, WW x WT waves)
 struct DtShape { int wb, tb, ww, wt, lds; };
+// 9-13: larger token panels per workgroup (the activation panel staged once for more weight rows' MFMAs), round 4
 constexpr DtShape kTiled[] = {{2, 2, 4, 2, 1}, {2, 2, 2, 2, 1}, {1, 2, 2, 2, 1}, {2, 1, 2, 2, 1},
-                              {2, 2, 2, 2, 0}, {2, 2, 4, 1, 0}, {1, 2, 2, 2, 0}, {1, 2, 4, 1, 0}, {1, 1, 2, 2, 0}};
+                              {2, 2, 2, 2, 0}, {2, 2, 4, 1, 0}, {1, 2, 2, 2, 0}, {1, 2, 4, 1, 0}, {1, 1, 2, 2, 0},
+                              {2, 2, 1, 4, 1}, {2, 4, 2, 2, 1}, {1, 4, 2, 2, 1}, {2, 4, 1, 4, 1}, {2, 4, 2, 2, 0}};
 constexpr int kNumTiled = static_cast<int>(sizeof(kTiled) / sizeof(kTiled[0]));
 int g_dt_force = -1;  // tuning: force configuration index (drl_decode_gemm_force_tiled), -1 = planner
 int g_dt_min_rows = 192;  // tuning: smallest M for the tiled path
 // 0 = never the tiled path (drl_decode_gemm_set_tiled), 1 = automatic, 2 = automatic with one K slice (tests:
 // the partial form in the fused qkv + RoPE launch's summation order)
 int g_dt_mode = 1;
+int g_dt_max_ks = 4;  // tuning: most K slices of a partial-sum plan (drl_decode_gemm_set_max_splits)
 
 // the tiled plan when the shape is in its range. Configuration by shape class, from the sweep of every
 // configuration at 128 / 256 / 512 rows (tools/kernel_bench.py --only decode_gemm, profiles/r02_decode_gemm.jsonl):
@@ -708,7 +714,7 @@ bool plan_decode_tiled(int64_t M, int64_t N, int64_t K, int epi, DgPlan& p) {
   const int64_t base = static_cast<int64_t>((p.tiles + rows - 1) / rows) * ((p.mbt + toks - 1) / toks);
   bool found = false;
   int64_t best_wgs = 0;
-  for (int ks = 1; ks <= (epi == EPI_PARTIAL && g_dt_mode == 1 ? 4 : 1); ++ks) {
+  for (int ks = 1; ks <= (epi == EPI_PARTIAL && g_dt_mode == 1 ? g_dt_max_ks : 1); ++ks) {
     // register ring: dt_depth k-steps per refill round; LDS stages: 2 k-steps
     if (nks % ks != 0 || (nks / ks) % (c.lds ? 4 : dt_depth(c.wb, c.tb, epi)) != 0) continue;
     const int64_t wgs = base * ks;
@@ -738,7 +744,13 @@ void launch_dt(const DgArgs& a, const DgPlan& p, hipStream_t s) {
     case 5: hipLaunchKernelGGL((decode_gemm_tiled_kernel<2, 2, 4, 1, EPI>), grid, dim3(256), 0, s, a); break;
     case 6: hipLaunchKernelGGL((decode_gemm_tiled_kernel<1, 2, 2, 2, EPI>), grid, dim3(256), 0, s, a); break;
     case 7: hipLaunchKernelGGL((decode_gemm_tiled_kernel<1, 2, 4, 1, EPI>), grid, dim3(256), 0, s, a); break;
-    default: hipLaunchKernelGGL((decode_gemm_tiled_kernel<1, 1, 2, 2, EPI>), grid, dim3(256), 0, s, a); break;
+    case 8: hipLaunchKernelGGL((decode_gemm_tiled_kernel<1, 1, 2, 2, EPI>), grid, dim3(256), 0, s, a); break;
+    // LDS-staged: (WR, WT, WB, TB) = waves along weight rows / tokens, blocks per wave
+    case 9: hipLaunchKernelGGL((decode_gemm_lds_kernel<1, 4, 2, 2, EPI>), grid, dim3(256), 0, s, a); break;
+    case 10: hipLaunchKernelGGL((decode_gemm_lds_kernel<2, 2, 2, 4, EPI>), grid, dim3(256), 0, s, a); break;
+    case 11: hipLaunchKernelGGL((decode_gemm_lds_kernel<2, 2, 1, 4, EPI>), grid, dim3(256), 0, s, a); break;
+    case 12: hipLaunchKernelGGL((decode_gemm_lds_kernel<1, 4, 2, 4, EPI>), grid, dim3(256), 0, s, a); break;
+    default: hipLaunchKernelGGL((decode_gemm_tiled_kernel<2, 4, 2, 2, EPI>), grid, dim3(256), 0, s, a); break;
   }
 }
 
@@ -772,6 +784,8 @@ void drl_decode_gemm_force_tiled(int32_t config, int32_t min_rows) {
 }
 
 void drl_decode_gemm_set_tiled(int32_t mode) { drl::g_dt_mode = (mode >= 0 && mode <= 2) ? mode : 1; }
+
+void drl_decode_gemm_set_max_splits(int32_t ks) { drl::g_dt_max_ks = (ks >= 1 && ks <= 16) ? ks : 4; }
 
 void drl_decode_gemm_set_plan(int32_t mb, int32_t ksw) {
   drl::g_dg_mb = (mb == 1 || mb == 2) ? mb : 0;

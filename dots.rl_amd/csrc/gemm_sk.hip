@@ -254,11 +254,17 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
     if (wr == 1) bar();  // the upper group runs one barrier behind
     for (int kt = k0; kt < k1; kt += 2) {
       const bool last = kt + 2 >= k1;
+      // K % 128 == 64 (the K = 896 projections): the last pair's second k-tile holds no data. Its copies still go out
+      // (as zeros: the vmcnt schedule stays static) and its barriers still run, but its fragment reads and MFMAs are
+      // skipped — they multiplied zeros, 1/8 of the main loop at K = 896 (uniform across the workgroup)
+      const bool empty2 = last && kt + 1 >= g.nkt;
 #pragma unroll
       for (int p = 0; p < 8; ++p) {
         const int lp = p & 3, qm = lp >> 1, qn = (lp == 1 || lp == 2) ? 1 : 0;
         const int buf = p >> 2;
-        if (lp == 0) {
+        const bool skip = buf == 1 && empty2;
+        if (skip) {
+        } else if (lp == 0) {
           read_b(buf, 2, 0);
           __builtin_amdgcn_sched_barrier(0);
           read_a(buf, 0);
@@ -282,21 +288,23 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
         bar();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);  // nothing that uses an asm read's result moves above its wait
-        __builtin_amdgcn_s_setprio(1);
+        if (!skip) {
+          __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+          for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int j = 0; j < 2; ++j)
+            for (int j = 0; j < 2; ++j)
 #pragma unroll
-            for (int kb = 0; kb < 2; ++kb) {
-              const u16x8 fa = AT ? join(at[i][kb][0], at[i][kb][1]) : af[i][kb];
-              const u16x8 fb = BT ? join(bt[qn][j][kb][0], bt[qn][j][kb][1]) : bq[qn][j][kb];
-              // operands swapped: the 16 x 16 block is accumulated transposed, so lane (fq, fr) holds output row
-              // fr, columns 4 fq .. 4 fq + 3 — the epilogue stores straight from registers
-              acc[qm][qn][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(fb), as_bf16x8(fa),
-                                                                          acc[qm][qn][i][j], 0, 0, 0);
-            }
-        __builtin_amdgcn_s_setprio(0);
+              for (int kb = 0; kb < 2; ++kb) {
+                const u16x8 fa = AT ? join(at[i][kb][0], at[i][kb][1]) : af[i][kb];
+                const u16x8 fb = BT ? join(bt[qn][j][kb][0], bt[qn][j][kb][1]) : bq[qn][j][kb];
+                // operands swapped: the 16 x 16 block is accumulated transposed, so lane (fq, fr) holds output row
+                // fr, columns 4 fq .. 4 fq + 3 — the epilogue stores straight from registers
+                acc[qm][qn][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(fb), as_bf16x8(fa),
+                                                                            acc[qm][qn][i][j], 0, 0, 0);
+              }
+          __builtin_amdgcn_s_setprio(0);
+        }
         bar();
       }
     }

@@ -513,6 +513,8 @@ void drl_decode_gemm_set_plan(int32_t mb, int32_t ksw);
 /* 192..512 rows run the MFMA-tiled form (2-D wave tiles over weight rows x tokens) for the partial and qkv + RoPE
  * projections: mode 1 (default); 0 = never (A/B tuning); 2 = tiled with one K slice (tests). */
 void drl_decode_gemm_set_tiled(int32_t mode);
+/* Tuning hook: most K slices (partial sums) of a tiled decode GEMM plan, 1..16 (default 4). Schedule only. */
+void drl_decode_gemm_set_max_splits(int32_t ks);
 /* Tuning hook: force tiled configuration `config` (-1 = planner) and the smallest M of the tiled path (0 = 192). */
 void drl_decode_gemm_force_tiled(int32_t config, int32_t min_rows);
 /* Elements of the packed copy of W (N, K) bf16 (swiglu: W = [gate | up], blocks interleave 16 + 16 rows). */

@@ -33,7 +33,7 @@ def _default_tuning():
 
 @pytest.mark.parametrize("al,bl", [(K_, K_), (K_, T_), (T_, K_), (T_, T_)])
 @pytest.mark.parametrize("M,N,K", [(300, 520, 256), (1024, 896, 1152), (96, 200, 4864), (2304, 2304, 384),
-                                   (130, 700, 192)])
+                                   (130, 700, 192), (777, 896, 896), (520, 1152, 64)])
 def test_layouts_bf16_and_f32(al, bl, M, N, K):
     g = torch.Generator(device="cuda").manual_seed(M * 7 + N + K + 3 * al + bl)
     a, fa = _op((M, K), al, g)
@@ -97,22 +97,24 @@ def test_forward_epilogues(M):
 @pytest.mark.parametrize("mode", [(0, 0, 0), (1, 0, 0), (2, 0, 0), (3, 0, 0), (3, 0, 5), (3, 0, 32), (1, 37, 0),
                                   (1, 7, 0)])
 @pytest.mark.parametrize("out_dtype", [torch.float32, torch.bfloat16])
-def test_decompositions_agree(mode, out_dtype):
+@pytest.mark.parametrize("K", [4864, 4800])
+def test_decompositions_agree(mode, out_dtype, K):
     """Automatic, stream-K, whole tiles, uniform split-K (automatic / 5 / 32 splits), odd grids: the same GEMM
-    within fp32 summation-order differences."""
+    within fp32 summation-order differences. K = 4800: an odd k-tile count (the last pair's empty second tile is
+    skipped by whichever segment holds it)."""
     dp_mode, grid, param = mode
     g = torch.Generator(device="cuda").manual_seed(11)
-    a = torch.randn(1000, 4864, generator=g, device="cuda").to(torch.bfloat16)
-    b = torch.randn(896, 4864, generator=g, device="cuda").to(torch.bfloat16)
+    a = torch.randn(1000, K, generator=g, device="cuda").to(torch.bfloat16)
+    b = torch.randn(896, K, generator=g, device="cuda").to(torch.bfloat16)
     bias = torch.randn(896, generator=g, device="cuda").to(torch.bfloat16) if out_dtype == torch.bfloat16 else None
     ref = a.double() @ b.double().t() + (bias.double() if bias is not None else 0)
     native.lib().drl_gemm_set_sk_tuning(grid, 0, dp_mode, param)
     out = torch.empty(1000, 896, device="cuda", dtype=out_dtype)
-    native.gemm(a, K_, b, K_, 1000, 896, 4864, out, bias=bias)
+    native.gemm(a, K_, b, K_, 1000, 896, K, out, bias=bias)
     if out_dtype == torch.float32:
-        torch.testing.assert_close(out.double(), ref, rtol=1e-6, atol=4e-6 * 4864 ** 0.5)
+        torch.testing.assert_close(out.double(), ref, rtol=1e-6, atol=4e-6 * K ** 0.5)
     else:
-        torch.testing.assert_close(out.double(), ref.to(torch.bfloat16).double(), rtol=8e-3, atol=4e-6 * 4864 ** 0.5)
+        torch.testing.assert_close(out.double(), ref.to(torch.bfloat16).double(), rtol=8e-3, atol=4e-6 * K ** 0.5)
 
 
 @pytest.mark.parametrize("al,bl,M,N,K", [(K_, K_, 6144, 896, 4864), (K_, T_, 2048, 896, 37888),

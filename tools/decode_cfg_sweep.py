@@ -18,7 +18,7 @@ from dots.rl_amd import native  # noqa: E402
 from dots.rl_amd.config import QWEN25_05B  # noqa: E402
 from dots.rl_amd.qwen2 import KVCache, PackedDecode, ParamStore, Qwen2Config, Qwen2Model  # noqa: E402
 
-NCFG = 9  # kTiled entries
+NCFG = 14  # kTiled entries
 
 
 def graph_time(fn, reps=5):
@@ -89,6 +89,17 @@ def main():
                 except RuntimeError as e:  # a configuration that does not take this shape
                     row["planner" if ci < 0 else f"cfg{ci}"] = str(e)[:40]
             lib.drl_decode_gemm_force_tiled(-1, 0)
+            if name in ("down", "o") and B >= 256:  # long / short K partials with more K slices
+                for ks in (8, 16):
+                    lib.drl_decode_gemm_set_max_splits(ks)
+                    for ci in range(NCFG):
+                        lib.drl_decode_gemm_force_tiled(ci, 1)
+                        try:
+                            row[f"cfg{ci}_ks{ks}"] = round(graph_time(lambda: [fn(i) for i in range(L)]) / L, 2)
+                        except RuntimeError as e:
+                            row[f"cfg{ci}_ks{ks}"] = str(e)[:40]
+                    lib.drl_decode_gemm_force_tiled(-1, 0)
+                lib.drl_decode_gemm_set_max_splits(4)
             # the one-round-trip kernel (4 waves per workgroup each on a K quarter, reduced in LDS) at these rows
             for mb in (1, 2):
                 lib.drl_decode_gemm_set_tiled(0)
