@@ -544,22 +544,32 @@ __global__ __launch_bounds__(512) void flash_dq_kernel(FlashBwdArgs a) {
   const uint16_t* ktbase = a.kt + bh * D * a.ld_t;
   const uint8_t* vrow = a.valid + b * a.ld_valid;
   const int nb = (min(T, t0 + 32) + 31) / 32;
-  u16x8 stage[TL::CPT];
-  dq_issue<D>(kbase, vbase, ktbase, a.ld_t, 0, T, tid, stage);
-  uint32_t vst = valid_issue(vrow, 0, T, tid);
-  dq_store<D>(lds_k[0], lds_v[0], lds_kt[0], tid, stage);
-  if (tid < 8) lds_vw[0][tid] = vst;
+  // key blocks staged global -> registers -> LDS two blocks ahead: block j's loads go out two iterations before
+  // its LDS store (register sets alternate by block parity), so each iteration's compute covers two iterations of
+  // load latency instead of one (the per-block compute is a few hundred cycles, an L2 / HBM round trip more)
+  u16x8 stage[2][TL::CPT];
+  uint32_t vst[2] = {0u, 0u};
+  auto issue_blk = [&](int j, int set) {
+    const int kk = j * 32;
+    if (kk + 32 <= T) {
+      dq_issue_full<D>(kbase, vbase, ktbase, a.ld_t, kk, tid, stage[set]);
+      if (tid < 8) vst[set] = *reinterpret_cast<const uint32_t*>(vrow + kk + 4 * tid);
+    } else {
+      dq_issue<D>(kbase, vbase, ktbase, a.ld_t, kk, T, tid, stage[set]);
+      vst[set] = valid_issue(vrow, kk, T, tid);
+    }
+  };
+  issue_blk(0, 0);
+  if (nb > 1) issue_blk(1, 1);
+  dq_store<D>(lds_k[0], lds_v[0], lds_kt[0], tid, stage[0]);
+  if (tid < 8) lds_vw[0][tid] = vst[0];
   __syncthreads();
   for (int ib = 0; ib < nb; ++ib) {
     const int cur = ib & 1, k0 = ib * 32;
-    if (ib + 1 < nb) {
-      if (k0 + 64 <= T) {
-        dq_issue_full<D>(kbase, vbase, ktbase, a.ld_t, k0 + 32, tid, stage);
-        if (tid < 8) vst = *reinterpret_cast<const uint32_t*>(vrow + k0 + 32 + 4 * tid);
-      } else {
-        dq_issue<D>(kbase, vbase, ktbase, a.ld_t, k0 + 32, T, tid, stage);
-        vst = valid_issue(vrow, k0 + 32, T, tid);
-      }
+    // block ib + 2 into the register set block ib left (stored to LDS in the previous iteration)
+    if (ib + 2 < nb) {
+      if (cur == 0) issue_blk(ib + 2, 0);
+      else issue_blk(ib + 2, 1);
     }
     if (computes) {
       f32x16 st = f32x16{}, dpt = f32x16{};
@@ -610,9 +620,14 @@ __global__ __launch_bounds__(512) void flash_dq_kernel(FlashBwdArgs a) {
         }
       }
     }
-    if (ib + 1 < nb) {
-      dq_store<D>(lds_k[cur ^ 1], lds_v[cur ^ 1], lds_kt[cur ^ 1], tid, stage);
-      if (tid < 8) lds_vw[cur ^ 1][tid] = vst;
+    if (ib + 1 < nb) {  // block ib + 1 (register set cur ^ 1) into the other LDS buffer
+      if (cur == 0) {
+        dq_store<D>(lds_k[1], lds_v[1], lds_kt[1], tid, stage[1]);
+        if (tid < 8) lds_vw[1][tid] = vst[1];
+      } else {
+        dq_store<D>(lds_k[0], lds_v[0], lds_kt[0], tid, stage[0]);
+        if (tid < 8) lds_vw[0][tid] = vst[0];
+      }
     }
     __syncthreads();
   }
@@ -671,6 +686,9 @@ __global__ __launch_bounds__(64 * NW) void flash_dkdv_kernel(FlashBwdArgs a) {
   static_assert(2 * MT * 16 * 64 * 4 <= NW * 2 * 32 * XROW * 2, "reduction buffer must fit the image space");
   __shared__ __attribute__((aligned(16))) uint16_t kv_lds[2][32 * KROW];  // this key tile's K and V rows
   __shared__ __attribute__((aligned(16))) uint16_t xw[NW][2][32 * XROW];   // [wave][Q / dO][position][d]
+  // per wave, two slots of [LSE of the tile's 32 queries | their delta], filled one query tile ahead by LDS-DMA
+  // (one 4-byte global_load_lds per tile): the softmax's row statistics no longer wait on a global load per tile
+  __shared__ __attribute__((aligned(16))) float lsd[NW][2][64];
   // [dk/dv][tile][register][lane]: conflict-free per register; aliases xw after the loop
   auto red = reinterpret_cast<float (*)[MT][16][64]>(&xw[0][0][0]);
   const int tid = threadIdx.x;
@@ -711,7 +729,16 @@ __global__ __launch_bounds__(64 * NW) void flash_dkdv_kernel(FlashBwdArgs a) {
   const float* dlr = a.delta + head * a.T;
   u16x8 qa[KS], da[KS];
   dkdv_rows<D>(qbase, a.dout, b, hkv, a.Hkv, a.G, g, T, k0 + li, h, qa, da);
+  // lanes 0-31: LSE of query tt + lane, lanes 32-63: its delta (clamped to T - 1; masked where read)
+  auto lsd_issue = [&](int tt, int slot) {
+    const int q = min(tt + li, T - 1);
+    __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)((h ? dlr : lser) + q),
+                                     (__attribute__((address_space(3))) void*)&lsd[wv][slot][0], 4, 0, 0);
+  };
+  lsd_issue(k0, 0);
   for (int t0 = k0; t0 < T; t0 += 32) {
+    const int slot = ((t0 - k0) >> 5) & 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this tile's LDS-DMA (and its Q / dO rows) landed
     // this tile's Q and dO rows into the wave's LDS image (row li, head dims 16s + 8h .. + 7); the transposed
     // operands of dV / dK are read back from it after the softmax (no head-dim-major copies in HBM)
 #pragma unroll
@@ -724,14 +751,13 @@ __global__ __launch_bounds__(64 * NW) void flash_dkdv_kernel(FlashBwdArgs a) {
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       const int qb = t0 + 8 * c + 4 * h;
-      if (rows_in) {
-        l4[c] = *reinterpret_cast<const float4*>(lser + qb);
-        d4[c] = *reinterpret_cast<const float4*>(dlr + qb);
-      } else {
-        l4[c] = make_float4(qb < T ? lser[qb] : -INFINITY, qb + 1 < T ? lser[qb + 1] : -INFINITY,
-                            qb + 2 < T ? lser[qb + 2] : -INFINITY, qb + 3 < T ? lser[qb + 3] : -INFINITY);
-        d4[c] = make_float4(qb < T ? dlr[qb] : 0.f, qb + 1 < T ? dlr[qb + 1] : 0.f, qb + 2 < T ? dlr[qb + 2] : 0.f,
-                            qb + 3 < T ? dlr[qb + 3] : 0.f);
+      l4[c] = *reinterpret_cast<const float4*>(&lsd[wv][slot][8 * c + 4 * h]);
+      d4[c] = *reinterpret_cast<const float4*>(&lsd[wv][slot][32 + 8 * c + 4 * h]);
+      if (!rows_in) {
+        l4[c] = make_float4(qb < T ? l4[c].x : -INFINITY, qb + 1 < T ? l4[c].y : -INFINITY,
+                            qb + 2 < T ? l4[c].z : -INFINITY, qb + 3 < T ? l4[c].w : -INFINITY);
+        d4[c] = make_float4(qb < T ? d4[c].x : 0.f, qb + 1 < T ? d4[c].y : 0.f, qb + 2 < T ? d4[c].z : 0.f,
+                            qb + 3 < T ? d4[c].w : 0.f);
       }
     }
     // S = Q K^T and dP = dO V^T: A = rows of query t0 + li; C row r -> query t0 + (r&3) + 8(r>>2) + 4h
@@ -745,6 +771,8 @@ __global__ __launch_bounds__(64 * NW) void flash_dkdv_kernel(FlashBwdArgs a) {
     }
     if (t0 + 64 <= T) dkdv_rows_full<D>(qbase, a.dout, b, hkv, a.Hkv, a.G, g, T, t0 + 32 + li, h, qa, da);
     else if (t0 + 32 < T) dkdv_rows<D>(qbase, a.dout, b, hkv, a.Hkv, a.G, g, T, t0 + 32 + li, h, qa, da);  // next tile
+    // the next tile's LSE / delta into the other slot (its last reader, the previous tile, consumed it above)
+    if (t0 + 32 < T) lsd_issue(t0 + 32, slot ^ 1);
     u16x8 pb[2], dsb[2];
     // block entirely at or below the diagonal, all keys valid, all queries in range: no mask, and every query
     // row has an allowed key (finite LSE)
