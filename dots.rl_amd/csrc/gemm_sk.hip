@@ -139,6 +139,10 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
   // tile's wc = 2, 3 waves multiplied zero columns. Plain / bias / fp32 epilogues (the SwiGLU forms pair columns).
   constexpr bool kNarrowOK = EPI == EPI_NONE || EPI == EPI_BIAS || EPI == EPI_F32;
   bool narrow = false;
+  // Short tiles: the last tile row when at most 128 of its 256 rows hold data (M = 896 / 1152: the o_proj, down_proj
+  // and qkv weight gradients): quadrant row 1 is all zero rows, so every wave skips its A reads and MFMAs (any
+  // epilogue: rows past M are never stored)
+  bool shortm = false;
   int arow = wr * 64, bcol = wc * 32;  // first A row of the wave's fragments in a half-tile, first B image row
   auto set_frags = [&](int n0) {
     narrow = kNarrowOK && n0 + 128 >= g.N;
@@ -165,6 +169,7 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
 
   auto setup_tile = [&](int m0, int n0) {
     set_frags(n0);
+    shortm = m0 + 128 >= g.M;
 #pragma unroll
     for (int h = 0; h < 4; ++h)
 #pragma unroll
@@ -282,8 +287,8 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
         const int lp = p & 3, qm = lp >> 1, qn = (lp == 1 || lp == 2) ? 1 : 0;
         const int buf = p >> 2;
         const bool skip = buf == 1 && empty2;
-        // narrow tile: the A half of the other quadrant row is never used by this wave
-        const bool a_off = narrow && wr != qm;
+        // narrow tile: the A half of the other quadrant row is never used by this wave; short tile: nor quadrant row 1
+        const bool a_off = (narrow && wr != qm) || (shortm && qm == 1);
         if (skip) {
         } else if (lp == 0) {
           read_b(buf, 2, 0);
