@@ -27,6 +27,8 @@ Reference call sites (file:line under /root/reference):
 * masked_mean known answers : tests/utils/test_torch_functional.py:55-66 (reference test, reproduced as data)
 * rollout-vs-actor debug metrics : verl/utils/debug/metrics.py:63-108
 * bf16 production-path update (fp32 and autocast-bf16 reference runs) : verl/workers/actor/dp_actor.py:110, 300-482
+* configs #4 / #5 at full depth (Llama-3-8B, Qwen2.5-7B; fp32 and CPU-bf16 teacher-forced log-probs) : HF models as
+  fsdp_workers.py:244-330 loads them
 """
 
 import hashlib
@@ -1370,7 +1372,8 @@ def gen_bf16_update():
     _ref_actor) and under its own torch.autocast(bf16) (dp_actor.py:110; on this CPU box the device name is 'cpu',
     so the CPU bf16 autocast runs). SDPA attention (fp32 score accumulation like the GPU's flash-attn). Recorded for
     both runs: log-probs / entropy, every update metric, per-tensor gradient norms and a fixed sample of gradient
-    elements (captured when the optimizer steps: the accumulated gradient of the 2 micro-batches, before clipping),
+    elements (captured when _optimizer_step calls clip_grad_norm_: the accumulated gradient of the 2 micro-batches,
+    before clipping),
     and the same sample of the parameter update. The bf16-vs-fp32 difference of the reference itself is the
     yardstick the production bf16 path is held to (tests/test_bf16_update_gpu.py)."""
     import bf16_update as bu
@@ -1401,14 +1404,14 @@ def gen_bf16_update():
         actor, opt = _ref_actor(model, acfg, lr)
         actor.device_name = "cuda" if mode == "fp32" else "cpu"  # "cpu": the reference's autocast(bf16) on CPU
         grads = {}
-        step0 = opt.step
+        clip0 = torch.nn.utils.clip_grad_norm_
 
-        def step(*a, _g=grads, _m=model, _s=step0, **k):
+        def clip(params, *a, _g=grads, _m=model, _c=clip0, **k):  # the gradient as accumulated, before clipping
             for n, prm in _m.named_parameters():
                 _g[n] = prm.grad.detach().clone()
-            return _s(*a, **k)
+            return _c(params, *a, **k)
 
-        opt.step = step
+        torch.nn.utils.clip_grad_norm_ = clip
         data = RefDataProto.from_dict(tensors={k: bt[k] for k in ("input_ids", "attention_mask", "position_ids",
                                                                    "responses")},
                                       meta_info={"micro_batch_size": bu.B // 2, "temperature": 1.0,
@@ -1425,6 +1428,7 @@ def gen_bf16_update():
                                                 "old_log_probs": old, "ref_log_prob": ref},
                                        meta_info={"temperature": 1.0})
         metrics = actor.update_policy(udata)
+        torch.nn.utils.clip_grad_norm_ = clip0
         assert len(grads) > 0
         run = {"metrics": {k: [float(x) for x in v] for k, v in metrics.items()},
                "grad_norms": {n: float(g.double().norm()) for n, g in grads.items()},
@@ -1443,6 +1447,71 @@ def gen_bf16_update():
     meta["ref"] = ("dp_actor.py:110 (autocast bf16), 300-482 (compute_log_prob, update_policy), 282-298 (clip + step); "
                    "fsdp_workers.py:454-459 (AdamW); HF Qwen2ForCausalLM, SDPA attention")
     _save("bf16_update.npz", arrays, meta)
+
+
+def gen_deep():
+    """Configs #4 / #5 at FULL depth (tests/golden/deep.py: Llama-3-8B 32 layers, Qwen2.5-7B 28 layers, counter-hash
+    weights): the reference HF models in fp32 (SDPA attention) and under the CPU bf16 autocast on 2 x (32 + 32)
+    tokens, teacher-forced: the response tokens' log-probs, entropy, logsumexp and the top-32 logits of every
+    response-predicting position (the bf16 run at the fp32 run's top-32 ids). Built on the meta device and filled
+    tensor by tensor, so one 30 GB model is in memory at a time."""
+    import deep
+    from transformers import LlamaConfig, LlamaForCausalLM, Qwen2Config, Qwen2ForCausalLM
+    from transformers.models.llama.modeling_llama import LlamaRotaryEmbedding
+    from transformers.models.qwen2.modeling_qwen2 import Qwen2RotaryEmbedding
+
+    arrays, meta = {}, {"ref": "HF LlamaForCausalLM / Qwen2ForCausalLM as fsdp_workers.py:244-330 loads them; "
+                               "logits -> log_softmax / entropy as dp_actor.py:263-272", "models": {}}
+    for which in ("llama", "qwen7b"):
+        cfgd = deep.MODELS[which]
+        if which == "llama":
+            cfg = LlamaConfig(**{k: v for k, v in cfgd.items() if k != "attention_bias"}, attention_bias=False,
+                              mlp_bias=False, attn_implementation="sdpa")
+            with torch.device("meta"):
+                model = LlamaForCausalLM(cfg)
+        else:
+            cfg = Qwen2Config(**cfgd, attn_implementation="sdpa")
+            with torch.device("meta"):
+                model = Qwen2ForCausalLM(cfg)
+        model = model.to_empty(device="cpu")
+        params = dict(model.named_parameters())
+        digest_sd = {}
+        for t, (name, shape) in enumerate(deep.hf_shapes(which)):
+            x = deep.tensor_np(which, t, name, shape)
+            with torch.no_grad():
+                params[name].copy_(x)
+            v = x.reshape(-1)
+            digest_sd[name] = v[torch.linspace(0, v.numel() - 1, 4096, dtype=torch.float64).long()].clone()
+            del x
+        assert set(params) == {n for n, _ in deep.hf_shapes(which)}, set(params) ^ {n for n, _ in deep.hf_shapes(which)}
+        model.model.rotary_emb = (LlamaRotaryEmbedding if which == "llama" else Qwen2RotaryEmbedding)(config=cfg)
+        model.eval()
+        ids, am, pos = deep.sequences(which)
+        P, R = deep.P, deep.R
+        resp = ids[:, P:]
+        with torch.no_grad():
+            lg = model(input_ids=ids, attention_mask=am, position_ids=pos, use_cache=False).logits[:, P - 1:P + R - 1]
+            lg = lg.float()
+            lsm = torch.log_softmax(lg, -1)
+            lp = lsm.gather(-1, resp.unsqueeze(-1)).squeeze(-1)
+            ent = -(lsm.exp() * lsm).sum(-1)
+            lse = torch.logsumexp(lg, -1)
+            top_l, top_i = lg.topk(32, -1)
+            with torch.autocast("cpu", dtype=torch.bfloat16):
+                lb = model(input_ids=ids, attention_mask=am, position_ids=pos, use_cache=False).logits[:, P - 1:P + R - 1]
+            lb = lb.float()
+            lsb = torch.log_softmax(lb, -1)
+        p = f"{which}_"
+        arrays.update({p + "input_ids": ids, p + "attention_mask": am, p + "position_ids": pos, p + "log_probs": lp,
+                       p + "entropy": ent, p + "lse": lse, p + "top32_ids": top_i, p + "top32_logits": top_l,
+                       p + "cpu_bf16_log_probs": lsb.gather(-1, resp.unsqueeze(-1)).squeeze(-1),
+                       p + "cpu_bf16_top32_logits": lb.gather(-1, top_i), p + "cpu_bf16_lse": torch.logsumexp(lb, -1),
+                       p + "cpu_bf16_entropy": -(lsb.exp() * lsb).sum(-1)})
+        meta["models"][which] = {"config": cfgd, "weight_digest": deep.sample_digest(digest_sd), "P": P, "R": R,
+                                 "cpu_bf16_logp_err_max": float((arrays[p + "cpu_bf16_log_probs"] - lp).abs().max())}
+        print(which, meta["models"][which]["cpu_bf16_logp_err_max"], flush=True)
+        del model, params, lg, lb, lsm, lsb
+    _save("deep.npz", arrays, meta)
 
 
 def gen_debug_metrics():
