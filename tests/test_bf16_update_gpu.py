@@ -17,9 +17,11 @@ quantity q, |q_ours - q_fp32| <= 2 |q_ref_bf16 - q_fp32| + floor, with
   * log-probs / entropy over the response mask: max and mean absolute difference (floor 1e-3 / 1e-4);
   * each update metric, per micro-batch (floor: one sigma of the metric's random walk under the reference's own
     per-token bf16 log-prob error; clip fractions one token of the micro-batch; grad norm 1e-3 relative);
-  * each parameter's gradient norm (relative, floor 1e-3) and a fixed sample of its gradient elements (relative L2,
-    floor 1e-3) — the gradient accumulated over both micro-batches, before clipping;
-  * the AdamW update of the same sample: the fraction of elements moving the other way than in fp32 (floor 1e-3).
+  * a fixed sample of each parameter's gradient elements (relative L2, floor 1e-3) and its gradient norm (relative;
+    floor 1e-3 + 3 e / sqrt(n), the norm's sampling noise under the reference's own elementwise error e over n
+    elements) — the gradient accumulated over both micro-batches, before clipping;
+  * the AdamW update of the same sample: the fraction of elements moving the other way than in fp32 (floor 1e-3 +
+    3 sigma of that fraction's binomial noise at the reference's rate over the sampled elements).
 """
 
 import os
@@ -176,16 +178,23 @@ def test_bf16_update_within_reference_bf16_error(fixture, form):
     for n, gn32 in runs["fp32"]["grad_norms"].items():
         gv = _hf_view(store, gflat, n).reshape(-1)
         gn16 = runs["bf16"]["grad_norms"][n]
-        _within(f"grad norm {n} (relative)", gv.double().norm().item() / gn32, gn16 / gn32, 1.0, 1e-3)
         idx = torch.from_numpy(embed_idx if n == "model.embed_tokens.weight" else bu.sample_index(n, gv.numel()))
         s32, s16 = z[f"fp32_grad.{n}"].astype(np.float64), z[f"bf16_grad.{n}"].astype(np.float64)
         sg = gv[idx.cuda()].double().cpu().numpy()
         nrm = np.linalg.norm(s32) + 1e-30
-        _within(f"grad sample {n} (relative L2)", np.linalg.norm(sg - s32) / nrm, np.linalg.norm(s16 - s32) / nrm,
-                0.0, 1e-3)
+        e16 = np.linalg.norm(s16 - s32) / nrm
+        _within(f"grad sample {n} (relative L2)", np.linalg.norm(sg - s32) / nrm, e16, 0.0, 1e-3)
+        # the norm is one scalar of the tensor: elementwise errors of relative size e move it by ~e / sqrt(n) at
+        # random (n elements), so a small tensor (a 128-element bias) gets that sampling noise as its floor (3 sigma)
+        _within(f"grad norm {n} (relative)", gv.double().norm().item() / gn32, gn16 / gn32, 1.0,
+                1e-3 + 3.0 * e16 / np.sqrt(gv.numel()))
+        # diagnostics: least-squares scale of each gradient sample against fp32 (1 = no systematic shrink / growth)
+        print(f"    scale {n}: ours {float(sg @ s32) / nrm ** 2:.5f}  reference bf16 {float(s16 @ s32) / nrm ** 2:.5f}")
         d = (_hf_view(store, store.master, n) - _hf_view(store, before, n)).reshape(-1)[idx.cuda()].double()
         d = d.cpu().numpy()
         d32, d16 = z[f"fp32_delta.{n}"], z[f"bf16_delta.{n}"]
         flip = lambda a: float(np.mean(np.sign(a) != np.sign(d32)))  # noqa: E731
-        _within(f"update direction {n} (flipped fraction)", flip(d), flip(d16), 0.0, 1e-3)
+        nn_ = d32.size  # binomial noise of a flip fraction over n sampled elements (3 sigma at the reference's rate)
+        _within(f"update direction {n} (flipped fraction)", flip(d), flip(d16), 0.0,
+                1e-3 + 3.0 * np.sqrt(max(flip(d16), 1.0 / nn_) / nn_))
     assert not _FAILS, "\n".join(_FAILS)

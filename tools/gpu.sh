@@ -7,6 +7,7 @@
 #   tests:<a>,<b>,...           the named pytest targets (files or node ids), -m gpu, verbose
 #   bench[:<steps>[:<warmup>]]  the default bench line (no CPU baseline) + the last step's drl_gemm launch log
 #   benchfull                   the driver's bench command (python bench.py, CPU baseline included)
+#   benchfused                  the bench with model.use_fused_kernels=True
 #   bench64                     the per-rank workload of N = 8 (64 sequences) ; bench128 / bench256 likewise
 #   profile                     rocprofv3 kernel stats of a 2-step bench + trace summary
 #   pmc_gemm                    FETCH_SIZE / WRITE_SIZE passes over drl_gemm -> profiles/pmc_drl_gemm.json
@@ -18,12 +19,16 @@ OUT=$ROOT/gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 
-run_tests() {  # $1 = log name, rest = pytest targets
+run_tests() {  # $1 = log name, rest = pytest targets. Failed assertions (pytest rc 1) are reported and the chain goes
+  # on; a crash, an interrupt or a time-limit kill (any other status) ends it.
   local log=$OUT/$1; shift
-  timeout -k 10 900 python -u -m pytest "$@" -m gpu -x -q --timeout 300 --timeout-method thread > "$log" 2>&1
+  timeout -k 10 900 python -u -m pytest "$@" -m gpu -q --timeout 300 --timeout-method thread > "$log" 2>&1
   local rc=$?
   tail -3 "$log"
-  [ $rc = 0 ] || { grep -E "FAIL|Error|assert" "$log" | head -30; return 1; }
+  [ $rc = 0 ] && return 0
+  grep -E "^FAILED|^ERROR|^BAD" "$log" | head -30
+  [ $rc = 1 ] && return 0
+  return 1
 }
 
 bench_rows() {  # $1 = sequences per step
@@ -49,6 +54,11 @@ for step in "$@"; do
       timeout -k 10 600 python -u bench.py > "$OUT/benchfull.json" 2> "$OUT/benchfull.err" \
         || { tail -20 "$OUT/benchfull.err"; exit 1; }
       cat "$OUT/benchfull.json" ;;
+    benchfused)  # model.use_fused_kernels=True (A21 forward + the vocabulary-blocked HIP backward)
+      timeout -k 10 500 python -u bench.py --steps 5 --warmup 2 --no-cpu-baseline \
+        --override actor_rollout_ref.model.use_fused_kernels=True > "$OUT/benchfused.json" 2> "$OUT/benchfused.err" \
+        || { tail -20 "$OUT/benchfused.err"; exit 1; }
+      cut -c1-900 "$OUT/benchfused.json" ;;
     bench64) bench_rows 64 || exit 1 ;;
     bench128) bench_rows 128 || exit 1 ;;
     bench256) bench_rows 256 || exit 1 ;;
