@@ -196,7 +196,8 @@ def load(path: str | None = None):
     with _lock:
         if _lib is not None:
             return _lib
-        p = path or LIB_PATH
+        # DRL_LIB_PATH: an alternative build of the same ABI (A/B kernel measurements, tools/gemm_sk_bench.py)
+        p = path or os.environ.get("DRL_LIB_PATH") or LIB_PATH
         if not os.path.exists(p):
             raise NativeLibraryError(
                 f"HIP library not found at {p}: build it with `python -c 'import __graft_entry__ as g; g.build()'` "

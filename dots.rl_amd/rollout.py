@@ -57,8 +57,10 @@ class MI355XRollout:
     def _capture(self, body):
         if self._graph_pool is None:
             self._graph_pool = torch.cuda.graph_pool_handle()
+        t0 = time.perf_counter()
         graph = capture_graph(body, self._graph_pool)
         self._graph = graph  # the previous graph goes only now, so the pool's use count never drops to zero
+        self.last_capture_s = time.perf_counter() - t0  # host time of the capture (the device is idle meanwhile)
         return graph
 
     def generate_sequences(self, prompts: DataProto) -> DataProto:

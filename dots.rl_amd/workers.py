@@ -173,7 +173,8 @@ class ActorRolloutRefWorker(Worker):
         output = self.rollout.generate_sequences(prompts)
         torch.cuda.synchronize()
         output.meta_info["timing"] = {"generate_sequences": time.perf_counter() - t0,
-                                      "generate_prefill": getattr(self.rollout, "last_prefill_s", 0.0)}
+                                      "generate_prefill": getattr(self.rollout, "last_prefill_s", 0.0),
+                                      "generate_capture": getattr(self.rollout, "last_capture_s", 0.0)}
         return self._out(output)
 
     @register(dispatch_mode=make_nd_compute_dataproto_dispatch_fn(mesh_name="actor"))

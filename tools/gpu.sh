@@ -11,6 +11,7 @@
 #   bench64                     the per-rank workload of N = 8 (64 sequences) ; bench128 / bench256 likewise
 #   profile                     rocprofv3 kernel stats of a 2-step bench + trace summary
 #   pmc_gemm                    FETCH_SIZE / WRITE_SIZE passes over drl_gemm -> profiles/pmc_drl_gemm.json
+#   ab:<lib>,<lib>,...          drl_gemm A/B over library builds (tools/gemm_ab.sh)
 #   py:<script>[:<args>]        python -u <script> <args> (args split on ':')
 set -o pipefail
 TAG=${1:?tag}; shift
@@ -78,6 +79,9 @@ for step in "$@"; do
       python3 tools/pmc_traffic.py drl_gemm "$OUT/pmc_FETCH_SIZE" "$OUT/pmc_WRITE_SIZE" || exit 1
       cp profiles/pmc_drl_gemm.json "$OUT/"
       find "$OUT" -name "*.csv" -size +20M -delete ;;
+    ab:*)  # A/B of GEMM builds: ab:<lib1>,<lib2>,...
+      IFS=',' read -ra L <<< "${step#ab:}"
+      bash tools/gemm_ab.sh "$OUT" "${L[@]}" || exit 1 ;;
     py:*)
       IFS=':' read -ra A <<< "${step#py:}"
       timeout -k 10 600 python -u "${A[@]}" > "$OUT/$(basename "${A[0]}" .py).out" 2>&1; rc=$?
