@@ -10,10 +10,12 @@ fp32 and under the CPU bf16 autocast.
 This repository's actor (DataParallelPPOActor.compute_log_prob, the production path) on the same weights:
   * fp32 (compute_dtype float32): log-probs and entropy within 5e-4 absolute at these depths (fp32 summation order
     over K up to 18944, 28-32 layers);
-  * bf16 (the production kernels: drl_gemm projections, the fused attention at head_dim 128, K2): per response
-    position, |log p - ref| and |entropy - ref| within twice the CPU bf16-autocast model's own error at that
-    position (floored at its median: a position where the CPU model happens to be near-exact says nothing about
-    another summation order), at most 2 % of the positions past that bound and none past 3x it.
+  * bf16 (the production kernels: drl_gemm projections, the fused attention at head_dim 128, K2): the distribution
+    of |log p - ref| and |entropy - ref| over the 64 response positions against the CPU bf16-autocast model's own
+    error distribution on the same positions — median within 1.5x, 90th percentile and maximum within 2x. (Per
+    position the two bf16 runs are independent realisations of 28-32 layers of rounding in different summation
+    orders: where the CPU model happens to be near-exact says nothing about ours, so the errors are compared as
+    distributions.)
 """
 
 import json
@@ -79,11 +81,11 @@ def test_full_depth_bf16_within_reference_bf16_error(ref, which):
     p = which + "_"
     for name, got, want, cpu in (("log-prob", lp, z[p + "log_probs"], z[p + "cpu_bf16_log_probs"]),
                                  ("entropy", ent, z[p + "entropy"], z[p + "cpu_bf16_entropy"])):
-        cpu_err = np.abs(cpu.astype(np.float64) - want)
-        bound = 2.0 * np.maximum(cpu_err, np.median(cpu_err))
-        err = np.abs(got - want)
-        print(f"{which} {name}: max err {err.max():.4f} (CPU bf16 {cpu_err.max():.4f}), median {np.median(err):.4f} "
-              f"({np.median(cpu_err):.4f}); past the bound at {int((err > bound).sum())} of {err.size}")
-        assert (err > bound).mean() <= 0.02, [(i, float(err.flat[i]), float(bound.flat[i]))
-                                               for i in np.argwhere(err.reshape(-1) > bound.reshape(-1))[:8, 0]]
-        assert (err <= 3.0 * bound).all(), float((err / bound).max())
+        cpu_err = np.abs(cpu.astype(np.float64) - want).reshape(-1)
+        err = np.abs(got - want).reshape(-1)
+        q = lambda e, f: float(np.quantile(e, f))  # noqa: E731
+        print(f"{which} {name}: ours median / p90 / max {q(err, .5):.4f} / {q(err, .9):.4f} / {err.max():.4f}, "
+              f"CPU bf16 {q(cpu_err, .5):.4f} / {q(cpu_err, .9):.4f} / {cpu_err.max():.4f}")
+        assert q(err, .5) <= 1.5 * q(cpu_err, .5) + 1e-4
+        assert q(err, .9) <= 2.0 * q(cpu_err, .9) + 1e-4
+        assert err.max() <= 2.0 * cpu_err.max() + 1e-4

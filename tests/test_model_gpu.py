@@ -103,7 +103,7 @@ def test_rollout_calculate_log_probs(use_hip_graph):
     """rollout.calculate_log_probs (vllm_rollout_spmd.py:350-395): the fp32 greedy rollout's rollout_log_probs are
     the reference HF model's log-probs of the same tokens (golden log_probs, 1e-4) inside the response and -1 past
     it; a bf16 sampled rollout's (T = 0.9) track the actor's compute_log_prob at that temperature (the decode step's
-    bf16 logits vs the full-sequence pass: 0.05) and feed the reference's debug metrics."""
+    bf16 logits vs the full-sequence pass: two bf16 roundings) and feed the reference's debug metrics."""
     from dots.rl_amd.config import to_attr
     from dots.rl_amd.dp_actor import DataParallelPPOActor
     from dots.rl_amd.metric_utils import calculate_debug_metrics
@@ -141,11 +141,15 @@ def test_rollout_calculate_log_probs(use_hip_graph):
     m = out.batch["attention_mask"][:, -24:].bool()
     rl = out.batch["rollout_log_probs"]
     assert (rl[~m] == -1.0).all()
-    assert (rl[m] - lp[m]).abs().max().item() < 0.05
+    # the decode step's bf16 logits against the full-sequence pass's: two bf16 roundings of logits up to |z| ~ 16
+    # (ulp 0.125) over T = 0.9, i.e. at most ~0.14 apart per token, and most tokens far closer
+    d = (rl[m] - lp[m]).abs()
+    assert d.max().item() < 0.14 and d.mean().item() < 0.02, (d.max().item(), d.mean().item())
     out.batch["old_log_probs"] = lp
     out.batch["response_mask"] = m.to(torch.int64)
     dm = calculate_debug_metrics(out)
     assert dm["training/rollout_probs_diff_max"] < 0.05 and dm["training/rollout_actor_probs_pearson_corr"] > 0.99
+    assert dm["training/rollout_probs_diff_valid"] == 1
 
 
 @pytest.mark.parametrize("temperature,key", [(1.0, "log_probs"), (0.7, "log_probs_t07")])
