@@ -120,47 +120,6 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
   const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)g.a, (short)0, (int)g.a_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)g.b, (short)0, (int)g.b_bytes, 0x00020000);
 
-  // fragment reads. Layout K: one ds_read_b128 (rows fr, k 8 fq .. 8 fq + 7 of a 32-deep k block). Layout T: two
-  // transposed reads (k rows 8 fq + 4 h2 + [0, 4)), lane 4q+p addressing row q, columns 4p .. 4p + 3.
-  const int tq = (lane & 15) >> 2, tp = lane & 3;
-  const int tsw = 2 * (tq | 4 * (fq & 1));  // swz_t of every row this lane addresses
-  const uint32_t lds32 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(
-      (__attribute__((address_space(3))) uint16_t*)lds));
-  auto tr_addr = [&](int region, int col0) {  // byte address of (row 8 fq + tq, 16-column block col0) of a T image
-    const int chunk = (col0 >> 3) + (tp >> 1);
-    return lds32 + 2 * (region + (8 * fq + tq) * 128 + 8 * (chunk ^ tsw) + 4 * (tp & 1));
-  };
-  uint32_t ta[4], tb[2];
-
-  // Narrow tiles: the last tile column when at most 128 of its 256 columns hold data (N = 896, 1152: 3.5 / 4.5 tile
-  // columns). Its 8 waves split 256 rows x 128 columns instead of 256 x 256: wave (wr, wc) computes quadrant row
-  // qm = wr only — rows wr * 128 + (wc >> 1) * 64 + [0, 64), columns (wc & 1) * 64 + [0, 64) — so each SIMD's two
-  // waves take turns by quadrant row: half the MFMAs and half the A-fragment reads of a full tile, where the full
-  // tile's wc = 2, 3 waves multiplied zero columns. Plain / bias / fp32 epilogues (the SwiGLU forms pair columns).
-  constexpr bool kNarrowOK = EPI == EPI_NONE || EPI == EPI_BIAS || EPI == EPI_F32;
-  bool narrow = false;
-  // Short tiles: the last tile row when at most 128 of its 256 rows hold data (M = 896 / 1152: the o_proj, down_proj
-  // and qkv weight gradients): quadrant row 1 is all zero rows, so every wave skips its A reads and MFMAs (any
-  // epilogue: rows past M are never stored)
-  bool shortm = false;
-  int arow = wr * 64, bcol = wc * 32;  // first A row of the wave's fragments in a half-tile, first B image row
-  auto set_frags = [&](int n0) {
-    narrow = kNarrowOK && n0 + 128 >= g.N;
-    arow = narrow ? (wc >> 1) * 64 : wr * 64;
-    bcol = narrow ? (wc & 1) * 32 : wc * 32;
-    if constexpr (AT) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) ta[i] = tr_addr(0, arow + i * 16);
-    }
-    if constexpr (BT) {
-#pragma unroll
-      for (int j = 0; j < 2; ++j) tb[j] = tr_addr(32768, bcol + j * 16);
-    }
-  };
-  // output row of quadrant row qm's first wave row, and the wave's first output column (tile-relative)
-  auto rbase = [&](int qm) { return narrow ? wr * 128 + (wc >> 1) * 64 : qm * 128 + wr * 64; };
-  auto cbase = [&]() { return narrow ? (wc & 1) * 64 : wc * 64; };
-
   // per-lane byte offsets of this wave's two copy instructions of each half-tile h (0 A0, 1 A1, 2 B0, 3 B1) for the
   // current tile, and the byte advance of one k-tile per operand
   uint32_t voff[4][2];
@@ -168,8 +127,6 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
   const uint32_t kstep_b = BT ? static_cast<uint32_t>(64 * g.ldb * 2) : 128u;
 
   auto setup_tile = [&](int m0, int n0) {
-    set_frags(n0);
-    shortm = m0 + 128 >= g.M;
 #pragma unroll
     for (int h = 0; h < 4; ++h)
 #pragma unroll
@@ -223,13 +180,32 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
   u16x8 af[4][2], bq[2][2][2];  // layout-K fragments
   uint64_t at[4][2][2], bt[2][2][2][2];  // layout-T fragment halves (i|j, kb, h2), joined at the MFMA
 
+  // fragment reads. Layout K: one ds_read_b128 (rows fr, k 8 fq .. 8 fq + 7 of a 32-deep k block). Layout T: two
+  // transposed reads (k rows 8 fq + 4 h2 + [0, 4)), lane 4q+p addressing row q, columns 4p .. 4p + 3.
+  const int tq = (lane & 15) >> 2, tp = lane & 3;
+  const int tsw = 2 * (tq | 4 * (fq & 1));  // swz_t of every row this lane addresses
+  const uint32_t lds32 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(
+      (__attribute__((address_space(3))) uint16_t*)lds));
+  auto tr_addr = [&](int region, int col0) {  // byte address of (row 8 fq + tq, 16-column block col0) of a T image
+    const int chunk = (col0 >> 3) + (tp >> 1);
+    return lds32 + 2 * (region + (8 * fq + tq) * 128 + 8 * (chunk ^ tsw) + 4 * (tp & 1));
+  };
+  uint32_t ta[4], tb[2];
+  if constexpr (AT) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ta[i] = tr_addr(0, wr * 64 + i * 16);
+  }
+  if constexpr (BT) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) tb[j] = tr_addr(32768, wc * 32 + j * 16);
+  }
   // half-tile h of k-tile buffer `buf` (compile-time after unrolling)
   auto read_a = [&](int buf, int h) {
     const uint16_t* Ah = lds + lds_half(h, buf);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       if constexpr (!AT) {
-        const int row = arow + i * 16 + fr;
+        const int row = wr * 64 + i * 16 + fr;
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
           af[i][kb] = *reinterpret_cast<const u16x8*>(Ah + row * 64 + 8 * ((4 * kb + fq) ^ swz_k(row)));
@@ -245,7 +221,7 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       if constexpr (!BT) {
-        const int row = bcol + j * 16 + fr;
+        const int row = wc * 32 + j * 16 + fr;
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
           bq[qn][j][kb] = *reinterpret_cast<const u16x8*>(Bh + row * 64 + 8 * ((4 * kb + fq) ^ swz_k(row)));
@@ -278,33 +254,24 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
     if (wr == 1) bar();  // the upper group runs one barrier behind
     for (int kt = k0; kt < k1; kt += 2) {
       const bool last = kt + 2 >= k1;
-      // K % 128 == 64 (the K = 896 projections): the last pair's second k-tile holds no data. Its copies still go out
-      // (as zeros: the vmcnt schedule stays static) and its barriers still run, but its fragment reads and MFMAs are
-      // skipped — they multiplied zeros, 1/8 of the main loop at K = 896 (uniform across the workgroup)
-      const bool empty2 = last && kt + 1 >= g.nkt;
 #pragma unroll
       for (int p = 0; p < 8; ++p) {
         const int lp = p & 3, qm = lp >> 1, qn = (lp == 1 || lp == 2) ? 1 : 0;
         const int buf = p >> 2;
-        const bool skip = buf == 1 && empty2;
-        // narrow tile: the A half of the other quadrant row is never used by this wave; short tile: nor quadrant row 1
-        const bool a_off = (narrow && wr != qm) || (shortm && qm == 1);
-        if (skip) {
-        } else if (lp == 0) {
+        if (lp == 0) {
           read_b(buf, 2, 0);
           __builtin_amdgcn_sched_barrier(0);
-          if (!a_off) read_a(buf, 0);
+          read_a(buf, 0);
         } else if (lp == 1) {
           read_b(buf, 3, 1);
         } else if (lp == 2) {
-          if (!a_off) read_a(buf, 1);
+          read_a(buf, 1);
         }
         constexpr int kH[8] = {1, 2, 0, 3, 1, 2, 0, 3};
         constexpr int kD[8] = {1, 2, 2, 2, 2, 3, 3, 3};
         if (p == 0 || !last) issue(kH[p], kD[p] & 1, kt + kD[p], k1);
         if (lp == 0) {  // the B0 reads (issued first) retired before the barrier (WAR of the next copies)
-          if (a_off) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // no A reads behind them to count on
-          else if constexpr (NA_READS >= 15) asm volatile("s_waitcnt lgkmcnt(15)" ::: "memory");
+          if constexpr (NA_READS >= 15) asm volatile("s_waitcnt lgkmcnt(15)" ::: "memory");
           else if constexpr (NA_READS == 8) asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
         }
         if (p == 3) {
@@ -315,23 +282,21 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
         bar();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);  // nothing that uses an asm read's result moves above its wait
-        if (!skip && !a_off) {
-          __builtin_amdgcn_s_setprio(1);
+        __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-          for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int j = 0; j < 2; ++j)
+          for (int j = 0; j < 2; ++j)
 #pragma unroll
-              for (int kb = 0; kb < 2; ++kb) {
-                const u16x8 fa = AT ? join(at[i][kb][0], at[i][kb][1]) : af[i][kb];
-                const u16x8 fb = BT ? join(bt[qn][j][kb][0], bt[qn][j][kb][1]) : bq[qn][j][kb];
-                // operands swapped: the 16 x 16 block is accumulated transposed, so lane (fq, fr) holds output row
-                // fr, columns 4 fq .. 4 fq + 3 — the epilogue stores straight from registers
-                acc[qm][qn][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(fb), as_bf16x8(fa),
-                                                                            acc[qm][qn][i][j], 0, 0, 0);
-              }
-          __builtin_amdgcn_s_setprio(0);
-        }
+            for (int kb = 0; kb < 2; ++kb) {
+              const u16x8 fa = AT ? join(at[i][kb][0], at[i][kb][1]) : af[i][kb];
+              const u16x8 fb = BT ? join(bt[qn][j][kb][0], bt[qn][j][kb][1]) : bq[qn][j][kb];
+              // operands swapped: the 16 x 16 block is accumulated transposed, so lane (fq, fr) holds output row
+              // fr, columns 4 fq .. 4 fq + 3 — the epilogue stores straight from registers
+              acc[qm][qn][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(fb), as_bf16x8(fa),
+                                                                          acc[qm][qn][i][j], 0, 0, 0);
+            }
+        __builtin_amdgcn_s_setprio(0);
         bar();
       }
     }
@@ -365,18 +330,17 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
       for (int qm = 0; qm < 2; ++qm)
 #pragma unroll
         for (int qn = 0; qn < 2; ++qn) {
-          if (narrow && qm != wr) continue;
 #pragma unroll
           for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int i = 0; i < 4; ++i)
               *reinterpret_cast<f32x4*>(st + (i * 16 + fr) * SLD + j * 16 + 4 * fq) = acc[qm][qn][i][j];
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          const int col = n0 + cbase() + qn * 32 + 4 * ch;
+          const int col = n0 + wc * 64 + qn * 32 + 4 * ch;
 #pragma unroll
           for (int it = 0; it < 8; ++it) {
             const int lr = it * 8 + (lane >> 3);
-            const int m = m0 + rbase(qm) + lr;
+            const int m = m0 + qm * 128 + wr * 64 + lr;
             const f32x4 v = *reinterpret_cast<const f32x4*>(st + lr * SLD + 4 * ch);
             if (m >= g.M || col >= g.N) continue;
             float* p = g.c32 + static_cast<int64_t>(m) * g.ldc + col;
@@ -470,11 +434,11 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
     } else {
       constexpr int SLD = 72;
       uint16_t* st = lds + wave * 64 * SLD;
-      const int ch = lane & 7, col = n0 + cbase() + ch * 8;
+      const int ch = lane & 7, col = n0 + wc * 64 + ch * 8;
       const bool vec = col + 8 <= g.N && (g.ldc & 7) == 0 && (reinterpret_cast<uintptr_t>(g.c) & 15) == 0 &&
                        (EPI != EPI_SWIGLU_BWD || ((g.ldc2 & 7) == 0 && (g.N & 7) == 0 &&
                                                   (reinterpret_cast<uintptr_t>(g.c2) & 15) == 0));
-      const bool interior = m0 + 256 <= g.M && n0 + (narrow ? 128 : 256) <= g.N && (g.ldc & 7) == 0 &&
+      const bool interior = m0 + 256 <= g.M && n0 + 256 <= g.N && (g.ldc & 7) == 0 &&
                             (reinterpret_cast<uintptr_t>(g.c) & 15) == 0;
       if constexpr (EPI == EPI_SWIGLU_BWD) {
         // the down_proj dgrad fused with the SwiGLU backward. Per quadrant: stage bf16(d a) through LDS, then read
@@ -587,7 +551,6 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
       } else {
 #pragma unroll
       for (int qm = 0; qm < 2; ++qm) {
-        if (narrow && qm != wr) continue;
 #pragma unroll
         for (int qn = 0; qn < 2; ++qn)
 #pragma unroll
@@ -596,7 +559,7 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
             float bb[4] = {0.f, 0.f, 0.f, 0.f};
             if constexpr (EPI == EPI_BIAS) {
 #pragma unroll
-              for (int e = 0; e < 4; ++e) bb[e] = bf16_to_f32(g.bias[min(n0 + cbase() + lc + e, g.N - 1)]);
+              for (int e = 0; e < 4; ++e) bb[e] = bf16_to_f32(g.bias[min(n0 + wc * 64 + lc + e, g.N - 1)]);
             }
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
@@ -616,7 +579,7 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if (EPI != EPI_SWIGLU_BWD && interior && !(g.dbg & 2)) {
           // whole tile inside C (uniform): one row base, rows 8 apart, no per-row tests
-          uint16_t* dst = g.c + static_cast<int64_t>(m0 + rbase(qm) + (lane >> 3)) * g.ldc + col;
+          uint16_t* dst = g.c + static_cast<int64_t>(m0 + qm * 128 + wr * 64 + (lane >> 3)) * g.ldc + col;
           const int64_t step = 8 * g.ldc;
 #pragma unroll
           for (int it = 0; it < 8; ++it)
@@ -628,7 +591,7 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
 #pragma unroll
         for (int it = 0; it < 8; ++it) {
           const int lr = it * 8 + (lane >> 3);
-          const int m = m0 + rbase(qm) + lr;
+          const int m = m0 + qm * 128 + wr * 64 + lr;
           const u16x8 v = *reinterpret_cast<const u16x8*>(st + lr * SLD + ch * 8);
           if (m >= g.M || col >= g.N) continue;
           uint16_t* dstp = g.c + static_cast<int64_t>(m) * g.ldc + col;
@@ -711,16 +674,16 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
 #pragma unroll
           for (int j = 0; j < 2; ++j) {
             const int reg = ((a * 2 + b) * 4 + i) * 2 + j;
-            if (reg < r0 || reg >= r1 || (narrow && a != wr)) continue;
+            if (reg < r0 || reg >= r1) continue;
             f32x4 v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rws, vt, reg * 8192, 16));
             for (int s2 = 1; s2 < S; ++s2)
               v += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rws, vt + s2 * SLAB * 4, reg * 8192, 16));
             // transposed block (see the epilogue): row fr, columns 4 fq + r
-            const int m = m0 + rbase(a) + i * 16 + fr;
+            const int m = m0 + a * 128 + wr * 64 + i * 16 + fr;
             if (m >= g.M) continue;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              const int col = n0 + cbase() + b * 32 + j * 16 + 4 * fq + r;
+              const int col = n0 + wc * 64 + b * 32 + j * 16 + 4 * fq + r;
               if (col >= g.N) continue;
               if constexpr (EPI == EPI_F32) {
                 float* p = g.c32 + static_cast<int64_t>(m) * g.ldc + col;
