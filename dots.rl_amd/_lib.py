@@ -92,7 +92,7 @@ F32 = ctypes.c_float
 SZ = ctypes.c_size_t
 
 # name -> (restype, argtypes); must match include/dotsrl_amd.h exactly
-ABI_VERSION = 4  # include/dotsrl_amd.h DRL_ABI_VERSION: the layouts below (PPOLossParams) are of this version
+ABI_VERSION = 5  # include/dotsrl_amd.h DRL_ABI_VERSION: the layouts below (PPOLossParams) are of this version
 
 SIGNATURES = {
     "drl_last_error": (ctypes.c_char_p, []),
@@ -147,8 +147,8 @@ SIGNATURES = {
                                           P]),
     "drl_decode_attention_vt_workspace_bytes": (SZ, [I64, I64, I64, I64]),
     "drl_decode_attention_set_plan": (None, [I32, I32]),
-    "drl_decode_attention_vt": (ctypes.c_int, [P, P, P, I32, P, I64, P, I64, I64, I64, I64, I64, I64, I64, I64, F32,
-                                               P, I64, P, SZ, P]),
+    "drl_decode_attention_vt": (ctypes.c_int, [P, P, P, I32, P, I64, P, I64, I64, I64, I64, I64, I64, I64, I64, I64,
+                                               I64, F32, P, I64, P, SZ, P]),
     "drl_flash_attn_bwd": (ctypes.c_int, [P, P, P, P, P, P, P, I32, P, I64, I64, I64, I64, I64, I64, I64, F32, P, P, P, P,
                                           P]),
     "drl_decode_attention": (ctypes.c_int, [P, P, P, I32, P, I64, P, I64, I64, I64, I64, I64, I64, I64, F32, P, P, SZ,

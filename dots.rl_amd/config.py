@@ -100,6 +100,9 @@ DEFAULTS = dict(
             # rollout.yaml:177: emit `rollout_log_probs` (log p of each sampled token under the decode step's own
             # logits, -1 past the response) -> training/rollout_probs_diff_* metrics (ray_trainer.py:1221-1225)
             calculate_log_probs=False,
+            # prefix caching of the n samples' shared prompt (vllm_rollout_spmd.py:195 runs vLLM with it on): each
+            # distinct prompt prefilled once, its keys read from one cache row by the group's decode attention
+            enable_prefix_caching=True,
         ),
         ref=dict(log_prob_micro_batch_size=None, log_prob_micro_batch_size_per_gpu=16, log_prob_use_dynamic_bsz=False,
                  log_prob_max_token_len_per_gpu=16384, exec_log_prob_tokens=196608,

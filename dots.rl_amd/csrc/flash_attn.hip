@@ -878,7 +878,29 @@ struct DecodeArgs {
   int64_t out_mbt;
   float* slabs;        // split-K: (B*Hkv, splits, 64 + 32*D) fp32 partial states (m, l, unnormalised o)
   unsigned* tickets;   // split-K: (B*Hkv) arrival counters, zero between launches
+  // prompt groups: sequences b = p * group + r (r < group) share one prompt, whose keys [0, shared) are read from
+  // cache row p (the rollout prefills each distinct prompt once); group 1 / shared 0: every row reads its own
+  int64_t group, shared;
 };
+
+// (sequence, KV head) of workgroup `bid` under prompt groups: the group's rows of one (prompt, head) run as
+// workgroups bid, bid + 8, ..., i.e. on one XCD under the observed round-robin dealing (MI355X_MICROARCH.md,
+// workgroup dispatch), next to each other in time, so the shared prompt keys one of them fetches are L2 hits for
+// the others (speed only: any placement gives the same result)
+__device__ __forceinline__ int64_t dec_grouped_bh(int64_t bid, int64_t group, int64_t Hkv, int64_t total) {
+  const int64_t units = total / group;
+  int64_t u, r;
+  if (units % 8 == 0) {
+    const int64_t slot = bid >> 3;
+    r = slot % group;
+    u = (slot / group) * 8 + (bid & 7);
+  } else {
+    u = bid / group;
+    r = bid % group;
+  }
+  const int64_t p = u / Hkv, hd = u - p * Hkv;
+  return (p * group + r) * Hkv + hd;
+}
 
 // one 32-key block of the cache for lane (qi, h): K rows (A operand of S^T = K Q^T), V^T columns
 // (A operand of O^T = V^T P^T) and the key-valid bytes of the keys this lane's scores cover
@@ -1088,12 +1110,22 @@ __global__ __launch_bounds__(64 * NW) void decode_mfma_kernel(DecodeArgs a) {
   __shared__ __attribute__((aligned(16))) float s_o[NW][MT][16][64];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int qi = lane & 31, h = lane >> 5;
-  const int64_t bh = blockIdx.x, b = bh / a.Hkv;
+  const int64_t bh = a.group > 1 ? dec_grouped_bh(blockIdx.x, a.group, a.Hkv, gridDim.x) : blockIdx.x;
+  const int64_t b = bh / a.Hkv;
   const int qpos = static_cast<int>(a.qpos_ptr ? *a.qpos_ptr : a.qpos);
   const int kend = static_cast<int>(min(a.L, static_cast<int64_t>(qpos) + 1));
   const uint16_t* kb = a.k + bh * a.ld_k * D;
   const uint16_t* vtb = a.vt + bh * vt_panel(a.ld_vt, D, a.ld_k);
   const uint8_t* vrow = a.valid + b * a.ld_valid;
+  // the shared prompt keys [0, a.shared) of this row: cache row b / group (same KV head)
+  const int64_t bs = b / a.group, bhs = bs * a.Hkv + (bh - b * a.Hkv);
+  const uint16_t* kbs = a.k + bhs * a.ld_k * D;
+  const uint16_t* vtbs = a.vt + bhs * vt_panel(a.ld_vt, D, a.ld_k);
+  const uint8_t* vrows = a.valid + bs * a.ld_valid;
+  auto load = [&](int k0, DecRaw<D>& r) {  // a.shared is a multiple of 32: a block is wholly shared or wholly own
+    if (k0 < a.shared) dec_load_raw<D>(kbs, vtbs, vrows, a.ld_vt, a.ld_valid, k0, kend, lane, h, r);
+    else dec_load_raw<D>(kb, vtb, vrow, a.ld_vt, a.ld_valid, k0, kend, lane, h, r);
+  };
   // split-K over gridDim.y workgroups: split y takes 32-key blocks [y*n/S, (y+1)*n/S) of the n live blocks;
   // each wave takes blocks ib0, ib0 + NW, ... and has its first NB (LEAN: 1) in flight together with q
   const int nall = (kend + 31) / 32, S = gridDim.y, y = blockIdx.y;
@@ -1105,7 +1137,7 @@ __global__ __launch_bounds__(64 * NW) void decode_mfma_kernel(DecodeArgs a) {
   uint16_t* vslot = kslot + 32 * D;                                 // D * 32 bf16
 #pragma unroll
   for (int j = 0; j < NR; ++j)
-    if (ib0 + j * NW < nblk) dec_load_raw<D>(kb, vtb, vrow, a.ld_vt, a.ld_valid, 32 * (ib0 + j * NW), kend, lane, h, R[j]);
+    if (ib0 + j * NW < nblk) load(32 * (ib0 + j * NW), R[j]);
   bf16x8 qf[KS];
   {
     const bool qv = qi < a.G;
@@ -1126,7 +1158,7 @@ __global__ __launch_bounds__(64 * NW) void decode_mfma_kernel(DecodeArgs a) {
     for (int ib = ib0; ib < nblk; ib += NW) {
       dec_stage<D>(R[0], kslot, vslot, lane);
       const uint32_t vb[4] = {R[0].vb[0], R[0].vb[1], R[0].vb[2], R[0].vb[3]};
-      if (ib + NW < nblk) dec_load_raw<D>(kb, vtb, vrow, a.ld_vt, a.ld_valid, 32 * (ib + NW), kend, lane, h, R[0]);
+      if (ib + NW < nblk) load(32 * (ib + NW), R[0]);
       dec_block_lds<D>(kslot, vslot, vb, qf, a.scale_log2, qi, h, m, lsum, o);
     }
   } else
@@ -1138,8 +1170,7 @@ __global__ __launch_bounds__(64 * NW) void decode_mfma_kernel(DecodeArgs a) {
       if (ibj < nblk) {
         DecBlock<D> blk;
         dec_reshape<D>(R[j], kslot, vslot, lane, qi, h, blk);
-        if (ibj + NB * NW < nblk)
-          dec_load_raw<D>(kb, vtb, vrow, a.ld_vt, a.ld_valid, 32 * (ibj + NB * NW), kend, lane, h, R[j]);
+        if (ibj + NB * NW < nblk) load(32 * (ibj + NB * NW), R[j]);
         dec_block<D>(blk, qf, a.scale_log2, m, lsum, o);
       }
     }
@@ -1362,8 +1393,8 @@ size_t drl_decode_attention_vt_workspace_bytes(int64_t B, int64_t Hkv, int64_t D
 int drl_decode_attention_vt(const void* q, const void* k_cache, const void* vt_cache, int32_t dt,
                             const uint8_t* key_valid, int64_t ld_valid, const int64_t* qpos_ptr, int64_t qpos,
                             int64_t B, int64_t Hkv, int64_t G, int64_t D, int64_t ld_k, int64_t ld_vt, int64_t L,
-                            float scale, void* out, int64_t out_mbt, void* workspace, size_t workspace_bytes,
-                            void* stream) {
+                            int64_t group, int64_t shared_keys, float scale, void* out, int64_t out_mbt,
+                            void* workspace, size_t workspace_bytes, void* stream) {
   using namespace drl;
   DRL_CHECK_ARG(q && k_cache && vt_cache && key_valid && out, "NULL input");
   DRL_CHECK_ARG(dt == DRL_BF16, "MFMA decode attention runs on bf16");
@@ -1376,9 +1407,13 @@ int drl_decode_attention_vt(const void* q, const void* k_cache, const void* vt_c
                 "ld_vt must be a multiple of 8 and key_valid rows 4-byte aligned");
   DRL_CHECK_ARG(aligned16(q) && aligned16(k_cache) && aligned16(vt_cache) && (reinterpret_cast<uintptr_t>(out) & 7u) == 0,
                 "misaligned operand (q, caches 16-byte aligned)");
+  DRL_CHECK_ARG(group >= 1 && B % group == 0 && shared_keys >= 0 && shared_keys % 32 == 0 && shared_keys <= L &&
+                    (group > 1 || shared_keys == 0),
+                "prompt groups: group must divide B, shared_keys a multiple of 32 within L (0 without groups)");
   DecodeArgs a{static_cast<const uint16_t*>(q), static_cast<const uint16_t*>(k_cache),
                static_cast<const uint16_t*>(vt_cache), key_valid, ld_valid, qpos_ptr, qpos, Hkv, G, ld_k, ld_vt, L,
-               scale * 1.4426950408889634f, static_cast<uint16_t*>(out), out_mbt, nullptr, nullptr};
+               scale * 1.4426950408889634f, static_cast<uint16_t*>(out), out_mbt, nullptr, nullptr, group,
+               shared_keys};
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int64_t wgs = B * Hkv, cus = cu_count();
   const int splits = decode_splits(B, Hkv, L);

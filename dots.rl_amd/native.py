@@ -924,9 +924,11 @@ def _linear_workspace(device, nbytes, kind="linear"):
     return ws
 
 
-def decode_attention_vt(q, k_cache, vt_cache, key_valid, L, out, qpos=None, qpos_dev=None, out_mbt=0):
+def decode_attention_vt(q, k_cache, vt_cache, key_valid, L, out, qpos=None, qpos_dev=None, out_mbt=0, group=1,
+                        shared_keys=0):
     """MFMA decode attention: q (B,Hkv,G,D) bf16, k_cache (B,Hkv,ld_k,D), vt_cache (B,Hkv,D,ld_vt). ``out_mbt`` > 0:
-    ``out`` is the fragment-packed (B, Hq*D) panel of the decode o_proj GEMM (decode_gemm layout)."""
+    ``out`` is the fragment-packed (B, Hq*D) panel of the decode o_proj GEMM (decode_gemm layout). Prompt groups:
+    rows p * group + r read keys < ``shared_keys`` (a multiple of 32) from cache row p."""
     _dev(q, k_cache, vt_cache, key_valid, out)
     B, Hkv, G, D = q.shape
     assert q.is_contiguous() and k_cache.is_contiguous() and out.is_contiguous()
@@ -938,7 +940,8 @@ def decode_attention_vt(q, k_cache, vt_cache, key_valid, L, out, qpos=None, qpos
     ws = _linear_workspace(q.device, nws, "decode_attention") if nws else None
     check(lib().drl_decode_attention_vt(_p(q), _p(k_cache), _p(vt_cache), _edt(q), _p(key_valid), key_valid.stride(0),
                                         _p(qpos_dev), qp, B, Hkv, G, D, k_cache.shape[2], vt_ld(vt_cache), L,
-                                        1.0 / math.sqrt(D), _p(out), int(out_mbt), _p(ws), nws, _stream()),
+                                        int(group), int(shared_keys), 1.0 / math.sqrt(D), _p(out), int(out_mbt),
+                                        _p(ws), nws, _stream()),
           "drl_decode_attention_vt")
     return out
 

@@ -496,7 +496,8 @@ def _layer_forward(m, i, x_prev, delta, pos, key_valid, save, cache=None, koff=0
         attn = torch.empty(B, 1, Hq * D, dtype=dt, device=dev)
         Lk = L if koff_dev is None else kbuf.shape[2]  # device position: the kernel stops at koff_dev
         if vt is not None:
-            native.decode_attention_vt(q.view(B, Hkv, G, D), kbuf, vt, key_valid, Lk, attn, qpos_dev=koff_dev)
+            native.decode_attention_vt(q.view(B, Hkv, G, D), kbuf, vt, key_valid, Lk, attn, qpos_dev=koff_dev,
+                                       group=cache.group, shared_keys=cache.shared)
         else:
             native.decode_attention(q.view(B, Hkv, G, D), kbuf, vbuf, key_valid, Lk, attn, qpos_dev=koff_dev)
         P = None
@@ -741,6 +742,7 @@ class KVCacheRows:
         self.valid = cache.valid[r0:r1]
         self.len = cache.len
         self.Tmax = cache.Tmax
+        self.group, self.shared = 1, 0
 
 
 class KVCache:
@@ -761,6 +763,29 @@ class KVCache:
         self.valid = torch.zeros(B, (Tmax + 3) // 4 * 4, dtype=torch.uint8, device=device)[:, :Tmax]
         self.len = 0
         self.Tmax = Tmax
+        # prompt groups (share_prompts): row p * group + r reads keys < shared from row p
+        self.group, self.shared = 1, 0
+
+    def share_prompts(self, group, P):
+        """After rows [0, B / group) were prefilled with the distinct prompts (keys [0, P)): rows p * group + r (the
+        group's samples of prompt p) read the whole 32-key blocks below P from row p in the MFMA decode attention
+        (drl_decode_attention_vt prompt groups); every row gets its own copy of the rest — the keys of the block
+        holding P - 1 when P % 32 != 0, all of them for the fp32 cache (row-major V, no grouped kernel) — and of
+        the prompt's key-valid bytes."""
+        B = self.valid.shape[0]
+        src = torch.arange(B, device=self.valid.device) // group
+        shared = P // 32 * 32 if self.vt[0] is not None else 0
+        for i in range(len(self.k)):
+            if shared < P:
+                self.k[i][:, :, shared:P] = self.k[i][src, :, shared:P]
+                if self.vt[i] is not None:
+                    b0, b1 = shared // 32, (P + 31) // 32
+                    self.vt[i][:, :, b0:b1] = self.vt[i][src, :, b0:b1]
+                else:
+                    self.v[i][:, :, :P] = self.v[i][src, :, :P]
+        self.valid[:, :P] = self.valid[src, :P]
+        self.len = P
+        self.group, self.shared = (group, shared) if shared > 0 else (1, 0)
 
     def vt_plain(self, i):
         """Layer i's V^T as a head-dim-major (B, Hkv, D, Tmax) copy (tests / inspection)."""
@@ -991,7 +1016,7 @@ class PackedDecode:
             native.decode_qkv_rope(self.h_p, w["qkv"], m.qkv_bias(i), pos, m.cos, m.sin, B, H, Hq, Hkv, D,
                                    self.q, cache.k[i], cache.vt[i], kpos_dev)
             native.decode_attention_vt(self.q, cache.k[i], cache.vt[i], cache.valid, Lk, self.attn_p,
-                                       qpos_dev=kpos_dev, out_mbt=mbt)
+                                       qpos_dev=kpos_dev, out_mbt=mbt, group=cache.group, shared_keys=cache.shared)
             native.decode_gemm(self.attn_p, w["o"], B, H, self.HD, partials=self.part_o)
             native.decode_rmsnorm(self.x, self.part_o, self.x, s.w(p + "post_attention_layernorm"), self.h_p, eps,
                                   mbt=mbt)

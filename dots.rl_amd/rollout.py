@@ -98,8 +98,17 @@ class MI355XRollout:
         m = self.module
         m.training = False
         cache = KVCache(m.cfg, B, P + R, dev, m.dtype)
+        group = self._prompt_group(idx, attention_mask, position_ids)
+        self.last_prompt_group = group
         t0 = time.perf_counter()
-        h = m.prefill(cache, idx, attention_mask, position_ids)
+        if group > 1:  # each distinct prompt prefilled once, its KV shared by the group's samples
+            Bu = B // group
+            h = m.prefill(KVCacheRows(cache, 0, Bu), idx[::group].contiguous(), attention_mask[::group].contiguous(),
+                          position_ids[::group].contiguous())
+            cache.share_prompts(group, P)
+            h = h.repeat_interleave(group, 0)
+        else:
+            h = m.prefill(cache, idx, attention_mask, position_ids)
         torch.cuda.synchronize()
         self.last_prefill_s = time.perf_counter() - t0
         responses = torch.empty(B, R, dtype=torch.int64, device=dev)
@@ -145,6 +154,21 @@ class MI355XRollout:
             tensors["rollout_log_probs"] = torch.where(resp_mask.bool(), rollout_lp, rollout_lp.new_full((), -1.0))
         return DataProto(batch=TensorBatch(tensors, batch_size=B))
 
+    def _prompt_group(self, idx, attention_mask, position_ids):
+        """Rows in runs of ``rollout.n`` identical prompts — the trainer's repeat(n, interleave=True) of the batch
+        (ray_trainer.py:1146) — are prefilled once per distinct prompt and decode against one copy of its keys:
+        the prefix caching the reference's vLLM rollout runs with (vllm_rollout_spmd.py:195,
+        enable_prefix_caching=True). Same tokens as prefilling every row: the rows' prompt keys / values are
+        identical. ``rollout.enable_prefix_caching`` False, another layout, or row lanes: 1 (every row its own)."""
+        cfg = self.config
+        n = int(cfg.get("n", 1) or 1)
+        B = idx.shape[0]
+        if n <= 1 or B % n or not cfg.get("enable_prefix_caching", True) or int(cfg.get("decode_lanes", 1) or 1) > 1:
+            return 1
+        same = torch.stack([(t.view(B // n, n, -1) == t.view(B // n, n, -1)[:, :1]).all()
+                            for t in (idx, attention_mask, position_ids)]).all()
+        return n if bool(same) else 1
+
     def _lp_col(self, rollout_lp, t):
         return dict(self._lp, logprob_out=rollout_lp[:, t]) if rollout_lp is not None else {}
 
@@ -160,7 +184,7 @@ class MI355XRollout:
         t_dev = torch.ones(1, dtype=torch.int64, device=responses.device)
         B = responses.shape[0]
         max_rows = int(self.config.get("packed_decode_max_rows", 512))
-        lanes = self._decode_lanes(B, max_rows) if rollout_lp is None else 1
+        lanes = self._decode_lanes(B, max_rows) if rollout_lp is None and cache.group == 1 else 1
         if lanes > 1:
             return self._decode_graphed_lanes(cache, responses, last_pos, P, R, sel, lanes)
         use = self.config.get("packed_decode", True) and PackedDecode.supported(m, B, max_rows)

@@ -24,7 +24,7 @@ extern "C" {
 
 /* 3: drl_ppo_loss_params gained policy_loss, cov_ratio, clip_cov_lb, clip_cov_ub, ppo_kl_coef, cov_seed (a caller
  * built against version 2 passes a shorter struct); drl_gemm (operand layouts, fp32 epilogues, stream-K) */
-#define DRL_ABI_VERSION 4
+#define DRL_ABI_VERSION 5
 
 /* ld_vt value selecting the key-blocked V^T cache layout (B, Hkv, ceil(cap / 32), D, 32) wherever a V^T
  * operand with a leading dimension ld_vt is taken (flash / decode attention, the rope and decode-projection
@@ -448,11 +448,15 @@ void drl_decode_attention_set_plan(int32_t waves, int32_t splits);
  * wave, fragments read from LDS); 2..4 = that many blocks in flight per wave (4 and 8 waves, D = 64; else 2).
  * Results are identical. */
 void drl_decode_attention_set_variant(int32_t variant);
+/* Prompt groups (the n samples of one prompt, hf_rollout.py's repeated prompts / vLLM's shared prefix): with
+ * group > 1, sequences b = p * group + r share one prompt, and keys j < shared_keys (a multiple of 32, <= L) are
+ * read from cache row p — K, V^T and key_valid — where the rollout prefilled each distinct prompt once; keys
+ * j >= shared_keys from row b. group 1 and shared_keys 0: every row reads its own keys. */
 int drl_decode_attention_vt(const void* q, const void* k_cache, const void* vt_cache, int32_t dt,
                             const uint8_t* key_valid, int64_t ld_valid, const int64_t* qpos_ptr, int64_t qpos,
                             int64_t B, int64_t Hkv, int64_t G, int64_t D, int64_t ld_k, int64_t ld_vt, int64_t L,
-                            float scale, void* out, int64_t out_mbt, void* workspace, size_t workspace_bytes,
-                            void* stream);
+                            int64_t group, int64_t shared_keys, float scale, void* out, int64_t out_mbt,
+                            void* workspace, size_t workspace_bytes, void* stream);
 /* Backward of drl_flash_attn_fwd for Tq == Tk == T, qoff = 0 (the training forward), recomputing P from lse:
  * q (B,Hkv,G,T,D), k / v (B,Hkv,T,D) row-major, kt (B,Hkv,D,ld_t) head-dim-major copy of k (written by
  * drl_rope_qkv_fwd), o and dout (B,T,Hkv*G*D), lse from the forward. delta: (B,Hkv,G,T) fp32 scratch.
