@@ -166,6 +166,7 @@ SIGNATURES = {
     "drl_gemm_set_sk_tuning": (None, [I32, I32, I32, I32]),
     "drl_gemm_set_debug": (None, [I32]),
     "drl_copy_rows": (ctypes.c_int, [P, I64, P, P, I64, P, I64, I64, P]),
+    "drl_sum_rows": (ctypes.c_int, [P, I64, P, I64, P, I64, P, I64, I64, I32, P]),
     "drl_colsum_bf16_workspace_bytes": (SZ, [I64, I64]),
     "drl_colsum_bf16_acc": (ctypes.c_int, [P, I64, I64, I64, P, P, SZ, P]),
     "drl_decode_gemm_force_tiled": (None, [I32, I32]),

@@ -62,7 +62,10 @@ DEFAULTS = dict(
               reward_fn_key="data_source"),
     actor_rollout_ref=dict(
         hybrid_engine=True,
+        # share_prompt_prefix: the n samples of a prompt run its tokens once in the log-prob / update passes
+        # (qwen2.PrefixShare: same values, the per-token work of the prompt done once per group)
         model=dict(path="random:qwen2.5-0.5b", override_config={}, use_remove_padding=False, use_fused_kernels=False,
+                   share_prompt_prefix=True,
                    enable_gradient_checkpointing=False, external_lib=None, dtype="bfloat16",
                    gemm_tuning="auto"),  # replay offline GEMM algorithm choices (workers._enable_gemm_tuning)
         actor=dict(

@@ -20,8 +20,75 @@ __global__ __launch_bounds__(256) void copy_rows_kernel(const uint8_t* src, int6
   for (int64_t c = threadIdx.x & 63; c < row_bytes / 16; c += 64) dp[c] = sp[c];
 }
 
+// dst[dst_idx[j]] = sum over k < K of src[src_idx[k * m + j]] (index < 0: no term), fp32 accumulation in k order:
+// the gradient of a packed row that K padded positions read (a prompt token shared by a group's samples). One wave
+// per output row, 16-B lanes (8 bf16 / 4 fp32 elements).
+template <typename T>
+__global__ __launch_bounds__(256) void sum_rows_kernel(const T* src, int64_t ld_src, const int64_t* src_idx,
+                                                       int64_t K, T* dst, int64_t ld_dst, const int64_t* dst_idx,
+                                                       int64_t m, int64_t cols) {
+  constexpr int E = 16 / sizeof(T);
+  const int64_t j = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  if (j >= m) return;
+  const int64_t d = dst_idx ? dst_idx[j] : j;
+  if (d < 0) return;
+  for (int64_t c = (threadIdx.x & 63) * E; c < cols; c += 64 * E) {
+    float acc[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) acc[e] = 0.f;
+    for (int64_t k = 0; k < K; ++k) {
+      const int64_t s = src_idx[k * m + j];
+      if (s < 0) continue;
+      const uint4 v = *reinterpret_cast<const uint4*>(src + s * ld_src + c);
+      if constexpr (sizeof(T) == 2) {
+        const uint16_t* h = reinterpret_cast<const uint16_t*>(&v);
+#pragma unroll
+        for (int e = 0; e < E; ++e) acc[e] += bf16_to_f32(h[e]);
+      } else {
+        const float* f = reinterpret_cast<const float*>(&v);
+#pragma unroll
+        for (int e = 0; e < E; ++e) acc[e] += f[e];
+      }
+    }
+    uint4 o;
+    if constexpr (sizeof(T) == 2) {
+      uint16_t* h = reinterpret_cast<uint16_t*>(&o);
+#pragma unroll
+      for (int e = 0; e < E; ++e) h[e] = f32_to_bf16(acc[e]);
+    } else {
+      float* f = reinterpret_cast<float*>(&o);
+#pragma unroll
+      for (int e = 0; e < E; ++e) f[e] = acc[e];
+    }
+    *reinterpret_cast<uint4*>(dst + d * ld_dst + c) = o;
+  }
+}
+
 }  // namespace
 }  // namespace drl
+
+extern "C" int drl_sum_rows(const void* src, int64_t ld_src, const int64_t* src_idx, int64_t K, void* dst,
+                            int64_t ld_dst, const int64_t* dst_idx, int64_t m, int64_t cols, int32_t dt,
+                            void* stream) {
+  using namespace drl;
+  DRL_CHECK_ARG(src && dst && src_idx && K >= 1 && m >= 0 && cols >= 1, "NULL operand or empty shape");
+  DRL_CHECK_ARG(dt == DRL_BF16 || dt == DRL_F32, "bf16 or fp32 rows");
+  const int64_t e = dt == DRL_BF16 ? 8 : 4;
+  DRL_CHECK_ARG(cols % e == 0 && ld_src % e == 0 && ld_dst % e == 0 && ld_src >= cols && ld_dst >= cols &&
+                    aligned16(src) && aligned16(dst),
+                "16-byte aligned rows of 16-byte multiples");
+  if (m == 0) return DRL_OK;
+  const dim3 grid(static_cast<unsigned>((m + 3) / 4));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (dt == DRL_BF16)
+    hipLaunchKernelGGL(sum_rows_kernel<uint16_t>, grid, dim3(256), 0, s, static_cast<const uint16_t*>(src), ld_src,
+                       src_idx, K, static_cast<uint16_t*>(dst), ld_dst, dst_idx, m, cols);
+  else
+    hipLaunchKernelGGL(sum_rows_kernel<float>, grid, dim3(256), 0, s, static_cast<const float*>(src), ld_src, src_idx,
+                       K, static_cast<float*>(dst), ld_dst, dst_idx, m, cols);
+  DRL_LAUNCH_CHECK();
+  return DRL_OK;
+}
 
 extern "C" int drl_copy_rows(const void* src, int64_t ld_src_bytes, const int64_t* src_idx, void* dst,
                              int64_t ld_dst_bytes, const int64_t* dst_idx, int64_t n_rows, int64_t row_bytes,

@@ -19,7 +19,7 @@ from . import native
 from .core_algos import cov_loss_kw, fused_actor_loss
 from .protocol import DataProto
 from .seqlen_balancing import prepare_dynamic_batch, restore_dynamic_batch
-from .qwen2 import Qwen2Model, RmPad, gather_rows
+from .qwen2 import PrefixShare, Qwen2Model, RmPad, gather_rows
 from .torch_functional import logprobs_and_entropy_from_logits
 
 
@@ -269,6 +269,7 @@ class DataParallelPPOActor:
         self.actor_optimizer = actor_optimizer
         self.use_remove_padding = config.get("use_remove_padding", False)
         self.use_fused_kernels = config.get("use_fused_kernels", False)
+        self.share_prompt_prefix = config.get("share_prompt_prefix", True)
 
     def _forward_micro_batch(self, micro_batch, temperature, calculate_entropy=False):
         """dp_actor.py:90-280: full-sequence forward, logits only at the R positions that predict the response
@@ -277,15 +278,20 @@ class DataParallelPPOActor:
         use_remove_padding (dp_actor.py:119-247): the backbone runs on the nnz attended tokens only (RmPad), the R
         predicting rows are gathered from the packed hidden states and the outputs at pad positions are 0 (the
         reference's pad_input). The reference takes the label of the last attended token from the next packed
-        sequence; that position is outside the response mask in both."""
+        sequence; that position is outside the response mask in both.
+
+        share_prompt_prefix (qwen2.PrefixShare): rows of the pass that share a prompt — the n samples of a GRPO
+        group — run the prompt's tokens once; their attention still reads every row's full sequence."""
         m = self.actor_module
         responses = micro_batch["responses"]
         B, R = responses.shape
         am = micro_batch["attention_mask"]
         keep = None
-        if self.use_remove_padding:
+        share = PrefixShare.build(micro_batch["input_ids"], am, R, keep_pads=not self.use_remove_padding) \
+            if self.share_prompt_prefix else None
+        if share is not None or self.use_remove_padding:
             T = am.shape[1]
-            rm = RmPad(am)
+            rm = share if share is not None else RmPad(am)
             h = m.hidden_states(micro_batch["input_ids"], am, micro_batch["position_ids"], rm=rm)
             sel = rm.inv.view(B, T)[:, T - R - 1:T - 1].reshape(-1).contiguous()
             h = gather_rows(h.view(rm.nnz, h.shape[-1]), sel)

@@ -812,6 +812,21 @@ def copy_rows(src, dst, src_idx=None, dst_idx=None, n=None):
     return dst
 
 
+def sum_rows(src, src_idx, dst, dst_idx=None):
+    """dst[dst_idx[j]] = sum_k src[src_idx[k, j]] for src_idx (K, m) (entries < 0 add nothing), fp32 accumulation in
+    k order (csrc/rows.hip): the gradient of a packed row read by several padded positions (prefix sharing)."""
+    _dev(src, dst, src_idx, dst_idx)
+    assert src.dim() == 2 and dst.dim() == 2 and src.stride(1) == 1 and dst.stride(1) == 1
+    assert src.dtype == dst.dtype and src.shape[1] == dst.shape[1] and src_idx.dim() == 2
+    K, m = src_idx.shape
+    for ix in (src_idx, dst_idx):
+        assert ix is None or (ix.dtype == torch.int64 and ix.is_contiguous())
+    assert dst_idx is None or dst_idx.numel() == m
+    check(lib().drl_sum_rows(_p(src), src.stride(0), _p(src_idx), K, _p(dst), dst.stride(0), _p(dst_idx), m,
+                             src.shape[1], _edt(src), _stream()), "drl_sum_rows")
+    return dst
+
+
 LAYOUT_K, LAYOUT_T = 0, 1
 
 

@@ -603,7 +603,7 @@ class _DecoderLayer(torch.autograd.Function):
         rm = ctx.rm
         attn = sv["attn"]
         if rm is not None:  # attention backward in the padded layout (zero gradient at the pad rows)
-            dattn = rm.unpack(dattn)
+            dattn = rm.unpack_grad(dattn)
             attn = sv["attn_pad"]
             B, T = rm.B, rm.T
         if isinstance(sv["P"], str):  # "flash": fused forward, fused backward
@@ -628,7 +628,7 @@ class _DecoderLayer(torch.autograd.Function):
             dk = torch.bmm(dS.transpose(1, 2), q3)
         dqkv = torch.empty(B, T, (Hq + 2 * Hkv) * D, dtype=dt, device=dx2.device)
         native.rope_qkv_bwd(dq, dk, dv, ctx.pos, m.cos, m.sin, Hq, Hkv, D, dqkv)
-        dqkv2 = dqkv.view(B * T, -1) if rm is None else rm.pack(dqkv.view(B * T, -1))
+        dqkv2 = dqkv.view(B * T, -1) if rm is None else rm.pack_grad(dqkv.view(B * T, -1))
         dh1 = dgrad_wgrad(dqkv2, s.w(p + "qkv_proj.weight"), s.g(p + "qkv_proj.weight"), sv["h1"].view(N, H))
         if m.cfg.attention_bias:
             if dqkv2.dtype == torch.bfloat16:
@@ -701,6 +701,102 @@ class RmPad:
     def tokens(self, t):
         """(B, T) per-token tensor (ids, positions) -> (1, nnz)."""
         return t.reshape(-1).index_select(0, self.idx).view(1, -1)
+
+    # adjoints used by the layer backward: pack's is the scatter unpack, unpack's the gather pack (each padded
+    # position holds at most one packed row and vice versa)
+    def unpack_grad(self, x):
+        return self.unpack(x)
+
+    def pack_grad(self, x):
+        return self.pack(x)
+
+
+class PrefixShare(RmPad):
+    """Prefix sharing of one pass's rows: the samples of one prompt (rows with identical input ids and attention mask
+    over the prompt) run the prompt's tokens once. The reference computes every sample's copy
+    (dp_actor.py:119-247); each copy's hidden states are the same function of the same tokens, so the per-token
+    work (embedding, norms, projections, MLP) runs on one of them and the copies only exist in the padded (B, T)
+    layout the attention reads. An RmPad whose packed rows are the distinct tokens:
+
+    * ``idx`` / ``nnz``: the packed tokens — every position except the shared copies (the group's first row, the
+      leader, holds the prompt; the other rows contribute their responses), and except the pads unless
+      ``keep_pads`` (the padded forward's values at pad positions, use_remove_padding False);
+    * ``inv`` (B*T,): the packed row each padded position reads — a shared copy reads its leader's token;
+    * shared positions are the prompt's first P - 1: the last prompt position predicts the first response token
+      and stays each row's own (its gradient is then the row's own, and the predicting rows are distinct).
+
+    unpack (packed -> padded) is the gather through ``inv``; its adjoint, pack_grad, adds the K copies' gradients
+    into the shared row (drl_sum_rows, fp32 in row order: deterministic). pack and its adjoint are RmPad's."""
+
+    @classmethod
+    def build(cls, input_ids, attention_mask, R, keep_pads=False):
+        """The pass's prompt groups, or None when no two rows share a prompt (P - 1 < 1 or all prompts distinct).
+        Two host reads: the rows' prompt hashes and one check that every row equals its leader over the prompt."""
+        B, T = attention_mask.shape
+        S = T - R - 1
+        if B < 2 or S < 1:
+            return None
+        dev = attention_mask.device
+        ids, am = input_ids[:, :S], attention_mask[:, :S]
+        g = torch.Generator(device="cpu").manual_seed(0x5EED)
+        w = torch.randint(1, 1 << 20, (2, S), generator=g, dtype=torch.int64).to(dev)
+        key = torch.stack([(ids.to(torch.int64) * w[0]).sum(-1), (am.to(torch.int64) * w[1]).sum(-1)], 1).cpu()
+        groups = {}
+        for b, k in enumerate(map(tuple, key.tolist())):
+            groups.setdefault(k, []).append(b)
+        members = list(groups.values())
+        if max(len(mm) for mm in members) < 2:
+            return None
+        leader = torch.empty(B, dtype=torch.int64)
+        for mm in members:
+            leader[mm] = mm[0]
+        leader = leader.to(dev)
+        if not bool(((ids == ids[leader]) & (am == am[leader])).all()):  # a hash collision: no sharing
+            return None
+        return cls(attention_mask, S, leader, members, keep_pads)
+
+    def __init__(self, attention_mask, S, leader, members, keep_pads):
+        B, T = attention_mask.shape
+        dev = attention_mask.device
+        self.B, self.T, self.S = B, T, S
+        rows = torch.arange(B, device=dev)
+        copy = (leader != rows)[:, None] & (torch.arange(T, device=dev) < S)[None, :]
+        own = ~copy if keep_pads else (attention_mask.bool() & ~copy)
+        self.idx = torch.nonzero(own.reshape(-1)).reshape(-1).contiguous()
+        self.nnz = int(self.idx.numel())
+        inv_own = torch.full((B * T,), -1, dtype=torch.int64, device=dev)
+        inv_own[self.idx] = torch.arange(self.nnz, dtype=torch.int64, device=dev)
+        inv_own = inv_own.view(B, T)
+        self.inv = torch.where(copy, inv_own[leader], inv_own).reshape(-1).contiguous()
+        self.groups = len(members)
+        # pack_grad: the shared packed rows (leader positions t < S that are packed tokens) and, per group member
+        # slot k, the padded position of member k's copy (-1 past the group's size)
+        shared = [mm for mm in members if len(mm) > 1]
+        K = max(len(mm) for mm in shared)
+        mem = torch.full((len(shared), K), -1, dtype=torch.int64)
+        for gi, mm in enumerate(shared):
+            mem[gi, :len(mm)] = torch.tensor(mm)
+        mem = mem.to(dev)
+        gi, t = torch.nonzero(own[mem[:, 0], :S], as_tuple=True)
+        self.sum_dst = inv_own[mem[gi, 0], t].contiguous()
+        m = mem[gi].t()  # (K, m)
+        self.sum_src = torch.where(m >= 0, m * T + t[None, :], torch.full_like(m, -1)).contiguous()
+
+    def unpack(self, x):
+        """(nnz, C) packed -> (B*T, C): every padded position reads its packed row (shared copies their leader's),
+        zero rows at the pads that hold no packed row."""
+        out = torch.zeros(self.B * self.T, x.shape[1], dtype=x.dtype, device=x.device)
+        return native.copy_rows(x, out, src_idx=self.inv, n=self.B * self.T)
+
+    def unpack_grad(self, x):
+        return RmPad.unpack(self, x)
+
+    def pack_grad(self, x):
+        """Adjoint of unpack: each packed row gets the sum of the gradients of the padded positions that read it."""
+        out = self.pack(x)
+        if self.sum_dst.numel():
+            native.sum_rows(x, self.sum_src, out, self.sum_dst)
+        return out
 
 
 class _GatherRows(torch.autograd.Function):

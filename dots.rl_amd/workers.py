@@ -136,6 +136,9 @@ class ActorRolloutRefWorker(Worker):
         cfg.ref.use_fused_kernels = fused
         # model.use_remove_padding likewise (fsdp_workers.py sets actor / ref use_remove_padding from the model)
         cfg.actor.use_remove_padding = cfg.ref.use_remove_padding = bool(cfg.model.get("use_remove_padding", False))
+        # model.share_prompt_prefix (this repository's): the samples of one prompt run its tokens once in the actor /
+        # ref passes (qwen2.PrefixShare; the rollout's counterpart is rollout.enable_prefix_caching)
+        cfg.actor.share_prompt_prefix = cfg.ref.share_prompt_prefix = bool(cfg.model.get("share_prompt_prefix", True))
         if self._is_actor:
             o = cfg.actor.optim
             betas = tuple(o.get("betas", (0.9, 0.999)))

@@ -593,6 +593,13 @@ void drl_gemm_set_debug(int32_t flags);
  * 16-byte aligned); a negative index skips the row. */
 int drl_copy_rows(const void* src, int64_t ld_src_bytes, const int64_t* src_idx, void* dst, int64_t ld_dst_bytes,
                   const int64_t* dst_idx, int64_t n_rows, int64_t row_bytes, void* stream);
+/* Row sums of prefix sharing (the adjoint of a gather in which K padded positions read one packed row — a prompt
+ * token shared by the samples of one prompt; the reference runs every sample's copy, dp_actor.py:119-247): for
+ * j < m, dst[dst_idx[j] (or j)] = sum over k < K of src[src_idx[k * m + j]] (an index < 0 adds nothing; a
+ * negative dst index skips the row), fp32 accumulation in k order, dt DRL_BF16 or DRL_F32; ld_src / ld_dst in
+ * elements, rows 16-byte aligned, cols a multiple of 16 bytes. */
+int drl_sum_rows(const void* src, int64_t ld_src, const int64_t* src_idx, int64_t K, void* dst, int64_t ld_dst,
+                 const int64_t* dst_idx, int64_t m, int64_t cols, int32_t dt, void* stream);
 
 
 
