@@ -143,14 +143,14 @@ SIGNATURES = {
     "drl_swiglu_fwd": (ctypes.c_int, [P, P, I32, I64, I64, P]),
     "drl_swiglu_bwd": (ctypes.c_int, [P, P, P, I32, I64, I64, P]),
     "drl_decode_attention_workspace_bytes": (SZ, [I64, I64, I64, I64, I64]),
-    "drl_flash_attn_fwd": (ctypes.c_int, [P, P, P, I32, P, I64, I64, I64, I64, I64, I64, I64, I64, I64, I64, F32, P, P,
-                                          P]),
+    "drl_flash_attn_fwd": (ctypes.c_int, [P, P, P, I32, P, I64, I64, I64, I64, I64, I64, I64, I64, I64, I64, P, F32,
+                                          P, P, P]),
     "drl_decode_attention_vt_workspace_bytes": (SZ, [I64, I64, I64, I64]),
     "drl_decode_attention_set_plan": (None, [I32, I32]),
     "drl_decode_attention_vt": (ctypes.c_int, [P, P, P, I32, P, I64, P, I64, I64, I64, I64, I64, I64, I64, I64, I64,
                                                I64, F32, P, I64, P, SZ, P]),
-    "drl_flash_attn_bwd": (ctypes.c_int, [P, P, P, P, P, P, P, I32, P, I64, I64, I64, I64, I64, I64, I64, F32, P, P, P, P,
-                                          P]),
+    "drl_flash_attn_bwd": (ctypes.c_int, [P, P, P, P, P, P, P, I32, P, I64, I64, I64, I64, I64, I64, I64, P, F32, P, P, P,
+                                          P, P]),
     "drl_decode_attention": (ctypes.c_int, [P, P, P, I32, P, I64, P, I64, I64, I64, I64, I64, I64, I64, F32, P, P, SZ,
                                             P]),
     "drl_linear_logprob_workspace_bytes": (SZ, [I64, I64, I64]),

@@ -36,6 +36,9 @@ struct FlashArgs {
   float* lse;     // (B, Hkv, G, Tq) natural-log LSE of the scaled scores, or nullptr
   int64_t Hkv, G, Tq, Tk, ld_k, ld_vt, qoff;
   float scale_log2;  // softmax scale * log2(e)
+  // optional (B,): query tiles wholly below q_start[b] are skipped (their out / lse rows are left unwritten) — the
+  // shared-prompt copies of prefix sharing, whose outputs nothing reads
+  const int32_t* q_start;
 };
 
 __device__ __forceinline__ bf16x8 as_bf16x8(u16x8 v) { return __builtin_bit_cast(bf16x8, v); }
@@ -225,6 +228,7 @@ __global__ __launch_bounds__(512, D == 64 ? 4 : 1) void flash_fwd_kernel(FlashAr
   xcd_tile_order(static_cast<int>(ntiles), static_cast<int>(gridDim.y), tile, bh);
   const int64_t b = bh / a.Hkv;
   const int64_t t0 = (ntiles - 1 - tile) * 32;  // longest causal rows first
+  if (a.q_start && t0 + 32 <= a.q_start[b]) return;  // uniform: a skipped tile
   const int64_t tq = t0 + qi;
   const bool qvalid = computes && tq < a.Tq;
 
@@ -409,6 +413,9 @@ struct FlashBwdArgs {
   uint16_t* dv;  // (B, Hkv, T, D)
   int64_t Hkv, G, T, ld_t;
   float scale, scale_log2;
+  // optional (B,): query tiles wholly below q_start[b] carry no gradient (dO = 0 there): dq is written as zeros,
+  // and the dK / dV key loops start at the first kept tile
+  const int32_t* q_start;
 };
 
 __device__ __forceinline__ float bf2f(uint16_t x) { return bf16_to_f32(x); }
@@ -515,6 +522,14 @@ __global__ __launch_bounds__(512) void flash_dq_kernel(FlashBwdArgs a) {
   const int tq = t0 + qi;
   const bool qvalid = computes && tq < T;
   const int64_t head = bh * a.G + (computes ? g : 0);
+  if (a.q_start && t0 + 32 <= a.q_start[b]) {  // uniform: a skipped tile's dq rows are zero
+    if (qvalid) {
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+        *reinterpret_cast<u16x8*>(a.dq + (head * T + tq) * D + 16 * s + 8 * h) = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+    return;
+  }
   bf16x8 qf[KS], dof[KS];
   float dl = 0.f;
   {
@@ -701,6 +716,8 @@ __global__ __launch_bounds__(64 * NW) void flash_dkdv_kernel(FlashBwdArgs a) {
   xcd_tile_order(ntiles, static_cast<int>(gridDim.y), tile, bh);
   const int64_t b = bh / a.Hkv, hkv = bh % a.Hkv;
   const int k0 = tile * 32;  // key tile 0 has the most query tiles: dispatched first
+  // first query tile of the loop: the causal start k0, or past the skipped tiles (q_start)
+  const int ts = a.q_start ? max(k0, a.q_start[b] & ~31) : k0;
   const int key = k0 + li;
   const bool kin = key < T;
   const bool kval = kin && a.valid[b * a.ld_valid + key] != 0;
@@ -728,16 +745,16 @@ __global__ __launch_bounds__(64 * NW) void flash_dkdv_kernel(FlashBwdArgs a) {
   const float* lser = a.lse + head * a.T;
   const float* dlr = a.delta + head * a.T;
   u16x8 qa[KS], da[KS];
-  dkdv_rows<D>(qbase, a.dout, b, hkv, a.Hkv, a.G, g, T, k0 + li, h, qa, da);
+  if (ts < T) dkdv_rows<D>(qbase, a.dout, b, hkv, a.Hkv, a.G, g, T, ts + li, h, qa, da);
   // lanes 0-31: LSE of query tt + lane, lanes 32-63: its delta (clamped to T - 1; masked where read)
   auto lsd_issue = [&](int tt, int slot) {
     const int q = min(tt + li, T - 1);
     __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)((h ? dlr : lser) + q),
                                      (__attribute__((address_space(3))) void*)&lsd[wv][slot][0], 4, 0, 0);
   };
-  lsd_issue(k0, 0);
-  for (int t0 = k0; t0 < T; t0 += 32) {
-    const int slot = ((t0 - k0) >> 5) & 1;
+  if (ts < T) lsd_issue(ts, 0);
+  for (int t0 = ts; t0 < T; t0 += 32) {
+    const int slot = ((t0 - ts) >> 5) & 1;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this tile's LDS-DMA (and its Q / dO rows) landed
     // this tile's Q and dO rows into the wave's LDS image (row li, head dims 16s + 8h .. + 7); the transposed
     // operands of dV / dK are read back from it after the softmax (no head-dim-major copies in HBM)
@@ -1317,7 +1334,8 @@ extern "C" {
 
 int drl_flash_attn_fwd(const void* q, const void* k, const void* vt, int32_t dt, const uint8_t* key_valid,
                        int64_t ld_valid, int64_t B, int64_t Hkv, int64_t G, int64_t D, int64_t Tq, int64_t Tk,
-                       int64_t ld_k, int64_t ld_vt, int64_t qoff, float scale, void* out, float* lse, void* stream) {
+                       int64_t ld_k, int64_t ld_vt, int64_t qoff, const int32_t* q_start, float scale, void* out,
+                       float* lse, void* stream) {
   using namespace drl;
   DRL_CHECK_ARG(q && k && vt && key_valid && out, "NULL input");
   DRL_CHECK_ARG(dt == DRL_BF16, "flash attention runs on bf16 operands");
@@ -1333,7 +1351,7 @@ int drl_flash_attn_fwd(const void* q, const void* k, const void* vt, int32_t dt,
                 "misaligned operand");
   FlashArgs a{static_cast<const uint16_t*>(q), static_cast<const uint16_t*>(k), static_cast<const uint16_t*>(vt),
               key_valid, ld_valid, static_cast<uint16_t*>(out), lse, Hkv, G, Tq, Tk, ld_k, ld_vt, qoff,
-              scale * 1.4426950408889634f};
+              scale * 1.4426950408889634f, q_start};
   const dim3 grid(static_cast<unsigned>((Tq + 31) / 32), static_cast<unsigned>(B * Hkv));
   const dim3 block(512);  // waves >= G stage K/V only
   hipStream_t s = static_cast<hipStream_t>(stream);
@@ -1345,8 +1363,8 @@ int drl_flash_attn_fwd(const void* q, const void* k, const void* vt, int32_t dt,
 
 int drl_flash_attn_bwd(const void* q, const void* k, const void* kt, const void* v, const void* o, const void* dout,
                        const float* lse, int32_t dt, const uint8_t* key_valid, int64_t ld_valid, int64_t B,
-                       int64_t Hkv, int64_t G, int64_t D, int64_t T, int64_t ld_t, float scale, float* delta, void* dq,
-                       void* dk, void* dv, void* stream) {
+                       int64_t Hkv, int64_t G, int64_t D, int64_t T, int64_t ld_t, const int32_t* q_start, float scale,
+                       float* delta, void* dq, void* dk, void* dv, void* stream) {
   using namespace drl;
   DRL_CHECK_ARG(q && k && kt && v && o && dout && lse && key_valid && delta && dq && dk && dv,
                 "NULL input");
@@ -1358,7 +1376,7 @@ int drl_flash_attn_bwd(const void* q, const void* k, const void* kt, const void*
   FlashBwdArgs a{static_cast<const uint16_t*>(q), static_cast<const uint16_t*>(k), static_cast<const uint16_t*>(kt),
                  static_cast<const uint16_t*>(v), static_cast<const uint16_t*>(o), static_cast<const uint16_t*>(dout),
                  lse, key_valid, ld_valid, delta, static_cast<uint16_t*>(dq), static_cast<uint16_t*>(dk),
-                 static_cast<uint16_t*>(dv), Hkv, G, T, ld_t, scale, scale * 1.4426950408889634f};
+                 static_cast<uint16_t*>(dv), Hkv, G, T, ld_t, scale, scale * 1.4426950408889634f, q_start};
   const dim3 grid(static_cast<unsigned>((T + 31) / 32), static_cast<unsigned>(B * Hkv));
   const dim3 block_dq(512);  // waves >= G only stage K / V / K^T
   const dim3 block_kv(static_cast<unsigned>(64 * (D == 64 ? G : std::min<int64_t>(G, 4))));

@@ -750,34 +750,38 @@ def _vt_cap_ok(vt, cap):
     assert vt.dim() != 5 or vt.shape[2] == (cap + 31) // 32, "key-blocked V^T must hold ceil(K capacity / 32) blocks"
 
 
-def flash_attn_fwd(q, k, vt, key_valid, out, Tk=None, qoff=0, lse=None):
+def flash_attn_fwd(q, k, vt, key_valid, out, Tk=None, qoff=0, lse=None, q_start=None):
     """Fused causal + key-padding attention (MFMA). q (B,Hkv,G,Tq,D) bf16, k (B,Hkv,>=Tk,D) (keys [0,Tk) used),
-    vt (B,Hkv,D,ld) with ld >= Tk a multiple of 8; out (B,Tq,Hkv*G*D); lse optional (B,Hkv,G,Tq) fp32."""
-    _dev(q, k, vt, key_valid, out, lse)
+    vt (B,Hkv,D,ld) with ld >= Tk a multiple of 8; out (B,Tq,Hkv*G*D); lse optional (B,Hkv,G,Tq) fp32;
+    q_start optional (B,) int32: query tiles of row b wholly below q_start[b] skipped (rows left unwritten)."""
+    _dev(q, k, vt, key_valid, out, lse, q_start)
+    assert q_start is None or (q_start.dtype == torch.int32 and q_start.numel() == q.shape[0])
     B, Hkv, G, Tq, D = q.shape
     Tk = k.shape[2] if Tk is None else Tk
     assert q.is_contiguous() and k.is_contiguous() and out.is_contiguous()
     assert key_valid.dtype == torch.uint8 and key_valid.stride(1) == 1
     _vt_cap_ok(vt, k.shape[2])
     check(lib().drl_flash_attn_fwd(_p(q), _p(k), _p(vt), _edt(q), _p(key_valid), key_valid.stride(0), B, Hkv, G, D,
-                                   Tq, Tk, k.shape[2], vt_ld(vt), qoff, 1.0 / math.sqrt(D), _p(out), _p(lse),
-                                   _stream()),
+                                   Tq, Tk, k.shape[2], vt_ld(vt), qoff, _p(q_start), 1.0 / math.sqrt(D), _p(out),
+                                   _p(lse), _stream()),
           "drl_flash_attn_fwd")
     return out
 
 
-def flash_attn_bwd(q, k, kt, v, o, dout, lse, key_valid, dq, dk, dv):
+def flash_attn_bwd(q, k, kt, v, o, dout, lse, key_valid, dq, dk, dv, q_start=None):
     """Backward of flash_attn_fwd (Tq == Tk, qoff 0): q (B,Hkv,G,T,D), k/v (B,Hkv,T,D), kt (B,Hkv,D,ld),
-    o/dout (B,T,Hq*D), lse (B,Hkv,G,T) -> dq (B,Hkv,G,T,D), dk/dv (B,Hkv,T,D)."""
-    _dev(q, k, kt, v, o, dout, lse, key_valid, dq, dk, dv)
+    o/dout (B,T,Hq*D), lse (B,Hkv,G,T) -> dq (B,Hkv,G,T,D), dk/dv (B,Hkv,T,D). q_start as in the forward (dout
+    zero on the skipped tiles)."""
+    _dev(q, k, kt, v, o, dout, lse, key_valid, dq, dk, dv, q_start)
+    assert q_start is None or (q_start.dtype == torch.int32 and q_start.numel() == q.shape[0])
     B, Hkv, G, T, D = q.shape
     assert kt.stride(-1) == 1 and kt.stride(-2) * D == kt.stride(1)
     for t in (q, k, v, o, dout, lse, dq, dk, dv):
         assert t.is_contiguous()
     delta = _ws.get(B * Hkv * G * T * 4, q.device)
     check(lib().drl_flash_attn_bwd(_p(q), _p(k), _p(kt), _p(v), _p(o), _p(dout), _p(lse), _edt(q), _p(key_valid),
-                                   key_valid.stride(0), B, Hkv, G, D, T, kt.stride(-2), 1.0 / math.sqrt(D), _p(delta),
-                                   _p(dq), _p(dk), _p(dv), _stream()),
+                                   key_valid.stride(0), B, Hkv, G, D, T, kt.stride(-2), _p(q_start), 1.0 / math.sqrt(D),
+                                   _p(delta), _p(dq), _p(dk), _p(dv), _stream()),
           "drl_flash_attn_bwd")
 
 

@@ -467,9 +467,10 @@ def _layer_forward(m, i, x_prev, delta, pos, key_valid, save, cache=None, koff=0
         native.rope_qkv_fwd(qkv, pos, m.cos, m.sin, Hq, Hkv, D, q, kbuf, vbuf, kt=kt, vt=vt)
         attn = torch.empty(B, T, Hq * D, dtype=dt, device=dev)
         lse = torch.empty(B, Hkv, G, T, dtype=torch.float32, device=dev)
-        native.flash_attn_fwd(q, kbuf, vt, key_valid, attn, lse=lse)
+        qs = getattr(rm, "q_start", None)
+        native.flash_attn_fwd(q, kbuf, vt, key_valid, attn, lse=lse, q_start=qs)
         del vt
-        save.update(kt=kt, lse=lse, key_valid=key_valid)
+        save.update(kt=kt, lse=lse, key_valid=key_valid, q_start=qs)
         P = "flash"
         return _layer_mlp(m, i, x, _repack(rm, attn, save), save, kbuf, vbuf, P, q, h1, rstd1)
     vt = None
@@ -488,7 +489,7 @@ def _layer_forward(m, i, x_prev, delta, pos, key_valid, save, cache=None, koff=0
     L = koff + T
     if flash:
         attn = torch.empty(B, T, Hq * D, dtype=dt, device=dev)
-        native.flash_attn_fwd(q, kbuf, vt, key_valid, attn, Tk=L, qoff=L - T)
+        native.flash_attn_fwd(q, kbuf, vt, key_valid, attn, Tk=L, qoff=L - T, q_start=getattr(rm, "q_start", None))
         P = None
     elif cache is not None and T == 1:
         # one new token: decode attention streams the cache once (MFMA kernel over V^T for bf16 caches,
@@ -612,7 +613,7 @@ class _DecoderLayer(torch.autograd.Function):
             dk = torch.empty_like(sv["k"])
             dv = torch.empty_like(sv["v"])
             native.flash_attn_bwd(sv["q"], sv["k"], sv["kt"], sv["v"], attn, dattn.view(B, T, Hq * D),
-                                  sv["lse"], sv["key_valid"], dq, dk, dv)
+                                  sv["lse"], sv["key_valid"], dq, dk, dv, q_start=sv["q_start"])
         else:
             dO = dattn.view(B, T, Hkv, G, D).permute(0, 2, 3, 1, 4).reshape(B * Hkv, G * T, D)
             q3 = sv["q"].view(B * Hkv, G * T, D)
@@ -769,6 +770,8 @@ class PrefixShare(RmPad):
         inv_own = inv_own.view(B, T)
         self.inv = torch.where(copy, inv_own[leader], inv_own).reshape(-1).contiguous()
         self.groups = len(members)
+        # the fused attention skips the copies' query tiles (their outputs are never packed, their gradient is 0)
+        self.q_start = torch.where(leader != rows, S, 0).to(torch.int32).contiguous()
         # pack_grad: the shared packed rows (leader positions t < S that are packed tokens) and, per group member
         # slot k, the padded position of member k's copy (-1 past the group's size)
         shared = [mm for mm in members if len(mm) > 1]

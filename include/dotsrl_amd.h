@@ -418,10 +418,13 @@ int drl_decode_attention(const void* q, const void* k_cache, const void* v_cache
  * transposed, ld_vt >= Tk, multiple of 8), key_valid (B, ld_valid) u8 with 4-byte aligned rows.
  * Query t attends to key j iff j <= t + qoff && key_valid[b, j]; out (B,Tq,Hkv*G*D) bf16 (the o_proj
  * input layout). lse (optional, (B,Hkv,G,Tq) fp32) = log sum_j exp(scale * s_tj) over allowed keys.
- * A query row with no allowed key writes zeros and lse = -inf. bf16, head_dim 64 or 128, G <= 8. */
+ * A query row with no allowed key writes zeros and lse = -inf. bf16, head_dim 64 or 128, G <= 8.
+ * q_start (optional, (B,) int32): the 32-query tiles of row b wholly below q_start[b] are skipped and their out /
+ * lse rows left unwritten — the shared-prompt copies under prefix sharing, which nothing reads. */
 int drl_flash_attn_fwd(const void* q, const void* k, const void* vt, int32_t dt, const uint8_t* key_valid,
                        int64_t ld_valid, int64_t B, int64_t Hkv, int64_t G, int64_t D, int64_t Tq, int64_t Tk,
-                       int64_t ld_k, int64_t ld_vt, int64_t qoff, float scale, void* out, float* lse, void* stream);
+                       int64_t ld_k, int64_t ld_vt, int64_t qoff, const int32_t* q_start, float scale, void* out,
+                       float* lse, void* stream);
 /* Decode attention on MFMA over a cache with V head-dim-major: q (B,Hkv,G,D) bf16 (one token), k_cache
  * (B,Hkv,ld_k,D), vt_cache (B,Hkv,D,ld_vt); keys j < L with key_valid[b, j] && j <= qpos (device scalar
  * *qpos_ptr when non-NULL). out (B,Hkv,G,D), or with out_mbt > 0 the (B, Hq*D) panel fragment-packed for
@@ -461,11 +464,13 @@ int drl_decode_attention_vt(const void* q, const void* k_cache, const void* vt_c
  * q (B,Hkv,G,T,D), k / v (B,Hkv,T,D) row-major, kt (B,Hkv,D,ld_t) head-dim-major copy of k (written by
  * drl_rope_qkv_fwd), o and dout (B,T,Hkv*G*D), lse from the forward. delta: (B,Hkv,G,T) fp32 scratch.
  * Outputs dq (B,Hkv,G,T,D), dk / dv (B,Hkv,T,D) bf16 (the drl_rope_qkv_bwd inputs). T and ld_t multiples
- * of 8; head_dim 64. Deterministic (the G heads' dK/dV partials are summed in a fixed order). */
+ * of 8; head_dim 64. Deterministic (the G heads' dK/dV partials are summed in a fixed order). q_start (optional,
+ * (B,) int32, as in the forward): dout is zero on the skipped query tiles — their dq rows are written as zeros and
+ * contribute nothing to dk / dv (not read: o, dout, lse of those rows may hold anything). */
 int drl_flash_attn_bwd(const void* q, const void* k, const void* kt, const void* v, const void* o, const void* dout,
                        const float* lse, int32_t dt, const uint8_t* key_valid, int64_t ld_valid, int64_t B,
-                       int64_t Hkv, int64_t G, int64_t D, int64_t T, int64_t ld_t, float scale, float* delta, void* dq,
-                       void* dk, void* dv, void* stream);
+                       int64_t Hkv, int64_t G, int64_t D, int64_t T, int64_t ld_t, const int32_t* q_start, float scale,
+                       float* delta, void* dq, void* dk, void* dv, void* stream);
 
 /* A21 fused lm_head + log-prob + entropy (MFMA; logits never written). Replaces FusedLinearForPPO.forward
  * (verl/utils/experimental/torch_functional.py:20-37, :153-216) and the Triton linear_cross_entropy forward

@@ -197,3 +197,46 @@ def test_compute_log_prob_independent_of_group_row_order():
     mask = am[:, -resp.shape[1]:].bool()
     for name in out:
         torch.testing.assert_close(out[name][mask], ref[mask], rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("D,G", [(64, 7), (128, 4)])
+def test_flash_q_start_skips_only_the_copies(D, G):
+    """q_start: the skipped query tiles' outputs are never written and nothing of theirs is read — poisoned o / lse
+    rows leave every other output bit-identical to the unskipped kernels, dq of the skipped rows is zero, and dk / dv
+    equal the unskipped backward's with dout zero on those rows (their terms are exact zeros)."""
+    from dots.rl_amd import native
+
+    B, Hkv, T = 4, 2, 160
+    g = torch.Generator(device="cuda").manual_seed(D)
+    q = torch.randn(B, Hkv, G, T, D, device="cuda", generator=g).to(torch.bfloat16)
+    k = torch.randn(B, Hkv, T, D, device="cuda", generator=g).to(torch.bfloat16)
+    v = torch.randn(B, Hkv, T, D, device="cuda", generator=g).to(torch.bfloat16)
+    dout = torch.randn(B, T, Hkv * G * D, device="cuda", generator=g).to(torch.bfloat16)
+    valid = torch.zeros(B, T, dtype=torch.uint8, device="cuda")
+    valid[:, 5:] = 1
+    kt = k.transpose(-1, -2).contiguous()
+    vt = v.transpose(-1, -2).contiguous()
+    qs = torch.tensor([0, 70, 64, 200], dtype=torch.int32, device="cuda")  # tiles below 64 / 64 / all skipped
+    skip = torch.zeros(B, T, dtype=torch.bool, device="cuda")
+    for b, s in enumerate(qs.tolist()):
+        skip[b, : s // 32 * 32] = True
+    dout = torch.where(skip[:, :, None], torch.zeros((), dtype=dout.dtype, device="cuda"), dout)
+    o0 = torch.empty(B, T, Hkv * G * D, dtype=torch.bfloat16, device="cuda")
+    l0 = torch.empty(B, Hkv, G, T, device="cuda")
+    native.flash_attn_fwd(q, k, vt, valid, o0, lse=l0)
+    o1 = torch.full_like(o0, float("nan"))
+    l1 = torch.full_like(l0, float("nan"))
+    native.flash_attn_fwd(q, k, vt, valid, o1, lse=l1, q_start=qs)
+    assert torch.equal(o1[~skip], o0[~skip]) and torch.isnan(o1[skip]).all()
+    lsk = skip[:, None, None, :].expand_as(l0)
+    assert torch.equal(l1[~lsk], l0[~lsk])
+    grads = []
+    for o, lse, kw in ((o0, l0, {}), (o1, l1, {"q_start": qs})):
+        dq = torch.full_like(q, float("nan"))
+        dk, dv = torch.empty_like(k), torch.empty_like(v)
+        native.flash_attn_bwd(q, k, kt, v, o, dout, lse, valid, dq, dk, dv, **kw)
+        grads.append((dq, dk, dv))
+    (dq0, dk0, dv0), (dq1, dk1, dv1) = grads
+    qsk = skip[:, None, None, :, None].expand_as(dq0)
+    assert torch.equal(dq1[~qsk], dq0[~qsk]) and torch.all(dq1[qsk] == 0)
+    assert torch.equal(dk1, dk0) and torch.equal(dv1, dv0)
