@@ -9,6 +9,7 @@
 #   benchfull                   the driver's bench command (python bench.py, CPU baseline included)
 #   benchfused                  the bench with model.use_fused_kernels=True
 #   bench64                     the per-rank workload of N = 8 (64 sequences) ; bench128 / bench256 likewise
+#   benchx:<name>:<k=v>,<k=v>   the bench (5 steps, 2 warmup) with config overrides -> bench_<name>.json
 #   profile                     rocprofv3 kernel stats of a 2-step bench + trace summary
 #   pmc_gemm                    FETCH_SIZE / WRITE_SIZE passes over drl_gemm -> profiles/pmc_drl_gemm.json
 #   ab:<lib>,<lib>,...          drl_gemm A/B over library builds (tools/gemm_ab.sh)
@@ -60,6 +61,11 @@ for step in "$@"; do
         --override actor_rollout_ref.model.use_fused_kernels=True > "$OUT/benchfused.json" 2> "$OUT/benchfused.err" \
         || { tail -20 "$OUT/benchfused.err"; exit 1; }
       cut -c1-900 "$OUT/benchfused.json" ;;
+    benchx:*)
+      IFS=':' read -ra A <<< "$step"; IFS=',' read -ra O <<< "${A[2]}"
+      timeout -k 10 500 python -u bench.py --steps 5 --warmup 2 --no-cpu-baseline --override "${O[@]}" \
+        > "$OUT/bench_${A[1]}.json" 2> "$OUT/bench_${A[1]}.err" || { tail -20 "$OUT/bench_${A[1]}.err"; exit 1; }
+      cut -c1-900 "$OUT/bench_${A[1]}.json" ;;
     bench64) bench_rows 64 || exit 1 ;;
     bench128) bench_rows 128 || exit 1 ;;
     bench256) bench_rows 256 || exit 1 ;;
