@@ -221,19 +221,21 @@ def _concat_rows(group):
             for k in ("input_ids", "attention_mask", "position_ids", "responses")}
 
 
-def exec_groups(cfg, model_cfg, micro_batches):
+def exec_groups(cfg, model_cfg, micro_batches, shared_tokens=0.0):
     """Micro-batches that run through the model in one pass. The reference runs one per forward / backward
     (dp_actor.py:392-466, dp_critic.py:214-250); their gradients only add up (each micro-batch's loss carries its own
     scale factor and token count), so consecutive micro-batches may share one pass over their concatenated rows: the
     GEMMs see 2-4x the rows (at 6144 rows the N = 896 projections fill 96 of 256 CUs). ``exec_micro_batches`` fixes
     the group size (1 = the reference's schedule); 0 groups as many as keep the saved activations under
-    ``exec_activation_gb``."""
+    ``exec_activation_gb``. ``shared_tokens``: the fraction of a micro-batch's tokens that prefix sharing runs once
+    for several rows (they hold no per-token activations of their own; the attention's stay padded)."""
     n = int(cfg.get("exec_micro_batches", 1) or 0)
     if n <= 0:
         H, I, L = model_cfg.hidden_size, model_cfg.intermediate_size, model_cfg.num_hidden_layers
         nq = (model_cfg.num_attention_heads + 2 * model_cfg.num_key_value_heads) * model_cfg.head_dim
-        # saved per token and layer: x, x2 (fp32), h1, h2, attn (bf16), q / k / v / k^T, gate|up and SwiGLU out
-        per_tok = L * (8 * H + 6 * H + 4 * nq + 6 * I)
+        # saved per token and layer: x, x2 (fp32), h1, h2, attn (bf16), gate|up and SwiGLU out per packed token;
+        # q / k / v / k^T (and the padded attention output) per padded position
+        per_tok = L * ((8 * H + 6 * H + 6 * I) * (1.0 - shared_tokens) + 4 * nq)
         budget = float(cfg.get("exec_activation_gb", 110)) * 2 ** 30
         if torch.cuda.is_available():
             # never plan past 40 % of the device — a static bound (not what happens to be free at the call), so the
@@ -311,8 +313,18 @@ class DataParallelPPOActor:
             ent = torch.where(keep, ent, 0.0) if ent is not None else None
         return ent, logp
 
-    def _exec_groups(self, micro_batches):
-        return exec_groups(self.config, self.actor_module.cfg, micro_batches)
+    def _exec_groups(self, micro_batches, mini_batch=None):
+        shared = 0.0
+        if self.share_prompt_prefix and mini_batch is not None and len(mini_batch) > 1:
+            # rows whose prompt equals the previous row's (the trainer's interleaved repeat): their first P - 1
+            # tokens are copies under prefix sharing (one device read per mini-batch)
+            ids = mini_batch.batch["input_ids"]
+            B, T = ids.shape
+            S = T - mini_batch.batch["responses"].shape[1] - 1
+            if S > 0:
+                dup = int((ids[1:, :S] == ids[:-1, :S]).all(-1).sum())
+                shared = dup * S / (B * T)
+        return exec_groups(self.config, self.actor_module.cfg, micro_batches, shared)
 
     def _log_prob_groups(self, micro_batches):
         """Forward-only passes: rows are independent, so consecutive micro-batches run as one pass of at most
@@ -386,7 +398,7 @@ class DataParallelPPOActor:
                     else:
                         rm = mini_batch.batch["response_mask"]
                         counts = rm.reshape(len(micro_batches), -1).sum(-1, dtype=torch.float64)
-                groups = self._exec_groups(micro_batches)
+                groups = self._exec_groups(micro_batches, mini_batch)
                 k = 0
                 for gi, group in enumerate(groups):
                     if gi == len(groups) - 1:  # gradients final after this backward: overlap the all-reduce

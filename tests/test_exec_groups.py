@@ -25,3 +25,8 @@ def test_exec_groups_budget():
     # 24 layers x 46336 B per token x 6144 tokens = 6.8 GB per micro-batch: 110 GB -> 16 per pass
     assert [len(g) for g in exec_groups({"exec_micro_batches": 0, "exec_activation_gb": 110}, cfg, mbs)] == [16, 16]
     assert [len(g) for g in exec_groups({"exec_micro_batches": 0, "exec_activation_gb": 40}, cfg, mbs)] == [6, 6, 5, 5, 5, 5]
+    # prefix sharing: 7 of every 8 rows' first 511 of 768 tokens are copies (58 % of the tokens) -> 529 KB per
+    # padded token: the 32 micro-batches fit one pass
+    shared = 224 * 511 / (256 * 768)
+    assert [len(g) for g in exec_groups({"exec_micro_batches": 0, "exec_activation_gb": 110}, cfg, mbs,
+                                        shared)] == [32]
