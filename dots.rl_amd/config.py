@@ -118,7 +118,8 @@ DEFAULTS = dict(
         fsdp_config=dict(shard="auto", fsdp_size=-1, param_offload=False, optimizer_offload=False),
         optim=dict(lr=1e-5, lr_warmup_steps_ratio=0.0, total_training_steps=-1, weight_decay=0.01, lr_warmup_steps=-1,
                    betas=[0.9, 0.999], eps=1e-8, warmup_style="constant", min_lr_ratio=0.0, num_cycles=0.5),
-        model=dict(path="random:qwen2.5-0.5b", override_config={}, use_remove_padding=False, dtype="bfloat16",
+        model=dict(path="random:qwen2.5-0.5b", override_config={}, use_remove_padding=False, share_prompt_prefix=True,
+                   dtype="bfloat16",
                    gemm_tuning="auto", seed=4321),
         ppo_mini_batch_size=None, ppo_micro_batch_size=None, ppo_micro_batch_size_per_gpu=8,
         forward_micro_batch_size=None, forward_micro_batch_size_per_gpu=16, use_dynamic_bsz=None,

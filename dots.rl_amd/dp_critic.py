@@ -19,7 +19,7 @@ from . import native
 from .dp_actor import FlatAdamW, _concat_rows, append_to_dict, exec_groups
 from .protocol import DataProto
 from .seqlen_balancing import prepare_dynamic_batch, restore_dynamic_batch
-from .qwen2 import Qwen2Model, RmPad, gather_rows
+from .qwen2 import PrefixShare, Qwen2Model, RmPad, gather_rows
 
 
 class _ValueHead(torch.autograd.Function):
@@ -56,6 +56,8 @@ class DataParallelPPOCritic:
         self.critic_module = critic_module
         self.critic_optimizer = critic_optimizer
         self.use_remove_padding = config.model.get("use_remove_padding", False) if "model" in config else False
+        # prefix sharing (qwen2.PrefixShare, as the actor's): a prompt group's prompt tokens run once
+        self.share_prompt_prefix = config.model.get("share_prompt_prefix", True) if "model" in config else True
 
     def _forward_micro_batch(self, micro_batch):
         """dp_critic.py:57-145: values = score(h)[:, -R-1:-1] (compute dtype, (bs, R)); use_remove_padding
@@ -64,8 +66,10 @@ class DataParallelPPOCritic:
         R = micro_batch["responses"].size(-1)
         am = micro_batch["attention_mask"]
         B, T = am.shape
-        if self.use_remove_padding:
-            rm = RmPad(am)
+        share = PrefixShare.build(micro_batch["input_ids"], am, R, keep_pads=not self.use_remove_padding) \
+            if self.share_prompt_prefix else None
+        if share is not None or self.use_remove_padding:
+            rm = share if share is not None else RmPad(am)
             h = m.hidden_states(micro_batch["input_ids"], am, micro_batch["position_ids"], rm=rm)
             sel = rm.inv.view(B, T)[:, T - R - 1:T - 1].reshape(-1).contiguous()
             v = value_head(m, gather_rows(h.view(rm.nnz, h.shape[-1]), sel)).view(B, R)

@@ -240,3 +240,31 @@ def test_flash_q_start_skips_only_the_copies(D, G):
     qsk = skip[:, None, None, :, None].expand_as(dq0)
     assert torch.equal(dq1[~qsk], dq0[~qsk]) and torch.all(dq1[qsk] == 0)
     assert torch.equal(dk1, dk0) and torch.equal(dv1, dv0)
+
+
+def test_fp32_critic_prefix_share_matches_unshared():
+    """The critic's values (dp_critic._forward_micro_batch) and its full gradient after a value loss, with and
+    without prefix sharing, on the reference tiny critic: fp32 rounding."""
+    from test_critic_gpu import _tiny_critic
+
+    from dots.rl_amd.config import to_attr
+    from dots.rl_amd.dp_critic import DataParallelPPOCritic
+
+    cfg, store, model = _tiny_critic()
+    ids, am, pos, resp = _groups(3, 4, 24, 16, cfg.vocab_size, 13)
+    R = resp.shape[1]
+    mask = am[:, -R:].bool()
+    mb = {"input_ids": ids, "attention_mask": am, "position_ids": pos, "responses": resp}
+    target = torch.linspace(-1, 1, R, device="cuda")
+    res = {}
+    for share in (False, True):
+        critic = DataParallelPPOCritic(to_attr({"model": {"share_prompt_prefix": share}}), model)
+        model.training = True
+        store.zero_grad()
+        v = critic._forward_micro_batch(mb)
+        (((v - target) ** 2) * mask).sum().backward()
+        res[share] = (v.detach(), store.grad.detach().clone())
+    (v0, g0), (v1, g1) = res[False], res[True]
+    torch.testing.assert_close(v1, v0, rtol=1e-5, atol=1e-5)
+    rel = ((g1 - g0).norm() / g0.norm()).item()
+    assert rel < 2e-6, rel
