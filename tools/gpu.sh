@@ -12,6 +12,7 @@
 #   benchx:<name>:<k=v>,<k=v>   the bench (5 steps, 2 warmup) with config overrides -> bench_<name>.json
 #   profile                     rocprofv3 kernel stats of a 2-step bench + trace summary
 #   pmc_gemm                    FETCH_SIZE / WRITE_SIZE passes over drl_gemm -> profiles/pmc_drl_gemm.json
+#   pmc_flash                   two SQ counter passes over the fused attention kernels (tools/flash_quick.py)
 #   ab:<lib>,<lib>,...          drl_gemm A/B over library builds (tools/gemm_ab.sh)
 #   py:<script>[:<args>]        python -u <script> <args> (args split on ':')
 set -o pipefail
@@ -84,6 +85,17 @@ for step in "$@"; do
       done
       python3 tools/pmc_traffic.py drl_gemm "$OUT/pmc_FETCH_SIZE" "$OUT/pmc_WRITE_SIZE" || exit 1
       cp profiles/pmc_drl_gemm.json "$OUT/"
+      find "$OUT" -name "*.csv" -size +20M -delete ;;
+    pmc_flash)
+      i=0
+      for pass in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_MFMA" \
+                  "SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_SALU SQ_INSTS_MFMA"; do
+        i=$((i+1))
+        timeout -s KILL 120 rocprofv3 --pmc $pass --kernel-include-regex flash_ -f csv -d "$OUT/fpmc$i" -o p \
+          -- python3 "$ROOT/tools/flash_quick.py" > "$OUT/fpmc$i.log" 2>&1 || { tail -5 "$OUT/fpmc$i.log"; exit 1; }
+      done
+      python3 tools/pmc_sq.py "$OUT/pmc_flash_sq.json" flash_fwd_kernel,flash_dq_kernel,flash_dkdv_kernel \
+        "$OUT/fpmc1" "$OUT/fpmc2" || exit 1
       find "$OUT" -name "*.csv" -size +20M -delete ;;
     ab:*)  # A/B of GEMM builds: ab:<lib1>,<lib2>,...
       IFS=',' read -ra L <<< "${step#ab:}"
