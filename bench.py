@@ -368,7 +368,11 @@ def main():
             "timing_spread_s": {k.split("/", 1)[1]: [min(v), sorted(v)[len(v) // 2], max(v)]
                                 for k in hist[0] if k.startswith("timing_s/")
                                 for v in [[h[k] for h in hist]]},
+            # the reference's perf/mfu/actor (flops_counter.estimate_flops over every row's tokens): with prompt
+            # groups run once (prompt_groups below) the executed FLOPs are fewer than the ones it counts
             "mfu_actor": sum(h.get("perf/mfu/actor", 0.0) for h in hist) / len(hist),
+            "prompt_groups": {"rollout.enable_prefix_caching": bool(ar.rollout.get("enable_prefix_caching", True)),
+                              "model.share_prompt_prefix": bool(ar.model.get("share_prompt_prefix", True))},
             "roofline": roofline,
             "roofline_k1": None,
             "cpu_baseline": None,
