@@ -196,7 +196,21 @@ class RayPPOTrainer:
         count (Karmarkar-Karp, equal-size partitions)."""
         am = batch.batch["attention_mask"]
         seqlens = am.view(am.shape[0], -1).sum(-1).tolist()
-        parts = get_seqlen_balanced_partitions(seqlens, k_partitions=self.n_gpus, equal_size=True)
+        parts = None
+        uid = batch.non_tensor_batch.get("uid")
+        if self.config.actor_rollout_ref.model.get("share_prompt_prefix", True) and uid is not None:
+            # prefix sharing runs a prompt's tokens once per rank that holds its samples: balance whole prompt
+            # groups (same Karmarkar-Karp over the groups' token sums) so each group stays on one rank
+            groups = {}
+            for i, u in enumerate(uid.tolist()):
+                groups.setdefault(u, []).append(i)
+            rows = list(groups.values())
+            if len({len(r) for r in rows}) == 1 and len(rows) % self.n_gpus == 0:
+                gsum = [sum(seqlens[i] for i in r) for r in rows]
+                gparts = get_seqlen_balanced_partitions(gsum, k_partitions=self.n_gpus, equal_size=True)
+                parts = [[i for g in gp for i in rows[g]] for gp in gparts]
+        if parts is None:
+            parts = get_seqlen_balanced_partitions(seqlens, k_partitions=self.n_gpus, equal_size=True)
         batch.reorder(torch.tensor([j for p in parts for j in p], device=am.device))
         metrics.update(log_seqlen_unbalance(seqlens, parts, logging_prefix))
 
