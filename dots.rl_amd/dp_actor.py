@@ -313,26 +313,30 @@ class DataParallelPPOActor:
             ent = torch.where(keep, ent, 0.0) if ent is not None else None
         return ent, logp
 
-    def _exec_groups(self, micro_batches, mini_batch=None):
-        shared = 0.0
-        if self.share_prompt_prefix and mini_batch is not None and len(mini_batch) > 1:
-            # rows whose prompt equals the previous row's (the trainer's interleaved repeat): their first P - 1
-            # tokens are copies under prefix sharing (one device read per mini-batch)
-            ids = mini_batch.batch["input_ids"]
-            B, T = ids.shape
-            S = T - mini_batch.batch["responses"].shape[1] - 1
-            if S > 0:
-                dup = int((ids[1:, :S] == ids[:-1, :S]).all(-1).sum())
-                shared = dup * S / (B * T)
-        return exec_groups(self.config, self.actor_module.cfg, micro_batches, shared)
+    def _shared_fraction(self, data):
+        """Fraction of the batch's tokens that prefix sharing runs once for several rows: the first P - 1 tokens of
+        every row whose prompt equals the previous row's (the trainer's interleaved repeat); one device read."""
+        if not self.share_prompt_prefix or data is None or len(data) < 2:
+            return 0.0
+        ids = data.batch["input_ids"]
+        B, T = ids.shape
+        S = T - data.batch["responses"].shape[1] - 1
+        if S <= 0:
+            return 0.0
+        return int((ids[1:, :S] == ids[:-1, :S]).all(-1).sum()) * S / (B * T)
 
-    def _log_prob_groups(self, micro_batches):
+    def _exec_groups(self, micro_batches, mini_batch=None):
+        return exec_groups(self.config, self.actor_module.cfg, micro_batches, self._shared_fraction(mini_batch))
+
+    def _log_prob_groups(self, micro_batches, data=None):
         """Forward-only passes: rows are independent, so consecutive micro-batches run as one pass of at most
-        ``exec_log_prob_tokens`` tokens (0: one micro-batch per pass, as the reference) — bigger GEMMs, same rows."""
+        ``exec_log_prob_tokens`` tokens (0: one micro-batch per pass, as the reference) — bigger GEMMs, same rows.
+        Tokens prefix sharing runs once per group count once."""
         budget = int(self.config.get("exec_log_prob_tokens", 0) or 0)
         if budget <= 0:
             return [[mb] for mb in micro_batches]
         toks = max(mb.batch["input_ids"].numel() for mb in micro_batches) if micro_batches else 1
+        toks = max(1, int(toks * (1.0 - self._shared_fraction(data))))
         return balanced_groups(micro_batches, max(1, budget // toks))
 
     @torch.no_grad()
@@ -348,7 +352,7 @@ class DataParallelPPOActor:
         else:
             micro_batches = data.split(micro_batch_size)
         lps, ents = [], []
-        for group in self._log_prob_groups(micro_batches):
+        for group in self._log_prob_groups(micro_batches, data if not use_dynamic_bsz else None):
             ent, lp = self._forward_micro_batch(_concat_rows(group), temperature, calculate_entropy)
             lps.append(lp)
             if calculate_entropy:
