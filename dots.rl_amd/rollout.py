@@ -165,7 +165,7 @@ class MI355XRollout:
         B = idx.shape[0]
         if n <= 1 or B % n or not cfg.get("enable_prefix_caching", True) or int(cfg.get("decode_lanes", 1) or 1) > 1:
             return 1
-        same = torch.stack([(t.view(B // n, n, -1) == t.view(B // n, n, -1)[:, :1]).all()
+        same = torch.stack([(t.reshape(B // n, n, -1) == t.reshape(B // n, n, -1)[:, :1]).all()
                             for t in (idx, attention_mask, position_ids)]).all()
         return n if bool(same) else 1
 
