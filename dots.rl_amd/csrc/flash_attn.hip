@@ -1138,9 +1138,10 @@ __global__ __launch_bounds__(64 * NW) void decode_mfma_kernel(DecodeArgs a) {
   const int64_t bs = b / a.group, bhs = bs * a.Hkv + (bh - b * a.Hkv);
   const uint16_t* kbs = a.k + bhs * a.ld_k * D;
   const uint16_t* vtbs = a.vt + bhs * vt_panel(a.ld_vt, D, a.ld_k);
-  const uint8_t* vrows = a.valid + bs * a.ld_valid;
+  // key validity always from the row's own bytes: every row holds its prompt's mask (KVCache.share_prompts), while
+  // a source row p < B / group is itself a sample of prompt p / group and carries THAT prompt's mask
   auto load = [&](int k0, DecRaw<D>& r) {  // a.shared is a multiple of 32: a block is wholly shared or wholly own
-    if (k0 < a.shared) dec_load_raw<D>(kbs, vtbs, vrows, a.ld_vt, a.ld_valid, k0, kend, lane, h, r);
+    if (k0 < a.shared) dec_load_raw<D>(kbs, vtbs, vrow, a.ld_vt, a.ld_valid, k0, kend, lane, h, r);
     else dec_load_raw<D>(kb, vtb, vrow, a.ld_vt, a.ld_valid, k0, kend, lane, h, r);
   };
   // split-K over gridDim.y workgroups: split y takes 32-key blocks [y*n/S, (y+1)*n/S) of the n live blocks;

@@ -40,6 +40,15 @@ def resolve_model_config(model_cfg) -> Qwen2Config:
         with open(os.path.join(path, "config.json")) as f:
             base = json.load(f)
     base.update(over)
+    if path.startswith("random:"):
+        # a random preset whose vocabulary the override shrank has no tokenizer behind it: its preset special ids
+        # (Qwen2.5: 151643 / 151645) are past the rows, so the last row is its EOS (and, below, its pad)
+        V = int(base.get("vocab_size", 0))
+        for key in ("eos_token_id", "pad_token_id", "bos_token_id"):
+            ids = base.get(key)
+            if key not in over and ids is not None and any(
+                    i >= V for i in (ids if isinstance(ids, (list, tuple)) else [ids])):
+                base[key] = V - 1 if key != "pad_token_id" else None
     # tokenizer.py:21-33 (set_pad_token_id): no pad id -> the eos id (the first one of a list); Meta-Llama-3-8B's
     # config.json has none, and the Qwen default (151643) is past its 128256-row vocabulary
     eos = base.get("eos_token_id")

@@ -48,14 +48,14 @@ def test_decode_attention_prompt_groups_equal_expanded(B, group, Hkv, G, D, cap,
     k[:, :, :shared] = k[src, :, :shared]
     vt[..., :shared] = vt[src][..., :shared]
     valid[:, :shared] = valid[src, :shared]
-    # the grouped cache: prompt p's keys only in row p, garbage in every other row's prompt region
+    # the grouped cache: prompt p's keys only in row p, garbage in every other row's prompt region; the key-valid
+    # bytes are every row's own (KVCache.share_prompts copies the mask to each row: row p < Bu is itself a sample
+    # of prompt p // group and carries that prompt's mask, not prompt p's)
     kg, vtg, vg = k.clone(), vt.clone(), valid.clone()
     kg[:, :, :shared] = torch.randn(B, Hkv, shared, D, device=DEV, generator=g).to(BF)
     vtg[..., :shared] = torch.randn(B, Hkv, D, shared, device=DEV, generator=g).to(BF)
-    vg[:, :shared] = 1
     kg[:Bu, :, :shared] = k[::group, :, :shared]
     vtg[:Bu, ..., :shared] = vt[::group, ..., :shared]
-    vg[:Bu, :shared] = valid[::group, :shared]
     vb, vbg = _blocked(vt, cap), _blocked(vtg, cap)
     qp = torch.tensor([L - 3], device=DEV)
     for kw in ({}, {"qpos_dev": qp}):
