@@ -1312,6 +1312,134 @@ __global__ __launch_bounds__(64 * NW) void decode_mfma_kernel(DecodeArgs a) {
   }
 }
 
+// Prompt groups on one workgroup: the rows p * group + r of one prompt read the same shared key blocks, so a
+// workgroup takes the query columns of 32 / G of them at once (G query heads each: 4 rows x 7 heads for Qwen2.5)
+// and each shared block is loaded ONCE for those rows (the per-row kernel loads it once per row, from L2 after the
+// first). Workgroup = (prompt p, KV head, column tile of 32 / G rows); its NW waves take the key blocks of residue
+// class w mod NW exactly as decode_mfma_kernel<D, NW> does per row: first the shared blocks (all columns), then
+// each row's own blocks of that class (only that row's columns take part: every other lane sees its keys as
+// invalid, and an all-invalid block is an exact no-op on the running state: alpha = 1, p = 0). Every column
+// therefore runs the per-row kernel's arithmetic in the per-row kernel's order — MFMA columns are independent,
+// the softmax is lane-local per column — and the result is bit-identical to decode_mfma_kernel<D, NW> on a cache
+// where every row holds its own copy of the prompt keys. Contract: the rows of a group have identical key-valid
+// bytes below `shared` (the rollout's KVCache.share_prompts copies them); the shared blocks' validity is read from
+// the group's first row. One block in flight per wave (the register-lean loop).
+template <int D, int NW>
+__global__ __launch_bounds__(64 * NW) void decode_group_kernel(DecodeArgs a) {
+  constexpr int KS = D / 16, MT = D / 32;
+  __shared__ float s_m[NW][32], s_l[NW][32];
+  __shared__ __attribute__((aligned(16))) float s_o[NW][MT][16][64];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int qi = lane & 31, h = lane >> 5;
+  const int G = static_cast<int>(a.G), group = static_cast<int>(a.group);
+  const int rpt = 32 / G, ntile = (group + rpt - 1) / rpt;
+  const int64_t units = gridDim.x / ntile;
+  int64_t unit, ct;
+  if (units % 8 == 0) {  // the column tiles of one (prompt, head) on one XCD, back to back
+    const int64_t slot = blockIdx.x >> 3;
+    ct = slot % ntile;
+    unit = (slot / ntile) * 8 + (blockIdx.x & 7);
+  } else {
+    unit = blockIdx.x / ntile;
+    ct = blockIdx.x % ntile;
+  }
+  const int64_t p = unit / a.Hkv, hd = unit - p * a.Hkv;
+  const int nr = min(rpt, group - static_cast<int>(ct) * rpt);  // rows of this tile
+  const int rl = qi / G, g = qi - rl * G;                         // this lane's column: local row, query head
+  const bool col_ok = rl < nr;
+  const int64_t b0 = p * group + ct * rpt;                        // first row of the tile
+  const int64_t bcol = b0 + (col_ok ? rl : 0);
+  const int qpos = static_cast<int>(a.qpos_ptr ? *a.qpos_ptr : a.qpos);
+  const int kend = static_cast<int>(min(a.L, static_cast<int64_t>(qpos) + 1));
+  const int64_t panel = vt_panel(a.ld_vt, D, a.ld_k);
+  const uint16_t* kbs = a.k + (p * a.Hkv + hd) * a.ld_k * D;     // shared keys: cache row p
+  const uint16_t* vtbs = a.vt + (p * a.Hkv + hd) * panel;
+  const uint8_t* vrows = a.valid + p * group * a.ld_valid;        // the group's first row's mask
+  const int nall = (kend + 31) / 32, nsh = min(static_cast<int>(a.shared / 32), nall);
+  const int n_sh = nsh > w ? (nsh - w + NW - 1) / NW : 0;         // shared blocks of class w
+  const int own0 = nsh + ((w - nsh) % NW + NW) % NW;              // first own block of class w
+  const int n_own = nall > own0 ? (nall - own0 + NW - 1) / NW : 0;
+  const int items = n_sh + nr * n_own;
+  // item j -> block index, source row (-1: shared) ; loads through the per-row kernel's raw loader
+  auto load = [&](int j, DecRaw<D>& r) {
+    if (j < n_sh) {
+      dec_load_raw<D>(kbs, vtbs, vrows, a.ld_vt, a.ld_valid, 32 * (w + j * NW), kend, lane, h, r);
+    } else {
+      const int jj = j - n_sh, rr = jj / n_own, ib = own0 + (jj - rr * n_own) * NW;
+      const int64_t bh = (b0 + rr) * a.Hkv + hd;
+      dec_load_raw<D>(a.k + bh * a.ld_k * D, a.vt + bh * panel, a.valid + (b0 + rr) * a.ld_valid, a.ld_vt,
+                      a.ld_valid, 32 * ib, kend, lane, h, r);
+    }
+  };
+  DecRaw<D> R0, R1;  // two items in flight per wave (named registers: static indexing)
+  uint16_t* kslot = reinterpret_cast<uint16_t*>(&s_o[w][0][0][0]);
+  uint16_t* vslot = kslot + 32 * D;
+  if (items > 0) load(0, R0);
+  if (items > 1) load(1, R1);
+  bf16x8 qf[KS];
+  {
+    const uint16_t* qrow = a.q + ((bcol * a.Hkv + hd) * a.G + g) * D + 8 * h;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      u16x8 v = *reinterpret_cast<const u16x8*>(qrow + 16 * s);
+      if (!col_ok) v = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      qf[s] = as_bf16x8(v);
+    }
+  }
+  f32x16 o[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) o[mt] = f32x16{};
+  float m = -INFINITY, lsum = 0.f;
+  // stage item j to the wave's slot, refill its registers with item j + 2, then the online-softmax step from LDS
+  auto step = [&](int j, DecRaw<D>& R) {
+    dec_stage<D>(R, kslot, vslot, lane);
+    // an own block takes part only in its row's columns
+    const bool act = j < n_sh || (j - n_sh) / n_own == rl;
+    const uint32_t vb[4] = {act ? R.vb[0] : 0u, act ? R.vb[1] : 0u, act ? R.vb[2] : 0u, act ? R.vb[3] : 0u};
+    if (j + 2 < items) load(j + 2, R);
+    dec_block_lds<D>(kslot, vslot, vb, qf, a.scale_log2, qi, h, m, lsum, o);
+  };
+  for (int j = 0; j < items; j += 2) {
+    step(j, R0);
+    if (j + 1 < items) step(j + 1, R1);
+  }
+  // merge the NW waves' states per column in wave order (decode_mfma_kernel's non-split merge)
+  const float lt = lsum + __shfl_xor(lsum, 32, kWave);
+  if (h == 0) { s_m[w][qi] = m; s_l[w][qi] = lt; }
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s_o[w][mt][r][lane] = o[mt][r];
+  __syncthreads();
+  if (!col_ok) return;
+  float mm = -INFINITY;
+#pragma unroll
+  for (int v = 0; v < NW; ++v) mm = fmaxf(mm, s_m[v][qi]);
+  const float mref = mm == -INFINITY ? 0.f : mm;
+  float sc[NW], ll = 0.f;
+#pragma unroll
+  for (int v = 0; v < NW; ++v) {
+    sc[v] = __builtin_amdgcn_exp2f(s_m[v][qi] - mref);
+    ll += s_l[v][qi] * sc[v];
+  }
+  const float inv = ll > 0.f ? 1.f / ll : 0.f;
+  const int64_t bh = bcol * a.Hkv + hd;
+  const int64_t kq = (hd * a.G + g) * D;  // column of (b, query head) in (Hq * D)
+  for (int gg = w; gg < 4 * MT; gg += NW) {
+    const int mt = gg >> 2, c = gg & 3;
+    u16x4 wv;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float acc = 0.f;
+#pragma unroll
+      for (int v = 0; v < NW; ++v) acc = fmaf(s_o[v][mt][4 * c + j][lane], sc[v], acc);
+      wv[j] = to_bf16_bits(acc * inv);
+    }
+    const int64_t k = kq + 32 * mt + 8 * c + 4 * h;
+    *reinterpret_cast<u16x4*>(dec_out_ptr(a, bcol, k, (bh * a.G + g) * D + 32 * mt + 8 * c + 4 * h)) = wv;
+  }
+}
+
 }  // namespace
 
 int g_dec_nw = 0, g_dec_splits = 0;  // tuning override (drl_decode_attention_set_plan), 0 = automatic
@@ -1434,6 +1562,28 @@ int drl_decode_attention_vt(const void* q, const void* k_cache, const void* vt_c
                scale * 1.4426950408889634f, static_cast<uint16_t*>(out), out_mbt, nullptr, nullptr, group,
                shared_keys};
   hipStream_t s = static_cast<hipStream_t>(stream);
+  if (group > 1 && shared_keys > 0) {
+    // prompt groups: one workgroup per (prompt, KV head, column tile of 32 / G rows), each shared block loaded once
+    // per tile (decode_group_kernel); bit-identical to the per-row kernel at the same wave count without splits.
+    // 8 waves (D = 64; 4 at D = 128) so a workgroup's key blocks are spread over as many in-flight loads as the
+    // per-row 8-wave plan (profiles/r04_decode_group.jsonl)
+    const int rpt = static_cast<int>(32 / G), ntile = static_cast<int>((group + rpt - 1) / rpt);
+    const int nwg = g_dec_nw ? g_dec_nw : (D == 64 ? 8 : 4);
+    DRL_CHECK_ARG(D == 64 ? (nwg == 2 || nwg == 4 || nwg == 8 || nwg == 16) : (nwg == 2 || nwg == 4),
+                  "prompt-group decode attention: %d waves at head_dim %lld", nwg, (long long)D);
+    const dim3 g_(static_cast<unsigned>(B / group * Hkv * ntile)), b_(64 * nwg);
+    if (D == 64) {
+      if (nwg == 2) hipLaunchKernelGGL((decode_group_kernel<64, 2>), g_, b_, 0, s, a);
+      else if (nwg == 4) hipLaunchKernelGGL((decode_group_kernel<64, 4>), g_, b_, 0, s, a);
+      else if (nwg == 8) hipLaunchKernelGGL((decode_group_kernel<64, 8>), g_, b_, 0, s, a);
+      else hipLaunchKernelGGL((decode_group_kernel<64, 16>), g_, b_, 0, s, a);
+    } else {
+      if (nwg == 2) hipLaunchKernelGGL((decode_group_kernel<128, 2>), g_, b_, 0, s, a);
+      else hipLaunchKernelGGL((decode_group_kernel<128, 4>), g_, b_, 0, s, a);
+    }
+    DRL_LAUNCH_CHECK();
+    return DRL_OK;
+  }
   const int64_t wgs = B * Hkv, cus = cu_count();
   const int splits = decode_splits(B, Hkv, L);
   // waves per workgroup and key-loop variant (tools/kernel_bench.py --only decode_sweep): 8 waves with two

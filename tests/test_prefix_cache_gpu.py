@@ -58,11 +58,24 @@ def test_decode_attention_prompt_groups_equal_expanded(B, group, Hkv, G, D, cap,
     vtg[:Bu, ..., :shared] = vt[::group, ..., :shared]
     vb, vbg = _blocked(vt, cap), _blocked(vtg, cap)
     qp = torch.tensor([L - 3], device=DEV)
-    for kw in ({}, {"qpos_dev": qp}):
-        a = native.decode_attention_vt(q, k, vb, valid[:, :cap], L, torch.empty_like(q), **kw)
-        b = native.decode_attention_vt(q, kg, vbg, vg[:, :cap], L, torch.empty_like(q), group=group,
-                                       shared_keys=shared, **kw)
-        assert torch.equal(a, b)
+    lib = native.lib()
+    # the grouped kernel (decode_group_kernel) runs the per-row kernel's arithmetic at its wave count without key
+    # splits: 8 waves at head_dim 64, 4 at 128 by default; forced plans apply to both
+    try:
+        for nw in ((0, 2, 4, 16) if D == 64 else (0, 2)):
+            for kw in ({}, {"qpos_dev": qp}):
+                lib.drl_decode_attention_set_plan(nw or (8 if D == 64 else 4), 1)
+                a = native.decode_attention_vt(q, k, vb, valid[:, :cap], L, torch.empty_like(q), **kw)
+                lib.drl_decode_attention_set_plan(nw, 0)
+                b = native.decode_attention_vt(q, kg, vbg, vg[:, :cap], L, torch.empty_like(q), group=group,
+                                               shared_keys=shared, **kw)
+                assert torch.equal(a, b), (nw, kw)
+    finally:
+        lib.drl_decode_attention_set_plan(0, 0)
+    # and close to the per-row kernel's own default plan (another wave count / key split: another fp32 order)
+    a = native.decode_attention_vt(q, k, vb, valid[:, :cap], L, torch.empty_like(q))
+    b = native.decode_attention_vt(q, kg, vbg, vg[:, :cap], L, torch.empty_like(q), group=group, shared_keys=shared)
+    torch.testing.assert_close(a.float(), b.float(), rtol=2e-2, atol=2e-2)
 
 
 def test_decode_attention_prompt_groups_rejects_bad_args():
