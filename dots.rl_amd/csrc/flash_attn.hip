@@ -937,16 +937,19 @@ struct DecRaw {
   u16x8 k[D / 16];
   u16x8 v[D / 16];
   uint32_t vb[4];
+  int k0;  // first key of the block
 };
 
+// Every load is a whole 16 B at an in-bounds address (rows clamped to kend - 1, V^T columns to the row). The
+// positions >= kend of a tail block are zeroed by dec_fix_tail when the block is consumed, not here: a select on
+// the loaded registers right after the load made the wave wait for it (and every load before it) at issue time,
+// which cost the prefetch of every tail block (most decode steps end in a partial block).
 template <int D>
 __device__ __forceinline__ void dec_load_raw(const uint16_t* kb, const uint16_t* vtb, const uint8_t* vrow,
                                              int64_t ld_vt, int64_t ld_valid, int k0, int kend, int lane, int h,
                                              DecRaw<D>& r) {
   constexpr int UPR = D / 8;  // 16-B units per K row
-  // every load is a whole 16 B at an in-bounds address (rows clamped to kend - 1, V^T columns to the row);
-  // positions >= kend are zeroed after the load, so the tail block costs no extra memory round trip
-  const bool tail = k0 + 32 > kend;
+  r.k0 = k0;
 #pragma unroll
   for (int i = 0; i < D / 16; ++i) {
     const int c = lane + 64 * i;
@@ -956,24 +959,36 @@ __device__ __forceinline__ void dec_load_raw(const uint16_t* kb, const uint16_t*
     r.v[i] = *reinterpret_cast<const u16x8*>(
         vtb + (ld_vt == DRL_VT_BLOCKED ? vt_index(c >> 2, kk, ld_vt, D)
                                        : static_cast<int64_t>(c >> 2) * ld_vt + min(static_cast<int64_t>(kk), ld_vt - 8)));
-    if (tail) {
-      if (key >= kend) r.k[i] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (kk + j >= kend) r.v[i][j] = 0;
-    }
   }
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
     const int kk = k0 + 8 * c + 4 * h;
-    uint32_t v = *reinterpret_cast<const uint32_t*>(vrow + min(static_cast<int64_t>(kk), ld_valid - 4));
-    if (tail) {
-      uint32_t keep = 0;
+    r.vb[c] = *reinterpret_cast<const uint32_t*>(vrow + min(static_cast<int64_t>(kk), ld_valid - 4));
+  }
+}
+
+// the tail block's positions >= kend: K rows and V^T columns zeroed, key-valid bytes cleared (a no-op elsewhere)
+template <int D>
+__device__ __forceinline__ void dec_fix_tail(DecRaw<D>& r, int kend, int64_t ld_valid, int lane, int h) {
+  constexpr int UPR = D / 8;
+  const int k0 = r.k0;
+  if (k0 + 32 <= kend) return;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) keep |= (kk + j < kend ? 0xffu : 0u) << (8 * j);
-      v = kk + 3 < ld_valid ? (v & keep) : 0u;
-    }
-    r.vb[c] = v;
+  for (int i = 0; i < D / 16; ++i) {
+    const int c = lane + 64 * i;
+    if (k0 + c / UPR >= kend) r.k[i] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    const int kk = k0 + 8 * (c & 3);
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (kk + j >= kend) r.v[i][j] = 0;
+  }
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int kk = k0 + 8 * c + 4 * h;
+    uint32_t keep = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) keep |= (kk + j < kend ? 0xffu : 0u) << (8 * j);
+    r.vb[c] = kk + 3 < ld_valid ? (r.vb[c] & keep) : 0u;
   }
 }
 
@@ -1174,6 +1189,7 @@ __global__ __launch_bounds__(64 * NW) void decode_mfma_kernel(DecodeArgs a) {
   if constexpr (LEAN) {
     // one block in flight per wave: stage it to the slot, issue the next, compute from LDS
     for (int ib = ib0; ib < nblk; ib += NW) {
+      dec_fix_tail<D>(R[0], kend, a.ld_valid, lane, h);
       dec_stage<D>(R[0], kslot, vslot, lane);
       const uint32_t vb[4] = {R[0].vb[0], R[0].vb[1], R[0].vb[2], R[0].vb[3]};
       if (ib + NW < nblk) load(32 * (ib + NW), R[0]);
@@ -1187,6 +1203,7 @@ __global__ __launch_bounds__(64 * NW) void decode_mfma_kernel(DecodeArgs a) {
       const int ibj = ib + j * NW;
       if (ibj < nblk) {
         DecBlock<D> blk;
+        dec_fix_tail<D>(R[j], kend, a.ld_valid, lane, h);
         dec_reshape<D>(R[j], kslot, vslot, lane, qi, h, blk);
         if (ibj + NB * NW < nblk) load(32 * (ibj + NB * NW), R[j]);
         dec_block<D>(blk, qf, a.scale_log2, m, lsum, o);
@@ -1392,6 +1409,7 @@ __global__ __launch_bounds__(64 * NW) void decode_group_kernel(DecodeArgs a) {
   float m = -INFINITY, lsum = 0.f;
   // stage item j to the wave's slot, refill its registers with item j + 2, then the online-softmax step from LDS
   auto step = [&](int j, DecRaw<D>& R) {
+    dec_fix_tail<D>(R, kend, a.ld_valid, lane, h);
     dec_stage<D>(R, kslot, vslot, lane);
     // an own block takes part only in its row's columns
     const bool act = j < n_sh || (j - n_sh) / n_own == rl;
@@ -1562,12 +1580,14 @@ int drl_decode_attention_vt(const void* q, const void* k_cache, const void* vt_c
                scale * 1.4426950408889634f, static_cast<uint16_t*>(out), out_mbt, nullptr, nullptr, group,
                shared_keys};
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (group > 1 && shared_keys > 0) {
+  const int rpt = static_cast<int>(32 / G), ntile = static_cast<int>((group + rpt - 1) / rpt);
+  if (group > 1 && shared_keys > 0 && B / group * Hkv * ntile * 2 >= cu_count()) {
     // prompt groups: one workgroup per (prompt, KV head, column tile of 32 / G rows), each shared block loaded once
     // per tile (decode_group_kernel); bit-identical to the per-row kernel at the same wave count without splits.
     // 8 waves (D = 64; 4 at D = 128) so a workgroup's key blocks are spread over as many in-flight loads as the
-    // per-row 8-wave plan (profiles/r04_decode_group.jsonl)
-    const int rpt = static_cast<int>(32 / G), ntile = static_cast<int>((group + rpt - 1) / rpt);
+    // per-row 8-wave plan (profiles/r04_decode_group.jsonl: 512 rows, 640 keys: 14.9 us against 25.1 for the
+    // per-row kernel reading the prompt rows). Below half a workgroup per CU (64 rows: 32 workgroups) the per-row
+    // kernel's one workgroup per (row, KV head) keeps more of the chip busy: 0.304 vs 0.331 s per 64-row rollout
     const int nwg = g_dec_nw ? g_dec_nw : (D == 64 ? 8 : 4);
     DRL_CHECK_ARG(D == 64 ? (nwg == 2 || nwg == 4 || nwg == 8 || nwg == 16) : (nwg == 2 || nwg == 4),
                   "prompt-group decode attention: %d waves at head_dim %lld", nwg, (long long)D);

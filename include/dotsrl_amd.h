@@ -455,7 +455,11 @@ void drl_decode_attention_set_variant(int32_t variant);
  * group > 1, sequences b = p * group + r share one prompt, and keys j < shared_keys (a multiple of 32, <= L) are
  * read from cache row p — K and V^T — where the rollout prefilled each distinct prompt once; keys j >= shared_keys
  * from row b. key_valid is always row b's own (every row holds its prompt's mask: row p < B / group is itself a
- * sample of prompt p / group). group 1 and shared_keys 0: every row reads its own keys. */
+ * sample of prompt p / group). group 1 and shared_keys 0: every row reads its own keys. With at least half a
+ * workgroup per CU of (prompt, KV head, 32 / G rows) tiles, one workgroup takes a tile's rows together and loads each
+ * shared block once for them; its result equals the per-row kernel's at the same wave count without key splits
+ * (8 waves at head_dim 64, 4 at 128; drl_decode_attention_set_plan forces both). Contract: the rows of a group have
+ * identical key_valid bytes below shared_keys (the rollout copies the prompt's mask to every row). */
 int drl_decode_attention_vt(const void* q, const void* k_cache, const void* vt_cache, int32_t dt,
                             const uint8_t* key_valid, int64_t ld_valid, const int64_t* qpos_ptr, int64_t qpos,
                             int64_t B, int64_t Hkv, int64_t G, int64_t D, int64_t ld_k, int64_t ld_vt, int64_t L,

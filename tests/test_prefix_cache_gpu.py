@@ -99,21 +99,26 @@ def _model(dtype, seed=4):
     return Qwen2Model(cfg, store)
 
 
-@pytest.mark.parametrize("dtype,P,do_sample", [(BF, 40, False), (BF, 40, True), (BF, 64, True),
-                                                (torch.float32, 40, True)])
-def test_rollout_prefix_caching_equals_prefill_per_row(dtype, P, do_sample):
+@pytest.mark.parametrize("dtype,P,do_sample,nprompt", [(BF, 40, False, 5), (BF, 40, True, 5), (BF, 64, True, 5),
+                                                        (torch.float32, 40, True, 5), (BF, 40, True, 128)])
+def test_rollout_prefix_caching_equals_prefill_per_row(dtype, P, do_sample, nprompt):
+    """128 prompts x 8 (1024 rows, one KV head): 128 prompt workgroups, so the grouped decode attention runs
+    decode_group_kernel; both rollouts at its 8-wave plan without key splits (the per-row kernel would take 2 waves
+    at 1024 rows: another fp32 summation order)."""
     from dots.rl_amd.config import to_attr
     from dots.rl_amd.protocol import DataProto
     from dots.rl_amd.rollout import MI355XRollout
 
     m = _model(dtype)
-    n, nprompt, R = 8, 5, 20
+    n, R = 8, 20
+    if nprompt > 5:
+        native.lib().drl_decode_attention_set_plan(8, 1)
     g = torch.Generator(device=DEV).manual_seed(P)
     ids = torch.randint(3, 512, (nprompt, P), device=DEV, generator=g)
     am = torch.ones(nprompt, P, dtype=torch.int64, device=DEV)
     for p in range(nprompt):
-        am[p, : 3 * p] = 0
-        ids[p, : 3 * p] = 0
+        am[p, : 3 * (p % 5)] = 0
+        ids[p, : 3 * (p % 5)] = 0
     pos = (am.cumsum(-1) - 1).clamp_min(0)
     rep = lambda t: t.repeat_interleave(n, 0)  # noqa: E731  (the trainer's repeat(n, interleave=True))
     outs = []
@@ -127,6 +132,7 @@ def test_rollout_prefix_caching_equals_prefill_per_row(dtype, P, do_sample):
             meta_info={"eos_token_id": 2, "pad_token_id": 0}))
         assert ro.last_prompt_group == (n if share else 1)
         outs.append(out.batch)
+    native.lib().drl_decode_attention_set_plan(0, 0)
     for key in ("responses", "input_ids", "attention_mask", "position_ids"):
         assert torch.equal(outs[0][key], outs[1][key]), key
     if do_sample:  # the group's samples differ from each other (each row its own Philox stream)

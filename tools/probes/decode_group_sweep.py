@@ -69,28 +69,49 @@ for L in (P + 32, P + 128, P + 256):
             print(json.dumps(dict(L=L, waves=w, variant=v, splits=s, error=str(e)[:120])), flush=True)
 lib.drl_decode_attention_set_plan(0, 0)
 lib.drl_decode_attention_set_variant(0)
-# the rollout's form: query position in device memory, cache length argument = capacity, packed output for the
-# o_proj GEMM (out_mbt = 16 token blocks), the query position sweeping 512..767 as the response grows
-qd = torch.zeros(1, dtype=torch.int64, device=DEV)
+# the rollout's form, taken apart: (b) host query position sweeping 512..767 with the capacity as the length
+# argument; (c) the position in device memory rewritten before each call (a fill kernel in the loop); (d) the
+# position in device memory, fixed; packed output for the o_proj GEMM in (c) / (d) as in the rollout
+qd = torch.full((1,), P + 127, dtype=torch.int64, device=DEV)
 outp = torch.empty(16 * 32 * Hkv * G * D, dtype=BF, device=DEV)
-for packed in (False, True):
-    i = [0]
 
-    def call():
-        k, vt = caches[i[0] % ncopy]
-        qd.fill_(P + (i[0] * 37) % R)
-        i[0] += 1
-        native.decode_attention_vt(q, k, vt, valid, cap, outp if packed else torch.empty_like(q), qpos_dev=qd,
-                                   out_mbt=16 if packed else 0, group=group, shared_keys=P)
 
+def timed(call, n=64):
     for _ in range(3):
         call()
     torch.cuda.synchronize()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record()
-    for _ in range(64):
+    for _ in range(n):
         call()
     b.record()
     b.synchronize()
-    print(json.dumps(dict(form="rollout", packed=packed, us_incl_fill=round(a.elapsed_time(b) * 1e3 / 64, 2))),
-          flush=True)
+    return round(a.elapsed_time(b) * 1e3 / n, 2)
+
+
+ctr = [0]
+
+
+def form(kind):
+    def call():
+        k, vt = caches[ctr[0] % ncopy]
+        ctr[0] += 1
+        if kind == "b":
+            native.decode_attention_vt(q, k, vt, valid, cap, torch.empty_like(q), qpos=P + (ctr[0] * 37) % R,
+                                       group=group, shared_keys=P)
+        elif kind == "c":
+            qd.fill_(P + (ctr[0] * 37) % R)
+            native.decode_attention_vt(q, k, vt, valid, cap, outp, qpos_dev=qd, out_mbt=16, group=group,
+                                       shared_keys=P)
+        elif kind == "fill":
+            qd.fill_(P + (ctr[0] * 37) % R)
+        else:
+            native.decode_attention_vt(q, k, vt, valid, cap, outp, qpos_dev=qd, out_mbt=16, group=group,
+                                       shared_keys=P)
+    return call
+
+
+for kind in ("b", "c", "d", "fill"):
+    print(json.dumps(dict(form=kind, us=timed(form(kind)))), flush=True)
+qd.fill_(P + 127)
+print(json.dumps(dict(form="d_L640", us=timed(form("d")))), flush=True)
