@@ -659,53 +659,27 @@ __global__ __launch_bounds__(512) void flash_dq_kernel(FlashBwdArgs a) {
   }
 }
 
-// dkdv_rows for a tile wholly below T (uniform test by the caller): no per-row range selects
-template <int D>
-__device__ __forceinline__ void dkdv_rows_full(const uint16_t* qbase, const uint16_t* dout, int64_t b, int64_t hkv,
-                                               int64_t Hkv, int64_t G, int g, int T, int tr, int h,
-                                               u16x8 (&qa)[D / 16], u16x8 (&da)[D / 16]) {
-  const uint16_t* qrow = qbase + static_cast<int64_t>(tr) * D + 8 * h;
-  const uint16_t* dorow = dout + (((b * T + tr) * Hkv + hkv) * G + g) * D + 8 * h;
-#pragma unroll
-  for (int s = 0; s < D / 16; ++s) {
-    qa[s] = *reinterpret_cast<const u16x8*>(qrow + 16 * s);
-    da[s] = *reinterpret_cast<const u16x8*>(dorow + 16 * s);
-  }
-}
-
-template <int D>
-__device__ __forceinline__ void dkdv_rows(const uint16_t* qbase, const uint16_t* dout, int64_t b, int64_t hkv,
-                                          int64_t Hkv, int64_t G, int g, int T, int tr, int h, u16x8 (&qa)[D / 16],
-                                          u16x8 (&da)[D / 16]) {
-  const bool rin = tr < T;
-  const uint16_t* qrow = qbase + static_cast<int64_t>(rin ? tr : 0) * D + 8 * h;
-  const uint16_t* dorow = dout + (((b * T + (rin ? tr : 0)) * Hkv + hkv) * G + g) * D + 8 * h;
-#pragma unroll
-  for (int s = 0; s < D / 16; ++s) {
-    qa[s] = *reinterpret_cast<const u16x8*>(qrow + 16 * s);
-    da[s] = *reinterpret_cast<const u16x8*>(dorow + 16 * s);
-    if (!rin) qa[s] = da[s] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-  }
-}
-
 // NW waves per workgroup; wave w handles query heads w, w + NW, ... of the KV head (its dK / dV partials
 // accumulate over them in registers). head_dim 64: NW = 8 (one head per wave, G <= 8); head_dim 128: NW = 4,
 // one wave per SIMD, so the 128 accumulator registers of dK^T / dV^T and the Q / dO rows fit without spilling.
 template <int D, int NW>
 __global__ __launch_bounds__(64 * NW) void flash_dkdv_kernel(FlashBwdArgs a) {
   constexpr int KS = D / 16, MT = D / 32, KROW = D + 8;
-  // per-wave swizzled image of the current query tile's Q and dO rows (ximg_off); after the key loop the same
-  // LDS holds the cross-wave dK / dV reduction
+  // per wave, two buffers of the swizzled image (ximg_off) of a query tile's Q and dO rows, filled two tiles ahead
+  // by LDS-DMA (global_load_lds of whole 16-B units, the swizzle applied on the source address: a wave instruction
+  // writes 1 KB lane-linearly); after the key loop the same LDS holds every wave's dK / dV partial for the
+  // cross-wave reduction
   constexpr int XROW = D;
+  constexpr int UPR = D / 8, RPI = 64 / UPR;  // 16-B units per row, rows per wave instruction
+  constexpr int NDMA = 2 * (32 / RPI) + 1;    // LDS-DMA instructions per query tile: Q, dO rows + LSE / delta
+  constexpr int PW = 2 * MT * 16 * 64;        // floats of one wave's dK^T + dV^T partial
+  constexpr int XW_ELEMS = NW * 4 * 32 * XROW > NW * PW * 2 ? NW * 4 * 32 * XROW : NW * PW * 2;
   static_assert(D == 64 || D == 128, "head_dim 64 or 128");
-  static_assert(2 * MT * 16 * 64 * 4 <= NW * 2 * 32 * XROW * 2, "reduction buffer must fit the image space");
   __shared__ __attribute__((aligned(16))) uint16_t kv_lds[2][32 * KROW];  // this key tile's K and V rows
-  __shared__ __attribute__((aligned(16))) uint16_t xw[NW][2][32 * XROW];   // [wave][Q / dO][position][d]
-  // per wave, two slots of [LSE of the tile's 32 queries | their delta], filled one query tile ahead by LDS-DMA
-  // (one 4-byte global_load_lds per tile): the softmax's row statistics no longer wait on a global load per tile
+  __shared__ __attribute__((aligned(16))) uint16_t xw_raw[XW_ELEMS];     // [wave][buffer][Q / dO][position][d]
+  auto xw = reinterpret_cast<uint16_t (*)[2][2][32 * XROW]>(xw_raw);
+  // per wave, two slots of [LSE of the tile's 32 queries | their delta], one per image buffer
   __shared__ __attribute__((aligned(16))) float lsd[NW][2][64];
-  // [dk/dv][tile][register][lane]: conflict-free per register; aliases xw after the loop
-  auto red = reinterpret_cast<float (*)[MT][16][64]>(&xw[0][0][0]);
   const int tid = threadIdx.x;
   const int lane = tid & 63, wv = tid >> 6;
   const int li = lane & 31, h = lane >> 5;
@@ -721,6 +695,43 @@ __global__ __launch_bounds__(64 * NW) void flash_dkdv_kernel(FlashBwdArgs a) {
   const int key = k0 + li;
   const bool kin = key < T;
   const bool kval = kin && a.valid[b * a.ld_valid + key] != 0;
+  // NW = 8 >= G: the block has exactly G waves, one head each (a one-trip loop the compiler folds)
+  const int g_end = NW >= 8 ? wv + 1 : static_cast<int>(a.G);
+  // query tile tt of head g into image buffer `buf`: rows tt .. tt + 31 of Q and dO (rows past T read row T - 1:
+  // finite values whose probabilities the LSE mask zeroes) and the rows' LSE (lanes 0-31) / delta (lanes 32-63)
+  // The copies are inline asm: hipcc's own global_load_lds makes it wait for every LDS-DMA in flight (vmcnt(0))
+  // before the next read of ANY of this kernel's LDS, which would drain the prefetch at each iteration's first
+  // read; the asm copies are invisible to it, and the loop counts them itself (vmcnt(NDMA) / vmcnt(0)).
+  const uint32_t lds_x = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(
+      (__attribute__((address_space(3))) uint16_t*)xw_raw));
+  const uint32_t lds_l = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(
+      (__attribute__((address_space(3))) float*)&lsd[0][0][0]));
+  auto tile_issue = [&](int g, int tt, int buf) {
+    const int64_t head = bh * a.G + g;
+    const uint16_t* qbase = a.q + head * a.T * D;
+    const uint32_t xb = lds_x + 2 * static_cast<uint32_t>(((wv * 2 + buf) * 2) * 32 * XROW);
+#pragma unroll
+    for (int i = 0; i < 32 / RPI; ++i) {
+      const int r = i * RPI + lane / UPR, u = (lane % UPR) ^ xsw(r);
+      const int64_t tr = min(tt + r, T - 1);
+      const uint16_t* srcq = qbase + tr * D + 8 * u;
+      const uint16_t* srcd = a.dout + (((b * T + tr) * a.Hkv + hkv) * a.G + g) * D + 8 * u;
+      const uint32_t dq_ = __builtin_amdgcn_readfirstlane(xb + 2 * i * RPI * XROW);
+      const uint32_t dd_ = __builtin_amdgcn_readfirstlane(xb + 2 * (32 * XROW + i * RPI * XROW));
+      asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" :: "v"(srcq), "s"(dq_) : "memory", "m0");
+      asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" :: "v"(srcd), "s"(dd_) : "memory", "m0");
+    }
+    const int q = min(tt + li, T - 1);
+    const float* srcl = (h ? a.delta : a.lse) + head * a.T + q;
+    const uint32_t dl_ = __builtin_amdgcn_readfirstlane(lds_l + 4 * static_cast<uint32_t>((wv * 2 + buf) * 64));
+    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dword %0, off" :: "v"(srcl), "s"(dl_) : "memory", "m0");
+  };
+  // the first head's first two query tiles are issued before the K / V staging, so the workgroup's opening memory
+  // round trips overlap (the staging barrier waits for all of them)
+  if (wv < g_end && ts < T) {
+    tile_issue(wv, ts, 0);
+    if (ts + 32 < T) tile_issue(wv, ts + 32, 1);
+  }
   // stage the key tile's K and V rows once; every wave (query head) reads them from LDS
   for (int c = tid; c < 2 * 32 * (D / 8); c += blockDim.x) {
     const int which = c / (32 * (D / 8)), cc = c % (32 * (D / 8)), row = cc / (D / 8), col = cc % (D / 8);
@@ -735,41 +746,33 @@ __global__ __launch_bounds__(64 * NW) void flash_dkdv_kernel(FlashBwdArgs a) {
   f32x16 dkt[MT], dvt[MT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) dkt[mt] = dvt[mt] = f32x16{};
-  uint16_t* xq = xw[wv][0];
-  uint16_t* xd = xw[wv][1];
-  // NW = 8 >= G: the block has exactly G waves, one head each (a one-trip loop the compiler folds)
-  const int g_end = NW >= 8 ? wv + 1 : static_cast<int>(a.G);
   for (int g = wv; g < g_end; g += NW) {
-  const int64_t head = bh * a.G + g;
-  const uint16_t* qbase = a.q + head * a.T * D;
-  const float* lser = a.lse + head * a.T;
-  const float* dlr = a.delta + head * a.T;
-  u16x8 qa[KS], da[KS];
-  if (ts < T) dkdv_rows<D>(qbase, a.dout, b, hkv, a.Hkv, a.G, g, T, ts + li, h, qa, da);
-  // lanes 0-31: LSE of query tt + lane, lanes 32-63: its delta (clamped to T - 1; masked where read)
-  auto lsd_issue = [&](int tt, int slot) {
-    const int q = min(tt + li, T - 1);
-    __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)((h ? dlr : lser) + q),
-                                     (__attribute__((address_space(3))) void*)&lsd[wv][slot][0], 4, 0, 0);
-  };
-  if (ts < T) lsd_issue(ts, 0);
+  if (g != wv && ts < T) {  // a later head of this wave (NW < G): its first two tiles now
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the previous head's reads of both buffers are done
+    tile_issue(g, ts, 0);
+    if (ts + 32 < T) tile_issue(g, ts + 32, 1);
+  }
   for (int t0 = ts; t0 < T; t0 += 32) {
-    const int slot = ((t0 - ts) >> 5) & 1;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this tile's LDS-DMA (and its Q / dO rows) landed
-    // this tile's Q and dO rows into the wave's LDS image (row li, head dims 16s + 8h .. + 7); the transposed
-    // operands of dV / dK are read back from it after the softmax (no head-dim-major copies in HBM)
+    const int buf = ((t0 - ts) >> 5) & 1;
+    const uint16_t* xq = xw[wv][buf][0];
+    const uint16_t* xd = xw[wv][buf][1];
+    // this tile's LDS-DMA landed; the next tile's (issued one iteration earlier) stays in flight
+    if (t0 + 32 < T) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NDMA) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    u16x8 qa[KS], da[KS];
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
-      *reinterpret_cast<u16x8*>(xq + ximg_off<XROW>(li, 16 * s + 8 * h)) = qa[s];
-      *reinterpret_cast<u16x8*>(xd + ximg_off<XROW>(li, 16 * s + 8 * h)) = da[s];
+      qa[s] = *reinterpret_cast<const u16x8*>(xq + ximg_off<XROW>(li, 16 * s + 8 * h));
+      da[s] = *reinterpret_cast<const u16x8*>(xd + ximg_off<XROW>(li, 16 * s + 8 * h));
     }
     float4 l4[4], d4[4];
     const bool rows_in = t0 + 32 <= T;  // uniform
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       const int qb = t0 + 8 * c + 4 * h;
-      l4[c] = *reinterpret_cast<const float4*>(&lsd[wv][slot][8 * c + 4 * h]);
-      d4[c] = *reinterpret_cast<const float4*>(&lsd[wv][slot][32 + 8 * c + 4 * h]);
+      l4[c] = *reinterpret_cast<const float4*>(&lsd[wv][buf][8 * c + 4 * h]);
+      d4[c] = *reinterpret_cast<const float4*>(&lsd[wv][buf][32 + 8 * c + 4 * h]);
       if (!rows_in) {
         l4[c] = make_float4(qb < T ? l4[c].x : -INFINITY, qb + 1 < T ? l4[c].y : -INFINITY,
                             qb + 2 < T ? l4[c].z : -INFINITY, qb + 3 < T ? l4[c].w : -INFINITY);
@@ -786,10 +789,6 @@ __global__ __launch_bounds__(64 * NW) void flash_dkdv_kernel(FlashBwdArgs a) {
       sc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(qa[s]), as_bf16x8(kv), sc, 0, 0, 0);
       dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(da[s]), as_bf16x8(vv), dp, 0, 0, 0);
     }
-    if (t0 + 64 <= T) dkdv_rows_full<D>(qbase, a.dout, b, hkv, a.Hkv, a.G, g, T, t0 + 32 + li, h, qa, da);
-    else if (t0 + 32 < T) dkdv_rows<D>(qbase, a.dout, b, hkv, a.Hkv, a.G, g, T, t0 + 32 + li, h, qa, da);  // next tile
-    // the next tile's LSE / delta into the other slot (its last reader, the previous tile, consumed it above)
-    if (t0 + 32 < T) lsd_issue(t0 + 32, slot ^ 1);
     u16x8 pb[2], dsb[2];
     // block entirely at or below the diagonal, all keys valid, all queries in range: no mask, and every query
     // row has an allowed key (finite LSE)
@@ -835,41 +834,43 @@ __global__ __launch_bounds__(64 * NW) void flash_dkdv_kernel(FlashBwdArgs a) {
         dkt[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(qtv), as_bf16x8(dsb[s]), dkt[mt], 0, 0, 0);
       }
     }
+    // refill this buffer with the tile two ahead once this wave's reads of it (and of its LSE slot) are done
+    if (t0 + 64 < T) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      tile_issue(g, t0 + 64, buf);
+    }
   }
   }  // query heads of this wave
-  // sum the waves' partials in LDS in wave order (deterministic), wave 0 writes; the buffer overlays the
-  // Q / dO images, so every wave must be past its key loop first
+  // every wave's partial into its own LDS slot (the buffer overlays the Q / dO images, so every wave must be past its
+  // key loop first), ONE barrier, then all threads sum 4-element groups over the waves in wave order — the additions
+  // (0 + p0) + p1 + ... of a wave-by-wave reduction, so the result is unchanged — and store them
   __syncthreads();
   const int nw = a.G < NW ? static_cast<int>(a.G) : NW;
-  for (int w = 0; w < nw; ++w) {
-    if (wv == w) {
+  float* part = reinterpret_cast<float*>(xw_raw);  // [wave][dk / dv][tile][register][lane]
+  if (wv < nw) {
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
+    for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          red[0][mt][r][lane] = (w == 0 ? 0.f : red[0][mt][r][lane]) + dkt[mt][r];
-          red[1][mt][r][lane] = (w == 0 ? 0.f : red[1][mt][r][lane]) + dvt[mt][r];
-        }
+      for (int r = 0; r < 16; ++r) {
+        part[wv * PW + (mt * 16 + r) * 64 + lane] = dkt[mt][r];
+        part[wv * PW + ((MT + mt) * 16 + r) * 64 + lane] = dvt[mt][r];
       }
-    }
-    __syncthreads();
   }
-  if (wv != 0 || !kin) return;
-  uint16_t* dkrow = a.dk + (bh * a.T + key) * D;
-  uint16_t* dvrow = a.dv + (bh * a.T + key) * D;
+  __syncthreads();
+  for (int gi = tid; gi < 2 * MT * 4 * 64; gi += blockDim.x) {
+    const int ln = gi & 63, c = (gi >> 6) & 3, mt = (gi >> 8) % MT, which = (gi >> 8) / MT;
+    const int kk = k0 + (ln & 31);
+    if (kk >= T) continue;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int w = 0; w < nw; ++w) {
 #pragma unroll
-  for (int mt = 0; mt < MT; ++mt) {
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      u16x4 wk, wv;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        wk[j] = to_bf16_bits(red[0][mt][4 * c + j][lane] * a.scale);
-        wv[j] = to_bf16_bits(red[1][mt][4 * c + j][lane]);
-      }
-      *reinterpret_cast<u16x4*>(dkrow + 32 * mt + 8 * c + 4 * h) = wk;
-      *reinterpret_cast<u16x4*>(dvrow + 32 * mt + 8 * c + 4 * h) = wv;
+      for (int j = 0; j < 4; ++j) acc[j] += part[w * PW + ((which * MT + mt) * 16 + 4 * c + j) * 64 + ln];
     }
+    u16x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = to_bf16_bits(which ? acc[j] : acc[j] * a.scale);
+    *reinterpret_cast<u16x4*>((which ? a.dv : a.dk) + (bh * a.T + kk) * D + 32 * mt + 8 * c + 4 * (ln >> 5)) = o;
   }
 }
 
