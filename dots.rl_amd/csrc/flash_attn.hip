@@ -333,11 +333,16 @@ __global__ __launch_bounds__(512, D == 64 ? 4 : 1) void flash_fwd_kernel(FlashAr
   // words travel with them
   u16x8 stage[2][TL::CPT];
   uint32_t vst[2] = {0u, 0u};
+  // the first two blocks: both issued before either is stored (one memory round trip, not two)
 #pragma unroll
   for (int sl = 0; sl < 2; ++sl)
     if (sl < nb) {
       kv_issue<D>(kbase, vtbase, a.ld_vt, sl * 32, a.Tk, tid, stage[sl]);
       vst[sl] = valid_issue(vrow, sl * 32, a.Tk, tid);
+    }
+#pragma unroll
+  for (int sl = 0; sl < 2; ++sl)
+    if (sl < nb) {
       kv_store<D>(lds_k[0][sl], lds_v[0][sl], tid, stage[sl]);
       if (tid < 8) lds_vw[0][sl][tid] = vst[sl];
     }
