@@ -466,23 +466,23 @@ __device__ __forceinline__ void dq_issue(const uint16_t* kb, const uint16_t* vb,
   }
 }
 
-// dq_issue for a block wholly below T (uniform test on k0 by the caller): no per-key bounds tests
+// dq_issue for a block wholly below T (uniform test on k0 by the caller): no per-key bounds tests, and branch-free —
+// every thread issues every one of its loads (a chunk index past the tile re-reads a row-major chunk that dq_store
+// discards), the source chosen by an address select. A load under a per-thread branch into a register initialised
+// to zero made hipcc wait for ALL loads in flight (vmcnt(0)) before each of them, serialising the two-ahead prefetch
+// into one memory round trip per chunk.
 template <int D>
 __device__ __forceinline__ void dq_issue_full(const uint16_t* kb, const uint16_t* vb, const uint16_t* ktb,
                                               int64_t ld_t, int k0, int tid, u16x8 (&r)[DqTile<D>::CPT]) {
   using TL = DqTile<D>;
 #pragma unroll
   for (int i = 0; i < TL::CPT; ++i) {
-    const int c = tid + 512 * i;
-    u16x8 v = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-    if (c < 2 * TL::RCH) {
-      const int cc = c % TL::RCH, row = cc / (D / 8), col = cc % (D / 8);
-      v = *reinterpret_cast<const u16x8*>((c < TL::RCH ? kb : vb) + static_cast<int64_t>(k0 + row) * D + col * 8);
-    } else if (c < TL::NCH) {
-      const int cc = c - 2 * TL::RCH, d = cc / 4, col = cc % 4;
-      v = *reinterpret_cast<const u16x8*>(ktb + static_cast<int64_t>(d) * ld_t + k0 + col * 8);
-    }
-    r[i] = v;
+    const int c0 = tid + 512 * i, c = c0 < TL::NCH ? c0 : c0 % (2 * TL::RCH);
+    const int cc = c % TL::RCH, row = cc / (D / 8), col = cc % (D / 8);
+    const uint16_t* rm = (c < TL::RCH ? kb : vb) + static_cast<int64_t>(k0 + row) * D + col * 8;
+    const int ct = c - 2 * TL::RCH, d = ct / 4, colt = ct % 4;
+    const uint16_t* tm = ktb + static_cast<int64_t>(d) * ld_t + k0 + colt * 8;
+    r[i] = *reinterpret_cast<const u16x8*>(c < 2 * TL::RCH ? rm : tm);
   }
 }
 
@@ -573,7 +573,7 @@ __global__ __launch_bounds__(512) void flash_dq_kernel(FlashBwdArgs a) {
     const int kk = j * 32;
     if (kk + 32 <= T) {
       dq_issue_full<D>(kbase, vbase, ktbase, a.ld_t, kk, tid, stage[set]);
-      if (tid < 8) vst[set] = *reinterpret_cast<const uint32_t*>(vrow + kk + 4 * tid);
+      vst[set] = *reinterpret_cast<const uint32_t*>(vrow + kk + 4 * (tid & 7));  // every thread: no branch
     } else {
       dq_issue<D>(kbase, vbase, ktbase, a.ld_t, kk, T, tid, stage[set]);
       vst[set] = valid_issue(vrow, kk, T, tid);
@@ -584,8 +584,11 @@ __global__ __launch_bounds__(512) void flash_dq_kernel(FlashBwdArgs a) {
   dq_store<D>(lds_k[0], lds_v[0], lds_kt[0], tid, stage[0]);
   if (tid < 8) lds_vw[0][tid] = vst[0];
   __syncthreads();
-  for (int ib = 0; ib < nb; ++ib) {
-    const int cur = ib & 1, k0 = ib * 32;
+  // one key block; cur (the LDS buffer and register set parity) is a literal at both call sites, so each parity is
+  // straight-line code with its own register set (a runtime parity branch let hipcc reuse one set's registers as
+  // temporaries in the other path, behind a vmcnt(0) that drained the two-ahead prefetch)
+  auto step = [&](const int ib, const int cur) __attribute__((always_inline)) {
+    const int k0 = ib * 32;
     // block ib + 2 into the register set block ib left (stored to LDS in the previous iteration)
     if (ib + 2 < nb) {
       if (cur == 0) issue_blk(ib + 2, 0);
@@ -650,6 +653,10 @@ __global__ __launch_bounds__(512) void flash_dq_kernel(FlashBwdArgs a) {
       }
     }
     __syncthreads();
+  };
+  for (int ib = 0; ib < nb; ib += 2) {
+    step(ib, 0);
+    if (ib + 1 < nb) step(ib + 1, 1);
   }
   if (!qvalid) return;
   uint16_t* dqrow = a.dq + (head * T + tq) * D;
@@ -706,7 +713,8 @@ __global__ __launch_bounds__(64 * NW) void flash_dkdv_kernel(FlashBwdArgs a) {
   // finite values whose probabilities the LSE mask zeroes) and the rows' LSE (lanes 0-31) / delta (lanes 32-63)
   // The copies are inline asm: hipcc's own global_load_lds makes it wait for every LDS-DMA in flight (vmcnt(0))
   // before the next read of ANY of this kernel's LDS, which would drain the prefetch at each iteration's first
-  // read; the asm copies are invisible to it, and the loop counts them itself (vmcnt(NDMA) / vmcnt(0)).
+  // read; the asm copies are invisible to it, and the loop counts them itself (vmcnt(NDMA) / vmcnt(0)). m0 is not
+  // declared clobbered (a reserved register: hipcc sets it itself before each of its own uses).
   const uint32_t lds_x = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(
       (__attribute__((address_space(3))) uint16_t*)xw_raw));
   const uint32_t lds_l = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(
@@ -723,13 +731,13 @@ __global__ __launch_bounds__(64 * NW) void flash_dkdv_kernel(FlashBwdArgs a) {
       const uint16_t* srcd = a.dout + (((b * T + tr) * a.Hkv + hkv) * a.G + g) * D + 8 * u;
       const uint32_t dq_ = __builtin_amdgcn_readfirstlane(xb + 2 * i * RPI * XROW);
       const uint32_t dd_ = __builtin_amdgcn_readfirstlane(xb + 2 * (32 * XROW + i * RPI * XROW));
-      asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" :: "v"(srcq), "s"(dq_) : "memory", "m0");
-      asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" :: "v"(srcd), "s"(dd_) : "memory", "m0");
+      asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" :: "v"(srcq), "s"(dq_) : "memory");
+      asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" :: "v"(srcd), "s"(dd_) : "memory");
     }
     const int q = min(tt + li, T - 1);
     const float* srcl = (h ? a.delta : a.lse) + head * a.T + q;
     const uint32_t dl_ = __builtin_amdgcn_readfirstlane(lds_l + 4 * static_cast<uint32_t>((wv * 2 + buf) * 64));
-    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dword %0, off" :: "v"(srcl), "s"(dl_) : "memory", "m0");
+    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dword %0, off" :: "v"(srcl), "s"(dl_) : "memory");
   };
   // the first head's first two query tiles are issued before the K / V staging, so the workgroup's opening memory
   // round trips overlap (the staging barrier waits for all of them)
