@@ -92,7 +92,7 @@ F32 = ctypes.c_float
 SZ = ctypes.c_size_t
 
 # name -> (restype, argtypes); must match include/dotsrl_amd.h exactly
-ABI_VERSION = 5  # include/dotsrl_amd.h DRL_ABI_VERSION: the layouts below (PPOLossParams) are of this version
+ABI_VERSION = 6  # include/dotsrl_amd.h DRL_ABI_VERSION: the layouts below (PPOLossParams) are of this version
 
 SIGNATURES = {
     "drl_last_error": (ctypes.c_char_p, []),
@@ -166,6 +166,7 @@ SIGNATURES = {
     "drl_gemm_set_sk_tuning": (None, [I32, I32, I32, I32]),
     "drl_gemm_set_debug": (None, [I32]),
     "drl_copy_rows": (ctypes.c_int, [P, I64, P, P, I64, P, I64, I64, P]),
+    "drl_gather_rows": (ctypes.c_int, [P, I64, P, P, I64, I64, I64, P]),
     "drl_sum_rows": (ctypes.c_int, [P, I64, P, I64, P, I64, P, I64, I64, I32, P]),
     "drl_colsum_bf16_workspace_bytes": (SZ, [I64, I64]),
     "drl_colsum_bf16_acc": (ctypes.c_int, [P, I64, I64, I64, P, P, SZ, P]),

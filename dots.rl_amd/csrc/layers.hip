@@ -638,14 +638,18 @@ __global__ __launch_bounds__(256) void add_rmsnorm_fwd_vec_kernel(const float* x
   const int lane = threadIdx.x & 63;
   if (row >= N) return;
   float2 v[K];
+  uint32_t d[K];
+  // every load of the row issued before the first use (a null test on delta inside the loop made hipcc wait for
+  // all loads in flight before each delta load: K dependent round trips per row)
 #pragma unroll
-  for (int k = 0; k < K; ++k) {
-    const int64_t j = row * H + 2 * lane + 128 * k;
-    v[k] = *reinterpret_cast<const float2*>(x_in + j);
-    if (delta) {
-      const uint32_t d = *reinterpret_cast<const uint32_t*>(delta + j);
-      v[k].x += bf16_to_f32(static_cast<uint16_t>(d & 0xffffu));
-      v[k].y += bf16_to_f32(static_cast<uint16_t>(d >> 16));
+  for (int k = 0; k < K; ++k) v[k] = *reinterpret_cast<const float2*>(x_in + row * H + 2 * lane + 128 * k);
+  if (delta) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) d[k] = *reinterpret_cast<const uint32_t*>(delta + row * H + 2 * lane + 128 * k);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      v[k].x += bf16_to_f32(static_cast<uint16_t>(d[k] & 0xffffu));
+      v[k].y += bf16_to_f32(static_cast<uint16_t>(d[k] >> 16));
     }
   }
   float ss = 0.f;

@@ -816,6 +816,20 @@ def copy_rows(src, dst, src_idx=None, dst_idx=None, n=None):
     return dst
 
 
+def gather_rows_zero(src, dst, src_idx):
+    """dst[i] = src[src_idx[i]] for every row i of dst, a zero row where src_idx[i] < 0 (csrc/rows.hip,
+    drl_gather_rows): pad_input's zero pad rows written by the gather itself, so ``dst`` may be uninitialised."""
+    _dev(src, dst, src_idx)
+    assert src.dim() == 2 and dst.dim() == 2 and src.stride(1) == 1 and dst.stride(1) == 1
+    assert src.dtype == dst.dtype and src.shape[1] == dst.shape[1]
+    n = dst.shape[0]
+    assert src_idx.dtype == torch.int64 and src_idx.is_contiguous() and src_idx.numel() >= n
+    es = src.element_size()
+    check(lib().drl_gather_rows(_p(src), src.stride(0) * es, _p(src_idx), _p(dst), dst.stride(0) * es, n,
+                                src.shape[1] * es, _stream()), "drl_gather_rows")
+    return dst
+
+
 def sum_rows(src, src_idx, dst, dst_idx=None):
     """dst[dst_idx[j]] = sum_k src[src_idx[k, j]] for src_idx (K, m) (entries < 0 add nothing), fp32 accumulation in
     k order (csrc/rows.hip): the gradient of a packed row read by several padded positions (prefix sharing)."""

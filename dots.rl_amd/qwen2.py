@@ -695,9 +695,10 @@ class RmPad:
         return native.copy_rows(x, out, src_idx=self.idx)
 
     def unpack(self, x):
-        """(nnz, C) packed rows -> (B*T, C) with zero rows at the pads (pad_input)."""
-        out = torch.zeros(self.B * self.T, x.shape[1], dtype=x.dtype, device=x.device)
-        return native.copy_rows(x, out, dst_idx=self.idx)
+        """(nnz, C) packed rows -> (B*T, C) with zero rows at the pads (pad_input): a gather through ``inv`` that
+        writes the pad rows' zeros itself (no memset of the padded buffer)."""
+        out = torch.empty(self.B * self.T, x.shape[1], dtype=x.dtype, device=x.device)
+        return native.gather_rows_zero(x, out, self.inv)
 
     def tokens(self, t):
         """(B, T) per-token tensor (ids, positions) -> (1, nnz)."""
@@ -767,6 +768,7 @@ class PrefixShare(RmPad):
         self.nnz = int(self.idx.numel())
         inv_own = torch.full((B * T,), -1, dtype=torch.int64, device=dev)
         inv_own[self.idx] = torch.arange(self.nnz, dtype=torch.int64, device=dev)
+        self.inv_own = inv_own  # each packed row at its own padded position only (unpack_grad)
         inv_own = inv_own.view(B, T)
         self.inv = torch.where(copy, inv_own[leader], inv_own).reshape(-1).contiguous()
         self.groups = len(members)
@@ -788,11 +790,14 @@ class PrefixShare(RmPad):
     def unpack(self, x):
         """(nnz, C) packed -> (B*T, C): every padded position reads its packed row (shared copies their leader's),
         zero rows at the pads that hold no packed row."""
-        out = torch.zeros(self.B * self.T, x.shape[1], dtype=x.dtype, device=x.device)
-        return native.copy_rows(x, out, src_idx=self.inv, n=self.B * self.T)
+        out = torch.empty(self.B * self.T, x.shape[1], dtype=x.dtype, device=x.device)
+        return native.gather_rows_zero(x, out, self.inv)
 
     def unpack_grad(self, x):
-        return RmPad.unpack(self, x)
+        """RmPad's unpack (the adjoint of pack): each packed row to its own padded position, zeros elsewhere —
+        including the shared copies' positions."""
+        out = torch.empty(self.B * self.T, x.shape[1], dtype=x.dtype, device=x.device)
+        return native.gather_rows_zero(x, out, self.inv_own)
 
     def pack_grad(self, x):
         """Adjoint of unpack: each packed row gets the sum of the gradients of the padded positions that read it."""
@@ -809,8 +814,8 @@ class _GatherRows(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, idx):
         ctx.idx, ctx.n = idx, x.shape[0]
-        out = torch.zeros(idx.shape[0], x.shape[1], dtype=x.dtype, device=x.device)
-        return native.copy_rows(x, out, src_idx=idx)
+        out = torch.empty(idx.shape[0], x.shape[1], dtype=x.dtype, device=x.device)
+        return native.gather_rows_zero(x.contiguous(), out, idx)
 
     @staticmethod
     def backward(ctx, dy):

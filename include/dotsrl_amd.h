@@ -24,7 +24,7 @@ extern "C" {
 
 /* 3: drl_ppo_loss_params gained policy_loss, cov_ratio, clip_cov_lb, clip_cov_ub, ppo_kl_coef, cov_seed (a caller
  * built against version 2 passes a shorter struct); drl_gemm (operand layouts, fp32 epilogues, stream-K) */
-#define DRL_ABI_VERSION 5
+#define DRL_ABI_VERSION 6
 
 /* ld_vt value selecting the key-blocked V^T cache layout (B, Hkv, ceil(cap / 32), D, 32) wherever a V^T
  * operand with a leading dimension ld_vt is taken (flash / decode attention, the rope and decode-projection
@@ -603,6 +603,10 @@ void drl_gemm_set_debug(int32_t flags);
  * 16-byte aligned); a negative index skips the row. */
 int drl_copy_rows(const void* src, int64_t ld_src_bytes, const int64_t* src_idx, void* dst, int64_t ld_dst_bytes,
                   const int64_t* dst_idx, int64_t n_rows, int64_t row_bytes, void* stream);
+/* The gather of drl_copy_rows that writes every destination row: row i of dst (i < n_rows) = row src_idx[i] of src,
+ * or zeros where src_idx[i] < 0 (pad_input's zero pad rows without a memset of the padded buffer first). */
+int drl_gather_rows(const void* src, int64_t ld_src_bytes, const int64_t* src_idx, void* dst, int64_t ld_dst_bytes,
+                    int64_t n_rows, int64_t row_bytes, void* stream);
 /* Row sums of prefix sharing (the adjoint of a gather in which K padded positions read one packed row — a prompt
  * token shared by the samples of one prompt; the reference runs every sample's copy, dp_actor.py:119-247): for
  * j < m, dst[dst_idx[j] (or j)] = sum over k < K of src[src_idx[k * m + j]] (an index < 0 adds nothing; a

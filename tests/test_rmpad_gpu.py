@@ -52,6 +52,15 @@ def test_copy_rows_matches_indexing(C, dtype):
     o2 = torch.empty(50, C, device="cuda", dtype=dtype)
     native.copy_rows(wide[:, :C], o2)
     assert torch.equal(o2, wide[:, :C])
+    # the zero-filling gather (drl_gather_rows): every destination row written, zeros where the index is negative,
+    # whatever the destination held (NaN here)
+    o3 = torch.full((200, C), float("nan"), device="cuda", dtype=dtype)
+    native.gather_rows_zero(src, o3, idx)
+    assert torch.equal(o3[keep], src[idx[keep]])
+    assert torch.all(o3[~keep] == 0)
+    o4 = torch.full((50, C), float("nan"), device="cuda", dtype=dtype)
+    native.gather_rows_zero(wide[:, :C], o4, torch.arange(50, device="cuda"))
+    assert torch.equal(o4, wide[:, :C])
 
 
 def test_rmpad_maps():
