@@ -133,6 +133,8 @@ SIGNATURES = {
     "drl_adamw_step": (ctypes.c_int, [P, P, P, P, P, I64, ctypes.POINTER(AdamWParams), P, P]),
     "drl_rope_qkv_fwd": (ctypes.c_int, [P, I32, P, P, P, I64, I64, I64, I64, I64, I64, P, P, P, I64, I64, P, P, P, P,
                                         I64, P]),
+    "drl_rope_qkv_fwd_rows": (ctypes.c_int, [P, P, I32, P, P, P, I64, I64, I64, I64, I64, I64, P, P, P, I64, I64, P, P,
+                                             P, P, I64, P]),
     "drl_rope_qkv_bwd": (ctypes.c_int, [P, P, P, I32, P, P, P, I64, I64, I64, I64, I64, I64, P, P]),
     "drl_masked_softmax_fwd": (ctypes.c_int, [P, P, I32, P, I64, I64, I64, I64, I64, I64, F32, P]),
     "drl_masked_softmax_bwd": (ctypes.c_int, [P, P, P, I32, I64, I64, F32, P]),

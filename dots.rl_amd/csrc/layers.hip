@@ -43,7 +43,23 @@ struct RopeArgs {
   E* kt;
   E* vt;
   int64_t ld_t;
+  // optional source row of each (b, t) in qkv (packed rows: remove-padding / prefix sharing), < 0 = a zero row;
+  // NULL: row b * T + t
+  const int64_t* src_row;
 };
+
+// the qkv row of (b, t): its packed row through src_row (a pad reads row 0 and is zeroed by its caller)
+template <typename E>
+__device__ __forceinline__ const E* rope_src(const RopeArgs<E>& a, int64_t bt, int64_t Hall, int64_t h, bool& zero) {
+  int64_t r = bt;
+  zero = false;
+  if (a.src_row) {
+    r = a.src_row[bt];
+    zero = r < 0;
+    r = zero ? 0 : r;
+  }
+  return a.qkv + (r * Hall + h) * a.D;
+}
 
 template <typename E>
 __global__ __launch_bounds__(256) void rope_qkv_fwd_kernel(RopeArgs<E> a) {
@@ -59,8 +75,9 @@ __global__ __launch_bounds__(256) void rope_qkv_fwd_kernel(RopeArgs<E> a) {
     const int64_t h = (i / half) % Hall;
     const int64_t bt = i / (half * Hall);
     const int64_t t = bt % a.T, b = bt / a.T;
-    const E* src = a.qkv + bt * Hall * a.D + h * a.D;
-    const float x1 = ldf(src, j), x2 = ldf(src, j + half);
+    bool zero;
+    const E* src = rope_src(a, bt, Hall, h, zero);
+    const float x1 = zero ? 0.f : ldf(src, j), x2 = zero ? 0.f : ldf(src, j + half);
     if (h < a.Hq + a.Hkv) {
       int64_t p = a.pos[b * a.T + t];
       p = p < 0 ? 0 : (p >= a.maxpos ? a.maxpos - 1 : p);
@@ -87,13 +104,13 @@ __global__ __launch_bounds__(256) void rope_qkv_fwd_kernel(RopeArgs<E> a) {
     } else {
       if (a.vt != nullptr) {
         E* dst = a.vt + (b * a.Hkv + (h - a.Hq - a.Hkv)) * vt_panel(a.ld_t, a.D, a.Tk);
-        dst[vt_index(j, koff + t, a.ld_t, a.D)] = src[j];
-        dst[vt_index(j + half, koff + t, a.ld_t, a.D)] = src[j + half];
+        stf(dst, vt_index(j, koff + t, a.ld_t, a.D), x1);  // exact: x1 is the element (or 0 for a pad row)
+        stf(dst, vt_index(j + half, koff + t, a.ld_t, a.D), x2);
       }
       if (a.v != nullptr) {
         E* dst = a.v + ((b * a.Hkv + (h - a.Hq - a.Hkv)) * a.Tk + koff + t) * a.D;
-        dst[j] = src[j];
-        dst[j + half] = src[j + half];
+        stf(dst, j, x1);
+        stf(dst, j + half, x2);
       }
     }
   }
@@ -138,8 +155,9 @@ __global__ __launch_bounds__(256) void rope_qkv_fwd_tiled_kernel(RopeArgs<E> a) 
     const int j = threadIdx.x % half;
     const int64_t t = t0 + p;
     if (t >= a.T) break;
-    const E* src = a.qkv + ((b * a.T + t) * Hall + h) * a.D;
-    float o1 = ldf(src, j), o2 = ldf(src, j + half);
+    bool zero;
+    const E* src = rope_src(a, b * a.T + t, Hall, h, zero);
+    float o1 = zero ? 0.f : ldf(src, j), o2 = zero ? 0.f : ldf(src, j + half);
     if (is_q || is_k) {
       int64_t ps = a.pos[b * a.T + t];
       ps = ps < 0 ? 0 : (ps >= a.maxpos ? a.maxpos - 1 : ps);
@@ -235,10 +253,15 @@ __global__ __launch_bounds__(256) void rope_qkv_fwd_tiled4_kernel(RopeArgs<E> a)
   for (int p = threadIdx.x / tpr; p < kRopeTile; p += rows_per_pass) {
     const int64_t t = t0 + p;
     if (t >= a.T) break;
-    const E* src = a.qkv + ((b * a.T + t) * Hall + h) * a.D;
+    bool zero;
+    const E* src = rope_src(a, b * a.T + t, Hall, h, zero);
     float o1[4], o2[4];
     ld4(src + j0, o1);
     ld4(src + j0 + half, o2);
+    if (zero) {  // a pad position of the packed source: zeros, as pad_input leaves them (select after the load)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o1[e] = o2[e] = 0.f;
+    }
     if (is_q || is_k) {
       int64_t ps = a.pos[b * a.T + t];
       ps = ps < 0 ? 0 : (ps >= a.maxpos ? a.maxpos - 1 : ps);
@@ -953,6 +976,14 @@ int drl_rope_qkv_fwd(const void* qkv, int32_t dt, const int64_t* position_ids, c
                      int64_t maxpos, int64_t B, int64_t T, int64_t Hq, int64_t Hkv, int64_t D, void* q, void* k,
                      void* v, int64_t Tk, int64_t koff, const int64_t* koff_dev, void* qt, void* kt, void* vt,
                      int64_t ld_t, void* stream) {
+  return drl_rope_qkv_fwd_rows(qkv, nullptr, dt, position_ids, cos_t, sin_t, maxpos, B, T, Hq, Hkv, D, q, k, v, Tk,
+                               koff, koff_dev, qt, kt, vt, ld_t, stream);
+}
+
+int drl_rope_qkv_fwd_rows(const void* qkv, const int64_t* src_row, int32_t dt, const int64_t* position_ids,
+                          const float* cos_t, const float* sin_t, int64_t maxpos, int64_t B, int64_t T, int64_t Hq,
+                          int64_t Hkv, int64_t D, void* q, void* k, void* v, int64_t Tk, int64_t koff,
+                          const int64_t* koff_dev, void* qt, void* kt, void* vt, int64_t ld_t, void* stream) {
   using namespace drl;
   DRL_CHECK_ARG(qkv && position_ids && cos_t && sin_t && q && k && (v || vt), "NULL input");
   DRL_CHECK_ARG((qt == nullptr && kt == nullptr && vt == nullptr) || (ld_t >= Tk && ld_t >= T) ||
@@ -964,7 +995,7 @@ int drl_rope_qkv_fwd(const void* qkv, int32_t dt, const int64_t* position_ids, c
   DRL_E_DISPATCH(dt, {
     RopeArgs<E> a{static_cast<const E*>(qkv), position_ids, cos_t, sin_t, static_cast<E*>(q), static_cast<E*>(k),
                   static_cast<E*>(v), B, T, Hq, Hkv, D, Tk, koff, maxpos, koff_dev, static_cast<E*>(qt),
-                  static_cast<E*>(kt), static_cast<E*>(vt), ld_t};
+                  static_cast<E*>(kt), static_cast<E*>(vt), ld_t, src_row};
     const bool vec4 = D % 8 == 0 && 256 % (D / 8) == 0 && aligned16(qkv) && aligned16(cos_t) && aligned16(sin_t) &&
                       (q == nullptr || aligned16(q)) && (k == nullptr || aligned16(k)) && (v == nullptr || aligned16(v));
     if ((qt || kt || vt) && T >= 16 && D <= 128 && D % 2 == 0 && 256 % (D / 2) == 0) {

@@ -643,19 +643,26 @@ def _edt(t):
 
 
 def rope_qkv_fwd(qkv, position_ids, cos_t, sin_t, Hq, Hkv, D, q, k, v, koff=0, koff_dev=None, vt=None, qt=None,
-                 kt=None):
+                 kt=None, src_rows=None):
     """qkv (B,T,(Hq+2Hkv)D) -> q (B,Hkv,G,T,D); k, v written at [:, :, koff:koff+T] of (B,Hkv,Tk,D).
 
     ``koff_dev`` (device int64 scalar) replaces ``koff`` for graph-captured decode steps. ``qt`` (B,Hkv,G,D,ld),
-    ``kt`` / ``vt`` (B,Hkv,D,ld): head-dim-major copies for the fused attention kernels (same ld)."""
-    B, T = qkv.shape[0], qkv.shape[1]
+    ``kt`` / ``vt`` (B,Hkv,D,ld): head-dim-major copies for the fused attention kernels (same ld). ``src_rows``
+    (B*T,) int64: qkv is packed (nnz, (Hq+2Hkv)D) and position (b, t) reads row src_rows[b*T+t] (< 0: zeros) —
+    drl_rope_qkv_fwd_rows, no padded copy of qkv; B, T then come from ``position_ids``."""
+    if src_rows is not None:
+        B, T = position_ids.shape[0], position_ids.shape[1]
+        assert qkv.dim() == 2 and qkv.is_contiguous() and src_rows.dtype == torch.int64 and src_rows.numel() == B * T
+        _dev(src_rows)
+    else:
+        B, T = qkv.shape[0], qkv.shape[1]
     lds = {(vt_ld(t) if t is vt else t.stride(-2)) for t in (qt, kt, vt) if t is not None}
     if vt is not None:
         _vt_cap_ok(vt, k.shape[2])
     assert len(lds) <= 1, "qt / kt / vt must share their row stride"
-    check(lib().drl_rope_qkv_fwd(_p(qkv), _edt(qkv), _p(position_ids), _p(cos_t), _p(sin_t), cos_t.shape[0], B, T,
-                                 Hq, Hkv, D, _p(q), _p(k), _p(v), k.shape[2], koff, _p(koff_dev), _p(qt), _p(kt),
-                                 _p(vt), lds.pop() if lds else 0, _stream()),
+    check(lib().drl_rope_qkv_fwd_rows(_p(qkv), _p(src_rows), _edt(qkv), _p(position_ids), _p(cos_t), _p(sin_t),
+                                      cos_t.shape[0], B, T, Hq, Hkv, D, _p(q), _p(k), _p(v), k.shape[2], koff,
+                                      _p(koff_dev), _p(qt), _p(kt), _p(vt), lds.pop() if lds else 0, _stream()),
           "drl_rope_qkv_fwd")
 
 

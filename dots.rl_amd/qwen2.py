@@ -447,10 +447,12 @@ def _layer_forward(m, i, x_prev, delta, pos, key_valid, save, cache=None, koff=0
         qkv = native.linear_fwd(h1.view(B * T, H), s.w(p + "qkv_proj.weight"), bias=m.qkv_bias(i))
     else:
         qkv = torch.addmm(m.qkv_bias(i), h1.view(B * T, H), s.w(p + "qkv_proj.weight").t())
-    if rm is not None:
-        qkv = rm.unpack(qkv)
+    src_rows = None
+    if rm is not None:  # RoPE reads the packed qkv through the inverse map: no padded copy of it
+        src_rows = rm.inv
         B, T = rm.B, rm.T
-    qkv = qkv.view(B, T, -1)
+    else:
+        qkv = qkv.view(B, T, -1)
     q = torch.empty(B, Hkv, G, T, D, dtype=dt, device=dev)
     # bf16 full-sequence passes run the fused MFMA attention (csrc/flash_attn.hip): log-probs and prefill
     # forward-only, the training forward with the LSE its fused backward needs; the unfused path (fp32 scores
@@ -464,7 +466,7 @@ def _layer_forward(m, i, x_prev, delta, pos, key_valid, save, cache=None, koff=0
         vbuf = torch.empty_like(kbuf)
         kt = torch.empty(B, Hkv, D, T, dtype=dt, device=dev)
         vt = torch.empty(B, Hkv, D, T, dtype=dt, device=dev)
-        native.rope_qkv_fwd(qkv, pos, m.cos, m.sin, Hq, Hkv, D, q, kbuf, vbuf, kt=kt, vt=vt)
+        native.rope_qkv_fwd(qkv, pos, m.cos, m.sin, Hq, Hkv, D, q, kbuf, vbuf, kt=kt, vt=vt, src_rows=src_rows)
         attn = torch.empty(B, T, Hq * D, dtype=dt, device=dev)
         lse = torch.empty(B, Hkv, G, T, dtype=torch.float32, device=dev)
         qs = getattr(rm, "q_start", None)
@@ -485,7 +487,7 @@ def _layer_forward(m, i, x_prev, delta, pos, key_valid, save, cache=None, koff=0
     else:  # bf16 caches keep V head-dim-major (cache.vt), the layout of the MFMA prefill / decode kernels
         kbuf, vbuf = cache.k[i], cache.v[i]
         vt = cache.vt[i]
-    native.rope_qkv_fwd(qkv, pos, m.cos, m.sin, Hq, Hkv, D, q, kbuf, vbuf, koff, koff_dev, vt=vt)
+    native.rope_qkv_fwd(qkv, pos, m.cos, m.sin, Hq, Hkv, D, q, kbuf, vbuf, koff, koff_dev, vt=vt, src_rows=src_rows)
     L = koff + T
     if flash:
         attn = torch.empty(B, T, Hq * D, dtype=dt, device=dev)

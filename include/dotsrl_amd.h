@@ -368,6 +368,13 @@ int drl_rope_qkv_fwd(const void* qkv, int32_t dt, const int64_t* position_ids, c
                      int64_t maxpos, int64_t B, int64_t T, int64_t Hq, int64_t Hkv, int64_t D, void* q, void* k,
                      void* v, int64_t Tk, int64_t koff, const int64_t* koff_dev, void* qt, void* kt, void* vt,
                      int64_t ld_t, void* stream);
+/* drl_rope_qkv_fwd over a packed qkv (remove-padding / prefix-sharing passes): the qkv row of position (b, t) is
+ * row src_row[b * T + t] of qkv (a negative entry: a zero row, the pad positions pad_input leaves zero), so the
+ * packed rows are never scattered into a padded (B * T) copy first. src_row NULL: drl_rope_qkv_fwd. */
+int drl_rope_qkv_fwd_rows(const void* qkv, const int64_t* src_row, int32_t dt, const int64_t* position_ids,
+                          const float* cos_t, const float* sin_t, int64_t maxpos, int64_t B, int64_t T, int64_t Hq,
+                          int64_t Hkv, int64_t D, void* q, void* k, void* v, int64_t Tk, int64_t koff,
+                          const int64_t* koff_dev, void* qt, void* kt, void* vt, int64_t ld_t, void* stream);
 int drl_rope_qkv_bwd(const void* dq, const void* dk, const void* dv, int32_t dt, const int64_t* position_ids,
                      const float* cos_t, const float* sin_t, int64_t maxpos, int64_t B, int64_t T, int64_t Hq,
                      int64_t Hkv, int64_t D, void* dqkv, void* stream);

@@ -250,3 +250,38 @@ def test_gae_step_with_remove_padding():
     m = trainer.fit(num_steps=1)[-1]
     for k in ["critic/vf_loss", "actor/pg_loss", "actor/kl_loss", "critic/grad_norm", "actor/grad_norm"]:
         assert k in m and np.isfinite(m[k]), k
+
+
+@pytest.mark.parametrize("dtype,heads", [(torch.bfloat16, True), (torch.float32, False)])
+def test_rope_reads_packed_rows_like_the_padded_copy(dtype, heads):
+    """drl_rope_qkv_fwd_rows (RoPE straight from the packed qkv through the inverse map, zeros at pads) equals RoPE on
+    the padded copy pad_input would build, bit for bit: the tiled kernel with head-dim-major copies (bf16) and the
+    generic one (fp32, no copies)."""
+    from dots.rl_amd import native
+
+    B, T, Hq, Hkv, D = 3, 40, 4, 2, 64
+    C = (Hq + 2 * Hkv) * D
+    g = torch.Generator(device="cuda").manual_seed(7)
+    am = torch.ones(B, T, dtype=torch.int64, device="cuda")
+    am[1, :9] = 0
+    am[2, :23] = 0
+    idx = torch.nonzero(am.reshape(-1)).reshape(-1)
+    inv = torch.full((B * T,), -1, dtype=torch.int64, device="cuda")
+    inv[idx] = torch.arange(idx.numel(), device="cuda")
+    packed = torch.randn(idx.numel(), C, device="cuda", generator=g).to(dtype)
+    padded = torch.zeros(B * T, C, device="cuda", dtype=dtype)
+    padded[idx] = packed
+    pos = (am.cumsum(-1) - 1).clamp_min(0).contiguous()
+    cos = torch.randn(64, D // 2, device="cuda", generator=g)
+    sin = torch.randn(64, D // 2, device="cuda", generator=g)
+    outs = []
+    for src, rows in ((padded.view(B, T, C), None), (packed, inv)):
+        q = torch.full((B, Hkv, Hq // Hkv, T, D), float("nan"), device="cuda", dtype=dtype)
+        k = torch.full((B, Hkv, T, D), float("nan"), device="cuda", dtype=dtype)
+        v = torch.full_like(k, float("nan"))
+        kt = torch.full((B, Hkv, D, T), float("nan"), device="cuda", dtype=dtype) if heads else None
+        vt = torch.full_like(kt, float("nan")) if heads else None
+        native.rope_qkv_fwd(src, pos, cos, sin, Hq, Hkv, D, q, k, v, kt=kt, vt=vt, src_rows=rows)
+        outs.append([t for t in (q, k, v, kt, vt) if t is not None])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
