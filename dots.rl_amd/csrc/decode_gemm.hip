@@ -350,10 +350,10 @@ __global__ __launch_bounds__(256) void decode_gemm_tiled_kernel(DgArgs a) {
 // "Pipelining across barriers"): counted vmcnt (own copies of this stage landed, the next stages' still in
 // flight) -> lgkmcnt(0) + raw s_barrier (everyone's copies landed; everyone's reads of the buffer about to be
 // refilled are done) -> refill the oldest buffer -> MFMAs from this stage's buffer. One __shared__ array.
-template <int WR, int WT, int WB, int TB, int EPI>
+template <int WR, int WT, int WB, int TB, int EPI, int KST = 2>
 __global__ __launch_bounds__(64 * WR * WT) void decode_gemm_lds_kernel(DgArgs a) {
   constexpr int NW = WR * WT, RB = WR * WB, TT = WT * TB, FR = RB + TT;
-  constexpr int KST = 2, NBUF = 3;
+  constexpr int NBUF = 3;
   constexpr int PER_WAVE = KST * FR / NW;  // LDS-DMA instructions per wave and stage
   static_assert(KST * FR % NW == 0, "copies must divide evenly over the waves");
   __shared__ __attribute__((aligned(16))) uint16_t lds[NBUF * KST * FR * 512];
@@ -402,9 +402,10 @@ __global__ __launch_bounds__(64 * WR * WT) void decode_gemm_lds_kernel(DgArgs a)
     else if constexpr (PER_WAVE == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     else if constexpr (PER_WAVE == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
     else if constexpr (PER_WAVE == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else if constexpr (PER_WAVE == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     else if constexpr (PER_WAVE == 9) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
     else static_assert(PER_WAVE == 2 || PER_WAVE == 3 || PER_WAVE == 4 || PER_WAVE == 5 || PER_WAVE == 6 ||
-                       PER_WAVE == 9, "vmcnt table");
+                       PER_WAVE == 8 || PER_WAVE == 9, "vmcnt table");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     issue(i + 2);  // into the buffer read in iteration i - 1 (every wave is past it)
@@ -670,10 +671,12 @@ bool plan_decode_gemm(int64_t M, int64_t N, int64_t K, int epi, DgPlan& p) {
 
 // tiled path: (WB, TB, WW, WT, lds) configurations instantiated (lds: the LDS-staged kernel, WW x WT waves)
 struct DtShape { int wb, tb, ww, wt, lds; };
-// 9-13: larger token panels per workgroup (the activation panel staged once for more weight rows' MFMAs), round 4
+// 9-13: larger token panels per workgroup (the activation panel staged once for more weight rows' MFMAs), round 4;
+// 14-16: LDS-staged with 4 k-steps per stage (half the barriers, twice the LDS: fewer resident workgroups)
 constexpr DtShape kTiled[] = {{2, 2, 4, 2, 1}, {2, 2, 2, 2, 1}, {1, 2, 2, 2, 1}, {2, 1, 2, 2, 1},
                               {2, 2, 2, 2, 0}, {2, 2, 4, 1, 0}, {1, 2, 2, 2, 0}, {1, 2, 4, 1, 0}, {1, 1, 2, 2, 0},
-                              {2, 2, 1, 4, 1}, {2, 4, 2, 2, 1}, {1, 4, 2, 2, 1}, {2, 4, 1, 4, 1}, {2, 4, 2, 2, 0}};
+                              {2, 2, 1, 4, 1}, {2, 4, 2, 2, 1}, {1, 4, 2, 2, 1}, {2, 4, 1, 4, 1}, {2, 4, 2, 2, 0},
+                              {1, 2, 2, 2, 1}, {2, 1, 2, 2, 1}, {2, 2, 2, 2, 1}};
 constexpr int kNumTiled = static_cast<int>(sizeof(kTiled) / sizeof(kTiled[0]));
 int g_dt_force = -1;  // tuning: force configuration index (drl_decode_gemm_force_tiled), -1 = planner
 int g_dt_min_rows = 192;  // tuning: smallest M for the tiled path
@@ -699,7 +702,9 @@ bool plan_decode_tiled(int64_t M, int64_t N, int64_t K, int epi, DgPlan& p) {
   int ci;
   if (g_dt_force >= 0) ci = g_dt_force;
   else if (epi == EPI_SWIGLU) ci = 2;
-  else if (K >= 2048) { if (M < 384 && g_dt_min_rows >= 192) return false; ci = 6; }
+  // long-K partials (down_proj): 4 k-steps per LDS stage (512 rows: 14.5 -> 13.5 us, 256 rows: 13.2 -> 12.3 against
+  // the register-ring and one-round-trip kernels; profiles/r04_decode_cfg_sweep_kst4.jsonl)
+  else if (K >= 2048) ci = 15;
   else {
     // short-K partials (o_proj): the one-round-trip kernel below 384 rows (256 rows: 6.75 -> 5.5 us)
     if (epi == EPI_PARTIAL && M < 384 && g_dt_force < 0 && g_dt_min_rows >= 192) return false;
@@ -750,6 +755,9 @@ void launch_dt(const DgArgs& a, const DgPlan& p, hipStream_t s) {
     case 10: hipLaunchKernelGGL((decode_gemm_lds_kernel<2, 2, 2, 4, EPI>), grid, dim3(256), 0, s, a); break;
     case 11: hipLaunchKernelGGL((decode_gemm_lds_kernel<2, 2, 1, 4, EPI>), grid, dim3(256), 0, s, a); break;
     case 12: hipLaunchKernelGGL((decode_gemm_lds_kernel<1, 4, 2, 4, EPI>), grid, dim3(256), 0, s, a); break;
+    case 14: hipLaunchKernelGGL((decode_gemm_lds_kernel<2, 2, 1, 2, EPI, 4>), grid, dim3(256), 0, s, a); break;
+    case 15: hipLaunchKernelGGL((decode_gemm_lds_kernel<2, 2, 2, 1, EPI, 4>), grid, dim3(256), 0, s, a); break;
+    case 16: hipLaunchKernelGGL((decode_gemm_lds_kernel<2, 2, 2, 2, EPI, 4>), grid, dim3(256), 0, s, a); break;
     default: hipLaunchKernelGGL((decode_gemm_tiled_kernel<2, 4, 2, 2, EPI>), grid, dim3(256), 0, s, a); break;
   }
 }

@@ -48,6 +48,29 @@ def test_decode_gemm_partials(M, N, K):
     assert torch.equal(part, native.decode_gemm(xp, wp, M, N, K))  # deterministic
 
 
+@pytest.mark.parametrize("M", [200, 512])
+@pytest.mark.parametrize("N,K", [(896, 4864), (896, 896)])
+def test_decode_gemm_every_tiled_configuration(M, N, K):
+    """Every MFMA-tiled configuration (csrc/decode_gemm.hip kTiled, forced) gives the planner's K-slice sums within
+    fp32 rounding of the fp32 product, deterministically."""
+    x = rnd(M, K, seed=M + 1)
+    w = rnd(N, K, scale=0.05, seed=N + K + 1)
+    ref = x.float() @ w.float().t()
+    wp = native.decode_pack_weight(w)
+    lib = native.lib()
+    try:
+        for ci in range(17):
+            lib.drl_decode_gemm_force_tiled(ci, 1)
+            ks, mbt = native.decode_gemm_plan(M, N, K)
+            xp = native.pack_activations(x, mbt)
+            part = native.decode_gemm(xp, wp, M, N, K)
+            err = (part.sum(0) - ref).abs().max().item() / ref.abs().max().item()
+            assert err < 1e-5, (ci, err)
+            assert torch.equal(part, native.decode_gemm(xp, wp, M, N, K)), ci
+    finally:
+        lib.drl_decode_gemm_force_tiled(-1, 0)
+
+
 @pytest.mark.parametrize("M", [5, 64, 128, 300, 512])
 @pytest.mark.parametrize("I,K", [(4864, 896), (128, 64)])
 def test_decode_gemm_swiglu_packed(M, I, K):
