@@ -694,14 +694,17 @@ int g_dt_max_ks = 4;  // tuning: most K slices of a partial-sum plan (drl_decode
 // K slices (partials only, each a multiple of 4 k-steps, <= 4): the fewest that give >= 160 workgroups, else the
 // most workgroups. p.mb = 0 marks a tiled plan; p.ksw = index into kTiled.
 bool plan_decode_tiled(int64_t M, int64_t N, int64_t K, int epi, DgPlan& p) {
-  if (g_dt_mode == 0 || M < g_dt_min_rows || M > 512 || K % 64 != 0 || N < 1) return false;
+  // gate_up + SwiGLU at 97..191 rows: the LDS-staged kernel with 4 k-steps per stage beats the one-round-trip kernel
+  // (128 rows: 11.1 -> 10.0 us; 64 rows: 9.7 against 8.0, so not below; profiles/r04_decode_cfg_sweep_rows64_128.jsonl)
+  const bool swiglu_mid = epi == EPI_SWIGLU && M > 96 && M < 192 && g_dt_min_rows >= 192 && g_dt_force < 0;
+  if (g_dt_mode == 0 || (M < g_dt_min_rows && !swiglu_mid) || M > 512 || K % 64 != 0 || N < 1) return false;
   // qkv + RoPE (whole K per output block): the one-round-trip kernel's 4 waves on K quarters beat every tiled
   // configuration from 192 rows on (512 rows: 14.2 -> 9.7 us, 256 rows: 14.3 -> 7.3;
   // profiles/r03_decode_cfg_sweep2.jsonl), unless a configuration is forced
   if (epi == EPI_ROPE && g_dt_force < 0) return false;
   int ci;
   if (g_dt_force >= 0) ci = g_dt_force;
-  else if (epi == EPI_SWIGLU) ci = 2;
+  else if (epi == EPI_SWIGLU) ci = swiglu_mid ? 14 : 2;
   // long-K partials (down_proj): 4 k-steps per LDS stage (512 rows: 14.5 -> 13.5 us, 256 rows: 13.2 -> 12.3 against
   // the register-ring and one-round-trip kernels; profiles/r04_decode_cfg_sweep_kst4.jsonl)
   else if (K >= 2048) ci = 15;

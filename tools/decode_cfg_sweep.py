@@ -81,7 +81,7 @@ def main():
         }
         for name, fn in projs.items():
             row = {"rows": B, "proj": name}
-            for ci in [-1] + (list(range(NCFG)) if B >= 128 else []):
+            for ci in [-1] + (list(range(NCFG)) if B >= 64 else []):
                 lib.drl_decode_gemm_force_tiled(ci, 1 if ci >= 0 else 0)
                 try:
                     us = graph_time(lambda: [fn(i) for i in range(L)]) / L
