@@ -2,7 +2,7 @@
 heads, 512 shared prompt keys, 1..256 response keys): every (waves, variant, splits) plan of drl_decode_attention_vt
 over cold caches (copies rotated past the MALL), outputs checked identical to the automatic plan.
 
-  python tools/probes/decode_group_sweep.py        -> one JSON line per (L, plan)"""
+  python tools/probes/decode_group_sweep.py [B]    -> one JSON line per (L, plan); B < 512: the per-row plans"""
 
 import json
 import sys
@@ -13,7 +13,7 @@ sys.path.insert(0, ".")
 from dots.rl_amd import native  # noqa: E402
 
 DEV, BF = "cuda", torch.bfloat16
-B, group, Hkv, G, D, P, R = 512, 8, 2, 7, 64, 512, 256
+B, group, Hkv, G, D, P, R = int(sys.argv[1]) if len(sys.argv) > 1 else 512, 8, 2, 7, 64, 512, 256
 cap = P + R
 lib = native.lib()
 g = torch.Generator(device=DEV).manual_seed(0)
@@ -29,6 +29,8 @@ q = torch.randn(B, Hkv, G, D, device=DEV, generator=g).to(BF)
 # decode_group_kernel at its default 8 waves and forced 2 / 4 / 16 (the per-row kernel's plans no longer apply
 # to grouped calls; its numbers before the grouped kernel: profiles/r04_decode_group_perrow.jsonl)
 plans = [(0, 0, 0), (2, 0, 0), (4, 0, 0), (16, 0, 0)]
+if B < 512:  # below the grouped kernel's threshold the per-row kernel runs: its (waves, variant, splits) plans
+    plans = [(0, 0, 0)] + [(w, v, sp) for w in (2, 4, 8, 16) for v in (0, 1, 2, 3, 4) for sp in (1, 2, 4)]
 for L in (P + 32, P + 128, P + 256):
     outs = {}
     for (w, v, s) in plans:
