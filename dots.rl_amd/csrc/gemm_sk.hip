@@ -808,6 +808,7 @@ struct SkTuning {
   int mode = 0;      // 0 automatic (whole tiles, or uniform split-K for few long-K tiles), 1 stream-K (whole-tile
                      // rounds + a stream-K tail), 2 whole tiles only, 3 uniform split-K
   int param = 0;     // mode 1: minimum k-pairs per workgroup; mode 3: splits per tile (0 automatic)
+  bool group_set = false;  // group given through drl_gemm_set_sk_tuning (else chosen per shape)
 };
 SkTuning g_sk;
 int g_sk_dbg = 0;
@@ -848,6 +849,7 @@ void drl_gemm_set_debug(int32_t flags) { drl::g_sk_dbg = flags; }
 void drl_gemm_set_sk_tuning(int32_t grid, int32_t group, int32_t mode, int32_t param) {
   drl::g_sk.grid = grid > 0 ? grid : 0;
   drl::g_sk.group = (group >= 1 && group <= 64) ? group : 4;
+  drl::g_sk.group_set = group >= 1 && group <= 64;
   drl::g_sk.mode = (mode >= 0 && mode <= 3) ? mode : 0;
   drl::g_sk.param = param > 0 ? param : 0;
 }
@@ -941,8 +943,16 @@ int drl_gemm(const void* a, int64_t lda, int32_t a_layout, const void* b, int64_
   g.dbg = g_sk_dbg;
   g.tm = static_cast<int>((M + 255) / 256);
   g.tn = static_cast<int>((N + 255) / 256);
-  g.gm = g_sk.group;
   g.P = static_cast<int>((K + 127) / 128);
+  // rasterization group (M-tiles per group), unless tuned: narrow outputs (4 / 5 tile columns) over short K take 16 / 8
+  // (the A panel shared by more workgroups of an XCD), over long K 1; few M-tiles x many tile columns (down_proj's
+  // weight gradient) 2; the lm_head forward's 594 tile columns 8 (profiles/r04_gemm_groups_82144.jsonl: 2-5 % each)
+  g.gm = g_sk.group;
+  if (!g_sk.group_set) {
+    if (g.tn <= 5) g.gm = g.P > 16 ? 1 : (g.tn == 5 ? 8 : 16);
+    else if (g.tm <= 5) g.gm = 2;
+    else if (g.tn >= 256) g.gm = 8;
+  }
   g.nkt = static_cast<int>((K + 63) / 64);
   g.n_tiles = g.tm * g.tn;
   const int cus = cu_count();

@@ -3,7 +3,7 @@ forward (y = x W^T), dgrad (dx = dy W) and wgrad (dW += dy^T x, fp32) of qkv / o
 (8 x 768) and log-prob (16 x 768) micro-batch rows, and the lm_head over the response rows. One JSON line per
 shape: microseconds and TFLOP/s of both, interleaved rounds in one process (cdna_hip_programming.md §5.4 rule 24).
 
-  python tools/gemm_sk_bench.py [--quick] [--tune]
+  python tools/gemm_sk_bench.py [--quick] [--tune] [--groups 1 2 4 8]
 """
 
 import argparse
@@ -61,6 +61,7 @@ def main():
     ap.add_argument("--no-lib", action="store_true", help="skip the hipBLASLt timing")
     ap.add_argument("--decode", type=int, default=None, help="only the decode-step shapes at this many rows")
     ap.add_argument("--only", nargs="*", default=None, help="only these shape names (e.g. gate_up_wgrad o_wgrad)")
+    ap.add_argument("--groups", type=int, nargs="*", default=None, help="also time these rasterization groups")
     args = ap.parse_args()
     from dots.rl_amd.workers import _enable_gemm_tuning
     _enable_gemm_tuning("auto")
@@ -113,6 +114,12 @@ def main():
                 sweep[f"g{grid}_m{mode}_p{param}"] = round(bench(ours, iters=10, rounds=2), 2)
             native.lib().drl_gemm_set_sk_tuning(0, 0, 0, 0)
             row["sweep_us"] = sweep
+        if args.groups:
+            row["group_us"] = {}
+            for gm in args.groups:
+                native.lib().drl_gemm_set_sk_tuning(0, gm, 0, 0)
+                row["group_us"][gm] = round(bench(ours, iters=10, rounds=3), 2)
+            native.lib().drl_gemm_set_sk_tuning(0, 0, 0, 0)
         print(json.dumps(row), flush=True)
 
 
