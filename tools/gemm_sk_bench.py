@@ -4,6 +4,9 @@ forward (y = x W^T), dgrad (dx = dy W) and wgrad (dW += dy^T x, fp32) of qkv / o
 shape: microseconds and TFLOP/s of both, interleaved rounds in one process (cdna_hip_programming.md §5.4 rule 24).
 
   python tools/gemm_sk_bench.py [--quick] [--tune] [--groups 1 2 4 8]
+
+The first shape a process times runs ~10-15 % slow (clocks / caches still cold: ours_us of the first shape against
+its own --groups / --tune entries, profiles/r04_decode_lm_head_sweep.jsonl); compare a shape's entries with each other.
 """
 
 import argparse
