@@ -371,6 +371,9 @@ def main():
             # the reference's perf/mfu/actor (flops_counter.estimate_flops over every row's tokens): with prompt
             # groups run once (prompt_groups below) the executed FLOPs are fewer than the ones it counts
             "mfu_actor": sum(h.get("perf/mfu/actor", 0.0) for h in hist) / len(hist),
+            # the FLOPs update_actor executed (flops_counter.executed_flops: prompt groups counted once, lm_head over
+            # the response rows) over its time and the dense bf16 peak
+            "mfu_actor_executed": sum(h.get("perf/mfu/actor_executed", 0.0) for h in hist) / len(hist),
             "prompt_groups": {"rollout.enable_prefix_caching": bool(ar.rollout.get("enable_prefix_caching", True)),
                               "model.share_prompt_prefix": bool(ar.model.get("share_prompt_prefix", True))},
             "roofline": roofline,

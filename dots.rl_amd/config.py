@@ -57,17 +57,22 @@ QWEN25_7B = dict(
 )
 RANDOM_MODELS = {"qwen2.5-0.5b": QWEN25_05B, "llama-3-8b": LLAMA3_8B, "qwen2.5-7b": QWEN25_7B}
 
+# worker profiler (actor.yaml:133-160, critic.yaml, ProfilerConfig): tool "roctx" (rocprofv3 --marker-trace ranges) or
+# "torch" (torch.profiler Chrome trace); which steps run between start_profile / stop_profile: global_profiler.steps
+PROFILER = dict(tool=None, enable=False, all_ranks=False, ranks=[], save_path="outputs/profile")
+
 DEFAULTS = dict(
     data=dict(train_batch_size=64, max_prompt_length=512, max_response_length=256, seed=1234,
               reward_fn_key="data_source"),
     actor_rollout_ref=dict(
         hybrid_engine=True,
         # share_prompt_prefix: the n samples of a prompt run its tokens once in the log-prob / update passes
-        # (qwen2.PrefixShare: same values, the per-token work of the prompt done once per group)
+        # (qwen2.PrefixShare: the per-token work of the prompt done once per group). Equal to the per-row passes in
+        # fp32 up to summation order; in bf16 up to bf16 rounding (the copies' prompt gradients are summed in fp32 and
+        # rounded once, and the GEMMs see other row counts), not bit-comparable — False restores per-row passes
         model=dict(path="random:qwen2.5-0.5b", override_config={}, use_remove_padding=False, use_fused_kernels=False,
                    share_prompt_prefix=True,
-                   enable_gradient_checkpointing=False, external_lib=None, dtype="bfloat16",
-                   gemm_tuning="auto"),  # replay offline GEMM algorithm choices (workers._enable_gemm_tuning)
+                   enable_gradient_checkpointing=False, external_lib=None, dtype="bfloat16"),
         actor=dict(
             strategy="mi355x", ppo_mini_batch_size=32, ppo_micro_batch_size=None, ppo_micro_batch_size_per_gpu=8,
             use_dynamic_bsz=False, ppo_max_token_len_per_gpu=16384, clip_ratio=0.2, clip_ratio_low=0.2,
@@ -89,6 +94,7 @@ DEFAULTS = dict(
             optim=dict(lr=1e-6, lr_warmup_steps_ratio=0.0, total_training_steps=-1, weight_decay=0.01,
                        lr_warmup_steps=-1, betas=[0.9, 0.999], eps=1e-8, warmup_style="constant", min_lr_ratio=0.0,
                        num_cycles=0.5),
+            profiler=dict(PROFILER),
         ),
         rollout=dict(
             name="mi355x", mode="sync", temperature=1.0, top_k=-1, top_p=1.0, do_sample=True, n=8,
@@ -106,10 +112,12 @@ DEFAULTS = dict(
             # prefix caching of the n samples' shared prompt (vllm_rollout_spmd.py:195 runs vLLM with it on): each
             # distinct prompt prefilled once, its keys read from one cache row by the group's decode attention
             enable_prefix_caching=True,
+            profiler=dict(PROFILER),
         ),
         ref=dict(log_prob_micro_batch_size=None, log_prob_micro_batch_size_per_gpu=16, log_prob_use_dynamic_bsz=False,
                  log_prob_max_token_len_per_gpu=16384, exec_log_prob_tokens=196608,
-                 entropy_from_logits_with_chunking=False, entropy_checkpointing=False),  # dp_ref.yaml:43-46
+                 entropy_from_logits_with_chunking=False, entropy_checkpointing=False,  # dp_ref.yaml:43-46
+                 profiler=dict(PROFILER)),
     ),
     # critic.yaml + dp_critic.yaml (used when algorithm.adv_estimator == "gae" or critic.enable)
     critic=dict(
@@ -119,17 +127,19 @@ DEFAULTS = dict(
         optim=dict(lr=1e-5, lr_warmup_steps_ratio=0.0, total_training_steps=-1, weight_decay=0.01, lr_warmup_steps=-1,
                    betas=[0.9, 0.999], eps=1e-8, warmup_style="constant", min_lr_ratio=0.0, num_cycles=0.5),
         model=dict(path="random:qwen2.5-0.5b", override_config={}, use_remove_padding=False, share_prompt_prefix=True,
-                   dtype="bfloat16",
-                   gemm_tuning="auto", seed=4321),
+                   dtype="bfloat16", seed=4321),
         ppo_mini_batch_size=None, ppo_micro_batch_size=None, ppo_micro_batch_size_per_gpu=8,
         forward_micro_batch_size=None, forward_micro_batch_size_per_gpu=16, use_dynamic_bsz=None,
         ppo_max_token_len_per_gpu=32768, forward_max_token_len_per_gpu=32768, ppo_epochs=None, shuffle=None,
         grad_clip=1.0, cliprange_value=0.5, loss_agg_mode=None, ulysses_sequence_parallel_size=1,
         exec_micro_batches=0, exec_activation_gb=110,  # as the actor's (dp_actor.exec_groups)
+        profiler=dict(PROFILER),
     ),
     algorithm=dict(gamma=1.0, lam=1.0, adv_estimator="grpo", norm_adv_by_std_in_grpo=True, use_kl_in_reward=False,
                    kl_penalty="kl", kl_ctrl=dict(type="fixed", kl_coef=0.001, horizon=10000, target_kl=0.1)),
     reward_model=dict(enable=False, reward_manager="synthetic_bernoulli", launch_reward_fn_async=False),
+    # ppo_trainer.yaml:269-290: the steps profiled (start_profile before, stop_profile after; ray_trainer.py:1096-1366)
+    global_profiler=dict(tool=None, steps=None, profile_continuous_steps=False, save_path="outputs/profile"),
     trainer=dict(balance_batch=False, total_epochs=1, total_training_steps=None, critic_warmup=0, n_gpus_per_node=1,
                  nnodes=1, save_freq=-1, test_freq=-1, logger=["console"], project_name="dots_rl_amd",
                  experiment_name="grpo"),

@@ -6,11 +6,11 @@
 //   C(m, n) = sum_k A(m, k) B(n, k)     A(m, k) = a[m * lda + k] (layout "K": row-major (M, K))
 //                                                 a[k * lda + m] (layout "T": row-major (K, M))
 //                                       B(n, k) likewise over (N, K) / (K, N)
-//   forward  A = x (K),  B = W (K)                    bf16 out, + bias / SwiGLU epilogues (as csrc/gemm.hip)
+//   forward  A = x (K),  B = W (K)                    bf16 out, + bias / SwiGLU epilogues
 //   dgrad    A = dy (K), B = W (T: W is (out, in) = (K, N))   bf16 out
 //   wgrad    A = dy (T), B = x (T)                    fp32 out, C (+)= acc
 //
-// Main loop: the 256 x 256 x (2 x 64) ping-pong of csrc/gemm.hip (8 phases per k-tile pair, upper wave group one
+// Main loop: a 256 x 256 x (2 x 64) ping-pong (round 2's forward-only kernel, since folded in here; 8 phases per k-tile pair, upper wave group one
 // barrier behind, counted vmcnt, 2 LDS buffers of 4 half-tiles), with every operand half-tile copied global -> LDS
 // by buffer_load ... lds (one 1-KB wave instruction per 16-B lane): reads outside the operand's byte range return
 // zeros, so row / column / k tails need no clamping (a k tail is zero in a T operand; K operands need K % 128 == 0).

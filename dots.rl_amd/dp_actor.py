@@ -221,14 +221,16 @@ def _concat_rows(group):
             for k in ("input_ids", "attention_mask", "position_ids", "responses")}
 
 
-def exec_groups(cfg, model_cfg, micro_batches, shared_tokens=0.0):
+def exec_groups(cfg, model_cfg, micro_batches, shared_tokens=0.0, resident_bytes=0):
     """Micro-batches that run through the model in one pass. The reference runs one per forward / backward
     (dp_actor.py:392-466, dp_critic.py:214-250); their gradients only add up (each micro-batch's loss carries its own
     scale factor and token count), so consecutive micro-batches may share one pass over their concatenated rows: the
     GEMMs see 2-4x the rows (at 6144 rows the N = 896 projections fill 96 of 256 CUs). ``exec_micro_batches`` fixes
     the group size (1 = the reference's schedule); 0 groups as many as keep the saved activations under
     ``exec_activation_gb``. ``shared_tokens``: the fraction of a micro-batch's tokens that prefix sharing runs once
-    for several rows (they hold no per-token activations of their own; the attention's stay padded)."""
+    for several rows (they hold no per-token activations of their own; the attention's stay padded), the smallest
+    over the micro-batches. ``resident_bytes``: device memory the worker holds for the whole run (parameter stores,
+    gradient, AdamW moments, the reference policy): the plan keeps within 70 % of what they leave."""
     n = int(cfg.get("exec_micro_batches", 1) or 0)
     if n <= 0:
         H, I, L = model_cfg.hidden_size, model_cfg.intermediate_size, model_cfg.num_hidden_layers
@@ -241,7 +243,10 @@ def exec_groups(cfg, model_cfg, micro_batches, shared_tokens=0.0):
             # never plan past 40 % of the device — a static bound (not what happens to be free at the call), so the
             # group size, and with it the GEMM shapes and the fp32 gradient summation order, is the same on every
             # rank, run and resume
-            budget = min(budget, 0.4 * torch.cuda.get_device_properties(torch.cuda.current_device()).total_memory)
+            total = torch.cuda.get_device_properties(torch.cuda.current_device()).total_memory
+            budget = min(budget, 0.4 * total)
+            if resident_bytes:  # what the resident state leaves (the same on every rank: a static bound too)
+                budget = min(budget, 0.7 * max(0, total - resident_bytes))
         toks = max(mb.batch["input_ids"].numel() for mb in micro_batches)
         n = max(1, int(budget // max(1, per_tok * toks)))
     return balanced_groups(micro_batches, n)
@@ -272,6 +277,7 @@ class DataParallelPPOActor:
         self.use_remove_padding = config.get("use_remove_padding", False)
         self.use_fused_kernels = config.get("use_fused_kernels", False)
         self.share_prompt_prefix = config.get("share_prompt_prefix", True)
+        self.exec_stats = {"tokens": 0, "attn_pairs": 0, "lm_rows": 0}
 
     def _forward_micro_batch(self, micro_batch, temperature, calculate_entropy=False):
         """dp_actor.py:90-280: full-sequence forward, logits only at the R positions that predict the response
@@ -291,8 +297,16 @@ class DataParallelPPOActor:
         keep = None
         share = PrefixShare.build(micro_batch["input_ids"], am, R, keep_pads=not self.use_remove_padding) \
             if self.share_prompt_prefix else None
+        T = am.shape[1]
+        if m.training:  # executed work of the update passes (exec_stats: the executed-FLOP MFU beside the reference's)
+            st = self.exec_stats
+            pairs = B * T * (T + 1) // 2  # causal (query, key) pairs the fused attention computes per head
+            if share is not None:  # q_start: the copies skip the shared prompt's queries
+                pairs -= (B - share.groups) * share.S * (share.S + 1) // 2
+            st["tokens"] += share.nnz if share is not None else (int(am.sum()) if self.use_remove_padding else B * T)
+            st["attn_pairs"] += pairs
+            st["lm_rows"] += B * R
         if share is not None or self.use_remove_padding:
-            T = am.shape[1]
             rm = share if share is not None else RmPad(am)
             h = m.hidden_states(micro_batch["input_ids"], am, micro_batch["position_ids"], rm=rm)
             sel = rm.inv.view(B, T)[:, T - R - 1:T - 1].reshape(-1).contiguous()
@@ -313,9 +327,11 @@ class DataParallelPPOActor:
             ent = torch.where(keep, ent, 0.0) if ent is not None else None
         return ent, logp
 
-    def _shared_fraction(self, data):
-        """Fraction of the batch's tokens that prefix sharing runs once for several rows: the first P - 1 tokens of
-        every row whose prompt equals the previous row's (the trainer's interleaved repeat); one device read."""
+    def _shared_fraction(self, data, rows_per_micro_batch=None):
+        """Fraction of the tokens that prefix sharing runs once for several rows: the first P - 1 tokens of every row
+        whose prompt equals the previous row's (the trainer's interleaved repeat). With ``rows_per_micro_batch`` the
+        smallest fraction over the micro-batches of that many rows (a row that opens a micro-batch counts as
+        unshared): the activation plan then holds for the least-shared pass. One device read."""
         if not self.share_prompt_prefix or data is None or len(data) < 2:
             return 0.0
         ids = data.batch["input_ids"]
@@ -323,10 +339,31 @@ class DataParallelPPOActor:
         S = T - data.batch["responses"].shape[1] - 1
         if S <= 0:
             return 0.0
-        return int((ids[1:, :S] == ids[:-1, :S]).all(-1).sum()) * S / (B * T)
+        same = torch.zeros(B, dtype=torch.int64, device=ids.device)
+        same[1:] = (ids[1:, :S] == ids[:-1, :S]).all(-1)
+        n = int(rows_per_micro_batch or B)
+        if n >= B:
+            return int(same.sum()) * S / (B * T)
+        same[::n] = 0
+        k = B // n * n
+        per = same[:k].view(-1, n).sum(-1).tolist() + ([int(same[k:].sum())] if k < B else [])
+        sizes = [n] * (k // n) + ([B - k] if k < B else [])
+        return min(c * S / (m * T) for c, m in zip(per, sizes))
+
+    def resident_bytes(self):
+        """Device memory held for the whole run: this actor's parameter store and AdamW moments plus what the worker
+        registered beside it (``extra_resident_bytes``: the reference policy's store)."""
+        b = self.actor_module.store.memory_bytes() + getattr(self, "extra_resident_bytes", 0)
+        opt = self.actor_optimizer
+        if opt is not None:
+            b += sum(t.numel() * t.element_size() for t in (getattr(opt, "exp_avg", None),
+                                                          getattr(opt, "exp_avg_sq", None)) if t is not None)
+        return b
 
     def _exec_groups(self, micro_batches, mini_batch=None):
-        return exec_groups(self.config, self.actor_module.cfg, micro_batches, self._shared_fraction(mini_batch))
+        rows = len(micro_batches[0]) if micro_batches and not self.config.get("use_dynamic_bsz", False) else None
+        return exec_groups(self.config, self.actor_module.cfg, micro_batches,
+                           self._shared_fraction(mini_batch, rows), self.resident_bytes())
 
     def _log_prob_groups(self, micro_batches, data=None):
         """Forward-only passes: rows are independent, so consecutive micro-batches run as one pass of at most

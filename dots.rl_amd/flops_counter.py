@@ -62,3 +62,20 @@ class FlopsCounter:
         """(achieved TFLOP/s over ``delta_time`` seconds for these valid-token counts, device peak TFLOP/s)."""
         tokens_sum = sum(batch_seqlens)
         return self._fn(tokens_sum, batch_seqlens, delta_time), get_device_flops()
+
+    def executed_flops(self, tokens=0, attn_pairs=0, lm_rows=0):
+        """Forward + backward FLOPs (in TFLOP, the unit estimate_flops' rate and peak share) that the update passes
+        actually executed, from the actor's exec_stats: ``tokens`` packed rows through the decoder layers (prefix
+        sharing runs a prompt group's tokens once; remove-padding skips pads), ``attn_pairs`` causal (query, key) pairs
+        per head the fused attention computed (the copies' skipped prompt queries excluded), ``lm_rows`` rows through
+        the lm_head (the response-predicting positions only). Dense: 6 FLOP per weight and row (2 forward, 4
+        backward); attention: 4 D FLOP per pair and head forward, 10 D backward (dS, dP, dQ, dK, dV and the
+        recomputed S)."""
+        c = self.config
+        H, V, L = c.hidden_size, c.vocab_size, c.num_hidden_layers
+        heads, kv_heads, inter = c.num_attention_heads, c.num_key_value_heads, c.intermediate_size
+        D = getattr(c, "head_dim", None) or H // heads
+        layer_n = H * inter * 3 + H * (heads * D + 2 * kv_heads * D + heads * D)
+        dense = 6 * (layer_n * L * tokens + V * H * lm_rows)
+        attn = 14 * D * heads * L * attn_pairs
+        return (dense + attn) / 1e12

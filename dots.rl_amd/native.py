@@ -904,8 +904,20 @@ def gemm(a, a_layout, b, b_layout, M, N, K, out, beta=False, bias=None, swiglu=F
     return out
 
 
+def _pad_to_64(t, dim):
+    """drl_gemm reduces K in steps of 64 (unless both operands are layout T): a 2-D operand whose reduction extent
+    (``dim``) is not a multiple of 64 gets a zero-padded device copy — zero products leave every fp32 sum exact.
+    Only models with such widths take it (every config of BASELINE.json has H, I, Hq*D multiples of 64)."""
+    n = t.shape[dim]
+    if n % 64 == 0:
+        return t
+    pad = (0, 64 - n % 64) if dim == 1 else (0, 0, 0, 64 - n % 64)
+    return torch.nn.functional.pad(t, pad)
+
+
 def linear_fwd(x, w, bias=None, swiglu=False, out=None, out_gu=None):
     """y = x W^T (+ bias) / SwiGLU(x [Wg | Wu]^T): x (M, K), w (N, K) -> (M, N) or (M, N / 2) bf16."""
+    x, w = _pad_to_64(x, 1), _pad_to_64(w, 1)
     M, K = x.shape
     N = w.shape[0]
     if out is None:
@@ -915,6 +927,7 @@ def linear_fwd(x, w, bias=None, swiglu=False, out=None, out_gu=None):
 
 def linear_dgrad(dy, w, out=None):
     """dx = dy W (F.linear's grad_input): dy (M, N_out) bf16, w (N_out, N_in) read in place -> (M, N_in) bf16."""
+    dy, w = _pad_to_64(dy, 1), _pad_to_64(w, 0)
     M, K = dy.shape
     N = w.shape[1]
     if out is None:
@@ -926,6 +939,7 @@ def linear_dgrad_swiglu_bwd(dy, w, gu, out=None):
     """The down_proj input gradient fused with the SwiGLU backward: da = bf16(dy W) (dy (M, H), w (H, I) read in
     place) -> dgu (M, 2I) = swiglu_bwd(gu, da) with gu (M, 2I) = the forward's [gate | up] (csrc/gemm_sk.hip)."""
     _dev(dy, w, gu)
+    dy, w = _pad_to_64(dy, 1), _pad_to_64(w, 0)
     M, K = dy.shape
     N = w.shape[1]
     assert dy.dtype == w.dtype == gu.dtype == torch.bfloat16 and dy.stride(1) == 1 and w.stride(1) == 1

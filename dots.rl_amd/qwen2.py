@@ -57,6 +57,10 @@ class Qwen2Config:
     # shared: the qkv GEMM epilogues read a constant zero bias instead of a parameter.
     attention_bias: bool = True
     rope_scaling: dict | None = None
+    # HF's attention switch: "eager" = the unfused bf16 attention (fp32 score GEMM on torch bmm + the HIP masked softmax
+    # + PV bmm), an explicit opt-in for head dims the fused kernels do not take (the tiny test models' 16); anything
+    # else ("sdpa", "flash_attention_2", None) = the fused kernels (csrc/flash_attn.hip), which raise when they cannot
+    attn_implementation: str | None = None
     model_type: str = "qwen2"
     extra: dict = field(default_factory=dict)
 
@@ -300,27 +304,36 @@ class ParamStore:
 
 # --------------------------------------------------------------------------------------------- GEMM helpers
 # Every bf16 GEMM of the full-sequence passes — forward, dgrad and wgrad of each projection and of the lm_head — runs
-# on csrc/gemm_sk.hip (drl_gemm: stream-K 256 x 256 ping-pong, weights read in their stored layout for the dgrad,
-# fp32 accumulation into the gradient buffer for the wgrad). DRL_GEMM=hipblaslt routes them to hipBLASLt instead (A/B
-# measurements only); the fp32 parity model (compute_dtype=float32) uses torch's fp32 GEMMs.
-GEMM_BACKEND = os.environ.get("DRL_GEMM", "hip")
+# on csrc/gemm_sk.hip (drl_gemm: 256 x 256 ping-pong tiles, weights read in their stored layout for the dgrad, fp32
+# accumulation into the gradient buffer for the wgrad); a reduction dimension that is not a multiple of 64 is
+# zero-padded on the device (native._pad_cols / _pad_rows) — there is no library fallback. The fp32 parity model
+# (compute_dtype=float32) uses torch's fp32 GEMMs.
 
 
 def _sk(*ts):
-    return GEMM_BACKEND == "hip" and all(t.dtype == torch.bfloat16 and t.is_cuda for t in ts)
+    """bf16 device operands: the drl_gemm path (every bf16 GEMM of the model)."""
+    return all(t.dtype == torch.bfloat16 and t.is_cuda for t in ts)
+
+
+def _fp32_only(t):
+    if t.dtype != torch.float32:
+        raise NotImplementedError(f"dtype {t.dtype}: bf16 GEMMs run on drl_gemm (device tensors); torch GEMMs serve "
+                                  "only the fp32 parity model")
 
 
 def linear(x, w, bias=None):
     """y = x W^T (+ bias) for x (N, in), w (out, in) in the compute dtype (bias added before the single rounding)."""
-    if _sk(x, w) and x.shape[1] % 64 == 0:
+    if _sk(x, w):
         return native.linear_fwd(x, w, bias=bias)
+    _fp32_only(x)
     return torch.addmm(bias, x, w.t()) if bias is not None else x @ w.t()
 
 
 def dgrad(dy, w):
     """dx = dy W (F.linear's grad_input) for dy (N, out), w (out, in)."""
-    if _sk(dy, w) and dy.shape[1] % 64 == 0:
+    if _sk(dy, w):
         return native.linear_dgrad(dy, w)
+    _fp32_only(dy)
     return dy @ w
 
 
@@ -328,10 +341,9 @@ def acc_wgrad(gw, dy, x):
     """gw (out, in) fp32 += dy^T x  with dy (N, out), x (N, in) in the compute dtype (fp32 accumulation in place)."""
     if _sk(dy, x):
         native.linear_wgrad(gw, dy, x)
-    elif dy.dtype == torch.float32:
+    else:
+        _fp32_only(dy)
         gw.addmm_(dy.t(), x)
-    else:  # accumulate in place (C = D, beta = 1): no temporary, no copy of the fp32 gradient
-        torch.addmm(gw, dy.t(), x, out_dtype=torch.float32, out=gw)
 
 
 # The weight gradient of a projection runs on a side stream while its input gradient runs on the current one: the
@@ -354,7 +366,7 @@ def dgrad_wgrad(dy, w, gw, x):
     """dx = dy W and gw (fp32) += dy^T x for one projection (dy (N, out), w (out, in), x (N, in)); returns dx. On
     drl_gemm the weight gradient is launched first on the side stream (its own workspace slot) and joined before
     returning, so callers see plain stream order."""
-    if not (CONCURRENT_WGRAD and _sk(dy, w, x) and dy.shape[1] % 64 == 0):
+    if not (CONCURRENT_WGRAD and _sk(dy, w, x)):
         dx = dgrad(dy, w)
         acc_wgrad(gw, dy, x)
         return dx
@@ -417,12 +429,13 @@ class _Embedding(torch.autograd.Function):
 
 
 # --------------------------------------------------------------------------------------------- decoder layer
-# Full-sequence projections (bias / SwiGLU fused in the epilogue) on drl_gemm (above) for every row count.
-HIP_GEMM_MIN_ROWS = 1  # kept for tests that pin the path
-
-
-def _hip_gemm(x, rows, K):
-    return _sk(x) and rows >= HIP_GEMM_MIN_ROWS and K % 64 == 0
+# Full-sequence projections (bias / SwiGLU fused in the epilogue) on drl_gemm (above) for every row count; torch GEMMs
+# only for the fp32 parity model.
+def _hip_gemm(x):
+    if _sk(x):
+        return True
+    _fp32_only(x)
+    return False
 
 
 def _layer_forward(m, i, x_prev, delta, pos, key_valid, save, cache=None, koff=0, koff_dev=None, rm=None):
@@ -443,7 +456,7 @@ def _layer_forward(m, i, x_prev, delta, pos, key_valid, save, cache=None, koff=0
     rstd1 = torch.empty(B * T, dtype=torch.float32, device=dev) if save is not None else None
     native.add_rmsnorm_fwd(x_prev, delta, x if delta is not None else None, s.w(p + "input_layernorm"), h1, rstd1,
                            cfg.rms_norm_eps)
-    if _hip_gemm(h1, B * T, H):
+    if _hip_gemm(h1):
         qkv = native.linear_fwd(h1.view(B * T, H), s.w(p + "qkv_proj.weight"), bias=m.qkv_bias(i))
     else:
         qkv = torch.addmm(m.qkv_bias(i), h1.view(B * T, H), s.w(p + "qkv_proj.weight").t())
@@ -459,6 +472,18 @@ def _layer_forward(m, i, x_prev, delta, pos, key_valid, save, cache=None, koff=0
     # GEMM + masked softmax + PV GEMM, probabilities kept for the backward) serves the fp32 parity model
     flash_ok = T > 1 and dt == torch.bfloat16 and D in (64, 128) and G <= 8 and key_valid.stride(0) % 4 == 0
     flash = save is None and flash_ok
+    if dt == torch.bfloat16 and not (cache is not None and T == 1):
+        # bf16 full-sequence attention is the fused kernel pair unless the config asks for eager attention: no silent
+        # torch bmm / softmax fallback
+        if cfg.attn_implementation == "eager":
+            flash_ok = flash = False
+        elif not flash_ok:
+            raise NotImplementedError(f"bf16 attention: the fused kernels (csrc/flash_attn.hip) need head_dim 64 / 128 "
+                                      f"and <= 8 query heads per KV head (head_dim {D}, {G} per KV head, T {T}); "
+                                      "attn_implementation='eager' selects the unfused path")
+        if save is not None and cache is None and T % 8 != 0:
+            raise NotImplementedError(f"bf16 training pass over T = {T} positions: the fused attention backward needs "
+                                      "T % 8 == 0 (pad prompt_length + response_length to a multiple of 8)")
     if save is not None and flash_ok and cache is None and T % 8 == 0:
         # training forward: fused attention that saves only the LSE; the backward (flash_attn_bwd)
         # recomputes P and needs a head-dim-major copy of k besides row-major k and v
@@ -540,7 +565,7 @@ def _layer_mlp(m, i, x, attn, save, kbuf, vbuf, P, q, h1, rstd1):
     D = cfg.head_dim
     p = f"layers.{i}."
     dev = x.device
-    if _hip_gemm(attn, B * T, Hq * D):
+    if _hip_gemm(attn):
         o = native.linear_fwd(attn.reshape(B * T, Hq * D), s.w(p + "o_proj"))
     else:
         o = attn.view(B * T, Hq * D) @ s.w(p + "o_proj").t()
@@ -548,7 +573,7 @@ def _layer_mlp(m, i, x, attn, save, kbuf, vbuf, P, q, h1, rstd1):
     h2 = torch.empty(B, T, H, dtype=dt, device=dev)
     rstd2 = torch.empty(B * T, dtype=torch.float32, device=dev) if save is not None else None
     native.add_rmsnorm_fwd(x, o, x2, s.w(p + "post_attention_layernorm"), h2, rstd2, cfg.rms_norm_eps)
-    if _hip_gemm(h2, B * T, H):
+    if _hip_gemm(h2):
         # SwiGLU fused into the gate_up GEMM's epilogue; gu = [g | u] written only when the backward needs it
         gu = torch.empty(B * T, 2 * cfg.intermediate_size, dtype=dt, device=dev) if save is not None else None
         a = native.linear_fwd(h2.view(B * T, H), s.w(p + "gate_up_proj"), swiglu=True, out_gu=gu)
@@ -587,7 +612,7 @@ class _DecoderLayer(torch.autograd.Function):
         lowp = dt == torch.bfloat16  # the bf16 operand of the next dgrad comes out of the norm backward's pass
         dm = g_mlp.to(dt).contiguous().view(N, H)
         # MLP
-        if _sk(dm, sv["gu"]) and dm.shape[1] % 64 == 0:
+        if _sk(dm, sv["gu"]):
             # down_proj dgrad with the SwiGLU backward in its epilogue (d a never written)
             acc_wgrad(s.g(p + "down_proj"), dm, sv["a"])
             dgu = native.linear_dgrad_swiglu_bwd(dm, s.w(p + "down_proj"), sv["gu"])

@@ -323,13 +323,47 @@ class RayPPOTrainer:
             batch = self._train_on(batch, metrics, timing_raw)
         return self._finish_metrics(batch, metrics, timing_raw)
 
+    def _profile_wgs(self):
+        wgs = [self.actor_rollout_wg]
+        if self.use_reference_policy and self.ref_policy_wg is not self.actor_rollout_wg:
+            wgs.append(self.ref_policy_wg)
+        if self.use_critic:
+            wgs.append(self.critic_wg)
+        if self.use_rm and self.rm_wg is not None and hasattr(self.rm_wg, "start_profile"):
+            wgs.append(self.rm_wg)
+        return wgs
+
+    def _start_profiling(self, do_profile: bool) -> None:
+        """ray_trainer.py:1011-1020 (the ref worker is the actor's own colocated worker: started once)."""
+        if do_profile:
+            for i, wg in enumerate(self._profile_wgs()):
+                if i == 0:
+                    wg.start_profile(role="e2e", profile_step=self.global_steps)
+                else:
+                    wg.start_profile()
+
+    def _stop_profiling(self, do_profile: bool) -> None:
+        """ray_trainer.py:1022-1031."""
+        if do_profile:
+            for wg in self._profile_wgs():
+                wg.stop_profile()
+
     def fit(self, num_steps=None):
-        """ray_trainer.py:1050-1405 training loop (synthetic data; no validation/checkpoint by default)."""
+        """ray_trainer.py:1050-1405 training loop (synthetic data; no validation/checkpoint by default), with the
+        global_profiler step selection of :1096-1113 / :1355-1366."""
         total = num_steps or self.total_training_steps or 1
+        gp = self.config.get("global_profiler", {}) or {}
+        steps = gp.get("steps")
+        continuous = bool(gp.get("profile_continuous_steps", False))
         self.global_steps = 1
         history = []
+        prev_p, cur_p = False, (self.global_steps in steps) if steps is not None else False
         for _ in range(total):
+            self._start_profiling((not prev_p and cur_p) if continuous else cur_p)
             m = self.step(self.train_dataloader.next())
+            next_p = (self.global_steps + 1 in steps) if steps is not None else False
+            self._stop_profiling((cur_p and not next_p) if continuous else cur_p)
+            prev_p, cur_p = cur_p, next_p
             history.append(m)
             self.global_steps += 1
         return history

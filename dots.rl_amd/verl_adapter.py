@@ -37,6 +37,8 @@ ACTOR_METHODS = {  # name -> (dispatch, mesh) as fsdp_workers.ActorRolloutRefWor
     "update_actor": ("nd", "actor"),
     "save_checkpoint": ("one_to_all", None),
     "load_checkpoint": ("one_to_all", None),
+    "start_profile": ("one_to_all", None),  # fsdp_workers.py:913-921 (DistProfilerExtension)
+    "stop_profile": ("one_to_all", None),
 }
 CRITIC_METHODS = {  # fsdp_workers.CriticWorker
     "init_model": ("one_to_all", None),
@@ -44,6 +46,8 @@ CRITIC_METHODS = {  # fsdp_workers.CriticWorker
     "update_critic": ("nd", "critic"),
     "save_checkpoint": ("one_to_all", None),
     "load_checkpoint": ("one_to_all", None),
+    "start_profile": ("one_to_all", None),
+    "stop_profile": ("one_to_all", None),
 }
 _DATA_METHODS = {"generate_sequences", "compute_log_prob", "compute_ref_log_prob", "update_actor",
                  "compute_values", "update_critic"}

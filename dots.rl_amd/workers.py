@@ -24,6 +24,7 @@ from .config import RANDOM_MODELS
 from .dp_actor import DataParallelPPOActor, FlatAdamW, lr_schedule
 from .dp_critic import DataParallelPPOCritic
 from .flops_counter import FlopsCounter
+from .profiler import DistProfiler
 from .protocol import DataProto
 from .qwen2 import param_specs, ParamStore, Qwen2Config, Qwen2Model
 from .rollout import MI355XRollout
@@ -63,30 +64,6 @@ def resolve_model_config(model_cfg) -> Qwen2Config:
     return cfg
 
 
-_TUNING_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuning", "tunableop_gfx950.csv")
-
-
-def _enable_gemm_tuning(setting):
-    """Replay hipBLASLt / rocBLAS algorithm choices measured offline for this model's GEMM shapes on MI355X
-    (PyTorch TunableOp results file, read-only: no tuning at run time). ``setting``: "auto" (the shipped
-    gfx950 file when running on gfx950), a CSV path, or None / "off"."""
-    if setting in (None, "off", False):
-        return
-    path = _TUNING_FILE if setting == "auto" else str(setting)
-    if setting == "auto" and "gfx950" not in torch.cuda.get_device_properties(torch.cuda.current_device()).gcnArchName:
-        return
-    if not os.path.exists(path):
-        return
-    import tempfile
-
-    import torch.cuda.tunable as tunable
-
-    tunable.enable(True)
-    tunable.tuning_enable(False)
-    tunable.set_filename(os.path.join(tempfile.gettempdir(), "dotsrl_tunableop%d.csv"), insert_device_ordinal=False)
-    tunable.read_file(path)
-
-
 class ActorRolloutRefWorker(Worker):
     def __init__(self, config, role: str = "actor_rollout_ref", output_device: str = "cuda"):
         super().__init__()
@@ -102,6 +79,9 @@ class ActorRolloutRefWorker(Worker):
         self.dp_rank = dist.get_rank() if dist.is_initialized() else 0
         for mesh in ("actor", "rollout"):
             self._register_dispatch_collect_info(mesh, dp_rank=self.dp_rank, is_collect=True)
+        # fsdp_workers.py:168-196: the actor's profiler config, else the rollout's, else the ref's
+        sec = config.actor if self._is_actor else (config.rollout if self._is_rollout else config.ref)
+        self.profiler = DistProfiler(rank=self.dp_rank, config=sec.get("profiler") if sec is not None else None)
         # fsdp_workers.py:209-242 batch-size normalisation (per-GPU sizes)
         a = config.actor
         if self._is_actor:
@@ -124,7 +104,6 @@ class ActorRolloutRefWorker(Worker):
     @register(dispatch_mode=Dispatch.ONE_TO_ALL)
     def init_model(self):
         cfg = self.config
-        _enable_gemm_tuning(cfg.model.get("gemm_tuning", "auto"))
         mcfg = resolve_model_config(cfg.model)
         self.model_config = mcfg
         self.flops_counter = FlopsCounter(mcfg)
@@ -163,6 +142,8 @@ class ActorRolloutRefWorker(Worker):
             self.ref_store.copy_from(self.store)
             self.ref_module = Qwen2Model(mcfg, self.ref_store)
             self.ref_policy = DataParallelPPOActor(cfg.ref, self.ref_module)
+            if self._is_actor:  # the update's activation plan leaves room for the reference policy's store
+                self.actor.extra_resident_bytes = self.ref_store.memory_bytes()
 
     def _load_hf_weights(self, path):
         from safetensors.torch import load_file
@@ -178,6 +159,7 @@ class ActorRolloutRefWorker(Worker):
 
     # ------------------------------------------------------------------------------------------ hot path
     @register(dispatch_mode=make_nd_compute_dataproto_dispatch_fn(mesh_name="rollout"))
+    @DistProfiler.annotate(color="red", role="rollout_generate")
     def generate_sequences(self, prompts: DataProto):
         """fsdp_workers.py:727-763."""
         prompts = prompts.to(self.device)
@@ -190,6 +172,7 @@ class ActorRolloutRefWorker(Worker):
         return self._out(output)
 
     @register(dispatch_mode=make_nd_compute_dataproto_dispatch_fn(mesh_name="actor"))
+    @DistProfiler.annotate(color="blue", role="actor_compute_log_prob")
     def compute_log_prob(self, data: DataProto):
         """fsdp_workers.py:765-805: old log-probs AND entropy (calculate_entropy=True, :788)."""
         data = data.to(self.device)
@@ -204,6 +187,7 @@ class ActorRolloutRefWorker(Worker):
         return self._out(out)
 
     @register(dispatch_mode=make_nd_compute_dataproto_dispatch_fn(mesh_name="actor"))
+    @DistProfiler.annotate(color="olive", role="ref_compute_log_prob")
     def compute_ref_log_prob(self, data: DataProto):
         """fsdp_workers.py:807-842."""
         data = data.to(self.device)
@@ -216,9 +200,13 @@ class ActorRolloutRefWorker(Worker):
         return self._out(DataProto.from_dict(tensors={"ref_log_prob": output}))
 
     @register(dispatch_mode=make_nd_compute_dataproto_dispatch_fn(mesh_name="actor"))
+    @DistProfiler.annotate(color="red", role="actor_update")
     def update_actor(self, data: DataProto):
         """fsdp_workers.py:684-725 (+ MFU with an MI355X peak, lr schedule step)."""
         data = data.to(self.device)
+        st = self.actor.exec_stats
+        for k in st:
+            st[k] = 0
         t0 = time.perf_counter()
         metrics = self.actor.update_policy(data=data)
         torch.cuda.synchronize()
@@ -227,6 +215,9 @@ class ActorRolloutRefWorker(Worker):
         if ntok:  # fsdp_workers.py:697-701
             est, promised = self.flops_counter.estimate_flops(ntok, dt)
             metrics["perf/mfu/actor"] = est * self.config.actor.ppo_epochs / promised / self.dp_size
+            # what ran: the reference formula counts every row's prompt, with prompt groups run once (prefix sharing)
+            # the executed forward + backward FLOPs of this rank are fewer (flops_counter.executed_flops)
+            metrics["perf/mfu/actor_executed"] = self.flops_counter.executed_flops(**st) / dt / promised
         metrics["perf/max_memory_allocated_gb"] = torch.cuda.max_memory_allocated() / 1024**3
         metrics["perf/max_memory_reserved_gb"] = torch.cuda.max_memory_reserved() / 1024**3
         metrics["perf/cpu_memory_used_gb"] = psutil.virtual_memory().used / 1024**3
@@ -247,6 +238,17 @@ class ActorRolloutRefWorker(Worker):
         sd = _load_store(self.store, self.actor_optimizer, local_path, "model_optim_rng")
         if self._is_rollout:
             self.rollout.calls = int(sd.get("rollout_calls", 0))
+
+    # ------------------------------------------------------------------------------------------ profiling
+    @register(dispatch_mode=Dispatch.ONE_TO_ALL)
+    def start_profile(self, **kwargs) -> None:
+        """fsdp_workers.py:913-916 (profile.py:234-237): start profiling this rank for the current training step."""
+        self.profiler.start(**kwargs)
+
+    @register(dispatch_mode=Dispatch.ONE_TO_ALL)
+    def stop_profile(self) -> None:
+        """fsdp_workers.py:918-921: stop profiling this rank (tool torch: write its trace)."""
+        self.profiler.stop()
 
 
 def _shard_spec(section, mcfg, dp_rank, dp_size):
@@ -326,6 +328,7 @@ class CriticWorker(Worker):
         self.dp_size = dp
         self.dp_rank = dist.get_rank() if dist.is_initialized() else 0
         self._register_dispatch_collect_info("critic", dp_rank=self.dp_rank, is_collect=True)
+        self.profiler = DistProfiler(rank=self.dp_rank, config=config.get("profiler"))  # fsdp_workers.py:927-937
         # fsdp_workers.py:979-1000 batch-size normalisation
         c = config
         c.ppo_mini_batch_size = c.ppo_mini_batch_size * c.get("rollout_n", 1) // dp
@@ -343,7 +346,6 @@ class CriticWorker(Worker):
     def init_model(self):
         """fsdp_workers.py:1003-1123 (_build_critic_model_optimizer + DataParallelPPOCritic)."""
         cfg = self.config
-        _enable_gemm_tuning(cfg.model.get("gemm_tuning", "auto"))
         mcfg = resolve_model_config(cfg.model)
         mcfg.num_labels = 1
         self.model_config = mcfg
@@ -373,6 +375,7 @@ class CriticWorker(Worker):
         return d.to(self.output_device) if self.output_device != "cuda" else d
 
     @register(dispatch_mode=make_nd_compute_dataproto_dispatch_fn(mesh_name="critic"))
+    @DistProfiler.annotate(color="cyan")
     def compute_values(self, data: DataProto):
         """fsdp_workers.py:1237-1258 -> values (bs, R) in the compute dtype."""
         data = data.to(self.device)
@@ -383,6 +386,7 @@ class CriticWorker(Worker):
         return self._out(DataProto.from_dict(tensors={"values": values}))
 
     @register(dispatch_mode=make_nd_compute_dataproto_dispatch_fn(mesh_name="critic"))
+    @DistProfiler.annotate(color="pink")
     def update_critic(self, data: DataProto):
         """fsdp_workers.py:1260-1292 (+ perf/mfu/critic with the MI355X peak, critic/lr, lr schedule step)."""
         data = data.to(self.device)
@@ -407,3 +411,14 @@ class CriticWorker(Worker):
     @register(dispatch_mode=Dispatch.ONE_TO_ALL)
     def load_checkpoint(self, local_path, hdfs_path=None, del_local_after_load=True):
         _load_store(self.store, self.critic_optimizer, local_path, "critic_model_optim")
+
+    # ------------------------------------------------------------------------------------------ profiling
+    @register(dispatch_mode=Dispatch.ONE_TO_ALL)
+    def start_profile(self, **kwargs) -> None:
+        """fsdp_workers.py:913-916 (profile.py:234-237): start profiling this rank for the current training step."""
+        self.profiler.start(**kwargs)
+
+    @register(dispatch_mode=Dispatch.ONE_TO_ALL)
+    def stop_profile(self) -> None:
+        """fsdp_workers.py:918-921: stop profiling this rank (tool torch: write its trace)."""
+        self.profiler.stop()

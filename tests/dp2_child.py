@@ -22,7 +22,7 @@ def build_config(world, shard=False):
         "actor_rollout_ref.rollout.n=1", "actor_rollout_ref.actor.ppo_mini_batch_size=4",
         "actor_rollout_ref.actor.ppo_micro_batch_size_per_gpu=1", "actor_rollout_ref.actor.optim.lr=1e-4",
         f"actor_rollout_ref.model.path={os.path.join(HERE, 'golden', 'tiny_qwen2')}",
-        "actor_rollout_ref.model.dtype=float32", "actor_rollout_ref.model.gemm_tuning=off",
+        "actor_rollout_ref.model.dtype=float32",
     ]).actor_rollout_ref
 
 

@@ -77,16 +77,28 @@ def embed_rows_index(input_ids):
     return np.unique(np.concatenate([touched, sample_index("model.embed_tokens.weight", CFG["vocab_size"] * H)]))
 
 
-def batch():
+GROUPS, N_PER = 4, 4  # the grouped batch: 4 prompts x n = 4 samples
+
+
+def batch(grouped=False):
     """input_ids, attention_mask, position_ids, responses, response_mask, old_log_probs noise, ref noise and
-    advantages: left-padded prompts (0..11 pads), responses of 6..48 tokens ending in EOS then pad."""
-    g = np.random.Generator(np.random.PCG64(SEED + 1))
+    advantages: left-padded prompts (0..11 pads), responses of 6..48 tokens ending in EOS then pad.
+
+    ``grouped``: the GRPO layout the trainer hands the actor (ray_trainer.py:1119 ``repeat(n, interleave=True)``):
+    GROUPS distinct prompts, each repeated N_PER times in consecutive rows (identical prompt tokens, pads and
+    positions), every row with its own response; its own seeded stream (the ungrouped batch is unchanged)."""
+    g = np.random.Generator(np.random.PCG64(SEED + (2 if grouped else 1)))
     V, pad, eos = CFG["vocab_size"], CFG["pad_token_id"], CFG["eos_token_id"]
     ids = torch.from_numpy(g.integers(0, 151643, (B, P + R), dtype=np.int64))
     am = torch.ones(B, P + R, dtype=torch.int64)
     npad = g.integers(0, 12, B)
     rlen = g.integers(6, R + 1, B)
     rlen[0] = R  # one full-length response (no EOS inside)
+    if grouped:
+        assert GROUPS * N_PER == B
+        lead = np.repeat(np.arange(GROUPS) * N_PER, N_PER)  # row -> its group's first row
+        ids[:, :P] = ids[torch.from_numpy(lead), :P]
+        npad = npad[lead]
     for b in range(B):
         am[b, :npad[b]] = 0
         ids[b, :npad[b]] = pad

@@ -1366,7 +1366,7 @@ def gen_lr_schedule():
                                             "ref": "fsdp_workers.py:461-486, torch_functional.py:509-575"})
 
 
-def gen_bf16_update():
+def gen_bf16_update(grouped=False):
     """The reference DataParallelPPOActor (dp_actor.py:300-482) at Qwen2.5-0.5B width (4 layers, full vocabulary,
     tied lm_head; tests/golden/bf16_update.py) run twice on the same inputs: in fp32 (autocast disabled, as
     _ref_actor) and under its own torch.autocast(bf16) (dp_actor.py:110; on this CPU box the device name is 'cpu',
@@ -1375,7 +1375,11 @@ def gen_bf16_update():
     elements (captured when _optimizer_step calls clip_grad_norm_: the accumulated gradient of the 2 micro-batches,
     before clipping),
     and the same sample of the parameter update. The bf16-vs-fp32 difference of the reference itself is the
-    yardstick the production bf16 path is held to (tests/test_bf16_update_gpu.py)."""
+    yardstick the production bf16 path is held to (tests/test_bf16_update_gpu.py).
+
+    ``grouped``: the same on bf16_update.batch(grouped=True) — 4 prompts x n = 4 in the trainer's interleaved repeat
+    — so the GPU side runs prefix sharing (qwen2.PrefixShare, flash q_start, drl_sum_rows) under the same bar; the
+    reference itself runs every row in full (it has no prefix sharing) -> bf16_update_grouped.npz."""
     import bf16_update as bu
     import verl.workers.actor.dp_actor as ref_dp
     from transformers import Qwen2Config, Qwen2ForCausalLM
@@ -1387,12 +1391,12 @@ def gen_bf16_update():
     ref_dp.logprobs_from_logits = lambda logits, labels, inplace_backward=True: vF.logprobs_from_logits_v2(
         logits.float(), labels)
     sd = bu.make_state_dict()
-    bt = bu.batch()
+    bt = bu.batch(grouped)
     lr = 1e-5
     acfg = _actor_cfg(entropy_coeff=0.001, ppo_mini_batch_size=bu.B, ppo_micro_batch_size_per_gpu=bu.B // 2)
     arrays = {k: v for k, v in bt.items() if not k.startswith("noise")}
     meta = {"config": dict(acfg, policy_loss=dict(acfg["policy_loss"])), "lr": lr, "model": bu.CFG,
-            "weight_checksum": bu.checksum(sd), "runs": {}}
+            "weight_checksum": bu.checksum(sd), "runs": {}, "grouped": bool(grouped)}
     old = ref = None
     embed_idx = bu.embed_rows_index(bt["input_ids"].numpy())
     for mode in ("fp32", "bf16"):
@@ -1446,7 +1450,11 @@ def gen_bf16_update():
     arrays["old_log_probs"], arrays["ref_log_prob"] = old, ref
     meta["ref"] = ("dp_actor.py:110 (autocast bf16), 300-482 (compute_log_prob, update_policy), 282-298 (clip + step); "
                    "fsdp_workers.py:454-459 (AdamW); HF Qwen2ForCausalLM, SDPA attention")
-    _save("bf16_update.npz", arrays, meta)
+    _save("bf16_update_grouped.npz" if grouped else "bf16_update.npz", arrays, meta)
+
+
+def gen_bf16_update_grouped():
+    gen_bf16_update(grouped=True)
 
 
 def gen_deep():

@@ -188,7 +188,7 @@ def test_grpo_fit_step_matches_reference(ci):
         "actor_rollout_ref.rollout.log_prob_micro_batch_size_per_gpu=4",
         "actor_rollout_ref.ref.log_prob_micro_batch_size_per_gpu=4", f"actor_rollout_ref.actor.optim.lr={m['lr']}",
         f"actor_rollout_ref.model.path={TINY}", "actor_rollout_ref.model.dtype=float32",
-        "actor_rollout_ref.model.gemm_tuning=off", "reward_model.enable=True", "reward_model.reward_manager=naive",
+        "reward_model.enable=True", "reward_model.reward_manager=naive",
         "trainer.balance_batch=False", "algorithm.adv_estimator=grpo",
     ])
     trainer = RayPPOTrainer(cfg, tokenizer=StubTokenizer(), rm_wg=_PresetRM(m["rm_scores"]),

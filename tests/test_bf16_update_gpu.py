@@ -38,13 +38,24 @@ sys.path.insert(0, os.path.join(HERE, "golden"))
 import bf16_update as bu  # noqa: E402
 
 
-@pytest.fixture(scope="module")
-def fixture():
+_SD = {}
+
+
+@pytest.fixture(scope="module", params=["bf16_update.npz", "bf16_update_grouped.npz"])
+def fixture(request):
+    """The fixture with 16 distinct prompts, and the grouped one (4 prompts x n = 4, interleaved as the trainer
+    repeats them): there the default model.share_prompt_prefix runs each prompt once (qwen2.PrefixShare, flash
+    q_start, drl_sum_rows) while the reference ran every row in full — the driver bench's production configuration
+    under the same bar."""
     from conftest import load_golden
 
-    z, meta = load_golden("bf16_update.npz")
-    sd = bu.make_state_dict()
+    z, meta = load_golden(request.param)
+    if "sd" not in _SD:
+        _SD["sd"] = bu.make_state_dict()
+    sd = _SD["sd"]
     assert bu.checksum(sd) == meta["weight_checksum"]
+    ref = bu.batch(grouped=bool(meta.get("grouped", False)))
+    assert np.array_equal(ref["input_ids"].numpy(), z["input_ids"]), "fixture inputs differ from bf16_update.batch()"
     return z, meta, sd
 
 
@@ -102,6 +113,13 @@ def _run(z, meta, sd, extra):
     opt.step = step
     actor = DataParallelPPOActor(acfg, model, opt)
     T = lambda k: torch.from_numpy(np.ascontiguousarray(z[k])).cuda()  # noqa: E731
+    # the grouped fixture must take the prefix-sharing path (and the other one must not)
+    from dots.rl_amd.qwen2 import PrefixShare
+
+    assert actor.share_prompt_prefix
+    sh = PrefixShare.build(T("input_ids")[:bu.B // 2], T("attention_mask")[:bu.B // 2], bu.R,
+                           keep_pads=not acfg.get("use_remove_padding", False))
+    assert (sh is not None) == bool(meta.get("grouped", False)), "prefix sharing engaged on the wrong fixture"
     data = DataProto.from_dict({k: T(k) for k in ("input_ids", "attention_mask", "position_ids", "responses")},
                                meta_info={"micro_batch_size": bu.B // 2, "temperature": 1.0, "use_dynamic_bsz": False})
     lp, ent = actor.compute_log_prob(data, calculate_entropy=True)

@@ -82,3 +82,24 @@ def test_update_step_bit_reproducible():
         trainer.fit(num_steps=1)
         masters.append(trainer.actor_rollout_wg.worker.store.master.clone())
     assert torch.equal(masters[0], masters[1]), (masters[0] - masters[1]).abs().max().item()
+
+
+def test_profile_step_records_the_hot_method_ranges(tmp_path):
+    """start_profile / stop_profile around global_profiler.steps (ray_trainer.py:1096-1366) with the torch tool: the
+    written trace holds the four annotated hot methods of the step (fsdp_workers.py:685,728,766,808) and their
+    device kernels; a step outside the list writes nothing."""
+    import json
+
+    trainer = _trainer("grpo", ["global_profiler.steps=[2]", "actor_rollout_ref.actor.profiler.tool=torch",
+                                "actor_rollout_ref.actor.profiler.enable=True",
+                                "actor_rollout_ref.actor.profiler.all_ranks=True",
+                                f"actor_rollout_ref.actor.profiler.save_path={tmp_path}"])
+    trainer.fit(num_steps=2)
+    prof = trainer.actor_rollout_wg.worker.profiler
+    assert prof.traces == [str(tmp_path / "prof_step_2_rank_0.json")]
+    with open(prof.traces[0]) as f:
+        ev = json.load(f)["traceEvents"]
+    names = {e.get("name") for e in ev}
+    assert {"generate_sequences", "compute_log_prob", "compute_ref_log_prob", "update_actor"} <= names, names
+    assert any(str(e.get("name", "")).startswith("void drl::") or "drl::" in str(e.get("name", "")) for e in ev
+               if e.get("cat") == "kernel"), "no HIP kernel of this package in the trace"

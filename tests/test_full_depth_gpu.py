@@ -113,14 +113,10 @@ def test_fp32_full_depth_matches_reference(ref, weights):
     np.testing.assert_allclose(ent, z["entropy"], rtol=1e-4, atol=atol)
 
 
-@pytest.mark.parametrize("packed,hip_gemm_rows", [(True, None), (False, None), (True, 1), (False, 1)])
-def test_bf16_full_depth_margin_checked(ref, weights, packed, hip_gemm_rows, monkeypatch):
-    """hip_gemm_rows=1: every full-sequence qkv / o_proj / gate_up projection (prefill, teacher-forced pass, the
-    unpacked decode step) on csrc/gemm.hip's ping-pong GEMM, held to the same reference margins"""
-    from dots.rl_amd import qwen2
-
-    if hip_gemm_rows is not None:
-        monkeypatch.setattr(qwen2, "HIP_GEMM_MIN_ROWS", hip_gemm_rows)
+@pytest.mark.parametrize("packed", [True, False])
+def test_bf16_full_depth_margin_checked(ref, weights, packed):
+    """Every full-sequence projection (prefill, the teacher-forced pass, the unpacked decode step) on drl_gemm
+    (csrc/gemm_sk.hip), the decode step packed (decode_gemm.hip) or unpacked, held to the reference margins"""
     z, meta = ref
     bound = 2.0 * meta["cpu_bf16_gap_err_max"]
     gaps = z["top2_gap"]
@@ -144,20 +140,25 @@ def test_bf16_full_depth_margin_checked(ref, weights, packed, hip_gemm_rows, mon
     print(f"bf16 {'packed' if packed else 'unpacked'} rollout: tokens matching the fp32 reference per row {matched}")
 
 
-@pytest.mark.parametrize("rows", [4, 512])
-def test_bf16_packed_decode_teacher_forced(ref, weights, rows):
+@pytest.mark.parametrize("rows,group", [(4, 1), (512, 1), (512, 128)])
+def test_bf16_packed_decode_teacher_forced(ref, weights, rows, group):
     """The decode path the bench runs — prefill, then qwen2.PackedDecode's graphed step (decode_gemm.hip projections,
     decode_mfma_kernel attention, dec_rmsnorm, the step prologue) — fed the reference's own tokens (teacher forcing,
     hf_rollout.py:112-171 generate's inputs), so every step sees the reference context; its lm_head logits against
     the reference HF fp32 logits of the same step. rows = 512: the fixture's 4 rows tiled 128 times, so the decode
     planner picks the bench's 512-row kernels (decode_gemm_lds / decode_gemm_tiled / decode_mfma_kernel<64, 2>,
-    profiles/r03_decode_step_512rows.txt); every row is held to the bound of its own source row."""
-    from dots.rl_amd.qwen2 import KVCache, PackedDecode
+    profiles/r03_decode_step_512rows.txt); every row is held to the bound of its own source row.
+    group = 128: the bench's prompt groups (rollout.enable_prefix_caching) — each source row repeated 128 times in
+    consecutive rows, its prompt prefilled once into cache row p and shared by the group (KVCache.share_prompts), so
+    the decode attention is decode_group_kernel (csrc/flash_attn.hip: one workgroup per prompt, KV head and 4-row
+    column tile), the kernel the bench's rollout spends the most decode time in."""
+    from dots.rl_amd.qwen2 import KVCache, KVCacheRows, PackedDecode
 
     z0, meta = ref
-    rep = rows // z0["prompt_ids"].shape[0]
-    z = {k: (np.concatenate([z0[k]] * rep, 0) if z0[k].ndim >= 1 and z0[k].shape[0] == z0["prompt_ids"].shape[0]
-             else z0[k]) for k in z0.files if k != "__meta__"}
+    n0 = z0["prompt_ids"].shape[0]
+    rep = rows // n0
+    tile = (lambda a: np.repeat(a, rep, 0)) if group > 1 else (lambda a: np.concatenate([a] * rep, 0))
+    z = {k: (tile(z0[k]) if z0[k].ndim >= 1 and z0[k].shape[0] == n0 else z0[k]) for k in z0.files if k != "__meta__"}
     model = _model(weights, torch.bfloat16)
     ids, am, pos = T(z["prompt_ids"]), T(z["prompt_attention_mask"]), T(z["prompt_position_ids"])
     B, P = ids.shape
@@ -168,7 +169,17 @@ def test_bf16_packed_decode_teacher_forced(ref, weights, rows):
     with torch.no_grad():
         cache = KVCache(model.cfg, B, P + R, ids.device, torch.bfloat16)
         cache.valid[:, :P] = am.to(torch.uint8)
-        h = model.prefill(cache, ids, am, pos)
+        if group > 1:  # MI355XRollout.generate_sequences' prefix-caching prefill (rollout.py:104-109)
+            assert group == rep and P % 32 == 0
+            Bu = B // group
+            cache.valid[:Bu, :P] = am[::group].to(torch.uint8)
+            h = model.prefill(KVCacheRows(cache, 0, Bu), ids[::group].contiguous(), am[::group].contiguous(),
+                              pos[::group].contiguous())
+            cache.share_prompts(group, P)
+            assert cache.group == group and cache.shared == P
+            h = h.repeat_interleave(group, 0)
+        else:
+            h = model.prefill(cache, ids, am, pos)
         logits = [model.logits(h).float()]
         packed = PackedDecode(model, B)
         t_dev = torch.ones(1, dtype=torch.int64, device=ids.device)

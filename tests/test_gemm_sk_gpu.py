@@ -71,6 +71,42 @@ def test_dgrad_reads_weight_in_place():
     torch.testing.assert_close(dx.float(), ref.to(torch.bfloat16).float(), rtol=8e-3, atol=1e-3)
 
 
+@pytest.mark.parametrize("K", [72, 840, 1000])
+def test_linear_reduction_not_multiple_of_64(K):
+    """A model width that is not a multiple of 64 (the K tail): forward (with bias), input gradient and the SwiGLU-
+    backward input gradient stay on drl_gemm through zero-padded operand copies (native._pad_to_64), no library
+    fallback (qwen2.linear / dgrad)."""
+    from dots.rl_amd import qwen2
+
+    g = torch.Generator(device="cuda").manual_seed(K)
+    x = torch.randn(300, K, generator=g, device="cuda").to(torch.bfloat16)
+    w = (torch.randn(520, K, generator=g, device="cuda") * 0.05).to(torch.bfloat16)
+    bias = torch.randn(520, generator=g, device="cuda").to(torch.bfloat16)
+    y = qwen2.linear(x, w, bias=bias)
+    ref = (x.double() @ w.double().t() + bias.double()).to(torch.bfloat16)
+    torch.testing.assert_close(y.float(), ref.float(), rtol=8e-3, atol=1e-3)
+    dy = torch.randn(300, K, generator=g, device="cuda").to(torch.bfloat16)
+    wt = (torch.randn(K, 520, generator=g, device="cuda") * 0.05).to(torch.bfloat16)
+    dx = qwen2.dgrad(dy, wt)
+    torch.testing.assert_close(dx.float(), (dy.double() @ wt.double()).to(torch.bfloat16).float(), rtol=8e-3,
+                               atol=1e-3)
+    gu = torch.randn(300, 2 * 512, generator=g, device="cuda").to(torch.bfloat16)
+    wd = (torch.randn(K, 512, generator=g, device="cuda") * 0.05).to(torch.bfloat16)
+    dgu = native.linear_dgrad_swiglu_bwd(dy, wd, gu)
+    da = native.linear_dgrad(dy, wd)
+    want = torch.empty_like(gu)
+    native.swiglu_bwd(gu, da, want)
+    assert torch.equal(dgu, want)
+
+
+def test_bf16_path_has_no_torch_fallback():
+    from dots.rl_amd import qwen2
+
+    with pytest.raises(NotImplementedError):
+        qwen2.linear(torch.randn(4, 64, dtype=torch.float16, device="cuda"),
+                     torch.randn(8, 64, dtype=torch.float16, device="cuda"))
+
+
 @pytest.mark.parametrize("M", [256, 777, 6144])
 def test_forward_epilogues(M):
     g = torch.Generator(device="cuda").manual_seed(M)

@@ -30,6 +30,8 @@ def build(dtype=torch.float32, trainable=True):
     from dots.rl_amd.qwen2 import ParamStore, Qwen2Config, Qwen2Model
 
     cfg = Qwen2Config.from_dict(json.load(open(os.path.join(TINY, "config.json"))))
+    if dtype == torch.bfloat16 and cfg.head_dim not in (64, 128):
+        cfg.attn_implementation = "eager"  # head_dim 16: the fused attention kernels take 64 / 128
     store = ParamStore(cfg, "cuda", compute_dtype=dtype, trainable=trainable)
     store.load_state_dict_hf(load_file(os.path.join(TINY, "model.safetensors")))
     return cfg, store, Qwen2Model(cfg, store)

@@ -136,3 +136,24 @@ def test_rollout_debug_metrics_match_reference(golden):
         assert set(got) == set(case["metrics"])
         for k, v in case["metrics"].items():
             assert got[k] == pytest.approx(v, rel=1e-5, abs=1e-7), k
+
+
+def test_executed_flops_counts_what_ran():
+    """FlopsCounter.executed_flops (perf/mfu/actor_executed): with every row's tokens executed, no prefix sharing and
+    the lm_head over every position, it equals the reference formula's dense part + this repository's attention
+    pricing (4 D forward + 10 D backward per causal pair and head, against the reference's 12 D per full s^2)."""
+    from dots.rl_amd.config import QWEN25_05B
+    from dots.rl_amd.flops_counter import FlopsCounter
+    from dots.rl_amd.qwen2 import Qwen2Config
+
+    c = Qwen2Config.from_dict(QWEN25_05B)
+    fc = FlopsCounter(c)
+    B, T = 4, 768
+    dense_ref = fc._estimate_qwen2_flops(B * T, [0] * B, 1.0)  # sq = 0: the dense part only (TFLOP)
+    # the reference counts the embedding as a second V x H matrix; executed_flops counts only the lm_head GEMM
+    emb = 6 * c.vocab_size * c.hidden_size * B * T / 1e12
+    got = fc.executed_flops(tokens=B * T, attn_pairs=0, lm_rows=B * T)
+    assert abs(got - (dense_ref - emb)) < 1e-9 * dense_ref
+    pairs = B * T * (T + 1) // 2
+    att = fc.executed_flops(attn_pairs=pairs)
+    assert abs(att - 14 * c.head_dim * c.num_attention_heads * c.num_hidden_layers * pairs / 1e12) < 1e-12

@@ -66,8 +66,6 @@ def main():
     ap.add_argument("--only", nargs="*", default=None, help="only these shape names (e.g. gate_up_wgrad o_wgrad)")
     ap.add_argument("--groups", type=int, nargs="*", default=None, help="also time these rasterization groups")
     args = ap.parse_args()
-    from dots.rl_amd.workers import _enable_gemm_tuning
-    _enable_gemm_tuning("auto")
     dev, bf = "cuda", torch.bfloat16
     g = torch.Generator(device=dev).manual_seed(0)
     for name, kind, M, N, K in shapes(args.quick, args.rows, args.decode):

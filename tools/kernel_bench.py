@@ -361,8 +361,6 @@ def fused_linear(Ns=(2048, 4096), H=896, V=151936):
 def decode_gemm(Ms=(32, 64, 128, 256, 512)):
     """Decode projections on fragment-packed operands (csrc/decode_gemm.hip) vs hipBLASLt at the Qwen2.5-0.5B
     shapes, weights rotating over > 600 MB of copies (each call streams W from HBM), graph-timed."""
-    from dots.rl_amd.workers import _enable_gemm_tuning
-    _enable_gemm_tuning("auto")
     dev, bf = "cuda", torch.bfloat16
     shapes = [("qkv_proj", 1152, 896, False), ("o_proj", 896, 896, False), ("gate_up_swiglu", 9728, 896, True),
               ("down_proj", 896, 4864, False)]
@@ -418,10 +416,8 @@ def decode_gemm(Ms=(32, 64, 128, 256, 512)):
 
 
 def train_gemms(Ms=(6144, 12288)):
-    """hipBLASLt on the transformer GEMMs of the log-prob / update micro-batches (replayed TunableOp choices):
+    """hipBLASLt on the transformer GEMMs of the log-prob / update micro-batches (hipBLASLt's default heuristics; a comparison only):
     forward y = x W^T, backward dx = dy W and dW += dy^T x (fp32 accumulate in place)."""
-    from dots.rl_amd.workers import _enable_gemm_tuning
-    _enable_gemm_tuning("auto")
     dev, bf = "cuda", torch.bfloat16
     res = []
     for name, N, K in (("qkv", 1152, 896), ("o_proj", 896, 896), ("gate_up", 9728, 896), ("down", 896, 4864)):
