@@ -350,10 +350,18 @@ __global__ __launch_bounds__(256) void decode_gemm_tiled_kernel(DgArgs a) {
 // "Pipelining across barriers"): counted vmcnt (own copies of this stage landed, the next stages' still in
 // flight) -> lgkmcnt(0) + raw s_barrier (everyone's copies landed; everyone's reads of the buffer about to be
 // refilled are done) -> refill the oldest buffer -> MFMAs from this stage's buffer. One __shared__ array.
-template <int WR, int WT, int WB, int TB, int EPI, int KST = 2>
+// NBUF: stage buffers, NBUF - 1 stages in flight ahead of the one consumed (round 5: 3 -> up to 6 — at 2 stages ahead
+// a workgroup kept 24 KB of copies in flight and each stage waited out most of an L2 / HBM round trip).
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int WR, int WT, int WB, int TB, int EPI, int KST = 2, int NBUF = 3>
 __global__ __launch_bounds__(64 * WR * WT) void decode_gemm_lds_kernel(DgArgs a) {
   constexpr int NW = WR * WT, RB = WR * WB, TT = WT * TB, FR = RB + TT;
-  constexpr int NBUF = 3;
+  static_assert(NBUF >= 3, "at least one stage ahead besides the one being refilled");
   constexpr int PER_WAVE = KST * FR / NW;  // LDS-DMA instructions per wave and stage
   static_assert(KST * FR % NW == 0, "copies must divide evenly over the waves");
   __shared__ __attribute__((aligned(16))) uint16_t lds[NBUF * KST * FR * 512];
@@ -393,22 +401,14 @@ __global__ __launch_bounds__(64 * WR * WT) void decode_gemm_lds_kernel(DgArgs a)
   for (int b = 0; b < WB; ++b)
 #pragma unroll
     for (int t = 0; t < TB; ++t) acc[b][t] = f32x16{};
-  issue(0);
-  issue(1);
+#pragma unroll
+  for (int j = 0; j < NBUF - 1; ++j) issue(j);
   for (int i = 0; i < nst; ++i) {
-    // own copies of stage i landed (stage i + 1's PER_WAVE may still be in flight)
-    if constexpr (PER_WAVE == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    else if constexpr (PER_WAVE == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-    else if constexpr (PER_WAVE == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else if constexpr (PER_WAVE == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-    else if constexpr (PER_WAVE == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    else if constexpr (PER_WAVE == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if constexpr (PER_WAVE == 9) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
-    else static_assert(PER_WAVE == 2 || PER_WAVE == 3 || PER_WAVE == 4 || PER_WAVE == 5 || PER_WAVE == 6 ||
-                       PER_WAVE == 8 || PER_WAVE == 9, "vmcnt table");
+    // own copies of stage i landed (stages i + 1 .. i + NBUF - 2, PER_WAVE each, may still be in flight)
+    wait_vmcnt<(NBUF - 2) * PER_WAVE>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    issue(i + 2);  // into the buffer read in iteration i - 1 (every wave is past it)
+    issue(i + NBUF - 1);  // into the buffer read in iteration i - 1 (every wave is past it)
     const uint16_t* buf = lds + (i % NBUF) * (KST * FR * 512);
 #pragma unroll
     for (int j = 0; j < KST; ++j) {
@@ -671,12 +671,15 @@ bool plan_decode_gemm(int64_t M, int64_t N, int64_t K, int epi, DgPlan& p) {
 
 // tiled path: (WB, TB, WW, WT, lds) configurations instantiated (lds: the LDS-staged kernel, WW x WT waves)
 struct DtShape { int wb, tb, ww, wt, lds; };
+// 17-22 (round 5): LDS-staged with deeper rings (NBUF stage buffers, NBUF - 1 stages in flight), larger tiles
 // 9-13: larger token panels per workgroup (the activation panel staged once for more weight rows' MFMAs), round 4;
 // 14-16: LDS-staged with 4 k-steps per stage (half the barriers, twice the LDS: fewer resident workgroups)
 constexpr DtShape kTiled[] = {{2, 2, 4, 2, 1}, {2, 2, 2, 2, 1}, {1, 2, 2, 2, 1}, {2, 1, 2, 2, 1},
                               {2, 2, 2, 2, 0}, {2, 2, 4, 1, 0}, {1, 2, 2, 2, 0}, {1, 2, 4, 1, 0}, {1, 1, 2, 2, 0},
                               {2, 2, 1, 4, 1}, {2, 4, 2, 2, 1}, {1, 4, 2, 2, 1}, {2, 4, 1, 4, 1}, {2, 4, 2, 2, 0},
-                              {1, 2, 2, 2, 1}, {2, 1, 2, 2, 1}, {2, 2, 2, 2, 1}};
+                              {1, 2, 2, 2, 1}, {2, 1, 2, 2, 1}, {2, 2, 2, 2, 1},
+                              {2, 2, 4, 2, 1}, {2, 2, 2, 2, 1}, {1, 2, 2, 2, 1}, {2, 1, 2, 2, 1}, {2, 2, 2, 2, 1},
+                              {1, 2, 2, 2, 1}};
 constexpr int kNumTiled = static_cast<int>(sizeof(kTiled) / sizeof(kTiled[0]));
 int g_dt_force = -1;  // tuning: force configuration index (drl_decode_gemm_force_tiled), -1 = planner
 int g_dt_min_rows = 192;  // tuning: smallest M for the tiled path
@@ -761,6 +764,12 @@ void launch_dt(const DgArgs& a, const DgPlan& p, hipStream_t s) {
     case 14: hipLaunchKernelGGL((decode_gemm_lds_kernel<2, 2, 1, 2, EPI, 4>), grid, dim3(256), 0, s, a); break;
     case 15: hipLaunchKernelGGL((decode_gemm_lds_kernel<2, 2, 2, 1, EPI, 4>), grid, dim3(256), 0, s, a); break;
     case 16: hipLaunchKernelGGL((decode_gemm_lds_kernel<2, 2, 2, 2, EPI, 4>), grid, dim3(256), 0, s, a); break;
+    case 17: hipLaunchKernelGGL((decode_gemm_lds_kernel<4, 2, 2, 2, EPI, 2, 6>), grid, dim3(512), 0, s, a); break;
+    case 18: hipLaunchKernelGGL((decode_gemm_lds_kernel<2, 2, 2, 2, EPI, 2, 6>), grid, dim3(256), 0, s, a); break;
+    case 19: hipLaunchKernelGGL((decode_gemm_lds_kernel<2, 2, 1, 2, EPI, 2, 6>), grid, dim3(256), 0, s, a); break;
+    case 20: hipLaunchKernelGGL((decode_gemm_lds_kernel<2, 2, 2, 1, EPI, 4, 5>), grid, dim3(256), 0, s, a); break;
+    case 21: hipLaunchKernelGGL((decode_gemm_lds_kernel<2, 2, 2, 2, EPI, 4, 4>), grid, dim3(256), 0, s, a); break;
+    case 22: hipLaunchKernelGGL((decode_gemm_lds_kernel<2, 2, 1, 2, EPI, 4, 4>), grid, dim3(256), 0, s, a); break;
     default: hipLaunchKernelGGL((decode_gemm_tiled_kernel<2, 4, 2, 2, EPI>), grid, dim3(256), 0, s, a); break;
   }
 }

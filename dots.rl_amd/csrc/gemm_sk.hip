@@ -967,7 +967,16 @@ int drl_gemm(const void* a, int64_t lda, int32_t a_layout, const void* b, int64_
   int mode = g_sk.mode;
   int S = 1;
   if (mode == 0 && g.n_tiles * 2 <= cap && g.P >= 256 && !epi_is_swiglu(epilogue)) {
-    mode = 1;  // very long K over few tiles (the lm_head dgrad: 32 tiles x 1187 k-pairs): stream-K measured best
+    if (g.n_tiles * 12 <= cap && !epi_whole_tiles(epilogue)) {
+      // very long K over at most a twelfth of the CUs in tiles (the small projections' weight gradients over the
+      // update pass's tokens: o 16, qkv 20 tiles x 642 k-pairs): uniform split-K over every CU, up to 16 slices —
+      // 246 -> 198 us (o, 12 slices) and 340 -> 264 us (qkv, 8 slices) against stream-K, whose tile heads add the
+      // other workgroups' slabs one after another (profiles/r05_gemm_wgrad_splitk.jsonl)
+      S = std::min(16, cap / g.n_tiles);
+      mode = 3;
+    } else {
+      mode = 1;  // very long K over few tiles (the lm_head dgrad: 32 tiles x 1187 k-pairs): stream-K measured best
+    }
   } else if (mode == 0 || mode == 3) {
     // at most 8 splits of >= 6 k-pairs each (profiles/r03_gemm_sk_sweep.jsonl: more or shorter splits lose to the
     // slab traffic and the per-split pipeline fill)

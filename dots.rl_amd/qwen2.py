@@ -481,7 +481,7 @@ def _layer_forward(m, i, x_prev, delta, pos, key_valid, save, cache=None, koff=0
             raise NotImplementedError(f"bf16 attention: the fused kernels (csrc/flash_attn.hip) need head_dim 64 / 128 "
                                       f"and <= 8 query heads per KV head (head_dim {D}, {G} per KV head, T {T}); "
                                       "attn_implementation='eager' selects the unfused path")
-        if save is not None and cache is None and T % 8 != 0:
+        elif save is not None and cache is None and T % 8 != 0:
             raise NotImplementedError(f"bf16 training pass over T = {T} positions: the fused attention backward needs "
                                       "T % 8 == 0 (pad prompt_length + response_length to a multiple of 8)")
     if save is not None and flash_ok and cache is None and T % 8 == 0:

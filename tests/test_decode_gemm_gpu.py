@@ -59,7 +59,7 @@ def test_decode_gemm_every_tiled_configuration(M, N, K):
     wp = native.decode_pack_weight(w)
     lib = native.lib()
     try:
-        for ci in range(17):
+        for ci in range(N_TILED):
             lib.drl_decode_gemm_force_tiled(ci, 1)
             ks, mbt = native.decode_gemm_plan(M, N, K)
             xp = native.pack_activations(x, mbt)
@@ -69,6 +69,41 @@ def test_decode_gemm_every_tiled_configuration(M, N, K):
             assert torch.equal(part, native.decode_gemm(xp, wp, M, N, K)), ci
     finally:
         lib.drl_decode_gemm_force_tiled(-1, 0)
+
+
+N_TILED = 23  # csrc/decode_gemm.hip kTiled entries
+
+
+@pytest.mark.parametrize("M", [64, 128, 300, 512])
+def test_decode_gemm_swiglu_every_tiled_configuration(M):
+    """The SwiGLU epilogue (whole K per workgroup) under every forced tiled configuration: every tiled configuration
+    accumulates each output block's k-steps in the same order, so all are bit-identical to one another, deterministic,
+    and within bf16 rounding of the one-round-trip kernel (4 waves on K quarters, another summation order)."""
+    I, K = 4864, 896
+    x = rnd(M, K, seed=M + 7)
+    w = rnd(2 * I, K, scale=0.05, seed=11)
+    wp = native.decode_pack_weight(w, swiglu=True)
+    lib = native.lib()
+    try:
+        lib.drl_decode_gemm_set_tiled(0)
+        ks, mbt = native.decode_gemm_plan(M, 2 * I, K, swiglu=True)
+        xp = native.pack_activations(x, mbt)
+        rt = native.unpack_activations(native.decode_gemm(xp, wp, M, 2 * I, K, swiglu=True), M, I, mbt).float()
+        lib.drl_decode_gemm_set_tiled(1)
+        want = None
+        for ci in range(N_TILED):
+            lib.drl_decode_gemm_force_tiled(ci, 1)
+            assert native.decode_gemm_plan(M, 2 * I, K, swiglu=True)[1] == mbt
+            got = native.decode_gemm(xp, wp, M, 2 * I, K, swiglu=True)
+            if want is None:
+                want = got.clone()
+                a = native.unpack_activations(got, M, I, mbt).float()
+                assert (a - rt).abs().max() <= 0.02 * rt.abs().max()
+            assert torch.equal(got[:mbt * 32 * I], want[:mbt * 32 * I]), ci
+            assert torch.equal(got, native.decode_gemm(xp, wp, M, 2 * I, K, swiglu=True)), ci
+    finally:
+        lib.drl_decode_gemm_force_tiled(-1, 0)
+        lib.drl_decode_gemm_set_tiled(1)
 
 
 @pytest.mark.parametrize("M", [5, 64, 128, 300, 512])

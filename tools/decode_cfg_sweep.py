@@ -18,7 +18,7 @@ from dots.rl_amd import native  # noqa: E402
 from dots.rl_amd.config import QWEN25_05B  # noqa: E402
 from dots.rl_amd.qwen2 import KVCache, PackedDecode, ParamStore, Qwen2Config, Qwen2Model  # noqa: E402
 
-NCFG = 17  # kTiled entries
+NCFG = 23  # kTiled entries
 
 
 def graph_time(fn, reps=5):

@@ -108,8 +108,8 @@ def main():
         if args.tune:
             sweep = {}
             for grid, mode, param in [(0, 1, 0), (0, 1, 8), (0, 1, 32), (0, 2, 0), (0, 3, 2), (0, 3, 4), (0, 3, 8),
-                                      (0, 3, 16), (0, 3, 32)]:
-                if mode == 3 and param and param * (M + 255) // 256 * ((N + 255) // 256) > 256:
+                                      (0, 3, 12), (0, 3, 16), (0, 3, 32)]:
+                if mode == 3 and param and param * ((M + 255) // 256) * ((N + 255) // 256) > 256:
                     continue
                 native.lib().drl_gemm_set_sk_tuning(grid, 0, mode, param)
                 sweep[f"g{grid}_m{mode}_p{param}"] = round(bench(ours, iters=10, rounds=2), 2)
