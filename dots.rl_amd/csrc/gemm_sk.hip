@@ -72,7 +72,9 @@ struct SkArgs {
   int dp_tiles;        // tiles dealt whole before the stream-K region
   int n_tiles;
   int beta;            // EPI_F32: 1 = C += acc
-  int splits;          // > 1: uniform split-K, workgroup wg = split (wg % splits) of tile (wg / splits)
+  int splits;          // > 1: uniform split-K, workgroup sk_base + j = split (j % splits) of tile sk_tile0 + j / splits
+  int sk_base;         // split-K after whole tiles: workgroups [0, sk_base) take whole tiles 0 .. sk_base - 1 first
+  int sk_tile0;        // first split tile (= sk_base; 0 for an all split-K grid)
   int dbg;             // measurement only (drl_gemm_set_debug): 1 = whole tiles skip their epilogue, 2 = the plain
                        // bf16 epilogue stages but does not store
 };
@@ -115,7 +117,13 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
   const int wr = wave >> 2, wc = wave & 3;
   const int fr = lane & 15, fq = lane >> 4;
   const int G = gridDim.x;
-  const int wg = xcd_remap(blockIdx.x, G);
+  // tail mode (whole tiles, then the last partial round's tiles split over the CUs): the whole-tile workgroups are
+  // XCD-remapped among themselves; the split slices keep their launch order, so they are dispatched after every whole
+  // tile and a tile's slices run side by side
+  const bool tail_mode = g.splits > 1 && g.sk_base > 0;
+  const int wg = (tail_mode && static_cast<int>(blockIdx.x) >= g.sk_base)
+                     ? static_cast<int>(blockIdx.x)
+                     : xcd_remap(blockIdx.x, tail_mode ? g.sk_base : G);
   const int half = g.N / 2;
   const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)g.a, (short)0, (int)g.a_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)g.b, (short)0, (int)g.b_bytes, 0x00020000);
@@ -622,8 +630,8 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
   // dgrad): the S workgroups of a tile each accumulate a k-pair range, publish it (sc1 slab + arrival count), wait for
   // all S arrivals, then each reduces 1/S of the tile's registers over the S slabs in split order (a fixed order:
   // bit-reproducible) and writes that share through the epilogue — the combine runs on all S workgroups at once.
-  if (g.splits > 1) {
-    const int S = g.splits, t = wg / S, sp = wg - t * S;
+  if (g.splits > 1 && wg >= g.sk_base) {
+    const int S = g.splits, rel = wg - g.sk_base, ti = rel / S, t = g.sk_tile0 + ti, sp = rel - ti * S;
     int m0, n0;
     {
       const int grp = t / (g.gm * g.tn), first = grp * g.gm, gmm = min(g.tm - first, g.gm), r = t % (g.gm * g.tn);
@@ -632,8 +640,9 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
     }
     setup_tile(m0, n0);
     run(sp * g.P / S, (sp + 1) * g.P / S);
-    const __amdgpu_buffer_rsrc_t rws = __builtin_amdgcn_make_buffer_rsrc((void*)g.ws, (short)0, G * SLAB * 4, 0x00020000);
-    const uint32_t vo = static_cast<uint32_t>(wg) * SLAB * 4 + threadIdx.x * 16;
+    const __amdgpu_buffer_rsrc_t rws =
+        __builtin_amdgcn_make_buffer_rsrc((void*)g.ws, (short)0, (G - g.sk_base) * SLAB * 4, 0x00020000);
+    const uint32_t vo = static_cast<uint32_t>(rel) * SLAB * 4 + threadIdx.x * 16;
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -648,7 +657,7 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
     // the count (sc1 loads) until all S slices arrived (MI355X_MICROARCH.md § visibility, first row of the sc1 table)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    gflag* cnt = (gflag*)(g.flags + t);
+    gflag* cnt = (gflag*)(g.flags + ti);
     if (threadIdx.x == 0) {
       __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       unsigned spins = 0;
@@ -664,7 +673,7 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the barrier
     // this slice's share of the tile: register groups [32 sp / S, 32 (sp + 1) / S)
     const int r0 = 32 * sp / S, r1 = 32 * (sp + 1) / S;
-    const uint32_t vt = static_cast<uint32_t>(t * S) * SLAB * 4 + threadIdx.x * 16;
+    const uint32_t vt = static_cast<uint32_t>(ti * S) * SLAB * 4 + threadIdx.x * 16;
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -712,6 +721,7 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
     run(0, g.P);
     if (!(g.dbg & 1)) epilogue(m0, n0);
   }
+  if (tail_mode) return;
 
   // ------------------------------------------------------------------------------------------ stream-K region
   // 32-bit iteration arithmetic (the host keeps the iteration space below 2^23)
@@ -990,6 +1000,7 @@ int drl_gemm(const void* a, int64_t lda, int32_t a_layout, const void* b, int64_
   if (mode == 3) {
     g.splits = S;
     g.dp_tiles = 0;
+    g.sk_base = g.sk_tile0 = 0;
     grid = g.n_tiles * S;
   } else if (mode == 2) {
     // whole tiles, one workgroup per tile (no workgroup waits on another, so no co-residency is needed): the hardware
@@ -997,6 +1008,22 @@ int drl_gemm(const void* a, int64_t lda, int32_t a_layout, const void* b, int64_
     // gradient) fills the CUs a short grid leaves idle instead of waiting behind a persistent grid's static rounds
     g.dp_tiles = g.n_tiles;
     grid = g_sk.grid > 0 ? std::min(cap, g.n_tiles) : g.n_tiles;
+    // a last round of at most a quarter of the CUs (the N = 896 outputs at the passes' token counts: 1284 = 5 x 256
+    // + 4 tiles, 2568 = 10 x 256 + 8) would hold the whole launch for one more tile time while the other CUs idle:
+    // over a long K (>= 16 k-pairs) those r tiles split K over S = cap / r slices instead (uniform split-K, <= 16
+    // slices): down_proj's forward at the update pass's 82144 rows 628 -> 611 us; at K = 896 (7 k-pairs) the slices'
+    // pipeline fill and combine cost more than the round they save (o_proj dgrad 151 -> 157 us), so not there
+    // (profiles/r05_gemm_tail_splitk.jsonl)
+    const int r = g.n_tiles % cap;
+    if (g_sk.mode == 0 && g_sk.grid == 0 && !epi_whole_tiles(epilogue) && g.n_tiles > cap && r > 0 && 4 * r <= cap &&
+        g.P >= 16) {
+      const int St = std::min({16, cap / r, g.P / 2});
+      if (St >= 2) {
+        g.splits = St;
+        g.dp_tiles = g.sk_base = g.sk_tile0 = g.n_tiles - r;
+        grid = g.n_tiles - r + r * St;
+      }
+    }
   } else {
     const int full = g.n_tiles / grid;
     const int dp = (g.n_tiles % grid == 0) ? g.n_tiles : std::max(0, full - 1) * grid;

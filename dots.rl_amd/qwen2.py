@@ -350,9 +350,26 @@ def acc_wgrad(gw, dy, x):
 # pair's workgroups share the CUs (gate_up's weight gradient is 152 tiles of 256 x 256 at any row count, the other
 # 104 CUs otherwise idle for its ~2 ms). It pays since whole-tile drl_gemm launches one workgroup per tile (the
 # hardware deals tiles to CUs as they free up; a persistent grid's static rounds could not take the idle CUs):
-# update 1.44 -> 1.38 s (round 3). DRL_CONCURRENT_WGRAD=0 turns it off.
+# update 1.44 -> 1.38 s (round 3). DRL_CONCURRENT_WGRAD=0 turns it off. Round 5: only where the weight gradient runs
+# as whole tiles that leave CUs idle (gate_up: 152 tiles of 256 x 256 over 642 k-pairs); the small projections'
+# weight gradients (qkv 20, o 16 tiles) now split K over every CU (csrc/gemm_sk.hip), and beside their input
+# gradients the pair took longer than the two in sequence (qkv 468 vs 190 + 242 us, o 392 vs 151 + 184 us per call,
+# profiles/r05_gemm_launches_splitk_concurrent.txt).
 CONCURRENT_WGRAD = os.environ.get("DRL_CONCURRENT_WGRAD", "1") != "0"
+CONCURRENT_DOWN = os.environ.get("DRL_CONCURRENT_DOWN", "0") == "1"  # measurement switch: down_proj's pair concurrent
 _SIDE_STREAMS = {}
+_CU_COUNT = {}
+
+
+def _concurrent_pair(gw):
+    """The weight gradient gw (out, in) runs beside its input gradient when drl_gemm deals it as whole 256 x 256 tiles
+    that fill more than half of the CUs but not all of them (gemm_sk.hip's automatic decomposition)."""
+    dev = gw.device.index
+    if dev not in _CU_COUNT:
+        _CU_COUNT[dev] = torch.cuda.get_device_properties(dev).multi_processor_count
+    cus = _CU_COUNT[dev]
+    tiles = -(-gw.shape[0] // 256) * -(-gw.shape[1] // 256)
+    return cus < 2 * tiles and tiles < cus
 
 
 def _side_stream(dev):
@@ -366,7 +383,7 @@ def dgrad_wgrad(dy, w, gw, x):
     """dx = dy W and gw (fp32) += dy^T x for one projection (dy (N, out), w (out, in), x (N, in)); returns dx. On
     drl_gemm the weight gradient is launched first on the side stream (its own workspace slot) and joined before
     returning, so callers see plain stream order."""
-    if not (CONCURRENT_WGRAD and _sk(dy, w, x)):
+    if not (CONCURRENT_WGRAD and _sk(dy, w, x) and _concurrent_pair(gw)):
         dx = dgrad(dy, w)
         acc_wgrad(gw, dy, x)
         return dx
@@ -614,8 +631,17 @@ class _DecoderLayer(torch.autograd.Function):
         # MLP
         if _sk(dm, sv["gu"]):
             # down_proj dgrad with the SwiGLU backward in its epilogue (d a never written)
-            acc_wgrad(s.g(p + "down_proj"), dm, sv["a"])
-            dgu = native.linear_dgrad_swiglu_bwd(dm, s.w(p + "down_proj"), sv["gu"])
+            if CONCURRENT_DOWN:
+                main = torch.cuda.current_stream()
+                side = _side_stream(dm.device)
+                side.wait_stream(main)
+                with torch.cuda.stream(side):
+                    native.linear_wgrad(s.g(p + "down_proj"), dm, sv["a"], ws_slot=1)
+                dgu = native.linear_dgrad_swiglu_bwd(dm, s.w(p + "down_proj"), sv["gu"])
+                main.wait_stream(side)
+            else:
+                acc_wgrad(s.g(p + "down_proj"), dm, sv["a"])
+                dgu = native.linear_dgrad_swiglu_bwd(dm, s.w(p + "down_proj"), sv["gu"])
         else:
             da = dgrad_wgrad(dm, s.w(p + "down_proj"), s.g(p + "down_proj"), sv["a"])
             dgu = torch.empty_like(sv["gu"])

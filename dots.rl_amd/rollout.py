@@ -10,6 +10,7 @@ The actor's bf16 compute buffer is read directly: no weight resharding between t
 
 from __future__ import annotations
 
+import gc
 import time
 
 import torch
@@ -34,14 +35,24 @@ def capture_graph(body, pool):
     global _CAPTURE_STREAM
     if _CAPTURE_STREAM is None:
         _CAPTURE_STREAM = torch.cuda.Stream()
+    # no garbage collection during the capture: an unreachable CUDAGraph (or event) destroyed by a collection inside
+    # it is a HIP call the capturing stream forbids, and the process aborts (seen in the GPU suite: a collection in
+    # the middle of a decode-lane capture). torch.cuda.graph runs a full gc.collect() before capturing instead; here
+    # that cost 45-75 ms per rollout (a large Python heap), so collection is only paused for the capture
     torch.cuda.synchronize()
     graph = torch.cuda.CUDAGraph()
-    with torch.cuda.stream(_CAPTURE_STREAM):
-        graph.capture_begin(pool=pool)
-        try:
-            body()
-        finally:
-            graph.capture_end()
+    enabled = gc.isenabled()
+    gc.disable()
+    try:
+        with torch.cuda.stream(_CAPTURE_STREAM):
+            graph.capture_begin(pool=pool)
+            try:
+                body()
+            finally:
+                graph.capture_end()
+    finally:
+        if enabled:
+            gc.enable()
     return graph
 
 

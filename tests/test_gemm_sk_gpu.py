@@ -50,6 +50,38 @@ def test_layouts_bf16_and_f32(al, bl, M, N, K):
     torch.testing.assert_close(out32.double(), ref, rtol=1e-6, atol=tol)
 
 
+@pytest.mark.parametrize("al,bl,M,N,K,out", [(K_, K_, 65836, 896, 896, "bias"), (K_, T_, 82144, 896, 1152, "bf16"),
+                                             (T_, T_, 16640, 1024, 520, "f32"), (K_, K_, 164288, 896, 4864, "bf16")])
+def test_last_round_split_k(al, bl, M, N, K, out):
+    """Whole-tile grids whose last round holds few tiles (n_tiles % 256 <= 64: the N = 896 outputs at the passes' token
+    counts) split those tiles' K over the CUs (uniform split-K after the whole tiles, csrc/gemm_sk.hip tail mode):
+    every epilogue kind against the fp64 product, and deterministic (split order fixed)."""
+    g = torch.Generator(device="cuda").manual_seed(M + K)
+    a, fa = _op((M, K), al, g, 0.5)
+    b, fb = _op((N, K), bl, g, 0.5)
+    tol = 4e-6 * K ** 0.5
+    # the first rows and the last 1536 (the split tail tiles are the last ones): the fp64 product of those rows only
+    rows = torch.cat([torch.arange(0, 512, device="cuda"), torch.arange(M - 1536, M, device="cuda")])
+    ref = fa(a)[rows].double() @ fb(b).double().t()
+    if out == "f32":
+        c = torch.full((M, N), 0.25, device="cuda")
+        native.gemm(a, al, b, bl, M, N, K, c, beta=True)
+        torch.testing.assert_close(c[rows].double(), ref + 0.25, rtol=1e-6, atol=tol)
+        c2 = torch.full((M, N), 0.25, device="cuda")
+        native.gemm(a, al, b, bl, M, N, K, c2, beta=True)
+        assert torch.equal(c, c2)
+        return
+    bias = torch.randn(N, generator=g, device="cuda").to(torch.bfloat16) if out == "bias" else None
+    if bias is not None:
+        ref = ref + bias.double()
+    c = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+    native.gemm(a, al, b, bl, M, N, K, c, bias=bias)
+    torch.testing.assert_close(c[rows].double(), ref.to(torch.bfloat16).double(), rtol=8e-3, atol=tol)
+    c2 = torch.empty_like(c)
+    native.gemm(a, al, b, bl, M, N, K, c2, bias=bias)
+    assert torch.equal(c, c2)
+
+
 @pytest.mark.parametrize("K", [64, 200, 6144, 6150])
 def test_wgrad_any_k(K):
     """Both operands layout T (the weight gradient over the token dimension): any token count, k tail zero."""
@@ -208,13 +240,16 @@ def test_wgrad_operand_over_2gb_splits_k():
     del dy, gw
 
 
-@pytest.mark.parametrize("M,N_out,N_in", [(6144, 1152, 896), (6144, 9728, 896), (6144, 896, 4864), (777, 896, 896)])
+@pytest.mark.parametrize("M,N_out,N_in", [(6144, 1152, 896), (6144, 9728, 896), (6144, 896, 4864), (777, 896, 896),
+                                         (82144, 896, 896)])
 def test_concurrent_dgrad_wgrad_matches_serial(M, N_out, N_in, monkeypatch):
     """qwen2.dgrad_wgrad: the weight gradient on the side stream (workspace slot 1) while the input gradient runs on
     the current stream gives bit-identical results to the serial pair, repeated back to back (slots reused)."""
     from dots.rl_amd import qwen2
 
     monkeypatch.setattr(qwen2, "CONCURRENT_WGRAD", True)
+    # every shape through the side stream, including the split-K weight gradients qwen2 now runs in sequence
+    monkeypatch.setattr(qwen2, "_concurrent_pair", lambda gw: True)
 
     g = torch.Generator(device="cuda").manual_seed(M + N_out)
     dy = torch.randn(M, N_out, device="cuda", generator=g).to(torch.bfloat16)

@@ -8,6 +8,7 @@
 #   bench[:<steps>[:<warmup>]]  the default bench line (no CPU baseline) + the last step's drl_gemm launch log
 #   benchfull                   the driver's bench command (python bench.py, CPU baseline included)
 #   benchfused                  the bench with model.use_fused_kernels=True
+#   benchenv:<name>:<V=x>,...   the bench (5 steps, 2 warmup) with environment switches -> bench_<name>.json
 #   bench64                     the per-rank workload of N = 8 (64 sequences) ; bench128 / bench256 likewise
 #   benchx:<name>:<k=v>,<k=v>   the bench (5 steps, 2 warmup) with config overrides -> bench_<name>.json
 #   profile                     rocprofv3 kernel stats of a 2-step bench + trace summary
@@ -67,6 +68,12 @@ for step in "$@"; do
       timeout -k 10 500 python -u bench.py --steps 5 --warmup 2 --no-cpu-baseline --override "${O[@]}" \
         > "$OUT/bench_${A[1]}.json" 2> "$OUT/bench_${A[1]}.err" || { tail -20 "$OUT/bench_${A[1]}.err"; exit 1; }
       cut -c1-900 "$OUT/bench_${A[1]}.json" ;;
+    benchenv:*)  # benchenv:<name>:<VAR=val>,<VAR=val>: the bench (5 steps, 2 warmup) with environment switches
+      IFS=':' read -ra A <<< "$step"; IFS=',' read -ra E <<< "${A[2]}"
+      env "${E[@]}" timeout -k 10 500 python -u bench.py --steps 5 --warmup 2 --no-cpu-baseline \
+        --launch-log "$OUT/gemm_launches_${A[1]}.jsonl" > "$OUT/bench_${A[1]}.json" 2> "$OUT/bench_${A[1]}.err" \
+        || { tail -20 "$OUT/bench_${A[1]}.err"; exit 1; }
+      cut -c1-900 "$OUT/bench_${A[1]}.json" ;;
     bench64) bench_rows 64 || exit 1 ;;
     bench128) bench_rows 128 || exit 1 ;;
     bench256) bench_rows 256 || exit 1 ;;
@@ -96,6 +103,16 @@ for step in "$@"; do
       done
       python3 tools/pmc_sq.py "$OUT/pmc_flash_sq.json" flash_fwd_kernel,flash_dq_kernel,flash_dkdv_kernel \
         "$OUT/fpmc1" "$OUT/fpmc2" || exit 1
+      find "$OUT" -name "*.csv" -size +20M -delete ;;
+    pmc_decattn)  # two SQ counter passes over the grouped decode attention (tools/probes/decode_attn_quick.py)
+      i=0
+      for pass in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_MFMA" \
+                  "SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_SALU"; do
+        i=$((i+1))
+        timeout -s KILL 120 rocprofv3 --pmc $pass --kernel-include-regex decode_group -f csv -d "$OUT/dpmc$i" -o p \
+          -- python3 "$ROOT/tools/probes/decode_attn_quick.py" 640 48 > "$OUT/dpmc$i.log" 2>&1 || { tail -5 "$OUT/dpmc$i.log"; exit 1; }
+      done
+      python3 tools/pmc_sq.py "$OUT/pmc_decattn_sq.json" decode_group_kernel "$OUT/dpmc1" "$OUT/dpmc2" || exit 1
       find "$OUT" -name "*.csv" -size +20M -delete ;;
     ab:*)  # A/B of GEMM builds: ab:<lib1>,<lib2>,...
       IFS=',' read -ra L <<< "${step#ab:}"
