@@ -1038,64 +1038,44 @@ __device__ __forceinline__ void dec_reshape(const DecRaw<D>& r, uint16_t* ks, ui
   for (int c = 0; c < 4; ++c) blk.vb[c] = r.vb[c];
 }
 
-// the online-softmax step of one 32-key block from its raw scores S^T (lane = query column, 16 keys per lane): the
-// key-valid mask only where some key of the block is invalid (a wave-uniform test: a block of all-valid keys skips
-// the 16 per-key selects), the max over the raw scores (the scale is positive, so max(s) * scale = max(s * scale)
-// exactly), the scale folded into the exponent's fma, and the O^T rescale skipped while the running maximum holds:
-// it moves only when a block's max exceeds it by more than 8 (log2 units), so p <= 2^8 and most blocks keep
-// alpha = 1 (the flash forward's deferred rescale); O / l is the same quotient either way. vfrag(mt, s) gives the
-// V^T A operand of O^T += V^T P^T for head-dim tile mt, k-step s.
-template <int D, typename VF>
-__device__ __forceinline__ void dec_softmax_pv(f32x16& st, const uint32_t (&vb)[4], float scale_log2, float& m,
-                                               float& lsum, f32x16 (&o)[D / 32], VF&& vfrag) {
-  constexpr int MT = D / 32;
-  const bool allv = (vb[0] & vb[1] & vb[2] & vb[3]) == 0x01010101u;
-  if (!__all(allv)) {
+// online-softmax step over one loaded block (scores, running max / sum, O^T accumulation)
+template <int D>
+__device__ __forceinline__ void dec_block(const DecBlock<D>& blk, const bf16x8 (&qf)[D / 16], float scale_log2,
+                                          float& m, float& lsum, f32x16 (&o)[D / 32]) {
+  constexpr int KS = D / 16, MT = D / 32;
+  f32x16 st = f32x16{};
 #pragma unroll
-    for (int c = 0; c < 4; ++c)
+  for (int s = 0; s < KS; ++s) st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(blk.kf[s]), qf[s], st, 0, 0, 0);
+  float x[16], mx = -INFINITY;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int r = 4 * c + j;
-        st[r] = ((vb[c] >> (8 * j)) & 0xffu) != 0u ? st[r] : -INFINITY;
-      }
-  }
-  float mxr = -INFINITY;
+  for (int c = 0; c < 4; ++c)
 #pragma unroll
-  for (int r = 0; r < 16; ++r) mxr = fmaxf(mxr, st[r]);
-  mxr = fmaxf(mxr, __shfl_xor(mxr, 32, kWave));
-  const float mx = mxr * scale_log2;
-  const float mn = mx > m + 8.f ? mx : m;
-  const float mref = mn == -INFINITY ? 0.f : mn;  // exp2(-inf - mref) = 0, never NaN
+    for (int j = 0; j < 4; ++j) {
+      const int r = 4 * c + j;
+      x[r] = ((blk.vb[c] >> (8 * j)) & 0xffu) != 0u ? st[r] * scale_log2 : -INFINITY;
+      mx = fmaxf(mx, x[r]);
+    }
+  mx = fmaxf(mx, __shfl_xor(mx, 32, kWave));
+  const float mn = fmaxf(m, mx);
+  const float mref = mn == -INFINITY ? 0.f : mn;
   const float alpha = __builtin_amdgcn_exp2f(m - mref);
   m = mn;
   float ps = 0.f;
   u16x8 pb[2];
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
-    const float p = __builtin_amdgcn_exp2f(fmaf(st[r], scale_log2, -mref));
+    const float p = __builtin_amdgcn_exp2f(x[r] - mref);
     ps += p;
     pb[r >> 3][r & 7] = to_bf16_bits(p);
   }
   lsum = lsum * alpha + ps;
-  const bool rescale = !__all(alpha == 1.f);
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
-    if (rescale) o[mt] *= alpha;
+    o[mt] *= alpha;
 #pragma unroll
     for (int s = 0; s < 2; ++s)
-      o[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(vfrag(mt, s)), as_bf16x8(pb[s]), o[mt], 0, 0, 0);
+      o[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(blk.vf[mt][s]), as_bf16x8(pb[s]), o[mt], 0, 0, 0);
   }
-}
-
-// online-softmax step over one loaded block (scores, running max / sum, O^T accumulation)
-template <int D>
-__device__ __forceinline__ void dec_block(const DecBlock<D>& blk, const bf16x8 (&qf)[D / 16], float scale_log2,
-                                          float& m, float& lsum, f32x16 (&o)[D / 32]) {
-  constexpr int KS = D / 16;
-  f32x16 st = f32x16{};
-#pragma unroll
-  for (int s = 0; s < KS; ++s) st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(blk.kf[s]), qf[s], st, 0, 0, 0);
-  dec_softmax_pv<D>(st, blk.vb, scale_log2, m, lsum, o, [&](int mt, int s) { return blk.vf[mt][s]; });
 }
 
 // raw block -> the wave's LDS slot only (fragments are read just in time by dec_block_lds)
@@ -1118,19 +1098,48 @@ template <int D>
 __device__ __forceinline__ void dec_block_lds(const uint16_t* ks, const uint16_t* vs, const uint32_t (&vb)[4],
                                               const bf16x8 (&qf)[D / 16], float scale_log2, int qi, int h, float& m,
                                               float& lsum, f32x16 (&o)[D / 32]) {
-  constexpr int KS = D / 16;
+  constexpr int KS = D / 16, MT = D / 32;
   f32x16 st = f32x16{};
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
     const u16x8 kf = *reinterpret_cast<const u16x8*>(ks + qi * D + 8 * ((2 * s + h) ^ (qi & 7)));
     st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(kf), qf[s], st, 0, 0, 0);
   }
-  dec_softmax_pv<D>(st, vb, scale_log2, m, lsum, o, [&](int mt, int s) {
+  float mx = -INFINITY;
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int r = 4 * c + j;
+      st[r] = ((vb[c] >> (8 * j)) & 0xffu) != 0u ? st[r] * scale_log2 : -INFINITY;
+      mx = fmaxf(mx, st[r]);
+    }
+  mx = fmaxf(mx, __shfl_xor(mx, 32, kWave));
+  const float mn = fmaxf(m, mx);
+  const float mref = mn == -INFINITY ? 0.f : mn;
+  const float alpha = __builtin_amdgcn_exp2f(m - mref);
+  m = mn;
+  float ps = 0.f;
+  u16x8 pb[2];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const float p = __builtin_amdgcn_exp2f(st[r] - mref);
+    ps += p;
+    pb[r >> 3][r & 7] = to_bf16_bits(p);
+  }
+  lsum = lsum * alpha + ps;
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    o[mt] *= alpha;
     const int d = 32 * mt + qi, sw = (d >> 2) & 7;
-    const u16x4 lo = *reinterpret_cast<const u16x4*>(vs + d * 32 + 4 * ((4 * s + h) ^ sw));
-    const u16x4 hi = *reinterpret_cast<const u16x4*>(vs + d * 32 + 4 * ((4 * s + 2 + h) ^ sw));
-    return u16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  });
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const u16x4 lo = *reinterpret_cast<const u16x4*>(vs + d * 32 + 4 * ((4 * s + h) ^ sw));
+      const u16x4 hi = *reinterpret_cast<const u16x4*>(vs + d * 32 + 4 * ((4 * s + 2 + h) ^ sw));
+      const u16x8 vf = u16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      o[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(vf), as_bf16x8(pb[s]), o[mt], 0, 0, 0);
+    }
+  }
 }
 
 // output element (sequence b, column k of (Hq * D)): row-major or fragment-packed (csrc/decode_gemm.hip layout)

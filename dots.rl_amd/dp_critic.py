@@ -116,7 +116,11 @@ class DataParallelPPOCritic:
                     grad_accum = cfg.ppo_mini_batch_size // cfg.ppo_micro_batch_size_per_gpu
                     micro_batches = mini_batch.split(cfg.ppo_micro_batch_size_per_gpu)
                 self.critic_optimizer.zero_grad()
-                groups = exec_groups(cfg, m.cfg, micro_batches)  # micro-batches sharing one pass (dp_actor)
+                # micro-batches sharing one pass (dp_actor), planned within what the critic's resident state leaves
+                opt = self.critic_optimizer
+                resident = m.store.memory_bytes() + sum(t.numel() * t.element_size()
+                                                        for t in (opt.exp_avg, opt.exp_avg_sq))
+                groups = exec_groups(cfg, m.cfg, micro_batches, resident_bytes=resident)
                 for gi, group in enumerate(groups):
                     if gi == len(groups) - 1:
                         self.critic_optimizer.begin_overlap(m)

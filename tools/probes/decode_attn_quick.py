@@ -1,6 +1,6 @@
 """A short workload for counter passes over the grouped decode attention (decode_group_kernel) in the rollout's form
 at 512 rows: groups of 8, 2 KV heads x 7 query heads, 512 shared prompt keys, L cached keys (default 640), the query
-position in device memory, cold caches (8 copies rotated). python tools/probes/decode_attn_quick.py [L] [calls]"""
+position in device memory, cold caches (8 copies rotated). python tools/probes/decode_attn_quick.py [L[,L...]] [calls]"""
 
 import sys
 
@@ -11,7 +11,7 @@ from dots.rl_amd import native  # noqa: E402
 
 DEV, BF = "cuda", torch.bfloat16
 B, group, Hkv, G, D, P, R = 512, 8, 2, 7, 64, 512, 256
-L = int(sys.argv[1]) if len(sys.argv) > 1 else 640
+Ls = [int(x) for x in sys.argv[1].split(",")] if len(sys.argv) > 1 else [640]
 calls = int(sys.argv[2]) if len(sys.argv) > 2 else 48
 cap = P + R
 g = torch.Generator(device=DEV).manual_seed(0)
@@ -19,14 +19,17 @@ caches = [(torch.randn(B, Hkv, cap, D, device=DEV, generator=g).to(BF),
            torch.randn(B, Hkv, cap // 32, D, 32, device=DEV, generator=g).to(BF)) for _ in range(8)]
 valid = torch.ones(B, cap, dtype=torch.uint8, device=DEV)
 q = torch.randn(B, Hkv, G, D, device=DEV, generator=g).to(BF)
-qd = torch.full((1,), L - 1, dtype=torch.int64, device=DEV)
 outp = torch.empty(16 * 32 * Hkv * G * D, dtype=BF, device=DEV)
 a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-for rep in range(2):
-    a.record()
-    for i in range(calls):
-        k, vt = caches[i % 8]
-        native.decode_attention_vt(q, k, vt, valid, cap, outp, qpos_dev=qd, out_mbt=16, group=group, shared_keys=P)
-    b.record()
-    b.synchronize()
-print(f"L={L}: {a.elapsed_time(b) * 1e3 / calls:.2f} us per call")
+res = []
+for L in Ls:
+    qd = torch.full((1,), L - 1, dtype=torch.int64, device=DEV)
+    for rep in range(2):
+        a.record()
+        for i in range(calls):
+            k, vt = caches[i % 8]
+            native.decode_attention_vt(q, k, vt, valid, cap, outp, qpos_dev=qd, out_mbt=16, group=group, shared_keys=P)
+        b.record()
+        b.synchronize()
+    res.append(f"L={L}: {a.elapsed_time(b) * 1e3 / calls:.2f}")
+print(" ".join(res), "us per call")
