@@ -202,7 +202,7 @@ def build_config(args):
         "actor_rollout_ref.ref.log_prob_micro_batch_size_per_gpu=16",
         "actor_rollout_ref.actor.use_kl_loss=True", "actor_rollout_ref.actor.kl_loss_coef=0.001",
         "actor_rollout_ref.actor.kl_loss_type=low_var_kl", "actor_rollout_ref.actor.entropy_coeff=0",
-        "algorithm.adv_estimator=grpo", "trainer.balance_batch=False",
+        "algorithm.adv_estimator=grpo", "trainer.balance_batch=False", "trainer.gc_freeze=True",
     ])
     if args.tiny:
         apply_overrides(cfg, ["+actor_rollout_ref.model.override_config.num_hidden_layers=2",
@@ -277,7 +277,14 @@ def main():
         trainer.global_steps += 1
     # DAPO draws its own generation batches inside step() (dynamic sampling)
     prompts = [None if args.dapo else trainer.train_dataloader.next() for _ in range(args.steps)]
+    if cfg.trainer.get("gc_freeze", False):  # the long-running job's host heap, frozen once warm (trainer.freeze_host_heap)
+        from dots.rl_amd.trainer import freeze_host_heap
+
+        freeze_host_heap()
     timer = native.KernelTimer(args.roofline_kernel, ROOFLINE[args.roofline_kernel][0], TAGS.get(args.roofline_kernel))
+    mark = os.environ.get("DRL_TRACE_MARK") == "1"  # a spin kernel on each side of the timed steps (trace windows)
+    if mark:
+        torch.cuda._sleep(1000)
     dist.barrier()
     torch.cuda.synchronize()
     ms0 = torch.cuda.memory_stats()
@@ -290,6 +297,8 @@ def main():
             hist.append(trainer.step(p))
             trainer.global_steps += 1
     torch.cuda.synchronize()
+    if mark:
+        torch.cuda._sleep(1000)
     dist.barrier()
     ms1 = torch.cuda.memory_stats()
     elapsed = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cuda")

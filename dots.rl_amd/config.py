@@ -140,7 +140,8 @@ DEFAULTS = dict(
     reward_model=dict(enable=False, reward_manager="synthetic_bernoulli", launch_reward_fn_async=False),
     # ppo_trainer.yaml:269-290: the steps profiled (start_profile before, stop_profile after; ray_trainer.py:1096-1366)
     global_profiler=dict(tool=None, steps=None, profile_continuous_steps=False, save_path="outputs/profile"),
-    trainer=dict(balance_batch=False, total_epochs=1, total_training_steps=None, critic_warmup=0, n_gpus_per_node=1,
+    # trainer.gc_freeze: freeze the host heap after init (trainer.freeze_host_heap; bench.py after its warmup)
+    trainer=dict(balance_batch=False, gc_freeze=False, total_epochs=1, total_training_steps=None, critic_warmup=0, n_gpus_per_node=1,
                  nnodes=1, save_freq=-1, test_freq=-1, logger=["console"], project_name="dots_rl_amd",
                  experiment_name="grpo"),
 )

@@ -223,8 +223,16 @@ class MI355XRollout:
 
         body()  # t = 1, eager
         graph = self._capture(body)
-        for _ in range(2, R):
-            graph.replay()
+        # no collection while the replays are enqueued: a pause of the launching thread drains the device queue (4 ms
+        # idle stretches inside the decode in the kernel trace)
+        enabled = gc.isenabled()
+        gc.disable()
+        try:
+            for _ in range(2, R):
+                graph.replay()
+        finally:
+            if enabled:
+                gc.enable()
         del graph, packed
 
     def _decode_lanes(self, B, max_rows):

@@ -78,10 +78,18 @@ for step in "$@"; do
     bench128) bench_rows 128 || exit 1 ;;
     bench256) bench_rows 256 || exit 1 ;;
     profile)
-      timeout -k 10 500 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/prof" -o run -- python3 "$ROOT/bench.py" \
-        --steps 2 --warmup 2 --no-cpu-baseline > "$OUT/prof.log" 2>&1 || { tail -20 "$OUT/prof.log"; exit 1; }
+      DRL_TRACE_MARK=1 timeout -k 10 500 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/prof" -o run -- python3 \
+        "$ROOT/bench.py" --steps 2 --warmup 2 --no-cpu-baseline > "$OUT/prof.log" 2>&1 || { tail -20 "$OUT/prof.log"; exit 1; }
       TR=$(find "$OUT/prof" -name "*kernel_trace.csv" | head -1)
       python3 tools/trace_summary.py "$TR" 30 > "$OUT/trace_summary.txt" || exit 1
+      python3 - "$TR" "$OUT/kernel_trace_min.csv.gz" <<'PYEOF' || exit 1
+import csv, gzip, sys
+with gzip.open(sys.argv[2], "wt") as f:
+    w = csv.writer(f)
+    w.writerow(["Kernel_Name", "Start_Timestamp", "End_Timestamp"])
+    for r in csv.DictReader(open(sys.argv[1])):
+        w.writerow([r["Kernel_Name"][:80], r["Start_Timestamp"], r["End_Timestamp"]])
+PYEOF
       find "$OUT/prof" -name "*kernel_trace.csv" -delete
       head -40 "$OUT/trace_summary.txt" ;;
     pmc_gemm)

@@ -19,6 +19,44 @@ def main():
                r.get("Workgroup_Size_X", r.get("Workgroup_Size", "")))
         shapes[name][key] += 1
         durs[(name, key)] += d
+    # GPU idle time: the union of every kernel interval against the trace's span, and the longest gaps between
+    # consecutive busy intervals (host-bound stretches: launches behind a synchronisation)
+    rows = list(csv.DictReader(open(path)))
+    # bench.py with DRL_TRACE_MARK=1 brackets its timed steps with two spin kernels: the window between them
+    marks = sorted(int(r["End_Timestamp"]) for r in rows if "spin_kernel" in r["Kernel_Name"])
+    lo, hi = (marks[0], marks[-1]) if len(marks) >= 2 else (0, 1 << 62)
+    sel = sorted(((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows
+                  if lo <= int(r["Start_Timestamp"]) and int(r["End_Timestamp"]) <= hi
+                  and "spin_kernel" not in r["Kernel_Name"]))
+    iv = [(a, b) for a, b, _ in sel]
+    names = {}  # end timestamp of a busy stretch -> (last kernel of it, first kernel after the gap)
+    if len(marks) >= 2:
+        print(f"window: the timed steps between the two DRL_TRACE_MARK spin kernels ({(hi - lo) / 1e6:.1f} ms)")
+    if iv:
+        busy, gaps, cs, ce, cn = 0, [], iv[0][0], iv[0][1], sel[0][2]
+        for a, b, nm in sel[1:]:
+            if a > ce:
+                busy += ce - cs
+                gaps.append((a - ce, ce))
+                names[ce] = (cn, nm)
+                cs, ce, cn = a, b, nm
+            else:
+                if b >= ce:
+                    cn = nm
+                ce = max(ce, b)
+        busy += ce - cs
+        span = iv[-1][1] - iv[0][0]
+        gaps.sort(reverse=True)
+        idle = span - busy
+        print(f"span {span / 1e6:.1f} ms, GPU busy (union of kernels) {busy / 1e6:.1f} ms, idle {idle / 1e6:.1f} ms "
+              f"({100.0 * idle / span:.1f} %) in {len(gaps)} gaps; gaps > 50 us: "
+              f"{sum(g for g, _ in gaps if g > 50000) / 1e6:.1f} ms in {sum(1 for g, _ in gaps if g > 50000)}; "
+              f"longest {[round(g / 1e3, 1) for g, _ in gaps[:8]]} us")
+        short = lambda n: n.replace("void ", "").replace("drl::(anonymous namespace)::", "")[:60]  # noqa: E731
+        for g, at in gaps[:16]:
+            before, after = names[at]
+            print(f"  gap {g / 1e3:9.1f} us at {(at - lo) / 1e6 if lo else at / 1e6:9.1f} ms: after {short(before)} | "
+                  f"before {short(after)}")
     for name, t in tot.most_common(top):
         print(f"{t / 1e6:9.1f} ms  {name[:110]}")
         for key, n in shapes[name].most_common(int(sys.argv[3]) if len(sys.argv) > 3 else 6):
