@@ -92,7 +92,7 @@ F32 = ctypes.c_float
 SZ = ctypes.c_size_t
 
 # name -> (restype, argtypes); must match include/dotsrl_amd.h exactly
-ABI_VERSION = 6  # include/dotsrl_amd.h DRL_ABI_VERSION: the layouts below (PPOLossParams) are of this version
+ABI_VERSION = 7  # include/dotsrl_amd.h DRL_ABI_VERSION: the layouts below (PPOLossParams) are of this version
 
 SIGNATURES = {
     "drl_last_error": (ctypes.c_char_p, []),
@@ -134,7 +134,7 @@ SIGNATURES = {
     "drl_rope_qkv_fwd": (ctypes.c_int, [P, I32, P, P, P, I64, I64, I64, I64, I64, I64, P, P, P, I64, I64, P, P, P, P,
                                         I64, P]),
     "drl_rope_qkv_fwd_rows": (ctypes.c_int, [P, P, I32, P, P, P, I64, I64, I64, I64, I64, I64, P, P, P, I64, I64, P, P,
-                                             P, P, I64, P]),
+                                             P, P, I64, P, P]),
     "drl_rope_qkv_bwd": (ctypes.c_int, [P, P, P, I32, P, P, P, I64, I64, I64, I64, I64, I64, P, P]),
     "drl_masked_softmax_fwd": (ctypes.c_int, [P, P, I32, P, I64, I64, I64, I64, I64, I64, F32, P]),
     "drl_masked_softmax_bwd": (ctypes.c_int, [P, P, P, I32, I64, I64, F32, P]),

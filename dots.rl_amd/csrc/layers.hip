@@ -46,7 +46,15 @@ struct RopeArgs {
   // optional source row of each (b, t) in qkv (packed rows: remove-padding / prefix sharing), < 0 = a zero row;
   // NULL: row b * T + t
   const int64_t* src_row;
+  // optional (B,): q rows t < (q_skip[b] & ~31) are not written (prefix sharing's copies: the fused attention skips
+  // those query tiles — drl_flash_attn_fwd / bwd q_start — and never reads them)
+  const int32_t* q_skip;
 };
+
+template <typename E>
+__device__ __forceinline__ int64_t rope_q_skip(const RopeArgs<E>& a, int64_t b) {
+  return a.q_skip ? static_cast<int64_t>(a.q_skip[b] & ~31) : 0;
+}
 
 // the qkv row of (b, t): its packed row through src_row (a pad reads row 0 and is zeroed by its caller)
 template <typename E>
@@ -75,6 +83,7 @@ __global__ __launch_bounds__(256) void rope_qkv_fwd_kernel(RopeArgs<E> a) {
     const int64_t h = (i / half) % Hall;
     const int64_t bt = i / (half * Hall);
     const int64_t t = bt % a.T, b = bt / a.T;
+    if (h < a.Hq && t < rope_q_skip(a, b)) continue;
     bool zero;
     const E* src = rope_src(a, bt, Hall, h, zero);
     const float x1 = zero ? 0.f : ldf(src, j), x2 = zero ? 0.f : ldf(src, j + half);
@@ -133,6 +142,7 @@ __global__ __launch_bounds__(256) void rope_qkv_fwd_tiled_kernel(RopeArgs<E> a) 
   const int64_t koff = a.koff_dev ? *a.koff_dev : a.koff;
   if (koff < 0 || koff + a.T > a.Tk) return;
   const bool is_q = h < a.Hq, is_k = !is_q && h < a.Hq + a.Hkv;
+  if (is_q && t0 + kRopeTile <= rope_q_skip(a, b)) return;  // a q tile no attention kernel reads
   E* rowdst;   // row-major destination base of this (b, head), indexed [pos][D]
   E* tdst;     // head-dim-major destination base, indexed [d * ld_t + pos]
   int64_t pos0;  // position offset of t = 0 in the destinations
@@ -230,6 +240,7 @@ __global__ __launch_bounds__(256) void rope_qkv_fwd_tiled4_kernel(RopeArgs<E> a)
   const int64_t koff = a.koff_dev ? *a.koff_dev : a.koff;
   if (koff < 0 || koff + a.T > a.Tk) return;
   const bool is_q = h < a.Hq, is_k = !is_q && h < a.Hq + a.Hkv;
+  if (is_q && t0 + kRopeTile <= rope_q_skip(a, b)) return;  // a q tile no attention kernel reads
   E* rowdst;   // row-major destination base of this (b, head), indexed [pos][D]
   E* tdst;     // head-dim-major destination base, indexed [d * ld_t + pos]
   int64_t pos0;  // position offset of t = 0 in the destinations
@@ -977,13 +988,14 @@ int drl_rope_qkv_fwd(const void* qkv, int32_t dt, const int64_t* position_ids, c
                      void* v, int64_t Tk, int64_t koff, const int64_t* koff_dev, void* qt, void* kt, void* vt,
                      int64_t ld_t, void* stream) {
   return drl_rope_qkv_fwd_rows(qkv, nullptr, dt, position_ids, cos_t, sin_t, maxpos, B, T, Hq, Hkv, D, q, k, v, Tk,
-                               koff, koff_dev, qt, kt, vt, ld_t, stream);
+                               koff, koff_dev, qt, kt, vt, ld_t, nullptr, stream);
 }
 
 int drl_rope_qkv_fwd_rows(const void* qkv, const int64_t* src_row, int32_t dt, const int64_t* position_ids,
                           const float* cos_t, const float* sin_t, int64_t maxpos, int64_t B, int64_t T, int64_t Hq,
                           int64_t Hkv, int64_t D, void* q, void* k, void* v, int64_t Tk, int64_t koff,
-                          const int64_t* koff_dev, void* qt, void* kt, void* vt, int64_t ld_t, void* stream) {
+                          const int64_t* koff_dev, void* qt, void* kt, void* vt, int64_t ld_t, const int32_t* q_skip,
+                          void* stream) {
   using namespace drl;
   DRL_CHECK_ARG(qkv && position_ids && cos_t && sin_t && q && k && (v || vt), "NULL input");
   DRL_CHECK_ARG((qt == nullptr && kt == nullptr && vt == nullptr) || (ld_t >= Tk && ld_t >= T) ||
@@ -995,7 +1007,7 @@ int drl_rope_qkv_fwd_rows(const void* qkv, const int64_t* src_row, int32_t dt, c
   DRL_E_DISPATCH(dt, {
     RopeArgs<E> a{static_cast<const E*>(qkv), position_ids, cos_t, sin_t, static_cast<E*>(q), static_cast<E*>(k),
                   static_cast<E*>(v), B, T, Hq, Hkv, D, Tk, koff, maxpos, koff_dev, static_cast<E*>(qt),
-                  static_cast<E*>(kt), static_cast<E*>(vt), ld_t, src_row};
+                  static_cast<E*>(kt), static_cast<E*>(vt), ld_t, src_row, q_skip};
     const bool vec4 = D % 8 == 0 && 256 % (D / 8) == 0 && aligned16(qkv) && aligned16(cos_t) && aligned16(sin_t) &&
                       (q == nullptr || aligned16(q)) && (k == nullptr || aligned16(k)) && (v == nullptr || aligned16(v));
     if ((qt || kt || vt) && T >= 16 && D <= 128 && D % 2 == 0 && 256 % (D / 2) == 0) {

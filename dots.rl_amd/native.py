@@ -643,13 +643,14 @@ def _edt(t):
 
 
 def rope_qkv_fwd(qkv, position_ids, cos_t, sin_t, Hq, Hkv, D, q, k, v, koff=0, koff_dev=None, vt=None, qt=None,
-                 kt=None, src_rows=None):
+                 kt=None, src_rows=None, q_skip=None):
     """qkv (B,T,(Hq+2Hkv)D) -> q (B,Hkv,G,T,D); k, v written at [:, :, koff:koff+T] of (B,Hkv,Tk,D).
 
     ``koff_dev`` (device int64 scalar) replaces ``koff`` for graph-captured decode steps. ``qt`` (B,Hkv,G,D,ld),
     ``kt`` / ``vt`` (B,Hkv,D,ld): head-dim-major copies for the fused attention kernels (same ld). ``src_rows``
     (B*T,) int64: qkv is packed (nnz, (Hq+2Hkv)D) and position (b, t) reads row src_rows[b*T+t] (< 0: zeros) —
-    drl_rope_qkv_fwd_rows, no padded copy of qkv; B, T then come from ``position_ids``."""
+    drl_rope_qkv_fwd_rows, no padded copy of qkv; B, T then come from ``position_ids``. ``q_skip`` (B,) int32: the
+    ``q_start`` of the fused attention that reads q — rows t < q_skip[b] & ~31 are left unwritten (never read)."""
     if src_rows is not None:
         B, T = position_ids.shape[0], position_ids.shape[1]
         assert qkv.dim() == 2 and qkv.is_contiguous() and src_rows.dtype == torch.int64 and src_rows.numel() == B * T
@@ -660,9 +661,13 @@ def rope_qkv_fwd(qkv, position_ids, cos_t, sin_t, Hq, Hkv, D, q, k, v, koff=0, k
     if vt is not None:
         _vt_cap_ok(vt, k.shape[2])
     assert len(lds) <= 1, "qt / kt / vt must share their row stride"
+    if q_skip is not None:
+        assert q_skip.dtype == torch.int32 and q_skip.numel() == B and q_skip.is_contiguous()
+        _dev(q_skip)
     check(lib().drl_rope_qkv_fwd_rows(_p(qkv), _p(src_rows), _edt(qkv), _p(position_ids), _p(cos_t), _p(sin_t),
                                       cos_t.shape[0], B, T, Hq, Hkv, D, _p(q), _p(k), _p(v), k.shape[2], koff,
-                                      _p(koff_dev), _p(qt), _p(kt), _p(vt), lds.pop() if lds else 0, _stream()),
+                                      _p(koff_dev), _p(qt), _p(kt), _p(vt), lds.pop() if lds else 0, _p(q_skip),
+                                      _stream()),
           "drl_rope_qkv_fwd")
 
 

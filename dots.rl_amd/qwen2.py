@@ -508,10 +508,11 @@ def _layer_forward(m, i, x_prev, delta, pos, key_valid, save, cache=None, koff=0
         vbuf = torch.empty_like(kbuf)
         kt = torch.empty(B, Hkv, D, T, dtype=dt, device=dev)
         vt = torch.empty(B, Hkv, D, T, dtype=dt, device=dev)
-        native.rope_qkv_fwd(qkv, pos, m.cos, m.sin, Hq, Hkv, D, q, kbuf, vbuf, kt=kt, vt=vt, src_rows=src_rows)
+        qs = getattr(rm, "q_start", None)  # prefix sharing: q rows the fused kernels never read are not written
+        native.rope_qkv_fwd(qkv, pos, m.cos, m.sin, Hq, Hkv, D, q, kbuf, vbuf, kt=kt, vt=vt, src_rows=src_rows,
+                            q_skip=qs)
         attn = torch.empty(B, T, Hq * D, dtype=dt, device=dev)
         lse = torch.empty(B, Hkv, G, T, dtype=torch.float32, device=dev)
-        qs = getattr(rm, "q_start", None)
         native.flash_attn_fwd(q, kbuf, vt, key_valid, attn, lse=lse, q_start=qs)
         del vt
         save.update(kt=kt, lse=lse, key_valid=key_valid, q_start=qs)
@@ -529,7 +530,9 @@ def _layer_forward(m, i, x_prev, delta, pos, key_valid, save, cache=None, koff=0
     else:  # bf16 caches keep V head-dim-major (cache.vt), the layout of the MFMA prefill / decode kernels
         kbuf, vbuf = cache.k[i], cache.v[i]
         vt = cache.vt[i]
-    native.rope_qkv_fwd(qkv, pos, m.cos, m.sin, Hq, Hkv, D, q, kbuf, vbuf, koff, koff_dev, vt=vt, src_rows=src_rows)
+    qs = getattr(rm, "q_start", None) if flash and cache is None else None
+    native.rope_qkv_fwd(qkv, pos, m.cos, m.sin, Hq, Hkv, D, q, kbuf, vbuf, koff, koff_dev, vt=vt, src_rows=src_rows,
+                        q_skip=qs)
     L = koff + T
     if flash:
         attn = torch.empty(B, T, Hq * D, dtype=dt, device=dev)

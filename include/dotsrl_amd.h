@@ -24,7 +24,7 @@ extern "C" {
 
 /* 3: drl_ppo_loss_params gained policy_loss, cov_ratio, clip_cov_lb, clip_cov_ub, ppo_kl_coef, cov_seed (a caller
  * built against version 2 passes a shorter struct); drl_gemm (operand layouts, fp32 epilogues, stream-K) */
-#define DRL_ABI_VERSION 6
+#define DRL_ABI_VERSION 7
 
 /* ld_vt value selecting the key-blocked V^T cache layout (B, Hkv, ceil(cap / 32), D, 32) wherever a V^T
  * operand with a leading dimension ld_vt is taken (flash / decode attention, the rope and decode-projection
@@ -370,11 +370,14 @@ int drl_rope_qkv_fwd(const void* qkv, int32_t dt, const int64_t* position_ids, c
                      int64_t ld_t, void* stream);
 /* drl_rope_qkv_fwd over a packed qkv (remove-padding / prefix-sharing passes): the qkv row of position (b, t) is
  * row src_row[b * T + t] of qkv (a negative entry: a zero row, the pad positions pad_input leaves zero), so the
- * packed rows are never scattered into a padded (B * T) copy first. src_row NULL: drl_rope_qkv_fwd. */
+ * packed rows are never scattered into a padded (B * T) copy first. src_row NULL: drl_rope_qkv_fwd.
+ * q_skip (B,) int32, optional (ABI 7): q rows t < (q_skip[b] & ~31) are left unwritten — pass the q_start of
+ * drl_flash_attn_fwd / _bwd, whose kernels never read those query tiles (prefix sharing's copies). */
 int drl_rope_qkv_fwd_rows(const void* qkv, const int64_t* src_row, int32_t dt, const int64_t* position_ids,
                           const float* cos_t, const float* sin_t, int64_t maxpos, int64_t B, int64_t T, int64_t Hq,
                           int64_t Hkv, int64_t D, void* q, void* k, void* v, int64_t Tk, int64_t koff,
-                          const int64_t* koff_dev, void* qt, void* kt, void* vt, int64_t ld_t, void* stream);
+                          const int64_t* koff_dev, void* qt, void* kt, void* vt, int64_t ld_t, const int32_t* q_skip,
+                          void* stream);
 int drl_rope_qkv_bwd(const void* dq, const void* dk, const void* dv, int32_t dt, const int64_t* position_ids,
                      const float* cos_t, const float* sin_t, int64_t maxpos, int64_t B, int64_t T, int64_t Hq,
                      int64_t Hkv, int64_t D, void* dqkv, void* stream);

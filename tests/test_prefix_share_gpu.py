@@ -172,6 +172,49 @@ def test_bf16_prefix_share_matches_unshared():
     assert rel < 2e-2, rel
 
 
+def test_bf16_prefix_share_skips_unread_q_rows(monkeypatch):
+    """RoPE leaves the q rows of the copies' skipped query tiles unwritten (q_skip = q_start): poisoning q with NaN
+    before RoPE, and RoPE without the skip, give bit-identical log-probs and gradients — no kernel reads those rows."""
+    from dots.rl_amd import native
+    from dots.rl_amd.config import to_attr
+    from dots.rl_amd.dp_actor import DataParallelPPOActor
+    from dots.rl_amd.qwen2 import ParamStore, Qwen2Config, Qwen2Model
+
+    cfg = Qwen2Config(vocab_size=4096, hidden_size=896, intermediate_size=4864, num_hidden_layers=2,
+                      num_attention_heads=14, num_key_value_heads=2, tie_word_embeddings=True)
+    store = ParamStore(cfg, "cuda", compute_dtype=torch.bfloat16, trainable=True)
+    store.init_random(5)
+    model = Qwen2Model(cfg, store)
+    ids, am, pos, resp = _groups(2, 4, 160, 64, cfg.vocab_size, 13)
+    R = resp.shape[1]
+    mask = am[:, -R:].bool()
+    mb = {"input_ids": ids, "attention_mask": am, "position_ids": pos, "responses": resp}
+    rope = native.rope_qkv_fwd
+    seen = []
+
+    def no_skip(*a, q_skip=None, **kw):
+        return rope(*a, **kw)
+
+    def poisoned(*a, q_skip=None, **kw):
+        seen.append(q_skip is not None and bool((q_skip >= 32).any()))
+        a[7].fill_(float("nan"))  # q
+        return rope(*a, q_skip=q_skip, **kw)
+
+    res = []
+    for wrap in (no_skip, poisoned):
+        monkeypatch.setattr(native, "rope_qkv_fwd", wrap)
+        actor = DataParallelPPOActor(to_attr({"share_prompt_prefix": True}), model)
+        model.training = True
+        store.zero_grad()
+        _, lp = actor._forward_micro_batch(mb, 1.0)
+        (lp * mask).sum().backward()
+        torch.cuda.synchronize()
+        res.append((lp.detach().clone(), store.grad.detach().clone()))
+    assert seen and all(seen)
+    assert torch.equal(res[0][0], res[1][0]) and torch.isfinite(res[1][0][mask]).all()
+    assert torch.equal(res[0][1], res[1][1])
+
+
 def test_compute_log_prob_independent_of_group_row_order():
     from dots.rl_amd.config import to_attr
     from dots.rl_amd.dp_actor import DataParallelPPOActor

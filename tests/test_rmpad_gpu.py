@@ -285,3 +285,44 @@ def test_rope_reads_packed_rows_like_the_padded_copy(dtype, heads):
         outs.append([t for t in (q, k, v, kt, vt) if t is not None])
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("dtype,heads", [(torch.bfloat16, True), (torch.float32, False)])
+def test_rope_q_skip_leaves_only_the_skipped_q_rows(dtype, heads):
+    """q_skip (prefix sharing's q_start): q rows t < q_skip[b] & ~31 are left as they were, every other q row and all
+    of k / v / kt / vt are bit-identical to the unskipped kernel — the tiled kernel (whole 64-row tiles skipped, the
+    rest of a partial tile written) and the generic one (per row)."""
+    from dots.rl_amd import native
+
+    B, T, Hq, Hkv, D = 4, 200, 4, 2, 64
+    C = (Hq + 2 * Hkv) * D
+    g = torch.Generator(device="cuda").manual_seed(11)
+    qkv = torch.randn(B, T, C, device="cuda", generator=g).to(dtype)
+    pos = torch.arange(T, device="cuda").repeat(B, 1).contiguous()
+    cos = torch.randn(T, D // 2, device="cuda", generator=g)
+    sin = torch.randn(T, D // 2, device="cuda", generator=g)
+    qs = torch.tensor([0, 150, 70, 500], dtype=torch.int32, device="cuda")
+    outs = []
+    for skip in (None, qs):
+        q = torch.full((B, Hkv, Hq // Hkv, T, D), float("nan"), device="cuda", dtype=dtype)
+        k = torch.full((B, Hkv, T, D), float("nan"), device="cuda", dtype=dtype)
+        v = torch.full_like(k, float("nan"))
+        kt = torch.full((B, Hkv, D, T), float("nan"), device="cuda", dtype=dtype) if heads else None
+        vt = torch.full_like(kt, float("nan")) if heads else None
+        native.rope_qkv_fwd(qkv, pos, cos, sin, Hq, Hkv, D, q, k, v, kt=kt, vt=vt, q_skip=skip)
+        outs.append([t for t in (q, k, v, kt, vt) if t is not None])
+    (q0, *rest0), (q1, *rest1) = outs
+    for a, b in zip(rest0, rest1):
+        assert torch.equal(a, b)
+    skipped = torch.zeros(B, T, dtype=torch.bool, device="cuda")
+    for b, s in enumerate(qs.tolist()):
+        skipped[b, : min(s // 32 * 32, T)] = True
+    sk = skipped[:, None, None, :, None].expand_as(q0)
+    assert torch.equal(q1[~sk], q0[~sk])
+    # what was skipped: all of it (generic kernel) or whole 64-row tiles (tiled), never a row past the bound
+    untouched = torch.isnan(q1).all(-1).all(2).all(1)  # (B, T)
+    assert not (untouched & ~skipped).any()
+    tile = 1 if not heads else 64
+    for b, s in enumerate(qs.tolist()):
+        lo = min(s // 32 * 32, T) // tile * tile
+        assert untouched[b, :lo].all()
