@@ -18,6 +18,19 @@
 // key), so their value is unobservable; HF's uniform row is not reproduced there.
 #include "common.h"
 
+// backward workgroup plans (profiles/r05_flash_bwd_ab.txt, update-pass shape B 256, T 768, head_dim 64):
+// dQ on 4-wave workgroups over head sets (2 per CU, each one's staging / epilogue beside the other's key loop) and
+// dK / dV on 2 key tiles per workgroup — with the tile copies' scalar addressing, 1362 -> 1235 us per backward
+#ifndef DQ_WAVES
+#define DQ_WAVES 4
+#endif
+#ifndef DKDV_KT64
+#define DKDV_KT64 2
+#endif
+#ifndef DKDV_WAVES64
+#define DKDV_WAVES64 8
+#endif
+
 namespace drl {
 namespace {
 
@@ -425,26 +438,33 @@ struct FlashBwdArgs {
 
 __device__ __forceinline__ float bf2f(uint16_t x) { return bf16_to_f32(x); }
 
+// a wave-uniform 64-bit value into SGPRs (readfirstlane of both halves)
+__device__ __forceinline__ uint64_t uniform64(uint64_t v) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v >> 32));
+  return (static_cast<uint64_t>(hi) << 32) | lo;
+}
+
 
 // dq_kernel's per-key-block tiles in LDS, shared by the G waves (query heads) of the workgroup:
 // K and V row-major [32 keys][D] (rows padded to D + 8 elements) and K^T [D][32 keys] (rows of 40, keys
 // permuted within each 16-key group as in KVTile's V^T: one ds_read_b128 per k-step of dQ^T += K^T dS^T).
-template <int D>
+template <int D, int NT = 512>
 struct DqTile {
   static constexpr int ROW = D + 8, TROW = 40;
   static constexpr int RSZ = 32 * ROW, TSZ = D * TROW;
   static constexpr int RCH = 32 * D / 8;        // 16-B chunks of one row-major tile
   static constexpr int NCH = 2 * RCH + D * 4;   // K, V, K^T
-  static constexpr int CPT = (NCH + 511) / 512;
+  static constexpr int CPT = (NCH + NT - 1) / NT;  // chunks per thread (NT-thread workgroups)
 };
 
-template <int D>
+template <int D, int NT>
 __device__ __forceinline__ void dq_issue(const uint16_t* kb, const uint16_t* vb, const uint16_t* ktb, int64_t ld_t,
-                                         int k0, int T, int tid, u16x8 (&r)[DqTile<D>::CPT]) {
-  using TL = DqTile<D>;
+                                         int k0, int T, int tid, u16x8 (&r)[DqTile<D, NT>::CPT]) {
+  using TL = DqTile<D, NT>;
 #pragma unroll
   for (int i = 0; i < TL::CPT; ++i) {
-    const int c = tid + 512 * i;
+    const int c = tid + NT * i;
     u16x8 v = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
     if (c < 2 * TL::RCH) {
       const int cc = c % TL::RCH, row = cc / (D / 8), col = cc % (D / 8);
@@ -471,13 +491,13 @@ __device__ __forceinline__ void dq_issue(const uint16_t* kb, const uint16_t* vb,
 // discards), the source chosen by an address select. A load under a per-thread branch into a register initialised
 // to zero made hipcc wait for ALL loads in flight (vmcnt(0)) before each of them, serialising the two-ahead prefetch
 // into one memory round trip per chunk.
-template <int D>
+template <int D, int NT>
 __device__ __forceinline__ void dq_issue_full(const uint16_t* kb, const uint16_t* vb, const uint16_t* ktb,
-                                              int64_t ld_t, int k0, int tid, u16x8 (&r)[DqTile<D>::CPT]) {
-  using TL = DqTile<D>;
+                                              int64_t ld_t, int k0, int tid, u16x8 (&r)[DqTile<D, NT>::CPT]) {
+  using TL = DqTile<D, NT>;
 #pragma unroll
   for (int i = 0; i < TL::CPT; ++i) {
-    const int c0 = tid + 512 * i, c = c0 < TL::NCH ? c0 : c0 % (2 * TL::RCH);
+    const int c0 = tid + NT * i, c = c0 < TL::NCH ? c0 : c0 % (2 * TL::RCH);
     const int cc = c % TL::RCH, row = cc / (D / 8), col = cc % (D / 8);
     const uint16_t* rm = (c < TL::RCH ? kb : vb) + static_cast<int64_t>(k0 + row) * D + col * 8;
     const int ct = c - 2 * TL::RCH, d = ct / 4, colt = ct % 4;
@@ -486,13 +506,13 @@ __device__ __forceinline__ void dq_issue_full(const uint16_t* kb, const uint16_t
   }
 }
 
-template <int D>
+template <int D, int NT>
 __device__ __forceinline__ void dq_store(uint16_t* kl, uint16_t* vl, uint16_t* ktl, int tid,
-                                         const u16x8 (&r)[DqTile<D>::CPT]) {
-  using TL = DqTile<D>;
+                                         const u16x8 (&r)[DqTile<D, NT>::CPT]) {
+  using TL = DqTile<D, NT>;
 #pragma unroll
   for (int i = 0; i < TL::CPT; ++i) {
-    const int c = tid + 512 * i;
+    const int c = tid + NT * i;
     if (c < 2 * TL::RCH) {
       const int cc = c % TL::RCH, row = cc / (D / 8), col = cc % (D / 8);
       *reinterpret_cast<u16x8*>((c < TL::RCH ? kl : vl) + row * TL::ROW + col * 8) = r[i];
@@ -505,23 +525,28 @@ __device__ __forceinline__ void dq_store(uint16_t* kl, uint16_t* vl, uint16_t* k
   }
 }
 
-template <int D>
-__global__ __launch_bounds__(512) void flash_dq_kernel(FlashBwdArgs a) {
-  constexpr int KS = D / 16, MT = D / 32;
-  using TL = DqTile<D>;
+// NW waves per workgroup over query heads hs * NW .. hs * NW + NW - 1 of the KV head (gridDim.y = B * Hkv * HS, HS =
+// ceil(G / NW) head sets); waves past G only stage K / V / K^T
+template <int D, int NW = 8>
+__global__ __launch_bounds__(64 * NW) void flash_dq_kernel(FlashBwdArgs a) {
+  constexpr int KS = D / 16, MT = D / 32, NT = 64 * NW;
+  using TL = DqTile<D, NT>;
   __shared__ __attribute__((aligned(16))) uint16_t lds_k[2][TL::RSZ];
   __shared__ __attribute__((aligned(16))) uint16_t lds_v[2][TL::RSZ];
   __shared__ __attribute__((aligned(16))) uint16_t lds_kt[2][TL::TSZ];
   __shared__ uint32_t lds_vw[2][8];
   const int tid = threadIdx.x;
-  const int lane = tid & 63, g = tid >> 6;
-  const bool computes = g < a.G;
+  const int HS = static_cast<int>((a.G + NW - 1) / NW);
+  const int lane = tid & 63;
   const int qi = lane & 31, h = lane >> 5;
   const int T = static_cast<int>(a.T);
   const int ntiles = (T + 31) / 32;
   int tile;
-  int64_t bh;
-  xcd_tile_order(ntiles, static_cast<int>(gridDim.y), tile, bh);
+  int64_t bhs;
+  xcd_tile_order(ntiles, static_cast<int>(gridDim.y), tile, bhs);
+  const int64_t bh = bhs / HS;
+  const int g = __builtin_amdgcn_readfirstlane(tid >> 6) + NW * static_cast<int>(bhs % HS);  // scalar: uniform branches
+  const bool computes = g < a.G;
   const int64_t b = bh / a.Hkv, hkv = bh % a.Hkv;
   const int t0 = (ntiles - 1 - tile) * 32;  // longest causal rows first
   const int tq = t0 + qi;
@@ -572,16 +597,16 @@ __global__ __launch_bounds__(512) void flash_dq_kernel(FlashBwdArgs a) {
   auto issue_blk = [&](int j, int set) {
     const int kk = j * 32;
     if (kk + 32 <= T) {
-      dq_issue_full<D>(kbase, vbase, ktbase, a.ld_t, kk, tid, stage[set]);
+      dq_issue_full<D, NT>(kbase, vbase, ktbase, a.ld_t, kk, tid, stage[set]);
       vst[set] = *reinterpret_cast<const uint32_t*>(vrow + kk + 4 * (tid & 7));  // every thread: no branch
     } else {
-      dq_issue<D>(kbase, vbase, ktbase, a.ld_t, kk, T, tid, stage[set]);
+      dq_issue<D, NT>(kbase, vbase, ktbase, a.ld_t, kk, T, tid, stage[set]);
       vst[set] = valid_issue(vrow, kk, T, tid);
     }
   };
   issue_blk(0, 0);
   if (nb > 1) issue_blk(1, 1);
-  dq_store<D>(lds_k[0], lds_v[0], lds_kt[0], tid, stage[0]);
+  dq_store<D, NT>(lds_k[0], lds_v[0], lds_kt[0], tid, stage[0]);
   if (tid < 8) lds_vw[0][tid] = vst[0];
   __syncthreads();
   // one key block; cur (the LDS buffer and register set parity) is a literal at both call sites, so each parity is
@@ -645,10 +670,10 @@ __global__ __launch_bounds__(512) void flash_dq_kernel(FlashBwdArgs a) {
     }
     if (ib + 1 < nb) {  // block ib + 1 (register set cur ^ 1) into the other LDS buffer
       if (cur == 0) {
-        dq_store<D>(lds_k[1], lds_v[1], lds_kt[1], tid, stage[1]);
+        dq_store<D, NT>(lds_k[1], lds_v[1], lds_kt[1], tid, stage[1]);
         if (tid < 8) lds_vw[1][tid] = vst[1];
       } else {
-        dq_store<D>(lds_k[0], lds_v[0], lds_kt[0], tid, stage[0]);
+        dq_store<D, NT>(lds_k[0], lds_v[0], lds_kt[0], tid, stage[0]);
         if (tid < 8) lds_vw[0][tid] = vst[0];
       }
     }
@@ -674,7 +699,11 @@ __global__ __launch_bounds__(512) void flash_dq_kernel(FlashBwdArgs a) {
 // NW waves per workgroup; wave w handles query heads w, w + NW, ... of the KV head (its dK / dV partials
 // accumulate over them in registers). head_dim 64: NW = 8 (one head per wave, G <= 8); head_dim 128: NW = 4,
 // one wave per SIMD, so the 128 accumulator registers of dK^T / dV^T and the Q / dO rows fit without spilling.
-template <int D, int NW>
+// KT key tiles per workgroup (head_dim 64: 2): each Q / dO tile a wave stages feeds the KT tiles' products, so the
+// L2 -> LDS traffic per MFMA halves (one 32-key tile per staged tile re-reads every query tile after it per key tile:
+// the per-CU ingest, not the matrix pipe, bounded the one-tile form). Each key tile's terms are the one-tile
+// kernel's, accumulated in the same (head, query tile) order: bit-identical to KT = 1.
+template <int D, int NW, int KT = 1>
 __global__ __launch_bounds__(64 * NW) void flash_dkdv_kernel(FlashBwdArgs a) {
   constexpr int KS = D / 16, MT = D / 32, KROW = D + 8;
   // per wave, two buffers of the swizzled image (ximg_off) of a query tile's Q and dO rows, filled two tiles ahead
@@ -683,30 +712,36 @@ __global__ __launch_bounds__(64 * NW) void flash_dkdv_kernel(FlashBwdArgs a) {
   // cross-wave reduction
   constexpr int XROW = D;
   constexpr int UPR = D / 8, RPI = 64 / UPR;  // 16-B units per row, rows per wave instruction
-  constexpr int NDMA = 2 * (32 / RPI) + 1;    // LDS-DMA instructions per query tile: Q, dO rows + LSE / delta
+  constexpr int NDMA = 2 * (32 / RPI) + 2;    // LDS-DMA instructions per query tile: Q, dO rows + LSE, delta
   constexpr int PW = 2 * MT * 16 * 64;        // floats of one wave's dK^T + dV^T partial
   constexpr int XW_ELEMS = NW * 4 * 32 * XROW > NW * PW * 2 ? NW * 4 * 32 * XROW : NW * PW * 2;
   static_assert(D == 64 || D == 128, "head_dim 64 or 128");
-  __shared__ __attribute__((aligned(16))) uint16_t kv_lds[2][32 * KROW];  // this key tile's K and V rows
+  __shared__ __attribute__((aligned(16))) uint16_t kv_lds[2][KT * 32 * KROW];  // the key tiles' K and V rows
   __shared__ __attribute__((aligned(16))) uint16_t xw_raw[XW_ELEMS];     // [wave][buffer][Q / dO][position][d]
   auto xw = reinterpret_cast<uint16_t (*)[2][2][32 * XROW]>(xw_raw);
   // per wave, two slots of [LSE of the tile's 32 queries | their delta], one per image buffer
   __shared__ __attribute__((aligned(16))) float lsd[NW][2][64];
   const int tid = threadIdx.x;
-  const int lane = tid & 63, wv = tid >> 6;
+  // the wave index as a scalar (readfirstlane): the heads, tile copies' base addresses and LDS slots derived from it
+  // stay in SGPRs instead of holding 64-bit per-lane copies in VGPRs through the loop
+  const int lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int li = lane & 31, h = lane >> 5;
   const int T = static_cast<int>(a.T);
   const int ntiles = (T + 31) / 32;
   int tile;
   int64_t bh;
-  xcd_tile_order(ntiles, static_cast<int>(gridDim.y), tile, bh);
+  xcd_tile_order((ntiles + KT - 1) / KT, static_cast<int>(gridDim.y), tile, bh);
   const int64_t b = bh / a.Hkv, hkv = bh % a.Hkv;
-  const int k0 = tile * 32;  // key tile 0 has the most query tiles: dispatched first
+  const int k0 = tile * 32 * KT;  // key tile 0 has the most query tiles: dispatched first
   // first query tile of the loop: the causal start k0, or past the skipped tiles (q_start)
   const int ts = a.q_start ? max(k0, a.q_start[b] & ~31) : k0;
-  const int key = k0 + li;
-  const bool kin = key < T;
-  const bool kval = kin && a.valid[b * a.ld_valid + key] != 0;
+  int keyj[KT];
+  bool kval[KT];
+#pragma unroll
+  for (int j = 0; j < KT; ++j) {
+    keyj[j] = k0 + 32 * j + li;
+    kval[j] = keyj[j] < T && a.valid[b * a.ld_valid + keyj[j]] != 0;
+  }
   // NW = 8 >= G: the block has exactly G waves, one head each (a one-trip loop the compiler folds)
   const int g_end = NW >= 8 ? wv + 1 : static_cast<int>(a.G);
   // query tile tt of head g into image buffer `buf`: rows tt .. tt + 31 of Q and dO (rows past T read row T - 1:
@@ -719,25 +754,32 @@ __global__ __launch_bounds__(64 * NW) void flash_dkdv_kernel(FlashBwdArgs a) {
       (__attribute__((address_space(3))) uint16_t*)xw_raw));
   const uint32_t lds_l = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(
       (__attribute__((address_space(3))) float*)&lsd[0][0][0]));
+  // Q / dO rows address as a wave-uniform base (SGPR pair: the head's Q panel, the (b, kv head, g) column of dO) plus a
+  // 32-bit per-lane byte offset (the saddr form), so a copy costs a few 32-bit ops instead of 64-bit index math
+  const uint32_t drow = static_cast<uint32_t>(a.Hkv * a.G * D * 2);  // bytes per dO row (all heads of a position)
   auto tile_issue = [&](int g, int tt, int buf) {
     const int64_t head = bh * a.G + g;
-    const uint16_t* qbase = a.q + head * a.T * D;
+    const uint64_t qb = uniform64(reinterpret_cast<uint64_t>(a.q + head * a.T * D));
+    const uint64_t db = uniform64(reinterpret_cast<uint64_t>(a.dout + ((b * T * a.Hkv + hkv) * a.G + g) * D));
     const uint32_t xb = lds_x + 2 * static_cast<uint32_t>(((wv * 2 + buf) * 2) * 32 * XROW);
 #pragma unroll
     for (int i = 0; i < 32 / RPI; ++i) {
       const int r = i * RPI + lane / UPR, u = (lane % UPR) ^ xsw(r);
-      const int64_t tr = min(tt + r, T - 1);
-      const uint16_t* srcq = qbase + tr * D + 8 * u;
-      const uint16_t* srcd = a.dout + (((b * T + tr) * a.Hkv + hkv) * a.G + g) * D + 8 * u;
+      const uint32_t tr = static_cast<uint32_t>(min(tt + r, T - 1));
+      const uint32_t oq = tr * (D * 2) + 16 * u, od = tr * drow + 16 * u;
       const uint32_t dq_ = __builtin_amdgcn_readfirstlane(xb + 2 * i * RPI * XROW);
       const uint32_t dd_ = __builtin_amdgcn_readfirstlane(xb + 2 * (32 * XROW + i * RPI * XROW));
-      asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" :: "v"(srcq), "s"(dq_) : "memory");
-      asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" :: "v"(srcd), "s"(dd_) : "memory");
+      asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dwordx4 %0, %1" :: "v"(oq), "s"(qb), "s"(dq_) : "memory");
+      asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dwordx4 %0, %1" :: "v"(od), "s"(db), "s"(dd_) : "memory");
     }
-    const int q = min(tt + li, T - 1);
-    const float* srcl = (h ? a.delta : a.lse) + head * a.T + q;
+    // LSE (lanes 0-31) and delta (lanes 32-63) of the tile's rows: one copy per lane half from its own SGPR base (both
+    // execute, each under its half's exec mask, and land lane-linearly in the same 64-float slot)
+    const uint32_t ol = static_cast<uint32_t>(min(tt + li, T - 1)) * 4u;
+    const uint64_t lb = uniform64(reinterpret_cast<uint64_t>(a.lse + head * a.T));
+    const uint64_t tb = uniform64(reinterpret_cast<uint64_t>(a.delta + head * a.T));
     const uint32_t dl_ = __builtin_amdgcn_readfirstlane(lds_l + 4 * static_cast<uint32_t>((wv * 2 + buf) * 64));
-    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dword %0, off" :: "v"(srcl), "s"(dl_) : "memory");
+    if (h == 0) asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dword %0, %1" :: "v"(ol), "s"(lb), "s"(dl_) : "memory");
+    else asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dword %0, %1" :: "v"(ol), "s"(tb), "s"(dl_) : "memory");
   };
   // the first head's first two query tiles are issued before the K / V staging, so the workgroup's opening memory
   // round trips overlap (the staging barrier waits for all of them)
@@ -745,20 +787,20 @@ __global__ __launch_bounds__(64 * NW) void flash_dkdv_kernel(FlashBwdArgs a) {
     tile_issue(wv, ts, 0);
     if (ts + 32 < T) tile_issue(wv, ts + 32, 1);
   }
-  // stage the key tile's K and V rows once; every wave (query head) reads them from LDS
-  for (int c = tid; c < 2 * 32 * (D / 8); c += blockDim.x) {
-    const int which = c / (32 * (D / 8)), cc = c % (32 * (D / 8)), row = cc / (D / 8), col = cc % (D / 8);
+  // stage the key tiles' K and V rows once; every wave (query head) reads them from LDS
+  for (int c = tid; c < 2 * KT * 32 * (D / 8); c += blockDim.x) {
+    const int which = c / (KT * 32 * (D / 8)), cc = c % (KT * 32 * (D / 8)), row = cc / (D / 8), col = cc % (D / 8);
     const int kk = k0 + row;
     u16x8 v = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
     if (kk < T) v = *reinterpret_cast<const u16x8*>((which ? a.v : a.k) + (bh * a.T + kk) * D + col * 8);
     *reinterpret_cast<u16x8*>(&kv_lds[which][row * KROW + col * 8]) = v;
   }
   __syncthreads();
-  const uint16_t* kl = kv_lds[0] + li * KROW + 8 * h;
-  const uint16_t* vl = kv_lds[1] + li * KROW + 8 * h;
-  f32x16 dkt[MT], dvt[MT];
+  f32x16 dkt[KT][MT], dvt[KT][MT];
 #pragma unroll
-  for (int mt = 0; mt < MT; ++mt) dkt[mt] = dvt[mt] = f32x16{};
+  for (int j = 0; j < KT; ++j)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) dkt[j][mt] = dvt[j][mt] = f32x16{};
   for (int g = wv; g < g_end; g += NW) {
   if (g != wv && ts < T) {  // a later head of this wave (NW < G): its first two tiles now
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the previous head's reads of both buffers are done
@@ -773,6 +815,13 @@ __global__ __launch_bounds__(64 * NW) void flash_dkdv_kernel(FlashBwdArgs a) {
     if (t0 + 32 < T) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NDMA) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
+    const bool rows_in = t0 + 32 <= T;  // uniform
+#pragma unroll
+    for (int kh = 0; kh < KT; ++kh) {
+    const int kj = k0 + 32 * kh, key = keyj[kh];
+    if (KT > 1 && t0 + 31 < kj) continue;  // uniform: every key of this tile is after every query row
+    // this query tile's Q / dO fragments and LSE / delta, read from the wave's LDS slots per key tile (re-reading them
+    // is cheaper than holding them live across the KT tiles' products)
     u16x8 qa[KS], da[KS];
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
@@ -780,7 +829,6 @@ __global__ __launch_bounds__(64 * NW) void flash_dkdv_kernel(FlashBwdArgs a) {
       da[s] = *reinterpret_cast<const u16x8*>(xd + ximg_off<XROW>(li, 16 * s + 8 * h));
     }
     float4 l4[4], d4[4];
-    const bool rows_in = t0 + 32 <= T;  // uniform
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       const int qb = t0 + 8 * c + 4 * h;
@@ -793,6 +841,8 @@ __global__ __launch_bounds__(64 * NW) void flash_dkdv_kernel(FlashBwdArgs a) {
                             qb + 3 < T ? d4[c].w : 0.f);
       }
     }
+    const uint16_t* kl = kv_lds[0] + (32 * kh + li) * KROW + 8 * h;
+    const uint16_t* vl = kv_lds[1] + (32 * kh + li) * KROW + 8 * h;
     // S = Q K^T and dP = dO V^T: A = rows of query t0 + li; C row r -> query t0 + (r&3) + 8(r>>2) + 4h
     f32x16 sc = f32x16{}, dp = f32x16{};
 #pragma unroll
@@ -805,7 +855,7 @@ __global__ __launch_bounds__(64 * NW) void flash_dkdv_kernel(FlashBwdArgs a) {
     u16x8 pb[2], dsb[2];
     // block entirely at or below the diagonal, all keys valid, all queries in range: no mask, and every query
     // row has an allowed key (finite LSE)
-    const bool full = __all(kval) && t0 >= k0 + 31 && rows_in;
+    const bool full = __all(kval[kh]) && t0 >= kj + 31 && rows_in;
     if (full) {
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
@@ -829,7 +879,7 @@ __global__ __launch_bounds__(64 * NW) void flash_dkdv_kernel(FlashBwdArgs a) {
       for (int j = 0; j < 4; ++j) {
         const int r = 4 * c + j;
         const float l2 = lv[j] == -INFINITY ? INFINITY : lv[j] * 1.4426950408889634f;  // no allowed key: p = 0
-        const bool ok = kval && key <= qb + j;
+        const bool ok = kval[kh] && key <= qb + j;
         const float p = ok ? __builtin_amdgcn_exp2f(fmaf(sc[r], a.scale_log2, -l2)) : 0.f;
         pb[r >> 3][r & 7] = to_bf16_bits(p);
         dsb[r >> 3][r & 7] = to_bf16_bits(p * (dp[r] - dv4[j]));
@@ -843,10 +893,11 @@ __global__ __launch_bounds__(64 * NW) void flash_dkdv_kernel(FlashBwdArgs a) {
       for (int s = 0; s < 2; ++s) {
         const u16x8 dov = lds_xt_operand<XROW>(xd, mt, s, lane);
         const u16x8 qtv = lds_xt_operand<XROW>(xq, mt, s, lane);
-        dvt[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(dov), as_bf16x8(pb[s]), dvt[mt], 0, 0, 0);
-        dkt[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(qtv), as_bf16x8(dsb[s]), dkt[mt], 0, 0, 0);
+        dvt[kh][mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(dov), as_bf16x8(pb[s]), dvt[kh][mt], 0, 0, 0);
+        dkt[kh][mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(qtv), as_bf16x8(dsb[s]), dkt[kh][mt], 0, 0, 0);
       }
     }
+    }  // key tiles
     // refill this buffer with the tile two ahead once this wave's reads of it (and of its LSE slot) are done
     if (t0 + 64 < T) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -857,33 +908,36 @@ __global__ __launch_bounds__(64 * NW) void flash_dkdv_kernel(FlashBwdArgs a) {
   }  // query heads of this wave
   // every wave's partial into its own LDS slot (the buffer overlays the Q / dO images, so every wave must be past its
   // key loop first), ONE barrier, then all threads sum 4-element groups over the waves in wave order — the additions
-  // (0 + p0) + p1 + ... of a wave-by-wave reduction, so the result is unchanged — and store them
-  __syncthreads();
+  // (0 + p0) + p1 + ... of a wave-by-wave reduction, so the result is unchanged — and store them; key tile by key tile
   const int nw = a.G < NW ? static_cast<int>(a.G) : NW;
   float* part = reinterpret_cast<float*>(xw_raw);  // [wave][dk / dv][tile][register][lane]
-  if (wv < nw) {
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
+  for (int j = 0; j < KT; ++j) {
+    __syncthreads();
+    if (wv < nw) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        part[wv * PW + (mt * 16 + r) * 64 + lane] = dkt[mt][r];
-        part[wv * PW + ((MT + mt) * 16 + r) * 64 + lane] = dvt[mt][r];
-      }
-  }
-  __syncthreads();
-  for (int gi = tid; gi < 2 * MT * 4 * 64; gi += blockDim.x) {
-    const int ln = gi & 63, c = (gi >> 6) & 3, mt = (gi >> 8) % MT, which = (gi >> 8) / MT;
-    const int kk = k0 + (ln & 31);
-    if (kk >= T) continue;
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int w = 0; w < nw; ++w) {
+      for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[j] += part[w * PW + ((which * MT + mt) * 16 + 4 * c + j) * 64 + ln];
+        for (int r = 0; r < 16; ++r) {
+          part[wv * PW + (mt * 16 + r) * 64 + lane] = dkt[j][mt][r];
+          part[wv * PW + ((MT + mt) * 16 + r) * 64 + lane] = dvt[j][mt][r];
+        }
     }
-    u16x4 o;
+    __syncthreads();
+    for (int gi = tid; gi < 2 * MT * 4 * 64; gi += blockDim.x) {
+      const int ln = gi & 63, c = (gi >> 6) & 3, mt = (gi >> 8) % MT, which = (gi >> 8) / MT;
+      const int kk = k0 + 32 * j + (ln & 31);
+      if (kk >= T) continue;
+      float acc[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int w = 0; w < nw; ++w) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) o[j] = to_bf16_bits(which ? acc[j] : acc[j] * a.scale);
-    *reinterpret_cast<u16x4*>((which ? a.dv : a.dk) + (bh * a.T + kk) * D + 32 * mt + 8 * c + 4 * (ln >> 5)) = o;
+        for (int e = 0; e < 4; ++e) acc[e] += part[w * PW + ((which * MT + mt) * 16 + 4 * c + e) * 64 + ln];
+      }
+      u16x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = to_bf16_bits(which ? acc[e] : acc[e] * a.scale);
+      *reinterpret_cast<u16x4*>((which ? a.dv : a.dk) + (bh * a.T + kk) * D + 32 * mt + 8 * c + 4 * (ln >> 5)) = o;
+    }
   }
 }
 
@@ -1539,14 +1593,18 @@ int drl_flash_attn_bwd(const void* q, const void* k, const void* kt, const void*
                  lse, key_valid, ld_valid, delta, static_cast<uint16_t*>(dq), static_cast<uint16_t*>(dk),
                  static_cast<uint16_t*>(dv), Hkv, G, T, ld_t, scale, scale * 1.4426950408889634f, q_start};
   const dim3 grid(static_cast<unsigned>((T + 31) / 32), static_cast<unsigned>(B * Hkv));
-  const dim3 block_dq(512);  // waves >= G only stage K / V / K^T
-  const dim3 block_kv(static_cast<unsigned>(64 * (D == 64 ? G : std::min<int64_t>(G, 4))));
+  constexpr int kDqWaves = DQ_WAVES, kDkdvWaves64 = DKDV_WAVES64, kKT64 = DKDV_KT64;
+  const dim3 grid_kv64(static_cast<unsigned>((T + 32 * kKT64 - 1) / (32 * kKT64)), static_cast<unsigned>(B * Hkv));
+  const dim3 grid_dq(static_cast<unsigned>((T + 31) / 32),
+                     static_cast<unsigned>(B * Hkv * ((G + kDqWaves - 1) / kDqWaves)));
+  const dim3 block_dq(64 * kDqWaves);  // waves >= G only stage K / V / K^T
+  const dim3 block_kv(static_cast<unsigned>(64 * std::min<int64_t>(G, D == 64 ? kDkdvWaves64 : 4)));
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (D == 64) {
-    hipLaunchKernelGGL(flash_dq_kernel<64>, grid, block_dq, 0, s, a);
-    hipLaunchKernelGGL((flash_dkdv_kernel<64, 8>), grid, block_kv, 0, s, a);
+    hipLaunchKernelGGL((flash_dq_kernel<64, kDqWaves>), grid_dq, block_dq, 0, s, a);
+    hipLaunchKernelGGL((flash_dkdv_kernel<64, kDkdvWaves64, kKT64>), grid_kv64, block_kv, 0, s, a);
   } else {
-    hipLaunchKernelGGL(flash_dq_kernel<128>, grid, block_dq, 0, s, a);
+    hipLaunchKernelGGL((flash_dq_kernel<128, kDqWaves>), grid_dq, block_dq, 0, s, a);
     hipLaunchKernelGGL((flash_dkdv_kernel<128, 4>), grid, block_kv, 0, s, a);
   }
   DRL_LAUNCH_CHECK();
