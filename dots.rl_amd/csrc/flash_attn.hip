@@ -1012,26 +1012,39 @@ struct DecRaw {
 // positions >= kend of a tail block are zeroed by dec_fix_tail when the block is consumed, not here: a select on
 // the loaded registers right after the load made the wave wait for it (and every load before it) at issue time,
 // which cost the prefetch of every tail block (most decode steps end in a partial block).
+// The loads are buffer loads through descriptors of the wave-uniform K panel / V^T panel / key-valid row (their bases
+// readfirstlane'd, so no waterfall loop: cdna_hip_programming.md T8 / T20) with 32-bit per-lane byte offsets: the
+// 64-bit per-lane index math of flat loads was most of the loop's VALU (52 VALU per MFMA, profiles/r05_pmc_decattn).
 template <int D>
 __device__ __forceinline__ void dec_load_raw(const uint16_t* kb, const uint16_t* vtb, const uint8_t* vrow,
                                              int64_t ld_vt, int64_t ld_valid, int k0, int kend, int lane, int h,
                                              DecRaw<D>& r) {
   constexpr int UPR = D / 8;  // 16-B units per K row
   r.k0 = k0;
-#pragma unroll
-  for (int i = 0; i < D / 16; ++i) {
-    const int c = lane + 64 * i;
-    const int key = k0 + c / UPR;
-    r.k[i] = *reinterpret_cast<const u16x8*>(kb + static_cast<int64_t>(min(key, kend - 1)) * D + 8 * (c % UPR));
-    const int kk = k0 + 8 * (c & 3);
-    r.v[i] = *reinterpret_cast<const u16x8*>(
-        vtb + (ld_vt == DRL_VT_BLOCKED ? vt_index(c >> 2, kk, ld_vt, D)
-                                       : static_cast<int64_t>(c >> 2) * ld_vt + min(static_cast<int64_t>(kk), ld_vt - 8)));
-  }
+  const auto rk = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(uniform64(reinterpret_cast<uint64_t>(kb))),
+                                                    0, 0x7fffffff, 0x00020000);
+  const auto rv = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(uniform64(reinterpret_cast<uint64_t>(vtb))),
+                                                    0, 0x7fffffff, 0x00020000);
+  const auto rb = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(uniform64(reinterpret_cast<uint64_t>(vrow))),
+                                                    0, 0x7fffffff, 0x00020000);
+  // the key-valid words first: the oldest loads of an item, so the consumer waits for them without draining the
+  // next item's loads behind them
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
     const int kk = k0 + 8 * c + 4 * h;
-    r.vb[c] = *reinterpret_cast<const uint32_t*>(vrow + min(static_cast<int64_t>(kk), ld_valid - 4));
+    r.vb[c] = __builtin_amdgcn_raw_buffer_load_b32(rb, min(kk, static_cast<int>(ld_valid) - 4), 0, 0);
+  }
+  const bool blocked = ld_vt == DRL_VT_BLOCKED;
+  const int ldv = static_cast<int>(blocked ? 0 : ld_vt);
+#pragma unroll
+  for (int i = 0; i < D / 16; ++i) {
+    const int c = lane + 64 * i;
+    const int key = min(k0 + c / UPR, kend - 1);
+    r.k[i] = __builtin_bit_cast(u16x8, __builtin_amdgcn_raw_buffer_load_b128(rk, (key * D + 8 * (c % UPR)) * 2, 0, 0));
+    const int d = c >> 2, kk = k0 + 8 * (c & 3);
+    // blocked (key >> 5) * 32 * D + d * 32 + (key & 31) with key = kk, k0 % 32 == 0; else d * ld_vt + key
+    const int vo = blocked ? k0 * D + d * 32 + 8 * (c & 3) : d * ldv + min(kk, ldv - 8);
+    r.v[i] = __builtin_bit_cast(u16x8, __builtin_amdgcn_raw_buffer_load_b128(rv, vo * 2, 0, 0));
   }
 }
 
@@ -1208,7 +1221,7 @@ __global__ __launch_bounds__(64 * NW) void decode_mfma_kernel(DecodeArgs a) {
   __shared__ float s_m[NW][32], s_l[NW][32];
   // per wave: its K / V^T staging slot during the key loop, then its partial O^T (same 64*D*2... bytes)
   __shared__ __attribute__((aligned(16))) float s_o[NW][MT][16][64];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);  // scalar wave index
   const int qi = lane & 31, h = lane >> 5;
   const int64_t bh = a.group > 1 ? dec_grouped_bh(blockIdx.x, a.group, a.Hkv, gridDim.x) : blockIdx.x;
   const int64_t b = bh / a.Hkv;
@@ -1413,8 +1426,9 @@ template <int D, int NW>
 __global__ __launch_bounds__(64 * NW) void decode_group_kernel(DecodeArgs a) {
   constexpr int KS = D / 16, MT = D / 32;
   __shared__ float s_m[NW][32], s_l[NW][32];
+  __shared__ __attribute__((aligned(16))) uint32_t s_vb[NW][4 * 64];  // per wave: the staged item's key-valid words
   __shared__ __attribute__((aligned(16))) float s_o[NW][MT][16][64];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);  // scalar wave index
   const int qi = lane & 31, h = lane >> 5;
   const int G = static_cast<int>(a.G), group = static_cast<int>(a.group);
   const int rpt = 32 / G, ntile = (group + rpt - 1) / rpt;
@@ -1459,8 +1473,13 @@ __global__ __launch_bounds__(64 * NW) void decode_group_kernel(DecodeArgs a) {
   DecRaw<D> R0, R1;  // two items in flight per wave (named registers: static indexing)
   uint16_t* kslot = reinterpret_cast<uint16_t*>(&s_o[w][0][0][0]);
   uint16_t* vslot = kslot + 32 * D;
-  if (items > 0) load(0, R0);
-  if (items > 1) load(1, R1);
+  // every load below is unconditional (item indices clamped to the last item; a phantom item past the end is staged
+  // and consumed as an all-invalid block): with a conditional refill hipcc cannot count the loads behind a register
+  // set and waits for every load in flight (vmcnt(0)) at each stage, one item in flight instead of two
+  if (items > 0) {
+    load(0, R0);
+    load(min(1, items - 1), R1);
+  }
   bf16x8 qf[KS];
   {
     const uint16_t* qrow = a.q + ((bcol * a.Hkv + hd) * a.G + g) * D + 8 * h;
@@ -1476,18 +1495,23 @@ __global__ __launch_bounds__(64 * NW) void decode_group_kernel(DecodeArgs a) {
   for (int mt = 0; mt < MT; ++mt) o[mt] = f32x16{};
   float m = -INFINITY, lsum = 0.f;
   // stage item j to the wave's slot, refill its registers with item j + 2, then the online-softmax step from LDS
+  // the key-valid words go through the wave's LDS slot with K / V^T: carried in registers past the refill of R they
+  // made hipcc wait for every load in flight (vmcnt(0)) at each step, one item in flight instead of two
+  u32x4* vbslot = reinterpret_cast<u32x4*>(&s_vb[w][0]);
   auto step = [&](int j, DecRaw<D>& R) {
     dec_fix_tail<D>(R, kend, a.ld_valid, lane, h);
     dec_stage<D>(R, kslot, vslot, lane);
-    // an own block takes part only in its row's columns
-    const bool act = j < n_sh || (j - n_sh) / n_own == rl;
-    const uint32_t vb[4] = {act ? R.vb[0] : 0u, act ? R.vb[1] : 0u, act ? R.vb[2] : 0u, act ? R.vb[3] : 0u};
-    if (j + 2 < items) load(j + 2, R);
+    // an own block takes part only in its row's columns; a phantom item (j >= items) in none
+    const bool act = j < items && (j < n_sh || (j - n_sh) / n_own == rl);
+    vbslot[lane] = act ? u32x4{R.vb[0], R.vb[1], R.vb[2], R.vb[3]} : u32x4{0u, 0u, 0u, 0u};
+    load(min(j + 2, items - 1), R);  // unconditional refill (past the end: the last item again)
+    const u32x4 v4 = vbslot[lane];
+    const uint32_t vb[4] = {v4[0], v4[1], v4[2], v4[3]};
     dec_block_lds<D>(kslot, vslot, vb, qf, a.scale_log2, qi, h, m, lsum, o);
   };
   for (int j = 0; j < items; j += 2) {
     step(j, R0);
-    if (j + 1 < items) step(j + 1, R1);
+    step(j + 1, R1);  // odd items: the last step is the phantom, an exact no-op on m / lsum / o (alpha = 1, p = 0)
   }
   // merge the NW waves' states per column in wave order (decode_mfma_kernel's non-split merge)
   const float lt = lsum + __shfl_xor(lsum, 32, kWave);
@@ -1644,6 +1668,9 @@ int drl_decode_attention_vt(const void* q, const void* k_cache, const void* vt_c
                 "ld_vt must be a multiple of 8 and key_valid rows 4-byte aligned");
   DRL_CHECK_ARG(aligned16(q) && aligned16(k_cache) && aligned16(vt_cache) && (reinterpret_cast<uintptr_t>(out) & 7u) == 0,
                 "misaligned operand (q, caches 16-byte aligned)");
+  DRL_CHECK_ARG(ld_k * D * 2 < (int64_t(1) << 31) && vt_panel(ld_vt, D, ld_k) * 2 < (int64_t(1) << 31) &&
+                    ld_valid < (int64_t(1) << 31),
+                "one sequence's K / V^T panel and key-valid row must be below 2 GB (31-bit buffer offsets)");
   DRL_CHECK_ARG(group >= 1 && B % group == 0 && shared_keys >= 0 && shared_keys % 32 == 0 && shared_keys <= L &&
                     (group > 1 || shared_keys == 0),
                 "prompt groups: group must divide B, shared_keys a multiple of 32 within L (0 without groups)");
