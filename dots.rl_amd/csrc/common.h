@@ -83,11 +83,9 @@ __device__ __forceinline__ float sigmoid_fast(float x) {
 }
 __device__ __forceinline__ float silu_fast(float x) { return x * sigmoid_fast(x); }
 __device__ __forceinline__ uint16_t f32_to_bf16(float f) {
-  // round-to-nearest-even; NaN stays NaN (quiet bit forced)
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x7fffffu)) return static_cast<uint16_t>((u >> 16) | 0x40u);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return static_cast<uint16_t>(u >> 16);
+  // round-to-nearest-even, NaN stays NaN: gfx950's v_cvt_pk_bf16_f32 (one instruction; the integer form — a NaN
+  // test, a carry add and a shift — was most of the VALU of the bf16-writing streams: K2's backward, the norms)
+  return __builtin_bit_cast(uint16_t, static_cast<__bf16>(f));
 }
 
 // Sampling as a race of exponential clocks (the Gumbel-max form of the categorical draw): token i wins iff
