@@ -501,7 +501,7 @@ if __name__ == "__main__":
             print(json.dumps(r), flush=True)
         sys.exit(0)
     if args.only == "rope":
-        for r in rope() + rope(B=8):
+        for r in rope() + rope(B=8) + rope(B=256):
             print(json.dumps(r), flush=True)
         sys.exit(0)
     if args.only == "decode_split":
