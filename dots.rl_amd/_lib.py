@@ -147,6 +147,8 @@ SIGNATURES = {
     "drl_decode_attention_workspace_bytes": (SZ, [I64, I64, I64, I64, I64]),
     "drl_flash_attn_fwd": (ctypes.c_int, [P, P, P, I32, P, I64, I64, I64, I64, I64, I64, I64, I64, I64, I64, P, F32,
                                           P, P, P]),
+    "drl_flash_attn_fwd_rows": (ctypes.c_int, [P, P, P, I32, P, I64, I64, I64, I64, I64, I64, I64, I64, I64, I64, P,
+                                               F32, P, P, P, P]),
     "drl_decode_attention_vt_workspace_bytes": (SZ, [I64, I64, I64, I64]),
     "drl_decode_attention_set_plan": (None, [I32, I32]),
     "drl_decode_attention_vt": (ctypes.c_int, [P, P, P, I32, P, I64, P, I64, I64, I64, I64, I64, I64, I64, I64, I64,

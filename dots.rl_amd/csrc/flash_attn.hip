@@ -52,6 +52,8 @@ struct FlashArgs {
   // optional (B,): query tiles wholly below q_start[b] are skipped (their out / lse rows are left unwritten) — the
   // shared-prompt copies of prefix sharing, whose outputs nothing reads
   const int32_t* q_start;
+  // optional (B * Tq,): out row of query (b, t) in a packed (rows, Hkv * G * D) out, < 0: not written
+  const int64_t* out_row;
 };
 
 __device__ __forceinline__ bf16x8 as_bf16x8(u16x8 v) { return __builtin_bit_cast(bf16x8, v); }
@@ -390,7 +392,11 @@ __global__ __launch_bounds__(512, D == 64 ? 4 : 1) void flash_fwd_kernel(FlashAr
   const float lt = pair_sum(lsum);
   const float inv = lt > 0.f ? 1.f / lt : 0.f;
   if (!qvalid) return;
-  uint16_t* orow = a.out + (((b * a.Tq + tq) * a.Hkv + (bh % a.Hkv)) * a.G + g) * D;
+  if (a.lse != nullptr && h == 0)
+    a.lse[(bh * a.G + g) * a.Tq + tq] = lt > 0.f ? (m + __builtin_amdgcn_logf(lt)) * 0.6931471805599453f : -INFINITY;
+  const int64_t orw = a.out_row ? a.out_row[b * a.Tq + tq] : (b * a.Tq + tq);
+  if (orw < 0) return;
+  uint16_t* orow = a.out + ((orw * a.Hkv + (bh % a.Hkv)) * a.G + g) * D;
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
 #pragma unroll
@@ -400,8 +406,6 @@ __global__ __launch_bounds__(512, D == 64 ? 4 : 1) void flash_fwd_kernel(FlashAr
       *reinterpret_cast<u16x4*>(orow + 32 * mt + 8 * c + 4 * h) = w;
     }
   }
-  if (a.lse != nullptr && h == 0)
-    a.lse[(bh * a.G + g) * a.Tq + tq] = lt > 0.f ? (m + __builtin_amdgcn_logf(lt)) * 0.6931471805599453f : -INFINITY;
 }
 
 // ------------------------------------------------------------------------------------------ backward
@@ -1575,6 +1579,14 @@ int drl_flash_attn_fwd(const void* q, const void* k, const void* vt, int32_t dt,
                        int64_t ld_valid, int64_t B, int64_t Hkv, int64_t G, int64_t D, int64_t Tq, int64_t Tk,
                        int64_t ld_k, int64_t ld_vt, int64_t qoff, const int32_t* q_start, float scale, void* out,
                        float* lse, void* stream) {
+  return drl_flash_attn_fwd_rows(q, k, vt, dt, key_valid, ld_valid, B, Hkv, G, D, Tq, Tk, ld_k, ld_vt, qoff, q_start,
+                                 scale, out, nullptr, lse, stream);
+}
+
+int drl_flash_attn_fwd_rows(const void* q, const void* k, const void* vt, int32_t dt, const uint8_t* key_valid,
+                            int64_t ld_valid, int64_t B, int64_t Hkv, int64_t G, int64_t D, int64_t Tq, int64_t Tk,
+                            int64_t ld_k, int64_t ld_vt, int64_t qoff, const int32_t* q_start, float scale, void* out,
+                            const int64_t* out_row, float* lse, void* stream) {
   using namespace drl;
   DRL_CHECK_ARG(q && k && vt && key_valid && out, "NULL input");
   DRL_CHECK_ARG(dt == DRL_BF16, "flash attention runs on bf16 operands");
@@ -1590,7 +1602,7 @@ int drl_flash_attn_fwd(const void* q, const void* k, const void* vt, int32_t dt,
                 "misaligned operand");
   FlashArgs a{static_cast<const uint16_t*>(q), static_cast<const uint16_t*>(k), static_cast<const uint16_t*>(vt),
               key_valid, ld_valid, static_cast<uint16_t*>(out), lse, Hkv, G, Tq, Tk, ld_k, ld_vt, qoff,
-              scale * 1.4426950408889634f, q_start};
+              scale * 1.4426950408889634f, q_start, out_row};
   const dim3 grid(static_cast<unsigned>((Tq + 31) / 32), static_cast<unsigned>(B * Hkv));
   const dim3 block(512);  // waves >= G stage K/V only
   hipStream_t s = static_cast<hipStream_t>(stream);

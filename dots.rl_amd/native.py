@@ -762,20 +762,25 @@ def _vt_cap_ok(vt, cap):
     assert vt.dim() != 5 or vt.shape[2] == (cap + 31) // 32, "key-blocked V^T must hold ceil(K capacity / 32) blocks"
 
 
-def flash_attn_fwd(q, k, vt, key_valid, out, Tk=None, qoff=0, lse=None, q_start=None):
+def flash_attn_fwd(q, k, vt, key_valid, out, Tk=None, qoff=0, lse=None, q_start=None, out_rows=None):
     """Fused causal + key-padding attention (MFMA). q (B,Hkv,G,Tq,D) bf16, k (B,Hkv,>=Tk,D) (keys [0,Tk) used),
     vt (B,Hkv,D,ld) with ld >= Tk a multiple of 8; out (B,Tq,Hkv*G*D); lse optional (B,Hkv,G,Tq) fp32;
-    q_start optional (B,) int32: query tiles of row b wholly below q_start[b] skipped (rows left unwritten)."""
-    _dev(q, k, vt, key_valid, out, lse, q_start)
+    q_start optional (B,) int32: query tiles of row b wholly below q_start[b] skipped (rows left unwritten).
+    ``out_rows`` (B*Tq,) int64: out is packed (rows, Hkv*G*D) and query (b, t) writes row out_rows[b*Tq+t] (< 0: not
+    written) — drl_flash_attn_fwd_rows."""
+    _dev(q, k, vt, key_valid, out, lse, q_start, out_rows)
     assert q_start is None or (q_start.dtype == torch.int32 and q_start.numel() == q.shape[0])
     B, Hkv, G, Tq, D = q.shape
     Tk = k.shape[2] if Tk is None else Tk
     assert q.is_contiguous() and k.is_contiguous() and out.is_contiguous()
     assert key_valid.dtype == torch.uint8 and key_valid.stride(1) == 1
+    if out_rows is not None:
+        assert out_rows.dtype == torch.int64 and out_rows.numel() == B * Tq and out_rows.is_contiguous()
+        assert out.dim() == 2 and out.shape[1] == Hkv * G * D
     _vt_cap_ok(vt, k.shape[2])
-    check(lib().drl_flash_attn_fwd(_p(q), _p(k), _p(vt), _edt(q), _p(key_valid), key_valid.stride(0), B, Hkv, G, D,
-                                   Tq, Tk, k.shape[2], vt_ld(vt), qoff, _p(q_start), 1.0 / math.sqrt(D), _p(out),
-                                   _p(lse), _stream()),
+    check(lib().drl_flash_attn_fwd_rows(_p(q), _p(k), _p(vt), _edt(q), _p(key_valid), key_valid.stride(0), B, Hkv, G,
+                                        D, Tq, Tk, k.shape[2], vt_ld(vt), qoff, _p(q_start), 1.0 / math.sqrt(D),
+                                        _p(out), _p(out_rows), _p(lse), _stream()),
           "drl_flash_attn_fwd")
     return out
 

@@ -534,6 +534,13 @@ def _layer_forward(m, i, x_prev, delta, pos, key_valid, save, cache=None, koff=0
     native.rope_qkv_fwd(qkv, pos, m.cos, m.sin, Hq, Hkv, D, q, kbuf, vbuf, koff, koff_dev, vt=vt, src_rows=src_rows,
                         q_skip=qs)
     L = koff + T
+    if flash and rm is not None and cache is None:
+        # forward-only pass over packed rows: the attention writes the packed rows itself (each padded query to its
+        # own packed row; pads without one and the shared copies are not written) — no padded output, no row copy
+        attn = torch.empty(rm.nnz, Hq * D, dtype=dt, device=dev)
+        native.flash_attn_fwd(q, kbuf, vt, key_valid, attn, Tk=L, qoff=L - T, q_start=getattr(rm, "q_start", None),
+                              out_rows=getattr(rm, "inv_own", rm.inv))
+        return _layer_mlp(m, i, x, attn.view(1, rm.nnz, -1), save, kbuf, vbuf, None, q, h1, rstd1)
     if flash:
         attn = torch.empty(B, T, Hq * D, dtype=dt, device=dev)
         native.flash_attn_fwd(q, kbuf, vt, key_valid, attn, Tk=L, qoff=L - T, q_start=getattr(rm, "q_start", None))

@@ -435,6 +435,15 @@ int drl_flash_attn_fwd(const void* q, const void* k, const void* vt, int32_t dt,
                        int64_t ld_valid, int64_t B, int64_t Hkv, int64_t G, int64_t D, int64_t Tq, int64_t Tk,
                        int64_t ld_k, int64_t ld_vt, int64_t qoff, const int32_t* q_start, float scale, void* out,
                        float* lse, void* stream);
+/* drl_flash_attn_fwd writing packed rows (remove-padding / prefix sharing, forward-only passes): out_row (B*Tq,)
+ * int64 gives the out row of query (b, t) — out is (rows, Hkv*G*D) — and a negative entry skips the query's output
+ * (pads; the shared-prompt copies, whose packed row is their leader's). The packed copy the o_proj reads is then
+ * written by the attention itself, with no padded (B, Tq) output and no row copy after it. out_row NULL:
+ * drl_flash_attn_fwd. */
+int drl_flash_attn_fwd_rows(const void* q, const void* k, const void* vt, int32_t dt, const uint8_t* key_valid,
+                            int64_t ld_valid, int64_t B, int64_t Hkv, int64_t G, int64_t D, int64_t Tq, int64_t Tk,
+                            int64_t ld_k, int64_t ld_vt, int64_t qoff, const int32_t* q_start, float scale, void* out,
+                            const int64_t* out_row, float* lse, void* stream);
 /* Decode attention on MFMA over a cache with V head-dim-major: q (B,Hkv,G,D) bf16 (one token), k_cache
  * (B,Hkv,ld_k,D), vt_cache (B,Hkv,D,ld_vt); keys j < L with key_valid[b, j] && j <= qpos (device scalar
  * *qpos_ptr when non-NULL). out (B,Hkv,G,D), or with out_mbt > 0 the (B, Hq*D) panel fragment-packed for

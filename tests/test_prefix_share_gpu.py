@@ -285,6 +285,34 @@ def test_flash_q_start_skips_only_the_copies(D, G):
     assert torch.equal(dk1, dk0) and torch.equal(dv1, dv0)
 
 
+def test_flash_packed_rows_equal_packing_the_padded_output():
+    """drl_flash_attn_fwd_rows: each query written straight to its packed row equals the padded output packed
+    afterwards, bit for bit; rows mapped to -1 (pads, shared copies) leave the packed buffer untouched."""
+    from dots.rl_amd import native
+
+    B, Hkv, G, D, T = 4, 2, 7, 64, 160
+    g = torch.Generator(device="cuda").manual_seed(3)
+    q = torch.randn(B, Hkv, G, T, D, device="cuda", generator=g).to(torch.bfloat16)
+    k = torch.randn(B, Hkv, T, D, device="cuda", generator=g).to(torch.bfloat16)
+    vt = torch.randn(B, Hkv, D, T, device="cuda", generator=g).to(torch.bfloat16)
+    valid = torch.ones(B, T, dtype=torch.uint8, device="cuda")
+    valid[1, :9] = 0
+    valid[3, :40] = 0
+    qs = torch.tensor([0, 70, 0, 64], dtype=torch.int32, device="cuda")
+    own = valid.bool().clone()
+    for b, s_ in enumerate(qs.tolist()):
+        own[b, :s_] = False
+    idx = torch.nonzero(own.reshape(-1)).reshape(-1)
+    rows = torch.full((B * T,), -1, dtype=torch.int64, device="cuda")
+    rows[idx] = torch.arange(idx.numel(), device="cuda")
+    pad = torch.empty(B, T, Hkv * G * D, dtype=torch.bfloat16, device="cuda")
+    native.flash_attn_fwd(q, k, vt, valid, pad, q_start=qs)
+    packed = torch.full((idx.numel() + 3, Hkv * G * D), float("nan"), dtype=torch.bfloat16, device="cuda")
+    native.flash_attn_fwd(q, k, vt, valid, packed, q_start=qs, out_rows=rows)
+    assert torch.equal(packed[:idx.numel()], pad.reshape(B * T, -1)[idx])
+    assert torch.isnan(packed[idx.numel():]).all()
+
+
 def test_fp32_critic_prefix_share_matches_unshared():
     """The critic's values (dp_critic._forward_micro_batch) and its full gradient after a value loss, with and
     without prefix sharing, on the reference tiny critic: fp32 rounding."""
