@@ -155,6 +155,8 @@ SIGNATURES = {
                                                I64, F32, P, I64, P, SZ, P]),
     "drl_flash_attn_bwd": (ctypes.c_int, [P, P, P, P, P, P, P, I32, P, I64, I64, I64, I64, I64, I64, I64, P, F32, P, P, P,
                                           P, P]),
+    "drl_flash_attn_bwd_rows": (ctypes.c_int, [P, P, P, P, P, P, P, P, I32, P, I64, I64, I64, I64, I64, I64, I64, P,
+                                               F32, P, P, P, P, P]),
     "drl_decode_attention": (ctypes.c_int, [P, P, P, I32, P, I64, P, I64, I64, I64, I64, I64, I64, I64, F32, P, P, SZ,
                                             P]),
     "drl_linear_logprob_workspace_bytes": (SZ, [I64, I64, I64]),

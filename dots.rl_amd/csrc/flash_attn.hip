@@ -438,6 +438,9 @@ struct FlashBwdArgs {
   // optional (B,): query tiles wholly below q_start[b] carry no gradient (dO = 0 there): dq is written as zeros,
   // and the dK / dV key loops start at the first kept tile
   const int32_t* q_start;
+  // optional (B * T,): o is packed (rows, Hkv * G * D) and query (b, t) reads row o_row[b * T + t]; a negative entry
+  // (a row whose dO is zero: pads, shared copies) reads row 0 — delta = rowsum(dO * O) = 0 either way
+  const int64_t* o_row;
 };
 
 __device__ __forceinline__ float bf2f(uint16_t x) { return bf16_to_f32(x); }
@@ -569,11 +572,13 @@ __global__ __launch_bounds__(64 * NW) void flash_dq_kernel(FlashBwdArgs a) {
   {
     const uint16_t* qrow = a.q + (head * T + (qvalid ? tq : 0)) * D + 8 * h;
     const int64_t orow_off = (((b * T + (qvalid ? tq : 0)) * a.Hkv + hkv) * a.G + (computes ? g : 0)) * D + 8 * h;
+    const int64_t oq = a.o_row ? max(a.o_row[b * T + (qvalid ? tq : 0)], int64_t(0)) : b * T + (qvalid ? tq : 0);
+    const int64_t oo_off = ((oq * a.Hkv + hkv) * a.G + (computes ? g : 0)) * D + 8 * h;  // O (packed or padded)
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       u16x8 qv = *reinterpret_cast<const u16x8*>(qrow + 16 * s);
       u16x8 dv = *reinterpret_cast<const u16x8*>(a.dout + orow_off + 16 * s);
-      const u16x8 ov = *reinterpret_cast<const u16x8*>(a.o + orow_off + 16 * s);
+      const u16x8 ov = *reinterpret_cast<const u16x8*>(a.o + oo_off + 16 * s);
       if (!qvalid) qv = dv = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
       for (int j = 0; j < 8; ++j) dl = fmaf(bf2f(dv[j]), bf2f(ov[j]), dl);
@@ -1616,6 +1621,15 @@ int drl_flash_attn_bwd(const void* q, const void* k, const void* kt, const void*
                        const float* lse, int32_t dt, const uint8_t* key_valid, int64_t ld_valid, int64_t B,
                        int64_t Hkv, int64_t G, int64_t D, int64_t T, int64_t ld_t, const int32_t* q_start, float scale,
                        float* delta, void* dq, void* dk, void* dv, void* stream) {
+  return drl_flash_attn_bwd_rows(q, k, kt, v, o, nullptr, dout, lse, dt, key_valid, ld_valid, B, Hkv, G, D, T, ld_t,
+                                 q_start, scale, delta, dq, dk, dv, stream);
+}
+
+int drl_flash_attn_bwd_rows(const void* q, const void* k, const void* kt, const void* v, const void* o,
+                            const int64_t* o_row, const void* dout, const float* lse, int32_t dt,
+                            const uint8_t* key_valid, int64_t ld_valid, int64_t B, int64_t Hkv, int64_t G, int64_t D,
+                            int64_t T, int64_t ld_t, const int32_t* q_start, float scale, float* delta, void* dq,
+                            void* dk, void* dv, void* stream) {
   using namespace drl;
   DRL_CHECK_ARG(q && k && kt && v && o && dout && lse && key_valid && delta && dq && dk && dv,
                 "NULL input");
@@ -1627,7 +1641,7 @@ int drl_flash_attn_bwd(const void* q, const void* k, const void* kt, const void*
   FlashBwdArgs a{static_cast<const uint16_t*>(q), static_cast<const uint16_t*>(k), static_cast<const uint16_t*>(kt),
                  static_cast<const uint16_t*>(v), static_cast<const uint16_t*>(o), static_cast<const uint16_t*>(dout),
                  lse, key_valid, ld_valid, delta, static_cast<uint16_t*>(dq), static_cast<uint16_t*>(dk),
-                 static_cast<uint16_t*>(dv), Hkv, G, T, ld_t, scale, scale * 1.4426950408889634f, q_start};
+                 static_cast<uint16_t*>(dv), Hkv, G, T, ld_t, scale, scale * 1.4426950408889634f, q_start, o_row};
   const dim3 grid(static_cast<unsigned>((T + 31) / 32), static_cast<unsigned>(B * Hkv));
   constexpr int kDqWaves = DQ_WAVES, kDkdvWaves64 = DKDV_WAVES64, kKT64 = DKDV_KT64;
   const dim3 grid_kv64(static_cast<unsigned>((T + 32 * kKT64 - 1) / (32 * kKT64)), static_cast<unsigned>(B * Hkv));

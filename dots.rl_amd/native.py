@@ -785,20 +785,23 @@ def flash_attn_fwd(q, k, vt, key_valid, out, Tk=None, qoff=0, lse=None, q_start=
     return out
 
 
-def flash_attn_bwd(q, k, kt, v, o, dout, lse, key_valid, dq, dk, dv, q_start=None):
+def flash_attn_bwd(q, k, kt, v, o, dout, lse, key_valid, dq, dk, dv, q_start=None, o_rows=None):
     """Backward of flash_attn_fwd (Tq == Tk, qoff 0): q (B,Hkv,G,T,D), k/v (B,Hkv,T,D), kt (B,Hkv,D,ld),
     o/dout (B,T,Hq*D), lse (B,Hkv,G,T) -> dq (B,Hkv,G,T,D), dk/dv (B,Hkv,T,D). q_start as in the forward (dout
-    zero on the skipped tiles)."""
-    _dev(q, k, kt, v, o, dout, lse, key_valid, dq, dk, dv, q_start)
+    zero on the skipped tiles). ``o_rows`` (B*T,) int64: o is the packed (rows, Hq*D) output the forward wrote
+    through the same map (drl_flash_attn_bwd_rows; dout zero at the map's negative entries)."""
+    _dev(q, k, kt, v, o, dout, lse, key_valid, dq, dk, dv, q_start, o_rows)
+    if o_rows is not None:
+        assert o_rows.dtype == torch.int64 and o_rows.numel() == q.shape[0] * q.shape[3] and o_rows.is_contiguous()
     assert q_start is None or (q_start.dtype == torch.int32 and q_start.numel() == q.shape[0])
     B, Hkv, G, T, D = q.shape
     assert kt.stride(-1) == 1 and kt.stride(-2) * D == kt.stride(1)
     for t in (q, k, v, o, dout, lse, dq, dk, dv):
         assert t.is_contiguous()
     delta = _ws.get(B * Hkv * G * T * 4, q.device)
-    check(lib().drl_flash_attn_bwd(_p(q), _p(k), _p(kt), _p(v), _p(o), _p(dout), _p(lse), _edt(q), _p(key_valid),
-                                   key_valid.stride(0), B, Hkv, G, D, T, kt.stride(-2), _p(q_start), 1.0 / math.sqrt(D),
-                                   _p(delta), _p(dq), _p(dk), _p(dv), _stream()),
+    check(lib().drl_flash_attn_bwd_rows(_p(q), _p(k), _p(kt), _p(v), _p(o), _p(o_rows), _p(dout), _p(lse), _edt(q),
+                                        _p(key_valid), key_valid.stride(0), B, Hkv, G, D, T, kt.stride(-2),
+                                        _p(q_start), 1.0 / math.sqrt(D), _p(delta), _p(dq), _p(dk), _p(dv), _stream()),
           "drl_flash_attn_bwd")
 
 

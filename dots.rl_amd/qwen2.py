@@ -511,13 +511,21 @@ def _layer_forward(m, i, x_prev, delta, pos, key_valid, save, cache=None, koff=0
         qs = getattr(rm, "q_start", None)  # prefix sharing: q rows the fused kernels never read are not written
         native.rope_qkv_fwd(qkv, pos, m.cos, m.sin, Hq, Hkv, D, q, kbuf, vbuf, kt=kt, vt=vt, src_rows=src_rows,
                             q_skip=qs)
-        attn = torch.empty(B, T, Hq * D, dtype=dt, device=dev)
         lse = torch.empty(B, Hkv, G, T, dtype=torch.float32, device=dev)
-        native.flash_attn_fwd(q, kbuf, vt, key_valid, attn, lse=lse, q_start=qs)
+        if rm is not None:
+            # packed rows written by the attention itself; the backward reads O through the same map
+            rows = getattr(rm, "inv_own", rm.inv)
+            attn = torch.empty(rm.nnz, Hq * D, dtype=dt, device=dev)
+            native.flash_attn_fwd(q, kbuf, vt, key_valid, attn, lse=lse, q_start=qs, out_rows=rows)
+            attn = attn.view(1, rm.nnz, -1)
+            save["o_rows"] = rows
+        else:
+            attn = torch.empty(B, T, Hq * D, dtype=dt, device=dev)
+            native.flash_attn_fwd(q, kbuf, vt, key_valid, attn, lse=lse, q_start=qs)
         del vt
         save.update(kt=kt, lse=lse, key_valid=key_valid, q_start=qs)
         P = "flash"
-        return _layer_mlp(m, i, x, _repack(rm, attn, save), save, kbuf, vbuf, P, q, h1, rstd1)
+        return _layer_mlp(m, i, x, attn, save, kbuf, vbuf, P, q, h1, rstd1)
     vt = None
     if cache is None:
         kbuf = torch.empty(B, Hkv, T, D, dtype=dt, device=dev)
@@ -668,7 +676,7 @@ class _DecoderLayer(torch.autograd.Function):
         attn = sv["attn"]
         if rm is not None:  # attention backward in the padded layout (zero gradient at the pad rows)
             dattn = rm.unpack_grad(dattn)
-            attn = sv["attn_pad"]
+            attn = sv.get("attn_pad", attn)  # the fused path keeps the packed O (read through sv["o_rows"])
             B, T = rm.B, rm.T
         if isinstance(sv["P"], str):  # "flash": fused forward, fused backward
             # fused attention backward (P recomputed from the saved LSE)
@@ -676,7 +684,8 @@ class _DecoderLayer(torch.autograd.Function):
             dk = torch.empty_like(sv["k"])
             dv = torch.empty_like(sv["v"])
             native.flash_attn_bwd(sv["q"], sv["k"], sv["kt"], sv["v"], attn, dattn.view(B, T, Hq * D),
-                                  sv["lse"], sv["key_valid"], dq, dk, dv, q_start=sv["q_start"])
+                                  sv["lse"], sv["key_valid"], dq, dk, dv, q_start=sv["q_start"],
+                                  o_rows=sv.get("o_rows"))
         else:
             dO = dattn.view(B, T, Hkv, G, D).permute(0, 2, 3, 1, 4).reshape(B * Hkv, G * T, D)
             q3 = sv["q"].view(B * Hkv, G * T, D)

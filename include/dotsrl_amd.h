@@ -495,6 +495,14 @@ int drl_flash_attn_bwd(const void* q, const void* k, const void* kt, const void*
                        const float* lse, int32_t dt, const uint8_t* key_valid, int64_t ld_valid, int64_t B,
                        int64_t Hkv, int64_t G, int64_t D, int64_t T, int64_t ld_t, const int32_t* q_start, float scale,
                        float* delta, void* dq, void* dk, void* dv, void* stream);
+/* drl_flash_attn_bwd with o packed (rows, Hkv*G*D) — the forward's drl_flash_attn_fwd_rows output — read through
+ * o_row (B*T,) (the same map; a negative entry reads row 0: those rows' dout is zero, so delta = 0 either way). dout
+ * stays padded (B, T, Hkv*G*D). o_row NULL: drl_flash_attn_bwd. */
+int drl_flash_attn_bwd_rows(const void* q, const void* k, const void* kt, const void* v, const void* o,
+                            const int64_t* o_row, const void* dout, const float* lse, int32_t dt,
+                            const uint8_t* key_valid, int64_t ld_valid, int64_t B, int64_t Hkv, int64_t G, int64_t D,
+                            int64_t T, int64_t ld_t, const int32_t* q_start, float scale, float* delta, void* dq,
+                            void* dk, void* dv, void* stream);
 
 /* A21 fused lm_head + log-prob + entropy (MFMA; logits never written). Replaces FusedLinearForPPO.forward
  * (verl/utils/experimental/torch_functional.py:20-37, :153-216) and the Triton linear_cross_entropy forward

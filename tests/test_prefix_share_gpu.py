@@ -311,6 +311,23 @@ def test_flash_packed_rows_equal_packing_the_padded_output():
     native.flash_attn_fwd(q, k, vt, valid, packed, q_start=qs, out_rows=rows)
     assert torch.equal(packed[:idx.numel()], pad.reshape(B * T, -1)[idx])
     assert torch.isnan(packed[idx.numel():]).all()
+    # the backward reading that packed O through the same map (dout zero at the unmapped rows, as unpack_grad
+    # leaves it) equals the backward over the padded O, bit for bit
+    lse = torch.empty(B, Hkv, G, T, device="cuda")
+    native.flash_attn_fwd(q, k, vt, valid, pad, lse=lse, q_start=qs)
+    packed = packed[:idx.numel()].contiguous()
+    dout = torch.randn(B * T, Hkv * G * D, device="cuda", generator=g).to(torch.bfloat16)
+    dout[rows < 0] = 0
+    dout = dout.view(B, T, -1)
+    kt = k.transpose(-1, -2).contiguous()
+    v = vt.transpose(-1, -2).contiguous()
+    res = []
+    for o, kw in ((pad, {}), (packed, {"o_rows": rows})):
+        dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+        native.flash_attn_bwd(q, k, kt, v, o, dout, lse, valid, dq, dk, dv, q_start=qs, **kw)
+        res.append((dq, dk, dv))
+    for a_, b_ in zip(*res):
+        assert torch.equal(a_, b_)
 
 
 def test_fp32_critic_prefix_share_matches_unshared():
