@@ -24,6 +24,8 @@ valid = torch.ones(B, cap, dtype=torch.uint8, device=DEV)
 q = torch.randn(B, Hkv, G, D, device=DEV, generator=g).to(BF)
 outp = torch.empty(16 * 32 * Hkv * G * D, dtype=BF, device=DEV)
 mbt = (B + 31) // 32
+if os.environ.get("DEC_NW"):  # forced waves per workgroup (drl_decode_attention_set_plan)
+    native.lib().drl_decode_attention_set_plan(int(os.environ["DEC_NW"]), 0)
 a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 res = []
 # the calls are captured in one HIP graph and replayed (the rollout's form): eager launches from Python are
