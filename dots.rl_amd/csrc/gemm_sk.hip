@@ -984,6 +984,12 @@ int drl_gemm(const void* a, int64_t lda, int32_t a_layout, const void* b, int64_
       // other workgroups' slabs one after another (profiles/r05_gemm_wgrad_splitk.jsonl)
       S = std::min(16, cap / g.n_tiles);
       mode = 3;
+    } else if (g.n_tiles * 3 <= cap && g.P < 1024 && !epi_whole_tiles(epilogue)) {
+      // at most a third of the CUs in tiles over a K below 1024 k-pairs (down_proj's weight gradient over the update
+      // pass's tokens: 76 tiles x 642 k-pairs): 3+ slices per tile, 890 -> 698 us against stream-K
+      // (profiles/r05_gemm_pair_probe.jsonl; 2 slices lose: 941 us)
+      S = cap / g.n_tiles;
+      mode = 3;
     } else {
       mode = 1;  // very long K over few tiles (the lm_head dgrad: 32 tiles x 1187 k-pairs): stream-K measured best
     }
