@@ -984,15 +984,22 @@ int drl_gemm(const void* a, int64_t lda, int32_t a_layout, const void* b, int64_
       // other workgroups' slabs one after another (profiles/r05_gemm_wgrad_splitk.jsonl)
       S = std::min(16, cap / g.n_tiles);
       mode = 3;
-    } else if (g.n_tiles * 3 <= cap && g.P < 1024 && !epi_whole_tiles(epilogue)) {
-      // at most a third of the CUs in tiles over a K below 1024 k-pairs (down_proj's weight gradient over the update
-      // pass's tokens: 76 tiles x 642 k-pairs): 3+ slices per tile, 890 -> 698 us against stream-K
-      // (profiles/r05_gemm_pair_probe.jsonl; 2 slices lose: 941 us)
+    } else if (g.n_tiles * 3 <= cap && (g.P < 1024 || g.n_tiles * 4 > cap) && !epi_whole_tiles(epilogue)) {
+      // 3 slices per tile where they fit the CUs (down_proj's weight gradient: 76 tiles x 642 / 1284 k-pairs at 82144 /
+      // 164288 tokens): 890 -> 698 and 1758 -> 1386 us against stream-K (profiles/r05_gemm_pair_probe.jsonl,
+      // profiles/r05_gemm_sk_sweep_pass_rows.jsonl; 2 slices lose: 941 us); 22-63 tiles over >= 1024 k-pairs stay on
+      // stream-K
       S = cap / g.n_tiles;
       mode = 3;
     } else {
       mode = 1;  // very long K over few tiles (the lm_head dgrad: 32 tiles x 1187 k-pairs): stream-K measured best
     }
+  } else if (mode == 0 && epi_is_swiglu(epilogue) && g.n_tiles >= 8 * cap && g_sk.grid == 0) {
+    // the gate_up + SwiGLU forward over a pass's tokens (38 tile columns x 321 / 642 tile rows: 47 / 95 rounds):
+    // persistent whole-tile rounds + a stream-K tail (each split tile's head combines its k-order partials, then the
+    // epilogue runs on the whole tile) against one workgroup per tile: 1282 -> 1232 us at 82144 rows, 2533 -> 2465
+    // at 164288 (profiles/r05_gemm_sk_sweep_pass_rows.jsonl)
+    mode = 1;
   } else if (mode == 0 || mode == 3) {
     // at most 8 splits of >= 6 k-pairs each (profiles/r03_gemm_sk_sweep.jsonl: more or shorter splits lose to the
     // slab traffic and the per-split pipeline fill)

@@ -288,3 +288,35 @@ def test_dgrad_swiglu_bwd_epilogue_matches_unfused(M):
     want2 = torch.empty_like(gu2)
     native.swiglu_bwd(gu2, da2, want2)
     assert torch.equal(native.linear_dgrad_swiglu_bwd(dm, w2, gu2), want2)
+
+
+@pytest.mark.parametrize("M", [14000])
+def test_swiglu_forward_stream_k_matches_whole_tiles(M):
+    """The gate_up + SwiGLU forward over >= 8 rounds of tiles runs persistent whole-tile rounds + a stream-K tail
+    (automatic); against one workgroup per tile (forced whole tiles): gu within one bf16 rounding of the fp32 sums
+    (only the tail's split tiles sum in another order), the SwiGLU output built from the kernel's own gu, and 8
+    launches bit-identical (k-order combine)."""
+    g = torch.Generator(device="cuda").manual_seed(M)
+    x = torch.randn(M, 896, generator=g, device="cuda").to(torch.bfloat16)
+    wgu = (torch.randn(2 * 4864, 896, generator=g, device="cuda") * 0.05).to(torch.bfloat16)
+    gu = torch.empty(M, 2 * 4864, dtype=torch.bfloat16, device="cuda")
+    a = native.linear_fwd(x, wgu, swiglu=True, out_gu=gu)
+    for _ in range(8):
+        gu2 = torch.empty_like(gu)
+        assert torch.equal(native.linear_fwd(x, wgu, swiglu=True, out_gu=gu2), a)
+        assert torch.equal(gu2, gu)
+    native.lib().drl_gemm_set_sk_tuning(0, 0, 2, 0)
+    try:
+        guw = torch.empty_like(gu)
+        aw = native.linear_fwd(x, wgu, swiglu=True, out_gu=guw)
+    finally:
+        native.lib().drl_gemm_set_sk_tuning(0, 0, 0, 0)
+    s = (x.float() @ wgu.float().t())
+    torch.testing.assert_close(gu.float(), s, rtol=8e-3, atol=1e-3)
+    assert (gu.float() - guw.float()).abs().max() <= 8e-3 * s.abs().max()
+    g2, u2 = gu[:, :4864].float(), gu[:, 4864:].float()
+    want = (torch.nn.functional.silu(g2).to(torch.bfloat16).float() * u2).to(torch.bfloat16)
+    torch.testing.assert_close(a.float(), want.float(), rtol=1e-2, atol=1e-3)
+    same = gu == guw
+    assert same.float().mean() > 0.9  # whole-tile rounds give the same bits; only the tail's split tiles may differ
+    assert torch.equal(a[same[:, :4864] & same[:, 4864:]], aw[same[:, :4864] & same[:, 4864:]])

@@ -107,8 +107,8 @@ def main():
         row.update(hipblaslt_us=t_lib, hipblaslt_TF=fl / t_lib / 1e6, ours_us=t_ours, ours_TF=fl / t_ours / 1e6)
         if args.tune:
             sweep = {}
-            for grid, mode, param in [(0, 1, 0), (0, 1, 8), (0, 1, 32), (0, 2, 0), (0, 3, 2), (0, 3, 4), (0, 3, 8),
-                                      (0, 3, 12), (0, 3, 16), (0, 3, 32)]:
+            for grid, mode, param in [(0, 1, 0), (0, 1, 8), (0, 1, 32), (0, 2, 0), (0, 3, 2), (0, 3, 3), (0, 3, 4),
+                                      (0, 3, 5), (0, 3, 6), (0, 3, 8), (0, 3, 10), (0, 3, 12), (0, 3, 16), (0, 3, 32)]:
                 if mode == 3 and param and param * ((M + 255) // 256) * ((N + 255) // 256) > 256:
                     continue
                 native.lib().drl_gemm_set_sk_tuning(grid, 0, mode, param)
