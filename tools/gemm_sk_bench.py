@@ -49,7 +49,8 @@ def shapes(quick, rows=None, decode=None):
                 ("down_fwd", "fwd", M, H, I)]
         if M in train:
             out += [("qkv_dgrad", "dgrad", M, H, NQ), ("o_dgrad", "dgrad", M, H, H), ("gate_up_dgrad", "dgrad", M, H, 2 * I),
-                    ("down_dgrad", "dgrad", M, I, H), ("qkv_wgrad", "wgrad", NQ, H, M), ("o_wgrad", "wgrad", H, H, M),
+                    ("down_dgrad", "dgrad", M, I, H), ("down_dgrad_swiglu_bwd", "dgrad_swiglu", M, I, H),
+                    ("qkv_wgrad", "wgrad", NQ, H, M), ("o_wgrad", "wgrad", H, H, M),
                     ("gate_up_wgrad", "wgrad", 2 * I, H, M), ("down_wgrad", "wgrad", H, I, M)]
     R = (max(train) // 768) * 256  # response rows of the pass (256 of every 768-token sequence)
     out += [("lm_head_fwd", "fwd", R, V, H), ("lm_head_dgrad", "dgrad", R, H, V), ("lm_head_wgrad", "wgrad", V, H, R)]
@@ -90,6 +91,12 @@ def main():
             a = torch.empty(M, N // 2, device=dev, dtype=bf)
             ours = lambda: native.linear_fwd(x, w, swiglu=sw)  # noqa: E731
             lib = (lambda: native.swiglu_fwd(x @ w.t(), a)) if sw else (lambda: x @ w.t())  # noqa: E731
+        elif kind == "dgrad_swiglu":  # da (M, N) = dy (M, K) @ Wd (K, N), then the SwiGLU backward into dgu (M, 2N)
+            dy = torch.randn(M, K, generator=g, device=dev).to(bf)
+            w = (torch.randn(K, N, generator=g, device=dev) * 0.05).to(bf)
+            gu = torch.randn(M, 2 * N, generator=g, device=dev).to(bf)
+            ours = lambda: native.linear_dgrad_swiglu_bwd(dy, w, gu)  # noqa: E731
+            lib = lambda: native.swiglu_bwd(gu, dy @ w, torch.empty_like(gu))  # noqa: E731
         elif kind == "dgrad":  # dx (M, N) = dy (M, K) @ W (K, N)
             dy = torch.randn(M, K, generator=g, device=dev).to(bf)
             w = (torch.randn(K, N, generator=g, device=dev) * 0.05).to(bf)
