@@ -65,6 +65,7 @@ struct SkArgs {
   unsigned* flags;     // gridDim.x publish flags + 1 timeout word (zero between launches)
   int64_t lda, ldb, ldc, ldc2;
   uint32_t a_bytes, b_bytes;
+  int64_t a_total;     // > 0: a layout-K A operand beyond one buffer range, its descriptor rebased per tile (a + m0 rows)
   int M, N, K;
   int tm, tn, gm;      // tiles along M and N; M-tiles per rasterization group
   int P;               // k-tile pairs per tile
@@ -125,7 +126,8 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
                      ? static_cast<int>(blockIdx.x)
                      : xcd_remap(blockIdx.x, tail_mode ? g.sk_base : G);
   const int half = g.N / 2;
-  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)g.a, (short)0, (int)g.a_bytes, 0x00020000);
+  __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)g.a, (short)0, (int)g.a_bytes, 0x00020000);
+  uint32_t a_end = g.a_bytes;  // ra's byte range (the out-of-range soffset of a phantom k-tile)
   const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)g.b, (short)0, (int)g.b_bytes, 0x00020000);
 
   // per-lane byte offsets of this wave's two copy instructions of each half-tile h (0 A0, 1 A1, 2 B0, 3 B1) for the
@@ -135,6 +137,17 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
   const uint32_t kstep_b = BT ? static_cast<uint32_t>(64 * g.ldb * 2) : 128u;
 
   auto setup_tile = [&](int m0, int n0) {
+    int am0 = m0;  // A rows are addressed from the descriptor's base row
+    if constexpr (!AT) {
+      if (g.a_total > 0) {  // the tile's rows onward as their own buffer range (every offset below stays 32-bit)
+        const int64_t off = static_cast<int64_t>(m0) * g.lda * 2;
+        const int64_t rem = g.a_total - off;
+        a_end = static_cast<uint32_t>(rem < 0x7fffffff ? rem : 0x7fffffff);
+        ra = __builtin_amdgcn_make_buffer_rsrc((void*)(reinterpret_cast<const char*>(g.a) + off), (short)0, (int)a_end,
+                                               0x00020000);
+        am0 = 0;
+      }
+    }
 #pragma unroll
     for (int h = 0; h < 4; ++h)
 #pragma unroll
@@ -146,7 +159,7 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
           const int hr = 8 * q + (lane >> 3), up = lane & 7;
           int grow;
           if (is_a) {
-            grow = m0 + (h & 1) * 128 + hr;
+            grow = am0 + (h & 1) * 128 + hr;
           } else if constexpr (EPI == EPI_SWIGLU) {
             // tile row blocks of 16 alternate gate / up rows of the same 16 output columns
             const int row = (hr >> 5) * 64 + (h & 1) * 32 + (hr & 31);
@@ -172,7 +185,7 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
     uint16_t* dst = lds + lds_half(h, buf);
     const bool is_a = h < 2;
     // k-tile past the data (K % 128 == 64): an soffset of the whole byte range puts every lane out of range (zeros)
-    const uint32_t soff = k >= g.nkt ? (is_a ? g.a_bytes : g.b_bytes)
+    const uint32_t soff = k >= g.nkt ? (is_a ? a_end : g.b_bytes)
                                      : static_cast<uint32_t>(k) * (is_a ? kstep_a : kstep_b);
 #pragma unroll
     for (int c = 0; c < 2; ++c)
@@ -868,22 +881,11 @@ int drl_gemm(const void* a, int64_t lda, int32_t a_layout, const void* b, int64_
              int64_t ldc, int32_t c_dtype, int32_t beta, int64_t M, int64_t N, int64_t K, const void* bias,
              int32_t epilogue, void* c2, int64_t ldc2, void* workspace, int64_t workspace_bytes, void* stream) {
   using namespace drl;
-  // a layout-K A operand beyond one buffer range (e.g. the prefill's 262144 x 4864 down_proj input): launches over
-  // row blocks (multiples of the 256-row tile), each with its own operand / output base — the same tiles, the same
-  // result
-  if (a_layout == DRL_LAYOUT_K && a && lda > 0 && M * lda * 2 + 320ll * lda * 2 >= (1ll << 31)) {
-    const int64_t rows = std::max<int64_t>(256, ((1ll << 31) / (lda * 2) - 320) / 256 * 256);
-    const int64_t es = c_dtype == DRL_F32 ? 4 : 2;
-    for (int64_t m0 = 0; m0 < M; m0 += rows) {
-      const int64_t mm = std::min(rows, M - m0);
-      const int rc = drl_gemm(static_cast<const char*>(a) + m0 * lda * 2, lda, a_layout, b, ldb, b_layout,
-                              static_cast<char*>(c) + m0 * ldc * es, ldc, c_dtype, beta, mm, N, K, bias, epilogue,
-                              c2 ? static_cast<char*>(c2) + m0 * ldc2 * 2 : nullptr, ldc2, workspace, workspace_bytes,
-                              stream);
-      if (rc != DRL_OK) return rc;
-    }
-    return DRL_OK;
-  }
+  // a layout-K A operand beyond one buffer range (the lm_head input gradient's d_logits, 65536 x 151936 bf16 = 19.9 GB;
+  // the prefill's 262144 x 4864 down_proj input) runs as ONE launch whose A descriptor is rebased per tile (base row m0,
+  // 32-bit offsets within the tile's rows onward) — round 4 launched row blocks of 26 tile rows each, 104 tiles over
+  // 256 CUs per launch; the same tiles, the same result
+  const bool a_rebase = a_layout == DRL_LAYOUT_K && a && lda > 0 && M * lda * 2 + 320ll * lda * 2 >= (1ll << 31);
   // a layout-T operand beyond one buffer range has K along its rows (the weight gradient over a long token batch, e.g.
   // the lm_head's d_logits^T at 8192 rows x 151936): K blocks of whole 128-deep k-pairs accumulated into the fp32
   // output (the first block with the caller's beta, the rest with beta = 1)
@@ -930,7 +932,8 @@ int drl_gemm(const void* a, int64_t lda, int32_t a_layout, const void* b, int64_
   // 32-bit buffer offsets: the byte range plus one tile of overhang must stay below 2^32
   const int64_t a_bytes = a_rows * lda * 2, b_bytes = b_rows * ldb * 2;
   // (below 2 GB: voffset + a whole-range soffset must not wrap around 2^32)
-  DRL_CHECK_ARG(a_bytes + 320ll * lda * 2 < (1ll << 31) && b_bytes + 320ll * ldb * 2 < (1ll << 31),
+  DRL_CHECK_ARG((a_rebase ? 576ll * lda * 2 : a_bytes + 320ll * lda * 2) < (1ll << 31) &&
+                    b_bytes + 320ll * ldb * 2 < (1ll << 31),
                 "operand larger than the 2 GB buffer range");
   const int64_t ncols = epilogue == DRL_GEMM_SWIGLU ? N / 2 : N;
   DRL_CHECK_ARG(ldc >= ncols && (c2 == nullptr || ldc2 >= N), "ldc");
@@ -946,7 +949,8 @@ int drl_gemm(const void* a, int64_t lda, int32_t a_layout, const void* b, int64_
   g.c2 = static_cast<uint16_t*>(c2);
   g.bias = static_cast<const uint16_t*>(bias);
   g.lda = lda; g.ldb = ldb; g.ldc = ldc; g.ldc2 = ldc2;
-  g.a_bytes = static_cast<uint32_t>(a_bytes);
+  g.a_bytes = static_cast<uint32_t>(a_rebase ? 0 : a_bytes);
+  g.a_total = a_rebase ? a_bytes : 0;
   g.b_bytes = static_cast<uint32_t>(b_bytes);
   g.M = static_cast<int>(M); g.N = static_cast<int>(N); g.K = static_cast<int>(K);
   g.beta = beta ? 1 : 0;

@@ -208,9 +208,10 @@ def test_race_screen(al, bl, M, N, K, mode):
     assert int(flags.abs().sum()) == 0  # every flag consumed and reset, no residency timeout recorded
 
 
-def test_operand_over_2gb_runs_as_row_blocks():
-    """The prefill's down_proj input (512 x 512 rows x 4864) is 2.5 GB, past one buffer range: drl_gemm launches
-    over row blocks; spot rows from each block against the fp32 reference."""
+def test_operand_over_2gb_rebases_per_tile():
+    """The prefill's down_proj input (512 x 512 rows x 4864) is 2.5 GB, past one buffer range: drl_gemm runs one
+    launch whose A descriptor is rebased per tile row; spot rows (first / last tiles, round-4 block edges) against the
+    fp32 reference."""
     M, N, K = 262144, 896, 4864
     g = torch.Generator(device="cuda").manual_seed(3)
     a = torch.empty(M, K, dtype=torch.bfloat16, device="cuda")
@@ -222,6 +223,22 @@ def test_operand_over_2gb_runs_as_row_blocks():
     ref = a[rows].float() @ b.float().t()
     torch.testing.assert_close(out[rows].float(), ref.to(torch.bfloat16).float(), rtol=8e-3, atol=2e-3)
     del a, out
+
+
+@pytest.mark.parametrize("M", [7000, 7168])
+def test_lm_head_dgrad_operand_over_2gb(M):
+    """The lm_head input gradient: d_logits (M x 151936 bf16, > 2 GB) as the layout-K A operand of dx = dy W with
+    W (151936, 896) layout T — one launch, A rebased per tile; the last tile's rows past M read as zeros (M = 7000).
+    Spot rows against fp32 torch."""
+    K, N = 151936, 896
+    g = torch.Generator(device="cuda").manual_seed(M)
+    dy = torch.randn(M, K, generator=g, device="cuda").to(torch.bfloat16)
+    w = (torch.randn(K, N, generator=g, device="cuda") * 0.05).to(torch.bfloat16)
+    dx = native.linear_dgrad(dy, w)
+    rows = torch.tensor([0, 255, 256, 3333, 6655, 6656, M - 2, M - 1], device="cuda")
+    ref = dy[rows].float() @ w.float()
+    torch.testing.assert_close(dx[rows].float(), ref.to(torch.bfloat16).float(), rtol=1e-2, atol=2e-2)
+    del dy, dx
 
 
 def test_wgrad_operand_over_2gb_splits_k():
