@@ -283,10 +283,10 @@ def main():
         freeze_host_heap()
     timer = native.KernelTimer(args.roofline_kernel, ROOFLINE[args.roofline_kernel][0], TAGS.get(args.roofline_kernel))
     mark = os.environ.get("DRL_TRACE_MARK") == "1"  # a spin kernel on each side of the timed steps (trace windows)
+    dist.barrier()  # (the first barrier of a run builds the communicator: seconds, kept out of the trace window)
+    torch.cuda.synchronize()
     if mark:
         torch.cuda._sleep(1000)
-    dist.barrier()
-    torch.cuda.synchronize()
     ms0 = torch.cuda.memory_stats()
     t0 = time.perf_counter()
     hist = []
