@@ -1030,9 +1030,10 @@ int drl_gemm(const void* a, int64_t lda, int32_t a_layout, const void* b, int64_
     // over a long K (>= 16 k-pairs) those r tiles split K over S = cap / r slices instead (uniform split-K, <= 16
     // slices): down_proj's forward at the update pass's 82144 rows 628 -> 611 us; at K = 896 (7 k-pairs) the slices'
     // pipeline fill and combine cost more than the round they save (o_proj dgrad 151 -> 157 us), so not there
-    // (profiles/r05_gemm_tail_splitk.jsonl)
+    // (profiles/r05_gemm_tail_splitk.jsonl); up to a third of the CUs since the lm_head weight gradient's K blocks
+    // (2376 tiles, r = 72, 52 k-pairs): 17.73 -> 17.33 ms per call (profiles/r05_gemm_tail3_lm_head_wgrad.jsonl)
     const int r = g.n_tiles % cap;
-    if (g_sk.mode == 0 && g_sk.grid == 0 && !epi_whole_tiles(epilogue) && g.n_tiles > cap && r > 0 && 4 * r <= cap &&
+    if (g_sk.mode == 0 && g_sk.grid == 0 && !epi_whole_tiles(epilogue) && g.n_tiles > cap && r > 0 && 3 * r <= cap &&
         g.P >= 16) {
       const int St = std::min({16, cap / r, g.P / 2});
       if (St >= 2) {
