@@ -72,14 +72,11 @@ def _gemm_sk_flops(a):
 
 
 def _gemm_sk_dispatches(a):
-    """Kernel dispatches of one drl_gemm call (rocprof counts these; the KernelTimer counts calls): an operand past
-    the 2 GB buffer range is split over several dispatches (csrc/gemm_sk.hip, drl_gemm: row blocks of a layout-K A,
-    K blocks of a layout-T operand)."""
+    """Kernel dispatches of one drl_gemm call (rocprof counts these; the KernelTimer counts calls): a layout-T operand
+    past the 2 GB buffer range is split over K blocks, one dispatch each (csrc/gemm_sk.hip, drl_gemm); a layout-K A
+    past it runs as one dispatch with its descriptor rebased per tile."""
     lda, a_layout, ldb, b_layout, M, N, K = a[1], a[2], a[4], a[5], a[10], a[11], a[12]
     lim = 1 << 31
-    if a_layout == 0 and lda > 0 and M * lda * 2 + 320 * lda * 2 >= lim:
-        rows = max(256, (lim // (lda * 2) - 320) // 256 * 256)
-        return sum(_gemm_sk_dispatches(a[:10] + (min(rows, M - m0),) + a[11:]) for m0 in range(0, M, rows))
     tb = [K * ld * 2 + 320 * ld * 2 if lay == 1 else 0 for lay, ld in ((a_layout, lda), (b_layout, ldb))]
     if max(tb) >= lim:
         ld = max(lda if a_layout == 1 else 0, ldb if b_layout == 1 else 0)

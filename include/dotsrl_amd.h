@@ -599,7 +599,8 @@ int drl_decode_rope(const float* partials, int32_t nsplit, const void* bias, con
  * dW += dy^T x (grad_weight, accumulated over micro-batches in fp32 as FSDP's fp32 gradient).
  *   C(m, n) (+)= sum_k A(m, k) B(n, k),  A(m, k) = a[m*lda + k] (DRL_LAYOUT_K) or a[k*lda + m] (DRL_LAYOUT_T),
  *                                        B(n, k) = b[n*ldb + k] (DRL_LAYOUT_K) or b[k*ldb + n] (DRL_LAYOUT_T).
- * bf16 operands, fp32 accumulation (a layout-K A operand over 2 GB runs as row blocks). c_dtype DRL_BF16 epilogues
+ * bf16 operands, fp32 accumulation (a layout-K A operand over 2 GB runs as one launch, its buffer descriptor
+ * rebased per tile). c_dtype DRL_BF16 epilogues
  * (bias / SwiGLU need both operands layout K): PLAIN c (M, N) = bf16(acc); BIAS c = bf16(acc + bias) (addmm: one
  * rounding); SWIGLU: B = [gate | up] (N = 2I rows), c (M, I) = bf16(bf16(silu(g)) * u) with g, u the bf16-rounded
  * gate / up sums, c2 (M, 2I) = [g | u] when not NULL (the backward's saved activation); DRL_F32 (plain epilogue): c = acc, or c += acc when beta != 0. K % 64 == 0 unless both
