@@ -1023,7 +1023,7 @@ struct DecRaw {
 // which cost the prefetch of every tail block (most decode steps end in a partial block).
 // The loads are buffer loads through descriptors of the wave-uniform K panel / V^T panel / key-valid row (their bases
 // readfirstlane'd, so no waterfall loop: cdna_hip_programming.md T8 / T20) with 32-bit per-lane byte offsets: the
-// 64-bit per-lane index math of flat loads was most of the loop's VALU (52 VALU per MFMA, profiles/r05_pmc_decattn).
+// 64-bit per-lane index math of flat loads was most of the loop's VALU (52 VALU per MFMA, profiles/r05_pmc_decattn_sq.json).
 template <int D>
 __device__ __forceinline__ void dec_load_raw(const uint16_t* kb, const uint16_t* vtb, const uint8_t* vrow,
                                              int64_t ld_vt, int64_t ld_valid, int k0, int kend, int lane, int h,
