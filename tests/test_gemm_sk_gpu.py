@@ -337,3 +337,19 @@ def test_swiglu_forward_stream_k_matches_whole_tiles(M):
     same = gu == guw
     assert same.float().mean() > 0.9  # whole-tile rounds give the same bits; only the tail's split tiles may differ
     assert torch.equal(a[same[:, :4864] & same[:, 4864:]], aw[same[:, :4864] & same[:, 4864:]])
+
+
+@pytest.mark.parametrize("T", [82144])
+def test_down_wgrad_automatic_split_k(T):
+    """down_proj's weight gradient over the update pass's tokens (76 tiles x 642 k-pairs) takes 3 uniform split-K
+    slices automatically: against fp32 torch (accumulated onto a non-zero gradient), and reproducible bit for bit."""
+    g = torch.Generator(device="cuda").manual_seed(T)
+    dy = torch.randn(T, 896, generator=g, device="cuda").to(torch.bfloat16)
+    x = torch.randn(T, 4864, generator=g, device="cuda").to(torch.bfloat16)
+    gw = torch.full((896, 4864), 0.5, device="cuda")
+    native.linear_wgrad(gw, dy, x)
+    ref = 0.5 + dy.double().t() @ x.double()  # fp64: the fp32 sums' summation-order error alone, ~1e-5 sqrt(T)
+    torch.testing.assert_close(gw.double(), ref, rtol=1e-6, atol=1e-5 * T ** 0.5)
+    gw2 = torch.full((896, 4864), 0.5, device="cuda")
+    native.linear_wgrad(gw2, dy, x)
+    assert torch.equal(gw, gw2)
