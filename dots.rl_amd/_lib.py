@@ -171,6 +171,7 @@ SIGNATURES = {
     "drl_gemm_workspace_bytes": (ctypes.c_int64, []),
     "drl_gemm_set_sk_tuning": (None, [I32, I32, I32, I32]),
     "drl_gemm_set_debug": (None, [I32]),
+    "drl_gemm_plan": (ctypes.c_int, [I64, I64, I64, I32, I32, P]),
     "drl_copy_rows": (ctypes.c_int, [P, I64, P, P, I64, P, I64, I64, P]),
     "drl_gather_rows": (ctypes.c_int, [P, I64, P, P, I64, I64, I64, P]),
     "drl_sum_rows": (ctypes.c_int, [P, I64, P, I64, P, I64, P, I64, I64, I32, P]),

@@ -859,6 +859,96 @@ int launch_sk_layout(SkArgs& g, int epi, int grid, hipStream_t s) {
 }  // namespace
 }  // namespace drl
 
+namespace drl {
+namespace {
+// The decomposition of one launch from its tile grid (g.tm, g.tn, g.P, g.n_tiles set) and the CU count: sets
+// g.splits / g.dp_tiles / g.sk_base / g.sk_tile0, the grid and the mode (1 stream-K, 2 whole tiles, 3 uniform
+// split-K). Host-only arithmetic (drl_gemm_plan reports it without a device).
+int plan_decomposition(SkArgs& g, int epilogue, int cus, int& grid, int& mode) {
+  // decomposition (grid never above the CU count: co-residency). Automatic: uniform split-K when the tiles fill at
+  // most half the CUs and K is long enough to split (S = the most splits that fit the CUs, >= 2 k-pairs each, <= 16;
+  // the SwiGLU epilogue pairs whole tiles, never split), else whole tiles in rounds.
+  const int cap = g_sk.grid > 0 ? std::min(g_sk.grid, cus) : cus;
+  grid = cap;
+  mode = g_sk.mode;
+  int S = 1;
+  if (mode == 0 && g.n_tiles * 2 <= cap && g.P >= 256 && !epi_is_swiglu(epilogue)) {
+    if (g.n_tiles * 12 <= cap && !epi_whole_tiles(epilogue)) {
+      // very long K over at most a twelfth of the CUs in tiles (the small projections' weight gradients over the
+      // update pass's tokens: o 16, qkv 20 tiles x 642 k-pairs): uniform split-K over every CU, up to 16 slices —
+      // 246 -> 198 us (o, 12 slices) and 340 -> 264 us (qkv, 8 slices) against stream-K, whose tile heads add the
+      // other workgroups' slabs one after another (profiles/r05_gemm_wgrad_splitk.jsonl)
+      S = std::min(16, cap / g.n_tiles);
+      mode = 3;
+    } else if (g.n_tiles * 3 <= cap && (g.P < 1024 || g.n_tiles * 4 > cap) && !epi_whole_tiles(epilogue)) {
+      // 3 slices per tile where they fit the CUs (down_proj's weight gradient: 76 tiles x 642 / 1284 k-pairs at 82144 /
+      // 164288 tokens): 890 -> 698 and 1758 -> 1386 us against stream-K (profiles/r05_gemm_pair_probe.jsonl,
+      // profiles/r05_gemm_sk_sweep_pass_rows.jsonl; 2 slices lose: 941 us); 22-63 tiles over >= 1024 k-pairs stay on
+      // stream-K
+      S = cap / g.n_tiles;
+      mode = 3;
+    } else {
+      mode = 1;  // very long K over few tiles (the lm_head dgrad: 32 tiles x 1187 k-pairs): stream-K measured best
+    }
+  } else if (mode == 0 && epi_is_swiglu(epilogue) && g.n_tiles >= 8 * cap && g_sk.grid == 0) {
+    // the gate_up + SwiGLU forward over a pass's tokens (38 tile columns x 321 / 642 tile rows: 47 / 95 rounds):
+    // persistent whole-tile rounds + a stream-K tail (each split tile's head combines its k-order partials, then the
+    // epilogue runs on the whole tile) against one workgroup per tile: 1282 -> 1232 us at 82144 rows, 2533 -> 2465
+    // at 164288 (profiles/r05_gemm_sk_sweep_pass_rows.jsonl)
+    mode = 1;
+  } else if (mode == 0 || mode == 3) {
+    // at most 8 splits of >= 6 k-pairs each (profiles/r03_gemm_sk_sweep.jsonl: more or shorter splits lose to the
+    // slab traffic and the per-split pipeline fill)
+    S = mode == 3 && g_sk.param > 0 ? g_sk.param : std::min({cap / std::max(1, g.n_tiles), 8, g.P / 6});
+    S = std::max(1, std::min({S, g.P, 32, cap / std::max(1, g.n_tiles)}));
+    if (epi_whole_tiles(epilogue) || g.n_tiles * 2 > cap) S = 1;
+    mode = S > 1 ? 3 : 2;
+  }
+  g.splits = 1;
+  if (mode == 3 && epi_whole_tiles(epilogue)) mode = 2;  // a forced split-K tuning: whole tiles instead
+  if (mode == 3) {
+    g.splits = S;
+    g.dp_tiles = 0;
+    g.sk_base = g.sk_tile0 = 0;
+    grid = g.n_tiles * S;
+  } else if (mode == 2) {
+    // whole tiles, one workgroup per tile (no workgroup waits on another, so no co-residency is needed): the hardware
+    // deals tiles to CUs as they free up, so a kernel on a second stream (the weight gradient beside its input
+    // gradient) fills the CUs a short grid leaves idle instead of waiting behind a persistent grid's static rounds
+    g.dp_tiles = g.n_tiles;
+    grid = g_sk.grid > 0 ? std::min(cap, g.n_tiles) : g.n_tiles;
+    // a last round of at most a quarter of the CUs (the N = 896 outputs at the passes' token counts: 1284 = 5 x 256
+    // + 4 tiles, 2568 = 10 x 256 + 8) would hold the whole launch for one more tile time while the other CUs idle:
+    // over a long K (>= 16 k-pairs) those r tiles split K over S = cap / r slices instead (uniform split-K, <= 16
+    // slices): down_proj's forward at the update pass's 82144 rows 628 -> 611 us; at K = 896 (7 k-pairs) the slices'
+    // pipeline fill and combine cost more than the round they save (o_proj dgrad 151 -> 157 us), so not there
+    // (profiles/r05_gemm_tail_splitk.jsonl); up to a third of the CUs since the lm_head weight gradient's K blocks
+    // (2376 tiles, r = 72, 52 k-pairs): 17.73 -> 17.33 ms per call (profiles/r05_gemm_tail3_lm_head_wgrad.jsonl)
+    const int r = g.n_tiles % cap;
+    if (g_sk.mode == 0 && g_sk.grid == 0 && !epi_whole_tiles(epilogue) && g.n_tiles > cap && r > 0 && 3 * r <= cap &&
+        g.P >= 16) {
+      const int St = std::min({16, cap / r, g.P / 2});
+      if (St >= 2) {
+        g.splits = St;
+        g.dp_tiles = g.sk_base = g.sk_tile0 = g.n_tiles - r;
+        grid = g.n_tiles - r + r * St;
+      }
+    }
+  } else {
+    const int full = g.n_tiles / grid;
+    const int dp = (g.n_tiles % grid == 0) ? g.n_tiles : std::max(0, full - 1) * grid;
+    g.dp_tiles = dp;
+    const int64_t I = static_cast<int64_t>(g.n_tiles - dp) * g.P;
+    const int min_iters = g_sk.param > 0 ? g_sk.param : 2;
+    DRL_CHECK_ARG(I < (1 << 23), "stream-K iteration space too large");
+    if (dp == 0 && I > 0) grid = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(grid, I / min_iters)));
+  }
+  return DRL_OK;
+}
+
+}  // namespace
+}  // namespace drl
+
 extern "C" {
 
 int64_t drl_gemm_workspace_bytes(void) {
@@ -868,6 +958,25 @@ int64_t drl_gemm_workspace_bytes(void) {
 }
 
 void drl_gemm_set_debug(int32_t flags) { drl::g_sk_dbg = flags; }
+
+int drl_gemm_plan(int64_t M, int64_t N, int64_t K, int32_t epilogue, int32_t cus, int32_t* info) {
+  using namespace drl;
+  DRL_CHECK_ARG(info != nullptr && M >= 1 && N >= 1 && K >= 1 && cus >= 1, "bad plan query");
+  DRL_CHECK_ARG(epilogue >= DRL_GEMM_PLAIN && epilogue <= DRL_GEMM_SWIGLU_BWD, "unknown epilogue %d", epilogue);
+  SkArgs g{};
+  g.tm = static_cast<int>((M + 255) / 256);
+  g.tn = static_cast<int>((N + 255) / 256);
+  g.P = static_cast<int>((K + 127) / 128);
+  g.n_tiles = g.tm * g.tn;
+  int grid = 0, mode = 0;
+  if (const int rc = plan_decomposition(g, epilogue, cus, grid, mode); rc != DRL_OK) return rc;
+  info[0] = mode;
+  info[1] = g.splits;
+  info[2] = grid;
+  info[3] = g.dp_tiles;
+  info[4] = g.sk_base;
+  return DRL_OK;
+}
 
 void drl_gemm_set_sk_tuning(int32_t grid, int32_t group, int32_t mode, int32_t param) {
   drl::g_sk.grid = grid > 0 ? grid : 0;
@@ -973,84 +1082,8 @@ int drl_gemm(const void* a, int64_t lda, int32_t a_layout, const void* b, int64_
   g.ws = static_cast<float*>(workspace);
   g.flags = reinterpret_cast<unsigned*>(static_cast<char*>(workspace) + static_cast<int64_t>(cus) * SLAB * 4);
 
-  // decomposition (grid never above the CU count: co-residency). Automatic: uniform split-K when the tiles fill at
-  // most half the CUs and K is long enough to split (S = the most splits that fit the CUs, >= 2 k-pairs each, <= 16;
-  // the SwiGLU epilogue pairs whole tiles, never split), else whole tiles in rounds.
-  const int cap = g_sk.grid > 0 ? std::min(g_sk.grid, cus) : cus;
-  int grid = cap;
-  int mode = g_sk.mode;
-  int S = 1;
-  if (mode == 0 && g.n_tiles * 2 <= cap && g.P >= 256 && !epi_is_swiglu(epilogue)) {
-    if (g.n_tiles * 12 <= cap && !epi_whole_tiles(epilogue)) {
-      // very long K over at most a twelfth of the CUs in tiles (the small projections' weight gradients over the
-      // update pass's tokens: o 16, qkv 20 tiles x 642 k-pairs): uniform split-K over every CU, up to 16 slices —
-      // 246 -> 198 us (o, 12 slices) and 340 -> 264 us (qkv, 8 slices) against stream-K, whose tile heads add the
-      // other workgroups' slabs one after another (profiles/r05_gemm_wgrad_splitk.jsonl)
-      S = std::min(16, cap / g.n_tiles);
-      mode = 3;
-    } else if (g.n_tiles * 3 <= cap && (g.P < 1024 || g.n_tiles * 4 > cap) && !epi_whole_tiles(epilogue)) {
-      // 3 slices per tile where they fit the CUs (down_proj's weight gradient: 76 tiles x 642 / 1284 k-pairs at 82144 /
-      // 164288 tokens): 890 -> 698 and 1758 -> 1386 us against stream-K (profiles/r05_gemm_pair_probe.jsonl,
-      // profiles/r05_gemm_sk_sweep_pass_rows.jsonl; 2 slices lose: 941 us); 22-63 tiles over >= 1024 k-pairs stay on
-      // stream-K
-      S = cap / g.n_tiles;
-      mode = 3;
-    } else {
-      mode = 1;  // very long K over few tiles (the lm_head dgrad: 32 tiles x 1187 k-pairs): stream-K measured best
-    }
-  } else if (mode == 0 && epi_is_swiglu(epilogue) && g.n_tiles >= 8 * cap && g_sk.grid == 0) {
-    // the gate_up + SwiGLU forward over a pass's tokens (38 tile columns x 321 / 642 tile rows: 47 / 95 rounds):
-    // persistent whole-tile rounds + a stream-K tail (each split tile's head combines its k-order partials, then the
-    // epilogue runs on the whole tile) against one workgroup per tile: 1282 -> 1232 us at 82144 rows, 2533 -> 2465
-    // at 164288 (profiles/r05_gemm_sk_sweep_pass_rows.jsonl)
-    mode = 1;
-  } else if (mode == 0 || mode == 3) {
-    // at most 8 splits of >= 6 k-pairs each (profiles/r03_gemm_sk_sweep.jsonl: more or shorter splits lose to the
-    // slab traffic and the per-split pipeline fill)
-    S = mode == 3 && g_sk.param > 0 ? g_sk.param : std::min({cap / std::max(1, g.n_tiles), 8, g.P / 6});
-    S = std::max(1, std::min({S, g.P, 32, cap / std::max(1, g.n_tiles)}));
-    if (epi_whole_tiles(epilogue) || g.n_tiles * 2 > cap) S = 1;
-    mode = S > 1 ? 3 : 2;
-  }
-  g.splits = 1;
-  if (mode == 3 && epi_whole_tiles(epilogue)) mode = 2;  // a forced split-K tuning: whole tiles instead
-  if (mode == 3) {
-    g.splits = S;
-    g.dp_tiles = 0;
-    g.sk_base = g.sk_tile0 = 0;
-    grid = g.n_tiles * S;
-  } else if (mode == 2) {
-    // whole tiles, one workgroup per tile (no workgroup waits on another, so no co-residency is needed): the hardware
-    // deals tiles to CUs as they free up, so a kernel on a second stream (the weight gradient beside its input
-    // gradient) fills the CUs a short grid leaves idle instead of waiting behind a persistent grid's static rounds
-    g.dp_tiles = g.n_tiles;
-    grid = g_sk.grid > 0 ? std::min(cap, g.n_tiles) : g.n_tiles;
-    // a last round of at most a quarter of the CUs (the N = 896 outputs at the passes' token counts: 1284 = 5 x 256
-    // + 4 tiles, 2568 = 10 x 256 + 8) would hold the whole launch for one more tile time while the other CUs idle:
-    // over a long K (>= 16 k-pairs) those r tiles split K over S = cap / r slices instead (uniform split-K, <= 16
-    // slices): down_proj's forward at the update pass's 82144 rows 628 -> 611 us; at K = 896 (7 k-pairs) the slices'
-    // pipeline fill and combine cost more than the round they save (o_proj dgrad 151 -> 157 us), so not there
-    // (profiles/r05_gemm_tail_splitk.jsonl); up to a third of the CUs since the lm_head weight gradient's K blocks
-    // (2376 tiles, r = 72, 52 k-pairs): 17.73 -> 17.33 ms per call (profiles/r05_gemm_tail3_lm_head_wgrad.jsonl)
-    const int r = g.n_tiles % cap;
-    if (g_sk.mode == 0 && g_sk.grid == 0 && !epi_whole_tiles(epilogue) && g.n_tiles > cap && r > 0 && 3 * r <= cap &&
-        g.P >= 16) {
-      const int St = std::min({16, cap / r, g.P / 2});
-      if (St >= 2) {
-        g.splits = St;
-        g.dp_tiles = g.sk_base = g.sk_tile0 = g.n_tiles - r;
-        grid = g.n_tiles - r + r * St;
-      }
-    }
-  } else {
-    const int full = g.n_tiles / grid;
-    const int dp = (g.n_tiles % grid == 0) ? g.n_tiles : std::max(0, full - 1) * grid;
-    g.dp_tiles = dp;
-    const int64_t I = static_cast<int64_t>(g.n_tiles - dp) * g.P;
-    const int min_iters = g_sk.param > 0 ? g_sk.param : 2;
-    DRL_CHECK_ARG(I < (1 << 23), "stream-K iteration space too large");
-    if (dp == 0 && I > 0) grid = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(grid, I / min_iters)));
-  }
+  int grid = 0, mode = 0;
+  if (const int rc = plan_decomposition(g, epilogue, cus, grid, mode); rc != DRL_OK) return rc;
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int epi = epilogue == DRL_GEMM_PLAIN ? (c_dtype == DRL_F32 ? EPI_F32 : EPI_NONE)
                   : epilogue == DRL_GEMM_BIAS ? EPI_BIAS : epilogue == DRL_GEMM_SWIGLU ? EPI_SWIGLU : EPI_SWIGLU_BWD;

@@ -623,6 +623,11 @@ void drl_gemm_set_sk_tuning(int32_t grid, int32_t group, int32_t dp_mode, int32_
 /* Measurement hook (never set in the product path): 1 = whole tiles skip their epilogue (no output written), to time
  * the main loop and the per-tile fixed cost apart; 0 = normal. */
 void drl_gemm_set_debug(int32_t flags);
+/* The decomposition drl_gemm would launch for one (M, N, K, epilogue) over `cus` CUs under the current tuning (host
+ * arithmetic only, no device): info[0] mode (1 stream-K, 2 whole tiles, 3 uniform split-K), info[1] split-K slices
+ * per split tile, info[2] workgroups, info[3] tiles dealt whole, info[4] first split workgroup (tail split-K).
+ * Per launch: an operand past the 2 GB buffer range (K blocks of a layout-T operand) is several launches. */
+int drl_gemm_plan(int64_t M, int64_t N, int64_t K, int32_t epilogue, int32_t cus, int32_t* info);
 
 
 /* Row gather / scatter of the remove-padding passes (flash_attn.bert_padding unpad_input / pad_input /
