@@ -179,11 +179,20 @@ def cpu_baseline(cfg):
     B = cfg.data.train_batch_size * ar.rollout.n
     n_mini = max(1, cfg.data.train_batch_size // ar.actor.ppo_mini_batch_size)
     r = cb.measure(resolve_model_config(ar.model), B, cfg.data.max_prompt_length, cfg.data.max_response_length,
-                   n_optimizer_steps=n_mini)
-    return {"value": 1.0 / r["step_s"], "unit": "PPO steps/s", "cores": r["threads"], "kind": "port",
-            "sample": r["sample"], "est_step_s": r["step_s"],
-            "value_range": [1.0 / r["step_s_range"][1], 1.0 / r["step_s_range"][0]],
-            "est_parts_s": {k: v for k, v in r.items() if k.endswith("_s") and k != "step_s"}}
+                   n_optimizer_steps=n_mini, group=int(ar.rollout.n))
+    out = {"value": 1.0 / r["step_s"], "unit": "PPO steps/s", "cores": r["threads"], "kind": "port",
+           "sample": r["sample"], "est_step_s": r["step_s"],
+           "value_range": [1.0 / r["step_s_range"][1], 1.0 / r["step_s_range"][0]],
+           "est_parts_s": {k: v for k, v in r.items() if k.endswith("_s") and k != "step_s"},
+           # what the headline priced: every row's prompt + response tokens, no prompt sharing (the reference's CPU
+           # FSDP path); the GPU line runs prompt groups once, so the shared-prompt estimate is given beside it
+           "tokens_per_row_priced": r["tokens_per_row"], "prompts_shared": False}
+    if "shared" in r:
+        sh = r["shared"]
+        out["shared_prompt_estimate"] = {"value": 1.0 / sh["step_s"], "unit": "PPO steps/s",
+                                         "est_step_s": sh["step_s"], "tokens_per_row_priced": sh["tokens_per_row"],
+                                         "prompts_shared": True, "group": sh["group"]}
+    return out
 
 
 def build_config(args):
@@ -374,12 +383,14 @@ def main():
             "timing_spread_s": {k.split("/", 1)[1]: [min(v), sorted(v)[len(v) // 2], max(v)]
                                 for k in hist[0] if k.startswith("timing_s/")
                                 for v in [[h[k] for h in hist]]},
-            # the reference's perf/mfu/actor (flops_counter.estimate_flops over every row's tokens): with prompt
-            # groups run once (prompt_groups below) the executed FLOPs are fewer than the ones it counts
-            "mfu_actor": sum(h.get("perf/mfu/actor", 0.0) for h in hist) / len(hist),
-            # the FLOPs update_actor executed (flops_counter.executed_flops: prompt groups counted once, lm_head over
-            # the response rows) over its time and the dense bf16 peak
-            "mfu_actor_executed": sum(h.get("perf/mfu/actor_executed", 0.0) for h in hist) / len(hist),
+            # headline MFU: the FLOPs update_actor executed (flops_counter.executed_flops: prompt groups counted once,
+            # lm_head over the response rows) over its time and the dense bf16 peak
+            "mfu_actor": sum(h.get("perf/mfu/actor_executed", 0.0) for h in hist) / len(hist),
+            "mfu_actor_basis": "executed FLOPs of update_actor / its time / 2.5 PFLOP/s dense bf16",
+            # the reference's perf/mfu/actor (flops_counter.estimate_flops over every row's prompt + response
+            # tokens): with prompt groups run once (prompt_groups below) it counts FLOPs that were never executed
+            "reference_formula": {"mfu_actor": sum(h.get("perf/mfu/actor", 0.0) for h in hist) / len(hist),
+                                  "basis": "verl flops_counter.estimate_flops over every row's tokens (perf/mfu/actor)"},
             "prompt_groups": {"rollout.enable_prefix_caching": bool(ar.rollout.get("enable_prefix_caching", True)),
                               "model.share_prompt_prefix": bool(ar.model.get("share_prompt_prefix", True))},
             "roofline": roofline,

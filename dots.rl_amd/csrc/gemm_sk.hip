@@ -26,9 +26,21 @@
 // the workgroup that holds the tile's k = 0 segment (its "head", always the LAST segment of that workgroup's range,
 // so the tails it waits for were computed first) adds its own accumulator and the tails' slabs in k order — a fixed
 // order, so results are bit-reproducible — and runs the epilogue. The flag is reset by its consumer: every launch
-// starts and ends with the flag words zero (graph-replay safe). Co-residency: the grid never exceeds the CU count
-// (one 128-KB-LDS workgroup per CU), and a consumer only ever waits for workgroups with a larger index, which the
-// dispatcher has started no later than itself.
+// starts and ends with the flag words zero (graph-replay safe).
+//
+// Co-residency (one 128-KB-LDS workgroup per CU; spinning workgroups need their partners resident):
+//   stream-K (mode 1) and all-split-K (mode 3): grid <= CU count, so every workgroup is resident at once; a stream-K
+//     head only waits for workgroups with a larger index, which the dispatcher started no later than itself;
+//   whole tiles (mode 2) nobody waits — EXCEPT the tail split-K form: whole tiles [0, sk_base) are followed by
+//     r * St split slices (r = tiles % CUs, r * St <= CU count) whose S slices spin on each other's arrival count.
+//     The grid then exceeds the CU count. It is deadlock-free because (a) the dispatcher deals workgroups in index
+//     order, so the slices (the highest indices) are dealt only after every whole tile has been placed, and a CU that
+//     frees up takes the next slice; (b) r * St <= CUs, so once the whole tiles drain, all slices of a tile fit at
+//     once; (c) no OTHER spinning launch runs concurrently on the chip — two spinning grids on two streams could each
+//     hold CUs the other's slices wait for. qwen2.dgrad_wgrad enforces (c) for the concurrent dgrad / wgrad pair (at
+//     most one of the two may take a spinning plan, drl_gemm_plan) and nothing else launches drl_gemm concurrently.
+// A spin that exceeds 2^28 polls records 1 in the timeout word (flags + CU count, inside the workspace for every grid)
+// and finishes with a wrong tile rather than hanging; tests read the word back (tests/test_gemm_sk_gpu.py).
 #include "common.h"
 
 namespace drl {
@@ -62,7 +74,9 @@ struct SkArgs {
   float* c32;          // EPI_F32 out (M, N)
   const uint16_t* bias;
   float* ws;           // stream-K slabs, gridDim.x x SLAB
-  unsigned* flags;     // gridDim.x publish flags + 1 timeout word (zero between launches)
+  unsigned* flags;     // publish flags / split-K arrival counts (zero between launches)
+  unsigned* tmo;       // the residency-timeout word: flags + CU count, a fixed index inside the workspace whatever the
+                       // grid (tail split-K grids exceed the CU count), zero unless a spin-wait timed out
   int64_t lda, ldb, ldc, ldc2;
   uint32_t a_bytes, b_bytes;
   int64_t a_total;     // > 0: a layout-K A operand beyond one buffer range, its descriptor rebased per tile (a + m0 rows)
@@ -677,7 +691,7 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
       while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < static_cast<unsigned>(S)) {
         __builtin_amdgcn_s_sleep(1);
         if (++spins > (1u << 28)) {  // residency violated: record it and finish (wrong tile) instead of hanging
-          __hip_atomic_store((gflag*)(g.flags + G), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store((gflag*)g.tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           break;
         }
       }
@@ -789,7 +803,7 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
             while (__hip_atomic_load((gflag*)(g.flags + w2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
               __builtin_amdgcn_s_sleep(1);
               if (++spins > (1u << 28)) {  // residency violated: record it and finish (wrong tile) instead of hanging
-                __hip_atomic_store((gflag*)(g.flags + G), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store((gflag*)g.tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 break;
               }
             }
@@ -912,7 +926,8 @@ int plan_decomposition(SkArgs& g, int epilogue, int cus, int& grid, int& mode) {
     g.sk_base = g.sk_tile0 = 0;
     grid = g.n_tiles * S;
   } else if (mode == 2) {
-    // whole tiles, one workgroup per tile (no workgroup waits on another, so no co-residency is needed): the hardware
+    // whole tiles, one workgroup per tile (no whole tile waits on another; the tail split-K slices below do, under the
+    // co-residency rules of the file header): the hardware
     // deals tiles to CUs as they free up, so a kernel on a second stream (the weight gradient beside its input
     // gradient) fills the CUs a short grid leaves idle instead of waiting behind a persistent grid's static rounds
     g.dp_tiles = g.n_tiles;
@@ -1081,6 +1096,7 @@ int drl_gemm(const void* a, int64_t lda, int32_t a_layout, const void* b, int64_
   const int cus = cu_count();
   g.ws = static_cast<float*>(workspace);
   g.flags = reinterpret_cast<unsigned*>(static_cast<char*>(workspace) + static_cast<int64_t>(cus) * SLAB * 4);
+  g.tmo = g.flags + cus;
 
   int grid = 0, mode = 0;
   if (const int rc = plan_decomposition(g, epilogue, cus, grid, mode); rc != DRL_OK) return rc;

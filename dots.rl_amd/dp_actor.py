@@ -19,7 +19,7 @@ from . import native
 from .core_algos import cov_loss_kw, fused_actor_loss
 from .protocol import DataProto
 from .seqlen_balancing import prepare_dynamic_batch, restore_dynamic_batch
-from .qwen2 import PrefixShare, Qwen2Model, RmPad, gather_rows
+from .qwen2 import PrefixShare, Qwen2Model, RmPad, gather_rows, pad_seq_columns
 from .torch_functional import logprobs_and_entropy_from_logits
 
 
@@ -293,28 +293,35 @@ class DataParallelPPOActor:
         m = self.actor_module
         responses = micro_batch["responses"]
         B, R = responses.shape
-        am = micro_batch["attention_mask"]
+        # T % 8 != 0 (e.g. max_response_length 250): pad columns the fused attention needs, sliced away below
+        ids, am, pos, padc = pad_seq_columns(m, micro_batch["input_ids"], micro_batch["attention_mask"],
+                                             micro_batch["position_ids"])
         keep = None
-        share = PrefixShare.build(micro_batch["input_ids"], am, R, keep_pads=not self.use_remove_padding) \
+        # the pad columns count as response positions for prefix sharing (never shared)
+        share = PrefixShare.build(ids, am, R + padc, keep_pads=not self.use_remove_padding) \
             if self.share_prompt_prefix else None
         T = am.shape[1]
+        T0 = T - padc
         if m.training:  # executed work of the update passes (exec_stats: the executed-FLOP MFU beside the reference's)
             st = self.exec_stats
             pairs = B * T * (T + 1) // 2  # causal (query, key) pairs the fused attention computes per head
-            if share is not None:  # q_start: the copies skip the shared prompt's queries
-                pairs -= (B - share.groups) * share.S * (share.S + 1) // 2
+            if share is not None:
+                # q_start: the copies skip the shared prompt's query tiles — whole 32-row tiles below q_start only
+                # (csrc/flash_attn.hip starts at q_start & ~31), so the skipped pairs are those of S0 = S & ~31 rows
+                S0 = share.S & ~31
+                pairs -= (B - share.groups) * S0 * (S0 + 1) // 2
             st["tokens"] += share.nnz if share is not None else (int(am.sum()) if self.use_remove_padding else B * T)
             st["attn_pairs"] += pairs
             st["lm_rows"] += B * R
         if share is not None or self.use_remove_padding:
             rm = share if share is not None else RmPad(am)
-            h = m.hidden_states(micro_batch["input_ids"], am, micro_batch["position_ids"], rm=rm)
-            sel = rm.inv.view(B, T)[:, T - R - 1:T - 1].reshape(-1).contiguous()
+            h = m.hidden_states(ids, am, pos, rm=rm)
+            sel = rm.inv.view(B, T)[:, T0 - R - 1:T0 - 1].reshape(-1).contiguous()
             h = gather_rows(h.view(rm.nnz, h.shape[-1]), sel)
             keep = (sel >= 0).view(B, R)
         else:
-            h = m.hidden_states(micro_batch["input_ids"], am, micro_batch["position_ids"])
-            h = h[:, -R - 1:-1, :].reshape(B * R, h.shape[-1])
+            h = m.hidden_states(ids, am, pos)
+            h = h[:, T0 - R - 1:T0 - 1, :].reshape(B * R, h.shape[-1])
         if self.use_fused_kernels:  # A21: no (B*R, V) logits (dp_actor.py:173-186 fused branch)
             logp, ent = m.fused_logprob(h, responses.reshape(-1), temperature, calculate_entropy)
         else:

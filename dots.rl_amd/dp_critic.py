@@ -19,7 +19,7 @@ from . import native
 from .dp_actor import FlatAdamW, _concat_rows, append_to_dict, exec_groups
 from .protocol import DataProto
 from .seqlen_balancing import prepare_dynamic_batch, restore_dynamic_batch
-from .qwen2 import PrefixShare, Qwen2Model, RmPad, gather_rows
+from .qwen2 import PrefixShare, Qwen2Model, RmPad, gather_rows, pad_seq_columns
 
 
 class _ValueHead(torch.autograd.Function):
@@ -64,18 +64,21 @@ class DataParallelPPOCritic:
         (dp_critic.py:69-107) runs the backbone on the attended tokens only and gives 0 at pad positions."""
         m = self.critic_module
         R = micro_batch["responses"].size(-1)
-        am = micro_batch["attention_mask"]
+        # T % 8 != 0: pad columns for the fused attention (qwen2.pad_seq_columns), sliced away below
+        ids, am, pos, padc = pad_seq_columns(m, micro_batch["input_ids"], micro_batch["attention_mask"],
+                                             micro_batch["position_ids"])
         B, T = am.shape
-        share = PrefixShare.build(micro_batch["input_ids"], am, R, keep_pads=not self.use_remove_padding) \
+        T0 = T - padc
+        share = PrefixShare.build(ids, am, R + padc, keep_pads=not self.use_remove_padding) \
             if self.share_prompt_prefix else None
         if share is not None or self.use_remove_padding:
             rm = share if share is not None else RmPad(am)
-            h = m.hidden_states(micro_batch["input_ids"], am, micro_batch["position_ids"], rm=rm)
-            sel = rm.inv.view(B, T)[:, T - R - 1:T - 1].reshape(-1).contiguous()
+            h = m.hidden_states(ids, am, pos, rm=rm)
+            sel = rm.inv.view(B, T)[:, T0 - R - 1:T0 - 1].reshape(-1).contiguous()
             v = value_head(m, gather_rows(h.view(rm.nnz, h.shape[-1]), sel)).view(B, R)
             return torch.where((sel >= 0).view(B, R), v, 0.0)
-        h = m.hidden_states(micro_batch["input_ids"], am, micro_batch["position_ids"])
-        h = h[:, -R - 1:-1, :].reshape(B * R, h.shape[-1])
+        h = m.hidden_states(ids, am, pos)
+        h = h[:, T0 - R - 1:T0 - 1, :].reshape(B * R, h.shape[-1])
         return value_head(m, h).view(B, R)
 
     @torch.no_grad()

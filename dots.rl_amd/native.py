@@ -7,6 +7,7 @@ in the gfx950 kernels of ``libdotsrl_amd.so``. Tensors must live on the GPU; any
 from __future__ import annotations
 
 import ctypes
+import functools
 import math
 import threading
 
@@ -915,6 +916,32 @@ def gemm(a, a_layout, b, b_layout, M, N, K, out, beta=False, bias=None, swiglu=F
                          1 if beta else 0, M, N, K, _p(bias), epi, _p(out_gu),
                          out_gu.stride(0) if out_gu is not None else 0, _p(ws), ws.numel(), _stream()), "drl_gemm")
     return out
+
+
+@functools.lru_cache(maxsize=4096)
+def gemm_plan(M, N, K, epilogue=0, cus=256):
+    """drl_gemm's decomposition of one launch (host-only arithmetic, csrc/gemm_sk.hip plan_decomposition):
+    (mode, splits, grid, dp_tiles, sk_base) — mode 1 stream-K, 2 whole tiles (splits > 1: tail split-K), 3 split-K."""
+    info = (ctypes.c_int32 * 5)()
+    check(lib().drl_gemm_plan(M, N, K, epilogue, cus, info), "drl_gemm_plan")
+    return tuple(info)
+
+
+def gemm_spins(M, N, K, epilogue=0, cus=256):
+    """True when the launch's plan has workgroups that spin-wait on other workgroups (stream-K, split-K, or whole tiles
+    with a split-K tail): such a launch must not run beside another spinning drl_gemm launch (csrc/gemm_sk.hip header,
+    co-residency rule (c))."""
+    mode, splits = gemm_plan(M, N, K, epilogue, cus)[:2]
+    return mode in (1, 3) or splits > 1
+
+
+def gemm_timeout_word(device=None, slot=0):
+    """The residency-timeout word of a drl_gemm workspace slot (0 unless a spin-wait gave up)."""
+    device = torch.device("cuda", torch.cuda.current_device()) if device is None else device
+    ws = _ws_gemm.get(device, slot)
+    n = lib().drl_gemm_workspace_bytes()
+    cus = (n - 256) // (256 * 256 * 4 + 4)
+    return int(ws[cus * 256 * 256 * 4:].view(torch.int32)[cus])
 
 
 def _pad_to_64(t, dim):

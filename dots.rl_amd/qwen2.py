@@ -306,7 +306,7 @@ class ParamStore:
 # Every bf16 GEMM of the full-sequence passes — forward, dgrad and wgrad of each projection and of the lm_head — runs
 # on csrc/gemm_sk.hip (drl_gemm: 256 x 256 ping-pong tiles, weights read in their stored layout for the dgrad, fp32
 # accumulation into the gradient buffer for the wgrad); a reduction dimension that is not a multiple of 64 is
-# zero-padded on the device (native._pad_cols / _pad_rows) — there is no library fallback. The fp32 parity model
+# zero-padded on the device (native._pad_to_64) — there is no library fallback. The fp32 parity model
 # (compute_dtype=float32) uses torch's fp32 GEMMs.
 
 
@@ -361,13 +361,17 @@ _SIDE_STREAMS = {}
 _CU_COUNT = {}
 
 
+def _cus(device):
+    dev = device.index
+    if dev not in _CU_COUNT:
+        _CU_COUNT[dev] = torch.cuda.get_device_properties(dev).multi_processor_count
+    return _CU_COUNT[dev]
+
+
 def _concurrent_pair(gw):
     """The weight gradient gw (out, in) runs beside its input gradient when drl_gemm deals it as whole 256 x 256 tiles
     that fill more than half of the CUs but not all of them (gemm_sk.hip's automatic decomposition)."""
-    dev = gw.device.index
-    if dev not in _CU_COUNT:
-        _CU_COUNT[dev] = torch.cuda.get_device_properties(dev).multi_processor_count
-    cus = _CU_COUNT[dev]
+    cus = _cus(gw.device)
     tiles = -(-gw.shape[0] // 256) * -(-gw.shape[1] // 256)
     return cus < 2 * tiles and tiles < cus
 
@@ -387,6 +391,10 @@ def dgrad_wgrad(dy, w, gw, x):
         dx = dgrad(dy, w)
         acc_wgrad(gw, dy, x)
         return dx
+    # co-residency rule (c) of csrc/gemm_sk.hip: at most one of two concurrent launches may spin-wait
+    cus = _cus(dy.device)
+    assert not (native.gemm_spins(gw.shape[0], gw.shape[1], dy.shape[0], cus=cus) and
+                native.gemm_spins(dy.shape[0], w.shape[1], dy.shape[1], cus=cus)), "two spinning drl_gemm plans side by side"
     main = torch.cuda.current_stream()
     side = _side_stream(dy.device)
     side.wait_stream(main)
@@ -650,6 +658,11 @@ class _DecoderLayer(torch.autograd.Function):
         if _sk(dm, sv["gu"]):
             # down_proj dgrad with the SwiGLU backward in its epilogue (d a never written)
             if CONCURRENT_DOWN:
+                H_, I_ = s.w(p + "down_proj").shape
+                cus = _cus(dm.device)
+                assert not (native.gemm_spins(H_, I_, N, cus=cus) and
+                            native.gemm_spins(N, I_, H_, native.GEMM_SWIGLU_BWD, cus=cus)), \
+                    "two spinning drl_gemm plans side by side"
                 main = torch.cuda.current_stream()
                 side = _side_stream(dm.device)
                 side.wait_stream(main)
@@ -783,6 +796,22 @@ class RmPad:
 
     def pack_grad(self, x):
         return self.pack(x)
+
+
+def pad_seq_columns(m, input_ids, attention_mask, position_ids, multiple=8):
+    """Right-pads a micro-batch's (B, T) columns to a multiple of 8 for the bf16 model: the fused attention backward
+    needs T % 8 == 0 and its forward a key-valid row stride % 4 == 0 (csrc/flash_attn.hip). The added columns are pads
+    (attention_mask 0, token 0, positions continuing): no real query attends to them (masked, and causally after every
+    real token), so every real position's values are unchanged and the caller slices its [T - R - 1, T - 1) rows at
+    the ORIGINAL T. The reference actor takes any T (dp_actor.py:90-280). Returns (ids, mask, positions, added)."""
+    T = input_ids.shape[1]
+    pad = (-T) % multiple
+    if pad == 0 or m.dtype != torch.bfloat16:
+        return input_ids, attention_mask, position_ids, 0
+    ids = F.pad(input_ids, (0, pad))
+    am = F.pad(attention_mask, (0, pad))
+    extra = position_ids[..., -1:] + torch.arange(1, pad + 1, device=position_ids.device, dtype=position_ids.dtype)
+    return ids, am, torch.cat([position_ids, extra], -1), pad
 
 
 class PrefixShare(RmPad):

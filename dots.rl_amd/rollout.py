@@ -39,21 +39,46 @@ def capture_graph(body, pool):
     # it is a HIP call the capturing stream forbids, and the process aborts (seen in the GPU suite: a collection in
     # the middle of a decode-lane capture). torch.cuda.graph runs a full gc.collect() before capturing instead; here
     # that cost 45-75 ms per rollout (a large Python heap), so collection is only paused for the capture
+    #
+    # Refcount-driven destruction is not covered by pausing the collector: body() must not drop the last reference to
+    # a CUDAGraph, an event or a stream. Audit of the bodies (round 6): the decode step bodies allocate tensors from
+    # the graph pool and free temporaries (allocator bookkeeping, no HIP call); every workspace they reach is sized
+    # before the capture and never replaced inside it (native._linear_workspace / _select_workspace raise instead);
+    # the previous graph is released by the caller only after this capture ends (MI355XRollout._capture). The one
+    # object the lanes body used to destroy inside the capture — the torch Event behind each Stream.wait_stream —
+    # is now created before the capture and kept alive past it (MI355XRollout._decode_graphed_lanes).
     torch.cuda.synchronize()
     graph = torch.cuda.CUDAGraph()
-    enabled = gc.isenabled()
-    gc.disable()
-    try:
+    with gc_paused():
         with torch.cuda.stream(_CAPTURE_STREAM):
             graph.capture_begin(pool=pool)
             try:
                 body()
             finally:
                 graph.capture_end()
-    finally:
-        if enabled:
-            gc.enable()
     return graph
+
+
+class gc_paused:
+    """Python's cyclic collector off inside the block, restored on exit (also on an exception) to what it was."""
+
+    def __enter__(self):
+        self.enabled = gc.isenabled()
+        gc.disable()
+        return self
+
+    def __exit__(self, *exc):
+        if self.enabled:
+            gc.enable()
+        return False
+
+
+def replay_graph(graph, n):
+    """``n`` replays of a captured step with the collector paused: a pause of the launching thread drains the device
+    queue (4 ms idle stretches inside the decode in the kernel trace)."""
+    with gc_paused():
+        for _ in range(n):
+            graph.replay()
 
 
 class MI355XRollout:
@@ -223,16 +248,7 @@ class MI355XRollout:
 
         body()  # t = 1, eager
         graph = self._capture(body)
-        # no collection while the replays are enqueued: a pause of the launching thread drains the device queue (4 ms
-        # idle stretches inside the decode in the kernel trace)
-        enabled = gc.isenabled()
-        gc.disable()
-        try:
-            for _ in range(2, R):
-                graph.replay()
-        finally:
-            if enabled:
-                gc.enable()
+        replay_graph(graph, max(0, R - 2))  # tokens 2 .. R - 1
         del graph, packed
 
     def _decode_lanes(self, B, max_rows):
@@ -283,19 +299,24 @@ class MI355XRollout:
         for j in range(lanes):  # t = 1, eager (sizes every lane's workspaces outside capture)
             body(j)
         side = [torch.cuda.Stream(device=dev) for _ in range(lanes - 1)]
+        # the fork / join events exist before the capture and outlive it (Stream.wait_stream would create and destroy
+        # one per call inside the capture)
+        fork = torch.cuda.Event()
+        joins = [torch.cuda.Event() for _ in side]
 
         def lanes_body():
             main = torch.cuda.current_stream()
+            fork.record(main)
             for s in side:
-                s.wait_stream(main)
+                s.wait_event(fork)
             body(0)
             for j, s in enumerate(side, start=1):
                 with torch.cuda.stream(s):
                     body(j)
-            for s in side:
-                main.wait_stream(s)
+            for s, ev in zip(side, joins):
+                ev.record(s)
+                main.wait_event(ev)
 
         graph = self._capture(lanes_body)
-        for _ in range(2, R):
-            graph.replay()
-        del graph, lane_state
+        replay_graph(graph, max(0, R - 2))
+        del graph, lane_state, fork, joins

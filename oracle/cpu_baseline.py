@@ -38,9 +38,13 @@ def _timeit(fn, reps=3):
     return ts[len(ts) // 2], (ts[0], ts[-1])
 
 
-def measure(cfg, B, P, R, n_optimizer_steps=2, seed=0, threads=None, reps=3):
+def measure(cfg, B, P, R, n_optimizer_steps=2, seed=0, threads=None, reps=3, group=1):
     """Returns dict(step_s=estimated seconds per full GRPO step (median sample), step_s_range=(min, max) over the
-    repetitions, parts..., sample=description)."""
+    repetitions, parts..., sample=description). The headline prices every row's P + R tokens, as the reference's
+    CPU FSDP path computes them (no prompt sharing). With ``group`` > 1 (GRPO's n samples per prompt, interleaved)
+    ``shared`` adds the estimate for the work the GPU line executes with prompt groups run once: the prefill over
+    B / group prompts, and the full-sequence passes over B / group x (P - 1) shared prompt tokens + B x (R + 1) own
+    tokens (qwen2.PrefixShare); the decode is unchanged."""
     if threads:
         torch.set_num_threads(threads)
     torch.manual_seed(seed)
@@ -96,6 +100,14 @@ def measure(cfg, B, P, R, n_optimizer_steps=2, seed=0, threads=None, reps=3):
     _, hi = parts_of(r_fwd[1] / (Bs * Ts), r_fb[1] / (Bs * Ts), c_dec_rng[1], r_adam[1])
     parts["step_s"] = step
     parts["step_s_range"] = (lo, hi)
+    parts["tokens_per_row"] = T
+    if group > 1:
+        tok_shared = (B // group) * (P - 1) + B * (R + 1)
+        c_fwd, c_fb = t_fwd / (Bs * Ts), t_fb / (Bs * Ts)
+        sh = {"rollout_s": (B // group) * P * c_fwd + B * (R - 1) * c_dec, "old_log_prob_s": tok_shared * c_fwd,
+              "ref_s": tok_shared * c_fwd, "update_actor_s": tok_shared * c_fb + n_optimizer_steps * t_adam}
+        parts["shared"] = {"step_s": sum(sh.values()), "tokens_per_row": tok_shared / B, "group": group,
+                           **{k + "_shared": v for k, v in sh.items()}}
     parts["per_token_s"] = {"fwd": t_fwd / (Bs * Ts), "fwd_bwd": t_fb / (Bs * Ts), "decode": c_dec,
                             "adamw_full": t_adam}
     parts["sample"] = (f"Qwen2.5-0.5B-shaped random fp32 model on CPU: fwd and fwd+bwd over {Bs}x{Ts} tokens, greedy "

@@ -67,3 +67,34 @@ def test_tail_split_k(plan):
     assert plan(82144, 896, 896) == dict(mode=2, splits=1, grid=1284, dp_tiles=1284, sk_base=0)
     # whole-tile epilogues never split
     assert plan(82144, 4864, 896, SWIGLU_BWD)["splits"] == 1
+
+
+@pytest.mark.parametrize("T", [82144, 164288, 98304, 196608])
+def test_concurrent_pairs_never_pair_two_spinning_plans(plan, T):
+    """Co-residency rule (c) of the gemm_sk.hip header: qwen2.dgrad_wgrad runs a weight gradient beside its input
+    gradient only where the weight gradient's whole tiles leave CUs idle (qwen2._concurrent_pair), and at most one of
+    the pair may spin-wait. Config #2's projections at the update pass's token counts: gate_up (the only concurrent
+    pair) has a non-spinning weight gradient beside a tail-split input gradient."""
+
+    def spins(p):
+        return p["mode"] in (1, 3) or p["splits"] > 1
+
+    H, I, NQ, HD = 896, 4864, 1152, 896
+    for out, inp in ((NQ, H), (H, HD), (2 * I, H), (H, I)):
+        tiles = -(-out // 256) * -(-inp // 256)
+        if not (CUS < 2 * tiles and tiles < CUS):  # qwen2._concurrent_pair
+            continue
+        wgrad, dgrad = plan(out, inp, T), plan(T, inp, out)
+        assert not (spins(wgrad) and spins(dgrad)), (out, inp, T, wgrad, dgrad)
+    # the measurement switch DRL_CONCURRENT_DOWN pairs down_proj's split-K weight gradient with the whole-tile
+    # SwiGLU-backward input gradient
+    assert not spins(plan(T, I, H, SWIGLU_BWD))
+
+
+def test_native_gemm_spins_matches_the_plan():
+    from dots.rl_amd import native
+
+    assert native.gemm_spins(82144, 896, 4864, cus=CUS)          # tail split-K
+    assert not native.gemm_spins(82144, 896, 896, cus=CUS)       # whole tiles
+    assert native.gemm_spins(896, 896, 82144, cus=CUS)           # uniform split-K
+    assert not native.gemm_spins(9728, 896, 82144, cus=CUS)      # gate_up weight gradient: whole tiles

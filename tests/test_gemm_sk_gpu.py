@@ -186,10 +186,13 @@ def test_decompositions_agree(mode, out_dtype, K):
 
 
 @pytest.mark.parametrize("al,bl,M,N,K", [(K_, K_, 6144, 896, 4864), (K_, T_, 2048, 896, 37888),
-                                         (T_, T_, 896, 896, 6144), (K_, K_, 6144, 9728, 896)])
+                                         (T_, T_, 896, 896, 6144), (K_, K_, 6144, 9728, 896),
+                                         (K_, K_, 16640, 1024, 4096)])
 @pytest.mark.parametrize("mode", [(0, 0), (1, 0), (3, 4)])
 def test_race_screen(al, bl, M, N, K, mode):
-    """16 launches bit-identical (split tiles are reduced in k order, whatever the arrival order)."""
+    """16 launches bit-identical (split tiles are reduced in k order, whatever the arrival order). 16640 x 1024 x 4096
+    under the automatic plan is the tail split-K form (260 tiles = 256 + 4 over 256 CUs: a grid above the CU count),
+    whose timeout word sits at the fixed index flags + CU count (read back below)."""
     native.lib().drl_gemm_set_sk_tuning(0, 0, mode[0], mode[1])
     g = torch.Generator(device="cuda").manual_seed(M + N + K)
     a, _ = _op((M, K), al, g)
@@ -206,6 +209,7 @@ def test_race_screen(al, bl, M, N, K, mode):
     cus = (n - 256) // (256 * 256 * 4 + 4)
     flags = ws[cus * 256 * 256 * 4:].view(torch.int32)[:cus + 1]
     assert int(flags.abs().sum()) == 0  # every flag consumed and reset, no residency timeout recorded
+    assert native.gemm_timeout_word(outs[0].device) == 0
 
 
 def test_operand_over_2gb_rebases_per_tile():

@@ -326,3 +326,44 @@ def test_rope_q_skip_leaves_only_the_skipped_q_rows(dtype, heads):
     for b, s in enumerate(qs.tolist()):
         lo = min(s // 32 * 32, T) // tile * tile
         assert untouched[b, :lo].all()
+
+
+@pytest.mark.parametrize("rmpad,share", [(False, False), (True, False), (True, True), (False, True)])
+def test_bf16_sequence_length_not_multiple_of_8(rmpad, share):
+    """T = P + R with T % 8 != 0 (R = 61, as max_response_length 250 would give): the reference actor takes any T
+    (dp_actor.py:90-280); the fused attention needs T % 8 == 0, so _forward_micro_batch right-pads the micro-batch's
+    columns (qwen2.pad_seq_columns) and slices the response rows at the original T. Against the same batch with
+    three more response columns that are already pads (R = 64, T % 8 == 0): the log-probs of the first 61 columns and
+    the gradient of loss = sum(mask * logp) agree up to summation order; prefix sharing (3 rows per prompt) too."""
+    from dots.rl_amd.config import to_attr
+    from dots.rl_amd.dp_actor import DataParallelPPOActor
+    from dots.rl_amd.qwen2 import ParamStore, Qwen2Config, Qwen2Model
+
+    cfg = Qwen2Config(vocab_size=4096, hidden_size=896, intermediate_size=4864, num_hidden_layers=2,
+                      num_attention_heads=14, num_key_value_heads=2, tie_word_embeddings=True)
+    store = ParamStore(cfg, "cuda", compute_dtype=torch.bfloat16, trainable=True)
+    store.init_random(3)
+    model = Qwen2Model(cfg, store)
+    P, R = 96, 61
+    ids, am, pos, _ = _ragged_batch(6, P, 64, cfg.vocab_size, 17)
+    am[:, P + R:] = 0  # the last three response columns are pads in every row
+    if share:  # two prompt groups of three rows
+        for lead in (0, 3):
+            ids[lead + 1:lead + 3, :P] = ids[lead, :P]
+            am[lead + 1:lead + 3, :P] = am[lead, :P]
+        pos = torch.clamp(torch.cumsum(am, -1) - 1, min=0)
+    res = {}
+    for r in (R, 64):
+        mb = {"input_ids": ids[:, :P + r].contiguous(), "attention_mask": am[:, :P + r].contiguous(),
+              "position_ids": pos[:, :P + r].contiguous(), "responses": ids[:, P:P + r].contiguous()}
+        actor = DataParallelPPOActor(to_attr({"use_remove_padding": rmpad, "share_prompt_prefix": share}), model)
+        model.training = True
+        store.zero_grad()
+        _, lp = actor._forward_micro_batch(mb, 1.0)
+        (lp[:, :R] * am[:, P:P + R]).sum().backward()
+        torch.cuda.synchronize()
+        res[r] = (lp[:, :R].detach().float(), store.grad.detach().clone())
+    (lp0, g0), (lp1, g1) = res[R], res[64]
+    mask = am[:, P:P + R].bool()
+    torch.testing.assert_close(lp0[mask], lp1[mask], rtol=0, atol=1e-2)
+    assert ((g0 - g1).norm() / g1.norm()).item() < 1e-3

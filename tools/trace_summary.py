@@ -52,11 +52,33 @@ def main():
               f"({100.0 * idle / span:.1f} %) in {len(gaps)} gaps; gaps > 50 us: "
               f"{sum(g for g, _ in gaps if g > 50000) / 1e6:.1f} ms in {sum(1 for g, _ in gaps if g > 50000)}; "
               f"longest {[round(g / 1e3, 1) for g, _ in gaps[:8]]} us")
+        # a gap of seconds is not a step's idle time: the first barrier of a run builds the communicator (older
+        # bench.py versions marked the window before it); report the idle net of such gaps beside the raw figure
+        big = sum(g for g, _ in gaps if g > 1_000_000_000)
+        if big:
+            print(f"net of {sum(1 for g, _ in gaps if g > 1_000_000_000)} gap(s) > 1 s (communicator setup): span "
+                  f"{(span - big) / 1e6:.1f} ms, idle {(idle - big) / 1e6:.1f} ms ({100.0 * (idle - big) / (span - big):.1f} %)")
         short = lambda n: n.replace("void ", "").replace("drl::(anonymous namespace)::", "")[:60]  # noqa: E731
         for g, at in gaps[:16]:
             before, after = names[at]
             print(f"  gap {g / 1e3:9.1f} us at {(at - lo) / 1e6 if lo else at / 1e6:9.1f} ms: after {short(before)} | "
                   f"before {short(after)}")
+    if len(marks) >= 2:
+        # per-kernel totals over the window only (the trace also holds the warmup steps and the setup)
+        tot = collections.Counter()
+        shapes = collections.defaultdict(collections.Counter)
+        durs = collections.defaultdict(float)
+        for r in rows:
+            a, b = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+            if not (lo <= a and b <= hi) or "spin_kernel" in r["Kernel_Name"]:
+                continue
+            name = r["Kernel_Name"]
+            key = (r.get("Grid_Size_X", r.get("Grid_Size", "")), r.get("Grid_Size_Y", ""),
+                   r.get("Workgroup_Size_X", r.get("Workgroup_Size", "")))
+            tot[name] += b - a
+            shapes[name][key] += 1
+            durs[(name, key)] += b - a
+        print("per-kernel totals below: inside the window only")
     for name, t in tot.most_common(top):
         print(f"{t / 1e6:9.1f} ms  {name[:110]}")
         for key, n in shapes[name].most_common(int(sys.argv[3]) if len(sys.argv) > 3 else 6):
