@@ -92,7 +92,7 @@ F32 = ctypes.c_float
 SZ = ctypes.c_size_t
 
 # name -> (restype, argtypes); must match include/dotsrl_amd.h exactly
-ABI_VERSION = 7  # include/dotsrl_amd.h DRL_ABI_VERSION: the layouts below (PPOLossParams) are of this version
+ABI_VERSION = 8  # include/dotsrl_amd.h DRL_ABI_VERSION: the layouts below (PPOLossParams) are of this version
 
 SIGNATURES = {
     "drl_last_error": (ctypes.c_char_p, []),
@@ -114,7 +114,8 @@ SIGNATURES = {
     "drl_reinforce_pp_advantage_return": (ctypes.c_int, [P, P, I32, I64, I64, F32, P, P, P, SZ, P]),
     "drl_remax_advantage_return": (ctypes.c_int, [P, P, P, I32, I64, I64, P, P, P]),
     "drl_decode_step_prologue_workspace_bytes": (SZ, []),
-    "drl_decode_step_prologue": (ctypes.c_int, [P, I64, P, P, P, I64, P, I32, I64, I64, I64, P, P, P, P, I64, P, SZ, P]),
+    "drl_decode_step_prologue": (ctypes.c_int, [P, I64, P, P, P, I64, P, I32, I64, I64, I64, P, P, P, P, I64, P, SZ, I64,
+                                                P]),
     "drl_gae_workspace_bytes": (SZ, [I64, I64]),
     "drl_gae_advantage_return": (ctypes.c_int, [P, P, I32, P, I32, I64, I64, F32, F32, P, P, P, SZ, P]),
     "drl_value_loss_workspace_bytes": (SZ, [I64, I64]),
@@ -185,6 +186,14 @@ SIGNATURES = {
     "drl_decode_pack_weight_rope": (ctypes.c_int, [P, I64, I64, I64, I64, P, P]),
     "drl_decode_qkv_rope": (ctypes.c_int, [P, P, P, P, P, P, I64, I64, I64, I64, I64, I64, P, P, P, I64, I64, P, P]),
     "drl_decode_rope": (ctypes.c_int, [P, I32, P, P, P, P, I64, I64, I64, I64, I64, P, P, P, P, I64, I64, I64, P, P]),
+    "drl_decode_norm_plan": (ctypes.c_int, [I64, I64, I64, I32, P, P, P]),
+    "drl_decode_norm_set_plan": (None, [I32, I32, I32]),
+    "drl_decode_resid_counter_bytes": (SZ, [I64, I64, I64]),
+    "drl_decode_gemm_resid": (ctypes.c_int, [P, P, I64, I64, I64, P, I64, P, P, SZ, P]),
+    "drl_decode_gemm_norm": (ctypes.c_int, [P, P, F32, P, I64, I64, I64, P, P]),
+    "drl_decode_qkv_rope_norm": (ctypes.c_int, [P, P, F32, P, P, P, P, P, I64, I64, I64, I64, I64, I64, P, P, P, I64,
+                                                I64, P, P]),
+    "drl_decode_final_norm": (ctypes.c_int, [P, I64, P, P, I64, I64, I64, F32, P]),
     "drl_linear_logprob_fwd": (ctypes.c_int, [P, I64, P, P, I32, I64, I64, I64, F32, P, P, P, P, SZ, P]),
     "drl_linear_logprob_dlogits": (ctypes.c_int, [P, I64, P, P, I32, I64, I64, I64, F32, P, P, P, P, P, I64, P]),
 }

@@ -88,9 +88,157 @@ struct DgArgs {
   const int64_t* koff_dev;
   int64_t maxpos, Tk, ld_vt;
   int Hq, Hkv, D;
+  // fused-norm decode (round 6): the fp32 residual stream kept fragment-packed (element (m, k) at pk_off(m, k, MBT),
+  // fp32), updated in place by the K-split producers (EPI_RESID) and normalised on the fly by the consumers
+  float* xr;            // packed fp32 residual stream (MBT blocks, H columns)
+  const float* nw;      // NORM consumers: the RMSNorm weight (K)
+  float eps;
+  unsigned* cnt;        // EPI_RESID over K slices: arrival counters (tiles x mgroups), zero between launches
+  int ksplit;
 };
 
-constexpr int EPI_PARTIAL = 0, EPI_SWIGLU = 1, EPI_ROPE = 2;
+constexpr int EPI_PARTIAL = 0, EPI_SWIGLU = 1, EPI_ROPE = 2, EPI_RESID = 3;
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+// the NW waves' partial tiles (red[wave][token block][register][lane]) summed in wave order: ((r0 + r1) + r2) + ...
+template <int NW, int MB>
+__device__ __forceinline__ float red_sum(const float (*red)[MB][16][64], int blk, int q, int ln) {
+  float v = red[0][blk][q][ln];
+#pragma unroll
+  for (int w = 1; w < NW; ++w) v += red[w][blk][q][ln];
+  return v;
+}
+
+// Epilogues of the one-round-trip kernels, from the partial tiles of NW waves in LDS (tile = the 32-row weight block,
+// ks = the K slice, mb0 = the first token block). C row i (weight row of the block) <-> register (i & 3) + 4 (i >> 3),
+// lane half (i >> 2) & 1; column = token.
+template <int NW, int MB, int EPI>
+__device__ __forceinline__ void red_epilogue(const DgArgs& a, const float (*red)[MB][16][64], int tile, int ks, int mb0,
+                                             int tid) {
+  constexpr int NT = 64 * NW;
+  if constexpr (EPI == EPI_PARTIAL) {
+    for (int e = tid; e < 1024 * MB; e += NT) {
+      const int tl = e >> 5, i = e & 31, blk = tl >> 5, ml = tl & 31;
+      const int m = (mb0 + blk) * 32 + ml, n = tile * 32 + i;
+      if (m >= a.M || n >= a.N) continue;
+      const int q = (i & 3) + 4 * (i >> 3), ln = ml + 32 * ((i >> 2) & 1);
+      a.part[(static_cast<int64_t>(ks) * a.M + m) * a.N + n] = red_sum<NW, MB>(red, blk, q, ln);
+    }
+  } else if constexpr (EPI == EPI_ROPE) {
+    // rows 0..15: d = 16 qq + c of head hd, rows 16..31 its partners d + D/2. qkv = bf16(acc + bias), then
+    // rope_qkv_fwd_kernel's rotation (q, k heads) and the cache writes at the device key offset koff
+    const int half = a.D / 2, per = half / 16, hd = tile / per, qq = tile % per;
+    const int64_t koff = *a.koff_dev;
+    for (int e = tid; e < 512 * MB; e += NT) {
+      const int tl = e >> 4, c = e & 15, blk = tl >> 5, ml = tl & 31;
+      const int m = (mb0 + blk) * 32 + ml;
+      if (m >= a.M) continue;
+      const int i1 = c, i2 = c + 16;
+      const int q1 = (i1 & 3) + 4 * (i1 >> 3), l1 = ml + 32 * ((i1 >> 2) & 1);
+      const int q2 = (i2 & 3) + 4 * (i2 >> 3), l2 = ml + 32 * ((i2 >> 2) & 1);
+      const int d1 = 16 * qq + c, d2 = d1 + half;
+      const int n1 = hd * a.D + d1, n2 = n1 + half;
+      const float x1 = bf16r(red_sum<NW, MB>(red, blk, q1, l1) + bf16_to_f32(a.bias[n1]));
+      const float x2 = bf16r(red_sum<NW, MB>(red, blk, q2, l2) + bf16_to_f32(a.bias[n2]));
+      if (hd < a.Hq + a.Hkv) {
+        int64_t p = a.pos[m];
+        p = p < 0 ? 0 : (p >= a.maxpos ? a.maxpos - 1 : p);
+        const float cs = a.cos_t[p * half + d1], sn = a.sin_t[p * half + d1];
+        const float o1 = fmaf(x1, cs, -(x2 * sn)), o2 = fmaf(x2, cs, x1 * sn);
+        uint16_t* dst;
+        if (hd < a.Hq) {
+          const int G = a.Hq / a.Hkv;
+          dst = a.q + ((static_cast<int64_t>(m) * a.Hkv + hd / G) * G + hd % G) * a.D;
+        } else {
+          dst = a.kc + ((static_cast<int64_t>(m) * a.Hkv + (hd - a.Hq)) * a.Tk + koff) * a.D;
+        }
+        dst[d1] = to_bf16_bits(o1);
+        dst[d2] = to_bf16_bits(o2);
+      } else {
+        uint16_t* dst = a.vt + (static_cast<int64_t>(m) * a.Hkv + (hd - a.Hq - a.Hkv)) * vt_panel(a.ld_vt, a.D, a.Tk);
+        dst[vt_index(d1, koff, a.ld_vt, a.D)] = to_bf16_bits(x1);
+        dst[vt_index(d2, koff, a.ld_vt, a.D)] = to_bf16_bits(x2);
+      }
+    }
+  } else if constexpr (EPI == EPI_SWIGLU) {
+    // SwiGLU: rows 0..15 gate, 16..31 up of output columns 16 * tile + c; thread -> (token, 8 columns)
+    for (int e = tid; e < 64 * MB; e += NT) {
+      const int tl = e >> 1, hc = e & 1, blk = tl >> 5, ml = tl & 31;
+      u16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int c = 8 * hc + j, ig = c, iu = c + 16;
+        const int qg = (ig & 3) + 4 * (ig >> 3), lg = ml + 32 * ((ig >> 2) & 1);
+        const int qu = (iu & 3) + 4 * (iu >> 3), lu = ml + 32 * ((iu >> 2) & 1);
+        const float g = bf16r(red_sum<NW, MB>(red, blk, qg, lg));
+        const float u = bf16r(red_sum<NW, MB>(red, blk, qu, lu));
+        o[j] = to_bf16_bits(bf16r(silu_fast(g)) * u);
+      }
+      // packed for the next GEMM (K' = half): k step = tile, 8-column half hc, token (mb0 + blk, ml)
+      *reinterpret_cast<u16x8*>(a.out + ((static_cast<int64_t>(tile) * a.MBT + mb0 + blk) * 64 + hc * 32 + ml) * 8) = o;
+    }
+  } else {
+    // EPI_RESID (o_proj / down_proj of the fused-norm decode): the residual add of the decoder layer,
+    // x = x + bf16(sum over K slices) (add_rmsnorm_fwd's order: d = ((0 + p_0) + p_1) + ..., then one rounding), on
+    // the packed fp32 residual stream in place. Thread -> (token, 4 consecutive output columns: rows 4c .. 4c + 3 of the
+    // block = registers 4 (c >> 1) .. + 3 of lane half c & 1). Over K slices every slice publishes its partial tile
+    // write-through (sc1 16-B stores, MI355X_MICROARCH.md § visibility, first row of the sc1 table), one lane's
+    // agent-scope add counts the arrivals, and the LAST slice to arrive — told by the value its add returned, no
+    // waiting, no grid barrier — sums the slices in slice order (sc1 loads) and updates the residual; it also resets
+    // the counter for the next launch.
+    static_assert(NW == 4 && MB <= 2, "the one-round-trip kernel's 256 threads: MB items per thread");
+    __shared__ int s_last;
+    const __amdgpu_buffer_rsrc_t rp =
+        __builtin_amdgcn_make_buffer_rsrc((void*)a.part, (short)0, a.ksplit * a.M * a.N * 4, 0x00020000);
+    float4 v[MB];
+    int mm[MB], nn[MB];
+#pragma unroll
+    for (int it = 0; it < MB; ++it) {
+      const int e = tid + 256 * it, tl = e >> 3, c = e & 7, blk = tl >> 5, ml = tl & 31;
+      mm[it] = (mb0 + blk) * 32 + ml;
+      nn[it] = tile * 32 + 4 * c;
+      const int ln = ml + 32 * (c & 1), q0 = 4 * (c >> 1);
+      v[it] = make_float4(red_sum<NW, MB>(red, blk, q0, ln), red_sum<NW, MB>(red, blk, q0 + 1, ln),
+                          red_sum<NW, MB>(red, blk, q0 + 2, ln), red_sum<NW, MB>(red, blk, q0 + 3, ln));
+      if (a.ksplit > 1 && mm[it] < a.M && nn[it] < a.N)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v[it]), rp,
+                                               static_cast<uint32_t>(((ks * a.M + mm[it]) * a.N + nn[it]) * 4), 0,
+                                               16 /* sc1 */);
+    }
+    if (a.ksplit > 1) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its write-through stores
+      __syncthreads();
+      if (tid == 0) {
+        typedef __attribute__((address_space(1))) unsigned gcnt;
+        gcnt* c = (gcnt*)(a.cnt + static_cast<int64_t>(tile) * gridDim.z + blockIdx.z);
+        const unsigned prev = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = prev == static_cast<unsigned>(a.ksplit - 1);
+        if (s_last) __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __syncthreads();
+      if (!s_last) return;
+    }
+#pragma unroll
+    for (int it = 0; it < MB; ++it) {
+      const int m = mm[it], n = nn[it];
+      if (m >= a.M || n >= a.N) continue;
+      float4 d = v[it];
+      if (a.ksplit > 1) {
+        d = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int k = 0; k < a.ksplit; ++k) {
+          const float4 p = k == ks ? v[it]
+                                   : __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                                         rp, static_cast<uint32_t>(((k * a.M + m) * a.N + n) * 4), 0, 16 /* sc1 */));
+          d.x += p.x; d.y += p.y; d.z += p.z; d.w += p.w;
+        }
+      }
+      float4* xp = reinterpret_cast<float4*>(a.xr + pk_off(m, n, a.MBT));
+      float4 x = *xp;
+      x.x += bf16r(d.x); x.y += bf16r(d.y); x.z += bf16r(d.z); x.w += bf16r(d.w);
+      *xp = x;
+    }
+  }
+}
 
 template <int MB, int KSW, int EPI>
 __global__ __launch_bounds__(256) void decode_gemm_kernel(DgArgs a) {
@@ -121,72 +269,105 @@ __global__ __launch_bounds__(256) void decode_gemm_kernel(DgArgs a) {
 #pragma unroll
     for (int q = 0; q < 16; ++q) red[wave][i][q][lane] = acc[i][q];
   __syncthreads();
-  // C row i (weight row of the block) <-> register (i & 3) + 4 (i >> 3), lane half (i >> 2) & 1; column = token
-  if constexpr (EPI == EPI_PARTIAL) {
-    for (int e = tid; e < 1024 * MB; e += 256) {
-      const int tl = e >> 5, i = e & 31, blk = tl >> 5, ml = tl & 31;
-      const int m = (mb0 + blk) * 32 + ml, n = tile * 32 + i;
-      if (m >= a.M || n >= a.N) continue;
-      const int q = (i & 3) + 4 * (i >> 3), ln = ml + 32 * ((i >> 2) & 1);
-      const float v = ((red[0][blk][q][ln] + red[1][blk][q][ln]) + red[2][blk][q][ln]) + red[3][blk][q][ln];
-      a.part[(static_cast<int64_t>(ks) * a.M + m) * a.N + n] = v;
-    }
-  } else if constexpr (EPI == EPI_ROPE) {
-    // rows 0..15: d = 16 qq + c of head hd, rows 16..31 its partners d + D/2. qkv = bf16(acc + bias), then
-    // rope_qkv_fwd_kernel's rotation (q, k heads) and the cache writes at the device key offset koff
-    const int half = a.D / 2, per = half / 16, hd = tile / per, qq = tile % per;
-    const int64_t koff = *a.koff_dev;
-    for (int e = tid; e < 512 * MB; e += 256) {
-      const int tl = e >> 4, c = e & 15, blk = tl >> 5, ml = tl & 31;
-      const int m = (mb0 + blk) * 32 + ml;
-      if (m >= a.M) continue;
-      const int i1 = c, i2 = c + 16;
-      const int q1 = (i1 & 3) + 4 * (i1 >> 3), l1 = ml + 32 * ((i1 >> 2) & 1);
-      const int q2 = (i2 & 3) + 4 * (i2 >> 3), l2 = ml + 32 * ((i2 >> 2) & 1);
-      const int d1 = 16 * qq + c, d2 = d1 + half;
-      const int n1 = hd * a.D + d1, n2 = n1 + half;
-      const float x1 = bf16r(((red[0][blk][q1][l1] + red[1][blk][q1][l1]) + red[2][blk][q1][l1]) + red[3][blk][q1][l1] +
-                             bf16_to_f32(a.bias[n1]));
-      const float x2 = bf16r(((red[0][blk][q2][l2] + red[1][blk][q2][l2]) + red[2][blk][q2][l2]) + red[3][blk][q2][l2] +
-                             bf16_to_f32(a.bias[n2]));
-      if (hd < a.Hq + a.Hkv) {
-        int64_t p = a.pos[m];
-        p = p < 0 ? 0 : (p >= a.maxpos ? a.maxpos - 1 : p);
-        const float cs = a.cos_t[p * half + d1], sn = a.sin_t[p * half + d1];
-        const float o1 = fmaf(x1, cs, -(x2 * sn)), o2 = fmaf(x2, cs, x1 * sn);
-        uint16_t* dst;
-        if (hd < a.Hq) {
-          const int G = a.Hq / a.Hkv;
-          dst = a.q + ((static_cast<int64_t>(m) * a.Hkv + hd / G) * G + hd % G) * a.D;
-        } else {
-          dst = a.kc + ((static_cast<int64_t>(m) * a.Hkv + (hd - a.Hq)) * a.Tk + koff) * a.D;
-        }
-        dst[d1] = to_bf16_bits(o1);
-        dst[d2] = to_bf16_bits(o2);
-      } else {
-        uint16_t* dst = a.vt + (static_cast<int64_t>(m) * a.Hkv + (hd - a.Hq - a.Hkv)) * vt_panel(a.ld_vt, a.D, a.Tk);
-        dst[vt_index(d1, koff, a.ld_vt, a.D)] = to_bf16_bits(x1);
-        dst[vt_index(d2, koff, a.ld_vt, a.D)] = to_bf16_bits(x2);
-      }
-    }
-  } else {
-    // SwiGLU: rows 0..15 gate, 16..31 up of output columns 16 * tile + c; thread -> (token, 8 columns)
-    for (int e = tid; e < 64 * MB; e += 256) {
-      const int tl = e >> 1, hc = e & 1, blk = tl >> 5, ml = tl & 31;
-      u16x8 o;
+  red_epilogue<4, MB, EPI>(a, red, tile, ks, mb0, tid);
+}
+
+// The decode RMSNorm folded into its consumer GEMM's prologue (round 6; replaces the dec_rmsnorm launch before qkv +
+// RoPE and before gate_up + SwiGLU): no norm launch, no grid barrier, nothing published between workgroups. Each
+// workgroup reads the packed fp32 residual x of its token blocks over the whole K (which it needs as its operand
+// anyway), every wave its K slice of NW: the wave's partial sums of squares per row meet in LDS (wave order, fixed:
+// deterministic), rstd = rsqrt(mean + eps) per row, and each fragment is normalised as it is packed for the MFMA:
+// y = bf16(w * (x * rstd)) — add_rmsnorm_fwd / HF Qwen2RMSNorm's rounding (fp32 statistics, weight times the fp32
+// normalised value, one bf16 rounding for the autocast GEMM input). The norm weight is staged in LDS (its loads issued
+// first, so their wait holds no fragment load). The fragment loads are issued before any arithmetic (one memory round
+// trip); whole K per workgroup, so the RoPE / SwiGLU epilogues apply.
+template <int NW, int MB, int KSW, int EPI>
+__global__ __launch_bounds__(64 * NW) void decode_norm_gemm_kernel(DgArgs a) {
+  static_assert(EPI == EPI_ROPE || EPI == EPI_SWIGLU, "whole-K epilogues");
+  constexpr int NT = 64 * NW, WPT = 1024 / NT;  // norm-weight float4s per thread: K <= 4096
+  static_assert(NW * MB >= 4, "the norm weight (<= 4096 floats) is staged in the reduction buffer");
+  __shared__ __attribute__((aligned(16))) float red[NW][MB][16][64];
+  __shared__ float s_ss[NW][MB][32];
+  float* s_w = &red[0][0][0][0];  // the norm weight lives in the reduction buffer until the MFMAs are done
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, ml = lane & 31, hh = lane >> 5;
+  const int tile = blockIdx.x, mb0 = blockIdx.z * MB;
+  const int s0 = wave * KSW;
+  float4 wn[WPT];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int c = 8 * hc + j, ig = c, iu = c + 16;
-        const int qg = (ig & 3) + 4 * (ig >> 3), lg = ml + 32 * ((ig >> 2) & 1);
-        const int qu = (iu & 3) + 4 * (iu >> 3), lu = ml + 32 * ((iu >> 2) & 1);
-        const float g = bf16r(((red[0][blk][qg][lg] + red[1][blk][qg][lg]) + red[2][blk][qg][lg]) + red[3][blk][qg][lg]);
-        const float u = bf16r(((red[0][blk][qu][lu] + red[1][blk][qu][lu]) + red[2][blk][qu][lu]) + red[3][blk][qu][lu]);
-        o[j] = to_bf16_bits(bf16r(silu_fast(g)) * u);
+  for (int j = 0; j < WPT; ++j) {
+    const int k = 4 * (tid + j * NT);
+    if (k < a.K) wn[j] = *reinterpret_cast<const float4*>(a.nw + k);
+  }
+  u16x8 wv[KSW];
+  float4 xv[KSW][MB][2];
+  const uint16_t* wp = a.w + (static_cast<int64_t>(tile) * a.nks + s0) * 512 + lane * 8;
+#pragma unroll
+  for (int s = 0; s < KSW; ++s) wv[s] = __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(wp + s * 512));
+#pragma unroll
+  for (int s = 0; s < KSW; ++s)
+#pragma unroll
+    for (int i = 0; i < MB; ++i) {
+      const float* xp = a.xr + ((static_cast<int64_t>(s0 + s) * a.MBT + mb0 + i) * 64 + lane) * 8;
+      xv[s][i][0] = *reinterpret_cast<const float4*>(xp);
+      xv[s][i][1] = *reinterpret_cast<const float4*>(xp + 4);
+    }
+  __builtin_amdgcn_sched_barrier(0);  // every load in flight before the first use
+#pragma unroll
+  for (int j = 0; j < WPT; ++j) {
+    const int k = 4 * (tid + j * NT);
+    if (k < a.K) *reinterpret_cast<float4*>(s_w + k) = wn[j];
+  }
+  // per-row sum of squares: lane (row ml, k half hh) over its KSW k-steps, the two halves, then the NW waves
+  float ss[MB];
+#pragma unroll
+  for (int i = 0; i < MB; ++i) {
+    ss[i] = 0.f;
+#pragma unroll
+    for (int s = 0; s < KSW; ++s)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const float4 x = xv[s][i][h];
+        ss[i] = fmaf(x.x, x.x, ss[i]);
+        ss[i] = fmaf(x.y, x.y, ss[i]);
+        ss[i] = fmaf(x.z, x.z, ss[i]);
+        ss[i] = fmaf(x.w, x.w, ss[i]);
       }
-      // packed for the next GEMM (K' = half): k step = tile, 8-column half hc, token (mb0 + blk, ml)
-      *reinterpret_cast<u16x8*>(a.out + ((static_cast<int64_t>(tile) * a.MBT + mb0 + blk) * 64 + hc * 32 + ml) * 8) = o;
+    ss[i] += __shfl_xor(ss[i], 32, kWave);  // commutative: both halves hold the same sum
+    if (hh == 0) s_ss[wave][i][ml] = ss[i];
+  }
+  __syncthreads();
+  float r[MB];
+#pragma unroll
+  for (int i = 0; i < MB; ++i) {
+    float t = s_ss[0][i][ml];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) t += s_ss[w][i][ml];
+    r[i] = rsqrtf(t / static_cast<float>(a.K) + a.eps);
+  }
+  f32x16 acc[MB];
+#pragma unroll
+  for (int i = 0; i < MB; ++i) acc[i] = f32x16{};
+#pragma unroll
+  for (int s = 0; s < KSW; ++s) {
+    const float* wk = s_w + 16 * (s0 + s) + 8 * hh;
+    const float4 w0 = *reinterpret_cast<const float4*>(wk), w1 = *reinterpret_cast<const float4*>(wk + 4);
+#pragma unroll
+    for (int i = 0; i < MB; ++i) {
+      const float4 x0 = xv[s][i][0], x1 = xv[s][i][1];
+      const u16x8 y = u16x8{f32_to_bf16(w0.x * (x0.x * r[i])), f32_to_bf16(w0.y * (x0.y * r[i])),
+                            f32_to_bf16(w0.z * (x0.z * r[i])), f32_to_bf16(w0.w * (x0.w * r[i])),
+                            f32_to_bf16(w1.x * (x1.x * r[i])), f32_to_bf16(w1.y * (x1.y * r[i])),
+                            f32_to_bf16(w1.z * (x1.z * r[i])), f32_to_bf16(w1.w * (x1.w * r[i]))};
+      acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(wv[s]), as_bf16x8(y), acc[i], 0, 0, 0);
     }
   }
+  __syncthreads();  // every wave's reads of the norm weight are done before the buffer takes the partial tiles
+#pragma unroll
+  for (int i = 0; i < MB; ++i)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) red[wave][i][q][lane] = acc[i][q];
+  __syncthreads();
+  red_epilogue<NW, MB, EPI>(a, red, tile, 0, mb0, tid);
 }
 
 // ------------------------------------------------------------------------------------------- tiled GEMM
@@ -439,7 +620,7 @@ __global__ __launch_bounds__(64 * WR * WT) void decode_gemm_lds_kernel(DgArgs a)
 template <int CH, int NS>
 __global__ __launch_bounds__(128) void dec_rmsnorm_kernel(const float* x_in, const float* part, int nsplit, float* x_out,
                                                           const float* w, uint16_t* y, int64_t M, int64_t H, int64_t MBT,
-                                                          float eps) {
+                                                          float eps, int64_t XMBT = 0) {
   __shared__ float s_ss[2];
   const int64_t row = blockIdx.x;
   const int tid = threadIdx.x;
@@ -451,8 +632,10 @@ __global__ __launch_bounds__(128) void dec_rmsnorm_kernel(const float* x_in, con
   for (int c = 0; c < CH; ++c) {
     const int64_t ch = tid + 128 * c;
     if (ch < nch) {
-      xv[c][0] = *reinterpret_cast<const float4*>(x_in + row * H + ch * 8);
-      xv[c][1] = *reinterpret_cast<const float4*>(x_in + row * H + ch * 8 + 4);
+      // XMBT > 0: x is the fused-norm decode's packed fp32 residual (8 consecutive columns contiguous)
+      const float* xr = XMBT > 0 ? x_in + pk_off(row, ch * 8, XMBT) : x_in + row * H + ch * 8;
+      xv[c][0] = *reinterpret_cast<const float4*>(xr);
+      xv[c][1] = *reinterpret_cast<const float4*>(xr + 4);
       // the norm weight with the row's first loads: no second memory round trip after the row sum
       wv[c][0] = *reinterpret_cast<const float4*>(w + ch * 8);
       wv[c][1] = *reinterpret_cast<const float4*>(w + ch * 8 + 4);
@@ -587,20 +770,21 @@ __global__ __launch_bounds__(128) void decode_prologue_kernel(const int64_t* res
                                                               int64_t* t_cur, const int64_t* last_pos, int64_t P,
                                                               const uint16_t* embed, int64_t V, int64_t H, float* x,
                                                               int64_t* pos, int64_t* kpos, uint8_t* valid,
-                                                              int64_t ld_valid, unsigned* ticket) {
+                                                              int64_t ld_valid, unsigned* ticket, int64_t x_mbt) {
   const int64_t b = blockIdx.x;
   const int tid = threadIdx.x;
   const int64_t t = *t_dev;
   int64_t tok = responses[b * ld_r + t - 1];
   tok = tok < 0 ? 0 : (tok >= V ? V - 1 : tok);
   const uint16_t* e = embed + tok * H;
-  float* xr = x + b * H;
   for (int64_t c = tid; c < H / 8; c += 128) {
     const u16x8 v = *reinterpret_cast<const u16x8*>(e + 8 * c);
-    *reinterpret_cast<float4*>(xr + 8 * c) = make_float4(bf16_to_f32(v[0]), bf16_to_f32(v[1]), bf16_to_f32(v[2]),
-                                                         bf16_to_f32(v[3]));
-    *reinterpret_cast<float4*>(xr + 8 * c + 4) = make_float4(bf16_to_f32(v[4]), bf16_to_f32(v[5]),
-                                                             bf16_to_f32(v[6]), bf16_to_f32(v[7]));
+    // x_mbt > 0: the fused-norm decode's packed fp32 residual stream
+    float* xr = x_mbt > 0 ? x + pk_off(b, 8 * c, x_mbt) : x + b * H + 8 * c;
+    *reinterpret_cast<float4*>(xr) = make_float4(bf16_to_f32(v[0]), bf16_to_f32(v[1]), bf16_to_f32(v[2]),
+                                                 bf16_to_f32(v[3]));
+    *reinterpret_cast<float4*>(xr + 4) = make_float4(bf16_to_f32(v[4]), bf16_to_f32(v[5]), bf16_to_f32(v[6]),
+                                                     bf16_to_f32(v[7]));
   }
   if (tid == 0) {
     pos[b] = last_pos[b] + t;
@@ -793,10 +977,249 @@ void launch_dg(const DgArgs& a, const DgPlan& p, hipStream_t s) {
   }
 }
 
+// fused-norm consumers: (waves, token blocks per workgroup, k16 steps per wave) instantiated; whole K per workgroup
+// (NW x KSW = K / 16). Registers in flight per lane: 4 KSW (weights) + 8 KSW MB (fp32 residual)
+struct DnShape { int nw, mb, ksw; };
+// (16 waves at K 3584 / 4096 would need more than their 128 registers per lane: those models take the unfused step)
+constexpr DnShape kNorm[] = {{4, 1, 14}, {8, 1, 7}, {8, 2, 7}, {4, 2, 7}};
+constexpr int kNumNorm = static_cast<int>(sizeof(kNorm) / sizeof(kNorm[0]));
+int g_dn_force = -1;     // tuning: force a kNorm configuration (drl_decode_norm_set_plan), -1 = planner
+int g_dn_max_rows = 128;  // the fused-norm decode up to this many rows (beyond: the tiled kernels + dec_rmsnorm)
+int g_dr_max_ks = 0;     // tuning: most K slices of an EPI_RESID plan (0 = the partial-sum planner's choice)
+
+// the consumer's configuration: the SwiGLU gate_up prefers 2 token blocks per workgroup (each weight fragment feeds
+// two MFMAs: the 17 MB weight is read once), qkv + RoPE one (twice the workgroups over a 2 MB weight); among those,
+// the fewest waves (longest per-wave chain that fits the registers)
+bool plan_norm(int64_t M, int64_t N, int64_t K, int epi, DgPlan& p) {
+  if (M < 1 || M > g_dn_max_rows || M > 512 || K % 64 != 0 || K > 4096 || N < 1) return false;
+  const int blocks = static_cast<int>((M + 31) / 32);
+  p.mbt = blocks == 1 ? 1 : (blocks + 1) / 2 * 2;
+  p.tiles = static_cast<int>(epi == EPI_SWIGLU ? (N / 2 + 15) / 16 : (N + 31) / 32);
+  const int nks = static_cast<int>(K / 16);
+  const int want_mb = epi == EPI_SWIGLU ? 2 : 1;
+  int best = -1;
+  for (int ci = 0; ci < kNumNorm; ++ci) {
+    const DnShape& c = kNorm[ci];
+    if (c.nw * c.ksw != nks || c.mb > p.mbt || p.mbt % c.mb != 0) continue;
+    if (g_dn_force >= 0 && ci != g_dn_force) continue;
+    if (best < 0) { best = ci; continue; }
+    const DnShape& b = kNorm[best];
+    const bool mb_better = (c.mb == want_mb) != (b.mb == want_mb) ? c.mb == want_mb : false;
+    if (mb_better || ((c.mb == want_mb) == (b.mb == want_mb) && c.mb == b.mb && c.nw < b.nw)) best = ci;
+  }
+  if (best < 0) return false;
+  p.mb = kNorm[best].mb;
+  p.ksw = best;  // index into kNorm
+  p.ksplit = 1;
+  p.mgroups = p.mbt / p.mb;
+  return true;
+}
+
+// the K-split residual producer: the one-round-trip kernel's partial-sum plan (never the tiled kernels)
+bool plan_resid(int64_t M, int64_t N, int64_t K, DgPlan& p) {
+  if (M > g_dn_max_rows || N % 4 != 0) return false;
+  const int max_ks = g_dt_max_ks;
+  if (g_dr_max_ks > 0) {  // tuning: at most g_dr_max_ks slices (1 = whole K per workgroup where a shape allows)
+    bool found = false;
+    for (const DgShape& c : kShapes) {
+      const int nks = static_cast<int>(K / 16);
+      if (K % 64 != 0 || nks % (4 * c.ksw) != 0) continue;
+      const int ks = nks / (4 * c.ksw);
+      const int blocks = static_cast<int>((M + 31) / 32), mbt = blocks == 1 ? 1 : (blocks + 1) / 2 * 2;
+      if (ks > g_dr_max_ks || c.mb > mbt || c.mb != 1) continue;
+      if (!found || ks > p.ksplit) {
+        p.mbt = mbt;
+        p.tiles = static_cast<int>((N + 31) / 32);
+        p.mb = 1;
+        p.ksw = c.ksw;
+        p.ksplit = ks;
+        p.mgroups = mbt;
+        found = true;
+      }
+    }
+    return found;
+  }
+  (void)max_ks;
+  return plan_decode_gemm(M, N, K, EPI_PARTIAL, p);
+}
+
+template <int EPI>
+void launch_dn(const DgArgs& a, const DgPlan& p, hipStream_t s) {
+  const DnShape c = kNorm[p.ksw];
+  const dim3 grid(p.tiles, 1, p.mgroups);
+#define DRL_DN(NW, MB, KSW) \
+  hipLaunchKernelGGL((decode_norm_gemm_kernel<NW, MB, KSW, EPI>), grid, dim3(64 * NW), 0, s, a)
+  switch (p.ksw) {
+    case 0: DRL_DN(4, 1, 14); break;
+    case 1: DRL_DN(8, 1, 7); break;
+    case 2: DRL_DN(8, 2, 7); break;
+    default: DRL_DN(4, 2, 7); break;
+  }
+#undef DRL_DN
+  (void)c;
+}
+
 }  // namespace
 }  // namespace drl
 
 extern "C" {
+
+void drl_decode_norm_set_plan(int32_t config, int32_t max_rows, int32_t resid_max_splits) {
+  drl::g_dn_force = (config >= 0 && config < drl::kNumNorm) ? config : -1;
+  drl::g_dn_max_rows = max_rows > 0 ? max_rows : 128;
+  drl::g_dr_max_ks = resid_max_splits > 0 ? resid_max_splits : 0;
+}
+
+int drl_decode_norm_plan(int64_t M, int64_t N, int64_t K, int32_t epilogue, int32_t* ksplit, int32_t* mbt,
+                         int32_t* config) {
+  drl::DgPlan p{};
+  bool ok;
+  if (epilogue == DRL_DECODE_RESID) ok = drl::plan_resid(M, N, K, p);
+  else if (epilogue == DRL_DECODE_SWIGLU) ok = drl::plan_norm(M, N, K, drl::EPI_SWIGLU, p);
+  else if (epilogue == DRL_DECODE_ROPE) ok = drl::plan_norm(M, N, K, drl::EPI_ROPE, p);
+  else return drl::fail(DRL_ERR_INVALID, "decode norm plan: unknown epilogue %d", epilogue);
+  if (!ok)
+    return drl::fail(DRL_ERR_UNSUPPORTED, "fused-norm decode: unsupported shape M=%lld N=%lld K=%lld", (long long)M,
+                     (long long)N, (long long)K);
+  if (ksplit) *ksplit = p.ksplit;
+  if (mbt) *mbt = p.mbt;
+  if (config) *config = epilogue == DRL_DECODE_RESID ? p.ksw : p.ksw;
+  return DRL_OK;
+}
+
+size_t drl_decode_resid_counter_bytes(int64_t M, int64_t N, int64_t K) {
+  drl::DgPlan p{};
+  if (!drl::plan_resid(M, N, K, p)) return 0;
+  return static_cast<size_t>(p.tiles) * p.mgroups * 4;
+}
+
+int drl_decode_gemm_resid(const void* x_packed, const void* w_packed, int64_t M, int64_t N, int64_t K, float* x_resid,
+                          int64_t x_mbt, float* partials, void* counters, size_t counter_bytes, void* stream) {
+  using namespace drl;
+  DRL_CHECK_ARG(x_packed && w_packed && x_resid, "NULL input");
+  DRL_CHECK_ARG(aligned16(x_packed) && aligned16(w_packed) && aligned16(x_resid), "16-byte aligned operands needed");
+  DgPlan p{};
+  if (!plan_resid(M, N, K, p))
+    return fail(DRL_ERR_UNSUPPORTED, "decode residual GEMM: unsupported shape M=%lld N=%lld K=%lld", (long long)M,
+                (long long)N, (long long)K);
+  DRL_CHECK_ARG(x_mbt == p.mbt, "x_mbt %lld != the plan's %d token blocks", (long long)x_mbt, p.mbt);
+  DRL_CHECK_ARG(p.ksplit == 1 || (partials && aligned16(partials) && counters &&
+                                  counter_bytes >= static_cast<size_t>(p.tiles) * p.mgroups * 4),
+                "K slices need the partial slabs (ksplit x M x N fp32) and zeroed counters");
+  DgArgs a{};
+  a.x = static_cast<const uint16_t*>(x_packed);
+  a.w = static_cast<const uint16_t*>(w_packed);
+  a.M = static_cast<int>(M);
+  a.N = static_cast<int>(N);
+  a.K = static_cast<int>(K);
+  a.MBT = p.mbt;
+  a.nks = static_cast<int>(K / 16);
+  a.tiles = p.tiles;
+  a.part = partials;
+  a.xr = x_resid;
+  a.cnt = static_cast<unsigned*>(counters);
+  a.ksplit = p.ksplit;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (p.mb == 1) launch_dg<1, EPI_RESID>(a, p, s);
+  else launch_dg<2, EPI_RESID>(a, p, s);
+  DRL_LAUNCH_CHECK();
+  return DRL_OK;
+}
+
+int drl_decode_gemm_norm(const float* x_resid, const float* norm_weight, float eps, const void* w_packed, int64_t M,
+                         int64_t N, int64_t K, void* out_packed, void* stream) {
+  using namespace drl;
+  DRL_CHECK_ARG(x_resid && norm_weight && w_packed && out_packed, "NULL input");
+  DRL_CHECK_ARG(aligned16(x_resid) && aligned16(norm_weight) && aligned16(w_packed) && aligned16(out_packed),
+                "16-byte aligned operands needed");
+  DRL_CHECK_ARG(N % 32 == 0, "SwiGLU needs N %% 32 == 0");
+  DgPlan p{};
+  if (!plan_norm(M, N, K, EPI_SWIGLU, p))
+    return fail(DRL_ERR_UNSUPPORTED, "decode norm + gate_up: unsupported shape M=%lld N=%lld K=%lld", (long long)M,
+                (long long)N, (long long)K);
+  DgArgs a{};
+  a.w = static_cast<const uint16_t*>(w_packed);
+  a.M = static_cast<int>(M);
+  a.N = static_cast<int>(N);
+  a.K = static_cast<int>(K);
+  a.MBT = p.mbt;
+  a.nks = static_cast<int>(K / 16);
+  a.tiles = p.tiles;
+  a.half = static_cast<int>(N / 2);
+  a.out = static_cast<uint16_t*>(out_packed);
+  a.xr = const_cast<float*>(x_resid);
+  a.nw = norm_weight;
+  a.eps = eps;
+  launch_dn<EPI_SWIGLU>(a, p, static_cast<hipStream_t>(stream));
+  DRL_LAUNCH_CHECK();
+  return DRL_OK;
+}
+
+int drl_decode_qkv_rope_norm(const float* x_resid, const float* norm_weight, float eps, const void* w_packed,
+                             const void* bias, const int64_t* position_ids, const float* cos_t, const float* sin_t,
+                             int64_t maxpos, int64_t M, int64_t K, int64_t Hq, int64_t Hkv, int64_t D, void* q,
+                             void* k_cache, void* vt_cache, int64_t Tk, int64_t ld_vt, const int64_t* koff_dev,
+                             void* stream) {
+  using namespace drl;
+  DRL_CHECK_ARG(x_resid && norm_weight && w_packed && bias && position_ids && cos_t && sin_t && q && k_cache &&
+                    vt_cache && koff_dev,
+                "NULL input");
+  DRL_CHECK_ARG(aligned16(x_resid) && aligned16(norm_weight) && aligned16(w_packed), "16-byte aligned operands needed");
+  DRL_CHECK_ARG(Hq >= 1 && Hkv >= 1 && Hq % Hkv == 0 && D % 32 == 0 && (ld_vt >= Tk || ld_vt == DRL_VT_BLOCKED) &&
+                    Tk >= 1 && maxpos >= 1,
+                "bad shape");
+  const int64_t N = (Hq + 2 * Hkv) * D;
+  DgPlan p{};
+  if (!plan_norm(M, N, K, EPI_ROPE, p))
+    return fail(DRL_ERR_UNSUPPORTED, "decode norm + qkv + rope: unsupported shape M=%lld N=%lld K=%lld", (long long)M,
+                (long long)N, (long long)K);
+  DgArgs a{};
+  a.w = static_cast<const uint16_t*>(w_packed);
+  a.M = static_cast<int>(M);
+  a.N = static_cast<int>(N);
+  a.K = static_cast<int>(K);
+  a.MBT = p.mbt;
+  a.nks = static_cast<int>(K / 16);
+  a.tiles = p.tiles;
+  a.bias = static_cast<const uint16_t*>(bias);
+  a.pos = position_ids;
+  a.cos_t = cos_t;
+  a.sin_t = sin_t;
+  a.q = static_cast<uint16_t*>(q);
+  a.kc = static_cast<uint16_t*>(k_cache);
+  a.vt = static_cast<uint16_t*>(vt_cache);
+  a.koff_dev = koff_dev;
+  a.maxpos = maxpos;
+  a.Tk = Tk;
+  a.ld_vt = ld_vt;
+  a.Hq = static_cast<int>(Hq);
+  a.Hkv = static_cast<int>(Hkv);
+  a.D = static_cast<int>(D);
+  a.xr = const_cast<float*>(x_resid);
+  a.nw = norm_weight;
+  a.eps = eps;
+  launch_dn<EPI_ROPE>(a, p, static_cast<hipStream_t>(stream));
+  DRL_LAUNCH_CHECK();
+  return DRL_OK;
+}
+
+int drl_decode_final_norm(const float* x_resid, int64_t x_mbt, const float* weight, void* y, int64_t M, int64_t H,
+                          int64_t y_mbt, float eps, void* stream) {
+  using namespace drl;
+  DRL_CHECK_ARG(x_resid && weight && y, "NULL input");
+  DRL_CHECK_ARG(M >= 1 && H >= 8 && H % 8 == 0 && H <= 8 * 128 * 4, "bad shape (H %% 8 == 0, H <= 4096)");
+  DRL_CHECK_ARG(x_mbt >= 1 && x_mbt * 32 >= M && (y_mbt == 0 || y_mbt * 32 >= M), "token blocks too few");
+  DRL_CHECK_ARG(aligned16(x_resid) && aligned16(y) && aligned16(weight), "16-byte aligned buffers needed");
+  const int ch = static_cast<int>((H / 8 + 127) / 128);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const dim3 grid(static_cast<unsigned>(M));
+  uint16_t* yy = static_cast<uint16_t*>(y);
+  if (ch <= 1) hipLaunchKernelGGL((dec_rmsnorm_kernel<1, 0>), grid, dim3(128), 0, s, x_resid, nullptr, 0, nullptr, weight, yy, M, H, y_mbt, eps, x_mbt);
+  else if (ch == 2) hipLaunchKernelGGL((dec_rmsnorm_kernel<2, 0>), grid, dim3(128), 0, s, x_resid, nullptr, 0, nullptr, weight, yy, M, H, y_mbt, eps, x_mbt);
+  else hipLaunchKernelGGL((dec_rmsnorm_kernel<4, 0>), grid, dim3(128), 0, s, x_resid, nullptr, 0, nullptr, weight, yy, M, H, y_mbt, eps, x_mbt);
+  DRL_LAUNCH_CHECK();
+  return DRL_OK;
+}
 
 void drl_decode_gemm_force_tiled(int32_t config, int32_t min_rows) {
   drl::g_dt_force = (config >= 0 && config < drl::kNumTiled) ? config : -1;
@@ -1000,19 +1423,20 @@ size_t drl_decode_step_prologue_workspace_bytes(void) { return 256; }
 int drl_decode_step_prologue(const int64_t* responses, int64_t ld_responses, int64_t* t_dev, int64_t* t_cur,
                              const int64_t* last_pos, int64_t prompt_len, const void* embed, int32_t dt, int64_t V,
                              int64_t H, int64_t B, float* x, int64_t* positions, int64_t* kpos, uint8_t* key_valid,
-                             int64_t ld_valid, void* workspace, size_t workspace_bytes, void* stream) {
+                             int64_t ld_valid, void* workspace, size_t workspace_bytes, int64_t x_mbt, void* stream) {
   using namespace drl;
   DRL_CHECK_ARG(responses && t_dev && t_cur && last_pos && embed && x && positions && kpos && key_valid,
                 "NULL input");
   DRL_CHECK_ARG(dt == DRL_BF16, "the decode step prologue reads a bf16 embedding");
   DRL_CHECK_ARG(B >= 1 && H >= 8 && H % 8 == 0 && V >= 1 && prompt_len >= 0, "bad shape (H %% 8 == 0)");
   DRL_CHECK_ARG(aligned16(embed) && aligned16(x), "embedding / x must be 16-byte aligned");
+  DRL_CHECK_ARG(x_mbt == 0 || x_mbt * 32 >= B, "x_mbt too small");
   if (!workspace || workspace_bytes < drl_decode_step_prologue_workspace_bytes())
     return fail(DRL_ERR_WORKSPACE, "prologue workspace: need 256 zero-filled bytes");
   hipLaunchKernelGGL(decode_prologue_kernel, dim3(static_cast<unsigned>(B)), dim3(128), 0,
                      static_cast<hipStream_t>(stream), responses, ld_responses, t_dev, t_cur, last_pos, prompt_len,
                      static_cast<const uint16_t*>(embed), V, H, x, positions, kpos, key_valid, ld_valid,
-                     static_cast<unsigned*>(workspace));
+                     static_cast<unsigned*>(workspace), x_mbt);
   DRL_LAUNCH_CHECK();
   return DRL_OK;
 }

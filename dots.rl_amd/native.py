@@ -1040,21 +1040,25 @@ def decode_attention_vt(q, k_cache, vt_cache, key_valid, L, out, qpos=None, qpos
     return out
 
 
-def decode_step_prologue(responses, t_dev, t_cur, last_pos, prompt_len, embed, x, positions, kpos, key_valid):
+def decode_step_prologue(responses, t_dev, t_cur, last_pos, prompt_len, embed, x, positions, kpos, key_valid,
+                         x_mbt=0):
     """One launch of the graphed decode step's bookkeeping (drl_decode_step_prologue): x = float(embed[previous
-    token]), positions = last_pos + t, key_valid[:, t + P - 1] = 1, kpos = t + P - 1, t_cur = t, t_dev += 1."""
+    token]), positions = last_pos + t, key_valid[:, t + P - 1] = 1, kpos = t + P - 1, t_cur = t, t_dev += 1.
+    ``x_mbt`` > 0: x is the fused-norm step's packed fp32 residual (x_mbt token blocks, flat)."""
     _dev(responses, t_dev, t_cur, last_pos, embed, x, positions, kpos, key_valid)
     assert responses.dtype == t_dev.dtype == t_cur.dtype == last_pos.dtype == positions.dtype == kpos.dtype == torch.int64
     assert embed.dtype == torch.bfloat16 and embed.is_contiguous() and x.dtype == torch.float32 and x.is_contiguous()
     assert key_valid.dtype == torch.uint8 and key_valid.stride(1) == 1 and responses.stride(1) == 1
-    B, H = x.shape
+    B, H = positions.numel(), embed.shape[1]
+    assert x.numel() >= (x_mbt * 32 if x_mbt else B) * H
     V = embed.shape[0]
     assert last_pos.is_contiguous() and last_pos.numel() == B and positions.numel() == B and embed.shape[1] == H
     L = lib()
     ws = _linear_workspace(x.device, L.drl_decode_step_prologue_workspace_bytes(), "decode_prologue")
     check(L.drl_decode_step_prologue(_p(responses), responses.stride(0), _p(t_dev), _p(t_cur), _p(last_pos),
                                      int(prompt_len), _p(embed), _lib.DRL_BF16, V, H, B, _p(x), _p(positions), _p(kpos),
-                                     _p(key_valid), key_valid.stride(0), _p(ws), ws.numel() * 8, _stream()),
+                                     _p(key_valid), key_valid.stride(0), _p(ws), ws.numel() * 8, int(x_mbt),
+                                     _stream()),
           "drl_decode_step_prologue")
 
 
@@ -1140,6 +1144,67 @@ def decode_rope(partials, bias, position_ids, cos_t, sin_t, Hq, Hkv, D, q, k_cac
     check(lib().drl_decode_rope(_p(partials), ns, _p(bias), _p(position_ids), _p(cos_t), _p(sin_t), cos_t.shape[0], B,
                                 Hq, Hkv, D, _p(q), _p(k_cache), _p(v_cache), _p(vt_cache), Tk, ld_vt, int(koff),
                                 _p(koff_dev), _stream()), "drl_decode_rope")
+
+
+# ------------------------------------------------------------------------------ fused-norm decode step (ABI 8)
+DECODE_RESID, DECODE_ROPE = 2, 3
+
+
+def decode_norm_plan(M, N, K, epilogue):
+    """(ksplit, mbt, config) of the fused-norm decode kernel for this shape (epilogue DECODE_RESID / DECODE_SWIGLU /
+    DECODE_ROPE), or None when the shape takes the unfused step."""
+    ks, mbt, cfg = ctypes.c_int32(0), ctypes.c_int32(0), ctypes.c_int32(0)
+    rc = lib().drl_decode_norm_plan(M, N, K, epilogue, ctypes.byref(ks), ctypes.byref(mbt), ctypes.byref(cfg))
+    return (ks.value, mbt.value, cfg.value) if rc == 0 else None
+
+
+def decode_gemm_resid(x_packed, w_packed, M, N, K, x_resid, x_mbt, partials, counters):
+    """o_proj / down_proj of the fused-norm step: x_resid (packed fp32) += bf16(x W^T) in place."""
+    _dev(x_packed, w_packed, x_resid, partials, counters)
+    assert x_resid.dtype == torch.float32 and x_resid.is_contiguous() and x_resid.numel() >= x_mbt * 32 * N
+    assert partials is None or (partials.dtype == torch.float32 and partials.is_contiguous())
+    nb = counters.numel() * counters.element_size() if counters is not None else 0
+    check(lib().drl_decode_gemm_resid(_p(x_packed), _p(w_packed), M, N, K, _p(x_resid), int(x_mbt), _p(partials),
+                                      _p(counters), nb, _stream()), "drl_decode_gemm_resid")
+
+
+def decode_gemm_norm(x_resid, norm_weight, eps, w_packed, M, N, K, out_packed):
+    """gate_up + SwiGLU of the fused-norm step on RMSNorm(x_resid) computed in the kernel's prologue."""
+    _dev(x_resid, norm_weight, w_packed, out_packed)
+    assert norm_weight.dtype == torch.float32 and norm_weight.is_contiguous() and norm_weight.numel() == K
+    check(lib().drl_decode_gemm_norm(_p(x_resid), _p(norm_weight), float(eps), _p(w_packed), M, N, K, _p(out_packed),
+                                     _stream()), "drl_decode_gemm_norm")
+    return out_packed
+
+
+def decode_qkv_rope_norm(x_resid, norm_weight, eps, w_packed, bias, position_ids, cos_t, sin_t, M, K, Hq, Hkv, D, q,
+                         k_cache, vt_cache, koff_dev):
+    """qkv + bias + RoPE + cache writes of the fused-norm step on RMSNorm(x_resid)."""
+    _dev(x_resid, norm_weight, w_packed, bias, position_ids, q, k_cache, vt_cache, koff_dev)
+    assert q.is_contiguous() and k_cache.is_contiguous() and norm_weight.dtype == torch.float32
+    _vt_cap_ok(vt_cache, k_cache.shape[2])
+    check(lib().drl_decode_qkv_rope_norm(_p(x_resid), _p(norm_weight), float(eps), _p(w_packed), _p(bias),
+                                         _p(position_ids), _p(cos_t), _p(sin_t), cos_t.shape[0], M, K, Hq, Hkv, D, _p(q),
+                                         _p(k_cache), _p(vt_cache), k_cache.shape[2], vt_ld(vt_cache), _p(koff_dev),
+                                         _stream()), "drl_decode_qkv_rope_norm")
+
+
+def decode_final_norm(x_resid, x_mbt, weight, y, M, H, eps, y_mbt=0):
+    """The model's final RMSNorm from the packed fp32 residual: y bf16 row-major (M, H) or packed (y_mbt > 0)."""
+    _dev(x_resid, weight, y)
+    check(lib().drl_decode_final_norm(_p(x_resid), int(x_mbt), _p(weight), _p(y), M, H, int(y_mbt), float(eps),
+                                      _stream()), "drl_decode_final_norm")
+    return y
+
+
+def pack_residual(x, mbt, out=None):
+    """Row-major fp32 (M, H) -> the fused-norm step's packed residual (mbt token blocks; rows >= M zero)."""
+    M, H = x.shape
+    xp = pack_activations(x, mbt)
+    if out is None:
+        return xp
+    out.view(-1)[:xp.numel()].copy_(xp)
+    return out
 
 
 def decode_pack_weight_rope(w, head_dim, out=None):

@@ -1155,9 +1155,11 @@ class PackedDecode:
                         for n, k, sw in ((NQ, H, False), (H, cfg.num_attention_heads * D, False), (2 * I, H, True),
                                          (H, I, False))))
 
-    def __init__(self, model, B, weights=None):
+    def __init__(self, model, B, weights=None, fused_norm=True):
         """``weights``: another PackedDecode's packed weights (the layout does not depend on B), shared by the
-        row lanes of one rollout instead of packed again."""
+        row lanes of one rollout instead of packed again. ``fused_norm``: the five-launch layer (the RMSNorms in the
+        consumer GEMMs' prologue, the residual adds in the o_proj / down_proj epilogues) where the fused kernels take
+        the shape (1..128 rows at Qwen2.5-0.5B width); otherwise the seven-launch layer."""
         cfg, s, dev = model.cfg, model.store, model.store.device
         self.model = model
         self.B = B
@@ -1169,6 +1171,16 @@ class PackedDecode:
                       "gu": native.decode_gemm_plan(B, 2 * I, H, True), "d": native.decode_gemm_plan(B, H, I)}
         self.mbt = self.plans["o"][1]
         assert all(p[1] == self.mbt for p in self.plans.values())
+        fplans = None
+        if fused_norm:
+            fplans = {"o": native.decode_norm_plan(B, H, self.HD, native.DECODE_RESID),
+                      "d": native.decode_norm_plan(B, H, I, native.DECODE_RESID),
+                      "gu": native.decode_norm_plan(B, 2 * I, H, native.DECODE_SWIGLU),
+                      "qkv": native.decode_norm_plan(B, self.NQ, H, native.DECODE_ROPE)}
+            if any(v is None or v[1] != self.mbt for v in fplans.values()):
+                fplans = None
+        self.fused = fplans is not None
+        self.fplans = fplans
         bf = torch.bfloat16
         self.w = weights if weights is not None else []
         for i in range(0 if weights is not None else cfg.num_hidden_layers):
@@ -1181,9 +1193,20 @@ class PackedDecode:
         self.h_p = torch.zeros(rows * H, dtype=bf, device=dev)        # RMSNorm out (packed; pad rows stay 0)
         self.attn_p = torch.zeros(rows * self.HD, dtype=bf, device=dev)
         self.a_p = torch.zeros(rows * I, dtype=bf, device=dev)        # SwiGLU out
-        self.part_o = torch.empty(self.plans["o"][0], B, H, device=dev)
-        self.part_d = torch.empty(self.plans["d"][0], B, H, device=dev)
-        self.x = torch.empty(B, H, device=dev)                         # fp32 residual stream
+        if self.fused:
+            # the packed fp32 residual stream (pad rows stay 0), K-slice scratch and arrival counters (left zeroed by
+            # every launch; the two producers run one after the other on the stream, so they share them)
+            self.xr = torch.zeros(rows * H, device=dev)
+            self.part_o = torch.empty(max(1, self.fplans["o"][0]), B, H, device=dev)
+            self.part_d = torch.empty(max(1, self.fplans["d"][0]), B, H, device=dev)
+            nb = max(native.lib().drl_decode_resid_counter_bytes(B, H, self.HD),
+                     native.lib().drl_decode_resid_counter_bytes(B, H, I))
+            self.cnt = torch.zeros((nb + 3) // 4, dtype=torch.int32, device=dev)
+            self.x = None
+        else:
+            self.part_o = torch.empty(self.plans["o"][0], B, H, device=dev)
+            self.part_d = torch.empty(self.plans["d"][0], B, H, device=dev)
+            self.x = torch.empty(B, H, device=dev)                         # fp32 residual stream
         self.q = torch.empty(B, Hkv, Hq // Hkv, D, dtype=bf, device=dev)
         self.h_out = torch.empty(B, H, dtype=bf, device=dev)
         self.pos = torch.empty(B, dtype=torch.int64, device=dev)   # step_from: rotary positions of the new token
@@ -1195,15 +1218,24 @@ class PackedDecode:
         """One graphed decode step driven by the device counter t_dev: the previous token of every row is
         responses[:, t - 1]; one prologue launch embeds it, sets positions / the cache slot / key_valid, publishes
         t (self.t_cur, the selection's step) and advances t_dev. Returns the final-norm hidden (B, H)."""
-        native.decode_step_prologue(responses, t_dev, self.t_cur, last_pos.reshape(-1).contiguous(), P,
-                                    self.model.store.w("embed_tokens"), self.x, self.pos, self.kpos, cache.valid)
+        if self.fused:
+            native.decode_step_prologue(responses, t_dev, self.t_cur, last_pos.reshape(-1).contiguous(), P,
+                                        self.model.store.w("embed_tokens"), self.xr, self.pos, self.kpos, cache.valid,
+                                        x_mbt=self.mbt)
+        else:
+            native.decode_step_prologue(responses, t_dev, self.t_cur, last_pos.reshape(-1).contiguous(), P,
+                                        self.model.store.w("embed_tokens"), self.x, self.pos, self.kpos, cache.valid)
         return self._layers(cache, self.pos, self.kpos)
 
     @torch.no_grad()
     def step(self, cache, tokens, positions, kpos_dev):
         """One token per sequence at device cache position kpos_dev; returns the final-norm hidden (B, H)."""
         s = self.model.store
-        self.x.copy_(F.embedding(tokens.view(-1), s.w("embed_tokens")))
+        x = F.embedding(tokens.view(-1), s.w("embed_tokens")).to(torch.float32)
+        if self.fused:
+            native.pack_residual(x, self.mbt, out=self.xr)
+        else:
+            self.x.copy_(x)
         cache.valid.index_fill_(1, kpos_dev, 1)
         return self._layers(cache, positions.view(-1), kpos_dev)
 
@@ -1214,6 +1246,21 @@ class PackedDecode:
         Hq, Hkv, D = cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim
         eps, mbt = cfg.rms_norm_eps, self.mbt
         Lk = cache.k[0].shape[2]
+        if self.fused:
+            # five launches per layer: the RMSNorms run in the consumers' prologues (qkv + RoPE, gate_up + SwiGLU),
+            # the residual adds in the producers' epilogues (o_proj, down_proj) on the packed fp32 residual xr
+            for i in range(cfg.num_hidden_layers):
+                p, w = f"layers.{i}.", self.w[i]
+                native.decode_qkv_rope_norm(self.xr, s.w(p + "input_layernorm"), eps, w["qkv"], m.qkv_bias(i), pos,
+                                            m.cos, m.sin, B, H, Hq, Hkv, D, self.q, cache.k[i], cache.vt[i], kpos_dev)
+                native.decode_attention_vt(self.q, cache.k[i], cache.vt[i], cache.valid, Lk, self.attn_p,
+                                           qpos_dev=kpos_dev, out_mbt=mbt, group=cache.group, shared_keys=cache.shared)
+                native.decode_gemm_resid(self.attn_p, w["o"], B, H, self.HD, self.xr, mbt, self.part_o, self.cnt)
+                native.decode_gemm_norm(self.xr, s.w(p + "post_attention_layernorm"), eps, w["gu"], B, 2 * I, H,
+                                        self.a_p)
+                native.decode_gemm_resid(self.a_p, w["d"], B, H, I, self.xr, mbt, self.part_d, self.cnt)
+            native.decode_final_norm(self.xr, mbt, s.w("norm"), self.h_out, B, H, eps)
+            return self.h_out
         prev = None
         for i in range(cfg.num_hidden_layers):
             p, w = f"layers.{i}.", self.w[i]

@@ -24,7 +24,7 @@ extern "C" {
 
 /* 3: drl_ppo_loss_params gained policy_loss, cov_ratio, clip_cov_lb, clip_cov_ub, ppo_kl_coef, cov_seed (a caller
  * built against version 2 passes a shorter struct); drl_gemm (operand layouts, fp32 epilogues, stream-K) */
-#define DRL_ABI_VERSION 7
+#define DRL_ABI_VERSION 8
 
 /* ld_vt value selecting the key-blocked V^T cache layout (B, Hkv, ceil(cap / 32), D, 32) wherever a V^T
  * operand with a leading dimension ld_vt is taken (flash / decode attention, the rope and decode-projection
@@ -458,12 +458,14 @@ size_t drl_decode_attention_vt_workspace_bytes(int64_t B, int64_t Hkv, int64_t D
  * t = *t_dev, for every row b: x[b, :] = float(embed[responses[b, t - 1], :]) (bf16 embedding (V, H) -> fp32
  * residual stream), positions[b] = last_pos[b] + t, key_valid[b, t + prompt_len - 1] = 1; then *kpos =
  * t + prompt_len - 1, *t_cur = t and *t_dev = t + 1 (the last workgroup, after every row has read t_dev).
- * workspace: drl_decode_step_prologue_workspace_bytes() bytes, zero-filled once (left zeroed by every call). */
+ * workspace: drl_decode_step_prologue_workspace_bytes() bytes, zero-filled once (left zeroed by every call).
+ * x_mbt > 0 (ABI 8): x is the fused-norm decode's packed fp32 residual (drl_decode_gemm_resid), x_mbt token blocks;
+ * 0: x row-major (B, H). */
 size_t drl_decode_step_prologue_workspace_bytes(void);
 int drl_decode_step_prologue(const int64_t* responses, int64_t ld_responses, int64_t* t_dev, int64_t* t_cur,
                              const int64_t* last_pos, int64_t prompt_len, const void* embed, int32_t dt, int64_t V,
                              int64_t H, int64_t B, float* x, int64_t* positions, int64_t* kpos, uint8_t* key_valid,
-                             int64_t ld_valid, void* workspace, size_t workspace_bytes, void* stream);
+                             int64_t ld_valid, void* workspace, size_t workspace_bytes, int64_t x_mbt, void* stream);
 /* Tuning hook (tools/kernel_bench.py): force waves per workgroup (2/4/8/16) and key splits; 0 = automatic. */
 void drl_decode_attention_set_plan(int32_t waves, int32_t splits);
 /* Tuning hook for forced plans (set_plan waves != 0): 1 = register-lean key loop (one block in flight per
@@ -544,7 +546,9 @@ int drl_linear_select_tokens(const void* hidden, int64_t ld_h, const void* weigh
  * zeros (allocate zero-filled, never write them). */
 typedef enum drl_decode_epilogue {
   DRL_DECODE_PARTIAL = 0, /* fp32 partial sums per K slice: partials (ksplit, M, N) */
-  DRL_DECODE_SWIGLU = 1   /* W = [gate | up] packed with swiglu=1: bf16(bf16(silu(g)) * u) packed (MBT, N/2) */
+  DRL_DECODE_SWIGLU = 1,  /* W = [gate | up] packed with swiglu=1: bf16(bf16(silu(g)) * u) packed (MBT, N/2) */
+  DRL_DECODE_RESID = 2,   /* drl_decode_norm_plan only: the residual producer drl_decode_gemm_resid */
+  DRL_DECODE_ROPE = 3     /* drl_decode_norm_plan only: the norm consumer drl_decode_qkv_rope_norm */
 } drl_decode_epilogue;
 /* ksplit (K slices = partial sums the consumer adds) and mbt (token blocks the packed panels need). */
 int drl_decode_gemm_plan(int64_t M, int64_t N, int64_t K, int32_t epilogue, int32_t* ksplit, int32_t* mbt);
@@ -589,6 +593,43 @@ int drl_decode_rope(const float* partials, int32_t nsplit, const void* bias, con
                     const float* cos_t, const float* sin_t, int64_t maxpos, int64_t B, int64_t Hq, int64_t Hkv,
                     int64_t D, void* q, void* k_cache, void* v_cache, void* vt_cache, int64_t Tk, int64_t ld_vt,
                     int64_t koff, const int64_t* koff_dev, void* stream);
+/* ---- Fused-norm decode step (ABI 8; 1..128 rows by default): the decoder layer's two RMSNorms folded into the
+ * consumer GEMMs' prologue, so a layer is five launches (qkv + RoPE, attention, o_proj, gate_up + SwiGLU, down_proj)
+ * instead of seven. Replaces, per decode token of HF generate (hf_rollout.py:112-124 -> modeling_qwen2), the
+ * residual adds of Qwen2DecoderLayer and Qwen2RMSNorm (input_layernorm / post_attention_layernorm) with the same
+ * rounding: x += bf16(o) in fp32, y = bf16(w * (x * rsqrt(mean(x^2) + eps))). The fp32 residual stream x_resid is
+ * kept packed: element (m, k) at the packed-activation offset above (fp32 elements), x_mbt token blocks, rows >= M
+ * zero. */
+/* Plan query: epilogue DRL_DECODE_RESID (ksplit: K slices of the residual producer, config: its k16 steps per wave),
+ * DRL_DECODE_SWIGLU (the gate_up consumer) or DRL_DECODE_ROPE (the qkv consumer; N = (Hq + 2 Hkv) D), config: the
+ * consumer's kernel configuration; mbt: the token blocks of every packed panel of the step. DRL_ERR_UNSUPPORTED when
+ * the shape takes the unfused path (more rows than the fused form's limit, K > 4096). */
+int drl_decode_norm_plan(int64_t M, int64_t N, int64_t K, int32_t epilogue, int32_t* ksplit, int32_t* mbt,
+                         int32_t* config);
+/* Tuning hook: force consumer configuration `config` (-1 = planner), the fused form's row limit (0 = 128) and the most
+ * K slices of the residual producer (0 = the partial-sum planner's choice; 1 = whole K where a shape allows). */
+void drl_decode_norm_set_plan(int32_t config, int32_t max_rows, int32_t resid_max_splits);
+/* Bytes of zeroed arrival counters drl_decode_gemm_resid needs (0 when the shape is not on the fused path). */
+size_t drl_decode_resid_counter_bytes(int64_t M, int64_t N, int64_t K);
+/* o_proj / down_proj of the fused-norm step: x_resid (packed fp32, x_mbt blocks, N columns) += bf16(x W^T) in place,
+ * the K slices summed in slice order by the slice that arrives last (no grid barrier). partials: ksplit x M x N fp32
+ * scratch; counters: drl_decode_resid_counter_bytes zero-filled bytes, left zeroed by every call. */
+int drl_decode_gemm_resid(const void* x_packed, const void* w_packed, int64_t M, int64_t N, int64_t K, float* x_resid,
+                          int64_t x_mbt, float* partials, void* counters, size_t counter_bytes, void* stream);
+/* gate_up + SwiGLU of the fused-norm step: y = RMSNorm(x_resid) with norm_weight (K fp32) computed per workgroup in
+ * the prologue, then drl_decode_gemm's SWIGLU epilogue (out packed, N/2 columns). */
+int drl_decode_gemm_norm(const float* x_resid, const float* norm_weight, float eps, const void* w_packed, int64_t M,
+                         int64_t N, int64_t K, void* out_packed, void* stream);
+/* qkv + bias + RoPE + cache writes of the fused-norm step: drl_decode_qkv_rope on RMSNorm(x_resid). */
+int drl_decode_qkv_rope_norm(const float* x_resid, const float* norm_weight, float eps, const void* w_packed,
+                             const void* bias, const int64_t* position_ids, const float* cos_t, const float* sin_t,
+                             int64_t maxpos, int64_t M, int64_t K, int64_t Hq, int64_t Hkv, int64_t D, void* q,
+                             void* k_cache, void* vt_cache, int64_t Tk, int64_t ld_vt, const int64_t* koff_dev,
+                             void* stream);
+/* The model's final norm of the fused-norm step (Qwen2Model.norm): y = bf16(w * x * rsqrt(mean(x^2) + eps)) from the
+ * packed residual, y packed (y_mbt blocks) or row-major (M, H) when y_mbt == 0. */
+int drl_decode_final_norm(const float* x_resid, int64_t x_mbt, const float* weight, void* y, int64_t M, int64_t H,
+                          int64_t y_mbt, float eps, void* stream);
 
 
 

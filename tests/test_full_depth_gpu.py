@@ -140,8 +140,9 @@ def test_bf16_full_depth_margin_checked(ref, weights, packed):
     print(f"bf16 {'packed' if packed else 'unpacked'} rollout: tokens matching the fp32 reference per row {matched}")
 
 
-@pytest.mark.parametrize("rows,group", [(4, 1), (512, 1), (512, 128)])
-def test_bf16_packed_decode_teacher_forced(ref, weights, rows, group):
+@pytest.mark.parametrize("rows,group,fused", [(4, 1, True), (512, 1, True), (512, 128, True), (64, 8, True),
+                                               (64, 8, False)])
+def test_bf16_packed_decode_teacher_forced(ref, weights, rows, group, fused):
     """The decode path the bench runs — prefill, then qwen2.PackedDecode's graphed step (decode_gemm.hip projections,
     decode_mfma_kernel attention, dec_rmsnorm, the step prologue) — fed the reference's own tokens (teacher forcing,
     hf_rollout.py:112-171 generate's inputs), so every step sees the reference context; its lm_head logits against
@@ -151,7 +152,10 @@ def test_bf16_packed_decode_teacher_forced(ref, weights, rows, group):
     group = 128: the bench's prompt groups (rollout.enable_prefix_caching) — each source row repeated 128 times in
     consecutive rows, its prompt prefilled once into cache row p and shared by the group (KVCache.share_prompts), so
     the decode attention is decode_group_kernel (csrc/flash_attn.hip: one workgroup per prompt, KV head and 4-row
-    column tile), the kernel the bench's rollout spends the most decode time in."""
+    column tile), the kernel the bench's rollout spends the most decode time in.
+    rows = 64, group = 8: the N = 8 rank's own decode (8 prompts x n = 8): the fused-norm five-launch layer
+    (decode_norm_gemm_kernel, the EPI_RESID producers, drl_decode_final_norm) and the per-row decode attention reading
+    the group's shared prompt keys (decode_mfma_kernel<64, 8>); fused = False the seven-launch layer at the same rows."""
     from dots.rl_amd.qwen2 import KVCache, KVCacheRows, PackedDecode
 
     z0, meta = ref
@@ -170,7 +174,7 @@ def test_bf16_packed_decode_teacher_forced(ref, weights, rows, group):
         cache = KVCache(model.cfg, B, P + R, ids.device, torch.bfloat16)
         cache.valid[:, :P] = am.to(torch.uint8)
         if group > 1:  # MI355XRollout.generate_sequences' prefix-caching prefill (rollout.py:104-109)
-            assert group == rep and P % 32 == 0
+            assert rep % group == 0 and P % 32 == 0
             Bu = B // group
             cache.valid[:Bu, :P] = am[::group].to(torch.uint8)
             h = model.prefill(KVCacheRows(cache, 0, Bu), ids[::group].contiguous(), am[::group].contiguous(),
@@ -181,7 +185,8 @@ def test_bf16_packed_decode_teacher_forced(ref, weights, rows, group):
         else:
             h = model.prefill(cache, ids, am, pos)
         logits = [model.logits(h).float()]
-        packed = PackedDecode(model, B)
+        packed = PackedDecode(model, B, fused_norm=fused)
+        assert packed.fused == (fused and B <= 128)
         t_dev = torch.ones(1, dtype=torch.int64, device=ids.device)
         last_pos = pos[:, -1].contiguous()
         out = torch.empty(B, model.cfg.vocab_size, device=ids.device)
