@@ -37,6 +37,14 @@ __device__ __forceinline__ int64_t pk_off(int64_t m, int64_t k, int64_t MBT) {
   return (((k >> 4) * MBT + (m >> 5)) * 64 + ((k >> 3) & 1) * 32 + (m & 31)) * 8 + (k & 7);
 }
 
+// packed fp32 residual (fused-norm step): the fragment of (32-row block, 16-deep k step) as two 1-KB halves, half j
+// holding k % 8 in [4j, 4j + 4) of every lane: element (m, k) at ((f * 2 + (k >> 2 & 1)) * 256 + lane * 4 + k % 4,
+// f = k/16 * MBT + m/32, lane = ((k/8) & 1) * 32 + m % 32 — each 16-B load of a fragment half is one coalesced 1-KB wave
+// read (a lane's 8 consecutive floats side by side would make every wave instruction span 2 KB)
+__host__ __device__ __forceinline__ int64_t pkf_off(int64_t m, int64_t k, int64_t MBT) {
+  return ((((k >> 4) * MBT + (m >> 5)) * 2 + ((k >> 2) & 1)) * 64 + ((k >> 3) & 1) * 32 + (m & 31)) * 4 + (k & 3);
+}
+
 // ------------------------------------------------------------------------------------------- packing
 // dst fragment (t, s, lane l): W row rowmap(t, l & 31), k = 16 s + 8 (l >> 5) .. + 7. SwiGLU packing
 // (half = I > 0): block t holds gate rows 16t..16t+15 then up rows I+16t..I+16t+15.
@@ -114,7 +122,7 @@ __device__ __forceinline__ float red_sum(const float (*red)[MB][16][64], int blk
 // lane half (i >> 2) & 1; column = token.
 template <int NW, int MB, int EPI>
 __device__ __forceinline__ void red_epilogue(const DgArgs& a, const float (*red)[MB][16][64], int tile, int ks, int mb0,
-                                             int tid) {
+                                             int tid, const float4* xres = nullptr) {
   constexpr int NT = 64 * NW;
   if constexpr (EPI == EPI_PARTIAL) {
     for (int e = tid; e < 1024 * MB; e += NT) {
@@ -194,7 +202,8 @@ __device__ __forceinline__ void red_epilogue(const DgArgs& a, const float (*red)
     int mm[MB], nn[MB];
 #pragma unroll
     for (int it = 0; it < MB; ++it) {
-      const int e = tid + 256 * it, tl = e >> 3, c = e & 7, blk = tl >> 5, ml = tl & 31;
+      // token fastest: 32 consecutive threads write one 512-B run of the packed residual, read consecutive LDS words
+      const int e = tid + 256 * it, ml = e & 31, c = (e >> 5) & 7, blk = it;
       mm[it] = (mb0 + blk) * 32 + ml;
       nn[it] = tile * 32 + 4 * c;
       const int ln = ml + 32 * (c & 1), q0 = 4 * (c >> 1);
@@ -232,10 +241,9 @@ __device__ __forceinline__ void red_epilogue(const DgArgs& a, const float (*red)
           d.x += p.x; d.y += p.y; d.z += p.z; d.w += p.w;
         }
       }
-      float4* xp = reinterpret_cast<float4*>(a.xr + pk_off(m, n, a.MBT));
-      float4 x = *xp;
+      float4 x = xres[it];  // loaded at the kernel's start (nobody else writes this tile's residual)
       x.x += bf16r(d.x); x.y += bf16r(d.y); x.z += bf16r(d.z); x.w += bf16r(d.w);
-      *xp = x;
+      *reinterpret_cast<float4*>(a.xr + pkf_off(m, n, a.MBT)) = x;
     }
   }
 }
@@ -255,6 +263,15 @@ __global__ __launch_bounds__(256) void decode_gemm_kernel(DgArgs a) {
 #pragma unroll
     for (int i = 0; i < MB; ++i)
       xv[s][i] = *reinterpret_cast<const u16x8*>(a.x + ((static_cast<int64_t>(s0 + s) * a.MBT + mb0 + i) * 64 + lane) * 8);
+  float4 xres[MB];
+  if constexpr (EPI == EPI_RESID) {  // the residual this thread may update, with the first loads (no later round trip)
+#pragma unroll
+    for (int it = 0; it < MB; ++it) {
+      const int e = tid + 256 * it, m = (mb0 + it) * 32 + (e & 31), n = tile * 32 + 4 * ((e >> 5) & 7);
+      xres[it] = m < a.M && n < a.N ? *reinterpret_cast<const float4*>(a.xr + pkf_off(m, n, a.MBT))
+                                    : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
   __builtin_amdgcn_sched_barrier(0);  // every load of the wave is in flight before the first MFMA
   f32x16 acc[MB];
 #pragma unroll
@@ -269,7 +286,7 @@ __global__ __launch_bounds__(256) void decode_gemm_kernel(DgArgs a) {
 #pragma unroll
     for (int q = 0; q < 16; ++q) red[wave][i][q][lane] = acc[i][q];
   __syncthreads();
-  red_epilogue<4, MB, EPI>(a, red, tile, ks, mb0, tid);
+  red_epilogue<4, MB, EPI>(a, red, tile, ks, mb0, tid, xres);
 }
 
 // The decode RMSNorm folded into its consumer GEMM's prologue (round 6; replaces the dec_rmsnorm launch before qkv +
@@ -307,9 +324,9 @@ __global__ __launch_bounds__(64 * NW) void decode_norm_gemm_kernel(DgArgs a) {
   for (int s = 0; s < KSW; ++s)
 #pragma unroll
     for (int i = 0; i < MB; ++i) {
-      const float* xp = a.xr + ((static_cast<int64_t>(s0 + s) * a.MBT + mb0 + i) * 64 + lane) * 8;
+      const float* xp = a.xr + (static_cast<int64_t>(s0 + s) * a.MBT + mb0 + i) * 512 + lane * 4;  // pkf_off
       xv[s][i][0] = *reinterpret_cast<const float4*>(xp);
-      xv[s][i][1] = *reinterpret_cast<const float4*>(xp + 4);
+      xv[s][i][1] = *reinterpret_cast<const float4*>(xp + 256);
     }
   __builtin_amdgcn_sched_barrier(0);  // every load in flight before the first use
 #pragma unroll
@@ -633,9 +650,9 @@ __global__ __launch_bounds__(128) void dec_rmsnorm_kernel(const float* x_in, con
     const int64_t ch = tid + 128 * c;
     if (ch < nch) {
       // XMBT > 0: x is the fused-norm decode's packed fp32 residual (8 consecutive columns contiguous)
-      const float* xr = XMBT > 0 ? x_in + pk_off(row, ch * 8, XMBT) : x_in + row * H + ch * 8;
+      const float* xr = XMBT > 0 ? x_in + pkf_off(row, ch * 8, XMBT) : x_in + row * H + ch * 8;
       xv[c][0] = *reinterpret_cast<const float4*>(xr);
-      xv[c][1] = *reinterpret_cast<const float4*>(xr + 4);
+      xv[c][1] = *reinterpret_cast<const float4*>(XMBT > 0 ? xr + 256 : xr + 4);
       // the norm weight with the row's first loads: no second memory round trip after the row sum
       wv[c][0] = *reinterpret_cast<const float4*>(w + ch * 8);
       wv[c][1] = *reinterpret_cast<const float4*>(w + ch * 8 + 4);
@@ -780,11 +797,11 @@ __global__ __launch_bounds__(128) void decode_prologue_kernel(const int64_t* res
   for (int64_t c = tid; c < H / 8; c += 128) {
     const u16x8 v = *reinterpret_cast<const u16x8*>(e + 8 * c);
     // x_mbt > 0: the fused-norm decode's packed fp32 residual stream
-    float* xr = x_mbt > 0 ? x + pk_off(b, 8 * c, x_mbt) : x + b * H + 8 * c;
+    float* xr = x_mbt > 0 ? x + pkf_off(b, 8 * c, x_mbt) : x + b * H + 8 * c;
     *reinterpret_cast<float4*>(xr) = make_float4(bf16_to_f32(v[0]), bf16_to_f32(v[1]), bf16_to_f32(v[2]),
                                                  bf16_to_f32(v[3]));
-    *reinterpret_cast<float4*>(xr + 4) = make_float4(bf16_to_f32(v[4]), bf16_to_f32(v[5]), bf16_to_f32(v[6]),
-                                                     bf16_to_f32(v[7]));
+    *reinterpret_cast<float4*>(x_mbt > 0 ? xr + 256 : xr + 4) =
+        make_float4(bf16_to_f32(v[4]), bf16_to_f32(v[5]), bf16_to_f32(v[6]), bf16_to_f32(v[7]));
   }
   if (tid == 0) {
     pos[b] = last_pos[b] + t;

@@ -1198,13 +1198,21 @@ def decode_final_norm(x_resid, x_mbt, weight, y, M, H, eps, y_mbt=0):
 
 
 def pack_residual(x, mbt, out=None):
-    """Row-major fp32 (M, H) -> the fused-norm step's packed residual (mbt token blocks; rows >= M zero)."""
+    """Row-major fp32 (M, H) -> the fused-norm step's packed residual (mbt token blocks; rows >= M zero): element
+    (m, k) at (((k//16 * mbt + m//32) * 2 + (k//4) % 2) * 64 + ((k//8) % 2) * 32 + m % 32) * 4 + k % 4."""
     M, H = x.shape
-    xp = pack_activations(x, mbt)
+    xp = torch.zeros(mbt * 32, H, dtype=x.dtype, device=x.device)
+    xp[:M] = x
+    # (m_blk, m_in, k16, k8, k4, e) -> (k16, m_blk, k4, k8, m_in, e)
+    xp = xp.view(mbt, 32, H // 16, 2, 2, 4).permute(2, 0, 4, 3, 1, 5).contiguous().view(-1)
     if out is None:
         return xp
     out.view(-1)[:xp.numel()].copy_(xp)
     return out
+
+
+def unpack_residual(xp, M, H, mbt):
+    return xp[:mbt * 32 * H].view(H // 16, mbt, 2, 2, 32, 4).permute(1, 4, 0, 3, 2, 5).reshape(mbt * 32, H)[:M]
 
 
 def decode_pack_weight_rope(w, head_dim, out=None):

@@ -1155,11 +1155,15 @@ class PackedDecode:
                         for n, k, sw in ((NQ, H, False), (H, cfg.num_attention_heads * D, False), (2 * I, H, True),
                                          (H, I, False))))
 
-    def __init__(self, model, B, weights=None, fused_norm=True):
+    def __init__(self, model, B, weights=None, fused_norm=False):
         """``weights``: another PackedDecode's packed weights (the layout does not depend on B), shared by the
         row lanes of one rollout instead of packed again. ``fused_norm``: the five-launch layer (the RMSNorms in the
         consumer GEMMs' prologue, the residual adds in the o_proj / down_proj epilogues) where the fused kernels take
-        the shape (1..128 rows at Qwen2.5-0.5B width); otherwise the seven-launch layer."""
+        the shape (1..128 rows at Qwen2.5-0.5B width); otherwise the seven-launch layer. Off by default: measured
+        slower (64 rows: 47.7 against 41.7 us per layer graph-replayed, profiles/r06_decode_fused_norm_sweep_rejected
+        .jsonl) — the gate_up consumer's workgroups each re-read the fp32 residual panel (twice the bytes of the packed
+        bf16 norm output they read otherwise), and the K-split down_proj's last-arriver combine costs more than the
+        norm launch it replaces."""
         cfg, s, dev = model.cfg, model.store, model.store.device
         self.model = model
         self.B = B

@@ -224,7 +224,7 @@ class MI355XRollout:
         if lanes > 1:
             return self._decode_graphed_lanes(cache, responses, last_pos, P, R, sel, lanes)
         use = self.config.get("packed_decode", True) and PackedDecode.supported(m, B, max_rows)
-        packed = PackedDecode(m, B, fused_norm=self.config.get("decode_fused_norm", True)) if use else None
+        packed = PackedDecode(m, B, fused_norm=self.config.get("decode_fused_norm", False)) if use else None
         self.last_packed_decode = packed is not None
 
         prologue = packed is not None and m.store.w("embed_tokens").dtype == torch.bfloat16 and \
@@ -281,7 +281,7 @@ class MI355XRollout:
         shared_w = None
         for j in range(lanes):
             r0, r1 = j * rows, (j + 1) * rows
-            pk = PackedDecode(m, rows, weights=shared_w, fused_norm=self.config.get("decode_fused_norm", True))
+            pk = PackedDecode(m, rows, weights=shared_w, fused_norm=self.config.get("decode_fused_norm", False))
             shared_w = pk.w
             sel_j = dict(sel, row_base=sel["row_base"] + r0, unfinished=sel["unfinished"][r0:r1])
             lane_state.append(dict(cache=KVCacheRows(cache, r0, r1), resp=responses[r0:r1], pk=pk, sel=sel_j,

@@ -67,17 +67,17 @@ def test_resid_equals_partials_then_rmsnorm_add(M, N, K, max_ks, norm_plan):
     first = None
     for rep in range(4):  # in place: each launch adds the same product again
         native.decode_gemm_resid(xp, wp, M, N, K, xr, mbt, partials, cnt)
-        got = native.unpack_activations(xr, M, N, mbt)
+        got = native.unpack_residual(xr, M, N, mbt)
         if rep == 0:
             first = got.clone()
             assert torch.equal(got, x_out)
         assert int(cnt.abs().sum()) == 0  # every launch leaves the arrival counters at zero
     # rows past M of the packed residual are never written
-    assert torch.count_nonzero(native.unpack_activations(xr, mbt * 32, N, mbt)[M:]) == 0
+    assert torch.count_nonzero(native.unpack_residual(xr, mbt * 32, N, mbt)[M:]) == 0
     # deterministic: the same start gives the same bits
     xr2 = native.pack_residual(res, mbt)
     native.decode_gemm_resid(xp, wp, M, N, K, xr2, mbt, partials, cnt)
-    assert torch.equal(native.unpack_activations(xr2, M, N, mbt), first)
+    assert torch.equal(native.unpack_residual(xr2, M, N, mbt), first)
 
 
 def _norm_ref(x, wn, eps):
@@ -164,7 +164,7 @@ def test_final_norm_from_packed_residual(M):
     H, eps = 896, 1e-6
     x = torch.randn(M, H, device=DEV)
     wn = torch.rand(H, device=DEV) + 0.5
-    mbt = max(1, (M + 31) // 32 + ((M + 31) // 32) % 2 * (M > 32))
+    mbt = native.decode_gemm_plan(M, H, H)[1]
     y0 = torch.empty(M, H, dtype=BF, device=DEV)
     native.decode_rmsnorm(x, None, None, wn, y0, eps, mbt=0)
     y1 = torch.empty(M, H, dtype=BF, device=DEV)
@@ -209,7 +209,7 @@ def test_fused_step_tracks_seven_launch_step(B, group):
         else:
             m.prefill(c, ids, am, pos)
         caches.append(c)
-    pf, pu = PackedDecode(m, B), PackedDecode(m, B, fused_norm=False)
+    pf, pu = PackedDecode(m, B, fused_norm=True), PackedDecode(m, B, fused_norm=False)
     assert pf.fused and not pu.fused
     toks = torch.randint(0, cfg.vocab_size, (B, R), device=DEV, generator=g)
     for t in range(1, R):
@@ -220,9 +220,10 @@ def test_fused_step_tracks_seven_launch_step(B, group):
         assert err < 3e-2, (t, err)
         assert (h0 - h1).abs().mean().item() < 3e-3 * h0.abs().mean().item() + 1e-6, t
     nn = P + R - 1
-    for i in range(cfg.num_hidden_layers):
-        for a, b in ((caches[0].k[i][:, :, :nn], caches[1].k[i][:, :, :nn]),
-                     (caches[0].vt_plain(i)[..., :nn], caches[1].vt_plain(i)[..., :nn])):
+    for i in range(cfg.num_hidden_layers):  # the response slots the steps wrote (prompt rows past a group's first
+        # cache row are never written under prefix caching)
+        for a, b in ((caches[0].k[i][:, :, P:nn], caches[1].k[i][:, :, P:nn]),
+                     (caches[0].vt_plain(i)[..., P:nn], caches[1].vt_plain(i)[..., P:nn])):
             assert (a.float() - b.float()).abs().max().item() <= 3e-2 * a.float().abs().max().item()
 
 
@@ -241,7 +242,8 @@ def test_fused_rollout_graph_equals_eager():
     am = torch.ones(B, P, dtype=torch.int64, device=DEV)
     pos = (am.cumsum(-1) - 1).clamp_min(0)
     rcfg = to_attr(dict(do_sample=False, temperature=1.0, top_k=-1, top_p=1.0, response_length=R, ignore_eos=True,
-                        seed=0, val_kwargs={}, use_hip_graph=True, packed_decode=True, n=group))
+                        seed=0, val_kwargs={}, use_hip_graph=True, packed_decode=True, n=group,
+                        decode_fused_norm=True))
     ro = MI355XRollout(m, rcfg)
     out = ro.generate_sequences(DataProto.from_dict({"input_ids": ids, "attention_mask": am, "position_ids": pos},
                                                     meta_info={"eos_token_id": 2, "pad_token_id": 0}))
@@ -252,7 +254,7 @@ def test_fused_rollout_graph_equals_eager():
     h = m.prefill(KVCacheRows(cache, 0, B // group), ids[::group].contiguous(), am[::group].contiguous(),
                   pos[::group].contiguous()).repeat_interleave(group, 0)
     cache.share_prompts(group, P)
-    pk = PackedDecode(m, B)
+    pk = PackedDecode(m, B, fused_norm=True)
     assert pk.fused
 
     def pick(h):
