@@ -182,7 +182,7 @@ SIGNATURES = {
     "drl_decode_pack_weight_elems": (SZ, [I64, I64, I32]),
     "drl_decode_pack_weight": (ctypes.c_int, [P, I64, I64, I64, I32, P, P]),
     "drl_decode_gemm": (ctypes.c_int, [P, P, I64, I64, I64, I32, P, P, P]),
-    "drl_decode_rmsnorm": (ctypes.c_int, [P, P, I32, P, P, P, I64, I64, I64, F32, P]),
+    "drl_decode_rmsnorm": (ctypes.c_int, [P, P, I32, P, P, P, I64, I64, I64, F32, P, I64, P]),
     "drl_decode_pack_weight_rope": (ctypes.c_int, [P, I64, I64, I64, I64, P, P]),
     "drl_decode_qkv_rope": (ctypes.c_int, [P, P, P, P, P, P, I64, I64, I64, I64, I64, I64, P, P, P, I64, I64, P, P]),
     "drl_decode_rope": (ctypes.c_int, [P, I32, P, P, P, P, I64, I64, I64, I64, I64, P, P, P, P, I64, I64, I64, P, P]),
@@ -193,7 +193,9 @@ SIGNATURES = {
     "drl_decode_gemm_norm": (ctypes.c_int, [P, P, F32, P, I64, I64, I64, P, P]),
     "drl_decode_qkv_rope_norm": (ctypes.c_int, [P, P, F32, P, P, P, P, P, I64, I64, I64, I64, I64, I64, P, P, P, I64,
                                                 I64, P, P]),
-    "drl_decode_final_norm": (ctypes.c_int, [P, I64, P, P, I64, I64, I64, F32, P]),
+    "drl_decode_final_norm": (ctypes.c_int, [P, I64, P, P, I64, I64, I64, F32, P, I64, P]),
+    "drl_decode_lm_head_plan": (ctypes.c_int, [I64, I64, I64, P]),
+    "drl_decode_lm_head": (ctypes.c_int, [P, I64, P, I64, I64, I64, P, I64, P]),
     "drl_linear_logprob_fwd": (ctypes.c_int, [P, I64, P, P, I32, I64, I64, I64, F32, P, P, P, P, SZ, P]),
     "drl_linear_logprob_dlogits": (ctypes.c_int, [P, I64, P, P, I32, I64, I64, I64, F32, P, P, P, P, P, I64, P]),
 }

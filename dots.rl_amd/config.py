@@ -104,6 +104,7 @@ DEFAULTS = dict(
             seed=1234, val_kwargs=dict(top_k=-1, top_p=1.0, temperature=0, n=1, do_sample=False),
             use_hip_graph=True,  # decode steps replayed from one captured HIP graph (rollout.py)
             packed_decode=True, packed_decode_max_rows=512,  # qwen2.PackedDecode (fragment-packed operands)
+            decode_lm_head=True,  # PackedDecode's lm_head kernel at <= 64 rows (csrc/decode_gemm.hip)
             decode_fused_norm=False,  # PackedDecode's five-launch layer (norms in the consumer GEMMs): measured slower
             fused_select=False,  # lm_head fused with K4 (csrc/fused_linear.hip)
             decode_lanes=1,  # row groups of the graphed decode step on concurrent streams (rollout._decode_lanes)

@@ -637,7 +637,8 @@ __global__ __launch_bounds__(64 * WR * WT) void decode_gemm_lds_kernel(DgArgs a)
 template <int CH, int NS>
 __global__ __launch_bounds__(128) void dec_rmsnorm_kernel(const float* x_in, const float* part, int nsplit, float* x_out,
                                                           const float* w, uint16_t* y, int64_t M, int64_t H, int64_t MBT,
-                                                          float eps, int64_t XMBT = 0) {
+                                                          float eps, int64_t XMBT = 0, uint16_t* y2 = nullptr,
+                                                          int64_t MBT2 = 0) {
   __shared__ float s_ss[2];
   const int64_t row = blockIdx.x;
   const int tid = threadIdx.x;
@@ -712,8 +713,12 @@ __global__ __launch_bounds__(128) void dec_rmsnorm_kernel(const float* x_in, con
     u16x8 o;
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = f32_to_bf16(wj[j] * (v[c][j] * r));
-    uint16_t* dst = MBT > 0 ? y + pk_off(row, ch * 8, MBT) : y + row * H + ch * 8;
-    *reinterpret_cast<u16x8*>(dst) = o;
+    if (y) {
+      uint16_t* dst = MBT > 0 ? y + pk_off(row, ch * 8, MBT) : y + row * H + ch * 8;
+      *reinterpret_cast<u16x8*>(dst) = o;
+    }
+    // the packed copy the decode lm_head reads (y2, MBT2 blocks), beside a row-major y
+    if (y2) *reinterpret_cast<u16x8*>(y2 + pk_off(row, ch * 8, MBT2)) = o;
   }
 }
 
@@ -812,6 +817,124 @@ __global__ __launch_bounds__(128) void decode_prologue_kernel(const int64_t* res
     *t_cur = t;
     *t_dev = t + 1;
     __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// ------------------------------------------------------------------------------------------- lm_head (<= 64 rows)
+// The decode step's lm_head at <= 64 token rows (the N = 8 rank's 64): logits = h W^T, a 272 MB weight stream for
+// 17 GFLOP — drl_gemm's 256 x 256 tiles over M = 64 ran it at 3.9 TB/s (594 tiles of 7 k-pairs never fill its
+// pipeline). Persistent: one workgroup per CU holds the packed bf16 activation panel (MB token blocks x NKS k16
+// steps, 112 KB at 64 rows x 896) in LDS for the whole launch, and owns a contiguous, balanced range of 32-row vocab
+// tiles. The packed weight of that range is one contiguous stream; its k16 steps are split evenly over the NWV waves
+// (stream-K inside the workgroup), each wave pulling its share through a DEPTH-deep register ring of 1-KB fragment
+// loads and running MB MFMAs per step against LDS fragments. A tile a wave finishes from k = 0 is written straight from
+// its accumulators (bf16, the drl_gemm epilogue's rounding); a tile split between two waves is summed once, after the
+// workgroup barrier, as (first wave's k prefix) + (second wave's suffix) — fixed order, deterministic. No workgroup
+// waits on another.
+struct LmArgs {
+  const uint16_t* h;  // packed bf16 panel (MB token blocks, NKS k16 steps)
+  const uint16_t* w;  // packed weight: tiles of 32 vocab rows x NKS k16 steps
+  uint16_t* out;      // logits (M, ld) bf16
+  int64_t ld;
+  int M, V, tiles;
+};
+
+template <int MB, int NKS, int NWV, int DEPTH>
+__global__ __launch_bounds__(64 * NWV) void decode_lm_head_kernel(LmArgs a) {
+  static_assert(MB * NKS * 512 * 2 >= NWV * MB * 16 * 64 * 4, "split-tile slots reuse the panel's LDS");
+  __shared__ __attribute__((aligned(16))) uint16_t s_x[MB * NKS * 512];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int G = gridDim.x, g = blockIdx.x;
+  const int t0 = static_cast<int>(static_cast<int64_t>(g) * a.tiles / G);
+  const int t1 = static_cast<int>(static_cast<int64_t>(g + 1) * a.tiles / G);
+  const int n_it = (t1 - t0) * NKS;
+  const int i0 = wave * n_it / NWV, i1 = (wave + 1) * n_it / NWV;  // the host keeps i1 - i0 >= NKS
+  const uint16_t* wp = a.w + static_cast<int64_t>(t0) * NKS * 512 + lane * 8;
+  u16x8 ring[DEPTH];
+#pragma unroll
+  for (int d = 0; d < DEPTH; ++d)
+    ring[d] = __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(wp + static_cast<int64_t>(min(i0 + d, i1 - 1)) * 512));
+  // the activation panel -> LDS by LDS-DMA (lane-linear 1-KB fragments: the panel's own layout)
+  for (int f = wave; f < MB * NKS; f += NWV)
+    __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(a.h + f * 512 + lane * 8),
+                                     (__attribute__((address_space(3))) void*)(s_x + f * 512), 16, 0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  f32x16 acc[MB], head[MB];
+#pragma unroll
+  for (int m = 0; m < MB; ++m) acc[m] = head[m] = f32x16{};
+  int ks = i0 % NKS, tile = t0 + i0 / NKS;
+  bool in_head = ks != 0, has_head = false;  // this wave's first tile started mid-way: its k = 0 part is the
+                                             // previous wave's tail
+  const int hh = lane >> 5, ml = lane & 31;
+  auto store_tile = [&](int t, const f32x16 (&c)[MB]) {
+#pragma unroll
+    for (int m = 0; m < MB; ++m) {
+      const int row = 32 * m + ml;
+      if (row >= a.M) continue;
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4) {
+        const int n = t * 32 + 8 * q4 + 4 * hh;  // registers 4 q4 .. + 3: vocab rows n .. n + 3
+        uint16_t* dst = a.out + static_cast<int64_t>(row) * a.ld + n;
+        if (n + 3 < a.V) {
+          *reinterpret_cast<u16x4*>(dst) = u16x4{to_bf16_bits(c[m][4 * q4]), to_bf16_bits(c[m][4 * q4 + 1]),
+                                                 to_bf16_bits(c[m][4 * q4 + 2]), to_bf16_bits(c[m][4 * q4 + 3])};
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (n + j < a.V) dst[j] = to_bf16_bits(c[m][4 * q4 + j]);
+        }
+      }
+    }
+  };
+  for (int base = i0; base < i1; base += DEPTH) {
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d) {
+      const int i = base + d;
+      if (i < i1) {
+#pragma unroll
+        for (int m = 0; m < MB; ++m) {
+          const u16x8 xf = *reinterpret_cast<const u16x8*>(s_x + (ks * MB + m) * 512 + lane * 8);
+          acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(ring[d]), as_bf16x8(xf), acc[m], 0, 0, 0);
+        }
+        ring[d] = __builtin_nontemporal_load(
+            reinterpret_cast<const u16x8*>(wp + static_cast<int64_t>(min(i + DEPTH, i1 - 1)) * 512));
+        if (++ks == NKS) {  // a tile's last k16 step
+          if (in_head) {
+#pragma unroll
+            for (int m = 0; m < MB; ++m) head[m] = acc[m];
+            in_head = false;
+            has_head = true;
+          } else {
+            store_tile(tile, acc);
+          }
+#pragma unroll
+          for (int m = 0; m < MB; ++m) acc[m] = f32x16{};
+          ks = 0;
+          ++tile;
+        }
+      }
+      // keep the refill here (decode_gemm_tiled_kernel: otherwise hipcc sinks each load next to its use)
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  // split tiles: every wave's head partial into LDS (the panel is no longer read), then each tail adds the next
+  // wave's head — the tile's k prefix + its suffix
+  __syncthreads();
+  float* slots = reinterpret_cast<float*>(s_x);
+  if (has_head) {
+#pragma unroll
+    for (int m = 0; m < MB; ++m)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) slots[((wave * MB + m) * 16 + q) * 64 + lane] = head[m][q];
+  }
+  __syncthreads();
+  if (ks != 0) {
+#pragma unroll
+    for (int m = 0; m < MB; ++m)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[m][q] += slots[(((wave + 1) * MB + m) * 16 + q) * 64 + lane];
+    store_tile(tile, acc);
   }
 }
 
@@ -1221,19 +1344,21 @@ int drl_decode_qkv_rope_norm(const float* x_resid, const float* norm_weight, flo
 }
 
 int drl_decode_final_norm(const float* x_resid, int64_t x_mbt, const float* weight, void* y, int64_t M, int64_t H,
-                          int64_t y_mbt, float eps, void* stream) {
+                          int64_t y_mbt, float eps, void* y_packed, int64_t packed_mbt, void* stream) {
   using namespace drl;
-  DRL_CHECK_ARG(x_resid && weight && y, "NULL input");
+  DRL_CHECK_ARG(x_resid && weight && (y || y_packed), "NULL input");
+  DRL_CHECK_ARG(!y_packed || (packed_mbt >= 1 && packed_mbt * 32 >= M && aligned16(y_packed)), "packed output");
   DRL_CHECK_ARG(M >= 1 && H >= 8 && H % 8 == 0 && H <= 8 * 128 * 4, "bad shape (H %% 8 == 0, H <= 4096)");
   DRL_CHECK_ARG(x_mbt >= 1 && x_mbt * 32 >= M && (y_mbt == 0 || y_mbt * 32 >= M), "token blocks too few");
-  DRL_CHECK_ARG(aligned16(x_resid) && aligned16(y) && aligned16(weight), "16-byte aligned buffers needed");
+  DRL_CHECK_ARG(aligned16(x_resid) && (!y || aligned16(y)) && aligned16(weight), "16-byte aligned buffers needed");
   const int ch = static_cast<int>((H / 8 + 127) / 128);
   hipStream_t s = static_cast<hipStream_t>(stream);
   const dim3 grid(static_cast<unsigned>(M));
   uint16_t* yy = static_cast<uint16_t*>(y);
-  if (ch <= 1) hipLaunchKernelGGL((dec_rmsnorm_kernel<1, 0>), grid, dim3(128), 0, s, x_resid, nullptr, 0, nullptr, weight, yy, M, H, y_mbt, eps, x_mbt);
-  else if (ch == 2) hipLaunchKernelGGL((dec_rmsnorm_kernel<2, 0>), grid, dim3(128), 0, s, x_resid, nullptr, 0, nullptr, weight, yy, M, H, y_mbt, eps, x_mbt);
-  else hipLaunchKernelGGL((dec_rmsnorm_kernel<4, 0>), grid, dim3(128), 0, s, x_resid, nullptr, 0, nullptr, weight, yy, M, H, y_mbt, eps, x_mbt);
+  uint16_t* y2 = static_cast<uint16_t*>(y_packed);
+  if (ch <= 1) hipLaunchKernelGGL((dec_rmsnorm_kernel<1, 0>), grid, dim3(128), 0, s, x_resid, nullptr, 0, nullptr, weight, yy, M, H, y_mbt, eps, x_mbt, y2, packed_mbt);
+  else if (ch == 2) hipLaunchKernelGGL((dec_rmsnorm_kernel<2, 0>), grid, dim3(128), 0, s, x_resid, nullptr, 0, nullptr, weight, yy, M, H, y_mbt, eps, x_mbt, y2, packed_mbt);
+  else hipLaunchKernelGGL((dec_rmsnorm_kernel<4, 0>), grid, dim3(128), 0, s, x_resid, nullptr, 0, nullptr, weight, yy, M, H, y_mbt, eps, x_mbt, y2, packed_mbt);
   DRL_LAUNCH_CHECK();
   return DRL_OK;
 }
@@ -1378,9 +1503,11 @@ int drl_decode_qkv_rope(const void* x_packed, const void* w_packed, const void* 
 }
 
 int drl_decode_rmsnorm(const float* x_in, const float* partials, int32_t nsplit, float* x_out, const float* weight,
-                       void* y, int64_t M, int64_t H, int64_t mbt, float eps, void* stream) {
+                       void* y, int64_t M, int64_t H, int64_t mbt, float eps, void* y_packed, int64_t packed_mbt,
+                       void* stream) {
   using namespace drl;
   DRL_CHECK_ARG(x_in && weight && y, "NULL input");
+  DRL_CHECK_ARG(!y_packed || (packed_mbt >= 1 && packed_mbt * 32 >= M && aligned16(y_packed)), "packed output");
   DRL_CHECK_ARG(M >= 1 && H >= 8 && H % 8 == 0 && H <= 8 * 128 * 4, "bad shape (H %% 8 == 0, H <= 4096)");
   DRL_CHECK_ARG(partials == nullptr || nsplit >= 1, "nsplit < 1");
   DRL_CHECK_ARG(mbt == 0 || mbt * 32 >= M, "mbt too small");
@@ -1392,7 +1519,8 @@ int drl_decode_rmsnorm(const float* x_in, const float* partials, int32_t nsplit,
   hipStream_t s = static_cast<hipStream_t>(stream);
   const dim3 grid(static_cast<unsigned>(M));
 #define DRL_DRN(C, NS) hipLaunchKernelGGL((dec_rmsnorm_kernel<C, NS>), grid, dim3(128), 0, s, x_in, partials, ns, x_out, \
-                                          weight, static_cast<uint16_t*>(y), M, H, mbt, eps)
+                                          weight, static_cast<uint16_t*>(y), M, H, mbt, eps, int64_t(0),           \
+                                          static_cast<uint16_t*>(y_packed), packed_mbt)
 #define DRL_DRN_NS(C)                \
   switch (ns) {                      \
     case 0: DRL_DRN(C, 0); break;    \
@@ -1431,6 +1559,41 @@ int drl_decode_rope(const float* partials, int32_t nsplit, const void* bias, con
   const int64_t n = B * (Hq + 2 * Hkv) * (D / 2);
   hipLaunchKernelGGL(dec_rope_kernel, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0,
                      static_cast<hipStream_t>(stream), a);
+  DRL_LAUNCH_CHECK();
+  return DRL_OK;
+}
+
+int drl_decode_lm_head_plan(int64_t M, int64_t V, int64_t K, int32_t* mbt) {
+  using namespace drl;
+  const int cus = cu_count();
+  const int64_t tiles = (V + 31) / 32;
+  // 64 rows at most (the panel in LDS), K = 896 (the instantiated panel width), enough vocab tiles that every wave
+  // of every workgroup owns at least one whole tile's k16 steps
+  if (M < 1 || M > 64 || K != 896 || V < 32 || cus <= 0 || tiles < 8 * 8)
+    return fail(DRL_ERR_UNSUPPORTED, "decode lm_head: unsupported shape M=%lld V=%lld K=%lld", (long long)M,
+                (long long)V, (long long)K);
+  if (mbt) *mbt = M > 32 ? 2 : 1;
+  return DRL_OK;
+}
+
+int drl_decode_lm_head(const void* h_packed, int64_t mbt, const void* w_packed, int64_t M, int64_t V, int64_t K,
+                       void* logits, int64_t ld, void* stream) {
+  using namespace drl;
+  DRL_CHECK_ARG(h_packed && w_packed && logits, "NULL input");
+  int32_t want = 0;
+  if (const int rc = drl_decode_lm_head_plan(M, V, K, &want); rc != DRL_OK) return rc;
+  DRL_CHECK_ARG(mbt == want, "h_packed must hold %d token blocks", want);
+  DRL_CHECK_ARG(aligned16(h_packed) && aligned16(w_packed) && (reinterpret_cast<uintptr_t>(logits) & 7u) == 0 &&
+                    ld >= V && ld % 4 == 0,
+                "alignment: packed operands 16 B, logits 8 B with ld %% 4 == 0");
+  LmArgs a{static_cast<const uint16_t*>(h_packed), static_cast<const uint16_t*>(w_packed),
+           static_cast<uint16_t*>(logits), ld, static_cast<int>(M), static_cast<int>(V), static_cast<int>((V + 31) / 32)};
+  constexpr int NWV = 8, DEPTH = 16;
+  // workgroups: one per CU while each of the NWV waves keeps >= one whole tile of k16 steps
+  const int grid = static_cast<int>(std::min<int64_t>(cu_count(), a.tiles / NWV));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (mbt == 1) hipLaunchKernelGGL((decode_lm_head_kernel<1, 56, NWV, DEPTH>), dim3(grid), dim3(64 * NWV), 0, s, a);
+  else hipLaunchKernelGGL((decode_lm_head_kernel<2, 56, NWV, DEPTH>), dim3(grid), dim3(64 * NWV), 0, s, a);
   DRL_LAUNCH_CHECK();
   return DRL_OK;
 }

@@ -1123,13 +1123,14 @@ def decode_gemm(x_packed, w_packed, M, N, K, swiglu=False, partials=None, out_pa
     return out_packed if swiglu else partials
 
 
-def decode_rmsnorm(x_in, partials, x_out, weight, y, eps, mbt=0):
-    """x_out = x_in + bf16(sum partials); y = RMSNorm(x_out) * w in bf16, packed (mbt > 0) or row-major."""
-    _dev(x_in, weight, y)
+def decode_rmsnorm(x_in, partials, x_out, weight, y, eps, mbt=0, y_packed=None, packed_mbt=0):
+    """x_out = x_in + bf16(sum partials); y = RMSNorm(x_out) * w in bf16, packed (mbt > 0) or row-major; with
+    ``y_packed`` also written packed (packed_mbt blocks: the decode lm_head's operand)."""
+    _dev(x_in, weight, y, y_packed)
     M, H = x_in.shape[0], x_in.shape[-1]
     ns = partials.shape[0] if partials is not None else 0
     check(lib().drl_decode_rmsnorm(_p(x_in), _p(partials), ns, _p(x_out), _p(weight), _p(y), M, H, int(mbt),
-                                   float(eps), _stream()), "drl_decode_rmsnorm")
+                                   float(eps), _p(y_packed), int(packed_mbt), _stream()), "drl_decode_rmsnorm")
 
 
 def decode_rope(partials, bias, position_ids, cos_t, sin_t, Hq, Hkv, D, q, k_cache, vt_cache=None, v_cache=None,
@@ -1189,12 +1190,28 @@ def decode_qkv_rope_norm(x_resid, norm_weight, eps, w_packed, bias, position_ids
                                          _stream()), "drl_decode_qkv_rope_norm")
 
 
-def decode_final_norm(x_resid, x_mbt, weight, y, M, H, eps, y_mbt=0):
-    """The model's final RMSNorm from the packed fp32 residual: y bf16 row-major (M, H) or packed (y_mbt > 0)."""
-    _dev(x_resid, weight, y)
+def decode_final_norm(x_resid, x_mbt, weight, y, M, H, eps, y_mbt=0, y_packed=None, packed_mbt=0):
+    """The model's final RMSNorm from the packed fp32 residual: y bf16 row-major (M, H) or packed (y_mbt > 0), and
+    optionally a second packed copy (y_packed, packed_mbt blocks)."""
+    _dev(x_resid, weight, y, y_packed)
     check(lib().drl_decode_final_norm(_p(x_resid), int(x_mbt), _p(weight), _p(y), M, H, int(y_mbt), float(eps),
-                                      _stream()), "drl_decode_final_norm")
+                                      _p(y_packed), int(packed_mbt), _stream()), "drl_decode_final_norm")
     return y
+
+
+def decode_lm_head_plan(M, V, K):
+    """Token blocks of the decode lm_head's packed operand, or None when the shape takes drl_gemm."""
+    mbt = ctypes.c_int32(0)
+    return mbt.value if lib().drl_decode_lm_head_plan(M, V, K, ctypes.byref(mbt)) == 0 else None
+
+
+def decode_lm_head(h_packed, mbt, w_packed, M, V, K, out):
+    """logits (M, V) bf16 = h W^T at <= 64 decode rows from the packed final-norm output (persistent kernel)."""
+    _dev(h_packed, w_packed, out)
+    assert out.dtype == torch.bfloat16 and out.stride(1) == 1 and out.shape == (M, V)
+    check(lib().drl_decode_lm_head(_p(h_packed), int(mbt), _p(w_packed), M, V, K, _p(out), out.stride(0), _stream()),
+          "drl_decode_lm_head")
+    return out
 
 
 def pack_residual(x, mbt, out=None):

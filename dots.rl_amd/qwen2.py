@@ -1040,17 +1040,19 @@ class Qwen2Model:
             return _Linear.apply(h, self.store.w(name), self.store.g(name), self._dummy)
         return linear(h.reshape(-1, h.shape[-1]), self.store.w(name)).view(*h.shape[:-1], -1)
 
-    def select_tokens(self, h, out_tokens, fused=True, logprob_out=None, logprob_temperature=1.0, **sel):
+    def select_tokens(self, h, out_tokens, fused=True, logprob_out=None, logprob_temperature=1.0, logits_fn=None,
+                      **sel):
         """Token selection from the final-norm hidden h (N, H): K4 fused with the lm_head on bf16 (the (N, V)
         logits are never written, csrc/fused_linear.hip), else lm_head logits + K4 (fp32 parity model, and
         sampling: the slice race and the top-k / top-p cut read the logits row). With ``logprob_out`` (the
         rollout's calculate_log_probs) the selected token's log p under logits / ``logprob_temperature`` is written
-        to the same column of it (native.token_logprob, one more pass over the logits rows)."""
+        to the same column of it (native.token_logprob, one more pass over the logits rows). ``logits_fn``: the
+        decode step's own lm_head (PackedDecode.logits) in place of self.logits."""
         w = self.store.w(self.lm_head_weight())
         if logprob_out is None and fused and not sel.get("do_sample") and self.dtype == torch.bfloat16 and \
-                h.shape[-1] % 64 == 0:
+                h.shape[-1] % 64 == 0 and logits_fn is None:
             return native.linear_select_tokens(h.contiguous(), w, out_tokens, **sel)
-        logits = self.logits(h)
+        logits = logits_fn(h) if logits_fn is not None else self.logits(h)
         native.select_tokens(logits, out_tokens, **sel)
         if logprob_out is not None:
             native.token_logprob(logits, out_tokens, logprob_out, logprob_temperature, dev_step=sel.get("dev_step"))
@@ -1155,7 +1157,7 @@ class PackedDecode:
                         for n, k, sw in ((NQ, H, False), (H, cfg.num_attention_heads * D, False), (2 * I, H, True),
                                          (H, I, False))))
 
-    def __init__(self, model, B, weights=None, fused_norm=False):
+    def __init__(self, model, B, weights=None, fused_norm=False, lm_head=True):
         """``weights``: another PackedDecode's packed weights (the layout does not depend on B), shared by the
         row lanes of one rollout instead of packed again. ``fused_norm``: the five-launch layer (the RMSNorms in the
         consumer GEMMs' prologue, the residual adds in the o_proj / down_proj epilogues) where the fused kernels take
@@ -1213,6 +1215,15 @@ class PackedDecode:
             self.x = torch.empty(B, H, device=dev)                         # fp32 residual stream
         self.q = torch.empty(B, Hkv, Hq // Hkv, D, dtype=bf, device=dev)
         self.h_out = torch.empty(B, H, dtype=bf, device=dev)
+        # the decode lm_head at <= 64 rows (csrc/decode_gemm.hip decode_lm_head_kernel: the packed h panel in LDS, the
+        # packed weight streamed once per token); the final norm also writes h packed for it
+        V = cfg.vocab_size
+        self.lm_mbt = native.decode_lm_head_plan(B, V, H) if lm_head else None
+        self.lm_w = None
+        if self.lm_mbt is not None:
+            self.lm_w = native.decode_pack_weight(s.w(model.lm_head_weight()))
+            self.h_pk = torch.zeros(self.lm_mbt * 32 * H, dtype=bf, device=dev)
+            self.logits_buf = torch.empty(B, V, dtype=bf, device=dev)
         self.pos = torch.empty(B, dtype=torch.int64, device=dev)   # step_from: rotary positions of the new token
         self.kpos = torch.empty(1, dtype=torch.int64, device=dev)  # step_from: its cache slot
         self.t_cur = torch.empty(1, dtype=torch.int64, device=dev)  # step_from: the step's t (Philox offset / column)
@@ -1263,7 +1274,9 @@ class PackedDecode:
                 native.decode_gemm_norm(self.xr, s.w(p + "post_attention_layernorm"), eps, w["gu"], B, 2 * I, H,
                                         self.a_p)
                 native.decode_gemm_resid(self.a_p, w["d"], B, H, I, self.xr, mbt, self.part_d, self.cnt)
-            native.decode_final_norm(self.xr, mbt, s.w("norm"), self.h_out, B, H, eps)
+            native.decode_final_norm(self.xr, mbt, s.w("norm"), self.h_out, B, H, eps,
+                                     y_packed=self.h_pk if self.lm_w is not None else None,
+                                     packed_mbt=self.lm_mbt or 0)
             return self.h_out
         prev = None
         for i in range(cfg.num_hidden_layers):
@@ -1279,8 +1292,18 @@ class PackedDecode:
             native.decode_gemm(self.h_p, w["gu"], B, 2 * I, H, swiglu=True, out_packed=self.a_p)
             native.decode_gemm(self.a_p, w["d"], B, H, I, partials=self.part_d)
             prev = self.part_d
-        native.decode_rmsnorm(self.x, prev, None, s.w("norm"), self.h_out, eps, mbt=0)
+        native.decode_rmsnorm(self.x, prev, None, s.w("norm"), self.h_out, eps, mbt=0,
+                              y_packed=self.h_pk if self.lm_w is not None else None, packed_mbt=self.lm_mbt or 0)
         return self.h_out
+
+    def logits(self, h):
+        """lm_head logits (B, V) bf16 of this step's final-norm output (h is self.h_out): the decode lm_head kernel
+        at <= 64 rows, the model's drl_gemm lm_head otherwise."""
+        if self.lm_w is not None and h is self.h_out:
+            cfg = self.model.cfg
+            return native.decode_lm_head(self.h_pk, self.lm_mbt, self.lm_w, self.B, cfg.vocab_size, cfg.hidden_size,
+                                         self.logits_buf)
+        return self.model.logits(h)
 
 
 def flops_per_token(cfg: Qwen2Config, seqlen: int) -> float:

@@ -224,18 +224,21 @@ class MI355XRollout:
         if lanes > 1:
             return self._decode_graphed_lanes(cache, responses, last_pos, P, R, sel, lanes)
         use = self.config.get("packed_decode", True) and PackedDecode.supported(m, B, max_rows)
-        packed = PackedDecode(m, B, fused_norm=self.config.get("decode_fused_norm", False)) if use else None
+        packed = PackedDecode(m, B, fused_norm=self.config.get("decode_fused_norm", False),
+                              lm_head=self.config.get("decode_lm_head", True)) if use else None
         self.last_packed_decode = packed is not None
 
         prologue = packed is not None and m.store.w("embed_tokens").dtype == torch.bfloat16 and \
             self.config.get("decode_prologue", True)
         last_pos_flat = last_pos.reshape(-1).contiguous()
 
+        lfn = packed.logits if packed is not None else None
+
         def body():
             if prologue:  # one launch: embedding, positions, cache slot, key_valid, t_cur, t_dev += 1
                 h = packed.step_from(cache, responses, t_dev, last_pos_flat, P)
                 m.select_tokens(h, responses[:, 0], fused=self._fused_select, step=0, dev_step=packed.t_cur,
-                                **self._lp_col(rollout_lp, 0), **sel)
+                                logits_fn=lfn, **self._lp_col(rollout_lp, 0), **sel)
                 return
             tok = responses.index_select(1, t_dev - 1)
             if packed is not None:
@@ -243,7 +246,7 @@ class MI355XRollout:
             else:
                 h = m.decode_step_dev(cache, tok, last_pos + t_dev, t_dev + (P - 1))
             m.select_tokens(h, responses[:, 0], fused=self._fused_select, step=0, dev_step=t_dev,
-                            **self._lp_col(rollout_lp, 0), **sel)
+                            logits_fn=lfn if packed is not None else None, **self._lp_col(rollout_lp, 0), **sel)
             t_dev.add_(1)
 
         body()  # t = 1, eager
@@ -281,7 +284,8 @@ class MI355XRollout:
         shared_w = None
         for j in range(lanes):
             r0, r1 = j * rows, (j + 1) * rows
-            pk = PackedDecode(m, rows, weights=shared_w, fused_norm=self.config.get("decode_fused_norm", False))
+            pk = PackedDecode(m, rows, weights=shared_w, fused_norm=self.config.get("decode_fused_norm", False),
+                              lm_head=False)
             shared_w = pk.w
             sel_j = dict(sel, row_base=sel["row_base"] + r0, unfinished=sel["unfinished"][r0:r1])
             lane_state.append(dict(cache=KVCacheRows(cache, r0, r1), resp=responses[r0:r1], pk=pk, sel=sel_j,

@@ -583,9 +583,11 @@ int drl_decode_qkv_rope(const void* x_packed, const void* w_packed, const void* 
                         const int64_t* koff_dev, void* stream);
 /* x_out = x_in + bf16(sum of nsplit partials (nsplit, M, H)) (partials may be NULL: no delta), y = bf16(w *
  * x_out * rsqrt(mean(x_out^2) + eps)) packed with mbt blocks, or row-major (M, H) when mbt == 0
- * (drl_add_rmsnorm_fwd semantics). H % 8 == 0. */
+ * (drl_add_rmsnorm_fwd semantics). H % 8 == 0. y_packed (ABI 8, may be NULL): the same y written a second time,
+ * packed with packed_mbt blocks (the decode lm_head's operand beside a row-major y). */
 int drl_decode_rmsnorm(const float* x_in, const float* partials, int32_t nsplit, float* x_out, const float* weight,
-                       void* y, int64_t M, int64_t H, int64_t mbt, float eps, void* stream);
+                       void* y, int64_t M, int64_t H, int64_t mbt, float eps, void* y_packed, int64_t packed_mbt,
+                       void* stream);
 /* One decode token per sequence: qkv = bf16(sum of nsplit partials (nsplit, B, (Hq+2Hkv)D) + bias), then
  * drl_rope_qkv_fwd's rotation: q (B, Hkv, G, D), k_cache (B, Hkv, Tk, D) row koff, V into vt_cache
  * (B, Hkv, D, ld_vt) column koff and/or v_cache (B, Hkv, Tk, D); koff_dev (device int64) overrides koff. */
@@ -629,7 +631,14 @@ int drl_decode_qkv_rope_norm(const float* x_resid, const float* norm_weight, flo
 /* The model's final norm of the fused-norm step (Qwen2Model.norm): y = bf16(w * x * rsqrt(mean(x^2) + eps)) from the
  * packed residual, y packed (y_mbt blocks) or row-major (M, H) when y_mbt == 0. */
 int drl_decode_final_norm(const float* x_resid, int64_t x_mbt, const float* weight, void* y, int64_t M, int64_t H,
-                          int64_t y_mbt, float eps, void* stream);
+                          int64_t y_mbt, float eps, void* y_packed, int64_t packed_mbt, void* stream);
+/* The decode step's lm_head at <= 64 rows (ABI 8; replaces nn.Linear lm_head of HF generate's per-token forward,
+ * hf_rollout.py:112-124): logits (M, ld) bf16 = bf16(h W^T) with h the packed final-norm output (mbt blocks from
+ * drl_decode_lm_head_plan) and W packed by drl_decode_pack_weight (V rows). K = 896. One workgroup per CU holds the h
+ * panel in LDS and streams its own contiguous range of the packed weight (no cross-workgroup dependence). */
+int drl_decode_lm_head_plan(int64_t M, int64_t V, int64_t K, int32_t* mbt);
+int drl_decode_lm_head(const void* h_packed, int64_t mbt, const void* w_packed, int64_t M, int64_t V, int64_t K,
+                       void* logits, int64_t ld, void* stream);
 
 
 

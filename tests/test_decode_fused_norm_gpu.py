@@ -259,7 +259,7 @@ def test_fused_rollout_graph_equals_eager():
 
     def pick(h):
         o = torch.empty(B, dtype=torch.int64, device=DEV)
-        return m.select_tokens(h, o, fused=False)
+        return m.select_tokens(h, o, fused=False, logits_fn=pk.logits)  # the step's own lm_head, as the rollout
 
     toks = [pick(h)]
     for t in range(1, R):
@@ -267,3 +267,52 @@ def test_fused_rollout_graph_equals_eager():
         h = pk.step(cache, toks[-1].view(B, 1), pos[:, -1] + t, kd)
         toks.append(pick(h))
     assert torch.equal(resp, torch.stack(toks, 1))
+
+
+@pytest.mark.parametrize("M", [1, 7, 32, 33, 64])
+@pytest.mark.parametrize("V", [151936, 5003])
+def test_decode_lm_head_matches_fp32_reference(M, V):
+    """The decode lm_head (persistent: the packed h panel in LDS, each workgroup streaming its contiguous range of the
+    packed weight, k16 steps split over 8 waves) against the fp32 product of the same bf16 operands rounded once to
+    bf16: within one bf16 rounding everywhere (the fp32 sums run in another order), bit-identical run to run; logits
+    columns past V untouched."""
+    K = 896
+    mbt = native.decode_lm_head_plan(M, V, K)
+    assert mbt == (2 if M > 32 else 1)
+    h = rnd(M, K, seed=M)
+    w = rnd(V, K, scale=0.05, seed=V)
+    hp = native.pack_activations(h, mbt)
+    wp = native.decode_pack_weight(w)
+    out = torch.full((M, V + 8), 7.0, dtype=BF, device=DEV)[:, :V]
+    native.decode_lm_head(hp, mbt, wp, M, V, K, out)
+    ref = h.float() @ w.float().t()
+    got = out.float()
+    err = (got - ref).abs()
+    assert (err <= ref.abs() * 2.0 ** -8 + 1e-3).float().mean().item() > 0.999
+    assert err.max().item() <= 2.0 ** -7 * ref.abs().max().item()
+    out2 = torch.empty(M, V, dtype=BF, device=DEV)
+    native.decode_lm_head(hp, mbt, wp, M, V, K, out2)
+    assert torch.equal(out.contiguous(), out2)
+    assert torch.all(out.as_strided((M, 8), (V + 8, 1), V).float() == 7.0)
+
+
+def test_packed_decode_logits_use_the_decode_lm_head():
+    """PackedDecode.logits at 64 rows: the decode lm_head on the final norm's packed copy == drl_gemm's lm_head on the
+    row-major h within one bf16 rounding; the same h in both forms."""
+    from dots.rl_amd.qwen2 import KVCache, PackedDecode
+
+    cfg, m = _width896_model(seed=5)
+    B, P = 64, 32
+    cache = KVCache(cfg, B, P + 4, DEV, BF)
+    ids = torch.randint(0, cfg.vocab_size, (B, P), device=DEV)
+    am = torch.ones(B, P, dtype=torch.int64, device=DEV)
+    pos = (am.cumsum(-1) - 1).clamp_min(0)
+    m.prefill(cache, ids, am, pos)
+    pk = PackedDecode(m, B)
+    assert pk.lm_w is not None
+    kd = torch.tensor([P], device=DEV)
+    h = pk.step(cache, ids[:, -1:], pos[:, -1] + 1, kd)
+    assert torch.equal(native.unpack_activations(pk.h_pk, B, cfg.hidden_size, pk.lm_mbt), h)
+    a = pk.logits(h).float()
+    b = m.logits(h).float()
+    assert (a - b).abs().max().item() <= 2.0 ** -7 * b.abs().max().item()

@@ -193,7 +193,7 @@ def test_bf16_packed_decode_teacher_forced(ref, weights, rows, group, fused):
 
         def body():  # token t-1 = the reference's, written at cache slot P+t-1, rotated at last_pos+t; t_dev += 1
             hh = packed.step_from(cache, resp, t_dev, last_pos, P)
-            out.copy_(model.logits(hh).float())
+            out.copy_(packed.logits(hh).float())  # the step's own lm_head (the decode kernel at <= 64 rows)
 
         body()
         logits.append(out.clone())
