@@ -283,7 +283,8 @@ def test_decode_lm_head_matches_fp32_reference(M, V):
     w = rnd(V, K, scale=0.05, seed=V)
     hp = native.pack_activations(h, mbt)
     wp = native.decode_pack_weight(w)
-    out = torch.full((M, V + 8), 7.0, dtype=BF, device=DEV)[:, :V]
+    ld = (V + 3) // 4 * 4 + 8  # the kernel's contract: ld % 4 == 0
+    out = torch.full((M, ld), 7.0, dtype=BF, device=DEV)[:, :V]
     native.decode_lm_head(hp, mbt, wp, M, V, K, out)
     ref = h.float() @ w.float().t()
     got = out.float()
@@ -293,7 +294,7 @@ def test_decode_lm_head_matches_fp32_reference(M, V):
     out2 = torch.empty(M, V, dtype=BF, device=DEV)
     native.decode_lm_head(hp, mbt, wp, M, V, K, out2)
     assert torch.equal(out.contiguous(), out2)
-    assert torch.all(out.as_strided((M, 8), (V + 8, 1), V).float() == 7.0)
+    assert torch.all(out.as_strided((M, ld - V), (ld, 1), V).float() == 7.0)
 
 
 def test_packed_decode_logits_use_the_decode_lm_head():
