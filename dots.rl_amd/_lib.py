@@ -195,6 +195,7 @@ SIGNATURES = {
                                                 I64, P, P]),
     "drl_decode_final_norm": (ctypes.c_int, [P, I64, P, P, I64, I64, I64, F32, P, I64, P]),
     "drl_decode_lm_head_plan": (ctypes.c_int, [I64, I64, I64, P]),
+    "drl_decode_lm_head_set_config": (None, [I32]),
     "drl_decode_lm_head": (ctypes.c_int, [P, I64, P, I64, I64, I64, P, I64, P]),
     "drl_linear_logprob_fwd": (ctypes.c_int, [P, I64, P, P, I32, I64, I64, I64, F32, P, P, P, P, SZ, P]),
     "drl_linear_logprob_dlogits": (ctypes.c_int, [P, I64, P, P, I32, I64, I64, I64, F32, P, P, P, P, P, I64, P]),

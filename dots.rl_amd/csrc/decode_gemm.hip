@@ -841,8 +841,9 @@ struct LmArgs {
 
 template <int MB, int NKS, int NWV, int DEPTH>
 __global__ __launch_bounds__(64 * NWV) void decode_lm_head_kernel(LmArgs a) {
-  static_assert(MB * NKS * 512 * 2 >= NWV * MB * 16 * 64 * 4, "split-tile slots reuse the panel's LDS");
-  __shared__ __attribute__((aligned(16))) uint16_t s_x[MB * NKS * 512];
+  // the split-tile slots (NWV x MB f32x16 per lane) reuse the panel's LDS once the panel is no longer read
+  constexpr int PANEL = MB * NKS * 512, SLOTS = NWV * MB * 16 * 64 * 2;
+  __shared__ __attribute__((aligned(16))) uint16_t s_x[PANEL > SLOTS ? PANEL : SLOTS];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int G = gridDim.x, g = blockIdx.x;
   const int t0 = static_cast<int>(static_cast<int64_t>(g) * a.tiles / G);
@@ -887,16 +888,24 @@ __global__ __launch_bounds__(64 * NWV) void decode_lm_head_kernel(LmArgs a) {
       }
     }
   };
+  // the panel fragments of the current k16 step, read one step ahead (the LDS latency under the MFMAs)
+  u16x8 xf[MB];
+#pragma unroll
+  for (int m = 0; m < MB; ++m) xf[m] = *reinterpret_cast<const u16x8*>(s_x + (ks * MB + m) * 512 + lane * 8);
   for (int base = i0; base < i1; base += DEPTH) {
 #pragma unroll
     for (int d = 0; d < DEPTH; ++d) {
       const int i = base + d;
       if (i < i1) {
+        const int kn = ks + 1 == NKS ? 0 : ks + 1;
+        u16x8 xn[MB];
 #pragma unroll
-        for (int m = 0; m < MB; ++m) {
-          const u16x8 xf = *reinterpret_cast<const u16x8*>(s_x + (ks * MB + m) * 512 + lane * 8);
-          acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(ring[d]), as_bf16x8(xf), acc[m], 0, 0, 0);
-        }
+        for (int m = 0; m < MB; ++m) xn[m] = *reinterpret_cast<const u16x8*>(s_x + (kn * MB + m) * 512 + lane * 8);
+#pragma unroll
+        for (int m = 0; m < MB; ++m)
+          acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(ring[d]), as_bf16x8(xf[m]), acc[m], 0, 0, 0);
+#pragma unroll
+        for (int m = 0; m < MB; ++m) xf[m] = xn[m];
         ring[d] = __builtin_nontemporal_load(
             reinterpret_cast<const u16x8*>(wp + static_cast<int64_t>(min(i + DEPTH, i1 - 1)) * 512));
         if (++ks == NKS) {  // a tile's last k16 step
@@ -944,6 +953,7 @@ struct DgPlan {
 };
 
 int g_dg_mb = 0, g_dg_ksw = 0;  // tuning override (drl_decode_gemm_set_plan), 0 = automatic
+int g_lm_cfg = -1;              // decode lm_head (waves, ring depth) configuration (drl_decode_lm_head_set_config)
 
 // (token blocks per workgroup, k16 steps per wave) instantiated; registers in flight 4 * ksw * (1 + mb)
 struct DgShape { int mb, ksw; };
@@ -1563,13 +1573,15 @@ int drl_decode_rope(const float* partials, int32_t nsplit, const void* bias, con
   return DRL_OK;
 }
 
+void drl_decode_lm_head_set_config(int32_t config) { drl::g_lm_cfg = (config >= 0 && config < 6) ? config : -1; }
+
 int drl_decode_lm_head_plan(int64_t M, int64_t V, int64_t K, int32_t* mbt) {
   using namespace drl;
   const int cus = cu_count();
   const int64_t tiles = (V + 31) / 32;
   // 64 rows at most (the panel in LDS), K = 896 (the instantiated panel width), enough vocab tiles that every wave
   // of every workgroup owns at least one whole tile's k16 steps
-  if (M < 1 || M > 64 || K != 896 || V < 32 || cus <= 0 || tiles < 8 * 8)
+  if (M < 1 || M > 64 || K != 896 || V < 32 || cus <= 0 || tiles < 16 * 8)
     return fail(DRL_ERR_UNSUPPORTED, "decode lm_head: unsupported shape M=%lld V=%lld K=%lld", (long long)M,
                 (long long)V, (long long)K);
   if (mbt) *mbt = M > 32 ? 2 : 1;
@@ -1588,12 +1600,28 @@ int drl_decode_lm_head(const void* h_packed, int64_t mbt, const void* w_packed, 
                 "alignment: packed operands 16 B, logits 8 B with ld %% 4 == 0");
   LmArgs a{static_cast<const uint16_t*>(h_packed), static_cast<const uint16_t*>(w_packed),
            static_cast<uint16_t*>(logits), ld, static_cast<int>(M), static_cast<int>(V), static_cast<int>((V + 31) / 32)};
-  constexpr int NWV = 8, DEPTH = 16;
+  // (waves, ring depth) instantiated; g_lm_cfg picks one (drl_decode_lm_head_set_config, tuning)
+  static constexpr int kCfg[][2] = {{8, 16}, {8, 24}, {8, 32}, {16, 8}, {4, 32}, {16, 12}};
+  // measured (profiles/r06_decode_lm_head_64rows.jsonl): 8 waves x 16 loads at 64 rows, 16 waves x 8 at <= 32
+  const int ci = g_lm_cfg >= 0 ? g_lm_cfg : (mbt == 1 ? 3 : 0);
+  const int NWV = kCfg[ci][0];
   // workgroups: one per CU while each of the NWV waves keeps >= one whole tile of k16 steps
   const int grid = static_cast<int>(std::min<int64_t>(cu_count(), a.tiles / NWV));
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (mbt == 1) hipLaunchKernelGGL((decode_lm_head_kernel<1, 56, NWV, DEPTH>), dim3(grid), dim3(64 * NWV), 0, s, a);
-  else hipLaunchKernelGGL((decode_lm_head_kernel<2, 56, NWV, DEPTH>), dim3(grid), dim3(64 * NWV), 0, s, a);
+#define DRL_LM(NW, DP)                                                                                              \
+  do {                                                                                                             \
+    if (mbt == 1) hipLaunchKernelGGL((decode_lm_head_kernel<1, 56, NW, DP>), dim3(grid), dim3(64 * NW), 0, s, a); \
+    else hipLaunchKernelGGL((decode_lm_head_kernel<2, 56, NW, DP>), dim3(grid), dim3(64 * NW), 0, s, a);         \
+  } while (0)
+  switch (ci) {
+    case 1: DRL_LM(8, 24); break;
+    case 2: DRL_LM(8, 32); break;
+    case 3: DRL_LM(16, 8); break;
+    case 4: DRL_LM(4, 32); break;
+    case 5: DRL_LM(16, 12); break;
+    default: DRL_LM(8, 16); break;
+  }
+#undef DRL_LM
   DRL_LAUNCH_CHECK();
   return DRL_OK;
 }

@@ -637,6 +637,9 @@ int drl_decode_final_norm(const float* x_resid, int64_t x_mbt, const float* weig
  * drl_decode_lm_head_plan) and W packed by drl_decode_pack_weight (V rows). K = 896. One workgroup per CU holds the h
  * panel in LDS and streams its own contiguous range of the packed weight (no cross-workgroup dependence). */
 int drl_decode_lm_head_plan(int64_t M, int64_t V, int64_t K, int32_t* mbt);
+/* Tuning hook: the decode lm_head's (waves per workgroup, weight loads in flight per wave) configuration 0..5
+ * (-1 = automatic). */
+void drl_decode_lm_head_set_config(int32_t config);
 int drl_decode_lm_head(const void* h_packed, int64_t mbt, const void* w_packed, int64_t M, int64_t V, int64_t K,
                        void* logits, int64_t ld, void* stream);
 

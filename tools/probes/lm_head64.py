@@ -39,8 +39,14 @@ for M in (64, 32, 1):
     h = torch.randn(M, K, device=DEV).to(BF)
     hp = native.pack_activations(h, mbt)
     out = torch.empty(M, V, dtype=BF, device=DEV)
-    t_dec = gt(lambda i: native.decode_lm_head(hp, mbt, wps[i % 4], M, V, K, out))
+    row = {"rows": M}
+    for ci in range(6):
+        native.lib().drl_decode_lm_head_set_config(ci)
+        t = gt(lambda i: native.decode_lm_head(hp, mbt, wps[i % 4], M, V, K, out))
+        row[f"decode_cfg{ci}_us"] = t
+        row[f"decode_cfg{ci}_TBps"] = round(V * K * 2 / t / 1e6, 2)
+    native.lib().drl_decode_lm_head_set_config(-1)
+    row["decode_auto_us"] = gt(lambda i: native.decode_lm_head(hp, mbt, wps[i % 4], M, V, K, out))
     t_gemm = gt(lambda i: native.linear_fwd(h, ws[i % 4], out=out))
-    print(json.dumps({"rows": M, "decode_lm_head_us": t_dec, "drl_gemm_us": t_gemm,
-                      "decode_TBps": round(V * K * 2 / t_dec / 1e6, 2), "gemm_TBps": round(V * K * 2 / t_gemm / 1e6, 2)}),
-          flush=True)
+    row.update(drl_gemm_us=t_gemm, gemm_TBps=round(V * K * 2 / t_gemm / 1e6, 2))
+    print(json.dumps(row), flush=True)
