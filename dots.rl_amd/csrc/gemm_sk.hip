@@ -80,6 +80,9 @@ struct SkArgs {
   int64_t lda, ldb, ldc, ldc2;
   uint32_t a_bytes, b_bytes;
   int64_t a_total;     // > 0: a layout-K A operand beyond one buffer range, its descriptor rebased per tile (a + m0 rows)
+                       // (layout T: the operand's total bytes, with a_kblk)
+  int a_kblk;          // > 0: a layout-T A operand beyond one buffer range (K along its rows): every tile walks its k
+                       // loop in blocks of a_kblk rows (a multiple of 128), the A descriptor rebased at each block
   int M, N, K;
   int tm, tn, gm;      // tiles along M and N; M-tiles per rasterization group
   int P;               // k-tile pairs per tile
@@ -90,6 +93,8 @@ struct SkArgs {
   int splits;          // > 1: uniform split-K, workgroup sk_base + j = split (j % splits) of tile sk_tile0 + j / splits
   int sk_base;         // split-K after whole tiles: workgroups [0, sk_base) take whole tiles 0 .. sk_base - 1 first
   int sk_tile0;        // first split tile (= sk_base; 0 for an all split-K grid)
+  int sk_order;        // all-split-K grids: 1 = slice-major workgroup order (drl_gemm_set_debug bit 8; measured mixed:
+                       // qkv wgrad 276 -> 264 us, o 200 -> 217, down 719 -> 726, profiles/r06_gemm_modes.jsonl)
   int dbg;             // measurement only (drl_gemm_set_debug): 1 = whole tiles skip their epilogue, 2 = the plain
                        // bf16 epilogue stages but does not store
 };
@@ -147,6 +152,7 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
   // per-lane byte offsets of this wave's two copy instructions of each half-tile h (0 A0, 1 A1, 2 B0, 3 B1) for the
   // current tile, and the byte advance of one k-tile per operand
   uint32_t voff[4][2];
+  int a_kt0 = 0;  // the first k-tile of ra's range (layout-T K blocks: ra rebased per block)
   const uint32_t kstep_a = AT ? static_cast<uint32_t>(64 * g.lda * 2) : 128u;
   const uint32_t kstep_b = BT ? static_cast<uint32_t>(64 * g.ldb * 2) : 128u;
 
@@ -200,7 +206,7 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
     const bool is_a = h < 2;
     // k-tile past the data (K % 128 == 64): an soffset of the whole byte range puts every lane out of range (zeros)
     const uint32_t soff = k >= g.nkt ? (is_a ? a_end : g.b_bytes)
-                                     : static_cast<uint32_t>(k) * (is_a ? kstep_a : kstep_b);
+                                     : static_cast<uint32_t>(is_a ? k - a_kt0 : k) * (is_a ? kstep_a : kstep_b);
 #pragma unroll
     for (int c = 0; c < 2; ++c)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(is_a ? ra : rb, (lds_void*)(dst + (wave + 8 * c) * 512 + lane * 8), 16,
@@ -271,16 +277,18 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
   constexpr int NB_READS = BT ? 8 : 4;   // LDS instructions of one B sub-tile read
   constexpr int NA_READS = AT ? 16 : 8;  // of one A sub-tile read
 
-  // one segment: k-tile pairs [p0, p1) of the current tile accumulated into acc (zeroed first)
-  auto run = [&](int p0, int p1) {
+  // one segment: k-tile pairs [p0, p1) of the current tile accumulated into acc (zeroed first unless keep)
+  auto run = [&](int p0, int p1, bool keep) __attribute__((always_inline)) {
+    if (!keep) {
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+      for (int a = 0; a < 2; ++a)
 #pragma unroll
-      for (int b = 0; b < 2; ++b)
+        for (int b = 0; b < 2; ++b)
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+          for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4{};
+            for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4{};
+    }
     const int k0 = 2 * p0, k1 = 2 * p1;  // k-tiles [k0, k1)
     issue(2, 0, k0, k1); issue(0, 0, k0, k1); issue(3, 0, k0, k1); issue(1, 0, k0, k1);
     issue(2, 1, k0 + 1, k1); issue(0, 1, k0 + 1, k1); issue(3, 1, k0 + 1, k1);
@@ -339,6 +347,29 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
     if (wr == 0) bar();  // balance the upper group's extra barrier
   };
   (void)NB_READS;
+  // k-pairs [p0, p1) of the current tile; a layout-T A operand past one buffer range is walked in blocks of a_kblk
+  // rows, the descriptor rebased at each (one launch, the fp32 output read and written once — the round-5 host loop
+  // launched one GEMM per block, each a read-modify-write of the whole output)
+  auto run_k = [&](int p0, int p1) __attribute__((always_inline)) {
+    const bool blk = AT && g.a_kblk > 0;
+    const int bp = blk ? g.a_kblk / 128 : max(p1, 1);  // k-pairs per block (one block without K blocking)
+    bool keep = false;
+    for (int q0 = blk ? (p0 / bp) * bp : p0; q0 < p1; q0 += bp) {
+      const int lo = max(p0, q0), hi = min(p1, q0 + bp);
+      if constexpr (AT) {
+        if (blk) {
+          const int64_t off = static_cast<int64_t>(q0) * 128 * g.lda * 2;
+          const int64_t rem = g.a_total - off;
+          a_end = static_cast<uint32_t>(rem < 0x7fffffff ? rem : 0x7fffffff);
+          ra = __builtin_amdgcn_make_buffer_rsrc((void*)(reinterpret_cast<const char*>(g.a) + off), (short)0,
+                                                 (int)a_end, 0x00020000);
+          a_kt0 = 2 * q0;
+        }
+      }
+      run(lo, hi, keep);
+      keep = true;
+    }
+  };
 
   // ------------------------------------------------------------------------------------------ epilogues
   // accumulator block (i, j) of quadrant (qm, qn), transposed (the MFMA's operands are swapped): lane (fq, fr) holds
@@ -658,7 +689,14 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
   // all S arrivals, then each reduces 1/S of the tile's registers over the S slabs in split order (a fixed order:
   // bit-reproducible) and writes that share through the epilogue — the combine runs on all S workgroups at once.
   if (g.splits > 1 && wg >= g.sk_base) {
-    const int S = g.splits, rel = wg - g.sk_base, ti = rel / S, t = g.sk_tile0 + ti, sp = rel - ti * S;
+    // slice order: tile-major (a tile's S slices on consecutive workgroups) or, with sk_order (all-split-K grids
+    // only), slice-major — the same k-range of every tile on consecutive workgroups, which the XCD remap places on
+    // one XCD at once, so tiles of one row / column read the same k window of A / B through the shared L2. The slab of
+    // (tile ti, slice s) sits at index s * nt + ti, the combine reads them in split order either way (same bits).
+    const int S = g.splits, rel = wg - g.sk_base, nt = (G - g.sk_base) / S;
+    const bool smaj = g.sk_order && g.sk_base == 0;
+    const int ti = smaj ? rel % nt : rel / S, t = g.sk_tile0 + ti, sp = smaj ? rel / nt : rel - ti * S;
+    const int slab_tile = smaj ? ti : ti * S, slab_step = smaj ? nt : 1;  // slab of (ti, s) = slab_tile + s * step
     int m0, n0;
     {
       const int grp = t / (g.gm * g.tn), first = grp * g.gm, gmm = min(g.tm - first, g.gm), r = t % (g.gm * g.tn);
@@ -666,10 +704,10 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
       n0 = (r / gmm) * 256;
     }
     setup_tile(m0, n0);
-    run(sp * g.P / S, (sp + 1) * g.P / S);
+    run_k(sp * g.P / S, (sp + 1) * g.P / S);
     const __amdgpu_buffer_rsrc_t rws =
         __builtin_amdgcn_make_buffer_rsrc((void*)g.ws, (short)0, (G - g.sk_base) * SLAB * 4, 0x00020000);
-    const uint32_t vo = static_cast<uint32_t>(rel) * SLAB * 4 + threadIdx.x * 16;
+    const uint32_t vo = static_cast<uint32_t>(slab_tile + sp * slab_step) * SLAB * 4 + threadIdx.x * 16;
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -700,7 +738,7 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the barrier
     // this slice's share of the tile: register groups [32 sp / S, 32 (sp + 1) / S)
     const int r0 = 32 * sp / S, r1 = 32 * (sp + 1) / S;
-    const uint32_t vt = static_cast<uint32_t>(ti * S) * SLAB * 4 + threadIdx.x * 16;
+    const uint32_t vt = static_cast<uint32_t>(slab_tile) * SLAB * 4 + threadIdx.x * 16;
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -713,7 +751,8 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
             if (reg < r0 || reg >= r1) continue;
             f32x4 v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rws, vt, reg * 8192, 16));
             for (int s2 = 1; s2 < S; ++s2)
-              v += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rws, vt + s2 * SLAB * 4, reg * 8192, 16));
+              v += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rws, vt + s2 * slab_step * SLAB * 4,
+                                                                                   reg * 8192, 16));
             // transposed block (see the epilogue): row fr, columns 4 fq + r
             const int m = m0 + a * 128 + wr * 64 + i * 16 + fr;
             if (m >= g.M) continue;
@@ -745,7 +784,7 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
     int m0, n0;
     tile_origin(t, m0, n0);
     setup_tile(m0, n0);
-    run(0, g.P);
+    run_k(0, g.P);
     if (!(g.dbg & 1)) epilogue(m0, n0);
   }
   if (tail_mode) return;
@@ -767,7 +806,7 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
     int m0, n0;
     tile_origin(t, m0, n0);
     setup_tile(m0, n0);
-    run(kb, ke);
+    run(kb, ke, false);
     if (kb != 0) {
       // tail: publish the partial tile (register order: coalesced 16-B lanes)
       // buffer stores: per-lane voffset + a constant soffset per register (no 64-bit address per register for the
@@ -849,6 +888,7 @@ struct SkTuning {
 };
 SkTuning g_sk;
 int g_sk_dbg = 0;
+int g_sk_kloop = 0;  // 1: layout-T operands past 2 GB as the round-5 host loop of K-block launches (A/B measurement)
 
 template <int AT, int BT>
 int launch_sk_layout(SkArgs& g, int epi, int grid, hipStream_t s) {
@@ -972,7 +1012,10 @@ int64_t drl_gemm_workspace_bytes(void) {
   return static_cast<int64_t>(cus) * drl::SLAB * 4 + static_cast<int64_t>(cus + 1) * 4 + 256;
 }
 
-void drl_gemm_set_debug(int32_t flags) { drl::g_sk_dbg = flags; }
+void drl_gemm_set_debug(int32_t flags) {
+  drl::g_sk_dbg = flags;
+  drl::g_sk_kloop = (flags & 16) ? 1 : 0;
+}
 
 int drl_gemm_plan(int64_t M, int64_t N, int64_t K, int32_t epilogue, int32_t cus, int32_t* info) {
   using namespace drl;
@@ -1014,7 +1057,22 @@ int drl_gemm(const void* a, int64_t lda, int32_t a_layout, const void* b, int64_
   // the lm_head's d_logits^T at 8192 rows x 151936): K blocks of whole 128-deep k-pairs accumulated into the fp32
   // output (the first block with the caller's beta, the rest with beta = 1)
   const auto t_bytes = [&](int32_t layout, int64_t ld) { return layout == DRL_LAYOUT_T ? K * ld * 2 + 320ll * ld * 2 : 0; };
-  if (a && b && lda > 0 && ldb > 0 && (t_bytes(a_layout, lda) >= (1ll << 31) || t_bytes(b_layout, ldb) >= (1ll << 31))) {
+  // a layout-T A past one buffer range with B within one: ONE launch whose tiles walk K in blocks (a_kblk), when the
+  // decomposition is whole tiles (+ a split-K tail) — the lm_head weight gradient's d_logits^T
+  bool a_kblocks = false;
+  if (a && b && lda > 0 && ldb > 0 && a_layout == DRL_LAYOUT_T && t_bytes(a_layout, lda) >= (1ll << 31) &&
+      t_bytes(b_layout, ldb) < (1ll << 31) && c_dtype == DRL_F32 && epilogue == DRL_GEMM_PLAIN && !g_sk_kloop) {
+    SkArgs q{};
+    q.tm = static_cast<int>((M + 255) / 256);
+    q.tn = static_cast<int>((N + 255) / 256);
+    q.P = static_cast<int>((K + 127) / 128);
+    q.n_tiles = q.tm * q.tn;
+    int grid_q = 0, mode_q = 0;
+    a_kblocks = plan_decomposition(q, epilogue, cu_count(), grid_q, mode_q) == DRL_OK && mode_q == 2 &&
+                lda * 2 * 128 < (1ll << 31) && M * 2 + 640 < (1ll << 31);
+  }
+  if (!a_kblocks && a && b && lda > 0 && ldb > 0 &&
+      (t_bytes(a_layout, lda) >= (1ll << 31) || t_bytes(b_layout, ldb) >= (1ll << 31))) {
     DRL_CHECK_ARG(c_dtype == DRL_F32 && epilogue == DRL_GEMM_PLAIN,
                   "a layout-T operand over 2 GB needs the fp32 accumulating output (K split)");
     const int64_t ld = std::max(a_layout == DRL_LAYOUT_T ? lda : 0, b_layout == DRL_LAYOUT_T ? ldb : 0);
@@ -1056,7 +1114,7 @@ int drl_gemm(const void* a, int64_t lda, int32_t a_layout, const void* b, int64_
   // 32-bit buffer offsets: the byte range plus one tile of overhang must stay below 2^32
   const int64_t a_bytes = a_rows * lda * 2, b_bytes = b_rows * ldb * 2;
   // (below 2 GB: voffset + a whole-range soffset must not wrap around 2^32)
-  DRL_CHECK_ARG((a_rebase ? 576ll * lda * 2 : a_bytes + 320ll * lda * 2) < (1ll << 31) &&
+  DRL_CHECK_ARG((a_rebase || a_kblocks ? 576ll * lda * 2 : a_bytes + 320ll * lda * 2) < (1ll << 31) &&
                     b_bytes + 320ll * ldb * 2 < (1ll << 31),
                 "operand larger than the 2 GB buffer range");
   const int64_t ncols = epilogue == DRL_GEMM_SWIGLU ? N / 2 : N;
@@ -1073,12 +1131,15 @@ int drl_gemm(const void* a, int64_t lda, int32_t a_layout, const void* b, int64_
   g.c2 = static_cast<uint16_t*>(c2);
   g.bias = static_cast<const uint16_t*>(bias);
   g.lda = lda; g.ldb = ldb; g.ldc = ldc; g.ldc2 = ldc2;
-  g.a_bytes = static_cast<uint32_t>(a_rebase ? 0 : a_bytes);
-  g.a_total = a_rebase ? a_bytes : 0;
+  g.a_bytes = static_cast<uint32_t>(a_rebase || a_kblocks ? 0 : a_bytes);
+  g.a_total = a_rebase || a_kblocks ? a_bytes : 0;
+  // K-block rows: the most whole k-pairs whose rows (plus a tile of overhang) stay inside one 2 GB range
+  g.a_kblk = a_kblocks ? static_cast<int>(std::max<int64_t>(128, ((1ll << 31) / (lda * 2) - 320) / 128 * 128)) : 0;
   g.b_bytes = static_cast<uint32_t>(b_bytes);
   g.M = static_cast<int>(M); g.N = static_cast<int>(N); g.K = static_cast<int>(K);
   g.beta = beta ? 1 : 0;
   g.dbg = g_sk_dbg;
+  g.sk_order = (g_sk_dbg & 8) ? 1 : 0;
   g.tm = static_cast<int>((M + 255) / 256);
   g.tn = static_cast<int>((N + 255) / 256);
   g.P = static_cast<int>((K + 127) / 128);

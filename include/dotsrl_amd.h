@@ -676,6 +676,8 @@ void drl_gemm_set_sk_tuning(int32_t grid, int32_t group, int32_t dp_mode, int32_
 /* Measurement hook (never set in the product path): 1 = whole tiles skip their epilogue (no output written), to time
  * the main loop and the per-tile fixed cost apart; 0 = normal. */
 void drl_gemm_set_debug(int32_t flags);
+/* (flags bit 8: all-split-K grids in slice-major workgroup order instead of tile-major — schedule only, the same
+ * bits; bit 16: a layout-T operand past 2 GB as the host loop of K-block launches; both for A/B measurement.) */
 /* The decomposition drl_gemm would launch for one (M, N, K, epilogue) over `cus` CUs under the current tuning (host
  * arithmetic only, no device): info[0] mode (1 stream-K, 2 whole tiles, 3 uniform split-K), info[1] split-K slices
  * per split tile, info[2] workgroups, info[3] tiles dealt whole, info[4] first split workgroup (tail split-K).

@@ -357,3 +357,33 @@ def test_down_wgrad_automatic_split_k(T):
     gw2 = torch.full((896, 4864), 0.5, device="cuda")
     native.linear_wgrad(gw2, dy, x)
     assert torch.equal(gw, gw2)
+
+
+def test_layout_t_operand_over_2gb_walks_k_in_one_launch():
+    """The lm_head weight gradient's d_logits^T (T x V bf16 past one 2 GB buffer range, layout T) as ONE launch whose
+    tiles walk K in blocks with the A descriptor rebased per block (round 6; round 5 launched one GEMM per K block, each
+    a read-modify-write of the fp32 output): against the K-block host loop (drl_gemm_set_debug bit 16, fp32 sums
+    rounded per block) within fp32 rounding, and spot rows against fp64; beta accumulates."""
+    T, V, H = 8192, 151936, 896
+    g = torch.Generator(device="cuda").manual_seed(5)
+    dy = torch.empty(T, V, dtype=torch.bfloat16, device="cuda")
+    for r0 in range(0, T, 1024):  # fill in slices (bounded temporaries)
+        dy[r0:r0 + 1024] = (torch.randn(1024, V, generator=g, device="cuda") * 0.1).to(torch.bfloat16)
+    x = torch.randn(T, H, generator=g, device="cuda").to(torch.bfloat16)
+    base = torch.randn(V, H, generator=g, device="cuda")
+    gw = base.clone()
+    native.linear_wgrad(gw, dy, x)  # one launch, K blocks inside
+    gw2 = base.clone()
+    native.lib().drl_gemm_set_debug(16)
+    try:
+        native.linear_wgrad(gw2, dy, x)  # the host loop of K-block launches
+    finally:
+        native.lib().drl_gemm_set_debug(0)
+    torch.testing.assert_close(gw, gw2, rtol=1e-5, atol=1e-4)
+    rows = torch.tensor([0, 1, 255, 256, 70000, V - 1], device="cuda")
+    ref = base[rows].double() + dy[:, rows].double().t() @ x.double()
+    torch.testing.assert_close(gw[rows].double(), ref, rtol=1e-5, atol=2e-4)
+    gw3 = base.clone()
+    native.linear_wgrad(gw3, dy, x)
+    assert torch.equal(gw, gw3)  # deterministic
+    del dy

@@ -122,6 +122,17 @@ PYEOF
       done
       python3 tools/pmc_sq.py "$OUT/pmc_decattn_sq.json" decode_group_kernel "$OUT/dpmc1" "$OUT/dpmc2" || exit 1
       find "$OUT" -name "*.csv" -size +20M -delete ;;
+    pmc_shapes)  # FETCH_SIZE / WRITE_SIZE per update-pass shape class (tools/probes/pmc_shapes.py)
+      timeout -k 10 300 rocprofv3 --kernel-trace -f csv -d "$OUT/shp_t" -o t -- python3 "$ROOT/tools/probes/pmc_shapes.py" \
+        > "$OUT/pmc_shapes.out" 2>&1 || { tail -5 "$OUT/pmc_shapes.out"; exit 1; }
+      for c in FETCH_SIZE WRITE_SIZE; do
+        timeout -s KILL 300 rocprofv3 --pmc $c --kernel-include-regex gemm_sk_kernel -f csv -d "$OUT/shp_$c" -o p \
+          -- python3 "$ROOT/tools/probes/pmc_shapes.py" > "$OUT/shp_$c.log" 2>&1 || { tail -5 "$OUT/shp_$c.log"; exit 1; }
+      done
+      python3 tools/pmc_shapes_summary.py "$OUT/pmc_shapes.out" "$OUT/shp_FETCH_SIZE" "$OUT/shp_WRITE_SIZE" \
+        "$(find "$OUT/shp_t" -name "*kernel_trace.csv" | head -1)" > "$OUT/pmc_shapes.json" || exit 1
+      find "$OUT" -name "*.csv" -size +20M -delete
+      python3 -c "import json; [print(r['shape'], round(r['ratio'], 2), round(r.get('tflops', 0))) for r in json.load(open('$OUT/pmc_shapes.json'))['shapes']]" ;;
     ab:*)  # A/B of GEMM builds: ab:<lib1>,<lib2>,...
       IFS=',' read -ra L <<< "${step#ab:}"
       bash tools/gemm_ab.sh "$OUT" "${L[@]}" || exit 1 ;;
