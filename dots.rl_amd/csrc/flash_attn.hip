@@ -705,6 +705,210 @@ __global__ __launch_bounds__(64 * NW) void flash_dq_kernel(FlashBwdArgs a) {
   }
 }
 
+// dQ over TWO adjacent 32-row query tiles per workgroup (round 6): each key block staged into LDS (K, V, K^T) feeds both
+// tiles' products, so the global -> LDS staging and the block barrier are paid once per two tiles' MFMAs; the lower
+// tile skips the upper tile's last (diagonal) block. Per (query row, head) every product, mask and rounding is the
+// one-tile kernel's in its order: bit-identical to flash_dq_kernel (tests/test_layers_gpu.py). KV2 = 1: the K / V
+// fragments of a block are read from LDS once and kept in registers for both tiles.
+template <int D, int NW = 4, int KV2 = 1>
+__global__ __launch_bounds__(64 * NW) void flash_dq2_kernel(FlashBwdArgs a) {
+  constexpr int KS = D / 16, MT = D / 32, NT = 64 * NW;
+  using TL = DqTile<D, NT>;
+  __shared__ __attribute__((aligned(16))) uint16_t lds_k[2][TL::RSZ];
+  __shared__ __attribute__((aligned(16))) uint16_t lds_v[2][TL::RSZ];
+  __shared__ __attribute__((aligned(16))) uint16_t lds_kt[2][TL::TSZ];
+  __shared__ uint32_t lds_vw[2][8];
+  const int tid = threadIdx.x;
+  const int HS = static_cast<int>((a.G + NW - 1) / NW);
+  const int lane = tid & 63;
+  const int qi = lane & 31, h = lane >> 5;
+  const int T = static_cast<int>(a.T);
+  const int ntiles = (T + 31) / 32, npairs = (ntiles + 1) / 2;
+  int pair;
+  int64_t bhs;
+  xcd_tile_order(npairs, static_cast<int>(gridDim.y), pair, bhs);
+  const int64_t bh = bhs / HS;
+  const int g = __builtin_amdgcn_readfirstlane(tid >> 6) + NW * static_cast<int>(bhs % HS);  // scalar: uniform branches
+  const bool computes = g < a.G;
+  const int64_t b = bh / a.Hkv, hkv = bh % a.Hkv;
+  const int64_t head = bh * a.G + (computes ? g : 0);
+  // tile 1: the pair's upper tile (longest causal rows first), tile 0 the one below it (absent for an odd first pair)
+  const int thi = ntiles - 1 - 2 * pair;
+  int t0[2] = {(thi - 1) * 32, thi * 32};
+  bool act[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const bool present = u == 1 || thi >= 1;
+    const bool skipped = present && a.q_start && t0[u] + 32 <= a.q_start[b];  // uniform: dq rows zero
+    if (skipped && computes && t0[u] + qi < T) {
+#pragma unroll
+      for (int s2 = 0; s2 < KS; ++s2)
+        *reinterpret_cast<u16x8*>(a.dq + (head * T + t0[u] + qi) * D + 16 * s2 + 8 * h) = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+    act[u] = present && !skipped;
+  }
+  if (!act[1]) return;  // the upper tile skipped: so is the lower (workgroup-uniform)
+  bf16x8 qf[2][KS], dof[2][KS];
+  float dl[2], lref[2];
+  int tq[2];
+  bool qvalid[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    tq[u] = t0[u] + qi;
+    qvalid[u] = computes && act[u] && tq[u] < T;
+    float d = 0.f;
+    const int tr = qvalid[u] ? tq[u] : 0;
+    const uint16_t* qrow = a.q + (head * T + tr) * D + 8 * h;
+    const int64_t orow_off = (((b * T + tr) * a.Hkv + hkv) * a.G + (computes ? g : 0)) * D + 8 * h;
+    const int64_t oq = a.o_row ? max(a.o_row[b * T + tr], int64_t(0)) : b * T + tr;
+    const int64_t oo_off = ((oq * a.Hkv + hkv) * a.G + (computes ? g : 0)) * D + 8 * h;
+#pragma unroll
+    for (int s2 = 0; s2 < KS; ++s2) {
+      u16x8 qv = *reinterpret_cast<const u16x8*>(qrow + 16 * s2);
+      u16x8 dv = *reinterpret_cast<const u16x8*>(a.dout + orow_off + 16 * s2);
+      const u16x8 ov = *reinterpret_cast<const u16x8*>(a.o + oo_off + 16 * s2);
+      if (!qvalid[u]) qv = dv = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d = fmaf(bf2f(dv[j]), bf2f(ov[j]), d);
+      qf[u][s2] = as_bf16x8(qv);
+      dof[u][s2] = as_bf16x8(dv);
+    }
+    d = pair_sum(d);  // delta = rowsum(dO * O) of query tq
+    dl[u] = d;
+    if (qvalid[u] && h == 0) a.delta[head * T + tq[u]] = d;
+    const float lse2 = qvalid[u] ? a.lse[head * T + tq[u]] * 1.4426950408889634f : -INFINITY;
+    lref[u] = lse2 == -INFINITY ? INFINITY : lse2;
+  }
+  f32x16 dqt[2][MT];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) dqt[u][mt] = f32x16{};
+  const uint16_t* kbase = a.k + bh * a.T * D;
+  const uint16_t* vbase = a.v + bh * a.T * D;
+  const uint16_t* ktbase = a.kt + bh * D * a.ld_t;
+  const uint8_t* vrow = a.valid + b * a.ld_valid;
+  const int nb = (min(T, t0[1] + 32) + 31) / 32;                   // blocks of the upper tile
+  const int nb_lo = act[0] ? (min(T, t0[0] + 32) + 31) / 32 : 0;  // of the lower tile
+  u16x8 stage[2][TL::CPT];
+  uint32_t vst[2] = {0u, 0u};
+  auto issue_blk = [&](int j, int set) {
+    const int kk = j * 32;
+    if (kk + 32 <= T) {
+      dq_issue_full<D, NT>(kbase, vbase, ktbase, a.ld_t, kk, tid, stage[set]);
+      vst[set] = *reinterpret_cast<const uint32_t*>(vrow + kk + 4 * (tid & 7));
+    } else {
+      dq_issue<D, NT>(kbase, vbase, ktbase, a.ld_t, kk, T, tid, stage[set]);
+      vst[set] = valid_issue(vrow, kk, T, tid);
+    }
+  };
+  issue_blk(0, 0);
+  if (nb > 1) issue_blk(1, 1);
+  dq_store<D, NT>(lds_k[0], lds_v[0], lds_kt[0], tid, stage[0]);
+  if (tid < 8) lds_vw[0][tid] = vst[0];
+  __syncthreads();
+  auto step = [&](const int ib, const int cur) __attribute__((always_inline)) {
+    const int k0 = ib * 32;
+    if (ib + 2 < nb) {
+      if (cur == 0) issue_blk(ib + 2, 0);
+      else issue_blk(ib + 2, 1);
+    }
+    if (computes) {
+      const uint16_t* kr = lds_k[cur] + qi * TL::ROW + 8 * h;
+      const uint16_t* vr = lds_v[cur] + qi * TL::ROW + 8 * h;
+      u16x8 kv[KV2 ? KS : 1], vv[KV2 ? KS : 1];
+      if constexpr (KV2) {
+#pragma unroll
+        for (int s2 = 0; s2 < KS; ++s2) {
+          kv[s2] = *reinterpret_cast<const u16x8*>(kr + 16 * s2);
+          vv[s2] = *reinterpret_cast<const u16x8*>(vr + 16 * s2);
+        }
+      }
+      const int kbase0 = k0 + 4 * h;
+      uint32_t vw[4];
+      bool allv = true;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        vw[c] = lds_vw[cur][h + 2 * c];
+        allv &= vw[c] == 0x01010101u;
+      }
+      allv = __all(allv);
+      u16x8 dsb[2][2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        if (u == 0 && ib >= nb_lo) continue;  // uniform: the lower tile's blocks end one earlier
+        f32x16 st = f32x16{}, dpt = f32x16{};
+#pragma unroll
+        for (int s2 = 0; s2 < KS; ++s2) {
+          const u16x8 k_ = KV2 ? kv[KV2 ? s2 : 0] : *reinterpret_cast<const u16x8*>(kr + 16 * s2);
+          const u16x8 v_ = KV2 ? vv[KV2 ? s2 : 0] : *reinterpret_cast<const u16x8*>(vr + 16 * s2);
+          st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(k_), qf[u][s2], st, 0, 0, 0);
+          dpt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(v_), dof[u][s2], dpt, 0, 0, 0);
+        }
+        const bool full = allv && k0 + 31 <= t0[u];
+        if (full) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float p = __builtin_amdgcn_exp2f(fmaf(st[r], a.scale_log2, -lref[u]));
+            dsb[u][r >> 3][r & 7] = to_bf16_bits(p * (dpt[r] - dl[u]));
+          }
+        } else {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int r = 4 * c + j;
+              const bool ok = ((vw[c] >> (8 * j)) & 0xffu) != 0u && kbase0 + 8 * c + j <= tq[u];
+              const float p = ok ? __builtin_amdgcn_exp2f(fmaf(st[r], a.scale_log2, -lref[u])) : 0.f;
+              dsb[u][r >> 3][r & 7] = to_bf16_bits(p * (dpt[r] - dl[u]));
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const uint16_t* ktl = lds_kt[cur] + (32 * mt + qi) * TL::TROW + 8 * h;
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const u16x8 kt_ = *reinterpret_cast<const u16x8*>(ktl + 16 * s2);
+          dqt[1][mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(kt_), as_bf16x8(dsb[1][s2]), dqt[1][mt], 0, 0, 0);
+          if (ib < nb_lo)
+            dqt[0][mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(kt_), as_bf16x8(dsb[0][s2]), dqt[0][mt], 0, 0,
+                                                                 0);
+        }
+      }
+    }
+    if (ib + 1 < nb) {
+      if (cur == 0) {
+        dq_store<D, NT>(lds_k[1], lds_v[1], lds_kt[1], tid, stage[1]);
+        if (tid < 8) lds_vw[1][tid] = vst[1];
+      } else {
+        dq_store<D, NT>(lds_k[0], lds_v[0], lds_kt[0], tid, stage[0]);
+        if (tid < 8) lds_vw[0][tid] = vst[0];
+      }
+    }
+    __syncthreads();
+  };
+  for (int ib = 0; ib < nb; ib += 2) {
+    step(ib, 0);
+    if (ib + 1 < nb) step(ib + 1, 1);
+  }
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    if (!qvalid[u]) continue;
+    uint16_t* dqrow = a.dq + (head * T + tq[u]) * D;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const u16x4 w = u16x4{to_bf16_bits(dqt[u][mt][4 * c] * a.scale), to_bf16_bits(dqt[u][mt][4 * c + 1] * a.scale),
+                              to_bf16_bits(dqt[u][mt][4 * c + 2] * a.scale), to_bf16_bits(dqt[u][mt][4 * c + 3] * a.scale)};
+        *reinterpret_cast<u16x4*>(dqrow + 32 * mt + 8 * c + 4 * h) = w;
+      }
+    }
+  }
+}
+
 // NW waves per workgroup; wave w handles query heads w, w + NW, ... of the KV head (its dK / dV partials
 // accumulate over them in registers). head_dim 64: NW = 8 (one head per wave, G <= 8); head_dim 128: NW = 4,
 // one wave per SIMD, so the 128 accumulator registers of dK^T / dV^T and the Q / dO rows fit without spilling.
@@ -1562,6 +1766,10 @@ __global__ __launch_bounds__(64 * NW) void decode_group_kernel(DecodeArgs a) {
 }  // namespace
 
 int g_dec_nw = 0, g_dec_splits = 0;  // tuning override (drl_decode_attention_set_plan), 0 = automatic
+int g_dq_variant = 0;  // drl_flash_attn_bwd_set_variant: 0 = one query tile per dQ workgroup, 1 = two tiles (K / V in
+                       // registers), 2 = two tiles re-reading K / V from LDS. The two-tile kernel measured slower
+                       // (update shape: 1227 -> 1474 us per backward, profiles/r06_flash_dq_two_tiles_rejected.jsonl):
+                       // 333 registers per lane, one wave per SIMD, where the one-tile kernel runs two workgroups per CU
 int g_dec_variant = 0;  // drl_decode_attention_set_variant: 1 = one block in flight (LDS fragments), 2..4 = ring depth
 
 // key splits for decode attention. Measured (tools/kernel_bench.py --only decode_sweep, B 64..512,
@@ -1650,8 +1858,13 @@ int drl_flash_attn_bwd_rows(const void* q, const void* k, const void* kt, const 
   const dim3 block_dq(64 * kDqWaves);  // waves >= G only stage K / V / K^T
   const dim3 block_kv(static_cast<unsigned>(64 * std::min<int64_t>(G, D == 64 ? kDkdvWaves64 : 4)));
   hipStream_t s = static_cast<hipStream_t>(stream);
+  // dQ over one query tile per workgroup; the two-tile form (flash_dq2_kernel) on request (A/B); head_dim 64
+  const dim3 grid_dq2(static_cast<unsigned>(((T + 31) / 32 + 1) / 2),
+                      static_cast<unsigned>(B * Hkv * ((G + kDqWaves - 1) / kDqWaves)));
   if (D == 64) {
-    hipLaunchKernelGGL((flash_dq_kernel<64, kDqWaves>), grid_dq, block_dq, 0, s, a);
+    if (g_dq_variant == 1) hipLaunchKernelGGL((flash_dq2_kernel<64, kDqWaves, 1>), grid_dq2, block_dq, 0, s, a);
+    else if (g_dq_variant == 2) hipLaunchKernelGGL((flash_dq2_kernel<64, kDqWaves, 0>), grid_dq2, block_dq, 0, s, a);
+    else hipLaunchKernelGGL((flash_dq_kernel<64, kDqWaves>), grid_dq, block_dq, 0, s, a);
     hipLaunchKernelGGL((flash_dkdv_kernel<64, kDkdvWaves64, kKT64>), grid_kv64, block_kv, 0, s, a);
   } else {
     hipLaunchKernelGGL((flash_dq_kernel<128, kDqWaves>), grid_dq, block_dq, 0, s, a);
@@ -1660,6 +1873,8 @@ int drl_flash_attn_bwd_rows(const void* q, const void* k, const void* kt, const 
   DRL_LAUNCH_CHECK();
   return DRL_OK;
 }
+
+void drl_flash_attn_bwd_set_variant(int32_t variant) { drl::g_dq_variant = (variant >= 0 && variant <= 2) ? variant : 0; }
 
 void drl_decode_attention_set_variant(int32_t variant) {
   drl::g_dec_variant = (variant >= 1 && variant <= 4) ? variant : 0;

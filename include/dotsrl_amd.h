@@ -468,6 +468,9 @@ int drl_decode_step_prologue(const int64_t* responses, int64_t ld_responses, int
                              int64_t ld_valid, void* workspace, size_t workspace_bytes, int64_t x_mbt, void* stream);
 /* Tuning hook (tools/kernel_bench.py): force waves per workgroup (2/4/8/16) and key splits; 0 = automatic. */
 void drl_decode_attention_set_plan(int32_t waves, int32_t splits);
+/* Tuning hook of the fused attention backward (head_dim 64): 0 = dQ over one query tile per workgroup (default),
+ * 1 = two query tiles per workgroup (K / V fragments in registers), 2 = two tiles re-reading them. Same bits. */
+void drl_flash_attn_bwd_set_variant(int32_t variant);
 /* Tuning hook for forced plans (set_plan waves != 0): 1 = register-lean key loop (one block in flight per
  * wave, fragments read from LDS); 2..4 = that many blocks in flight per wave (4 and 8 waves, D = 64; else 2).
  * Results are identical. */

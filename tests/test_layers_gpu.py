@@ -367,3 +367,48 @@ def test_colsum_bf16_acc(N, C):
     got = native.colsum_bf16_acc(x, out.clone())
     assert (got.double() - want).abs().max().item() <= 1e-5 * (x.double().abs().sum(0).max().item() + 1)
     assert torch.equal(got, native.colsum_bf16_acc(x, out.clone()))
+
+
+@pytest.mark.parametrize("B,Hkv,G,T,qs", [(2, 2, 7, 256, None), (1, 2, 7, 104, None), (2, 1, 4, 64, None),
+                                          (3, 2, 8, 96, None), (2, 2, 7, 200, [0, 70]), (2, 2, 7, 256, [0, 128]),
+                                          (1, 2, 7, 32, None), (2, 2, 7, 768, [0, 511])])
+def test_flash_dq_two_tiles_bit_identical(B, Hkv, G, T, qs):
+    """The dQ kernel over two query tiles per workgroup (csrc/flash_attn.hip flash_dq2_kernel, K / V fragments held
+    in registers or re-read per tile) == the one-tile kernel bit for bit: odd and even tile counts, a ragged last tile,
+    key-valid holes, and q_start skipping whole lower tiles of a pair (prefix sharing's copies)."""
+    D = 64
+    g = torch.Generator(device=DEV).manual_seed(T + G + B)
+    q = torch.randn(B, Hkv, G, T, D, device=DEV, generator=g).to(torch.bfloat16)
+    k = torch.randn(B, Hkv, T, D, device=DEV, generator=g).to(torch.bfloat16)
+    v = torch.randn(B, Hkv, T, D, device=DEV, generator=g).to(torch.bfloat16)
+    dout = torch.randn(B, T, Hkv * G * D, device=DEV, generator=g).to(torch.bfloat16)
+    valid = torch.zeros(B, (T + 3) // 4 * 4, dtype=torch.uint8, device=DEV)
+    valid[:, :T] = 1
+    for b in range(B):
+        valid[b, : 5 * b] = 0
+    q_start = torch.tensor(qs, dtype=torch.int32, device=DEV) if qs is not None else None
+    if q_start is not None:  # dO is zero on the skipped query rows (the forward never produced them)
+        for b, s in enumerate(qs):
+            dout[b, : s // 32 * 32] = 0
+    ld = (T + 7) // 8 * 8
+    kt = torch.zeros(B, Hkv, D, ld, device=DEV, dtype=torch.bfloat16)
+    kt[..., :T] = k.transpose(-1, -2)
+    vt = torch.zeros_like(kt)
+    vt[..., :T] = v.transpose(-1, -2)
+    o = torch.zeros(B, T, Hkv * G * D, device=DEV, dtype=torch.bfloat16)
+    lse = torch.empty(B, Hkv, G, T, device=DEV)
+    native.flash_attn_fwd(q, k, vt, valid, o, lse=lse, q_start=q_start)
+    outs = {}
+    lib = native.lib()
+    try:
+        for var in (0, 1, 2):
+            lib.drl_flash_attn_bwd_set_variant(var)
+            dq = torch.full_like(q, float("nan"))
+            dk, dv = torch.empty_like(k), torch.empty_like(v)
+            native.flash_attn_bwd(q, k, kt, v, o, dout, lse, valid, dq, dk, dv, q_start=q_start)
+            outs[var] = (dq, dk, dv)
+    finally:
+        lib.drl_flash_attn_bwd_set_variant(0)
+    for var in (1, 2):
+        for a_, b_ in zip(outs[var], outs[0]):
+            assert torch.equal(a_, b_), var
