@@ -75,6 +75,8 @@ for step in "$@"; do
         || { tail -20 "$OUT/bench_${A[1]}.err"; exit 1; }
       cut -c1-900 "$OUT/bench_${A[1]}.json" ;;
     bench64) bench_rows 64 || exit 1 ;;
+    smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.txt" 2>&1 \
+             || { tail -20 "$OUT/smoke.txt"; exit 1; }; tail -3 "$OUT/smoke.txt" ;;
     bench128) bench_rows 128 || exit 1 ;;
     bench256) bench_rows 256 || exit 1 ;;
     profile)
@@ -82,6 +84,7 @@ for step in "$@"; do
         "$ROOT/bench.py" --steps 2 --warmup 2 --no-cpu-baseline > "$OUT/prof.log" 2>&1 || { tail -20 "$OUT/prof.log"; exit 1; }
       TR=$(find "$OUT/prof" -name "*kernel_trace.csv" | head -1)
       python3 tools/trace_summary.py "$TR" 30 > "$OUT/trace_summary.txt" || exit 1
+      python3 tools/decode_gaps.py "$TR" > "$OUT/decode_step_512rows.txt" 2>&1 || true
       python3 - "$TR" "$OUT/kernel_trace_min.csv.gz" <<'PYEOF' || exit 1
 import csv, gzip, sys
 with gzip.open(sys.argv[2], "wt") as f:
