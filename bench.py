@@ -75,9 +75,16 @@ def _gemm_sk_dispatches(a):
     """Kernel dispatches of one drl_gemm call (rocprof counts these; the KernelTimer counts calls): a layout-T operand
     past the 2 GB buffer range is split over K blocks, one dispatch each (csrc/gemm_sk.hip, drl_gemm); a layout-K A
     past it runs as one dispatch with its descriptor rebased per tile."""
+    from dots.rl_amd import _lib, native
+
     lda, a_layout, ldb, b_layout, M, N, K = a[1], a[2], a[4], a[5], a[10], a[11], a[12]
     lim = 1 << 31
     tb = [K * ld * 2 + 320 * ld * 2 if lay == 1 else 0 for lay, ld in ((a_layout, lda), (b_layout, ldb))]
+    # round 6: a layout-T A past the range (B within it, fp32 plain output, a whole-tile plan) walks its K blocks
+    # inside ONE launch (the lm_head weight gradient)
+    if (a_layout == 1 and tb[0] >= lim and tb[1] < lim and a[8] == _lib.DRL_F32 and a[14] == 0
+            and native.gemm_plan(M, N, K, 0)[0] == 2):
+        return 1
     if max(tb) >= lim:
         ld = max(lda if a_layout == 1 else 0, ldb if b_layout == 1 else 0)
         kb = max(128, (lim // (ld * 2) - 320) // 128 * 128)
