@@ -152,6 +152,7 @@ SIGNATURES = {
                                                F32, P, P, P, P]),
     "drl_decode_attention_vt_workspace_bytes": (SZ, [I64, I64, I64, I64]),
     "drl_decode_attention_set_plan": (None, [I32, I32]),
+    "drl_decode_group_set_plan": (None, [I32, I32, I32]),
     "drl_flash_attn_bwd_set_variant": (None, [I32]),
     "drl_decode_attention_vt": (ctypes.c_int, [P, P, P, I32, P, I64, P, I64, I64, I64, I64, I64, I64, I64, I64, I64,
                                                I64, F32, P, I64, P, SZ, P]),

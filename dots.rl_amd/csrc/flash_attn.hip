@@ -1179,6 +1179,7 @@ struct DecodeArgs {
   // prompt groups: sequences b = p * group + r (r < group) share one prompt, whose keys [0, shared) are read from
   // cache row p (the rollout prefills each distinct prompt once); group 1 / shared 0: every row reads its own
   int64_t group, shared;
+  int64_t rpt;  // decode_group_kernel: rows per column tile (0: 32 / G, every column of the MFMA tile in use)
 };
 
 // (sequence, KV head) of workgroup `bid` under prompt groups: the group's rows of one (prompt, head) run as
@@ -1635,7 +1636,7 @@ __global__ __launch_bounds__(64 * NW) void decode_mfma_kernel(DecodeArgs a) {
 // where every row holds its own copy of the prompt keys. Contract: the rows of a group have identical key-valid
 // bytes below `shared` (the rollout's KVCache.share_prompts copies them); the shared blocks' validity is read from
 // the group's first row. One block in flight per wave (the register-lean loop).
-template <int D, int NW>
+template <int D, int NW, int NB = 2>
 __global__ __launch_bounds__(64 * NW) void decode_group_kernel(DecodeArgs a) {
   constexpr int KS = D / 16, MT = D / 32;
   __shared__ float s_m[NW][32], s_l[NW][32];
@@ -1644,7 +1645,7 @@ __global__ __launch_bounds__(64 * NW) void decode_group_kernel(DecodeArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);  // scalar wave index
   const int qi = lane & 31, h = lane >> 5;
   const int G = static_cast<int>(a.G), group = static_cast<int>(a.group);
-  const int rpt = 32 / G, ntile = (group + rpt - 1) / rpt;
+  const int rpt = a.rpt > 0 ? static_cast<int>(a.rpt) : 32 / G, ntile = (group + rpt - 1) / rpt;
   const int64_t units = gridDim.x / ntile;
   int64_t unit, ct;
   if (units % 8 == 0) {  // the column tiles of one (prompt, head) on one XCD, back to back
@@ -1683,15 +1684,15 @@ __global__ __launch_bounds__(64 * NW) void decode_group_kernel(DecodeArgs a) {
                       a.ld_valid, 32 * ib, kend, lane, h, r);
     }
   };
-  DecRaw<D> R0, R1;  // two items in flight per wave (named registers: static indexing)
+  DecRaw<D> R[NB];  // NB items in flight per wave (static indexing: every use below is unrolled)
   uint16_t* kslot = reinterpret_cast<uint16_t*>(&s_o[w][0][0][0]);
   uint16_t* vslot = kslot + 32 * D;
   // every load below is unconditional (item indices clamped to the last item; a phantom item past the end is staged
   // and consumed as an all-invalid block): with a conditional refill hipcc cannot count the loads behind a register
-  // set and waits for every load in flight (vmcnt(0)) at each stage, one item in flight instead of two
+  // set and waits for every load in flight (vmcnt(0)) at each stage, one item in flight instead of NB
   if (items > 0) {
-    load(0, R0);
-    load(min(1, items - 1), R1);
+#pragma unroll
+    for (int j = 0; j < NB; ++j) load(min(j, items - 1), R[j]);
   }
   bf16x8 qf[KS];
   {
@@ -1717,14 +1718,15 @@ __global__ __launch_bounds__(64 * NW) void decode_group_kernel(DecodeArgs a) {
     // an own block takes part only in its row's columns; a phantom item (j >= items) in none
     const bool act = j < items && (j < n_sh || (j - n_sh) / n_own == rl);
     vbslot[lane] = act ? u32x4{R.vb[0], R.vb[1], R.vb[2], R.vb[3]} : u32x4{0u, 0u, 0u, 0u};
-    load(min(j + 2, items - 1), R);  // unconditional refill (past the end: the last item again)
+    load(min(j + NB, items - 1), R);  // unconditional refill (past the end: the last item again)
     const u32x4 v4 = vbslot[lane];
     const uint32_t vb[4] = {v4[0], v4[1], v4[2], v4[3]};
     dec_block_lds<D>(kslot, vslot, vb, qf, a.scale_log2, qi, h, m, lsum, o);
   };
-  for (int j = 0; j < items; j += 2) {
-    step(j, R0);
-    step(j + 1, R1);  // odd items: the last step is the phantom, an exact no-op on m / lsum / o (alpha = 1, p = 0)
+  for (int j = 0; j < items; j += NB) {
+    // items past the end are phantoms: an exact no-op on m / lsum / o (alpha = 1, p = 0)
+#pragma unroll
+    for (int i = 0; i < NB; ++i) step(j + i, R[i]);
   }
   // merge the NW waves' states per column in wave order (decode_mfma_kernel's non-split merge)
   const float lt = lsum + __shfl_xor(lsum, 32, kWave);
@@ -1763,6 +1765,194 @@ __global__ __launch_bounds__(64 * NW) void decode_group_kernel(DecodeArgs a) {
   }
 }
 
+// decode_group_kernel with the rows' own blocks balanced over the waves. There, wave w takes every own block of class
+// w (block index = w mod NW) for all the tile's rows: at 512 rows x 2 KV heads (4 rows per tile, 16 shared + 1..8 own
+// blocks, 8 waves) the waves holding an own class run 2 shared + 4 own items while the rest run 2, so the critical
+// path is 6 items at every cache length. Here a column's state per class is still built in the per-row kernel's order —
+// the class's shared blocks, then its own blocks — but the own part runs as units (class c, row r), dealt round-robin
+// over the waves after the shared phase: each wave leaves its class state in LDS after its shared items (one barrier),
+// a unit loads its class's state, runs row r's own blocks of that class (only row r's columns take part: every other
+// column sees all-invalid blocks, an exact no-op) and writes back row r's columns of the state. Units of one class touch
+// disjoint columns, so they may run on any waves in any order: the result is bit-identical to decode_group_kernel (and
+// the per-row kernel) at the same wave count, with 2 + ceil(4 * own / 8) items on the critical path instead of 6.
+template <int D, int NW, int NB = 2>
+__global__ __launch_bounds__(64 * NW) void decode_group_bal_kernel(DecodeArgs a) {
+  constexpr int KS = D / 16, MT = D / 32;
+  __shared__ __attribute__((aligned(16))) uint16_t s_stage[NW][64 * D];  // per wave: K [32][D], V^T [D][32]
+  __shared__ __attribute__((aligned(16))) float s_so[NW][MT][16][64];   // class states: O^T accumulators
+  __shared__ float s_sm[NW][64], s_sl[NW][64];                          // class states: running max / sum per lane
+  __shared__ __attribute__((aligned(16))) uint32_t s_vb[NW][4 * 64];
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int qi = lane & 31, h = lane >> 5;
+  const int G = static_cast<int>(a.G), group = static_cast<int>(a.group);
+  const int rpt = a.rpt > 0 ? static_cast<int>(a.rpt) : 32 / G, ntile = (group + rpt - 1) / rpt;
+  const int64_t units = gridDim.x / ntile;
+  int64_t unit, ct;
+  if (units % 8 == 0) {
+    const int64_t slot = blockIdx.x >> 3;
+    ct = slot % ntile;
+    unit = (slot / ntile) * 8 + (blockIdx.x & 7);
+  } else {
+    unit = blockIdx.x / ntile;
+    ct = blockIdx.x % ntile;
+  }
+  const int64_t p = unit / a.Hkv, hd = unit - p * a.Hkv;
+  const int nr = min(rpt, group - static_cast<int>(ct) * rpt);
+  const int rl = qi / G, g = qi - rl * G;
+  const bool col_ok = rl < nr;
+  const int64_t b0 = p * group + ct * rpt;
+  const int64_t bcol = b0 + (col_ok ? rl : 0);
+  const int qpos = static_cast<int>(a.qpos_ptr ? *a.qpos_ptr : a.qpos);
+  const int kend = static_cast<int>(min(a.L, static_cast<int64_t>(qpos) + 1));
+  const int64_t panel = vt_panel(a.ld_vt, D, a.ld_k);
+  const uint16_t* kbs = a.k + (p * a.Hkv + hd) * a.ld_k * D;
+  const uint16_t* vtbs = a.vt + (p * a.Hkv + hd) * panel;
+  const uint8_t* vrows = a.valid + p * group * a.ld_valid;
+  const int nall = (kend + 31) / 32, nsh = min(static_cast<int>(a.shared / 32), nall);
+  const int n_sh = nsh > w ? (nsh - w + NW - 1) / NW : 0;  // shared blocks of class w
+  const int nown = nall - nsh;                              // own blocks of every row
+  const int nunits = min(nown, NW) * nr;                    // unit u: class index u / nr (class (nsh + u / nr) % NW)
+  // own blocks of the class with index j: nsh + j, nsh + j + NW, ...
+  auto unit_items = [&](int u) { return (nown - u / nr + NW - 1) / NW; };
+  int n_oi = 0;
+  for (int u = w; u < nunits; u += NW) n_oi += unit_items(u);
+  const int items = n_sh + n_oi;
+  // own item jj of this wave -> its unit and its place in the unit (scalar walk over the wave's few units)
+  auto locate = [&](int jj, int& u) {
+    u = w;
+    for (;;) {
+      const int n = unit_items(u);
+      if (jj < n) break;
+      jj -= n;
+      u += NW;
+    }
+    return jj;
+  };
+  auto load = [&](int j, DecRaw<D>& r) {
+    if (j < n_sh) {
+      dec_load_raw<D>(kbs, vtbs, vrows, a.ld_vt, a.ld_valid, 32 * (w + j * NW), kend, lane, h, r);
+    } else {
+      int u;
+      const int i = locate(j - n_sh, u);
+      const int jc = u / nr, rr = u - jc * nr;
+      const int64_t bh = (b0 + rr) * a.Hkv + hd;
+      dec_load_raw<D>(a.k + bh * a.ld_k * D, a.vt + bh * panel, a.valid + (b0 + rr) * a.ld_valid, a.ld_vt,
+                      a.ld_valid, 32 * (nsh + jc + NW * i), kend, lane, h, r);
+    }
+  };
+  DecRaw<D> R[NB];
+  uint16_t* kslot = &s_stage[w][0];
+  uint16_t* vslot = kslot + 32 * D;
+  if (items > 0) {
+#pragma unroll
+    for (int j = 0; j < NB; ++j) load(min(j, items - 1), R[j]);
+  }
+  bf16x8 qf[KS];
+  {
+    const uint16_t* qrow = a.q + ((bcol * a.Hkv + hd) * a.G + g) * D + 8 * h;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      u16x8 v = *reinterpret_cast<const u16x8*>(qrow + 16 * s);
+      if (!col_ok) v = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      qf[s] = as_bf16x8(v);
+    }
+  }
+  f32x16 o[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) o[mt] = f32x16{};
+  float m = -INFINITY, lsum = 0.f;
+  auto save = [&](int cls) {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s_so[cls][mt][r][lane] = o[mt][r];
+    s_sm[cls][lane] = m;
+    s_sl[cls][lane] = lsum;
+  };
+  auto restore = [&](int cls) {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[mt][r] = s_so[cls][mt][r][lane];
+    m = s_sm[cls][lane];
+    lsum = s_sl[cls][lane];
+  };
+  // every wave: its class state after its shared items -> LDS, then one barrier (raw s_barrier: a __syncthreads fence
+  // would drain the loads in flight)
+  bool crossed = false;
+  auto cross = [&] {
+    save(w);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    crossed = true;
+  };
+  int cur_u = -1;
+  u32x4* vbslot = reinterpret_cast<u32x4*>(&s_vb[w][0]);
+  auto step = [&](int j, DecRaw<D>& R) {
+    int row = -1, cls = 0;
+    bool last = false;
+    if (j >= n_sh && j < items) {
+      if (!crossed) cross();
+      int u;
+      const int i = locate(j - n_sh, u);
+      const int jc = u / nr;
+      row = u - jc * nr;
+      cls = (nsh + jc) % NW;
+      if (u != cur_u) {  // the unit's first item: its class state (the previous unit was written back)
+        restore(cls);
+        cur_u = u;
+      }
+      last = i == unit_items(u) - 1;
+    }
+    dec_fix_tail<D>(R, kend, a.ld_valid, lane, h);
+    dec_stage<D>(R, kslot, vslot, lane);
+    const bool act = j < items && (row < 0 || row == rl);
+    vbslot[lane] = act ? u32x4{R.vb[0], R.vb[1], R.vb[2], R.vb[3]} : u32x4{0u, 0u, 0u, 0u};
+    load(min(j + NB, items - 1), R);
+    const u32x4 v4 = vbslot[lane];
+    const uint32_t vb[4] = {v4[0], v4[1], v4[2], v4[3]};
+    dec_block_lds<D>(kslot, vslot, vb, qf, a.scale_log2, qi, h, m, lsum, o);
+    if (last && rl == row) save(cls);  // row `row`'s columns of the class state
+  };
+  for (int j = 0; j < items; j += NB) {
+#pragma unroll
+    for (int i = 0; i < NB; ++i) step(j + i, R[i]);
+  }
+  if (!crossed) cross();
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  if (!col_ok) return;
+  // merge the NW class states per column in class order (decode_group_kernel's merge)
+  float mm = -INFINITY;
+#pragma unroll
+  for (int v = 0; v < NW; ++v) mm = fmaxf(mm, s_sm[v][qi]);
+  const float mref = mm == -INFINITY ? 0.f : mm;
+  float sc[NW], ll = 0.f;
+#pragma unroll
+  for (int v = 0; v < NW; ++v) {
+    sc[v] = __builtin_amdgcn_exp2f(s_sm[v][qi] - mref);
+    ll += (s_sl[v][qi] + s_sl[v][qi + 32]) * sc[v];
+  }
+  const float inv = ll > 0.f ? 1.f / ll : 0.f;
+  const int64_t bh = bcol * a.Hkv + hd;
+  const int64_t kq = (hd * a.G + g) * D;
+  for (int gg = w; gg < 4 * MT; gg += NW) {
+    const int mt = gg >> 2, c = gg & 3;
+    u16x4 wv;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float acc = 0.f;
+#pragma unroll
+      for (int v = 0; v < NW; ++v) acc = fmaf(s_so[v][mt][4 * c + j][lane], sc[v], acc);
+      wv[j] = to_bf16_bits(acc * inv);
+    }
+    const int64_t k = kq + 32 * mt + 8 * c + 4 * h;
+    *reinterpret_cast<u16x4*>(dec_out_ptr(a, bcol, k, (bh * a.G + g) * D + 32 * mt + 8 * c + 4 * h)) = wv;
+  }
+}
+
 }  // namespace
 
 int g_dec_nw = 0, g_dec_splits = 0;  // tuning override (drl_decode_attention_set_plan), 0 = automatic
@@ -1770,6 +1960,11 @@ int g_dq_variant = 0;  // drl_flash_attn_bwd_set_variant: 0 = one query tile per
                        // registers), 2 = two tiles re-reading K / V from LDS. The two-tile kernel measured slower
                        // (update shape: 1227 -> 1474 us per backward, profiles/r06_flash_dq_two_tiles_rejected.jsonl):
                        // 333 registers per lane, one wave per SIMD, where the one-tile kernel runs two workgroups per CU
+// drl_decode_group_set_plan: rows per column tile (0 = 32 / G). Items in flight per wave: 2 (3 or 4 spill at 8 waves
+// and measured 1.5-3x slower; fewer rows per tile re-read the shared blocks per tile and measured slower too:
+// profiles/r06_decode_group_sweep.jsonl)
+int g_grp_rpt = 0;
+int g_grp_bal = -1;               // drl_decode_group_set_plan: own blocks balanced over the waves (-1 = automatic)
 int g_dec_variant = 0;  // drl_decode_attention_set_variant: 1 = one block in flight (LDS fragments), 2..4 = ring depth
 
 // key splits for decode attention. Measured (tools/kernel_bench.py --only decode_sweep, B 64..512,
@@ -1880,6 +2075,12 @@ void drl_decode_attention_set_variant(int32_t variant) {
   drl::g_dec_variant = (variant >= 1 && variant <= 4) ? variant : 0;
 }
 
+void drl_decode_group_set_plan(int32_t rows_per_tile, int32_t depth, int32_t balanced) {
+  drl::g_grp_rpt = rows_per_tile >= 1 && rows_per_tile <= 32 ? rows_per_tile : 0;
+  (void)depth;
+  drl::g_grp_bal = balanced == 0 || balanced == 1 ? balanced : -1;
+}
+
 void drl_decode_attention_set_plan(int32_t waves, int32_t splits) {
   drl::g_dec_nw = (waves == 2 || waves == 4 || waves == 8 || waves == 16) ? waves : 0;
   drl::g_dec_splits = (splits >= 1 && splits <= 16) ? splits : 0;
@@ -1920,8 +2121,8 @@ int drl_decode_attention_vt(const void* q, const void* k_cache, const void* vt_c
                scale * 1.4426950408889634f, static_cast<uint16_t*>(out), out_mbt, nullptr, nullptr, group,
                shared_keys};
   hipStream_t s = static_cast<hipStream_t>(stream);
-  const int rpt = static_cast<int>(32 / G), ntile = static_cast<int>((group + rpt - 1) / rpt);
-  if (group > 1 && shared_keys > 0 && B / group * Hkv * ntile * 2 >= cu_count()) {
+  const int rpt0 = static_cast<int>(32 / G), ntile0 = static_cast<int>((group + rpt0 - 1) / rpt0);
+  if (group > 1 && shared_keys > 0 && B / group * Hkv * ntile0 * 2 >= cu_count()) {
     // prompt groups: one workgroup per (prompt, KV head, column tile of 32 / G rows), each shared block loaded once
     // per tile (decode_group_kernel); bit-identical to the per-row kernel at the same wave count without splits.
     // 8 waves (D = 64; 4 at D = 128) so a workgroup's key blocks are spread over as many in-flight loads as the
@@ -1931,8 +2132,16 @@ int drl_decode_attention_vt(const void* q, const void* k_cache, const void* vt_c
     const int nwg = g_dec_nw ? g_dec_nw : (D == 64 ? 8 : 4);
     DRL_CHECK_ARG(D == 64 ? (nwg == 2 || nwg == 4 || nwg == 8 || nwg == 16) : (nwg == 2 || nwg == 4),
                   "prompt-group decode attention: %d waves at head_dim %lld", nwg, (long long)D);
+    const int rpt = g_grp_rpt ? std::min(g_grp_rpt, rpt0) : rpt0, ntile = static_cast<int>((group + rpt - 1) / rpt);
+    a.rpt = rpt;
     const dim3 g_(static_cast<unsigned>(B / group * Hkv * ntile)), b_(64 * nwg);
-    if (D == 64) {
+    const bool bal = g_grp_bal != 0;
+    if (bal && D == 64 && (nwg == 4 || nwg == 8)) {
+      if (nwg == 4) hipLaunchKernelGGL((decode_group_bal_kernel<64, 4>), g_, b_, 0, s, a);
+      else hipLaunchKernelGGL((decode_group_bal_kernel<64, 8>), g_, b_, 0, s, a);
+    } else if (bal && D == 128 && nwg == 4) {
+      hipLaunchKernelGGL((decode_group_bal_kernel<128, 4>), g_, b_, 0, s, a);
+    } else if (D == 64) {
       if (nwg == 2) hipLaunchKernelGGL((decode_group_kernel<64, 2>), g_, b_, 0, s, a);
       else if (nwg == 4) hipLaunchKernelGGL((decode_group_kernel<64, 4>), g_, b_, 0, s, a);
       else if (nwg == 8) hipLaunchKernelGGL((decode_group_kernel<64, 8>), g_, b_, 0, s, a);

@@ -27,9 +27,13 @@ def _blocked(vt_plain, cap):
     return out.view(B, Hkv, D, nb, 32).permute(0, 1, 3, 2, 4).contiguous()
 
 
-# (B, group, Hkv, G, D, cap, L, shared): 512 rows in groups of 8 (the bench: XCD-grouped mapping, 128 units);
-# 12 rows in groups of 4 over 2 heads (6 units: the plain mapping); a small grid (split plan); head_dim 128
+# (B, group, Hkv, G, D, cap, L, shared): 512 rows in groups of 8 (the bench: XCD-grouped mapping, 128 units); the same
+# with 24 own blocks per row (3 per class: multi-block units of the balanced schedule) and with 5 shared blocks (waves
+# without a shared item); 12 rows in groups of 4 over 2 heads (6 units: the plain mapping); a small grid (split plan);
+# head_dim 128
 @pytest.mark.parametrize("B,group,Hkv,G,D,cap,L,shared", [(512, 8, 2, 7, 64, 768, 640, 512),
+                                                          (512, 8, 2, 7, 64, 1024, 1000, 256),
+                                                          (512, 8, 2, 7, 64, 400, 390, 160),
                                                           (12, 4, 2, 7, 64, 300, 290, 96),
                                                           (8, 4, 1, 8, 64, 2048, 2000, 1024),
                                                           (16, 2, 4, 4, 128, 200, 170, 160)])
@@ -59,19 +63,23 @@ def test_decode_attention_prompt_groups_equal_expanded(B, group, Hkv, G, D, cap,
     vb, vbg = _blocked(vt, cap), _blocked(vtg, cap)
     qp = torch.tensor([L - 3], device=DEV)
     lib = native.lib()
-    # the grouped kernel (decode_group_kernel) runs the per-row kernel's arithmetic at its wave count without key
-    # splits: 8 waves at head_dim 64, 4 at 128 by default; forced plans apply to both
+    # the grouped kernels (decode_group_kernel: own blocks by block class; decode_group_bal_kernel: own blocks balanced
+    # over the waves through class states in LDS) run the per-row kernel's arithmetic at its wave count without key
+    # splits: 8 waves at head_dim 64, 4 at 128 by default; forced plans apply to both; 2 rows per column tile as well
     try:
         for nw in ((0, 2, 4, 16) if D == 64 else (0, 2)):
             for kw in ({}, {"qpos_dev": qp}):
                 lib.drl_decode_attention_set_plan(nw or (8 if D == 64 else 4), 1)
                 a = native.decode_attention_vt(q, k, vb, valid[:, :cap], L, torch.empty_like(q), **kw)
                 lib.drl_decode_attention_set_plan(nw, 0)
-                b = native.decode_attention_vt(q, kg, vbg, vg[:, :cap], L, torch.empty_like(q), group=group,
-                                               shared_keys=shared, **kw)
-                assert torch.equal(a, b), (nw, kw)
+                for bal, rpt in ((0, 0), (1, 0), (1, 2)):
+                    lib.drl_decode_group_set_plan(rpt, 0, bal)
+                    b = native.decode_attention_vt(q, kg, vbg, vg[:, :cap], L, torch.empty_like(q), group=group,
+                                                   shared_keys=shared, **kw)
+                    assert torch.equal(a, b), (nw, kw, bal, rpt)
     finally:
         lib.drl_decode_attention_set_plan(0, 0)
+        lib.drl_decode_group_set_plan(0, 0, -1)
     # and close to the per-row kernel's own default plan (another wave count / key split: another fp32 order)
     a = native.decode_attention_vt(q, k, vb, valid[:, :cap], L, torch.empty_like(q))
     b = native.decode_attention_vt(q, kg, vbg, vg[:, :cap], L, torch.empty_like(q), group=group, shared_keys=shared)
