@@ -1180,16 +1180,30 @@ struct DecodeArgs {
   // cache row p (the rollout prefills each distinct prompt once); group 1 / shared 0: every row reads its own
   int64_t group, shared;
   int64_t rpt;  // decode_group_kernel: rows per column tile (0: 32 / G, every column of the MFMA tile in use)
+  int64_t xmap;  // workgroup -> XCD placement: 0 = units dealt round-robin over the XCDs, 1 = a contiguous eighth of the
+                 // units (and so of the cache rows and their pages) per XCD
 };
+
+// workgroup bid's index in an XCD-major order (xmap 1): the dispatcher deals consecutive workgroups to the 8 XCDs in turn
+// (MI355X_MICROARCH.md, workgroup dispatch), so XCD x runs bid = x, x + 8, ...; renumbered, XCD x takes indices
+// [x * total / 8, (x + 1) * total / 8)
+__device__ __forceinline__ int64_t dec_xcd_major(int64_t bid, int64_t total) {
+  return (bid & 7) * (total >> 3) + (bid >> 3);
+}
 
 // (sequence, KV head) of workgroup `bid` under prompt groups: the group's rows of one (prompt, head) run as
 // workgroups bid, bid + 8, ..., i.e. on one XCD under the observed round-robin dealing (MI355X_MICROARCH.md,
 // workgroup dispatch), next to each other in time, so the shared prompt keys one of them fetches are L2 hits for
 // the others (speed only: any placement gives the same result)
-__device__ __forceinline__ int64_t dec_grouped_bh(int64_t bid, int64_t group, int64_t Hkv, int64_t total) {
+__device__ __forceinline__ int64_t dec_grouped_bh(int64_t bid, int64_t group, int64_t Hkv, int64_t total,
+                                                  int64_t xmap = 0) {
   const int64_t units = total / group;
   int64_t u, r;
-  if (units % 8 == 0) {
+  if (xmap && total % 8 == 0) {
+    const int64_t idx = dec_xcd_major(bid, total);
+    u = idx / group;
+    r = idx % group;
+  } else if (units % 8 == 0) {
     const int64_t slot = bid >> 3;
     r = slot % group;
     u = (slot / group) * 8 + (bid & 7);
@@ -1437,7 +1451,8 @@ __global__ __launch_bounds__(64 * NW) void decode_mfma_kernel(DecodeArgs a) {
   __shared__ __attribute__((aligned(16))) float s_o[NW][MT][16][64];
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);  // scalar wave index
   const int qi = lane & 31, h = lane >> 5;
-  const int64_t bh = a.group > 1 ? dec_grouped_bh(blockIdx.x, a.group, a.Hkv, gridDim.x) : blockIdx.x;
+  const int64_t bh = a.group > 1 ? dec_grouped_bh(blockIdx.x, a.group, a.Hkv, gridDim.x, a.xmap)
+                                 : (a.xmap && gridDim.x % 8 == 0 ? dec_xcd_major(blockIdx.x, gridDim.x) : blockIdx.x);
   const int64_t b = bh / a.Hkv;
   const int qpos = static_cast<int>(a.qpos_ptr ? *a.qpos_ptr : a.qpos);
   const int kend = static_cast<int>(min(a.L, static_cast<int64_t>(qpos) + 1));
@@ -1648,7 +1663,11 @@ __global__ __launch_bounds__(64 * NW) void decode_group_kernel(DecodeArgs a) {
   const int rpt = a.rpt > 0 ? static_cast<int>(a.rpt) : 32 / G, ntile = (group + rpt - 1) / rpt;
   const int64_t units = gridDim.x / ntile;
   int64_t unit, ct;
-  if (units % 8 == 0) {  // the column tiles of one (prompt, head) on one XCD, back to back
+  if (a.xmap && gridDim.x % 8 == 0) {
+    const int64_t idx = dec_xcd_major(blockIdx.x, gridDim.x);
+    unit = idx / ntile;
+    ct = idx % ntile;
+  } else if (units % 8 == 0) {  // the column tiles of one (prompt, head) on one XCD, back to back
     const int64_t slot = blockIdx.x >> 3;
     ct = slot % ntile;
     unit = (slot / ntile) * 8 + (blockIdx.x & 7);
@@ -1788,7 +1807,11 @@ __global__ __launch_bounds__(64 * NW) void decode_group_bal_kernel(DecodeArgs a)
   const int rpt = a.rpt > 0 ? static_cast<int>(a.rpt) : 32 / G, ntile = (group + rpt - 1) / rpt;
   const int64_t units = gridDim.x / ntile;
   int64_t unit, ct;
-  if (units % 8 == 0) {
+  if (a.xmap && gridDim.x % 8 == 0) {
+    const int64_t idx = dec_xcd_major(blockIdx.x, gridDim.x);
+    unit = idx / ntile;
+    ct = idx % ntile;
+  } else if (units % 8 == 0) {
     const int64_t slot = blockIdx.x >> 3;
     ct = slot % ntile;
     unit = (slot / ntile) * 8 + (blockIdx.x & 7);
@@ -1964,6 +1987,7 @@ int g_dq_variant = 0;  // drl_flash_attn_bwd_set_variant: 0 = one query tile per
 // and measured 1.5-3x slower; fewer rows per tile re-read the shared blocks per tile and measured slower too:
 // profiles/r06_decode_group_sweep.jsonl)
 int g_grp_rpt = 0;
+int g_dec_xmap = 0;  // drl_decode_group_set_plan: workgroup -> XCD placement of the decode attention (DecodeArgs::xmap)
 int g_grp_bal = -1;               // drl_decode_group_set_plan: own blocks balanced over the waves (-1 = automatic)
 int g_dec_variant = 0;  // drl_decode_attention_set_variant: 1 = one block in flight (LDS fragments), 2..4 = ring depth
 
@@ -2075,9 +2099,9 @@ void drl_decode_attention_set_variant(int32_t variant) {
   drl::g_dec_variant = (variant >= 1 && variant <= 4) ? variant : 0;
 }
 
-void drl_decode_group_set_plan(int32_t rows_per_tile, int32_t depth, int32_t balanced) {
+void drl_decode_group_set_plan(int32_t rows_per_tile, int32_t xcd_map, int32_t balanced) {
   drl::g_grp_rpt = rows_per_tile >= 1 && rows_per_tile <= 32 ? rows_per_tile : 0;
-  (void)depth;
+  drl::g_dec_xmap = xcd_map == 1 ? 1 : 0;
   drl::g_grp_bal = balanced == 0 || balanced == 1 ? balanced : -1;
 }
 
@@ -2119,7 +2143,7 @@ int drl_decode_attention_vt(const void* q, const void* k_cache, const void* vt_c
   DecodeArgs a{static_cast<const uint16_t*>(q), static_cast<const uint16_t*>(k_cache),
                static_cast<const uint16_t*>(vt_cache), key_valid, ld_valid, qpos_ptr, qpos, Hkv, G, ld_k, ld_vt, L,
                scale * 1.4426950408889634f, static_cast<uint16_t*>(out), out_mbt, nullptr, nullptr, group,
-               shared_keys};
+               shared_keys, 0, g_dec_xmap};
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int rpt0 = static_cast<int>(32 / G), ntile0 = static_cast<int>((group + rpt0 - 1) / rpt0);
   if (group > 1 && shared_keys > 0 && B / group * Hkv * ntile0 * 2 >= cu_count()) {
@@ -2135,7 +2159,10 @@ int drl_decode_attention_vt(const void* q, const void* k_cache, const void* vt_c
     const int rpt = g_grp_rpt ? std::min(g_grp_rpt, rpt0) : rpt0, ntile = static_cast<int>((group + rpt - 1) / rpt);
     a.rpt = rpt;
     const dim3 g_(static_cast<unsigned>(B / group * Hkv * ntile)), b_(64 * nwg);
-    const bool bal = g_grp_bal != 0;
+    // balanced own blocks: bit-identical but measured slower at every cache length of the bench (512 rows, L 520..767:
+    // 13.3 / 14.2 / 15.3 / 20.4 / 22.1 against 13.1 / 13.6 / 12.9 / 18.0 / 20.1 us, profiles/r06_decode_group_sweep.jsonl):
+    // the items on a wave's path are not what bounds the call; on request only
+    const bool bal = g_grp_bal == 1;
     if (bal && D == 64 && (nwg == 4 || nwg == 8)) {
       if (nwg == 4) hipLaunchKernelGGL((decode_group_bal_kernel<64, 4>), g_, b_, 0, s, a);
       else hipLaunchKernelGGL((decode_group_bal_kernel<64, 8>), g_, b_, 0, s, a);

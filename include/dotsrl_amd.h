@@ -468,10 +468,11 @@ int drl_decode_step_prologue(const int64_t* responses, int64_t ld_responses, int
                              int64_t ld_valid, void* workspace, size_t workspace_bytes, int64_t x_mbt, void* stream);
 /* Tuning hook (tools/kernel_bench.py): force waves per workgroup (2/4/8/16) and key splits; 0 = automatic. */
 void drl_decode_attention_set_plan(int32_t waves, int32_t splits);
-/* Tuning hook of the prompt-group decode attention (ABI 8): rows per column tile (1..32 / G; 0 = 32 / G) and the
- * own-block schedule (1 = balanced over the waves, 0 = by block class, -1 = automatic); depth is reserved (2 items in
- * flight per wave). Results are identical for every plan. */
-void drl_decode_group_set_plan(int32_t rows_per_tile, int32_t depth, int32_t balanced);
+/* Tuning hook of the decode attention's work placement (ABI 8): rows per column tile of the prompt-group kernel
+ * (1..32 / G; 0 = 32 / G), workgroup -> XCD map of both kernels (0 = units round-robin over the XCDs, 1 = a contiguous
+ * eighth of the cache rows per XCD) and the prompt-group kernel's own-block schedule (1 = balanced over the waves,
+ * 0 = by block class, -1 = automatic). Results are identical for every plan. */
+void drl_decode_group_set_plan(int32_t rows_per_tile, int32_t xcd_map, int32_t balanced);
 /* Tuning hook of the fused attention backward (head_dim 64): 0 = dQ over one query tile per workgroup (default),
  * 1 = two query tiles per workgroup (K / V fragments in registers), 2 = two tiles re-reading them. Same bits. */
 void drl_flash_attn_bwd_set_variant(int32_t variant);

@@ -72,11 +72,11 @@ def test_decode_attention_prompt_groups_equal_expanded(B, group, Hkv, G, D, cap,
                 lib.drl_decode_attention_set_plan(nw or (8 if D == 64 else 4), 1)
                 a = native.decode_attention_vt(q, k, vb, valid[:, :cap], L, torch.empty_like(q), **kw)
                 lib.drl_decode_attention_set_plan(nw, 0)
-                for bal, rpt in ((0, 0), (1, 0), (1, 2)):
-                    lib.drl_decode_group_set_plan(rpt, 0, bal)
+                for bal, rpt, xmap in ((0, 0, 0), (1, 0, 0), (1, 2, 0), (0, 0, 1)):
+                    lib.drl_decode_group_set_plan(rpt, xmap, bal)
                     b = native.decode_attention_vt(q, kg, vbg, vg[:, :cap], L, torch.empty_like(q), group=group,
                                                    shared_keys=shared, **kw)
-                    assert torch.equal(a, b), (nw, kw, bal, rpt)
+                    assert torch.equal(a, b), (nw, kw, bal, rpt, xmap)
     finally:
         lib.drl_decode_attention_set_plan(0, 0)
         lib.drl_decode_group_set_plan(0, 0, -1)
