@@ -120,9 +120,22 @@ __device__ __forceinline__ float red_sum(const float (*red)[MB][16][64], int blk
 // Epilogues of the one-round-trip kernels, from the partial tiles of NW waves in LDS (tile = the 32-row weight block,
 // ks = the K slice, mb0 = the first token block). C row i (weight row of the block) <-> register (i & 3) + 4 (i >> 3),
 // lane half (i >> 2) & 1; column = token.
+// the RoPE epilogue's per-thread operands, loaded with the kernel's first loads instead of behind the reduction: the
+// key offset, the two bias values of the thread's column pair (the column is the same in every iteration: 256 threads,
+// 16 columns) and, per iteration, the cos / sin of its token's position — issued as soon as the positions land, so
+// their round trip runs under the MFMAs and the reduction (inline, the epilogue's dependent pos -> cos / sin loads were
+// two memory round trips per iteration after the reduction)
+template <int MB>
+struct RopePre {
+  int64_t koff;
+  float b1, b2;
+  float cs[2 * MB], sn[2 * MB];
+};
+
 template <int NW, int MB, int EPI>
 __device__ __forceinline__ void red_epilogue(const DgArgs& a, const float (*red)[MB][16][64], int tile, int ks, int mb0,
-                                             int tid, const float4* xres = nullptr) {
+                                             int tid, const float4* xres = nullptr,
+                                             const RopePre<MB>* pre = nullptr) {
   constexpr int NT = 64 * NW;
   if constexpr (EPI == EPI_PARTIAL) {
     for (int e = tid; e < 1024 * MB; e += NT) {
@@ -136,8 +149,10 @@ __device__ __forceinline__ void red_epilogue(const DgArgs& a, const float (*red)
     // rows 0..15: d = 16 qq + c of head hd, rows 16..31 its partners d + D/2. qkv = bf16(acc + bias), then
     // rope_qkv_fwd_kernel's rotation (q, k heads) and the cache writes at the device key offset koff
     const int half = a.D / 2, per = half / 16, hd = tile / per, qq = tile % per;
-    const int64_t koff = *a.koff_dev;
-    for (int e = tid; e < 512 * MB; e += NT) {
+    const int64_t koff = pre ? pre->koff : *a.koff_dev;
+#pragma unroll
+    for (int it = 0; it < 512 * MB / NT; ++it) {
+      const int e = tid + NT * it;
       const int tl = e >> 4, c = e & 15, blk = tl >> 5, ml = tl & 31;
       const int m = (mb0 + blk) * 32 + ml;
       if (m >= a.M) continue;
@@ -146,12 +161,19 @@ __device__ __forceinline__ void red_epilogue(const DgArgs& a, const float (*red)
       const int q2 = (i2 & 3) + 4 * (i2 >> 3), l2 = ml + 32 * ((i2 >> 2) & 1);
       const int d1 = 16 * qq + c, d2 = d1 + half;
       const int n1 = hd * a.D + d1, n2 = n1 + half;
-      const float x1 = bf16r(red_sum<NW, MB>(red, blk, q1, l1) + bf16_to_f32(a.bias[n1]));
-      const float x2 = bf16r(red_sum<NW, MB>(red, blk, q2, l2) + bf16_to_f32(a.bias[n2]));
+      const float x1 = bf16r(red_sum<NW, MB>(red, blk, q1, l1) + (pre ? pre->b1 : bf16_to_f32(a.bias[n1])));
+      const float x2 = bf16r(red_sum<NW, MB>(red, blk, q2, l2) + (pre ? pre->b2 : bf16_to_f32(a.bias[n2])));
       if (hd < a.Hq + a.Hkv) {
-        int64_t p = a.pos[m];
-        p = p < 0 ? 0 : (p >= a.maxpos ? a.maxpos - 1 : p);
-        const float cs = a.cos_t[p * half + d1], sn = a.sin_t[p * half + d1];
+        float cs, sn;
+        if (pre) {
+          cs = pre->cs[it];
+          sn = pre->sn[it];
+        } else {
+          int64_t p = a.pos[m];
+          p = p < 0 ? 0 : (p >= a.maxpos ? a.maxpos - 1 : p);
+          cs = a.cos_t[p * half + d1];
+          sn = a.sin_t[p * half + d1];
+        }
         const float o1 = fmaf(x1, cs, -(x2 * sn)), o2 = fmaf(x2, cs, x1 * sn);
         uint16_t* dst;
         if (hd < a.Hq) {
@@ -272,7 +294,34 @@ __global__ __launch_bounds__(256) void decode_gemm_kernel(DgArgs a) {
                                     : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
+  RopePre<MB> pre;
+  int64_t posv[2 * MB];
+  if constexpr (EPI == EPI_ROPE) {  // the epilogue's operands with the first loads (RopePre)
+    const int per = a.D / 32, c = tid & 15, d1 = 16 * (tile % per) + c, n1 = (tile / per) * a.D + d1;
+    pre.koff = *a.koff_dev;
+    pre.b1 = bf16_to_f32(a.bias[n1]);
+    pre.b2 = bf16_to_f32(a.bias[n1 + a.D / 2]);
+#pragma unroll
+    for (int it = 0; it < 2 * MB; ++it) {
+      const int tl = (tid + 256 * it) >> 4, m = (mb0 + (tl >> 5)) * 32 + (tl & 31);
+      posv[it] = a.pos[m < a.M ? m : 0];
+    }
+  }
   __builtin_amdgcn_sched_barrier(0);  // every load of the wave is in flight before the first MFMA
+  if constexpr (EPI == EPI_ROPE) {
+    // cos / sin as soon as the positions land (after the operand loads: the MFMAs below wait for those anyway)
+    const int half = a.D / 2, per = half / 16, hd = tile / per, d1 = 16 * (tile % per) + (tid & 15);
+    if (hd < a.Hq + a.Hkv) {
+#pragma unroll
+      for (int it = 0; it < 2 * MB; ++it) {
+        int64_t p = posv[it];
+        p = p < 0 ? 0 : (p >= a.maxpos ? a.maxpos - 1 : p);
+        pre.cs[it] = a.cos_t[p * half + d1];
+        pre.sn[it] = a.sin_t[p * half + d1];
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
   f32x16 acc[MB];
 #pragma unroll
   for (int i = 0; i < MB; ++i) acc[i] = f32x16{};
@@ -286,7 +335,7 @@ __global__ __launch_bounds__(256) void decode_gemm_kernel(DgArgs a) {
 #pragma unroll
     for (int q = 0; q < 16; ++q) red[wave][i][q][lane] = acc[i][q];
   __syncthreads();
-  red_epilogue<4, MB, EPI>(a, red, tile, ks, mb0, tid, xres);
+  red_epilogue<4, MB, EPI>(a, red, tile, ks, mb0, tid, xres, EPI == EPI_ROPE ? &pre : nullptr);
 }
 
 // The decode RMSNorm folded into its consumer GEMM's prologue (round 6; replaces the dec_rmsnorm launch before qkv +

@@ -1187,32 +1187,33 @@ struct DecodeArgs {
 // workgroup bid's index in an XCD-major order (xmap 1): the dispatcher deals consecutive workgroups to the 8 XCDs in turn
 // (MI355X_MICROARCH.md, workgroup dispatch), so XCD x runs bid = x, x + 8, ...; renumbered, XCD x takes indices
 // [x * total / 8, (x + 1) * total / 8)
-__device__ __forceinline__ int64_t dec_xcd_major(int64_t bid, int64_t total) {
-  return (bid & 7) * (total >> 3) + (bid >> 3);
+__device__ __forceinline__ unsigned dec_xcd_major(unsigned bid, unsigned total) {
+  return (bid & 7u) * (total >> 3) + (bid >> 3);
 }
 
 // (sequence, KV head) of workgroup `bid` under prompt groups: the group's rows of one (prompt, head) run as
 // workgroups bid, bid + 8, ..., i.e. on one XCD under the observed round-robin dealing (MI355X_MICROARCH.md,
 // workgroup dispatch), next to each other in time, so the shared prompt keys one of them fetches are L2 hits for
-// the others (speed only: any placement gives the same result)
-__device__ __forceinline__ int64_t dec_grouped_bh(int64_t bid, int64_t group, int64_t Hkv, int64_t total,
+// the others (speed only: any placement gives the same result). 32-bit arithmetic: a 64-bit division is a software
+// routine of ~100 instructions, and this mapping runs before the first load of every workgroup
+__device__ __forceinline__ int64_t dec_grouped_bh(unsigned bid, unsigned group, unsigned Hkv, unsigned total,
                                                   int64_t xmap = 0) {
-  const int64_t units = total / group;
-  int64_t u, r;
-  if (xmap && total % 8 == 0) {
-    const int64_t idx = dec_xcd_major(bid, total);
+  const unsigned units = total / group;
+  unsigned u, r;
+  if (xmap && total % 8u == 0) {
+    const unsigned idx = dec_xcd_major(bid, total);
     u = idx / group;
     r = idx % group;
-  } else if (units % 8 == 0) {
-    const int64_t slot = bid >> 3;
+  } else if (units % 8u == 0) {
+    const unsigned slot = bid >> 3;
     r = slot % group;
-    u = (slot / group) * 8 + (bid & 7);
+    u = (slot / group) * 8u + (bid & 7u);
   } else {
     u = bid / group;
     r = bid % group;
   }
-  const int64_t p = u / Hkv, hd = u - p * Hkv;
-  return (p * group + r) * Hkv + hd;
+  const unsigned p = u / Hkv, hd = u - p * Hkv;
+  return (static_cast<int64_t>(p) * group + r) * Hkv + hd;
 }
 
 // one 32-key block of the cache for lane (qi, h): K rows (A operand of S^T = K Q^T), V^T columns
@@ -1451,36 +1452,45 @@ __global__ __launch_bounds__(64 * NW) void decode_mfma_kernel(DecodeArgs a) {
   __shared__ __attribute__((aligned(16))) float s_o[NW][MT][16][64];
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);  // scalar wave index
   const int qi = lane & 31, h = lane >> 5;
-  const int64_t bh = a.group > 1 ? dec_grouped_bh(blockIdx.x, a.group, a.Hkv, gridDim.x, a.xmap)
+  const unsigned hkv32 = static_cast<unsigned>(a.Hkv), grp32 = static_cast<unsigned>(a.group);
+  const int64_t bh = a.group > 1 ? dec_grouped_bh(blockIdx.x, grp32, hkv32, gridDim.x, a.xmap)
                                  : (a.xmap && gridDim.x % 8 == 0 ? dec_xcd_major(blockIdx.x, gridDim.x) : blockIdx.x);
-  const int64_t b = bh / a.Hkv;
-  const int qpos = static_cast<int>(a.qpos_ptr ? *a.qpos_ptr : a.qpos);
-  const int kend = static_cast<int>(min(a.L, static_cast<int64_t>(qpos) + 1));
+  const unsigned b32 = static_cast<unsigned>(bh) / hkv32;  // 32-bit: see dec_grouped_bh
+  const int64_t b = b32;
   const uint16_t* kb = a.k + bh * a.ld_k * D;
   const uint16_t* vtb = a.vt + bh * vt_panel(a.ld_vt, D, a.ld_k);
   const uint8_t* vrow = a.valid + b * a.ld_valid;
   // the shared prompt keys [0, a.shared) of this row: cache row b / group (same KV head)
-  const int64_t bs = b / a.group, bhs = bs * a.Hkv + (bh - b * a.Hkv);
+  const int64_t bs = b32 / grp32, bhs = bs * a.Hkv + (bh - b * a.Hkv);
   const uint16_t* kbs = a.k + bhs * a.ld_k * D;
   const uint16_t* vtbs = a.vt + bhs * vt_panel(a.ld_vt, D, a.ld_k);
   // key validity always from the row's own bytes: every row holds its prompt's mask (KVCache.share_prompts), while
   // a source row p < B / group is itself a sample of prompt p / group and carries THAT prompt's mask
-  auto load = [&](int k0, DecRaw<D>& r) {  // a.shared is a multiple of 32: a block is wholly shared or wholly own
-    if (k0 < a.shared) dec_load_raw<D>(kbs, vtbs, vrow, a.ld_vt, a.ld_valid, k0, kend, lane, h, r);
-    else dec_load_raw<D>(kb, vtb, vrow, a.ld_vt, a.ld_valid, k0, kend, lane, h, r);
+  auto load_to = [&](int k0, int kcap, DecRaw<D>& r) {  // a.shared is a multiple of 32: wholly shared or wholly own
+    if (k0 < a.shared) dec_load_raw<D>(kbs, vtbs, vrow, a.ld_vt, a.ld_valid, k0, kcap, lane, h, r);
+    else dec_load_raw<D>(kb, vtb, vrow, a.ld_vt, a.ld_valid, k0, kcap, lane, h, r);
   };
+  constexpr int NR = LEAN ? 1 : NB;
+  DecRaw<D> R[NR];
+  // without key splits a wave's first block is block w whatever the query position: it is issued before the position
+  // (a device scalar) is known, its keys clamped to the cache capacity instead of kend (in bounds either way; the keys
+  // >= kend of a tail block are zeroed by dec_fix_tail when it is consumed, and a wave without blocks never reads it),
+  // so the position's load runs beside the first key loads instead of ahead of them. Same values: bit-identical.
+  const bool spec = gridDim.y == 1 && 32 * w + 32 <= a.ld_k;
+  if (spec) load_to(32 * w, static_cast<int>(a.ld_k), R[0]);
+  const int qpos = static_cast<int>(a.qpos_ptr ? *a.qpos_ptr : a.qpos);
+  const int kend = static_cast<int>(min(a.L, static_cast<int64_t>(qpos) + 1));
+  auto load = [&](int k0, DecRaw<D>& r) { load_to(k0, kend, r); };
   // split-K over gridDim.y workgroups: split y takes 32-key blocks [y*n/S, (y+1)*n/S) of the n live blocks;
   // each wave takes blocks ib0, ib0 + NW, ... and has its first NB (LEAN: 1) in flight together with q
   const int nall = (kend + 31) / 32, S = gridDim.y, y = blockIdx.y;
   const int bbeg = y * nall / S, nblk = (y + 1) * nall / S;
   const int ib0 = bbeg + w;
-  constexpr int NR = LEAN ? 1 : NB;
-  DecRaw<D> R[NR];
   uint16_t* kslot = reinterpret_cast<uint16_t*>(&s_o[w][0][0][0]);  // 32 * D bf16
   uint16_t* vslot = kslot + 32 * D;                                 // D * 32 bf16
 #pragma unroll
   for (int j = 0; j < NR; ++j)
-    if (ib0 + j * NW < nblk) load(32 * (ib0 + j * NW), R[j]);
+    if (ib0 + j * NW < nblk && !(spec && j == 0)) load(32 * (ib0 + j * NW), R[j]);
   bf16x8 qf[KS];
   {
     const bool qv = qi < a.G;
@@ -1661,33 +1671,46 @@ __global__ __launch_bounds__(64 * NW) void decode_group_kernel(DecodeArgs a) {
   const int qi = lane & 31, h = lane >> 5;
   const int G = static_cast<int>(a.G), group = static_cast<int>(a.group);
   const int rpt = a.rpt > 0 ? static_cast<int>(a.rpt) : 32 / G, ntile = (group + rpt - 1) / rpt;
-  const int64_t units = gridDim.x / ntile;
-  int64_t unit, ct;
+  const unsigned units = gridDim.x / static_cast<unsigned>(ntile), nt32 = static_cast<unsigned>(ntile);
+  unsigned unit, ct;  // 32-bit mapping (dec_grouped_bh)
   if (a.xmap && gridDim.x % 8 == 0) {
-    const int64_t idx = dec_xcd_major(blockIdx.x, gridDim.x);
-    unit = idx / ntile;
-    ct = idx % ntile;
+    const unsigned idx = dec_xcd_major(blockIdx.x, gridDim.x);
+    unit = idx / nt32;
+    ct = idx % nt32;
   } else if (units % 8 == 0) {  // the column tiles of one (prompt, head) on one XCD, back to back
-    const int64_t slot = blockIdx.x >> 3;
-    ct = slot % ntile;
-    unit = (slot / ntile) * 8 + (blockIdx.x & 7);
+    const unsigned slot = blockIdx.x >> 3;
+    ct = slot % nt32;
+    unit = (slot / nt32) * 8 + (blockIdx.x & 7);
   } else {
-    unit = blockIdx.x / ntile;
-    ct = blockIdx.x % ntile;
+    unit = blockIdx.x / nt32;
+    ct = blockIdx.x % nt32;
   }
-  const int64_t p = unit / a.Hkv, hd = unit - p * a.Hkv;
+  const unsigned p32 = unit / static_cast<unsigned>(a.Hkv);
+  const int64_t p = p32, hd = unit - p32 * static_cast<unsigned>(a.Hkv);
   const int nr = min(rpt, group - static_cast<int>(ct) * rpt);  // rows of this tile
   const int rl = qi / G, g = qi - rl * G;                         // this lane's column: local row, query head
   const bool col_ok = rl < nr;
   const int64_t b0 = p * group + ct * rpt;                        // first row of the tile
   const int64_t bcol = b0 + (col_ok ? rl : 0);
-  const int qpos = static_cast<int>(a.qpos_ptr ? *a.qpos_ptr : a.qpos);
-  const int kend = static_cast<int>(min(a.L, static_cast<int64_t>(qpos) + 1));
   const int64_t panel = vt_panel(a.ld_vt, D, a.ld_k);
   const uint16_t* kbs = a.k + (p * a.Hkv + hd) * a.ld_k * D;     // shared keys: cache row p
   const uint16_t* vtbs = a.vt + (p * a.Hkv + hd) * panel;
   const uint8_t* vrows = a.valid + p * group * a.ld_valid;        // the group's first row's mask
-  const int nall = (kend + 31) / 32, nsh = min(static_cast<int>(a.shared / 32), nall);
+  DecRaw<D> R[NB];  // NB items in flight per wave (static indexing: every use below is unrolled)
+  // the wave's first NB shared blocks (w, w + NW, ...) issued before the query position is known, keys clamped to the
+  // cache capacity (decode_mfma_kernel's speculative first block); kept when the item list starts with them (every
+  // decode step: the position is past the prompt), reloaded otherwise
+  const int nsh_all = static_cast<int>(a.shared / 32);
+  bool spec[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    spec[j] = nsh_all > w + j * NW;
+    if (spec[j])
+      dec_load_raw<D>(kbs, vtbs, vrows, a.ld_vt, a.ld_valid, 32 * (w + j * NW), static_cast<int>(a.ld_k), lane, h, R[j]);
+  }
+  const int qpos = static_cast<int>(a.qpos_ptr ? *a.qpos_ptr : a.qpos);
+  const int kend = static_cast<int>(min(a.L, static_cast<int64_t>(qpos) + 1));
+  const int nall = (kend + 31) / 32, nsh = min(nsh_all, nall);
   const int n_sh = nsh > w ? (nsh - w + NW - 1) / NW : 0;         // shared blocks of class w
   const int own0 = nsh + ((w - nsh) % NW + NW) % NW;              // first own block of class w
   const int n_own = nall > own0 ? (nall - own0 + NW - 1) / NW : 0;
@@ -1703,7 +1726,6 @@ __global__ __launch_bounds__(64 * NW) void decode_group_kernel(DecodeArgs a) {
                       a.ld_valid, 32 * ib, kend, lane, h, r);
     }
   };
-  DecRaw<D> R[NB];  // NB items in flight per wave (static indexing: every use below is unrolled)
   uint16_t* kslot = reinterpret_cast<uint16_t*>(&s_o[w][0][0][0]);
   uint16_t* vslot = kslot + 32 * D;
   // every load below is unconditional (item indices clamped to the last item; a phantom item past the end is staged
@@ -1711,7 +1733,8 @@ __global__ __launch_bounds__(64 * NW) void decode_group_kernel(DecodeArgs a) {
   // set and waits for every load in flight (vmcnt(0)) at each stage, one item in flight instead of NB
   if (items > 0) {
 #pragma unroll
-    for (int j = 0; j < NB; ++j) load(min(j, items - 1), R[j]);
+    for (int j = 0; j < NB; ++j)
+      if (!(spec[j] && nsh == nsh_all)) load(min(j, items - 1), R[j]);  // item j is shared block w + j NW: issued
   }
   bf16x8 qf[KS];
   {
@@ -1805,21 +1828,22 @@ __global__ __launch_bounds__(64 * NW) void decode_group_bal_kernel(DecodeArgs a)
   const int qi = lane & 31, h = lane >> 5;
   const int G = static_cast<int>(a.G), group = static_cast<int>(a.group);
   const int rpt = a.rpt > 0 ? static_cast<int>(a.rpt) : 32 / G, ntile = (group + rpt - 1) / rpt;
-  const int64_t units = gridDim.x / ntile;
-  int64_t unit, ct;
+  const unsigned units = gridDim.x / static_cast<unsigned>(ntile), nt32 = static_cast<unsigned>(ntile);
+  unsigned unit, ct;  // 32-bit mapping (dec_grouped_bh)
   if (a.xmap && gridDim.x % 8 == 0) {
-    const int64_t idx = dec_xcd_major(blockIdx.x, gridDim.x);
-    unit = idx / ntile;
-    ct = idx % ntile;
+    const unsigned idx = dec_xcd_major(blockIdx.x, gridDim.x);
+    unit = idx / nt32;
+    ct = idx % nt32;
   } else if (units % 8 == 0) {
-    const int64_t slot = blockIdx.x >> 3;
-    ct = slot % ntile;
-    unit = (slot / ntile) * 8 + (blockIdx.x & 7);
+    const unsigned slot = blockIdx.x >> 3;
+    ct = slot % nt32;
+    unit = (slot / nt32) * 8 + (blockIdx.x & 7);
   } else {
-    unit = blockIdx.x / ntile;
-    ct = blockIdx.x % ntile;
+    unit = blockIdx.x / nt32;
+    ct = blockIdx.x % nt32;
   }
-  const int64_t p = unit / a.Hkv, hd = unit - p * a.Hkv;
+  const unsigned p32 = unit / static_cast<unsigned>(a.Hkv);
+  const int64_t p = p32, hd = unit - p32 * static_cast<unsigned>(a.Hkv);
   const int nr = min(rpt, group - static_cast<int>(ct) * rpt);
   const int rl = qi / G, g = qi - rl * G;
   const bool col_ok = rl < nr;

@@ -1,8 +1,36 @@
-"""Summarise a rocprofv3 kernel_trace.csv: for the kernels with the most total time, the distinct launch
-shapes (grid x workgroup) with call counts and mean duration. Usage: python tools/trace_summary.py trace.csv [N]"""
+"""Summarise a rocprofv3 kernel_trace.csv (or .csv.gz): for the kernels with the most total time, the distinct launch
+shapes (grid x workgroup) with call counts and mean duration, and how much of each kernel's time other kernels ran
+beside it (the concurrent streams of the update pass: a kernel's in-situ duration then includes sharing the chip).
+Usage: python tools/trace_summary.py trace.csv [N]"""
 import collections
 import csv
+import gzip
 import sys
+
+
+def _open(path):
+    return gzip.open(path, "rt") if path.endswith(".gz") else open(path)
+
+
+def overlapped(sel):
+    """sel: sorted (start, end, name) -> {name: ns during which at least one other kernel was running}"""
+    ev = []
+    for i, (a, b, _) in enumerate(sel):
+        ev.append((a, 1, i))
+        ev.append((b, 0, i))  # ends before starts at equal timestamps
+    ev.sort()
+    shared = collections.Counter()
+    active, prev = set(), None
+    for t, kind, i in ev:
+        if prev is not None and len(active) >= 2 and t > prev:
+            for j in active:
+                shared[sel[j][2]] += t - prev
+        prev = t
+        if kind:
+            active.add(i)
+        else:
+            active.discard(i)
+    return shared
 
 
 def main():
@@ -11,7 +39,7 @@ def main():
     tot = collections.Counter()
     shapes = collections.defaultdict(collections.Counter)
     durs = collections.defaultdict(float)
-    for r in csv.DictReader(open(path)):
+    for r in csv.DictReader(_open(path)):
         name = r["Kernel_Name"]
         d = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
         tot[name] += d
@@ -21,7 +49,7 @@ def main():
         durs[(name, key)] += d
     # GPU idle time: the union of every kernel interval against the trace's span, and the longest gaps between
     # consecutive busy intervals (host-bound stretches: launches behind a synchronisation)
-    rows = list(csv.DictReader(open(path)))
+    rows = list(csv.DictReader(_open(path)))
     # bench.py with DRL_TRACE_MARK=1 brackets its timed steps with two spin kernels: the window between them
     marks = sorted(int(r["End_Timestamp"]) for r in rows if "spin_kernel" in r["Kernel_Name"])
     lo, hi = (marks[0], marks[-1]) if len(marks) >= 2 else (0, 1 << 62)
@@ -79,8 +107,13 @@ def main():
             shapes[name][key] += 1
             durs[(name, key)] += b - a
         print("per-kernel totals below: inside the window only")
+    shared = overlapped(sel) if len(marks) >= 2 and sel else collections.Counter()
+    if shared:
+        print(f"kernel time beside another kernel (concurrent streams): {sum(shared.values()) / 1e6:.1f} ms of "
+              f"{sum(tot.values()) / 1e6:.1f} ms")
     for name, t in tot.most_common(top):
-        print(f"{t / 1e6:9.1f} ms  {name[:110]}")
+        ov = f"  ({100.0 * shared[name] / t:.0f} % of it beside another kernel)" if shared.get(name) else ""
+        print(f"{t / 1e6:9.1f} ms  {name[:110]}{ov}")
         for key, n in shapes[name].most_common(int(sys.argv[3]) if len(sys.argv) > 3 else 6):
             print(f"      grid={key[0]}x{key[1]} wg={key[2]}  calls={n}  mean={durs[(name, key)] / n / 1e3:.1f} us")
 
