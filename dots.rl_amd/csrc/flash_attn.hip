@@ -1244,31 +1244,32 @@ struct DecRaw {
 // The loads are buffer loads through descriptors of the wave-uniform K panel / V^T panel / key-valid row (their bases
 // readfirstlane'd, so no waterfall loop: cdna_hip_programming.md T8 / T20) with 32-bit per-lane byte offsets: the
 // 64-bit per-lane index math of flat loads was most of the loop's VALU (52 VALU per MFMA, profiles/r05_pmc_decattn_sq.json).
+// The descriptors' byte ranges are the row's K panel (kcap keys), V^T panel and key-valid row: a key past the panel,
+// a V^T column past the plain panel's row or a key-valid word past the row reads as zero (buffer range check), so no
+// per-lane clamp is needed — the keys past kend within the panel are garbage until dec_fix_tail zeroes them (K rows,
+// V^T columns) and masks their key-valid bytes when the block is consumed
 template <int D>
 __device__ __forceinline__ void dec_load_raw(const uint16_t* kb, const uint16_t* vtb, const uint8_t* vrow,
-                                             int64_t ld_vt, int64_t ld_valid, int k0, int kend, int lane, int h,
+                                             int64_t ld_vt, int64_t ld_valid, int k0, int kcap, int lane, int h,
                                              DecRaw<D>& r) {
   constexpr int UPR = D / 8;  // 16-B units per K row
   r.k0 = k0;
+  const bool blocked = ld_vt == DRL_VT_BLOCKED;
   const auto rk = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(uniform64(reinterpret_cast<uint64_t>(kb))),
-                                                    0, 0x7fffffff, 0x00020000);
+                                                    0, kcap * D * 2, 0x00020000);
   const auto rv = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(uniform64(reinterpret_cast<uint64_t>(vtb))),
-                                                    0, 0x7fffffff, 0x00020000);
+                                                    0, static_cast<int>(vt_panel(ld_vt, D, kcap)) * 2, 0x00020000);
   const auto rb = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(uniform64(reinterpret_cast<uint64_t>(vrow))),
-                                                    0, 0x7fffffff, 0x00020000);
+                                                    0, static_cast<int>(ld_valid), 0x00020000);
   // the key-valid words first: the oldest loads of an item, so the consumer waits for them without draining the
   // next item's loads behind them
 #pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    const int kk = k0 + 8 * c + 4 * h;
-    r.vb[c] = __builtin_amdgcn_raw_buffer_load_b32(rb, min(kk, static_cast<int>(ld_valid) - 4), 0, 0);
-  }
-  const bool blocked = ld_vt == DRL_VT_BLOCKED;
+  for (int c = 0; c < 4; ++c) r.vb[c] = __builtin_amdgcn_raw_buffer_load_b32(rb, k0 + 8 * c + 4 * h, 0, 0);
   const int ldv = static_cast<int>(blocked ? 0 : ld_vt);
 #pragma unroll
   for (int i = 0; i < D / 16; ++i) {
     const int c = lane + 64 * i;
-    const int key = min(k0 + c / UPR, kend - 1);
+    const int key = k0 + c / UPR;
     r.k[i] = __builtin_bit_cast(u16x8, __builtin_amdgcn_raw_buffer_load_b128(rk, (key * D + 8 * (c % UPR)) * 2, 0, 0));
     const int d = c >> 2, kk = k0 + 8 * (c & 3);
     // blocked (key >> 5) * 32 * D + d * 32 + (key & 31) with key = kk, k0 % 32 == 0; else d * ld_vt + key
@@ -1402,14 +1403,24 @@ __device__ __forceinline__ void dec_block_lds(const uint16_t* ks, const uint16_t
     st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(kf), qf[s], st, 0, 0, 0);
   }
   float mx = -INFINITY;
+  // every key of the block valid for every lane (the common case: a full block past the left padding): the unmasked
+  // form, the same products (uniform branch)
+  if (__all((vb[0] & vb[1] & vb[2] & vb[3]) == 0x01010101u)) {
 #pragma unroll
-  for (int c = 0; c < 4; ++c)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int r = 4 * c + j;
-      st[r] = ((vb[c] >> (8 * j)) & 0xffu) != 0u ? st[r] * scale_log2 : -INFINITY;
+    for (int r = 0; r < 16; ++r) {
+      st[r] = st[r] * scale_log2;
       mx = fmaxf(mx, st[r]);
     }
+  } else {
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int r = 4 * c + j;
+        st[r] = ((vb[c] >> (8 * j)) & 0xffu) != 0u ? st[r] * scale_log2 : -INFINITY;
+        mx = fmaxf(mx, st[r]);
+      }
+  }
   mx = fmaxf(mx, __shfl_xor(mx, 32, kWave));
   const float mn = fmaxf(m, mx);
   const float mref = mn == -INFINITY ? 0.f : mn;
@@ -1480,7 +1491,7 @@ __global__ __launch_bounds__(64 * NW) void decode_mfma_kernel(DecodeArgs a) {
   if (spec) load_to(32 * w, static_cast<int>(a.ld_k), R[0]);
   const int qpos = static_cast<int>(a.qpos_ptr ? *a.qpos_ptr : a.qpos);
   const int kend = static_cast<int>(min(a.L, static_cast<int64_t>(qpos) + 1));
-  auto load = [&](int k0, DecRaw<D>& r) { load_to(k0, kend, r); };
+  auto load = [&](int k0, DecRaw<D>& r) { load_to(k0, static_cast<int>(a.ld_k), r); };
   // split-K over gridDim.y workgroups: split y takes 32-key blocks [y*n/S, (y+1)*n/S) of the n live blocks;
   // each wave takes blocks ib0, ib0 + NW, ... and has its first NB (LEAN: 1) in flight together with q
   const int nall = (kend + 31) / 32, S = gridDim.y, y = blockIdx.y;
@@ -1718,12 +1729,12 @@ __global__ __launch_bounds__(64 * NW) void decode_group_kernel(DecodeArgs a) {
   // item j -> block index, source row (-1: shared) ; loads through the per-row kernel's raw loader
   auto load = [&](int j, DecRaw<D>& r) {
     if (j < n_sh) {
-      dec_load_raw<D>(kbs, vtbs, vrows, a.ld_vt, a.ld_valid, 32 * (w + j * NW), kend, lane, h, r);
+      dec_load_raw<D>(kbs, vtbs, vrows, a.ld_vt, a.ld_valid, 32 * (w + j * NW), static_cast<int>(a.ld_k), lane, h, r);
     } else {
       const int jj = j - n_sh, rr = jj / n_own, ib = own0 + (jj - rr * n_own) * NW;
       const int64_t bh = (b0 + rr) * a.Hkv + hd;
       dec_load_raw<D>(a.k + bh * a.ld_k * D, a.vt + bh * panel, a.valid + (b0 + rr) * a.ld_valid, a.ld_vt,
-                      a.ld_valid, 32 * ib, kend, lane, h, r);
+                      a.ld_valid, 32 * ib, static_cast<int>(a.ld_k), lane, h, r);
     }
   };
   uint16_t* kslot = reinterpret_cast<uint16_t*>(&s_o[w][0][0][0]);
@@ -1877,14 +1888,14 @@ __global__ __launch_bounds__(64 * NW) void decode_group_bal_kernel(DecodeArgs a)
   };
   auto load = [&](int j, DecRaw<D>& r) {
     if (j < n_sh) {
-      dec_load_raw<D>(kbs, vtbs, vrows, a.ld_vt, a.ld_valid, 32 * (w + j * NW), kend, lane, h, r);
+      dec_load_raw<D>(kbs, vtbs, vrows, a.ld_vt, a.ld_valid, 32 * (w + j * NW), static_cast<int>(a.ld_k), lane, h, r);
     } else {
       int u;
       const int i = locate(j - n_sh, u);
       const int jc = u / nr, rr = u - jc * nr;
       const int64_t bh = (b0 + rr) * a.Hkv + hd;
       dec_load_raw<D>(a.k + bh * a.ld_k * D, a.vt + bh * panel, a.valid + (b0 + rr) * a.ld_valid, a.ld_vt,
-                      a.ld_valid, 32 * (nsh + jc + NW * i), kend, lane, h, r);
+                      a.ld_valid, 32 * (nsh + jc + NW * i), static_cast<int>(a.ld_k), lane, h, r);
     }
   };
   DecRaw<D> R[NB];
