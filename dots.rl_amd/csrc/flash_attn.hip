@@ -1455,12 +1455,13 @@ __device__ __forceinline__ uint16_t* dec_out_ptr(const DecodeArgs& a, int64_t b,
   return a.out + ((((k >> 4) * a.out_mbt + (b >> 5)) * 64 + ((k >> 3) & 1) * 32 + (b & 31)) * 8 + (k & 7));
 }
 
-template <int D, int NW, bool LEAN = false, bool SPLIT = false, int NB = 2>
+template <int D, int NW, bool LEAN = false, bool SPLIT = false, int NB = 2, int LNB = 1>
 __global__ __launch_bounds__(64 * NW) void decode_mfma_kernel(DecodeArgs a) {
   constexpr int KS = D / 16, MT = D / 32;
   __shared__ float s_m[NW][32], s_l[NW][32];
   // per wave: its K / V^T staging slot during the key loop, then its partial O^T (same 64*D*2... bytes)
   __shared__ __attribute__((aligned(16))) float s_o[NW][MT][16][64];
+  __shared__ __attribute__((aligned(16))) uint32_t s_vb[LEAN && LNB > 1 ? NW : 1][4 * 64];  // deep lean ring only
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);  // scalar wave index
   const int qi = lane & 31, h = lane >> 5;
   const unsigned hkv32 = static_cast<unsigned>(a.Hkv), grp32 = static_cast<unsigned>(a.group);
@@ -1481,7 +1482,7 @@ __global__ __launch_bounds__(64 * NW) void decode_mfma_kernel(DecodeArgs a) {
     if (k0 < a.shared) dec_load_raw<D>(kbs, vtbs, vrow, a.ld_vt, a.ld_valid, k0, kcap, lane, h, r);
     else dec_load_raw<D>(kb, vtb, vrow, a.ld_vt, a.ld_valid, k0, kcap, lane, h, r);
   };
-  constexpr int NR = LEAN ? 1 : NB;
+  constexpr int NR = LEAN ? LNB : NB;
   DecRaw<D> R[NR];
   // without key splits a wave's first block is block w whatever the query position: it is issued before the position
   // (a device scalar) is known, its keys clamped to the cache capacity instead of kend (in bounds either way; the keys
@@ -1499,9 +1500,18 @@ __global__ __launch_bounds__(64 * NW) void decode_mfma_kernel(DecodeArgs a) {
   const int ib0 = bbeg + w;
   uint16_t* kslot = reinterpret_cast<uint16_t*>(&s_o[w][0][0][0]);  // 32 * D bf16
   uint16_t* vslot = kslot + 32 * D;                                 // D * 32 bf16
+  const int nit = ib0 < nblk ? (nblk - ib0 + NW - 1) / NW : 0;        // this wave's blocks
+  if constexpr (LEAN && LNB > 1) {  // every load unconditional: block indices clamped to the wave's last block
+    if (nit > 0) {
 #pragma unroll
-  for (int j = 0; j < NR; ++j)
-    if (ib0 + j * NW < nblk && !(spec && j == 0)) load(32 * (ib0 + j * NW), R[j]);
+      for (int j = 0; j < LNB; ++j)
+        if (!(spec && j == 0)) load(32 * (ib0 + min(j, nit - 1) * NW), R[j]);
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < NR; ++j)
+      if (ib0 + j * NW < nblk && !(spec && j == 0)) load(32 * (ib0 + j * NW), R[j]);
+  }
   bf16x8 qf[KS];
   {
     const bool qv = qi < a.G;
@@ -1517,7 +1527,28 @@ __global__ __launch_bounds__(64 * NW) void decode_mfma_kernel(DecodeArgs a) {
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) o[mt] = f32x16{};
   float m = -INFINITY, lsum = 0.f;
-  if constexpr (LEAN) {
+  if constexpr (LEAN && LNB > 1) {
+    // LNB blocks in flight per wave (decode_group_kernel's ring): stage block j, refill its registers with block
+    // j + LNB (clamped to the wave's last block: an unconditional refill, so hipcc counts the loads behind each register
+    // set instead of waiting for all of them), then the softmax step from LDS. A block past the wave's end is staged
+    // and consumed with no valid key (an exact no-op: alpha = 1, p = 0); the key-valid words go through the wave's LDS
+    // slot (carried in registers past the refill they made hipcc drain every load). Same blocks, same order: bit-identical
+    // to the one-in-flight loop.
+    u32x4* vbslot = reinterpret_cast<u32x4*>(&s_vb[w][0]);
+    for (int j = 0; j < nit; j += LNB) {
+#pragma unroll
+      for (int i = 0; i < LNB; ++i) {
+        const int jj = j + i;
+        dec_fix_tail<D>(R[i], kend, a.ld_valid, lane, h);
+        dec_stage<D>(R[i], kslot, vslot, lane);
+        vbslot[lane] = jj < nit ? u32x4{R[i].vb[0], R[i].vb[1], R[i].vb[2], R[i].vb[3]} : u32x4{0u, 0u, 0u, 0u};
+        load(32 * (ib0 + min(jj + LNB, nit - 1) * NW), R[i]);
+        const u32x4 v4 = vbslot[lane];
+        const uint32_t vb[4] = {v4[0], v4[1], v4[2], v4[3]};
+        dec_block_lds<D>(kslot, vslot, vb, qf, a.scale_log2, qi, h, m, lsum, o);
+      }
+    }
+  } else if constexpr (LEAN) {
     // one block in flight per wave: stage it to the slot, issue the next, compute from LDS
     for (int ib = ib0; ib < nblk; ib += NW) {
       dec_fix_tail<D>(R[0], kend, a.ld_valid, lane, h);
@@ -2024,6 +2055,7 @@ int g_dq_variant = 0;  // drl_flash_attn_bwd_set_variant: 0 = one query tile per
 int g_grp_rpt = 0;
 int g_dec_xmap = 0;  // drl_decode_group_set_plan: workgroup -> XCD placement of the decode attention (DecodeArgs::xmap)
 int g_grp_bal = -1;               // drl_decode_group_set_plan: own blocks balanced over the waves (-1 = automatic)
+int g_dec_lean_depth = 0;  // blocks in flight of the automatic register-lean plan (0 = the planner's choice)
 int g_dec_variant = 0;  // drl_decode_attention_set_variant: 1 = one block in flight (LDS fragments), 2..4 = ring depth
 
 // key splits for decode attention. Measured (tools/kernel_bench.py --only decode_sweep, B 64..512,
@@ -2131,7 +2163,7 @@ int drl_flash_attn_bwd_rows(const void* q, const void* k, const void* kt, const 
 void drl_flash_attn_bwd_set_variant(int32_t variant) { drl::g_dq_variant = (variant >= 0 && variant <= 2) ? variant : 0; }
 
 void drl_decode_attention_set_variant(int32_t variant) {
-  drl::g_dec_variant = (variant >= 1 && variant <= 4) ? variant : 0;
+  drl::g_dec_variant = (variant >= 1 && variant <= 5) ? variant : 0;
 }
 
 void drl_decode_group_set_plan(int32_t rows_per_tile, int32_t xcd_map, int32_t balanced) {
@@ -2226,10 +2258,14 @@ int drl_decode_attention_vt(const void* q, const void* k_cache, const void* vt_c
   // 11.5 -> 9.7 us, B=128: 15.0 -> 12.0); 4 waves measured 35.8 vs 37.3 us at B=512 in isolation but 41.9 vs
   // 39.3 in the rollout (rocprof), so 2 waves beyond two workgroups per CU
   const int nw = g_dec_nw ? g_dec_nw : (wgs <= cus ? 8 : (wgs <= 2 * cus ? 4 : 2));
-  const bool lean = g_dec_nw ? g_dec_variant == 1 : true;
+  const bool lean = g_dec_nw ? (g_dec_variant == 1 || g_dec_variant >= 5) : true;
   // blocks in flight per wave (small grids): all of a wave's blocks at the cache capacity, up to 4
   const int64_t per_wave = ((L + 31) / 32 + nw - 1) / nw;
   const int nb = g_dec_nw ? (g_dec_variant > 2 ? g_dec_variant : 2) : (per_wave >= 4 ? 4 : per_wave >= 3 ? 3 : 2);
+  // blocks in flight per wave of the register-lean loop: 2 when a wave has two or more blocks and the grid is at most
+  // one workgroup per CU (3 spill at 8 waves' 256 registers); forced plans: variant 5 = 2
+  const int ldepth = g_dec_nw ? (g_dec_variant == 5 ? 2 : 1)
+                              : (g_dec_lean_depth ? g_dec_lean_depth : (wgs <= cus && per_wave >= 2 ? 2 : 1));
   if (splits > 1) {
     const size_t need = drl_decode_attention_vt_workspace_bytes(B, Hkv, D, L);
     if (!workspace || workspace_bytes < need || (reinterpret_cast<uintptr_t>(workspace) & 255u))
@@ -2241,6 +2277,8 @@ int drl_decode_attention_vt(const void* q, const void* k_cache, const void* vt_c
   do {                                                                                                           \
     const dim3 g_(B * Hkv, splits), b_(64 * NN);                                                                  \
     if (splits > 1) hipLaunchKernelGGL((decode_mfma_kernel<DD, NN, false, true>), g_, b_, 0, s, a);              \
+    else if (lean && ldepth >= 2 && DD == 64 && NN == 8)                                                         \
+      hipLaunchKernelGGL((decode_mfma_kernel<DD, NN, true, false, 2, 2>), g_, b_, 0, s, a);                      \
     else if (lean) hipLaunchKernelGGL((decode_mfma_kernel<DD, NN, true, false>), g_, b_, 0, s, a);              \
     else {                                                                                                       \
       bool done_ = false;                                                                                        \

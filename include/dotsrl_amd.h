@@ -477,8 +477,8 @@ void drl_decode_group_set_plan(int32_t rows_per_tile, int32_t xcd_map, int32_t b
  * 1 = two query tiles per workgroup (K / V fragments in registers), 2 = two tiles re-reading them. Same bits. */
 void drl_flash_attn_bwd_set_variant(int32_t variant);
 /* Tuning hook for forced plans (set_plan waves != 0): 1 = register-lean key loop (one block in flight per
- * wave, fragments read from LDS); 2..4 = that many blocks in flight per wave (4 and 8 waves, D = 64; else 2).
- * Results are identical. */
+ * wave, fragments read from LDS); 2..4 = that many blocks in flight per wave (4 and 8 waves, D = 64; else 2);
+ * 5 = the register-lean loop with 2 blocks in flight (8 waves, D = 64). Results are identical. */
 void drl_decode_attention_set_variant(int32_t variant);
 /* Prompt groups (the n samples of one prompt, hf_rollout.py's repeated prompts / vLLM's shared prefix): with
  * group > 1, sequences b = p * group + r share one prompt, and keys j < shared_keys (a multiple of 32, <= L) are

@@ -357,6 +357,39 @@ def test_decode_attention_vt_split_plans(waves, splits):
         lib.drl_decode_attention_set_plan(0, 0)
 
 
+@pytest.mark.parametrize("B,group,shared,cap,L", [(64, 8, 512, 768, 520), (64, 8, 512, 768, 767), (64, 8, 512, 768, 544),
+                                                 (6, 1, 0, 640, 600), (16, 2, 96, 300, 290), (8, 1, 0, 100, 40)])
+def test_decode_attention_lean_ring_bit_identical(B, group, shared, cap, L):
+    """The register-lean loop with two key blocks in flight per wave (the planner's choice when the grid fits the chip:
+    the N = 8 rank's 64 rows) == the one-in-flight loop bit for bit (same blocks, same order; a block past a wave's
+    end consumed with no valid key), at 8 waves without key splits: prompt groups, a tail block, a wave with one
+    block, left padding, a short cache."""
+    Hkv, G, D = 2, 7, 64
+    g = torch.Generator(device=DEV).manual_seed(B + L)
+    q = torch.randn(B, Hkv, G, D, device=DEV, generator=g).to(torch.bfloat16)
+    k = torch.randn(B, Hkv, cap, D, device=DEV, generator=g).to(torch.bfloat16)
+    vt = torch.randn(B, Hkv, (cap + 31) // 32, D, 32, device=DEV, generator=g).to(torch.bfloat16)
+    valid = torch.ones(B, (cap + 3) // 4 * 4, dtype=torch.uint8, device=DEV)
+    for b in range(B):
+        valid[b, : 3 * (b % 5)] = 0
+    qp = torch.tensor([L - 1], device=DEV)
+    lib = native.lib()
+    kw = dict(group=group, shared_keys=shared) if group > 1 else {}
+    outs = []
+    try:
+        for variant in (1, 5):  # one / two blocks in flight
+            lib.drl_decode_attention_set_plan(8, 1)
+            lib.drl_decode_attention_set_variant(variant)
+            outs.append(native.decode_attention_vt(q, k, vt, valid, cap, torch.empty_like(q), qpos_dev=qp, **kw))
+    finally:
+        lib.drl_decode_attention_set_plan(0, 0)
+        lib.drl_decode_attention_set_variant(0)
+    assert torch.equal(outs[0], outs[1])
+    if B * Hkv <= 256:  # the planner's own choice at this grid is the two-block ring
+        auto = native.decode_attention_vt(q, k, vt, valid, cap, torch.empty_like(q), qpos_dev=qp, **kw)
+        assert torch.equal(auto, outs[1])
+
+
 @pytest.mark.parametrize("N,C", [(6144, 1152), (100, 200), (1, 64), (12288, 1152)])
 def test_colsum_bf16_acc(N, C):
     """qkv bias gradient: column sums of bf16 dqkv accumulated into the fp32 gradient, deterministic."""
