@@ -360,10 +360,10 @@ def test_decode_attention_vt_split_plans(waves, splits):
 @pytest.mark.parametrize("B,group,shared,cap,L", [(64, 8, 512, 768, 520), (64, 8, 512, 768, 767), (64, 8, 512, 768, 544),
                                                  (6, 1, 0, 640, 600), (16, 2, 96, 300, 290), (8, 1, 0, 100, 40)])
 def test_decode_attention_lean_ring_bit_identical(B, group, shared, cap, L):
-    """The register-lean loop with two key blocks in flight per wave (the planner's choice when the grid fits the chip:
-    the N = 8 rank's 64 rows) == the one-in-flight loop bit for bit (same blocks, same order; a block past a wave's
-    end consumed with no valid key), at 8 waves without key splits: prompt groups, a tail block, a wave with one
-    block, left padding, a short cache."""
+    """The register-lean loop with two key blocks in flight per wave (on request: measured slower than one at the
+    N = 8 rank's 64 rows) == the one-in-flight loop bit for bit (same blocks, same order; a block past a wave's end
+    consumed with no valid key), at 8 waves without key splits: prompt groups, a tail block, a wave with one block,
+    left padding, a short cache; and the planner's own choice equals both."""
     Hkv, G, D = 2, 7, 64
     g = torch.Generator(device=DEV).manual_seed(B + L)
     q = torch.randn(B, Hkv, G, D, device=DEV, generator=g).to(torch.bfloat16)
@@ -385,7 +385,7 @@ def test_decode_attention_lean_ring_bit_identical(B, group, shared, cap, L):
         lib.drl_decode_attention_set_plan(0, 0)
         lib.drl_decode_attention_set_variant(0)
     assert torch.equal(outs[0], outs[1])
-    if B * Hkv <= 256:  # the planner's own choice at this grid is the two-block ring
+    if B * Hkv <= 256:  # the planner's own plan at this grid: 8 waves, no key split
         auto = native.decode_attention_vt(q, k, vt, valid, cap, torch.empty_like(q), qpos_dev=qp, **kw)
         assert torch.equal(auto, outs[1])
 
