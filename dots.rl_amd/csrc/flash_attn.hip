@@ -2264,7 +2264,7 @@ int drl_decode_attention_vt(const void* q, const void* k_cache, const void* vt_c
   const int nb = g_dec_nw ? (g_dec_variant > 2 ? g_dec_variant : 2) : (per_wave >= 4 ? 4 : per_wave >= 3 ? 3 : 2);
   // blocks in flight per wave of the register-lean loop: 1. Two (variant 5 of a forced plan; 3 spill at 8 waves' 256
   // registers) measured slower at the N = 8 rank's 64 rows: 7.1 -> 8.8 / 7.3 -> 8.4 / 8.6 -> 10.9 us per call at L = 520 /
-  // 640 / 767, 206 -> 254 us per token in situ (profiles/r06_decode_attn_lean2_rejected.jsonl): the phantom step that
+  // 640 / 767, 206 -> 254 us per token in situ (profiles/r06_decode_attn_lean2_rejected.jsonl, profiles/r06_decode_step_64rows_lean2_rejected.txt): the phantom step that
   // pads a wave's 2-3 blocks to the ring and the key-valid hand-off through LDS cost more than the overlap gives
   const int ldepth = g_dec_nw ? (g_dec_variant == 5 ? 2 : 1) : (g_dec_lean_depth ? g_dec_lean_depth : 1);
   if (splits > 1) {
