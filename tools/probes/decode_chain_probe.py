@@ -10,7 +10,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from dots.rl_amd import native  # noqa: E402
 from dots.rl_amd.qwen2 import KVCache, PackedDecode, ParamStore, Qwen2Config, Qwen2Model  # noqa: E402
 
@@ -46,8 +46,8 @@ def main():
 
     variants = {
         "full": {},
-        "no_rmsnorm": {"decode_rmsnorm": lambda x, p, xo, w, y, eps, mbt=0: None if mbt else
-                       orig["decode_rmsnorm"](x, p, xo, w, y, eps, mbt=mbt)},
+        "no_rmsnorm": {"decode_rmsnorm": lambda x, p, xo, w, y, eps, mbt=0, **kw: None if mbt else
+                       orig["decode_rmsnorm"](x, p, xo, w, y, eps, mbt=mbt, **kw)},
         "no_qkv": {"decode_qkv_rope": noop},
         "no_attention": {"decode_attention_vt": noop},
         "no_o": {"decode_gemm": gemm_skip("o")},

@@ -12,8 +12,8 @@ from gemm_sk_bench import bench  # noqa: E402
 from dots.rl_amd import native  # noqa: E402
 
 bf = torch.bfloat16
-for M, N in ((24576, 9728), (24576, 896), (61440, 9728)):
-    for K in (896,):
+for M, N in [tuple(int(v) for v in a.split('x')) for a in sys.argv[1:]] or ((24576, 9728), (24576, 896), (61440, 9728)):
+    for K in (896, 1792):
         x = torch.randn(M, K, device="cuda", dtype=bf)
         w = torch.randn(N, K, device="cuda", dtype=bf) * 0.05
         b = torch.randn(N, device="cuda", dtype=bf)
