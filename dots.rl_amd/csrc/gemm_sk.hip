@@ -43,6 +43,8 @@
 // and finishes with a wrong tile rather than hanging; tests read the word back (tests/test_gemm_sk_gpu.py).
 #include "common.h"
 
+#include <type_traits>
+
 namespace drl {
 namespace {
 
@@ -156,7 +158,10 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
   const uint32_t kstep_a = AT ? static_cast<uint32_t>(64 * g.lda * 2) : 128u;
   const uint32_t kstep_b = BT ? static_cast<uint32_t>(64 * g.ldb * 2) : 128u;
 
-  auto setup_tile = [&](int m0, int n0) {
+  // hn (a half-width tile: at most 128 valid columns, the last tile column of N % 256 in (0, 128]): B half 2 holds the
+  // tile's 128 columns contiguously (wave wc reads columns wc * 32 ..), half 3 is never read (its copies go out of
+  // range: zeros, no memory traffic)
+  auto setup_tile = [&](int m0, int n0, bool hn = false) {
     int am0 = m0;  // A rows are addressed from the descriptor's base row
     if constexpr (!AT) {
       if (g.a_total > 0) {  // the tile's rows onward as their own buffer range (every offset below stays 32-bit)
@@ -186,27 +191,30 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
             const int bb = row >> 4, col = min(n0 / 2 + 16 * (bb >> 1) + (row & 15), half - 1);
             grow = (bb & 1) ? half + col : col;
           } else {
-            grow = n0 + (hr >> 5) * 64 + (h & 1) * 32 + (hr & 31);
+            grow = hn ? n0 + hr : n0 + (hr >> 5) * 64 + (h & 1) * 32 + (hr & 31);
           }
           const int64_t ld = is_a ? g.lda : g.ldb;
           voff[h][c] = static_cast<uint32_t>((static_cast<int64_t>(grow) * ld + 8 * (up ^ swz_k(hr))) * 2);
         } else {
           const int row = 4 * q + (lane >> 4), ch = (lane & 15) ^ swz_t(row);
-          const int col = is_a ? m0 + (h & 1) * 128 + 8 * ch : n0 + (ch >> 2) * 64 + (h & 1) * 32 + (ch & 3) * 8;
+          const int col = is_a ? m0 + (h & 1) * 128 + 8 * ch
+                               : (hn ? n0 + 8 * ch : n0 + (ch >> 2) * 64 + (h & 1) * 32 + (ch & 3) * 8);
           const int64_t ld = is_a ? g.lda : g.ldb;
           voff[h][c] = static_cast<uint32_t>((static_cast<int64_t>(row) * ld + col) * 2);
         }
       }
   };
   // buf = kt & 1, passed as a constant of the unrolled schedule (segments start at even k-tiles)
-  auto issue = [&](int h, int buf, int kt, int kt_end) {
+  auto issue = [&](int h, int buf, int kt, int kt_end, bool hn = false) {
     // past the segment's end: repeat its last k-tile into a buffer nobody reads again (keeps vmcnt counts static)
     const int k = min(kt, kt_end - 1);
     uint16_t* dst = lds + lds_half(h, buf);
     const bool is_a = h < 2;
-    // k-tile past the data (K % 128 == 64): an soffset of the whole byte range puts every lane out of range (zeros)
-    const uint32_t soff = k >= g.nkt ? (is_a ? a_end : g.b_bytes)
-                                     : static_cast<uint32_t>(is_a ? k - a_kt0 : k) * (is_a ? kstep_a : kstep_b);
+    // k-tile past the data (K % 128 == 64), or B half 3 of a half-width tile: an soffset of the whole byte range puts
+    // every lane out of range (zeros)
+    const uint32_t soff = (k >= g.nkt || (hn && h == 3))
+                              ? (is_a ? a_end : g.b_bytes)
+                              : static_cast<uint32_t>(is_a ? k - a_kt0 : k) * (is_a ? kstep_a : kstep_b);
 #pragma unroll
     for (int c = 0; c < 2; ++c)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(is_a ? ra : rb, (lds_void*)(dst + (wave + 8 * c) * 512 + lane * 8), 16,
@@ -278,7 +286,10 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
   constexpr int NA_READS = AT ? 16 : 8;  // of one A sub-tile read
 
   // one segment: k-tile pairs [p0, p1) of the current tile accumulated into acc (zeroed first unless keep)
-  auto run = [&](int p0, int p1, bool keep) __attribute__((always_inline)) {
+  // hn (uniform): a half-width tile — the quadrants qn = 1 hold no columns, so their MFMAs are skipped by a scalar
+  // branch (those phases keep their copies and barriers: the schedule's vmcnt counts and the wave groups'
+  // pairing stay as they are; one instance of the loop — a second, compile-time instance spilled 120-340 registers)
+  auto run = [&](int p0, int p1, bool keep, bool hn) __attribute__((always_inline)) {
     if (!keep) {
 #pragma unroll
       for (int a = 0; a < 2; ++a)
@@ -290,8 +301,8 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
             for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4{};
     }
     const int k0 = 2 * p0, k1 = 2 * p1;  // k-tiles [k0, k1)
-    issue(2, 0, k0, k1); issue(0, 0, k0, k1); issue(3, 0, k0, k1); issue(1, 0, k0, k1);
-    issue(2, 1, k0 + 1, k1); issue(0, 1, k0 + 1, k1); issue(3, 1, k0 + 1, k1);
+    issue(2, 0, k0, k1, hn); issue(0, 0, k0, k1, hn); issue(3, 0, k0, k1, hn); issue(1, 0, k0, k1, hn);
+    issue(2, 1, k0 + 1, k1, hn); issue(0, 1, k0 + 1, k1, hn); issue(3, 1, k0 + 1, k1, hn);
     asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     bar();
     if (wr == 1) bar();  // the upper group runs one barrier behind
@@ -306,13 +317,14 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
           __builtin_amdgcn_sched_barrier(0);
           read_a(buf, 0);
         } else if (lp == 1) {
-          read_b(buf, 3, 1);
+          read_b(buf, 3, 1);  // also for a half-width tile (unread there): a conditional read kept bq[1] live across
+                              // the loop (16 registers spilled)
         } else if (lp == 2) {
           read_a(buf, 1);
         }
         constexpr int kH[8] = {1, 2, 0, 3, 1, 2, 0, 3};
         constexpr int kD[8] = {1, 2, 2, 2, 2, 3, 3, 3};
-        if (p == 0 || !last) issue(kH[p], kD[p] & 1, kt + kD[p], k1);
+        if (p == 0 || !last) issue(kH[p], kD[p] & 1, kt + kD[p], k1, hn);
         if (lp == 0) {  // the B0 reads (issued first) retired before the barrier (WAR of the next copies)
           if constexpr (NA_READS >= 15) asm volatile("s_waitcnt lgkmcnt(15)" ::: "memory");
           else if constexpr (NA_READS == 8) asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
@@ -326,6 +338,7 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);  // nothing that uses an asm read's result moves above its wait
         __builtin_amdgcn_s_setprio(1);
+        if (!(hn && qn == 1))
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -350,7 +363,7 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
   // k-pairs [p0, p1) of the current tile; a layout-T A operand past one buffer range is walked in blocks of a_kblk
   // rows, the descriptor rebased at each (one launch, the fp32 output read and written once — the round-5 host loop
   // launched one GEMM per block, each a read-modify-write of the whole output)
-  auto run_k = [&](int p0, int p1) __attribute__((always_inline)) {
+  auto run_k = [&](int p0, int p1, bool hn) __attribute__((always_inline)) {
     const bool blk = AT && g.a_kblk > 0;
     const int bp = blk ? g.a_kblk / 128 : max(p1, 1);  // k-pairs per block (one block without K blocking)
     bool keep = false;
@@ -366,7 +379,7 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
           a_kt0 = 2 * q0;
         }
       }
-      run(lo, hi, keep);
+      run(lo, hi, keep, hn);
       keep = true;
     }
   };
@@ -379,7 +392,10 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
   // 3.7 us per 256 x 256 tile, profiles/r03_gemm_fixed_cost.jsonl) — then read back as 16-B row pieces for coalesced
   // 128-B row stores (storing the 8-B pieces straight from the registers, 16 rows x 32 B per wave instruction,
   // measured 3x slower).
-  auto epilogue = [&](int m0, int n0) {
+  // HALF: a half-width tile (setup_tile's hn): accumulator block (i, j) of quadrant (qm, 0) holds tile columns
+  // wc * 32 + j * 16 + 4 fq + (0..3); the quadrants qn = 1 hold nothing
+  auto epilogue = [&](int m0, int n0, auto half_tag) {
+    constexpr bool HALF = decltype(half_tag)::value;
     bar();  // every fragment read retired and every copy drained: LDS is free for staging
     if (g.dbg & 4) {  // measurement: the epilogue's two barriers only
       bar();
@@ -396,13 +412,14 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
       for (int qm = 0; qm < 2; ++qm)
 #pragma unroll
         for (int qn = 0; qn < 2; ++qn) {
+          if (HALF && qn == 1) continue;
 #pragma unroll
           for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int i = 0; i < 4; ++i)
               *reinterpret_cast<f32x4*>(st + (i * 16 + fr) * SLD + j * 16 + 4 * fq) = acc[qm][qn][i][j];
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          const int col = n0 + wc * 64 + qn * 32 + 4 * ch;
+          const int col = HALF ? n0 + wc * 32 + 4 * ch : n0 + wc * 64 + qn * 32 + 4 * ch;
 #pragma unroll
           for (int it = 0; it < 8; ++it) {
             const int lr = it * 8 + (lane >> 3);
@@ -614,6 +631,50 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
         stage(1);
         if (whole) fast(1);
         else rows(1);
+      } else if constexpr (HALF) {
+        // half-width tile: per quadrant the wave's 64 x 32 block, stored as 4 16-B pieces per 64-B row
+        const int c4 = lane & 3, colh = n0 + wc * 32 + c4 * 8;
+        const bool vech = colh + 8 <= g.N && (g.ldc & 7) == 0 && (reinterpret_cast<uintptr_t>(g.c) & 15) == 0;
+#pragma unroll
+        for (int qm = 0; qm < 2; ++qm) {
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const int lc = j * 16 + 4 * fq;
+            float bb[4] = {0.f, 0.f, 0.f, 0.f};
+            if constexpr (EPI == EPI_BIAS) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) bb[e] = bf16_to_f32(g.bias[min(n0 + wc * 32 + lc + e, g.N - 1)]);
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const f32x4 v = acc[qm][0][i][j];
+              uint2 w;
+              if constexpr (EPI == EPI_BIAS) {
+                w.x = pk_bf16(v[0] + bb[0], v[1] + bb[1]);
+                w.y = pk_bf16(v[2] + bb[2], v[3] + bb[3]);
+              } else {
+                w.x = pk_bf16(v[0], v[1]);
+                w.y = pk_bf16(v[2], v[3]);
+              }
+              *reinterpret_cast<uint2*>(st + (i * 16 + fr) * SLD + lc) = w;
+            }
+          }
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+          for (int it = 0; it < 4; ++it) {
+            const int lr = it * 16 + (lane >> 2);
+            const int m = m0 + qm * 128 + wr * 64 + lr;
+            const u16x8 v = *reinterpret_cast<const u16x8*>(st + lr * SLD + c4 * 8);
+            if (m >= g.M || colh >= g.N) continue;
+            uint16_t* dstp = g.c + static_cast<int64_t>(m) * g.ldc + colh;
+            if (vech) {
+              *reinterpret_cast<u16x8*>(dstp) = v;
+            } else {
+              for (int e = 0; e < 8 && colh + e < g.N; ++e) dstp[e] = v[e];
+            }
+          }
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
       } else {
 #pragma unroll
       for (int qm = 0; qm < 2; ++qm) {
@@ -704,7 +765,7 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
       n0 = (r / gmm) * 256;
     }
     setup_tile(m0, n0);
-    run_k(sp * g.P / S, (sp + 1) * g.P / S);
+    run_k(sp * g.P / S, (sp + 1) * g.P / S, false);
     const __amdgpu_buffer_rsrc_t rws =
         __builtin_amdgcn_make_buffer_rsrc((void*)g.ws, (short)0, (G - g.sk_base) * SLAB * 4, 0x00020000);
     const uint32_t vo = static_cast<uint32_t>(slab_tile + sp * slab_step) * SLAB * 4 + threadIdx.x * 16;
@@ -780,12 +841,25 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
   }
 
   // ------------------------------------------------------------------------------------------ whole tiles
+  // a half-width tile (the last tile column of N % 256 in (0, 128]: the N = 896 / 1152 outputs): half the MFMAs
+  // (plain / fp32 epilogues; drl_gemm_set_debug bit 32 turns it off). Layout-T B only (the input and weight
+  // gradients): in the layout-K B kernels (the forwards) the extra path cost registers (11 -> 38 spilled) and their
+  // whole launch 2-8 % (profiles/r06_gemm_half_tile_ab.txt), more than the skipped MFMAs give back
+  constexpr bool kHalfOk = (EPI == EPI_NONE || EPI == EPI_BIAS || EPI == EPI_F32) && BT == 1;
   for (int t = wg; t < g.dp_tiles; t += G) {
     int m0, n0;
     tile_origin(t, m0, n0);
-    setup_tile(m0, n0);
-    run_k(0, g.P);
-    if (!(g.dbg & 1)) epilogue(m0, n0);
+    const bool hn = kHalfOk && n0 + 128 >= g.N && !(g.dbg & 32);
+    setup_tile(m0, n0, hn);
+    run_k(0, g.P, hn);
+    if (g.dbg & 1) continue;
+    if constexpr (kHalfOk) {
+      if (hn) {
+        epilogue(m0, n0, std::true_type{});
+        continue;
+      }
+    }
+    epilogue(m0, n0, std::false_type{});
   }
   if (tail_mode) return;
 
@@ -806,7 +880,7 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
     int m0, n0;
     tile_origin(t, m0, n0);
     setup_tile(m0, n0);
-    run(kb, ke, false);
+    run(kb, ke, false, false);
     if (kb != 0) {
       // tail: publish the partial tile (register order: coalesced 16-B lanes)
       // buffer stores: per-lane voffset + a constant soffset per register (no 64-bit address per register for the
@@ -867,7 +941,7 @@ __global__ __launch_bounds__(512) void gemm_sk_kernel(SkArgs g) {
               }
         }
       }
-      epilogue(m0, n0);
+      epilogue(m0, n0, std::false_type{});
     }
     it = ts * g.P + ke;
     bar();  // LDS free (the tail path stages nothing, but the next segment's copies must not pass slower waves)

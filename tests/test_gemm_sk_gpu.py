@@ -387,3 +387,34 @@ def test_layout_t_operand_over_2gb_walks_k_in_one_launch():
     native.linear_wgrad(gw3, dy, x)
     assert torch.equal(gw, gw3)  # deterministic
     del dy
+
+
+@pytest.mark.parametrize("al,bl", [(K_, K_), (K_, T_), (T_, K_), (T_, T_)])
+@pytest.mark.parametrize("M,N,K", [(777, 896, 896), (520, 1152, 320), (300, 520, 1280), (2304, 384, 640),
+                                   (16640, 896, 2048)])
+def test_half_width_last_tile_column_bit_identical(al, bl, M, N, K):
+    """The last tile column of N % 256 in (0, 128] (the N = 896 / 1152 outputs) runs half-width tiles: B's 128 columns
+    in one LDS half, the other quadrant's MFMAs skipped (csrc/gemm_sk.hip, setup_tile hn). Same k order per output, so
+    the bf16 (plain / bias) and fp32 (store / accumulate) results equal the full-width tiles' bit for bit (debug bit
+    32 forces the full-width path)."""
+    g = torch.Generator(device="cuda").manual_seed(M + 3 * N + K + al + 5 * bl)
+    a, fa = _op((M, K), al, g)
+    b, fb = _op((N, K), bl, g)
+    bias = torch.randn(N, generator=g, device="cuda").to(torch.bfloat16) if al == K_ and bl == K_ else None
+    c0 = torch.randn(M, N, generator=g, device="cuda")
+    res = []
+    try:
+        for dbg in (0, 32):
+            native.lib().drl_gemm_set_debug(dbg)
+            out = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+            native.gemm(a, al, b, bl, M, N, K, out, bias=bias)
+            out32 = c0.clone()
+            native.gemm(a, al, b, bl, M, N, K, out32, beta=True)
+            res.append((out, out32))
+    finally:
+        native.lib().drl_gemm_set_debug(0)
+    assert torch.equal(res[0][0], res[1][0])
+    assert torch.equal(res[0][1], res[1][1])
+    ref = fa(a).double() @ fb(b).double().t() + (bias.double() if bias is not None else 0.0)
+    torch.testing.assert_close(res[0][0].double(), ref.to(torch.bfloat16).double(), rtol=8e-3,
+                               atol=4e-6 * K ** 0.5 + 1e-2 * (bias is not None))
