@@ -681,8 +681,11 @@ int64_t drl_gemm_workspace_bytes(void);
  * rounds while they fill the grid, stream-K for the last one or two; 1 = all stream-K; 2 = whole tiles only),
  * min_iters (minimum k-tile pairs per workgroup of an all-stream-K grid, 0 = 2). Schedule only, same result. */
 void drl_gemm_set_sk_tuning(int32_t grid, int32_t group, int32_t dp_mode, int32_t min_iters);
-/* Measurement hook (never set in the product path): 1 = whole tiles skip their epilogue (no output written), to time
- * the main loop and the per-tile fixed cost apart; 0 = normal. */
+/* Measurement hook (never set in the product path), bit flags, 0 = normal: 1 = whole tiles skip their epilogue (no
+ * output written), to time the main loop and the per-tile fixed cost apart; 2 = the plain epilogue stages but does not
+ * store; 4 = the epilogue's barriers only; 8 = slice-major split-K workgroup order; 16 = layout-T operands past 2 GB as
+ * a host loop of K-block launches; 32 = full-width tiles for the last tile column of N % 256 in (0, 128] (the
+ * half-width path off: same results bit for bit). */
 void drl_gemm_set_debug(int32_t flags);
 /* (flags bit 8: all-split-K grids in slice-major workgroup order instead of tile-major — schedule only, the same
  * bits; bit 16: a layout-T operand past 2 GB as the host loop of K-block launches; both for A/B measurement.) */
