@@ -99,11 +99,17 @@ __device__ __forceinline__ u16x4 lds_tr16(const uint16_t* p) {
 // unit u ^ f(r). f is a bijection on r & 7 (conflict-free 16-B row writes: 8 consecutive rows cover all 8
 // units) that also flips bit 2 between rows r and r + 2 (the 4 rows of a transposing read never share banks).
 __device__ __forceinline__ int xsw(int r) { return (r & 7) ^ ((r & 2) << 1); }
+// 128-B rows (head_dim 64): the unit mask also keeps the wave's 16-B row reads (ds_read_b128, lane groups {0-3, 12-15,
+// 20-27} / {4-11, 16-19, 28-31} of each half) conflict-free — the 8 even and the 8 odd rows of each lane group take 8
+// distinct masks (xsw gave each mask to two of them: 2-way conflicts on every Q / dO fragment read of the dK / dV
+// kernel) — while rows r and r + 2 (r % 4 == 0) still differ in bit 2 for the transposing reads
+template <int XR>
+__device__ __forceinline__ int xswz(int r) { return XR == 64 ? (((r >> 3) & 3) | ((r << 1) & 4)) : xsw(r); }
 // XR = row length in elements (the head dim: 64 -> 128-B rows, 128 -> 256-B rows; the swizzle permutes the
 // 16-B units within each aligned group of 8)
 template <int XR = 64>
 __device__ __forceinline__ int ximg_off(int r, int col) {  // element offset of (row r, column col)
-  return r * XR + 8 * ((col >> 3) ^ xsw(r)) + (col & 7);
+  return r * XR + 8 * ((col >> 3) ^ xswz<XR>(r)) + (col & 7);
 }
 
 // A operand "X^T" (rows = head dim, k = positions in the accumulator order) of a 32-position x 64 tile X in
@@ -977,7 +983,7 @@ __global__ __launch_bounds__(64 * NW) void flash_dkdv_kernel(FlashBwdArgs a) {
     const uint32_t xb = lds_x + 2 * static_cast<uint32_t>(((wv * 2 + buf) * 2) * 32 * XROW);
 #pragma unroll
     for (int i = 0; i < 32 / RPI; ++i) {
-      const int r = i * RPI + lane / UPR, u = (lane % UPR) ^ xsw(r);
+      const int r = i * RPI + lane / UPR, u = (lane % UPR) ^ xswz<XROW>(r);
       const uint32_t tr = static_cast<uint32_t>(min(tt + r, T - 1));
       const uint32_t oq = tr * (D * 2) + 16 * u, od = tr * drow + 16 * u;
       const uint32_t dq_ = __builtin_amdgcn_readfirstlane(xb + 2 * i * RPI * XROW);
