@@ -152,6 +152,16 @@ struct KVTile {
 // d = c' / 4, 16-B column c' % 4 (keys 8*col .. 8*col+7). Keys >= Tk load as zero.
 // the same for a block wholly below Tk (the caller's test is on k0 alone, so it is uniform over the
 // workgroup): no per-key bounds tests in the steady-state key loop
+// dQ's K^T chunk cc of a staged key block -> (row d, 16-B column col of the block's 4): 8 rows x 4 columns per 32
+// chunks, the row fastest. The staging store of a chunk is two 8-B writes to the permuted places of its 80-B row (20
+// dwords): with d fastest, the 16 lanes of each ds_write_b64 lane group write 8 rows x 2 columns = 32 distinct banks,
+// where d = cc / 4 put rows r .. r + 3 in a group (rows r and r + 2 share 4 banks: 2-way conflicts, 1.2M conflict
+// cycles per dispatch). Same LDS image. The forward's V^T staging keeps d = cc / 4: there the remap (row-fastest, or
+// rows {r, r + 1, r + 4, r + 5} with 4 columns each) removed its conflicts too but measured 1-2 % slower
+// (profiles/r06_flash_staging_conflicts.txt)
+__device__ __forceinline__ int tr_row(int cc) { return 8 * (cc >> 5) + (cc & 7); }
+__device__ __forceinline__ int tr_col(int cc) { return (cc >> 3) & 3; }
+
 template <int D>
 __device__ __forceinline__ void kv_issue_full(const uint16_t* kbase, const uint16_t* vtbase, int64_t ld_vt,
                                               int64_t k0, int tid, u16x8 (&r)[KVTile<D>::CPT]) {
@@ -484,7 +494,7 @@ __device__ __forceinline__ void dq_issue(const uint16_t* kb, const uint16_t* vb,
       const int key = k0 + row;
       if (key < T) v = *reinterpret_cast<const u16x8*>((c < TL::RCH ? kb : vb) + static_cast<int64_t>(key) * D + col * 8);
     } else if (c < TL::NCH) {
-      const int cc = c - 2 * TL::RCH, d = cc / 4, col = cc % 4;
+      const int cc = c - 2 * TL::RCH, d = tr_row(cc), col = tr_col(cc);
       const int kk = k0 + col * 8;
       const uint16_t* src = ktb + static_cast<int64_t>(d) * ld_t + kk;
       if (kk + 7 < T) {
@@ -513,7 +523,7 @@ __device__ __forceinline__ void dq_issue_full(const uint16_t* kb, const uint16_t
     const int c0 = tid + NT * i, c = c0 < TL::NCH ? c0 : c0 % (2 * TL::RCH);
     const int cc = c % TL::RCH, row = cc / (D / 8), col = cc % (D / 8);
     const uint16_t* rm = (c < TL::RCH ? kb : vb) + static_cast<int64_t>(k0 + row) * D + col * 8;
-    const int ct = c - 2 * TL::RCH, d = ct / 4, colt = ct % 4;
+    const int ct = c - 2 * TL::RCH, d = tr_row(ct), colt = tr_col(ct);
     const uint16_t* tm = ktb + static_cast<int64_t>(d) * ld_t + k0 + colt * 8;
     r[i] = *reinterpret_cast<const u16x8*>(c < 2 * TL::RCH ? rm : tm);
   }
@@ -530,7 +540,7 @@ __device__ __forceinline__ void dq_store(uint16_t* kl, uint16_t* vl, uint16_t* k
       const int cc = c % TL::RCH, row = cc / (D / 8), col = cc % (D / 8);
       *reinterpret_cast<u16x8*>((c < TL::RCH ? kl : vl) + row * TL::ROW + col * 8) = r[i];
     } else if (c < TL::NCH) {
-      const int cc = c - 2 * TL::RCH, d = cc / 4, col = cc % 4;
+      const int cc = c - 2 * TL::RCH, d = tr_row(cc), col = tr_col(cc);
       uint16_t* dst = ktl + d * TL::TROW + (col >> 1) * 16 + (col & 1) * 4;  // permuted (DqTile)
       *reinterpret_cast<u16x4*>(dst) = u16x4{r[i][0], r[i][1], r[i][2], r[i][3]};
       *reinterpret_cast<u16x4*>(dst + 8) = u16x4{r[i][4], r[i][5], r[i][6], r[i][7]};
